@@ -1,0 +1,446 @@
+// torch-facing glue for the gfx950 kernels (module paddlebox_amd._pbx_hip).
+// Everything here is shape checking + pointer plumbing; no compute.
+#include <ATen/hip/HIPContext.h>
+#include <torch/extension.h>
+
+#include <stdexcept>
+
+#include "kernels.h"
+
+namespace py = pybind11;
+using torch::Tensor;
+
+namespace pbx {
+
+static hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+#define PBX_CHECK(cond, msg)                                     \
+  do {                                                           \
+    if (!(cond)) throw std::runtime_error(std::string("pbx: ") + msg); \
+  } while (0)
+
+static void check_cuda(const Tensor& t, const char* name) {
+  PBX_CHECK(t.is_cuda(), std::string(name) + " must be a GPU tensor");
+  PBX_CHECK(t.is_contiguous(), std::string(name) + " must be contiguous");
+}
+template <typename T>
+static T* ptr(const Tensor& t) {
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+template <typename T>
+static T* optr(const c10::optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+// --------------------------------------------------------------- GPU table
+class GpuTable {
+ public:
+  GpuTable(int dim, int64_t capacity, int64_t stash_cap, int device)
+      : dim_(dim), device_(device) {
+    PBX_CHECK(dim >= 1 && dim <= 128, "embedx dim must be in [1,128]");
+    const RowLayout l = make_row_layout(dim);
+    stride_ = l.stride;
+    nb_ = (uint64_t)((capacity + kBucketSlots - 1) / kBucketSlots);
+    if (nb_ < 1) nb_ = 1;
+    stash_cap_ = stash_cap;
+    auto opt8 = torch::TensorOptions().dtype(torch::kInt64).device(torch::kCUDA, device);
+    auto opt4 = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device);
+    auto optf = torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device);
+    keys_ = torch::full({(int64_t)nb_ * kBucketSlots}, -1, opt8);  // kEmptyKey
+    fill_ = torch::zeros({(int64_t)nb_}, opt4);
+    values_ = torch::zeros({(int64_t)nb_ * kBucketSlots + stash_cap_, stride_}, optf);
+    stash_keys_ = torch::full({std::max<int64_t>(stash_cap_, 1)}, -1, opt8);
+    scratch_ = torch::zeros({8}, opt8);  // [stash_n, ovf_n, fail_n, count, cursor...]
+  }
+  TableDev view() const {
+    TableDev t;
+    t.keys = ptr<uint64_t>(keys_);
+    t.fill = ptr<uint32_t>(fill_);
+    t.values = ptr<float>(values_);
+    t.nb = nb_;
+    t.stash_keys = ptr<uint64_t>(stash_keys_);
+    t.stash_n = reinterpret_cast<uint32_t*>(ptr<int64_t>(scratch_) + 0);
+    t.stash_cap = (uint32_t)stash_cap_;
+    t.stride = stride_;
+    t.dim = dim_;
+    return t;
+  }
+  Tensor probe(const Tensor& h, const c10::optional<Tensor>& n_dev) {
+    check_cuda(h, "h");
+    auto rows = torch::empty({h.numel()}, h.options().dtype(torch::kInt64));
+    launch_table_probe(view(), ptr<uint64_t>(h), h.numel(), optr<int32_t>(n_dev), ptr<int64_t>(rows), cur_stream());
+    return rows;
+  }
+  // Insert unique mixed keys (those not present). Returns number of keys that
+  // could not be placed (0 normally).  Synchronises (build phase only).
+  int64_t insert(const Tensor& h, const c10::optional<Tensor>& n_dev, const SparseSGDConfig& cfg,
+                 uint64_t seed, bool init_embedx) {
+    check_cuda(h, "h");
+    const int64_t n = h.numel();
+    if (n == 0) return 0;
+    auto s = cur_stream();
+    Tensor rows = probe(h, n_dev);
+    auto ovf = torch::empty({n}, h.options());
+    auto ctr = torch::zeros({4}, h.options().dtype(torch::kInt32));
+    launch_table_insert(view(), ptr<uint64_t>(h), n, optr<int32_t>(n_dev), ptr<int64_t>(rows), cfg, seed,
+                        init_embedx ? 1 : 0, ptr<uint64_t>(ovf), reinterpret_cast<uint32_t*>(ptr<int32_t>(ctr)), s);
+    launch_table_clamp_fill(view(), s);
+    launch_table_resolve_overflow(view(), ptr<uint64_t>(ovf), reinterpret_cast<uint32_t*>(ptr<int32_t>(ctr)), cfg,
+                                  seed, init_embedx ? 1 : 0, reinterpret_cast<uint32_t*>(ptr<int32_t>(ctr) + 1), s);
+    auto host = ctr.cpu();
+    last_overflow_ = host[0].item<int32_t>();
+    return host[1].item<int32_t>();
+  }
+  int64_t last_overflow() const { return last_overflow_; }
+  int64_t size() {
+    auto c = torch::zeros({1}, keys_.options());
+    launch_table_count(view(), reinterpret_cast<unsigned long long*>(ptr<int64_t>(c)), cur_stream());
+    int64_t stash = stash_n();
+    return c.cpu().item<int64_t>() + stash;
+  }
+  int64_t stash_n() { return scratch_.narrow(0, 0, 1).cpu().item<int64_t>() & 0xFFFFFFFF; }
+  // Export all (mixed key, value row) pairs.
+  std::pair<Tensor, Tensor> export_all(bool with_values) {
+    const int64_t n = size();
+    auto k = torch::empty({n}, keys_.options());
+    Tensor v = with_values ? torch::empty({n, stride_}, values_.options()) : Tensor();
+    auto cur = torch::zeros({1}, keys_.options());
+    if (n > 0)
+      launch_table_export(view(), ptr<uint64_t>(k), with_values ? ptr<float>(v) : nullptr,
+                          reinterpret_cast<unsigned long long*>(ptr<int64_t>(cur)), cur_stream());
+    return {k, v};
+  }
+  void assign(const Tensor& rows, const Tensor& vals) {
+    check_cuda(rows, "rows");
+    check_cuda(vals, "vals");
+    PBX_CHECK(vals.dim() == 2 && vals.size(0) == rows.numel(), "assign: shape");
+    launch_table_assign(view(), ptr<int64_t>(rows), ptr<float>(vals), rows.numel(), (int)vals.size(1), cur_stream());
+  }
+  int64_t shrink(const ShrinkConfig& c) {
+    auto d = torch::zeros({1}, keys_.options());
+    launch_table_shrink(view(), c, reinterpret_cast<unsigned long long*>(ptr<int64_t>(d)), cur_stream());
+    return d.cpu().item<int64_t>();
+  }
+  Tensor gather_pull(const Tensor& rows, const c10::optional<Tensor>& n_dev, int out_stride) {
+    check_cuda(rows, "rows");
+    auto out = torch::empty({rows.numel(), out_stride}, values_.options());
+    launch_gather_pull(view(), ptr<int64_t>(rows), optr<int32_t>(n_dev), rows.numel(), ptr<float>(out), out_stride,
+                       cur_stream());
+    return out;
+  }
+  void push_adagrad(const Tensor& rows, const Tensor& push, const c10::optional<Tensor>& n_dev,
+                    const SparseSGDConfig& cfg, uint64_t seed) {
+    check_cuda(rows, "rows");
+    check_cuda(push, "push");
+    PBX_CHECK(push.dim() == 2 && push.size(1) >= push_width(dim_), "push record width");
+    launch_push_adagrad(view(), ptr<int64_t>(rows), ptr<float>(push), (int)push.size(1), optr<int32_t>(n_dev),
+                        rows.numel(), cfg, seed, cur_stream());
+  }
+  Tensor keys() const { return keys_; }
+  Tensor values() const { return values_; }
+  Tensor fill() const { return fill_; }
+  int dim() const { return dim_; }
+  int stride() const { return stride_; }
+  int64_t capacity() const { return (int64_t)nb_ * kBucketSlots; }
+  int64_t nbuckets() const { return (int64_t)nb_; }
+
+ private:
+  int dim_;
+  int device_;
+  int stride_;
+  uint64_t nb_;
+  int64_t stash_cap_;
+  int64_t last_overflow_ = 0;
+  Tensor keys_, fill_, values_, stash_keys_, scratch_;
+};
+
+// --------------------------------------------------------------- dedup
+struct DedupWorkspace {
+  int64_t cap;
+  Tensor h_tmp, h_sorted, idx_tmp, perm, flags, scan, uid, uniq_h, seg, u_count, temp;
+  size_t temp_bytes;
+  DedupWorkspace(int64_t cap_, int device) : cap(cap_) {
+    auto o8 = torch::TensorOptions().dtype(torch::kInt64).device(torch::kCUDA, device);
+    auto o4 = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device);
+    h_tmp = torch::empty({cap}, o8);
+    h_sorted = torch::empty({cap}, o8);
+    idx_tmp = torch::empty({cap}, o4);
+    perm = torch::empty({cap}, o4);
+    flags = torch::empty({cap}, o4);
+    scan = torch::empty({cap}, o4);
+    uid = torch::empty({cap}, o4);
+    uniq_h = torch::empty({cap}, o8);
+    seg = torch::empty({cap + 1}, o4);
+    u_count = torch::zeros({2}, o4);  // [U, n_valid]
+    temp_bytes = dedup_temp_bytes(cap);
+    temp = torch::empty({(int64_t)temp_bytes}, torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, device));
+  }
+  // keys: int64 tensor (n <= cap).  Results live in this workspace.
+  void run(const Tensor& keys, bool mixed) {
+    check_cuda(keys, "keys");
+    const int64_t n = keys.numel();
+    PBX_CHECK(n <= cap, "dedup: more keys than workspace capacity");
+    launch_dedup(ptr<uint64_t>(keys), n, mixed, ptr<uint64_t>(h_tmp), ptr<uint64_t>(h_sorted), ptr<int32_t>(idx_tmp),
+                 ptr<int32_t>(perm), ptr<int32_t>(flags), ptr<int32_t>(scan), ptr<int32_t>(uid), ptr<uint64_t>(uniq_h),
+                 ptr<int32_t>(seg), ptr<int32_t>(u_count), temp.data_ptr(), temp_bytes, cur_stream());
+    last_n = n;
+  }
+  int64_t last_n = 0;
+};
+
+// --------------------------------------------------------------- free ops
+static void fill_occurrence(const Tensor& lod, int S, int B, Tensor occ_slot, Tensor occ_ins) {
+  check_cuda(lod, "lod");
+  PBX_CHECK(lod.numel() == (int64_t)S * (B + 1), "lod shape");
+  launch_fill_occurrence(ptr<int64_t>(lod), S, B, ptr<int32_t>(occ_slot), ptr<int32_t>(occ_ins), cur_stream());
+}
+
+static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_index, const Tensor& uid,
+                            const Tensor& lod, int S, int B, int E, Tensor out, int col_offset, bool use_cvm,
+                            int cvm_offset, bool clk_filter, float pad_value, bool need_filter, float show_coeff,
+                            float clk_coeff, float threshold, int quant_ratio, bool embed_threshold_filter,
+                            float embed_threshold, int embed_thres_size) {
+  check_cuda(src, "src");
+  check_cuda(uid, "uid");
+  check_cuda(lod, "lod");
+  check_cuda(out, "out");
+  PBX_CHECK(src.dim() == 2 && src.size(1) >= E, "src width < E");
+  PBX_CHECK(out.dim() == 2 && out.size(0) == B, "out shape");
+  SeqpoolCvmArgs a;
+  a.src = ptr<float>(src);
+  a.src_stride = (int)src.size(1);
+  a.src_index = optr<int64_t>(src_index);
+  a.uid = ptr<int32_t>(uid);
+  a.lod = ptr<int64_t>(lod);
+  a.S = S;
+  a.B = B;
+  a.E = E;
+  a.out = ptr<float>(out);
+  a.out_stride = (int)out.size(1);
+  a.col_offset = col_offset;
+  a.use_cvm = use_cvm;
+  a.cvm_offset = cvm_offset;
+  a.clk_filter = clk_filter;
+  a.pad_value = pad_value;
+  a.need_filter = need_filter;
+  a.show_coeff = show_coeff;
+  a.clk_coeff = clk_coeff;
+  a.threshold = threshold;
+  a.quant_ratio = quant_ratio;
+  a.embed_threshold_filter = embed_threshold_filter;
+  a.embed_threshold = embed_threshold;
+  a.embed_thres_size = embed_thres_size;
+  PBX_CHECK(col_offset + (int64_t)S * seqpool_cvm_out_width(a) <= out.size(1), "out too narrow");
+  launch_seqpool_cvm_fwd(a, cur_stream());
+}
+
+static void push_merge(const Tensor& dout, int col_offset, const Tensor& cvm, int cvm_offset, bool use_cvm,
+                       bool clk_filter, int E, const Tensor& perm, const Tensor& uid, const Tensor& occ_slot,
+                       const Tensor& occ_ins, const Tensor& slot_ids, const Tensor& n_valid, Tensor push,
+                       const c10::optional<Tensor>& push_index, float bs_scale, int dim) {
+  check_cuda(dout, "dout");
+  check_cuda(cvm, "cvm");
+  check_cuda(push, "push");
+  PBX_CHECK(cvm_offset == 2, "fused push merge requires cvm_offset == 2");
+  PBX_CHECK(E == 3 + dim, "E must be 3 + dim");
+  PBX_CHECK(dim == 4 || dim == 8 || dim == 16 || dim == 32, "fused push merge: dim in {4,8,16,32}");
+  PBX_CHECK(push.dim() == 2 && push.size(1) >= push_width(dim), "push width");
+  PushMergeArgs a;
+  a.dout = ptr<float>(dout);
+  a.out_stride = (int)dout.size(1);
+  a.col_offset = col_offset;
+  a.cvm = ptr<float>(cvm);
+  a.cvm_offset = cvm_offset;
+  a.use_cvm = use_cvm;
+  a.clk_filter = clk_filter;
+  a.E = E;
+  a.perm = ptr<int32_t>(perm);
+  a.uid = ptr<int32_t>(uid);
+  a.occ_slot = ptr<int32_t>(occ_slot);
+  a.occ_ins = ptr<int32_t>(occ_ins);
+  a.slot_ids = ptr<float>(slot_ids);
+  a.n_valid = ptr<int32_t>(n_valid);
+  a.n = perm.numel();
+  a.push = ptr<float>(push);
+  a.push_stride = (int)push.size(1);
+  a.push_index = optr<int64_t>(push_index);
+  a.bs_scale = bs_scale;
+  a.dim = dim;
+  launch_push_merge(a, cur_stream());
+}
+
+static void push_merge_records(const Tensor& rec, const Tensor& perm, const Tensor& uid, const Tensor& n_valid,
+                               int dim, Tensor out) {
+  check_cuda(rec, "rec");
+  check_cuda(out, "out");
+  PBX_CHECK(dim == 4 || dim == 8 || dim == 16 || dim == 32, "merge records: dim in {4,8,16,32}");
+  launch_push_merge_records(ptr<float>(rec), (int)rec.size(1), ptr<int32_t>(perm), ptr<int32_t>(uid),
+                            ptr<int32_t>(n_valid), perm.numel(), dim, ptr<float>(out), (int)out.size(1), cur_stream());
+}
+
+static void shard_pack(const Tensor& uniq_h, const Tensor& u_count, int nranks, int64_t cap, Tensor send,
+                       Tensor send_index, Tensor overflow) {
+  check_cuda(uniq_h, "uniq_h");
+  PBX_CHECK(send.numel() == nranks * cap, "send shape");
+  launch_shard_pack(ptr<uint64_t>(uniq_h), ptr<int32_t>(u_count), send_index.numel(), nranks, cap,
+                    ptr<uint64_t>(send), ptr<int64_t>(send_index), ptr<int32_t>(overflow), cur_stream());
+}
+
+static void gather_by_uid(const Tensor& src, const Tensor& uid, Tensor out, int width) {
+  check_cuda(src, "src");
+  check_cuda(out, "out");
+  launch_gather_by_uid(ptr<float>(src), (int)src.size(1), ptr<int32_t>(uid), uid.numel(), ptr<float>(out),
+                       (int)out.size(1), width, cur_stream());
+}
+
+static std::vector<Tensor> data_norm_fwd(const Tensor& x, const Tensor& bsize, const Tensor& bsum, const Tensor& bsq,
+                                         const c10::optional<Tensor>& scale_w, const c10::optional<Tensor>& bias) {
+  check_cuda(x, "x");
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  auto y = torch::empty_like(x);
+  auto means = torch::empty({C}, x.options());
+  auto scales = torch::empty({C}, x.options());
+  launch_data_norm_fwd(ptr<float>(x), N, C, ptr<float>(bsize), ptr<float>(bsum), ptr<float>(bsq), ptr<float>(y),
+                       ptr<float>(means), ptr<float>(scales), optr<float>(scale_w), optr<float>(bias), cur_stream());
+  return {y, means, scales};
+}
+
+static std::vector<Tensor> data_norm_bwd(const Tensor& x, const Tensor& dy, const Tensor& means, const Tensor& scales,
+                                         float eps, bool need_dx, const c10::optional<Tensor>& scale_w) {
+  check_cuda(x, "x");
+  check_cuda(dy, "dy");
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  Tensor dx = need_dx ? torch::empty_like(x) : Tensor();
+  auto stats = torch::empty({3, C}, x.options());
+  launch_data_norm_bwd(ptr<float>(x), ptr<float>(dy), N, C, ptr<float>(means), ptr<float>(scales), eps,
+                       need_dx ? ptr<float>(dx) : nullptr, ptr<float>(stats), optr<float>(scale_w), cur_stream());
+  return {dx, stats};
+}
+
+static void data_norm_update(Tensor bsize, Tensor bsum, Tensor bsq, const Tensor& stats, float decay) {
+  launch_data_norm_update(ptr<float>(bsize), ptr<float>(bsum), ptr<float>(bsq), ptr<float>(stats),
+                          (int)bsize.numel(), decay, cur_stream());
+}
+
+static Tensor fm_fwd(const Tensor& x, int S, int D, int col0, int fstride) {
+  check_cuda(x, "x");
+  auto out = torch::empty({x.size(0)}, x.options());
+  launch_fm_fwd(ptr<float>(x), (int)x.size(0), S, D, (int)x.size(1), col0, fstride, ptr<float>(out), cur_stream());
+  return out;
+}
+
+static void fm_bwd(const Tensor& x, const Tensor& dout, int S, int D, int col0, int fstride, Tensor dx,
+                   bool accumulate) {
+  check_cuda(x, "x");
+  check_cuda(dx, "dx");
+  PBX_CHECK(dx.size(1) == x.size(1), "fm_bwd: dx must match x layout");
+  launch_fm_bwd(ptr<float>(x), ptr<float>(dout), (int)x.size(0), S, D, (int)x.size(1), col0, fstride, ptr<float>(dx),
+                (int)dx.size(1), accumulate ? 1 : 0, cur_stream());
+}
+
+static std::vector<Tensor> sigmoid_logloss(const Tensor& logit, const Tensor& label, float grad_scale) {
+  check_cuda(logit, "logit");
+  const int B = (int)logit.numel();
+  auto pred = torch::empty_like(logit);
+  auto dz = torch::empty_like(logit);
+  auto loss = torch::zeros({1}, logit.options());
+  launch_sigmoid_logloss(ptr<float>(logit), ptr<float>(label), B, ptr<float>(pred), ptr<float>(loss), ptr<float>(dz),
+                         grad_scale, cur_stream());
+  return {pred, loss, dz};
+}
+
+static void auc_accumulate(const Tensor& pred, const Tensor& label, const c10::optional<Tensor>& mask, Tensor table,
+                           Tensor stats) {
+  check_cuda(pred, "pred");
+  check_cuda(table, "table");
+  PBX_CHECK(table.scalar_type() == torch::kFloat64 && stats.scalar_type() == torch::kFloat64, "auc tables are f64");
+  launch_auc_accumulate(ptr<float>(pred), ptr<float>(label), optr<float>(mask), (int)pred.numel(),
+                        (int)(table.numel() / 2), ptr<double>(table), ptr<double>(stats), cur_stream());
+}
+
+static void adam_flat(Tensor p, const Tensor& g, Tensor m, Tensor v, float lr, float b1, float b2, float eps,
+                      float b1pow, float b2pow, float grad_scale, float wd) {
+  check_cuda(p, "p");
+  PBX_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam sizes");
+  launch_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), lr, b1, b2, eps, b1pow,
+                   b2pow, grad_scale, wd, cur_stream());
+}
+
+}  // namespace pbx
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  using namespace pbx;
+  m.doc() = "PaddleBox-capability engine: hand-written gfx950 (MI355X) kernels";
+  py::class_<SparseSGDConfig>(m, "SparseSGDConfig")
+      .def(py::init<>())
+      .def_readwrite("nonclk_coeff", &SparseSGDConfig::nonclk_coeff)
+      .def_readwrite("clk_coeff", &SparseSGDConfig::clk_coeff)
+      .def_readwrite("min_bound", &SparseSGDConfig::min_bound)
+      .def_readwrite("max_bound", &SparseSGDConfig::max_bound)
+      .def_readwrite("learning_rate", &SparseSGDConfig::learning_rate)
+      .def_readwrite("initial_g2sum", &SparseSGDConfig::initial_g2sum)
+      .def_readwrite("initial_range", &SparseSGDConfig::initial_range)
+      .def_readwrite("mf_create_thresholds", &SparseSGDConfig::mf_create_thresholds)
+      .def_readwrite("mf_learning_rate", &SparseSGDConfig::mf_learning_rate)
+      .def_readwrite("mf_initial_g2sum", &SparseSGDConfig::mf_initial_g2sum)
+      .def_readwrite("mf_initial_range", &SparseSGDConfig::mf_initial_range)
+      .def_readwrite("mf_min_bound", &SparseSGDConfig::mf_min_bound)
+      .def_readwrite("mf_max_bound", &SparseSGDConfig::mf_max_bound)
+      .def_readwrite("nodeid_slot", &SparseSGDConfig::nodeid_slot)
+      .def_readwrite("feature_learning_rate", &SparseSGDConfig::feature_learning_rate)
+      .def_readwrite("use_feature_lr", &SparseSGDConfig::use_feature_lr);
+  py::class_<ShrinkConfig>(m, "ShrinkConfig")
+      .def(py::init<>())
+      .def_readwrite("show_click_decay_rate", &ShrinkConfig::show_click_decay_rate)
+      .def_readwrite("delete_threshold", &ShrinkConfig::delete_threshold)
+      .def_readwrite("delete_after_unseen_days", &ShrinkConfig::delete_after_unseen_days)
+      .def_readwrite("nonclk_coeff", &ShrinkConfig::nonclk_coeff)
+      .def_readwrite("clk_coeff", &ShrinkConfig::clk_coeff);
+  py::class_<GpuTable>(m, "GpuTable")
+      .def(py::init<int, int64_t, int64_t, int>(), py::arg("dim"), py::arg("capacity"), py::arg("stash_cap") = 4096,
+           py::arg("device") = 0)
+      .def("probe", &GpuTable::probe, py::arg("h"), py::arg("n_dev") = py::none())
+      .def("insert", &GpuTable::insert, py::arg("h"), py::arg("n_dev"), py::arg("cfg"), py::arg("seed"),
+           py::arg("init_embedx"))
+      .def("last_overflow", &GpuTable::last_overflow)
+      .def("size", &GpuTable::size)
+      .def("stash_n", &GpuTable::stash_n)
+      .def("export_all", &GpuTable::export_all)
+      .def("assign", &GpuTable::assign)
+      .def("shrink", &GpuTable::shrink)
+      .def("gather_pull", &GpuTable::gather_pull, py::arg("rows"), py::arg("n_dev"), py::arg("out_stride"))
+      .def("push_adagrad", &GpuTable::push_adagrad)
+      .def_property_readonly("keys", &GpuTable::keys)
+      .def_property_readonly("values", &GpuTable::values)
+      .def_property_readonly("fill", &GpuTable::fill)
+      .def_property_readonly("dim", &GpuTable::dim)
+      .def_property_readonly("stride", &GpuTable::stride)
+      .def_property_readonly("capacity", &GpuTable::capacity)
+      .def_property_readonly("nbuckets", &GpuTable::nbuckets);
+  py::class_<DedupWorkspace>(m, "DedupWorkspace")
+      .def(py::init<int64_t, int>())
+      .def("run", &DedupWorkspace::run, py::arg("keys"), py::arg("mixed") = false)
+      .def_readonly("cap", &DedupWorkspace::cap)
+      .def_readonly("h_sorted", &DedupWorkspace::h_sorted)
+      .def_readonly("perm", &DedupWorkspace::perm)
+      .def_readonly("uid", &DedupWorkspace::uid)
+      .def_readonly("uniq_h", &DedupWorkspace::uniq_h)
+      .def_readonly("seg", &DedupWorkspace::seg)
+      .def_readonly("u_count", &DedupWorkspace::u_count);
+  m.def("fill_occurrence", &fill_occurrence);
+  m.def("seqpool_cvm_fwd", &seqpool_cvm_fwd);
+  m.def("push_merge", &push_merge);
+  m.def("push_merge_records", &push_merge_records);
+  m.def("shard_pack", &shard_pack);
+  m.def("gather_by_uid", &gather_by_uid);
+  m.def("data_norm_fwd", &data_norm_fwd);
+  m.def("data_norm_bwd", &data_norm_bwd);
+  m.def("data_norm_update", &data_norm_update);
+  m.def("fm_fwd", &fm_fwd);
+  m.def("fm_bwd", &fm_bwd);
+  m.def("sigmoid_logloss", &sigmoid_logloss);
+  m.def("auc_accumulate", &auc_accumulate);
+  m.def("adam_flat", &adam_flat);
+  m.def("mix64", [](uint64_t k) { return mix64(k); });
+  m.def("unmix64", [](uint64_t k) { return unmix64(k); });
+}

@@ -1,0 +1,190 @@
+// Launcher API for the hand-written gfx950 kernels.  The .hip translation
+// units include only HIP headers (fast to build); the torch-facing glue in
+// csrc/hip/bindings.cpp calls these with raw pointers + the current stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+#include "../common/pbx_common.h"
+
+namespace pbx {
+
+// ---------------------------------------------------------------- hash table
+struct TableDev {
+  uint64_t* keys = nullptr;   // [nb*16] mixed keys, kEmptyKey = free
+  uint32_t* fill = nullptr;   // [nb] occupied prefix length of each bucket
+  float* values = nullptr;    // [(nb*16 + stash_cap) * stride]
+  uint64_t nb = 0;            // number of buckets
+  uint64_t* stash_keys = nullptr;  // [stash_cap]
+  uint32_t* stash_n = nullptr;     // device scalar
+  uint32_t stash_cap = 0;
+  int stride = 16;  // floats per row
+  int dim = 8;      // embedx dim
+};
+
+// rows[i] = row id of h[i] or -1.  n_dev (optional) = device-side count.
+void launch_table_probe(const TableDev& t, const uint64_t* h, int64_t n, const int32_t* n_dev,
+                        int64_t* rows, hipStream_t s);
+// Insert unique keys h[i] whose rows[i] < 0.  Overflowing keys are appended to
+// ovf_keys (count in ovf_n) for launch_table_resolve_overflow.
+void launch_table_insert(const TableDev& t, const uint64_t* h, int64_t n, const int32_t* n_dev,
+                         const int64_t* rows, const SparseSGDConfig& cfg, uint64_t seed,
+                         int init_embedx, uint64_t* ovf_keys, uint32_t* ovf_n, hipStream_t s);
+void launch_table_clamp_fill(const TableDev& t, hipStream_t s);
+// Serial cuckoo displacement for the (rare) keys that did not fit; falls back
+// to the stash.  fail_n counts keys that could not be placed anywhere.
+void launch_table_resolve_overflow(const TableDev& t, const uint64_t* ovf_keys,
+                                   const uint32_t* ovf_n, const SparseSGDConfig& cfg, uint64_t seed,
+                                   int init_embedx, uint32_t* fail_n, hipStream_t s);
+// Compact every bucket to a prefix and delete rows flagged in del (by row id).
+void launch_table_count(const TableDev& t, unsigned long long* count, hipStream_t s);
+// Write (h, value row) of every occupied slot into out arrays starting at
+// atomic cursor; used for save / rehash / host write-back.
+void launch_table_export(const TableDev& t, uint64_t* out_keys, float* out_vals,
+                         unsigned long long* cursor, hipStream_t s);
+// Overwrite value rows for rows[i] >= 0 with vals[i].
+void launch_table_assign(const TableDev& t, const int64_t* rows, const float* vals, int64_t n,
+                         int vals_stride, hipStream_t s);
+// Shrink: decay show/click, age unseen_days, delete rows below thresholds.
+struct ShrinkConfig {
+  float show_click_decay_rate = 0.98f;
+  float delete_threshold = 0.8f;
+  float delete_after_unseen_days = 30.f;
+  float nonclk_coeff = 0.1f;
+  float clk_coeff = 1.0f;
+};
+void launch_table_shrink(const TableDev& t, const ShrinkConfig& c, unsigned long long* deleted,
+                         hipStream_t s);
+
+// ---------------------------------------------------------------- dedup
+// Temp-storage sizing for the hipCUB radix sort / scan used by dedup.
+size_t dedup_temp_bytes(int64_t n);
+// From keys (uint64 feasigns) of length n (padded entries == kEmptyKey are
+// ignored): h_sorted (unique-first), perm (sorted position -> original index),
+// uid[i] (original index -> unique id, -1 for padding), uniq_h[U], seg[U+1]
+// (segment starts into perm), u_count (device scalar U).
+void launch_dedup(const uint64_t* keys, int64_t n, bool keys_are_mixed, uint64_t* h_tmp,
+                  uint64_t* h_sorted, int32_t* idx_tmp, int32_t* perm, int32_t* flags,
+                  int32_t* scan, int32_t* uid, uint64_t* uniq_h, int32_t* seg, int32_t* u_count,
+                  void* temp, size_t temp_bytes, hipStream_t s);
+
+// ---------------------------------------------------------------- slot metadata
+// Flat slot-major key layout: keys of slot s for instance b are
+// [lod[s*(B+1)+b], lod[s*(B+1)+b+1]).  Writes occ_slot / occ_ins per key.
+void launch_fill_occurrence(const int64_t* lod, int S, int B, int32_t* occ_slot, int32_t* occ_ins,
+                            hipStream_t s);
+
+// ---------------------------------------------------------------- pull
+// out[u, 0:P] = table row (rows[u]) head (P = 3 + D), zeros if row < 0.
+void launch_gather_pull(const TableDev& t, const int64_t* rows, const int32_t* n_dev, int64_t n,
+                        float* out, int out_stride, hipStream_t s);
+
+// Fused seqpool + CVM over the pull record source.
+struct SeqpoolCvmArgs {
+  const float* src = nullptr;   // record base
+  int src_stride = 0;           // floats per record
+  const int64_t* src_index = nullptr;  // unique id -> record index (nullable: identity)
+  const int32_t* uid = nullptr;        // occurrence -> unique id
+  const int64_t* lod = nullptr;        // [S*(B+1)]
+  int S = 0, B = 0;
+  int E = 11;                 // pulled record width used (cvm_offset + ...)
+  float* out = nullptr;       // [B, out_stride], slot s at column col_offset + s*Eo
+  int out_stride = 0;
+  int col_offset = 0;
+  int use_cvm = 1;
+  int cvm_offset = 2;
+  int clk_filter = 0;
+  float pad_value = 0.f;
+  int need_filter = 0;
+  float show_coeff = 0.2f, clk_coeff = 1.0f, threshold = 0.96f;
+  int quant_ratio = 0;
+  int embed_threshold_filter = 0;
+  float embed_threshold = 0.f;
+  int embed_thres_size = 0;
+};
+int seqpool_cvm_out_width(const SeqpoolCvmArgs& a);
+void launch_seqpool_cvm_fwd(const SeqpoolCvmArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- push
+// Segmented merge of per-occurrence gradients into per-unique push records.
+// Gradient source for occurrence k (instance b, slot s):
+//   cvm cols      <- cvm[b*cvm_offset + c]
+//   embed cols    <- dout[b*out_stride + col_offset + s*Eo + (c - cvm_offset + (use_cvm?cvm_offset:0))]
+// push[uidx(u)] = [slot_id, show, click, -bs*embed_g, -bs*embedx_g...]
+struct PushMergeArgs {
+  const float* dout = nullptr;
+  int out_stride = 0, col_offset = 0;
+  const float* cvm = nullptr;
+  int cvm_offset = 2;
+  int use_cvm = 1;
+  int clk_filter = 0;
+  int E = 11;  // pull record width (3 + D)
+  const int32_t* perm = nullptr;     // sorted position -> occurrence
+  const int32_t* uid = nullptr;      // occurrence -> unique
+  const int32_t* occ_slot = nullptr;
+  const int32_t* occ_ins = nullptr;
+  const float* slot_ids = nullptr;   // [S] slot id (as float, BoxPS convention)
+  const int32_t* n_valid = nullptr;  // device: number of valid (non-pad) occurrences
+  int64_t n = 0;                     // upper bound of occurrences (launch size)
+  float* push = nullptr;             // [U_cap, push_stride]
+  int push_stride = 12;
+  const int64_t* push_index = nullptr;  // unique -> push row (nullable: identity)
+  float bs_scale = 1.f;              // multiply embed grads by -bs_scale
+  int dim = 8;
+};
+void launch_push_merge(const PushMergeArgs& a, hipStream_t s);
+// Owner-side merge of received push records rec[j] (j over n entries) keyed by
+// uid_r[j] (sorted by perm_r) into out[u].
+void launch_push_merge_records(const float* rec, int rec_stride, const int32_t* perm,
+                               const int32_t* uid, const int32_t* n_valid, int64_t n, int dim,
+                               float* out, int out_stride, hipStream_t s);
+// Sparse Adagrad (+show/click stats, embedx creation) on table rows.
+void launch_push_adagrad(const TableDev& t, const int64_t* rows, const float* push,
+                         int push_stride, const int32_t* n_dev, int64_t n,
+                         const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s);
+// Zero the first U rows (U from device) of a [cap, stride] buffer.
+void launch_zero_rows(float* buf, int stride, const int32_t* n_dev, int64_t cap, hipStream_t s);
+
+// ---------------------------------------------------------------- sharding
+// Unique mixed keys (sorted) -> per-owner fixed-capacity send buffer [N, C]
+// (kEmptyKey padded) + send_index[u] = o*C + (u - start_o) + overflow flag.
+void launch_shard_pack(const uint64_t* uniq_h, const int32_t* u_count, int64_t u_cap, int nranks,
+                       int64_t cap, uint64_t* send, int64_t* send_index, int32_t* overflow,
+                       hipStream_t s);
+// resp[j] = pulled[uid_r[j]] for received entries (invalid -> zeros).
+void launch_gather_by_uid(const float* src, int src_stride, const int32_t* uid, int64_t n,
+                          float* out, int out_stride, int width, hipStream_t s);
+
+// ---------------------------------------------------------------- dense ops
+void launch_data_norm_fwd(const float* x, int N, int C, const float* bsize, const float* bsum,
+                          const float* bsq, float* y, float* means, float* scales,
+                          const float* scale_w, const float* bias, hipStream_t s);
+void launch_data_norm_bwd(const float* x, const float* dy, int N, int C, const float* means,
+                          const float* scales, float eps, float* dx, float* stats /*[3,C]*/,
+                          const float* scale_w, hipStream_t s);
+void launch_data_norm_update(float* bsize, float* bsum, float* bsq, const float* stats, int C,
+                             float decay, hipStream_t s);
+
+// DeepFM second-order FM over S fields of dim D read from x[b, col0 + s*fstride + d].
+void launch_fm_fwd(const float* x, int B, int S, int D, int row_stride, int col0, int fstride,
+                   float* out, hipStream_t s);
+void launch_fm_bwd(const float* x, const float* dout, int B, int S, int D, int row_stride,
+                   int col0, int fstride, float* dx, int dx_stride, int accumulate, hipStream_t s);
+
+// Fused sigmoid + log-loss (+ grad of mean loss).
+void launch_sigmoid_logloss(const float* logit, const float* label, int B, float* pred,
+                            float* loss_sum, float* dlogit, float grad_scale, hipStream_t s);
+
+// Streaming AUC histogram: table[label][bucket] += 1 and error sums
+// (stats: [abserr, sqrerr, pred_sum, label_sum, count]) in double.
+void launch_auc_accumulate(const float* pred, const float* label, const float* mask, int B,
+                           int nbuckets, double* table /*[2,nbuckets]*/, double* stats,
+                           hipStream_t s);
+
+// Flat Adam over a contiguous fp32 buffer.
+void launch_adam_flat(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
+                      float b2, float eps, float b1pow, float b2pow, float grad_scale,
+                      float weight_decay, hipStream_t s);
+
+}  // namespace pbx

@@ -1,0 +1,479 @@
+// Pull / seqpool+CVM / push-merge / sparse-Adagrad kernels for CDNA4.
+//
+// Reference behaviour:
+//   pull copy        paddle/fluid/framework/fleet/box_wrapper.cu:74-143  (PullCopy)
+//   push merge       box_wrapper.cu:417-512 (PushMergeCopy / ...Atomic)
+//   seqpool + CVM    paddle/fluid/operators/fused/fused_seqpool_cvm_op.cu:34-527 (fwd),
+//                    :813-1015 (bwd: CVM input written into the show/click columns)
+//   sparse Adagrad   heter_ps/optimizer.cuh.h:42-133, ctr_accessor.cc:245-279
+//
+// MI355X design: the forward reads value rows straight out of the table (or
+// the exchanged pull buffer) and writes the pooled, CVM-transformed slot block
+// directly into the concatenated dense input (no [L, 11] intermediate, no
+// separate concat).  The backward never materialises per-occurrence gradients:
+// one thread per *sorted occurrence* gathers its pooled-output gradient and a
+// wave-level segmented scan merges duplicates (skew-proof for Zipf-hot keys),
+// then the Adagrad update runs in place on the table rows.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace pbx {
+namespace {
+
+constexpr int kMaxE = 132;  // max pull width handled (D <= 128)
+
+template <int E>
+struct Acc {
+  float v[E];
+};
+
+// ---------------------------------------------------------------- occurrence map
+__global__ void k_fill_occ(const int64_t* __restrict__ lod, int S, int B, int32_t* __restrict__ occ_slot,
+                           int32_t* __restrict__ occ_ins) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)S * B) return;
+  const int s = (int)(t / B), b = (int)(t % B);
+  const int64_t st = lod[(int64_t)s * (B + 1) + b], en = lod[(int64_t)s * (B + 1) + b + 1];
+  for (int64_t k = st; k < en; ++k) {
+    occ_slot[k] = s;
+    occ_ins[k] = b;
+  }
+}
+
+// ---------------------------------------------------------------- gather pull
+__global__ void k_gather_pull(TableDev t, const int64_t* __restrict__ rows, const int32_t* n_dev, int64_t n,
+                              float* __restrict__ out, int out_stride) {
+  const int64_t nn = n_dev ? (int64_t)*n_dev : n;
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nn) return;
+  const int P = kPullHead + t.dim;
+  const int64_t r = rows[u];
+  float* o = out + u * out_stride;
+  if (r < 0) {
+    for (int c = 0; c < out_stride; ++c) o[c] = 0.f;
+    return;
+  }
+  const float4* src = reinterpret_cast<const float4*>(t.values + r * (int64_t)t.stride);
+  const int n4 = out_stride / 4;
+  if ((out_stride & 3) == 0 && n4 * 4 <= t.stride) {
+    float4* o4 = reinterpret_cast<float4*>(o);
+    for (int c4 = 0; c4 < n4; ++c4) {
+      float4 v = src[c4];
+      const int c = c4 * 4;
+      if (c + 0 >= P) v.x = 0.f;
+      if (c + 1 >= P) v.y = 0.f;
+      if (c + 2 >= P) v.z = 0.f;
+      if (c + 3 >= P) v.w = 0.f;
+      o4[c4] = v;
+    }
+  } else {
+    const float* s1 = t.values + r * (int64_t)t.stride;
+    for (int c = 0; c < out_stride; ++c) o[c] = c < P ? s1[c] : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------- seqpool + cvm fwd
+__device__ __forceinline__ float quant(float v, int q) {
+  return (float)((int)(v * q + 0.5f)) / (float)q;
+}
+
+template <int E>
+__device__ __forceinline__ void load_row(const float* __restrict__ p, float* v) {
+  if constexpr ((E + 3) / 4 * 4 <= 16) {
+    // rows are 16-B aligned with stride >= round4(E)
+    const float4* p4 = reinterpret_cast<const float4*>(p);
+#pragma unroll
+    for (int c4 = 0; c4 < (E + 3) / 4; ++c4) {
+      const float4 x = p4[c4];
+      if (c4 * 4 + 0 < E) v[c4 * 4 + 0] = x.x;
+      if (c4 * 4 + 1 < E) v[c4 * 4 + 1] = x.y;
+      if (c4 * 4 + 2 < E) v[c4 * 4 + 2] = x.z;
+      if (c4 * 4 + 3 < E) v[c4 * 4 + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < E; ++c) v[c] = p[c];
+  }
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)a.S * a.B) return;
+  // instance-major so a wave writes contiguous output rows
+  const int b = (int)(t / a.S), s = (int)(t % a.S);
+  const int64_t st = a.lod[(int64_t)s * (a.B + 1) + b], en = a.lod[(int64_t)s * (a.B + 1) + b + 1];
+  float acc[E];
+#pragma unroll
+  for (int c = 0; c < E; ++c) acc[c] = a.pad_value;
+  for (int64_t k = st; k < en; ++k) {
+    const int32_t u = a.uid[k];
+    if (u < 0) continue;
+    const int64_t ri = a.src_index ? a.src_index[u] : (int64_t)u;
+    if (ri < 0) continue;
+    float v[E];
+    load_row<E>(a.src + ri * (int64_t)a.src_stride, v);
+    if (a.need_filter || a.embed_threshold_filter) {
+      const float show = v[0], clk = v[1];
+      if ((show - clk) * a.show_coeff + clk * a.clk_coeff < a.threshold) continue;
+      if (a.embed_threshold_filter) {
+        float sc = 0.f;
+        for (int i = 1; i < a.embed_thres_size; ++i) sc += v[a.cvm_offset + i] * v[a.cvm_offset + i];
+        sc = sqrtf(sc) + fabsf(v[a.cvm_offset]);
+        if (sc < a.embed_threshold) continue;
+      }
+    }
+    if (a.quant_ratio > 0) {
+#pragma unroll
+      for (int c = 0; c < E; ++c) acc[c] += (c < a.cvm_offset) ? v[c] : quant(v[c], a.quant_ratio);
+    } else {
+#pragma unroll
+      for (int c = 0; c < E; ++c) acc[c] += v[c];
+    }
+  }
+  // CVM epilogue, written straight into the concatenated output row
+  const int Eo = a.use_cvm ? (a.clk_filter ? E - 1 : E) : E - a.cvm_offset;
+  float* o = a.out + (int64_t)b * a.out_stride + a.col_offset + (int64_t)s * Eo;
+  if (a.use_cvm) {
+    const float ls = logf(acc[0] + 1.f);
+    o[0] = ls;
+    if (a.clk_filter) {
+#pragma unroll
+      for (int c = 2; c < E; ++c) o[c - 1] = acc[c];
+    } else {
+      o[1] = logf(acc[1] + 1.f) - ls;
+#pragma unroll
+      for (int c = 2; c < E; ++c) o[c] = acc[c];
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < E; ++c)
+      if (c >= a.cvm_offset) o[c - a.cvm_offset] = acc[c];
+  }
+}
+
+// generic width (slow path, runtime E)
+__global__ void k_seqpool_cvm_generic(SeqpoolCvmArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)a.S * a.B) return;
+  const int b = (int)(t / a.S), s = (int)(t % a.S);
+  const int E = a.E;
+  const int64_t st = a.lod[(int64_t)s * (a.B + 1) + b], en = a.lod[(int64_t)s * (a.B + 1) + b + 1];
+  const int Eo = a.use_cvm ? (a.clk_filter ? E - 1 : E) : E - a.cvm_offset;
+  float* o = a.out + (int64_t)b * a.out_stride + a.col_offset + (int64_t)s * Eo;
+  float show_sum = a.pad_value, clk_sum = a.pad_value;
+  for (int c = 0; c < E; ++c) {
+    float acc = a.pad_value;
+    for (int64_t k = st; k < en; ++k) {
+      const int32_t u = a.uid[k];
+      if (u < 0) continue;
+      const int64_t ri = a.src_index ? a.src_index[u] : (int64_t)u;
+      if (ri < 0) continue;
+      const float* v = a.src + ri * (int64_t)a.src_stride;
+      if (a.need_filter && (v[0] - v[1]) * a.show_coeff + v[1] * a.clk_coeff < a.threshold) continue;
+      acc += (a.quant_ratio > 0 && c >= a.cvm_offset) ? quant(v[c], a.quant_ratio) : v[c];
+    }
+    if (c == 0) show_sum = acc;
+    if (c == 1) clk_sum = acc;
+    if (a.use_cvm) {
+      if (c == 0) o[0] = logf(show_sum + 1.f);
+      else if (c == 1) { if (!a.clk_filter) o[1] = logf(clk_sum + 1.f) - logf(show_sum + 1.f); }
+      else o[a.clk_filter ? c - 1 : c] = acc;
+    } else if (c >= a.cvm_offset) {
+      o[c - a.cvm_offset] = acc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- push merge
+// Q = 3 + D merged values per unique: [show, click, embed_g, embedx_g...]
+struct DoutSource {
+  PushMergeArgs a;
+  __device__ __forceinline__ void load(int32_t k, float* g, int Q) const {
+    const int b = a.occ_ins[k], s = a.occ_slot[k];
+    const int co = a.cvm_offset;
+    g[0] = a.cvm[(int64_t)b * co + 0];
+    g[1] = co > 1 ? a.cvm[(int64_t)b * co + 1] : 0.f;
+    const int E = a.E;
+    const int Eo = a.use_cvm ? (a.clk_filter ? E - 1 : E) : E - co;
+    const float* d = a.dout + (int64_t)b * a.out_stride + a.col_offset + (int64_t)s * Eo;
+    for (int c = co; c < E; ++c) {
+      const int oc = a.use_cvm ? (a.clk_filter ? c - 1 : c) : c - co;
+      g[2 + (c - co)] = d[oc];
+    }
+    (void)Q;
+  }
+  __device__ __forceinline__ float slot(int32_t k) const { return a.slot_ids ? a.slot_ids[a.occ_slot[k]] : (float)a.occ_slot[k]; }
+};
+
+template <int Q, typename Src>
+__global__ __launch_bounds__(256) void k_push_merge(Src src, const int32_t* __restrict__ perm,
+                                                    const int32_t* __restrict__ uid, const int32_t* n_valid,
+                                                    int64_t n, float* __restrict__ push, int push_stride,
+                                                    const int64_t* __restrict__ push_index, float neg_bs,
+                                                    int scale_from) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t pv = n_valid ? (int64_t)*n_valid : n;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_base = p - lane;
+  if (wave_base >= pv) return;  // whole wave idle
+  int32_t u = -1;
+  int32_t k = -1;
+  float g[Q];
+#pragma unroll
+  for (int c = 0; c < Q; ++c) g[c] = 0.f;
+  if (p < pv) {
+    k = perm[p];
+    u = uid[k];
+    src.load(k, g, Q);
+  }
+  // wave segmented inclusive scan keyed by u
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t uo = __shfl_up(u, off);
+#pragma unroll
+    for (int c = 0; c < Q; ++c) {
+      const float go = __shfl_up(g[c], off);
+      if (lane >= off && uo == u) g[c] += go;
+    }
+  }
+  const int32_t un = __shfl_down(u, 1);
+  const int32_t u_lane0 = __shfl(u, 0);
+  const bool tail = (lane == 63) || (un != u);
+  if (p >= pv || u < 0 || !tail) return;
+  const int64_t prow = push_index ? push_index[u] : (int64_t)u;
+  if (prow < 0) return;
+  float* dst = push + prow * push_stride;
+  // The in-wave scan covers the whole segment unless it spills over a wave
+  // boundary (occurrences are sorted by unique id, so a segment is contiguous).
+  bool complete = true;
+  if (lane == 63 && p + 1 < pv && uid[perm[p + 1]] == u) complete = false;
+  if (u_lane0 == u && wave_base > 0 && uid[perm[wave_base - 1]] == u) complete = false;
+  if (complete) {
+    dst[kPushSlot] = src.slot(k);
+    dst[kPushShow] = g[0];
+    dst[kPushClick] = g[1];
+#pragma unroll
+    for (int c = 2; c < Q; ++c) dst[kPushEmbedG + (c - 2)] = c >= scale_from ? g[c] * neg_bs : g[c];
+  } else {
+    dst[kPushSlot] = src.slot(k);
+    atomicAdd(&dst[kPushShow], g[0]);
+    atomicAdd(&dst[kPushClick], g[1]);
+#pragma unroll
+    for (int c = 2; c < Q; ++c) atomicAdd(&dst[kPushEmbedG + (c - 2)], c >= scale_from ? g[c] * neg_bs : g[c]);
+  }
+}
+
+// records source: rec[k] = [slot, show, click, embed_g, embedx_g...] (already scaled)
+struct RecordSource {
+  const float* rec;
+  int stride;
+  __device__ __forceinline__ void load(int32_t k, float* g, int Q) const {
+    const float* r = rec + (int64_t)k * stride;
+    for (int c = 0; c < Q; ++c) g[c] = r[1 + c];
+  }
+  __device__ __forceinline__ float slot(int32_t k) const { return rec[(int64_t)k * stride]; }
+};
+
+// ---------------------------------------------------------------- sparse adagrad
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+__global__ __launch_bounds__(256) void k_push_adagrad(TableDev t, const int64_t* __restrict__ rows,
+                                                      const float* __restrict__ push, int push_stride,
+                                                      const int32_t* n_dev, int64_t n, SparseSGDConfig cfg,
+                                                      uint64_t seed) {
+  const int64_t nn = n_dev ? (int64_t)*n_dev : n;
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nn) return;
+  const int64_t r = rows[u];
+  if (r < 0) return;
+  const RowLayout l = make_row_layout(t.dim);
+  float* v = t.values + r * (int64_t)t.stride;
+  const float* g = push + u * push_stride;
+  const float slot = g[kPushSlot], g_show = g[kPushShow], g_click = g[kPushClick];
+  v[l.slot] = slot;
+  const float show = v[kShow] + g_show;
+  const float click = v[kClick] + g_click;
+  v[kShow] = show;
+  v[kClick] = click;
+  v[l.delta_score] += cfg.nonclk_coeff * (g_show - g_click) + cfg.clk_coeff * g_click;
+  v[l.unseen_days] = 0.f;
+  const float scale = g_show > 0.f ? g_show : 1.f;
+  float lr = cfg.learning_rate, mf_lr = cfg.mf_learning_rate;
+  if (cfg.use_feature_lr && slot != cfg.nodeid_slot) { lr = cfg.feature_learning_rate; mf_lr = cfg.feature_learning_rate; }
+  {  // embed_w (1-d Adagrad)
+    const float g2 = v[l.embed_g2sum];
+    const float ratio = lr * sqrtf(cfg.initial_g2sum / (cfg.initial_g2sum + g2));
+    const float sg = g[kPushEmbedG] / scale;
+    v[kEmbedW] = clampf(v[kEmbedW] + sg * ratio, cfg.min_bound, cfg.max_bound);
+    v[l.embed_g2sum] = g2 + sg * sg;
+  }
+  if (v[l.mf_size] == 0.f) {
+    if (cfg.nonclk_coeff * (show - click) + cfg.clk_coeff * click >= cfg.mf_create_thresholds) {
+      v[l.mf_size] = 1.f;
+      const uint64_t salt = seed ^ (uint64_t)r * 0x9E3779B97F4A7C15ULL;
+      for (int d = 0; d < t.dim; ++d) v[kEmbedx + d] = hash_uniform(salt, d) * cfg.mf_initial_range;
+    }
+  } else {
+    const float g2 = v[l.embedx_g2sum];
+    const float ratio = mf_lr * sqrtf(cfg.mf_initial_g2sum / (cfg.mf_initial_g2sum + g2));
+    float add = 0.f;
+    for (int d = 0; d < t.dim; ++d) {
+      const float sg = g[kPushEmbedxG + d] / scale;
+      v[kEmbedx + d] = clampf(v[kEmbedx + d] + sg * ratio, cfg.mf_min_bound, cfg.mf_max_bound);
+      add += sg * sg;
+    }
+    v[l.embedx_g2sum] = g2 + add / (float)t.dim;
+  }
+}
+
+// ---------------------------------------------------------------- sharding helpers
+__device__ __forceinline__ int64_t owner_lower_bound(const uint64_t* h, int64_t U, uint32_t o, uint32_t N) {
+  int64_t lo = 0, hi = U;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (owner_of(h[mid], N) < o) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void k_shard_pack_send(const uint64_t* __restrict__ uniq_h, const int32_t* u_count, int nranks,
+                                  int64_t cap, uint64_t* __restrict__ send, int32_t* overflow) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)nranks * cap) return;
+  const uint32_t o = (uint32_t)(t / cap);
+  const int64_t j = t % cap;
+  const int64_t U = *u_count;
+  const int64_t st = owner_lower_bound(uniq_h, U, o, nranks);
+  const int64_t en = owner_lower_bound(uniq_h, U, o + 1, nranks);
+  const int64_t cnt = en - st;
+  send[t] = (j < cnt) ? uniq_h[st + j] : kEmptyKey;
+  if (j == 0 && cnt > cap) atomicOr(overflow, 1);
+}
+
+__global__ void k_shard_index(const uint64_t* __restrict__ uniq_h, const int32_t* u_count, int64_t u_cap,
+                              int nranks, int64_t cap, int64_t* __restrict__ send_index) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= u_cap) return;
+  const int64_t U = *u_count;
+  if (u >= U) { send_index[u] = -1; return; }
+  const uint32_t o = owner_of(uniq_h[u], nranks);
+  const int64_t st = owner_lower_bound(uniq_h, U, o, nranks);
+  const int64_t j = u - st;
+  send_index[u] = j < cap ? (int64_t)o * cap + j : -1;
+}
+
+__global__ void k_gather_by_uid(const float* __restrict__ src, int src_stride, const int32_t* __restrict__ uid,
+                                int64_t n, float* __restrict__ out, int out_stride, int width) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int32_t u = uid[j];
+  float* o = out + j * out_stride;
+  if (u < 0) {
+    for (int c = 0; c < width; ++c) o[c] = 0.f;
+    return;
+  }
+  const float* s = src + (int64_t)u * src_stride;
+  if ((width & 3) == 0 && (src_stride & 3) == 0 && (out_stride & 3) == 0) {
+    const float4* s4 = reinterpret_cast<const float4*>(s);
+    float4* o4 = reinterpret_cast<float4*>(o);
+    for (int c = 0; c < width / 4; ++c) o4[c] = s4[c];
+  } else {
+    for (int c = 0; c < width; ++c) o[c] = s[c];
+  }
+}
+
+inline unsigned int nblk(int64_t n, int per = 256) {
+  int64_t b = (n + per - 1) / per;
+  return (unsigned int)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+void launch_fill_occurrence(const int64_t* lod, int S, int B, int32_t* occ_slot, int32_t* occ_ins,
+                            hipStream_t s) {
+  if ((int64_t)S * B == 0) return;
+  hipLaunchKernelGGL(k_fill_occ, dim3(nblk((int64_t)S * B)), dim3(256), 0, s, lod, S, B, occ_slot, occ_ins);
+}
+
+void launch_gather_pull(const TableDev& t, const int64_t* rows, const int32_t* n_dev, int64_t n,
+                        float* out, int out_stride, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather_pull, dim3(nblk(n)), dim3(256), 0, s, t, rows, n_dev, n, out, out_stride);
+}
+
+int seqpool_cvm_out_width(const SeqpoolCvmArgs& a) {
+  return a.use_cvm ? (a.clk_filter ? a.E - 1 : a.E) : a.E - a.cvm_offset;
+}
+
+void launch_seqpool_cvm_fwd(const SeqpoolCvmArgs& a, hipStream_t s) {
+  const int64_t n = (int64_t)a.S * a.B;
+  if (n == 0) return;
+  const dim3 g(nblk(n)), b(256);
+  const bool aligned = (a.src_stride % 4) == 0;
+  switch (aligned ? a.E : -1) {
+    case 11: hipLaunchKernelGGL(k_seqpool_cvm<11>, g, b, 0, s, a); break;
+    case 12: hipLaunchKernelGGL(k_seqpool_cvm<12>, g, b, 0, s, a); break;
+    case 19: hipLaunchKernelGGL(k_seqpool_cvm<19>, g, b, 0, s, a); break;
+    case 35: hipLaunchKernelGGL(k_seqpool_cvm<35>, g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL(k_seqpool_cvm_generic, g, b, 0, s, a); break;
+  }
+}
+
+void launch_push_merge(const PushMergeArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  const dim3 g(nblk(a.n)), b(256);
+  DoutSource src{a};
+  const float neg_bs = -a.bs_scale;
+  // values [show, click, embed_g, embedx_g...] -> scale from index 2 on
+  switch (a.dim) {
+    case 8: hipLaunchKernelGGL((k_push_merge<11, DoutSource>), g, b, 0, s, src, a.perm, a.uid, a.n_valid, a.n, a.push, a.push_stride, a.push_index, neg_bs, 2); break;
+    case 16: hipLaunchKernelGGL((k_push_merge<19, DoutSource>), g, b, 0, s, src, a.perm, a.uid, a.n_valid, a.n, a.push, a.push_stride, a.push_index, neg_bs, 2); break;
+    case 32: hipLaunchKernelGGL((k_push_merge<35, DoutSource>), g, b, 0, s, src, a.perm, a.uid, a.n_valid, a.n, a.push, a.push_stride, a.push_index, neg_bs, 2); break;
+    case 4: hipLaunchKernelGGL((k_push_merge<7, DoutSource>), g, b, 0, s, src, a.perm, a.uid, a.n_valid, a.n, a.push, a.push_stride, a.push_index, neg_bs, 2); break;
+    default: break;  // unsupported dims rejected on the host side
+  }
+}
+
+void launch_push_merge_records(const float* rec, int rec_stride, const int32_t* perm,
+                               const int32_t* uid, const int32_t* n_valid, int64_t n, int dim,
+                               float* out, int out_stride, hipStream_t s) {
+  if (n <= 0) return;
+  const dim3 g(nblk(n)), b(256);
+  RecordSource src{rec, rec_stride};
+  switch (dim) {
+    case 8: hipLaunchKernelGGL((k_push_merge<11, RecordSource>), g, b, 0, s, src, perm, uid, n_valid, n, out, out_stride, (const int64_t*)nullptr, 1.f, 1 << 20); break;
+    case 16: hipLaunchKernelGGL((k_push_merge<19, RecordSource>), g, b, 0, s, src, perm, uid, n_valid, n, out, out_stride, (const int64_t*)nullptr, 1.f, 1 << 20); break;
+    case 32: hipLaunchKernelGGL((k_push_merge<35, RecordSource>), g, b, 0, s, src, perm, uid, n_valid, n, out, out_stride, (const int64_t*)nullptr, 1.f, 1 << 20); break;
+    case 4: hipLaunchKernelGGL((k_push_merge<7, RecordSource>), g, b, 0, s, src, perm, uid, n_valid, n, out, out_stride, (const int64_t*)nullptr, 1.f, 1 << 20); break;
+    default: break;
+  }
+}
+
+void launch_push_adagrad(const TableDev& t, const int64_t* rows, const float* push,
+                         int push_stride, const int32_t* n_dev, int64_t n,
+                         const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_push_adagrad, dim3(nblk(n)), dim3(256), 0, s, t, rows, push, push_stride, n_dev, n, cfg, seed);
+}
+
+void launch_zero_rows(float* buf, int stride, const int32_t* n_dev, int64_t cap, hipStream_t s) {
+  (void)n_dev;
+  (void)hipMemsetAsync(buf, 0, (size_t)cap * stride * sizeof(float), s);
+}
+
+void launch_shard_pack(const uint64_t* uniq_h, const int32_t* u_count, int64_t u_cap, int nranks,
+                       int64_t cap, uint64_t* send, int64_t* send_index, int32_t* overflow,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(k_shard_pack_send, dim3(nblk((int64_t)nranks * cap)), dim3(256), 0, s, uniq_h, u_count, nranks, cap, send, overflow);
+  hipLaunchKernelGGL(k_shard_index, dim3(nblk(u_cap)), dim3(256), 0, s, uniq_h, u_count, u_cap, nranks, cap, send_index);
+}
+
+void launch_gather_by_uid(const float* src, int src_stride, const int32_t* uid, int64_t n,
+                          float* out, int out_stride, int width, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather_by_uid, dim3(nblk(n)), dim3(256), 0, s, src, src_stride, uid, n, out, out_stride, width);
+}
+
+}  // namespace pbx

@@ -1,0 +1,160 @@
+"""Dense CTR ops with autograd: data_norm, FM interaction, sigmoid+logloss,
+streaming AUC.  GPU tensors run the hand-written gfx950 kernels
+(csrc/hip/dense_ops.hip); CPU tensors run ``reference``.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+from . import reference as ref
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ---------------------------------------------------------------- data_norm
+class _DataNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bsize, bsum, bsq, scale_w, bias, eps, decay, sync_group, update, training):
+        x = x.contiguous().float()
+        if _gpu(x):
+            y, means, scales = _native.hip().data_norm_fwd(x, bsize, bsum, bsq, scale_w, bias)
+        else:
+            y, means, scales = ref.data_norm_fwd(x, bsize, bsum, bsq, scale_w, bias)
+        ctx.save_for_backward(x, means, scales, bsize, bsum, bsq, scale_w)
+        ctx.eps, ctx.decay, ctx.group, ctx.update, ctx.training = eps, decay, sync_group, update, training
+        ctx.has_sw = scale_w is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, means, scales, bsize, bsum, bsq, scale_w = ctx.saved_tensors
+        dy = dy.contiguous().float()
+        if _gpu(x):
+            dx, stats = _native.hip().data_norm_bwd(x, dy, means, scales, ctx.eps, True, scale_w)
+        else:
+            dx, stats = ref.data_norm_bwd(x, dy, means, scales, ctx.eps, scale_w)
+        if ctx.group is not None and dist.is_initialized() and dist.get_world_size(ctx.group) > 1:
+            # one fused all-reduce of [3, C] (reference does 3 separate ones,
+            # data_norm_op.cu:203-230)
+            dist.all_reduce(stats, group=ctx.group)
+        if ctx.update and ctx.training:
+            if _gpu(x):
+                _native.hip().data_norm_update(bsize, bsum, bsq, stats, ctx.decay)
+            else:
+                ref.data_norm_update(bsize, bsum, bsq, stats, ctx.decay)
+        dsw = dbias = None
+        if ctx.has_sw:
+            xn = (x - means) * scales
+            dsw = (dy * xn).sum(0)
+            dbias = dy.sum(0)
+        return dx, None, None, None, dsw, dbias, None, None, None, None, None
+
+
+class DataNorm(torch.nn.Module):
+    """data_norm layer (py/fluid/layers/nn.py:3490-3676): running summary
+    normalisation; summaries are updated by the backward with decay
+    0.9999999 (not by the optimizer)."""
+
+    def __init__(self, C: int, epsilon: float = 1e-5, summary_decay_rate: float = 0.9999999,
+                 sync_stats: bool = False, enable_scale_and_shift: bool = False, batch_size_default: float = 1e4,
+                 batch_sum_default: float = 0.0, batch_square_sum_default: float = 1e4, slot_dim: int = -1):
+        super().__init__()
+        self.C = C
+        self.eps = epsilon
+        self.decay = summary_decay_rate
+        self.sync_stats = sync_stats
+        self.slot_dim = slot_dim
+        self.register_buffer("batch_size", torch.full((C,), float(batch_size_default)))
+        self.register_buffer("batch_sum", torch.full((C,), float(batch_sum_default)))
+        self.register_buffer("batch_square_sum", torch.full((C,), float(batch_square_sum_default)))
+        if enable_scale_and_shift:
+            self.scale_w = torch.nn.Parameter(torch.ones(C))
+            self.bias = torch.nn.Parameter(torch.zeros(C))
+        else:
+            self.scale_w = None
+            self.bias = None
+        self.update_norm = True
+        self.group = None
+
+    def forward(self, x):
+        return _DataNorm.apply(x, self.batch_size, self.batch_sum, self.batch_square_sum, self.scale_w, self.bias,
+                               self.eps, self.decay, self.group if self.sync_stats else None, self.update_norm,
+                               self.training)
+
+
+# ---------------------------------------------------------------- FM
+class _FM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, S, D, col0, fstride):
+        x = x.contiguous().float()
+        if _gpu(x):
+            out = _native.hip().fm_fwd(x, S, D, col0, fstride)
+        else:
+            out = ref.fm_fwd(x, S, D, col0, fstride)
+        ctx.save_for_backward(x)
+        ctx.args = (S, D, col0, fstride)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x,) = ctx.saved_tensors
+        S, D, col0, fstride = ctx.args
+        dout = dout.contiguous().float()
+        if _gpu(x):
+            dx = torch.zeros_like(x)
+            _native.hip().fm_bwd(x, dout, S, D, col0, fstride, dx, False)
+        else:
+            with torch.enable_grad():
+                xx = x.detach().requires_grad_(True)
+                y = ref.fm_fwd(xx, S, D, col0, fstride)
+                (dx,) = torch.autograd.grad(y, xx, dout)
+        return dx, None, None, None, None
+
+
+def fm_interaction(x: torch.Tensor, S: int, D: int, col0: int, fstride: int) -> torch.Tensor:
+    """DeepFM 2nd-order term 0.5*sum_d[(sum_s v)^2 - sum_s v^2] over S fields of
+    dim D stored at x[:, col0 + s*fstride + d]."""
+    return _FM.apply(x, S, D, col0, fstride)
+
+
+# ---------------------------------------------------------------- loss
+class _SigmoidLogLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logit, label):
+        logit = logit.contiguous().float().view(-1)
+        label = label.contiguous().float().view(-1)
+        B = logit.numel()
+        if _gpu(logit):
+            pred, loss, dz = _native.hip().sigmoid_logloss(logit, label, 1.0 / B)
+        else:
+            pred, loss, dz = ref.sigmoid_logloss(logit, label, 1.0 / B)
+        ctx.save_for_backward(dz)
+        ctx.mark_non_differentiable(pred)
+        return loss[0] / B, pred
+
+    @staticmethod
+    def backward(ctx, gl, gp):
+        (dz,) = ctx.saved_tensors
+        return dz * gl, None
+
+
+def sigmoid_logloss(logit: torch.Tensor, label: torch.Tensor):
+    """(mean log-loss, sigmoid prediction) with the gradient fused."""
+    return _SigmoidLogLoss.apply(logit, label)
+
+
+# ---------------------------------------------------------------- AUC
+def auc_accumulate(pred: torch.Tensor, label: torch.Tensor, table: torch.Tensor, stats: torch.Tensor,
+                   mask: Optional[torch.Tensor] = None):
+    pred = pred.detach().contiguous().float().view(-1)
+    label = label.detach().contiguous().float().view(-1)
+    if _gpu(pred):
+        _native.hip().auc_accumulate(pred, label, mask, table, stats)
+    else:
+        ref.auc_accumulate(pred, label, table, stats, mask)

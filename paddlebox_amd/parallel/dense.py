@@ -1,0 +1,116 @@
+"""Dense-parameter arena + data-parallel sync + fused optimizer.
+
+All dense parameters of a model live in ONE contiguous fp32 buffer and their
+gradients in another (the reference packs params for fused sync,
+``boxps_worker.cc:481-520`` AllocParamTensor, and ``coalesce_tensor`` for
+gradient fusion).  That makes data-parallel sync a single RCCL all-reduce
+(one bucket: CTR MLPs are a few MB, well inside the one-shot regime of the
+xGMI mesh) and the optimizer a single fused Adam launch.
+
+Sync modes (``trainer_desc.proto:121-129`` / ``boxps_worker.cc:1191-1258``):
+  * ``grad_allreduce``  -- all-reduce grads every step (transpiler GradAllReduce)
+  * ``kstep``           -- local steps, parameter averaging every k steps
+                            (sync_dense_mode 2, DenseKStepALL)
+  * ``none``            -- no sync
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+from ..ops import reference as ref
+
+
+class DenseArena:
+    def __init__(self, params: Iterable[torch.nn.Parameter], device: torch.device):
+        self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        # pad each param to 4 floats so every view is 16-B aligned
+        sizes = [(p.numel() + 3) // 4 * 4 for p in self.params]
+        total = sum(sizes)
+        self.numel = n
+        self.flat = torch.zeros(total, device=device)
+        self.grad = torch.zeros(total, device=device)
+        off = 0
+        self.views = []
+        for p, sz in zip(self.params, sizes):
+            v = self.flat[off:off + p.numel()].view_as(p)
+            v.copy_(p.data)
+            p.data = v
+            p.grad = self.grad[off:off + p.numel()].view_as(p)
+            self.views.append((off, p.numel()))
+            off += sz
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return {"flat": self.flat}
+
+
+class FlatAdam:
+    """Adam over the whole arena in one kernel (Paddle adam semantics)."""
+
+    def __init__(self, arena: DenseArena, lr: float = 1e-3, beta1: float = 0.9, beta2: float = 0.999,
+                 epsilon: float = 1e-8, weight_decay: float = 0.0):
+        self.a = arena
+        self.lr, self.b1, self.b2, self.eps, self.wd = lr, beta1, beta2, epsilon, weight_decay
+        self.m = torch.zeros_like(arena.flat)
+        self.v = torch.zeros_like(arena.flat)
+        self.t = 0
+        # beta powers kept on the host (deterministic; no per-step D2H)
+        self.b1pow = 1.0
+        self.b2pow = 1.0
+
+    def step(self, grad_scale: float = 1.0):
+        self.t += 1
+        self.b1pow *= self.b1
+        self.b2pow *= self.b2
+        if self.a.flat.is_cuda:
+            _native.hip().adam_flat(self.a.flat, self.a.grad, self.m, self.v, self.lr, self.b1, self.b2, self.eps,
+                                    self.b1pow, self.b2pow, grad_scale, self.wd)
+        else:
+            ref.adam_flat(self.a.flat, self.a.grad, self.m, self.v, self.lr, self.b1, self.b2, self.eps, self.b1pow,
+                          self.b2pow, grad_scale, self.wd)
+
+    def state_dict(self):
+        return {"m": self.m, "v": self.v, "t": self.t, "b1pow": self.b1pow, "b2pow": self.b2pow}
+
+    def load_state_dict(self, sd):
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        self.t, self.b1pow, self.b2pow = sd["t"], sd["b1pow"], sd["b2pow"]
+
+
+class DenseSync:
+    """Data-parallel dense synchronisation over RCCL (or gloo on CPU)."""
+
+    def __init__(self, arena: DenseArena, mode: str = "grad_allreduce", k: int = 1, group=None):
+        self.a = arena
+        self.mode = mode
+        self.k = max(1, k)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.steps = 0
+
+    def grad_scale(self) -> float:
+        return 1.0 / self.world if (self.mode == "grad_allreduce" and self.world > 1) else 1.0
+
+    def before_step(self):
+        """Called after backward, before the optimizer."""
+        if self.world > 1 and self.mode == "grad_allreduce":
+            dist.all_reduce(self.a.grad, group=self.group)
+
+    def after_step(self):
+        self.steps += 1
+        if self.world > 1 and self.mode == "kstep" and self.steps % self.k == 0:
+            self.sync_params()
+
+    def sync_params(self):
+        """Parameter averaging (boxps_worker.cc:1235-1239: sum then x 1/devices)."""
+        if self.world > 1:
+            dist.all_reduce(self.a.flat, group=self.group)
+            self.a.flat.mul_(1.0 / self.world)

@@ -1,0 +1,405 @@
+"""Per-batch sparse pipeline: dedup -> (key all-to-all) -> probe -> pull ->
+fused seqpool+CVM, and the mirror push path with fused sparse Adagrad.
+
+This is the engine behind ``pull_box_sparse``/``push_box_sparse`` and
+``fused_seqpool_cvm`` (reference pipeline: ``box_wrapper_impl.h:25-234``
+pull, ``:373-522`` push; BoxPS ``PullSparseGPU/PushSparseGPU`` closed).
+
+MI355X design points
+--------------------
+* No host synchronisation per batch: the unique count lives on the device
+  and every kernel is launched for the static upper bound, so a whole training
+  step can be captured in one HIP graph.
+* Sorting by ``h = mix64(key)`` makes the unique list come out grouped by owner
+  GPU (``owner = floor(h*N/2^64)`` is monotone in h): the key all-to-all needs no
+  partition pass.  The exchange uses fixed per-peer capacity ``C`` so
+  ``all_to_all_single`` has static equal splits (graph-capturable, one RCCL
+  call per direction, ragged bytes padded to C).  Overflow (a peer receiving
+  more than C uniques -- needs adversarial keys) is flagged on the device and
+  checked at pass end.
+* One GPU (world=1): the forward reads value rows straight out of the table.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+from ..ops import reference as ref
+from .config import PSConfig, SparseSGDConfig, padded, pull_width, push_width
+from .cpu_table import CpuSparseTable
+from .gpu_table import GpuSparseTable
+
+
+@dataclass
+class SeqpoolParams:
+    use_cvm: bool = True
+    cvm_offset: int = 2
+    clk_filter: bool = False
+    pad_value: float = 0.0
+    need_filter: bool = False
+    show_coeff: float = 0.2
+    clk_coeff: float = 1.0
+    threshold: float = 0.96
+    quant_ratio: int = 0
+    embed_threshold_filter: bool = False
+    embed_threshold: float = 0.0
+    embed_thres_size: int = 0
+
+    def out_width(self, E: int) -> int:
+        return ref.seqpool_cvm_out_width(E, self.use_cvm, self.cvm_offset, self.clk_filter)
+
+
+@dataclass
+class PullState:
+    """What the push of the same batch needs (DeviceBoxData equivalent,
+    box_wrapper.h:378-435)."""
+
+    B: int
+    S: int
+    L: int
+    lod: torch.Tensor
+    uid: torch.Tensor = None
+    perm: torch.Tensor = None
+    counts: torch.Tensor = None  # device [U, n_valid]
+    rows: torch.Tensor = None  # world==1: table rows per unique
+    send_index: Optional[torch.Tensor] = None
+    rows_r: Optional[torch.Tensor] = None
+    extra: dict = field(default_factory=dict)
+
+
+class SparseEngine:
+    """Sparse embedding engine for one rank (one GPU, or the CPU)."""
+
+    def __init__(
+        self,
+        cfg: PSConfig,
+        max_keys: int,
+        device: torch.device,
+        capacity: int = 1 << 20,
+        slot_ids: Optional[List[float]] = None,
+        group=None,
+        cap_factor: float = 1.25,
+        auto_insert: bool = False,
+    ):
+        self.cfg = cfg
+        self.dim = cfg.embedx_dim
+        self.E = pull_width(self.dim)
+        self.P = padded(self.E)  # exchanged pull record stride (16-B rows)
+        self.Q = padded(push_width(self.dim))
+        self.device = torch.device(device)
+        self.max_keys = int(max_keys)
+        self.group = group
+        self.world = dist.get_world_size(group) if (group is not None or (dist.is_available() and dist.is_initialized())) else 1
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        self.auto_insert = auto_insert
+        self.test_mode = False
+        self.is_gpu = self.device.type == "cuda"
+        shard_cap = int(math.ceil(capacity / self.world)) if self.world > 1 else capacity
+        if self.is_gpu:
+            self.table = GpuSparseTable(self.dim, shard_cap, self.device)
+            self._hip = _native.hip()
+            self._sgd_native = cfg.sgd.to_native(self._hip)
+            with torch.cuda.device(self.device):
+                self.ws = self._hip.DedupWorkspace(self.max_keys, self.device.index or 0)
+            self.occ_slot = torch.empty(self.max_keys, dtype=torch.int32, device=self.device)
+            self.occ_ins = torch.empty(self.max_keys, dtype=torch.int32, device=self.device)
+            if self.world > 1:
+                self.C = int(math.ceil(self.max_keys / self.world * cap_factor)) + 64
+                n = self.world * self.C
+                with torch.cuda.device(self.device):
+                    self.ws_r = self._hip.DedupWorkspace(n, self.device.index or 0)
+                self.send = torch.empty(n, dtype=torch.int64, device=self.device)
+                self.recv = torch.empty(n, dtype=torch.int64, device=self.device)
+                self.send_index = torch.empty(self.max_keys, dtype=torch.int64, device=self.device)
+                self.overflow = torch.zeros(1, dtype=torch.int32, device=self.device)
+                self.resp = torch.empty(n, self.P, device=self.device)
+                self.resp_back = torch.empty(n, self.P, device=self.device)
+                self.push_send = torch.empty(n, self.Q, device=self.device)
+                self.push_recv = torch.empty(n, self.Q, device=self.device)
+                self.push_merged = torch.empty(n, self.Q, device=self.device)
+            else:
+                self.push_buf = torch.empty(self.max_keys, self.Q, device=self.device)
+        else:
+            self.table = CpuSparseTable(self.dim)
+        self.slot_ids = torch.tensor(slot_ids if slot_ids is not None else [], dtype=torch.float32,
+                                     device=self.device)
+        self._seed = 1234
+
+    # ------------------------------------------------------------------ build
+    def set_slot_ids(self, slot_ids: List[float]):
+        self.slot_ids = torch.tensor(slot_ids, dtype=torch.float32, device=self.device)
+
+    def register_keys(self, keys: torch.Tensor, init_embedx: bool = False):
+        """Feed-pass key registration: make every key of the coming pass
+        resident at its owner shard (BoxPS FeedPass/EndFeedPass,
+        box_wrapper.cc:120-169).  Collective over the group when world > 1."""
+        keys = keys.reshape(-1).to(self.device)
+        keys = keys[keys != -1]
+        if self.is_gpu:
+            h = torch.unique(ref.mix64(keys))
+        else:
+            h = torch.unique(ref.mix64(keys))
+        if self.world > 1:
+            owner = ref.owner_of(h, self.world)
+            order = torch.argsort(owner, stable=True)
+            h = h[order]
+            counts = torch.bincount(owner, minlength=self.world)
+            in_counts = torch.empty_like(counts)
+            dist.all_to_all_single(in_counts, counts, group=self.group)
+            recv = torch.empty(int(in_counts.sum()), dtype=torch.int64, device=self.device)
+            dist.all_to_all_single(recv, h, in_counts.tolist(), counts.tolist(), group=self.group)
+            h = torch.unique(recv)
+        self.table.insert_mixed(h, self.cfg.sgd, init_embedx=init_embedx)
+
+    def insert_local_mixed(self, h: torch.Tensor, init_embedx: bool = False):
+        """Insert mixed keys already known to belong to this shard."""
+        self.table.insert_mixed(h, self.cfg.sgd, init_embedx=init_embedx)
+
+    # ------------------------------------------------------------------ pull
+    def pull_seqpool_cvm(self, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int, out: torch.Tensor,
+                         col_offset: int, sp: SeqpoolParams) -> PullState:
+        """Fused pull + seqpool + CVM written into out[:, col_offset:...].
+
+        keys: int64 [Lcap] slot-major flat keys, -1 padded; lod: int64 [S*(B+1)].
+        """
+        if not self.is_gpu:
+            return self._cpu_pull_seqpool(keys, lod, B, S, out, col_offset, sp)
+        st = self._pull_common(keys, lod, B, S)
+        h = self._hip
+        if self.world == 1:
+            src, src_index = self.table.values, st.rows
+        else:
+            src, src_index = self.resp_back, self.send_index
+        h.seqpool_cvm_fwd(src, src_index, self.ws.uid, lod, S, B, self.E, out, col_offset, sp.use_cvm,
+                          sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter, sp.show_coeff, sp.clk_coeff,
+                          sp.threshold, sp.quant_ratio, sp.embed_threshold_filter, sp.embed_threshold,
+                          sp.embed_thres_size)
+        return st
+
+    def _pull_common(self, keys, lod, B, S) -> PullState:
+        h = self._hip
+        L = keys.numel()
+        assert L <= self.max_keys, f"batch has {L} keys > engine max_keys {self.max_keys}"
+        self.ws.run(keys, False)
+        h.fill_occurrence(lod, S, B, self.occ_slot, self.occ_ins)
+        st = PullState(B=B, S=S, L=L, lod=lod, uid=self.ws.uid, perm=self.ws.perm, counts=self.ws.u_count)
+        if self.world == 1:
+            st.rows = self.table.probe(self.ws.uniq_h[:L], self.ws.u_count)
+            if self.auto_insert and not self.test_mode:
+                self._auto_insert(st, L)
+            return st
+        # sharded: pack per-owner, exchange keys, owner-side dedup/probe/gather
+        h.shard_pack(self.ws.uniq_h, self.ws.u_count, self.world, self.C, self.send, self.send_index[:L],
+                     self.overflow)
+        dist.all_to_all_single(self.recv, self.send, group=self.group)
+        self.ws_r.run(self.recv, True)
+        n = self.world * self.C
+        rows_r = self.table.probe(self.ws_r.uniq_h, self.ws_r.u_count)
+        if self.auto_insert and not self.test_mode:
+            miss = (rows_r[: int(self.ws_r.u_count[0].item())] < 0)
+            if bool(miss.any()):
+                U = int(self.ws_r.u_count[0].item())
+                self.table.insert_mixed(self.ws_r.uniq_h[:U][miss], self.cfg.sgd)
+                rows_r = self.table.probe(self.ws_r.uniq_h, self.ws_r.u_count)
+        pulled = self.table.t.gather_pull(rows_r, self.ws_r.u_count, self.P)
+        h.gather_by_uid(pulled, self.ws_r.uid, self.resp, self.P)
+        dist.all_to_all_single(self.resp_back, self.resp, group=self.group)
+        st.send_index = self.send_index[:L]
+        st.rows_r = rows_r
+        return st
+
+    def _auto_insert(self, st: PullState, L: int):
+        U = int(self.ws.u_count[0].item())
+        miss = st.rows[:U] < 0
+        if bool(miss.any()):
+            self.table.insert_mixed(self.ws.uniq_h[:U][miss], self.cfg.sgd)
+            st.rows = self.table.probe(self.ws.uniq_h[:L], self.ws.u_count)
+
+    # ------------------------------------------------------------------ push
+    def push_seqpool_cvm(self, st: PullState, dout: torch.Tensor, cvm: torch.Tensor, col_offset: int,
+                         sp: SeqpoolParams, bs_scale: float):
+        """Backward of the fused op = push_box_sparse with fused Adagrad."""
+        if self.test_mode:
+            return
+        if not self.is_gpu:
+            return self._cpu_push(st, dout, cvm, col_offset, sp, bs_scale)
+        h = self._hip
+        L = st.L
+        dout = dout.contiguous()
+        if self.world == 1:
+            push = self.push_buf
+            push[:L].zero_()
+            h.push_merge(dout, col_offset, cvm.contiguous(), sp.cvm_offset, sp.use_cvm, sp.clk_filter, self.E,
+                         self.ws.perm[:L], self.ws.uid, self.occ_slot, self.occ_ins, self._slot_ids(st.S),
+                         self.ws.u_count[1:], push[:L], None, float(bs_scale), self.dim)
+            self._seed += 1
+            self.table.t.push_adagrad(st.rows, push[:L], self.ws.u_count, self._sgd_native, self._seed)
+            return
+        self.push_send.zero_()
+        h.push_merge(dout, col_offset, cvm.contiguous(), sp.cvm_offset, sp.use_cvm, sp.clk_filter, self.E,
+                     self.ws.perm[:L], self.ws.uid, self.occ_slot, self.occ_ins, self._slot_ids(st.S),
+                     self.ws.u_count[1:], self.push_send, st.send_index, float(bs_scale), self.dim)
+        dist.all_to_all_single(self.push_recv, self.push_send, group=self.group)
+        self.push_merged.zero_()
+        h.push_merge_records(self.push_recv, self.ws_r.perm, self.ws_r.uid, self.ws_r.u_count[1:], self.dim,
+                             self.push_merged)
+        self._seed += 1
+        self.table.t.push_adagrad(st.rows_r, self.push_merged, self.ws_r.u_count, self._sgd_native, self._seed)
+
+    def _slot_ids(self, S: int) -> torch.Tensor:
+        if self.slot_ids.numel() < S:
+            self.slot_ids = torch.arange(S, dtype=torch.float32, device=self.device)
+        return self.slot_ids
+
+    def check_overflow(self) -> bool:
+        if self.world > 1 and self.is_gpu:
+            return bool(self.overflow.item())
+        return False
+
+    # ------------------------------------------------------------------ unfused pull (pull_box_sparse)
+    def pull_records(self, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int):
+        """pull_box_sparse: per-occurrence pull records [L, 3+D] (box_wrapper.cu:74-143)."""
+        L = keys.numel()
+        if not self.is_gpu:
+            uniq, uid = ref.dedup(keys)
+            rows = self.table.probe(uniq)
+            pulled = self.table.gather_pull(rows, self.P)
+            st = PullState(B=B, S=S, L=L, lod=lod, uid=uid, rows=rows)
+            st.extra["uniq"] = uniq
+            recs = torch.where((keys != -1).unsqueeze(1), pulled[uid.long().clamp(min=0)], torch.zeros(1))
+            return recs[:, : self.E], st
+        st = self._pull_common(keys, lod, B, S)
+        if self.world == 1:
+            pulled = self.table.t.gather_pull(st.rows, self.ws.u_count, self.P)
+            recs = torch.empty(L, self.P, device=self.device)
+            self._hip.gather_by_uid(pulled, self.ws.uid[:L], recs, self.P)
+        else:
+            # resp_back rows indexed by send_index[uid]
+            idx = self.send_index[:L][self.ws.uid[:L].long().clamp(min=0)]
+            ok = (self.ws.uid[:L] >= 0) & (idx >= 0)
+            recs = torch.where(ok.unsqueeze(1), self.resp_back[idx.clamp(min=0)], torch.zeros((), device=self.device))
+        return recs[:, : self.E], st
+
+    def push_records(self, st: PullState, grads: torch.Tensor, cvm_cols: int, bs_scale: float,
+                     slot_of_occ: Optional[torch.Tensor] = None):
+        """push_box_sparse from per-occurrence grads [L, 3+D] of the pull output:
+        columns < cvm_cols are show/click statistics, the rest are scaled by
+        -bs (box_wrapper.cu:344-475)."""
+        if self.test_mode:
+            return
+        L = st.L
+        D = self.dim
+        g = grads.float()
+        rec = torch.zeros(L, self.Q, device=grads.device)
+        if slot_of_occ is None:
+            slot_of_occ, _ = ref.occurrence_map(st.lod.cpu(), st.S, st.B)
+            slot_of_occ = slot_of_occ.to(grads.device)
+        rec[:, 0] = self._slot_ids(st.S)[slot_of_occ.long()]
+        rec[:, 1] = g[:, 0]
+        rec[:, 2] = g[:, 1]
+        rec[:, 3:4 + D] = g[:, 2:3 + D] * (-bs_scale)
+        if not self.is_gpu:
+            U = st.extra["uniq"].numel()
+            merged = torch.zeros(U, self.Q)
+            ok = st.uid >= 0
+            merged.index_add_(0, st.uid[ok].long(), rec[ok])
+            merged[:, 0] = 0
+            merged[st.uid[ok].long(), 0] = rec[ok, 0]
+            self.table.push_adagrad(st.rows, merged, self.cfg.sgd)
+            return
+        h = self._hip
+        if self.world == 1:
+            push = self.push_buf
+            push[:L].zero_()
+            h.push_merge_records(rec, self.ws.perm[:L], self.ws.uid, self.ws.u_count[1:], D, push[:L])
+            self._seed += 1
+            self.table.t.push_adagrad(st.rows, push[:L], self.ws.u_count, self._sgd_native, self._seed)
+            return
+        # merge locally per unique into the owner send layout, then exchange
+        U_cap = L
+        merged = torch.zeros(U_cap, self.Q, device=self.device)
+        h.push_merge_records(rec, self.ws.perm[:L], self.ws.uid, self.ws.u_count[1:], D, merged)
+        self.push_send.zero_()
+        idx = st.send_index
+        ok = idx >= 0
+        self.push_send[idx[ok]] = merged[ok]
+        dist.all_to_all_single(self.push_recv, self.push_send, group=self.group)
+        self.push_merged.zero_()
+        h.push_merge_records(self.push_recv, self.ws_r.perm, self.ws_r.uid, self.ws_r.u_count[1:], D,
+                             self.push_merged)
+        self._seed += 1
+        self.table.t.push_adagrad(st.rows_r, self.push_merged, self.ws_r.u_count, self._sgd_native, self._seed)
+
+    # ------------------------------------------------------------------ CPU path
+    def _cpu_pull_seqpool(self, keys, lod, B, S, out, col_offset, sp: SeqpoolParams) -> PullState:
+        L = keys.numel()
+        valid = keys != -1
+        uniq, uid = ref.dedup(keys[valid])
+        full_uid = torch.full((L,), -1, dtype=torch.int32)
+        full_uid[valid] = uid
+        if self.world > 1:
+            return self._cpu_pull_sharded(keys, lod, B, S, out, col_offset, sp, uniq, full_uid)
+        rows = self.table.probe(uniq)
+        if self.auto_insert and not self.test_mode and bool((rows < 0).any()):
+            self.table.insert_mixed(uniq[rows < 0], self.cfg.sgd)
+            rows = self.table.probe(uniq)
+        pulled = self.table.gather_pull(rows, self.P)
+        y = ref.seqpool_cvm(pulled, full_uid, lod, S, B, self.E, sp.use_cvm, sp.cvm_offset, sp.clk_filter,
+                            sp.pad_value, sp.need_filter, sp.show_coeff, sp.clk_coeff, sp.threshold,
+                            sp.quant_ratio, sp.embed_threshold_filter, sp.embed_threshold, sp.embed_thres_size)
+        out[:, col_offset:col_offset + y.shape[1]] = y
+        st = PullState(B=B, S=S, L=L, lod=lod, uid=full_uid, rows=rows)
+        st.extra["U"] = uniq.numel()
+        return st
+
+    def _cpu_pull_sharded(self, keys, lod, B, S, out, col_offset, sp, uniq, full_uid) -> PullState:
+        W = self.world
+        owner = ref.owner_of(uniq, W)
+        order = torch.argsort(owner, stable=True)
+        uniq_o = uniq[order]
+        counts = torch.bincount(owner, minlength=W)
+        in_counts = torch.empty_like(counts)
+        dist.all_to_all_single(in_counts, counts, group=self.group)
+        recv = torch.empty(int(in_counts.sum()), dtype=torch.int64)
+        dist.all_to_all_single(recv, uniq_o, in_counts.tolist(), counts.tolist(), group=self.group)
+        rows_r = self.table.probe(recv)
+        if self.auto_insert and not self.test_mode and bool((rows_r < 0).any()):
+            self.table.insert_mixed(torch.unique(recv[rows_r < 0]), self.cfg.sgd)
+            rows_r = self.table.probe(recv)
+        pulled_r = self.table.gather_pull(rows_r, self.P)
+        back = torch.empty(uniq.numel(), self.P)
+        dist.all_to_all_single(back, pulled_r, counts.tolist(), in_counts.tolist(), group=self.group)
+        pulled = torch.empty_like(back)
+        pulled[order] = back
+        y = ref.seqpool_cvm(pulled, full_uid, lod, S, B, self.E, sp.use_cvm, sp.cvm_offset, sp.clk_filter,
+                            sp.pad_value, sp.need_filter, sp.show_coeff, sp.clk_coeff, sp.threshold,
+                            sp.quant_ratio, sp.embed_threshold_filter, sp.embed_threshold, sp.embed_thres_size)
+        out[:, col_offset:col_offset + y.shape[1]] = y
+        st = PullState(B=B, S=S, L=keys.numel(), lod=lod, uid=full_uid)
+        st.extra.update(U=uniq.numel(), order=order, counts=counts, in_counts=in_counts, rows_r=rows_r,
+                        recv=recv)
+        return st
+
+    def _cpu_push(self, st: PullState, dout, cvm, col_offset, sp: SeqpoolParams, bs_scale):
+        U = st.extra["U"]
+        push = ref.push_merge(dout, cvm, st.uid, st.lod, st.S, st.B, U, self.dim, self._slot_ids(st.S), bs_scale,
+                              sp.use_cvm, sp.clk_filter, col_offset, sp.cvm_offset)
+        if self.world == 1:
+            self.table.push_adagrad(st.rows, push, self.cfg.sgd)
+            return
+        e = st.extra
+        send = push[e["order"]]
+        recv = torch.empty(int(e["in_counts"].sum()), push.shape[1])
+        dist.all_to_all_single(recv, send, e["in_counts"].tolist(), e["counts"].tolist(), group=self.group)
+        # merge duplicates from different senders, then update
+        uq, inv = torch.unique(e["recv"], return_inverse=True)
+        merged = torch.zeros(uq.numel(), push.shape[1])
+        merged.index_add_(0, inv, recv)
+        merged[inv, 0] = recv[:, 0]
+        rows = self.table.probe(uq)
+        self.table.push_adagrad(rows, merged, self.cfg.sgd)

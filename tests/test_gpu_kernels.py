@@ -1,0 +1,263 @@
+"""Numerics of the hand-written gfx950 kernels vs plain-PyTorch fp32 references.
+
+All tests need an MI355X (marker ``gpu``); they fail loudly if the HIP
+extension is missing (no eager fallback on GPU tensors).
+"""
+import math
+
+import pytest
+import torch
+
+from paddlebox_amd import _native
+from paddlebox_amd.data.synthetic import CriteoSynth, ragged_batch
+from paddlebox_amd.ops import reference as ref
+from paddlebox_amd.ps.config import PSConfig, SparseSGDConfig, row_layout
+from paddlebox_amd.ps.sparse_engine import SeqpoolParams, SparseEngine
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def hip():
+    return _native.hip()
+
+
+def test_mix64_matches_reference():
+    keys = torch.randint(0, 2**62, (1000,), dtype=torch.int64)
+    for k in keys[:10].tolist():
+        assert hip().mix64(k) == ref.mix64_int(k)
+        assert hip().unmix64(hip().mix64(k)) == k
+    t = ref.mix64(keys)
+    assert [ (x & ((1 << 64) - 1)) for x in t[:10].tolist()] == [ref.mix64_int(k) for k in keys[:10].tolist()]
+
+
+def test_dedup_matches_unique():
+    torch.manual_seed(0)
+    n = 50000
+    keys = torch.randint(0, 3000, (n,), dtype=torch.int64, device=DEV)
+    keys[-100:] = -1  # padding
+    ws = hip().DedupWorkspace(n, 0)
+    ws.run(keys, False)
+    U = int(ws.u_count[0])
+    nvalid = int(ws.u_count[1])
+    h = ref.mix64(keys[:-100])
+    uq = torch.unique(h)
+    assert U == uq.numel()
+    assert nvalid == n - 100
+    got = ws.uniq_h[:U]
+    # sorted as uint64: compare as sets
+    assert torch.equal(torch.sort(got).values, torch.sort(uq).values)
+    uid = ws.uid[: n - 100].long()
+    assert torch.equal(got[uid], h)
+    assert bool((ws.uid[n - 100:] == -1).all())
+    seg = ws.seg[: U + 1].long()
+    perm = ws.perm[:nvalid].long()
+    # every segment holds occurrences of one key
+    for u in [0, 1, U // 2, U - 1]:
+        occ = perm[seg[u]:seg[u + 1]]
+        assert bool((h[occ] == got[u]).all())
+
+
+def test_table_insert_probe_high_load():
+    t = hip().GpuTable(8, 200_000, 1024, 0)
+    cap = t.capacity
+    n = int(cap * 0.9)
+    keys = torch.unique(ref.mix64(torch.randint(0, 2**60, (n,), dtype=torch.int64, device=DEV)))
+    fails = t.insert(keys, None, SparseSGDConfig().to_native(hip()), 7, True)
+    assert fails == 0
+    assert t.size() == keys.numel()
+    rows = t.probe(keys, None)
+    assert bool((rows >= 0).all())
+    assert torch.unique(rows).numel() == keys.numel()
+    other = ref.mix64(torch.randint(2**61, 2**62, (1000,), dtype=torch.int64, device=DEV))
+    assert bool((t.probe(other, None) == -1).all())
+    # embedx initialised and flagged created
+    l = row_layout(8)
+    v = t.values[rows[:100]]
+    assert bool((v[:, l["mf_size"]] == 1).all())
+    assert float(v[:, 3:11].abs().max()) <= 1e-4 + 1e-9
+    # re-inserting existing keys is a no-op
+    t.insert(keys[:1000], None, SparseSGDConfig().to_native(hip()), 8, False)
+    assert t.size() == keys.numel()
+    k, vals = t.export_all(True)
+    assert k.numel() == keys.numel()
+    assert torch.equal(torch.sort(k).values, torch.sort(keys).values)
+
+
+def _engine(dim=8, max_keys=100000, cap=1 << 18, device=DEV):
+    cfg = PSConfig(embedx_dim=dim)
+    cfg.sgd.mf_create_thresholds = 2.0
+    return SparseEngine(cfg, max_keys=max_keys, device=torch.device(device), capacity=cap)
+
+
+@pytest.mark.parametrize("ragged", [False, True])
+@pytest.mark.parametrize("use_cvm", [True, False])
+def test_seqpool_cvm_matches_reference(ragged, use_cvm):
+    torch.manual_seed(1)
+    if ragged:
+        b = ragged_batch(64, 5, 4, 50, seed=3, device=DEV)
+    else:
+        b = CriteoSynth(total_features=100000, seed=2, device=DEV).batch(128)
+    eng = _engine()
+    eng.register_keys(b.keys, init_embedx=True)
+    sp = SeqpoolParams(use_cvm=use_cvm)
+    # give rows non-trivial show/click/embed values
+    vals = eng.table.values
+    vals[:, :3] = torch.rand_like(vals[:, :3]) * 5
+    Eo = sp.out_width(eng.E)
+    out = torch.zeros(b.B, b.S * Eo, device=DEV)
+    st = eng.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out, 0, sp)
+    # reference from the table rows
+    uniq, uid = ref.dedup(b.keys)
+    rows = eng.table.probe(uniq)
+    src = vals[rows]
+    exp = ref.seqpool_cvm(src, uid, b.lod, b.S, b.B, eng.E, use_cvm=use_cvm)
+    torch.testing.assert_close(out, exp, rtol=1e-5, atol=1e-5)
+
+
+def test_seqpool_filter_quant():
+    b = ragged_batch(32, 4, 5, 40, seed=5, device=DEV)
+    eng = _engine()
+    eng.register_keys(b.keys, init_embedx=True)
+    vals = eng.table.values
+    vals[:, :2] = torch.rand_like(vals[:, :2]) * 3
+    vals[:, 2:11] = torch.randn_like(vals[:, 2:11])
+    sp = SeqpoolParams(need_filter=True, quant_ratio=128, threshold=0.5, pad_value=0.1)
+    out = torch.zeros(b.B, b.S * 11, device=DEV)
+    eng.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out, 0, sp)
+    uniq, uid = ref.dedup(b.keys)
+    src = vals[eng.table.probe(uniq)]
+    exp = ref.seqpool_cvm(src, uid, b.lod, b.S, b.B, 11, need_filter=True, quant_ratio=128, threshold=0.5,
+                          pad_value=0.1)
+    torch.testing.assert_close(out, exp, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("ragged", [False, True])
+def test_push_adagrad_matches_reference(ragged):
+    torch.manual_seed(4)
+    if ragged:
+        b = ragged_batch(64, 6, 6, 30, seed=9, device=DEV)
+    else:
+        b = CriteoSynth(total_features=20000, alpha=1.3, seed=5, device=DEV).batch(512)
+    eng = _engine()
+    eng.register_keys(b.keys, init_embedx=False)
+    vals = eng.table.values
+    vals[:, 2] = torch.randn_like(vals[:, 2]) * 0.1
+    # half the rows already have embedx created
+    l = row_layout(8)
+    created = torch.rand(vals.shape[0], device=DEV) < 0.5
+    vals[created, l["mf_size"]] = 1
+    vals[created, 3:11] = torch.randn_like(vals[created, 3:11]) * 0.01
+    sp = SeqpoolParams()
+    uniq, uid = ref.dedup(b.keys)
+    rows = eng.table.probe(uniq)
+    before = vals[rows].clone()
+    out = torch.zeros(b.B, b.S * 11, device=DEV)
+    st = eng.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out, 0, sp)
+    dout = torch.randn_like(out) * 0.01
+    eng.push_seqpool_cvm(st, dout, b.cvm, 0, sp, float(b.B))
+    after = vals[rows]
+    push = ref.push_merge(dout, b.cvm, uid, b.lod, b.S, b.B, uniq.numel(), 8, eng._slot_ids(b.S), float(b.B))
+    exp = ref.adagrad_update(before, push, 8, eng.cfg.sgd)
+    # newly created embedx are random: compare them by range only
+    newly = (before[:, l["mf_size"]] == 0) & (exp[:, l["mf_size"]] == 1)
+    cols = [c for c in range(exp.shape[1]) if not (3 <= c < 11)]
+    torch.testing.assert_close(after[:, cols], exp[:, cols], rtol=2e-4, atol=2e-5)
+    keep = ~newly
+    torch.testing.assert_close(after[keep, 3:11], exp[keep, 3:11], rtol=2e-4, atol=2e-5)
+    if bool(newly.any()):
+        x = after[newly, 3:11]
+        assert float(x.min()) >= 0 and float(x.max()) <= eng.cfg.sgd.mf_initial_range
+
+
+def test_pull_box_sparse_records_and_push():
+    b = ragged_batch(16, 3, 3, 20, seed=11, device=DEV)
+    eng = _engine()
+    eng.register_keys(b.keys, init_embedx=True)
+    eng.table.values[:, :3] = torch.rand_like(eng.table.values[:, :3])
+    recs, st = eng.pull_records(b.keys, b.lod, b.B, b.S)
+    uniq, uid = ref.dedup(b.keys)
+    exp = eng.table.values[eng.table.probe(uniq)][uid.long(), :11]
+    torch.testing.assert_close(recs, exp)
+    g = torch.randn_like(recs) * 0.01
+    before = eng.table.values.clone()
+    eng.push_records(st, g, 2, float(b.B))
+    assert not torch.equal(before, eng.table.values)
+
+
+def test_data_norm_fm_loss_auc_adam():
+    torch.manual_seed(0)
+    N, C = 300, 77
+    x = torch.randn(N, C, device=DEV)
+    bs = torch.full((C,), 1e4, device=DEV)
+    bsum = torch.randn(C, device=DEV)
+    bsq = torch.full((C,), 1e4, device=DEV) + torch.rand(C, device=DEV)
+    y, m, s = hip().data_norm_fwd(x, bs, bsum, bsq, None, None)
+    ye, me, se = ref.data_norm_fwd(x, bs, bsum, bsq)
+    torch.testing.assert_close(y, ye)
+    dy = torch.randn_like(x)
+    dx, st = hip().data_norm_bwd(x, dy, m, s, 1e-5, True, None)
+    dxe, ste = ref.data_norm_bwd(x, dy, me, se, 1e-5)
+    torch.testing.assert_close(dx, dxe)
+    torch.testing.assert_close(st, ste, rtol=1e-4, atol=1e-5)
+    # FM
+    B, S, D, Eo = 64, 26, 8, 11
+    xx = torch.randn(B, S * Eo + 13, device=DEV)
+    f = hip().fm_fwd(xx, S, D, 3, Eo)
+    torch.testing.assert_close(f, ref.fm_fwd(xx, S, D, 3, Eo), rtol=1e-4, atol=1e-4)
+    go = torch.randn(B, device=DEV)
+    dxx = torch.zeros_like(xx)
+    hip().fm_bwd(xx, go, S, D, 3, Eo, dxx, False)
+    xr = xx.clone().requires_grad_(True)
+    (gr,) = torch.autograd.grad(ref.fm_fwd(xr, S, D, 3, Eo), xr, go)
+    torch.testing.assert_close(dxx, gr, rtol=1e-4, atol=1e-4)
+    # loss
+    z = torch.randn(1000, device=DEV)
+    lab = (torch.rand(1000, device=DEV) < 0.3).float()
+    p, l, dz = hip().sigmoid_logloss(z, lab, 1e-3)
+    pe, le, dze = ref.sigmoid_logloss(z, lab, 1e-3)
+    torch.testing.assert_close(p, pe)
+    torch.testing.assert_close(l, le, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(dz, dze)
+    # auc
+    T = 1000
+    tab = torch.zeros(2 * T, dtype=torch.float64, device=DEV)
+    stt = torch.zeros(5, dtype=torch.float64, device=DEV)
+    hip().auc_accumulate(p, lab, None, tab, stt)
+    tab2 = torch.zeros_like(tab)
+    st2 = torch.zeros_like(stt)
+    ref.auc_accumulate(p, lab, tab2, st2)
+    torch.testing.assert_close(tab, tab2)
+    torch.testing.assert_close(stt, st2)
+    # adam
+    n = 1003
+    pp = torch.randn(n, device=DEV)
+    gg = torch.randn(n, device=DEV)
+    m1 = torch.zeros(n, device=DEV)
+    v1 = torch.zeros(n, device=DEV)
+    p2, m2, v2 = pp.clone(), m1.clone(), v1.clone()
+    hip().adam_flat(pp, gg, m1, v1, 1e-3, 0.9, 0.999, 1e-8, 0.9, 0.999, 0.5, 0.0)
+    ref.adam_flat(p2, gg, m2, v2, 1e-3, 0.9, 0.999, 1e-8, 0.9, 0.999, 0.5, 0.0)
+    torch.testing.assert_close(pp, p2)
+
+
+def test_deepfm_trains_on_gpu():
+    from paddlebox_amd.models.deepfm import DeepFM
+    from paddlebox_amd.parallel.dense import DenseArena, FlatAdam
+
+    synth = CriteoSynth(total_features=200000, alpha=1.1, seed=0, device=DEV)
+    eng = SparseEngine(PSConfig(embedx_dim=8), max_keys=1024 * 26, device=torch.device(DEV), capacity=300000,
+                       auto_insert=True)
+    model = DeepFM(eng, hidden=(64, 32)).to(DEV)
+    arena = DenseArena(model.parameters(), torch.device(DEV))
+    opt = FlatAdam(arena, lr=3e-3)
+    losses = []
+    for i in range(60):
+        b = synth.batch(1024)
+        arena.zero_grad()
+        loss, pred = model(b)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    assert math.isfinite(losses[-1])
+    assert sum(losses[-10:]) / 10 < sum(losses[:10]) / 10
