@@ -136,6 +136,12 @@ class GpuTable {
     launch_push_adagrad(view(), ptr<int64_t>(rows), ptr<float>(push), (int)push.size(1), optr<int32_t>(n_dev),
                         rows.numel(), cfg, seed, cur_stream());
   }
+  void clear() {
+    keys_.fill_(-1);
+    fill_.zero_();
+    scratch_.zero_();
+    stash_keys_.fill_(-1);
+  }
   Tensor keys() const { return keys_; }
   Tensor values() const { return values_; }
   Tensor fill() const { return fill_; }
@@ -410,6 +416,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("shrink", &GpuTable::shrink)
       .def("gather_pull", &GpuTable::gather_pull, py::arg("rows"), py::arg("n_dev"), py::arg("out_stride"))
       .def("push_adagrad", &GpuTable::push_adagrad)
+      .def("clear", &GpuTable::clear)
       .def_property_readonly("keys", &GpuTable::keys)
       .def_property_readonly("values", &GpuTable::values)
       .def_property_readonly("fill", &GpuTable::fill)

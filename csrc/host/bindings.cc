@@ -1,0 +1,344 @@
+// pybind glue for the native host runtime (module paddlebox_amd._pbx_host).
+#include <torch/extension.h>
+
+#include "cpu_ps.h"
+#include "metrics.h"
+#include "runtime.h"
+#include "slot_dataset.h"
+
+namespace py = pybind11;
+using torch::Tensor;
+
+namespace pbx {
+
+static void req_cpu(const Tensor& t, const char* n) {
+  if (!t.device().is_cpu() || !t.is_contiguous())
+    throw std::runtime_error(std::string("pbx host: ") + n + " must be a contiguous CPU tensor");
+}
+
+static SparseSGDConfig cfg_from_list(const std::vector<float>& c) {
+  SparseSGDConfig s;
+  if (c.size() < 16) throw std::runtime_error("sgd config list must have 16 entries");
+  s.nonclk_coeff = c[0];
+  s.clk_coeff = c[1];
+  s.min_bound = c[2];
+  s.max_bound = c[3];
+  s.learning_rate = c[4];
+  s.initial_g2sum = c[5];
+  s.initial_range = c[6];
+  s.mf_create_thresholds = c[7];
+  s.mf_learning_rate = c[8];
+  s.mf_initial_g2sum = c[9];
+  s.mf_initial_range = c[10];
+  s.mf_min_bound = c[11];
+  s.mf_max_bound = c[12];
+  s.nodeid_slot = c[13];
+  s.feature_learning_rate = c[14];
+  s.use_feature_lr = (int)c[15];
+  return s;
+}
+
+static Tensor to_tensor_u64(const std::vector<uint64_t>& v) {
+  auto t = torch::empty({(int64_t)v.size()}, torch::kInt64);
+  if (!v.empty()) memcpy(t.data_ptr(), v.data(), v.size() * 8);
+  return t;
+}
+static Tensor to_tensor_f(const std::vector<float>& v, int64_t cols) {
+  const int64_t rows = cols ? (int64_t)v.size() / cols : 0;
+  auto t = torch::empty({rows, cols}, torch::kFloat32);
+  if (!v.empty()) memcpy(t.data_ptr(), v.data(), v.size() * 4);
+  return t;
+}
+
+}  // namespace pbx
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  using namespace pbx;
+  register_default_flags();
+  m.doc() = "PaddleBox-capability engine: native host runtime";
+
+  // ---------------------------------------------------------------- flags
+  m.def("flags_all", [] { return Flags::ins().all(); });
+  m.def("flags_help", [] { return Flags::ins().help(); });
+  m.def("flag_get", [](const std::string& n) { return Flags::ins().get(n); });
+  m.def("flag_set", [](const std::string& n, const std::string& v) { Flags::ins().set(n, v); });
+  m.def("flag_define", [](const std::string& n, const std::string& d, const std::string& h) { Flags::ins().define(n, d, h); });
+
+  // ---------------------------------------------------------------- CPU table
+  py::class_<SaveFilter>(m, "SaveFilter")
+      .def(py::init<>())
+      .def_readwrite("base_threshold", &SaveFilter::base_threshold)
+      .def_readwrite("delta_threshold", &SaveFilter::delta_threshold)
+      .def_readwrite("delta_keep_days", &SaveFilter::delta_keep_days)
+      .def_readwrite("embedx_threshold", &SaveFilter::embedx_threshold)
+      .def_readwrite("nonclk_coeff", &SaveFilter::nonclk_coeff)
+      .def_readwrite("clk_coeff", &SaveFilter::clk_coeff);
+  py::class_<CpuTable>(m, "CpuTable")
+      .def(py::init<int, int>(), py::arg("dim"), py::arg("nshards") = 16)
+      .def_property_readonly("dim", &CpuTable::dim)
+      .def_property_readonly("stride", &CpuTable::stride)
+      .def("size", &CpuTable::size)
+      .def("probe", [](const CpuTable& t, const Tensor& h) {
+        req_cpu(h, "h");
+        auto rows = torch::empty({h.numel()}, torch::kInt64);
+        py::gil_scoped_release nogil;
+        t.probe((const uint64_t*)h.data_ptr(), h.numel(), rows.data_ptr<int64_t>());
+        return rows;
+      })
+      .def("insert", [](CpuTable& t, const Tensor& h, float ir, float mir, int init_x, uint64_t seed) {
+        req_cpu(h, "h");
+        py::gil_scoped_release nogil;
+        t.insert((const uint64_t*)h.data_ptr(), h.numel(), ir, mir, init_x != 0, seed);
+      })
+      .def("gather", [](const CpuTable& t, const Tensor& rows) {
+        req_cpu(rows, "rows");
+        auto out = torch::empty({rows.numel(), t.stride()}, torch::kFloat32);
+        py::gil_scoped_release nogil;
+        t.gather(rows.data_ptr<int64_t>(), rows.numel(), out.data_ptr<float>());
+        return out;
+      })
+      .def("assign", [](CpuTable& t, const Tensor& rows, const Tensor& vals) {
+        req_cpu(rows, "rows");
+        req_cpu(vals, "vals");
+        t.assign(rows.data_ptr<int64_t>(), rows.numel(), vals.data_ptr<float>(), (int)vals.size(1));
+      })
+      .def("push_adagrad", [](CpuTable& t, const Tensor& rows, const Tensor& push, const std::vector<float>& cfg) {
+        req_cpu(rows, "rows");
+        req_cpu(push, "push");
+        auto c = cfg_from_list(cfg);
+        static uint64_t seed = 99;
+        seed++;
+        py::gil_scoped_release nogil;
+        t.push_adagrad(rows.data_ptr<int64_t>(), rows.numel(), push.data_ptr<float>(), (int)push.size(1), c, seed);
+      })
+      .def("shrink", &CpuTable::shrink)
+      .def("export_all", [](const CpuTable& t) {
+        std::vector<uint64_t> k;
+        std::vector<float> v;
+        t.export_all(&k, &v);
+        return py::make_tuple(to_tensor_u64(k), to_tensor_f(v, t.stride()));
+      })
+      .def("select_for_save", [](CpuTable& t, int mode, const SaveFilter& f) {
+        std::vector<uint64_t> k;
+        std::vector<float> v;
+        t.select_for_save(mode, f, &k, &v);
+        return py::make_tuple(to_tensor_u64(k), to_tensor_f(v, t.stride()));
+      })
+      .def("erase", [](CpuTable& t, const Tensor& h) {
+        req_cpu(h, "h");
+        return t.erase((const uint64_t*)h.data_ptr(), h.numel());
+      })
+      .def("clear", &CpuTable::clear);
+
+  // ---------------------------------------------------------------- metrics
+  py::class_<AucCalculator>(m, "AucCalculator")
+      .def(py::init<int>(), py::arg("table_size") = 1000000)
+      .def("reset", &AucCalculator::reset)
+      .def_property_readonly("table_size", &AucCalculator::table_size)
+      .def("add", [](AucCalculator& c, const Tensor& pred, const Tensor& label, const c10::optional<Tensor>& mask,
+                     float scale) {
+        req_cpu(pred, "pred");
+        req_cpu(label, "label");
+        const float* mk = mask.has_value() ? mask->data_ptr<float>() : nullptr;
+        c.add(pred.data_ptr<float>(), label.data_ptr<float>(), mk, pred.numel(), scale);
+      }, py::arg("pred"), py::arg("label"), py::arg("mask") = py::none(), py::arg("sample_scale") = 1.0f)
+      .def("add_float_label", [](AucCalculator& c, const Tensor& pred, const Tensor& label, const c10::optional<Tensor>& mask) {
+        const float* mk = mask.has_value() ? mask->data_ptr<float>() : nullptr;
+        c.add_float_label(pred.data_ptr<float>(), label.data_ptr<float>(), mk, pred.numel());
+      }, py::arg("pred"), py::arg("label"), py::arg("mask") = py::none())
+      .def("add_continue", [](AucCalculator& c, const Tensor& pred, const Tensor& label, const c10::optional<Tensor>& mask) {
+        const float* mk = mask.has_value() ? mask->data_ptr<float>() : nullptr;
+        c.add_continue(pred.data_ptr<float>(), label.data_ptr<float>(), mk, pred.numel());
+      }, py::arg("pred"), py::arg("label"), py::arg("mask") = py::none())
+      .def("add_uid", [](AucCalculator& c, const Tensor& pred, const Tensor& label, const Tensor& uid) {
+        c.add_uid(pred.data_ptr<float>(), label.data_ptr<float>(), (const uint64_t*)uid.data_ptr(), pred.numel());
+      })
+      .def("add_nan_inf", [](AucCalculator& c, const Tensor& pred) { c.add_nan_inf(pred.data_ptr<float>(), pred.numel()); })
+      .def("merge_tables", [](AucCalculator& c, const Tensor& table, const Tensor& stats) {
+        req_cpu(table, "table");
+        c.merge_tables(table.data_ptr<double>(), stats.data_ptr<double>());
+      })
+      .def("tables", [](AucCalculator& c) {
+        auto t = torch::empty({2, c.table_size()}, torch::kFloat64);
+        memcpy(t.data_ptr<double>(), c.neg().data(), c.table_size() * 8);
+        memcpy(t.data_ptr<double>() + c.table_size(), c.pos().data(), c.table_size() * 8);
+        auto e = c.local_err();
+        auto et = torch::empty({5}, torch::kFloat64);
+        memcpy(et.data_ptr<double>(), e.data(), 40);
+        return py::make_tuple(t, et);
+      })
+      .def("compute", [](AucCalculator& c, const c10::optional<Tensor>& tables, const c10::optional<Tensor>& err) {
+        if (tables.has_value()) {
+          const double* p = tables->data_ptr<double>();
+          c.compute(p, p + c.table_size(), err.has_value() ? err->data_ptr<double>() : nullptr);
+        } else {
+          c.compute_local();
+        }
+      }, py::arg("tables") = py::none(), py::arg("err") = py::none())
+      .def("compute_continue", [](AucCalculator& c, const c10::optional<Tensor>& err) {
+        c.compute_continue(err.has_value() ? err->data_ptr<double>() : nullptr);
+      }, py::arg("err") = py::none())
+      .def("compute_wuauc", &AucCalculator::compute_wuauc)
+      .def("compute_nan_inf", &AucCalculator::compute_nan_inf)
+      .def_readonly("auc", &AucCalculator::auc)
+      .def_readonly("bucket_error", &AucCalculator::bucket_error)
+      .def_readonly("mae", &AucCalculator::mae)
+      .def_readonly("rmse", &AucCalculator::rmse)
+      .def_readonly("actual_ctr", &AucCalculator::actual_ctr)
+      .def_readonly("predicted_ctr", &AucCalculator::predicted_ctr)
+      .def_readonly("size", &AucCalculator::size)
+      .def_readonly("actual_value", &AucCalculator::actual_value)
+      .def_readonly("predicted_value", &AucCalculator::predicted_value)
+      .def_readonly("uauc", &AucCalculator::uauc)
+      .def_readonly("wuauc", &AucCalculator::wuauc)
+      .def_readonly("user_cnt", &AucCalculator::user_cnt)
+      .def_readonly("nan_cnt", &AucCalculator::nan_cnt)
+      .def_readonly("inf_cnt", &AucCalculator::inf_cnt)
+      .def_readonly("nan_rate", &AucCalculator::nan_rate)
+      .def_readonly("inf_rate", &AucCalculator::inf_rate)
+      .def_readonly("nan_inf_rate", &AucCalculator::nan_inf_rate)
+      .def_readonly("nan_inf_size", &AucCalculator::nan_inf_size);
+
+  // ---------------------------------------------------------------- dataset
+  py::class_<SlotDesc>(m, "SlotDesc")
+      .def(py::init<>())
+      .def(py::init([](const std::string& name, const std::string& type, bool used, bool dense, int dim) {
+             SlotDesc s;
+             s.name = name;
+             s.type = (type.empty() || type[0] == 'u' || type[0] == 'i') ? 'u' : 'f';
+             s.used = used;
+             s.dense = dense;
+             s.dense_dim = dim;
+             return s;
+           }),
+           py::arg("name"), py::arg("type") = "uint64", py::arg("used") = true, py::arg("dense") = false,
+           py::arg("dim") = 1)
+      .def_readwrite("name", &SlotDesc::name)
+      .def_readwrite("used", &SlotDesc::used)
+      .def_readwrite("dense", &SlotDesc::dense)
+      .def_readwrite("dense_dim", &SlotDesc::dense_dim);
+  py::class_<ParseConfig>(m, "ParseConfig")
+      .def(py::init<>())
+      .def_readwrite("parse_ins_id", &ParseConfig::parse_ins_id)
+      .def_readwrite("parse_logkey", &ParseConfig::parse_logkey)
+      .def_readwrite("sample_rate", &ParseConfig::sample_rate)
+      .def_readwrite("sample_seed", &ParseConfig::sample_seed);
+  py::class_<SlotDataset>(m, "SlotDataset")
+      .def(py::init<>())
+      .def("set_slots", &SlotDataset::set_slots)
+      .def("set_filelist", &SlotDataset::set_filelist)
+      .def("set_pipe_command", &SlotDataset::set_pipe_command)
+      .def("set_thread_num", &SlotDataset::set_thread_num)
+      .def("set_parse", &SlotDataset::set_parse)
+      .def("load_into_memory", &SlotDataset::load_into_memory, py::call_guard<py::gil_scoped_release>())
+      .def("preload_into_memory", &SlotDataset::preload_into_memory)
+      .def("wait_preload_done", &SlotDataset::wait_preload_done, py::call_guard<py::gil_scoped_release>())
+      .def("add_lines", &SlotDataset::add_lines)
+      .def("release_memory", &SlotDataset::release_memory)
+      .def("size", &SlotDataset::size)
+      .def("bad_lines", &SlotDataset::bad_lines)
+      .def("collect_keys", [](const SlotDataset& d, bool unique) {
+        std::vector<uint64_t> k;
+        {
+          py::gil_scoped_release nogil;
+          k = d.collect_keys(unique);
+        }
+        return to_tensor_u64(k);
+      }, py::arg("unique") = true)
+      .def("shuffle", &SlotDataset::shuffle)
+      .def("set_order", [](SlotDataset& d, const Tensor& o) {
+        req_cpu(o, "order");
+        std::vector<int64_t> v(o.data_ptr<int64_t>(), o.data_ptr<int64_t>() + o.numel());
+        d.set_order(v);
+      })
+      .def("order", [](const SlotDataset& d) {
+        auto& o = d.order();
+        auto t = torch::empty({(int64_t)o.size()}, torch::kInt64);
+        if (!o.empty()) memcpy(t.data_ptr(), o.data(), o.size() * 8);
+        return t;
+      })
+      .def("merge_by_search_id", [](SlotDataset& d) {
+        auto off = d.merge_by_search_id();
+        auto t = torch::empty({(int64_t)off.size()}, torch::kInt64);
+        memcpy(t.data_ptr(), off.data(), off.size() * 8);
+        return t;
+      })
+      .def("num_sparse_slots", &SlotDataset::num_sparse_slots)
+      .def("dense_width", &SlotDataset::dense_width)
+      .def("sparse_slot_names", &SlotDataset::sparse_slot_names)
+      .def("dense_slot_names", &SlotDataset::dense_slot_names)
+      .def("dense_slot_dims", &SlotDataset::dense_slot_dims)
+      .def("build_batch", [](const SlotDataset& d, int64_t begin, int64_t count, bool pin) {
+        auto dims = d.batch_dims(begin, count);
+        auto opt64 = torch::TensorOptions().dtype(torch::kInt64).pinned_memory(pin);
+        auto optf = torch::TensorOptions().dtype(torch::kFloat32).pinned_memory(pin);
+        const int S = d.num_sparse_slots();
+        auto keys = torch::empty({dims.L}, opt64);
+        auto lod = torch::empty({(int64_t)S * (dims.B + 1)}, opt64);
+        auto dense = torch::empty({(int64_t)dims.B, d.dense_width()}, optf);
+        {
+          py::gil_scoped_release nogil;
+          d.build_batch(begin, count, keys.data_ptr<int64_t>(), lod.data_ptr<int64_t>(),
+                        d.dense_width() ? dense.data_ptr<float>() : nullptr);
+        }
+        return py::make_tuple(keys, lod, dense);
+      }, py::arg("begin"), py::arg("count"), py::arg("pin") = false)
+      .def("build_rank_offset", [](const SlotDataset& d, int64_t begin, int64_t count, int max_rank) {
+        auto out = torch::empty({count, 2 * max_rank + 1}, torch::kInt32);
+        d.build_rank_offset(begin, count, max_rank, out.data_ptr<int32_t>());
+        return out;
+      })
+      .def("search_ids", [](const SlotDataset& d) { return to_tensor_u64(d.store().search_id); })
+      .def("cmatch_rank", [](const SlotDataset& d) {
+        const auto& s = d.store();
+        auto t = torch::empty({(int64_t)s.cmatch.size()}, torch::kInt64);
+        auto* p = t.data_ptr<int64_t>();
+        for (size_t i = 0; i < s.cmatch.size(); ++i) p[i] = ((int64_t)s.cmatch[i] << 32) | (int64_t)s.rank[i];
+        return t;
+      })
+      .def("ins_ids", [](const SlotDataset& d) { return d.store().ins_id; })
+      .def("save_archive", &SlotDataset::save_archive)
+      .def("load_archive", &SlotDataset::load_archive, py::arg("path"), py::arg("append") = true)
+      .def("export_records", [](const SlotDataset& d, const Tensor& idx) {
+        // serialise a subset (for the inter-rank shuffle service)
+        std::vector<int64_t> v(idx.data_ptr<int64_t>(), idx.data_ptr<int64_t>() + idx.numel());
+        RecordStore st = d.store().select(v);
+        auto u = to_tensor_u64(st.u64);
+        auto uo = torch::from_blob(st.u64_off.data(), {(int64_t)st.u64_off.size()}, torch::kInt64).clone();
+        auto f = torch::from_blob(st.f32.data(), {(int64_t)st.f32.size()}, torch::kFloat32).clone();
+        auto fo = torch::from_blob(st.f32_off.data(), {(int64_t)st.f32_off.size()}, torch::kInt64).clone();
+        auto sid = to_tensor_u64(st.search_id);
+        std::vector<int64_t> cr(st.cmatch.size());
+        for (size_t i = 0; i < cr.size(); ++i) cr[i] = ((int64_t)st.cmatch[i] << 32) | st.rank[i];
+        auto crt = torch::from_blob(cr.data(), {(int64_t)cr.size()}, torch::kInt64).clone();
+        return py::make_tuple(u, uo, f, fo, sid, crt);
+      })
+      .def("import_records", [](SlotDataset& d, const Tensor& u, const Tensor& uo, const Tensor& f, const Tensor& fo,
+                                const Tensor& sid, const Tensor& cr) {
+        RecordStore st;
+        auto& cur = d.mutable_store();
+        st.reset(cur.nu, cur.nf);
+        st.u64.assign((const uint64_t*)u.data_ptr(), (const uint64_t*)u.data_ptr() + u.numel());
+        st.u64_off.assign(uo.data_ptr<int64_t>(), uo.data_ptr<int64_t>() + uo.numel());
+        st.f32.assign(f.data_ptr<float>(), f.data_ptr<float>() + f.numel());
+        st.f32_off.assign(fo.data_ptr<int64_t>(), fo.data_ptr<int64_t>() + fo.numel());
+        st.search_id.assign((const uint64_t*)sid.data_ptr(), (const uint64_t*)sid.data_ptr() + sid.numel());
+        for (int64_t i = 0; i < cr.numel(); ++i) {
+          st.cmatch.push_back((uint32_t)(cr.data_ptr<int64_t>()[i] >> 32));
+          st.rank.push_back((uint32_t)(cr.data_ptr<int64_t>()[i] & 0xffffffff));
+        }
+        cur.append(st);
+        std::vector<int64_t> ord(cur.nrec());
+        for (int64_t i = 0; i < (int64_t)ord.size(); ++i) ord[i] = i;
+        d.set_order(ord);
+        return st.nrec();
+      })
+      .def("replace_store_with", [](SlotDataset& d, const Tensor& keep) {
+        std::vector<int64_t> v(keep.data_ptr<int64_t>(), keep.data_ptr<int64_t>() + keep.numel());
+        RecordStore st = d.store().select(v);
+        d.mutable_store() = std::move(st);
+        std::vector<int64_t> ord(d.store().nrec());
+        for (int64_t i = 0; i < (int64_t)ord.size(); ++i) ord[i] = i;
+        d.set_order(ord);
+      });
+}

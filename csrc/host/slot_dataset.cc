@@ -1,0 +1,499 @@
+#include "slot_dataset.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <numeric>
+#include <random>
+#include <stdexcept>
+#include <unordered_set>
+
+#include "../common/pbx_common.h"
+#include "runtime.h"
+
+namespace pbx {
+
+// ---------------------------------------------------------------- store
+void RecordStore::reset(int nu_, int nf_) {
+  nu = nu_;
+  nf = nf_;
+  u64.clear();
+  f32.clear();
+  u64_off.assign(1, 0);
+  f32_off.assign(1, 0);
+  ins_id.clear();
+  search_id.clear();
+  cmatch.clear();
+  rank.clear();
+}
+
+void RecordStore::append(const RecordStore& o) {
+  const int64_t ub = (int64_t)u64.size(), fb = (int64_t)f32.size();
+  u64.insert(u64.end(), o.u64.begin(), o.u64.end());
+  f32.insert(f32.end(), o.f32.begin(), o.f32.end());
+  for (size_t i = 1; i < o.u64_off.size(); ++i) u64_off.push_back(o.u64_off[i] + ub);
+  for (size_t i = 1; i < o.f32_off.size(); ++i) f32_off.push_back(o.f32_off[i] + fb);
+  ins_id.insert(ins_id.end(), o.ins_id.begin(), o.ins_id.end());
+  search_id.insert(search_id.end(), o.search_id.begin(), o.search_id.end());
+  cmatch.insert(cmatch.end(), o.cmatch.begin(), o.cmatch.end());
+  rank.insert(rank.end(), o.rank.begin(), o.rank.end());
+}
+
+RecordStore RecordStore::select(const std::vector<int64_t>& idx) const {
+  RecordStore r;
+  r.reset(nu, nf);
+  for (int64_t i : idx) {
+    for (int j = 0; j < nu; ++j) {
+      const int64_t b = u64_off[i * nu + j], e = u64_off[i * nu + j + 1];
+      r.u64.insert(r.u64.end(), u64.begin() + b, u64.begin() + e);
+      r.u64_off.push_back((int64_t)r.u64.size());
+    }
+    for (int j = 0; j < nf; ++j) {
+      const int64_t b = f32_off[i * nf + j], e = f32_off[i * nf + j + 1];
+      r.f32.insert(r.f32.end(), f32.begin() + b, f32.begin() + e);
+      r.f32_off.push_back((int64_t)r.f32.size());
+    }
+    if (!ins_id.empty()) r.ins_id.push_back(ins_id[i]);
+    r.search_id.push_back(search_id[i]);
+    r.cmatch.push_back(cmatch[i]);
+    r.rank.push_back(rank[i]);
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------- dataset
+SlotDataset::SlotDataset() {}
+SlotDataset::~SlotDataset() {
+  if (preload_ && preload_->joinable()) preload_->join();
+}
+
+void SlotDataset::set_slots(const std::vector<SlotDesc>& slots) {
+  slots_ = slots;
+  u_idx_.assign(slots.size(), -1);
+  f_idx_.assign(slots.size(), -1);
+  sparse_slots_.clear();
+  dense_refs_.clear();
+  int nu = 0, nf = 0, col = 0;
+  for (size_t i = 0; i < slots.size(); ++i) {
+    const auto& s = slots[i];
+    if (!s.used) continue;
+    if (s.type == 'u') {
+      u_idx_[i] = nu;
+      if (s.dense) {
+        dense_refs_.push_back({'u', nu, s.dense_dim, col});
+        col += s.dense_dim;
+      } else {
+        sparse_slots_.push_back(nu);
+      }
+      ++nu;
+    } else {
+      f_idx_[i] = nf;
+      dense_refs_.push_back({'f', nf, s.dense ? s.dense_dim : std::max(1, s.dense_dim), col});
+      col += s.dense ? s.dense_dim : std::max(1, s.dense_dim);
+      ++nf;
+    }
+  }
+  dense_width_ = col;
+  store_.reset(nu, nf);
+}
+
+std::vector<std::string> SlotDataset::sparse_slot_names() const {
+  std::vector<std::string> out;
+  for (size_t i = 0; i < slots_.size(); ++i)
+    if (slots_[i].used && slots_[i].type == 'u' && !slots_[i].dense) out.push_back(slots_[i].name);
+  return out;
+}
+std::vector<std::string> SlotDataset::dense_slot_names() const {
+  std::vector<std::string> out;
+  for (size_t i = 0; i < slots_.size(); ++i)
+    if (slots_[i].used && (slots_[i].type == 'f' || slots_[i].dense)) out.push_back(slots_[i].name);
+  return out;
+}
+std::vector<int> SlotDataset::dense_slot_dims() const {
+  std::vector<int> out;
+  for (auto& d : dense_refs_) out.push_back(d.dim);
+  return out;
+}
+
+static bool parse_logkey(const char* s, size_t len, uint64_t* sid, uint32_t* cm, uint32_t* rk) {
+  if (len < 32) return false;
+  char buf[17];
+  memcpy(buf, s + 16, 16);
+  buf[16] = 0;
+  *sid = strtoull(buf, nullptr, 16);
+  memcpy(buf, s + 11, 3);
+  buf[3] = 0;
+  *cm = (uint32_t)strtoul(buf, nullptr, 16);
+  memcpy(buf, s + 14, 2);
+  buf[2] = 0;
+  *rk = (uint32_t)strtoul(buf, nullptr, 16);
+  return true;
+}
+
+bool SlotDataset::parse_line(const char* str, size_t len, RecordStore* st) const {
+  const char* end = str + len;
+  char* p = const_cast<char*>(str);
+  std::string ins_id;
+  uint64_t sid = 0;
+  uint32_t cm = 0, rk = 0;
+  auto read_token = [&](std::string* out) -> bool {
+    long n = strtol(p, &p, 10);
+    if (n != 1) return false;
+    while (p < end && *p == ' ') ++p;
+    const char* b = p;
+    while (p < end && *p != ' ' && *p != '\n' && *p != '\t') ++p;
+    out->assign(b, p - b);
+    return true;
+  };
+  if (parse_.parse_ins_id) {
+    if (!read_token(&ins_id)) return false;
+  }
+  if (parse_.parse_logkey) {
+    std::string lk;
+    if (!read_token(&lk)) return false;
+    parse_logkey(lk.data(), lk.size(), &sid, &cm, &rk);
+    ins_id = lk;
+  }
+  if (parse_.sample_rate < 1.0f) {
+    const uint64_t hh = mix64(std::hash<std::string>()(std::string(str, std::min<size_t>(len, 64))) ^ parse_.sample_seed);
+    if ((float)(hh >> 40) / 16777216.0f >= parse_.sample_rate) return false;
+  }
+  const int nu = store_.nu, nf = store_.nf;
+  thread_local std::vector<std::vector<uint64_t>> uvals;
+  thread_local std::vector<std::vector<float>> fvals;
+  uvals.resize(nu);
+  fvals.resize(nf);
+  for (auto& v : uvals) v.clear();
+  for (auto& v : fvals) v.clear();
+  int64_t total_sparse = 0;
+  for (size_t i = 0; i < slots_.size(); ++i) {
+    const SlotDesc& s = slots_[i];
+    char* q = p;
+    long num = strtol(p, &q, 10);
+    if (q == p || num <= 0) return false;  // reference: the number of ids can not be zero
+    p = q;
+    if (s.used && s.type == 'u') {
+      auto& v = uvals[u_idx_[i]];
+      for (long j = 0; j < num; ++j) {
+        const uint64_t x = strtoull(p, &q, 10);
+        if (q == p) return false;
+        p = q;
+        if (x == 0 && !s.dense) continue;
+        v.push_back(x);
+        if (!s.dense) ++total_sparse;
+      }
+    } else if (s.used && s.type == 'f') {
+      auto& v = fvals[f_idx_[i]];
+      for (long j = 0; j < num; ++j) {
+        const float x = strtof(p, &q);
+        if (q == p) return false;
+        p = q;
+        if (std::fabs(x) < 1e-6f && !s.dense) continue;
+        v.push_back(x);
+      }
+    } else {
+      for (long j = 0; j < num; ++j) {
+        while (p < end && *p == ' ') ++p;
+        while (p < end && *p != ' ' && *p != '\n') ++p;
+      }
+    }
+  }
+  if (total_sparse == 0 && !sparse_slots_.empty()) return false;
+  for (int j = 0; j < nu; ++j) {
+    st->u64.insert(st->u64.end(), uvals[j].begin(), uvals[j].end());
+    st->u64_off.push_back((int64_t)st->u64.size());
+  }
+  for (int j = 0; j < nf; ++j) {
+    st->f32.insert(st->f32.end(), fvals[j].begin(), fvals[j].end());
+    st->f32_off.push_back((int64_t)st->f32.size());
+  }
+  if (parse_.parse_ins_id || parse_.parse_logkey) st->ins_id.push_back(ins_id);
+  st->search_id.push_back(sid);
+  st->cmatch.push_back(cm);
+  st->rank.push_back(rk);
+  return true;
+}
+
+int64_t SlotDataset::load_files(const std::vector<std::string>& files, RecordStore* out) {
+  const int T = std::max(1, std::min<int>(threads_, (int)files.size()));
+  std::vector<RecordStore> parts(T);
+  std::atomic<size_t> next{0};
+  std::atomic<int64_t> bad{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) {
+    parts[t].reset(store_.nu, store_.nf);
+    th.emplace_back([&, t] {
+      for (;;) {
+        const size_t fi = next++;
+        if (fi >= files.size()) break;
+        const std::string& f = files[fi];
+        FILE* fp = nullptr;
+        bool is_pipe = false;
+        if (pipe_command_.empty() || pipe_command_ == "cat") {
+          fp = fopen(f.c_str(), "r");
+        } else {
+          const std::string cmd = pipe_command_ + " < '" + f + "'";
+          fp = popen(cmd.c_str(), "r");
+          is_pipe = true;
+        }
+        if (!fp) {
+          bad += 1;
+          continue;
+        }
+        char* line = nullptr;
+        size_t cap = 0;
+        ssize_t n;
+        while ((n = getline(&line, &cap, fp)) > 0) {
+          if (n <= 1) continue;
+          if (!parse_line(line, (size_t)n, &parts[t])) bad += 1;
+        }
+        free(line);
+        if (is_pipe) pclose(fp); else fclose(fp);
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  for (auto& pt : parts) out->append(pt);
+  bad_lines_ += bad.load();
+  return out->nrec();
+}
+
+int64_t SlotDataset::load_into_memory() {
+  RecordStore st;
+  st.reset(store_.nu, store_.nf);
+  load_files(files_, &st);
+  store_.append(st);
+  order_.resize(store_.nrec());
+  std::iota(order_.begin(), order_.end(), 0);
+  return store_.nrec();
+}
+
+void SlotDataset::preload_into_memory() {
+  if (preload_ && preload_->joinable()) preload_->join();
+  preload_store_.reset(store_.nu, store_.nf);
+  auto files = files_;
+  preload_.reset(new std::thread([this, files] { load_files(files, &preload_store_); }));
+}
+
+int64_t SlotDataset::wait_preload_done() {
+  if (preload_ && preload_->joinable()) preload_->join();
+  store_.append(preload_store_);
+  preload_store_.reset(store_.nu, store_.nf);
+  order_.resize(store_.nrec());
+  std::iota(order_.begin(), order_.end(), 0);
+  return store_.nrec();
+}
+
+int64_t SlotDataset::add_lines(const std::vector<std::string>& lines) {
+  int64_t ok = 0;
+  for (auto& l : lines) {
+    if (parse_line(l.data(), l.size(), &store_)) ++ok; else ++bad_lines_;
+  }
+  order_.resize(store_.nrec());
+  std::iota(order_.begin(), order_.end(), 0);
+  return ok;
+}
+
+void SlotDataset::release_memory() {
+  store_.reset(store_.nu, store_.nf);
+  order_.clear();
+  store_.u64.shrink_to_fit();
+  store_.f32.shrink_to_fit();
+}
+
+std::vector<uint64_t> SlotDataset::collect_keys(bool unique) const {
+  std::vector<uint64_t> keys;
+  const int64_t n = store_.nrec();
+  const int nu = store_.nu;
+  for (int64_t i = 0; i < n; ++i)
+    for (int j : sparse_slots_) {
+      const int64_t b = store_.u64_off[i * nu + j], e = store_.u64_off[i * nu + j + 1];
+      keys.insert(keys.end(), store_.u64.begin() + b, store_.u64.begin() + e);
+    }
+  if (unique) {
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  }
+  return keys;
+}
+
+void SlotDataset::shuffle(uint64_t seed) {
+  std::mt19937_64 rng(seed);
+  std::shuffle(order_.begin(), order_.end(), rng);
+}
+
+std::vector<int64_t> SlotDataset::merge_by_search_id() {
+  std::stable_sort(order_.begin(), order_.end(),
+                   [this](int64_t a, int64_t b) { return store_.search_id[a] < store_.search_id[b]; });
+  std::vector<int64_t> off{0};
+  for (size_t i = 1; i < order_.size(); ++i)
+    if (store_.search_id[order_[i]] != store_.search_id[order_[i - 1]]) off.push_back((int64_t)i);
+  off.push_back((int64_t)order_.size());
+  return off;
+}
+
+SlotDataset::BatchDims SlotDataset::batch_dims(int64_t begin, int64_t count) const {
+  BatchDims d;
+  d.B = (int)count;
+  const int nu = store_.nu;
+  for (int64_t r = begin; r < begin + count; ++r) {
+    const int64_t i = order_[r];
+    for (int j : sparse_slots_) d.L += store_.u64_off[i * nu + j + 1] - store_.u64_off[i * nu + j];
+  }
+  return d;
+}
+
+void SlotDataset::build_batch(int64_t begin, int64_t count, int64_t* keys, int64_t* lod, float* dense) const {
+  const int nu = store_.nu, nf = store_.nf;
+  const int B = (int)count;
+  int64_t k = 0;
+  for (size_t s = 0; s < sparse_slots_.size(); ++s) {
+    const int j = sparse_slots_[s];
+    int64_t* l = lod + (int64_t)s * (B + 1);
+    for (int b = 0; b < B; ++b) {
+      l[b] = k;
+      const int64_t i = order_[begin + b];
+      const int64_t e0 = store_.u64_off[i * nu + j], e1 = store_.u64_off[i * nu + j + 1];
+      for (int64_t e = e0; e < e1; ++e) keys[k++] = (int64_t)store_.u64[e];
+    }
+    l[B] = k;
+  }
+  if (dense && dense_width_ > 0) {
+    for (int b = 0; b < B; ++b) {
+      const int64_t i = order_[begin + b];
+      float* row = dense + (int64_t)b * dense_width_;
+      for (const auto& d : dense_refs_) {
+        int64_t e0, e1;
+        if (d.type == 'u') {
+          e0 = store_.u64_off[i * nu + d.idx];
+          e1 = store_.u64_off[i * nu + d.idx + 1];
+        } else {
+          e0 = store_.f32_off[i * nf + d.idx];
+          e1 = store_.f32_off[i * nf + d.idx + 1];
+        }
+        for (int c = 0; c < d.dim; ++c) {
+          const int64_t e = e0 + c;
+          float v = 0.f;
+          if (e < e1) v = d.type == 'u' ? (float)store_.u64[e] : store_.f32[e];
+          row[d.col + c] = v;
+        }
+      }
+    }
+  }
+}
+
+void SlotDataset::build_rank_offset(int64_t begin, int64_t count, int max_rank, int32_t* out) const {
+  const int col = 2 * max_rank + 1;
+  for (int64_t i = 0; i < count * col; ++i) out[i] = -1;
+  auto rank_of = [&](int64_t r) -> int {
+    const int64_t i = order_[begin + r];
+    const uint32_t cm = store_.cmatch[i], rk = store_.rank[i];
+    if ((cm == 222 || cm == 223) && rk <= (uint32_t)max_rank && rk != 0) return (int)rk;
+    return -1;
+  };
+  int64_t g0 = 0;
+  while (g0 < count) {
+    int64_t g1 = g0 + 1;
+    const uint64_t sid = store_.search_id[order_[begin + g0]];
+    while (g1 < count && store_.search_id[order_[begin + g1]] == sid) ++g1;
+    for (int64_t j = g0; j < g1; ++j) {
+      const int rank = rank_of(j);
+      out[j * col] = rank;
+      if (rank > 0) {
+        for (int64_t k = g0; k < g1; ++k) {
+          const int fr = rank_of(k);
+          if (fr > 0) {
+            const int m = fr - 1;
+            out[j * col + 2 * m + 1] = fr;
+            out[j * col + 2 * m + 2] = (int32_t)k;
+          }
+        }
+      }
+    }
+    g0 = g1;
+  }
+}
+
+// ---------------------------------------------------------------- archive
+static const uint64_t kArchiveMagic = 0x50425841524348ULL;  // "PBXARCH"
+
+template <typename T>
+static void wvec(FILE* f, const std::vector<T>& v) {
+  const uint64_t n = v.size();
+  fwrite(&n, 8, 1, f);
+  if (n) fwrite(v.data(), sizeof(T), n, f);
+}
+template <typename T>
+static bool rvec(FILE* f, std::vector<T>* v) {
+  uint64_t n = 0;
+  if (fread(&n, 8, 1, f) != 1) return false;
+  v->resize(n);
+  return n == 0 || fread(v->data(), sizeof(T), n, f) == n;
+}
+
+void SlotDataset::save_archive(const std::string& path) const {
+  FILE* f = fopen(path.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot open archive for write: " + path);
+  fwrite(&kArchiveMagic, 8, 1, f);
+  const int32_t hdr[2] = {store_.nu, store_.nf};
+  fwrite(hdr, 4, 2, f);
+  wvec(f, store_.u64);
+  wvec(f, store_.u64_off);
+  wvec(f, store_.f32);
+  wvec(f, store_.f32_off);
+  wvec(f, store_.search_id);
+  wvec(f, store_.cmatch);
+  wvec(f, store_.rank);
+  const uint64_t ni = store_.ins_id.size();
+  fwrite(&ni, 8, 1, f);
+  for (auto& s : store_.ins_id) {
+    const uint32_t l = (uint32_t)s.size();
+    fwrite(&l, 4, 1, f);
+    fwrite(s.data(), 1, l, f);
+  }
+  fclose(f);
+}
+
+int64_t SlotDataset::load_archive(const std::string& path, bool append) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("cannot open archive: " + path);
+  uint64_t magic = 0;
+  int32_t hdr[2];
+  if (fread(&magic, 8, 1, f) != 1 || magic != kArchiveMagic || fread(hdr, 4, 2, f) != 2) {
+    fclose(f);
+    throw std::runtime_error("bad archive: " + path);
+  }
+  if (hdr[0] != store_.nu || hdr[1] != store_.nf) {
+    fclose(f);
+    throw std::runtime_error("archive slot layout mismatch: " + path);
+  }
+  RecordStore st;
+  st.nu = hdr[0];
+  st.nf = hdr[1];
+  bool ok = rvec(f, &st.u64) && rvec(f, &st.u64_off) && rvec(f, &st.f32) && rvec(f, &st.f32_off) &&
+            rvec(f, &st.search_id) && rvec(f, &st.cmatch) && rvec(f, &st.rank);
+  uint64_t ni = 0;
+  ok = ok && fread(&ni, 8, 1, f) == 1;
+  for (uint64_t i = 0; ok && i < ni; ++i) {
+    uint32_t l = 0;
+    ok = fread(&l, 4, 1, f) == 1;
+    std::string s(l, '\0');
+    ok = ok && (l == 0 || fread(&s[0], 1, l, f) == l);
+    st.ins_id.push_back(s);
+  }
+  fclose(f);
+  if (!ok) throw std::runtime_error("truncated archive: " + path);
+  if (!append) store_.reset(store_.nu, store_.nf);
+  store_.append(st);
+  order_.resize(store_.nrec());
+  std::iota(order_.begin(), order_.end(), 0);
+  return st.nrec();
+}
+
+}  // namespace pbx

@@ -1,0 +1,140 @@
+// In-memory slot dataset for pass-based CTR training.
+//
+// Behaviour reproduced (not code): SlotRecord CSR storage (fw/data_feed.h:96-240),
+// the MultiSlot text parser with optional ins_id/logkey prefix and zero-feasign
+// dropping (fw/data_feed.cc:4024-4134, parser_log_key :2385-2395),
+// PadBoxSlotDataset load / feed-pass key collection / PrepareTrain batching
+// (fw/data_set.cc:1905-2860), dense-slot expansion (ExpandSlotRecord
+// :3244-3303), page-view merge by search_id (:2648-2688), rank_offset build
+// (data_feed.cu:1319-1369), and the O_DIRECT-style binary archive for
+// "load into disk" mode (data_feed.cc:2824-2992).
+//
+// MI355X-first: records are stored columnar (one CSR per pass, not one heap
+// object per instance), so building a batch is a handful of memcpy's into
+// pinned staging buffers that go to HBM in a single H2D copy per tensor.
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace pbx {
+
+struct SlotDesc {
+  std::string name;
+  char type = 'u';  // 'u' = uint64 feasigns, 'f' = float
+  bool used = true;
+  bool dense = false;  // dense slot: fixed width, zeros kept
+  int dense_dim = 1;
+};
+
+struct ParseConfig {
+  bool parse_ins_id = false;
+  bool parse_logkey = false;
+  float sample_rate = 1.0f;
+  uint64_t sample_seed = 0;
+};
+
+// Columnar CSR store of a pass.
+struct RecordStore {
+  int nu = 0, nf = 0;  // used uint64 / float slot counts
+  std::vector<uint64_t> u64;
+  std::vector<int64_t> u64_off{0};  // [nrec*nu + 1]
+  std::vector<float> f32;
+  std::vector<int64_t> f32_off{0};  // [nrec*nf + 1]
+  std::vector<std::string> ins_id;
+  std::vector<uint64_t> search_id;
+  std::vector<uint32_t> cmatch, rank;
+  int64_t nrec() const { return nu ? (int64_t)(u64_off.size() - 1) / nu : (nf ? (int64_t)(f32_off.size() - 1) / nf : (int64_t)search_id.size()); }
+  void reset(int nu_, int nf_);
+  void append(const RecordStore& o);
+  RecordStore select(const std::vector<int64_t>& idx) const;
+};
+
+class SlotDataset {
+ public:
+  SlotDataset();
+  ~SlotDataset();
+  void set_slots(const std::vector<SlotDesc>& slots);
+  void set_filelist(const std::vector<std::string>& files) { files_ = files; }
+  void set_pipe_command(const std::string& cmd) { pipe_command_ = cmd; }
+  void set_thread_num(int n) { threads_ = n < 1 ? 1 : n; }
+  void set_parse(const ParseConfig& c) { parse_ = c; }
+
+  // parse one line into store (returns false if dropped / no sparse feasign)
+  bool parse_line(const char* line, size_t len, RecordStore* st) const;
+  int64_t load_into_memory();      // blocking
+  void preload_into_memory();      // async
+  int64_t wait_preload_done();
+  int64_t add_lines(const std::vector<std::string>& lines);  // in-memory lines (tests)
+  void release_memory();
+
+  int64_t size() const { return store_.nrec(); }
+  const RecordStore& store() const { return store_; }
+  RecordStore& mutable_store() { return store_; }
+
+  // feed-pass keys: every feasign of sparse uint64 slots (optionally unique)
+  std::vector<uint64_t> collect_keys(bool unique) const;
+
+  // order of records for this pass (shuffle: Fisher-Yates with seed)
+  void shuffle(uint64_t seed);
+  void set_order(const std::vector<int64_t>& order) { order_ = order; }
+  const std::vector<int64_t>& order() const { return order_; }
+
+  // page-view merge: group consecutive records by search_id (after sorting
+  // by search_id); returns pv group offsets into order_
+  std::vector<int64_t> merge_by_search_id();
+
+  // Batch assembly over order_[begin, begin+count): writes
+  //  keys  [L]            sparse slots, slot-major
+  //  lod   [S*(B+1)]
+  //  dense [B, dense_width] (dense slots, padded/truncated)
+  // returns L.  sizes via batch_sizes().
+  struct BatchDims {
+    int64_t L = 0;
+    int B = 0;
+  };
+  BatchDims batch_dims(int64_t begin, int64_t count) const;
+  void build_batch(int64_t begin, int64_t count, int64_t* keys, int64_t* lod, float* dense) const;
+  // rank_offset [B, 2*max_rank+1] for PV batches (data_feed.cu:1319-1369)
+  void build_rank_offset(int64_t begin, int64_t count, int max_rank, int32_t* out) const;
+
+  int num_sparse_slots() const { return (int)sparse_slots_.size(); }
+  int dense_width() const { return dense_width_; }
+  std::vector<std::string> sparse_slot_names() const;
+  std::vector<std::string> dense_slot_names() const;
+  std::vector<int> dense_slot_dims() const;
+
+  // binary archive ("load into disk" mode)
+  void save_archive(const std::string& path) const;
+  int64_t load_archive(const std::string& path, bool append);
+
+  int64_t bad_lines() const { return bad_lines_; }
+
+ private:
+  int64_t load_files(const std::vector<std::string>& files, RecordStore* out);
+  std::vector<SlotDesc> slots_;
+  // index mapping: slot i -> used uint64 idx / used float idx (-1 = unused)
+  std::vector<int> u_idx_, f_idx_;
+  std::vector<int> sparse_slots_;  // used uint64 idx of sparse slots
+  struct DenseRef {
+    char type;
+    int idx;
+    int dim;
+    int col;
+  };
+  std::vector<DenseRef> dense_refs_;
+  int dense_width_ = 0;
+  std::vector<std::string> files_;
+  std::string pipe_command_ = "cat";
+  int threads_ = 4;
+  ParseConfig parse_;
+  RecordStore store_;
+  std::vector<int64_t> order_;
+  std::unique_ptr<std::thread> preload_;
+  RecordStore preload_store_;
+  int64_t bad_lines_ = 0;
+};
+
+}  // namespace pbx

@@ -13,6 +13,8 @@ PyTorch.  CPU tensors use the reference implementations in
 from __future__ import annotations
 
 import importlib
+
+import torch  # noqa: F401  (loads libc10 / libtorch for the extensions)
 import os
 
 _hip_mod = None

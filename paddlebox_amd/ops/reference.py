@@ -61,6 +61,28 @@ def unmix64_int(z: int) -> int:
     return z
 
 
+def _unxorshift_t(x: torch.Tensor, s: int) -> torch.Tensor:
+    r = x
+    for _ in range(64 // s + 1):
+        r = x ^ _lsr(r, s)
+    return r
+
+
+_I1 = _s64(0x96DE1B173F119089)
+_I2 = _s64(0x319642B2D24D8EC3)
+
+
+def unmix64(z: torch.Tensor) -> torch.Tensor:
+    """Inverse of :func:`mix64` (recover feasigns from stored table keys)."""
+    z = z.to(torch.int64)
+    z = _unxorshift_t(z, 31)
+    z = z * _I2
+    z = _unxorshift_t(z, 27)
+    z = z * _I1
+    z = _unxorshift_t(z, 30)
+    return z
+
+
 def owner_of(h: torch.Tensor, n: int) -> torch.Tensor:
     """floor(uint64(h) * n / 2^64) (pbx::owner_of)."""
     if n == 1:

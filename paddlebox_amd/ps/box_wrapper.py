@@ -1,0 +1,411 @@
+"""BoxWrapper: the BoxPS facade (singleton) -- pass lifecycle, feature table,
+tiers, checkpoints, metrics, phases, timers.
+
+Reference contract: ``fw/fleet/box_wrapper.{h,cc}`` (SetInstance :651-684,
+pass lifecycle :120-210, model IO :1201-1324, metrics :916-1083, timers
+:1085-1138) and the closed BoxPS API enumerated in SURVEY §2.1.
+
+Process model (MI355X-first): one process per GPU; this object is the
+per-process instance.  The feature table is sharded over the ranks of the
+process group by ``owner_of(mix64(key))``; key/value exchange is all-to-all
+over RCCL (see ``sparse_engine``).
+
+Tiers:
+  * ``hbm`` (default): the GPU table holds the whole shard (288 GB HBM3E per
+    MI355X holds ~3.5e9 8-dim features); feed pass inserts new keys.
+  * ``tiered``: the host table (native C++ CpuTable) is authoritative; each
+    pass stages its working set into HBM at EndFeedPass and writes it back at
+    EndPass; cold host rows spill to the SSD segment store.
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from ..metrics.registry import MetricRegistry
+from ..ops import reference as ref
+from ..utils import flags as _flags
+from ..utils.dayid import make_day_id_str
+from ..utils.log import logger
+from ..utils.timer import StageTimers
+from . import checkpoint as ckpt
+from .config import PSConfig, feature_pull_offsets, feature_push_offsets
+from .cpu_table import CpuSparseTable
+from .sparse_engine import SparseEngine
+from .ssd_tier import SsdStore
+
+
+class PSAgent:
+    """Thread-sharded feed-pass key collector (boxps::PSAgentBase AddKey/AddKeys,
+    box_wrapper.cc:1185-1200)."""
+
+    def __init__(self, n_threads: int = 30):
+        self.n = n_threads
+        self._parts: List[List[torch.Tensor]] = [[] for _ in range(n_threads)]
+        self._lock = threading.Lock()
+
+    def add_key(self, key: int, tid: int = 0):
+        self._parts[tid % self.n].append(torch.tensor([key], dtype=torch.int64))
+
+    def add_keys(self, keys: torch.Tensor, tid: int = 0):
+        self._parts[tid % self.n].append(keys.reshape(-1).to(torch.int64).cpu())
+
+    def keys(self) -> torch.Tensor:
+        allk = [t for p in self._parts for t in p]
+        if not allk:
+            return torch.empty(0, dtype=torch.int64)
+        k = torch.cat(allk)
+        k = k[(k != 0) & (k != -1)]
+        return torch.unique(k)
+
+
+class BoxWrapper:
+    _instance: Optional["BoxWrapper"] = None
+
+    def __init__(self, embedx_dim: int = 8, expand_embed_dim: int = 0, feature_type: int = 0,
+                 pull_embedx_scale: float = 1.0, device=None, group=None, cfg: Optional[PSConfig] = None):
+        self.cfg = cfg or PSConfig(embedx_dim=embedx_dim, expand_embed_dim=expand_embed_dim,
+                                   feature_type=feature_type, pull_embedx_scale=pull_embedx_scale)
+        self.group = group
+        ready = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if ready else 1
+        self.rank = dist.get_rank(group) if ready else 0
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(device)
+        self.engine: Optional[SparseEngine] = None
+        self.slot_vector: List[int] = []
+        self.slot_omit: List[int] = []
+        self.lr_map: Dict[str, float] = {}
+        self.metrics = MetricRegistry(group)
+        self.timers = StageTimers(self.device)
+        self.mode = "hbm"
+        self.host: Optional[CpuSparseTable] = None
+        self.ssd: Optional[SsdStore] = None
+        self.day_id = None
+        self.pass_id = 0
+        self.in_pass = False
+        self.test_mode = False
+        self.dataset_name = ""
+        self.input_table_dim = 0
+        self._agent: Optional[PSAgent] = None
+        self._pass_keys: Optional[torch.Tensor] = None
+        self.max_keys = 1 << 20
+        self.capacity = 1 << 22
+        BoxWrapper._instance = self
+
+    # ---------------------------------------------------------------- instance
+    @staticmethod
+    def set_instance(*a, **k) -> "BoxWrapper":
+        return BoxWrapper(*a, **k)
+
+    @staticmethod
+    def get_instance() -> "BoxWrapper":
+        if BoxWrapper._instance is None:
+            raise RuntimeError("BoxWrapper not initialised")
+        return BoxWrapper._instance
+
+    # ---------------------------------------------------------------- init
+    def initialize_gpu_and_load_model(self, conf_file: str = "", slot_vector: Sequence[int] = (),
+                                      slot_omit_in_feedpass: Sequence[int] = (), model_path: str = "",
+                                      lr_map: Optional[Dict[str, float]] = None, max_keys: Optional[int] = None,
+                                      capacity: Optional[int] = None, mode: Optional[str] = None,
+                                      ssd_path: Optional[str] = None, auto_insert: bool = False):
+        """Parse the PS config, bind the device, register slots, load a base
+        model (box_wrapper.cc:1201-1242)."""
+        if conf_file and os.path.exists(conf_file):
+            loaded = PSConfig.load(conf_file)
+            loaded.embedx_dim = self.cfg.embedx_dim
+            self.cfg = loaded
+        self.slot_vector = list(slot_vector)
+        self.slot_omit = list(slot_omit_in_feedpass)
+        self.lr_map = dict(lr_map or {})
+        mk = _flags.get_int("padbox_max_keys_per_batch")
+        self.max_keys = int(max_keys or mk or self.max_keys)
+        self.capacity = int(capacity or self.cfg.tier.hbm_capacity or self.capacity)
+        self.mode = mode or ("tiered" if (ssd_path or self.cfg.tier.ssd_path) else "hbm")
+        self.engine = SparseEngine(self.cfg, self.max_keys, self.device, capacity=self.capacity,
+                                   slot_ids=[float(s) for s in self.slot_vector] or None, group=self.group,
+                                   auto_insert=auto_insert)
+        if self.mode == "tiered":
+            self.host = CpuSparseTable(self.cfg.embedx_dim)
+            p = ssd_path or self.cfg.tier.ssd_path
+            if p:
+                self.ssd = SsdStore(os.path.join(p, f"rank{self.rank:05d}"), self.host.stride)
+        if model_path:
+            self.load_model(model_path)
+        return 0
+
+    def set_slot_vector(self, slots: Sequence[int]):
+        self.slot_vector = list(slots)
+        if self.engine is not None:
+            self.engine.set_slot_ids([float(s) for s in slots])
+
+    # ---------------------------------------------------------------- feature layout
+    def get_feature_pull_offsets(self):
+        return feature_pull_offsets(self.cfg.embedx_dim, self.cfg.expand_embed_dim)
+
+    def get_feature_push_offsets(self):
+        return feature_push_offsets(self.cfg.embedx_dim, self.cfg.expand_embed_dim)
+
+    @property
+    def cvm_offset(self) -> int:
+        return self.get_feature_pull_offsets()["cvm_offset"]
+
+    # ---------------------------------------------------------------- feed pass
+    def begin_feed_pass(self, date: Optional[str] = None) -> PSAgent:
+        if date is not None:
+            self.day_id = make_day_id_str(date)
+        self._agent = PSAgent()
+        return self._agent
+
+    def end_feed_pass(self, agent: Optional[PSAgent] = None):
+        agent = agent or self._agent
+        keys = agent.keys() if agent is not None else torch.empty(0, dtype=torch.int64)
+        with self.timers.span("feed_pass"):
+            self._stage_keys(keys)
+        self._agent = None
+
+    def feed_pass(self, dataset_or_keys, date: Optional[str] = None):
+        """FeedPass(date, keys) (deprecated form) / BoxHelper::ReadData2Memory."""
+        agent = self.begin_feed_pass(date)
+        if isinstance(dataset_or_keys, torch.Tensor):
+            agent.add_keys(dataset_or_keys)
+        else:
+            agent.add_keys(dataset_or_keys.collect_keys())
+        self.end_feed_pass(agent)
+
+    def _route(self, h: torch.Tensor) -> torch.Tensor:
+        """Send mixed keys to their owner rank; returns this rank's keys."""
+        if self.world == 1:
+            return torch.unique(h)
+        dev = self.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        h = h.to(dev)
+        owner = ref.owner_of(h, self.world)
+        order = torch.argsort(owner, stable=True)
+        h = h[order]
+        counts = torch.bincount(owner, minlength=self.world)
+        rc = torch.empty_like(counts)
+        dist.all_to_all_single(rc, counts, group=self.group)
+        recv = torch.empty(int(rc.sum()), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(recv, h, rc.tolist(), counts.tolist(), group=self.group)
+        return torch.unique(recv)
+
+    def _stage_keys(self, keys: torch.Tensor):
+        eng = self._require_engine()
+        h = self._route(ref.mix64(keys.to(self.device if self.device.type == "cuda" else "cpu")))
+        h = h.to(eng.device)
+        if self.mode == "hbm":
+            eng.insert_local_mixed(h)
+            return
+        # tiered: host is authoritative
+        hc = h.cpu()
+        rows = self.host.probe(hc)
+        miss = rows < 0
+        if bool(miss.any()) and self.ssd is not None:
+            found, vals = self.ssd.get(hc[miss])
+            if bool(found.any()):
+                mk = hc[miss][found]
+                self.host.insert_mixed(mk, self.cfg.sgd)
+                self.host.assign(mk, vals[found])
+                self.ssd.delete(mk)
+        self.host.insert_mixed(hc, self.cfg.sgd)
+        vals = self.host.read(hc)
+        self._pass_keys = hc
+        eng.table.clear()
+        eng.insert_local_mixed(h)
+        eng.table.assign(h, vals.to(eng.device))
+
+    # ---------------------------------------------------------------- pass
+    def begin_pass(self):
+        self.in_pass = True
+        self.pass_id += 1
+
+    def end_pass(self, need_save_delta: bool = False):
+        """EndPass: write back the working set (tiered), check exchange
+        overflow, optional forced HBM release (box_wrapper.cc:186-210)."""
+        eng = self._require_engine()
+        if eng.check_overflow():
+            raise RuntimeError("sparse key exchange overflowed its per-peer capacity this pass; "
+                               "raise SparseEngine cap_factor")
+        if self.mode == "tiered":
+            with self.timers.span("end_pass_writeback"):
+                h, v = eng.table.export(True)
+                self.host.assign(h.cpu(), v.cpu())
+                if self.ssd is not None:
+                    self._spill_cold()
+        if _flags.get_bool("enable_force_hbm_recyle") and self.device.type == "cuda":
+            torch.cuda.empty_cache()
+        self.in_pass = False
+
+    def _spill_cold(self, unseen_threshold: float = 1.0):
+        from .config import row_layout
+
+        h, v = self.host.export(True)
+        if h.numel() == 0:
+            return
+        l = row_layout(self.cfg.embedx_dim)
+        cold = v[:, l["unseen_days"]] >= unseen_threshold
+        if bool(cold.any()):
+            self.ssd.put(h[cold], v[cold])
+            self.host._native.erase(h[cold].contiguous()) if self.host._native is not None else None
+
+    def set_test_mode(self, is_test: bool):
+        self.test_mode = bool(is_test)
+        if self.engine is not None:
+            self.engine.test_mode = self.test_mode
+
+    # ---------------------------------------------------------------- model IO
+    def _authoritative(self):
+        return self.host if self.mode == "tiered" else self._require_engine().table
+
+    def save_base(self, batch_model_path: str, xbox_model_path: str, date: str = "") -> str:
+        """Full batch model + xbox base (box_wrapper.cc:1286-1305)."""
+        if self.mode == "tiered" and self.engine is not None and self.in_pass:
+            h, v = self.engine.table.export(True)
+            self.host.assign(h.cpu(), v.cpu())
+        t = self._authoritative()
+        n = ckpt.save_batch_model(t, batch_model_path, self.rank, date)
+        sg = self.cfg.sgd
+        x = ckpt.save_xbox(t, xbox_model_path, "base", self.cfg.save, sg.nonclk_coeff, sg.clk_coeff, self.rank)
+        if self.rank == 0:
+            ckpt.write_manifest(os.path.dirname(os.path.abspath(batch_model_path)) or ".", date=date,
+                                pass_id=self.pass_id, embedx_dim=self.cfg.embedx_dim, world=self.world,
+                                batch_model=batch_model_path, xbox=xbox_model_path, mode=self.mode,
+                                flags=_flags.all_flags())
+        return f"{batch_model_path} batch={n} xbox_base={x}"
+
+    def save_delta(self, xbox_model_path: str) -> str:
+        t = self._authoritative()
+        sg = self.cfg.sgd
+        x = ckpt.save_xbox(t, xbox_model_path, "delta", self.cfg.save, sg.nonclk_coeff, sg.clk_coeff, self.rank)
+        return f"{xbox_model_path} xbox_delta={x}"
+
+    def load_model(self, model_path: str, merge: bool = False):
+        """Load a batch model (all parts); rows are routed to their owners."""
+        keys, vals = ckpt.load_batch_model_parts(model_path)
+        if keys.size == 0:
+            return 0
+        k = torch.from_numpy(keys.view("int64").copy())
+        v = torch.from_numpy(vals)
+        h = ref.mix64(k)
+        if self.world > 1:
+            mine = ref.owner_of(h, self.world) == self.rank
+            h, v = h[mine], v[mine]
+        t = self._authoritative()
+        if merge:
+            cur = t.read(h.to(getattr(t, "device", "cpu")))
+            v = v.to(cur.device)
+            v[:, 0:2] += cur[:, 0:2]
+        dev = getattr(t, "device", torch.device("cpu"))
+        t.insert_mixed(h.to(dev), self.cfg.sgd)
+        t.assign(h.to(dev), v.to(dev).float())
+        return int(h.numel())
+
+    def merge_model(self, path: str):
+        return self.load_model(path, merge=True)
+
+    def merge_multi_models(self, paths: Sequence[str], update_type: int = 0, idx: int = 0):
+        n = 0
+        for p in paths:
+            n += self.load_model(p, merge=(update_type != 0))
+        return n
+
+    def load_ssd2mem(self, date: Optional[str] = None):
+        """Preload SSD rows into host memory (LoadSSD2Mem)."""
+        if self.ssd is None or self.host is None:
+            return 0
+        n = 0
+        for keys, vp in list(self.ssd.segments):
+            h = torch.from_numpy(keys.copy())
+            found, vals = self.ssd.get(h)
+            self.host.insert_mixed(h[found], self.cfg.sgd)
+            self.host.assign(h[found], vals[found])
+            n += int(found.sum())
+        return n
+
+    def shrink_table(self) -> int:
+        t = self._authoritative()
+        return t.shrink(self.cfg.shrink)
+
+    def shrink_resource(self):
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+
+    def check_need_limit_mem(self) -> bool:
+        if self.device.type != "cuda":
+            return False
+        free, total = torch.cuda.mem_get_info(self.device)
+        return free < 0.05 * total
+
+    def release_pool(self):
+        self.shrink_resource()
+
+    def finalize(self):
+        self.engine = None
+        BoxWrapper._instance = None
+
+    # ---------------------------------------------------------------- metrics / phases
+    def init_metric(self, *a, **k):
+        return self.metrics.init_metric(*a, **k)
+
+    def get_metric_msg(self, name):
+        return self.metrics.get_metric_msg(name)
+
+    def get_continue_metric_msg(self, name):
+        return self.metrics.get_continue_metric_msg(name)
+
+    def get_nan_inf_metric_msg(self, name):
+        return self.metrics.get_nan_inf_metric_msg(name)
+
+    def get_metric_name_list(self, metric_phase: int = -1):
+        return self.metrics.get_metric_name_list(metric_phase)
+
+    def flip_phase(self):
+        self.metrics.flip_phase()
+
+    def set_phase(self, p):
+        self.metrics.set_phase(p)
+
+    @property
+    def phase(self):
+        return self.metrics.phase
+
+    # ---------------------------------------------------------------- misc API parity
+    def set_dataset_name(self, name: str):
+        self.dataset_name = name
+
+    def set_input_table_dim(self, dim: int):
+        self.input_table_dim = dim
+
+    def init_afs_api(self, fs_name: str = "", fs_user: str = "", pass_wd: str = "", conf_path: str = ""):
+        from ..utils.fs import BoxFileMgr
+
+        self.fs = BoxFileMgr()
+        return 0
+
+    def print_device_info(self) -> str:
+        s = f"rank={self.rank}/{self.world} device={self.device} mode={self.mode}"
+        if self.engine is not None:
+            s += f" table={self.engine.table.size()} rows, {self.engine.table.memory_bytes() / 2**30:.2f} GiB"
+        if self.device.type == "cuda":
+            free, total = torch.cuda.mem_get_info(self.device)
+            s += f" hbm_free={free / 2**30:.1f}/{total / 2**30:.1f} GiB"
+        logger().info(s)
+        return s
+
+    def print_sync_timer(self) -> str:
+        s = self.timers.format()
+        logger().info(f"[rank {self.rank}] {s}")
+        return s
+
+    # ---------------------------------------------------------------- helpers
+    def _require_engine(self) -> SparseEngine:
+        if self.engine is None:
+            self.initialize_gpu_and_load_model()
+        return self.engine

@@ -138,6 +138,17 @@ class CpuSparseTable:
         self._keys, self._vals = self._keys[keep], v[keep]
         return deleted
 
+    def clear(self):
+        if self._native is not None:
+            self._native.clear()
+        else:
+            self._keys = torch.empty(0, dtype=torch.int64)
+            self._vals = torch.empty(0, self.stride, dtype=torch.float32)
+
+    def select_for_save(self, mode: int, f) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Native xbox filter (mode 0 base, 1 delta, 2 all); resets delta."""
+        return self._native.select_for_save(mode, f)
+
     def memory_bytes(self) -> int:
         return self.size() * (8 + 4 * self.stride)
 

@@ -72,6 +72,9 @@ class GpuSparseTable:
         out[ok] = self.t.values[rows[ok]]
         return out
 
+    def clear(self):
+        self.t.clear()
+
     def shrink(self, cfg: ShrinkConfig) -> int:
         return int(self.t.shrink(cfg.to_native(self._mod)))
 

@@ -1,0 +1,101 @@
+"""FLAGS_* registry (PaddleBox flag set, reference platform/flags.cc:926-1013).
+
+Backed by the native registry in ``_pbx_host`` when built (so C++ components
+see the same values); otherwise a Python dict seeded from the environment.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict
+
+_DEFAULTS: Dict[str, str] = {
+    "enable_pullpush_dedup_keys": "true",
+    "enable_pull_box_padding_zero": "true",
+    "padbox_record_pool_max_size": "2000000",
+    "padbox_slotrecord_extend_dim": "2",
+    "padbox_slotpool_thread_num": "1",
+    "padbox_dataset_shuffle_thread_num": "20",
+    "padbox_dataset_merge_thread_num": "20",
+    "padbox_dataset_disable_shuffle": "false",
+    "padbox_dataset_disable_polling": "false",
+    "padbox_dataset_enable_unrollinstance": "false",
+    "padbox_auc_runner_mode": "false",
+    "padbox_disable_ins_shuffle": "false",
+    "padbox_enable_gc": "true",
+    "padbox_enable_print_op_debug": "false",
+    "enable_print_dump_field_debug": "false",
+    "enable_print_dump_info_debug": "false",
+    "padbox_enable_sharding_stage": "false",
+    "padbox_dump_debug_lineid": "",
+    "use_gpu_replica_cache": "false",
+    "gpu_replica_cache_dim": "8",
+    "fix_dayid": "false",
+    "enable_binding_train_cpu": "true",
+    "enable_sync_dense_moment": "false",
+    "enable_dense_nccl_barrier": "false",
+    "enable_shuffle_by_searchid": "false",
+    "enbale_slotpool_auto_clear": "false",
+    "enable_slotpool_wait_release": "false",
+    "enable_slotrecord_reset_shrink": "false",
+    "enable_ins_parser_file": "false",
+    "enable_ins_parser_add_file_path": "false",
+    "lineid_have_extend_info": "false",
+    "dump_filed_same_as_aibox": "false",
+    "enable_dump_main_program": "false",
+    "enable_debug_print_metrics_info": "false",
+    "check_nan_inf": "false",
+    "enable_force_hbm_recyle": "false",
+    "enable_force_mem_recyle": "false",
+    "padbox_max_keys_per_batch": "0",
+}
+_py: Dict[str, str] = {k: os.environ.get("FLAGS_" + k, v) for k, v in _DEFAULTS.items()}
+
+
+def _native():
+    try:
+        from .. import _native as n
+
+        return n.host() if n.host_available() else None
+    except Exception:  # pragma: no cover
+        return None
+
+
+def get(name: str) -> str:
+    h = _native()
+    if h is not None:
+        return h.flag_get(name)
+    return _py[name]
+
+
+def get_bool(name: str) -> bool:
+    return get(name).lower() in ("1", "true", "yes")
+
+
+def get_int(name: str) -> int:
+    return int(get(name))
+
+
+def set_flags(d: Dict[str, object]):
+    """paddle.set_flags({'FLAGS_x': v}) equivalent (prefix optional)."""
+    h = _native()
+    for k, v in d.items():
+        k = k[6:] if k.startswith("FLAGS_") else k
+        sv = str(v).lower() if isinstance(v, bool) else str(v)
+        if k not in _py:
+            raise KeyError(f"unknown flag {k}")
+        if h is not None:
+            h.flag_set(k, sv)
+        if k not in _py:
+            raise KeyError(f"unknown flag {k}")
+        _py[k] = sv
+
+
+def get_flags(names) -> Dict[str, str]:
+    if isinstance(names, str):
+        names = [names]
+    return {("FLAGS_" + n if not n.startswith("FLAGS_") else n): get(n.replace("FLAGS_", "", 1)) for n in names}
+
+
+def all_flags() -> Dict[str, str]:
+    h = _native()
+    return dict(h.flags_all()) if h is not None else dict(_py)

@@ -1,0 +1,185 @@
+"""CPU engine: fused pull/push semantics, pass lifecycle, tiers, checkpoints,
+metrics (BASELINE config 1: in-process CPU PS)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from paddlebox_amd.data.synthetic import CriteoSynth, ragged_batch
+from paddlebox_amd.models.deepfm import DeepFM
+from paddlebox_amd.ops import reference as ref
+from paddlebox_amd.parallel.dense import DenseArena, FlatAdam
+from paddlebox_amd.ps.box_wrapper import BoxWrapper
+from paddlebox_amd.ps.config import PSConfig, row_layout
+from paddlebox_amd.ps.sparse_engine import SeqpoolParams, SparseEngine
+
+CPU = torch.device("cpu")
+
+
+def _engine(**kw):
+    cfg = PSConfig(embedx_dim=8)
+    cfg.sgd.mf_create_thresholds = 0.05
+    return SparseEngine(cfg, max_keys=100000, device=CPU, **kw)
+
+
+def test_engine_pull_push_roundtrip():
+    b = ragged_batch(16, 4, 3, 30, seed=0)
+    eng = _engine()
+    eng.register_keys(b.keys)
+    assert eng.table.size() == torch.unique(b.keys).numel()
+    sp = SeqpoolParams()
+    out = torch.zeros(b.B, b.S * 11)
+    st = eng.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out, 0, sp)
+    # fresh table: show/click 0 -> log(1)=0, embed 0
+    assert out.abs().sum() == 0
+    dout = torch.randn_like(out) * 0.01
+    eng.push_seqpool_cvm(st, dout, b.cvm, 0, sp, float(b.B))
+    uniq, uid = ref.dedup(b.keys)
+    v = eng.table.read(uniq)
+    cnt = torch.bincount(uid.long(), minlength=uniq.numel()).float()
+    torch.testing.assert_close(v[:, 0], cnt)  # show = occurrences
+    assert (v[:, row_layout(8)["mf_size"]] == 1).all()  # created (score 0.1*show >= 0.05)
+    out2 = torch.zeros_like(out)
+    eng.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out2, 0, sp)
+    assert out2.abs().sum() > 0
+
+
+def test_deepfm_trains_on_cpu_and_auc_rises():
+    torch.manual_seed(0)
+    synth = CriteoSynth(total_features=50000, alpha=1.2, seed=0)
+    eng = SparseEngine(PSConfig(embedx_dim=8), max_keys=512 * 26, device=CPU, auto_insert=True)
+    model = DeepFM(eng, hidden=(32, 16))
+    arena = DenseArena(model.parameters(), CPU)
+    opt = FlatAdam(arena, lr=5e-3)
+    tab = torch.zeros(2 * 1000, dtype=torch.float64)
+    st = torch.zeros(5, dtype=torch.float64)
+    losses = []
+    for i in range(60):
+        b = synth.batch(512)
+        arena.zero_grad()
+        loss, pred = model(b)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.detach()))
+        if i >= 40:
+            ref.auc_accumulate(pred.detach(), b.label, tab, st)
+    assert np.mean(losses[-10:]) < np.mean(losses[:10])
+    from paddlebox_amd import _native
+
+    c = _native.host().AucCalculator(1000)
+    c.merge_tables(tab, st)
+    c.compute()
+    assert c.auc > 0.54  # learnable synthetic signal, short run
+
+
+def test_box_wrapper_pass_lifecycle_and_checkpoint(tmp_path):
+    box = BoxWrapper(8, device="cpu")
+    box.initialize_gpu_and_load_model(slot_vector=[1, 2, 3], max_keys=50000)
+    b = ragged_batch(32, 3, 3, 40, seed=5)
+    box.feed_pass(b.keys, "20240101")
+    box.begin_pass()
+    eng = box.engine
+    sp = SeqpoolParams()
+    out = torch.zeros(b.B, b.S * 11)
+    for _ in range(3):
+        st = eng.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out, 0, sp)
+        eng.push_seqpool_cvm(st, torch.randn_like(out), b.cvm, 0, sp, float(b.B))
+    box.end_pass()
+    n = box.engine.table.size()
+    h, v = box.engine.table.export(True)  # batch model is written before xbox resets delta_score
+    msg = box.save_base(str(tmp_path / "batch"), str(tmp_path / "xbox"), "20240101")
+    assert "batch=" in msg
+    assert os.path.exists(tmp_path / "manifest.json")
+    # reload into a fresh wrapper
+    box2 = BoxWrapper(8, device="cpu")
+    box2.initialize_gpu_and_load_model(slot_vector=[1, 2, 3], max_keys=50000, model_path=str(tmp_path / "batch"))
+    assert box2.engine.table.size() == n
+    v2 = box2.engine.table.read(h)
+    torch.testing.assert_close(v2, v)
+    # xbox text parses back
+    from paddlebox_amd.ps import checkpoint as ck
+
+    keys, rows = ck.load_xbox_text(str(tmp_path / "xbox" / "part-00000.txt"), 8)
+    assert keys.shape[0] <= n
+    # delta after more training
+    box.begin_pass()
+    st = eng.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out, 0, sp)
+    eng.push_seqpool_cvm(st, torch.randn_like(out), b.cvm, 0, sp, float(b.B))
+    box.end_pass(True)
+    assert "xbox_delta" in box.save_delta(str(tmp_path / "delta"))
+    assert box.shrink_table() >= 0
+
+
+def test_tiered_mode_with_ssd(tmp_path):
+    box = BoxWrapper(8, device="cpu")
+    box.initialize_gpu_and_load_model(slot_vector=[1, 2], max_keys=50000, mode="tiered",
+                                      ssd_path=str(tmp_path / "ssd"))
+    eng = box.engine
+    sp = SeqpoolParams()
+    b1 = ragged_batch(16, 2, 2, 20, seed=1)
+    box.feed_pass(b1.keys)
+    box.begin_pass()
+    out = torch.zeros(b1.B, b1.S * 11)
+    st = eng.pull_seqpool_cvm(b1.keys, b1.lod, b1.B, b1.S, out, 0, sp)
+    eng.push_seqpool_cvm(st, torch.randn_like(out), b1.cvm, 0, sp, float(b1.B))
+    box.end_pass()
+    uniq = torch.unique(ref.mix64(b1.keys))
+    host_rows = box.host.read(uniq)
+    assert (host_rows[:, 0] > 0).all()  # written back
+    # age everything (no deletion) -> spill to SSD on the next end_pass
+    box.cfg.shrink.delete_threshold = 0.0
+    box.shrink_table()
+    b2 = ragged_batch(16, 2, 2, 20, seed=2)
+    b2.keys += 10**6
+    box.feed_pass(b2.keys)
+    box.begin_pass()
+    box.end_pass()
+    assert len(box.ssd) > 0
+    # b1 keys come back from SSD with their statistics
+    box.feed_pass(b1.keys)
+    got = box.engine.table.read(uniq)
+    torch.testing.assert_close(got[:, 0], host_rows[:, 0] * box.cfg.shrink.show_click_decay_rate)
+
+
+def test_metric_registry_kinds():
+    box = BoxWrapper(8, device="cpu")
+    box.initialize_gpu_and_load_model(max_keys=1000)
+    box.init_metric("AucCalculator", "auc", "label", "pred", bucket_size=1000)
+    box.init_metric("MaskAucCalculator", "mauc", "label", "pred", mask_varname="mask", bucket_size=1000)
+    box.init_metric("CmatchRankAucCalculator", "crauc", "label", "pred", cmatch_rank_varname="cr",
+                    cmatch_rank_group="222_1 223_2", bucket_size=1000)
+    box.init_metric("ContinueMaskCalculator", "cont", "label", "pred", mask_varname="mask")
+    box.init_metric("NanInfCalculator", "nan", "label", "pred")
+    box.init_metric("MultiTaskAucCalculator", "mt", "label", "pred pred2", cmatch_rank_varname="cr",
+                    cmatch_rank_group="222_1 223_2", bucket_size=1000)
+    box.init_metric("WuAucCalculator", "wu", "label", "pred", uid_varname="uid", bucket_size=1000)
+    n = 400
+    p = torch.rand(n)
+    y = (torch.rand(n) < p).float()
+    cr = torch.where(torch.rand(n) < 0.5, torch.tensor((222 << 32) | 1), torch.tensor((223 << 32) | 2))
+    fetch = {"label": y, "pred": p, "pred2": p, "mask": (torch.rand(n) < 0.5).float(), "cr": cr,
+             "uid": torch.randint(0, 10, (n,))}
+    box.metrics.add_batch(fetch)
+    m = box.get_metric_msg("auc")
+    assert len(m) == 8 and 0.6 < m[0] <= 1.0 and m[-1] == n
+    assert box.get_metric_msg("mauc")[-1] == pytest.approx(float(fetch["mask"].sum()))
+    assert box.get_metric_msg("crauc")[-1] == n
+    assert len(box.get_continue_metric_msg("cont")) == 5
+    assert box.get_nan_inf_metric_msg("nan")[0] == 0
+    assert box.get_metric_msg("mt")[-1] == n
+    wu = box.get_metric_msg("wu")
+    assert wu[2] > 0
+    # phase gating
+    box.init_metric("AucCalculator", "join_only", "label", "pred", metric_phase=1, bucket_size=1000)
+    box.set_phase(0)
+    box.metrics.add_batch(fetch)
+    assert box.get_metric_msg("join_only")[-1] == 0
+
+
+def test_day_id():
+    from paddlebox_amd.utils.dayid import make_day_id
+
+    # 2019-08-17 00:00 UTC = day 18125; with the -8h offset -> 18124
+    assert make_day_id(2019, 8, 17, fix_dayid=True) == 18125
+    assert make_day_id(2019, 8, 17, fix_dayid=False) == 18124
