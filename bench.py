@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--num-batches", type=int, default=16, help="distinct synthetic batches cycled")
     ap.add_argument("--no-prefill", action="store_true")
     ap.add_argument("--hidden", type=str, default="400,400,400")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=True,
+                    help="capture the train step into HIP graphs (default)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -93,6 +96,7 @@ def main():
     model = DeepFM(engine, num_slots=S, dense_dim=13, hidden=hidden).to(device)
     if world > 1:
         model.dn.group = dist.group.WORLD
+        model.dn.sync_stats = True
     arena = DenseArena(model.parameters(), device)
     opt = FlatAdam(arena, lr=1e-3)
     sync = DenseSync(arena, mode="grad_allreduce")
@@ -104,30 +108,53 @@ def main():
     auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
     auc_stats = torch.zeros(5, dtype=torch.float64, device=device)
 
-    def fetch(i):
-        with torch.cuda.stream(copy_stream):
-            b = host_batches[i % len(host_batches)].to(device, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(copy_stream)
-        return b, ev
-
-    def step(b, ev):
-        torch.cuda.current_stream().wait_event(ev)
-        for t in (b.keys, b.lod, b.dense, b.label, b.cvm):
-            t.record_stream(torch.cuda.current_stream())
+    def train_step(b):
         arena.zero_grad()
         loss, pred = model(b)
         loss.backward()
         sync.before_step()
         opt.step(sync.grad_scale())
         auc_accumulate(pred, b.label, auc_table, auc_stats)
-        return loss
+        return loss.detach()
 
-    nxt = fetch(0)
+    nb = len(host_batches)
+    graphed = None
+    if args.graph:
+        try:
+            from paddlebox_amd.runtime.graph_step import GraphedTrainStep
+
+            graphed = GraphedTrainStep(train_step, host_batches[0], device)
+            log(rank, "[bench] training step captured into HIP graphs")
+        except Exception as e:  # pragma: no cover - depends on runtime
+            log(rank, f"[bench] graph capture failed ({e!r}); running eagerly")
+            graphed = None
+
+    if graphed is not None:
+        graphed.load(0, host_batches[0])
+
+        def run(i):
+            graphed.load((i + 1) % graphed.n, host_batches[(i + 1) % nb])
+            return graphed.run(i % graphed.n)
+    else:
+        def fetch(i):
+            with torch.cuda.stream(copy_stream):
+                b = host_batches[i % nb].to(device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(copy_stream)
+            return b, ev
+
+        pending = [fetch(0)]
+
+        def run(i):
+            b, ev = pending.pop()
+            pending.append(fetch(i + 1))
+            torch.cuda.current_stream().wait_event(ev)
+            for t in (b.keys, b.lod, b.dense, b.label, b.cvm):
+                t.record_stream(torch.cuda.current_stream())
+            return train_step(b)
+
     for i in range(args.warmup):
-        cur = nxt
-        nxt = fetch(i + 1)
-        step(*cur)
+        run(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -135,9 +162,7 @@ def main():
     t_start = time.perf_counter()
     loss = None
     for i in range(args.steps):
-        cur = nxt
-        nxt = fetch(args.warmup + i + 1)
-        loss = step(*cur)
+        loss = run(args.warmup + i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

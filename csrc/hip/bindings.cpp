@@ -318,8 +318,170 @@ static std::vector<Tensor> data_norm_bwd(const Tensor& x, const Tensor& dy, cons
   const int N = (int)x.size(0), C = (int)x.size(1);
   Tensor dx = need_dx ? torch::empty_like(x) : Tensor();
   auto stats = torch::empty({3, C}, x.options());
+  auto acc = torch::empty({2, C}, x.options());
   launch_data_norm_bwd(ptr<float>(x), ptr<float>(dy), N, C, ptr<float>(means), ptr<float>(scales), eps,
-                       need_dx ? ptr<float>(dx) : nullptr, ptr<float>(stats), optr<float>(scale_w), cur_stream());
+                       need_dx ? ptr<float>(dx) : nullptr, ptr<float>(stats), ptr<float>(acc), optr<float>(scale_w),
+                       cur_stream());
+  return {dx, stats};
+}
+
+// ---------------------------------------------------------------- MLP (MFMA GEMM)
+static void check_bf16(const Tensor& t, const char* n) {
+  check_cuda(t, n);
+  PBX_CHECK(t.scalar_type() == torch::kBFloat16 && t.dim() == 2, std::string(n) + " must be bf16 2-D");
+}
+
+// y = act(x w^T + b): x bf16 [M,K], w bf16 [N,K], b f32 [N] -> y bf16 [M,N]
+static Tensor linear_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool relu) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  PBX_CHECK(w.size(1) == K, "linear_fwd: K mismatch");
+  PBX_CHECK(K % 8 == 0, "linear_fwd: K must be a multiple of 8 (pad the input)");
+  auto y = torch::empty({M, N}, x.options());
+  GemmArgs g;
+  g.A = reinterpret_cast<const unsigned short*>(x.data_ptr());
+  g.B = reinterpret_cast<const unsigned short*>(w.data_ptr());
+  g.C = y.data_ptr();
+  g.bias = optr<float>(bias);
+  g.M = M; g.N = N; g.K = K;
+  g.lda = K; g.ldb = K; g.ldc = N;
+  g.a_kcontig = true; g.b_kcontig = true;
+  g.epi = relu ? EPI_BIAS_RELU_BF16 : EPI_BIAS_BF16;
+  launch_gemm(g, cur_stream());
+  return y;
+}
+
+// Backward of linear_fwd.  dy bf16 [M,N] (grad wrt the layer output),
+// ymask (the layer output when relu was applied), x bf16 [M,K], w bf16 [N,K].
+// Accumulates dW f32 [N,K] and db f32 [N]; returns dx bf16 [M,K] (or undefined).
+static Tensor linear_bwd(const Tensor& dy, const c10::optional<Tensor>& ymask, const Tensor& x, const Tensor& w,
+                         Tensor dW, Tensor db, bool need_dx, int k_split) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  const int M = (int)dy.size(0), N = (int)dy.size(1), K = (int)x.size(1);
+  PBX_CHECK(w.size(0) == N && w.size(1) == K && x.size(0) == M, "linear_bwd shapes");
+  PBX_CHECK(N % 8 == 0 && K % 8 == 0, "linear_bwd: N, K must be multiples of 8");
+  auto s = cur_stream();
+  const unsigned short* mk = ymask.has_value() ? reinterpret_cast<const unsigned short*>(ymask->data_ptr()) : nullptr;
+  Tensor dx;
+  if (need_dx) {
+    dx = torch::empty({M, K}, x.options());
+    GemmArgs g;
+    g.A = reinterpret_cast<const unsigned short*>(dy.data_ptr());
+    g.maskA = mk;
+    g.B = reinterpret_cast<const unsigned short*>(w.data_ptr());
+    g.C = dx.data_ptr();
+    g.M = M; g.N = K; g.K = N;
+    g.lda = N; g.ldb = K; g.ldc = K;
+    g.a_kcontig = true; g.b_kcontig = false;
+    g.epi = EPI_BF16;
+    launch_gemm(g, s);
+  }
+  // dW (+db via the virtual ones column), split-K over the batch
+  const int ks = k_split > 0 ? k_split : 512;
+  const int splits = (M + ks - 1) / ks;
+  auto slab = torch::empty({splits, N, K + 1}, dW.options());
+  GemmArgs g;
+  g.A = reinterpret_cast<const unsigned short*>(dy.data_ptr());
+  g.maskA = mk;
+  g.B = reinterpret_cast<const unsigned short*>(x.data_ptr());
+  g.C = slab.data_ptr();
+  g.M = N; g.N = K; g.K = M;
+  g.lda = N; g.ldb = K; g.ldc = K + 1;
+  g.a_kcontig = false; g.b_kcontig = false;
+  g.ones_col_b = K;
+  g.epi = EPI_F32_SLAB;
+  g.k_per_split = ks;
+  g.slab_stride = (int64_t)N * (K + 1);
+  launch_gemm(g, s);
+  launch_slab_reduce(ptr<float>(slab), splits, g.slab_stride, N, K, K + 1, ptr<float>(dW), ptr<float>(db), 1.f, s);
+  return dx;
+}
+
+static Tensor gemv_out(const Tensor& h, const Tensor& w, const c10::optional<Tensor>& b) {
+  check_bf16(h, "h");
+  const int M = (int)h.size(0), K = (int)h.size(1);
+  auto out = torch::empty({M}, h.options().dtype(torch::kFloat32));
+  launch_gemv_out(reinterpret_cast<const unsigned short*>(h.data_ptr()), M, K, K, ptr<float>(w), optr<float>(b),
+                  ptr<float>(out), cur_stream());
+  return out;
+}
+
+static Tensor gemv_out_bwd(const Tensor& h, const Tensor& w, const Tensor& dout, Tensor dw, Tensor db) {
+  check_bf16(h, "h");
+  const int M = (int)h.size(0), K = (int)h.size(1);
+  auto dh = torch::empty_like(h);
+  auto d = dout.contiguous();
+  auto part = torch::empty({gemv_out_bwd_blocks(M), K + 1}, dw.options());
+  launch_gemv_out_bwd(reinterpret_cast<const unsigned short*>(h.data_ptr()), M, K, K, ptr<float>(w), ptr<float>(d),
+                      reinterpret_cast<unsigned short*>(dh.data_ptr()), ptr<float>(dw), ptr<float>(db),
+                      ptr<float>(part), cur_stream());
+  return dh;
+}
+
+static void cast_bf16(const Tensor& x, Tensor y) {
+  check_cuda(x, "x");
+  PBX_CHECK(y.scalar_type() == torch::kBFloat16 && y.numel() == x.numel(), "cast_bf16");
+  launch_f32_to_bf16(ptr<float>(x), reinterpret_cast<unsigned short*>(y.data_ptr()), x.numel(), cur_stream());
+}
+
+// Fused data_norm + first/FM head.  Returns (y bf16 [B,Cp], lin [B], means, scales).
+static std::vector<Tensor> head_fwd(const Tensor& x, int S, int Eo, int ew_col, int D, int Cp,
+                                    const c10::optional<Tensor>& bsize, const c10::optional<Tensor>& bsum,
+                                    const c10::optional<Tensor>& bsq) {
+  check_cuda(x, "x");
+  PBX_CHECK(x.scalar_type() == torch::kFloat32 && x.dim() == 2, "head: x must be fp32 [B, C]");
+  const int B = (int)x.size(0), C = (int)x.size(1);
+  PBX_CHECK(Cp >= C && S * Eo <= C, "head: bad widths");
+  PBX_CHECK(head_lds_bytes(C, D) <= 160 * 1024, "head: row slab exceeds LDS");
+  HeadArgs a;
+  a.x = ptr<float>(x);
+  a.B = B; a.C = C; a.Cp = Cp; a.S = S; a.Eo = Eo; a.ew_col = ew_col; a.D = D;
+  auto y = torch::empty({B, Cp}, x.options().dtype(torch::kBFloat16));
+  auto lin = torch::empty({B}, x.options());
+  Tensor means, scales;
+  if (bsize.has_value()) {
+    means = torch::empty({C}, x.options());
+    scales = torch::empty({C}, x.options());
+    a.bsize = ptr<float>(*bsize); a.bsum = ptr<float>(*bsum); a.bsq = ptr<float>(*bsq);
+    a.means = ptr<float>(means); a.scales = ptr<float>(scales);
+  }
+  a.y = reinterpret_cast<unsigned short*>(y.data_ptr());
+  a.lin = ptr<float>(lin);
+  launch_head_fwd(a, cur_stream());
+  return {y, lin, means, scales};
+}
+
+// Backward: returns (dx fp32 [B,C], stats [3,C] or undefined).
+static std::vector<Tensor> head_bwd(const Tensor& x, const c10::optional<Tensor>& dy, const Tensor& dlin, int S,
+                                    int Eo, int ew_col, int D, int Cp, const c10::optional<Tensor>& means,
+                                    const c10::optional<Tensor>& scales, float eps) {
+  check_cuda(x, "x");
+  const int B = (int)x.size(0), C = (int)x.size(1);
+  HeadArgs a;
+  a.x = ptr<float>(x);
+  a.B = B; a.C = C; a.Cp = Cp; a.S = S; a.Eo = Eo; a.ew_col = ew_col; a.D = D;
+  auto dx = torch::empty_like(x);
+  Tensor stats, acc;
+  if (dy.has_value()) {
+    PBX_CHECK(dy->scalar_type() == torch::kBFloat16 && dy->size(1) == Cp && dy->is_contiguous(), "head: dy");
+    a.dy = reinterpret_cast<const unsigned short*>(dy->data_ptr());
+  }
+  auto dl = dlin.contiguous();
+  a.dlin = ptr<float>(dl);
+  a.dx = ptr<float>(dx);
+  if (means.has_value()) {
+    acc = torch::empty({head_blocks(B), 2 * C}, x.options());
+    stats = torch::empty({3, C}, x.options());
+    a.means = ptr<float>(*means);
+    a.scales = ptr<float>(*scales);
+    a.stat_acc = ptr<float>(acc);
+  }
+  launch_head_bwd(a, cur_stream());
+  if (means.has_value())
+    launch_dn_stats(ptr<float>(acc), head_blocks(B), C, B, eps, ptr<float>(stats), cur_stream());
   return {dx, stats};
 }
 
@@ -364,12 +526,13 @@ static void auc_accumulate(const Tensor& pred, const Tensor& label, const c10::o
                         (int)(table.numel() / 2), ptr<double>(table), ptr<double>(stats), cur_stream());
 }
 
-static void adam_flat(Tensor p, const Tensor& g, Tensor m, Tensor v, float lr, float b1, float b2, float eps,
-                      float b1pow, float b2pow, float grad_scale, float wd) {
+static void adam_flat(Tensor p, const Tensor& g, Tensor m, Tensor v, Tensor pows, float lr, float b1, float b2,
+                      float eps, float grad_scale, float wd) {
   check_cuda(p, "p");
   PBX_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam sizes");
-  launch_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), lr, b1, b2, eps, b1pow,
-                   b2pow, grad_scale, wd, cur_stream());
+  PBX_CHECK(pows.is_cuda() && pows.numel() >= 2 && pows.scalar_type() == torch::kFloat32, "adam pows");
+  launch_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), lr, b1, b2, eps,
+                   ptr<float>(pows), grad_scale, wd, cur_stream());
 }
 
 }  // namespace pbx
@@ -443,6 +606,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("data_norm_fwd", &data_norm_fwd);
   m.def("data_norm_bwd", &data_norm_bwd);
   m.def("data_norm_update", &data_norm_update);
+  m.def("head_fwd", &head_fwd);
+  m.def("head_bwd", &head_bwd);
+  m.def("linear_fwd", &linear_fwd);
+  m.def("linear_bwd", &linear_bwd);
+  m.def("gemv_out", &gemv_out);
+  m.def("gemv_out_bwd", &gemv_out_bwd);
+  m.def("cast_bf16", &cast_bf16);
   m.def("fm_fwd", &fm_fwd);
   m.def("fm_bwd", &fm_bwd);
   m.def("sigmoid_logloss", &sigmoid_logloss);

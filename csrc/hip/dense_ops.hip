@@ -39,21 +39,25 @@ __global__ void k_dn_fwd(const float* __restrict__ x, int N, int C, const float*
   }
 }
 
-// grid: (ceil(C/64)), block 256 = 4 waves; lane -> column, wave -> row phase
+// grid: (ceil(C/64), row chunks of 64); block 256 = 4 waves; lane -> column,
+// wave -> row phase.  Partial column sums go to acc[2, C] with one atomic per
+// column per block; k_dn_finish turns them into the summary stats.
+constexpr int kDnRows = 64;
 __global__ __launch_bounds__(256) void k_dn_bwd(const float* __restrict__ x, const float* __restrict__ dy, int N,
                                                 int C, const float* __restrict__ means,
-                                                const float* __restrict__ scales, float eps,
-                                                float* __restrict__ dx, float* __restrict__ stats,
-                                                const float* scale_w) {
+                                                const float* __restrict__ scales, float* __restrict__ dx,
+                                                float* __restrict__ acc, const float* scale_w) {
   __shared__ float s_sum[4][64];
   __shared__ float s_sq[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * kDnRows;
+  const int r1 = min(N, r0 + kDnRows);
   float sum = 0.f, sq = 0.f;
   if (c < C) {
     const float mean = means[c];
     const float sc = scales[c] * (scale_w ? scale_w[c] : 1.f);
-    for (int r = w; r < N; r += 4) {
+    for (int r = r0 + w; r < r1; r += 4) {
       const int64_t i = (int64_t)r * C + c;
       const float xv = x[i];
       sum += xv;
@@ -66,12 +70,17 @@ __global__ __launch_bounds__(256) void k_dn_bwd(const float* __restrict__ x, con
   s_sq[w][lane] = sq;
   __syncthreads();
   if (w == 0 && c < C) {
-    const float ts = s_sum[0][lane] + s_sum[1][lane] + s_sum[2][lane] + s_sum[3][lane];
-    const float tq = s_sq[0][lane] + s_sq[1][lane] + s_sq[2][lane] + s_sq[3][lane];
-    stats[c] = 1.f;
-    stats[C + c] = ts / (float)N;
-    stats[2 * C + c] = tq / (float)N + eps;
+    atomicAdd(&acc[c], s_sum[0][lane] + s_sum[1][lane] + s_sum[2][lane] + s_sum[3][lane]);
+    atomicAdd(&acc[C + c], s_sq[0][lane] + s_sq[1][lane] + s_sq[2][lane] + s_sq[3][lane]);
   }
+}
+
+__global__ void k_dn_finish(const float* __restrict__ acc, int C, int N, float eps, float* __restrict__ stats) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  stats[c] = 1.f;
+  stats[C + c] = acc[c] / (float)N;
+  stats[2 * C + c] = acc[C + c] / (float)N + eps;
 }
 
 __global__ void k_dn_update(float* bsize, float* bsum, float* bsq, const float* __restrict__ st, int C,
@@ -173,10 +182,20 @@ __global__ void k_auc(const float* __restrict__ pred, const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------- Adam (flat)
+// beta powers live on the device (pows[0]=beta1^t, pows[1]=beta2^t) so the
+// whole optimizer step can be replayed from a HIP graph.
+__global__ void k_adam_pows(float* pows, float b1, float b2) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    pows[0] *= b1;
+    pows[1] *= b2;
+  }
+}
+
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                        float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
-                       float b1pow, float b2pow, float gs, float wd) {
+                       const float* __restrict__ pows, float gs, float wd) {
   const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const float b1pow = pows[0], b2pow = pows[1];
   const float lr_t = lr * sqrtf(1.f - b2pow) / (1.f - b1pow);
   if ((i4 + 1) * 4 <= n) {
     float4 pp = reinterpret_cast<float4*>(p)[i4];
@@ -215,10 +234,13 @@ void launch_data_norm_fwd(const float* x, int N, int C, const float* bsize, cons
 }
 
 void launch_data_norm_bwd(const float* x, const float* dy, int N, int C, const float* means,
-                          const float* scales, float eps, float* dx, float* stats,
+                          const float* scales, float eps, float* dx, float* stats, float* acc,
                           const float* scale_w, hipStream_t s) {
   if (C == 0) return;
-  hipLaunchKernelGGL(k_dn_bwd, dim3((C + 63) / 64), dim3(256), 0, s, x, dy, N, C, means, scales, eps, dx, stats, scale_w);
+  (void)hipMemsetAsync(acc, 0, 2 * (size_t)C * sizeof(float), s);
+  const dim3 g((C + 63) / 64, (N + kDnRows - 1) / kDnRows);
+  hipLaunchKernelGGL(k_dn_bwd, g, dim3(256), 0, s, x, dy, N, C, means, scales, dx, acc, scale_w);
+  hipLaunchKernelGGL(k_dn_finish, dim3(nblk(C)), dim3(256), 0, s, acc, C, N, eps, stats);
 }
 
 void launch_data_norm_update(float* bsize, float* bsum, float* bsq, const float* stats, int C,
@@ -252,11 +274,12 @@ void launch_auc_accumulate(const float* pred, const float* label, const float* m
 }
 
 void launch_adam_flat(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
-                      float b2, float eps, float b1pow, float b2pow, float grad_scale,
-                      float weight_decay, hipStream_t s) {
+                      float b2, float eps, float* pows, float grad_scale, float weight_decay,
+                      hipStream_t s) {
   if (n == 0) return;
   const int64_t n4 = (n + 3) / 4;
-  hipLaunchKernelGGL(k_adam, dim3(nblk(n4)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, b1pow, b2pow, grad_scale, weight_decay);
+  hipLaunchKernelGGL(k_adam_pows, dim3(1), dim3(64), 0, s, pows, b1, b2);
+  hipLaunchKernelGGL(k_adam, dim3(nblk(n4)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, pows, grad_scale, weight_decay);
 }
 
 }  // namespace pbx

@@ -1,0 +1,181 @@
+// Fused CTR "head": data_norm + DeepFM first/second-order terms over the
+// concatenated [pooled slots | dense] matrix, and its backward.
+//
+// Replaces a chain of ~10 kernels (data_norm fwd, bf16 cast for the MLP, FM
+// fwd, first-order slice+sum; FM bwd, data_norm bwd + stats, 3 gradient adds)
+// with one pass over x per direction.  A workgroup owns RB consecutive rows:
+// rows are contiguous in memory, so the block's slab is staged into LDS with
+// fully coalesced loads, then FM reductions read LDS; the data_norm summary
+// statistics are reduced per block in LDS and added to a [2, C] accumulator
+// with one atomic per column per block.
+//
+// Semantics: data_norm (reference paddle/fluid/operators/data_norm_op.cu:38-104)
+// and the DeepFM FM term 0.5*sum_d[(sum_s v)^2 - sum_s v^2].
+#include <hip/hip_bf16.h>
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace pbx {
+namespace {
+
+constexpr int kRB = 16;  // rows per workgroup
+
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  // round-to-nearest-even
+  unsigned int u = __float_as_uint(f);
+  const unsigned int lsb = (u >> 16) & 1u;
+  u += 0x7FFFu + lsb;
+  return (unsigned short)(u >> 16);
+}
+__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(((unsigned int)h) << 16); }
+
+// dynamic LDS: xs[kRB][C] floats + s1[kRB][D]
+__global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* xs = lds;
+  const int C = a.C, Cp = a.Cp;
+  const int row0 = blockIdx.x * kRB;
+  const int rows = min(kRB, a.B - row0);
+  if (rows <= 0) return;
+  // 1) stage + data_norm output (bf16, padded to Cp)
+  for (int i = threadIdx.x; i < rows * Cp; i += blockDim.x) {
+    const int r = i / Cp, c = i - r * Cp;
+    float yv = 0.f;
+    if (c < C) {
+      const float v = a.x[(int64_t)(row0 + r) * C + c];
+      xs[r * C + c] = v;
+      if (a.bsize) {
+        const float bs = a.bsize[c];
+        const float mean = a.bsum[c] / bs;
+        const float sc = sqrtf(bs / a.bsq[c]);
+        yv = (v - mean) * sc;
+      } else {
+        yv = v;
+      }
+    }
+    a.y[(int64_t)(row0 + r) * Cp + c] = f2bf(yv);
+  }
+  if (blockIdx.x == 0 && a.means) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const float bs = a.bsize[c];
+      a.means[c] = a.bsum[c] / bs;
+      a.scales[c] = sqrtf(bs / a.bsq[c]);
+    }
+  }
+  __syncthreads();
+  // 2) first + FM per row: 16 threads per row (kRB=16 rows x 16 = 256)
+  const int r = threadIdx.x >> 4, t = threadIdx.x & 15;
+  float lin = 0.f;
+  if (r < rows) {
+    const float* xr = xs + r * C;
+    // first order: sum over slots of embed_w column
+    for (int s = t; s < a.S; s += 16) lin += xr[s * a.Eo + a.ew_col];
+    // FM: lane t handles dims d = t, t+16, ... (D <= 16 typical)
+    for (int d = t; d < a.D; d += 16) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int s = 0; s < a.S; ++s) {
+        const float v = xr[s * a.Eo + a.ew_col + 1 + d];
+        s1 += v;
+        s2 += v * v;
+      }
+      lin += 0.5f * (s1 * s1 - s2);
+    }
+  }
+  for (int off = 8; off > 0; off >>= 1) lin += __shfl_xor(lin, off, 16);
+  if (r < rows && t == 0) a.lin[row0 + r] = lin;
+}
+
+__global__ __launch_bounds__(256) void k_head_bwd(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int C = a.C, Cp = a.Cp, D = a.D;
+  float* xs = lds;                 // [kRB][C]
+  float* s1s = lds + kRB * C;      // [kRB][D]
+  const int row0 = blockIdx.x * kRB;
+  const int rows = min(kRB, a.B - row0);
+  if (rows <= 0) return;
+  for (int i = threadIdx.x; i < rows * C; i += blockDim.x) {
+    xs[i] = a.x[(int64_t)row0 * C + i];  // rows are contiguous
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < rows * D; i += blockDim.x) {
+    const int r = i / D, d = i - r * D;
+    const float* xr = xs + r * C;
+    float s1 = 0.f;
+    for (int s = 0; s < a.S; ++s) s1 += xr[s * a.Eo + a.ew_col + 1 + d];
+    s1s[r * D + d] = s1;
+  }
+  __syncthreads();
+  const int sparse_w = a.S * a.Eo;
+  for (int i = threadIdx.x; i < rows * C; i += blockDim.x) {
+    const int r = i / C, c = i - r * C;
+    const float sc = a.scales ? a.scales[c] : 1.f;
+    float g = a.dy ? bf2f(a.dy[(int64_t)(row0 + r) * Cp + c]) * sc : 0.f;
+    if (c < sparse_w) {
+      const int j = c % a.Eo;
+      const float dl = a.dlin[row0 + r];
+      if (j == a.ew_col) {
+        g += dl;
+      } else if (j > a.ew_col && j <= a.ew_col + D) {
+        const int d = j - a.ew_col - 1;
+        g += dl * (s1s[r * D + d] - xs[i]);
+      }
+    }
+    a.dx[(int64_t)row0 * C + i] = g;
+  }
+  // data_norm summary partials: sum x and sum (x-mean)^2 per column
+  if (a.stat_acc) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const float mean = a.means[c];
+      float sx = 0.f, sq = 0.f;
+      for (int r = 0; r < rows; ++r) {
+        const float v = xs[r * C + c];
+        sx += v;
+        sq += (v - mean) * (v - mean);
+      }
+      // per-block partial row (no same-address atomics across blocks)
+      a.stat_acc[(int64_t)blockIdx.x * 2 * C + c] = sx;
+      a.stat_acc[(int64_t)blockIdx.x * 2 * C + C + c] = sq;
+    }
+  }
+}
+
+// stats[3, C] from the [nrows, 2C] partial slab
+__global__ void k_dn_stats(const float* __restrict__ part, int nrows, int C, int N, float eps,
+                           float* __restrict__ stats) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float sx = 0.f, sq = 0.f;
+  for (int r = 0; r < nrows; ++r) {
+    sx += part[(int64_t)r * 2 * C + c];
+    sq += part[(int64_t)r * 2 * C + C + c];
+  }
+  stats[c] = 1.f;
+  stats[C + c] = sx / (float)N;
+  stats[2 * C + c] = sq / (float)N + eps;
+}
+
+}  // namespace
+
+size_t head_lds_bytes(int C, int D) { return (size_t)kRB * (C + D) * sizeof(float); }
+
+void launch_head_fwd(const HeadArgs& a, hipStream_t s) {
+  if (a.B == 0) return;
+  const unsigned g = (unsigned)((a.B + kRB - 1) / kRB);
+  hipLaunchKernelGGL(k_head_fwd, dim3(g), dim3(256), head_lds_bytes(a.C, a.D), s, a);
+}
+
+void launch_head_bwd(const HeadArgs& a, hipStream_t s) {
+  if (a.B == 0) return;
+  const unsigned g = (unsigned)((a.B + kRB - 1) / kRB);
+  hipLaunchKernelGGL(k_head_bwd, dim3(g), dim3(256), head_lds_bytes(a.C, a.D), s, a);
+}
+
+int head_blocks(int B) { return (B + kRB - 1) / kRB; }
+
+void launch_dn_stats(const float* part, int nrows, int C, int N, float eps, float* stats, hipStream_t s) {
+  if (C == 0) return;
+  hipLaunchKernelGGL(k_dn_stats, dim3((C + 255) / 256), dim3(256), 0, s, part, nrows, C, N, eps, stats);
+}
+
+}  // namespace pbx

@@ -162,9 +162,61 @@ void launch_data_norm_fwd(const float* x, int N, int C, const float* bsize, cons
                           const float* scale_w, const float* bias, hipStream_t s);
 void launch_data_norm_bwd(const float* x, const float* dy, int N, int C, const float* means,
                           const float* scales, float eps, float* dx, float* stats /*[3,C]*/,
-                          const float* scale_w, hipStream_t s);
+                          float* acc /*[2,C] scratch*/, const float* scale_w, hipStream_t s);
 void launch_data_norm_update(float* bsize, float* bsum, float* bsq, const float* stats, int C,
                              float decay, hipStream_t s);
+
+// bf16 MFMA GEMM for the MLP (csrc/hip/gemm.hip): C[M,N] = A'[M,K] B'[K,N]
+// with A'(m,k) at A[m*lda+k] (a_kcontig) or A[k*lda+m]; B'(k,n) at
+// B[n*ldb+k] (b_kcontig) or B[k*ldb+n].
+enum GemmEpi { EPI_BIAS_RELU_BF16 = 0, EPI_BIAS_BF16 = 1, EPI_BF16 = 2, EPI_F32_SLAB = 3 };
+struct GemmArgs {
+  const unsigned short* A = nullptr;
+  const unsigned short* maskA = nullptr;  // relu' mask in A's layout (bf16), optional
+  const unsigned short* B = nullptr;
+  void* C = nullptr;
+  const float* bias = nullptr;
+  int M = 0, N = 0, K = 0;
+  int lda = 0, ldb = 0, ldc = 0;
+  bool a_kcontig = true, b_kcontig = true;
+  int ones_col_b = -1;  // virtual all-ones B column at n == ones_col_b (bias grad)
+  int epi = EPI_BF16;
+  int k_per_split = 1 << 30;
+  int64_t slab_stride = 0;
+};
+void launch_gemm(const GemmArgs& g, hipStream_t s);
+void launch_slab_reduce(const float* slab, int splits, int64_t slab_stride, int M, int N, int ldc, float* dW,
+                        float* db, float scale, hipStream_t s);
+void launch_gemv_out(const unsigned short* h, int M, int K, int ldh, const float* w, const float* b, float* out,
+                     hipStream_t s);
+int gemv_out_bwd_blocks(int M);
+// part: scratch [gemv_out_bwd_blocks(M), K+1] f32 (per-block partial sums)
+void launch_gemv_out_bwd(const unsigned short* h, int M, int K, int ldh, const float* w, const float* dout,
+                         unsigned short* dh, float* dw, float* db, float* part, hipStream_t s);
+void launch_f32_to_bf16(const float* x, unsigned short* y, int64_t n, hipStream_t s);
+
+// Fused data_norm + first-order + FM head (csrc/hip/head_ops.hip).
+struct HeadArgs {
+  const float* x = nullptr;  // [B, C] fp32 (pooled slot blocks | dense)
+  int B = 0, C = 0, Cp = 0;  // Cp = C padded to a multiple of 8 (GEMM K)
+  int S = 0, Eo = 11, ew_col = 2, D = 8;
+  const float* bsize = nullptr;  // data_norm summaries (null = no data_norm)
+  const float* bsum = nullptr;
+  const float* bsq = nullptr;
+  float* means = nullptr;   // [C] out (fwd)
+  float* scales = nullptr;  // [C] out (fwd) / in (bwd)
+  unsigned short* y = nullptr;  // [B, Cp] bf16 out (fwd)
+  float* lin = nullptr;         // [B] first + FM out (fwd)
+  const unsigned short* dy = nullptr;  // [B, Cp] bf16 in (bwd)
+  const float* dlin = nullptr;         // [B] in (bwd)
+  float* dx = nullptr;                 // [B, C] out (bwd)
+  float* stat_acc = nullptr;           // [head_blocks(B), 2C] per-block partial sums (bwd)
+};
+size_t head_lds_bytes(int C, int D);
+int head_blocks(int B);
+void launch_head_fwd(const HeadArgs& a, hipStream_t s);
+void launch_head_bwd(const HeadArgs& a, hipStream_t s);
+void launch_dn_stats(const float* part, int nrows, int C, int N, float eps, float* stats, hipStream_t s);
 
 // DeepFM second-order FM over S fields of dim D read from x[b, col0 + s*fstride + d].
 void launch_fm_fwd(const float* x, int B, int S, int D, int row_stride, int col0, int fstride,
@@ -182,9 +234,10 @@ void launch_auc_accumulate(const float* pred, const float* label, const float* m
                            int nbuckets, double* table /*[2,nbuckets]*/, double* stats,
                            hipStream_t s);
 
-// Flat Adam over a contiguous fp32 buffer.
+// Flat Adam over a contiguous fp32 buffer; pows = device [beta1^t, beta2^t]
+// (advanced in-stream, graph-replayable).
 void launch_adam_flat(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
-                      float b2, float eps, float b1pow, float b2pow, float grad_scale,
-                      float weight_decay, hipStream_t s);
+                      float b2, float eps, float* pows, float grad_scale, float weight_decay,
+                      hipStream_t s);
 
 }  // namespace pbx

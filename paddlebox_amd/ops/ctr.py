@@ -88,6 +88,80 @@ class DataNorm(torch.nn.Module):
                                self.training)
 
 
+# ---------------------------------------------------------------- fused CTR head
+class _CtrHead(torch.autograd.Function):
+    """y = data_norm(x) (bf16, padded to Cp) and lin = first-order + FM, one
+    kernel each way on the GPU (csrc/hip/head_ops.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, dn: Optional[DataNorm], S, Eo, ew_col, D, Cp):
+        x = x.contiguous().float()
+        has_dn = dn is not None
+        if _gpu(x):
+            if has_dn:
+                y, lin, means, scales = _native.hip().head_fwd(x, S, Eo, ew_col, D, Cp, dn.batch_size, dn.batch_sum,
+                                                                dn.batch_square_sum)
+            else:
+                y, lin, means, scales = _native.hip().head_fwd(x, S, Eo, ew_col, D, Cp, None, None, None)
+        else:
+            if has_dn:
+                y, means, scales = ref.data_norm_fwd(x, dn.batch_size, dn.batch_sum, dn.batch_square_sum)
+            else:
+                y, means, scales = x, None, None
+            if Cp > y.shape[1]:
+                y = torch.nn.functional.pad(y, (0, Cp - y.shape[1]))
+            lin = x[:, ew_col:S * Eo:Eo].sum(1) + ref.fm_fwd(x, S, D, ew_col + 1, Eo)
+        ctx.save_for_backward(x)
+        ctx.means, ctx.scales = means, scales
+        ctx.dn, ctx.args = dn, (S, Eo, ew_col, D, Cp)
+        return y, lin
+
+    @staticmethod
+    def backward(ctx, dy, dlin):
+        (x,) = ctx.saved_tensors
+        S, Eo, ew_col, D, Cp = ctx.args
+        dn = ctx.dn
+        if dlin is None:
+            dlin = torch.zeros(x.shape[0], device=x.device)
+        if _gpu(x):
+            dyc = dy.contiguous() if dy is not None else None
+            if dyc is not None and dyc.dtype != torch.bfloat16:
+                dyc = dyc.to(torch.bfloat16)
+            dx, stats = _native.hip().head_bwd(x, dyc, dlin.contiguous().float(), S, Eo, ew_col, D, Cp, ctx.means,
+                                              ctx.scales, dn.eps if dn is not None else 0.0)
+        else:
+            with torch.enable_grad():
+                xx = x.detach().requires_grad_(True)
+                if dn is not None:
+                    y = (xx - ctx.means) * ctx.scales
+                else:
+                    y = xx
+                if Cp > y.shape[1]:
+                    y = torch.nn.functional.pad(y, (0, Cp - y.shape[1]))
+                lin = xx[:, ew_col:S * Eo:Eo].sum(1) + ref.fm_fwd(xx, S, D, ew_col + 1, Eo)
+                outs, grads = [lin], [dlin]
+                if dy is not None:
+                    outs.append(y)
+                    grads.append(dy.float())
+                (dx,) = torch.autograd.grad(outs, xx, grads)
+            stats = None
+            if dn is not None:
+                _, stats = ref.data_norm_bwd(x, x, ctx.means, ctx.scales, dn.eps)
+        if dn is not None and dn.training and dn.update_norm:
+            if dn.sync_stats and dn.group is not None and dist.is_initialized() and dist.get_world_size(dn.group) > 1:
+                dist.all_reduce(stats, group=dn.group)
+            if _gpu(x):
+                _native.hip().data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, stats, dn.decay)
+            else:
+                ref.data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, stats, dn.decay)
+        return dx, None, None, None, None, None, None
+
+
+def ctr_head(x: torch.Tensor, dn: Optional["DataNorm"], S: int, Eo: int, ew_col: int, D: int, Cp: int):
+    """(data_norm(x) as the MLP input [B, Cp], first-order + FM logit part [B])."""
+    return _CtrHead.apply(x, dn, S, Eo, ew_col, D, Cp)
+
+
 # ---------------------------------------------------------------- FM
 class _FM(torch.autograd.Function):
     @staticmethod

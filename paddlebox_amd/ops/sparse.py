@@ -17,10 +17,25 @@ import torch
 from ..ps.sparse_engine import SeqpoolParams, SparseEngine
 
 
+_ANCHORS = {}
+
+
+def _anchor(device) -> torch.Tensor:
+    """A leaf that requires grad, fed to the sparse Functions so their output
+    is part of the autograd graph even when no dense input requires grad
+    (the sparse table update happens in their backward)."""
+    d = torch.device(device)
+    a = _ANCHORS.get(d)
+    if a is None:
+        a = torch.zeros((), device=d, requires_grad=True)
+        _ANCHORS[d] = a
+    return a
+
+
 class _PullSeqpoolCvmConcat(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, dense: Optional[torch.Tensor], keys: torch.Tensor, lod: torch.Tensor, cvm: torch.Tensor,
-                engine: SparseEngine, B: int, S: int, sp: SeqpoolParams, bs_scale: float):
+    def forward(ctx, anchor: torch.Tensor, dense: Optional[torch.Tensor], keys: torch.Tensor, lod: torch.Tensor,
+                cvm: torch.Tensor, engine: SparseEngine, B: int, S: int, sp: SeqpoolParams, bs_scale: float):
         E = engine.E
         Eo = sp.out_width(E)
         Dd = 0 if dense is None else dense.shape[1]
@@ -38,7 +53,7 @@ class _PullSeqpoolCvmConcat(torch.autograd.Function):
         (cvm,) = ctx.saved_tensors
         ctx.engine.push_seqpool_cvm(ctx.st, dout, cvm, 0, ctx.sp, ctx.bs_scale)
         ddense = dout[:, ctx.S * ctx.Eo:] if ctx.Dd else None
-        return ddense, None, None, None, None, None, None, None, None
+        return None, ddense, None, None, None, None, None, None, None, None
 
 
 def pull_seqpool_cvm_concat(engine: SparseEngine, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int,
@@ -50,7 +65,7 @@ def pull_seqpool_cvm_concat(engine: SparseEngine, keys: torch.Tensor, lod: torch
     sparse table and passes d(dense) through."""
     sp = sp or SeqpoolParams()
     bs = float(B if bs_scale is None else bs_scale)
-    return _PullSeqpoolCvmConcat.apply(dense, keys, lod, cvm, engine, B, S, sp, bs)
+    return _PullSeqpoolCvmConcat.apply(_anchor(keys.device), dense, keys, lod, cvm, engine, B, S, sp, bs)
 
 
 class _PullBoxSparse(torch.autograd.Function):
@@ -70,5 +85,5 @@ class _PullBoxSparse(torch.autograd.Function):
 def pull_box_sparse(engine: SparseEngine, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int,
                     bs_scale: Optional[float] = None) -> torch.Tensor:
     """Per-occurrence pull records [L, 3+D] = [show, click, embed_w, embedx...]."""
-    anchor = torch.zeros((), requires_grad=True, device=keys.device)
-    return _PullBoxSparse.apply(anchor, keys, lod, engine, B, S, float(B if bs_scale is None else bs_scale))
+    return _PullBoxSparse.apply(_anchor(keys.device), keys, lod, engine, B, S,
+                                float(B if bs_scale is None else bs_scale))

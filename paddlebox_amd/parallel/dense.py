@@ -60,29 +60,27 @@ class FlatAdam:
         self.lr, self.b1, self.b2, self.eps, self.wd = lr, beta1, beta2, epsilon, weight_decay
         self.m = torch.zeros_like(arena.flat)
         self.v = torch.zeros_like(arena.flat)
-        self.t = 0
-        # beta powers kept on the host (deterministic; no per-step D2H)
-        self.b1pow = 1.0
-        self.b2pow = 1.0
+        # [beta1^t, beta2^t] on the device: advanced by the kernel itself so the
+        # step is HIP-graph replayable (no host scalars baked into the graph)
+        self.pows = torch.ones(2, dtype=torch.float32, device=arena.flat.device)
 
     def step(self, grad_scale: float = 1.0):
-        self.t += 1
-        self.b1pow *= self.b1
-        self.b2pow *= self.b2
         if self.a.flat.is_cuda:
-            _native.hip().adam_flat(self.a.flat, self.a.grad, self.m, self.v, self.lr, self.b1, self.b2, self.eps,
-                                    self.b1pow, self.b2pow, grad_scale, self.wd)
+            _native.hip().adam_flat(self.a.flat, self.a.grad, self.m, self.v, self.pows, self.lr, self.b1, self.b2,
+                                    self.eps, grad_scale, self.wd)
         else:
-            ref.adam_flat(self.a.flat, self.a.grad, self.m, self.v, self.lr, self.b1, self.b2, self.eps, self.b1pow,
-                          self.b2pow, grad_scale, self.wd)
+            self.pows[0] *= self.b1
+            self.pows[1] *= self.b2
+            ref.adam_flat(self.a.flat, self.a.grad, self.m, self.v, self.lr, self.b1, self.b2, self.eps,
+                          float(self.pows[0]), float(self.pows[1]), grad_scale, self.wd)
 
     def state_dict(self):
-        return {"m": self.m, "v": self.v, "t": self.t, "b1pow": self.b1pow, "b2pow": self.b2pow}
+        return {"m": self.m, "v": self.v, "pows": self.pows}
 
     def load_state_dict(self, sd):
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
-        self.t, self.b1pow, self.b2pow = sd["t"], sd["b1pow"], sd["b2pow"]
+        self.pows.copy_(sd["pows"])
 
 
 class DenseSync:

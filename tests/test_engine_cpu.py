@@ -65,6 +65,10 @@ def test_deepfm_trains_on_cpu_and_auc_rises():
         if i >= 40:
             ref.auc_accumulate(pred.detach(), b.label, tab, st)
     assert np.mean(losses[-10:]) < np.mean(losses[:10])
+    # the backward of the model reached the sparse table (push) and data_norm
+    h, v = eng.table.export(True)
+    assert float(v[:, 0].sum()) == pytest.approx(60 * 512 * 26)  # show = every occurrence
+    assert float(model.dn.batch_size[0]) != 1e4
     from paddlebox_amd import _native
 
     c = _native.host().AucCalculator(1000)

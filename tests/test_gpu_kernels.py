@@ -236,7 +236,9 @@ def test_data_norm_fm_loss_auc_adam():
     m1 = torch.zeros(n, device=DEV)
     v1 = torch.zeros(n, device=DEV)
     p2, m2, v2 = pp.clone(), m1.clone(), v1.clone()
-    hip().adam_flat(pp, gg, m1, v1, 1e-3, 0.9, 0.999, 1e-8, 0.9, 0.999, 0.5, 0.0)
+    pows = torch.ones(2, device=DEV)
+    hip().adam_flat(pp, gg, m1, v1, pows, 1e-3, 0.9, 0.999, 1e-8, 0.5, 0.0)
+    torch.testing.assert_close(pows, torch.tensor([0.9, 0.999], device=DEV))
     ref.adam_flat(p2, gg, m2, v2, 1e-3, 0.9, 0.999, 1e-8, 0.9, 0.999, 0.5, 0.0)
     torch.testing.assert_close(pp, p2)
 
@@ -261,3 +263,70 @@ def test_deepfm_trains_on_gpu():
         losses.append(float(loss))
     assert math.isfinite(losses[-1])
     assert sum(losses[-10:]) / 10 < sum(losses[:10]) / 10
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 400, 304), (8192, 400, 400), (64, 64, 64), (130, 72, 24)])
+def test_mfma_linear_fwd_bwd(M, N, K):
+    torch.manual_seed(M + N + K)
+    x = _bf(torch.randn(M, K, device=DEV))
+    w = _bf(torch.randn(N, K, device=DEV) * 0.1)
+    b = torch.randn(N, device=DEV)
+    y = hip().linear_fwd(x, w, b, True)
+    ye = torch.relu(x.float() @ w.float().t() + b)
+    torch.testing.assert_close(y.float(), ye, rtol=2e-2, atol=2e-2)
+    y2 = hip().linear_fwd(x, w, b, False)
+    torch.testing.assert_close(y2.float(), x.float() @ w.float().t() + b, rtol=2e-2, atol=2e-2)
+    dy = _bf(torch.randn(M, N, device=DEV))
+    dW = torch.zeros(N, K, device=DEV)
+    db = torch.zeros(N, device=DEV)
+    dx = hip().linear_bwd(dy, y, x, w, dW, db, True, 128)
+    dz = dy.float() * (y.float() > 0)
+    torch.testing.assert_close(dx.float(), dz @ w.float(), rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(dW, dz.t() @ x.float(), rtol=1e-2, atol=5e-2)
+    torch.testing.assert_close(db, dz.sum(0), rtol=1e-2, atol=5e-2)
+
+
+def test_gemv_out():
+    h = _bf(torch.rand(777, 400, device=DEV))
+    w = torch.randn(400, device=DEV)
+    b = torch.randn(1, device=DEV)
+    out = hip().gemv_out(h, w, b)
+    torch.testing.assert_close(out, h.float() @ w + b, rtol=1e-4, atol=1e-3)
+    dout = torch.randn(777, device=DEV)
+    dw = torch.zeros(400, device=DEV)
+    db = torch.zeros(1, device=DEV)
+    dh = hip().gemv_out_bwd(h, w, dout, dw, db)
+    torch.testing.assert_close(dh.float(), dout[:, None] * w[None, :], rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dw, dout @ h.float(), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(db, dout.sum().view(1), rtol=1e-4, atol=1e-3)
+
+
+def test_ctr_head_gpu_matches_cpu():
+    from paddlebox_amd.ops.ctr import DataNorm, ctr_head
+
+    torch.manual_seed(0)
+    B, S, Eo, D = 100, 26, 11, 8
+    C = S * Eo + 13
+    Cp = (C + 7) // 8 * 8
+    x = torch.randn(B, C)
+    dn_c = DataNorm(C)
+    dn_c.batch_sum.normal_()
+    dn_g = DataNorm(C).to(DEV)
+    dn_g.load_state_dict(dn_c.state_dict())
+    xc = x.clone().requires_grad_(True)
+    xg = x.to(DEV).requires_grad_(True)
+    yc, lc = ctr_head(xc, dn_c, S, Eo, 2, D, Cp)
+    yg, lg = ctr_head(xg, dn_g, S, Eo, 2, D, Cp)
+    torch.testing.assert_close(yg.float().cpu(), yc, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(lg.cpu(), lc, rtol=1e-4, atol=1e-3)
+    dy = torch.randn(B, Cp).to(torch.bfloat16).float()
+    dl = torch.randn(B)
+    ((yc * dy).sum() + (lc * dl).sum()).backward()  # one backward -> one summary update
+    ((yg.float() * dy.to(DEV)).sum() + (lg * dl.to(DEV)).sum()).backward()
+    torch.testing.assert_close(xg.grad.cpu(), xc.grad, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dn_g.batch_sum.cpu(), dn_c.batch_sum, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dn_g.batch_square_sum.cpu(), dn_c.batch_square_sum, rtol=1e-4, atol=1e-3)
