@@ -480,8 +480,10 @@ static std::vector<Tensor> head_bwd(const Tensor& x, const c10::optional<Tensor>
     a.stat_acc = ptr<float>(acc);
   }
   launch_head_bwd(a, cur_stream());
-  if (means.has_value())
-    launch_dn_stats(ptr<float>(acc), head_blocks(B), C, B, eps, ptr<float>(stats), cur_stream());
+  if (means.has_value()) {
+    auto sums = torch::empty({2 * C}, x.options());
+    launch_dn_stats(ptr<float>(acc), head_blocks(B), C, B, eps, ptr<float>(stats), ptr<float>(sums), cur_stream());
+  }
   return {dx, stats};
 }
 

@@ -145,6 +145,10 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 #pragma unroll
   for (int i = 0; i < NACC; ++i) acc[i] = (f32x16){0};
   const int NB = g.N + (g.ones_col_b >= 0 ? 1 : 0);
+  // 1-tile-ahead register prefetch into a 2-deep LDS ring.  (Measured on
+  // MI355X: a deeper all-tiles-in-registers variant was 2x slower -- the
+  // per-tile guards made hipcc wait vmcnt(0) per load; see
+  // profiles/r1_gemm_notes.md.)
   Stage<BM> sa;
   Stage<BN> sb;
   int buf = 0;
@@ -256,15 +260,6 @@ __global__ __launch_bounds__(256) void k_gemv_out_bwd(const unsigned short* __re
   }
 }
 
-// column sums of the [nblk, K+1] partial slab, accumulated into dw[K], db[1]
-__global__ void k_colsum_acc(const float* __restrict__ part, int nrows, int K, float* __restrict__ dw,
-                             float* __restrict__ db) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k > K) return;
-  float s = 0.f;
-  for (int r = 0; r < nrows; ++r) s += part[(int64_t)r * (K + 1) + k];
-  if (k < K) dw[k] += s; else db[0] += s;
-}
 
 __global__ void k_f32_to_bf16(const float* __restrict__ x, unsigned short* __restrict__ y, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -281,13 +276,8 @@ inline unsigned int nblk(int64_t n, int per = 256) {
 void launch_gemm(const GemmArgs& g, hipStream_t s) {
   const int NB = g.N + (g.ones_col_b >= 0 ? 1 : 0);
   const int splits = (g.K + g.k_per_split - 1) / g.k_per_split;
-  if (g.M >= 1024) {  // tall: 128x64 tiles (4 waves stacked in M, 2 accumulators each)
-    dim3 grid((NB + 63) / 64, (g.M + 127) / 128, splits);
-    hipLaunchKernelGGL((k_gemm<128, 64, 4, 1>), grid, dim3(256), 0, s, g);
-  } else {
-    dim3 grid((NB + 63) / 64, (g.M + 63) / 64, splits);
-    hipLaunchKernelGGL((k_gemm<64, 64, 2, 2>), grid, dim3(256), 0, s, g);
-  }
+  dim3 grid((NB + 63) / 64, (g.M + 63) / 64, splits);
+  hipLaunchKernelGGL((k_gemm<64, 64, 2, 2>), grid, dim3(256), 0, s, g);
 }
 
 void launch_slab_reduce(const float* slab, int splits, int64_t slab_stride, int M, int N, int ldc, float* dW,
@@ -307,7 +297,7 @@ void launch_gemv_out_bwd(const unsigned short* h, int M, int K, int ldh, const f
                          unsigned short* dh, float* dw, float* db, float* part, hipStream_t s) {
   const int nb = gemv_out_bwd_blocks(M);
   hipLaunchKernelGGL(k_gemv_out_bwd, dim3(nb), dim3(256), 0, s, h, M, K, ldh, w, dout, dh, part);
-  hipLaunchKernelGGL(k_colsum_acc, dim3(nblk(K + 1)), dim3(256), 0, s, part, nb, K, dw, db);
+  launch_colsum_acc(part, nb, K + 1, dw, K, db, s);
 }
 
 void launch_f32_to_bf16(const float* x, unsigned short* y, int64_t n, hipStream_t s) {

@@ -140,19 +140,13 @@ __global__ __launch_bounds__(256) void k_head_bwd(HeadArgs a) {
   }
 }
 
-// stats[3, C] from the [nrows, 2C] partial slab
-__global__ void k_dn_stats(const float* __restrict__ part, int nrows, int C, int N, float eps,
-                           float* __restrict__ stats) {
+// stats[3, C] from the column-reduced [2C] sums
+__global__ void k_dn_stats(const float* __restrict__ acc, int C, int N, float eps, float* __restrict__ stats) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  float sx = 0.f, sq = 0.f;
-  for (int r = 0; r < nrows; ++r) {
-    sx += part[(int64_t)r * 2 * C + c];
-    sq += part[(int64_t)r * 2 * C + C + c];
-  }
   stats[c] = 1.f;
-  stats[C + c] = sx / (float)N;
-  stats[2 * C + c] = sq / (float)N + eps;
+  stats[C + c] = acc[c] / (float)N;
+  stats[2 * C + c] = acc[C + c] / (float)N + eps;
 }
 
 }  // namespace
@@ -173,9 +167,12 @@ void launch_head_bwd(const HeadArgs& a, hipStream_t s) {
 
 int head_blocks(int B) { return (B + kRB - 1) / kRB; }
 
-void launch_dn_stats(const float* part, int nrows, int C, int N, float eps, float* stats, hipStream_t s) {
+void launch_dn_stats(const float* part, int nrows, int C, int N, float eps, float* stats, float* acc,
+                     hipStream_t s) {
   if (C == 0) return;
-  hipLaunchKernelGGL(k_dn_stats, dim3((C + 255) / 256), dim3(256), 0, s, part, nrows, C, N, eps, stats);
+  (void)hipMemsetAsync(acc, 0, 2 * (size_t)C * sizeof(float), s);
+  launch_colsum_acc(part, nrows, 2 * C, acc, -1, nullptr, s);
+  hipLaunchKernelGGL(k_dn_stats, dim3((C + 255) / 256), dim3(256), 0, s, acc, C, N, eps, stats);
 }
 
 }  // namespace pbx

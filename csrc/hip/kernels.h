@@ -189,6 +189,8 @@ void launch_slab_reduce(const float* slab, int splits, int64_t slab_stride, int 
                         float* db, float scale, hipStream_t s);
 void launch_gemv_out(const unsigned short* h, int M, int K, int ldh, const float* w, const float* b, float* out,
                      hipStream_t s);
+// out[c] += sum_r part[r, c] for c < split_col, out2[c - split_col] += ... otherwise
+void launch_colsum_acc(const float* part, int R, int W, float* out, int split_col, float* out2, hipStream_t s);
 int gemv_out_bwd_blocks(int M);
 // part: scratch [gemv_out_bwd_blocks(M), K+1] f32 (per-block partial sums)
 void launch_gemv_out_bwd(const unsigned short* h, int M, int K, int ldh, const float* w, const float* dout,
@@ -216,7 +218,9 @@ size_t head_lds_bytes(int C, int D);
 int head_blocks(int B);
 void launch_head_fwd(const HeadArgs& a, hipStream_t s);
 void launch_head_bwd(const HeadArgs& a, hipStream_t s);
-void launch_dn_stats(const float* part, int nrows, int C, int N, float eps, float* stats, hipStream_t s);
+// acc: scratch [2C]
+void launch_dn_stats(const float* part, int nrows, int C, int N, float eps, float* stats, float* acc,
+                     hipStream_t s);
 
 // DeepFM second-order FM over S fields of dim D read from x[b, col0 + s*fstride + d].
 void launch_fm_fwd(const float* x, int B, int S, int D, int row_stride, int col0, int fstride,

@@ -29,6 +29,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
+from ..parallel.comm import Comm, default_comm
 from ..ops import reference as ref
 from .config import PSConfig, SparseSGDConfig, padded, pull_width, push_width
 from .cpu_table import CpuSparseTable
@@ -85,6 +86,7 @@ class SparseEngine:
         group=None,
         cap_factor: float = 1.25,
         auto_insert: bool = False,
+        comm: Optional[Comm] = None,
     ):
         self.cfg = cfg
         self.dim = cfg.embedx_dim
@@ -94,8 +96,9 @@ class SparseEngine:
         self.device = torch.device(device)
         self.max_keys = int(max_keys)
         self.group = group
-        self.world = dist.get_world_size(group) if (group is not None or (dist.is_available() and dist.is_initialized())) else 1
-        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        self.comm = comm if comm is not None else default_comm(group)
+        self.world = self.comm.world if self.comm is not None else 1
+        self.rank = self.comm.rank if self.comm is not None else 0
         self.auto_insert = auto_insert
         self.test_mode = False
         self.is_gpu = self.device.type == "cuda"
@@ -150,9 +153,9 @@ class SparseEngine:
             h = h[order]
             counts = torch.bincount(owner, minlength=self.world)
             in_counts = torch.empty_like(counts)
-            dist.all_to_all_single(in_counts, counts, group=self.group)
+            self.comm.all_to_all_single(in_counts, counts)
             recv = torch.empty(int(in_counts.sum()), dtype=torch.int64, device=self.device)
-            dist.all_to_all_single(recv, h, in_counts.tolist(), counts.tolist(), group=self.group)
+            self.comm.all_to_all_single(recv, h, in_counts.tolist(), counts.tolist())
             h = torch.unique(recv)
         self.table.insert_mixed(h, self.cfg.sgd, init_embedx=init_embedx)
 
@@ -196,7 +199,7 @@ class SparseEngine:
         # sharded: pack per-owner, exchange keys, owner-side dedup/probe/gather
         h.shard_pack(self.ws.uniq_h, self.ws.u_count, self.world, self.C, self.send, self.send_index[:L],
                      self.overflow)
-        dist.all_to_all_single(self.recv, self.send, group=self.group)
+        self.comm.all_to_all_single(self.recv, self.send)
         self.ws_r.run(self.recv, True)
         n = self.world * self.C
         rows_r = self.table.probe(self.ws_r.uniq_h, self.ws_r.u_count)
@@ -208,7 +211,7 @@ class SparseEngine:
                 rows_r = self.table.probe(self.ws_r.uniq_h, self.ws_r.u_count)
         pulled = self.table.t.gather_pull(rows_r, self.ws_r.u_count, self.P)
         h.gather_by_uid(pulled, self.ws_r.uid, self.resp, self.P)
-        dist.all_to_all_single(self.resp_back, self.resp, group=self.group)
+        self.comm.all_to_all_single(self.resp_back, self.resp)
         st.send_index = self.send_index[:L]
         st.rows_r = rows_r
         return st
@@ -244,7 +247,7 @@ class SparseEngine:
         h.push_merge(dout, col_offset, cvm.contiguous(), sp.cvm_offset, sp.use_cvm, sp.clk_filter, self.E,
                      self.ws.perm[:L], self.ws.uid, self.occ_slot, self.occ_ins, self._slot_ids(st.S),
                      self.ws.u_count[1:], self.push_send, st.send_index, float(bs_scale), self.dim)
-        dist.all_to_all_single(self.push_recv, self.push_send, group=self.group)
+        self.comm.all_to_all_single(self.push_recv, self.push_send)
         self.push_merged.zero_()
         h.push_merge_records(self.push_recv, self.ws_r.perm, self.ws_r.uid, self.ws_r.u_count[1:], self.dim,
                              self.push_merged)
@@ -328,7 +331,7 @@ class SparseEngine:
         idx = st.send_index
         ok = idx >= 0
         self.push_send[idx[ok]] = merged[ok]
-        dist.all_to_all_single(self.push_recv, self.push_send, group=self.group)
+        self.comm.all_to_all_single(self.push_recv, self.push_send)
         self.push_merged.zero_()
         h.push_merge_records(self.push_recv, self.ws_r.perm, self.ws_r.uid, self.ws_r.u_count[1:], D,
                              self.push_merged)
@@ -364,16 +367,16 @@ class SparseEngine:
         uniq_o = uniq[order]
         counts = torch.bincount(owner, minlength=W)
         in_counts = torch.empty_like(counts)
-        dist.all_to_all_single(in_counts, counts, group=self.group)
+        self.comm.all_to_all_single(in_counts, counts)
         recv = torch.empty(int(in_counts.sum()), dtype=torch.int64)
-        dist.all_to_all_single(recv, uniq_o, in_counts.tolist(), counts.tolist(), group=self.group)
+        self.comm.all_to_all_single(recv, uniq_o, in_counts.tolist(), counts.tolist())
         rows_r = self.table.probe(recv)
         if self.auto_insert and not self.test_mode and bool((rows_r < 0).any()):
             self.table.insert_mixed(torch.unique(recv[rows_r < 0]), self.cfg.sgd)
             rows_r = self.table.probe(recv)
         pulled_r = self.table.gather_pull(rows_r, self.P)
         back = torch.empty(uniq.numel(), self.P)
-        dist.all_to_all_single(back, pulled_r, counts.tolist(), in_counts.tolist(), group=self.group)
+        self.comm.all_to_all_single(back, pulled_r, counts.tolist(), in_counts.tolist())
         pulled = torch.empty_like(back)
         pulled[order] = back
         y = ref.seqpool_cvm(pulled, full_uid, lod, S, B, self.E, sp.use_cvm, sp.cvm_offset, sp.clk_filter,
@@ -395,7 +398,7 @@ class SparseEngine:
         e = st.extra
         send = push[e["order"]]
         recv = torch.empty(int(e["in_counts"].sum()), push.shape[1])
-        dist.all_to_all_single(recv, send, e["in_counts"].tolist(), e["counts"].tolist(), group=self.group)
+        self.comm.all_to_all_single(recv, send, e["in_counts"].tolist(), e["counts"].tolist())
         # merge duplicates from different senders, then update
         uq, inv = torch.unique(e["recv"], return_inverse=True)
         merged = torch.zeros(uq.numel(), push.shape[1])
