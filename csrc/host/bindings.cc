@@ -1,13 +1,20 @@
 // pybind glue for the native host runtime (module paddlebox_amd._pbx_host).
 #include <torch/extension.h>
 
+#include "async_dense.h"
 #include "cpu_ps.h"
+#include "dump.h"
 #include "metrics.h"
 #include "runtime.h"
 #include "slot_dataset.h"
 
 namespace py = pybind11;
 using torch::Tensor;
+
+#define PBX_HOST_CHECK(c, msg) \
+  do {                         \
+    if (!(c)) throw std::runtime_error(std::string("pbx host: ") + (msg)); \
+  } while (0)
 
 namespace pbx {
 
@@ -340,5 +347,103 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         std::vector<int64_t> ord(d.store().nrec());
         for (int64_t i = 0; i < (int64_t)ord.size(); ++i) ord[i] = i;
         d.set_order(ord);
+      })
+      .def("batch_ins_ids", [](const SlotDataset& d, int64_t begin, int64_t count) {
+        const auto& o = d.order();
+        const auto& ids = d.store().ins_id;
+        std::vector<std::string> out((size_t)count);
+        for (int64_t i = 0; i < count; ++i) {
+          const int64_t r = o.empty() ? begin + i : o[(size_t)(begin + i)];
+          if (r >= 0 && r < (int64_t)ids.size()) out[(size_t)i] = ids[(size_t)r];
+        }
+        return out;
+      })
+      .def("batch_cmatch_rank", [](const SlotDataset& d, int64_t begin, int64_t count) {
+        const auto& o = d.order();
+        const auto& s = d.store();
+        auto t = torch::zeros({count}, torch::kInt64);
+        auto* p = t.data_ptr<int64_t>();
+        for (int64_t i = 0; i < count; ++i) {
+          const int64_t r = o.empty() ? begin + i : o[(size_t)(begin + i)];
+          if (r >= 0 && r < (int64_t)s.cmatch.size()) p[i] = ((int64_t)s.cmatch[(size_t)r] << 32) | s.rank[(size_t)r];
+        }
+        return t;
+      });
+
+  // ---------------------------------------------------------------- dump
+  m.def("xxh64", [](const std::string& s, uint64_t seed) { return xxh64(s.data(), s.size(), seed); },
+        py::arg("s"), py::arg("seed") = 0);
+  py::class_<DumpWriter>(m, "DumpWriter")
+      .def(py::init<const std::string&, int, int, size_t>(), py::arg("dir"), py::arg("device_id") = 0,
+           py::arg("threads") = 4, py::arg("max_file_len") = (size_t)1 << 31)
+      .def("dump_fields", [](DumpWriter& w, const std::vector<std::string>& lineids,
+                             const std::vector<std::string>& names, const std::vector<Tensor>& mats, int dump_mode,
+                             int dump_interval, bool extend) {
+        std::vector<const float*> ptrs;
+        std::vector<int64_t> widths;
+        int64_t B = (int64_t)lineids.size();
+        std::vector<Tensor> keep;
+        for (const auto& m0 : mats) {
+          auto m1 = m0.to(torch::kCPU).to(torch::kFloat32).contiguous();
+          PBX_HOST_CHECK(m1.dim() >= 1 && m1.size(0) == B, "dump field rows != batch size");
+          keep.push_back(m1);
+          ptrs.push_back(m1.data_ptr<float>());
+          widths.push_back(B ? m1.numel() / B : 0);
+        }
+        py::gil_scoped_release nogil;
+        return w.dump_fields(lineids, names, ptrs, widths, B, dump_mode, dump_interval, extend);
+      }, py::arg("lineids"), py::arg("names"), py::arg("mats"), py::arg("dump_mode") = 0,
+         py::arg("dump_interval") = 1, py::arg("lineid_have_extend_info") = false)
+      .def("dump_params", [](DumpWriter& w, int batch_id, const std::vector<std::string>& names,
+                             const std::vector<Tensor>& ts) {
+        std::vector<const float*> ptrs;
+        std::vector<int64_t> lens;
+        std::vector<Tensor> keep;
+        for (const auto& t0 : ts) {
+          auto t1 = t0.to(torch::kCPU).to(torch::kFloat32).contiguous();
+          keep.push_back(t1);
+          ptrs.push_back(t1.data_ptr<float>());
+          lens.push_back(t1.numel());
+        }
+        py::gil_scoped_release nogil;
+        w.dump_params(batch_id, names, ptrs, lens);
+      })
+      .def("flush", &DumpWriter::flush)
+      .def("files", &DumpWriter::files);
+
+  // ---------------------------------------------------------------- async dense table
+  py::class_<AsyncDenseTable>(m, "AsyncDenseTable")
+      .def(py::init([](const Tensor& params, int64_t adam_len, const Tensor& lr, int device_num, int threads) {
+             req_cpu(params, "params");
+             req_cpu(lr, "lr");
+             auto p = params.to(torch::kFloat32).contiguous();
+             auto l = lr.to(torch::kFloat32).contiguous();
+             PBX_HOST_CHECK(l.numel() == adam_len, "lr must have adam_len elements");
+             return new AsyncDenseTable(p.data_ptr<float>(), p.numel(), adam_len, l.data_ptr<float>(), device_num,
+                                        threads);
+           }),
+           py::arg("params"), py::arg("adam_len"), py::arg("lr"), py::arg("device_num") = 1, py::arg("threads") = 8)
+      .def("pull", [](AsyncDenseTable& t, Tensor out) {
+        req_cpu(out, "out");
+        PBX_HOST_CHECK(out.numel() == t.total_len() && out.is_contiguous(), "pull: bad output");
+        py::gil_scoped_release nogil;
+        t.pull(out.data_ptr<float>());
+      })
+      .def("push", [](AsyncDenseTable& t, const Tensor& g) {
+        auto g1 = g.to(torch::kCPU).to(torch::kFloat32).contiguous();
+        PBX_HOST_CHECK(g1.numel() == t.total_len(), "push: bad gradient length");
+        py::gil_scoped_release nogil;
+        t.push(g1.data_ptr<float>());
+      })
+      .def("wait_idle", &AsyncDenseTable::wait_idle, py::call_guard<py::gil_scoped_release>())
+      .def("finalize", &AsyncDenseTable::finalize, py::call_guard<py::gil_scoped_release>())
+      .def("updates", &AsyncDenseTable::updates)
+      .def("total_len", &AsyncDenseTable::total_len)
+      .def("snapshot", [](AsyncDenseTable& t, int64_t adam_len) {
+        auto p = torch::empty({t.total_len()}, torch::kFloat32);
+        auto m = torch::empty({adam_len}, torch::kFloat32);
+        auto v = torch::empty({adam_len}, torch::kFloat32);
+        t.snapshot(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>());
+        return py::make_tuple(p, m, v);
       });
 }

@@ -60,6 +60,7 @@ class SlotBatch:
     dense_names: List[str]
     dense_dims: List[int]
     extra: Dict[str, torch.Tensor] = field(default_factory=dict)
+    lod_host: Optional[torch.Tensor] = None  # CPU copy of lod (slot boundaries without a device sync)
 
     def dense_var(self, name: str) -> torch.Tensor:
         col = 0
@@ -70,9 +71,10 @@ class SlotBatch:
         raise KeyError(name)
 
     def to(self, device, non_blocking=False) -> "SlotBatch":
-        mv = lambda t: t.to(device, non_blocking=non_blocking)  # noqa: E731
+        mv = lambda t: t.to(device, non_blocking=non_blocking) if isinstance(t, torch.Tensor) else t  # noqa: E731
+        lh = self.lod if self.lod.device.type == "cpu" else self.lod_host
         return SlotBatch(mv(self.keys), mv(self.lod), mv(self.dense), self.B, self.S, self.sparse_names,
-                         self.dense_names, self.dense_dims, {k: mv(v) for k, v in self.extra.items()})
+                         self.dense_names, self.dense_dims, {k: mv(v) for k, v in self.extra.items()}, lh)
 
     # compat with the synthetic Batch used by the models
     @property
@@ -358,6 +360,10 @@ class PadBoxSlotDataset(DatasetBase):
             b.extra["cvm"] = torch.stack([torch.ones_like(lab), lab], 1)
         if self.rank_offset:
             b.extra[self.rank_offset] = self._native.build_rank_offset(begin, count, 3)
+        if self.parse_ins_id:
+            b.extra["ins_ids"] = self._native.batch_ins_ids(begin, count)
+        if self.parse_logkey:
+            b.extra["cmatch_rank"] = self._native.batch_cmatch_rank(begin, count)
         return b
 
     def batches(self, device=None, prefetch: int = 2, shuffle: Optional[bool] = None):

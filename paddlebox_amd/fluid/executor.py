@@ -1,0 +1,369 @@
+"""Executor: runs fluid programs on one MI355X (one process per GPU).
+
+``Executor.run`` executes a program on a feed dict; ``train_from_dataset`` /
+``infer_from_dataset`` hand the program to the BoxPS trainer
+(``paddlebox_amd/runtime/trainer.py``), mirroring
+``py/fluid/executor.py:1787-1936`` -> ``core.Executor.run_from_dataset`` ->
+``BoxPSTrainer``/``BoxPSWorker`` (``fw/boxps_trainer.cc``, ``fw/boxps_worker.cc``).
+
+A :class:`Session` is the per-(program, scope) compiled state: the lowered
+step list, the dense parameter arena + fused optimizer, and the dense sync
+policy.  It is created lazily and cached on the executor.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..parallel.dense import DenseArena, DenseSync, FlatAdagrad, FlatAdam, FlatMomentum, FlatSGD
+from .framework import (LoDTensor, Parameter, Program, Scope, Variable, default_main_program,
+                        default_startup_program, global_scope, to_device, torch_dtype)
+from .kernels import KERNELS, Ragged
+from .lowering import Lowered, lower
+
+
+def _box():
+    from ..ps.box_wrapper import BoxWrapper
+
+    return BoxWrapper._instance
+
+
+class ExecContext:
+    """Per-run variable environment handed to the kernels."""
+
+    def __init__(self, session: "Session", batch=None, training: bool = True, B: int = 0):
+        self.s = session
+        self.env: Dict[str, Any] = {}
+        self.batch = batch
+        self.training = training
+        self.B = B
+
+    # session passthroughs
+    @property
+    def device(self):
+        return self.s.device
+
+    @property
+    def scope(self) -> Scope:
+        return self.s.scope
+
+    @property
+    def generator(self):
+        return self.s.generator
+
+    @property
+    def generator_dev(self):
+        return self.s.generator_dev
+
+    @property
+    def group(self):
+        return self.s.group
+
+    @property
+    def box(self):
+        b = _box()
+        if b is None:
+            raise RuntimeError("BoxWrapper is not initialised (fluid.core.BoxWrapper(...) + "
+                               "initialize_gpu_and_load_model) but the program uses BoxPS ops")
+        return b
+
+    @property
+    def engine(self):
+        e = self.box.engine
+        if e is None:
+            raise RuntimeError("BoxWrapper.initialize_gpu_and_load_model() has not been called")
+        return e
+
+    @property
+    def cache(self) -> dict:
+        return self.s.cache
+
+    def get(self, v):
+        name = v if isinstance(v, str) else v.name
+        if name in self.env:
+            return self.env[name]
+        if name in self.s.logical:
+            return self.s.logical[name]
+        if name in self.s.scope:
+            return self.s.scope.get(name)
+        raise KeyError(f"variable '{name}' has no value (not fed / not computed)")
+
+    def set(self, v, val):
+        self.env[v if isinstance(v, str) else v.name] = val
+
+    def param(self, v) -> torch.Tensor:
+        return self.get(v)
+
+    def storage(self, v) -> torch.Tensor:
+        return self.s.storage[v if isinstance(v, str) else v.name]
+
+
+def _make_opt(spec: dict, arena: DenseArena, lr_mult: float = 1.0):
+    t = spec["type"]
+    lr = spec["lr"] * lr_mult
+    if t == "adam":
+        return FlatAdam(arena, lr, spec.get("beta1", 0.9), spec.get("beta2", 0.999), spec.get("epsilon", 1e-8))
+    if t == "adamw":
+        return FlatAdam(arena, lr, spec.get("beta1", 0.9), spec.get("beta2", 0.999), spec.get("epsilon", 1e-8),
+                        spec.get("weight_decay", 0.01))
+    if t == "momentum":
+        return FlatMomentum(arena, lr, spec.get("momentum", 0.9), spec.get("use_nesterov", False))
+    if t == "adagrad":
+        return FlatAdagrad(arena, lr, spec.get("epsilon", 1e-6), spec.get("initial_accumulator_value", 0.0))
+    return FlatSGD(arena, lr)
+
+
+class Session:
+    def __init__(self, program: Program, scope: Scope, device: torch.device, fetch_names=(), group=None,
+                 sync_mode: Optional[str] = None, sync_k: int = 1, fuse: bool = True):
+        self.program = program
+        self.scope = scope
+        self.device = device
+        self.group = group
+        self.cache: dict = {}
+        self.generator = torch.Generator().manual_seed(program.random_seed or 0)
+        self.generator_dev = None
+        self.training = program._optimize is not None and not program._is_test
+        box = _box()
+        cvm_off = 2
+        self.lowered: Lowered = lower(program, fetch_names, gpu=device.type == "cuda", engine_cvm_offset=cvm_off,
+                                      fuse=fuse)
+        self.storage: Dict[str, torch.Tensor] = {}
+        self.logical: Dict[str, torch.Tensor] = {}
+        self._materialize()
+        self.arenas: List[DenseArena] = []
+        self.opts = []
+        self.syncs: List[DenseSync] = []
+        if self.training:
+            self._build_optimizer(sync_mode, sync_k)
+        self.data_vars = [v for v in program.global_block().vars.values() if v.is_data]
+        self.box = box
+
+    # -------------------------------------------------------------- params
+    def _materialize(self):
+        blk = self.program.global_block()
+        opt_params = set(self.program._optimize["params"]) if self.program._optimize else set()
+        for p in blk.all_parameters():
+            if p.name not in self.scope:
+                t = torch.empty([max(1, s) for s in p.shape], dtype=torch_dtype(p.dtype))
+                p.initializer(t, self.generator)
+                self.scope.set(p.name, t.to(self.device))
+            cur = self.scope.get(p.name).to(self.device)
+            spec = self.lowered.storage.get(p.name)
+            trainable = p.name in opt_params and self.training
+            if spec is None or spec.kind == "plain":
+                st = cur.reshape(spec.shape) if spec is not None else cur
+            elif spec.kind == "t_pad":
+                st = torch.zeros(spec.shape, dtype=cur.dtype, device=self.device)
+                K, N = spec.logical
+                st[:N, :K] = cur.reshape(K, N).t()
+            else:  # "pad"
+                st = torch.zeros(spec.shape, dtype=cur.dtype, device=self.device)
+                st[: spec.logical[0]] = cur.reshape(-1)
+            if trainable:
+                st = torch.nn.Parameter(st.contiguous())
+            self.storage[p.name] = st
+        self._refresh_logical()
+
+    def _refresh_logical(self):
+        for name, st in self.storage.items():
+            spec = self.lowered.storage.get(name)
+            if spec is None or spec.kind == "plain":
+                lg = st.view(spec.logical) if spec is not None else st
+            elif spec.kind == "t_pad":
+                K, N = spec.logical
+                lg = st[:N, :K].t()
+            else:
+                lg = st[: spec.logical[0]]
+            self.logical[name] = lg
+            # scope tensors alias the live storage (np.array(scope var) sees training)
+            self.scope._tensors[name] = lg
+
+    def _build_optimizer(self, sync_mode, sync_k):
+        spec = self.program._optimize["optimizer"].spec()
+        blk = self.program.global_block()
+        groups: Dict[float, List[torch.nn.Parameter]] = {}
+        for name, st in self.storage.items():
+            if isinstance(st, torch.nn.Parameter):
+                lr = blk.var(name).optimize_attr.get("learning_rate", 1.0) if isinstance(blk.var(name), Parameter) \
+                    else 1.0
+                box = _box()
+                if box is not None and box.lr_map:
+                    for pat, v in box.lr_map.items():
+                        if pat in name:
+                            lr = v / max(spec["lr"], 1e-30)
+                groups.setdefault(lr, []).append(st)
+        world = dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
+        if sync_mode is None:
+            sync_mode = "grad_allreduce" if world > 1 else "none"
+        for lr_mult, ps in groups.items():
+            arena = DenseArena(ps, self.device)
+            self.arenas.append(arena)
+            self.opts.append(_make_opt(spec, arena, lr_mult))
+            self.syncs.append(DenseSync(arena, sync_mode, sync_k, self.group))
+        # arena rebinding moved the storage: re-point logical views
+        self._refresh_logical()
+
+    # -------------------------------------------------------------- feeding
+    def feed_batch(self, ctx: ExecContext, batch):
+        """Bind a SlotBatch (dataset / synthetic) to the program's data vars."""
+        B = batch.B
+        ctx.B = B
+        S = batch.S
+        lod = batch.lod.view(S, B + 1) if S else None
+        lh = batch.lod_host if batch.lod_host is not None else batch.lod.cpu()
+        lh = lh.view(S, B + 1) if S else None
+        sparse_idx = {n: i for i, n in enumerate(batch.sparse_names)}
+        for v in self.data_vars:
+            if v.name in sparse_idx:
+                s = sparse_idx[v.name]
+                a, e = int(lh[s, 0]), int(lh[s, B])
+                ctx.set(v, Ragged(batch.keys[a:e], lod[s] - a, B, s))
+            elif v.name in batch.dense_names:
+                ctx.set(v, batch.dense_var(v.name))
+            elif v.name in batch.extra:
+                ctx.set(v, batch.extra[v.name])
+
+    def feed_dict(self, ctx: ExecContext, feed: Dict[str, Any]):
+        B = 0
+        for name, val in (feed or {}).items():
+            v = self.program.global_block().vars.get(name)
+            if isinstance(val, LoDTensor):
+                t = val.value.to(self.device)
+                if val.lod():
+                    offs = torch.tensor(val.lod()[-1], dtype=torch.int64, device=self.device)
+                    if v is not None and v.dtype == "int64":
+                        t = t.reshape(-1)
+                    ctx.set(name, Ragged(t, offs, offs.numel() - 1))
+                    B = B or offs.numel() - 1
+                    continue
+            elif isinstance(val, torch.Tensor):
+                t = val.to(self.device)
+            else:
+                arr = np.asarray(val)
+                t = torch.as_tensor(arr).to(self.device)
+            if v is not None and v.dtype in ("float32",) and t.dtype == torch.float64:
+                t = t.float()
+            ctx.set(name, t)
+            B = B or (t.shape[0] if t.dim() else 1)
+        ctx.B = ctx.B or B
+
+    # -------------------------------------------------------------- run
+    def forward(self, ctx: ExecContext):
+        for op in self.lowered.steps:
+            KERNELS[op.type](ctx, op)
+
+    def step(self, ctx: ExecContext):
+        """forward + backward + dense sync + optimizer (one training batch)."""
+        self.forward(ctx)
+        if not (self.training and ctx.training):
+            return
+        loss = ctx.get(self.program._optimize["loss"])
+        loss = loss.values if isinstance(loss, Ragged) else loss
+        for a in self.arenas:
+            a.zero_grad()
+        loss.float().sum().backward()
+        for s, o in zip(self.syncs, self.opts):
+            s.before_step()
+            o.step(s.grad_scale())
+            s.after_step()
+
+    def fetch(self, ctx: ExecContext, fetch_list, return_numpy=True):
+        out = []
+        for f in fetch_list or []:
+            v = ctx.get(f)
+            t = v.values if isinstance(v, Ragged) else v
+            t = t.detach()
+            if return_numpy:
+                out.append(t.float().cpu().numpy() if t.dtype == torch.bfloat16 else t.cpu().numpy())
+            else:
+                out.append(LoDTensor(t))
+        return out
+
+
+class Executor:
+    def __init__(self, place=None):
+        self.place = place
+        self.device = to_device(place)
+        self._sessions: Dict[tuple, Session] = {}
+
+    def _session(self, program: Program, scope: Scope, fetch_names=(), **kw) -> Session:
+        key = (id(program), program._version, id(scope), tuple(sorted(fetch_names)))
+        s = self._sessions.get(key)
+        if s is None:
+            s = Session(program, scope, self.device, fetch_names, **kw)
+            self._sessions = {k: v for k, v in self._sessions.items() if k[0] != id(program)}
+            self._sessions[key] = s
+        return s
+
+    @staticmethod
+    def _is_startup(program: Program) -> bool:
+        ops = program.global_block().ops
+        return bool(ops) and all(op.type == "init_param" for op in ops)
+
+    def run(self, program: Optional[Program] = None, feed=None, fetch_list=None, feed_var_name="feed",
+            fetch_var_name="fetch", scope: Optional[Scope] = None, return_numpy=True, use_program_cache=False,
+            **_):
+        program = program or default_main_program()
+        program = getattr(program, "_program", program)  # CompiledProgram
+        scope = scope or global_scope()
+        if self._is_startup(program) or not program.global_block().ops:
+            ctx = ExecContext(_StartupSession(scope, self.device, program), training=False)
+            for op in program.global_block().ops:
+                KERNELS[op.type](ctx, op)
+            return []
+        names = [f if isinstance(f, str) else f.name for f in (fetch_list or [])]
+        s = self._session(program, scope, names)
+        ctx = ExecContext(s, training=s.training)
+        s.feed_dict(ctx, feed)
+        s.step(ctx)
+        return s.fetch(ctx, names, return_numpy)
+
+    def train_from_dataset(self, program=None, dataset=None, scope=None, thread=0, debug=False, fetch_list=None,
+                           fetch_info=None, print_period=100, fetch_handler=None):
+        from ..runtime.trainer import create_trainer
+
+        program = getattr(program or default_main_program(), "_program", program or default_main_program())
+        trainer = create_trainer(self, program, scope or global_scope(), dataset, infer=False, debug=debug,
+                                 fetch_list=fetch_list, fetch_info=fetch_info, print_period=print_period,
+                                 fetch_handler=fetch_handler)
+        return trainer.run()
+
+    def infer_from_dataset(self, program=None, dataset=None, scope=None, thread=0, debug=False, fetch_list=None,
+                           fetch_info=None, print_period=100, fetch_handler=None):
+        from ..runtime.trainer import create_trainer
+
+        program = getattr(program or default_main_program(), "_program", program or default_main_program())
+        trainer = create_trainer(self, program, scope or global_scope(), dataset, infer=True, debug=debug,
+                                 fetch_list=fetch_list, fetch_info=fetch_info, print_period=print_period,
+                                 fetch_handler=fetch_handler)
+        return trainer.run()
+
+    def close(self):
+        self._sessions.clear()
+
+
+class _StartupSession:
+    def __init__(self, scope, device, program):
+        self.scope = scope
+        self.device = device
+        self.generator = torch.Generator().manual_seed(program.random_seed or 0)
+        self.generator_dev = None
+        self.group = None
+        self.cache = {}
+        self.logical = {}
+        self.storage = {}
+
+
+class CompiledProgram:
+    """Accepted for API compatibility; programs are always lowered/fused."""
+
+    def __init__(self, program_or_graph, build_strategy=None):
+        self._program = program_or_graph
+
+    def with_data_parallel(self, loss_name=None, build_strategy=None, exec_strategy=None, share_vars_from=None,
+                           places=None):
+        return self

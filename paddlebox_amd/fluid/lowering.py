@@ -1,0 +1,208 @@
+"""Program lowering: op list -> executable steps, with PaddleBox fusions.
+
+The reference runs every op of the program through the generic operator
+interpreter (``BoxPSWorker::TrainFiles``, ``fw/boxps_worker.cc:1278-1357``);
+here the program is pattern-matched once and the CTR hot chains are replaced
+by the fused MI355X kernels:
+
+1. ``pull_box_sparse -> fused_seqpool_cvm``  =>  ``__pull_seqpool_cvm``: one
+   fused dedup/probe/gather/pool/CVM kernel chain writing straight into the
+   concat buffer; its backward is the fused push-merge + sparse Adagrad
+   (no per-occurrence pull records are materialised).
+2. ``concat([seqpool outs..., dense...], axis=1)`` consuming those outputs
+   is absorbed: the fused op writes the concat buffer and the per-slot
+   outputs become column views of it.
+3. (GPU) ``fc(relu) -> ... -> fc(relu) [-> fc(size=1)]`` chains  =>
+   ``__fused_mlp``: bf16 MFMA GEMMs with fused bias/ReLU epilogues, a GEMV
+   logit head, ReLU-mask prologues and split-K dW/db in the backward.  The
+   fc weights of a fused chain are stored ``[out, in]`` (padded to 8) in the
+   dense arena; the scope exposes the logical ``[in, out]`` view.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+from .framework import Operator, Program, Variable
+from .kernels import KERNELS
+
+
+def pad8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+@dataclass
+class StorageSpec:
+    """How a parameter is stored in the dense arena."""
+
+    kind: str  # "plain" | "t_pad" ([out_p, in_p] transposed) | "pad" (1-D padded)
+    shape: Tuple[int, ...]  # storage shape
+    logical: Tuple[int, ...]  # fluid shape
+
+
+@dataclass
+class Lowered:
+    steps: List[Operator]
+    storage: Dict[str, StorageSpec] = field(default_factory=dict)
+    fusions: List[str] = field(default_factory=list)
+
+    def describe(self) -> str:
+        return "\n".join(f"{op.type}: {op.input_arg_names} -> {op.output_arg_names}" for op in self.steps)
+
+
+def _consumers(ops: List[Operator]) -> Dict[str, List[int]]:
+    c: Dict[str, List[int]] = {}
+    for i, op in enumerate(ops):
+        for n in op.input_arg_names:
+            c.setdefault(n, []).append(i)
+    return c
+
+
+def _synthetic(block, type_, inputs, outputs, attrs) -> Operator:
+    op = Operator.__new__(Operator)
+    op.block, op.type = block, type_
+    op.inputs = {k: list(v) for k, v in inputs.items()}
+    op.outputs = {k: list(v) for k, v in outputs.items()}
+    op.attrs = dict(attrs)
+    return op
+
+
+_SEQPOOL_FUSABLE = {"fused_seqpool_cvm"}
+
+
+def _fuse_pull_seqpool(ops: List[Operator], fetch: set, engine_cvm_offset: int, notes: List[str]):
+    cons = _consumers(ops)
+    out = list(ops)
+    removed = set()
+    for i, op in enumerate(ops):
+        if op.type != "pull_box_sparse":
+            continue
+        outs = op.outputs["Out"]
+        users = {j for v in outs for j in cons.get(v.name, [])}
+        if len(users) != 1 or any(v.name in fetch for v in outs):
+            continue
+        j = users.pop()
+        f = ops[j]
+        if f.type not in _SEQPOOL_FUSABLE or [v.name for v in f.inputs["X"]] != [v.name for v in outs]:
+            continue
+        a = f.attrs
+        if a.get("embedx_concate_size", 1) != 1 or a.get("cvm_offset", 2) != engine_cvm_offset:
+            continue
+        if any(len(cons.get(v.name, [])) != 1 for v in outs):
+            continue
+        fused = _synthetic(op.block, "__pull_seqpool_cvm", {"Ids": op.inputs["Ids"], "CVM": f.inputs["CVM"]},
+                           {"Out": f.outputs["Out"]}, dict(a, size=op.attrs.get("size")))
+        # the fused op must run where the seqpool ran (its CVM input may be computed after the pull)
+        out[j] = fused
+        removed.add(i)
+        notes.append(f"pull_box_sparse+fused_seqpool_cvm ({len(outs)} slots) -> __pull_seqpool_cvm")
+    return [op for k, op in enumerate(out) if k not in removed]
+
+
+def _absorb_concat(ops: List[Operator], notes: List[str]):
+    produced_at: Dict[str, int] = {}
+    for i, op in enumerate(ops):
+        for n in op.output_arg_names:
+            produced_at[n] = i
+    cons = _consumers(ops)
+    removed = set()
+    for i, op in enumerate(ops):
+        if op.type != "__pull_seqpool_cvm" or op.outputs.get("Concat"):
+            continue
+        names = [v.name for v in op.outputs["Out"]]
+        for j in sorted({k for n in names for k in cons.get(n, [])}):
+            c = ops[j]
+            if c.type != "concat" or c.attrs.get("axis", 0) not in (1, -1):
+                continue
+            xs = c.inputs["X"]
+            if [v.name for v in xs[:len(names)]] != names:
+                continue
+            rest = xs[len(names):]
+            # tail inputs must be available before the fused op runs
+            if any(produced_at.get(v.name, -1) >= i for v in rest):
+                continue
+            op.inputs["Dense"] = list(rest)
+            op.outputs["Concat"] = c.outputs["Out"]
+            removed.add(j)
+            notes.append(f"concat of {len(names)} seqpool outputs (+{len(rest)} dense) absorbed")
+            break
+    return [op for k, op in enumerate(ops) if k not in removed]
+
+
+def _fc_ok(op: Operator) -> bool:
+    return (op.type == "fc" and op.attrs.get("in_num_col_dims", 1) == 1 and len(op.inputs["Input"]) == 1
+            and bool(op.inputs.get("Bias")) and len(op.inputs["W"][0].shape) == 2)
+
+
+def _fuse_mlp(ops: List[Operator], fetch: set, storage: Dict[str, StorageSpec], notes: List[str]):
+    cons = _consumers(ops)
+    used = set()
+    out = list(ops)
+    removed = set()
+    for i, op in enumerate(ops):
+        if i in used or not _fc_ok(op) or op.attrs.get("activation_type") != "relu":
+            continue
+        chain = [i]
+        cur = op
+        head = None
+        while True:
+            o = cur.outputs["Out"][0].name
+            us = cons.get(o, [])
+            if o in fetch or len(us) != 1:
+                break
+            nxt = ops[us[0]]
+            if not _fc_ok(nxt) or nxt.inputs["Input"][0].name != o:
+                break
+            if nxt.attrs.get("activation_type") == "relu":
+                chain.append(us[0])
+                cur = nxt
+                continue
+            if nxt.attrs.get("activation_type", "") == "" and nxt.inputs["W"][0].shape[1] == 1:
+                head = us[0]
+            break
+        ws = [ops[k].inputs["W"][0] for k in chain]
+        bs = [ops[k].inputs["Bias"][0] for k in chain]
+        for w, b in zip(ws, bs):
+            K, N = w.shape
+            storage[w.name] = StorageSpec("t_pad", (pad8(N), pad8(K)), (K, N))
+            storage[b.name] = StorageSpec("pad", (pad8(N),), (N,))
+        ins = {"X": ops[i].inputs["Input"], "W": ws, "B": bs}
+        last = ops[chain[-1]]
+        attrs = {"out_dim": last.inputs["W"][0].shape[1]}
+        if head is not None:
+            h = ops[head]
+            wo, bo = h.inputs["W"][0], h.inputs["Bias"][0]
+            H = wo.shape[0]
+            storage[wo.name] = StorageSpec("t_pad", (1, pad8(H)), (H, 1))
+            storage[bo.name] = StorageSpec("plain", (1,), (1,))
+            ins["WOut"], ins["BOut"] = [wo], [bo]
+            outv = h.outputs["Out"]
+        else:
+            outv = last.outputs["Out"]
+        fused = _synthetic(op.block, "__fused_mlp", ins, {"Out": outv}, attrs)
+        end = head if head is not None else chain[-1]
+        out[end] = fused
+        for k in chain:
+            used.add(k)
+            if k != end:
+                removed.add(k)
+        notes.append(f"fc chain of {len(chain)} relu layers{' + logit head' if head is not None else ''}"
+                     " -> __fused_mlp")
+    return [op for k, op in enumerate(out) if k not in removed]
+
+
+def lower(program: Program, fetch_names=(), gpu: bool = True, engine_cvm_offset: int = 2,
+          fuse: bool = True) -> Lowered:
+    ops = list(program.global_block().ops)
+    fetch = set(fetch_names)
+    notes: List[str] = []
+    storage: Dict[str, StorageSpec] = {}
+    if fuse:
+        ops = _fuse_pull_seqpool(ops, fetch, engine_cvm_offset, notes)
+        ops = _absorb_concat(ops, notes)
+        if gpu:
+            ops = _fuse_mlp(ops, fetch, storage, notes)
+    for op in ops:
+        if op.type not in KERNELS:
+            raise NotImplementedError(f"no kernel for op '{op.type}'")
+    return Lowered(ops, storage, notes)

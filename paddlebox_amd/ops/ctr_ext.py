@@ -1,0 +1,621 @@
+"""The PaddleBox CTR op family beyond the DeepFM hot path.
+
+Semantics follow the reference kernels (cited per op); each op is an
+autograd-aware function.  Where the reference gradient is not the true
+derivative (CVM columns carrying show/click into the push, scaled_fc's bias
+gradient) the reference behaviour is reproduced with a custom Function.
+GPU tensors use the hand-written kernels in ``csrc/hip/ctr_ext.hip`` when
+the op has one (see ``_hip_or_none``); the torch expressions here are the
+fp32 reference the kernel tests compare against.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+
+
+def _hip_or_none(t: torch.Tensor):
+    return _native.hip() if t.is_cuda else None
+
+
+def _seg_ids(offsets: torch.Tensor, L: int) -> torch.Tensor:
+    """instance id of each of the L rows given [B+1] offsets."""
+    return torch.searchsorted(offsets[1:].contiguous(), torch.arange(L, device=offsets.device), right=True)
+
+
+# ================================================================== sequence_pool
+def sequence_pool(x: torch.Tensor, offsets: torch.Tensor, B: int, pooltype: str = "SUM",
+                  pad_value: float = 0.0) -> torch.Tensor:
+    L = x.shape[0]
+    seg = _seg_ids(offsets, L)
+    x2 = x.reshape(L, -1)
+    cnt = (offsets[1:] - offsets[:-1]).to(x.dtype).unsqueeze(1)
+    out = torch.zeros(B, x2.shape[1], dtype=x.dtype, device=x.device).index_add(0, seg, x2)
+    pt = pooltype.upper()
+    if pt == "AVERAGE":
+        out = out / cnt.clamp(min=1)
+    elif pt == "SQRT":
+        out = out / cnt.clamp(min=1).sqrt()
+    elif pt == "MAX":
+        out = torch.full((B, x2.shape[1]), float("-inf"), dtype=x.dtype, device=x.device)
+        out = out.index_reduce(0, seg, x2, "amax")
+    elif pt == "FIRST":
+        out = x2[offsets[:-1].clamp(max=max(L - 1, 0))]
+    elif pt == "LAST":
+        out = x2[(offsets[1:] - 1).clamp(min=0)]
+    empty = (cnt == 0)
+    return torch.where(empty, torch.full_like(out, pad_value), out)
+
+
+def auc_from_hist(pos: torch.Tensor, neg: torch.Tensor) -> torch.Tensor:
+    """ROC AUC from per-threshold positive/negative counts (phi auc kernel)."""
+    p = pos.double().flip(0)
+    n = neg.double().flip(0)
+    tp = torch.cumsum(p, 0)
+    fp = torch.cumsum(n, 0)
+    tp_prev = torch.cat([tp.new_zeros(1), tp[:-1]])
+    fp_prev = torch.cat([fp.new_zeros(1), fp[:-1]])
+    area = ((fp - fp_prev) * (tp + tp_prev) / 2).sum()
+    denom = tp[-1] * fp[-1]
+    return torch.where(denom > 0, area / denom.clamp(min=1e-300), torch.zeros_like(area))
+
+
+# ================================================================== cvm
+class _Cvm(torch.autograd.Function):
+    """cvm op (operators/cvm_op.h:25-57): y = [log(show+1), log(clk+1)-log(show+1), rest]
+    (use_cvm) or drop the two cvm columns; dx's cvm columns carry the CVM input."""
+
+    @staticmethod
+    def forward(ctx, x, cvm, use_cvm):
+        ctx.use_cvm = use_cvm
+        ctx.save_for_backward(cvm)
+        ctx.width = x.shape[-1]
+        if use_cvm:
+            y = x.clone()
+            y[..., 0] = torch.log(x[..., 0] + 1)
+            y[..., 1] = torch.log(x[..., 1] + 1) - y[..., 0]
+            return y
+        return x[..., 2:].contiguous()
+
+    @staticmethod
+    def backward(ctx, dy):
+        (cvm,) = ctx.saved_tensors
+        n = dy.shape[0]
+        dx = dy.new_empty(n, ctx.width)
+        off = 0 if ctx.use_cvm else 2
+        dx[:, off:] = dy
+        dx[:, :2] = cvm.reshape(-1, 2)[:n] if cvm.shape[0] == n else cvm.reshape(-1, 2)[0]
+        return dx, None, None
+
+
+def cvm(x: torch.Tensor, cvm_t: torch.Tensor, use_cvm: bool = True) -> torch.Tensor:
+    return _Cvm.apply(x, cvm_t, use_cvm)
+
+
+# ================================================================== seqpool-CVM family over records
+def _quant(v: torch.Tensor, q: int) -> torch.Tensor:
+    return torch.trunc(v * q + 0.5) / q if q > 0 else v
+
+
+class _SeqpoolCvmVariant(torch.autograd.Function):
+    """Generic fused_seqpool_cvm* over per-occurrence records.
+
+    ``variant`` in {"std", "diff_thres", "conv", "pcoc", "tradew", "credit"};
+    forward: filtered (+quantised) SUM pool (+pad) per (slot, instance) then the
+    variant's CVM epilogue; backward: broadcast the pooled grad to every row of
+    the sequence and overwrite the statistic columns with the CVM input, which
+    is how show/click reach push_box_sparse (fused_seqpool_cvm_op.cu:813-1015
+    and the per-variant grad kernels)."""
+
+    @staticmethod
+    def forward(ctx, cvm_in, variant, attrs, offsets_list, B, qvals, *xs):
+        a = attrs
+        outs, saved = [], []
+        for x, off in zip(xs, offsets_list):
+            L, E = x.shape
+            seg = _seg_ids(off, L)
+            show, clk = x[:, 0], x[:, 1] if E > 1 else x[:, 0]
+            keep = torch.ones(L, dtype=torch.bool, device=x.device)
+            if a.get("need_filter"):
+                thr = a["threshold"]
+                if variant == "diff_thres" and a.get("xbox_diff_thres_filter"):
+                    thr = a["threshold_vec"][len(outs)]
+                keep &= (show - clk) * a["show_coeff"] + clk * a["clk_coeff"] >= thr
+            co = a.get("cvm_offset", 2)
+            if a.get("embed_threshold_filter"):
+                ets = a.get("embed_thres_size", 0)
+                emb = x[:, co:co + max(ets, 1)]
+                score = emb[:, 1:].pow(2).sum(1).sqrt() + emb[:, 0].abs()
+                keep &= score >= a["embed_threshold"]
+            q = a.get("quant_ratio", 0)
+            mcol = a.get("max_cvm_offset", co) if variant == "pcoc" else co
+            vals = x.clone()
+            if q > 0:
+                vals[:, mcol:] = _quant(vals[:, mcol:], q)
+            if variant == "tradew":
+                tn, tid = a["trade_num"], a["trade_id"]
+                emb = vals[:, co + tn:]
+                if tid >= 0:
+                    emb = emb * vals[:, co + tid:co + tid + 1]
+                vals = torch.cat([vals[:, :co], emb], 1)
+            vals = vals * keep.unsqueeze(1).to(vals.dtype)
+            pooled = torch.zeros(B, vals.shape[1], dtype=x.dtype, device=x.device).index_add(0, seg, vals)
+            pooled = pooled + a.get("pad_value", 0.0)
+            ecs = a.get("embedx_concate_size", 1)
+            if ecs > 1:
+                pooled = _concat_pool(vals, off, B, ecs, a.get("pad_value", 0.0))
+            outs.append(_cvm_epilogue(variant, pooled, a, ecs))
+            saved.append((L, E, seg))
+        ctx.variant, ctx.attrs, ctx.B, ctx.saved = variant, a, B, saved
+        ctx.offsets_list = offsets_list
+        ctx.save_for_backward(cvm_in, qvals if qvals is not None else torch.zeros(0), *xs)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        cvm_in, qvals, *xs = ctx.saved_tensors
+        a, variant = ctx.attrs, ctx.variant
+        co = a.get("cvm_offset", 2)
+        grads = []
+        for (L, E, seg), dout, x in zip(ctx.saved, douts, xs):
+            dpool = _cvm_epilogue_grad(variant, dout, a, E, cvm_in, qvals, ctx.B)
+            ecs = a.get("embedx_concate_size", 1)
+            if ecs > 1:
+                g = _concat_pool_grad(dpool, ctx.offsets_list[len(grads)], L, E, ecs)
+            else:
+                g = dpool[seg]
+            if variant == "tradew":
+                tn, tid = a["trade_num"], a["trade_id"]
+                full = x.new_zeros(L, E)
+                full[:, :co] = g[:, :co]
+                emb_g = g[:, co:]
+                if tid >= 0:
+                    w = x[:, co + tid:co + tid + 1]
+                    full[:, co + tn:] = emb_g * w
+                    full[:, co + tid] = (emb_g * x[:, co + tn:]).sum(1)
+                    full[:, :co] = 0.0
+                else:
+                    full[:, co + tn:] = emb_g
+                g = full
+            grads.append(g)
+        return (None, None, None, None, None, None) + tuple(grads)
+
+
+def _concat_pool(vals, off, B, ecs, pad):
+    """embedx_concate: block k of an instance holds only its k-th row."""
+    L, E = vals.shape
+    out = torch.full((B, ecs, E), pad, dtype=vals.dtype, device=vals.device)
+    starts = off[:-1]
+    lens = off[1:] - off[:-1]
+    for k in range(ecs):
+        has = lens > k
+        idx = (starts + k).clamp(max=max(L - 1, 0))
+        out[:, k] += torch.where(has.unsqueeze(1), vals[idx], torch.zeros_like(vals[idx]))
+    return out.reshape(B, ecs * E)
+
+
+def _concat_pool_grad(dpool, off, L, E, ecs):
+    """Reference grad: block k -> row k; the last block also feeds all
+    remaining rows (FusedSeqpoolCVM*GradKernel*Concate)."""
+    B = off.numel() - 1
+    dp = dpool.reshape(B, ecs, E)
+    seg = _seg_ids(off, L)
+    pos = torch.arange(L, device=off.device) - off[seg]
+    k = pos.clamp(max=ecs - 1)
+    return dp[seg, k]
+
+
+def _cvm_epilogue(variant, p, a, ecs=1):
+    use_cvm = a.get("use_cvm", True)
+    co = a.get("cvm_offset", 2)
+    if ecs > 1:
+        B = p.shape[0]
+        E = p.shape[1] // ecs
+        blocks = [_cvm_epilogue(variant, p[:, k * E:(k + 1) * E], a, 1) for k in range(ecs)]
+        return torch.cat(blocks, 1) if blocks else p.new_zeros(B, 0)
+    lg = lambda v: torch.log(v + 1)  # noqa: E731
+    if variant in ("std", "diff_thres", "tradew"):
+        if not use_cvm:
+            return p[:, co + (a.get("embed_thres_size", 0) if variant == "std" else 0):]
+        s = lg(p[:, 0])
+        c = lg(p[:, 1]) - s
+        if a.get("clk_filter"):
+            return torch.cat([s[:, None], p[:, 2:]], 1)
+        return torch.cat([s[:, None], c[:, None], p[:, 2:]], 1)
+    if variant == "conv":
+        if not use_cvm:
+            return p[:, co:]
+        s, c, v = lg(p[:, 0]), lg(p[:, 1]), lg(p[:, 2]) - lg(p[:, 1])
+        if a.get("show_filter"):
+            return torch.cat([c[:, None], v[:, None], p[:, 3:]], 1)
+        return torch.cat([s[:, None], c[:, None], v[:, None], p[:, 3:]], 1)
+    if variant == "credit":
+        if not use_cvm:
+            return p[:, co:]
+        st = lg(p[:, :co])
+        if a.get("show_filter"):
+            return torch.cat([st[:, 1:], p[:, co:]], 1)
+        return torch.cat([st, p[:, co:]], 1)
+    if variant == "pcoc":
+        mco = a.get("max_cvm_offset", co)
+        if not use_cvm:
+            return p[:, mco:]
+        pk = co - 4
+        diff = mco - 2 - 2 * pk
+        s = lg(p[:, 0])
+        cols = [s[:, None], (lg(p[:, 1]) - s)[:, None]]
+        for j in range(pk):
+            cols.append((lg(p[:, 4 + j]) - lg(p[:, 2]))[:, None])
+        for j in range(pk):
+            cols.append((lg(p[:, 4 + j]) - lg(p[:, 3]))[:, None])
+        cols.append(p[:, 2 + 2 * pk + diff:])
+        return torch.cat(cols, 1)
+    raise ValueError(variant)
+
+
+def _cvm_epilogue_grad(variant, dout, a, E, cvm_in, qvals, B):
+    """[B, E_pool] gradient of the pooled value (statistic columns = CVM input)."""
+    use_cvm = a.get("use_cvm", True)
+    co = a.get("cvm_offset", 2)
+    ecs = a.get("embedx_concate_size", 1)
+    if variant == "tradew":
+        E = E - a["trade_num"]
+    if ecs > 1:
+        Eo = dout.shape[1] // ecs
+        blocks = [_cvm_epilogue_grad(variant, dout[:, k * Eo:(k + 1) * Eo], dict(a, embedx_concate_size=1), E,
+                                     cvm_in, qvals, B) for k in range(ecs)]
+        return torch.cat(blocks, 1)
+    g = dout.new_zeros(B, E)
+    cv = cvm_in.reshape(B, -1)
+    if variant == "pcoc":
+        mco = a.get("max_cvm_offset", co)
+        pk = co - 4
+        g[:, :4] = cv[:, :4]
+        if pk > 0:
+            q = qvals.reshape(B, pk) if qvals is not None and qvals.numel() == B * pk else dout.new_zeros(B, pk)
+            g[:, 4:co] = q
+        if use_cvm:
+            diff = mco - 2 - 2 * pk
+            g[:, mco:] = dout[:, mco - diff:]
+        else:
+            g[:, mco:] = dout
+        return g
+    ncv = min(co, cv.shape[1])
+    g[:, :ncv] = cv[:, :ncv]
+    if not use_cvm:
+        skip = a.get("embed_thres_size", 0) if variant == "std" else 0
+        g[:, co + skip:] = dout
+        return g
+    if variant in ("std", "diff_thres", "tradew"):
+        if a.get("clk_filter"):
+            g[:, 2:] = dout[:, 1:]
+        else:
+            g[:, 2:] = dout[:, 2:]
+    elif variant in ("conv", "credit"):
+        if a.get("show_filter"):
+            g[:, co:] = dout[:, co - 1:]
+        else:
+            g[:, co:] = dout[:, co:]
+    return g
+
+
+_VARIANT = {
+    "fused_seqpool_cvm": "std", "fused_seqpool_cvm_with_diff_thres": "diff_thres",
+    "fused_seqpool_cvm_with_conv": "conv", "fused_seqpool_cvm_with_pcoc": "pcoc",
+    "fused_seqpool_cvm_tradew": "tradew", "fused_seqpool_cvm_with_credit": "credit",
+}
+
+
+def seqpool_cvm_variant(op_type: str, xs: Sequence[torch.Tensor], offsets: Sequence[torch.Tensor], B: int,
+                        cvm_in: torch.Tensor, attrs: Dict, qvals: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
+    variant = _VARIANT[op_type]
+    return list(_SeqpoolCvmVariant.apply(cvm_in, variant, dict(attrs), list(offsets), B, qvals,
+                                         *[x.float() for x in xs]))
+
+
+# ================================================================== masked data_norm
+class _MaskedDataNorm(torch.autograd.Function):
+    """masked_data_norm (operators/masked_data_norm_op.cu:39-130)."""
+
+    @staticmethod
+    def forward(ctx, x, mask, bsize, bsum, bsq, sw, bias, eps, decay, group, update, training):
+        means = bsum / bsize
+        scales = torch.sqrt(bsize / bsq)
+        m = (mask > 0).unsqueeze(1)
+        y = torch.where(m, (x - means) * scales, torch.zeros_like(x))
+        if sw is not None:
+            y = torch.where(m, y * sw + bias, y)
+        ctx.save_for_backward(x, mask, means, scales, bsize, bsum, bsq, sw if sw is not None else torch.zeros(0))
+        ctx.eps, ctx.decay, ctx.group, ctx.update, ctx.training = eps, decay, group, update, training
+        ctx.has_sw = sw is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mask, means, scales, bsize, bsum, bsq, sw = ctx.saved_tensors
+        m = (mask > 0).unsqueeze(1)
+        g = dy * sw if ctx.has_sw else dy
+        dx = torch.where(m, g * scales, torch.zeros_like(dy))
+        n = m.sum()
+        xm = x * m
+        stats = torch.stack([
+            (n > 0).to(x.dtype).expand(x.shape[1]),
+            xm.sum(0) / n.clamp(min=1),
+            (((x - means) ** 2) * m).sum(0) / n.clamp(min=1) + ctx.eps * (n > 0).to(x.dtype),
+        ])
+        if ctx.group is not None and dist.is_initialized() and dist.get_world_size(ctx.group) > 1:
+            dist.all_reduce(stats, group=ctx.group)
+        if ctx.update and ctx.training:
+            upd = stats[0] > 0
+            with torch.no_grad():
+                bsize.copy_(torch.where(upd, bsize * ctx.decay + stats[0], bsize))
+                bsum.copy_(torch.where(upd, bsum * ctx.decay + stats[1], bsum))
+                bsq.copy_(torch.where(upd, bsq * ctx.decay + stats[2], bsq))
+        dsw = dbias = None
+        if ctx.has_sw:
+            xn = torch.where(m, (x - means) * scales, torch.zeros_like(x))
+            dsw = (dy * xn).sum(0)
+            dbias = (dy * m).sum(0)
+        return dx, None, None, None, None, dsw, dbias, None, None, None, None, None
+
+
+def masked_data_norm(x, mask, bsize, bsum, bsq, sw, bias, eps, decay, group, update, training):
+    return _MaskedDataNorm.apply(x, mask, bsize, bsum, bsq, sw, bias, eps, decay, group, update, training)
+
+
+# ================================================================== cross_norm_hadamard
+def _cross_raw(x: torch.Tensor, F: int, E: int) -> torch.Tensor:
+    """[B, F*(3E+1)] un-normalised [a, b, a*b, <a,b>] blocks."""
+    B = x.shape[0]
+    xv = x.reshape(B, F, 2, E)
+    a, b = xv[:, :, 0], xv[:, :, 1]
+    ab = a * b
+    return torch.cat([a, b, ab, ab.sum(-1, keepdim=True)], -1).reshape(B, F * (3 * E + 1))
+
+
+class _CrossNormHadamard(torch.autograd.Function):
+    """cross_norm_hadamard (operators/cross_norm_hadamard.cu.h:44-240).
+
+    Forward matches the reference.  The input gradient is the exact
+    derivative of the forward; the reference kernel
+    (``nncross_normbackpropagate_multi``) reads b's direct term from a's
+    column block, which this implementation does not reproduce (no reference
+    unit test pins that path)."""
+
+    @staticmethod
+    def forward(ctx, x, summary, F, E, eps, decay, group, training):
+        raw = _cross_raw(x, F, E)
+        means = summary[1] / summary[0]
+        scales = torch.sqrt(summary[0] / summary[2])
+        ctx.save_for_backward(x, raw, means, scales, summary)
+        ctx.F, ctx.E, ctx.eps, ctx.decay, ctx.group, ctx.training = F, E, eps, decay, group, training
+        return (raw - means) * scales
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, raw, means, scales, summary = ctx.saved_tensors
+        F, E = ctx.F, ctx.E
+        B = x.shape[0]
+        g = (dy * scales).reshape(B, F, 3 * E + 1)
+        xv = x.reshape(B, F, 2, E)
+        a, b = xv[:, :, 0], xv[:, :, 1]
+        ga = g[..., :E] + g[..., 2 * E:3 * E] * b + g[..., 3 * E:] * b
+        gb = g[..., E:2 * E] + g[..., 2 * E:3 * E] * a + g[..., 3 * E:] * a
+        dx = torch.stack([ga, gb], 2).reshape(B, F * 2 * E)
+        stats = torch.stack([torch.ones_like(means), raw.mean(0), ((raw - means) ** 2).mean(0) + ctx.eps])
+        if ctx.group is not None and dist.is_initialized() and dist.get_world_size(ctx.group) > 1:
+            dist.all_reduce(stats, group=ctx.group)
+        if ctx.training:
+            with torch.no_grad():
+                summary.mul_(ctx.decay).add_(stats)
+        return dx, None, None, None, None, None, None, None
+
+
+def cross_norm_hadamard(x, summary, F, E, eps, decay, group=None, training=True):
+    return _CrossNormHadamard.apply(x, summary, F, E, eps, decay, group, training)
+
+
+# ================================================================== rank_attention
+def _rank_gather(x, rank_offset, W, max_rank):
+    """Per instance i and peer k: (x[index_k] masked, W block (lower*R+faster_k))."""
+    B, C = x.shape
+    R = max_rank
+    ro = rank_offset.long()
+    lower = ro[:, 0] - 1
+    P = W.shape[1]
+    Wb = W.reshape(R * R, C, P)
+    xs, ws, valid = [], [], []
+    for k in range(R):
+        faster = ro[:, 2 * k + 1] - 1
+        idx = ro[:, 2 * k + 2].clamp(0, B - 1)
+        ok = (lower >= 0) & (faster >= 0)
+        blk = (lower.clamp(min=0) * R + faster.clamp(min=0))
+        xs.append(x[idx] * ok.unsqueeze(1).to(x.dtype))
+        ws.append(blk)
+        valid.append(ok)
+    return xs, ws, valid, Wb
+
+
+def rank_attention(x: torch.Tensor, rank_offset: torch.Tensor, W: torch.Tensor, max_rank: int) -> torch.Tensor:
+    """out[i] = sum_k [valid] x[index_k] @ W[(lower*R + faster_k)*C : +C]
+    (rank_attention.cu.h:28-190 / numpy ref test_rank_attention_op.py:25-110)."""
+    hip = _hip_or_none(x)
+    if hip is not None and hasattr(hip, "rank_attention_fwd"):
+        return _RankAttentionHip.apply(x.contiguous(), rank_offset.to(torch.int32).contiguous(), W, max_rank)
+    xs, blks, _, Wb = _rank_gather(x, rank_offset, W, max_rank)
+    out = 0
+    for xk, bk in zip(xs, blks):
+        out = out + torch.bmm(xk.unsqueeze(1), Wb[bk]).squeeze(1)
+    return out
+
+
+class _RankAttentionHip(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ro, W, R):
+        h = _native.hip()
+        ctx.save_for_backward(x, ro, W)
+        ctx.R = R
+        return h.rank_attention_fwd(x, ro, W.contiguous(), R)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, ro, W = ctx.saved_tensors
+        h = _native.hip()
+        dx, dW = h.rank_attention_bwd(x, ro, W.contiguous(), dout.contiguous(), ctx.R)
+        return dx, None, dW, None
+
+
+# ================================================================== batch_fc
+def batch_fc(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, batchcount: int = 0,
+             transpose_weight: bool = False) -> torch.Tensor:
+    """batch_fc (operators/batch_fc_op.cu:195-330):
+    * default: x [P, N, in], W [P, in, out], b [P, out] -> [P, N, out]
+    * transpose_weight: x [bc, N, in], W [in, bc*out], b [1, bc*out] -> [bc, N, out]
+    * batchcount>0: x [N, bc*in], W [in, bc*out], b [bc*out] -> [N, bc*out]
+    """
+    if transpose_weight:
+        bc = x.shape[0]
+        od = W.shape[1] // bc
+        Wb = W.reshape(W.shape[0], bc, od).permute(1, 0, 2)
+        return torch.bmm(x, Wb) + b.reshape(bc, 1, od)
+    if batchcount > 0:
+        N = x.shape[0]
+        inf = x.shape[1] // batchcount
+        of = W.shape[1] // batchcount
+        xb = x.reshape(N, batchcount, inf).permute(1, 0, 2)
+        Wb = W.reshape(inf, batchcount, of).permute(1, 0, 2)
+        y = torch.bmm(xb, Wb).permute(1, 0, 2).reshape(N, batchcount * of)
+        return y + b.reshape(1, -1)
+    return torch.baddbmm(b.unsqueeze(1), x, W)
+
+
+# ================================================================== scaled fc family
+class _ScaledFc(torch.autograd.Function):
+    """scaled_fc (operators/scaled_fc_op.cu:144-330): y = x@W + bias*bs/is
+    (the reference's fp16 scaling is numerically transparent in bf16/fp32);
+    reference gradients: dx = dy W^T, dW = x^T dy, db = colsum(dy)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, in_scale, bias_scale, grad_scale):
+        ctx.save_for_backward(x, W)
+        return x @ W + b.reshape(1, -1) * (bias_scale / in_scale)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        return dy @ W.t(), x.t() @ dy, dy.sum(0).reshape(-1), None, None, None
+
+
+def scaled_fc(x, W, b, in_scale, bias_scale, grad_scale=256.0):
+    return _ScaledFc.apply(x, W, b, in_scale, bias_scale, grad_scale)
+
+
+def int8_quantize(v: torch.Tensor, expand: float, clip: float, rng: float) -> torch.Tensor:
+    """kernel_cast_and_padding (scaled_int8fc_op.cu:38-80): clip(v*expand, +-clip)
+    quantised with interval 2*clip/range, trunc(v/interval + 0.5)."""
+    e = v * expand
+    e = torch.where(e >= 1e-6, torch.where(e - clip > 1e-6, torch.full_like(e, clip), e),
+                    torch.where(e + clip < 1e-6, torch.full_like(e, -clip), e))
+    interval = 2 * clip / rng
+    return torch.trunc(e / interval + 0.5).clamp(-128, 127)
+
+
+class _ScaledInt8Fc(torch.autograd.Function):
+    """scaled_int8fc: int8 GEMM forward, fp32 straight-through backward
+    (scaled_int8fc_op.cu:290-440).  Output scale reproduces the reference's
+    cast_and_cut: acc * (2*input_clip/range) / (input_expand*weight_expand)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, a):
+        rng = a["int8_range"]
+        qx = int8_quantize(x, a["input_expand_factor"], a["input_clip_factor"], rng)
+        qw = int8_quantize(W, a["weight_expand_factor"], a["weight_clip_factor"], rng)
+        hip = _hip_or_none(x)
+        if hip is not None and hasattr(hip, "int8_gemm"):
+            acc = hip.int8_gemm(qx.to(torch.int8).contiguous(), qw.to(torch.int8).contiguous())
+        else:
+            acc = qx.double() @ qw.double()
+        interval = 2 * a["input_clip_factor"] / rng
+        y = acc.float() / (a["input_expand_factor"] * a["weight_expand_factor"]) * interval
+        ctx.save_for_backward(x, W)
+        return y + b.reshape(1, -1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        return dy @ W.t(), x.t() @ dy, dy.sum(0).reshape(-1), None
+
+
+def scaled_int8fc(x, W, b, attrs):
+    return _ScaledInt8Fc.apply(x, W, b, dict(attrs))
+
+
+# ================================================================== concat family
+def partial_concat(xs: Sequence[torch.Tensor], start: int, length: int) -> torch.Tensor:
+    """partial_concat (test_partial_concat_op.py np_partial_concat)."""
+    size = xs[0].shape[1]
+    if start < 0:
+        start += size
+    if length < 0:
+        length = size - start
+    return torch.cat([x[:, start:start + length] for x in xs], 1)
+
+
+def partial_sum(xs: Sequence[torch.Tensor], start: int, length: int) -> torch.Tensor:
+    size = xs[0].shape[1]
+    if start < 0:
+        start += size
+    end = size if length < 0 else start + length
+    out = xs[0][:, start:end]
+    for x in xs[1:]:
+        out = out + x[:, start:end]
+    return out
+
+
+def fused_concat(xs: Sequence[torch.Tensor], offset: int, length: int) -> torch.Tensor:
+    """fused_concat (fused_concat_op.cu FusedColsConcatKernel): equal-width inputs,
+    columns [offset, offset+length) of each, concatenated."""
+    return torch.cat([x[:, offset:offset + length] for x in xs], 1)
+
+
+def fused_seqpool_concat(groups: Sequence[Sequence[torch.Tensor]], col_ranges) -> List[torch.Tensor]:
+    """fused_seqpool_concat (fused_concat_op.cu:34-115): output j = concat over
+    groups i of groups[i][j][:, start_i:start_i+dim_i]."""
+    n = len(groups[0])
+    return [torch.cat([g[j][:, s:s + d] for g, (s, d) in zip(groups, col_ranges)], 1) for j in range(n)]
+
+
+def shuffle_batch(x: torch.Tensor, gen: Optional[torch.Generator] = None) -> torch.Tensor:
+    perm = torch.randperm(x.shape[0], generator=gen, device=gen.device if gen is not None else x.device) \
+        if gen is not None else torch.randperm(x.shape[0], device=x.device)
+    return x[perm.to(x.device)]
+
+
+# ================================================================== fused_seq_tensor
+def fused_seq_tensor(x: torch.Tensor, ad: torch.Tensor, batch_count: int, max_length: int, slot_num: int,
+                     fea_emb_dim: int, ad_slot_num: int, ad_slot_offset: int):
+    """DIN sequence tensors (fused_seq_tensor_op.cu): Input [ins, bc*slot*T*E],
+    ADInput [ins, bc*ad_slot*E] -> DINOut [bc, ins*T, 4*ad_slot*E] =
+    [seq, ad, seq-ad, seq*ad], MaskOut [bc, ins, T], SideInfoOut
+    [bc, ins*T, side_slot*E], ADSlotSessionOut [bc, ins*T, ad_slot, E]."""
+    ins = x.shape[0]
+    bc, T, E, S, A = batch_count, max_length, fea_emb_dim, slot_num, ad_slot_num
+    xv = x.reshape(ins, bc, S, T, E).permute(1, 0, 3, 2, 4)  # [bc, ins, T, S, E]
+    adv = ad.reshape(ins, bc, A, E).permute(1, 0, 2, 3).unsqueeze(2)  # [bc, ins, 1, A, E]
+    seq = xv[:, :, :, ad_slot_offset:ad_slot_offset + A]  # [bc, ins, T, A, E]
+    adb = adv.expand_as(seq)
+    din = torch.cat([seq, adb, seq - adb, seq * adb], 3).reshape(bc, ins * T, 4 * A * E)
+    side_off = A if ad_slot_offset == 0 else 0
+    side = xv[:, :, :, side_off:side_off + (S - A)].reshape(bc, ins * T, (S - A) * E)
+    mask = (xv.sum((3, 4)).abs() > 1e-8).to(x.dtype)  # [bc, ins, T]
+    sess = seq.reshape(bc, ins * T, A, E)
+    if bc == 1:
+        din = din.reshape(ins, T, 4 * A * E)
+        mask = mask.reshape(ins, T)
+        side = side.reshape(ins, T, (S - A) * E)
+        sess = sess.reshape(ins, T, A * E)
+    return din, mask, side, sess

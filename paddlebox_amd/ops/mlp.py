@@ -10,7 +10,7 @@ CPU tensors use plain fp32 PyTorch (the reference path).
 """
 from __future__ import annotations
 
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import torch
 from torch import nn
@@ -22,36 +22,72 @@ def pad8(n: int) -> int:
     return (n + 7) // 8 * 8
 
 
-class _FusedMLPFn(torch.autograd.Function):
+def _ensure_grad(p: torch.Tensor):
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
+
+
+def _bf16_copies(ws: Sequence[torch.Tensor], cache: List[torch.Tensor]) -> List[torch.Tensor]:
+    h = _native.hip()
+    if len(cache) != len(ws) or any(c.shape != w.shape for c, w in zip(cache, ws)):
+        cache[:] = [torch.empty(w.shape, dtype=torch.bfloat16, device=w.device) for w in ws]
+    for w, c in zip(ws, cache):
+        h.cast_bf16(w.detach(), c)
+    return cache
+
+
+class _MLPFn(torch.autograd.Function):
+    """Functional fused MLP: ``len(ws)`` ReLU layers (W: [N, K] fp32 master
+    weights, K % 8 == 0) and an optional single-logit GEMV head.  Parameter
+    gradients are accumulated straight into ``p.grad`` (dense-arena views);
+    returns [M] fp32 logits (head) or the last bf16 hidden [M, N]."""
+
     @staticmethod
-    def forward(ctx, x, mod: "FusedMLP", *params):
+    def forward(ctx, x, ws, bs, w_out, b_out, cache, k_split, *params):
         h = _native.hip()
-        wb = mod.bf16_weights()
+        wb = _bf16_copies(ws, cache)
         hs = [x]
         cur = x
-        for i, w in enumerate(wb):
-            cur = h.linear_fwd(cur, w, mod.b[i], True)
+        for w, b in zip(wb, bs):
+            cur = h.linear_fwd(cur, w, b, True)
             hs.append(cur)
-        out = h.gemv_out(cur, mod.w_out.view(-1), mod.b_out)
-        ctx.mod = mod
-        ctx.hs = hs
-        ctx.wb = wb
+        ctx.ws, ctx.bs, ctx.w_out, ctx.b_out = ws, bs, w_out, b_out
+        ctx.hs, ctx.wb, ctx.k_split = hs, wb, k_split
         ctx.x_needs_grad = x.requires_grad
-        return out
+        ctx.n_params = len(params)
+        if w_out is not None:
+            return h.gemv_out(cur, w_out.view(-1), b_out)
+        return cur
 
     @staticmethod
     def backward(ctx, dout):
         h = _native.hip()
-        mod, hs, wb = ctx.mod, ctx.hs, ctx.wb
-        mod.ensure_grads()
-        dh = h.gemv_out_bwd(hs[-1], mod.w_out.view(-1), dout.float(), mod.w_out.grad.view(-1), mod.b_out.grad)
-        dx = None
+        hs, wb = ctx.hs, ctx.wb
+        if ctx.w_out is not None:
+            dh = h.gemv_out_bwd(hs[-1], ctx.w_out.view(-1), dout.float().contiguous(),
+                                _ensure_grad(ctx.w_out).view(-1), _ensure_grad(ctx.b_out))
+        else:
+            dh = dout.to(torch.bfloat16).contiguous()
         for i in reversed(range(len(wb))):
             need_dx = i > 0 or ctx.x_needs_grad
-            dh = h.linear_bwd(dh, hs[i + 1], hs[i], wb[i], mod.w[i].grad, mod.b[i].grad, need_dx, mod.k_split)
-        dx = dh if ctx.x_needs_grad else None
+            dh = h.linear_bwd(dh, hs[i + 1], hs[i], wb[i], _ensure_grad(ctx.ws[i]), _ensure_grad(ctx.bs[i]),
+                              need_dx, ctx.k_split)
         ctx.hs = None
-        return (dx, None) + (None,) * (len(mod.w) * 2 + 2)
+        dx = dh if ctx.x_needs_grad else None
+        return (dx,) + (None,) * (6 + ctx.n_params)
+
+
+def fused_mlp(x: torch.Tensor, ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor],
+              w_out: Optional[torch.Tensor], b_out: Optional[torch.Tensor], cache: List[torch.Tensor],
+              k_split: int = 512) -> torch.Tensor:
+    """x: [M, K0] (cast to bf16 and zero-padded to ws[0].shape[1])."""
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    if x.shape[1] != ws[0].shape[1]:
+        x = torch.nn.functional.pad(x, (0, ws[0].shape[1] - x.shape[1]))
+    params = list(ws) + list(bs) + ([w_out, b_out] if w_out is not None else [])
+    return _MLPFn.apply(x.contiguous(), list(ws), list(bs), w_out, b_out, cache, k_split, *params)
 
 
 class FusedMLP(nn.Module):
@@ -97,7 +133,7 @@ class FusedMLP(nn.Module):
                 x = x.to(torch.bfloat16)
             if x.shape[1] != self.in_dim:
                 x = torch.nn.functional.pad(x, (0, self.in_dim - x.shape[1]))
-            return _FusedMLPFn.apply(x.contiguous(), self, *self.parameters())
+            return fused_mlp(x, list(self.w), list(self.b), self.w_out, self.b_out, self._bf16, self.k_split)
         x = x.float()
         if x.shape[1] != self.in_dim:
             x = torch.nn.functional.pad(x, (0, self.in_dim - x.shape[1]))

@@ -112,3 +112,57 @@ class DenseSync:
         if self.world > 1:
             dist.all_reduce(self.a.flat, group=self.group)
             self.a.flat.mul_(1.0 / self.world)
+
+
+class FlatSGD:
+    """p -= lr * g over the whole arena (one axpy)."""
+
+    def __init__(self, arena: DenseArena, lr: float = 0.01, weight_decay: float = 0.0):
+        self.a, self.lr, self.wd = arena, lr, weight_decay
+
+    def step(self, grad_scale: float = 1.0):
+        g = self.a.grad
+        if self.wd:
+            self.a.flat.mul_(1.0 - self.lr * self.wd)
+        self.a.flat.add_(g, alpha=-self.lr * grad_scale)
+
+    def state_dict(self):
+        return {}
+
+    def load_state_dict(self, sd):
+        pass
+
+
+class FlatMomentum:
+    def __init__(self, arena: DenseArena, lr: float = 0.01, momentum: float = 0.9, use_nesterov: bool = False):
+        self.a, self.lr, self.mu, self.nesterov = arena, lr, momentum, use_nesterov
+        self.vel = torch.zeros_like(arena.flat)
+
+    def step(self, grad_scale: float = 1.0):
+        g = self.a.grad if grad_scale == 1.0 else self.a.grad * grad_scale
+        self.vel.mul_(self.mu).add_(g)
+        upd = g.add(self.vel, alpha=self.mu) if self.nesterov else self.vel
+        self.a.flat.add_(upd, alpha=-self.lr)
+
+    def state_dict(self):
+        return {"velocity": self.vel}
+
+    def load_state_dict(self, sd):
+        self.vel.copy_(sd["velocity"])
+
+
+class FlatAdagrad:
+    def __init__(self, arena: DenseArena, lr: float = 0.01, epsilon: float = 1e-6, initial_accumulator_value=0.0):
+        self.a, self.lr, self.eps = arena, lr, epsilon
+        self.acc = torch.full_like(arena.flat, float(initial_accumulator_value))
+
+    def step(self, grad_scale: float = 1.0):
+        g = self.a.grad if grad_scale == 1.0 else self.a.grad * grad_scale
+        self.acc.addcmul_(g, g)
+        self.a.flat.addcdiv_(g, self.acc.sqrt().add_(self.eps), value=-self.lr)
+
+    def state_dict(self):
+        return {"moment": self.acc}
+
+    def load_state_dict(self, sd):
+        self.acc.copy_(sd["moment"])

@@ -1,0 +1,338 @@
+"""BoxPS trainer / device worker (dataset-driven training loop).
+
+Reference: ``BoxPSTrainer`` (``fw/boxps_trainer.cc:27-320``) and
+``BoxPSWorker`` (``fw/boxps_worker.cc:373-1482``, hot loop ``TrainFiles``
+:1278-1357), configured by ``trainer_desc.proto:121-129`` / the Python
+``BoxPSWorker._gen_worker_desc`` (``py/fluid/device_worker.py:623-652``).
+
+MI355X design: one process per GPU, so the trainer owns exactly one worker
+(the reference's worker-thread-per-GPU becomes a rank; ``thread`` is
+accepted and ignored).  Per batch the worker
+  1. binds the device batch (prefetched + H2D-copied on a side stream by the
+     dataset) to the program's data variables,
+  2. runs the lowered program (fused pull/seqpool/CVM, fused MLP, ...),
+  3. backward (sparse push + data_norm summaries happen inside it),
+  4. dense sync per ``sync_dense_mode`` and the fused optimizer step --
+     or, in async mode, pushes the flat gradient to the host
+     :class:`AsyncDenseTable` and pulls fresh parameters,
+  5. accumulates the registered metrics on the device, dumps fields,
+     checks NaN/Inf, and prints ``fetch_info`` every ``print_period``.
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+from ..fluid.executor import ExecContext, Session
+from ..fluid.kernels import Ragged
+from ..utils import flags as _flags
+from ..utils.log import logger
+
+log = logger()
+
+# sync_dense_mode (boxps_worker.cc:393-395,1191-1258)
+SYNC_NONE = 0
+SYNC_KSTEP_NODE = 1
+SYNC_KSTEP_ALL = 2
+SYNC_DATA_NORM = 3
+
+
+@dataclass
+class TrainerDesc:
+    async_mode: bool = False
+    sync_dense_mode: int = 0
+    sync_weight_step: int = 1
+    sync_one_ring: bool = False
+    param_need_sync: List[str] = field(default_factory=list)
+    dump_fields: List[str] = field(default_factory=list)
+    dump_fields_path: str = ""
+    dump_param: List[str] = field(default_factory=list)
+    dump_thread_num: int = 1
+    dump_mode: int = 0
+    dump_interval: int = 1
+    check_nan_var_names: List[str] = field(default_factory=list)
+    profile: bool = False
+
+    @staticmethod
+    def from_program(program) -> "TrainerDesc":
+        d = TrainerDesc()
+        po = program._pipeline_opt or {}
+        fo = program._fleet_opt or {}
+        d.async_mode = bool(po.get("async_mode", False))
+        d.sync_dense_mode = int(po.get("sync_dense_mode", 0))
+        d.sync_weight_step = max(1, int(po.get("sync_weight_step", 1) or 1))
+        d.sync_one_ring = bool(po.get("sync_one_ring", False))
+        d.param_need_sync = list(po.get("param_need_sync", []))
+        d.dump_thread_num = int(po.get("dump_thread_num", fo.get("dump_thread_num", 1)))
+        d.dump_fields = list(fo.get("dump_fields", []))
+        d.dump_fields_path = fo.get("dump_fields_path", "")
+        d.dump_param = list(fo.get("dump_param", []))
+        d.dump_mode = int(fo.get("dump_fields_mode", 1 if fo.get("dump_interval", 1) > 1 else 0))
+        d.dump_interval = int(fo.get("dump_interval", 1))
+        d.check_nan_var_names = list(fo.get("check_nan_var_names", []))
+        return d
+
+
+class _FetchView(dict):
+    """name -> tensor view of an ExecContext env for the metric registry."""
+
+    def __init__(self, ctx: ExecContext, batch):
+        super().__init__()
+        self.ctx, self.batch = ctx, batch
+
+    def __missing__(self, name):
+        if name == "__cmatch_rank__" and self.batch is not None and "cmatch_rank" in self.batch.extra:
+            return self.batch.extra["cmatch_rank"]
+        v = self.ctx.get(name)
+        return v.values if isinstance(v, Ragged) else v
+
+    def __contains__(self, name):
+        try:
+            self[name]
+            return True
+        except KeyError:
+            return False
+
+
+class AsyncDense:
+    """Async dense mode: params + Adam moments live in the native host table
+    (``csrc/host/async_dense.cc``); the GPU keeps a working copy that is
+    refreshed from the table before each batch."""
+
+    def __init__(self, session: Session, lr: float, device_num: int = 1, threads: int = 8):
+        self.s = session
+        self.arenas = session.arenas
+        flat = torch.cat([a.flat.detach().cpu() for a in self.arenas]) if self.arenas else torch.zeros(0)
+        self.adam_len = flat.numel()
+        summ = [t for n, t in session.storage.items() if not isinstance(t, torch.nn.Parameter)
+                and n.endswith(("batch_size", "batch_sum", "batch_square_sum"))]
+        self.summ = summ
+        init = torch.cat([flat] + [t.detach().float().cpu().reshape(-1) for t in summ]) if summ else flat
+        lrs = torch.full((self.adam_len,), float(lr))
+        self.table = _native.host().AsyncDenseTable(init.contiguous(), self.adam_len, lrs, device_num, threads)
+        self.host = torch.empty(init.numel(), dtype=torch.float32).pin_memory() if torch.cuda.is_available() \
+            else torch.empty(init.numel(), dtype=torch.float32)
+        self.summary_grads: Dict[int, torch.Tensor] = {}
+
+    def pull(self):
+        self.table.pull(self.host)
+        off = 0
+        for a in self.arenas:
+            n = a.flat.numel()
+            a.flat.data.copy_(self.host[off:off + n], non_blocking=True)
+            off += n
+        for t in self.summ:
+            n = t.numel()
+            t.copy_(self.host[off:off + n].view_as(t), non_blocking=True)
+            off += n
+
+    def push(self, summary_stats: Optional[List[torch.Tensor]] = None):
+        parts = [a.grad.detach().float().cpu() for a in self.arenas]
+        for i, t in enumerate(self.summ):
+            st = summary_stats[i] if summary_stats and i < len(summary_stats) else torch.zeros(t.numel())
+            parts.append(st.detach().float().cpu().reshape(-1))
+        self.table.push(torch.cat(parts) if parts else torch.zeros(0))
+
+    def finalize(self):
+        self.table.finalize()
+        self.pull()
+
+
+class BoxPSWorker:
+    def __init__(self, trainer: "BoxPSTrainer"):
+        self.t = trainer
+        self.s: Session = trainer.session
+        self.batches = 0
+        self.timers = {"read": 0.0, "step": 0.0, "metric": 0.0, "dump": 0.0}
+
+    def train_files(self) -> Dict[str, float]:
+        t = self.t
+        s = self.s
+        box = t.box
+        ds = t.dataset
+        dev = s.device
+        desc = t.desc
+        plan_batches = ds.batches(dev) if ds is not None else iter(())
+        t0 = time.time()
+        last = time.time()
+        n_ins = 0
+        for batch in plan_batches:
+            t_read = time.time()
+            self.timers["read"] += t_read - last
+            ctx = ExecContext(s, batch, training=not t.infer)
+            s.feed_batch(ctx, batch)
+            if t.async_dense is not None:
+                t.async_dense.pull()
+            if t.infer:
+                with torch.no_grad():
+                    s.forward(ctx)
+            elif t.async_dense is not None:
+                s.forward(ctx)
+                loss = ctx.get(s.program._optimize["loss"])
+                for a in s.arenas:
+                    a.zero_grad()
+                (loss.values if isinstance(loss, Ragged) else loss).float().sum().backward()
+                t.async_dense.push()
+            else:
+                s.step(ctx)
+                self._dense_sync_extra()
+            t_step = time.time()
+            self.timers["step"] += t_step - t_read
+            if box is not None and box.metrics.metrics:
+                box.metrics.add_batch(_FetchView(ctx, batch))
+            t_met = time.time()
+            self.timers["metric"] += t_met - t_step
+            if t.dumper is not None and desc.dump_fields:
+                self._dump(ctx, batch)
+            self.timers["dump"] += time.time() - t_met
+            if _flags.get_bool("check_nan_inf"):
+                self._check_nan_inf(ctx)
+            self.batches += 1
+            n_ins += batch.B
+            if t.fetch_list and t.print_period > 0 and self.batches % t.print_period == 0:
+                self._print_fetch(ctx)
+            last = time.time()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        el = time.time() - t0
+        return {"batches": self.batches, "instances": n_ins, "seconds": el,
+                "ins_per_sec": n_ins / el if el > 0 else 0.0, **self.timers}
+
+    def _dense_sync_extra(self):
+        """sync_dense_mode 3: average only the data_norm summaries every k steps."""
+        t = self.t
+        if t.desc.sync_dense_mode != SYNC_DATA_NORM or t.world <= 1:
+            return
+        if self.batches % t.desc.sync_weight_step != 0:
+            return
+        summ = [v for n, v in self.s.storage.items() if not isinstance(v, torch.nn.Parameter)
+                and n.endswith(("batch_size", "batch_sum", "batch_square_sum"))]
+        if summ:
+            flat = torch.cat([v.reshape(-1) for v in summ])
+            dist.all_reduce(flat, group=t.group)
+            flat.mul_(1.0 / t.world)
+            off = 0
+            for v in summ:
+                v.copy_(flat[off:off + v.numel()].view_as(v))
+                off += v.numel()
+
+    def _dump(self, ctx, batch):
+        t = self.t
+        names, mats = [], []
+        for f in t.desc.dump_fields:
+            try:
+                v = ctx.get(f)
+            except KeyError:
+                continue
+            v = v.values if isinstance(v, Ragged) else v
+            if v.dim() == 0 or v.shape[0] != batch.B:
+                continue
+            names.append(f)
+            mats.append(v.detach().float().reshape(batch.B, -1))
+        if not names:
+            return
+        lineids = batch.extra.get("ins_ids") if isinstance(batch.extra.get("ins_ids"), list) else None
+        if lineids is None:
+            lineids = [str(self.batches * batch.B + i) for i in range(batch.B)]
+        t.dumper.dump_fields(lineids, names, mats, t.desc.dump_mode, t.desc.dump_interval,
+                             _flags.get_bool("lineid_have_extend_info"))
+
+    def _check_nan_inf(self, ctx):
+        for name, v in ctx.env.items():
+            v = v.values if isinstance(v, Ragged) else v
+            if isinstance(v, torch.Tensor) and v.is_floating_point():
+                if not bool(torch.isfinite(v).all()):
+                    raise FloatingPointError(f"NaN/Inf detected in variable '{name}' at batch {self.batches}")
+
+    def _print_fetch(self, ctx):
+        t = self.t
+        parts = []
+        for i, f in enumerate(t.fetch_list):
+            name = f if isinstance(f, str) else f.name
+            info = t.fetch_info[i] if t.fetch_info and i < len(t.fetch_info) else name
+            v = ctx.get(name)
+            v = v.values if isinstance(v, Ragged) else v
+            parts.append(f"{info}: {v.detach().float().mean().item():.6f}")
+        log.info("batch %d  %s", self.batches, "  ".join(parts))
+
+
+class BoxPSTrainer:
+    def __init__(self, executor, program, scope, dataset, infer=False, debug=False, fetch_list=None,
+                 fetch_info=None, print_period=100, fetch_handler=None):
+        from ..ps.box_wrapper import BoxWrapper
+
+        self.exe = executor
+        self.program = program
+        self.scope = scope
+        self.dataset = dataset
+        self.infer = infer
+        self.debug = debug
+        self.fetch_list = list(fetch_list or [])
+        self.fetch_info = list(fetch_info or [])
+        self.print_period = print_period
+        self.fetch_handler = fetch_handler
+        self.desc = TrainerDesc.from_program(program)
+        self.box = BoxWrapper._instance
+        self.group = getattr(dataset, "group", None)
+        ready = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(self.group) if ready else 1
+        self.rank = dist.get_rank(self.group) if ready else 0
+        sync_mode, k = self._sync_policy()
+        names = [f if isinstance(f, str) else f.name for f in self.fetch_list]
+        names += [f for f in self.desc.dump_fields]
+        if self.box is not None:
+            for m in self.box.metrics.metrics.values():
+                names += [m.label_var, m.pred_var] + [x for x in (m.mask_var, m.cmatch_rank_var, m.uid_var) if x]
+                names += m.pred_list + m.mask_list
+        self.session = executor._session(program, scope, names, sync_mode=sync_mode, sync_k=k,
+                                          group=self.group)
+        self.async_dense = None
+        if self.desc.async_mode and not infer and program._optimize is not None:
+            spec = program._optimize["optimizer"].spec()
+            self.async_dense = AsyncDense(self.session, spec["lr"], device_num=1,
+                                          threads=int(os.environ.get("PBX_ASYNC_DENSE_THREADS", "8")))
+        self.dumper = None
+        if self.desc.dump_fields and self.desc.dump_fields_path:
+            dev_id = self.session.device.index or 0
+            ddir = os.path.join(self.desc.dump_fields_path, f"rank{self.rank:03d}")
+            os.makedirs(ddir, exist_ok=True)
+            self.dumper = _native.host().DumpWriter(ddir, dev_id, max(1, self.desc.dump_thread_num))
+        self.worker = BoxPSWorker(self)
+
+    def _sync_policy(self):
+        d = self.desc
+        if self.world <= 1:
+            return "none", 1
+        if d.sync_dense_mode in (SYNC_KSTEP_ALL,):
+            return "kstep", d.sync_weight_step
+        if d.sync_dense_mode == SYNC_KSTEP_NODE:
+            return "none", 1  # single node: nothing crosses nodes
+        if d.sync_dense_mode == SYNC_DATA_NORM:
+            return "none", 1
+        return "grad_allreduce", 1
+
+    def run(self):
+        stats = self.worker.train_files()
+        if self.async_dense is not None:
+            self.async_dense.finalize()
+        if self.dumper is not None:
+            if self.desc.dump_param:
+                ts = [self.session.logical[n] for n in self.desc.dump_param if n in self.session.logical]
+                self.dumper.dump_params(self.worker.batches, [n for n in self.desc.dump_param
+                                                              if n in self.session.logical], ts)
+            self.dumper.flush()
+        if self.debug:
+            log.info("trainer stats: %s", stats)
+        return stats
+
+
+def create_trainer(executor, program, scope, dataset, **kw) -> BoxPSTrainer:
+    """TrainerFactory: every program runs on the BoxPS trainer (the reference
+    picks it from ``program._pipeline_opt['trainer']``)."""
+    return BoxPSTrainer(executor, program, scope, dataset, **kw)

@@ -1,0 +1,223 @@
+"""fluid front end: program building, lowering/fusion, Executor.run,
+BoxPS pass driver + train_from_dataset, io, dump, async dense (CPU)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import paddlebox_amd.fluid as fluid
+from paddlebox_amd.fluid import framework
+from paddlebox_amd.ps.box_wrapper import BoxWrapper
+
+S = 4
+DENSE = 3
+
+
+def _lines(n, seed=0, vocab=400):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        toks = []
+        ids = []
+        for s in range(S):
+            k = int(rng.integers(1, 4))
+            v = (rng.zipf(1.3, size=k) % vocab + 1 + 1000 * (s + 1)).tolist()
+            ids.append(v)
+        score = sum(1 for v in ids[0] if v % 3 == 0) - 0.5
+        label = int(rng.random() < 1 / (1 + np.exp(-2 * score)))
+        toks += ["1", str(label)]
+        for v in ids:
+            toks += [str(len(v))] + [str(x) for x in v]
+        d = rng.random(DENSE).round(3).tolist()
+        toks += [str(DENSE)] + [str(x) for x in d]
+        out.append(" ".join(toks))
+    return out
+
+
+def _build(hidden=(16, 8), fuse_names=True):
+    main, startup = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, startup), fluid.unique_name.guard():
+        label = fluid.layers.data("label", shape=[1], dtype="int64")
+        slots = [fluid.layers.data(f"slot{i}", shape=[1], dtype="int64", lod_level=1) for i in range(S)]
+        dense = fluid.layers.data("dense", shape=[DENSE], dtype="float32")
+        show = fluid.layers.fill_constant_batch_size_like(label, shape=[-1, 1], dtype="float32", value=1.0)
+        click = fluid.layers.cast(label, "float32")
+        cvm = fluid.layers.concat([show, click], axis=1)
+        embs = fluid.layers._pull_box_sparse(slots, size=11)
+        pooled = fluid.contrib.layers.fused_seqpool_cvm(embs, "sum", cvm)
+        x = fluid.layers.concat(pooled + [dense], axis=1)
+        x = fluid.layers.data_norm(x, name="dn")
+        h = x
+        for i, n in enumerate(hidden):
+            h = fluid.layers.fc(h, n, act="relu", name=f"fc{i}")
+        logit = fluid.layers.fc(h, 1, name="out")
+        pred = fluid.layers.sigmoid(logit)
+        loss = fluid.layers.reduce_mean(fluid.layers.sigmoid_cross_entropy_with_logits(logit, click))
+        opt = fluid.optimizer.BoxPSOptimizer(fluid.optimizer.Adam(learning_rate=0.01))
+        opt.minimize(loss)
+    return main, startup, slots, label, dense, pred, loss
+
+
+def _files(tmp_path, n_files=2, n=300):
+    fs = []
+    for i in range(n_files):
+        p = tmp_path / f"part-{i}.txt"
+        p.write_text("\n".join(_lines(n, seed=i)) + "\n")
+        fs.append(str(p))
+    return fs
+
+
+@pytest.fixture
+def box():
+    b = fluid.core.BoxWrapper(8, device="cpu", new=True)
+    b.cfg.sgd.mf_create_thresholds = 0.0
+    b.initialize_gpu_and_load_model(slot_vector=list(range(S)), max_keys=200000)
+    yield b
+    BoxWrapper._instance = None
+
+
+def test_program_building_and_lowering(box):
+    main, startup, *_ = _build()
+    types = [op.type for op in main.global_block().ops]
+    assert "pull_box_sparse" in types and "fused_seqpool_cvm" in types and "data_norm" in types
+    assert len(startup.global_block().ops) == len(main.all_parameters())
+    from paddlebox_amd.fluid.lowering import lower
+
+    low = lower(main, gpu=True)
+    steps = [op.type for op in low.steps]
+    assert "__pull_seqpool_cvm" in steps and "pull_box_sparse" not in steps
+    assert "__fused_mlp" in steps and "fc" not in steps
+    assert any("absorbed" in n for n in low.fusions)
+    # CPU lowering keeps the fp32 fc ops
+    assert "fc" in [op.type for op in lower(main, gpu=False).steps]
+
+
+def test_train_from_dataset_and_metrics(box, tmp_path):
+    main, startup, slots, label, dense, pred, loss = _build()
+    exe = fluid.Executor(fluid.CPUPlace())
+    exe.run(startup)
+    ds = fluid.DatasetFactory().create_dataset("PadBoxSlotDataset")
+    ds.set_use_var([label] + slots + [dense])
+    ds.set_batch_size(64)
+    ds.set_filelist(_files(tmp_path))
+    box.init_metric("AucCalculator", "auc", label.name, pred.name, bucket_size=1000)
+    boxps = fluid.core.BoxPS(ds)
+    boxps.set_date(2024, 1, 1)
+    boxps.read_ins_into_memory()
+    assert box.engine.table.size() > 0
+    w0 = np.array(fluid.global_scope().find_var("fc0.w_0").get_tensor()).copy()
+    for _ in range(3):
+        boxps.begin_pass()
+        stats = exe.train_from_dataset(main, ds, fetch_list=[loss], print_period=5)
+        boxps.end_pass()
+    assert stats["batches"] == 10 and stats["instances"] == 600
+    w1 = np.array(fluid.global_scope().find_var("fc0.w_0").get_tensor())
+    assert not np.allclose(w0, w1)  # dense params trained, visible through the scope
+    bs = np.array(fluid.global_scope().find_var("dn.batch_size").get_tensor())
+    assert (bs > 1e4).all()  # data_norm summaries updated by the backward
+    msg = box.get_metric_msg("auc")
+    assert msg[7] == 1800 and msg[0] > 0.5
+
+
+def test_fused_and_unfused_paths_agree(box, tmp_path):
+    """The lowering's fused pull+seqpool+CVM op must equal the reference
+    op-by-op program (pull_box_sparse records -> fused_seqpool_cvm)."""
+    main, startup, slots, label, dense, pred, loss = _build()
+    lines = _lines(64, seed=7)
+    ds = fluid.DatasetFactory().create_dataset("PadBoxSlotDataset")
+    ds.set_use_var([label] + slots + [dense])
+    ds.set_batch_size(64)
+    ds.add_lines(lines)
+    box.feed_pass(ds, "20240101")
+    # warm the table so pulls are non-trivial
+    from paddlebox_amd.fluid.executor import ExecContext, Session
+
+    batch = ds.build_batch(0, 64)
+    outs = {}
+    for fuse in (True, False):
+        scope = fluid.Scope()
+        exe = fluid.Executor(fluid.CPUPlace())
+        exe.run(startup, scope=scope)
+        s = Session(main, scope, torch.device("cpu"), fuse=fuse)
+        s.training = False
+        ctx = ExecContext(s, batch, training=False)
+        s.feed_batch(ctx, batch)
+        s.forward(ctx)
+        outs[fuse] = ctx.get(pred).detach().clone()
+    torch.testing.assert_close(outs[True], outs[False])
+
+
+def test_executor_run_with_feed_dict(box):
+    main, startup, slots, label, dense, pred, loss = _build()
+    exe = fluid.Executor(fluid.CPUPlace())
+    exe.run(startup)
+    rng = np.random.default_rng(0)
+    B = 8
+    feed = {"label": rng.integers(0, 2, (B, 1)).astype("int64"), "dense": rng.random((B, DENSE)).astype("float32")}
+    keys = []
+    for i in range(S):
+        lens = rng.integers(1, 3, B)
+        vals = rng.integers(1, 50, int(lens.sum())) + 1000 * (i + 1)
+        keys.append(vals)
+        feed[f"slot{i}"] = fluid.create_lod_tensor(vals.reshape(-1, 1).astype("int64"), [lens.tolist()],
+                                                   fluid.CPUPlace())
+    box.feed_pass(torch.as_tensor(np.concatenate(keys)), "20240101")
+    l0 = None
+    for _ in range(20):
+        (lv,) = exe.run(main, feed=feed, fetch_list=[loss])
+        l0 = l0 if l0 is not None else float(lv)
+    assert float(lv) < l0
+
+
+def test_io_roundtrip(box, tmp_path):
+    main, startup, *_ = _build()
+    exe = fluid.Executor(fluid.CPUPlace())
+    exe.run(startup)
+    saved = fluid.io.save_persistables(exe, str(tmp_path / "m"), main)
+    assert "fc0.w_0" in saved and "dn.batch_size" in saved
+    w = np.array(fluid.global_scope().find_var("fc0.w_0").get_tensor()).copy()
+    fluid.global_scope().find_var("fc0.w_0").set_value(np.zeros_like(w))
+    fluid.io.load_persistables(exe, str(tmp_path / "m"), main)
+    np.testing.assert_allclose(np.array(fluid.global_scope().find_var("fc0.w_0").get_tensor()), w)
+    fluid.io.save_persistables(exe, str(tmp_path / "st"), main, filename="params.safetensors")
+    assert os.path.exists(tmp_path / "st" / "params.safetensors")
+
+
+def test_dump_fields_and_async_dense(box, tmp_path):
+    main, startup, slots, label, dense, pred, loss = _build()
+    main._fleet_opt = {"dump_fields": [pred.name], "dump_fields_path": str(tmp_path / "dump"),
+                       "dump_param": ["fc0.b_0"]}
+    main._pipeline_opt["async_mode"] = True
+    exe = fluid.Executor(fluid.CPUPlace())
+    exe.run(startup)
+    ds = fluid.DatasetFactory().create_dataset("PadBoxSlotDataset")
+    ds.set_use_var([label] + slots + [dense])
+    ds.set_batch_size(50)
+    ds.set_filelist(_files(tmp_path, 1, 200))
+    boxps = fluid.core.BoxPS(ds)
+    boxps.read_ins_into_memory()
+    boxps.begin_pass()
+    w0 = np.array(fluid.global_scope().find_var("fc0.w_0").get_tensor()).copy()
+    stats = exe.train_from_dataset(main, ds)
+    boxps.end_pass()
+    assert stats["batches"] == 4
+    w1 = np.array(fluid.global_scope().find_var("fc0.w_0").get_tensor())
+    assert not np.allclose(w0, w1)  # async table applied the pushed gradients
+    files = sorted(os.listdir(tmp_path / "dump" / "rank000"))
+    assert files
+    text = "".join(open(tmp_path / "dump" / "rank000" / f).read() for f in files)
+    lines = [l for l in text.splitlines() if l and not l.startswith("(")]
+    assert len(lines) == 200
+    f0 = lines[0].split("\t")[1]
+    assert f0.startswith(pred.name + ":1:")
+    assert any(l.startswith("(4,fc0.b_0,16)") for l in text.splitlines())
+
+
+def test_xxh64_known_values():
+    from paddlebox_amd import _native
+
+    h = _native.host()
+    assert h.xxh64("", 0) == 0xEF46DB3751D8E999
+    assert h.xxh64("a", 0) == 0xD24EC4F1A98C6E5B
+    assert h.xxh64("abc", 0) == 0x44BC2CF5AD770999
