@@ -14,8 +14,9 @@ import re
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
+    name = re.sub(r"^void ", "", name)
     name = re.sub(r"\(.*", "", name)
-    name = name.replace("pbx::(anonymous namespace)::", "pbx::")
     if name.startswith("Cijk_"):
         return "hipBLASLt GEMM " + name.split("_MT")[1].split("_")[0] if "_MT" in name else "hipBLASLt GEMM"
     if "rocprim" in name:
