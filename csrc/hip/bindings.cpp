@@ -430,16 +430,31 @@ static void cast_bf16(const Tensor& x, Tensor y) {
 // Fused data_norm + first/FM head.  Returns (y bf16 [B,Cp], lin [B], means, scales).
 static std::vector<Tensor> head_fwd(const Tensor& x, int S, int Eo, int ew_col, int D, int Cp,
                                     const c10::optional<Tensor>& bsize, const c10::optional<Tensor>& bsum,
-                                    const c10::optional<Tensor>& bsq) {
+                                    const c10::optional<Tensor>& bsq, const c10::optional<Tensor>& y_out,
+                                    const c10::optional<Tensor>& yT_out) {
   check_cuda(x, "x");
   PBX_CHECK(x.scalar_type() == torch::kFloat32 && x.dim() == 2, "head: x must be fp32 [B, C]");
   const int B = (int)x.size(0), C = (int)x.size(1);
-  PBX_CHECK(Cp >= C && S * Eo <= C, "head: bad widths");
+  PBX_CHECK(Cp >= C && Cp <= (C + 7) / 8 * 8 + 8 && S * Eo <= C, "head: bad widths");
   PBX_CHECK(head_lds_bytes(C, D) <= 160 * 1024, "head: row slab exceeds LDS");
   HeadArgs a;
   a.x = ptr<float>(x);
   a.B = B; a.C = C; a.Cp = Cp; a.S = S; a.Eo = Eo; a.ew_col = ew_col; a.D = D;
-  auto y = torch::empty({B, Cp}, x.options().dtype(torch::kBFloat16));
+  Tensor y;
+  if (y_out.has_value() && y_out->defined()) {
+    y = *y_out;
+    check_cuda(y, "y_out");
+    PBX_CHECK(y.scalar_type() == torch::kBFloat16 && y.size(0) == B && y.size(1) >= Cp, "head: y_out shape");
+    a.ldy = (int)y.size(1);
+  } else {
+    y = torch::empty({B, Cp}, x.options().dtype(torch::kBFloat16));
+  }
+  if (yT_out.has_value() && yT_out->defined()) {
+    check_cuda(*yT_out, "yT_out");
+    PBX_CHECK(yT_out->size(0) >= Cp && yT_out->size(1) >= B, "head: yT_out shape");
+    a.yT = reinterpret_cast<unsigned short*>(yT_out->data_ptr());
+    a.ldyt = (int)yT_out->size(1);
+  }
   auto lin = torch::empty({B}, x.options());
   Tensor means, scales;
   if (bsize.has_value()) {
@@ -466,8 +481,9 @@ static std::vector<Tensor> head_bwd(const Tensor& x, const c10::optional<Tensor>
   auto dx = torch::empty_like(x);
   Tensor stats, acc;
   if (dy.has_value()) {
-    PBX_CHECK(dy->scalar_type() == torch::kBFloat16 && dy->size(1) == Cp && dy->is_contiguous(), "head: dy");
+    PBX_CHECK(dy->scalar_type() == torch::kBFloat16 && dy->size(1) >= Cp && dy->is_contiguous(), "head: dy");
     a.dy = reinterpret_cast<const unsigned short*>(dy->data_ptr());
+    a.ldy = (int)dy->size(1);
   }
   auto dl = dlin.contiguous();
   a.dlin = ptr<float>(dl);
@@ -486,6 +502,127 @@ static std::vector<Tensor> head_bwd(const Tensor& x, const c10::optional<Tensor>
   }
   return {dx, stats};
 }
+
+// --------------------------------------------------------------- fused MLP workspace
+// Persistent, zero-initialised buffers in the layout contract of mlp.hip, for
+// a fixed batch M and layer widths dims = [K0, H1, ..., Hn] (multiples of 8).
+class MlpWorkspace {
+ public:
+  MlpWorkspace(int64_t M, std::vector<int64_t> dims, int device, int64_t k_split)
+      : M_(M), dims_(dims), ksplit_(k_split) {
+    PBX_CHECK(dims.size() >= 2, "mlp: need at least one hidden layer");
+    for (auto d : dims) PBX_CHECK(d > 0 && d % 8 == 0, "mlp: widths must be multiples of 8");
+    PBX_CHECK(k_split % 64 == 0 && k_split > 0, "mlp: k_split must be a positive multiple of 64");
+    auto ob = torch::TensorOptions().dtype(torch::kBFloat16).device(torch::kCUDA, device);
+    auto of = torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device);
+    ldM_ = p64(M);
+    const int n = (int)dims.size() - 1;
+    for (int i = 0; i <= n; ++i) {
+      X_.push_back(torch::zeros({M, p64(dims[i])}, ob));
+      auto xt = torch::zeros({p64(dims[i] + 1), ldM_}, ob);
+      xt[dims[i]].narrow(0, 0, M).fill_(1.0);  // bias ones row
+      XT_.push_back(xt);
+    }
+    for (int l = 0; l < n; ++l) {
+      dZ_.push_back(torch::zeros({M, p64(dims[l + 1])}, ob));
+      dZT_.push_back(torch::zeros({p64(dims[l + 1]), ldM_}, ob));
+      Wb_.push_back(torch::zeros({p64(dims[l + 1]), p64(dims[l])}, ob));
+      WTb_.push_back(torch::zeros({p64(dims[l]), p64(dims[l + 1])}, ob));
+    }
+    dX0_ = torch::zeros({M, p64(dims[0])}, ob);
+    logits_ = torch::zeros({M}, of);
+    part_ = torch::zeros({mlp_gemv_bwd_blocks((int)M), dims[n] + 1}, of);
+  }
+  static int64_t p64(int64_t v) { return (v + 63) / 64 * 64; }
+
+  Tensor forward(const std::vector<Tensor>& W, const std::vector<Tensor>& b, const Tensor& wout, const Tensor& bout) {
+    const int n = (int)dims_.size() - 1;
+    PBX_CHECK((int)W.size() == n && (int)b.size() == n, "mlp.forward: layer count");
+    auto s = cur_stream();
+    PBX_CHECK(n <= kMaxMlpLayers, "mlp: too many layers");
+    CastWtBatch cb;
+    cb.n = n;
+    cb.tile_off[0] = 0;
+    for (int l = 0; l < n; ++l) {
+      const int K = (int)dims_[l], N = (int)dims_[l + 1];
+      check_cuda(W[l], "W");
+      PBX_CHECK(W[l].size(0) == N && W[l].size(1) == K, "mlp.forward: W shape");
+      cb.w[l] = ptr<float>(W[l]);
+      cb.wb[l] = bptr(Wb_[l]);
+      cb.wtb[l] = bptr(WTb_[l]);
+      cb.N[l] = N; cb.K[l] = K; cb.pN[l] = (int)p64(N); cb.pK[l] = (int)p64(K);
+      cb.tile_off[l + 1] = cb.tile_off[l] + (cb.pN[l] / 32) * (cb.pK[l] / 32);
+    }
+    launch_cast_wt(cb, s);
+    for (int l = 0; l < n; ++l) {
+      const int K = (int)dims_[l], N = (int)dims_[l + 1];
+      MlpGemmArgs g;
+      g.A = bptr(X_[l]); g.lda = (int)p64(K);
+      g.B = bptr(Wb_[l]); g.ldb = (int)p64(K);
+      g.M = (int)M_; g.N = (int)p64(N); g.K = (int)p64(K);
+      g.C = bptr(X_[l + 1]); g.ldc = (int)p64(N);
+      g.CT = bptr(XT_[l + 1]); g.ldct = (int)ldM_;
+      g.ncols_valid = N;
+      g.bias = ptr<float>(b[l]);
+      g.relu = 1;
+      launch_mlp_gemm(g, MLP_EPI_FWD, s);
+    }
+    launch_mlp_gemv_fwd(bptr(X_[n]), (int)M_, (int)dims_[n], (int)p64(dims_[n]), ptr<float>(wout), ptr<float>(bout),
+                        ptr<float>(logits_), s);
+    return logits_;
+  }
+
+  // Accumulates parameter grads into dW/db/dwout/dbout; returns dX0 when need_dx.
+  Tensor backward(const Tensor& dlogit, const std::vector<Tensor>& dW, const std::vector<Tensor>& db,
+                  const Tensor& wout, Tensor dwout, Tensor dbout, bool need_dx) {
+    const int n = (int)dims_.size() - 1;
+    auto s = cur_stream();
+    auto dl = dlogit.contiguous();
+    const int H = (int)dims_[n];
+    launch_mlp_gemv_bwd(bptr(X_[n]), (int)M_, H, (int)p64(H), ptr<float>(wout), ptr<float>(dl), bptr(dZ_[n - 1]),
+                        bptr(dZT_[n - 1]), (int)ldM_, ptr<float>(part_), ptr<float>(dwout), ptr<float>(dbout), s);
+    for (int l = n - 1; l >= 0; --l) {
+      const int K = (int)dims_[l], N = (int)dims_[l + 1];
+      check_cuda(dW[l], "dW");
+      MlpGemmArgs g;  // dW_l += dZ_l^T [X_l | 1]
+      g.A = bptr(dZT_[l]); g.lda = (int)ldM_;
+      g.B = bptr(XT_[l]); g.ldb = (int)ldM_;
+      g.M = N; g.N = K + 1; g.K = (int)ldM_;
+      g.k_per_split = (int)ksplit_;
+      g.dW = ptr<float>(dW[l]); g.lddw = K; g.db = ptr<float>(db[l]);
+      g.ncols_valid = K; g.nrows_valid = N;
+      launch_mlp_gemm(g, MLP_EPI_DW, s);
+      if (l > 0 || need_dx) {
+        MlpGemmArgs d;  // dZ_{l-1} = (dZ_l W_l) . [X_l > 0]
+        d.A = bptr(dZ_[l]); d.lda = (int)p64(N);
+        d.B = bptr(WTb_[l]); d.ldb = (int)p64(N);
+        d.M = (int)M_; d.N = (int)p64(K); d.K = (int)p64(N);
+        d.C = l > 0 ? bptr(dZ_[l - 1]) : bptr(dX0_);
+        d.ldc = (int)p64(K);
+        d.CT = l > 0 ? bptr(dZT_[l - 1]) : nullptr;
+        d.ldct = (int)ldM_;
+        d.ncols_valid = K;
+        d.mask = l > 0 ? bptr(X_[l]) : nullptr;
+        d.ldmask = (int)p64(K);
+        launch_mlp_gemm(d, MLP_EPI_DX, s);
+      }
+    }
+    return need_dx ? dX0_ : Tensor();
+  }
+  Tensor x(int i) const { return X_.at(i); }
+  Tensor xt(int i) const { return XT_.at(i); }
+  Tensor dz(int i) const { return dZ_.at(i); }
+  Tensor dx0() const { return dX0_; }
+  int64_t M() const { return M_; }
+
+ private:
+  static unsigned short* bptr(const Tensor& t) { return reinterpret_cast<unsigned short*>(t.data_ptr()); }
+  int64_t M_, ldM_;
+  std::vector<int64_t> dims_;
+  int64_t ksplit_;
+  std::vector<Tensor> X_, XT_, dZ_, dZT_, Wb_, WTb_;
+  Tensor dX0_, logits_, part_;
+};
 
 static void data_norm_update(Tensor bsize, Tensor bsum, Tensor bsq, const Tensor& stats, float decay) {
   launch_data_norm_update(ptr<float>(bsize), ptr<float>(bsum), ptr<float>(bsq), ptr<float>(stats),
@@ -599,6 +736,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("uniq_h", &DedupWorkspace::uniq_h)
       .def_readonly("seg", &DedupWorkspace::seg)
       .def_readonly("u_count", &DedupWorkspace::u_count);
+  py::class_<MlpWorkspace>(m, "MlpWorkspace")
+      .def(py::init<int64_t, std::vector<int64_t>, int, int64_t>(), py::arg("M"), py::arg("dims"),
+           py::arg("device"), py::arg("k_split") = 1024)
+      .def("forward", &MlpWorkspace::forward)
+      .def("backward", &MlpWorkspace::backward)
+      .def("x", &MlpWorkspace::x)
+      .def("xt", &MlpWorkspace::xt)
+      .def("dz", &MlpWorkspace::dz)
+      .def("dx0", &MlpWorkspace::dx0)
+      .def_property_readonly("M", &MlpWorkspace::M);
   m.def("fill_occurrence", &fill_occurrence);
   m.def("seqpool_cvm_fwd", &seqpool_cvm_fwd);
   m.def("push_merge", &push_merge);

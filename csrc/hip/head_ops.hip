@@ -35,9 +35,11 @@ __global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* xs = lds;
   const int C = a.C, Cp = a.Cp;
+  const int ldy = a.ldy ? a.ldy : Cp;
   const int row0 = blockIdx.x * kRB;
   const int rows = min(kRB, a.B - row0);
   if (rows <= 0) return;
+  unsigned short* ys = reinterpret_cast<unsigned short*>(xs + kRB * (C + a.D));  // [kRB][Cp] bf16 (for y^T)
   // 1) stage + data_norm output (bf16, padded to Cp)
   for (int i = threadIdx.x; i < rows * Cp; i += blockDim.x) {
     const int r = i / Cp, c = i - r * Cp;
@@ -54,7 +56,9 @@ __global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
         yv = v;
       }
     }
-    a.y[(int64_t)(row0 + r) * Cp + c] = f2bf(yv);
+    const unsigned short yb = f2bf(yv);
+    a.y[(int64_t)(row0 + r) * ldy + c] = yb;
+    if (a.yT) ys[r * Cp + c] = yb;
   }
   if (blockIdx.x == 0 && a.means) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -64,6 +68,23 @@ __global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
     }
   }
   __syncthreads();
+  if (a.yT) {  // y^T[c][row0 .. row0+rows): one 32-byte run per column
+    for (int c = threadIdx.x; c < Cp; c += blockDim.x) {
+      unsigned short* dst = a.yT + (int64_t)c * a.ldyt + row0;
+      if (rows == kRB && ((row0 & 7) == 0) && ((a.ldyt & 7) == 0)) {
+        uint4 v0, v1;
+        unsigned int p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = (unsigned)ys[(2 * j) * Cp + c] | ((unsigned)ys[(2 * j + 1) * Cp + c] << 16);
+        v0 = make_uint4(p[0], p[1], p[2], p[3]);
+        v1 = make_uint4(p[4], p[5], p[6], p[7]);
+        reinterpret_cast<uint4*>(dst)[0] = v0;
+        reinterpret_cast<uint4*>(dst)[1] = v1;
+      } else {
+        for (int r = 0; r < rows; ++r) dst[r] = ys[r * Cp + c];
+      }
+    }
+  }
   // 2) first + FM per row: 16 threads per row (kRB=16 rows x 16 = 256)
   const int r = threadIdx.x >> 4, t = threadIdx.x & 15;
   float lin = 0.f;
@@ -110,7 +131,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(HeadArgs a) {
   for (int i = threadIdx.x; i < rows * C; i += blockDim.x) {
     const int r = i / C, c = i - r * C;
     const float sc = a.scales ? a.scales[c] : 1.f;
-    float g = a.dy ? bf2f(a.dy[(int64_t)(row0 + r) * Cp + c]) * sc : 0.f;
+    float g = a.dy ? bf2f(a.dy[(int64_t)(row0 + r) * (a.ldy ? a.ldy : Cp) + c]) * sc : 0.f;
     if (c < sparse_w) {
       const int j = c % a.Eo;
       const float dl = a.dlin[row0 + r];
@@ -151,7 +172,10 @@ __global__ void k_dn_stats(const float* __restrict__ acc, int C, int N, float ep
 
 }  // namespace
 
-size_t head_lds_bytes(int C, int D) { return (size_t)kRB * (C + D) * sizeof(float); }
+size_t head_lds_bytes(int C, int D) {
+  // fp32 row slab + FM sums, then the bf16 y slab for the transposed write
+  return (size_t)kRB * (C + D) * sizeof(float) + (size_t)kRB * ((C + 7) / 8 * 8 + 8) * sizeof(unsigned short);
+}
 
 void launch_head_fwd(const HeadArgs& a, hipStream_t s) {
   if (a.B == 0) return;

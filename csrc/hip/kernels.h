@@ -207,9 +207,12 @@ struct HeadArgs {
   const float* bsq = nullptr;
   float* means = nullptr;   // [C] out (fwd)
   float* scales = nullptr;  // [C] out (fwd) / in (bwd)
-  unsigned short* y = nullptr;  // [B, Cp] bf16 out (fwd)
+  unsigned short* y = nullptr;  // [B, ldy] bf16 out (fwd), columns >= Cp untouched
+  int ldy = 0;                  // row stride of y / dy (0 = Cp)
+  unsigned short* yT = nullptr; // optional [Cp][ldyt] transposed copy of y (fwd)
+  int ldyt = 0;
   float* lin = nullptr;         // [B] first + FM out (fwd)
-  const unsigned short* dy = nullptr;  // [B, Cp] bf16 in (bwd)
+  const unsigned short* dy = nullptr;  // [B, ldy] bf16 in (bwd)
   const float* dlin = nullptr;         // [B] in (bwd)
   float* dx = nullptr;                 // [B, C] out (bwd)
   float* stat_acc = nullptr;           // [head_blocks(B), 2C] per-block partial sums (bwd)
@@ -243,5 +246,47 @@ void launch_auc_accumulate(const float* pred, const float* label, const float* m
 void launch_adam_flat(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                       float b2, float eps, float* pows, float grad_scale, float weight_decay,
                       hipStream_t s);
+
+// ---------------------------------------------------------------- fused MLP engine (mlp.hip)
+enum MlpEpi { MLP_EPI_FWD = 0, MLP_EPI_DX = 1, MLP_EPI_DW = 2 };
+struct MlpGemmArgs {
+  const unsigned short* A = nullptr;  // [M rows][lda] k-contiguous bf16
+  const unsigned short* B = nullptr;  // [N rows][ldb] k-contiguous bf16
+  int lda = 0, ldb = 0;
+  int M = 0, N = 0, K = 0;  // K: multiple of 64, zero padded in both operands
+  int k_per_split = 1 << 30;
+  // FWD / DX
+  unsigned short* C = nullptr;  // [M][ldc]
+  int ldc = 0;
+  unsigned short* CT = nullptr;  // optional transposed copy [ncols_valid][ldct]
+  int ldct = 0;
+  int ncols_valid = 0;  // FWD/DX: real output width (bias / CT rows); DW: real K (col == it -> db)
+  int nrows_valid = 0;  // DW: real N of dW
+  const float* bias = nullptr;
+  int relu = 0;
+  const unsigned short* mask = nullptr;  // DX: [M][ldmask], zero the output where mask <= 0
+  int ldmask = 0;
+  // DW
+  float* dW = nullptr;  // [nrows_valid][lddw] fp32 (atomic accumulate)
+  int lddw = 0;
+  float* db = nullptr;
+};
+void launch_mlp_gemm(const MlpGemmArgs& g, int epi, hipStream_t s);
+constexpr int kMaxMlpLayers = 8;
+struct CastWtBatch {  // all layers' fp32 -> bf16 (W, W^T) casts in one launch
+  const float* w[kMaxMlpLayers];
+  unsigned short* wb[kMaxMlpLayers];
+  unsigned short* wtb[kMaxMlpLayers];
+  int N[kMaxMlpLayers], K[kMaxMlpLayers], pN[kMaxMlpLayers], pK[kMaxMlpLayers];
+  int tile_off[kMaxMlpLayers + 1];  // prefix sum of 32x32 tiles per layer
+  int n = 0;
+};
+void launch_cast_wt(const CastWtBatch& c, hipStream_t s);
+void launch_mlp_gemv_fwd(const unsigned short* h, int M, int K, int ld, const float* w, const float* b, float* out,
+                         hipStream_t s);
+int mlp_gemv_bwd_blocks(int M);
+void launch_mlp_gemv_bwd(const unsigned short* h, int M, int K, int ld, const float* w, const float* dout,
+                         unsigned short* dz, unsigned short* dzt, int ldt, float* part, float* dw, float* db,
+                         hipStream_t s);
 
 }  // namespace pbx

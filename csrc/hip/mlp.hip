@@ -1,0 +1,306 @@
+// Fused CTR MLP engine: every GEMM in "NT" form (both operands k-contiguous)
+// on v_mfma_f32_32x32x16_bf16, with operand tiles streamed global -> LDS by
+// global_load_lds_dwordx4 (LDS-DMA, no VGPR staging) through a 3-deep ring
+// (two k-tiles in flight across each barrier: counted vmcnt + raw s_barrier).
+//
+// Layout contract (owned by the MlpWorkspace in bindings.cpp):
+//  * activations X_i [M][ldX] bf16, ldX = pad64(K_i), pad columns zero;
+//  * transposed copies X_i^T [pad64(K_i+1)][ldM] bf16, ldM = pad64(M), with
+//    row K_i == 1.0 (the bias "ones" row: db falls out of the dW GEMM);
+//  * weights W_i bf16 [pad64(N_i)][pad64(K_i)] and W_i^T [pad64(K_i)][pad64(N_i)],
+//    zero padded, cast from the fp32 masters [N_i][K_i] every step;
+//  * gradients dZ_i [M][pad64(N_i)] and dZ_i^T [pad64(N_i)][ldM].
+// The GEMM K extent is therefore always a multiple of 64 with zero padding,
+// so the main loop has no guards; rows past M/N are clamped (computed, not
+// stored).  Producers apply the ReLU masks in their epilogues, which is what
+// lets the operands go straight from HBM into LDS.
+//
+//   fwd   Y_i  = relu(X_i W_i^T + b_i)   -> Y_i (=X_{i+1}), Y_i^T      EPI_FWD
+//   bwd   dW_i += dZ_i^T X_i  (+ db_i)    split-K over M, fp32 atomics  EPI_DW
+//   bwd   dZ_{i-1} = (dZ_i W_i) . [X_i>0] -> dZ_{i-1}, dZ_{i-1}^T      EPI_DX
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace pbx {
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+
+constexpr int TK = 64, NSTAGE = 3;
+
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  unsigned int u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(((unsigned int)h) << 16); }
+
+// LDS image of a rows x 64-k tile: row r is 8 chunks of 16 B; logical
+// chunk c lives at physical chunk c ^ (r & 7) (conflict-free ds_read_b128
+// fragment reads; the swizzle is applied on the global side of the DMA).
+__device__ __forceinline__ int lds_off(int r, int c) { return r * TK + ((c ^ (r & 7)) << 3); }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Block tile BM x BN, 4 waves as WM x WN, each wave 32 x (BN/WN) =
+// NACC 32x32 accumulators sharing one A fragment per k-step.
+template <int EPI, int BM, int BN, int WM>
+__global__ __launch_bounds__(256) void k_gemm_nt(MlpGemmArgs g) {
+  constexpr int WN = 4 / WM;
+  constexpr int NACC = BN / WN / 32;
+  constexpr int NA = BM / 32, NB = BN / 32;  // 16-B DMAs per thread per stage
+  constexpr int STAGE = (BM + BN) * TK;
+  static_assert(BM / WM == 32 && NACC >= 1, "tile layout");
+  __shared__ __attribute__((aligned(16))) unsigned short smem[NSTAGE * STAGE];
+  // XCD-aware bijective remap: consecutive work-group ids (same A row panel)
+  // land on one XCD so the panel is served from that XCD's L2.
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int nwg = nx * ny;
+  const int lin = blockIdx.y * nx + blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = lin % 8;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + lin / 8;
+  const int bm = wgid / nx, bn = wgid % nx;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int kbeg = blockIdx.z * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = (kend - kbeg) / TK;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w / WN, wn = w % WN;
+  const int r = lane & 31, hh = lane >> 5;
+
+  // DMA sources: chunk id qq = j*256 + threadIdx.x (one 64-lane instruction
+  // moves 1 KB = 8 rows); chunk qq -> row qq/8, physical chunk qq%8.
+  const unsigned short* ga[NA];
+  const unsigned short* gb[NB];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int qq = j * 256 + threadIdx.x;
+    const int row = qq >> 3, c = (qq & 7) ^ (row & 7);
+    ga[j] = g.A + (int64_t)min(m0 + row, g.M - 1) * g.lda + kbeg + c * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int qq = j * 256 + threadIdx.x;
+    const int row = qq >> 3, c = (qq & 7) ^ (row & 7);
+    gb[j] = g.B + (int64_t)min(n0 + row, g.N - 1) * g.ldb + kbeg + c * 8;
+  }
+  const int wbase = (w * 64) * 8;  // wave-uniform LDS element offset of this wave's 1 KB per instruction
+  auto issue = [&](int stage, int kt) {
+    unsigned short* base = smem + stage * STAGE;
+#pragma unroll
+    for (int j = 0; j < NA; ++j)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ga[j] + kt * TK), (lds_ptr_t)(base + j * 2048 + wbase), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(gb[j] + kt * TK), (lds_ptr_t)(base + BM * TK + j * 2048 + wbase),
+                                       16, 0, 0);
+  };
+
+  f32x16 acc[NACC];
+#pragma unroll
+  for (int i = 0; i < NACC; ++i) acc[i] = (f32x16){0};
+  if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int t = 0; t < nk; ++t) {
+    // retire tile t; tile t+1 (NA+NB DMAs per thread) stays in flight
+    if (t + 1 < nk) wait_vm<NA + NB>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // buffer (t+2)%3 was last read in iteration t-1; every wave is past it
+    if (t + 2 < nk) issue((t + 2) % NSTAGE, t + 2);
+    const unsigned short* As = smem + (t % NSTAGE) * STAGE;
+    const unsigned short* Bs = As + BM * TK;
+    const int ra = wm * 32 + r;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(As + lds_off(ra, ks * 2 + hh));
+#pragma unroll
+      for (int i = 0; i < NACC; ++i) {
+        const int rb = wn * (BN / WN) + i * 32 + r;
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(Bs + lds_off(rb, ks * 2 + hh));
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[i], 0, 0, 0);
+      }
+    }
+  }
+
+  // epilogue; C/D map: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+  const int mb = m0 + wm * 32 + 4 * hh;
+#pragma unroll
+  for (int i = 0; i < NACC; ++i) {
+    const int n = n0 + wn * (BN / WN) + i * 32 + r;
+    if (EPI == MLP_EPI_DW) {
+      if (n > g.ncols_valid) continue;  // col ncols_valid = ones row -> db
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int m = mb + (reg & 3) + 8 * (reg >> 2);
+        if (m >= g.nrows_valid) continue;
+        if (n < g.ncols_valid) atomicAdd(&g.dW[(int64_t)m * g.lddw + n], acc[i][reg]);
+        else atomicAdd(&g.db[m], acc[i][reg]);
+      }
+      continue;
+    }
+    float bias = 0.f;
+    if (EPI == MLP_EPI_FWD && g.bias && n < g.ncols_valid) bias = g.bias[n];
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      unsigned short o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mb + j + 8 * grp;
+        float v = acc[i][grp * 4 + j] + bias;
+        if (EPI == MLP_EPI_FWD) {
+          if (g.relu) v = v > 0.f ? v : 0.f;
+        } else if (g.mask && m < g.M) {  // relu' of this layer's input
+          if ((short)g.mask[(int64_t)m * g.ldmask + n] <= 0) v = 0.f;
+        }
+        o[j] = f2bf(v);
+        if (m < g.M) g.C[(int64_t)m * g.ldc + n] = o[j];
+      }
+      const int m4 = mb + 8 * grp;  // 4 consecutive rows -> one 8-byte store into the transposed copy
+      if (g.CT && n < g.ncols_valid && m4 < g.M) {
+        if (m4 + 3 < g.M) {
+          uint2 pk;
+          pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
+          pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
+          *reinterpret_cast<uint2*>(g.CT + (int64_t)n * g.ldct + m4) = pk;
+        } else {
+          for (int j = 0; j < 4 && m4 + j < g.M; ++j) g.CT[(int64_t)n * g.ldct + m4 + j] = o[j];
+        }
+      }
+    }
+  }
+}
+
+// fp32 master W [N][K] -> bf16 W [pN][pK] and W^T [pK][pN] (zero padded),
+// all layers in one launch (1-D grid over every layer's 32x32 tiles).
+__global__ __launch_bounds__(256) void k_cast_wt(CastWtBatch c) {
+  __shared__ unsigned short t[32][33];
+  int l = 0;
+  while (l + 1 < c.n && (int)blockIdx.x >= c.tile_off[l + 1]) ++l;
+  const int tile = blockIdx.x - c.tile_off[l];
+  const int tk = (c.pK[l] + 31) / 32;
+  const int n0 = (tile / tk) * 32, k0 = (tile % tk) * 32;
+  const int N = c.N[l], K = c.K[l], pN = c.pN[l], pK = c.pK[l];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int i = ty; i < 32; i += 8) {
+    const int n = n0 + i, k = k0 + tx;
+    const unsigned short v = (n < N && k < K) ? f2bf(c.w[l][(int64_t)n * K + k]) : (unsigned short)0;
+    t[i][tx] = v;
+    if (n < pN && k < pK) c.wb[l][(int64_t)n * pK + k] = v;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int k = k0 + i, n = n0 + tx;
+    if (k < pK && n < pN) c.wtb[l][(int64_t)k * pN + n] = t[tx][i];
+  }
+}
+
+// logit = h . w_out + b   (h [M][ld] bf16, K valid columns)
+__global__ __launch_bounds__(256) void k_gemv_fwd(const unsigned short* __restrict__ h, int M, int K, int ld,
+                                                  const float* __restrict__ w, const float* __restrict__ b,
+                                                  float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  float s = 0.f;
+  for (int k = lane * 2; k < K; k += 128) {
+    const unsigned int p = *reinterpret_cast<const unsigned int*>(h + (int64_t)m * ld + k);
+    s += bf2f((unsigned short)(p & 0xffff)) * w[k];
+    if (k + 1 < K) s += bf2f((unsigned short)(p >> 16)) * w[k + 1];
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) out[m] = s + (b ? b[0] : 0.f);
+}
+
+// Output-layer backward: dZ[m,k] = dout[m]*w[k]*[h>0] into dZ [M][ld] and
+// dZ^T [K][ldt]; per-block partial rows of dw (cols < K) and db (col K).
+// Block = kGB rows x all K; thread -> column k (row-major accesses are
+// coalesced across threads; the transposed run per thread is 2 x 16 B).
+constexpr int kGB = 16;
+__global__ __launch_bounds__(256) void k_gemv_bwd(const unsigned short* __restrict__ h, int M, int K, int ld,
+                                                  const float* __restrict__ w, const float* __restrict__ dout,
+                                                  unsigned short* __restrict__ dz, unsigned short* __restrict__ dzt,
+                                                  int ldt, float* __restrict__ part) {
+  const int m0 = blockIdx.x * kGB;
+  const int rows = min(kGB, M - m0);
+  float d[kGB];
+#pragma unroll
+  for (int j = 0; j < kGB; ++j) d[j] = j < rows ? dout[m0 + j] : 0.f;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    const float wk = w[k];
+    float acc = 0.f;
+    unsigned int pk[kGB / 2];
+#pragma unroll
+    for (int j = 0; j < kGB; ++j) {
+      unsigned short o = 0;
+      if (j < rows) {
+        const int64_t off = (int64_t)(m0 + j) * ld + k;
+        const float hv = bf2f(h[off]);
+        acc += d[j] * hv;
+        o = hv > 0.f ? f2bf(d[j] * wk) : (unsigned short)0;
+        dz[off] = o;
+      }
+      if (j & 1) pk[j >> 1] |= (unsigned)o << 16;
+      else pk[j >> 1] = o;
+    }
+    unsigned short* dst = dzt + (int64_t)k * ldt + m0;
+    if (rows == kGB && ((m0 & 7) == 0) && ((ldt & 7) == 0)) {
+      reinterpret_cast<uint4*>(dst)[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      reinterpret_cast<uint4*>(dst)[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+    } else {
+      for (int j = 0; j < rows; ++j) dst[j] = (unsigned short)((pk[j >> 1] >> ((j & 1) * 16)) & 0xffff);
+    }
+    part[(int64_t)blockIdx.x * (K + 1) + k] = acc;
+  }
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < kGB; ++j) s += d[j];
+    part[(int64_t)blockIdx.x * (K + 1) + K] = s;
+  }
+}
+
+}  // namespace
+
+void launch_mlp_gemm(const MlpGemmArgs& g, int epi, hipStream_t s) {
+  const int splits = (g.K + g.k_per_split - 1) / g.k_per_split;
+  if (epi == MLP_EPI_DW) {  // 64x64 tiles: dW is only ~400 x 400
+    dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, splits);
+    hipLaunchKernelGGL((k_gemm_nt<MLP_EPI_DW, 64, 64, 2>), grid, dim3(256), 0, s, g);
+    return;
+  }
+  // 128 x 64 tiles, 4 waves stacked in M (each 32 x 64: the A fragment feeds 2 MFMAs)
+  dim3 grid((g.N + 63) / 64, (g.M + 127) / 128, splits);
+  if (epi == MLP_EPI_FWD) hipLaunchKernelGGL((k_gemm_nt<MLP_EPI_FWD, 128, 64, 4>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((k_gemm_nt<MLP_EPI_DX, 128, 64, 4>), grid, dim3(256), 0, s, g);
+}
+
+void launch_cast_wt(const CastWtBatch& c, hipStream_t s) {
+  if (c.n == 0) return;
+  hipLaunchKernelGGL(k_cast_wt, dim3(c.tile_off[c.n]), dim3(256), 0, s, c);
+}
+
+void launch_mlp_gemv_fwd(const unsigned short* h, int M, int K, int ld, const float* w, const float* b, float* out,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_gemv_fwd, dim3((M + 3) / 4), dim3(256), 0, s, h, M, K, ld, w, b, out);
+}
+
+int mlp_gemv_bwd_blocks(int M) { return (M + kGB - 1) / kGB; }
+
+void launch_mlp_gemv_bwd(const unsigned short* h, int M, int K, int ld, const float* w, const float* dout,
+                         unsigned short* dz, unsigned short* dzt, int ldt, float* part, float* dw, float* db,
+                         hipStream_t s) {
+  const int nb = mlp_gemv_bwd_blocks(M);
+  hipLaunchKernelGGL(k_gemv_bwd, dim3(nb), dim3(256), 0, s, h, M, K, ld, w, dout, dz, dzt, ldt, part);
+  launch_colsum_acc(part, nb, K + 1, dw, K, db, s);
+}
+
+}  // namespace pbx

@@ -45,14 +45,22 @@ class DeepFM(nn.Module):
         self.dn = DataNorm(C) if use_data_norm else None
         self.mlp = FusedMLP(C, hidden, 1)
         self.bias = nn.Parameter(torch.zeros(1))
+        self.use_workspace = True
         # column of embed_w inside each slot block; embedx follow it
         self.ew_col = 2 if self.sp.use_cvm and not self.sp.clk_filter else (1 if self.sp.use_cvm else 0)
 
     def forward(self, batch):
         B, S = batch.B, batch.S
         x = pull_seqpool_cvm_concat(self.engine, batch.keys, batch.lod, B, S, batch.cvm, batch.dense, self.sp)
-        y, lin = ctr_head(x, self.dn, S, self.Eo, self.ew_col, self.D, self.Cp)
-        deep = self.mlp(y)
+        if x.is_cuda and self.use_workspace:
+            # the head writes the MLP input (and its transpose) straight into
+            # the MLP workspace; the MLP streams it HBM -> LDS by DMA
+            ws = self.mlp.workspace(B, x.device)
+            y, lin = ctr_head(x, self.dn, S, self.Eo, self.ew_col, self.D, self.Cp, ws.x(0), ws.xt(0))
+            deep = self.mlp.forward_ws(y)
+        else:
+            y, lin = ctr_head(x, self.dn, S, self.Eo, self.ew_col, self.D, self.Cp)
+            deep = self.mlp(y)
         logit = deep + lin + self.bias
         loss, pred = sigmoid_logloss(logit, batch.label)
         return loss, pred

@@ -94,15 +94,16 @@ class _CtrHead(torch.autograd.Function):
     kernel each way on the GPU (csrc/hip/head_ops.hip)."""
 
     @staticmethod
-    def forward(ctx, x, dn: Optional[DataNorm], S, Eo, ew_col, D, Cp):
+    def forward(ctx, x, dn: Optional[DataNorm], S, Eo, ew_col, D, Cp, y_out=None, yT_out=None):
         x = x.contiguous().float()
         has_dn = dn is not None
         if _gpu(x):
             if has_dn:
                 y, lin, means, scales = _native.hip().head_fwd(x, S, Eo, ew_col, D, Cp, dn.batch_size, dn.batch_sum,
-                                                                dn.batch_square_sum)
+                                                                dn.batch_square_sum, y_out, yT_out)
             else:
-                y, lin, means, scales = _native.hip().head_fwd(x, S, Eo, ew_col, D, Cp, None, None, None)
+                y, lin, means, scales = _native.hip().head_fwd(x, S, Eo, ew_col, D, Cp, None, None, None, y_out,
+                                                                yT_out)
         else:
             if has_dn:
                 y, means, scales = ref.data_norm_fwd(x, dn.batch_size, dn.batch_sum, dn.batch_square_sum)
@@ -154,12 +155,15 @@ class _CtrHead(torch.autograd.Function):
                 _native.hip().data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, stats, dn.decay)
             else:
                 ref.data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, stats, dn.decay)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
-def ctr_head(x: torch.Tensor, dn: Optional["DataNorm"], S: int, Eo: int, ew_col: int, D: int, Cp: int):
-    """(data_norm(x) as the MLP input [B, Cp], first-order + FM logit part [B])."""
-    return _CtrHead.apply(x, dn, S, Eo, ew_col, D, Cp)
+def ctr_head(x: torch.Tensor, dn: Optional["DataNorm"], S: int, Eo: int, ew_col: int, D: int, Cp: int,
+             y_out: Optional[torch.Tensor] = None, yT_out: Optional[torch.Tensor] = None):
+    """(data_norm(x) as the MLP input [B, Cp] -- or written into the MLP
+    workspace's X0 [B, ld] / X0^T buffers when given --, first-order + FM
+    logit part [B])."""
+    return _CtrHead.apply(x, dn, S, Eo, ew_col, D, Cp, y_out, yT_out)
 
 
 # ---------------------------------------------------------------- FM

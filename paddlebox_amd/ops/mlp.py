@@ -78,6 +78,27 @@ class _MLPFn(torch.autograd.Function):
         return (dx,) + (None,) * (6 + ctx.n_params)
 
 
+class _MLPWsFn(torch.autograd.Function):
+    """Fused MLP over the persistent MlpWorkspace (csrc/hip/mlp.hip)."""
+
+    @staticmethod
+    def forward(ctx, x0, mod, *params):
+        ws = mod._ws
+        logits = ws.forward(list(mod.w), list(mod.b), mod.w_out.view(-1), mod.b_out)
+        ctx.mod = mod
+        ctx.need_dx = x0.requires_grad
+        ctx.n_params = len(params)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogit):
+        mod = ctx.mod
+        mod.ensure_grads()
+        dx0 = mod._ws.backward(dlogit.float().contiguous(), [w.grad for w in mod.w], [b.grad for b in mod.b],
+                               mod.w_out.view(-1), mod.w_out.grad.view(-1), mod.b_out.grad, ctx.need_dx)
+        return (dx0 if ctx.need_dx else None, None) + (None,) * ctx.n_params
+
+
 def fused_mlp(x: torch.Tensor, ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor],
               w_out: Optional[torch.Tensor], b_out: Optional[torch.Tensor], cache: List[torch.Tensor],
               k_split: int = 512) -> torch.Tensor:
@@ -113,6 +134,21 @@ class FusedMLP(nn.Module):
         self.b_out = nn.Parameter(torch.zeros(1))
         self._bf16: List[torch.Tensor] = []
         self.k_split = 512
+        self.k_split_dw = 1024  # split-K over the batch for the workspace dW GEMMs
+        self._ws = None
+
+    # ---- workspace path (csrc/hip/mlp.hip): persistent padded activations +
+    # transposed copies so every GEMM streams both operands HBM -> LDS by DMA
+    def workspace(self, M: int, device: torch.device):
+        if self._ws is None or self._ws.M != M:
+            dims = [self.in_dim] + list(self.hidden)
+            self._ws = _native.hip().MlpWorkspace(M, dims, device.index or 0, self.k_split_dw)
+        return self._ws
+
+    def forward_ws(self, x0: torch.Tensor) -> torch.Tensor:
+        """x0 = workspace.x(0) already filled (and x0^T = workspace.xt(0)) by
+        the producer (the CTR head).  Returns [M] logits."""
+        return _MLPWsFn.apply(x0, self, *self.parameters())
 
     def bf16_weights(self) -> List[torch.Tensor]:
         h = _native.hip()

@@ -330,3 +330,53 @@ def test_ctr_head_gpu_matches_cpu():
     torch.testing.assert_close(xg.grad.cpu(), xc.grad, rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(dn_g.batch_sum.cpu(), dn_c.batch_sum, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dn_g.batch_square_sum.cpu(), dn_c.batch_square_sum, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,dims", [(8192, [280, 400, 400, 400]), (300, [24, 72, 8]), (1000, [64, 128, 64])])
+def test_mlp_workspace_matches_fp32(M, dims):
+    """Workspace MLP (DMA-staged NT GEMMs, transposed activations, fused
+    masks, split-K atomics) vs an fp32 reference on the same bf16 inputs."""
+    from paddlebox_amd.ops.mlp import FusedMLP
+
+    torch.manual_seed(M)
+    mlp = FusedMLP(dims[0], dims[1:], 1).to(DEV)
+    mlp.ensure_grads()
+    for p in mlp.parameters():
+        p.grad.zero_()
+    ws = mlp.workspace(M, torch.device(DEV))
+    x = _bf(torch.randn(M, dims[0], device=DEV))
+    ws.x(0)[:, :dims[0]] = x
+    ws.xt(0)[:dims[0], :M] = x.t()
+    x0 = ws.x(0).detach().requires_grad_(True)
+    logits = mlp.forward_ws(x0)
+    # reference with bf16-rounded weights and activations
+    h = x.float()
+    hs = [h]
+    for w, b in zip(mlp.w, mlp.b):
+        h = torch.relu(h @ _bf(w).float().t() + b).to(torch.bfloat16).float()
+        hs.append(h)
+    ref_logit = h @ mlp.w_out.view(-1) + mlp.b_out
+    torch.testing.assert_close(logits, ref_logit, rtol=3e-2, atol=3e-2)
+    dl = torch.randn(M, device=DEV)
+    logits.backward(dl)
+    # reference backward on the activations the kernels stored (so ReLU masks
+    # agree exactly), gradients rounded to bf16 where the kernels store them
+    torch.testing.assert_close(ws.x(len(dims) - 1)[:, :dims[-1]].float(), hs[-1], rtol=3e-2, atol=3e-2)
+    hs = [ws.x(i)[:, :dims[i]].float() for i in range(len(dims))]
+    wo = mlp.w_out.detach().view(-1)
+    dz = (dl[:, None] * wo[None, :] * (hs[-1] > 0)).to(torch.bfloat16).float()
+    gw, gb = [None] * len(hs[:-1]), [None] * len(hs[:-1])
+    g_wo = dl @ hs[-1]
+    dx = None
+    for l in reversed(range(len(mlp.w))):
+        gw[l] = dz.t() @ hs[l]
+        gb[l] = dz.sum(0)
+        dx = dz @ _bf(mlp.w[l].detach()).float()
+        if l > 0:
+            dz = (dx * (hs[l] > 0)).to(torch.bfloat16).float()
+    for w, g in zip(mlp.w, gw):
+        torch.testing.assert_close(w.grad, g, rtol=2e-2, atol=1e-2 * float(g.abs().max()))
+    for b, g in zip(mlp.b, gb):
+        torch.testing.assert_close(b.grad, g, rtol=2e-2, atol=1e-2 * float(g.abs().max()))
+    torch.testing.assert_close(mlp.w_out.grad.view(-1), g_wo, rtol=2e-2, atol=1e-2 * float(g_wo.abs().max()))
+    torch.testing.assert_close(x0.grad[:, :dims[0]].float(), dx, rtol=2e-2, atol=1e-2 * float(dx.abs().max()))
