@@ -165,9 +165,23 @@ struct DedupWorkspace {
   int64_t cap;
   Tensor h_tmp, h_sorted, idx_tmp, perm, flags, scan, uid, uniq_h, seg, u_count, temp;
   size_t temp_bytes;
-  DedupWorkspace(int64_t cap_, int device) : cap(cap_) {
+  bool hash = false;
+  Tensor tk, tu, slot, slot_of_u, cnt, rank;
+  uint64_t tmask = 0;
+  DedupWorkspace(int64_t cap_, int device, bool hash_) : cap(cap_), hash(hash_) {
     auto o8 = torch::TensorOptions().dtype(torch::kInt64).device(torch::kCUDA, device);
     auto o4 = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device);
+    if (hash) {
+      int64_t tcap = 1024;
+      while (tcap < 2 * cap) tcap <<= 1;  // load <= 0.5
+      tmask = (uint64_t)tcap - 1;
+      tk = torch::full({tcap}, -1, o8);  // kEmptyKey
+      tu = torch::full({tcap}, -1, o4);
+      slot = torch::empty({cap}, o4);
+      slot_of_u = torch::empty({cap}, o4);
+      cnt = torch::zeros({cap + 1}, o4);
+      rank = torch::empty({cap}, o4);
+    }
     h_tmp = torch::empty({cap}, o8);
     h_sorted = torch::empty({cap}, o8);
     idx_tmp = torch::empty({cap}, o4);
@@ -177,8 +191,8 @@ struct DedupWorkspace {
     uid = torch::empty({cap}, o4);
     uniq_h = torch::empty({cap}, o8);
     seg = torch::empty({cap + 1}, o4);
-    u_count = torch::zeros({2}, o4);  // [U, n_valid]
-    temp_bytes = dedup_temp_bytes(cap);
+    u_count = torch::zeros({3}, o4);  // [U, n_valid, U of the previous hash run]
+    temp_bytes = hash ? hash_dedup_temp_bytes(cap) : dedup_temp_bytes(cap);
     temp = torch::empty({(int64_t)temp_bytes}, torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, device));
   }
   // keys: int64 tensor (n <= cap).  Results live in this workspace.
@@ -186,6 +200,19 @@ struct DedupWorkspace {
     check_cuda(keys, "keys");
     const int64_t n = keys.numel();
     PBX_CHECK(n <= cap, "dedup: more keys than workspace capacity");
+    if (hash) {
+      HashDedupArgs a;
+      a.keys = ptr<uint64_t>(keys);
+      a.n = n; a.cap = cap; a.mixed = mixed ? 1 : 0;
+      a.tk = ptr<uint64_t>(tk); a.tu = ptr<int32_t>(tu); a.tmask = tmask;
+      a.slot = ptr<int32_t>(slot); a.slot_of_u = ptr<int32_t>(slot_of_u);
+      a.cnt = ptr<int32_t>(cnt); a.rank = ptr<int32_t>(rank);
+      a.uid = ptr<int32_t>(uid); a.perm = ptr<int32_t>(perm); a.uniq_h = ptr<uint64_t>(uniq_h);
+      a.seg = ptr<int32_t>(seg); a.u_count = ptr<int32_t>(u_count);
+      launch_dedup_hash(a, temp.data_ptr(), temp_bytes, cur_stream());
+      last_n = n;
+      return;
+    }
     launch_dedup(ptr<uint64_t>(keys), n, mixed, ptr<uint64_t>(h_tmp), ptr<uint64_t>(h_sorted), ptr<int32_t>(idx_tmp),
                  ptr<int32_t>(perm), ptr<int32_t>(flags), ptr<int32_t>(scan), ptr<int32_t>(uid), ptr<uint64_t>(uniq_h),
                  ptr<int32_t>(seg), ptr<int32_t>(u_count), temp.data_ptr(), temp_bytes, cur_stream());
@@ -727,8 +754,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("capacity", &GpuTable::capacity)
       .def_property_readonly("nbuckets", &GpuTable::nbuckets);
   py::class_<DedupWorkspace>(m, "DedupWorkspace")
-      .def(py::init<int64_t, int>())
+      .def(py::init<int64_t, int, bool>(), py::arg("cap"), py::arg("device"), py::arg("hash") = true)
       .def("run", &DedupWorkspace::run, py::arg("keys"), py::arg("mixed") = false)
+      .def_readonly("hash", &DedupWorkspace::hash)
       .def_readonly("cap", &DedupWorkspace::cap)
       .def_readonly("h_sorted", &DedupWorkspace::h_sorted)
       .def_readonly("perm", &DedupWorkspace::perm)

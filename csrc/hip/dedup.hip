@@ -68,6 +68,188 @@ __global__ void k_emit(const uint64_t* __restrict__ hs, const int32_t* __restric
   }
 }
 
+
+// ---------------------------------------------------------------- hash dedup
+// Sort-free variant (single-shard engine and the owner side of the key
+// all-to-all, where the unique list needs no particular order):
+//   insert   : open-addressing insert of h into a scratch table (64-bit CAS,
+//              linear probing); the inserting lane takes the next unique id
+//              (one atomic per wave: ballot + mbcnt) and records uniq_h / slot
+//   rank     : per block, occurrences are counted per unique id in an LDS
+//              hash (LDS atomics), then ONE global atomicAdd per distinct id per
+//              block returns the block's base -> rank of every occurrence
+//              within its id (Zipf-hot ids see <= #blocks global atomics)
+//   scan     : exclusive sum of the per-id counts -> seg
+//   scatter  : perm[seg[u] + rank] = occurrence
+// The table is cleaned lazily at the start of the next run (only the U
+// slots that were used), so no per-batch memset of the table.
+constexpr int kRankItems = 4;      // occurrences per thread in k_hash_rank
+constexpr int kRankLds = 2048;     // LDS hash entries per block (load <= 0.5)
+
+__global__ void k_hash_cleanup(int32_t* __restrict__ u_count, const int32_t* __restrict__ slot_of_u,
+                               uint64_t* __restrict__ tk, int32_t* __restrict__ tu, int32_t* __restrict__ cnt,
+                               int64_t cap) {
+  // u_count = [U, n_valid, U of the previous run]; the previous run's
+  // scatter kernel saved its U into [2], so [0..1] can be reset here
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u == 0) {
+    u_count[0] = 0;
+    u_count[1] = 0;
+  }
+  if (u >= cap || u >= u_count[2]) return;
+  const int32_t p = slot_of_u[u];
+  tk[p] = kEmptyKey;
+  tu[p] = -1;
+  cnt[u] = 0;
+}
+
+// Block-level pre-dedup in LDS (64-bit CAS) so a Zipf-hot key costs at most
+// one global table operation per block, and a read-before-CAS so keys that
+// are already present take no atomic at all.
+constexpr int kInsItems = 4;
+constexpr int kInsLds = 2048;
+__global__ __launch_bounds__(256) void k_hash_insert(const uint64_t* __restrict__ keys, int64_t n, int mixed,
+                                                     uint64_t* __restrict__ tk, int32_t* __restrict__ tu,
+                                                     uint64_t tmask, int32_t* __restrict__ slot,
+                                                     int32_t* __restrict__ slot_of_u, uint64_t* __restrict__ uniq_h,
+                                                     int32_t* __restrict__ u_count) {
+  __shared__ unsigned long long lk[kInsLds];
+  __shared__ int32_t lslot[kInsLds];
+  __shared__ int32_t nvalid_blk;
+  for (int e = threadIdx.x; e < kInsLds; e += blockDim.x) lk[e] = (unsigned long long)kEmptyKey;
+  if (threadIdx.x == 0) nvalid_blk = 0;
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * (blockDim.x * kInsItems);
+  const int lane = threadIdx.x & 63;
+  int pos[kInsItems];
+  bool own[kInsItems];
+  uint64_t hv[kInsItems];
+  int nv = 0;
+  // 1) block-local dedup
+#pragma unroll
+  for (int t = 0; t < kInsItems; ++t) {
+    const int64_t i = i0 + t * blockDim.x + threadIdx.x;
+    pos[t] = -1;
+    own[t] = false;
+    if (i >= n) continue;
+    const uint64_t k = keys[i];
+    if (k == kEmptyKey) {
+      slot[i] = -1;
+      continue;
+    }
+    ++nv;
+    const uint64_t h = mixed ? k : mix64(k);
+    hv[t] = h;
+    unsigned e = (unsigned)(rehash64(h) >> 40) & (kInsLds - 1);
+    for (;;) {
+      const unsigned long long old = atomicCAS(&lk[e], (unsigned long long)kEmptyKey, (unsigned long long)h);
+      if (old == (unsigned long long)kEmptyKey) { own[t] = true; break; }
+      if (old == (unsigned long long)h) break;
+      e = (e + 1) & (kInsLds - 1);
+    }
+    pos[t] = (int)e;
+  }
+  if (nv) atomicAdd(&nvalid_blk, nv);
+  // 2) one global insert per distinct key of the block
+  bool won[kInsItems];
+  uint64_t gp[kInsItems];
+#pragma unroll
+  for (int t = 0; t < kInsItems; ++t) {
+    won[t] = false;
+    if (!own[t]) continue;
+    const uint64_t h = hv[t];
+    uint64_t p = rehash64(h) & tmask;
+    for (;;) {
+      unsigned long long cur = *reinterpret_cast<volatile unsigned long long*>(&tk[p]);
+      if (cur == (unsigned long long)h) break;
+      if (cur == (unsigned long long)kEmptyKey) {
+        cur = atomicCAS(reinterpret_cast<unsigned long long*>(&tk[p]), (unsigned long long)kEmptyKey,
+                        (unsigned long long)h);
+        if (cur == (unsigned long long)kEmptyKey) { won[t] = true; break; }
+        if (cur == (unsigned long long)h) break;
+      }
+      p = (p + 1) & tmask;
+    }
+    gp[t] = p;
+    lslot[pos[t]] = (int32_t)p;
+  }
+  // new ids: one counter atomic per wave per item round
+#pragma unroll
+  for (int t = 0; t < kInsItems; ++t) {
+    const unsigned long long wm = __ballot(won[t]);
+    int base = 0;
+    if (lane == 0 && wm) base = atomicAdd(&u_count[0], __popcll(wm));
+    base = __shfl(base, 0);
+    if (won[t]) {
+      const int u = base + __popcll(wm & ((1ull << lane) - 1ull));
+      tu[gp[t]] = u;
+      uniq_h[u] = hv[t];
+      slot_of_u[u] = (int32_t)gp[t];
+    }
+  }
+  __syncthreads();
+  // 3) every occurrence takes its key's global slot
+#pragma unroll
+  for (int t = 0; t < kInsItems; ++t) {
+    const int64_t i = i0 + t * blockDim.x + threadIdx.x;
+    if (pos[t] >= 0) slot[i] = lslot[pos[t]];
+  }
+  if (threadIdx.x == 0 && nvalid_blk) atomicAdd(&u_count[1], nvalid_blk);
+}
+
+__global__ __launch_bounds__(256) void k_hash_rank(const int32_t* __restrict__ slot, const int32_t* __restrict__ tu,
+                                                   int64_t n, int32_t* __restrict__ uid, int32_t* __restrict__ cnt,
+                                                   int32_t* __restrict__ rank) {
+  __shared__ int32_t lkey[kRankLds];
+  __shared__ int32_t lcnt[kRankLds];
+  for (int e = threadIdx.x; e < kRankLds; e += blockDim.x) {
+    lkey[e] = -1;
+    lcnt[e] = 0;
+  }
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * (blockDim.x * kRankItems);
+  int pos[kRankItems], lr[kRankItems];
+#pragma unroll
+  for (int t = 0; t < kRankItems; ++t) {
+    const int64_t i = i0 + t * blockDim.x + threadIdx.x;
+    pos[t] = -1;
+    if (i >= n) continue;
+    const int32_t sl = slot[i];
+    const int32_t u = sl >= 0 ? tu[sl] : -1;
+    uid[i] = u;
+    if (u < 0) continue;
+    unsigned e = ((unsigned)u * 2654435761u) & (kRankLds - 1);
+    for (;;) {
+      const int32_t old = atomicCAS(&lkey[e], -1, u);
+      if (old == -1 || old == u) break;
+      e = (e + 1) & (kRankLds - 1);
+    }
+    pos[t] = (int)e;
+    lr[t] = atomicAdd(&lcnt[e], 1);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kRankLds; e += blockDim.x) {
+    const int32_t u = lkey[e];
+    if (u >= 0) lcnt[e] = atomicAdd(&cnt[u], lcnt[e]);  // block base within id u
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < kRankItems; ++t) {
+    const int64_t i = i0 + t * blockDim.x + threadIdx.x;
+    if (pos[t] >= 0) rank[i] = lcnt[pos[t]] + lr[t];
+  }
+}
+
+__global__ void k_hash_scatter(const int32_t* __restrict__ uid, const int32_t* __restrict__ rank,
+                               const int32_t* __restrict__ seg, int64_t n, int32_t* __restrict__ perm,
+                               int32_t* __restrict__ u_count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) u_count[2] = u_count[0];  // for the next run's cleanup
+  if (i >= n) return;
+  const int32_t u = uid[i];
+  if (u >= 0) perm[seg[u] + rank[i]] = (int32_t)i;
+}
+
 }  // namespace
 
 size_t dedup_temp_bytes(int64_t n) {
@@ -96,6 +278,33 @@ void launch_dedup(const uint64_t* keys, int64_t n, bool keys_are_mixed, uint64_t
   (void)hipcub::DeviceScan::InclusiveSum(temp, tb, flags, scan, (int)n, s);
   hipLaunchKernelGGL(k_emit, dim3(g), dim3(256), 0, s, h_sorted, perm, flags, scan, n, uid, uniq_h,
                      seg, u_count);
+}
+
+size_t hash_dedup_temp_bytes(int64_t cap) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr, (int)(cap + 1));
+  return b + 256;
+}
+
+void launch_dedup_hash(const HashDedupArgs& a, void* temp, size_t temp_bytes, hipStream_t s) {
+  const int64_t cap = a.cap;
+  const unsigned gc = (unsigned)((cap + 255) / 256);
+  hipLaunchKernelGGL(k_hash_cleanup, dim3(gc), dim3(256), 0, s, a.u_count, a.slot_of_u, a.tk, a.tu, a.cnt, cap);
+  if (a.n <= 0) {
+    (void)hipMemsetAsync(a.seg, 0, sizeof(int32_t), s);
+    (void)hipMemsetAsync(a.u_count + 2, 0, sizeof(int32_t), s);
+    return;
+  }
+  const unsigned g = (unsigned)((a.n + 255) / 256);
+  const unsigned gi = (unsigned)((a.n + 256 * kInsItems - 1) / (256 * kInsItems));
+  hipLaunchKernelGGL(k_hash_insert, dim3(gi), dim3(256), 0, s, a.keys, a.n, a.mixed, a.tk, a.tu, a.tmask, a.slot,
+                     a.slot_of_u, a.uniq_h, a.u_count);
+  const unsigned gr = (unsigned)((a.n + 256 * kRankItems - 1) / (256 * kRankItems));
+  hipLaunchKernelGGL(k_hash_rank, dim3(gr), dim3(256), 0, s, a.slot, a.tu, a.n, a.uid, a.cnt, a.rank);
+  size_t tb = temp_bytes;
+  // cnt[u] == 0 for u >= U, so seg[U] (and every later entry) = number of valid occurrences
+  (void)hipcub::DeviceScan::ExclusiveSum(temp, tb, a.cnt, a.seg, (int)(cap + 1), s);
+  hipLaunchKernelGGL(k_hash_scatter, dim3(g), dim3(256), 0, s, a.uid, a.rank, a.seg, a.n, a.perm, a.u_count);
 }
 
 }  // namespace pbx

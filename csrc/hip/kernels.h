@@ -69,6 +69,29 @@ void launch_dedup(const uint64_t* keys, int64_t n, bool keys_are_mixed, uint64_t
                   int32_t* scan, int32_t* uid, uint64_t* uniq_h, int32_t* seg, int32_t* u_count,
                   void* temp, size_t temp_bytes, hipStream_t s);
 
+// Sort-free dedup (same outputs; uniq_h in insertion order, perm grouped by
+// unique id).  Scratch table tk/tu [tmask+1] must start as kEmptyKey / -1 and
+// cnt [cap+1] as 0; the launch cleans what the previous run used.
+struct HashDedupArgs {
+  const uint64_t* keys = nullptr;
+  int64_t n = 0, cap = 0;
+  int mixed = 0;
+  uint64_t* tk = nullptr;
+  int32_t* tu = nullptr;
+  uint64_t tmask = 0;
+  int32_t* slot = nullptr;       // [cap]
+  int32_t* slot_of_u = nullptr;  // [cap]
+  int32_t* cnt = nullptr;        // [cap+1]
+  int32_t* rank = nullptr;       // [cap]
+  int32_t* uid = nullptr;
+  int32_t* perm = nullptr;
+  uint64_t* uniq_h = nullptr;
+  int32_t* seg = nullptr;  // [cap+1]
+  int32_t* u_count = nullptr;
+};
+size_t hash_dedup_temp_bytes(int64_t cap);
+void launch_dedup_hash(const HashDedupArgs& a, void* temp, size_t temp_bytes, hipStream_t s);
+
 // ---------------------------------------------------------------- slot metadata
 // Flat slot-major key layout: keys of slot s for instance b are
 // [lod[s*(B+1)+b], lod[s*(B+1)+b+1]).  Writes occ_slot / occ_ins per key.

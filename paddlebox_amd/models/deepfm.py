@@ -28,6 +28,23 @@ from ..ops.sparse import pull_seqpool_cvm_concat
 from ..ps.sparse_engine import SeqpoolParams, SparseEngine
 
 
+class _StageWs(torch.autograd.Function):
+    """Copy a [B, Cp] bf16 head output into the MLP workspace input (and its
+    transpose); gradient = the workspace's dX0 columns."""
+
+    @staticmethod
+    def forward(ctx, y, ws, Cp):
+        x0 = ws.x(0)
+        x0[:, :Cp].copy_(y)
+        ws.xt(0)[:Cp, : y.shape[0]].copy_(y.t())
+        ctx.Cp = Cp
+        return x0.view_as(x0)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[:, : ctx.Cp].contiguous(), None, None
+
+
 class DeepFM(nn.Module):
     def __init__(self, engine: SparseEngine, num_slots: int = 26, dense_dim: int = 13,
                  hidden: Sequence[int] = (400, 400, 400), use_data_norm: bool = True,
@@ -46,6 +63,7 @@ class DeepFM(nn.Module):
         self.mlp = FusedMLP(C, hidden, 1)
         self.bias = nn.Parameter(torch.zeros(1))
         self.use_workspace = True
+        self.head_into_workspace = True
         # column of embed_w inside each slot block; embedx follow it
         self.ew_col = 2 if self.sp.use_cvm and not self.sp.clk_filter else (1 if self.sp.use_cvm else 0)
 
@@ -56,7 +74,11 @@ class DeepFM(nn.Module):
             # the head writes the MLP input (and its transpose) straight into
             # the MLP workspace; the MLP streams it HBM -> LDS by DMA
             ws = self.mlp.workspace(B, x.device)
-            y, lin = ctr_head(x, self.dn, S, self.Eo, self.ew_col, self.D, self.Cp, ws.x(0), ws.xt(0))
+            if self.head_into_workspace:
+                y, lin = ctr_head(x, self.dn, S, self.Eo, self.ew_col, self.D, self.Cp, ws.x(0), ws.xt(0))
+            else:
+                y0, lin = ctr_head(x, self.dn, S, self.Eo, self.ew_col, self.D, self.Cp)
+                y = _StageWs.apply(y0, ws, self.Cp)
             deep = self.mlp.forward_ws(y)
         else:
             y, lin = ctr_head(x, self.dn, S, self.Eo, self.ew_col, self.D, self.Cp)

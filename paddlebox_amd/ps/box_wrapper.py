@@ -97,6 +97,9 @@ class BoxWrapper:
         self._pass_keys: Optional[torch.Tensor] = None
         self.max_keys = 1 << 20
         self.capacity = 1 << 22
+        self._replica = None
+        self._input_table = None
+        self._expand = None
         BoxWrapper._instance = self
 
     # ---------------------------------------------------------------- instance
@@ -200,6 +203,8 @@ class BoxWrapper:
         eng = self._require_engine()
         h = self._route(ref.mix64(keys.to(self.device if self.device.type == "cuda" else "cpu")))
         h = h.to(eng.device)
+        if self._expand is not None:
+            self._expand.engine.insert_local_mixed(h.to(self._expand.engine.device))
         if self.mode == "hbm":
             eng.insert_local_mixed(h)
             return
@@ -382,6 +387,34 @@ class BoxWrapper:
 
     def set_input_table_dim(self, dim: int):
         self.input_table_dim = dim
+        self.input_table.set_dim(dim)
+
+    # ---------------------------------------------------------------- auxiliary tables
+    @property
+    def replica_cache(self):
+        """GpuReplicaCache for pull_cache_value (created on first use)."""
+        if self._replica is None:
+            from .extras import GpuReplicaCache
+
+            self._replica = GpuReplicaCache(self.cfg.embedx_dim + 3, self.device)
+        return self._replica
+
+    @property
+    def input_table(self):
+        if self._input_table is None:
+            from .extras import InputTable
+
+            self._input_table = InputTable(self.input_table_dim)
+        return self._input_table
+
+    def pull_extended(self, keys, lod, B, S, emb_size: int, ext_size: int):
+        """pull_box_extended_sparse: (records [L, emb_size], expand [L, ext_size])."""
+        if self._expand is None:
+            from .extras import ExpandEmbedding
+
+            dim = self.cfg.expand_embed_dim or ext_size
+            self._expand = ExpandEmbedding(self._require_engine(), dim)
+        return self._expand.pull(keys, lod, B, S, emb_size, ext_size)
 
     def init_afs_api(self, fs_name: str = "", fs_user: str = "", pass_wd: str = "", conf_path: str = ""):
         from ..utils.fs import BoxFileMgr

@@ -1,0 +1,144 @@
+"""Auxiliary BoxWrapper tables.
+
+* :class:`GpuReplicaCache` -- small fully replicated per-GPU embedding table
+  addressed by a dense offset (the data feed stores offsets as feasigns);
+  ``pull_cache_value`` gathers rows.  Reference ``GpuReplicaCache``
+  (``fw/fleet/box_wrapper.h:63-122``, kernel ``box_wrapper.cu:1210-1224``).
+* :class:`InputTable` -- string key -> dense vector host table used by
+  ``lookup_input`` (``box_wrapper.h:124-197``); the data feed maps keys to
+  offsets, lookups gather on the host and copy to the device.
+* :class:`ExpandEmbedding` -- the "expand" embedding of
+  ``pull_box_extended_sparse`` (``ops/pull_box_extended_sparse_op.*``): a
+  second sparse engine keyed by the same feasigns whose embedx holds the
+  expand vector; pulled/pushed alongside the main records.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+
+class GpuReplicaCache:
+    def __init__(self, dim: int, device=None):
+        self.dim = int(dim)
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self._host: List[np.ndarray] = []
+        self._n = 0
+        self.table: Optional[torch.Tensor] = None
+
+    def add_items(self, rows) -> int:
+        """Append rows [n, dim]; returns the offset of the first one."""
+        a = np.asarray(rows, dtype=np.float32).reshape(-1, self.dim)
+        off = self._n
+        self._host.append(a)
+        self._n += a.shape[0]
+        return off
+
+    def to_hbm(self):
+        data = np.concatenate(self._host, 0) if self._host else np.zeros((0, self.dim), np.float32)
+        self.table = torch.from_numpy(data).to(self.device)
+        return self.table
+
+    def pull(self, ids: torch.Tensor, size: int) -> torch.Tensor:
+        if self.table is None:
+            self.to_hbm()
+        idx = ids.reshape(-1).to(self.table.device).long().clamp(0, max(self._n - 1, 0))
+        out = self.table.index_select(0, idx)
+        if size != self.dim:
+            out = out[:, :size] if size < self.dim else torch.nn.functional.pad(out, (0, size - self.dim))
+        return out
+
+    def __len__(self):
+        return self._n
+
+
+class InputTable:
+    def __init__(self, dim: int = 0):
+        self.dim = int(dim)
+        self.index: Dict[str, int] = {}
+        self._rows: List[np.ndarray] = []
+        self._data: Optional[np.ndarray] = None
+
+    def set_dim(self, dim: int):
+        self.dim = int(dim)
+
+    def add_index_data(self, key: str, vec) -> int:
+        v = np.asarray(vec, dtype=np.float32).reshape(-1)
+        if self.dim == 0:
+            self.dim = v.size
+        if key in self.index:
+            return self.index[key]
+        off = len(self._rows)
+        self.index[key] = off
+        self._rows.append(v[: self.dim])
+        self._data = None
+        return off
+
+    def get_offset(self, key: str) -> int:
+        return self.index.get(key, -1)
+
+    def lookup(self, ids: torch.Tensor, size: int, device) -> torch.Tensor:
+        if self._data is None:
+            self._data = np.stack(self._rows, 0) if self._rows else np.zeros((0, self.dim), np.float32)
+        idx = ids.reshape(-1).cpu().numpy().astype(np.int64)
+        out = np.zeros((idx.size, size), np.float32)
+        ok = (idx >= 0) & (idx < self._data.shape[0])
+        w = min(size, self.dim)
+        out[ok, :w] = self._data[idx[ok], :w]
+        return torch.from_numpy(out).to(device)
+
+    def size(self) -> int:
+        return len(self._rows)
+
+
+class _PullExtended(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, keys, lod, main, ext, B, S, emb_size, ext_size, bs_scale):
+        recs, st = main.pull_records(keys, lod, B, S)
+        erecs, est = ext.pull_records(keys, lod, B, S)
+        ctx.main, ctx.ext, ctx.st, ctx.est, ctx.bs = main, ext, st, est, bs_scale
+        ctx.emb_size, ctx.ext_size, ctx.E = emb_size, ext_size, recs.shape[1]
+        out = recs[:, :emb_size] if emb_size <= recs.shape[1] else torch.nn.functional.pad(
+            recs, (0, emb_size - recs.shape[1]))
+        ex = erecs[:, 3:3 + ext_size]
+        return out.contiguous(), ex.contiguous()
+
+    @staticmethod
+    def backward(ctx, g, gex):
+        E = ctx.E
+        gm = torch.zeros(g.shape[0], E, device=g.device, dtype=torch.float32)
+        w = min(E, g.shape[1])
+        gm[:, :w] = g[:, :w].float()
+        ctx.main.push_records(ctx.st, gm, 2, ctx.bs)
+        if gex is not None:
+            ge = torch.zeros(gex.shape[0], 3 + ctx.ext.dim, device=gex.device, dtype=torch.float32)
+            ge[:, :2] = gm[:, :2]  # same show/click statistics drive the expand rows
+            ge[:, 3:3 + gex.shape[1]] = gex.float()
+            ctx.ext.push_records(ctx.est, ge, 2, ctx.bs)
+        return (None,) * 10
+
+
+class ExpandEmbedding:
+    """Expand-embedding companion engine (same keys, embedx = expand vector)."""
+
+    def __init__(self, main_engine, expand_dim: int):
+        from .config import PSConfig
+        from .sparse_engine import SparseEngine
+
+        cfg = PSConfig(embedx_dim=int(expand_dim))
+        cfg.sgd = main_engine.cfg.sgd
+        self.engine = SparseEngine(cfg, main_engine.max_keys, main_engine.device,
+                                   capacity=getattr(main_engine.table, "capacity", 1 << 20),
+                                   group=main_engine.group, auto_insert=True, comm=main_engine.comm)
+        self.main = main_engine
+
+    def register_keys(self, keys: torch.Tensor):
+        self.engine.register_keys(keys)
+
+    def pull(self, keys, lod, B, S, emb_size, ext_size) -> Tuple[torch.Tensor, torch.Tensor]:
+        from ..ops.sparse import _anchor
+
+        return _PullExtended.apply(_anchor(keys.device), keys, lod, self.main, self.engine, B, S, emb_size,
+                                   ext_size, float(B))

@@ -108,14 +108,17 @@ class SparseEngine:
             self._hip = _native.hip()
             self._sgd_native = cfg.sgd.to_native(self._hip)
             with torch.cuda.device(self.device):
-                self.ws = self._hip.DedupWorkspace(self.max_keys, self.device.index or 0)
+                # sender-side dedup must emit the unique keys grouped by owner
+                # shard (sorted h) for the key all-to-all; a single shard and
+                # the owner side take the sort-free hash dedup
+                self.ws = self._hip.DedupWorkspace(self.max_keys, self.device.index or 0, self.world == 1)
             self.occ_slot = torch.empty(self.max_keys, dtype=torch.int32, device=self.device)
             self.occ_ins = torch.empty(self.max_keys, dtype=torch.int32, device=self.device)
             if self.world > 1:
                 self.C = int(math.ceil(self.max_keys / self.world * cap_factor)) + 64
                 n = self.world * self.C
                 with torch.cuda.device(self.device):
-                    self.ws_r = self._hip.DedupWorkspace(n, self.device.index or 0)
+                    self.ws_r = self._hip.DedupWorkspace(n, self.device.index or 0, True)
                 self.send = torch.empty(n, dtype=torch.int64, device=self.device)
                 self.recv = torch.empty(n, dtype=torch.int64, device=self.device)
                 self.send_index = torch.empty(self.max_keys, dtype=torch.int64, device=self.device)

@@ -51,23 +51,67 @@ def test_sparse_and_data_norm_updated_through_backward():
     assert float(model.dn.batch_size[0]) != 1e4
 
 
-def test_graph_replay_matches_eager():
-    # eager reference
+@pytest.mark.parametrize("use_ws", [False, True])
+def test_graph_replay_matches_eager(use_ws):
+    # eager reference, run to completion first (interleaving eager steps of a
+    # second model with graph replays is covered by test_two_models_eager)
     eng_e, model_e, arena_e, opt_e, batches = _setup()
+    model_e.use_workspace = use_ws
     step_e = _step_fn(model_e, arena_e, opt_e)
-    # graphed run from identical initial state
-    eng_g, model_g, arena_g, opt_g, _ = _setup()
-    step_g = _step_fn(model_g, arena_g, opt_g)
-    # GraphedTrainStep warms up 3 eager steps on batch 0: mirror that
     for _ in range(3):
         step_e(batches[0])
-    g = GraphedTrainStep(step_g, batches[0], DEV, warmup=3)
     for i in range(1, 6):
         step_e(batches[i])
+    torch.cuda.synchronize()
+    flat_e = arena_e.flat.clone()
+    h, ve = eng_e.table.export(True)
+    # graphed run from identical initial state
+    eng_g, model_g, arena_g, opt_g, _ = _setup()
+    model_g.use_workspace = use_ws
+    step_g = _step_fn(model_g, arena_g, opt_g)
+    g = GraphedTrainStep(step_g, batches[0], DEV, warmup=3)
+    for i in range(1, 6):
         g.load(i % 2, batches[i])
         g.run(i % 2)
     torch.cuda.synchronize()
-    torch.testing.assert_close(arena_g.flat, arena_e.flat, rtol=1e-3, atol=1e-4)
-    h, ve = eng_e.table.export(True)
+    torch.testing.assert_close(arena_g.flat, flat_e, rtol=1e-3, atol=1e-4)
     vg = eng_g.table.read(h)
     torch.testing.assert_close(vg[:, :13], ve[:, :13], rtol=1e-3, atol=1e-4)
+
+
+def test_mlp_workspace_graph_replay():
+    """The MLP workspace path captured in a HIP graph replays like eager."""
+    from paddlebox_amd.ops.mlp import FusedMLP
+
+    torch.manual_seed(0)
+    M, dims = 256, [304, 32, 16]
+    mlp = FusedMLP(dims[0], dims[1:], 1).to(DEV)
+    mlp.ensure_grads()
+    ws = mlp.workspace(M, DEV)
+    x = torch.randn(M, dims[0], device=DEV).to(torch.bfloat16)
+    ws.x(0)[:, :dims[0]] = x
+    ws.xt(0)[:dims[0], :M] = x.t()
+    dl = torch.randn(M, device=DEV)
+
+    def step():
+        for p in mlp.parameters():
+            p.grad.zero_()
+        lg = mlp.forward_ws(ws.x(0).requires_grad_(False))
+        out = ws.backward(dl, [w.grad for w in mlp.w], [b.grad for b in mlp.b], mlp.w_out.view(-1),
+                          mlp.w_out.grad.view(-1), mlp.b_out.grad, True)
+        return lg
+
+    step()
+    ref = [p.grad.clone() for p in mlp.parameters()]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    g.replay()
+    torch.cuda.synchronize()
+    for p, r in zip(mlp.parameters(), ref):
+        torch.testing.assert_close(p.grad, r, rtol=1e-4, atol=1e-4)

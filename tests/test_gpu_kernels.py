@@ -31,12 +31,16 @@ def test_mix64_matches_reference():
     assert [ (x & ((1 << 64) - 1)) for x in t[:10].tolist()] == [ref.mix64_int(k) for k in keys[:10].tolist()]
 
 
-def test_dedup_matches_unique():
+@pytest.mark.parametrize("hash_mode", [True, False])
+def test_dedup_matches_unique(hash_mode):
     torch.manual_seed(0)
     n = 50000
+    ws = hip().DedupWorkspace(n, 0, hash_mode)
+    # a first, different batch: the hash table must be cleaned between runs
+    ws.run(torch.randint(0, 10**9, (n // 2,), dtype=torch.int64, device=DEV), False)
     keys = torch.randint(0, 3000, (n,), dtype=torch.int64, device=DEV)
+    keys[:2000] = 7  # one Zipf-hot key
     keys[-100:] = -1  # padding
-    ws = hip().DedupWorkspace(n, 0)
     ws.run(keys, False)
     U = int(ws.u_count[0])
     nvalid = int(ws.u_count[1])
