@@ -55,20 +55,28 @@ def main():
     ap.add_argument("--batch-per-gpu", type=int, default=8192)
     ap.add_argument("--total-features", type=float, default=1e9)
     ap.add_argument("--alpha", type=float, default=1.05)
-    ap.add_argument("--num-batches", type=int, default=16, help="distinct synthetic batches cycled")
+    ap.add_argument("--num-batches", type=int, default=128,
+                    help="distinct synthetic batches cycled (enough that the model does not memorise them)")
     ap.add_argument("--no-prefill", action="store_true")
     ap.add_argument("--hidden", type=str, default="400,400,400")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
                     help="capture the train step into HIP graphs (default)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
+    ap.add_argument("--diag-windows", type=int, default=0,
+                    help="after the measurement, time this many more K-step windows (stderr only)")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="run the multi-GPU exchange/all-reduce path even on 1 rank (rehearsal)")
     args = ap.parse_args()
+    if args.force_collectives:
+        os.environ["PBX_FORCE_COLLECTIVES"] = "1"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    if world > 1:
+    multi = world > 1 or args.force_collectives
+    if multi:
         dist.init_process_group("nccl", device_id=device)
 
     B = args.batch_per_gpu
@@ -94,22 +102,31 @@ def main():
 
     hidden = tuple(int(x) for x in args.hidden.split(","))
     model = DeepFM(engine, num_slots=S, dense_dim=13, hidden=hidden).to(device)
-    if world > 1:
+    if multi:
         model.dn.group = dist.group.WORLD
         model.dn.sync_stats = True
     arena = DenseArena(model.parameters(), device)
-    opt = FlatAdam(arena, lr=1e-3)
+    opt = FlatAdam(arena, lr=1e-3, clear_grad=True)  # grads zeroed by the update kernel
     sync = DenseSync(arena, mode="grad_allreduce")
 
     # "load into memory": the pass's batches live in pinned host memory;
     # every step copies its batch H2D on a side stream (overlapped).
-    host_batches = [synth.batch(B).to("cpu").pin_memory() for _ in range(args.num_batches)]
+    from paddlebox_amd.runtime.graph_step import pack_batch
+
+    # each batch is one pinned byte buffer (one H2D DMA per step), and every
+    # buffer is streamed to the device once up front so the timed steps do not
+    # pay the driver's first-touch cost of a pinned range
+    host_batches = [pack_batch(synth.batch(B).to("cpu"), pin=True) for _ in range(args.num_batches)]
+    scratch = torch.empty_like(host_batches[0]._flat, device=device)
+    for hb in host_batches:
+        scratch.copy_(hb._flat, non_blocking=True)
+    torch.cuda.synchronize()
+    del scratch
     copy_stream = torch.cuda.Stream(device)
     auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
     auc_stats = torch.zeros(5, dtype=torch.float64, device=device)
 
     def train_step(b):
-        arena.zero_grad()
         loss, pred = model(b)
         loss.backward()
         sync.before_step()
@@ -156,22 +173,32 @@ def main():
     for i in range(args.warmup):
         run(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     loss = None
     for i in range(args.steps):
         loss = run(args.warmup + i)
+    t_enq = time.perf_counter() - t_start
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t_start
-    if world > 1:
+    if multi:
         t = torch.tensor([dt], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    log(rank, f"[bench] host enqueue {t_enq / args.steps * 1e3:.4f} ms/step, wall {dt / args.steps * 1e3:.4f} ms/step")
+    # diagnostics only (after the measurement): further windows of K steps
+    for w in range(args.diag_windows):
+        torch.cuda.synchronize()
+        t0w = time.perf_counter()
+        for i in range(args.steps):
+            run(args.warmup + args.steps * (w + 1) + i)
+        torch.cuda.synchronize()
+        log(rank, f"[bench] diag window {w}: {(time.perf_counter() - t0w) / args.steps * 1e3:.4f} ms/step")
     overflow = engine.check_overflow()
     samples = B * world * args.steps
     value = samples / dt
@@ -203,8 +230,15 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if multi:
+        # the captured graphs hold RCCL work: tearing the communicator down
+        # under them can block, so leave the process without it once every
+        # rank is done (output is flushed above)
+        dist.barrier()
+        torch.cuda.synchronize()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

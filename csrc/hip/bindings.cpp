@@ -136,6 +136,27 @@ class GpuTable {
     launch_push_adagrad(view(), ptr<int64_t>(rows), ptr<float>(push), (int)push.size(1), optr<int32_t>(n_dev),
                         rows.numel(), cfg, seed, cur_stream());
   }
+  // owner side of the sharded pull: out[j] = pull head of rows[uid[j]]
+  void gather_rows_by_uid(const Tensor& rows, const Tensor& uid, Tensor out) {
+    check_cuda(rows, "rows");
+    check_cuda(uid, "uid");
+    check_cuda(out, "out");
+    PBX_CHECK(out.dim() == 2 && out.size(0) == uid.numel(), "gather_rows_by_uid: out rows");
+    PBX_CHECK(out.size(1) % 4 == 0 && out.size(1) <= stride_, "gather_rows_by_uid: out stride");
+    launch_gather_rows_by_uid(view(), ptr<int64_t>(rows), ptr<int32_t>(uid), uid.numel(), ptr<float>(out),
+                              (int)out.size(1), cur_stream());
+  }
+  // owner side of the sharded push: merge each unique's received records and
+  // apply Adagrad in one pass; false if not vectorisable for this dim
+  bool push_adagrad_seg(const Tensor& rows, const Tensor& rec, const Tensor& perm, const Tensor& seg,
+                        const Tensor& cnt, const Tensor& n_dev, const SparseSGDConfig& cfg, uint64_t seed) {
+    check_cuda(rows, "rows");
+    check_cuda(rec, "rec");
+    PBX_CHECK(rec.dim() == 2 && rec.size(1) >= push_width(dim_), "push record width");
+    return launch_push_adagrad_seg(view(), ptr<int64_t>(rows), ptr<float>(rec), (int)rec.size(1),
+                                   ptr<int32_t>(perm), ptr<int32_t>(seg), ptr<int32_t>(cnt), ptr<int32_t>(n_dev),
+                                   rows.numel(), cfg, seed, cur_stream());
+  }
   void clear() {
     keys_.fill_(-1);
     fill_.zero_();
@@ -191,7 +212,7 @@ struct DedupWorkspace {
     uid = torch::empty({cap}, o4);
     uniq_h = torch::empty({cap}, o8);
     seg = torch::empty({cap + 1}, o4);
-    u_count = torch::zeros({3}, o4);  // [U, n_valid, U of the previous hash run]
+    u_count = torch::zeros({4}, o4);  // [U, n_valid, U of the previous hash run, segment cursor]
     temp_bytes = hash ? hash_dedup_temp_bytes(cap) : dedup_temp_bytes(cap);
     temp = torch::empty({(int64_t)temp_bytes}, torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, device));
   }
@@ -232,7 +253,8 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
                             const Tensor& lod, int S, int B, int E, Tensor out, int col_offset, bool use_cvm,
                             int cvm_offset, bool clk_filter, float pad_value, bool need_filter, float show_coeff,
                             float clk_coeff, float threshold, int quant_ratio, bool embed_threshold_filter,
-                            float embed_threshold, int embed_thres_size) {
+                            float embed_threshold, int embed_thres_size, const c10::optional<Tensor>& dense,
+                            int dense_col) {
   check_cuda(src, "src");
   check_cuda(uid, "uid");
   check_cuda(lod, "lod");
@@ -264,6 +286,15 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
   a.embed_threshold = embed_threshold;
   a.embed_thres_size = embed_thres_size;
   PBX_CHECK(col_offset + (int64_t)S * seqpool_cvm_out_width(a) <= out.size(1), "out too narrow");
+  if (dense.has_value() && dense->defined()) {
+    check_cuda(*dense, "dense");
+    PBX_CHECK(dense->dim() == 2 && dense->size(0) == B && dense->scalar_type() == torch::kFloat32,
+              "dense must be f32 [B, Dd]");
+    PBX_CHECK(S > 0 && dense_col >= 0 && dense_col + dense->size(1) <= out.size(1), "dense columns out of range");
+    a.dense = ptr<float>(*dense);
+    a.dense_dim = (int)dense->size(1);
+    a.dense_col = dense_col;
+  }
   launch_seqpool_cvm_fwd(a, cur_stream());
 }
 
@@ -317,6 +348,19 @@ static void shard_pack(const Tensor& uniq_h, const Tensor& u_count, int nranks, 
   PBX_CHECK(send.numel() == nranks * cap, "send shape");
   launch_shard_pack(ptr<uint64_t>(uniq_h), ptr<int32_t>(u_count), send_index.numel(), nranks, cap,
                     ptr<uint64_t>(send), ptr<int64_t>(send_index), ptr<int32_t>(overflow), cur_stream());
+}
+
+static void shard_pack_hash(const Tensor& uniq_h, const Tensor& u_count, int nranks, int64_t cap, Tensor send,
+                            Tensor send_index, Tensor ocnt, Tensor overflow) {
+  check_cuda(uniq_h, "uniq_h");
+  check_cuda(send, "send");
+  PBX_CHECK(send.numel() == nranks * cap, "send shape");
+  PBX_CHECK(nranks >= 1 && nranks <= 64, "shard_pack_hash: 1..64 ranks");
+  PBX_CHECK(ocnt.numel() >= nranks && ocnt.scalar_type() == torch::kInt32, "ocnt");
+  PBX_CHECK(send_index.numel() >= uniq_h.numel(), "send_index too short");
+  launch_shard_pack_hash(ptr<uint64_t>(uniq_h), ptr<int32_t>(u_count), uniq_h.numel(), nranks, cap,
+                         ptr<uint64_t>(send), ptr<int64_t>(send_index), ptr<int32_t>(ocnt), ptr<int32_t>(overflow),
+                         cur_stream());
 }
 
 static void gather_by_uid(const Tensor& src, const Tensor& uid, Tensor out, int width) {
@@ -683,6 +727,24 @@ static std::vector<Tensor> sigmoid_logloss(const Tensor& logit, const Tensor& la
   return {pred, loss, dz};
 }
 
+static std::vector<Tensor> logit_loss(const Tensor& a, const c10::optional<Tensor>& b, const Tensor& label) {
+  check_cuda(a, "a");
+  check_cuda(label, "label");
+  const int B = (int)a.numel();
+  PBX_CHECK(label.numel() == B && a.scalar_type() == torch::kFloat32 && label.scalar_type() == torch::kFloat32,
+            "logit_loss: a/label must be f32 [B]");
+  if (b.has_value() && b->defined()) {
+    check_cuda(*b, "b");
+    PBX_CHECK(b->numel() == B && b->scalar_type() == torch::kFloat32, "logit_loss: b must be f32 [B]");
+  }
+  auto pred = torch::empty({B}, a.options());
+  auto dz = torch::empty({B}, a.options());
+  auto loss = torch::empty({1}, a.options());
+  launch_logit_loss(ptr<float>(a), optr<float>(b), ptr<float>(label), B, ptr<float>(pred), ptr<float>(dz),
+                    ptr<float>(loss), cur_stream());
+  return {loss, pred, dz};
+}
+
 static void auc_accumulate(const Tensor& pred, const Tensor& label, const c10::optional<Tensor>& mask, Tensor table,
                            Tensor stats) {
   check_cuda(pred, "pred");
@@ -692,13 +754,13 @@ static void auc_accumulate(const Tensor& pred, const Tensor& label, const c10::o
                         (int)(table.numel() / 2), ptr<double>(table), ptr<double>(stats), cur_stream());
 }
 
-static void adam_flat(Tensor p, const Tensor& g, Tensor m, Tensor v, Tensor pows, float lr, float b1, float b2,
-                      float eps, float grad_scale, float wd) {
+static void adam_flat(Tensor p, Tensor g, Tensor m, Tensor v, Tensor pows, float lr, float b1, float b2,
+                      float eps, float grad_scale, float wd, bool clear_grad) {
   check_cuda(p, "p");
   PBX_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam sizes");
   PBX_CHECK(pows.is_cuda() && pows.numel() >= 2 && pows.scalar_type() == torch::kFloat32, "adam pows");
   launch_adam_flat(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), lr, b1, b2, eps,
-                   ptr<float>(pows), grad_scale, wd, cur_stream());
+                   ptr<float>(pows), grad_scale, wd, clear_grad, cur_stream());
 }
 
 }  // namespace pbx
@@ -745,6 +807,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("shrink", &GpuTable::shrink)
       .def("gather_pull", &GpuTable::gather_pull, py::arg("rows"), py::arg("n_dev"), py::arg("out_stride"))
       .def("push_adagrad", &GpuTable::push_adagrad)
+      .def("gather_rows_by_uid", &GpuTable::gather_rows_by_uid)
+      .def("push_adagrad_seg", &GpuTable::push_adagrad_seg)
       .def("clear", &GpuTable::clear)
       .def_property_readonly("keys", &GpuTable::keys)
       .def_property_readonly("values", &GpuTable::values)
@@ -763,6 +827,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("uid", &DedupWorkspace::uid)
       .def_readonly("uniq_h", &DedupWorkspace::uniq_h)
       .def_readonly("seg", &DedupWorkspace::seg)
+      .def_readonly("cnt", &DedupWorkspace::cnt)
       .def_readonly("u_count", &DedupWorkspace::u_count);
   py::class_<MlpWorkspace>(m, "MlpWorkspace")
       .def(py::init<int64_t, std::vector<int64_t>, int, int64_t>(), py::arg("M"), py::arg("dims"),
@@ -775,10 +840,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("dx0", &MlpWorkspace::dx0)
       .def_property_readonly("M", &MlpWorkspace::M);
   m.def("fill_occurrence", &fill_occurrence);
-  m.def("seqpool_cvm_fwd", &seqpool_cvm_fwd);
+  m.def("seqpool_cvm_fwd", &seqpool_cvm_fwd, py::arg("src"), py::arg("src_index"), py::arg("uid"), py::arg("lod"),
+        py::arg("S"), py::arg("B"), py::arg("E"), py::arg("out"), py::arg("col_offset"), py::arg("use_cvm"),
+        py::arg("cvm_offset"), py::arg("clk_filter"), py::arg("pad_value"), py::arg("need_filter"),
+        py::arg("show_coeff"), py::arg("clk_coeff"), py::arg("threshold"), py::arg("quant_ratio"),
+        py::arg("embed_threshold_filter"), py::arg("embed_threshold"), py::arg("embed_thres_size"),
+        py::arg("dense") = py::none(), py::arg("dense_col") = 0);
   m.def("push_merge", &push_merge);
   m.def("push_merge_records", &push_merge_records);
   m.def("shard_pack", &shard_pack);
+  m.def("shard_pack_hash", &shard_pack_hash);
   m.def("gather_by_uid", &gather_by_uid);
   m.def("data_norm_fwd", &data_norm_fwd);
   m.def("data_norm_bwd", &data_norm_bwd);
@@ -794,7 +865,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fm_bwd", &fm_bwd);
   m.def("sigmoid_logloss", &sigmoid_logloss);
   m.def("auc_accumulate", &auc_accumulate);
-  m.def("adam_flat", &adam_flat);
+  m.def("logit_loss", &logit_loss, py::arg("a"), py::arg("b"), py::arg("label"));
+  m.def("adam_flat", &adam_flat, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pows"),
+        py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("grad_scale"), py::arg("wd"),
+        py::arg("clear_grad") = false);
   m.def("mix64", [](uint64_t k) { return mix64(k); });
   m.def("unmix64", [](uint64_t k) { return unmix64(k); });
 }

@@ -70,31 +70,41 @@ __global__ void k_emit(const uint64_t* __restrict__ hs, const int32_t* __restric
 
 
 // ---------------------------------------------------------------- hash dedup
-// Sort-free variant (single-shard engine and the owner side of the key
-// all-to-all, where the unique list needs no particular order):
-//   insert   : open-addressing insert of h into a scratch table (64-bit CAS,
-//              linear probing); the inserting lane takes the next unique id
-//              (one atomic per wave: ballot + mbcnt) and records uniq_h / slot
+// Sort-free variant (no consumer needs the unique list in any order: the
+// single-shard engine, the sender before the owner pack, and the owner side
+// of the key all-to-all):
+//   insert   : block-local pre-dedup in an LDS hash, then one open-addressing
+//              insert per distinct key into a scratch table (read before CAS);
+//              the block's winners take their unique ids with ONE global
+//              atomic (a single counter word saturates near 90 returning
+//              atomics/us, so per-wave allocation was the bottleneck)
 //   rank     : per block, occurrences are counted per unique id in an LDS
 //              hash (LDS atomics), then ONE global atomicAdd per distinct id per
 //              block returns the block's base -> rank of every occurrence
-//              within its id (Zipf-hot ids see <= #blocks global atomics)
-//   scan     : exclusive sum of the per-id counts -> seg
+//              within its id (Zipf-hot ids see <= #blocks global atomics);
+//              cnt[u] ends as the occurrence count of u
+//   seg      : block exclusive scan of cnt + one atomic per block on a cursor:
+//              seg[u] = start of u's run in perm.  Runs are contiguous but not
+//              in id order (nobody needs that), which replaces a device-wide
+//              scan (two launches) with one short kernel
 //   scatter  : perm[seg[u] + rank] = occurrence
 // The table is cleaned lazily at the start of the next run (only the U
 // slots that were used), so no per-batch memset of the table.
+// u_count = [U, n_valid, U of the previous run, segment cursor]
 constexpr int kRankItems = 4;      // occurrences per thread in k_hash_rank
 constexpr int kRankLds = 2048;     // LDS hash entries per block (load <= 0.5)
+constexpr int kSegItems = 4;       // unique ids per thread in k_seg_alloc
 
 __global__ void k_hash_cleanup(int32_t* __restrict__ u_count, const int32_t* __restrict__ slot_of_u,
                                uint64_t* __restrict__ tk, int32_t* __restrict__ tu, int32_t* __restrict__ cnt,
                                int64_t cap) {
-  // u_count = [U, n_valid, U of the previous run]; the previous run's
-  // scatter kernel saved its U into [2], so [0..1] can be reset here
+  // the previous run's scatter kernel saved its U into [2], so [0], [1] and
+  // the cursor [3] can be reset here
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u == 0) {
     u_count[0] = 0;
     u_count[1] = 0;
+    u_count[3] = 0;
   }
   if (u >= cap || u >= u_count[2]) return;
   const int32_t p = slot_of_u[u];
@@ -106,8 +116,8 @@ __global__ void k_hash_cleanup(int32_t* __restrict__ u_count, const int32_t* __r
 // Block-level pre-dedup in LDS (64-bit CAS) so a Zipf-hot key costs at most
 // one global table operation per block, and a read-before-CAS so keys that
 // are already present take no atomic at all.
-constexpr int kInsItems = 4;
-constexpr int kInsLds = 2048;
+constexpr int kInsItems = 2;
+constexpr int kInsLds = 1024;
 __global__ __launch_bounds__(256) void k_hash_insert(const uint64_t* __restrict__ keys, int64_t n, int mixed,
                                                      uint64_t* __restrict__ tk, int32_t* __restrict__ tu,
                                                      uint64_t tmask, int32_t* __restrict__ slot,
@@ -115,12 +125,14 @@ __global__ __launch_bounds__(256) void k_hash_insert(const uint64_t* __restrict_
                                                      int32_t* __restrict__ u_count) {
   __shared__ unsigned long long lk[kInsLds];
   __shared__ int32_t lslot[kInsLds];
-  __shared__ int32_t nvalid_blk;
+  __shared__ int32_t nvalid_blk, nwon_blk, base_blk;
   for (int e = threadIdx.x; e < kInsLds; e += blockDim.x) lk[e] = (unsigned long long)kEmptyKey;
-  if (threadIdx.x == 0) nvalid_blk = 0;
+  if (threadIdx.x == 0) {
+    nvalid_blk = 0;
+    nwon_blk = 0;
+  }
   __syncthreads();
   const int64_t i0 = (int64_t)blockIdx.x * (blockDim.x * kInsItems);
-  const int lane = threadIdx.x & 63;
   int pos[kInsItems];
   bool own[kInsItems];
   uint64_t hv[kInsItems];
@@ -173,28 +185,31 @@ __global__ __launch_bounds__(256) void k_hash_insert(const uint64_t* __restrict_
     gp[t] = p;
     lslot[pos[t]] = (int32_t)p;
   }
-  // new ids: one counter atomic per wave per item round
+  // new ids: block-local ranks (LDS atomics), one global atomic per block
+  int lid[kInsItems];
 #pragma unroll
-  for (int t = 0; t < kInsItems; ++t) {
-    const unsigned long long wm = __ballot(won[t]);
-    int base = 0;
-    if (lane == 0 && wm) base = atomicAdd(&u_count[0], __popcll(wm));
-    base = __shfl(base, 0);
-    if (won[t]) {
-      const int u = base + __popcll(wm & ((1ull << lane) - 1ull));
-      tu[gp[t]] = u;
-      uniq_h[u] = hv[t];
-      slot_of_u[u] = (int32_t)gp[t];
-    }
+  for (int t = 0; t < kInsItems; ++t) lid[t] = won[t] ? atomicAdd(&nwon_blk, 1) : -1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    base_blk = nwon_blk ? atomicAdd(&u_count[0], nwon_blk) : 0;
+    if (nvalid_blk) atomicAdd(&u_count[1], nvalid_blk);
   }
   __syncthreads();
-  // 3) every occurrence takes its key's global slot
+#pragma unroll
+  for (int t = 0; t < kInsItems; ++t) {
+    if (!won[t]) continue;
+    const int u = base_blk + lid[t];
+    tu[gp[t]] = u;
+    uniq_h[u] = hv[t];
+    slot_of_u[u] = (int32_t)gp[t];
+  }
+  // 3) every occurrence takes its key's global slot (lslot is complete
+  // after the barriers above)
 #pragma unroll
   for (int t = 0; t < kInsItems; ++t) {
     const int64_t i = i0 + t * blockDim.x + threadIdx.x;
     if (pos[t] >= 0) slot[i] = lslot[pos[t]];
   }
-  if (threadIdx.x == 0 && nvalid_blk) atomicAdd(&u_count[1], nvalid_blk);
 }
 
 __global__ __launch_bounds__(256) void k_hash_rank(const int32_t* __restrict__ slot, const int32_t* __restrict__ tu,
@@ -240,6 +255,40 @@ __global__ __launch_bounds__(256) void k_hash_rank(const int32_t* __restrict__ s
   }
 }
 
+__global__ __launch_bounds__(256) void k_seg_alloc(const int32_t* __restrict__ cnt, int32_t* __restrict__ u_count,
+                                                   int32_t* __restrict__ seg) {
+  __shared__ int32_t wsum[4];
+  __shared__ int32_t base;
+  const int64_t U = u_count[0];
+  const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x * kSegItems) + (int64_t)threadIdx.x * kSegItems;
+  if ((int64_t)blockIdx.x * (blockDim.x * kSegItems) >= U) return;  // block-uniform
+  int c[kSegItems];
+  int tot = 0;
+#pragma unroll
+  for (int t = 0; t < kSegItems; ++t) {
+    c[t] = (u0 + t < U) ? cnt[u0 + t] : 0;
+    tot += c[t];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = tot;  // inclusive wave scan of the per-thread totals
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) base = atomicAdd(&u_count[3], wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+  __syncthreads();
+  int p = base + x - tot;
+  for (int i = 0; i < w; ++i) p += wsum[i];
+#pragma unroll
+  for (int t = 0; t < kSegItems; ++t) {
+    if (u0 + t < U) seg[u0 + t] = p;
+    p += c[t];
+  }
+}
+
 __global__ void k_hash_scatter(const int32_t* __restrict__ uid, const int32_t* __restrict__ rank,
                                const int32_t* __restrict__ seg, int64_t n, int32_t* __restrict__ perm,
                                int32_t* __restrict__ u_count) {
@@ -281,9 +330,8 @@ void launch_dedup(const uint64_t* keys, int64_t n, bool keys_are_mixed, uint64_t
 }
 
 size_t hash_dedup_temp_bytes(int64_t cap) {
-  size_t b = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr, (int)(cap + 1));
-  return b + 256;
+  (void)cap;
+  return 256;
 }
 
 void launch_dedup_hash(const HashDedupArgs& a, void* temp, size_t temp_bytes, hipStream_t s) {
@@ -301,9 +349,10 @@ void launch_dedup_hash(const HashDedupArgs& a, void* temp, size_t temp_bytes, hi
                      a.slot_of_u, a.uniq_h, a.u_count);
   const unsigned gr = (unsigned)((a.n + 256 * kRankItems - 1) / (256 * kRankItems));
   hipLaunchKernelGGL(k_hash_rank, dim3(gr), dim3(256), 0, s, a.slot, a.tu, a.n, a.uid, a.cnt, a.rank);
-  size_t tb = temp_bytes;
-  // cnt[u] == 0 for u >= U, so seg[U] (and every later entry) = number of valid occurrences
-  (void)hipcub::DeviceScan::ExclusiveSum(temp, tb, a.cnt, a.seg, (int)(cap + 1), s);
+  (void)temp;
+  (void)temp_bytes;
+  const unsigned gs = (unsigned)((a.n + 256 * kSegItems - 1) / (256 * kSegItems));  // U <= n
+  hipLaunchKernelGGL(k_seg_alloc, dim3(gs), dim3(256), 0, s, a.cnt, a.u_count, a.seg);
   hipLaunchKernelGGL(k_hash_scatter, dim3(g), dim3(256), 0, s, a.uid, a.rank, a.seg, a.n, a.perm, a.u_count);
 }
 

@@ -146,24 +146,74 @@ __global__ void k_sigmoid_logloss(const float* __restrict__ z, const float* __re
   if ((threadIdx.x & 63) == 0 && loss_sum) atomicAdd(loss_sum, l);
 }
 
+// logit = a + b (deep + wide/FM parts), sigmoid, log-loss mean and its
+// gradient in ONE launch (replaces the add, loss zero-fill, loss kernel,
+// scale and bias-grad reduction kernels).  One 1024-thread block: the loss
+// mean is a plain store, no zero-initialised accumulator.
+__global__ __launch_bounds__(1024) void k_logit_loss(const float* __restrict__ a, const float* __restrict__ b,
+                                                     const float* __restrict__ y, int B, float* __restrict__ pred,
+                                                     float* __restrict__ dz, float* __restrict__ loss_mean) {
+  __shared__ float red[16];
+  const float inv = 1.f / (float)B;
+  float l = 0.f;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    const float zi = a[i] + (b ? b[i] : 0.f), yi = y[i];
+    const float p = 1.f / (1.f + expf(-zi));
+    pred[i] = p;
+    l += fmaxf(zi, 0.f) - zi * yi + log1pf(expf(-fabsf(zi)));
+    dz[i] = (p - yi) * inv;
+  }
+  for (int off = 32; off > 0; off >>= 1) l += __shfl_down(l, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+    loss_mean[0] = s * inv;
+  }
+}
+
 // ---------------------------------------------------------------- AUC
-__global__ void k_auc(const float* __restrict__ pred, const float* __restrict__ label,
-                      const float* __restrict__ mask, int B, int T, double* __restrict__ table,
-                      double* __restrict__ stats) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// Predictions of a converged CTR model pile up in a few buckets, so each
+// block first counts its kAucItems*256 samples per bucket in an LDS hash
+// (integer LDS atomics) and then issues one fp64 global atomic per distinct
+// bucket; the five error sums are block-reduced to one atomic each.
+constexpr int kAucItems = 4;
+constexpr int kAucLds = 2048;
+__global__ __launch_bounds__(256) void k_auc(const float* __restrict__ pred, const float* __restrict__ label,
+                                             const float* __restrict__ mask, int B, int T,
+                                             double* __restrict__ table, double* __restrict__ stats) {
+  __shared__ int32_t hk[kAucLds];
+  __shared__ int32_t hc[kAucLds];
+  __shared__ double red[5][4];
+  for (int e = threadIdx.x; e < kAucLds; e += blockDim.x) {
+    hk[e] = -1;
+    hc[e] = 0;
+  }
+  __syncthreads();
   double ae = 0, se = 0, ps = 0, ls = 0, cnt = 0;
-  if (i < B && (!mask || mask[i] != 0.f)) {
+#pragma unroll
+  for (int t = 0; t < kAucItems; ++t) {
+    const int i = (blockIdx.x * kAucItems + t) * blockDim.x + threadIdx.x;
+    if (i >= B || (mask && mask[i] == 0.f)) continue;
     const float p = pred[i];
     const int lab = label[i] > 0.5f ? 1 : 0;
     int pos = (int)(p * T);
     pos = pos < 0 ? 0 : (pos > T - 1 ? T - 1 : pos);
-    atomicAdd(&table[(int64_t)lab * T + pos], 1.0);
+    const int key = lab * T + pos;
+    unsigned e = ((unsigned)key * 2654435761u) >> 21;  // 11 bits
+    for (;;) {
+      const int old = atomicCAS(&hk[e], -1, key);
+      if (old == -1 || old == key) break;
+      e = (e + 1) & (kAucLds - 1);
+    }
+    atomicAdd(&hc[e], 1);
     const double d = (double)p - (double)lab;
-    ae = fabs(d);
-    se = d * d;
-    ps = p;
-    ls = lab;
-    cnt = 1;
+    ae += fabs(d);
+    se += d * d;
+    ps += p;
+    ls += lab;
+    cnt += 1;
   }
   for (int off = 32; off > 0; off >>= 1) {
     ae += __shfl_down(ae, off);
@@ -172,13 +222,20 @@ __global__ void k_auc(const float* __restrict__ pred, const float* __restrict__ 
     ls += __shfl_down(ls, off);
     cnt += __shfl_down(cnt, off);
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&stats[0], ae);
-    atomicAdd(&stats[1], se);
-    atomicAdd(&stats[2], ps);
-    atomicAdd(&stats[3], ls);
-    atomicAdd(&stats[4], cnt);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][w] = ae;
+    red[1][w] = se;
+    red[2][w] = ps;
+    red[3][w] = ls;
+    red[4][w] = cnt;
   }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kAucLds; e += blockDim.x)
+    if (hk[e] >= 0) atomicAdd(&table[hk[e]], (double)hc[e]);
+  if (threadIdx.x < 5 && red[4][0] + red[4][1] + red[4][2] + red[4][3] > 0)
+    atomicAdd(&stats[threadIdx.x],
+              red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3]);
 }
 
 // ---------------------------------------------------------------- Adam (flat)
@@ -191,15 +248,18 @@ __global__ void k_adam_pows(float* pows, float b1, float b2) {
   }
 }
 
-__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+// clear_grad: zero the gradient after consuming it, so the next backward can
+// accumulate into it without a separate zero-fill launch
+__global__ void k_adam(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                        float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
-                       const float* __restrict__ pows, float gs, float wd) {
+                       const float* __restrict__ pows, float gs, float wd, int clear_grad) {
   const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const float b1pow = pows[0], b2pow = pows[1];
   const float lr_t = lr * sqrtf(1.f - b2pow) / (1.f - b1pow);
   if ((i4 + 1) * 4 <= n) {
     float4 pp = reinterpret_cast<float4*>(p)[i4];
     const float4 gg = reinterpret_cast<const float4*>(g)[i4];
+    if (clear_grad) reinterpret_cast<float4*>(g)[i4] = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 mm = reinterpret_cast<float4*>(m)[i4];
     float4 vv = reinterpret_cast<float4*>(v)[i4];
     float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
@@ -216,6 +276,7 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
   } else {
     for (int64_t i = i4 * 4; i < n; ++i) {
       const float gk = g[i] * gs + wd * p[i];
+      if (clear_grad) g[i] = 0.f;
       m[i] = b1 * m[i] + (1.f - b1) * gk;
       v[i] = b2 * v[i] + (1.f - b2) * gk * gk;
       p[i] -= lr_t * m[i] / (sqrtf(v[i]) + eps * sqrtf(1.f - b2pow));
@@ -261,6 +322,12 @@ void launch_fm_bwd(const float* x, const float* dout, int B, int S, int D, int r
   hipLaunchKernelGGL(k_fm_bwd, dim3(nblk(B)), dim3(256), 0, s, x, dout, B, S, D, row_stride, col0, fstride, dx, dx_stride, accumulate);
 }
 
+void launch_logit_loss(const float* a, const float* b, const float* label, int B, float* pred, float* dz,
+                       float* loss_mean, hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(k_logit_loss, dim3(1), dim3(1024), 0, s, a, b, label, B, pred, dz, loss_mean);
+}
+
 void launch_sigmoid_logloss(const float* logit, const float* label, int B, float* pred,
                             float* loss_sum, float* dlogit, float grad_scale, hipStream_t s) {
   if (B == 0) return;
@@ -270,16 +337,18 @@ void launch_sigmoid_logloss(const float* logit, const float* label, int B, float
 void launch_auc_accumulate(const float* pred, const float* label, const float* mask, int B,
                            int nbuckets, double* table, double* stats, hipStream_t s) {
   if (B == 0) return;
-  hipLaunchKernelGGL(k_auc, dim3(nblk(B)), dim3(256), 0, s, pred, label, mask, B, nbuckets, table, stats);
+  hipLaunchKernelGGL(k_auc, dim3(nblk(B, 256 * kAucItems)), dim3(256), 0, s, pred, label, mask, B, nbuckets, table,
+                     stats);
 }
 
-void launch_adam_flat(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
+void launch_adam_flat(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1,
                       float b2, float eps, float* pows, float grad_scale, float weight_decay,
-                      hipStream_t s) {
+                      bool clear_grad, hipStream_t s) {
   if (n == 0) return;
   const int64_t n4 = (n + 3) / 4;
   hipLaunchKernelGGL(k_adam_pows, dim3(1), dim3(64), 0, s, pows, b1, b2);
-  hipLaunchKernelGGL(k_adam, dim3(nblk(n4)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, pows, grad_scale, weight_decay);
+  hipLaunchKernelGGL(k_adam, dim3(nblk(n4)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps, pows, grad_scale,
+                     weight_decay, clear_grad ? 1 : 0);
 }
 
 }  // namespace pbx

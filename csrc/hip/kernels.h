@@ -125,6 +125,11 @@ struct SeqpoolCvmArgs {
   int embed_threshold_filter = 0;
   float embed_threshold = 0.f;
   int embed_thres_size = 0;
+  // optional dense features copied into out[b, dense_col : dense_col + dense_dim]
+  // by the same launch (the concat of the pooled slots with the dense slots)
+  const float* dense = nullptr;
+  int dense_dim = 0;
+  int dense_col = 0;
 };
 int seqpool_cvm_out_width(const SeqpoolCvmArgs& a);
 void launch_seqpool_cvm_fwd(const SeqpoolCvmArgs& a, hipStream_t s);
@@ -178,6 +183,21 @@ void launch_shard_pack(const uint64_t* uniq_h, const int32_t* u_count, int64_t u
 // resp[j] = pulled[uid_r[j]] for received entries (invalid -> zeros).
 void launch_gather_by_uid(const float* src, int src_stride, const int32_t* uid, int64_t n,
                           float* out, int out_stride, int width, hipStream_t s);
+// Owner pack after the sort-free dedup: unique keys (any order) -> per-owner
+// fixed-capacity segments of send [nranks*cap] (kEmptyKey padded) and
+// send_index[u]; ocnt [nranks] scratch; overflow flag is sticky.
+void launch_shard_pack_hash(const uint64_t* uniq_h, const int32_t* u_count, int64_t u_cap, int nranks, int64_t cap,
+                            uint64_t* send, int64_t* send_index, int32_t* ocnt, int32_t* overflow, hipStream_t s);
+// out[j] = pull head of table row rows[uid[j]] (zeros if uid/row < 0);
+// out_stride % 4 == 0 and <= table stride.
+void launch_gather_rows_by_uid(const TableDev& t, const int64_t* rows, const int32_t* uid, int64_t n, float* out,
+                               int out_stride, hipStream_t s);
+// Fused owner-side merge + Adagrad: unique u's records are
+// rec[perm[seg[u] + j]], j < cnt[u].  Returns false if the dim/stride has no
+// vectorised instantiation (caller falls back to merge + launch_push_adagrad).
+bool launch_push_adagrad_seg(const TableDev& t, const int64_t* rows, const float* rec, int rec_stride,
+                             const int32_t* perm, const int32_t* seg, const int32_t* cnt, const int32_t* n_dev,
+                             int64_t n, const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s);
 
 // ---------------------------------------------------------------- dense ops
 void launch_data_norm_fwd(const float* x, int N, int C, const float* bsize, const float* bsum,
@@ -258,6 +278,10 @@ void launch_fm_bwd(const float* x, const float* dout, int B, int S, int D, int r
 void launch_sigmoid_logloss(const float* logit, const float* label, int B, float* pred,
                             float* loss_sum, float* dlogit, float grad_scale, hipStream_t s);
 
+// z = a + b (b nullable); pred = sigmoid(z), dz = (pred - y)/B, loss_mean = mean BCE.
+void launch_logit_loss(const float* a, const float* b, const float* label, int B, float* pred, float* dz,
+                       float* loss_mean, hipStream_t s);
+
 // Streaming AUC histogram: table[label][bucket] += 1 and error sums
 // (stats: [abserr, sqrerr, pred_sum, label_sum, count]) in double.
 void launch_auc_accumulate(const float* pred, const float* label, const float* mask, int B,
@@ -266,9 +290,9 @@ void launch_auc_accumulate(const float* pred, const float* label, const float* m
 
 // Flat Adam over a contiguous fp32 buffer; pows = device [beta1^t, beta2^t]
 // (advanced in-stream, graph-replayable).
-void launch_adam_flat(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
+void launch_adam_flat(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1,
                       float b2, float eps, float* pows, float grad_scale, float weight_decay,
-                      hipStream_t s);
+                      bool clear_grad, hipStream_t s);
 
 // ---------------------------------------------------------------- fused MLP engine (mlp.hip)
 enum MlpEpi { MLP_EPI_FWD = 0, MLP_EPI_DX = 1, MLP_EPI_DW = 2 };

@@ -103,6 +103,11 @@ __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
   if (t >= (int64_t)a.S * a.B) return;
   // instance-major so a wave writes contiguous output rows
   const int b = (int)(t / a.S), s = (int)(t % a.S);
+  if (s == 0 && a.dense) {
+    const float* src = a.dense + (int64_t)b * a.dense_dim;
+    float* dst = a.out + (int64_t)b * a.out_stride + a.dense_col;
+    for (int c = 0; c < a.dense_dim; ++c) dst[c] = src[c];
+  }
   const int64_t st = a.lod[(int64_t)s * (a.B + 1) + b], en = a.lod[(int64_t)s * (a.B + 1) + b + 1];
   float acc[E];
 #pragma unroll
@@ -159,6 +164,11 @@ __global__ void k_seqpool_cvm_generic(SeqpoolCvmArgs a) {
   if (t >= (int64_t)a.S * a.B) return;
   const int b = (int)(t / a.S), s = (int)(t % a.S);
   const int E = a.E;
+  if (s == 0 && a.dense) {
+    const float* src = a.dense + (int64_t)b * a.dense_dim;
+    float* dst = a.out + (int64_t)b * a.out_stride + a.dense_col;
+    for (int c = 0; c < a.dense_dim; ++c) dst[c] = src[c];
+  }
   const int64_t st = a.lod[(int64_t)s * (a.B + 1) + b], en = a.lod[(int64_t)s * (a.B + 1) + b + 1];
   const int Eo = a.use_cvm ? (a.clk_filter ? E - 1 : E) : E - a.cvm_offset;
   float* o = a.out + (int64_t)b * a.out_stride + a.col_offset + (int64_t)s * Eo;
@@ -328,6 +338,134 @@ __global__ __launch_bounds__(256) void k_push_adagrad(TableDev t, const int64_t*
   }
 }
 
+// Vectorised variant for the common embedx dims: the row (stride 4k floats,
+// 16-B aligned) and the push record move as float4s with compile-time field
+// indices, so the whole update is a handful of wide loads/stores instead of
+// ~20 dependent scalar accesses per row.
+template <int D>
+struct RowF {
+  static constexpr int kG2 = 3 + D, kXG2 = 4 + D, kDelta = 5 + D, kSlot = 6 + D, kUnseen = 7 + D, kMf = 8 + D;
+  static constexpr int kStride = ((9 + D) + 3) & ~3;
+  static constexpr int kQ = 4 + D;                 // push record floats used
+  static constexpr int kQ4 = (kQ + 3) / 4;         // float4s covering it
+};
+
+template <int D>
+__device__ __forceinline__ void adagrad_row(float* __restrict__ row, const float* g, const SparseSGDConfig& cfg,
+                                            uint64_t seed, int64_t r) {
+  using L = RowF<D>;
+  float v[L::kStride];
+  float4* r4 = reinterpret_cast<float4*>(row);
+#pragma unroll
+  for (int i = 0; i < L::kStride / 4; ++i) {
+    const float4 x = r4[i];
+    v[4 * i] = x.x;
+    v[4 * i + 1] = x.y;
+    v[4 * i + 2] = x.z;
+    v[4 * i + 3] = x.w;
+  }
+  const float slot = g[kPushSlot], g_show = g[kPushShow], g_click = g[kPushClick];
+  v[L::kSlot] = slot;
+  const float show = v[kShow] + g_show;
+  const float click = v[kClick] + g_click;
+  v[kShow] = show;
+  v[kClick] = click;
+  v[L::kDelta] += cfg.nonclk_coeff * (g_show - g_click) + cfg.clk_coeff * g_click;
+  v[L::kUnseen] = 0.f;
+  const float scale = g_show > 0.f ? g_show : 1.f;
+  float lr = cfg.learning_rate, mf_lr = cfg.mf_learning_rate;
+  if (cfg.use_feature_lr && slot != cfg.nodeid_slot) { lr = cfg.feature_learning_rate; mf_lr = cfg.feature_learning_rate; }
+  {
+    const float g2 = v[L::kG2];
+    const float ratio = lr * sqrtf(cfg.initial_g2sum / (cfg.initial_g2sum + g2));
+    const float sg = g[kPushEmbedG] / scale;
+    v[kEmbedW] = clampf(v[kEmbedW] + sg * ratio, cfg.min_bound, cfg.max_bound);
+    v[L::kG2] = g2 + sg * sg;
+  }
+  if (v[L::kMf] == 0.f) {
+    if (cfg.nonclk_coeff * (show - click) + cfg.clk_coeff * click >= cfg.mf_create_thresholds) {
+      v[L::kMf] = 1.f;
+      const uint64_t salt = seed ^ (uint64_t)r * 0x9E3779B97F4A7C15ULL;
+#pragma unroll
+      for (int d = 0; d < D; ++d) v[kEmbedx + d] = hash_uniform(salt, d) * cfg.mf_initial_range;
+    }
+  } else {
+    const float g2 = v[L::kXG2];
+    const float ratio = mf_lr * sqrtf(cfg.mf_initial_g2sum / (cfg.mf_initial_g2sum + g2));
+    float add = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float sg = g[kPushEmbedxG + d] / scale;
+      v[kEmbedx + d] = clampf(v[kEmbedx + d] + sg * ratio, cfg.mf_min_bound, cfg.mf_max_bound);
+      add += sg * sg;
+    }
+    v[L::kXG2] = g2 + add / (float)D;
+  }
+#pragma unroll
+  for (int i = 0; i < L::kStride / 4; ++i) r4[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+}
+
+template <int D>
+__device__ __forceinline__ void load_push(const float* __restrict__ p, float* g) {
+  using L = RowF<D>;
+  const float4* p4 = reinterpret_cast<const float4*>(p);
+#pragma unroll
+  for (int i = 0; i < L::kQ4; ++i) {
+    const float4 x = p4[i];
+    if (4 * i < L::kQ) g[4 * i] = x.x;
+    if (4 * i + 1 < L::kQ) g[4 * i + 1] = x.y;
+    if (4 * i + 2 < L::kQ) g[4 * i + 2] = x.z;
+    if (4 * i + 3 < L::kQ) g[4 * i + 3] = x.w;
+  }
+}
+
+// push_stride must be a multiple of 4 and >= 4*kQ4 (the engine's padded record)
+template <int D>
+__global__ __launch_bounds__(256) void k_push_adagrad_v(TableDev t, const int64_t* __restrict__ rows,
+                                                        const float* __restrict__ push, int push_stride,
+                                                        const int32_t* n_dev, int64_t n, SparseSGDConfig cfg,
+                                                        uint64_t seed) {
+  const int64_t nn = n_dev ? (int64_t)*n_dev : n;
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nn) return;
+  const int64_t r = rows[u];
+  if (r < 0) return;
+  float g[RowF<D>::kQ4 * 4];
+  load_push<D>(push + u * push_stride, g);
+  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
+}
+
+// Owner side of the sharded push: the records of unique u (at most one per
+// sender, so a short bounded run) are perm[seg[u] .. seg[u]+cnt[u]) of the
+// received buffer; merge them in registers and apply Adagrad in place --
+// no merged-record buffer, no memset, no separate merge launch.
+template <int D>
+__global__ __launch_bounds__(256) void k_push_adagrad_seg(TableDev t, const int64_t* __restrict__ rows,
+                                                          const float* __restrict__ rec, int rec_stride,
+                                                          const int32_t* __restrict__ perm,
+                                                          const int32_t* __restrict__ seg,
+                                                          const int32_t* __restrict__ cnt, const int32_t* n_dev,
+                                                          int64_t n, SparseSGDConfig cfg, uint64_t seed) {
+  const int64_t nn = n_dev ? (int64_t)*n_dev : n;
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nn) return;
+  const int64_t r = rows[u];
+  if (r < 0) return;
+  constexpr int QP = RowF<D>::kQ4 * 4;
+  float g[QP];
+#pragma unroll
+  for (int c = 0; c < QP; ++c) g[c] = 0.f;
+  const int s0 = seg[u], m = cnt[u];
+  for (int j = 0; j < m; ++j) {
+    float x[QP];
+    load_push<D>(rec + (int64_t)perm[s0 + j] * rec_stride, x);
+    g[kPushSlot] = x[kPushSlot];
+#pragma unroll
+    for (int c = 1; c < QP; ++c) g[c] += x[c];
+  }
+  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
+}
+
 // ---------------------------------------------------------------- sharding helpers
 __device__ __forceinline__ int64_t owner_lower_bound(const uint64_t* h, int64_t U, uint32_t o, uint32_t N) {
   int64_t lo = 0, hi = U;
@@ -381,6 +519,76 @@ __global__ void k_gather_by_uid(const float* __restrict__ src, int src_stride, c
     for (int c = 0; c < width / 4; ++c) o4[c] = s4[c];
   } else {
     for (int c = 0; c < width; ++c) o[c] = s[c];
+  }
+}
+
+// Sender-side owner pack after the sort-free dedup (unique ids in arbitrary
+// order): per block, unique keys are counted per owner in LDS, one global
+// atomic per (block, owner) reserves their slots in the owner's fixed-capacity
+// segment of the send buffer.  send must be pre-filled with kEmptyKey and
+// ocnt zeroed; keys past the capacity are flagged (overflow) and dropped.
+constexpr int kMaxRanks = 64;
+__global__ __launch_bounds__(256) void k_shard_pack_hash(const uint64_t* __restrict__ uniq_h,
+                                                         const int32_t* __restrict__ u_count, int nranks,
+                                                         int64_t cap, uint64_t* __restrict__ send,
+                                                         int64_t* __restrict__ send_index, int32_t* __restrict__ ocnt,
+                                                         int32_t* __restrict__ overflow) {
+  __shared__ int32_t lc[kMaxRanks];
+  __shared__ int32_t lb[kMaxRanks];
+  const int64_t U = *u_count;
+  const int64_t b0 = (int64_t)blockIdx.x * blockDim.x;
+  if (b0 >= U) return;  // block-uniform
+  if (threadIdx.x < nranks) lc[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t u = b0 + threadIdx.x;
+  uint32_t o = 0;
+  int lp = -1;
+  uint64_t h = 0;
+  if (u < U) {
+    h = uniq_h[u];
+    o = owner_of(h, (uint32_t)nranks);
+    lp = atomicAdd(&lc[o], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x < nranks) lb[threadIdx.x] = lc[threadIdx.x] ? atomicAdd(&ocnt[threadIdx.x], lc[threadIdx.x]) : 0;
+  __syncthreads();
+  if (u < U) {
+    const int64_t p = (int64_t)lb[o] + lp;
+    if (p < cap) {
+      send[(int64_t)o * cap + p] = h;
+      send_index[u] = (int64_t)o * cap + p;
+    } else {
+      send_index[u] = -1;
+      atomicOr(overflow, 1);
+    }
+  }
+}
+
+// Owner-side pull answer straight from the table: out[j] = pull head of the
+// row of received entry j (zeros for padding / missing keys).
+__global__ __launch_bounds__(256) void k_gather_rows_by_uid(TableDev t, const int64_t* __restrict__ rows,
+                                                            const int32_t* __restrict__ uid, int64_t n,
+                                                            float* __restrict__ out, int out_stride) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int32_t u = uid[j];
+  const int64_t r = u >= 0 ? rows[u] : -1;
+  const int P = kPullHead + t.dim;
+  float4* o4 = reinterpret_cast<float4*>(out + j * out_stride);
+  const int n4 = out_stride / 4;
+  if (r < 0) {
+    for (int c = 0; c < n4; ++c) o4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  const float4* s4 = reinterpret_cast<const float4*>(t.values + r * (int64_t)t.stride);
+  for (int c = 0; c < n4; ++c) {
+    float4 v = s4[c];
+    const int b = c * 4;
+    if (b + 0 >= P) v.x = 0.f;
+    if (b + 1 >= P) v.y = 0.f;
+    if (b + 2 >= P) v.z = 0.f;
+    if (b + 3 >= P) v.w = 0.f;
+    o4[c] = v;
   }
 }
 
@@ -451,11 +659,58 @@ void launch_push_merge_records(const float* rec, int rec_stride, const int32_t* 
   }
 }
 
+template <int D>
+static bool vec_push_ok(const TableDev& t, int push_stride) {
+  return t.dim == D && t.stride == RowF<D>::kStride && push_stride % 4 == 0 && push_stride >= RowF<D>::kQ4 * 4;
+}
+
 void launch_push_adagrad(const TableDev& t, const int64_t* rows, const float* push,
                          int push_stride, const int32_t* n_dev, int64_t n,
                          const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_push_adagrad, dim3(nblk(n)), dim3(256), 0, s, t, rows, push, push_stride, n_dev, n, cfg, seed);
+  const dim3 g(nblk(n)), b(256);
+  if (vec_push_ok<8>(t, push_stride))
+    hipLaunchKernelGGL(k_push_adagrad_v<8>, g, b, 0, s, t, rows, push, push_stride, n_dev, n, cfg, seed);
+  else if (vec_push_ok<16>(t, push_stride))
+    hipLaunchKernelGGL(k_push_adagrad_v<16>, g, b, 0, s, t, rows, push, push_stride, n_dev, n, cfg, seed);
+  else if (vec_push_ok<4>(t, push_stride))
+    hipLaunchKernelGGL(k_push_adagrad_v<4>, g, b, 0, s, t, rows, push, push_stride, n_dev, n, cfg, seed);
+  else if (vec_push_ok<32>(t, push_stride))
+    hipLaunchKernelGGL(k_push_adagrad_v<32>, g, b, 0, s, t, rows, push, push_stride, n_dev, n, cfg, seed);
+  else
+    hipLaunchKernelGGL(k_push_adagrad, g, b, 0, s, t, rows, push, push_stride, n_dev, n, cfg, seed);
+}
+
+bool launch_push_adagrad_seg(const TableDev& t, const int64_t* rows, const float* rec, int rec_stride,
+                             const int32_t* perm, const int32_t* seg, const int32_t* cnt, const int32_t* n_dev,
+                             int64_t n, const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s) {
+  if (n <= 0) return true;
+  const dim3 g(nblk(n)), b(256);
+  if (vec_push_ok<8>(t, rec_stride))
+    hipLaunchKernelGGL(k_push_adagrad_seg<8>, g, b, 0, s, t, rows, rec, rec_stride, perm, seg, cnt, n_dev, n, cfg, seed);
+  else if (vec_push_ok<16>(t, rec_stride))
+    hipLaunchKernelGGL(k_push_adagrad_seg<16>, g, b, 0, s, t, rows, rec, rec_stride, perm, seg, cnt, n_dev, n, cfg, seed);
+  else if (vec_push_ok<4>(t, rec_stride))
+    hipLaunchKernelGGL(k_push_adagrad_seg<4>, g, b, 0, s, t, rows, rec, rec_stride, perm, seg, cnt, n_dev, n, cfg, seed);
+  else if (vec_push_ok<32>(t, rec_stride))
+    hipLaunchKernelGGL(k_push_adagrad_seg<32>, g, b, 0, s, t, rows, rec, rec_stride, perm, seg, cnt, n_dev, n, cfg, seed);
+  else
+    return false;
+  return true;
+}
+
+void launch_shard_pack_hash(const uint64_t* uniq_h, const int32_t* u_count, int64_t u_cap, int nranks, int64_t cap,
+                            uint64_t* send, int64_t* send_index, int32_t* ocnt, int32_t* overflow, hipStream_t s) {
+  (void)hipMemsetAsync(send, 0xFF, (size_t)nranks * cap * sizeof(uint64_t), s);  // kEmptyKey
+  (void)hipMemsetAsync(ocnt, 0, (size_t)nranks * sizeof(int32_t), s);
+  hipLaunchKernelGGL(k_shard_pack_hash, dim3(nblk(u_cap)), dim3(256), 0, s, uniq_h, u_count, nranks, cap, send,
+                     send_index, ocnt, overflow);
+}
+
+void launch_gather_rows_by_uid(const TableDev& t, const int64_t* rows, const int32_t* uid, int64_t n, float* out,
+                               int out_stride, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather_rows_by_uid, dim3(nblk(n)), dim3(256), 0, s, t, rows, uid, n, out, out_stride);
 }
 
 void launch_zero_rows(float* buf, int stride, const int32_t* n_dev, int64_t cap, hipStream_t s) {

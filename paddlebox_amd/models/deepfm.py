@@ -9,7 +9,7 @@ Graph (PaddleBox canonical CTR graph, SURVEY Appendix B, plus the FM term):
         first order  = sum_s embed_w(s)
         second order = FM over embedx[8]
     deep = FusedMLP 400-400-400 -> 1       MFMA GEMMs, bias+ReLU fused
-    logit = first + second + deep -> fused sigmoid + logloss
+    logit = (first + second) + deep -> fused add + sigmoid + logloss
 
 The embedding update happens in the backward of the pull (push_box_sparse
 with fused sparse Adagrad); dense params live in one flat arena updated by
@@ -22,7 +22,7 @@ from typing import Sequence
 import torch
 from torch import nn
 
-from ..ops.ctr import DataNorm, ctr_head, sigmoid_logloss
+from ..ops.ctr import DataNorm, ctr_head, logit_logloss
 from ..ops.mlp import FusedMLP, pad8
 from ..ops.sparse import pull_seqpool_cvm_concat
 from ..ps.sparse_engine import SeqpoolParams, SparseEngine
@@ -60,8 +60,8 @@ class DeepFM(nn.Module):
         self.in_dim = C
         self.Cp = pad8(C)
         self.dn = DataNorm(C) if use_data_norm else None
+        # the global bias is the MLP output layer's bias (b_out)
         self.mlp = FusedMLP(C, hidden, 1)
-        self.bias = nn.Parameter(torch.zeros(1))
         self.use_workspace = True
         self.head_into_workspace = True
         # column of embed_w inside each slot block; embedx follow it
@@ -83,6 +83,6 @@ class DeepFM(nn.Module):
         else:
             y, lin = ctr_head(x, self.dn, S, self.Eo, self.ew_col, self.D, self.Cp)
             deep = self.mlp(y)
-        logit = deep + lin + self.bias
-        loss, pred = sigmoid_logloss(logit, batch.label)
+        # logit = deep + lin, sigmoid, log-loss and its gradient: one kernel
+        loss, pred = logit_logloss(deep, lin, batch.label)
         return loss, pred

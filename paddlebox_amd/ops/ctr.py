@@ -10,6 +10,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
+from ..parallel.comm import collective_active
 from . import reference as ref
 
 
@@ -39,7 +40,7 @@ class _DataNorm(torch.autograd.Function):
             dx, stats = _native.hip().data_norm_bwd(x, dy, means, scales, ctx.eps, True, scale_w)
         else:
             dx, stats = ref.data_norm_bwd(x, dy, means, scales, ctx.eps, scale_w)
-        if ctx.group is not None and dist.is_initialized() and dist.get_world_size(ctx.group) > 1:
+        if ctx.group is not None and collective_active(ctx.group):
             # one fused all-reduce of [3, C] (reference does 3 separate ones,
             # data_norm_op.cu:203-230)
             dist.all_reduce(stats, group=ctx.group)
@@ -149,7 +150,7 @@ class _CtrHead(torch.autograd.Function):
             if dn is not None:
                 _, stats = ref.data_norm_bwd(x, x, ctx.means, ctx.scales, dn.eps)
         if dn is not None and dn.training and dn.update_norm:
-            if dn.sync_stats and dn.group is not None and dist.is_initialized() and dist.get_world_size(dn.group) > 1:
+            if dn.sync_stats and dn.group is not None and collective_active(dn.group):
                 dist.all_reduce(stats, group=dn.group)
             if _gpu(x):
                 _native.hip().data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, stats, dn.decay)
@@ -225,6 +226,39 @@ class _SigmoidLogLoss(torch.autograd.Function):
 def sigmoid_logloss(logit: torch.Tensor, label: torch.Tensor):
     """(mean log-loss, sigmoid prediction) with the gradient fused."""
     return _SigmoidLogLoss.apply(logit, label)
+
+
+class _LogitLoss(torch.autograd.Function):
+    """loss, pred = BCE(sigmoid(a + b), label): the sum of the two logit parts,
+    the sigmoid, the mean log-loss and its gradient in one kernel; the
+    backward is a single scale of the saved gradient, shared by both parts."""
+
+    @staticmethod
+    def forward(ctx, a, b, label):
+        a = a.contiguous().float().view(-1)
+        label = label.contiguous().float().view(-1)
+        bb = b.contiguous().float().view(-1) if b is not None else None
+        if _gpu(a):
+            loss, pred, dz = _native.hip().logit_loss(a, bb, label)
+        else:
+            z = a + bb if bb is not None else a
+            pred, loss_sum, dz = ref.sigmoid_logloss(z, label, 1.0 / a.numel())
+            loss = loss_sum / a.numel()
+        ctx.save_for_backward(dz)
+        ctx.has_b = b is not None
+        ctx.mark_non_differentiable(pred)
+        return loss.view(()), pred
+
+    @staticmethod
+    def backward(ctx, gl, gp):
+        (dz,) = ctx.saved_tensors
+        g = dz * gl
+        return g, (g if ctx.has_b else None), None
+
+
+def logit_logloss(a: torch.Tensor, b: Optional[torch.Tensor], label: torch.Tensor):
+    """(mean log-loss, prediction) of logit = a + b, fused."""
+    return _LogitLoss.apply(a, b, label)
 
 
 # ---------------------------------------------------------------- AUC

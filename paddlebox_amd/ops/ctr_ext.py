@@ -16,6 +16,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
+from ..parallel.comm import collective_active
 
 
 def _hip_or_none(t: torch.Tensor):
@@ -347,7 +348,7 @@ class _MaskedDataNorm(torch.autograd.Function):
             xm.sum(0) / n.clamp(min=1),
             (((x - means) ** 2) * m).sum(0) / n.clamp(min=1) + ctx.eps * (n > 0).to(x.dtype),
         ])
-        if ctx.group is not None and dist.is_initialized() and dist.get_world_size(ctx.group) > 1:
+        if ctx.group is not None and collective_active(ctx.group):
             dist.all_reduce(stats, group=ctx.group)
         if ctx.update and ctx.training:
             upd = stats[0] > 0
@@ -407,7 +408,7 @@ class _CrossNormHadamard(torch.autograd.Function):
         gb = g[..., E:2 * E] + g[..., 2 * E:3 * E] * a + g[..., 3 * E:] * a
         dx = torch.stack([ga, gb], 2).reshape(B, F * 2 * E)
         stats = torch.stack([torch.ones_like(means), raw.mean(0), ((raw - means) ** 2).mean(0) + ctx.eps])
-        if ctx.group is not None and dist.is_initialized() and dist.get_world_size(ctx.group) > 1:
+        if ctx.group is not None and collective_active(ctx.group):
             dist.all_reduce(stats, group=ctx.group)
         if ctx.training:
             with torch.no_grad():

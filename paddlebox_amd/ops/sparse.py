@@ -40,9 +40,8 @@ class _PullSeqpoolCvmConcat(torch.autograd.Function):
         Eo = sp.out_width(E)
         Dd = 0 if dense is None else dense.shape[1]
         out = torch.empty(B, S * Eo + Dd, dtype=torch.float32, device=keys.device)
-        st = engine.pull_seqpool_cvm(keys, lod, B, S, out, 0, sp)
-        if Dd:
-            out[:, S * Eo:] = dense
+        # the dense features are written by the same launch (no concat copy)
+        st = engine.pull_seqpool_cvm(keys, lod, B, S, out, 0, sp, dense=dense if Dd else None, dense_col=S * Eo)
         ctx.engine, ctx.st, ctx.sp, ctx.bs_scale = engine, st, sp, bs_scale
         ctx.S, ctx.Eo, ctx.Dd = S, Eo, Dd
         ctx.save_for_backward(cvm)

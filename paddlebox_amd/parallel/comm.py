@@ -12,6 +12,7 @@ and ``c_mixallgather_op.cc:221-327``; BoxPS's closed GPU<->GPU key routing.
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import List, Optional, Sequence
 
@@ -60,8 +61,23 @@ class TorchDistComm(Comm):
         return dist.get_backend(self.group)
 
 
+def force_collectives() -> bool:
+    """``PBX_FORCE_COLLECTIVES=1``: run every collective of the multi-GPU path
+    (key/value/grad all-to-all, dense all-reduce, data_norm stats) even for a
+    world of one rank.  A 1-GPU box rehearses the exact N-GPU step -- RCCL
+    calls captured inside the HIP graph included -- this way."""
+    return os.environ.get("PBX_FORCE_COLLECTIVES", "0") == "1"
+
+
+def collective_active(group=None) -> bool:
+    """True when collectives over ``group`` must actually run."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size(group) > 1 or force_collectives()
+
+
 def default_comm(group=None) -> Optional[Comm]:
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if collective_active(group):
         return TorchDistComm(group)
     return None
 

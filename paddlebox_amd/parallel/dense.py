@@ -22,6 +22,7 @@ import torch.distributed as dist
 
 from .. import _native
 from ..ops import reference as ref
+from .comm import collective_active
 
 
 class DenseArena:
@@ -55,9 +56,12 @@ class FlatAdam:
     """Adam over the whole arena in one kernel (Paddle adam semantics)."""
 
     def __init__(self, arena: DenseArena, lr: float = 1e-3, beta1: float = 0.9, beta2: float = 0.999,
-                 epsilon: float = 1e-8, weight_decay: float = 0.0):
+                 epsilon: float = 1e-8, weight_decay: float = 0.0, clear_grad: bool = False):
         self.a = arena
         self.lr, self.b1, self.b2, self.eps, self.wd = lr, beta1, beta2, epsilon, weight_decay
+        # clear_grad: the update kernel zeroes the gradient arena after use, so
+        # the training step needs no separate zero_grad launch
+        self.clear_grad = clear_grad
         self.m = torch.zeros_like(arena.flat)
         self.v = torch.zeros_like(arena.flat)
         # [beta1^t, beta2^t] on the device: advanced by the kernel itself so the
@@ -67,12 +71,14 @@ class FlatAdam:
     def step(self, grad_scale: float = 1.0):
         if self.a.flat.is_cuda:
             _native.hip().adam_flat(self.a.flat, self.a.grad, self.m, self.v, self.pows, self.lr, self.b1, self.b2,
-                                    self.eps, grad_scale, self.wd)
+                                    self.eps, grad_scale, self.wd, self.clear_grad)
         else:
             self.pows[0] *= self.b1
             self.pows[1] *= self.b2
             ref.adam_flat(self.a.flat, self.a.grad, self.m, self.v, self.lr, self.b1, self.b2, self.eps,
                           float(self.pows[0]), float(self.pows[1]), grad_scale, self.wd)
+            if self.clear_grad:
+                self.a.grad.zero_()
 
     def state_dict(self):
         return {"m": self.m, "v": self.v, "pows": self.pows}
@@ -92,6 +98,7 @@ class DenseSync:
         self.k = max(1, k)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.active = collective_active(group)
         self.steps = 0
 
     def grad_scale(self) -> float:
@@ -99,17 +106,17 @@ class DenseSync:
 
     def before_step(self):
         """Called after backward, before the optimizer."""
-        if self.world > 1 and self.mode == "grad_allreduce":
+        if self.active and self.mode == "grad_allreduce":
             dist.all_reduce(self.a.grad, group=self.group)
 
     def after_step(self):
         self.steps += 1
-        if self.world > 1 and self.mode == "kstep" and self.steps % self.k == 0:
+        if self.active and self.mode == "kstep" and self.steps % self.k == 0:
             self.sync_params()
 
     def sync_params(self):
         """Parameter averaging (boxps_worker.cc:1235-1239: sum then x 1/devices)."""
-        if self.world > 1:
+        if self.active:
             dist.all_reduce(self.a.flat, group=self.group)
             self.a.flat.mul_(1.0 / self.world)
 

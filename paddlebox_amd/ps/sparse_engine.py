@@ -98,6 +98,9 @@ class SparseEngine:
         self.group = group
         self.comm = comm if comm is not None else default_comm(group)
         self.world = self.comm.world if self.comm is not None else 1
+        # sharded = the key/value/grad exchange runs (world > 1, or forced for a
+        # 1-rank rehearsal of the multi-GPU step, see parallel.comm)
+        self.sharded = self.comm is not None
         self.rank = self.comm.rank if self.comm is not None else 0
         self.auto_insert = auto_insert
         self.test_mode = False
@@ -108,13 +111,12 @@ class SparseEngine:
             self._hip = _native.hip()
             self._sgd_native = cfg.sgd.to_native(self._hip)
             with torch.cuda.device(self.device):
-                # sender-side dedup must emit the unique keys grouped by owner
-                # shard (sorted h) for the key all-to-all; a single shard and
-                # the owner side take the sort-free hash dedup
-                self.ws = self._hip.DedupWorkspace(self.max_keys, self.device.index or 0, self.world == 1)
+                # sort-free hash dedup everywhere: the sender packs its unique
+                # keys per owner with a counting pass (shard_pack_hash)
+                self.ws = self._hip.DedupWorkspace(self.max_keys, self.device.index or 0, True)
             self.occ_slot = torch.empty(self.max_keys, dtype=torch.int32, device=self.device)
             self.occ_ins = torch.empty(self.max_keys, dtype=torch.int32, device=self.device)
-            if self.world > 1:
+            if self.sharded:
                 self.C = int(math.ceil(self.max_keys / self.world * cap_factor)) + 64
                 n = self.world * self.C
                 with torch.cuda.device(self.device):
@@ -123,6 +125,7 @@ class SparseEngine:
                 self.recv = torch.empty(n, dtype=torch.int64, device=self.device)
                 self.send_index = torch.empty(self.max_keys, dtype=torch.int64, device=self.device)
                 self.overflow = torch.zeros(1, dtype=torch.int32, device=self.device)
+                self.ocnt = torch.zeros(self.world, dtype=torch.int32, device=self.device)
                 self.resp = torch.empty(n, self.P, device=self.device)
                 self.resp_back = torch.empty(n, self.P, device=self.device)
                 self.push_send = torch.empty(n, self.Q, device=self.device)
@@ -150,7 +153,7 @@ class SparseEngine:
             h = torch.unique(ref.mix64(keys))
         else:
             h = torch.unique(ref.mix64(keys))
-        if self.world > 1:
+        if self.sharded:
             owner = ref.owner_of(h, self.world)
             order = torch.argsort(owner, stable=True)
             h = h[order]
@@ -168,23 +171,30 @@ class SparseEngine:
 
     # ------------------------------------------------------------------ pull
     def pull_seqpool_cvm(self, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int, out: torch.Tensor,
-                         col_offset: int, sp: SeqpoolParams) -> PullState:
-        """Fused pull + seqpool + CVM written into out[:, col_offset:...].
+                         col_offset: int, sp: SeqpoolParams, dense: Optional[torch.Tensor] = None,
+                         dense_col: int = 0) -> PullState:
+        """Fused pull + seqpool + CVM written into out[:, col_offset:...]
+        (+ the dense features into out[:, dense_col:...] by the same launch).
 
         keys: int64 [Lcap] slot-major flat keys, -1 padded; lod: int64 [S*(B+1)].
         """
         if not self.is_gpu:
-            return self._cpu_pull_seqpool(keys, lod, B, S, out, col_offset, sp)
+            st = self._cpu_pull_seqpool(keys, lod, B, S, out, col_offset, sp)
+            if dense is not None:
+                out[:, dense_col:dense_col + dense.shape[1]] = dense
+            return st
         st = self._pull_common(keys, lod, B, S)
         h = self._hip
-        if self.world == 1:
+        if not self.sharded:
             src, src_index = self.table.values, st.rows
         else:
             src, src_index = self.resp_back, self.send_index
+        if dense is not None:
+            dense = dense.contiguous().float()
         h.seqpool_cvm_fwd(src, src_index, self.ws.uid, lod, S, B, self.E, out, col_offset, sp.use_cvm,
                           sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter, sp.show_coeff, sp.clk_coeff,
                           sp.threshold, sp.quant_ratio, sp.embed_threshold_filter, sp.embed_threshold,
-                          sp.embed_thres_size)
+                          sp.embed_thres_size, dense, dense_col)
         return st
 
     def _pull_common(self, keys, lod, B, S) -> PullState:
@@ -194,17 +204,16 @@ class SparseEngine:
         self.ws.run(keys, False)
         h.fill_occurrence(lod, S, B, self.occ_slot, self.occ_ins)
         st = PullState(B=B, S=S, L=L, lod=lod, uid=self.ws.uid, perm=self.ws.perm, counts=self.ws.u_count)
-        if self.world == 1:
+        if not self.sharded:
             st.rows = self.table.probe(self.ws.uniq_h[:L], self.ws.u_count)
             if self.auto_insert and not self.test_mode:
                 self._auto_insert(st, L)
             return st
         # sharded: pack per-owner, exchange keys, owner-side dedup/probe/gather
-        h.shard_pack(self.ws.uniq_h, self.ws.u_count, self.world, self.C, self.send, self.send_index[:L],
-                     self.overflow)
+        h.shard_pack_hash(self.ws.uniq_h, self.ws.u_count, self.world, self.C, self.send, self.send_index,
+                          self.ocnt, self.overflow)
         self.comm.all_to_all_single(self.recv, self.send)
         self.ws_r.run(self.recv, True)
-        n = self.world * self.C
         rows_r = self.table.probe(self.ws_r.uniq_h, self.ws_r.u_count)
         if self.auto_insert and not self.test_mode:
             miss = (rows_r[: int(self.ws_r.u_count[0].item())] < 0)
@@ -212,8 +221,8 @@ class SparseEngine:
                 U = int(self.ws_r.u_count[0].item())
                 self.table.insert_mixed(self.ws_r.uniq_h[:U][miss], self.cfg.sgd)
                 rows_r = self.table.probe(self.ws_r.uniq_h, self.ws_r.u_count)
-        pulled = self.table.t.gather_pull(rows_r, self.ws_r.u_count, self.P)
-        h.gather_by_uid(pulled, self.ws_r.uid, self.resp, self.P)
+        # owner answers straight from the table rows (no intermediate pull buffer)
+        self.table.t.gather_rows_by_uid(rows_r, self.ws_r.uid, self.resp)
         self.comm.all_to_all_single(self.resp_back, self.resp)
         st.send_index = self.send_index[:L]
         st.rows_r = rows_r
@@ -237,7 +246,7 @@ class SparseEngine:
         h = self._hip
         L = st.L
         dout = dout.contiguous()
-        if self.world == 1:
+        if not self.sharded:
             push = self.push_buf
             push[:L].zero_()
             h.push_merge(dout, col_offset, cvm.contiguous(), sp.cvm_offset, sp.use_cvm, sp.clk_filter, self.E,
@@ -251,11 +260,19 @@ class SparseEngine:
                      self.ws.perm[:L], self.ws.uid, self.occ_slot, self.occ_ins, self._slot_ids(st.S),
                      self.ws.u_count[1:], self.push_send, st.send_index, float(bs_scale), self.dim)
         self.comm.all_to_all_single(self.push_recv, self.push_send)
-        self.push_merged.zero_()
-        h.push_merge_records(self.push_recv, self.ws_r.perm, self.ws_r.uid, self.ws_r.u_count[1:], self.dim,
-                             self.push_merged)
+        self._owner_update(st.rows_r, self.push_recv)
+
+    def _owner_update(self, rows_r: torch.Tensor, recv: torch.Tensor):
+        """Owner side of the push: each unique key got at most one merged record
+        per sender; merge them and apply sparse Adagrad in one kernel."""
         self._seed += 1
-        self.table.t.push_adagrad(st.rows_r, self.push_merged, self.ws_r.u_count, self._sgd_native, self._seed)
+        ws = self.ws_r
+        if self.table.t.push_adagrad_seg(rows_r, recv, ws.perm, ws.seg, ws.cnt, ws.u_count, self._sgd_native,
+                                         self._seed):
+            return
+        self.push_merged.zero_()
+        self._hip.push_merge_records(recv, ws.perm, ws.uid, ws.u_count[1:], self.dim, self.push_merged)
+        self.table.t.push_adagrad(rows_r, self.push_merged, ws.u_count, self._sgd_native, self._seed)
 
     def _slot_ids(self, S: int) -> torch.Tensor:
         if self.slot_ids.numel() < S:
@@ -263,7 +280,7 @@ class SparseEngine:
         return self.slot_ids
 
     def check_overflow(self) -> bool:
-        if self.world > 1 and self.is_gpu:
+        if self.sharded and self.is_gpu:
             return bool(self.overflow.item())
         return False
 
@@ -280,7 +297,7 @@ class SparseEngine:
             recs = torch.where((keys != -1).unsqueeze(1), pulled[uid.long().clamp(min=0)], torch.zeros(1))
             return recs[:, : self.E], st
         st = self._pull_common(keys, lod, B, S)
-        if self.world == 1:
+        if not self.sharded:
             pulled = self.table.t.gather_pull(st.rows, self.ws.u_count, self.P)
             recs = torch.empty(L, self.P, device=self.device)
             self._hip.gather_by_uid(pulled, self.ws.uid[:L], recs, self.P)
@@ -319,7 +336,7 @@ class SparseEngine:
             self.table.push_adagrad(st.rows, merged, self.cfg.sgd)
             return
         h = self._hip
-        if self.world == 1:
+        if not self.sharded:
             push = self.push_buf
             push[:L].zero_()
             h.push_merge_records(rec, self.ws.perm[:L], self.ws.uid, self.ws.u_count[1:], D, push[:L])
@@ -335,11 +352,7 @@ class SparseEngine:
         ok = idx >= 0
         self.push_send[idx[ok]] = merged[ok]
         self.comm.all_to_all_single(self.push_recv, self.push_send)
-        self.push_merged.zero_()
-        h.push_merge_records(self.push_recv, self.ws_r.perm, self.ws_r.uid, self.ws_r.u_count[1:], D,
-                             self.push_merged)
-        self._seed += 1
-        self.table.t.push_adagrad(st.rows_r, self.push_merged, self.ws_r.u_count, self._sgd_native, self._seed)
+        self._owner_update(st.rows_r, self.push_recv)
 
     # ------------------------------------------------------------------ CPU path
     def _cpu_pull_seqpool(self, keys, lod, B, S, out, col_offset, sp: SeqpoolParams) -> PullState:
@@ -348,7 +361,7 @@ class SparseEngine:
         uniq, uid = ref.dedup(keys[valid])
         full_uid = torch.full((L,), -1, dtype=torch.int32)
         full_uid[valid] = uid
-        if self.world > 1:
+        if self.sharded:
             return self._cpu_pull_sharded(keys, lod, B, S, out, col_offset, sp, uniq, full_uid)
         rows = self.table.probe(uniq)
         if self.auto_insert and not self.test_mode and bool((rows < 0).any()):
@@ -395,7 +408,7 @@ class SparseEngine:
         U = st.extra["U"]
         push = ref.push_merge(dout, cvm, st.uid, st.lod, st.S, st.B, U, self.dim, self._slot_ids(st.S), bs_scale,
                               sp.use_cvm, sp.clk_filter, col_offset, sp.cvm_offset)
-        if self.world == 1:
+        if not self.sharded:
             self.table.push_adagrad(st.rows, push, self.cfg.sgd)
             return
         e = st.extra

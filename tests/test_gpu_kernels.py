@@ -56,10 +56,22 @@ def test_dedup_matches_unique(hash_mode):
     assert bool((ws.uid[n - 100:] == -1).all())
     seg = ws.seg[: U + 1].long()
     perm = ws.perm[:nvalid].long()
-    # every segment holds occurrences of one key
+    counts = torch.bincount(uid, minlength=U)
+    if hash_mode:
+        # runs are contiguous but in no particular order: [seg[u], seg[u] + cnt[u])
+        assert torch.equal(ws.cnt[:U].long(), counts)
+        ends = seg[:U] + counts
+        order = torch.argsort(seg[:U])
+        assert int(seg[order[0]]) == 0 and torch.equal(seg[order[1:]], ends[order[:-1]])
+        assert int(ends[order[-1]]) == nvalid
+    else:
+        ends = seg[1:U + 1]
+    # every segment holds exactly the occurrences of one key
     for u in [0, 1, U // 2, U - 1]:
-        occ = perm[seg[u]:seg[u + 1]]
+        occ = perm[seg[u]:ends[u]]
+        assert occ.numel() == int(counts[u])
         assert bool((h[occ] == got[u]).all())
+    assert torch.equal(torch.sort(perm).values, torch.arange(nvalid, device=perm.device))
 
 
 def test_table_insert_probe_high_load():
