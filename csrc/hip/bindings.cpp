@@ -157,6 +157,43 @@ class GpuTable {
                                    ptr<int32_t>(perm), ptr<int32_t>(seg), ptr<int32_t>(cnt), ptr<int32_t>(n_dev),
                                    rows.numel(), cfg, seed, cur_stream());
   }
+  // single-shard push: merge per unique key + Adagrad in one pass (acc: all-zero
+  // scratch [>= U_cap, stride], kept zero; inc: [>= ceil(n/64)] int32 scratch)
+  bool push_merge_apply(const Tensor& dout, int col_offset, const Tensor& cvm, bool use_cvm, bool clk_filter, int E,
+                        const Tensor& perm, const Tensor& uid, const Tensor& occ_slot, const Tensor& occ_ins,
+                        const Tensor& slot_ids, const Tensor& n_valid, Tensor acc, Tensor inc, float bs_scale,
+                        const Tensor& rows, const SparseSGDConfig& cfg, uint64_t seed) {
+    check_cuda(dout, "dout");
+    check_cuda(cvm, "cvm");
+    check_cuda(acc, "acc");
+    check_cuda(rows, "rows");
+    PBX_CHECK(E == 3 + dim_, "push_merge_apply: E must be 3 + dim");
+    PBX_CHECK(cvm.dim() == 2 && cvm.size(1) == 2, "push_merge_apply: cvm must be [B, 2]");
+    PBX_CHECK(acc.dim() == 2 && acc.size(0) >= perm.numel() && acc.size(0) >= rows.numel(), "push_merge_apply: acc rows");
+    PBX_CHECK(inc.numel() * 64 >= perm.numel(), "push_merge_apply: inc too small");
+    PushMergeArgs a;
+    a.dout = ptr<float>(dout);
+    a.out_stride = (int)dout.size(1);
+    a.col_offset = col_offset;
+    a.cvm = ptr<float>(cvm);
+    a.cvm_offset = 2;
+    a.use_cvm = use_cvm;
+    a.clk_filter = clk_filter;
+    a.E = E;
+    a.perm = ptr<int32_t>(perm);
+    a.uid = ptr<int32_t>(uid);
+    a.occ_slot = ptr<int32_t>(occ_slot);
+    a.occ_ins = ptr<int32_t>(occ_ins);
+    a.slot_ids = ptr<float>(slot_ids);
+    a.n_valid = ptr<int32_t>(n_valid);
+    a.n = perm.numel();
+    a.push = ptr<float>(acc);
+    a.push_stride = (int)acc.size(1);
+    a.push_index = nullptr;
+    a.bs_scale = bs_scale;
+    a.dim = dim_;
+    return launch_push_merge_apply(a, view(), ptr<int64_t>(rows), ptr<int32_t>(inc), cfg, seed, cur_stream());
+  }
   void clear() {
     keys_.fill_(-1);
     fill_.zero_();
@@ -809,6 +846,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("push_adagrad", &GpuTable::push_adagrad)
       .def("gather_rows_by_uid", &GpuTable::gather_rows_by_uid)
       .def("push_adagrad_seg", &GpuTable::push_adagrad_seg)
+      .def("push_merge_apply", &GpuTable::push_merge_apply)
       .def("clear", &GpuTable::clear)
       .def_property_readonly("keys", &GpuTable::keys)
       .def_property_readonly("values", &GpuTable::values)

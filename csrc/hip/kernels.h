@@ -199,6 +199,13 @@ bool launch_push_adagrad_seg(const TableDev& t, const int64_t* rows, const float
                              const int32_t* perm, const int32_t* seg, const int32_t* cnt, const int32_t* n_dev,
                              int64_t n, const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s);
 
+// Single-shard fused push: merge the batch gradients per unique key and apply
+// Adagrad in place (a.push = acc scratch [U_cap, stride], kept all-zero;
+// inc [ceil(n/64)] scratch).  False if the dim/stride/layout has no fused
+// instantiation (caller falls back to launch_push_merge + launch_push_adagrad).
+bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const int64_t* rows, int32_t* inc,
+                             const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s);
+
 // ---------------------------------------------------------------- dense ops
 void launch_data_norm_fwd(const float* x, int N, int C, const float* bsize, const float* bsum,
                           const float* bsq, float* y, float* means, float* scales,

@@ -466,6 +466,93 @@ __global__ __launch_bounds__(256) void k_push_adagrad_seg(TableDev t, const int6
   adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
 }
 
+// Single-shard push, merge + Adagrad in one pass over the batch gradients.
+// perm lists the occurrences grouped by unique id (unique u owns the run
+// perm[seg[u] .. seg[u]+cnt[u])).  Each wave segmented-scans 64 consecutive
+// occurrences; a run lying wholly inside the wave is applied to its table
+// row straight from registers.  A run crossing a wave boundary is summed
+// into acc[u] (all-zero between steps) and the wave holding its first
+// occurrence files u in inc[] for k_push_finish, which applies it and
+// re-zeroes acc[u]: no merged-record buffer, no memset, one read of dout.
+// (Reference: PushMergeCopy + PushSparseGPU, box_wrapper.cu:417-512.)
+template <int D>
+__global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, TableDev t, const int64_t* __restrict__ rows,
+                                                          float* __restrict__ acc, int acc_stride,
+                                                          int32_t* __restrict__ inc, float neg_bs,
+                                                          SparseSGDConfig cfg, uint64_t seed) {
+  constexpr int Q = 3 + D;
+  const PushMergeArgs& a = src.a;
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t pv = (int64_t)*a.n_valid;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_base = p - lane;
+  if (wave_base >= pv) return;  // whole wave idle
+  int32_t u = -1, k = -1;
+  float g[Q];
+#pragma unroll
+  for (int c = 0; c < Q; ++c) g[c] = 0.f;
+  if (p < pv) {
+    k = a.perm[p];
+    u = a.uid[k];
+    src.load(k, g, Q);
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t uo = __shfl_up(u, off);
+#pragma unroll
+    for (int c = 0; c < Q; ++c) {
+      const float go = __shfl_up(g[c], off);
+      if (lane >= off && uo == u) g[c] += go;
+    }
+  }
+  const int32_t u_first = __shfl(u, 0), u_last = __shfl(u, 63);
+  int cn = 0, cp = 0;
+  if (lane == 63 && p + 1 < pv) cn = a.uid[a.perm[p + 1]] == u;
+  if (lane == 0 && wave_base > 0) cp = a.uid[a.perm[wave_base - 1]] == u;
+  const int cont_next = __shfl(cn, 63), cont_prev = __shfl(cp, 0);
+  if (lane == 63) inc[wave_base >> 6] = (cont_next && !(cont_prev && u_first == u_last)) ? u_last : -1;
+  const int32_t un = __shfl_down(u, 1);
+  const bool tail = lane == 63 || un != u;
+  if (p >= pv || u < 0 || !tail) return;
+  float rec[RowF<D>::kQ4 * 4];
+#pragma unroll
+  for (int c = 0; c < RowF<D>::kQ4 * 4; ++c) rec[c] = 0.f;
+  rec[kPushSlot] = src.slot(k);
+  rec[kPushShow] = g[0];
+  rec[kPushClick] = g[1];
+#pragma unroll
+  for (int c = 2; c < Q; ++c) rec[kPushEmbedG + (c - 2)] = g[c] * neg_bs;
+  const bool straddle = (u == u_last && cont_next) || (u == u_first && cont_prev);
+  if (!straddle) {
+    const int64_t r = rows[u];
+    if (r >= 0) adagrad_row<D>(t.values + r * (int64_t)t.stride, rec, cfg, seed, r);
+    return;
+  }
+  float* dst = acc + (int64_t)u * acc_stride;
+  dst[kPushSlot] = rec[kPushSlot];
+#pragma unroll
+  for (int c = 1; c < RowF<D>::kQ; ++c) atomicAdd(&dst[c], rec[c]);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_push_finish(TableDev t, const int64_t* __restrict__ rows,
+                                                     float* __restrict__ acc, int acc_stride,
+                                                     const int32_t* __restrict__ inc, const int32_t* n_valid,
+                                                     SparseSGDConfig cfg, uint64_t seed) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= ((int64_t)*n_valid + 63) / 64) return;
+  const int32_t u = inc[w];
+  if (u < 0) return;
+  float* ap = acc + (int64_t)u * acc_stride;
+  float g[RowF<D>::kQ4 * 4];
+  load_push<D>(ap, g);
+  float4* a4 = reinterpret_cast<float4*>(ap);
+#pragma unroll
+  for (int i = 0; i < RowF<D>::kQ4; ++i) a4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int64_t r = rows[u];
+  if (r >= 0) adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
+}
+
 // ---------------------------------------------------------------- sharding helpers
 __device__ __forceinline__ int64_t owner_lower_bound(const uint64_t* h, int64_t U, uint32_t o, uint32_t N) {
   int64_t lo = 0, hi = U;
@@ -697,6 +784,29 @@ bool launch_push_adagrad_seg(const TableDev& t, const int64_t* rows, const float
   else
     return false;
   return true;
+}
+
+bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const int64_t* rows, int32_t* inc,
+                             const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s) {
+  if (a.cvm_offset != 2 || a.push_index != nullptr || a.n_valid == nullptr || a.E != 3 + t.dim) return false;
+  if (a.n <= 0) return true;
+  const dim3 g(nblk(a.n)), gf(nblk((a.n + 63) / 64)), b(256);
+  DoutSource src{a};
+  const float neg_bs = -a.bs_scale;
+#define PBX_MERGE_APPLY(D)                                                                                   \
+  if (vec_push_ok<D>(t, a.push_stride)) {                                                                    \
+    hipLaunchKernelGGL(k_push_merge_apply<D>, g, b, 0, s, src, t, rows, a.push, a.push_stride, inc, neg_bs,  \
+                       cfg, seed);                                                                           \
+    hipLaunchKernelGGL(k_push_finish<D>, gf, b, 0, s, t, rows, a.push, a.push_stride, inc, a.n_valid, cfg,   \
+                       seed);                                                                                \
+    return true;                                                                                             \
+  }
+  PBX_MERGE_APPLY(8)
+  PBX_MERGE_APPLY(16)
+  PBX_MERGE_APPLY(4)
+  PBX_MERGE_APPLY(32)
+#undef PBX_MERGE_APPLY
+  return false;
 }
 
 void launch_shard_pack_hash(const uint64_t* uniq_h, const int32_t* u_count, int64_t u_cap, int nranks, int64_t cap,

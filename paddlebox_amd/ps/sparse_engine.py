@@ -133,6 +133,10 @@ class SparseEngine:
                 self.push_merged = torch.empty(n, self.Q, device=self.device)
             else:
                 self.push_buf = torch.empty(self.max_keys, self.Q, device=self.device)
+                # fused merge+Adagrad scratch: straddling-run accumulators
+                # (kept all-zero between steps) and per-wave run owners
+                self.push_acc = torch.zeros(self.max_keys, self.Q, device=self.device)
+                self.push_inc = torch.empty((self.max_keys + 63) // 64 + 1, dtype=torch.int32, device=self.device)
         else:
             self.table = CpuSparseTable(self.dim)
         self.slot_ids = torch.tensor(slot_ids if slot_ids is not None else [], dtype=torch.float32,
@@ -247,6 +251,15 @@ class SparseEngine:
         L = st.L
         dout = dout.contiguous()
         if not self.sharded:
+            if sp.cvm_offset == 2 and cvm.shape[1] == 2:
+                self._seed += 1
+                if self.table.t.push_merge_apply(dout, col_offset, cvm.contiguous(), sp.use_cvm, sp.clk_filter, self.E,
+                                                 self.ws.perm[:L], self.ws.uid, self.occ_slot, self.occ_ins,
+                                                 self._slot_ids(st.S), self.ws.u_count[1:], self.push_acc,
+                                                 self.push_inc, float(bs_scale), st.rows, self._sgd_native,
+                                                 self._seed):
+                    return
+                self._seed -= 1
             push = self.push_buf
             push[:L].zero_()
             h.push_merge(dout, col_offset, cvm.contiguous(), sp.cvm_offset, sp.use_cvm, sp.clk_filter, self.E,
