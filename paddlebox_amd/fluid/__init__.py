@@ -8,8 +8,9 @@ paddlebox_amd.fluid as fluid``, or ``import paddle.fluid as fluid`` via the
 ``paddle`` alias package at the repo root); programs are lowered to the
 fused gfx950 kernels (see ``lowering.py``).
 """
-from . import contrib, core, initializer, io, layers, optimizer  # noqa: F401
+from . import contrib, core, initializer, io, layers, optimizer, transpiler  # noqa: F401
 from .dataset import DatasetFactory  # noqa: F401
+from .transpiler import DistributeTranspiler, DistributeTranspilerConfig  # noqa: F401
 from .executor import CompiledProgram, Executor  # noqa: F401
 from .framework import (CPUPlace, CUDAPinnedPlace, CUDAPlace, LoDTensor, Parameter, ParamAttr,  # noqa: F401
                         Program, Scope, Variable, WeightNormParamAttr, cpu_places, create_lod_tensor, cuda_places,

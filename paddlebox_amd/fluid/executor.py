@@ -197,11 +197,27 @@ class Session:
                             lr = v / max(spec["lr"], 1e-30)
                 groups.setdefault(lr, []).append(st)
         world = dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
+        coll = getattr(self.program, "_collective", None) or {}
+        sharded = coll.get("mode") == "sharding" and spec["type"] in ("adam", "adamw")
+        if sync_mode is None and coll:
+            # transpiler / fleet choice (py/fluid/transpiler/collective.py modes)
+            sync_mode = {"grad_allreduce": "grad_allreduce", "local_sgd": "local_sgd", "allgather": "allgather",
+                         "sharding": "none"}.get(coll.get("mode"), "grad_allreduce")
+            sync_k = int(coll.get("k", sync_k))
         if sync_mode is None:
             sync_mode = "grad_allreduce" if world > 1 else "none"
         for lr_mult, ps in groups.items():
             arena = DenseArena(ps, self.device)
             self.arenas.append(arena)
+            if sharded:
+                # ZeRO-1: reduce-scatter grads, Adam on this rank's slice, all-gather params
+                from ..parallel.sharding import ShardedFlatAdam
+
+                self.opts.append(ShardedFlatAdam(arena, spec["lr"] * lr_mult, spec.get("beta1", 0.9),
+                                                 spec.get("beta2", 0.999), spec.get("epsilon", 1e-8),
+                                                 spec.get("weight_decay", 0.0), self.group))
+                self.syncs.append(DenseSync(arena, "none", 1, self.group))
+                continue
             self.opts.append(_make_opt(spec, arena, lr_mult))
             self.syncs.append(DenseSync(arena, sync_mode, sync_k, self.group))
         # arena rebinding moved the storage: re-point logical views
@@ -267,9 +283,7 @@ class Session:
             a.zero_grad()
         loss.float().sum().backward()
         for s, o in zip(self.syncs, self.opts):
-            s.before_step()
-            o.step(s.grad_scale())
-            s.after_step()
+            s.apply(o)
 
     def fetch(self, ctx: ExecContext, fetch_list, return_numpy=True):
         out = []

@@ -351,6 +351,7 @@ class Program:
         self._version = 0
         self._pipeline_opt: Optional[dict] = None
         self._optimize: Optional[dict] = None  # set by Optimizer.minimize
+        self._collective: Optional[dict] = None  # set by transpiler / fleet (dense sync mode)
         self._fleet_opt: Optional[dict] = None
         self._is_test = False
         self._startup: Optional["Program"] = None
@@ -397,6 +398,7 @@ class Program:
         p._is_test = for_test
         if not for_test:
             p._optimize = self._optimize
+            p._collective = self._collective
             p._pipeline_opt = self._pipeline_opt
         p._version = self._version
         return p

@@ -109,9 +109,29 @@ class DenseSync:
         if self.active and self.mode == "grad_allreduce":
             dist.all_reduce(self.a.grad, group=self.group)
 
+    def apply(self, opt):
+        """Sync + optimizer update for one step, every mode.
+
+        ``allgather`` is the transpiler's MultiThread all_gather mode
+        (``py/fluid/transpiler/collective.py:499-636``): every rank gathers all
+        ranks' gradients and runs one optimizer update per gathered gradient,
+        in rank order, so all replicas stay identical."""
+        if self.active and self.mode == "allgather":
+            g = self.a.grad
+            parts = [torch.empty_like(g) for _ in range(self.world)]
+            dist.all_gather(parts, g, group=self.group)
+            for p in parts:
+                g.copy_(p)
+                opt.step(1.0 / self.world)
+            self.after_step()
+            return
+        self.before_step()
+        opt.step(self.grad_scale())
+        self.after_step()
+
     def after_step(self):
         self.steps += 1
-        if self.active and self.mode == "kstep" and self.steps % self.k == 0:
+        if self.active and self.mode in ("kstep", "local_sgd") and self.steps % self.k == 0:
             self.sync_params()
 
     def sync_params(self):

@@ -309,6 +309,8 @@ class BoxPSTrainer:
         d = self.desc
         if self.world <= 1:
             return "none", 1
+        if getattr(self.program, "_collective", None):
+            return None, 1  # the transpiler / fleet strategy decides (Session._build_optimizer)
         if d.sync_dense_mode in (SYNC_KSTEP_ALL,):
             return "kstep", d.sync_weight_step
         if d.sync_dense_mode == SYNC_KSTEP_NODE:

@@ -16,13 +16,21 @@ import torch
 
 
 class StageTimers:
-    def __init__(self, device=None, enabled: bool = True, roctx: bool = False):
+    def __init__(self, device=None, enabled: bool = True, roctx: bool = False, trace: bool = False,
+                 rank: int = 0):
         self.device = device
         self.enabled = enabled
         self.roctx = roctx and torch.cuda.is_available()
         self.gpu_spans: Dict[str, List] = defaultdict(list)
         self.cpu_spans: Dict[str, float] = defaultdict(float)
         self.counts: Dict[str, int] = defaultdict(int)
+        # chrome-trace recording (tools/timeline.py equivalent): host spans and,
+        # on the GPU, event pairs timed against one origin event
+        self.trace = trace
+        self.rank = rank
+        self._events: List[tuple] = []
+        self._t0 = time.perf_counter()
+        self._origin = None
 
     @contextmanager
     def span(self, name: str):
@@ -34,15 +42,22 @@ class StageTimers:
             torch.cuda.nvtx.range_push(name)
         t0 = time.perf_counter()
         if use_gpu:
+            if self.trace and self._origin is None:
+                self._origin = torch.cuda.Event(enable_timing=True)
+                self._origin.record()
+                self._origin_cpu = t0
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
         try:
             yield
         finally:
+            t1 = time.perf_counter()
             if use_gpu:
                 e.record()
                 self.gpu_spans[name].append((s, e))
-            self.cpu_spans[name] += time.perf_counter() - t0
+            if self.trace:
+                self._events.append((name, t0, t1, (s, e) if use_gpu else None))
+            self.cpu_spans[name] += t1 - t0
             self.counts[name] += 1
             if self.roctx:
                 torch.cuda.nvtx.range_pop()
@@ -59,6 +74,29 @@ class StageTimers:
             self.cpu_spans.clear()
             self.counts.clear()
         return out
+
+    def chrome_trace(self) -> Dict:
+        """Recorded spans as a chrome://tracing / Perfetto JSON object: one
+        "host" and one "gpu" track per rank (pid = rank)."""
+        if any(ev[3] is not None for ev in self._events):
+            torch.cuda.synchronize()
+        out = []
+        for name, t0, t1, ge in self._events:
+            out.append({"name": name, "ph": "X", "pid": self.rank, "tid": "host",
+                        "ts": (t0 - self._t0) * 1e6, "dur": (t1 - t0) * 1e6})
+            if ge is not None and self._origin is not None:
+                s, e = ge
+                base = (self._origin_cpu - self._t0) * 1e6
+                out.append({"name": name, "ph": "X", "pid": self.rank, "tid": "gpu",
+                            "ts": base + self._origin.elapsed_time(s) * 1e3, "dur": s.elapsed_time(e) * 1e3})
+        return {"traceEvents": out, "displayTimeUnit": "ms"}
+
+    def export_chrome_trace(self, path: str) -> str:
+        import json
+
+        with open(path, "w") as f:
+            json.dump(self.chrome_trace(), f)
+        return path
 
     def format(self, reset: bool = True) -> str:
         r = self.report(reset)
