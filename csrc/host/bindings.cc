@@ -237,6 +237,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_pipe_command", &SlotDataset::set_pipe_command)
       .def("set_thread_num", &SlotDataset::set_thread_num)
       .def("set_parse", &SlotDataset::set_parse)
+      .def("set_so_parser", &SlotDataset::set_so_parser)
+      .def("has_so_parser", &SlotDataset::has_so_parser)
       .def("load_into_memory", &SlotDataset::load_into_memory, py::call_guard<py::gil_scoped_release>())
       .def("preload_into_memory", &SlotDataset::preload_into_memory)
       .def("wait_preload_done", &SlotDataset::wait_preload_done, py::call_guard<py::gil_scoped_release>())

@@ -1,0 +1,50 @@
+// Instance-parser plugin ABI: user parsers shipped as shared objects and
+// loaded with dlopen, chosen per dataset by `set_so_parser_name`.
+//
+// Behaviour reproduced (not code): the reference's ISlotParser plugin contract
+// (fw/data_feed.h:1964-2015 -- Init(slots), ParseOneInstance(line, GetInsFunc)
+// which may emit any number of instances per line; loader SlotInsParserMgr
+// data_feed.cc:3604-3670).  The reference ABI passes C++ objects
+// (SlotRecord, std::function) across the .so boundary; ours is a plain C ABI
+// so a plugin needs no headers beyond this one and no matching C++ runtime.
+//
+// A plugin exports three symbols:
+//
+//   void* pbx_parser_create(int nslots, const char* const* slot_names,
+//                           const char* slot_types);   // 'u' uint64 / 'f' float
+//   int   pbx_parser_parse_line(void* parser, const char* line, size_t len,
+//                               const pbx_ins_sink* sink);
+//         -> number of instances emitted (0 = line dropped), < 0 = parse error
+//   void  pbx_parser_destroy(void* parser);
+//
+// For every instance the plugin calls `add_u64` / `add_f32` for the slots it
+// has values for (slot = index into the slot list given at create time; the
+// values of slots the dataset does not use are discarded by the host),
+// optionally `set_meta`, then `commit`.  `parse_line` is called concurrently
+// from the loader threads with the same parser handle, so it must be
+// re-entrant (keep per-line state on the stack).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pbx_ins_sink {
+  void* ctx;
+  void (*add_u64)(void* ctx, int slot, const uint64_t* v, int n);
+  void (*add_f32)(void* ctx, int slot, const float* v, int n);
+  void (*set_meta)(void* ctx, const char* ins_id, int ins_id_len, uint64_t search_id, uint32_t cmatch,
+                   uint32_t rank);
+  // returns 1 if the instance was kept (it has at least one sparse feasign)
+  int (*commit)(void* ctx);
+} pbx_ins_sink;
+
+typedef void* (*pbx_parser_create_fn)(int, const char* const*, const char*);
+typedef int (*pbx_parser_parse_line_fn)(void*, const char*, size_t, const pbx_ins_sink*);
+typedef void (*pbx_parser_destroy_fn)(void*);
+
+#ifdef __cplusplus
+}
+#endif

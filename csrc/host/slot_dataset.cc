@@ -1,5 +1,7 @@
 #include "slot_dataset.h"
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
@@ -15,6 +17,7 @@
 #include <unordered_set>
 
 #include "../common/pbx_common.h"
+#include "parser_plugin.h"
 #include "runtime.h"
 
 namespace pbx {
@@ -136,7 +139,135 @@ static bool parse_logkey(const char* s, size_t len, uint64_t* sid, uint32_t* cm,
   return true;
 }
 
+// ---------------------------------------------------------------- plugin
+struct SlotDataset::Plugin {
+  void* so = nullptr;
+  void* parser = nullptr;
+  pbx_parser_parse_line_fn parse = nullptr;
+  pbx_parser_destroy_fn destroy = nullptr;
+  ~Plugin() {
+    if (parser && destroy) destroy(parser);
+    if (so) dlclose(so);
+  }
+};
+
+namespace {
+// per-instance staging handed to the plugin through pbx_ins_sink
+struct SinkCtx {
+  const std::vector<int>* u_idx;
+  const std::vector<int>* f_idx;
+  const std::vector<SlotDesc>* slots;
+  bool keep_ins_id;
+  bool need_sparse;
+  RecordStore* st;
+  std::vector<std::vector<uint64_t>> u;
+  std::vector<std::vector<float>> f;
+  std::string ins_id;
+  uint64_t sid = 0;
+  uint32_t cm = 0, rk = 0;
+  int64_t sparse = 0;
+  int kept = 0;
+  void clear() {
+    for (auto& v : u) v.clear();
+    for (auto& v : f) v.clear();
+    ins_id.clear();
+    sid = 0;
+    cm = rk = 0;
+    sparse = 0;
+  }
+};
+
+void sink_add_u64(void* c, int slot, const uint64_t* v, int n) {
+  SinkCtx* s = (SinkCtx*)c;
+  if (slot < 0 || slot >= (int)s->slots->size() || n <= 0) return;
+  const int j = (*s->u_idx)[slot];
+  if (j < 0) return;  // unused or float slot
+  s->u[j].insert(s->u[j].end(), v, v + n);
+  if (!(*s->slots)[slot].dense) s->sparse += n;
+}
+
+void sink_add_f32(void* c, int slot, const float* v, int n) {
+  SinkCtx* s = (SinkCtx*)c;
+  if (slot < 0 || slot >= (int)s->slots->size() || n <= 0) return;
+  const int j = (*s->f_idx)[slot];
+  if (j < 0) return;
+  s->f[j].insert(s->f[j].end(), v, v + n);
+}
+
+void sink_set_meta(void* c, const char* id, int len, uint64_t sid, uint32_t cm, uint32_t rk) {
+  SinkCtx* s = (SinkCtx*)c;
+  if (id && len > 0) s->ins_id.assign(id, (size_t)len);
+  s->sid = sid;
+  s->cm = cm;
+  s->rk = rk;
+}
+
+int sink_commit(void* c) {
+  SinkCtx* s = (SinkCtx*)c;
+  int ok = !(s->need_sparse && s->sparse == 0);
+  if (ok) {
+    RecordStore* st = s->st;
+    for (auto& v : s->u) {
+      st->u64.insert(st->u64.end(), v.begin(), v.end());
+      st->u64_off.push_back((int64_t)st->u64.size());
+    }
+    for (auto& v : s->f) {
+      st->f32.insert(st->f32.end(), v.begin(), v.end());
+      st->f32_off.push_back((int64_t)st->f32.size());
+    }
+    if (s->keep_ins_id) st->ins_id.push_back(s->ins_id);
+    st->search_id.push_back(s->sid);
+    st->cmatch.push_back(s->cm);
+    st->rank.push_back(s->rk);
+    s->kept += 1;
+  }
+  s->clear();
+  return ok;
+}
+}  // namespace
+
+void SlotDataset::set_so_parser(const std::string& path) {
+  plugin_.reset();
+  if (path.empty()) return;
+  auto pl = std::make_shared<Plugin>();
+  pl->so = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+  if (!pl->so) throw std::runtime_error(std::string("so parser: dlopen failed: ") + dlerror());
+  auto create = (pbx_parser_create_fn)dlsym(pl->so, "pbx_parser_create");
+  pl->parse = (pbx_parser_parse_line_fn)dlsym(pl->so, "pbx_parser_parse_line");
+  pl->destroy = (pbx_parser_destroy_fn)dlsym(pl->so, "pbx_parser_destroy");
+  if (!create || !pl->parse || !pl->destroy)
+    throw std::runtime_error("so parser " + path + ": missing pbx_parser_{create,parse_line,destroy}");
+  std::vector<const char*> names;
+  std::string types;
+  for (auto& s : slots_) {
+    names.push_back(s.name.c_str());
+    types.push_back(s.type);
+  }
+  pl->parser = create((int)slots_.size(), names.data(), types.c_str());
+  if (!pl->parser) throw std::runtime_error("so parser " + path + ": pbx_parser_create returned null");
+  plugin_ = pl;
+}
+
+bool SlotDataset::parse_plugin_line(const char* line, size_t len, RecordStore* st) const {
+  thread_local SinkCtx ctx;
+  ctx.u_idx = &u_idx_;
+  ctx.f_idx = &f_idx_;
+  ctx.slots = &slots_;
+  ctx.keep_ins_id = parse_.parse_ins_id || parse_.parse_logkey;
+  ctx.need_sparse = !sparse_slots_.empty();
+  ctx.st = st;
+  ctx.u.resize(store_.nu);
+  ctx.f.resize(store_.nf);
+  ctx.clear();
+  ctx.kept = 0;
+  pbx_ins_sink sink{&ctx, sink_add_u64, sink_add_f32, sink_set_meta, sink_commit};
+  const int n = plugin_->parse(plugin_->parser, line, len, &sink);
+  ctx.clear();  // an instance the plugin never committed is discarded
+  return n > 0 && ctx.kept > 0;
+}
+
 bool SlotDataset::parse_line(const char* str, size_t len, RecordStore* st) const {
+  if (plugin_) return parse_plugin_line(str, len, st);
   const char* end = str + len;
   char* p = const_cast<char*>(str);
   std::string ins_id;

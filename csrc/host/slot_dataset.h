@@ -61,6 +61,9 @@ class SlotDataset {
   void set_pipe_command(const std::string& cmd) { pipe_command_ = cmd; }
   void set_thread_num(int n) { threads_ = n < 1 ? 1 : n; }
   void set_parse(const ParseConfig& c) { parse_ = c; }
+  // dlopen an instance-parser plugin (parser_plugin.h); "" = built-in parser
+  void set_so_parser(const std::string& path);
+  bool has_so_parser() const { return plugin_ != nullptr; }
 
   // parse one line into store (returns false if dropped / no sparse feasign)
   bool parse_line(const char* line, size_t len, RecordStore* st) const;
@@ -113,6 +116,9 @@ class SlotDataset {
   int64_t bad_lines() const { return bad_lines_; }
 
  private:
+  struct Plugin;
+  bool parse_plugin_line(const char* line, size_t len, RecordStore* st) const;
+  std::shared_ptr<Plugin> plugin_;
   int64_t load_files(const std::vector<std::string>& files, RecordStore* out);
   std::vector<SlotDesc> slots_;
   // index mapping: slot i -> used uint64 idx / used float idx (-1 = unused)

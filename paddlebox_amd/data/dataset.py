@@ -202,6 +202,8 @@ class PadBoxSlotDataset(DatasetBase):
         pc.parse_logkey = self.parse_logkey
         pc.sample_rate = self.sample_rate
         self._native.set_parse(pc)
+        if self.so_parser_name:  # user instance-parser plugin (csrc/host/parser_plugin.h)
+            self._native.set_so_parser(os.path.abspath(self.so_parser_name))
         self._native.set_pipe_command(self.pipe_command)
         self._native.set_thread_num(self.thread_num)
         self._configured = True
