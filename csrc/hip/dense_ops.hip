@@ -150,26 +150,52 @@ __global__ void k_sigmoid_logloss(const float* __restrict__ z, const float* __re
 // gradient in ONE launch (replaces the add, loss zero-fill, loss kernel,
 // scale and bias-grad reduction kernels).  One 1024-thread block: the loss
 // mean is a plain store, no zero-initialised accumulator.
-__global__ __launch_bounds__(1024) void k_logit_loss(const float* __restrict__ a, const float* __restrict__ b,
-                                                     const float* __restrict__ y, int B, float* __restrict__ pred,
-                                                     float* __restrict__ dz, float* __restrict__ loss_mean) {
-  __shared__ float red[16];
+// One element per thread over many blocks (a single 1024-thread block left
+// the chip idle for ~11 us at B=8192).  Each block writes its partial loss
+// sum; the last block to arrive (ticket counter) adds the partials in block
+// order, so the mean is deterministic, and re-arms the ticket for the next
+// launch (graph-replay safe; one loss launch in flight per device).
+constexpr int kLossBlock = 256;
+constexpr int kLossMaxBlocks = 1024;
+__device__ float g_loss_part[kLossMaxBlocks];
+__device__ unsigned int g_loss_ticket;
+
+__global__ __launch_bounds__(kLossBlock) void k_logit_loss(const float* __restrict__ a, const float* __restrict__ b,
+                                                           const float* __restrict__ y, int B, int per_thread,
+                                                           float* __restrict__ pred, float* __restrict__ dz,
+                                                           float* __restrict__ loss_mean) {
+  __shared__ float red[kLossBlock / 64];
+  __shared__ bool last;
   const float inv = 1.f / (float)B;
   float l = 0.f;
-  for (int i = threadIdx.x; i < B; i += blockDim.x) {
-    const float zi = a[i] + (b ? b[i] : 0.f), yi = y[i];
-    const float p = 1.f / (1.f + expf(-zi));
-    pred[i] = p;
-    l += fmaxf(zi, 0.f) - zi * yi + log1pf(expf(-fabsf(zi)));
-    dz[i] = (p - yi) * inv;
+  const int base = blockIdx.x * kLossBlock * per_thread + threadIdx.x;
+  for (int k = 0; k < per_thread; ++k) {
+    const int i = base + k * kLossBlock;
+    if (i < B) {
+      const float zi = a[i] + (b ? b[i] : 0.f), yi = y[i];
+      const float p = 1.f / (1.f + __expf(-zi));
+      pred[i] = p;
+      l += fmaxf(zi, 0.f) - zi * yi + log1pf(__expf(-fabsf(zi)));
+      dz[i] = (p - yi) * inv;
+    }
   }
   for (int off = 32; off > 0; off >>= 1) l += __shfl_down(l, off);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
   __syncthreads();
   if (threadIdx.x == 0) {
     float s = 0.f;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+    for (int w = 0; w < kLossBlock / 64; ++w) s += red[w];
+    g_loss_part[blockIdx.x] = s;
+    __threadfence();
+    last = atomicAdd(&g_loss_ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __threadfence();
+    float s = 0.f;
+    for (unsigned int k = 0; k < gridDim.x; ++k) s += __hip_atomic_load(&g_loss_part[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     loss_mean[0] = s * inv;
+    g_loss_ticket = 0u;
   }
 }
 
@@ -325,7 +351,10 @@ void launch_fm_bwd(const float* x, const float* dout, int B, int S, int D, int r
 void launch_logit_loss(const float* a, const float* b, const float* label, int B, float* pred, float* dz,
                        float* loss_mean, hipStream_t s) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(k_logit_loss, dim3(1), dim3(1024), 0, s, a, b, label, B, pred, dz, loss_mean);
+  int per_thread = 1;
+  while ((B + kLossBlock * per_thread - 1) / (kLossBlock * per_thread) > kLossMaxBlocks) per_thread *= 2;
+  const int grid = (B + kLossBlock * per_thread - 1) / (kLossBlock * per_thread);
+  hipLaunchKernelGGL(k_logit_loss, dim3(grid), dim3(kLossBlock), 0, s, a, b, label, B, per_thread, pred, dz, loss_mean);
 }
 
 void launch_sigmoid_logloss(const float* logit, const float* label, int B, float* pred,

@@ -20,6 +20,8 @@
 //   bwd   dZ_{i-1} = (dZ_i W_i) . [X_i>0] -> dZ_{i-1}, dZ_{i-1}^T      EPI_DX
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace pbx {
@@ -275,6 +277,18 @@ void launch_mlp_gemm(const MlpGemmArgs& g, int epi, hipStream_t s) {
   if (epi == MLP_EPI_DW) {  // 64x64 tiles: dW is only ~400 x 400
     dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, splits);
     hipLaunchKernelGGL((k_gemm_nt<MLP_EPI_DW, 64, 64, 2>), grid, dim3(256), 0, s, g);
+    return;
+  }
+  // PBX_MLP_TILE=64: 64 x 64 tiles (2 x 2 waves) -- twice the work-groups for
+  // latency hiding at small N; default 128 x 64.
+  static const int tile = [] {
+    const char* e = getenv("PBX_MLP_TILE");
+    return e ? atoi(e) : 128;
+  }();
+  if (tile == 64) {
+    dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, splits);
+    if (epi == MLP_EPI_FWD) hipLaunchKernelGGL((k_gemm_nt<MLP_EPI_FWD, 64, 64, 2>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((k_gemm_nt<MLP_EPI_DX, 64, 64, 2>), grid, dim3(256), 0, s, g);
     return;
   }
   // 128 x 64 tiles, 4 waves stacked in M (each 32 x 64: the A fragment feeds 2 MFMAs)

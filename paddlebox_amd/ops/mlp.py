@@ -12,6 +12,8 @@ from __future__ import annotations
 
 from typing import List, Optional, Sequence
 
+import os
+
 import torch
 from torch import nn
 
@@ -134,7 +136,8 @@ class FusedMLP(nn.Module):
         self.b_out = nn.Parameter(torch.zeros(1))
         self._bf16: List[torch.Tensor] = []
         self.k_split = 512
-        self.k_split_dw = 1024  # split-K over the batch for the workspace dW GEMMs
+        # split-K over the batch for the workspace dW GEMMs
+        self.k_split_dw = int(os.environ.get("PBX_KSPLIT_DW", "1024"))
         self._ws = None
 
     # ---- workspace path (csrc/hip/mlp.hip): persistent padded activations +

@@ -396,3 +396,19 @@ def test_mlp_workspace_matches_fp32(M, dims):
         torch.testing.assert_close(b.grad, g, rtol=2e-2, atol=1e-2 * float(g.abs().max()))
     torch.testing.assert_close(mlp.w_out.grad.view(-1), g_wo, rtol=2e-2, atol=1e-2 * float(g_wo.abs().max()))
     torch.testing.assert_close(x0.grad[:, :dims[0]].float(), dx, rtol=2e-2, atol=1e-2 * float(dx.abs().max()))
+
+
+@pytest.mark.parametrize("B", [1, 300, 8192, 300001])
+def test_logit_loss_multiblock(B):
+    torch.manual_seed(B)
+    a = torch.randn(B, device=DEV) * 3
+    b = torch.randn(B, device=DEV)
+    y = (torch.rand(B, device=DEV) < 0.3).float()
+    for _ in range(2):  # second launch checks the ticket re-arms
+        loss, pred, dz = hip().logit_loss(a, b, y)
+    z = (a + b).double()
+    pe = torch.sigmoid(z)
+    le = torch.nn.functional.binary_cross_entropy_with_logits(z, y.double())
+    torch.testing.assert_close(pred.double(), pe, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dz.double(), (pe - y.double()) / B, rtol=1e-5, atol=1e-9)
+    assert float(loss) == pytest.approx(float(le), rel=1e-5)
