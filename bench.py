@@ -50,8 +50,8 @@ def log(rank, *a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--batch-per-gpu", type=int, default=8192)
     ap.add_argument("--total-features", type=float, default=1e9)
     ap.add_argument("--alpha", type=float, default=1.05)

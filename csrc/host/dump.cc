@@ -98,6 +98,7 @@ DumpWriter::DumpWriter(const std::string& dir, int device_id, int n_threads, siz
   if (n_threads <= 0) n_threads = 1;
   ::mkdir(dir.c_str(), 0777);
   fds_.resize(n_threads);
+  fd_mu_.reset(new std::mutex[n_threads]);
   pool_.reset(new ThreadPool(n_threads));
 }
 
@@ -115,6 +116,12 @@ void DumpWriter::open_if_needed(int tid) {
   f.len = 0;
   std::lock_guard<std::mutex> lk(mu_);
   opened_.emplace_back(name);
+}
+
+void DumpWriter::emit(int tid, const std::string& s) {
+  std::lock_guard<std::mutex> lk(fd_mu_[tid]);
+  open_if_needed(tid);
+  write(tid, s);
 }
 
 void DumpWriter::write(int tid, const std::string& s) {
@@ -171,15 +178,11 @@ int64_t DumpWriter::dump_fields(const std::vector<std::string>& lineids, const s
         s.push_back('\n');
         ++lines;
         if (s.size() > (4u << 20)) {
-          open_if_needed(tid);
-          write(tid, s);
+          emit(tid, s);
           s.clear();
         }
       }
-      if (!s.empty()) {
-        open_if_needed(tid);
-        write(tid, s);
-      }
+      if (!s.empty()) emit(tid, s);
     }));
   }
   for (auto& f : fs) f.get();
@@ -199,12 +202,13 @@ void DumpWriter::dump_params(int batch_id, const std::vector<std::string>& names
     }
     s.push_back('\n');
   }
-  open_if_needed(0);
-  write(0, s);
+  emit(0, s);
 }
 
 void DumpWriter::flush() {
-  for (auto& f : fds_) {
+  for (size_t t = 0; t < fds_.size(); ++t) {
+    std::lock_guard<std::mutex> lk(fd_mu_[t]);
+    Fd& f = fds_[t];
     if (f.fd < 0) continue;
     if (f.len > 0) ::fsync(f.fd);
     ::close(f.fd);
@@ -213,6 +217,9 @@ void DumpWriter::flush() {
   }
 }
 
-std::vector<std::string> DumpWriter::files() const { return opened_; }
+std::vector<std::string> DumpWriter::files() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return opened_;
+}
 
 }  // namespace pbx

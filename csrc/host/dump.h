@@ -42,12 +42,16 @@ class DumpWriter {
   };
   void open_if_needed(int tid);
   void write(int tid, const std::string& s);
+  // open + write under the slot's own lock: a slot is touched by whichever pool
+  // thread runs its task, by dump_params on the caller thread and by flush()
+  void emit(int tid, const std::string& s);
   std::string dir_;
   int device_id_;
   size_t max_len_;
   std::vector<Fd> fds_;
+  std::unique_ptr<std::mutex[]> fd_mu_;  // one per Fd slot (uncontended)
   std::vector<std::string> opened_;
-  std::mutex mu_;
+  mutable std::mutex mu_;
   std::unique_ptr<ThreadPool> pool_;
 };
 
