@@ -64,6 +64,10 @@ def main():
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--diag-windows", type=int, default=0,
                     help="after the measurement, time this many more K-step windows (stderr only)")
+    ap.add_argument("--graph-warm", type=int, default=32,
+                    help="load+replay cycles run right after capture (runtime warm-up, part of graph setup)")
+    ap.add_argument("--host-diag", action="store_true",
+                    help="after the measurement, split host time into replay / H2D load (stderr only)")
     ap.add_argument("--force-collectives", action="store_true",
                     help="run the multi-GPU exchange/all-reduce path even on 1 rank (rehearsal)")
     args = ap.parse_args()
@@ -141,7 +145,8 @@ def main():
             from paddlebox_amd.runtime.graph_step import GraphedTrainStep
 
             graphed = GraphedTrainStep(train_step, host_batches[0], device)
-            log(rank, "[bench] training step captured into HIP graphs")
+            graphed.warm(host_batches, replays=args.graph_warm)
+            log(rank, f"[bench] training step captured into HIP graphs ({args.graph_warm} warm replays)")
         except Exception as e:  # pragma: no cover - depends on runtime
             log(rank, f"[bench] graph capture failed ({e!r}); running eagerly")
             graphed = None
@@ -199,6 +204,21 @@ def main():
             run(args.warmup + args.steps * (w + 1) + i)
         torch.cuda.synchronize()
         log(rank, f"[bench] diag window {w}: {(time.perf_counter() - t0w) / args.steps * 1e3:.4f} ms/step")
+    if args.host_diag and graphed is not None:
+        # where the host time of a step goes: replay alone, H2D load alone, both
+        for name, fn in (("replay", lambda i: graphed.graphs[i % 2][0].replay()),
+                         ("load", lambda i: graphed.load(i % 2, host_batches[i % nb])),
+                         ("load+run", lambda i: run(i))):
+            for w in range(3):
+                torch.cuda.synchronize()
+                t0w = time.perf_counter()
+                for i in range(args.steps):
+                    fn(i)
+                th = time.perf_counter() - t0w
+                torch.cuda.synchronize()
+                tw = time.perf_counter() - t0w
+                log(rank, f"[bench] host-diag {name} window {w}: host {th / args.steps * 1e3:.4f} "
+                          f"wall {tw / args.steps * 1e3:.4f} ms/step")
     overflow = engine.check_overflow()
     samples = B * world * args.steps
     value = samples / dt
