@@ -66,6 +66,8 @@ def main():
                     help="after the measurement, time this many more K-step windows (stderr only)")
     ap.add_argument("--graph-warm", type=int, default=32,
                     help="load+replay cycles run right after capture (runtime warm-up, part of graph setup)")
+    ap.add_argument("--trace-steps", type=int, default=0,
+                    help="before warmup, print per-step host time of load / replay for this many steps (stderr)")
     ap.add_argument("--host-diag", action="store_true",
                     help="after the measurement, split host time into replay / H2D load (stderr only)")
     ap.add_argument("--force-collectives", action="store_true",
@@ -110,7 +112,9 @@ def main():
         model.dn.group = dist.group.WORLD
         model.dn.sync_stats = True
     arena = DenseArena(model.parameters(), device)
-    opt = FlatAdam(arena, lr=1e-3, clear_grad=True)  # grads zeroed by the update kernel
+    # one update launch for the dense side: Adam + bf16 tower weight re-pack +
+    # data_norm summary update; grads zeroed by the same kernel
+    opt = FlatAdam(arena, lr=1e-3, clear_grad=True).fuse(mlps=[model.mlp], data_norms=[model.dn])
     sync = DenseSync(arena, mode="grad_allreduce")
 
     # "load into memory": the pass's batches live in pinned host memory;
@@ -129,13 +133,17 @@ def main():
     copy_stream = torch.cuda.Stream(device)
     auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
     auc_stats = torch.zeros(5, dtype=torch.float64, device=device)
+    fused_auc = getattr(model, "use_tower", False)
+    if fused_auc:  # streaming AUC accumulated by the tower's loss epilogue
+        model.tower.auc = (auc_table, auc_stats, None)
 
     def train_step(b):
         loss, pred = model(b)
         loss.backward()
         sync.before_step()
         opt.step(sync.grad_scale())
-        auc_accumulate(pred, b.label, auc_table, auc_stats)
+        if not fused_auc:
+            auc_accumulate(pred, b.label, auc_table, auc_stats)
         return loss.detach()
 
     nb = len(host_batches)
@@ -175,6 +183,19 @@ def main():
                 t.record_stream(torch.cuda.current_stream())
             return train_step(b)
 
+    if args.trace_steps and graphed is not None:
+        # diagnostics: per-step host time of the H2D load and the replay
+        tl, tr = [], []
+        for i in range(args.trace_steps):
+            t0 = time.perf_counter()
+            graphed.load((i + 1) % graphed.n, host_batches[(i + 1) % nb])
+            t1 = time.perf_counter()
+            graphed.run(i % graphed.n)
+            tr.append(time.perf_counter() - t1)
+            tl.append(t1 - t0)
+        torch.cuda.synchronize()
+        log(rank, "[bench] trace load us: " + " ".join(f"{x * 1e6:.0f}" for x in tl))
+        log(rank, "[bench] trace run  us: " + " ".join(f"{x * 1e6:.0f}" for x in tr))
     for i in range(args.warmup):
         run(i)
     torch.cuda.synchronize()

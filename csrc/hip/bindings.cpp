@@ -539,12 +539,13 @@ static void cast_bf16(const Tensor& x, Tensor y) {
 static std::vector<Tensor> head_fwd(const Tensor& x, int S, int Eo, int ew_col, int D, int Cp,
                                     const c10::optional<Tensor>& bsize, const c10::optional<Tensor>& bsum,
                                     const c10::optional<Tensor>& bsq, const c10::optional<Tensor>& y_out,
-                                    const c10::optional<Tensor>& yT_out) {
+                                    const c10::optional<Tensor>& yT_out, const c10::optional<Tensor>& ymp_out,
+                                    const c10::optional<Tensor>& stat_part) {
   check_cuda(x, "x");
   PBX_CHECK(x.scalar_type() == torch::kFloat32 && x.dim() == 2, "head: x must be fp32 [B, C]");
   const int B = (int)x.size(0), C = (int)x.size(1);
-  PBX_CHECK(Cp >= C && Cp <= (C + 7) / 8 * 8 + 8 && S * Eo <= C, "head: bad widths");
-  PBX_CHECK(head_lds_bytes(C, D) <= 160 * 1024, "head: row slab exceeds LDS");
+  PBX_CHECK(Cp >= C && Cp <= (C + 31) / 32 * 32 + 8 && S * Eo <= C, "head: bad widths");
+  PBX_CHECK(head_lds_bytes(C, D, Cp) <= 160 * 1024, "head: row slab exceeds LDS");
   HeadArgs a;
   a.x = ptr<float>(x);
   a.B = B; a.C = C; a.Cp = Cp; a.S = S; a.Eo = Eo; a.ew_col = ew_col; a.D = D;
@@ -563,6 +564,16 @@ static std::vector<Tensor> head_fwd(const Tensor& x, int S, int Eo, int ew_col, 
     a.yT = reinterpret_cast<unsigned short*>(yT_out->data_ptr());
     a.ldyt = (int)yT_out->size(1);
   }
+  if (ymp_out.has_value() && ymp_out->defined()) {
+    check_cuda(*ymp_out, "ymp_out");
+    PBX_CHECK(Cp % 32 == 0 && ymp_out->numel() >= (int64_t)(B + 15) / 16 * 16 * Cp, "head: ymp_out size / Cp % 32");
+    a.ymp = reinterpret_cast<unsigned short*>(ymp_out->data_ptr());
+  }
+  if (stat_part.has_value() && stat_part->defined()) {
+    check_cuda(*stat_part, "stat_part");
+    PBX_CHECK(stat_part->numel() >= (int64_t)head_blocks(B) * 2 * C, "head: stat_part size");
+    a.stat_part = ptr<float>(*stat_part);
+  }
   auto lin = torch::empty({B}, x.options());
   Tensor means, scales;
   if (bsize.has_value()) {
@@ -578,9 +589,10 @@ static std::vector<Tensor> head_fwd(const Tensor& x, int S, int Eo, int ew_col, 
 }
 
 // Backward: returns (dx fp32 [B,C], stats [3,C] or undefined).
-static std::vector<Tensor> head_bwd(const Tensor& x, const c10::optional<Tensor>& dy, const Tensor& dlin, int S,
-                                    int Eo, int ew_col, int D, int Cp, const c10::optional<Tensor>& means,
-                                    const c10::optional<Tensor>& scales, float eps) {
+static std::vector<Tensor> head_bwd(const Tensor& x, const c10::optional<Tensor>& dy,
+                                    const c10::optional<Tensor>& dlin, int S, int Eo, int ew_col, int D, int Cp,
+                                    const c10::optional<Tensor>& means, const c10::optional<Tensor>& scales,
+                                    float eps, const c10::optional<Tensor>& dlin_scale, bool want_stats) {
   check_cuda(x, "x");
   const int B = (int)x.size(0), C = (int)x.size(1);
   HeadArgs a;
@@ -593,18 +605,25 @@ static std::vector<Tensor> head_bwd(const Tensor& x, const c10::optional<Tensor>
     a.dy = reinterpret_cast<const unsigned short*>(dy->data_ptr());
     a.ldy = (int)dy->size(1);
   }
-  auto dl = dlin.contiguous();
-  a.dlin = ptr<float>(dl);
+  Tensor dl;
+  if (dlin.has_value() && dlin->defined()) {
+    dl = dlin->contiguous();
+    PBX_CHECK(dl.numel() == B, "head: dlin size");
+    a.dlin = ptr<float>(dl);
+  }
+  a.dlin_scale = optr<float>(dlin_scale);
   a.dx = ptr<float>(dx);
-  if (means.has_value()) {
-    acc = torch::empty({head_blocks(B), 2 * C}, x.options());
-    stats = torch::empty({3, C}, x.options());
+  if (means.has_value() && means->defined() && scales.has_value() && scales->defined()) {
     a.means = ptr<float>(*means);
     a.scales = ptr<float>(*scales);
+  }
+  if (want_stats && means.has_value() && means->defined()) {
+    acc = torch::empty({head_blocks(B), 2 * C}, x.options());
+    stats = torch::empty({3, C}, x.options());
     a.stat_acc = ptr<float>(acc);
   }
   launch_head_bwd(a, cur_stream());
-  if (means.has_value()) {
+  if (a.stat_acc) {
     auto sums = torch::empty({2 * C}, x.options());
     launch_dn_stats(ptr<float>(acc), head_blocks(B), C, B, eps, ptr<float>(stats), ptr<float>(sums), cur_stream());
   }
@@ -802,8 +821,13 @@ static void adam_flat(Tensor p, Tensor g, Tensor m, Tensor v, Tensor pows, float
 
 }  // namespace pbx
 
+namespace pbx {
+void bind_tower(py::module& m);
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   using namespace pbx;
+  bind_tower(m);
   m.doc() = "PaddleBox-capability engine: hand-written gfx950 (MI355X) kernels";
   py::class_<SparseSGDConfig>(m, "SparseSGDConfig")
       .def(py::init<>())
@@ -892,8 +916,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("data_norm_fwd", &data_norm_fwd);
   m.def("data_norm_bwd", &data_norm_bwd);
   m.def("data_norm_update", &data_norm_update);
-  m.def("head_fwd", &head_fwd);
-  m.def("head_bwd", &head_bwd);
+  m.def("head_fwd", &head_fwd, py::arg("x"), py::arg("S"), py::arg("Eo"), py::arg("ew_col"), py::arg("D"),
+        py::arg("Cp"), py::arg("bsize"), py::arg("bsum"), py::arg("bsq"), py::arg("y_out") = py::none(),
+        py::arg("yT_out") = py::none(), py::arg("ymp_out") = py::none(), py::arg("stat_part") = py::none());
+  m.def("head_blocks", &head_blocks);
+  m.def("head_bwd", &head_bwd, py::arg("x"), py::arg("dy"), py::arg("dlin"), py::arg("S"), py::arg("Eo"),
+        py::arg("ew_col"), py::arg("D"), py::arg("Cp"), py::arg("means"), py::arg("scales"), py::arg("eps"),
+        py::arg("dlin_scale") = py::none(), py::arg("want_stats") = true);
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_bwd", &linear_bwd);
   m.def("gemv_out", &gemv_out);

@@ -1,0 +1,320 @@
+// torch glue for the fused dense tower (tower.hip) and the fused Adam.
+// Buffers live in a persistent TowerWorkspace (fixed batch M and widths), so
+// a captured training step replays against stable addresses.
+#include <ATen/hip/HIPContext.h>
+#include <torch/extension.h>
+
+#include <cstdlib>
+#include <stdexcept>
+
+#include "kernels.h"
+
+namespace py = pybind11;
+using torch::Tensor;
+
+namespace pbx {
+namespace {
+
+hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+#define TW_CHECK(cond, msg)                                                 \
+  do {                                                                      \
+    if (!(cond)) throw std::runtime_error(std::string("pbx tower: ") + msg); \
+  } while (0)
+
+template <typename T>
+T* P(const Tensor& t) {
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+template <typename T>
+T* OP(const c10::optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+unsigned short* BP(const Tensor& t) { return reinterpret_cast<unsigned short*>(t.data_ptr()); }
+int64_t pad(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+void check_f32(const Tensor& t, int64_t numel, const char* what) {
+  TW_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kFloat32, std::string(what) + ": f32 GPU");
+  TW_CHECK(numel < 0 || t.numel() == numel, std::string(what) + ": size");
+}
+
+}  // namespace
+
+class TowerWorkspace {
+ public:
+  TowerWorkspace(int64_t M, std::vector<int64_t> dims, int device, int64_t dw_splits)
+      : M_(M), dims_(dims), splits_(dw_splits) {
+    TW_CHECK(dims.size() >= 2 && dims.size() - 1 <= (size_t)kMaxTowerLayers, "1..8 hidden layers");
+    TW_CHECK(M > 0, "M > 0");
+    TW_CHECK(dw_splits == 1 || dw_splits == 2, "dw_splits in {1, 2}");
+    for (auto d : dims) TW_CHECK(d > 0 && d <= 2048, "widths in 1..2048");
+    auto ob = torch::TensorOptions().dtype(torch::kBFloat16).device(torch::kCUDA, device);
+    auto of = torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device);
+    auto oi = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device);
+    Mp_ = tower_nwg((int)M) * 32;
+    L_ = (int)dims.size() - 1;
+    int64_t maxw = 0;
+    for (auto d : dims) maxw = std::max(maxw, pad(d, 32));
+    lds_ld_ = (int)maxw + 8;
+    TW_CHECK((size_t)2 * 32 * lds_ld_ * 2 <= 150 * 1024, "widths exceed the LDS tile budget");
+    const int64_t K0p = pad(dims[0], 32);
+    x0_ = torch::zeros({M, K0p}, ob);
+    x0mp_ = torch::zeros({Mp_ * K0p}, ob);
+    dx0_ = torch::zeros({M, K0p}, ob);
+    int64_t boff = 0;
+    for (int l = 0; l < L_; ++l) {
+      const int64_t Kp = pad(dims[l], 32), Np = pad(dims[l + 1], 32);
+      wp_.push_back(torch::zeros({Np * Kp}, ob));
+      wtp_.push_back(torch::zeros({Np * Kp}, ob));
+      xmp_.push_back(torch::zeros({Mp_ * Np}, ob));
+      dzmp_.push_back(torch::zeros({Mp_ * Np}, ob));
+      boff_.push_back(boff);
+      boff += Np;
+    }
+    dwout_off_ = (int)boff;
+    dbout_off_ = (int)(boff + pad(dims[L_], 32));
+    bias_ld_ = dbout_off_ + 1;
+    const int nwg = (int)(Mp_ / 32);
+    bias_part_ = torch::zeros({nwg, bias_ld_}, of);
+    pred_ = torch::zeros({M}, of);
+    dz_ = torch::zeros({M}, of);
+    loss_ = torch::zeros({1}, of);
+    part_ = torch::zeros({nwg * 8}, of);
+    ticket_ = torch::zeros({1}, oi);
+  }
+
+  // fp32 master weights W_l [N_l][K_l] -> packed bf16 copies (one launch)
+  void pack(const std::vector<Tensor>& W) {
+    TW_CHECK((int)W.size() == L_, "pack: layer count");
+    TowerArgs a = base();
+    const float* w[kMaxTowerLayers];
+    for (int l = 0; l < L_; ++l) {
+      check_f32(W[l], dims_[l + 1] * dims_[l], "W");
+      w[l] = P<float>(W[l]);
+    }
+    launch_tower_pack(a, w, stream());
+  }
+
+  std::vector<Tensor> forward(const std::vector<Tensor>& b, const Tensor& w_out, const Tensor& b_out,
+                              const c10::optional<Tensor>& lin, const Tensor& label,
+                              const c10::optional<Tensor>& auc_table, const c10::optional<Tensor>& auc_stats,
+                              const c10::optional<Tensor>& auc_mask) {
+    TW_CHECK((int)b.size() == L_, "forward: layer count");
+    TowerArgs a = base();
+    for (int l = 0; l < L_; ++l) {
+      check_f32(b[l], dims_[l + 1], "bias");
+      a.ly[l].bias = P<float>(b[l]);
+    }
+    check_f32(w_out, dims_[L_], "w_out");
+    check_f32(b_out, 1, "b_out");
+    check_f32(label, M_, "label");
+    a.w_out = P<float>(w_out);
+    a.b_out = P<float>(b_out);
+    if (lin.has_value() && lin->defined()) check_f32(*lin, M_, "lin");
+    a.lin = OP<float>(lin);
+    a.label = P<float>(label);
+    if (auc_table.has_value() && auc_table->defined()) {
+      TW_CHECK(auc_table->scalar_type() == torch::kFloat64 && auc_stats.has_value() &&
+                   auc_stats->scalar_type() == torch::kFloat64 && auc_stats->numel() >= 5,
+               "auc tables are f64 [2, T] / [5]");
+      a.auc_table = OP<double>(auc_table);
+      a.auc_stats = OP<double>(auc_stats);
+      a.auc_buckets = (int)(auc_table->numel() / 2);
+      a.auc_mask = OP<float>(auc_mask);
+    }
+    launch_tower_fwd(a, stream());
+    return {loss_, pred_, dz_};
+  }
+
+  // Parameter grads are ACCUMULATED (+=) into dW/db/dw_out/db_out.  Optional
+  // data_norm stat partials [dn_rows][2C] are reduced into dn_stats [3, C].
+  Tensor backward(const c10::optional<Tensor>& dloss, const Tensor& w_out, const std::vector<Tensor>& dW,
+                  const std::vector<Tensor>& db, const Tensor& dw_out, const Tensor& db_out, bool need_dx,
+                  const c10::optional<Tensor>& dn_part,
+                  int64_t dn_rows, double dn_eps, const c10::optional<Tensor>& dn_stats) {
+    TW_CHECK((int)dW.size() == L_ && (int)db.size() == L_, "backward: layer count");
+    TowerArgs a = base();
+    for (int l = 0; l < L_; ++l) {
+      check_f32(dW[l], dims_[l + 1] * dims_[l], "dW");
+      check_f32(db[l], dims_[l + 1], "db");
+      a.ly[l].dw = P<float>(dW[l]);
+      a.ly[l].db = P<float>(db[l]);
+    }
+    check_f32(w_out, dims_[L_], "w_out");
+    check_f32(dw_out, dims_[L_], "dw_out");
+    check_f32(db_out, 1, "db_out");
+    a.w_out = P<float>(w_out);  // dX_L = g w_out^T
+    a.dw_out = P<float>(dw_out);
+    a.db_out = P<float>(db_out);
+    a.dloss = OP<float>(dloss);
+    a.need_dx0 = need_dx ? 1 : 0;
+    a.dx0 = BP(dx0_);
+    a.lddx0 = (int)dx0_.size(1);
+    if (dn_part.has_value() && dn_part->defined()) {
+      TW_CHECK(dn_stats.has_value() && dn_stats->defined(), "dn_stats required with dn_part");
+      const int C = (int)(dn_stats->numel() / 3);
+      TW_CHECK(dn_part->numel() >= dn_rows * 2 * C, "dn_part size");
+      a.dn_part = OP<float>(dn_part);
+      a.dn_rows = (int)dn_rows;
+      a.dn_C = C;
+      a.dn_eps = (float)dn_eps;
+      a.dn_stats = OP<float>(dn_stats);
+    }
+    auto s = stream();
+    launch_tower_bwd(a, s);
+    launch_tower_dw(a, s);
+    return need_dx ? dx0_ : Tensor();
+  }
+
+  // (wp, wtp, N, K, Np, Kp) per layer, for the optimizer's fused re-pack
+  std::vector<py::tuple> pack_regions() const {
+    std::vector<py::tuple> r;
+    for (int l = 0; l < L_; ++l)
+      r.push_back(py::make_tuple(wp_[l], wtp_[l], dims_[l + 1], dims_[l], pad(dims_[l + 1], 32), pad(dims_[l], 32)));
+    return r;
+  }
+
+  Tensor x0() const { return x0_; }
+  Tensor x0mp() const { return x0mp_; }
+  Tensor xmp(int l) const { return xmp_.at(l); }
+  Tensor dzmp(int l) const { return dzmp_.at(l); }
+  Tensor dx0() const { return dx0_; }
+  Tensor wp(int l) const { return wp_.at(l); }
+  Tensor wtp(int l) const { return wtp_.at(l); }
+  int64_t M() const { return M_; }
+  int64_t Mp() const { return Mp_; }
+
+ private:
+  TowerArgs base() const {
+    TowerArgs a;
+    a.M = (int)M_;
+    a.Mp = (int)Mp_;
+    a.L = L_;
+    a.lds_ld = lds_ld_;
+    a.x0 = BP(x0_);
+    a.ld0 = (int)x0_.size(1);
+    a.x0mp = BP(x0mp_);
+    for (int l = 0; l < L_; ++l) {
+      TowerLayerDev& d = a.ly[l];
+      d.wp = BP(wp_[l]);
+      d.wtp = BP(wtp_[l]);
+      d.K = (int)dims_[l];
+      d.N = (int)dims_[l + 1];
+      d.Kp = (int)pad(dims_[l], 32);
+      d.Np = (int)pad(dims_[l + 1], 32);
+      d.xmp = BP(xmp_[l]);
+      d.dzmp = BP(dzmp_[l]);
+      d.bias_off = (int)boff_[l];
+    }
+    a.pred = P<float>(pred_);
+    a.dz = P<float>(dz_);
+    a.loss = P<float>(loss_);
+    a.part = P<float>(part_);
+    a.ticket = reinterpret_cast<unsigned int*>(ticket_.data_ptr());
+    a.bias_part = P<float>(bias_part_);
+    a.bias_ld = bias_ld_;
+    a.dwout_off = dwout_off_;
+    a.dbout_off = dbout_off_;
+    a.dw_splits = (int)splits_;
+    static const int dbg = [] {
+      const char* e = getenv("PBX_TOWER_DEBUG");
+      return e ? atoi(e) : 0;
+    }();
+    a.debug = dbg;
+    return a;
+  }
+
+  int64_t M_, Mp_ = 0;
+  std::vector<int64_t> dims_;
+  int64_t splits_;
+  int L_ = 0, lds_ld_ = 0, bias_ld_ = 0, dwout_off_ = 0, dbout_off_ = 0;
+  std::vector<int64_t> boff_;
+  Tensor x0_, x0mp_, dx0_, bias_part_, pred_, dz_, loss_, part_, ticket_;
+  std::vector<Tensor> wp_, wtp_, xmp_, dzmp_;
+};
+
+// Adam over the flat arena + fused extras (see kernels.h AdamExtras).
+// pack: [(arena_offset, wp, wtp, N, K, Np, Kp)], dn: [(stats, bsize, bsum, bsq, decay)]
+static void adam_fused(Tensor p, Tensor g, Tensor m, Tensor v, Tensor pows, Tensor ticket, double lr, double b1,
+                       double b2, double eps, double grad_scale, double wd, bool clear_grad,
+                       const std::vector<py::tuple>& pack, const std::vector<py::tuple>& dn) {
+  check_f32(p, -1, "p");
+  TW_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "adam sizes");
+  TW_CHECK(pows.is_cuda() && pows.numel() >= 2 && pows.scalar_type() == torch::kFloat32, "adam pows");
+  TW_CHECK(ticket.is_cuda() && ticket.scalar_type() == torch::kInt32, "adam ticket");
+  TW_CHECK(pack.size() <= (size_t)kMaxPackRegions && dn.size() <= (size_t)kMaxDnUpdates, "too many extras");
+  AdamExtras x;
+  x.n_pack = (int)pack.size();
+  for (size_t i = 0; i < pack.size(); ++i) {
+    const auto& t = pack[i];
+    x.pack_off[i] = t[0].cast<int64_t>();
+    x.pack_wp[i] = BP(t[1].cast<Tensor>());
+    x.pack_wtp[i] = BP(t[2].cast<Tensor>());
+    x.pack_N[i] = t[3].cast<int>();
+    x.pack_K[i] = t[4].cast<int>();
+    x.pack_Np[i] = t[5].cast<int>();
+    x.pack_Kp[i] = t[6].cast<int>();
+    TW_CHECK(x.pack_off[i] >= 0 && x.pack_off[i] + (int64_t)x.pack_N[i] * x.pack_K[i] <= p.numel(), "pack range");
+  }
+  x.n_dn = (int)dn.size();
+  for (size_t i = 0; i < dn.size(); ++i) {
+    const auto& t = dn[i];
+    auto st = t[0].cast<Tensor>();
+    auto bs = t[1].cast<Tensor>();
+    x.dn_C[i] = (int)bs.numel();
+    TW_CHECK(st.numel() == 3 * bs.numel(), "dn stats must be [3, C]");
+    x.dn_stats[i] = P<float>(st);
+    x.dn_bsize[i] = P<float>(bs);
+    x.dn_bsum[i] = P<float>(t[2].cast<Tensor>());
+    x.dn_bsq[i] = P<float>(t[3].cast<Tensor>());
+    x.dn_decay[i] = t[4].cast<float>();
+  }
+  x.ticket = reinterpret_cast<unsigned int*>(ticket.data_ptr());
+  launch_adam_fused(P<float>(p), P<float>(g), P<float>(m), P<float>(v), p.numel(), (float)lr, (float)b1, (float)b2,
+                    (float)eps, P<float>(pows), (float)grad_scale, (float)wd, clear_grad, x, stream());
+}
+
+// Raw async H2D copy on the current stream.  torch's copy_ from pinned memory
+// records a fresh event in the caching host allocator for every copy and only
+// reclaims them on allocation; a training loop that re-uses the same pinned
+// batches never allocates, the events pile up and every few dozen copies the
+// runtime stalls the host for milliseconds (profiles/r2_h2d_stall.txt).  Buffer
+// reuse is ordered by the caller's own events instead.
+static void memcpy_h2d(Tensor dst, const Tensor& src) {
+  TW_CHECK(dst.is_cuda() && dst.is_contiguous(), "memcpy_h2d: dst must be a contiguous GPU tensor");
+  TW_CHECK(!src.is_cuda() && src.is_contiguous() && src.is_pinned(), "memcpy_h2d: src must be contiguous pinned host memory");
+  const size_t n = (size_t)dst.numel() * dst.element_size();
+  TW_CHECK((size_t)src.numel() * src.element_size() == n, "memcpy_h2d: size mismatch");
+  if (hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), n, hipMemcpyHostToDevice, stream()) != hipSuccess)
+    throw std::runtime_error("pbx: hipMemcpyAsync H2D failed");
+}
+
+void bind_tower(py::module& m) {
+  m.def("memcpy_h2d", &memcpy_h2d, py::arg("dst"), py::arg("src"));
+  py::class_<TowerWorkspace>(m, "TowerWorkspace")
+      .def(py::init<int64_t, std::vector<int64_t>, int, int64_t>(), py::arg("M"), py::arg("dims"),
+           py::arg("device"), py::arg("dw_splits") = 2)
+      .def("pack", &TowerWorkspace::pack)
+      .def("forward", &TowerWorkspace::forward, py::arg("b"), py::arg("w_out"), py::arg("b_out"), py::arg("lin"),
+           py::arg("label"), py::arg("auc_table") = py::none(), py::arg("auc_stats") = py::none(),
+           py::arg("auc_mask") = py::none())
+      .def("backward", &TowerWorkspace::backward, py::arg("dloss"), py::arg("w_out"), py::arg("dW"), py::arg("db"),
+           py::arg("dw_out"),
+           py::arg("db_out"), py::arg("need_dx"), py::arg("dn_part") = py::none(), py::arg("dn_rows") = 0,
+           py::arg("dn_eps") = 0.0, py::arg("dn_stats") = py::none())
+      .def("pack_regions", &TowerWorkspace::pack_regions)
+      .def("x0", &TowerWorkspace::x0)
+      .def("x0mp", &TowerWorkspace::x0mp)
+      .def("xmp", &TowerWorkspace::xmp)
+      .def("dzmp", &TowerWorkspace::dzmp)
+      .def("dx0", &TowerWorkspace::dx0)
+      .def("wp", &TowerWorkspace::wp)
+      .def("wtp", &TowerWorkspace::wtp)
+      .def_property_readonly("M", &TowerWorkspace::M)
+      .def_property_readonly("Mp", &TowerWorkspace::Mp);
+  m.def("adam_fused", &adam_fused, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pows"),
+        py::arg("ticket"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("grad_scale"),
+        py::arg("wd"), py::arg("clear_grad"), py::arg("pack"), py::arg("dn"));
+}
+
+}  // namespace pbx

@@ -58,7 +58,10 @@ __global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
     }
     const unsigned short yb = f2bf(yv);
     a.y[(int64_t)(row0 + r) * ldy + c] = yb;
-    if (a.yT) ys[r * Cp + c] = yb;
+    if (a.yT || a.ymp) ys[r * Cp + c] = yb;
+  }
+  if (a.ymp) {  // rows past B are zero in the m-packed copy
+    for (int i = threadIdx.x; i < (kRB - rows) * Cp; i += blockDim.x) ys[rows * Cp + i] = 0;
   }
   if (blockIdx.x == 0 && a.means) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -68,6 +71,33 @@ __global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
     }
   }
   __syncthreads();
+  if (a.ymp) {  // m-packed copy for the tower dW GEMM: chunk (row0/16, nb), 16 B per lane
+    const int NB = Cp / 32;
+    const int64_t mb = row0 / kRB;
+    for (int i = threadIdx.x; i < NB * 64; i += blockDim.x) {
+      const int nb = i >> 6, l = i & 63;
+      unsigned int p[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        p[j] = (unsigned)ys[(8 * (l >> 5) + 2 * j) * Cp + 32 * nb + (l & 31)] |
+               ((unsigned)ys[(8 * (l >> 5) + 2 * j + 1) * Cp + 32 * nb + (l & 31)] << 16);
+      *reinterpret_cast<uint4*>(a.ymp + ((mb * NB + nb) * 64 + l) * 8) = make_uint4(p[0], p[1], p[2], p[3]);
+    }
+  }
+  if (a.stat_part && a.means) {  // data_norm batch statistics, per-block partial row
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const float bs = a.bsize[c];
+      const float mean = a.bsum[c] / bs;
+      float sx = 0.f, sq = 0.f;
+      for (int r = 0; r < rows; ++r) {
+        const float v = xs[r * C + c];
+        sx += v;
+        sq += (v - mean) * (v - mean);
+      }
+      a.stat_part[(int64_t)blockIdx.x * 2 * C + c] = sx;
+      a.stat_part[(int64_t)blockIdx.x * 2 * C + C + c] = sq;
+    }
+  }
   if (a.yT) {  // y^T[c][row0 .. row0+rows): one 32-byte run per column
     for (int c = threadIdx.x; c < Cp; c += blockDim.x) {
       unsigned short* dst = a.yT + (int64_t)c * a.ldyt + row0;
@@ -132,9 +162,9 @@ __global__ __launch_bounds__(256) void k_head_bwd(HeadArgs a) {
     const int r = i / C, c = i - r * C;
     const float sc = a.scales ? a.scales[c] : 1.f;
     float g = a.dy ? bf2f(a.dy[(int64_t)(row0 + r) * (a.ldy ? a.ldy : Cp) + c]) * sc : 0.f;
-    if (c < sparse_w) {
+    if (c < sparse_w && a.dlin) {
       const int j = c % a.Eo;
-      const float dl = a.dlin[row0 + r];
+      const float dl = a.dlin[row0 + r] * (a.dlin_scale ? a.dlin_scale[0] : 1.f);
       if (j == a.ew_col) {
         g += dl;
       } else if (j > a.ew_col && j <= a.ew_col + D) {
@@ -172,21 +202,22 @@ __global__ void k_dn_stats(const float* __restrict__ acc, int C, int N, float ep
 
 }  // namespace
 
-size_t head_lds_bytes(int C, int D) {
-  // fp32 row slab + FM sums, then the bf16 y slab for the transposed write
-  return (size_t)kRB * (C + D) * sizeof(float) + (size_t)kRB * ((C + 7) / 8 * 8 + 8) * sizeof(unsigned short);
+size_t head_lds_bytes(int C, int D, int Cp) {
+  // fp32 row slab + FM sums, then the bf16 y slab for the transposed / packed write
+  const int w = Cp > (C + 7) / 8 * 8 + 8 ? Cp : (C + 7) / 8 * 8 + 8;
+  return (size_t)kRB * (C + D) * sizeof(float) + (size_t)kRB * w * sizeof(unsigned short);
 }
 
 void launch_head_fwd(const HeadArgs& a, hipStream_t s) {
   if (a.B == 0) return;
   const unsigned g = (unsigned)((a.B + kRB - 1) / kRB);
-  hipLaunchKernelGGL(k_head_fwd, dim3(g), dim3(256), head_lds_bytes(a.C, a.D), s, a);
+  hipLaunchKernelGGL(k_head_fwd, dim3(g), dim3(256), head_lds_bytes(a.C, a.D, a.Cp), s, a);
 }
 
 void launch_head_bwd(const HeadArgs& a, hipStream_t s) {
   if (a.B == 0) return;
   const unsigned g = (unsigned)((a.B + kRB - 1) / kRB);
-  hipLaunchKernelGGL(k_head_bwd, dim3(g), dim3(256), head_lds_bytes(a.C, a.D), s, a);
+  hipLaunchKernelGGL(k_head_bwd, dim3(g), dim3(256), head_lds_bytes(a.C, a.D, a.Cp), s, a);
 }
 
 int head_blocks(int B) { return (B + kRB - 1) / kRB; }

@@ -263,11 +263,14 @@ struct HeadArgs {
   int ldyt = 0;
   float* lin = nullptr;         // [B] first + FM out (fwd)
   const unsigned short* dy = nullptr;  // [B, ldy] bf16 in (bwd)
-  const float* dlin = nullptr;         // [B] in (bwd)
+  const float* dlin = nullptr;         // [B] in (bwd), nullable (= 0)
+  const float* dlin_scale = nullptr;   // optional device scalar multiplying dlin (bwd)
   float* dx = nullptr;                 // [B, C] out (bwd)
   float* stat_acc = nullptr;           // [head_blocks(B), 2C] per-block partial sums (bwd)
+  unsigned short* ymp = nullptr;       // optional m-packed copy of y (fwd; Cp % 32 == 0, B rows padded to 16)
+  float* stat_part = nullptr;          // optional [head_blocks(B), 2C] batch-stat partials computed in fwd
 };
-size_t head_lds_bytes(int C, int D);
+size_t head_lds_bytes(int C, int D, int Cp);
 int head_blocks(int B);
 void launch_head_fwd(const HeadArgs& a, hipStream_t s);
 void launch_head_bwd(const HeadArgs& a, hipStream_t s);
@@ -342,5 +345,100 @@ int mlp_gemv_bwd_blocks(int M);
 void launch_mlp_gemv_bwd(const unsigned short* h, int M, int K, int ld, const float* w, const float* dout,
                          unsigned short* dz, unsigned short* dzt, int ldt, float* part, float* dw, float* db,
                          hipStream_t s);
+
+// ---------------------------------------------------------------- fused dense tower (tower.hip)
+// Whole CTR MLP (ReLU layers + 1-logit output + sigmoid/log-loss + AUC) as
+// three launches: a row-tile-resident forward, a row-tile-resident backward
+// (dX chain) and one grouped dW GEMM (+ bias / data_norm column reductions).
+//
+// Layouts (all bf16 = unsigned short; dims padded to multiples of 32, Mp =
+// pad32(M)):
+//  * "MP" (m-packed) activations Z[M][N]: 1 KB chunks [Mp/16][Np/32][64][8];
+//    lane l, element j of chunk (mb, nb) = Z[16mb + 8(l/32) + j][32nb + l%32]
+//    -- exactly the MFMA 32x32x16 operand fragment with m as the reduction
+//    dim, so the dW GEMM streams both operands 1 KB at a time.
+//  * packed W  [Np/32][Kp/16][64][8]: lane l, j = W[32nb + l%32][16kb + 8(l/32) + j]
+//  * packed Wt [Kp/32][Np/16][64][8]: lane l, j = W[16nb + 8(l/32) + j][32kb + l%32]
+constexpr int kMaxTowerLayers = 8;
+struct TowerLayerDev {
+  const unsigned short* wp = nullptr;   // packed W
+  const unsigned short* wtp = nullptr;  // packed W^T
+  const float* bias = nullptr;          // [N]
+  int K = 0, N = 0, Kp = 0, Np = 0;
+  unsigned short* xmp = nullptr;   // MP of this layer's output X_{l+1}
+  unsigned short* dzmp = nullptr;  // MP of dZ_{l+1}
+  float* dw = nullptr;             // [N][K] fp32 grad (accumulated)
+  float* db = nullptr;             // [N]
+  int bias_off = 0;                // column of this layer's db partials in a bias_part row
+};
+struct TowerArgs {
+  int M = 0, Mp = 0, L = 0;
+  int lds_ld = 0;  // LDS row stride in elements (max padded width + 8)
+  const unsigned short* x0 = nullptr;  // row-major input [M][ld0] (>= Kp_0 cols, pad cols 0)
+  int ld0 = 0;
+  const unsigned short* x0mp = nullptr;  // MP(X0)
+  TowerLayerDev ly[kMaxTowerLayers];
+  const float* w_out = nullptr;  // [N_L]
+  const float* b_out = nullptr;  // [1]
+  const float* lin = nullptr;    // [M] extra logit part (first-order + FM), nullable
+  const float* label = nullptr;  // [M]
+  float* pred = nullptr;         // [M]
+  float* dz = nullptr;           // [M] d(mean loss)/d logit
+  float* loss = nullptr;         // [1] mean loss
+  float* part = nullptr;         // [nwg][8] per-WG partials (loss, 5 AUC sums)
+  unsigned int* ticket = nullptr;  // zero between launches
+  double* auc_table = nullptr;   // [2, auc_buckets] (nullable = no AUC)
+  double* auc_stats = nullptr;   // [5]
+  int auc_buckets = 0;
+  const float* auc_mask = nullptr;
+  // backward
+  const float* dloss = nullptr;  // scalar upstream grad of the loss (nullable = 1)
+  unsigned short* dx0 = nullptr;  // row-major [M][lddx0] grad wrt X0
+  int lddx0 = 0;
+  int need_dx0 = 1;
+  float* bias_part = nullptr;  // [nwg][bias_ld]: db partials per layer, dw_out, db_out
+  int bias_ld = 0, dwout_off = 0, dbout_off = 0;
+  float* dw_out = nullptr;
+  float* db_out = nullptr;
+  // data_norm batch statistics, reduced by the dW launch: part [dn_rows][2C]
+  // (sum x, sum (x-mean)^2) -> stats [3][C] (1, sum/N, sq/N + eps)
+  const float* dn_part = nullptr;
+  int dn_rows = 0, dn_C = 0;
+  float dn_eps = 0.f;
+  float* dn_stats = nullptr;
+  int dw_splits = 2;
+  int debug = 0;  // timing experiments only (PBX_TOWER_DEBUG): 1 no loss reduction, 2 no dW reductions, 4 no dW GEMM
+};
+int tower_nwg(int M);
+size_t tower_lds_bytes(const TowerArgs& a);
+void launch_tower_fwd(const TowerArgs& a, hipStream_t s);
+void launch_tower_bwd(const TowerArgs& a, hipStream_t s);
+void launch_tower_dw(const TowerArgs& a, hipStream_t s);
+// fp32 [N][K] -> packed W / W^T (pads zero), all layers in one launch
+void launch_tower_pack(const TowerArgs& a, const float* const* w, hipStream_t s);
+
+// Flat Adam with fused extras: beta powers advanced by the last workgroup
+// (ticket), weight regions re-packed to bf16 tower layouts, data_norm
+// summaries updated from their batch statistics.
+constexpr int kMaxPackRegions = 8;
+constexpr int kMaxDnUpdates = 4;
+struct AdamExtras {
+  int n_pack = 0;
+  int64_t pack_off[kMaxPackRegions];  // arena element offset of W [N][K]
+  int pack_N[kMaxPackRegions], pack_K[kMaxPackRegions], pack_Np[kMaxPackRegions], pack_Kp[kMaxPackRegions];
+  unsigned short* pack_wp[kMaxPackRegions];
+  unsigned short* pack_wtp[kMaxPackRegions];
+  int n_dn = 0;
+  const float* dn_stats[kMaxDnUpdates];
+  float* dn_bsize[kMaxDnUpdates];
+  float* dn_bsum[kMaxDnUpdates];
+  float* dn_bsq[kMaxDnUpdates];
+  int dn_C[kMaxDnUpdates];
+  float dn_decay[kMaxDnUpdates];
+  unsigned int* ticket = nullptr;
+};
+void launch_adam_fused(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
+                       float* pows, float grad_scale, float weight_decay, bool clear_grad, const AdamExtras& x,
+                       hipStream_t s);
 
 }  // namespace pbx

@@ -4,12 +4,12 @@ Graph (PaddleBox canonical CTR graph, SURVEY Appendix B, plus the FM term):
 
     pull_box_sparse -> fused_seqpool_cvm   one HIP kernel, written straight
                                            into the [pooled | dense] buffer
-    ctr_head                               one HIP kernel each way:
-        data_norm(x) -> bf16 MLP input
-        first order  = sum_s embed_w(s)
-        second order = FM over embedx[8]
-    deep = FusedMLP 400-400-400 -> 1       MFMA GEMMs, bias+ReLU fused
-    logit = (first + second) + deep -> fused add + sigmoid + logloss
+    CtrTower (ops/tower.py, csrc/hip/tower.hip), forward = 2 launches:
+        k_head_fwd : data_norm(x) -> bf16 MLP input, first order
+                     sum_s embed_w(s) + FM over embedx[8]
+        k_tower_fwd: MLP 400-400-400 -> 1 on MFMA with activations held in
+                     LDS, + (first + FM), sigmoid, logloss, AUC
+    backward = k_tower_bwd + k_tower_dw + k_head_bwd
 
 The embedding update happens in the backward of the pull (push_box_sparse
 with fused sparse Adagrad); dense params live in one flat arena updated by
@@ -25,6 +25,7 @@ from torch import nn
 from ..ops.ctr import DataNorm, ctr_head, logit_logloss
 from ..ops.mlp import FusedMLP, pad8
 from ..ops.sparse import pull_seqpool_cvm_concat
+from ..ops.tower import CtrTower
 from ..ps.sparse_engine import SeqpoolParams, SparseEngine
 
 
@@ -66,11 +67,17 @@ class DeepFM(nn.Module):
         self.head_into_workspace = True
         # column of embed_w inside each slot block; embedx follow it
         self.ew_col = 2 if self.sp.use_cvm and not self.sp.clk_filter else (1 if self.sp.use_cvm else 0)
+        # fused head + MLP + loss (csrc/hip/tower.hip); use_tower=False keeps
+        # the per-layer GEMM path (mlp.hip) for comparison
+        self.tower = CtrTower(self.mlp, self.dn, self.S, self.Eo, self.ew_col, self.D, use_head_lin=True)
+        self.use_tower = True
 
     def forward(self, batch):
         B, S = batch.B, batch.S
         x = pull_seqpool_cvm_concat(self.engine, batch.keys, batch.lod, B, S, batch.cvm, batch.dense, self.sp)
-        if x.is_cuda and self.use_workspace:
+        if self.use_tower or not x.is_cuda:
+            return self.tower(x, batch.label)
+        if self.use_workspace:
             # the head writes the MLP input (and its transpose) straight into
             # the MLP workspace; the MLP streams it HBM -> LDS by DMA
             ws = self.mlp.workspace(B, x.device)

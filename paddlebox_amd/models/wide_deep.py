@@ -22,6 +22,7 @@ from torch import nn
 from ..ops.ctr import DataNorm, ctr_head, logit_logloss
 from ..ops.mlp import FusedMLP, pad8
 from ..ops.sparse import pull_seqpool_cvm_concat
+from ..ops.tower import CtrTower
 from ..ps.sparse_engine import SeqpoolParams, SparseEngine
 
 
@@ -41,10 +42,14 @@ class WideDeep(nn.Module):
         self.dn = DataNorm(C) if use_data_norm else None
         self.mlp = FusedMLP(C, hidden, 1)
         self.ew_col = 2 if self.sp.use_cvm and not self.sp.clk_filter else (1 if self.sp.use_cvm else 0)
+        self.tower = CtrTower(self.mlp, self.dn, self.S, self.Eo, self.ew_col, 0, use_head_lin=True)
+        self.use_tower = True
 
     def forward(self, batch):
         B, S = batch.B, batch.S
         x = pull_seqpool_cvm_concat(self.engine, batch.keys, batch.lod, B, S, batch.cvm, batch.dense, self.sp)
+        if self.use_tower or not x.is_cuda:
+            return self.tower(x, batch.label)
         if x.is_cuda:
             ws = self.mlp.workspace(B, x.device)
             y, wide = ctr_head(x, self.dn, S, self.Eo, self.ew_col, 0, self.Cp, ws.x(0), ws.xt(0))

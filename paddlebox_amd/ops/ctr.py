@@ -82,6 +82,11 @@ class DataNorm(torch.nn.Module):
             self.bias = None
         self.update_norm = True
         self.group = None
+        # batch statistics [3, C] written by the fused tower backward; the
+        # summary update is applied there, or by FlatAdam's fused kernel when
+        # it owns this layer (fused_update = True)
+        self.register_buffer("stats", torch.zeros(3 * C))
+        self.fused_update = False
 
     def forward(self, x):
         return _DataNorm.apply(x, self.batch_size, self.batch_sum, self.batch_square_sum, self.scale_w, self.bias,

@@ -139,6 +139,28 @@ class FusedMLP(nn.Module):
         # split-K over the batch for the workspace dW GEMMs
         self.k_split_dw = int(os.environ.get("PBX_KSPLIT_DW", "1024"))
         self._ws = None
+        self._tw = None
+        # packed bf16 tower weights are valid (re-packed by FlatAdam's fused
+        # kernel after every update when it owns this MLP; anything else that
+        # writes the fp32 masters must call invalidate_pack())
+        self._packed = False
+        self.packed_by_optimizer = False
+
+    # ---- fused tower path (csrc/hip/tower.hip)
+    def tower_workspace(self, M: int, device: torch.device):
+        if self._tw is None or self._tw.M != M:
+            dims = [self.in_dim] + list(self.hidden)
+            self._tw = _native.hip().TowerWorkspace(M, dims, device.index or 0, 2)
+            self._packed = False
+        return self._tw
+
+    def ensure_packed(self):
+        if not self._packed or not self.packed_by_optimizer:
+            self._tw.pack([w.detach() for w in self.w])
+            self._packed = True
+
+    def invalidate_pack(self):
+        self._packed = False
 
     # ---- workspace path (csrc/hip/mlp.hip): persistent padded activations +
     # transposed copies so every GEMM streams both operands HBM -> LDS by DMA

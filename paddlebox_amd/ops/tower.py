@@ -1,0 +1,135 @@
+"""CTR dense tower: fused head (data_norm + first-order/FM) + MLP + loss as
+one autograd node, on the three-launch HIP tower (csrc/hip/tower.hip).
+
+Forward  : k_head_fwd (data_norm -> bf16 MLP input in row-major and m-packed
+           layouts, lin = first-order + FM, data_norm batch-stat partials)
+           k_tower_fwd (all ReLU layers, output GEMV, sigmoid, log-loss,
+           d loss/d logit, AUC histogram)
+Backward : k_tower_bwd (dX chain) + k_tower_dw (grouped dW GEMM, bias /
+           output-layer grads, data_norm stats) + k_head_bwd (dx for the
+           sparse push)
+
+The extra logit term is either the head's ``lin`` (DeepFM: first + FM; Wide&Deep:
+first-order "wide" part) or an external tensor (DCN-V2 cross branch), whose
+gradient is ``dz * dloss``.
+
+Reference semantics: data_norm (paddle/fluid/operators/data_norm_op.cu:38-104),
+fc + relu, sigmoid + log_loss, auc (paddle/phi/kernels/gpu/auc_kernel.cu:25-80).
+CPU tensors run the same math in plain fp32 PyTorch.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+from ..parallel.comm import collective_active
+from . import reference as ref
+
+
+def pad32(n: int) -> int:
+    return (n + 31) // 32 * 32
+
+
+class _CtrTowerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, extra, label, t: "CtrTower", *params):
+        h = _native.hip()
+        mlp, dn = t.mlp, t.dn
+        B = x.shape[0]
+        ws = mlp.tower_workspace(B, x.device)
+        mlp.ensure_packed()
+        x = x.contiguous()
+        if dn is not None:
+            part = t._dn_part(B, x.device)
+            _, lin, means, scales = h.head_fwd(x, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim), dn.batch_size,
+                                               dn.batch_sum, dn.batch_square_sum, y_out=ws.x0(),
+                                               ymp_out=ws.x0mp(), stat_part=part)
+        else:
+            _, lin, means, scales = h.head_fwd(x, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim), None, None, None,
+                                               y_out=ws.x0(), ymp_out=ws.x0mp())
+        if extra is not None:
+            lin_use = extra.detach().contiguous().float().view(-1)
+        elif t.use_head_lin:
+            lin_use = lin
+        else:
+            lin_use = None
+        auc = t.auc
+        loss, pred, dz = ws.forward(list(mlp.b), mlp.w_out.view(-1), mlp.b_out, lin_use, label.contiguous().view(-1),
+                                    auc[0] if auc else None, auc[1] if auc else None, auc[2] if auc else None)
+        ctx.t, ctx.ws = t, ws
+        ctx.save_for_backward(x)
+        ctx.means, ctx.scales, ctx.dz = means, scales, dz
+        ctx.has_extra = extra is not None
+        ctx.mark_non_differentiable(pred)
+        return loss.view(()), pred
+
+    @staticmethod
+    def backward(ctx, gl, gp):
+        h = _native.hip()
+        t, ws = ctx.t, ctx.ws
+        mlp, dn = t.mlp, t.dn
+        (x,) = ctx.saved_tensors
+        B = x.shape[0]
+        mlp.ensure_grads()
+        gl = gl.contiguous().float().view(1)
+        dn_on = dn is not None and dn.training and dn.update_norm
+        dx0 = ws.backward(gl, mlp.w_out.detach().view(-1), [w.grad for w in mlp.w], [b.grad for b in mlp.b],
+                          mlp.w_out.grad.view(-1),
+                          mlp.b_out.grad, True, t._dn_part(B, x.device) if dn_on else None,
+                          h.head_blocks(B) if dn_on else 0, dn.eps if dn is not None else 0.0,
+                          dn.stats if dn_on else None)
+        if dn_on:
+            if dn.sync_stats and dn.group is not None and collective_active(dn.group):
+                dist.all_reduce(dn.stats, group=dn.group)
+            if not dn.fused_update:
+                h.data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, dn.stats, dn.decay)
+        use_lin = t.use_head_lin and not ctx.has_extra
+        dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim),
+                           ctx.means, ctx.scales, dn.eps if dn is not None else 0.0, dlin_scale=gl,
+                           want_stats=False)
+        d_extra = ctx.dz * gl if ctx.has_extra else None
+        return (dx, d_extra, None, None) + (None,) * (len(t._params))
+
+
+class CtrTower:
+    """Binds a FusedMLP (+ optional DataNorm) into the fused tower.
+
+    S slot blocks of width Eo (embed_w at ew_col, D embedx after it) followed by
+    dense columns make up the input x [B, C]."""
+
+    def __init__(self, mlp, dn, S: int, Eo: int, ew_col: int, D: int, use_head_lin: bool = True):
+        self.mlp, self.dn = mlp, dn
+        self.S, self.Eo, self.ew_col, self.D = S, Eo, ew_col, D
+        self.use_head_lin = use_head_lin
+        self.auc = None  # (table [2, T] f64, stats [5] f64, mask or None): fused AUC accumulation
+        self._part = None
+        self._params = list(mlp.parameters())
+
+    def _dn_part(self, B, device):
+        h = _native.hip()
+        n = h.head_blocks(B) * 2 * self.dn.C
+        if self._part is None or self._part.numel() != n:
+            self._part = torch.zeros(n, device=device)
+        return self._part
+
+    def __call__(self, x: torch.Tensor, label: torch.Tensor, extra: Optional[torch.Tensor] = None
+                 ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(mean log-loss, prediction) for x [B, C]."""
+        if x.is_cuda:
+            return _CtrTowerFn.apply(x, extra, label, self, *self._params)
+        return self._cpu(x, label, extra)
+
+    def _cpu(self, x, label, extra):
+        from .ctr import ctr_head, logit_logloss
+
+        Cp = self.mlp.in_dim
+        y, lin = ctr_head(x, self.dn, self.S, self.Eo, self.ew_col, self.D, Cp)
+        deep = self.mlp(y)
+        other = extra if extra is not None else (lin if self.use_head_lin else None)
+        loss, pred = logit_logloss(deep, other, label)
+        if self.auc is not None:
+            ref.auc_accumulate(pred.detach(), label.view(-1), self.auc[0], self.auc[1], self.auc[2])
+        return loss, pred

@@ -44,6 +44,14 @@ class DenseArena:
             p.grad = self.grad[off:off + p.numel()].view_as(p)
             self.views.append((off, p.numel()))
             off += sz
+        # callbacks run when something other than the optimizer rewrites the
+        # fp32 masters (parameter averaging, checkpoint load): derived copies
+        # such as the packed bf16 tower weights must be rebuilt
+        self.on_modified = []
+
+    def notify_modified(self):
+        for f in self.on_modified:
+            f()
 
     def zero_grad(self):
         self.grad.zero_()
@@ -67,11 +75,42 @@ class FlatAdam:
         # [beta1^t, beta2^t] on the device: advanced by the kernel itself so the
         # step is HIP-graph replayable (no host scalars baked into the graph)
         self.pows = torch.ones(2, dtype=torch.float32, device=arena.flat.device)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=arena.flat.device)
+        self._fuse_mlps, self._fuse_dns = [], []
+
+    def fuse(self, mlps=(), data_norms=()):
+        """Let the update kernel also (a) re-pack the bf16 tower copies of
+        these MLPs' weights and (b) apply these data_norm layers' summary
+        updates from their batch statistics -- one launch per step for the
+        whole dense side (csrc/hip/tower.hip k_adam_fused)."""
+        if not self.a.flat.is_cuda:
+            return self
+        self._fuse_mlps = [m for m in mlps if m is not None]
+        self._fuse_dns = [d for d in data_norms if d is not None]
+        for m in self._fuse_mlps:
+            m.packed_by_optimizer = True
+        for d in self._fuse_dns:
+            d.fused_update = True
+        self.a.on_modified.extend(m.invalidate_pack for m in self._fuse_mlps)
+        return self
+
+    def _extras(self):
+        base = self.a.flat.data_ptr()
+        pack = []
+        for mlp in self._fuse_mlps:
+            if mlp._tw is None:
+                continue  # the tower packs on its first forward
+            for (wp, wtp, N, K, Np, Kp), w in zip(mlp._tw.pack_regions(), mlp.w):
+                pack.append(((w.data_ptr() - base) // 4, wp, wtp, N, K, Np, Kp))
+        dn = [(d.stats, d.batch_size, d.batch_sum, d.batch_square_sum, d.decay)
+              for d in self._fuse_dns if d.training and d.update_norm]
+        return pack, dn
 
     def step(self, grad_scale: float = 1.0):
         if self.a.flat.is_cuda:
-            _native.hip().adam_flat(self.a.flat, self.a.grad, self.m, self.v, self.pows, self.lr, self.b1, self.b2,
-                                    self.eps, grad_scale, self.wd, self.clear_grad)
+            pack, dn = self._extras()
+            _native.hip().adam_fused(self.a.flat, self.a.grad, self.m, self.v, self.pows, self.ticket, self.lr,
+                                     self.b1, self.b2, self.eps, grad_scale, self.wd, self.clear_grad, pack, dn)
         else:
             self.pows[0] *= self.b1
             self.pows[1] *= self.b2
@@ -139,6 +178,7 @@ class DenseSync:
         if self.active:
             dist.all_reduce(self.a.flat, group=self.group)
             self.a.flat.mul_(1.0 / self.world)
+            self.a.notify_modified()
 
 
 class FlatSGD:

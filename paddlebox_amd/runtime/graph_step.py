@@ -18,6 +18,8 @@ from typing import Any, Callable, List, Sequence
 
 import torch
 
+from .. import _native
+
 
 def _tensor_fields(b) -> List[str]:
     return [f.name for f in dataclasses.fields(b) if isinstance(getattr(b, f.name), torch.Tensor)]
@@ -58,7 +60,7 @@ def clone_batch(b, device):
 
 class GraphedTrainStep:
     def __init__(self, step_fn: Callable[[Any], Any], example_batch, device, n_buffers: int = 2,
-                 warmup: int = 3):
+                 warmup: int = 3, max_inflight: int = 3):
         self.device = torch.device(device)
         self.step_fn = step_fn
         self.fields = _tensor_fields(example_batch)
@@ -85,6 +87,14 @@ class GraphedTrainStep:
         self.free = [torch.cuda.Event() for _ in self.bufs]
         for e in self.free:
             e.record(cur)
+        # Host throttle: replay i waits (on the host) for replay i - max_inflight
+        # to finish.  Unthrottled, the host runs tens of steps ahead and the
+        # runtime periodically blocks it for 6-12 ms to recycle its launch
+        # resources (profiles/r2_h2d_stall.txt) -- far longer than the queued
+        # GPU work -- so a bounded queue is both steadier and faster.
+        self.max_inflight = max(1, int(max_inflight))
+        self.done = [torch.cuda.Event() for _ in range(self.max_inflight)]
+        self.step_no = 0
 
     @property
     def n(self) -> int:
@@ -97,7 +107,11 @@ class GraphedTrainStep:
         with torch.cuda.stream(self.copy_stream):
             self.copy_stream.wait_event(self.free[i])
             if src_flat is not None and src_flat.numel() == dst._flat.numel():
-                dst._flat.copy_(src_flat, non_blocking=True)  # same layout: one DMA
+                if src_flat.is_pinned():
+                    # one raw DMA; reuse of both buffers is ordered by free/ready
+                    _native.hip().memcpy_h2d(dst._flat, src_flat)
+                else:
+                    dst._flat.copy_(src_flat, non_blocking=True)
             else:
                 for f in self.fields:
                     getattr(dst, f).copy_(getattr(host_batch, f), non_blocking=True)
@@ -105,10 +119,15 @@ class GraphedTrainStep:
 
     def run(self, i: int):
         cur = torch.cuda.current_stream(self.device)
+        slot = self.step_no % self.max_inflight
+        if self.step_no >= self.max_inflight:
+            self.done[slot].synchronize()
         cur.wait_event(self.ready[i])
         g, out = self.graphs[i]
         g.replay()
         self.free[i].record(cur)
+        self.done[slot].record(cur)
+        self.step_no += 1
         return out
 
     def warm(self, host_batches: Sequence[Any], replays: int = 32):

@@ -23,9 +23,9 @@ def rel(p):
     return os.path.relpath(p, ROOT)
 
 
-hip_sources = sorted(glob.glob(os.path.join(ROOT, "csrc", "hip", "*.hip"))) + [
-    os.path.join(ROOT, "csrc", "hip", "bindings.cpp")
-]
+hip_sources = sorted(glob.glob(os.path.join(ROOT, "csrc", "hip", "*.hip"))) + sorted(
+    glob.glob(os.path.join(ROOT, "csrc", "hip", "*.cpp"))
+)
 host_sources = sorted(glob.glob(os.path.join(ROOT, "csrc", "host", "*.cc")))
 
 exts = [
