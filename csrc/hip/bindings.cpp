@@ -162,7 +162,7 @@ class GpuTable {
   bool push_merge_apply(const Tensor& dout, int col_offset, const Tensor& cvm, bool use_cvm, bool clk_filter, int E,
                         const Tensor& perm, const Tensor& uid, const Tensor& occ_slot, const Tensor& occ_ins,
                         const Tensor& slot_ids, const Tensor& n_valid, Tensor acc, Tensor inc, float bs_scale,
-                        const Tensor& rows, const SparseSGDConfig& cfg, uint64_t seed) {
+                        const Tensor& rows, const SparseSGDConfig& cfg, uint64_t seed, int embed_thres_size) {
     check_cuda(dout, "dout");
     check_cuda(cvm, "cvm");
     check_cuda(acc, "acc");
@@ -192,6 +192,7 @@ class GpuTable {
     a.push_index = nullptr;
     a.bs_scale = bs_scale;
     a.dim = dim_;
+    a.embed_thres_size = use_cvm ? 0 : embed_thres_size;
     return launch_push_merge_apply(a, view(), ptr<int64_t>(rows), ptr<int32_t>(inc), cfg, seed, cur_stream());
   }
   void clear() {
@@ -291,7 +292,8 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
                             int cvm_offset, bool clk_filter, float pad_value, bool need_filter, float show_coeff,
                             float clk_coeff, float threshold, int quant_ratio, bool embed_threshold_filter,
                             float embed_threshold, int embed_thres_size, const c10::optional<Tensor>& dense,
-                            int dense_col) {
+                            int dense_col, const c10::optional<Tensor>& occ_slot,
+                            const c10::optional<Tensor>& occ_ins) {
   check_cuda(src, "src");
   check_cuda(uid, "uid");
   check_cuda(lod, "lod");
@@ -323,6 +325,12 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
   a.embed_threshold = embed_threshold;
   a.embed_thres_size = embed_thres_size;
   PBX_CHECK(col_offset + (int64_t)S * seqpool_cvm_out_width(a) <= out.size(1), "out too narrow");
+  if (occ_slot.has_value() && occ_slot->defined()) {  // occurrence map written by the same launch
+    PBX_CHECK(occ_ins.has_value() && occ_ins->defined(), "occ_ins required with occ_slot");
+    PBX_CHECK(occ_slot->numel() >= uid.numel() && occ_ins->numel() >= uid.numel(), "occ buffers too small");
+    a.occ_slot = ptr<int32_t>(*occ_slot);
+    a.occ_ins = ptr<int32_t>(*occ_ins);
+  }
   if (dense.has_value() && dense->defined()) {
     check_cuda(*dense, "dense");
     PBX_CHECK(dense->dim() == 2 && dense->size(0) == B && dense->scalar_type() == torch::kFloat32,
@@ -338,7 +346,7 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
 static void push_merge(const Tensor& dout, int col_offset, const Tensor& cvm, int cvm_offset, bool use_cvm,
                        bool clk_filter, int E, const Tensor& perm, const Tensor& uid, const Tensor& occ_slot,
                        const Tensor& occ_ins, const Tensor& slot_ids, const Tensor& n_valid, Tensor push,
-                       const c10::optional<Tensor>& push_index, float bs_scale, int dim) {
+                       const c10::optional<Tensor>& push_index, float bs_scale, int dim, int embed_thres_size) {
   check_cuda(dout, "dout");
   check_cuda(cvm, "cvm");
   check_cuda(push, "push");
@@ -367,6 +375,7 @@ static void push_merge(const Tensor& dout, int col_offset, const Tensor& cvm, in
   a.push_index = optr<int64_t>(push_index);
   a.bs_scale = bs_scale;
   a.dim = dim;
+  a.embed_thres_size = use_cvm ? 0 : embed_thres_size;
   launch_push_merge(a, cur_stream());
 }
 
@@ -907,8 +916,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cvm_offset"), py::arg("clk_filter"), py::arg("pad_value"), py::arg("need_filter"),
         py::arg("show_coeff"), py::arg("clk_coeff"), py::arg("threshold"), py::arg("quant_ratio"),
         py::arg("embed_threshold_filter"), py::arg("embed_threshold"), py::arg("embed_thres_size"),
-        py::arg("dense") = py::none(), py::arg("dense_col") = 0);
-  m.def("push_merge", &push_merge);
+        py::arg("dense") = py::none(), py::arg("dense_col") = 0, py::arg("occ_slot") = py::none(),
+        py::arg("occ_ins") = py::none());
+  m.def("push_merge", &push_merge, py::arg("dout"), py::arg("col_offset"), py::arg("cvm"), py::arg("cvm_offset"),
+        py::arg("use_cvm"), py::arg("clk_filter"), py::arg("E"), py::arg("perm"), py::arg("uid"), py::arg("occ_slot"),
+        py::arg("occ_ins"), py::arg("slot_ids"), py::arg("n_valid"), py::arg("push"), py::arg("push_index"),
+        py::arg("bs_scale"), py::arg("dim"), py::arg("embed_thres_size") = 0);
   m.def("push_merge_records", &push_merge_records);
   m.def("shard_pack", &shard_pack);
   m.def("shard_pack_hash", &shard_pack_hash);

@@ -130,6 +130,10 @@ struct SeqpoolCvmArgs {
   const float* dense = nullptr;
   int dense_dim = 0;
   int dense_col = 0;
+  // optional occurrence map (occ_slot[k] = s, occ_ins[k] = b) written as the
+  // keys are walked, so the push needs no separate fill launch
+  int32_t* occ_slot = nullptr;
+  int32_t* occ_ins = nullptr;
 };
 int seqpool_cvm_out_width(const SeqpoolCvmArgs& a);
 void launch_seqpool_cvm_fwd(const SeqpoolCvmArgs& a, hipStream_t s);
@@ -160,6 +164,7 @@ struct PushMergeArgs {
   const int64_t* push_index = nullptr;  // unique -> push row (nullable: identity)
   float bs_scale = 1.f;              // multiply embed grads by -bs_scale
   int dim = 8;
+  int embed_thres_size = 0;          // use_cvm = 0: leading embed columns dropped from the output
 };
 void launch_push_merge(const PushMergeArgs& a, hipStream_t s);
 // Owner-side merge of received push records rec[j] (j over n entries) keyed by

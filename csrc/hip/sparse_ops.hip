@@ -113,6 +113,10 @@ __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
 #pragma unroll
   for (int c = 0; c < E; ++c) acc[c] = a.pad_value;
   for (int64_t k = st; k < en; ++k) {
+    if (a.occ_slot) {
+      a.occ_slot[k] = s;
+      a.occ_ins[k] = b;
+    }
     const int32_t u = a.uid[k];
     if (u < 0) continue;
     const int64_t ri = a.src_index ? a.src_index[u] : (int64_t)u;
@@ -123,8 +127,10 @@ __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
       const float show = v[0], clk = v[1];
       if ((show - clk) * a.show_coeff + clk * a.clk_coeff < a.threshold) continue;
       if (a.embed_threshold_filter) {
+        // 0 means the whole embedding (fused_seqpool_cvm_op.cu:596-599)
+        const int ets = a.embed_thres_size > 0 ? a.embed_thres_size : E - a.cvm_offset;
         float sc = 0.f;
-        for (int i = 1; i < a.embed_thres_size; ++i) sc += v[a.cvm_offset + i] * v[a.cvm_offset + i];
+        for (int i = 1; i < ets; ++i) sc += v[a.cvm_offset + i] * v[a.cvm_offset + i];
         sc = sqrtf(sc) + fabsf(v[a.cvm_offset]);
         if (sc < a.embed_threshold) continue;
       }
@@ -138,7 +144,8 @@ __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
     }
   }
   // CVM epilogue, written straight into the concatenated output row
-  const int Eo = a.use_cvm ? (a.clk_filter ? E - 1 : E) : E - a.cvm_offset;
+  const int skip = a.use_cvm ? 0 : a.cvm_offset + a.embed_thres_size;
+  const int Eo = a.use_cvm ? (a.clk_filter ? E - 1 : E) : E - skip;
   float* o = a.out + (int64_t)b * a.out_stride + a.col_offset + (int64_t)s * Eo;
   if (a.use_cvm) {
     const float ls = logf(acc[0] + 1.f);
@@ -154,7 +161,7 @@ __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
   } else {
 #pragma unroll
     for (int c = 0; c < E; ++c)
-      if (c >= a.cvm_offset) o[c - a.cvm_offset] = acc[c];
+      if (c >= skip) o[c - skip] = acc[c];
   }
 }
 
@@ -170,8 +177,16 @@ __global__ void k_seqpool_cvm_generic(SeqpoolCvmArgs a) {
     for (int c = 0; c < a.dense_dim; ++c) dst[c] = src[c];
   }
   const int64_t st = a.lod[(int64_t)s * (a.B + 1) + b], en = a.lod[(int64_t)s * (a.B + 1) + b + 1];
-  const int Eo = a.use_cvm ? (a.clk_filter ? E - 1 : E) : E - a.cvm_offset;
+  const int skip = a.use_cvm ? 0 : a.cvm_offset + a.embed_thres_size;
+  const int Eo = a.use_cvm ? (a.clk_filter ? E - 1 : E) : E - skip;
+  const int ets = a.embed_thres_size > 0 ? a.embed_thres_size : E - a.cvm_offset;
   float* o = a.out + (int64_t)b * a.out_stride + a.col_offset + (int64_t)s * Eo;
+  if (a.occ_slot) {
+    for (int64_t k = st; k < en; ++k) {
+      a.occ_slot[k] = s;
+      a.occ_ins[k] = b;
+    }
+  }
   float show_sum = a.pad_value, clk_sum = a.pad_value;
   for (int c = 0; c < E; ++c) {
     float acc = a.pad_value;
@@ -181,7 +196,14 @@ __global__ void k_seqpool_cvm_generic(SeqpoolCvmArgs a) {
       const int64_t ri = a.src_index ? a.src_index[u] : (int64_t)u;
       if (ri < 0) continue;
       const float* v = a.src + ri * (int64_t)a.src_stride;
-      if (a.need_filter && (v[0] - v[1]) * a.show_coeff + v[1] * a.clk_coeff < a.threshold) continue;
+      if ((a.need_filter || a.embed_threshold_filter) &&
+          (v[0] - v[1]) * a.show_coeff + v[1] * a.clk_coeff < a.threshold)
+        continue;
+      if (a.embed_threshold_filter) {
+        float sc = 0.f;
+        for (int i = 1; i < ets; ++i) sc += v[a.cvm_offset + i] * v[a.cvm_offset + i];
+        if (sqrtf(sc) + fabsf(v[a.cvm_offset]) < a.embed_threshold) continue;
+      }
       acc += (a.quant_ratio > 0 && c >= a.cvm_offset) ? quant(v[c], a.quant_ratio) : v[c];
     }
     if (c == 0) show_sum = acc;
@@ -190,8 +212,8 @@ __global__ void k_seqpool_cvm_generic(SeqpoolCvmArgs a) {
       if (c == 0) o[0] = logf(show_sum + 1.f);
       else if (c == 1) { if (!a.clk_filter) o[1] = logf(clk_sum + 1.f) - logf(show_sum + 1.f); }
       else o[a.clk_filter ? c - 1 : c] = acc;
-    } else if (c >= a.cvm_offset) {
-      o[c - a.cvm_offset] = acc;
+    } else if (c >= skip) {
+      o[c - skip] = acc;
     }
   }
 }
@@ -203,14 +225,16 @@ struct DoutSource {
   __device__ __forceinline__ void load(int32_t k, float* g, int Q) const {
     const int b = a.occ_ins[k], s = a.occ_slot[k];
     const int co = a.cvm_offset;
-    g[0] = a.cvm[(int64_t)b * co + 0];
-    g[1] = co > 1 ? a.cvm[(int64_t)b * co + 1] : 0.f;
+    const int ets = a.use_cvm ? 0 : a.embed_thres_size;
+    // dropped columns: zero grads, and the cvm ones too (op.cu:958-969)
+    g[0] = ets ? 0.f : a.cvm[(int64_t)b * co + 0];
+    g[1] = (co > 1 && !ets) ? a.cvm[(int64_t)b * co + 1] : 0.f;
     const int E = a.E;
-    const int Eo = a.use_cvm ? (a.clk_filter ? E - 1 : E) : E - co;
+    const int Eo = a.use_cvm ? (a.clk_filter ? E - 1 : E) : E - co - ets;
     const float* d = a.dout + (int64_t)b * a.out_stride + a.col_offset + (int64_t)s * Eo;
     for (int c = co; c < E; ++c) {
-      const int oc = a.use_cvm ? (a.clk_filter ? c - 1 : c) : c - co;
-      g[2 + (c - co)] = d[oc];
+      const int oc = a.use_cvm ? (a.clk_filter ? c - 1 : c) : c - co - ets;
+      g[2 + (c - co)] = oc >= 0 ? d[oc] : 0.f;
     }
     (void)Q;
   }
@@ -699,7 +723,7 @@ void launch_gather_pull(const TableDev& t, const int64_t* rows, const int32_t* n
 }
 
 int seqpool_cvm_out_width(const SeqpoolCvmArgs& a) {
-  return a.use_cvm ? (a.clk_filter ? a.E - 1 : a.E) : a.E - a.cvm_offset;
+  return a.use_cvm ? (a.clk_filter ? a.E - 1 : a.E) : a.E - a.cvm_offset - a.embed_thres_size;
 }
 
 void launch_seqpool_cvm_fwd(const SeqpoolCvmArgs& a, hipStream_t s) {

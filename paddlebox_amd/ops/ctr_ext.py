@@ -129,7 +129,8 @@ class _SeqpoolCvmVariant(torch.autograd.Function):
             co = a.get("cvm_offset", 2)
             if a.get("embed_threshold_filter"):
                 ets = a.get("embed_thres_size", 0)
-                emb = x[:, co:co + max(ets, 1)]
+                ets = ets if ets > 0 else E - co  # 0 = the whole embedding (op.cu:596-599)
+                emb = x[:, co:co + ets]
                 score = emb[:, 1:].pow(2).sum(1).sqrt() + emb[:, 0].abs()
                 keep &= score >= a["embed_threshold"]
             q = a.get("quant_ratio", 0)
@@ -286,9 +287,10 @@ def _cvm_epilogue_grad(variant, dout, a, E, cvm_in, qvals, B):
             g[:, mco:] = dout
         return g
     ncv = min(co, cv.shape[1])
-    g[:, :ncv] = cv[:, :ncv]
+    skip = a.get("embed_thres_size", 0) if (variant == "std" and not use_cvm) else 0
+    if skip == 0:  # with dropped columns the cvm grads are zero too (op.cu:958-969)
+        g[:, :ncv] = cv[:, :ncv]
     if not use_cvm:
-        skip = a.get("embed_thres_size", 0) if variant == "std" else 0
         g[:, co + skip:] = dout
         return g
     if variant in ("std", "diff_thres", "tradew"):

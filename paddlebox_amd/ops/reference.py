@@ -159,8 +159,10 @@ def seqpool_cvm(
         show, clk = rows[:, 0], rows[:, 1]
         keep &= (show - clk) * show_coeff + clk * clk_coeff >= threshold
         if embed_threshold_filter:
+            # 0 means the whole embedding (fused_seqpool_cvm_op.cu:596-599)
+            ets = embed_thres_size if embed_thres_size > 0 else E - cvm_offset
             e = rows[:, cvm_offset:]
-            sc = torch.sqrt((e[:, 1:embed_thres_size] ** 2).sum(1)) + e[:, 0].abs()
+            sc = torch.sqrt((e[:, 1:ets] ** 2).sum(1)) + e[:, 0].abs()
             keep &= sc >= embed_threshold
     if quant_ratio > 0:
         q = rows[:, cvm_offset:]
@@ -177,12 +179,14 @@ def seqpool_cvm(
         else:
             out = torch.cat([ls, torch.log(pooled[..., 1:2] + 1) - ls, pooled[..., 2:]], -1)
     else:
-        out = pooled[..., cvm_offset:]
+        out = pooled[..., cvm_offset + embed_thres_size:]
     return out.reshape(B, -1)
 
 
-def seqpool_cvm_out_width(E: int, use_cvm: bool, cvm_offset: int, clk_filter: bool) -> int:
-    return (E - 1 if clk_filter else E) if use_cvm else E - cvm_offset
+def seqpool_cvm_out_width(E: int, use_cvm: bool, cvm_offset: int, clk_filter: bool, embed_thres_size: int = 0) -> int:
+    """fused_seqpool_cvm output width (fused_seqpool_cvm_op.cc:85-96): without
+    CVM the cvm columns and embed_thres_size more leading columns are dropped."""
+    return (E - 1 if clk_filter else E) if use_cvm else E - cvm_offset - embed_thres_size
 
 
 def push_merge(
@@ -200,6 +204,7 @@ def push_merge(
     clk_filter: bool = False,
     col_offset: int = 0,
     cvm_offset: int = 2,
+    embed_thres_size: int = 0,
 ) -> torch.Tensor:
     """Per-unique push records [U, 4+dim] = [slot, show, click, embed_g, embedx_g]
     from the pooled-output gradient (fused_seqpool_cvm_op.cu:813-1015 +
@@ -211,13 +216,15 @@ def push_merge(
     occ_slot, occ_ins = occ_slot.to(dev).long(), occ_ins.to(dev).long()
     L = occ_slot.numel()
     uid = uid[:L].to(torch.int64)
-    Eo = seqpool_cvm_out_width(E, use_cvm, cvm_offset, clk_filter)
+    ets = 0 if use_cvm else embed_thres_size
+    Eo = seqpool_cvm_out_width(E, use_cvm, cvm_offset, clk_filter, ets)
     g = torch.zeros(L, 3 + dim, dtype=torch.float32, device=dev)
-    g[:, 0] = cvm[occ_ins, 0]
-    g[:, 1] = cvm[occ_ins, 1]
+    if ets == 0:  # with dropped columns the cvm grads are zero too (op.cu:958-969)
+        g[:, 0] = cvm[occ_ins, 0]
+        g[:, 1] = cvm[occ_ins, 1]
     base = col_offset + occ_slot * Eo
-    for c in range(cvm_offset, E):
-        oc = (c - 1 if clk_filter else c) if use_cvm else c - cvm_offset
+    for c in range(cvm_offset + ets, E):
+        oc = (c - 1 if clk_filter else c) if use_cvm else c - cvm_offset - ets
         g[:, 2 + c - cvm_offset] = dout[occ_ins, base + oc]
     valid = uid >= 0
     merged = torch.zeros(U, 3 + dim, dtype=torch.float32, device=dev)

@@ -64,6 +64,9 @@ class _CtrTowerFn(torch.autograd.Function):
         ctx.means, ctx.scales, ctx.dz = means, scales, dz
         ctx.has_extra = extra is not None
         ctx.mark_non_differentiable(pred)
+        # no zero-filled grad for pred, no ones-filled grad needed for the loss
+        # (a None dloss means 1): two fill launches less per step
+        ctx.set_materialize_grads(False)
         return loss.view(()), pred
 
     @staticmethod
@@ -74,7 +77,8 @@ class _CtrTowerFn(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         B = x.shape[0]
         mlp.ensure_grads()
-        gl = gl.contiguous().float().view(1)
+        if gl is not None:
+            gl = gl.contiguous().float().view(1)
         dn_on = dn is not None and dn.training and dn.update_norm
         dx0 = ws.backward(gl, mlp.w_out.detach().view(-1), [w.grad for w in mlp.w], [b.grad for b in mlp.b],
                           mlp.w_out.grad.view(-1),
@@ -90,7 +94,7 @@ class _CtrTowerFn(torch.autograd.Function):
         dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim),
                            ctx.means, ctx.scales, dn.eps if dn is not None else 0.0, dlin_scale=gl,
                            want_stats=False)
-        d_extra = ctx.dz * gl if ctx.has_extra else None
+        d_extra = (ctx.dz * gl if gl is not None else ctx.dz.clone()) if ctx.has_extra else None
         return (dx, d_extra, None, None) + (None,) * (len(t._params))
 
 

@@ -52,7 +52,36 @@ class SeqpoolParams:
     embed_thres_size: int = 0
 
     def out_width(self, E: int) -> int:
-        return ref.seqpool_cvm_out_width(E, self.use_cvm, self.cvm_offset, self.clk_filter)
+        return ref.seqpool_cvm_out_width(E, self.use_cvm, self.cvm_offset, self.clk_filter,
+                                         0 if self.use_cvm else self.embed_thres_size)
+
+
+class _PullSlot:
+    """Per-pull device buffers (the dedup workspace, occurrence map and, when
+    sharded, the exchange buffers).  The engine rotates through a ring of these
+    so that several pulls can be outstanding before their pushes -- e.g. two
+    pull ops in one program -- without the second overwriting what the first
+    one's backward needs.  ``gen`` detects a push against a recycled slot."""
+
+    def __init__(self, eng: "SparseEngine"):
+        dev = eng.device
+        h = eng._hip
+        with torch.cuda.device(dev):
+            self.ws = h.DedupWorkspace(eng.max_keys, dev.index or 0, True)
+        self.occ_slot = torch.empty(eng.max_keys, dtype=torch.int32, device=dev)
+        self.occ_ins = torch.empty(eng.max_keys, dtype=torch.int32, device=dev)
+        self.gen = 0
+        if eng.sharded:
+            n = eng.world * eng.C
+            with torch.cuda.device(dev):
+                self.ws_r = h.DedupWorkspace(n, dev.index or 0, True)
+            self.send = torch.empty(n, dtype=torch.int64, device=dev)
+            self.recv = torch.empty(n, dtype=torch.int64, device=dev)
+            self.send_index = torch.empty(eng.max_keys, dtype=torch.int64, device=dev)
+            self.ocnt = torch.zeros(eng.world, dtype=torch.int32, device=dev)
+            self.resp = torch.empty(n, eng.P, device=dev)
+            self.resp_back = torch.empty(n, eng.P, device=dev)
+            self.rows_r = None
 
 
 @dataclass
@@ -70,6 +99,8 @@ class PullState:
     rows: torch.Tensor = None  # world==1: table rows per unique
     send_index: Optional[torch.Tensor] = None
     rows_r: Optional[torch.Tensor] = None
+    slot: Optional[_PullSlot] = None  # GPU: the buffers this pull used
+    gen: int = 0
     extra: dict = field(default_factory=dict)
 
 
@@ -87,6 +118,7 @@ class SparseEngine:
         cap_factor: float = 1.25,
         auto_insert: bool = False,
         comm: Optional[Comm] = None,
+        pull_ring: int = 2,
     ):
         self.cfg = cfg
         self.dim = cfg.embedx_dim
@@ -110,24 +142,16 @@ class SparseEngine:
             self.table = GpuSparseTable(self.dim, shard_cap, self.device)
             self._hip = _native.hip()
             self._sgd_native = cfg.sgd.to_native(self._hip)
-            with torch.cuda.device(self.device):
-                # sort-free hash dedup everywhere: the sender packs its unique
-                # keys per owner with a counting pass (shard_pack_hash)
-                self.ws = self._hip.DedupWorkspace(self.max_keys, self.device.index or 0, True)
-            self.occ_slot = torch.empty(self.max_keys, dtype=torch.int32, device=self.device)
-            self.occ_ins = torch.empty(self.max_keys, dtype=torch.int32, device=self.device)
             if self.sharded:
                 self.C = int(math.ceil(self.max_keys / self.world * cap_factor)) + 64
+            # ring of per-pull buffers (sort-free hash dedup everywhere: the
+            # sender packs its unique keys per owner with a counting pass)
+            self._slots = [_PullSlot(self) for _ in range(max(1, int(pull_ring)))]
+            self._next_slot = 0
+            self._cur = self._slots[0]
+            if self.sharded:
                 n = self.world * self.C
-                with torch.cuda.device(self.device):
-                    self.ws_r = self._hip.DedupWorkspace(n, self.device.index or 0, True)
-                self.send = torch.empty(n, dtype=torch.int64, device=self.device)
-                self.recv = torch.empty(n, dtype=torch.int64, device=self.device)
-                self.send_index = torch.empty(self.max_keys, dtype=torch.int64, device=self.device)
                 self.overflow = torch.zeros(1, dtype=torch.int32, device=self.device)
-                self.ocnt = torch.zeros(self.world, dtype=torch.int32, device=self.device)
-                self.resp = torch.empty(n, self.P, device=self.device)
-                self.resp_back = torch.empty(n, self.P, device=self.device)
                 self.push_send = torch.empty(n, self.Q, device=self.device)
                 self.push_recv = torch.empty(n, self.Q, device=self.device)
                 self.push_merged = torch.empty(n, self.Q, device=self.device)
@@ -187,57 +211,78 @@ class SparseEngine:
             if dense is not None:
                 out[:, dense_col:dense_col + dense.shape[1]] = dense
             return st
-        st = self._pull_common(keys, lod, B, S)
+        # the occurrence map is written by the seqpool launch itself
+        st = self._pull_common(keys, lod, B, S, fill_occ=False)
+        sl = st.slot
         h = self._hip
         if not self.sharded:
             src, src_index = self.table.values, st.rows
         else:
-            src, src_index = self.resp_back, self.send_index
+            src, src_index = sl.resp_back, sl.send_index
         if dense is not None:
             dense = dense.contiguous().float()
-        h.seqpool_cvm_fwd(src, src_index, self.ws.uid, lod, S, B, self.E, out, col_offset, sp.use_cvm,
+        h.seqpool_cvm_fwd(src, src_index, sl.ws.uid, lod, S, B, self.E, out, col_offset, sp.use_cvm,
                           sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter, sp.show_coeff, sp.clk_coeff,
                           sp.threshold, sp.quant_ratio, sp.embed_threshold_filter, sp.embed_threshold,
-                          sp.embed_thres_size, dense, dense_col)
+                          sp.embed_thres_size if not sp.use_cvm else 0, dense, dense_col,
+                          occ_slot=sl.occ_slot, occ_ins=sl.occ_ins)
         return st
 
-    def _pull_common(self, keys, lod, B, S) -> PullState:
+    def _take_slot(self) -> _PullSlot:
+        sl = self._slots[self._next_slot % len(self._slots)]
+        self._next_slot += 1
+        sl.gen += 1
+        self._cur = sl
+        return sl
+
+    def _check_slot(self, st: PullState) -> _PullSlot:
+        sl = st.slot
+        if sl is None or sl.gen != st.gen:
+            raise RuntimeError(
+                f"stale pull state: its buffers were reused by a later pull (more than {len(self._slots)} pulls "
+                "outstanding before their push); construct the SparseEngine with a larger pull_ring")
+        return sl
+
+    def _pull_common(self, keys, lod, B, S, fill_occ: bool = True) -> PullState:
         h = self._hip
         L = keys.numel()
         assert L <= self.max_keys, f"batch has {L} keys > engine max_keys {self.max_keys}"
-        self.ws.run(keys, False)
-        h.fill_occurrence(lod, S, B, self.occ_slot, self.occ_ins)
-        st = PullState(B=B, S=S, L=L, lod=lod, uid=self.ws.uid, perm=self.ws.perm, counts=self.ws.u_count)
+        sl = self._take_slot()
+        ws = sl.ws
+        ws.run(keys, False)
+        if fill_occ:
+            h.fill_occurrence(lod, S, B, sl.occ_slot, sl.occ_ins)
+        st = PullState(B=B, S=S, L=L, lod=lod, uid=ws.uid, perm=ws.perm, counts=ws.u_count, slot=sl, gen=sl.gen)
         if not self.sharded:
-            st.rows = self.table.probe(self.ws.uniq_h[:L], self.ws.u_count)
+            st.rows = self.table.probe(ws.uniq_h[:L], ws.u_count)
             if self.auto_insert and not self.test_mode:
                 self._auto_insert(st, L)
             return st
         # sharded: pack per-owner, exchange keys, owner-side dedup/probe/gather
-        h.shard_pack_hash(self.ws.uniq_h, self.ws.u_count, self.world, self.C, self.send, self.send_index,
-                          self.ocnt, self.overflow)
-        self.comm.all_to_all_single(self.recv, self.send)
-        self.ws_r.run(self.recv, True)
-        rows_r = self.table.probe(self.ws_r.uniq_h, self.ws_r.u_count)
+        h.shard_pack_hash(ws.uniq_h, ws.u_count, self.world, self.C, sl.send, sl.send_index, sl.ocnt, self.overflow)
+        self.comm.all_to_all_single(sl.recv, sl.send)
+        sl.ws_r.run(sl.recv, True)
+        rows_r = self.table.probe(sl.ws_r.uniq_h, sl.ws_r.u_count)
         if self.auto_insert and not self.test_mode:
-            miss = (rows_r[: int(self.ws_r.u_count[0].item())] < 0)
+            miss = (rows_r[: int(sl.ws_r.u_count[0].item())] < 0)
             if bool(miss.any()):
-                U = int(self.ws_r.u_count[0].item())
-                self.table.insert_mixed(self.ws_r.uniq_h[:U][miss], self.cfg.sgd)
-                rows_r = self.table.probe(self.ws_r.uniq_h, self.ws_r.u_count)
+                U = int(sl.ws_r.u_count[0].item())
+                self.table.insert_mixed(sl.ws_r.uniq_h[:U][miss], self.cfg.sgd)
+                rows_r = self.table.probe(sl.ws_r.uniq_h, sl.ws_r.u_count)
         # owner answers straight from the table rows (no intermediate pull buffer)
-        self.table.t.gather_rows_by_uid(rows_r, self.ws_r.uid, self.resp)
-        self.comm.all_to_all_single(self.resp_back, self.resp)
-        st.send_index = self.send_index[:L]
+        self.table.t.gather_rows_by_uid(rows_r, sl.ws_r.uid, sl.resp)
+        self.comm.all_to_all_single(sl.resp_back, sl.resp)
+        st.send_index = sl.send_index[:L]
         st.rows_r = rows_r
         return st
 
     def _auto_insert(self, st: PullState, L: int):
-        U = int(self.ws.u_count[0].item())
+        ws = st.slot.ws
+        U = int(ws.u_count[0].item())
         miss = st.rows[:U] < 0
         if bool(miss.any()):
-            self.table.insert_mixed(self.ws.uniq_h[:U][miss], self.cfg.sgd)
-            st.rows = self.table.probe(self.ws.uniq_h[:L], self.ws.u_count)
+            self.table.insert_mixed(ws.uniq_h[:U][miss], self.cfg.sgd)
+            st.rows = self.table.probe(ws.uniq_h[:L], ws.u_count)
 
     # ------------------------------------------------------------------ push
     def push_seqpool_cvm(self, st: PullState, dout: torch.Tensor, cvm: torch.Tensor, col_offset: int,
@@ -247,39 +292,42 @@ class SparseEngine:
             return
         if not self.is_gpu:
             return self._cpu_push(st, dout, cvm, col_offset, sp, bs_scale)
+        sl = self._check_slot(st)
+        ws = sl.ws
         h = self._hip
         L = st.L
         dout = dout.contiguous()
+        ets = 0 if sp.use_cvm else sp.embed_thres_size
         if not self.sharded:
             if sp.cvm_offset == 2 and cvm.shape[1] == 2:
                 self._seed += 1
                 if self.table.t.push_merge_apply(dout, col_offset, cvm.contiguous(), sp.use_cvm, sp.clk_filter, self.E,
-                                                 self.ws.perm[:L], self.ws.uid, self.occ_slot, self.occ_ins,
-                                                 self._slot_ids(st.S), self.ws.u_count[1:], self.push_acc,
+                                                 ws.perm[:L], ws.uid, sl.occ_slot, sl.occ_ins,
+                                                 self._slot_ids(st.S), ws.u_count[1:], self.push_acc,
                                                  self.push_inc, float(bs_scale), st.rows, self._sgd_native,
-                                                 self._seed):
+                                                 self._seed, ets):
                     return
                 self._seed -= 1
             push = self.push_buf
             push[:L].zero_()
             h.push_merge(dout, col_offset, cvm.contiguous(), sp.cvm_offset, sp.use_cvm, sp.clk_filter, self.E,
-                         self.ws.perm[:L], self.ws.uid, self.occ_slot, self.occ_ins, self._slot_ids(st.S),
-                         self.ws.u_count[1:], push[:L], None, float(bs_scale), self.dim)
+                         ws.perm[:L], ws.uid, sl.occ_slot, sl.occ_ins, self._slot_ids(st.S),
+                         ws.u_count[1:], push[:L], None, float(bs_scale), self.dim, ets)
             self._seed += 1
-            self.table.t.push_adagrad(st.rows, push[:L], self.ws.u_count, self._sgd_native, self._seed)
+            self.table.t.push_adagrad(st.rows, push[:L], ws.u_count, self._sgd_native, self._seed)
             return
         self.push_send.zero_()
         h.push_merge(dout, col_offset, cvm.contiguous(), sp.cvm_offset, sp.use_cvm, sp.clk_filter, self.E,
-                     self.ws.perm[:L], self.ws.uid, self.occ_slot, self.occ_ins, self._slot_ids(st.S),
-                     self.ws.u_count[1:], self.push_send, st.send_index, float(bs_scale), self.dim)
+                     ws.perm[:L], ws.uid, sl.occ_slot, sl.occ_ins, self._slot_ids(st.S),
+                     ws.u_count[1:], self.push_send, st.send_index, float(bs_scale), self.dim, ets)
         self.comm.all_to_all_single(self.push_recv, self.push_send)
-        self._owner_update(st.rows_r, self.push_recv)
+        self._owner_update(sl, st.rows_r, self.push_recv)
 
-    def _owner_update(self, rows_r: torch.Tensor, recv: torch.Tensor):
+    def _owner_update(self, sl: _PullSlot, rows_r: torch.Tensor, recv: torch.Tensor):
         """Owner side of the push: each unique key got at most one merged record
         per sender; merge them and apply sparse Adagrad in one kernel."""
         self._seed += 1
-        ws = self.ws_r
+        ws = sl.ws_r
         if self.table.t.push_adagrad_seg(rows_r, recv, ws.perm, ws.seg, ws.cnt, ws.u_count, self._sgd_native,
                                          self._seed):
             return
@@ -310,15 +358,16 @@ class SparseEngine:
             recs = torch.where((keys != -1).unsqueeze(1), pulled[uid.long().clamp(min=0)], torch.zeros(1))
             return recs[:, : self.E], st
         st = self._pull_common(keys, lod, B, S)
+        sl = st.slot
         if not self.sharded:
-            pulled = self.table.t.gather_pull(st.rows, self.ws.u_count, self.P)
+            pulled = self.table.t.gather_pull(st.rows, sl.ws.u_count, self.P)
             recs = torch.empty(L, self.P, device=self.device)
-            self._hip.gather_by_uid(pulled, self.ws.uid[:L], recs, self.P)
+            self._hip.gather_by_uid(pulled, sl.ws.uid[:L], recs, self.P)
         else:
             # resp_back rows indexed by send_index[uid]
-            idx = self.send_index[:L][self.ws.uid[:L].long().clamp(min=0)]
-            ok = (self.ws.uid[:L] >= 0) & (idx >= 0)
-            recs = torch.where(ok.unsqueeze(1), self.resp_back[idx.clamp(min=0)], torch.zeros((), device=self.device))
+            idx = sl.send_index[:L][sl.ws.uid[:L].long().clamp(min=0)]
+            ok = (sl.ws.uid[:L] >= 0) & (idx >= 0)
+            recs = torch.where(ok.unsqueeze(1), sl.resp_back[idx.clamp(min=0)], torch.zeros((), device=self.device))
         return recs[:, : self.E], st
 
     def push_records(self, st: PullState, grads: torch.Tensor, cvm_cols: int, bs_scale: float,
@@ -348,24 +397,26 @@ class SparseEngine:
             merged[st.uid[ok].long(), 0] = rec[ok, 0]
             self.table.push_adagrad(st.rows, merged, self.cfg.sgd)
             return
+        sl = self._check_slot(st)
+        ws = sl.ws
         h = self._hip
         if not self.sharded:
             push = self.push_buf
             push[:L].zero_()
-            h.push_merge_records(rec, self.ws.perm[:L], self.ws.uid, self.ws.u_count[1:], D, push[:L])
+            h.push_merge_records(rec, ws.perm[:L], ws.uid, ws.u_count[1:], D, push[:L])
             self._seed += 1
-            self.table.t.push_adagrad(st.rows, push[:L], self.ws.u_count, self._sgd_native, self._seed)
+            self.table.t.push_adagrad(st.rows, push[:L], ws.u_count, self._sgd_native, self._seed)
             return
         # merge locally per unique into the owner send layout, then exchange
         U_cap = L
         merged = torch.zeros(U_cap, self.Q, device=self.device)
-        h.push_merge_records(rec, self.ws.perm[:L], self.ws.uid, self.ws.u_count[1:], D, merged)
+        h.push_merge_records(rec, ws.perm[:L], ws.uid, ws.u_count[1:], D, merged)
         self.push_send.zero_()
         idx = st.send_index
         ok = idx >= 0
         self.push_send[idx[ok]] = merged[ok]
         self.comm.all_to_all_single(self.push_recv, self.push_send)
-        self._owner_update(st.rows_r, self.push_recv)
+        self._owner_update(sl, st.rows_r, self.push_recv)
 
     # ------------------------------------------------------------------ CPU path
     def _cpu_pull_seqpool(self, keys, lod, B, S, out, col_offset, sp: SeqpoolParams) -> PullState:
@@ -420,7 +471,7 @@ class SparseEngine:
     def _cpu_push(self, st: PullState, dout, cvm, col_offset, sp: SeqpoolParams, bs_scale):
         U = st.extra["U"]
         push = ref.push_merge(dout, cvm, st.uid, st.lod, st.S, st.B, U, self.dim, self._slot_ids(st.S), bs_scale,
-                              sp.use_cvm, sp.clk_filter, col_offset, sp.cvm_offset)
+                              sp.use_cvm, sp.clk_filter, col_offset, sp.cvm_offset, sp.embed_thres_size)
         if not self.sharded:
             self.table.push_adagrad(st.rows, push, self.cfg.sgd)
             return

@@ -412,3 +412,85 @@ def test_logit_loss_multiblock(B):
     torch.testing.assert_close(pred.double(), pe, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(dz.double(), (pe - y.double()) / B, rtol=1e-5, atol=1e-9)
     assert float(loss) == pytest.approx(float(le), rel=1e-5)
+
+
+def test_two_outstanding_pulls_push_their_own_state():
+    """Two pulls before either push (two pull ops in one program): each push
+    must use its own pull's dedup/occurrence buffers (pull ring).  Expected:
+    the same table as pull2 -> push2 -> pull1 -> push1 on a fresh engine (push
+    results depend on the gradients and key structure, not on pulled values)."""
+    b1 = ragged_batch(48, 5, 4, 40, seed=21, device=DEV)
+    b2 = ragged_batch(48, 5, 4, 40, seed=22, device=DEV)
+    g = torch.Generator(device=DEV).manual_seed(7)
+    d1 = torch.randn(b1.B, b1.S * 11, device=DEV, generator=g) * 0.01
+    d2 = torch.randn(b2.B, b2.S * 11, device=DEV, generator=g) * 0.01
+    sp = SeqpoolParams()
+    tables = []
+    for mode in ("interleaved", "one_at_a_time"):
+        eng = _engine()
+        eng.register_keys(torch.cat([b1.keys, b2.keys]), init_embedx=True)
+        l = row_layout(8)
+        vals = eng.table.values
+        vals[:, l["mf_size"]] = 1  # embedx already created: updates are deterministic
+        o1 = torch.zeros(b1.B, b1.S * 11, device=DEV)
+        o2 = torch.zeros(b2.B, b2.S * 11, device=DEV)
+        if mode == "interleaved":
+            s1 = eng.pull_seqpool_cvm(b1.keys, b1.lod, b1.B, b1.S, o1, 0, sp)
+            s2 = eng.pull_seqpool_cvm(b2.keys, b2.lod, b2.B, b2.S, o2, 0, sp)
+            eng.push_seqpool_cvm(s2, d2, b2.cvm, 0, sp, float(b2.B))
+            eng.push_seqpool_cvm(s1, d1, b1.cvm, 0, sp, float(b1.B))
+        else:
+            s2 = eng.pull_seqpool_cvm(b2.keys, b2.lod, b2.B, b2.S, o2, 0, sp)
+            eng.push_seqpool_cvm(s2, d2, b2.cvm, 0, sp, float(b2.B))
+            s1 = eng.pull_seqpool_cvm(b1.keys, b1.lod, b1.B, b1.S, o1, 0, sp)
+            eng.push_seqpool_cvm(s1, d1, b1.cvm, 0, sp, float(b1.B))
+        uq = torch.unique(torch.cat([b1.keys, b2.keys]))
+        uq = uq[uq != -1]
+        tables.append(eng.table.read(ref.mix64(uq)))
+    torch.testing.assert_close(tables[0], tables[1], rtol=1e-5, atol=1e-6)
+
+
+def test_stale_pull_state_raises():
+    b = ragged_batch(16, 3, 3, 20, seed=11, device=DEV)
+    cfg = PSConfig(embedx_dim=8)
+    eng = SparseEngine(cfg, max_keys=100000, device=torch.device(DEV), capacity=1 << 16, pull_ring=1)
+    eng.register_keys(b.keys)
+    sp = SeqpoolParams()
+    out = torch.zeros(b.B, b.S * 11, device=DEV)
+    s1 = eng.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out, 0, sp)
+    eng.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out, 0, sp)
+    with pytest.raises(RuntimeError, match="stale pull state"):
+        eng.push_seqpool_cvm(s1, torch.zeros_like(out), b.cvm, 0, sp, float(b.B))
+
+
+@pytest.mark.parametrize("ets", [0, 3])
+def test_seqpool_embed_threshold_no_cvm(ets):
+    """embed_threshold_filter with embed_thres_size 0 (= whole embedding) and
+    use_cvm=False dropping cvm_offset + embed_thres_size columns, fwd + push."""
+    b = ragged_batch(32, 4, 5, 40, seed=5, device=DEV)
+    eng = _engine()
+    eng.register_keys(b.keys, init_embedx=True)
+    vals = eng.table.values
+    torch.manual_seed(8)
+    vals[:, :2] = torch.rand_like(vals[:, :2]) * 3
+    vals[:, 2:11] = torch.randn_like(vals[:, 2:11]) * 0.5
+    sp = SeqpoolParams(use_cvm=False, embed_threshold_filter=True, embed_threshold=1.0, embed_thres_size=ets,
+                       threshold=0.0)
+    Eo = sp.out_width(11)
+    assert Eo == 11 - 2 - ets
+    out = torch.zeros(b.B, b.S * Eo, device=DEV)
+    st = eng.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out, 0, sp)
+    uniq, uid = ref.dedup(b.keys)
+    rows = eng.table.probe(uniq)
+    src = vals[rows].clone()
+    exp = ref.seqpool_cvm(src, uid, b.lod, b.S, b.B, 11, use_cvm=False, embed_threshold_filter=True,
+                          embed_threshold=1.0, embed_thres_size=ets, threshold=0.0)
+    torch.testing.assert_close(out, exp, rtol=1e-5, atol=1e-5)
+    dout = torch.randn_like(out) * 0.01
+    before = vals[rows].clone()
+    eng.push_seqpool_cvm(st, dout, b.cvm, 0, sp, float(b.B))
+    push = ref.push_merge(dout, b.cvm, uid, b.lod, b.S, b.B, uniq.numel(), 8, eng._slot_ids(b.S), float(b.B),
+                          use_cvm=False, embed_thres_size=ets)
+    exp_rows = ref.adagrad_update(before, push, 8, eng.cfg.sgd)
+    after = vals[rows]
+    torch.testing.assert_close(after[:, :3], exp_rows[:, :3], rtol=2e-4, atol=2e-5)
