@@ -90,8 +90,26 @@ def main():
     synth = CriteoSynth(total_features=total, alpha=args.alpha, seed=1000 + rank, device=str(device))
     S = synth.S
     cfg = PSConfig(embedx_dim=8)
+
+    # "load into memory": the pass's batches live in pinned host memory; every
+    # step copies its batch H2D (one DMA) on a side stream, overlapped
+    from paddlebox_amd.runtime.graph_step import pack_batch
+
+    host_batches = [pack_batch(synth.batch(B).to("cpu"), pin=True) for _ in range(args.num_batches)]
+    xcap = None
+    if multi:
+        # the pass is known before it is trained (BoxPS feed pass): size the key
+        # exchange exactly by distinct keys per owner, max over batches and ranks
+        from paddlebox_amd.ps.sparse_engine import exchange_capacity_for
+
+        xc = torch.tensor([exchange_capacity_for([hb.keys.to(device) for hb in host_batches], world)], device=device)
+        dist.all_reduce(xc, op=dist.ReduceOp.MAX)
+        xcap = int(xc.item())
+        log(rank, f"[bench] key exchange capacity {xcap} per peer (heuristic bound would be "
+                  f"{int(math.ceil(B * S / world * 1.25)) + 64})")
     engine = SparseEngine(cfg, max_keys=B * S, device=device, capacity=synth.total_features,
-                          slot_ids=[float(s + 1) for s in range(S)], auto_insert=args.no_prefill)
+                          slot_ids=[float(s + 1) for s in range(S)], auto_insert=args.no_prefill,
+                          exchange_capacity=xcap)
 
     t0 = time.time()
     if not args.no_prefill:
@@ -108,23 +126,26 @@ def main():
 
     hidden = tuple(int(x) for x in args.hidden.split(","))
     model = DeepFM(engine, num_slots=S, dense_dim=13, hidden=hidden).to(device)
+    C = model.dn.C
+    arena = DenseArena(model.parameters(), device, extra_grad=3 * C if multi else 0)
     if multi:
+        # data_norm batch statistics are summed across ranks in the SAME
+        # all-reduce as the dense gradients (tail of the gradient buffer)
         model.dn.group = dist.group.WORLD
         model.dn.sync_stats = True
-    arena = DenseArena(model.parameters(), device)
+        model.dn.stats = arena.grad_tail(3 * C)
+        model.dn.stats_in_grad_bucket = True
     # one update launch for the dense side: Adam + bf16 tower weight re-pack +
     # data_norm summary update; grads zeroed by the same kernel
     opt = FlatAdam(arena, lr=1e-3, clear_grad=True).fuse(mlps=[model.mlp], data_norms=[model.dn])
-    sync = DenseSync(arena, mode="grad_allreduce")
+    # the dense all-reduce runs on its own communicator and side stream, started
+    # as soon as the tower's gradients are final: it overlaps the sparse push
+    sync = DenseSync(arena, mode="grad_allreduce",
+                     overlap_group=dist.new_group(list(range(world))) if multi else None)
+    model.tower.on_dense_grads = sync.launch
 
-    # "load into memory": the pass's batches live in pinned host memory;
-    # every step copies its batch H2D on a side stream (overlapped).
-    from paddlebox_amd.runtime.graph_step import pack_batch
-
-    # each batch is one pinned byte buffer (one H2D DMA per step), and every
-    # buffer is streamed to the device once up front so the timed steps do not
-    # pay the driver's first-touch cost of a pinned range
-    host_batches = [pack_batch(synth.batch(B).to("cpu"), pin=True) for _ in range(args.num_batches)]
+    # every pinned batch buffer is streamed to the device once up front so the
+    # timed steps do not pay the driver's first-touch cost of a pinned range
     scratch = torch.empty_like(host_batches[0]._flat, device=device)
     for hb in host_batches:
         scratch.copy_(hb._flat, non_blocking=True)

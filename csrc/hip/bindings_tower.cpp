@@ -239,7 +239,7 @@ static void adam_fused(Tensor p, Tensor g, Tensor m, Tensor v, Tensor pows, Tens
                        double b2, double eps, double grad_scale, double wd, bool clear_grad,
                        const std::vector<py::tuple>& pack, const std::vector<py::tuple>& dn) {
   check_f32(p, -1, "p");
-  TW_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "adam sizes");
+  TW_CHECK(g.numel() >= p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "adam sizes");
   TW_CHECK(pows.is_cuda() && pows.numel() >= 2 && pows.scalar_type() == torch::kFloat32, "adam pows");
   TW_CHECK(ticket.is_cuda() && ticket.scalar_type() == torch::kInt32, "adam ticket");
   TW_CHECK(pack.size() <= (size_t)kMaxPackRegions && dn.size() <= (size_t)kMaxDnUpdates, "too many extras");

@@ -85,11 +85,13 @@ class _CtrTowerFn(torch.autograd.Function):
                           mlp.b_out.grad, True, t._dn_part(B, x.device) if dn_on else None,
                           h.head_blocks(B) if dn_on else 0, dn.eps if dn is not None else 0.0,
                           dn.stats if dn_on else None)
-        if dn_on:
+        if dn_on and not getattr(dn, "stats_in_grad_bucket", False):
             if dn.sync_stats and dn.group is not None and collective_active(dn.group):
                 dist.all_reduce(dn.stats, group=dn.group)
-            if not dn.fused_update:
-                h.data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, dn.stats, dn.decay)
+        if dn_on and not dn.fused_update:
+            h.data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, dn.stats, dn.decay)
+        if t.on_dense_grads is not None:  # e.g. start the dense all-reduce, overlapped with the sparse push
+            t.on_dense_grads()
         use_lin = t.use_head_lin and not ctx.has_extra
         dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim),
                            ctx.means, ctx.scales, dn.eps if dn is not None else 0.0, dlin_scale=gl,
@@ -109,6 +111,9 @@ class CtrTower:
         self.S, self.Eo, self.ew_col, self.D = S, Eo, ew_col, D
         self.use_head_lin = use_head_lin
         self.auc = None  # (table [2, T] f64, stats [5] f64, mask or None): fused AUC accumulation
+        # called in the backward once every dense gradient (and data_norm
+        # statistic) of the tower is final, before the sparse push runs
+        self.on_dense_grads = None
         self._part = None
         self._params = list(mlp.parameters())
 

@@ -26,7 +26,11 @@ from .comm import collective_active
 
 
 class DenseArena:
-    def __init__(self, params: Iterable[torch.nn.Parameter], device: torch.device):
+    def __init__(self, params: Iterable[torch.nn.Parameter], device: torch.device, extra_grad: int = 0):
+        """``extra_grad`` floats are appended to the gradient buffer (not to the
+        parameters): values that must be summed across ranks together with the
+        gradients -- e.g. data_norm batch statistics -- ride in the same single
+        all-reduce instead of a collective of their own (``grad_tail``)."""
         self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
         n = sum(p.numel() for p in self.params)
         # pad each param to 4 floats so every view is 16-B aligned
@@ -34,7 +38,8 @@ class DenseArena:
         total = sum(sizes)
         self.numel = n
         self.flat = torch.zeros(total, device=device)
-        self.grad = torch.zeros(total, device=device)
+        self.grad = torch.zeros(total + (int(extra_grad) + 3) // 4 * 4, device=device)
+        self._tail = total
         off = 0
         self.views = []
         for p, sz in zip(self.params, sizes):
@@ -52,6 +57,20 @@ class DenseArena:
     def notify_modified(self):
         for f in self.on_modified:
             f()
+
+    def grad_tail(self, n: int) -> torch.Tensor:
+        """Reserve n floats of the extra gradient region (summed by the dense
+        all-reduce, never touched by the optimizer)."""
+        if self._tail + n > self.grad.numel():
+            raise ValueError("DenseArena: extra_grad region exhausted")
+        v = self.grad[self._tail:self._tail + n]
+        self._tail += (n + 3) // 4 * 4
+        return v
+
+    @property
+    def param_grad(self) -> torch.Tensor:
+        """The gradient entries of the parameters (without the extra region)."""
+        return self.grad[: self.flat.numel()]
 
     def zero_grad(self):
         self.grad.zero_()
@@ -109,15 +128,15 @@ class FlatAdam:
     def step(self, grad_scale: float = 1.0):
         if self.a.flat.is_cuda:
             pack, dn = self._extras()
-            _native.hip().adam_fused(self.a.flat, self.a.grad, self.m, self.v, self.pows, self.ticket, self.lr,
+            _native.hip().adam_fused(self.a.flat, self.a.param_grad, self.m, self.v, self.pows, self.ticket, self.lr,
                                      self.b1, self.b2, self.eps, grad_scale, self.wd, self.clear_grad, pack, dn)
         else:
             self.pows[0] *= self.b1
             self.pows[1] *= self.b2
-            ref.adam_flat(self.a.flat, self.a.grad, self.m, self.v, self.lr, self.b1, self.b2, self.eps,
+            ref.adam_flat(self.a.flat, self.a.param_grad, self.m, self.v, self.lr, self.b1, self.b2, self.eps,
                           float(self.pows[0]), float(self.pows[1]), grad_scale, self.wd)
             if self.clear_grad:
-                self.a.grad.zero_()
+                self.a.param_grad.zero_()
 
     def state_dict(self):
         return {"m": self.m, "v": self.v, "pows": self.pows}
@@ -131,7 +150,12 @@ class FlatAdam:
 class DenseSync:
     """Data-parallel dense synchronisation over RCCL (or gloo on CPU)."""
 
-    def __init__(self, arena: DenseArena, mode: str = "grad_allreduce", k: int = 1, group=None):
+    def __init__(self, arena: DenseArena, mode: str = "grad_allreduce", k: int = 1, group=None,
+                 overlap_group=None):
+        """``overlap_group``: a process group of its own (own communicator) on
+        which ``launch()`` runs the gradient all-reduce on a side stream, so it
+        overlaps the rest of the backward (the sparse push and its key
+        all-to-all, which use the default group)."""
         self.a = arena
         self.mode = mode
         self.k = max(1, k)
@@ -139,12 +163,33 @@ class DenseSync:
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.active = collective_active(group)
         self.steps = 0
+        self.overlap_group = overlap_group
+        self._stream = None
+        self._launched = False
+
+    def launch(self):
+        """Start the gradient all-reduce now, on a side stream (call when the
+        dense gradients are final); ``before_step`` joins it."""
+        if not (self.active and self.mode == "grad_allreduce") or not self.a.grad.is_cuda:
+            return
+        dev = self.a.grad.device
+        cur = torch.cuda.current_stream(dev)
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(dev)
+        self._stream.wait_stream(cur)
+        with torch.cuda.stream(self._stream):
+            dist.all_reduce(self.a.grad, group=self.overlap_group if self.overlap_group is not None else self.group)
+        self._launched = True
 
     def grad_scale(self) -> float:
         return 1.0 / self.world if (self.mode == "grad_allreduce" and self.world > 1) else 1.0
 
     def before_step(self):
         """Called after backward, before the optimizer."""
+        if self._launched:
+            torch.cuda.current_stream(self.a.grad.device).wait_stream(self._stream)
+            self._launched = False
+            return
         if self.active and self.mode == "grad_allreduce":
             dist.all_reduce(self.a.grad, group=self.group)
 

@@ -104,6 +104,28 @@ class PullState:
     extra: dict = field(default_factory=dict)
 
 
+def exchange_capacity_for(key_batches, world: int, comm: Optional[Comm] = None) -> int:
+    """Exact per-peer capacity of the key exchange for a known set of batches
+    (a pass is loaded before it is trained, as in BoxPS FeedPass): the largest
+    number of distinct keys any batch sends to one owner, max-reduced over the
+    ranks when ``comm`` is given.  Sizing by distinct keys per owner instead of
+    by occurrences shrinks the exchanged buffers ~4x on Criteo-shaped batches
+    (U/L ~ 0.32) and makes overflow impossible for these batches."""
+    worst = 0
+    for k in key_batches:
+        k = k.reshape(-1)
+        k = k[k != -1]
+        if k.numel() == 0:
+            continue
+        h = torch.unique(ref.mix64(k))
+        worst = max(worst, int(torch.bincount(ref.owner_of(h, world), minlength=world).max()))
+    if comm is not None:
+        t = torch.tensor([worst], dtype=torch.int64, device=getattr(comm, "device", None) or "cpu")
+        comm.all_reduce(t, "max")
+        worst = int(t.item())
+    return worst + 64
+
+
 class SparseEngine:
     """Sparse embedding engine for one rank (one GPU, or the CPU)."""
 
@@ -119,6 +141,7 @@ class SparseEngine:
         auto_insert: bool = False,
         comm: Optional[Comm] = None,
         pull_ring: int = 2,
+        exchange_capacity: Optional[int] = None,
     ):
         self.cfg = cfg
         self.dim = cfg.embedx_dim
@@ -143,7 +166,13 @@ class SparseEngine:
             self._hip = _native.hip()
             self._sgd_native = cfg.sgd.to_native(self._hip)
             if self.sharded:
-                self.C = int(math.ceil(self.max_keys / self.world * cap_factor)) + 64
+                # per-peer exchange slots: exact when the pass's batches were
+                # pre-scanned (exchange_capacity_for), else a heuristic bound
+                # with a sticky device-side overflow flag
+                if exchange_capacity is not None:
+                    self.C = (int(exchange_capacity) + 63) // 64 * 64
+                else:
+                    self.C = int(math.ceil(self.max_keys / self.world * cap_factor)) + 64
             # ring of per-pull buffers (sort-free hash dedup everywhere: the
             # sender packs its unique keys per owner with a counting pass)
             self._slots = [_PullSlot(self) for _ in range(max(1, int(pull_ring)))]
