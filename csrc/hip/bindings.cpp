@@ -832,11 +832,13 @@ static void adam_flat(Tensor p, Tensor g, Tensor m, Tensor v, Tensor pows, float
 
 namespace pbx {
 void bind_tower(py::module& m);
+void bind_ctr(py::module& m);
 }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   using namespace pbx;
   bind_tower(m);
+  bind_ctr(m);
   m.doc() = "PaddleBox-capability engine: hand-written gfx950 (MI355X) kernels";
   py::class_<SparseSGDConfig>(m, "SparseSGDConfig")
       .def(py::init<>())

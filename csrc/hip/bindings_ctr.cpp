@@ -1,0 +1,238 @@
+// torch glue for the CTR op-family kernels (ctr_ext.hip): shape checks and
+// pointer plumbing only.
+#include <ATen/hip/HIPContext.h>
+#include <torch/extension.h>
+
+#include <stdexcept>
+
+#include "kernels.h"
+
+namespace py = pybind11;
+using torch::Tensor;
+
+namespace pbx {
+namespace {
+
+hipStream_t cs() { return at::hip::getCurrentHIPStream().stream(); }
+
+#define CX_CHECK(cond, msg)                                               \
+  do {                                                                    \
+    if (!(cond)) throw std::runtime_error(std::string("pbx ctr: ") + msg); \
+  } while (0)
+
+void f32(const Tensor& t, const char* n) {
+  CX_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32, std::string(n) + " must be an f32 GPU tensor");
+}
+template <typename T>
+T* P(const Tensor& t) {
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+template <typename T>
+T* OP(const c10::optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+// generic strided batched fp32 GEMM: C = alpha A B (+ bias * bias_scale) (+ C)
+void sgemm(const Tensor& A, const Tensor& B, Tensor C, const c10::optional<Tensor>& bias, int64_t M, int64_t N,
+           int64_t K, int64_t batch, std::vector<int64_t> a_strides, std::vector<int64_t> b_strides, int64_t sC,
+           int64_t ldc, int64_t sBias, double bias_scale, double alpha, bool accumulate) {
+  f32(A, "A");
+  f32(B, "B");
+  f32(C, "C");
+  CX_CHECK(a_strides.size() == 3 && b_strides.size() == 3, "strides are (batch, row, col)");
+  SgemmArgs g;
+  g.A = P<float>(A);
+  g.B = P<float>(B);
+  g.C = P<float>(C);
+  g.bias = OP<float>(bias);
+  g.M = (int)M; g.N = (int)N; g.K = (int)K; g.batch = (int)batch;
+  g.sA = a_strides[0]; g.rsA = a_strides[1]; g.csA = a_strides[2];
+  g.sB = b_strides[0]; g.rsB = b_strides[1]; g.csB = b_strides[2];
+  g.sC = sC; g.ldc = ldc; g.sBias = sBias;
+  g.bias_scale = (float)bias_scale;
+  g.alpha = (float)alpha;
+  g.accumulate = accumulate ? 1 : 0;
+  // bounds of the furthest element touched by each operand
+  auto span = [](int64_t b, int64_t sb, int64_t r, int64_t sr, int64_t c, int64_t sc) {
+    return (b - 1) * sb + (r - 1) * sr + (c - 1) * sc;
+  };
+  CX_CHECK(span(batch, g.sA, M, g.rsA, K, g.csA) < A.numel(), "A too small for its strides");
+  CX_CHECK(span(batch, g.sB, K, g.rsB, N, g.csB) < B.numel(), "B too small for its strides");
+  CX_CHECK(span(batch, sC, M, ldc, N, 1) < C.numel(), "C too small for its strides");
+  launch_sgemm(g, cs());
+}
+
+void colsum_strided(const Tensor& x, int64_t batch, int64_t M, int64_t N, int64_t sb, int64_t ld, Tensor out,
+                    int64_t so, bool accumulate) {
+  f32(x, "x");
+  f32(out, "out");
+  launch_colsum_strided(P<float>(x), (int)batch, (int)M, (int)N, sb, ld, P<float>(out), so, accumulate, cs());
+}
+
+// scaled_int8fc forward: y = int8(x) . int8(W) * interval / (ie * we) + b
+Tensor int8_fc(const Tensor& x, const Tensor& W, const Tensor& b, double ie, double ic, double we, double wc,
+               double range) {
+  f32(x, "x");
+  f32(W, "W");
+  f32(b, "b");
+  CX_CHECK(x.dim() == 2 && W.dim() == 2 && x.size(1) == W.size(0), "int8_fc: x [N, K], W [K, O]");
+  const int N = (int)x.size(0), K = (int)x.size(1), O = (int)W.size(1);
+  const int Kp = (K + 31) / 32 * 32;
+  auto oi = x.options().dtype(torch::kInt8);
+  auto qx = torch::zeros({N, Kp}, oi);
+  auto qwt = torch::zeros({O, Kp}, oi);
+  auto xc = x.contiguous(), Wc = W.contiguous();
+  launch_i8_quant(P<float>(xc), N, K, Kp, (float)ie, (float)ic, (float)range, false, P<signed char>(qx), cs());
+  launch_i8_quant(P<float>(Wc), K, O, Kp, (float)we, (float)wc, (float)range, true, P<signed char>(qwt), cs());
+  auto y = torch::empty({N, O}, x.options());
+  const float scale = (float)(2.0 * ic / range / (ie * we));
+  auto bc = b.contiguous();
+  launch_i8_gemm(P<signed char>(qx), P<signed char>(qwt), N, O, Kp, scale, P<float>(bc), P<float>(y), O, cs());
+  return y;
+}
+
+Tensor rank_attention_fwd(const Tensor& x, const Tensor& ro, const Tensor& W, int64_t R) {
+  f32(x, "x");
+  f32(W, "W");
+  CX_CHECK(ro.is_cuda() && ro.scalar_type() == torch::kInt32 && ro.dim() == 2 && ro.size(1) >= 2 * R + 1,
+           "rank_offset must be int32 [B, 2R+1]");
+  CX_CHECK(R >= 1 && R <= 8, "max_rank in 1..8");
+  const int B = (int)x.size(0), C = (int)x.size(1), P_ = (int)W.size(1);
+  CX_CHECK(W.size(0) == R * R * C, "W must be [R*R*C, P]");
+  auto xc = x.contiguous(), Wc = W.contiguous(), roc = ro.contiguous();
+  auto out = torch::empty({B, P_}, x.options());
+  launch_rank_attention_fwd(P<float>(xc), P<int>(roc), (int)roc.size(1), P<float>(Wc), B, C, P_, (int)R,
+                            P<float>(out), cs());
+  return out;
+}
+
+std::vector<Tensor> rank_attention_bwd(const Tensor& x, const Tensor& ro, const Tensor& W, const Tensor& dout,
+                                       int64_t R) {
+  f32(x, "x");
+  f32(dout, "dout");
+  const int B = (int)x.size(0), C = (int)x.size(1), P_ = (int)W.size(1);
+  auto xc = x.contiguous(), Wc = W.contiguous(), roc = ro.contiguous(), dc = dout.contiguous();
+  auto dexp = torch::empty({B, R, C}, x.options());
+  auto dx = torch::empty_like(xc);
+  auto dW = torch::zeros_like(Wc);
+  launch_rank_attention_bwd(P<float>(xc), P<float>(dc), P<int>(roc), (int)roc.size(1), P<float>(Wc), B, C, P_,
+                            (int)R, P<float>(dexp), P<float>(dx), P<float>(dW), cs());
+  return {dx, dW};
+}
+
+Tensor cvm_fwd(const Tensor& x, bool use_cvm) {
+  f32(x, "x");
+  auto xc = x.contiguous();
+  const int W = (int)xc.size(-1);
+  const int64_t n = xc.numel() / W;
+  auto sizes = xc.sizes().vec();
+  if (!use_cvm) sizes.back() = W - 2;
+  auto y = torch::empty(sizes, x.options());
+  launch_cvm_fwd(P<float>(xc), n, W, use_cvm, P<float>(y), cs());
+  return y;
+}
+
+Tensor cvm_bwd(const Tensor& dy, const Tensor& cvm, int64_t W, bool use_cvm) {
+  f32(dy, "dy");
+  f32(cvm, "cvm");
+  auto dyc = dy.contiguous(), cc = cvm.contiguous();
+  const int Wo = use_cvm ? (int)W : (int)W - 2;
+  const int64_t n = dyc.numel() / Wo;
+  const int64_t crow = cc.numel() / 2;
+  CX_CHECK(crow == n || crow == 1, "cvm rows must match dy rows (or be 1)");
+  auto dx = torch::empty({n, W}, dy.options());
+  launch_cvm_bwd(P<float>(dyc), P<float>(cc), n, (int)W, use_cvm, (int)crow, P<float>(dx), cs());
+  return dx;
+}
+
+std::vector<Tensor> masked_dn_fwd(const Tensor& x, const Tensor& mask, const Tensor& bsize, const Tensor& bsum,
+                                  const Tensor& bsq, const c10::optional<Tensor>& sw,
+                                  const c10::optional<Tensor>& bias, double eps) {
+  f32(x, "x");
+  f32(mask, "mask");
+  auto xc = x.contiguous(), mc = mask.contiguous();
+  const int N = (int)xc.size(0), C = (int)xc.size(1);
+  auto y = torch::empty_like(xc);
+  const int rows = mdn_blocks(N);
+  auto part = torch::empty({rows, 3, C}, x.options());
+  launch_masked_dn_fwd(P<float>(xc), P<float>(mc), N, C, P<float>(bsize), P<float>(bsum), P<float>(bsq),
+                       OP<float>(sw), OP<float>(bias), P<float>(y), P<float>(part), cs());
+  auto stats = torch::empty({3, C}, x.options());
+  launch_mdn_stats(P<float>(part), rows, C, (float)eps, P<float>(stats), cs());
+  return {y, stats};
+}
+
+std::vector<Tensor> masked_dn_bwd(const Tensor& x, const Tensor& dy, const Tensor& mask, const Tensor& bsize,
+                                  const Tensor& bsum, const Tensor& bsq, const c10::optional<Tensor>& sw) {
+  f32(x, "x");
+  f32(dy, "dy");
+  auto xc = x.contiguous(), dc = dy.contiguous(), mc = mask.contiguous();
+  const int N = (int)xc.size(0), C = (int)xc.size(1);
+  auto dx = torch::empty_like(xc);
+  const bool has_sw = sw.has_value() && sw->defined();
+  const int rows = mdn_blocks(N);
+  Tensor part, dsw, dbias;
+  if (has_sw) part = torch::empty({rows, 2, C}, x.options());
+  launch_masked_dn_bwd(P<float>(xc), P<float>(dc), P<float>(mc), N, C, P<float>(bsize), P<float>(bsum), P<float>(bsq),
+                       OP<float>(sw), P<float>(dx), has_sw ? P<float>(part) : nullptr, cs());
+  if (has_sw) {
+    auto g = torch::empty({2, C}, x.options());
+    launch_colsum_rows(P<float>(part), rows, 2, C, ColAffine(), P<float>(g), cs());
+    dsw = g[0];
+    dbias = g[1];
+  }
+  return {dx, dsw, dbias};
+}
+
+std::vector<Tensor> cnh_fwd(const Tensor& x, const Tensor& summary, int64_t F, int64_t E, double eps) {
+  f32(x, "x");
+  f32(summary, "summary");
+  auto xc = x.contiguous();
+  const int B = (int)xc.size(0);
+  const int W = (int)(F * (3 * E + 1));
+  CX_CHECK(xc.size(1) == F * 2 * E && summary.numel() == 3 * W, "cross_norm_hadamard shapes");
+  CX_CHECK((size_t)2 * W * sizeof(float) <= 64 * 1024, "cross_norm_hadamard: too many output columns");
+  auto y = torch::empty({B, W}, x.options());
+  const int rows = cnh_blocks(B);
+  auto part = torch::empty({rows, 2, W}, x.options());
+  auto sc = summary.contiguous();
+  launch_cnh_fwd(P<float>(xc), B, (int)F, (int)E, P<float>(sc), P<float>(y), P<float>(part), cs());
+  // batch stats [1, mean raw, mean (raw-mean)^2 + eps]: rows 1 and 2 of the reduced partials
+  auto stats = torch::empty({3, W}, x.options());
+  ColAffine f;
+  f.mul[0] = 1.f / (float)B;
+  f.mul[1] = 1.f / (float)B;
+  f.add[1] = (float)eps;
+  launch_colsum_rows(P<float>(part), rows, 2, W, f, P<float>(stats) + W, cs());
+  stats[0].fill_(1.0);
+  return {y, stats};
+}
+
+Tensor cnh_bwd(const Tensor& x, const Tensor& dy, const Tensor& summary, int64_t F, int64_t E) {
+  f32(x, "x");
+  f32(dy, "dy");
+  auto xc = x.contiguous(), dc = dy.contiguous(), sc = summary.contiguous();
+  auto dx = torch::empty_like(xc);
+  launch_cnh_bwd(P<float>(xc), P<float>(dc), (int)xc.size(0), (int)F, (int)E, P<float>(sc), P<float>(dx), cs());
+  return dx;
+}
+
+}  // namespace
+
+void bind_ctr(py::module& m) {
+  m.def("sgemm", &sgemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"),
+        py::arg("K"), py::arg("batch"), py::arg("a_strides"), py::arg("b_strides"), py::arg("sC"), py::arg("ldc"),
+        py::arg("sBias") = 0, py::arg("bias_scale") = 1.0, py::arg("alpha") = 1.0, py::arg("accumulate") = false);
+  m.def("colsum_strided", &colsum_strided);
+  m.def("int8_fc", &int8_fc);
+  m.def("rank_attention_fwd", &rank_attention_fwd);
+  m.def("rank_attention_bwd", &rank_attention_bwd);
+  m.def("cvm_fwd", &cvm_fwd);
+  m.def("cvm_bwd", &cvm_bwd);
+  m.def("masked_dn_fwd", &masked_dn_fwd);
+  m.def("masked_dn_bwd", &masked_dn_bwd);
+  m.def("cnh_fwd", &cnh_fwd);
+  m.def("cnh_bwd", &cnh_bwd);
+}
+
+}  // namespace pbx

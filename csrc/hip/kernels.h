@@ -446,4 +446,54 @@ void launch_adam_fused(float* p, float* g, float* m, float* v, int64_t n, float 
                        float* pows, float grad_scale, float weight_decay, bool clear_grad, const AdamExtras& x,
                        hipStream_t s);
 
+// ---------------------------------------------------------------- CTR op family (ctr_ext.hip)
+// C[b](m, n) = alpha * sum_k A[b](m, k) B[b](k, n) (+ bias[b][n] * bias_scale)
+// (+ C_old when accumulate); A(m,k) = A[b*sA + m*rsA + k*csA], B(k,n) =
+// B[b*sB + k*rsB + n*csB], C row-major with ldc.  fp32 throughout.
+struct SgemmArgs {
+  const float* A = nullptr;
+  const float* B = nullptr;
+  float* C = nullptr;
+  const float* bias = nullptr;
+  int M = 0, N = 0, K = 0, batch = 1;
+  int64_t sA = 0, rsA = 0, csA = 0;
+  int64_t sB = 0, rsB = 0, csB = 0;
+  int64_t sC = 0, ldc = 0, sBias = 0;
+  float bias_scale = 1.f, alpha = 1.f;
+  int accumulate = 0;
+};
+void launch_sgemm(const SgemmArgs& g, hipStream_t s);
+void launch_colsum_strided(const float* x, int batch, int M, int N, int64_t sb, int64_t ld, float* out, int64_t so,
+                           bool accumulate, hipStream_t s);
+void launch_i8_quant(const float* x, int R, int C, int ldo, float expand, float clip, float range, bool transpose,
+                     signed char* out, hipStream_t s);
+void launch_i8_gemm(const signed char* qx, const signed char* qwt, int M, int N, int Kp, float scale,
+                    const float* bias, float* y, int ldy, hipStream_t s);
+void launch_rank_attention_fwd(const float* x, const int* ro, int ld, const float* W, int B, int C, int P, int R,
+                               float* out, hipStream_t s);
+// dexp: scratch [B][R][C]; dx overwritten; dW accumulated (atomics)
+void launch_rank_attention_bwd(const float* x, const float* dout, const int* ro, int ld, const float* W, int B, int C,
+                               int P, int R, float* dexp, float* dx, float* dW, hipStream_t s);
+void launch_cvm_fwd(const float* x, int64_t n, int W, bool use_cvm, float* y, hipStream_t s);
+void launch_cvm_bwd(const float* dy, const float* cvm, int64_t n, int W, bool use_cvm, int cvm_rows, float* dx,
+                    hipStream_t s);
+int mdn_blocks(int N);
+void launch_masked_dn_fwd(const float* x, const float* mask, int N, int C, const float* bsize, const float* bsum,
+                          const float* bsq, const float* sw, const float* bias, float* y, float* part /*[blocks][3][C]*/,
+                          hipStream_t s);
+void launch_masked_dn_bwd(const float* x, const float* dy, const float* mask, int N, int C, const float* bsize,
+                          const float* bsum, const float* bsq, const float* sw, float* dx,
+                          float* part /*[blocks][2][C] or null*/, hipStream_t s);
+void launch_mdn_stats(const float* part, int rows, int C, float eps, float* stats, hipStream_t s);
+int cnh_blocks(int B);
+void launch_cnh_fwd(const float* x, int B, int F, int E, const float* summary, float* y, float* part /*[blocks][2][W]*/,
+                    hipStream_t s);
+void launch_cnh_bwd(const float* x, const float* dy, int B, int F, int E, const float* summary, float* dx,
+                    hipStream_t s);
+struct ColAffine {
+  float mul[4] = {1.f, 1.f, 1.f, 1.f};
+  float add[4] = {0.f, 0.f, 0.f, 0.f};
+};
+void launch_colsum_rows(const float* part, int rows, int Q, int C, const ColAffine& f, float* out, hipStream_t s);
+
 }  // namespace pbx

@@ -4,9 +4,11 @@ Semantics follow the reference kernels (cited per op); each op is an
 autograd-aware function.  Where the reference gradient is not the true
 derivative (CVM columns carrying show/click into the push, scaled_fc's bias
 gradient) the reference behaviour is reproduced with a custom Function.
-GPU tensors use the hand-written kernels in ``csrc/hip/ctr_ext.hip`` when
-the op has one (see ``_hip_or_none``); the torch expressions here are the
-fp32 reference the kernel tests compare against.
+GPU tensors run the hand-written kernels in ``csrc/hip/ctr_ext.hip``
+(batch_fc / scaled_fc / scaled_int8fc / rank_attention / cvm /
+masked_data_norm / cross_norm_hadamard); the torch expressions here are the
+CPU path and the fp32 reference the GPU tests compare against
+(tests/test_gpu_ctr_ops.py).
 """
 from __future__ import annotations
 
@@ -17,10 +19,6 @@ import torch.distributed as dist
 
 from .. import _native
 from ..parallel.comm import collective_active
-
-
-def _hip_or_none(t: torch.Tensor):
-    return _native.hip() if t.is_cuda else None
 
 
 def _seg_ids(offsets: torch.Tensor, L: int) -> torch.Tensor:
@@ -93,7 +91,25 @@ class _Cvm(torch.autograd.Function):
         return dx, None, None
 
 
+class _CvmHip(torch.autograd.Function):
+    """GPU cvm: k_cvm_fwd / k_cvm_bwd (csrc/hip/ctr_ext.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, cvm, use_cvm):
+        ctx.use_cvm, ctx.width, ctx.lead = use_cvm, x.shape[-1], x.shape[:-1]
+        ctx.save_for_backward(cvm)
+        return _native.hip().cvm_fwd(x, use_cvm)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (cvm,) = ctx.saved_tensors
+        dx = _native.hip().cvm_bwd(dy.float(), cvm.float(), ctx.width, ctx.use_cvm)
+        return dx.reshape(*ctx.lead, ctx.width), None, None
+
+
 def cvm(x: torch.Tensor, cvm_t: torch.Tensor, use_cvm: bool = True) -> torch.Tensor:
+    if x.is_cuda:
+        return _CvmHip.apply(x.float().contiguous(), cvm_t, use_cvm)
     return _Cvm.apply(x, cvm_t, use_cvm)
 
 
@@ -350,14 +366,7 @@ class _MaskedDataNorm(torch.autograd.Function):
             xm.sum(0) / n.clamp(min=1),
             (((x - means) ** 2) * m).sum(0) / n.clamp(min=1) + ctx.eps * (n > 0).to(x.dtype),
         ])
-        if ctx.group is not None and collective_active(ctx.group):
-            dist.all_reduce(stats, group=ctx.group)
-        if ctx.update and ctx.training:
-            upd = stats[0] > 0
-            with torch.no_grad():
-                bsize.copy_(torch.where(upd, bsize * ctx.decay + stats[0], bsize))
-                bsum.copy_(torch.where(upd, bsum * ctx.decay + stats[1], bsum))
-                bsq.copy_(torch.where(upd, bsq * ctx.decay + stats[2], bsq))
+        _dn_update(stats, ctx.group, ctx.update, ctx.training, ctx.decay, bsize, bsum, bsq)
         dsw = dbias = None
         if ctx.has_sw:
             xn = torch.where(m, (x - means) * scales, torch.zeros_like(x))
@@ -366,7 +375,47 @@ class _MaskedDataNorm(torch.autograd.Function):
         return dx, None, None, None, None, dsw, dbias, None, None, None, None, None
 
 
+def _dn_update(stats, group, update, training, decay, bsize, bsum, bsq):
+    if group is not None and collective_active(group):
+        dist.all_reduce(stats, group=group)
+    if update and training:
+        upd = stats[0] > 0
+        with torch.no_grad():
+            bsize.copy_(torch.where(upd, bsize * decay + stats[0], bsize))
+            bsum.copy_(torch.where(upd, bsum * decay + stats[1], bsum))
+            bsq.copy_(torch.where(upd, bsq * decay + stats[2], bsq))
+
+
+class _MaskedDataNormHip(torch.autograd.Function):
+    """GPU masked_data_norm: k_mdn_fwd normalises and emits per-block masked
+    statistic partials in the same pass (reduced by k_mdn_stats), k_mdn_bwd
+    produces dx and the scale/bias gradient partials; the summary update of
+    the reference's backward (masked_data_norm_op.cu:200-290) uses the
+    statistics computed in the forward."""
+
+    @staticmethod
+    def forward(ctx, x, mask, bsize, bsum, bsq, sw, bias, eps, decay, group, update, training):
+        h = _native.hip()
+        y, stats = h.masked_dn_fwd(x, mask, bsize, bsum, bsq, sw, bias, eps)
+        ctx.save_for_backward(x, mask, bsize, bsum, bsq, sw if sw is not None else torch.zeros(0))
+        ctx.stats, ctx.has_sw = stats, sw is not None
+        ctx.args = (group, update, training, decay)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mask, bsize, bsum, bsq, sw = ctx.saved_tensors
+        dx, dsw, dbias = _native.hip().masked_dn_bwd(x, dy.float().contiguous(), mask, bsize, bsum, bsq,
+                                                     sw if ctx.has_sw else None)
+        group, update, training, decay = ctx.args
+        _dn_update(ctx.stats, group, update, training, decay, bsize, bsum, bsq)
+        return dx, None, None, None, None, dsw, dbias, None, None, None, None, None
+
+
 def masked_data_norm(x, mask, bsize, bsum, bsq, sw, bias, eps, decay, group, update, training):
+    if x.is_cuda:
+        return _MaskedDataNormHip.apply(x.float().contiguous(), mask.float().reshape(-1).contiguous(), bsize, bsum,
+                                        bsq, sw, bias, eps, decay, group, update, training)
     return _MaskedDataNorm.apply(x, mask, bsize, bsum, bsq, sw, bias, eps, decay, group, update, training)
 
 
@@ -418,7 +467,35 @@ class _CrossNormHadamard(torch.autograd.Function):
         return dx, None, None, None, None, None, None, None
 
 
+class _CrossNormHadamardHip(torch.autograd.Function):
+    """GPU cross_norm_hadamard: k_cnh_fwd builds [a, b, a*b, <a,b>] per field,
+    normalises with the running summary and emits the batch-statistic
+    partials in the same pass; k_cnh_bwd is the exact input gradient."""
+
+    @staticmethod
+    def forward(ctx, x, summary, F, E, eps, decay, group, training):
+        y, stats = _native.hip().cnh_fwd(x, summary, F, E, eps)
+        ctx.save_for_backward(x, summary)
+        ctx.stats, ctx.args = stats, (F, E, decay, group, training)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, summary = ctx.saved_tensors
+        F, E, decay, group, training = ctx.args
+        dx = _native.hip().cnh_bwd(x, dy.float().contiguous(), summary, F, E)
+        stats = ctx.stats
+        if group is not None and collective_active(group):
+            dist.all_reduce(stats, group=group)
+        if training:
+            with torch.no_grad():
+                summary.mul_(decay).add_(stats.reshape(summary.shape))
+        return dx, None, None, None, None, None, None, None
+
+
 def cross_norm_hadamard(x, summary, F, E, eps, decay, group=None, training=True):
+    if x.is_cuda and 2 * F * (3 * E + 1) * 4 <= 64 * 1024:
+        return _CrossNormHadamardHip.apply(x.float().contiguous(), summary, F, E, eps, decay, group, training)
     return _CrossNormHadamard.apply(x, summary, F, E, eps, decay, group, training)
 
 
@@ -434,8 +511,9 @@ def _rank_gather(x, rank_offset, W, max_rank):
     xs, ws, valid = [], [], []
     for k in range(R):
         faster = ro[:, 2 * k + 1] - 1
-        idx = ro[:, 2 * k + 2].clamp(0, B - 1)
-        ok = (lower >= 0) & (faster >= 0)
+        raw = ro[:, 2 * k + 2]
+        idx = raw.clamp(0, B - 1)
+        ok = (lower >= 0) & (faster >= 0) & (raw >= 0) & (raw < B)
         blk = (lower.clamp(min=0) * R + faster.clamp(min=0))
         xs.append(x[idx] * ok.unsqueeze(1).to(x.dtype))
         ws.append(blk)
@@ -446,9 +524,9 @@ def _rank_gather(x, rank_offset, W, max_rank):
 def rank_attention(x: torch.Tensor, rank_offset: torch.Tensor, W: torch.Tensor, max_rank: int) -> torch.Tensor:
     """out[i] = sum_k [valid] x[index_k] @ W[(lower*R + faster_k)*C : +C]
     (rank_attention.cu.h:28-190 / numpy ref test_rank_attention_op.py:25-110)."""
-    hip = _hip_or_none(x)
-    if hip is not None and hasattr(hip, "rank_attention_fwd"):
-        return _RankAttentionHip.apply(x.contiguous(), rank_offset.to(torch.int32).contiguous(), W, max_rank)
+    if x.is_cuda and 1 <= max_rank <= 8:
+        return _RankAttentionHip.apply(x.float().contiguous(), rank_offset.to(torch.int32).contiguous(), W,
+                                       max_rank)
     xs, blks, _, Wb = _rank_gather(x, rank_offset, W, max_rank)
     out = 0
     for xk, bk in zip(xs, blks):
@@ -457,6 +535,11 @@ def rank_attention(x: torch.Tensor, rank_offset: torch.Tensor, W: torch.Tensor, 
 
 
 class _RankAttentionHip(torch.autograd.Function):
+    """GPU rank_attention: k_ra_fwd stages each used W block through LDS for
+    a 64-instance tile; backward = k_ra_dexp (per-peer input gradient),
+    k_ra_dx (the reference's gather-form merge, rank_attention.cu.h:120-190)
+    and k_ra_dw (per-block parameter gradient)."""
+
     @staticmethod
     def forward(ctx, x, ro, W, R):
         h = _native.hip()
@@ -473,6 +556,61 @@ class _RankAttentionHip(torch.autograd.Function):
 
 
 # ================================================================== batch_fc
+def _sg(A, B, C, M, N, K, batch, a_str, b_str, sC, ldc, bias=None, sBias=0, bias_scale=1.0):
+    """C = A B (+ bias * bias_scale) through k_sgemm; strides are
+    (batch, row, col) in elements, so permuted layouts need no copies."""
+    _native.hip().sgemm(A, B, C, bias, M, N, K, batch, list(a_str), list(b_str), sC, ldc, sBias, bias_scale)
+    return C
+
+
+def _batch_fc_geom(mode, xs, ws):
+    """Operand strides of the three batch_fc layouts as (batch, M, K, N, x
+    strides, W strides, out strides (sC, ldc), bias stride, x shape)."""
+    if mode == "default":  # x [P, N, in], W [P, in, out]
+        P, N, I = xs
+        O = ws[2]
+        return P, N, I, O, (N * I, I, 1), (I * O, O, 1), (N * O, O), O, (P, N, O)
+    if mode == "transpose":  # x [bc, N, in], W [in, bc*out]
+        P, N, I = xs
+        O = ws[1] // P
+        return P, N, I, O, (N * I, I, 1), (O, P * O, 1), (N * O, O), O, (P, N, O)
+    N, PI = xs  # batchcount: x [N, bc*in], W [in, bc*out]
+    P = mode
+    I, O = PI // P, ws[1] // P
+    return P, N, I, O, (I, P * I, 1), (O, P * O, 1), (O, P * O), O, (N, P * O)
+
+
+class _BatchFcHip(torch.autograd.Function):
+    """GPU batch_fc (batch_fc_op.cu:195-567): every layout is one strided
+    batched k_sgemm with the bias fused into the epilogue; backward is two
+    more strided GEMMs (dx = dy W^T, dW = x^T dy) and a strided column sum."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, mode):
+        P, N, I, O, xst, wst, (sC, ldc), sb, oshape = _batch_fc_geom(mode, x.shape, W.shape)
+        y = x.new_empty(oshape)
+        _sg(x, W, y, N, O, I, P, xst, wst, sC, ldc, b, sb)
+        ctx.save_for_backward(x, W)
+        ctx.geom, ctx.bshape = (P, N, I, O, xst, wst, sC, ldc), b.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        P, N, I, O, xst, wst, sC, ldc = ctx.geom
+        dy = dy.float().contiguous()
+        h = _native.hip()
+        dx = torch.empty_like(x)
+        # dx[p] (N x I) = dy[p] (N x O) . W[p]^T (O x I); dx shares x's strides
+        _sg(dy, W, dx, N, I, O, P, (sC, ldc, 1), (wst[0], wst[2], wst[1]), xst[0], xst[1])
+        # dW[p] (I x O) = x[p]^T (I x N) . dy[p] (N x O); dW shares W's strides
+        dW = torch.empty_like(W)
+        _sg(x, dy, dW, I, O, N, P, (xst[0], xst[2], xst[1]), (sC, ldc, 1), wst[0], wst[1])
+        db = x.new_empty(ctx.bshape)
+        h.colsum_strided(dy, P, N, O, sC, ldc, db, O, False)
+        return dx, dW, db, None
+
+
 def batch_fc(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, batchcount: int = 0,
              transpose_weight: bool = False) -> torch.Tensor:
     """batch_fc (operators/batch_fc_op.cu:195-330):
@@ -480,6 +618,9 @@ def batch_fc(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, batchcount: int 
     * transpose_weight: x [bc, N, in], W [in, bc*out], b [1, bc*out] -> [bc, N, out]
     * batchcount>0: x [N, bc*in], W [in, bc*out], b [bc*out] -> [N, bc*out]
     """
+    if x.is_cuda:
+        mode = "transpose" if transpose_weight else (batchcount if batchcount > 0 else "default")
+        return _BatchFcHip.apply(x.float().contiguous(), W.float().contiguous(), b.float().contiguous(), mode)
     if transpose_weight:
         bc = x.shape[0]
         od = W.shape[1] // bc
@@ -497,23 +638,50 @@ def batch_fc(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, batchcount: int 
 
 
 # ================================================================== scaled fc family
+def _fc_backward_hip(x, W, dy):
+    """dx = dy W^T, dW = x^T dy, db = colsum(dy) for x [N, K], W [K, O]."""
+    N, K = x.shape
+    O = W.shape[1]
+    dy = dy.float().contiguous()
+    dx = x.new_empty(N, K)
+    _sg(dy, W, dx, N, K, O, 1, (0, O, 1), (0, 1, O), 0, K)
+    dW = W.new_empty(K, O)
+    _sg(x, dy, dW, K, O, N, 1, (0, 1, K), (0, O, 1), 0, O)
+    db = W.new_empty(O)
+    _native.hip().colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
+    return dx, dW, db
+
+
 class _ScaledFc(torch.autograd.Function):
     """scaled_fc (operators/scaled_fc_op.cu:144-330): y = x@W + bias*bs/is
     (the reference's fp16 scaling is numerically transparent in bf16/fp32);
-    reference gradients: dx = dy W^T, dW = x^T dy, db = colsum(dy)."""
+    reference gradients: dx = dy W^T, dW = x^T dy, db = colsum(dy).
+    GPU tensors run k_sgemm with the scaled bias fused into the epilogue."""
 
     @staticmethod
     def forward(ctx, x, W, b, in_scale, bias_scale, grad_scale):
         ctx.save_for_backward(x, W)
+        ctx.bshape = b.shape
+        if x.is_cuda:
+            N, K = x.shape
+            O = W.shape[1]
+            return _sg(x, W, x.new_empty(N, O), N, O, K, 1, (0, K, 1), (0, O, 1), 0, O, b.reshape(-1), 0,
+                       bias_scale / in_scale)
         return x @ W + b.reshape(1, -1) * (bias_scale / in_scale)
 
     @staticmethod
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
-        return dy @ W.t(), x.t() @ dy, dy.sum(0).reshape(-1), None, None, None
+        if x.is_cuda:
+            dx, dW, db = _fc_backward_hip(x, W, dy)
+        else:
+            dx, dW, db = dy @ W.t(), x.t() @ dy, dy.sum(0)
+        return dx, dW, db.reshape(ctx.bshape), None, None, None
 
 
 def scaled_fc(x, W, b, in_scale, bias_scale, grad_scale=256.0):
+    if x.is_cuda:
+        x, W, b = x.float().contiguous(), W.float().contiguous(), b.float().contiguous()
     return _ScaledFc.apply(x, W, b, in_scale, bias_scale, grad_scale)
 
 
@@ -535,25 +703,31 @@ class _ScaledInt8Fc(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b, a):
         rng = a["int8_range"]
+        ctx.save_for_backward(x, W)
+        ctx.bshape = b.shape
+        if x.is_cuda:  # k_i8_quant x2 + k_i8_gemm (int8 MFMA, dequantising epilogue)
+            return _native.hip().int8_fc(x, W, b.reshape(-1), a["input_expand_factor"], a["input_clip_factor"],
+                                         a["weight_expand_factor"], a["weight_clip_factor"], rng)
         qx = int8_quantize(x, a["input_expand_factor"], a["input_clip_factor"], rng)
         qw = int8_quantize(W, a["weight_expand_factor"], a["weight_clip_factor"], rng)
-        hip = _hip_or_none(x)
-        if hip is not None and hasattr(hip, "int8_gemm"):
-            acc = hip.int8_gemm(qx.to(torch.int8).contiguous(), qw.to(torch.int8).contiguous())
-        else:
-            acc = qx.double() @ qw.double()
+        acc = qx.double() @ qw.double()
         interval = 2 * a["input_clip_factor"] / rng
         y = acc.float() / (a["input_expand_factor"] * a["weight_expand_factor"]) * interval
-        ctx.save_for_backward(x, W)
         return y + b.reshape(1, -1)
 
     @staticmethod
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
-        return dy @ W.t(), x.t() @ dy, dy.sum(0).reshape(-1), None
+        if x.is_cuda:
+            dx, dW, db = _fc_backward_hip(x, W, dy)
+        else:
+            dx, dW, db = dy @ W.t(), x.t() @ dy, dy.sum(0)
+        return dx, dW, db.reshape(ctx.bshape), None
 
 
 def scaled_int8fc(x, W, b, attrs):
+    if x.is_cuda:
+        x, W, b = x.float().contiguous(), W.float().contiguous(), b.float().contiguous()
     return _ScaledInt8Fc.apply(x, W, b, dict(attrs))
 
 

@@ -1,0 +1,118 @@
+"""CPU semantics of the CTR op family (ops/ctr_ext.py): each op against a
+direct evaluation of its definition, and autograd against finite
+differences where the reference gradient is the true derivative.  The GPU
+kernels are checked against these same torch paths in test_gpu_ctr_ops.py."""
+import math
+
+import torch
+
+from paddlebox_amd.ops import ctr_ext as cx
+from tests.ctr_data import page_view_ranks, rank_attention_loop
+
+
+def test_rank_attention_forward_and_grad():
+    g = torch.Generator().manual_seed(0)
+    R, C, P = 3, 5, 4
+    ro = page_view_ranks(12, R, g)
+    B = ro.shape[0]
+    x = torch.rand(B, C, generator=g, dtype=torch.float64)
+    W = torch.rand(R * R * C, P, generator=g, dtype=torch.float64)
+    torch.testing.assert_close(cx.rank_attention(x, ro, W, R), rank_attention_loop(x, ro, W, R))
+    x.requires_grad_(True)
+    W.requires_grad_(True)
+    assert torch.autograd.gradcheck(lambda a, w: cx.rank_attention(a, ro, w, R), (x, W))
+
+
+def test_batch_fc_layouts():
+    g = torch.Generator().manual_seed(1)
+    P, N, I, O = 3, 5, 4, 6
+    x = torch.randn(P, N, I, generator=g, dtype=torch.float64)
+    W = torch.randn(P, I, O, generator=g, dtype=torch.float64)
+    b = torch.randn(P, O, generator=g, dtype=torch.float64)
+    ref = torch.stack([x[p] @ W[p] + b[p] for p in range(P)])
+    torch.testing.assert_close(cx.batch_fc(x, W, b), ref)
+    # transpose_weight: W [in, bc*out]
+    Wt = torch.randn(I, P * O, generator=g, dtype=torch.float64)
+    bt = torch.randn(1, P * O, generator=g, dtype=torch.float64)
+    ref = torch.stack([x[p] @ Wt[:, p * O:(p + 1) * O] + bt[0, p * O:(p + 1) * O] for p in range(P)])
+    torch.testing.assert_close(cx.batch_fc(x, Wt, bt, transpose_weight=True), ref)
+    # batchcount: x [N, bc*in]
+    xb = torch.randn(N, P * I, generator=g, dtype=torch.float64)
+    bb = torch.randn(P * O, generator=g, dtype=torch.float64)
+    ref = torch.cat([xb[:, p * I:(p + 1) * I] @ Wt[:, p * O:(p + 1) * O] for p in range(P)], 1) + bb
+    torch.testing.assert_close(cx.batch_fc(xb, Wt, bb, batchcount=P), ref)
+
+
+def test_scaled_fc_and_int8fc():
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(7, 9, generator=g)
+    W = torch.randn(9, 5, generator=g)
+    b = torch.randn(1, 5, generator=g)
+    y = cx.scaled_fc(x, W, b, 4.0, 2.0)
+    torch.testing.assert_close(y, x @ W + b * 0.5)
+    a = dict(input_expand_factor=16.0, input_clip_factor=2.0, weight_expand_factor=32.0, weight_clip_factor=3.0,
+             int8_range=127.0)
+    y8 = cx.scaled_int8fc(x, W, b, a)
+    qx = cx.int8_quantize(x, 16.0, 2.0, 127.0)
+    qw = cx.int8_quantize(W, 32.0, 3.0, 127.0)
+    exp = (qx.double() @ qw.double()).float() * (2 * 2.0 / 127.0) / (16.0 * 32.0) + b
+    torch.testing.assert_close(y8, exp)
+    # the quantiser clips to +-clip before rounding
+    assert float(cx.int8_quantize(torch.tensor([10.0]), 1.0, 2.0, 127.0)) == 64.0  # trunc(2/(4/127)+.5)
+
+
+def test_cvm_forward_and_backward():
+    x = torch.tensor([[3.0, 1.0, 0.5, -1.0], [0.0, 0.0, 2.0, 4.0]], requires_grad=True)
+    cvm = torch.tensor([[1.0, 0.0], [1.0, 1.0]])
+    y = cx.cvm(x, cvm, True)
+    torch.testing.assert_close(y[:, 0], torch.log(x[:, 0] + 1).detach())
+    torch.testing.assert_close(y[:, 1], (torch.log(x[:, 1] + 1) - torch.log(x[:, 0] + 1)).detach())
+    y.sum().backward()
+    torch.testing.assert_close(x.grad[:, :2], cvm)
+    torch.testing.assert_close(x.grad[:, 2:], torch.ones(2, 2))
+    assert cx.cvm(x, cvm, False).shape == (2, 2)
+
+
+def test_masked_data_norm_and_update():
+    g = torch.Generator().manual_seed(3)
+    N, C = 10, 4
+    x = torch.randn(N, C, generator=g, dtype=torch.float64, requires_grad=True)
+    mask = (torch.rand(N, generator=g) > 0.4).double()
+    bsize = torch.full((C,), 5.0, dtype=torch.float64)
+    bsum = torch.randn(C, generator=g, dtype=torch.float64)
+    bsq = torch.full((C,), 7.0, dtype=torch.float64)
+    sw = torch.rand(C, generator=g, dtype=torch.float64, requires_grad=True)
+    bias = torch.randn(C, generator=g, dtype=torch.float64, requires_grad=True)
+    s0 = (bsize.clone(), bsum.clone(), bsq.clone())
+    y = cx.masked_data_norm(x, mask, bsize, bsum, bsq, sw, bias, 1e-4, 0.9, None, True, True)
+    mean, scale = s0[1] / s0[0], torch.sqrt(s0[0] / s0[2])
+    m = mask.bool().unsqueeze(1)
+    exp = torch.where(m, (x - mean) * scale * sw + bias, torch.zeros_like(x))
+    torch.testing.assert_close(y, exp)
+    y.pow(2).sum().backward()
+    n = mask.sum()
+    xm = x.detach()[mask.bool()]
+    torch.testing.assert_close(bsize, s0[0] * 0.9 + 1)
+    torch.testing.assert_close(bsum, s0[1] * 0.9 + xm.sum(0) / n)
+    torch.testing.assert_close(bsq, s0[2] * 0.9 + ((xm - mean) ** 2).sum(0) / n + 1e-4)
+    # masked rows get no gradient; the rest is the true derivative
+    assert float(x.grad[~mask.bool()].abs().sum()) == 0.0
+    torch.testing.assert_close(x.grad, torch.where(m, 2 * exp * sw * scale, torch.zeros_like(x)))
+
+
+def test_cross_norm_hadamard_grad_and_summary():
+    g = torch.Generator().manual_seed(4)
+    B, F, E = 6, 2, 3
+    W = F * (3 * E + 1)
+    x = torch.randn(B, F * 2 * E, generator=g, dtype=torch.float64, requires_grad=True)
+    summary = torch.stack([torch.full((W,), 4.0), torch.randn(W, generator=g), torch.full((W,), 9.0)]).double()
+    assert torch.autograd.gradcheck(
+        lambda a: cx.cross_norm_hadamard(a, summary.clone(), F, E, 1e-4, 0.99, training=False), (x,))
+    s_before = summary.clone()
+    y = cx.cross_norm_hadamard(x, summary, F, E, 1e-4, 0.99)
+    y.sum().backward()
+    raw = cx._cross_raw(x.detach(), F, E)
+    mean = s_before[1] / s_before[0]
+    stats = torch.stack([torch.ones(W, dtype=torch.float64), raw.mean(0), ((raw - mean) ** 2).mean(0) + 1e-4])
+    torch.testing.assert_close(summary, s_before * 0.99 + stats)
+    assert math.isfinite(float(y.detach().sum()))

@@ -1,0 +1,159 @@
+"""GPU CTR op family (csrc/hip/ctr_ext.hip) against the fp32/fp64 torch paths
+of ops/ctr_ext.py run on the CPU: forward values, every gradient and the
+running-statistic updates."""
+import pytest
+import torch
+
+from paddlebox_amd import _native
+from paddlebox_amd.ops import ctr_ext as cx
+from tests.ctr_data import page_view_ranks
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _pair(*ts):
+    """(cpu fp64 leaf, gpu fp32 leaf) pairs of the same values."""
+    out = []
+    for t in ts:
+        c = t.double().clone().requires_grad_(True)
+        d = t.float().to(DEV).requires_grad_(True)
+        out.append((c, d))
+    return out
+
+
+def _close(gpu, cpu, rtol=1e-4, atol=1e-4):
+    torch.testing.assert_close(gpu.detach().cpu().double(), cpu.detach(), rtol=rtol, atol=atol)
+
+
+def test_native_ctr_kernels_loaded():
+    h = _native.hip()
+    for name in ("sgemm", "int8_fc", "rank_attention_fwd", "cvm_fwd", "masked_dn_fwd", "cnh_fwd"):
+        assert hasattr(h, name), name
+
+
+@pytest.mark.parametrize("R", [1, 3, 8])
+def test_rank_attention_gpu(R):
+    g = torch.Generator().manual_seed(R)
+    C, P = 37, 70
+    ro = page_view_ranks(300, R, g)
+    B = ro.shape[0]
+    (xc, xg), (wc, wg) = _pair(torch.rand(B, C, generator=g), torch.rand(R * R * C, P, generator=g))
+    yc = cx.rank_attention(xc, ro, wc, R)
+    yg = cx.rank_attention(xg, ro.to(DEV), wg, R)
+    _close(yg, yc)
+    d = torch.randn(B, P, generator=g)
+    yc.backward(d.double())
+    yg.backward(d.to(DEV))
+    _close(xg.grad, xc.grad)
+    _close(wg.grad, wc.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("mode", ["default", "transpose", "batchcount"])
+def test_batch_fc_gpu(mode):
+    g = torch.Generator().manual_seed(5)
+    P, N, I, O = 4, 150, 70, 90
+    if mode == "default":
+        shapes = [(P, N, I), (P, I, O), (P, O)]
+        kw = {}
+    elif mode == "transpose":
+        shapes = [(P, N, I), (I, P * O), (1, P * O)]
+        kw = dict(transpose_weight=True)
+    else:
+        shapes = [(N, P * I), (I, P * O), (P * O,)]
+        kw = dict(batchcount=P)
+    (xc, xg), (wc, wg), (bc, bg) = _pair(*[torch.randn(*s, generator=g) for s in shapes])
+    yc = cx.batch_fc(xc, wc, bc, **kw)
+    yg = cx.batch_fc(xg, wg, bg, **kw)
+    _close(yg, yc)
+    d = torch.randn(*yc.shape, generator=g)
+    yc.backward(d.double())
+    yg.backward(d.to(DEV))
+    for a, b in ((xg, xc), (wg, wc), (bg, bc)):
+        _close(a.grad, b.grad, atol=1e-3)
+
+
+def test_scaled_fc_gpu():
+    g = torch.Generator().manual_seed(6)
+    (xc, xg), (wc, wg), (bc, bg) = _pair(torch.randn(300, 130, generator=g), torch.randn(130, 65, generator=g),
+                                         torch.randn(1, 65, generator=g))
+    yc = cx.scaled_fc(xc, wc, bc, 8.0, 2.0)
+    yg = cx.scaled_fc(xg, wg, bg, 8.0, 2.0)
+    _close(yg, yc)
+    d = torch.randn(300, 65, generator=g)
+    yc.backward(d.double())
+    yg.backward(d.to(DEV))
+    for a, b in ((xg, xc), (wg, wc), (bg, bc)):
+        _close(a.grad, b.grad, atol=1e-3)
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (257, 100, 65), (64, 32, 64)])
+def test_scaled_int8fc_gpu_exact(shape):
+    """int8 MFMA accumulation is exact: the GPU result equals the fp64 oracle
+    up to the final fp32 scale/bias rounding."""
+    N, K, O = shape
+    g = torch.Generator().manual_seed(N + K)
+    x, W, b = torch.randn(N, K, generator=g), torch.randn(K, O, generator=g) * 0.2, torch.randn(O, generator=g)
+    a = dict(input_expand_factor=10.0, input_clip_factor=3.0, weight_expand_factor=40.0, weight_clip_factor=5.0,
+             int8_range=127.0)
+    yc = cx.scaled_int8fc(x, W, b, a)
+    yg = cx.scaled_int8fc(x.to(DEV), W.to(DEV), b.to(DEV), a)
+    torch.testing.assert_close(yg.cpu(), yc, rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("use_cvm", [True, False])
+def test_cvm_gpu(use_cvm):
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(500, 11, generator=g) * 5
+    cv = torch.rand(500, 2, generator=g)
+    (xc, xg), = _pair(x)
+    yc = cx.cvm(xc, cv.double(), use_cvm)
+    yg = cx.cvm(xg, cv.to(DEV), use_cvm)
+    _close(yg, yc, rtol=1e-5, atol=1e-5)
+    d = torch.randn(*yc.shape, generator=g)
+    yc.backward(d.double())
+    yg.backward(d.to(DEV))
+    _close(xg.grad, xc.grad, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("with_sw", [True, False])
+def test_masked_data_norm_gpu(with_sw):
+    g = torch.Generator().manual_seed(8)
+    N, C = 333, 70
+    x = torch.randn(N, C, generator=g) * 2 + 1
+    mask = (torch.rand(N, generator=g) > 0.3).float()
+    stats = [torch.full((C,), 100.0), torch.randn(C, generator=g) * 10, torch.full((C,), 150.0)]
+    (xc, xg), (swc, swg), (bc, bg) = _pair(x, torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g))
+    sc = [s.double().clone() for s in stats]
+    sg = [s.to(DEV).clone() for s in stats]
+    yc = cx.masked_data_norm(xc, mask.double(), *sc, swc if with_sw else None, bc if with_sw else None, 1e-4, 0.99,
+                             None, True, True)
+    yg = cx.masked_data_norm(xg, mask.to(DEV), *sg, swg if with_sw else None, bg if with_sw else None, 1e-4, 0.99,
+                             None, True, True)
+    _close(yg, yc)
+    d = torch.randn(N, C, generator=g)
+    yc.backward(d.double())
+    yg.backward(d.to(DEV))
+    _close(xg.grad, xc.grad)
+    if with_sw:
+        _close(swg.grad, swc.grad, atol=1e-3)
+        _close(bg.grad, bc.grad, atol=1e-3)
+    for a, b in zip(sg, sc):
+        _close(a, b, rtol=1e-5, atol=1e-4)
+
+
+def test_cross_norm_hadamard_gpu():
+    g = torch.Generator().manual_seed(9)
+    B, F, E = 300, 5, 8
+    W = F * (3 * E + 1)
+    summary = torch.stack([torch.full((W,), 50.0), torch.randn(W, generator=g), torch.full((W,), 80.0)])
+    sc, sg = summary.double().clone(), summary.to(DEV).clone()
+    (xc, xg), = _pair(torch.randn(B, F * 2 * E, generator=g))
+    yc = cx.cross_norm_hadamard(xc, sc, F, E, 1e-4, 0.999)
+    yg = cx.cross_norm_hadamard(xg, sg, F, E, 1e-4, 0.999)
+    _close(yg, yc)
+    d = torch.randn(B, W, generator=g)
+    yc.backward(d.double())
+    yg.backward(d.to(DEV))
+    _close(xg.grad, xc.grad)
+    _close(sg, sc, rtol=1e-5, atol=1e-4)
