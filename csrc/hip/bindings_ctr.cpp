@@ -217,9 +217,105 @@ Tensor cnh_bwd(const Tensor& x, const Tensor& dy, const Tensor& summary, int64_t
   return dx;
 }
 
+// ints: need_filter, embed_filter, ets, co, quant, mcol, tradew, tn, tid, ecs, Epool, Eo
+// floats: show_coeff, clk_coeff, embed_threshold, pad
+SpvArgs spv_args(const Tensor& x, const Tensor& row_base, const Tensor& off, int64_t S, int64_t B,
+                 const std::vector<int64_t>& ints, const std::vector<double>& fl) {
+  f32(x, "x");
+  CX_CHECK(ints.size() == 12 && fl.size() == 4, "spv: 12 int and 4 float attributes");
+  CX_CHECK(row_base.scalar_type() == torch::kInt32 && row_base.numel() == S, "row_base int32 [S]");
+  CX_CHECK(off.scalar_type() == torch::kInt32 && off.numel() == S * (B + 1), "offsets int32 [S][B+1]");
+  SpvArgs a;
+  a.x = P<float>(x);
+  a.E = (int)x.size(1);
+  a.row_base = P<int>(row_base);
+  a.off = P<int>(off);
+  a.S = (int)S;
+  a.B = (int)B;
+  a.need_filter = (int)ints[0];
+  a.embed_filter = (int)ints[1];
+  a.ets = (int)ints[2];
+  a.co = (int)ints[3];
+  a.quant = (int)ints[4];
+  a.mcol = (int)ints[5];
+  a.tradew = (int)ints[6];
+  a.tn = (int)ints[7];
+  a.tid = (int)ints[8];
+  a.ecs = (int)ints[9];
+  a.Epool = (int)ints[10];
+  a.Eo = (int)ints[11];
+  a.show_coeff = (float)fl[0];
+  a.clk_coeff = (float)fl[1];
+  a.embed_threshold = (float)fl[2];
+  a.pad = (float)fl[3];
+  CX_CHECK(a.Epool <= 4095 && a.Epool + (a.tradew ? a.tn : 0) == a.E, "spv: pool width");
+  CX_CHECK((size_t)4 * a.ecs * a.Epool * sizeof(float) <= 64 * 1024, "spv: ecs * pool width too large");
+  CX_CHECK(!a.embed_filter || a.co + a.ets <= a.E, "spv: embed filter width");
+  CX_CHECK(!a.tradew || a.tid < a.tn, "spv: trade_id out of range");
+  return a;
+}
+
+Tensor spv_fwd(const Tensor& x, const Tensor& row_base, const Tensor& off, const Tensor& thr, const Tensor& ftab,
+               int64_t S, int64_t B, std::vector<int64_t> ints, std::vector<double> fl) {
+  SpvArgs a = spv_args(x, row_base, off, S, B, ints, fl);
+  CX_CHECK(ftab.scalar_type() == torch::kInt32 && ftab.numel() == a.Eo, "ftab int32 [Eo]");
+  f32(thr, "thr");
+  CX_CHECK(thr.numel() == S, "thr [S]");
+  a.thr = P<float>(thr);
+  a.ftab = P<int>(ftab);
+  auto out = torch::empty({S, B, (int64_t)a.ecs * a.Eo}, x.options());
+  a.out = P<float>(out);
+  launch_spv_fwd(a, cs());
+  return out;
+}
+
+Tensor spv_bwd(const Tensor& x, const Tensor& row_base, const Tensor& off, const Tensor& btab, const Tensor& dout,
+               const Tensor& cvm, const c10::optional<Tensor>& qv, int64_t S, int64_t B, std::vector<int64_t> ints,
+               std::vector<double> fl) {
+  SpvArgs a = spv_args(x, row_base, off, S, B, ints, fl);
+  CX_CHECK(btab.scalar_type() == torch::kInt32 && btab.numel() == a.Epool, "btab int32 [Epool]");
+  f32(dout, "dout");
+  f32(cvm, "cvm");
+  CX_CHECK(dout.numel() == S * B * a.ecs * a.Eo, "dout [S][B][ecs*Eo]");
+  a.btab = P<int>(btab);
+  a.dout = P<float>(dout);
+  a.cvm = P<float>(cvm);
+  a.ncv = (int)(cvm.numel() / B);
+  if (qv.has_value() && qv->defined() && qv->numel() > 0) {
+    f32(*qv, "qv");
+    a.qv = P<float>(*qv);
+    a.nq = (int)(qv->numel() / B);
+  }
+  auto dx = torch::empty_like(x);
+  a.dx = P<float>(dx);
+  launch_spv_bwd(a, cs());
+  return dx;
+}
+
+std::vector<Tensor> fused_seq_tensor(const Tensor& x, const Tensor& ad, int64_t bc, int64_t T, int64_t E, int64_t S,
+                                     int64_t A, int64_t ad_off) {
+  f32(x, "x");
+  f32(ad, "ad");
+  auto xc = x.contiguous(), ac = ad.contiguous();
+  const int64_t ins = xc.size(0);
+  CX_CHECK(xc.numel() == ins * bc * S * T * E && ac.numel() == ins * bc * A * E, "fused_seq_tensor shapes");
+  CX_CHECK(A <= S && ad_off >= 0 && ad_off + A <= S, "fused_seq_tensor ad slots");
+  auto o = x.options();
+  auto din = torch::empty({bc, ins * T, 4 * A * E}, o);
+  auto mask = torch::empty({bc, ins, T}, o);
+  auto side = torch::empty({bc, ins * T, (S - A) * E}, o);
+  auto sess = torch::empty({bc, ins * T, A, E}, o);
+  launch_fused_seq_tensor(P<float>(xc), P<float>(ac), (int)ins, (int)bc, (int)T, (int)E, (int)S, (int)A, (int)ad_off,
+                          P<float>(din), P<float>(mask), P<float>(side), P<float>(sess), cs());
+  return {din, mask, side, sess};
+}
+
 }  // namespace
 
 void bind_ctr(py::module& m) {
+  m.def("spv_fwd", &spv_fwd);
+  m.def("spv_bwd", &spv_bwd);
+  m.def("fused_seq_tensor", &fused_seq_tensor);
   m.def("sgemm", &sgemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"),
         py::arg("K"), py::arg("batch"), py::arg("a_strides"), py::arg("b_strides"), py::arg("sC"), py::arg("ldc"),
         py::arg("sBias") = 0, py::arg("bias_scale") = 1.0, py::arg("alpha") = 1.0, py::arg("accumulate") = false);

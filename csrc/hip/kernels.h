@@ -496,4 +496,45 @@ struct ColAffine {
 };
 void launch_colsum_rows(const float* part, int rows, int Q, int C, const ColAffine& f, float* out, hipStream_t s);
 
+// fused_seqpool_cvm variant family (seqpool_variants.hip).  The per-variant
+// CVM epilogue and its gradient are column tables built on the host:
+//   ftab[c]  (op << 24) | (s1 << 12) | s2, op: 0 copy p[s1], 1 log(p[s1]+1),
+//            2 log(p[s1]+1) - log(p[s2]+1)
+//   btab[e]  (op << 24) | idx, op: 0 zero, 1 cvm[b][idx], 2 qv[b][idx], 3 dout[idx]
+struct SpvArgs {
+  const float* x = nullptr;  // records [L_total][E]
+  int E = 0;
+  const int* row_base = nullptr;  // [S] first record of slot s
+  const int* off = nullptr;       // [S][B+1] instance offsets within the slot
+  int S = 0, B = 0;
+  int need_filter = 0;
+  float show_coeff = 0.f, clk_coeff = 1.f;
+  const float* thr = nullptr;  // [S] show/click threshold per slot
+  int embed_filter = 0;
+  float embed_threshold = 0.f;
+  int ets = 0;  // width of the embedding scored by the embed filter
+  int co = 2;
+  int quant = 0, mcol = 2;
+  int tradew = 0, tn = 0, tid = -1;
+  int ecs = 1;
+  float pad = 0.f;
+  int Epool = 0, Eo = 0;
+  const int* ftab = nullptr;
+  const int* btab = nullptr;
+  float* out = nullptr;  // [S][B][ecs*Eo]
+  const float* dout = nullptr;
+  const float* cvm = nullptr;
+  int ncv = 0;
+  const float* qv = nullptr;
+  int nq = 0;
+  float* dx = nullptr;  // [L_total][E]
+};
+void launch_spv_fwd(const SpvArgs& a, hipStream_t s);
+void launch_spv_bwd(const SpvArgs& a, hipStream_t s);
+// fused_seq_tensor: x [ins][bc][S][T][E], ad [ins][bc][A][E] -> din
+// [bc][ins][T][4][A][E], mask [bc][ins][T], side [bc][ins][T][S-A][E],
+// sess [bc][ins][T][A][E]
+void launch_fused_seq_tensor(const float* x, const float* ad, int ins, int bc, int T, int E, int S, int A,
+                             int ad_off, float* din, float* mask, float* side, float* sess, hipStream_t s);
+
 }  // namespace pbx

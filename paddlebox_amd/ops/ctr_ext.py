@@ -6,7 +6,9 @@ derivative (CVM columns carrying show/click into the push, scaled_fc's bias
 gradient) the reference behaviour is reproduced with a custom Function.
 GPU tensors run the hand-written kernels in ``csrc/hip/ctr_ext.hip``
 (batch_fc / scaled_fc / scaled_int8fc / rank_attention / cvm /
-masked_data_norm / cross_norm_hadamard); the torch expressions here are the
+masked_data_norm / cross_norm_hadamard) and ``csrc/hip/seqpool_variants.hip``
+(the fused_seqpool_cvm variant family, fused_seq_tensor); the torch
+expressions here are the
 CPU path and the fp32 reference the GPU tests compare against
 (tests/test_gpu_ctr_ops.py).
 """
@@ -329,9 +331,128 @@ _VARIANT = {
 }
 
 
+_F_COPY, _F_LOG, _F_LOGDIFF = 0, 1, 2
+_G_ZERO, _G_CVM, _G_QVAL, _G_DOUT = 0, 1, 2, 3
+
+
+def _spv_tables(variant: str, a: Dict, E: int, ncv: int, has_q: bool):
+    """Column tables of one variant's CVM epilogue (forward: output column ->
+    op on pooled columns) and its gradient (pooled column -> source), the
+    same mapping _cvm_epilogue / _cvm_epilogue_grad spell out with slicing.
+    Returns (ftab [(op, s1, s2)], btab [(op, idx)], Epool)."""
+    use_cvm = a.get("use_cvm", True)
+    co = a.get("cvm_offset", 2)
+    Ep = E - a["trade_num"] if variant == "tradew" else E
+    f: List = []
+    g = [(_G_ZERO, 0)] * Ep
+
+    def dout_from(pool0, out0):  # g[pool0 + i] = dout[out0 + i]
+        for i in range(Ep - pool0):
+            g[pool0 + i] = (_G_DOUT, out0 + i)
+
+    if variant == "pcoc":
+        mco = a.get("max_cvm_offset", co)
+        pk = co - 4
+        if use_cvm:
+            f = [(_F_LOG, 0, 0), (_F_LOGDIFF, 1, 0)]
+            f += [(_F_LOGDIFF, 4 + j, 2) for j in range(pk)] + [(_F_LOGDIFF, 4 + j, 3) for j in range(pk)]
+        f += [(_F_COPY, c, 0) for c in range(mco, Ep)]
+        for j in range(min(4, ncv)):
+            g[j] = (_G_CVM, j)
+        if pk > 0 and has_q:
+            for j in range(pk):
+                g[4 + j] = (_G_QVAL, j)
+        dout_from(mco, mco - (mco - 2 - 2 * pk) if use_cvm else 0)
+        return f, g, Ep
+    skip = a.get("embed_thres_size", 0) if (variant == "std" and not use_cvm) else 0
+    if skip == 0:
+        for j in range(min(co, ncv)):
+            g[j] = (_G_CVM, j)
+    if not use_cvm:
+        f = [(_F_COPY, c, 0) for c in range(co + skip, Ep)]
+        dout_from(co + skip, 0)
+        return f, g, Ep
+    if variant in ("std", "diff_thres", "tradew"):
+        f = [(_F_LOG, 0, 0)] + ([] if a.get("clk_filter") else [(_F_LOGDIFF, 1, 0)])
+        f += [(_F_COPY, c, 0) for c in range(2, Ep)]
+        dout_from(2, 1 if a.get("clk_filter") else 2)
+    elif variant == "conv":
+        f = ([] if a.get("show_filter") else [(_F_LOG, 0, 0)]) + [(_F_LOG, 1, 0), (_F_LOGDIFF, 2, 1)]
+        f += [(_F_COPY, c, 0) for c in range(3, Ep)]
+        dout_from(co, co - 1 if a.get("show_filter") else co)
+    elif variant == "credit":
+        f = [(_F_LOG, j, 0) for j in range(1 if a.get("show_filter") else 0, co)]
+        f += [(_F_COPY, c, 0) for c in range(co, Ep)]
+        dout_from(co, co - 1 if a.get("show_filter") else co)
+    else:
+        raise ValueError(variant)
+    return f, g, Ep
+
+
+def _enc_f(f):
+    return [(op << 24) | (s1 << 12) | s2 for op, s1, s2 in f]
+
+
+def _enc_g(g):
+    return [(op << 24) | idx for op, idx in g]
+
+
+class _SeqpoolCvmVariantHip(torch.autograd.Function):
+    """GPU fused_seqpool_cvm variants: k_spv_fwd / k_spv_bwd
+    (csrc/hip/seqpool_variants.hip) driven by _spv_tables."""
+
+    @staticmethod
+    def forward(ctx, cvm_in, variant, a, offsets_list, B, qvals, *xs):
+        dev = xs[0].device
+        E = xs[0].shape[1]
+        S = len(xs)
+        cv = cvm_in.float().reshape(B, -1).contiguous()
+        has_q = variant == "pcoc" and qvals is not None and qvals.numel() == B * (a.get("cvm_offset", 2) - 4)
+        f, g, Ep = _spv_tables(variant, a, E, cv.shape[1], has_q)
+        co = a.get("cvm_offset", 2)
+        ecs = a.get("embedx_concate_size", 1)
+        ets = a.get("embed_thres_size", 0)
+        ints = [int(bool(a.get("need_filter"))), int(bool(a.get("embed_threshold_filter"))),
+                ets if ets > 0 else E - co, co, int(a.get("quant_ratio", 0)),
+                a.get("max_cvm_offset", co) if variant == "pcoc" else co,
+                int(variant == "tradew"), a.get("trade_num", 0) if variant == "tradew" else 0,
+                a.get("trade_id", -1) if variant == "tradew" else -1, ecs, Ep, len(f)]
+        fl = [a.get("show_coeff", 0.0), a.get("clk_coeff", 1.0), a.get("embed_threshold", 0.0),
+              a.get("pad_value", 0.0)]
+        if variant == "diff_thres" and a.get("xbox_diff_thres_filter"):
+            thr = torch.tensor([float(t) for t in a["threshold_vec"][:S]], dtype=torch.float32)
+        else:
+            thr = torch.full((S,), float(a.get("threshold", 0.0)))
+        lens = [x.shape[0] for x in xs]
+        rb = torch.tensor([sum(lens[:i]) for i in range(S)], dtype=torch.int32)
+        x = torch.cat([x.float() for x in xs]).contiguous()
+        off = torch.stack([o.to(dev, torch.int32) for o in offsets_list]).contiguous()
+        t = lambda v, dt=torch.int32: torch.tensor(v, dtype=dt).to(dev)  # noqa: E731
+        ftab, btab = t(_enc_f(f)), t(_enc_g(g))
+        rb, thr = rb.to(dev), thr.to(dev)
+        h = _native.hip()
+        out = h.spv_fwd(x, rb, off, thr, ftab, S, B, ints, fl)
+        q = qvals.float().reshape(B, -1).contiguous() if has_q else None
+        ctx.save_for_backward(x, rb, off, btab, cv, q if q is not None else torch.zeros(0))
+        ctx.meta = (S, B, ints, fl, lens, has_q)
+        return tuple(out.unbind(0))
+
+    @staticmethod
+    def backward(ctx, *douts):
+        x, rb, off, btab, cv, q = ctx.saved_tensors
+        S, B, ints, fl, lens, has_q = ctx.meta
+        W = ints[9] * ints[11]
+        d = torch.stack([dd.float() if dd is not None else x.new_zeros(B, W) for dd in douts]).contiguous()
+        dx = _native.hip().spv_bwd(x, rb, off, btab, d, cv, q if has_q else None, S, B, ints, fl)
+        return (None, None, None, None, None, None) + tuple(dx.split(lens))
+
+
 def seqpool_cvm_variant(op_type: str, xs: Sequence[torch.Tensor], offsets: Sequence[torch.Tensor], B: int,
                         cvm_in: torch.Tensor, attrs: Dict, qvals: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
     variant = _VARIANT[op_type]
+    if xs and xs[0].is_cuda:
+        return list(_SeqpoolCvmVariantHip.apply(cvm_in, variant, dict(attrs), list(offsets), B, qvals,
+                                                *[x.float() for x in xs]))
     return list(_SeqpoolCvmVariant.apply(cvm_in, variant, dict(attrs), list(offsets), B, qvals,
                                          *[x.float() for x in xs]))
 
@@ -781,6 +902,13 @@ def fused_seq_tensor(x: torch.Tensor, ad: torch.Tensor, batch_count: int, max_le
     [bc, ins*T, side_slot*E], ADSlotSessionOut [bc, ins*T, ad_slot, E]."""
     ins = x.shape[0]
     bc, T, E, S, A = batch_count, max_length, fea_emb_dim, slot_num, ad_slot_num
+    if x.is_cuda:  # k_fused_seq_tensor: all four outputs in one pass
+        din, mask, side, sess = _native.hip().fused_seq_tensor(x.float(), ad.float(), bc, T, E, S, A, ad_slot_offset)
+        sess = sess.reshape(bc, ins * T, A, E)
+        if bc == 1:
+            return (din.reshape(ins, T, 4 * A * E), mask.reshape(ins, T), side.reshape(ins, T, (S - A) * E),
+                    sess.reshape(ins, T, A * E))
+        return din, mask, side, sess
     xv = x.reshape(ins, bc, S, T, E).permute(1, 0, 3, 2, 4)  # [bc, ins, T, S, E]
     adv = ad.reshape(ins, bc, A, E).permute(1, 0, 2, 3).unsqueeze(2)  # [bc, ins, 1, A, E]
     seq = xv[:, :, :, ad_slot_offset:ad_slot_offset + A]  # [bc, ins, T, A, E]

@@ -116,3 +116,49 @@ def test_cross_norm_hadamard_grad_and_summary():
     stats = torch.stack([torch.ones(W, dtype=torch.float64), raw.mean(0), ((raw - mean) ** 2).mean(0) + 1e-4])
     torch.testing.assert_close(summary, s_before * 0.99 + stats)
     assert math.isfinite(float(y.detach().sum()))
+
+
+def _variant_cases():
+    base = dict(use_cvm=True, cvm_offset=2)
+    yield "std", dict(base)
+    yield "std", dict(base, clk_filter=True)
+    yield "std", dict(base, use_cvm=False, embed_thres_size=3)
+    yield "diff_thres", dict(base, use_cvm=False)
+    yield "tradew", dict(base, trade_num=2, trade_id=1)
+    yield "conv", dict(base, cvm_offset=3)
+    yield "conv", dict(base, cvm_offset=3, show_filter=True)
+    yield "credit", dict(base, cvm_offset=4, show_filter=True)
+    yield "credit", dict(base, cvm_offset=4)
+    yield "pcoc", dict(base, cvm_offset=6, max_cvm_offset=8)
+    yield "pcoc", dict(base, cvm_offset=6, max_cvm_offset=8, use_cvm=False)
+
+
+def _apply_tables(f, g, p, dout, cv, qv):
+    lg = lambda v: torch.log(v + 1)  # noqa: E731
+    cols = []
+    for op, s1, s2 in f:
+        cols.append(p[:, s1] if op == cx._F_COPY else (lg(p[:, s1]) if op == cx._F_LOG else lg(p[:, s1]) - lg(p[:, s2])))
+    grad = torch.stack([torch.zeros(p.shape[0]) if op == cx._G_ZERO else
+                        (cv[:, i] if op == cx._G_CVM else (qv[:, i] if op == cx._G_QVAL else dout[:, i]))
+                        for op, i in g], 1)
+    return torch.stack(cols, 1), grad
+
+
+def test_seqpool_variant_tables_match_epilogues():
+    """The column tables the GPU kernels run reproduce the slicing-form
+    epilogue and gradient of every variant."""
+    g = torch.Generator().manual_seed(11)
+    B, E = 5, 12
+    for variant, a in _variant_cases():
+        Ep = E - a.get("trade_num", 0) if variant == "tradew" else E
+        p = torch.rand(B, Ep, generator=g) * 3
+        cv = torch.rand(B, 4, generator=g)
+        qv = torch.rand(B, 2, generator=g)
+        f, gt, ep = cx._spv_tables(variant, a, E, cv.shape[1], variant == "pcoc")
+        assert ep == Ep
+        exp = cx._cvm_epilogue(variant, p, a)
+        dout = torch.rand(B, exp.shape[1], generator=g)
+        got, grad = _apply_tables(f, gt, p, dout, cv, qv)
+        torch.testing.assert_close(got, exp, msg=f"{variant} {a}")
+        eg = cx._cvm_epilogue_grad(variant, dout, a, E, cv, qv, B)
+        torch.testing.assert_close(grad, eg, msg=f"{variant} {a} grad")

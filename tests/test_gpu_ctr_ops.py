@@ -23,7 +23,7 @@ def _pair(*ts):
 
 
 def _close(gpu, cpu, rtol=1e-4, atol=1e-4):
-    torch.testing.assert_close(gpu.detach().cpu().double(), cpu.detach(), rtol=rtol, atol=atol)
+    torch.testing.assert_close(gpu.detach().cpu().double(), cpu.detach().double(), rtol=rtol, atol=atol)
 
 
 def test_native_ctr_kernels_loaded():
@@ -157,3 +157,75 @@ def test_cross_norm_hadamard_gpu():
     yg.backward(d.to(DEV))
     _close(xg.grad, xc.grad)
     _close(sg, sc, rtol=1e-5, atol=1e-4)
+
+
+def _records(g, B, S, E, max_len=4):
+    xs, offs = [], []
+    for _ in range(S):
+        lens = torch.randint(0, max_len + 1, (B,), generator=g)
+        off = torch.cat([torch.zeros(1, dtype=torch.long), lens.cumsum(0)])
+        L = int(off[-1])
+        x = torch.rand(L, E, generator=g) * 2
+        x[:, 0] = torch.randint(0, 20, (L,), generator=g).float()  # show
+        x[:, 1] = (x[:, 0] * torch.rand(L, generator=g)).floor()  # click <= show
+        xs.append(x)
+        offs.append(off)
+    return xs, offs
+
+
+_GPU_VARIANTS = [
+    ("fused_seqpool_cvm", dict(use_cvm=True, cvm_offset=2, pad_value=0.5)),
+    ("fused_seqpool_cvm", dict(use_cvm=True, cvm_offset=2, need_filter=True, show_coeff=0.2, clk_coeff=1.0,
+                               threshold=1.5, quant_ratio=64, clk_filter=True)),
+    ("fused_seqpool_cvm", dict(use_cvm=False, cvm_offset=2, embed_threshold_filter=True, embed_threshold=1.2,
+                               embed_thres_size=4)),
+    ("fused_seqpool_cvm", dict(use_cvm=True, cvm_offset=2, embedx_concate_size=3, pad_value=0.1)),
+    ("fused_seqpool_cvm_with_diff_thres", dict(use_cvm=True, cvm_offset=2, need_filter=True, show_coeff=0.2,
+                                               clk_coeff=1.0, threshold=1.0, xbox_diff_thres_filter=True,
+                                               threshold_vec=[0.5, 2.0, 4.0])),
+    ("fused_seqpool_cvm_with_conv", dict(use_cvm=True, cvm_offset=3, show_filter=True)),
+    ("fused_seqpool_cvm_with_conv", dict(use_cvm=True, cvm_offset=3)),
+    ("fused_seqpool_cvm_with_pcoc", dict(use_cvm=True, cvm_offset=6, max_cvm_offset=8, quant_ratio=128)),
+    ("fused_seqpool_cvm_tradew", dict(use_cvm=True, cvm_offset=2, trade_num=3, trade_id=1)),
+    ("fused_seqpool_cvm_tradew", dict(use_cvm=False, cvm_offset=2, trade_num=3, trade_id=-1)),
+    ("fused_seqpool_cvm_with_credit", dict(use_cvm=True, cvm_offset=4, show_filter=True)),
+]
+
+
+@pytest.mark.parametrize("case", range(len(_GPU_VARIANTS)))
+def test_seqpool_cvm_variants_gpu(case):
+    op, attrs = _GPU_VARIANTS[case]
+    g = torch.Generator().manual_seed(100 + case)
+    B, S, E = 97, 3, 18
+    xs, offs = _records(g, B, S, E)
+    co = attrs["cvm_offset"]
+    cv = torch.rand(B, max(co, 4), generator=g)
+    qv = torch.rand(B, co - 4, generator=g) if op.endswith("pcoc") else None
+    pc = [x.double().requires_grad_(True) for x in xs]
+    pg = [x.to(DEV).requires_grad_(True) for x in xs]
+    oc = cx.seqpool_cvm_variant(op, pc, offs, B, cv.double(), attrs, qv.double() if qv is not None else None)
+    og = cx.seqpool_cvm_variant(op, pg, [o.to(DEV) for o in offs], B, cv.to(DEV), attrs,
+                                qv.to(DEV) if qv is not None else None)
+    assert len(og) == S
+    ds = []
+    for a, b in zip(og, oc):
+        _close(a, b, rtol=1e-5, atol=1e-5)
+        ds.append(torch.randn(*b.shape, generator=g))
+    torch.autograd.backward(oc, [d.double() for d in ds])
+    torch.autograd.backward(og, [d.to(DEV) for d in ds])
+    for a, b in zip(pg, pc):
+        _close(a.grad, b.grad, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("bc,ad_off", [(1, 0), (3, 2)])
+def test_fused_seq_tensor_gpu(bc, ad_off):
+    g = torch.Generator().manual_seed(bc)
+    ins, T, E, S, A = 37, 5, 8, 6, 2
+    x = torch.randn(ins, bc * S * T * E, generator=g)
+    x[:, : T * E] = 0.0  # some all-zero steps for the mask
+    ad = torch.randn(ins, bc * A * E, generator=g)
+    exp = cx.fused_seq_tensor(x, ad, bc, T, S, E, A, ad_off)
+    got = cx.fused_seq_tensor(x.to(DEV), ad.to(DEV), bc, T, S, E, A, ad_off)
+    for a, b in zip(got, exp):
+        assert a.shape == b.shape
+        torch.testing.assert_close(a.cpu(), b, rtol=1e-6, atol=1e-6)
