@@ -70,6 +70,8 @@ def main():
                     help="before warmup, print per-step host time of load / replay for this many steps (stderr)")
     ap.add_argument("--host-diag", action="store_true",
                     help="after the measurement, split host time into replay / H2D load (stderr only)")
+    ap.add_argument("--mlp-dtype", choices=("bf16", "fp32"), default="bf16",
+                    help="bf16: fused MFMA tower (default); fp32: the reference's fp32 fc precision")
     ap.add_argument("--force-collectives", action="store_true",
                     help="run the multi-GPU exchange/all-reduce path even on 1 rank (rehearsal)")
     args = ap.parse_args()
@@ -96,6 +98,10 @@ def main():
     from paddlebox_amd.runtime.graph_step import pack_batch
 
     host_batches = [pack_batch(synth.batch(B).to("cpu"), pin=True) for _ in range(args.num_batches)]
+    # sparse work per step: distinct keys per batch (U) over key occurrences (L)
+    u_per_batch = [int(torch.unique(hb.keys.to(device)).numel()) for hb in host_batches]
+    l_per_batch = int(host_batches[0].keys.numel())
+    u_over_l = sum(u_per_batch) / (len(u_per_batch) * l_per_batch)
     xcap = None
     if multi:
         # the pass is known before it is trained (BoxPS feed pass): size the key
@@ -126,18 +132,24 @@ def main():
 
     hidden = tuple(int(x) for x in args.hidden.split(","))
     model = DeepFM(engine, num_slots=S, dense_dim=13, hidden=hidden).to(device)
+    fp32 = args.mlp_dtype == "fp32"
+    if fp32:
+        model.precision = "fp32"
     C = model.dn.C
     arena = DenseArena(model.parameters(), device, extra_grad=3 * C if multi else 0)
     if multi:
-        # data_norm batch statistics are summed across ranks in the SAME
-        # all-reduce as the dense gradients (tail of the gradient buffer)
         model.dn.group = dist.group.WORLD
         model.dn.sync_stats = True
-        model.dn.stats = arena.grad_tail(3 * C)
-        model.dn.stats_in_grad_bucket = True
+        if not fp32:
+            # data_norm batch statistics are summed across ranks in the SAME
+            # all-reduce as the dense gradients (tail of the gradient buffer)
+            model.dn.stats = arena.grad_tail(3 * C)
+            model.dn.stats_in_grad_bucket = True
     # one update launch for the dense side: Adam + bf16 tower weight re-pack +
     # data_norm summary update; grads zeroed by the same kernel
-    opt = FlatAdam(arena, lr=1e-3, clear_grad=True).fuse(mlps=[model.mlp], data_norms=[model.dn])
+    opt = FlatAdam(arena, lr=1e-3, clear_grad=True)
+    if not fp32:
+        opt.fuse(mlps=[model.mlp], data_norms=[model.dn])
     # the dense all-reduce runs on its own communicator and side stream, started
     # as soon as the tower's gradients are final: it overlaps the sparse push
     sync = DenseSync(arena, mode="grad_allreduce",
@@ -154,7 +166,7 @@ def main():
     copy_stream = torch.cuda.Stream(device)
     auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
     auc_stats = torch.zeros(5, dtype=torch.float64, device=device)
-    fused_auc = getattr(model, "use_tower", False)
+    fused_auc = getattr(model, "use_tower", False) and not fp32
     if fused_auc:  # streaming AUC accumulated by the tower's loss epilogue
         model.tower.auc = (auc_table, auc_stats, None)
 
@@ -281,7 +293,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.mlp_dtype,
             "data": "synthetic (Criteo-1TB-shape: 13 dense + 26 sparse slots, 1e9-feature space, "
                     f"power-law alpha={args.alpha}), random-init weights",
             "config": {
@@ -291,6 +303,11 @@ def main():
                 "seq_len": S,
                 "total_features": synth.total_features,
                 "parallelism": f"dp{world}+sparse-shard{world}",
+                "mlp_dtype": args.mlp_dtype,
+                "unique_keys_per_batch": round(sum(u_per_batch) / len(u_per_batch), 1),
+                "keys_per_batch": l_per_batch,
+                "u_over_l": round(u_over_l, 4),
+                "table_hit_rate": 1.0 if not args.no_prefill else None,
             },
         }
         print(json.dumps(out), flush=True)

@@ -22,7 +22,7 @@ from typing import Sequence
 import torch
 from torch import nn
 
-from ..ops.ctr import DataNorm, ctr_head, logit_logloss
+from ..ops.ctr import DataNorm, ctr_head, fm_interaction, logit_logloss
 from ..ops.mlp import FusedMLP, pad8
 from ..ops.sparse import pull_seqpool_cvm_concat
 from ..ops.tower import CtrTower
@@ -71,10 +71,15 @@ class DeepFM(nn.Module):
         # the per-layer GEMM path (mlp.hip) for comparison
         self.tower = CtrTower(self.mlp, self.dn, self.S, self.Eo, self.ew_col, self.D, use_head_lin=True)
         self.use_tower = True
+        # "fp32": the reference's precision (fluid fc = fp32 GEMMs): fp32
+        # data_norm / FM kernels and fp32 library GEMMs for the MLP
+        self.precision = "bf16"
 
     def forward(self, batch):
         B, S = batch.B, batch.S
         x = pull_seqpool_cvm_concat(self.engine, batch.keys, batch.lod, B, S, batch.cvm, batch.dense, self.sp)
+        if self.precision == "fp32" and x.is_cuda:
+            return self._forward_fp32(x, batch.label)
         if self.use_tower or not x.is_cuda:
             return self.tower(x, batch.label)
         if self.use_workspace:
@@ -93,3 +98,10 @@ class DeepFM(nn.Module):
         # logit = deep + lin, sigmoid, log-loss and its gradient: one kernel
         loss, pred = logit_logloss(deep, lin, batch.label)
         return loss, pred
+
+    def _forward_fp32(self, x, label):
+        y = self.dn(x) if self.dn is not None else x
+        lin = x[:, self.ew_col:self.S * self.Eo:self.Eo].sum(1) + fm_interaction(x, self.S, self.D, self.ew_col + 1,
+                                                                                 self.Eo)
+        deep = self.mlp.forward_fp32(y)
+        return logit_logloss(deep, lin, label)

@@ -188,6 +188,16 @@ class FusedMLP(nn.Module):
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
 
+    def forward_fp32(self, x: torch.Tensor) -> torch.Tensor:
+        """fp32 MLP on any device (library fp32 GEMMs on the GPU): the
+        reference's fluid fc precision, kept for precision comparisons."""
+        x = x.float()
+        if x.shape[1] != self.in_dim:
+            x = torch.nn.functional.pad(x, (0, self.in_dim - x.shape[1]))
+        for w, b in zip(self.w, self.b):
+            x = torch.relu(torch.addmm(b, x, w.t()))
+        return torch.addmm(self.b_out, x, self.w_out.t()).view(-1)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.is_cuda:
             if x.dtype != torch.bfloat16:
