@@ -35,11 +35,13 @@ static T* optr(const c10::optional<Tensor>& t) {
 // --------------------------------------------------------------- GPU table
 class GpuTable {
  public:
-  GpuTable(int dim, int64_t capacity, int64_t stash_cap, int device)
+  GpuTable(int dim, int64_t capacity, int64_t stash_cap, int device, int extra = 0)
       : dim_(dim), device_(device) {
     PBX_CHECK(dim >= 1 && dim <= 128, "embedx dim must be in [1,128]");
+    PBX_CHECK(extra >= 0 && extra <= 1024, "extra row floats");
     const RowLayout l = make_row_layout(dim);
-    stride_ = l.stride;
+    // codec state (feature_ops.hip) follows the standard tail
+    stride_ = extra > 0 ? ((l.mf_size + 1 + extra) + 3) & ~3 : l.stride;
     nb_ = (uint64_t)((capacity + kBucketSlots - 1) / kBucketSlots);
     if (nb_ < 1) nb_ = 1;
     stash_cap_ = stash_cap;
@@ -194,6 +196,42 @@ class GpuTable {
     a.dim = dim_;
     a.embed_thres_size = use_cvm ? 0 : embed_thres_size;
     return launch_push_merge_apply(a, view(), ptr<int64_t>(rows), ptr<int32_t>(inc), cfg, seed, cur_stream());
+  }
+  // ---- feature-type codec (feature_ops.hip)
+  void codec_check(const CodecDev& c) const {
+    PBX_CHECK(c.Wx + c.We == dim_, "codec storage width != table dim");
+    PBX_CHECK(c.mf + 1 + c.extra <= stride_, "codec state exceeds the row stride");
+  }
+  Tensor codec_pull(const CodecDev& c, const Tensor& rows, const c10::optional<Tensor>& uid,
+                    const c10::optional<Tensor>& n_dev, int64_t n, Tensor out) {
+    codec_check(c);
+    check_cuda(rows, "rows");
+    check_cuda(out, "out");
+    PBX_CHECK(out.dim() == 2 && out.size(0) >= n && out.size(1) >= 3 + c.D + c.De, "codec_pull: out shape");
+    if (uid.has_value() && uid->defined()) PBX_CHECK(uid->numel() >= n, "codec_pull: uid");
+    else PBX_CHECK(rows.numel() >= n, "codec_pull: rows");
+    launch_codec_pull(view(), c, ptr<int64_t>(rows), optr<int32_t>(uid), optr<int32_t>(n_dev), n, ptr<float>(out),
+                      (int)out.size(1), cur_stream());
+    return out;
+  }
+  void codec_update(const CodecDev& c, const Tensor& rows, const Tensor& push, const c10::optional<Tensor>& n_dev,
+                    const SparseSGDConfig& cfg, uint64_t seed) {
+    codec_check(c);
+    check_cuda(rows, "rows");
+    check_cuda(push, "push");
+    PBX_CHECK(push.dim() == 2 && push.size(0) >= rows.numel() && push.size(1) >= 4 + c.D + c.De,
+              "codec_update: push record width");
+    launch_codec_update(view(), c, ptr<int64_t>(rows), ptr<float>(push), (int)push.size(1), optr<int32_t>(n_dev),
+                        rows.numel(), cfg, seed, cur_stream());
+  }
+  void codec_init(const CodecDev& c, const Tensor& rows, const Tensor& h, const SparseSGDConfig& cfg, uint64_t seed,
+                  bool init_embedx) {
+    codec_check(c);
+    check_cuda(rows, "rows");
+    check_cuda(h, "h");
+    PBX_CHECK(h.numel() == rows.numel(), "codec_init: one key per row");
+    launch_codec_init(view(), c, ptr<int64_t>(rows), ptr<uint64_t>(h), rows.numel(), cfg, seed, init_embedx ? 1 : 0,
+                      cur_stream());
   }
   void clear() {
     keys_.fill_(-1);
@@ -383,7 +421,12 @@ static void push_merge_records(const Tensor& rec, const Tensor& perm, const Tens
                                int dim, Tensor out) {
   check_cuda(rec, "rec");
   check_cuda(out, "out");
-  PBX_CHECK(dim == 4 || dim == 8 || dim == 16 || dim == 32, "merge records: dim in {4,8,16,32}");
+  // records are merged over dim rounded up to a multiple of 4 (the padding
+  // columns of a record are zero); the record strides must cover it
+  PBX_CHECK(dim >= 1 && dim <= 60, "merge records: dim in [1, 60]");
+  const int dim4 = (dim + 3) & ~3;
+  PBX_CHECK(rec.size(1) >= dim4 + 4 && out.size(1) >= dim4 + 4, "merge records: record stride < 4 + round4(dim)");
+  dim = dim4;
   launch_push_merge_records(ptr<float>(rec), (int)rec.size(1), ptr<int32_t>(perm), ptr<int32_t>(uid),
                             ptr<int32_t>(n_valid), perm.numel(), dim, ptr<float>(out), (int)out.size(1), cur_stream());
 }
@@ -865,9 +908,28 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("delete_after_unseen_days", &ShrinkConfig::delete_after_unseen_days)
       .def_readwrite("nonclk_coeff", &ShrinkConfig::nonclk_coeff)
       .def_readwrite("clk_coeff", &ShrinkConfig::clk_coeff);
+  py::class_<CodecDev>(m, "Codec")
+      .def(py::init([](int kind, int D, int De, float qscale, float beta1, float beta2, float eps) {
+             PBX_CHECK(kind >= 0 && kind <= 2, "codec kind 0/1/2");
+             PBX_CHECK(D >= 1 && De >= 0 && D + De <= 256, "codec dims");
+             return make_codec(kind, D, De, qscale, beta1, beta2, eps);
+           }),
+           py::arg("kind"), py::arg("D"), py::arg("De") = 0, py::arg("qscale") = 1.f, py::arg("beta1") = 0.9f,
+           py::arg("beta2") = 0.999f, py::arg("eps") = 1e-8f)
+      .def_readonly("kind", &CodecDev::kind)
+      .def_readonly("D", &CodecDev::D)
+      .def_readonly("De", &CodecDev::De)
+      .def_readonly("Wx", &CodecDev::Wx)
+      .def_readonly("We", &CodecDev::We)
+      .def_readonly("qscale", &CodecDev::qscale)
+      .def_readonly("mf", &CodecDev::mf)
+      .def_readonly("eg2", &CodecDev::eg2)
+      .def_readonly("adam", &CodecDev::adam)
+      .def_readonly("extra", &CodecDev::extra)
+      .def_property_readonly("storage_dim", [](const CodecDev& c) { return c.Wx + c.We; });
   py::class_<GpuTable>(m, "GpuTable")
-      .def(py::init<int, int64_t, int64_t, int>(), py::arg("dim"), py::arg("capacity"), py::arg("stash_cap") = 4096,
-           py::arg("device") = 0)
+      .def(py::init<int, int64_t, int64_t, int, int>(), py::arg("dim"), py::arg("capacity"),
+           py::arg("stash_cap") = 4096, py::arg("device") = 0, py::arg("extra") = 0)
       .def("probe", &GpuTable::probe, py::arg("h"), py::arg("n_dev") = py::none())
       .def("insert", &GpuTable::insert, py::arg("h"), py::arg("n_dev"), py::arg("cfg"), py::arg("seed"),
            py::arg("init_embedx"))
@@ -882,6 +944,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("gather_rows_by_uid", &GpuTable::gather_rows_by_uid)
       .def("push_adagrad_seg", &GpuTable::push_adagrad_seg)
       .def("push_merge_apply", &GpuTable::push_merge_apply)
+      .def("codec_pull", &GpuTable::codec_pull, py::arg("codec"), py::arg("rows"), py::arg("uid"), py::arg("n_dev"),
+           py::arg("n"), py::arg("out"))
+      .def("codec_update", &GpuTable::codec_update)
+      .def("codec_init", &GpuTable::codec_init)
+      .def_property_readonly("stride", &GpuTable::stride)
       .def("clear", &GpuTable::clear)
       .def_property_readonly("keys", &GpuTable::keys)
       .def_property_readonly("values", &GpuTable::values)

@@ -496,6 +496,55 @@ struct ColAffine {
 };
 void launch_colsum_rows(const float* part, int rows, int Q, int C, const ColAffine& f, float* out, hipStream_t s);
 
+// ---------------------------------------------------------------- feature types
+// Row codec of the GPU PS (feature_ops.hip): kind 0 fp32 Adagrad, 1 int16
+// embedx/expand Adagrad, 2 fp32 SparseAdam; De = expand (NNCross) columns.
+struct CodecDev {
+  int kind = 0;
+  int D = 8, De = 0;
+  int Wx = 8, We = 0;  // storage words of embedx / expand
+  float qscale = 1.f;
+  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f;
+  int g2 = 0, xg2 = 0, delta = 0, slot = 0, unseen = 0, mf = 0;
+  int eg2 = 0;   // expand g2sum (Adagrad, De > 0)
+  int adam = 0;  // first SparseAdam state word
+  int extra = 0;  // floats after the standard tail
+};
+// fills storage widths and field offsets for (kind, D, De)
+inline CodecDev make_codec(int kind, int D, int De, float qscale, float beta1, float beta2, float eps) {
+  CodecDev c;
+  c.kind = kind;
+  c.D = D;
+  c.De = De;
+  c.Wx = kind == 1 ? (D + 1) / 2 : D;
+  c.We = kind == 1 ? (De + 1) / 2 : De;
+  c.qscale = qscale;
+  c.beta1 = beta1;
+  c.beta2 = beta2;
+  c.eps = eps;
+  const RowLayout l = make_row_layout(c.Wx + c.We);
+  c.g2 = l.embed_g2sum;
+  c.xg2 = l.embedx_g2sum;
+  c.delta = l.delta_score;
+  c.slot = l.slot;
+  c.unseen = l.unseen_days;
+  c.mf = l.mf_size;
+  int used = l.mf_size + 1;
+  c.eg2 = used;
+  if (De > 0) used += 1;
+  c.adam = used;
+  if (kind == 2) used += 6 + 2 * (D + De);
+  c.extra = used - (l.mf_size + 1);
+  return c;
+}
+void launch_codec_pull(const TableDev& t, const CodecDev& c, const int64_t* rows, const int32_t* uid,
+                       const int32_t* n_dev, int64_t n, float* out, int out_stride, hipStream_t s);
+void launch_codec_update(const TableDev& t, const CodecDev& c, const int64_t* rows, const float* push,
+                         int push_stride, const int32_t* n_dev, int64_t n, const SparseSGDConfig& cfg, uint64_t seed,
+                         hipStream_t s);
+void launch_codec_init(const TableDev& t, const CodecDev& c, const int64_t* rows, const uint64_t* keys, int64_t n,
+                       const SparseSGDConfig& cfg, uint64_t seed, int init_embedx, hipStream_t s);
+
 // fused_seqpool_cvm variant family (seqpool_variants.hip).  The per-variant
 // CVM epilogue and its gradient are column tables built on the host:
 //   ftab[c]  (op << 24) | (s1 << 12) | s2, op: 0 copy p[s1], 1 log(p[s1]+1),

@@ -766,6 +766,23 @@ void launch_push_merge_records(const float* rec, int rec_stride, const int32_t* 
     case 16: hipLaunchKernelGGL((k_push_merge<19, RecordSource>), g, b, 0, s, src, perm, uid, n_valid, n, out, out_stride, (const int64_t*)nullptr, 1.f, 1 << 20); break;
     case 32: hipLaunchKernelGGL((k_push_merge<35, RecordSource>), g, b, 0, s, src, perm, uid, n_valid, n, out, out_stride, (const int64_t*)nullptr, 1.f, 1 << 20); break;
     case 4: hipLaunchKernelGGL((k_push_merge<7, RecordSource>), g, b, 0, s, src, perm, uid, n_valid, n, out, out_stride, (const int64_t*)nullptr, 1.f, 1 << 20); break;
+#define PBX_MERGE_REC(DIM)                                                                                  \
+  case DIM:                                                                                                 \
+    hipLaunchKernelGGL((k_push_merge<DIM + 3, RecordSource>), g, b, 0, s, src, perm, uid, n_valid, n, out, \
+                       out_stride, (const int64_t*)nullptr, 1.f, 1 << 20);                                  \
+    break;
+    PBX_MERGE_REC(12)
+    PBX_MERGE_REC(20)
+    PBX_MERGE_REC(24)
+    PBX_MERGE_REC(28)
+    PBX_MERGE_REC(36)
+    PBX_MERGE_REC(40)
+    PBX_MERGE_REC(44)
+    PBX_MERGE_REC(48)
+    PBX_MERGE_REC(52)
+    PBX_MERGE_REC(56)
+    PBX_MERGE_REC(60)
+#undef PBX_MERGE_REC
     default: break;
   }
 }

@@ -409,6 +409,12 @@ class BoxWrapper:
 
     def pull_extended(self, keys, lod, B, S, emb_size: int, ext_size: int):
         """pull_box_extended_sparse: (records [L, emb_size], expand [L, ext_size])."""
+        eng = self._require_engine()
+        if getattr(eng, "codec", None) is not None and eng.codec.De >= ext_size:
+            # GPU PS rows carry the expand block: one pull / push for both
+            from .extras import pull_extended_codec
+
+            return pull_extended_codec(eng, keys, lod, B, S, emb_size, ext_size)
         if self._expand is None:
             from .extras import ExpandEmbedding
 

@@ -89,6 +89,14 @@ class PSConfig:
     expand_embed_dim: int = 0
     feature_type: int = 0  # 0 normal, 1 quant int16 embedx, 2 variable/expand
     pull_embedx_scale: float = 1.0
+    # sparse optimizer of the GPU PS rows: "adagrad" (default) or "adam"
+    # (SparseAdam, heter_ps/optimizer.cuh.h:147-330)
+    sparse_optimizer: str = "adagrad"
+    adam_beta1: float = 0.9
+    adam_beta2: float = 0.999
+    adam_epsilon: float = 1e-8
+    # route fp32 Adagrad through the row-codec kernels too (testing)
+    force_codec: bool = False
     sgd: SparseSGDConfig = field(default_factory=SparseSGDConfig)
     shrink: ShrinkConfig = field(default_factory=ShrinkConfig)
     save: SaveConfig = field(default_factory=SaveConfig)

@@ -120,6 +120,41 @@ class _PullExtended(torch.autograd.Function):
         return (None,) * 10
 
 
+class _PullExtendedCodec(torch.autograd.Function):
+    """pull_box_extended_sparse on one engine whose rows carry the expand
+    block (feature codec with De > 0, csrc/hip/feature_ops.hip): one pull
+    returns [show, click, embed_w, embedx[D], expand[De]] per occurrence and
+    one push updates both blocks."""
+
+    @staticmethod
+    def forward(ctx, anchor, keys, lod, eng, B, S, emb_size, ext_size, bs_scale):
+        recs, st = eng.pull_records(keys, lod, B, S, with_expand=True)
+        E = 3 + eng.dim
+        ctx.eng, ctx.st, ctx.bs, ctx.E, ctx.W = eng, st, bs_scale, E, recs.shape[1]
+        out = recs[:, :min(emb_size, E)]
+        if emb_size > E:
+            out = torch.nn.functional.pad(out, (0, emb_size - E))
+        ex = recs[:, E:E + ext_size]
+        return out.contiguous(), ex.contiguous()
+
+    @staticmethod
+    def backward(ctx, g, gex):
+        gm = torch.zeros(ctx.st.L, ctx.W, device=ctx.st.lod.device, dtype=torch.float32)
+        if g is not None:
+            w = min(ctx.E, g.shape[1])
+            gm[:, :w] = g[:, :w].float()
+        if gex is not None:
+            gm[:, ctx.E:ctx.E + gex.shape[1]] = gex.float()
+        ctx.eng.push_records(ctx.st, gm, 2, ctx.bs)
+        return (None,) * 9
+
+
+def pull_extended_codec(eng, keys, lod, B, S, emb_size: int, ext_size: int):
+    from ..ops.sparse import _anchor
+
+    return _PullExtendedCodec.apply(_anchor(keys.device), keys, lod, eng, B, S, emb_size, ext_size, float(B))
+
+
 class ExpandEmbedding:
     """Expand-embedding companion engine (same keys, embedx = expand vector)."""
 

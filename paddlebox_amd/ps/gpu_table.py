@@ -18,16 +18,26 @@ from .config import ShrinkConfig, SparseSGDConfig, row_layout
 
 
 class GpuSparseTable:
+    """``codec`` (ps/feature_types.FeatureCodec) selects a non-default row
+    layout: the native table then stores ``codec.storage_dim`` embedding words
+    plus the codec state, and ``export`` / ``assign`` / ``read`` speak the
+    canonical fp32 layout ``row_layout(D + De)`` (+ codec state)."""
+
     def __init__(self, dim: int, capacity: int, device: torch.device, stash_cap: int = 4096,
-                 load_factor: float = 0.85):
-        self.dim = dim
+                 load_factor: float = 0.85, codec=None):
+        self.codec = codec
+        self.dim = codec.DX if codec is not None else dim
         self.device = torch.device(device)
         self.load_factor = load_factor
         slots = int(math.ceil(max(capacity, 16) / load_factor))
         self._mod = _native.hip()
         with torch.cuda.device(self.device):
-            self.t = self._mod.GpuTable(dim, slots, stash_cap, self.device.index or 0)
-        self.layout = row_layout(dim)
+            if codec is None:
+                self.t = self._mod.GpuTable(dim, slots, stash_cap, self.device.index or 0)
+            else:
+                self.t = self._mod.GpuTable(codec.storage_dim, slots, stash_cap, self.device.index or 0, codec.extra)
+                assert int(self.t.stride) == codec.raw_stride
+        self.layout = row_layout(self.dim)
         self._seed = 0x5EED
 
     # -- build ------------------------------------------------------------
@@ -37,7 +47,20 @@ class GpuSparseTable:
         if h.numel() == 0:
             return 0
         self._seed += 1
-        fails = self.t.insert(h.contiguous(), n_dev, sgd.to_native(self._mod), self._seed, init_embedx)
+        if self.codec is not None:
+            # the insert zeroes new rows; the codec then writes its state (and
+            # the encoded embedding when init_embedx) into exactly those rows
+            if n_dev is not None:  # build phase: a host sync is fine here
+                h, n_dev = h[:int(n_dev.reshape(-1)[0].item())], None
+            h = h.contiguous()
+            new = h[self.t.probe(h, None) < 0]
+            fails = self.t.insert(h, None, sgd.to_native(self._mod), self._seed, False)
+            if new.numel():
+                new = new.contiguous()
+                rows = self.t.probe(new, None)
+                self.t.codec_init(self.codec.native(), rows, new, sgd.to_native(self._mod), self._seed, init_embedx)
+        else:
+            fails = self.t.insert(h.contiguous(), n_dev, sgd.to_native(self._mod), self._seed, init_embedx)
         if fails:
             raise RuntimeError(f"GpuSparseTable: {fails} keys could not be placed (table full?)")
         return fails
@@ -59,16 +82,25 @@ class GpuSparseTable:
 
     def export(self, with_values: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
         k, v = self.t.export_all(with_values)
+        if with_values and self.codec is not None:
+            v = self.codec.decode(v)
         return k, (v if with_values else None)
 
     def assign(self, h: torch.Tensor, vals: torch.Tensor):
         rows = self.probe(h)
-        self.t.assign(rows, vals.contiguous().float())
+        vals = vals.contiguous().float()
+        if self.codec is not None:
+            vals = self.codec.encode(vals)
+        self.t.assign(rows, vals)
 
     def read(self, h: torch.Tensor) -> torch.Tensor:
         rows = self.probe(h)
-        out = torch.zeros(h.numel(), self.layout["stride"], device=self.device)
         ok = rows >= 0
+        if self.codec is not None:
+            out = torch.zeros(h.numel(), self.codec.canon_width, device=self.device)
+            out[ok] = self.codec.decode(self.t.values[rows[ok]])
+            return out
+        out = torch.zeros(h.numel(), self.layout["stride"], device=self.device)
         out[ok] = self.t.values[rows[ok]]
         return out
 

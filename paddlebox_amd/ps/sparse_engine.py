@@ -33,6 +33,7 @@ from ..parallel.comm import Comm, default_comm
 from ..ops import reference as ref
 from .config import PSConfig, SparseSGDConfig, padded, pull_width, push_width
 from .cpu_table import CpuSparseTable
+from .feature_types import FeatureCodec
 from .gpu_table import GpuSparseTable
 
 
@@ -161,8 +162,19 @@ class SparseEngine:
         self.test_mode = False
         self.is_gpu = self.device.type == "cuda"
         shard_cap = int(math.ceil(capacity / self.world)) if self.world > 1 else capacity
+        # non-default feature types (int16 embedx, expand block, SparseAdam):
+        # rows go through the codec kernels (ps/feature_types.py)
+        self.codec = FeatureCodec.from_config(cfg)
+        if self.codec is not None and not self.is_gpu_device():
+            if self.codec.kind != 0:
+                raise NotImplementedError("feature_type / sparse_optimizer='adam' need the GPU parameter server")
+            self.codec = None  # CPU: the expand block is served by ps.extras.ExpandEmbedding
+        self.xdim = self.codec.DX if self.codec is not None else self.dim
+        if self.codec is not None:
+            self.P = padded(3 + self.xdim)
+            self.Q = padded(4 + self.xdim)
         if self.is_gpu:
-            self.table = GpuSparseTable(self.dim, shard_cap, self.device)
+            self.table = GpuSparseTable(self.dim, shard_cap, self.device, codec=self.codec)
             self._hip = _native.hip()
             self._sgd_native = cfg.sgd.to_native(self._hip)
             if self.sharded:
@@ -186,6 +198,8 @@ class SparseEngine:
                 self.push_merged = torch.empty(n, self.Q, device=self.device)
             else:
                 self.push_buf = torch.empty(self.max_keys, self.Q, device=self.device)
+                if self.codec is not None:  # decoded pull records of the batch's unique keys
+                    self.pull_buf = torch.empty(self.max_keys, self.P, device=self.device)
                 # fused merge+Adagrad scratch: straddling-run accumulators
                 # (kept all-zero between steps) and per-wave run owners
                 self.push_acc = torch.zeros(self.max_keys, self.Q, device=self.device)
@@ -197,6 +211,9 @@ class SparseEngine:
         self._seed = 1234
 
     # ------------------------------------------------------------------ build
+    def is_gpu_device(self) -> bool:
+        return self.device.type == "cuda"
+
     def set_slot_ids(self, slot_ids: List[float]):
         self.slot_ids = torch.tensor(slot_ids, dtype=torch.float32, device=self.device)
 
@@ -244,7 +261,10 @@ class SparseEngine:
         st = self._pull_common(keys, lod, B, S, fill_occ=False)
         sl = st.slot
         h = self._hip
-        if not self.sharded:
+        if not self.sharded and self.codec is not None:
+            self.table.t.codec_pull(self.codec.native(), st.rows, None, sl.ws.u_count, st.L, self.pull_buf)
+            src, src_index = self.pull_buf, None
+        elif not self.sharded:
             src, src_index = self.table.values, st.rows
         else:
             src, src_index = sl.resp_back, sl.send_index
@@ -299,7 +319,10 @@ class SparseEngine:
                 self.table.insert_mixed(sl.ws_r.uniq_h[:U][miss], self.cfg.sgd)
                 rows_r = self.table.probe(sl.ws_r.uniq_h, sl.ws_r.u_count)
         # owner answers straight from the table rows (no intermediate pull buffer)
-        self.table.t.gather_rows_by_uid(rows_r, sl.ws_r.uid, sl.resp)
+        if self.codec is not None:
+            self.table.t.codec_pull(self.codec.native(), rows_r, sl.ws_r.uid, None, sl.resp.shape[0], sl.resp)
+        else:
+            self.table.t.gather_rows_by_uid(rows_r, sl.ws_r.uid, sl.resp)
         self.comm.all_to_all_single(sl.resp_back, sl.resp)
         st.send_index = sl.send_index[:L]
         st.rows_r = rows_r
@@ -328,7 +351,7 @@ class SparseEngine:
         dout = dout.contiguous()
         ets = 0 if sp.use_cvm else sp.embed_thres_size
         if not self.sharded:
-            if sp.cvm_offset == 2 and cvm.shape[1] == 2:
+            if sp.cvm_offset == 2 and cvm.shape[1] == 2 and self.codec is None:
                 self._seed += 1
                 if self.table.t.push_merge_apply(dout, col_offset, cvm.contiguous(), sp.use_cvm, sp.clk_filter, self.E,
                                                  ws.perm[:L], ws.uid, sl.occ_slot, sl.occ_ins,
@@ -343,7 +366,7 @@ class SparseEngine:
                          ws.perm[:L], ws.uid, sl.occ_slot, sl.occ_ins, self._slot_ids(st.S),
                          ws.u_count[1:], push[:L], None, float(bs_scale), self.dim, ets)
             self._seed += 1
-            self.table.t.push_adagrad(st.rows, push[:L], ws.u_count, self._sgd_native, self._seed)
+            self._update_rows(st.rows, push[:L], ws.u_count)
             return
         self.push_send.zero_()
         h.push_merge(dout, col_offset, cvm.contiguous(), sp.cvm_offset, sp.use_cvm, sp.clk_filter, self.E,
@@ -357,12 +380,20 @@ class SparseEngine:
         per sender; merge them and apply sparse Adagrad in one kernel."""
         self._seed += 1
         ws = sl.ws_r
-        if self.table.t.push_adagrad_seg(rows_r, recv, ws.perm, ws.seg, ws.cnt, ws.u_count, self._sgd_native,
-                                         self._seed):
+        if self.codec is None and self.table.t.push_adagrad_seg(rows_r, recv, ws.perm, ws.seg, ws.cnt, ws.u_count,
+                                                                self._sgd_native, self._seed):
             return
         self.push_merged.zero_()
-        self._hip.push_merge_records(recv, ws.perm, ws.uid, ws.u_count[1:], self.dim, self.push_merged)
-        self.table.t.push_adagrad(rows_r, self.push_merged, ws.u_count, self._sgd_native, self._seed)
+        self._hip.push_merge_records(recv, ws.perm, ws.uid, ws.u_count[1:], self.xdim, self.push_merged)
+        self._update_rows(rows_r, self.push_merged, ws.u_count)
+
+    def _update_rows(self, rows: torch.Tensor, push: torch.Tensor, n_dev: torch.Tensor):
+        """Apply merged per-unique push records to the table rows (sparse
+        Adagrad, or the feature-type codec's rule)."""
+        if self.codec is not None:
+            self.table.t.codec_update(self.codec.native(), rows, push, n_dev, self._sgd_native, self._seed)
+        else:
+            self.table.t.push_adagrad(rows, push, n_dev, self._sgd_native, self._seed)
 
     def _slot_ids(self, S: int) -> torch.Tensor:
         if self.slot_ids.numel() < S:
@@ -375,9 +406,11 @@ class SparseEngine:
         return False
 
     # ------------------------------------------------------------------ unfused pull (pull_box_sparse)
-    def pull_records(self, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int):
-        """pull_box_sparse: per-occurrence pull records [L, 3+D] (box_wrapper.cu:74-143)."""
+    def pull_records(self, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int, with_expand: bool = False):
+        """pull_box_sparse: per-occurrence pull records [L, 3+D] (box_wrapper.cu:74-143);
+        with_expand: [L, 3+D+De] including the expand block (pull_box_extended_sparse)."""
         L = keys.numel()
+        W = 3 + self.xdim if with_expand else self.E
         if not self.is_gpu:
             uniq, uid = ref.dedup(keys)
             rows = self.table.probe(uniq)
@@ -389,7 +422,11 @@ class SparseEngine:
         st = self._pull_common(keys, lod, B, S)
         sl = st.slot
         if not self.sharded:
-            pulled = self.table.t.gather_pull(st.rows, sl.ws.u_count, self.P)
+            if self.codec is not None:
+                pulled = torch.empty(L, self.P, device=self.device)
+                self.table.t.codec_pull(self.codec.native(), st.rows, None, sl.ws.u_count, L, pulled)
+            else:
+                pulled = self.table.t.gather_pull(st.rows, sl.ws.u_count, self.P)
             recs = torch.empty(L, self.P, device=self.device)
             self._hip.gather_by_uid(pulled, sl.ws.uid[:L], recs, self.P)
         else:
@@ -397,7 +434,7 @@ class SparseEngine:
             idx = sl.send_index[:L][sl.ws.uid[:L].long().clamp(min=0)]
             ok = (sl.ws.uid[:L] >= 0) & (idx >= 0)
             recs = torch.where(ok.unsqueeze(1), sl.resp_back[idx.clamp(min=0)], torch.zeros((), device=self.device))
-        return recs[:, : self.E], st
+        return recs[:, :W], st
 
     def push_records(self, st: PullState, grads: torch.Tensor, cvm_cols: int, bs_scale: float,
                      slot_of_occ: Optional[torch.Tensor] = None):
@@ -407,7 +444,7 @@ class SparseEngine:
         if self.test_mode:
             return
         L = st.L
-        D = self.dim
+        D = min(self.xdim, grads.shape[1] - 3) if self.is_gpu else self.dim
         g = grads.float()
         rec = torch.zeros(L, self.Q, device=grads.device)
         if slot_of_occ is None:
@@ -432,14 +469,14 @@ class SparseEngine:
         if not self.sharded:
             push = self.push_buf
             push[:L].zero_()
-            h.push_merge_records(rec, ws.perm[:L], ws.uid, ws.u_count[1:], D, push[:L])
+            h.push_merge_records(rec, ws.perm[:L], ws.uid, ws.u_count[1:], self.xdim, push[:L])
             self._seed += 1
-            self.table.t.push_adagrad(st.rows, push[:L], ws.u_count, self._sgd_native, self._seed)
+            self._update_rows(st.rows, push[:L], ws.u_count)
             return
         # merge locally per unique into the owner send layout, then exchange
         U_cap = L
         merged = torch.zeros(U_cap, self.Q, device=self.device)
-        h.push_merge_records(rec, ws.perm[:L], ws.uid, ws.u_count[1:], D, merged)
+        h.push_merge_records(rec, ws.perm[:L], ws.uid, ws.u_count[1:], self.xdim, merged)
         self.push_send.zero_()
         idx = st.send_index
         ok = idx >= 0
