@@ -6,6 +6,7 @@
 #include "dump.h"
 #include "metrics.h"
 #include "runtime.h"
+#include "auc_runner.h"
 #include "slot_dataset.h"
 
 namespace py = pybind11;
@@ -275,6 +276,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("num_sparse_slots", &SlotDataset::num_sparse_slots)
       .def("dense_width", &SlotDataset::dense_width)
       .def("sparse_slot_names", &SlotDataset::sparse_slot_names)
+      .def("sparse_slot_u64_index", &SlotDataset::sparse_slot_u64_index)
       .def("dense_slot_names", &SlotDataset::dense_slot_names)
       .def("dense_slot_dims", &SlotDataset::dense_slot_dims)
       .def("build_batch", [](const SlotDataset& d, int64_t begin, int64_t count, bool pin) {
@@ -373,6 +375,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       });
 
   // ---------------------------------------------------------------- dump
+  py::class_<AucRunner>(m, "AucRunner")
+      .def(py::init<int, int, uint64_t>(), py::arg("pool_size"), py::arg("threads") = 4, py::arg("seed") = 0)
+      .def("set_eval_slots", &AucRunner::set_eval_slots)
+      .def("sample", [](AucRunner& a, SlotDataset& d) { a.sample(d.store()); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("candidate_keys", [](const AucRunner& a) { return to_tensor_u64(a.candidate_keys()); })
+      .def("shuffle", [](AucRunner& a, SlotDataset& d, const std::vector<int>& slots) {
+             return a.shuffle(&d.mutable_store(), slots);
+           }, py::call_guard<py::gil_scoped_release>())
+      .def("replaced", &AucRunner::replaced)
+      .def("pool_entries", &AucRunner::pool_entries);
   m.def("xxh64", [](const std::string& s, uint64_t seed) { return xxh64(s.data(), s.size(), seed); },
         py::arg("s"), py::arg("seed") = 0);
   py::class_<DumpWriter>(m, "DumpWriter")

@@ -106,6 +106,8 @@ class SlotDataset {
   int num_sparse_slots() const { return (int)sparse_slots_.size(); }
   int dense_width() const { return dense_width_; }
   std::vector<std::string> sparse_slot_names() const;
+  // used-uint64 index of each sparse slot (order of sparse_slot_names)
+  const std::vector<int>& sparse_slot_u64_index() const { return sparse_slots_; }
   std::vector<std::string> dense_slot_names() const;
   std::vector<int> dense_slot_dims() const;
 

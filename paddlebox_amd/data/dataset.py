@@ -160,6 +160,7 @@ class DatasetBase:
         self.current_phase = int(p)
 
     def set_fea_eval(self, record_candidate_size=0, fea_eval=True):
+        self.record_candidate_size = int(record_candidate_size)
         self.fea_eval = fea_eval
 
     def set_date(self, date: str):
@@ -398,9 +399,27 @@ class PadBoxSlotDataset(DatasetBase):
         th.join()
 
     def slots_shuffle(self, slots):
-        """AucRunner-style slot shuffle: permute the feasigns of the given
-        slots across instances (BoxHelper::SlotsShuffle)."""
-        self._shuffled_slots = set(slots)
+        """Replace the feasigns of ``slots`` in every instance by those of a
+        random other instance (reservoir-sampled), restoring the slots of the
+        previous call first; ``[]`` restores only.  With a BoxWrapper in
+        AucRunner mode this is BoxHelper::SlotsShuffle (phase flip, the
+        runner's candidates, box_wrapper.h:1185-1209); otherwise
+        Dataset::SlotsShuffle with a local reservoir (data_set.cc:1583-1614)."""
+        from ..ps.auc_runner import AucRunner
+
+        runner = getattr(self.box, "auc_runner", None) if self.box is not None else None
+        if runner is not None:
+            self.box.flip_phase()
+        else:
+            runner = getattr(self, "_slot_shuffler", None)
+            if runner is None or not runner.covers(self, slots):
+                if runner is not None:
+                    runner.shuffle(self, [])
+                size = getattr(self, "record_candidate_size", 0) or 10000
+                runner = AucRunner([list(slots)], 4, size)
+                runner.prepare(self)
+                self._slot_shuffler = runner
+        return runner.shuffle(self, list(slots))
 
     def __len__(self):
         return int(self._native.size())

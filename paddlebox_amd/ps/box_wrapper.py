@@ -100,6 +100,8 @@ class BoxWrapper:
         self._replica = None
         self._input_table = None
         self._expand = None
+        # AucRunner (slot-importance evaluation); None = train/test mode
+        self.auc_runner = None
         BoxWrapper._instance = self
 
     # ---------------------------------------------------------------- instance
@@ -181,7 +183,25 @@ class BoxWrapper:
             agent.add_keys(dataset_or_keys)
         else:
             agent.add_keys(dataset_or_keys.collect_keys())
+            if self.auc_runner is not None:
+                # GetRandomReplace + AddReplaceFeasign: the replacement
+                # candidates' feasigns join this pass's working set
+                agent.add_keys(self.auc_runner.prepare(dataset_or_keys))
         self.end_feed_pass(agent)
+
+    # ---------------------------------------------------------------- AucRunner
+    def initialize_auc_runner(self, slot_eval: Sequence[Sequence[str]], thread_num: int = 4, pool_size: int = 10000,
+                              slot_list: Sequence[str] = ()):
+        """InitializeAucRunner (box_wrapper.h:908-946): evaluation mode over
+        ``len(slot_eval)`` phases; ``slot_eval[i]`` is a group of slot names
+        whose feasigns get replaced by random other instances' ones."""
+        from .auc_runner import AucRunner
+
+        self.auc_runner = AucRunner(slot_eval, thread_num, pool_size)
+        return self.auc_runner
+
+    def auc_runner_mode(self) -> int:
+        return 1 if self.auc_runner is not None else 0
 
     def _route(self, h: torch.Tensor) -> torch.Tensor:
         """Send mixed keys to their owner rank; returns this rank's keys."""
