@@ -7,6 +7,7 @@
 #include "metrics.h"
 #include "runtime.h"
 #include "auc_runner.h"
+#include "tier_store.h"
 #include "slot_dataset.h"
 
 namespace py = pybind11;
@@ -375,6 +376,96 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       });
 
   // ---------------------------------------------------------------- dump
+  py::class_<HostTier>(m, "HostTier")
+      .def(py::init<int, int, int64_t>(), py::arg("stride"), py::arg("threads") = 16,
+           py::arg("chunk_rows") = 1 << 20)
+      .def("size", &HostTier::size)
+      .def("memory_bytes", &HostTier::memory_bytes)
+      .def("numa_nodes", &HostTier::numa_nodes)
+      .def("stride", &HostTier::stride)
+      .def("probe", [](const HostTier& t, const Tensor& h) {
+        auto hc = h.contiguous();
+        auto rows = torch::empty({hc.numel()}, torch::kInt64);
+        {
+          py::gil_scoped_release g;
+          t.probe(reinterpret_cast<const uint64_t*>(hc.data_ptr<int64_t>()), hc.numel(), rows.data_ptr<int64_t>());
+        }
+        return rows;
+      })
+      .def("insert", [](HostTier& t, const Tensor& h) {
+        auto hc = h.contiguous();
+        auto rows = torch::empty({hc.numel()}, torch::kInt64);
+        int64_t fresh = 0;
+        {
+          py::gil_scoped_release g;
+          t.insert(reinterpret_cast<const uint64_t*>(hc.data_ptr<int64_t>()), hc.numel(), rows.data_ptr<int64_t>(),
+                   &fresh);
+        }
+        return py::make_tuple(rows, fresh);
+      })
+      .def("gather", [](const HostTier& t, const Tensor& rows, Tensor out) {
+        TORCH_CHECK(out.is_contiguous() && out.dim() == 2 && out.size(0) >= rows.numel() &&
+                    out.scalar_type() == torch::kFloat32, "gather: out [n, stride] f32");
+        auto rc = rows.contiguous();
+        py::gil_scoped_release g;
+        t.gather(rc.data_ptr<int64_t>(), rc.numel(), out.data_ptr<float>(), (int)out.size(1));
+      })
+      .def("scatter", [](HostTier& t, const Tensor& rows, const Tensor& vals) {
+        auto rc = rows.contiguous();
+        auto vc = vals.contiguous().to(torch::kFloat32);
+        TORCH_CHECK(vc.dim() == 2 && vc.size(0) >= rc.numel(), "scatter: vals");
+        py::gil_scoped_release g;
+        t.scatter(rc.data_ptr<int64_t>(), rc.numel(), vc.data_ptr<float>(), (int)vc.size(1));
+      })
+      .def("erase", [](HostTier& t, const Tensor& h) {
+        auto hc = h.contiguous();
+        return t.erase(reinterpret_cast<const uint64_t*>(hc.data_ptr<int64_t>()), hc.numel());
+      })
+      .def("export_all", [](const HostTier& t) {
+        std::vector<uint64_t> k;
+        std::vector<float> v;
+        t.export_all(&k, &v);
+        return py::make_tuple(to_tensor_u64(k), to_tensor_f(v, t.stride()));
+      })
+      .def("select_ge", [](const HostTier& t, int col, float thr) {
+        std::vector<uint64_t> k;
+        std::vector<float> v;
+        t.select_ge(col, thr, &k, &v);
+        return py::make_tuple(to_tensor_u64(k), to_tensor_f(v, t.stride()));
+      })
+      .def("clear", &HostTier::clear);
+  py::class_<SsdLog>(m, "SsdLog")
+      .def(py::init<const std::string&, int, int64_t>(), py::arg("dir"), py::arg("stride"),
+           py::arg("segment_bytes") = 64ll << 20)
+      .def("size", &SsdLog::size)
+      .def("disk_bytes", &SsdLog::disk_bytes)
+      .def("direct_io", &SsdLog::direct_io)
+      .def("segments", &SsdLog::segments)
+      .def("put", [](SsdLog& s, const Tensor& h, const Tensor& v) {
+        auto hc = h.contiguous();
+        auto vc = v.contiguous().to(torch::kFloat32);
+        TORCH_CHECK(vc.dim() == 2 && vc.size(0) == hc.numel(), "put: one row per key");
+        py::gil_scoped_release g;
+        s.put(reinterpret_cast<const uint64_t*>(hc.data_ptr<int64_t>()), vc.data_ptr<float>(), hc.numel(),
+              (int)vc.size(1));
+      })
+      .def("get", [](const SsdLog& s, const Tensor& h) {
+        auto hc = h.contiguous();
+        auto found = torch::zeros({hc.numel()}, torch::kUInt8);
+        auto out = torch::empty({hc.numel(), s.stride()}, torch::kFloat32);
+        {
+          py::gil_scoped_release g;
+          s.get(reinterpret_cast<const uint64_t*>(hc.data_ptr<int64_t>()), hc.numel(), found.data_ptr<uint8_t>(),
+                out.data_ptr<float>(), s.stride());
+        }
+        return py::make_tuple(found.to(torch::kBool), out);
+      })
+      .def("erase", [](SsdLog& s, const Tensor& h) {
+        auto hc = h.contiguous();
+        return s.erase(reinterpret_cast<const uint64_t*>(hc.data_ptr<int64_t>()), hc.numel());
+      })
+      .def("compact", &SsdLog::compact, py::arg("min_live") = 0.5, py::call_guard<py::gil_scoped_release>())
+      .def("keys", [](const SsdLog& s) { return to_tensor_u64(s.keys()); });
   py::class_<AucRunner>(m, "AucRunner")
       .def(py::init<int, int, uint64_t>(), py::arg("pool_size"), py::arg("threads") = 4, py::arg("seed") = 0)
       .def("set_eval_slots", &AucRunner::set_eval_slots)

@@ -1,0 +1,592 @@
+#include "tier_store.h"
+
+#include <dirent.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <thread>
+
+namespace pbx {
+
+// ====================================================================== HostTier
+static std::vector<int> parse_cpulist(const std::string& s) {
+  std::vector<int> out;
+  std::stringstream ss(s);
+  std::string tok;
+  while (std::getline(ss, tok, ',')) {
+    if (tok.empty()) continue;
+    const auto dash = tok.find('-');
+    if (dash == std::string::npos) {
+      out.push_back(std::atoi(tok.c_str()));
+    } else {
+      const int a = std::atoi(tok.substr(0, dash).c_str()), b = std::atoi(tok.substr(dash + 1).c_str());
+      for (int c = a; c <= b; ++c) out.push_back(c);
+    }
+  }
+  return out;
+}
+
+static std::vector<std::vector<int>> numa_topology() {
+  std::vector<std::vector<int>> nodes;
+  for (int n = 0; n < 64; ++n) {
+    std::ifstream f("/sys/devices/system/node/node" + std::to_string(n) + "/cpulist");
+    if (!f) break;
+    std::string s;
+    std::getline(f, s);
+    auto cpus = parse_cpulist(s);
+    if (!cpus.empty()) nodes.push_back(cpus);
+  }
+  return nodes;
+}
+
+HostTier::HostTier(int stride, int threads, int64_t chunk_rows)
+    : stride_(stride), chunk_rows_(chunk_rows < 1024 ? 1024 : chunk_rows), shards_(kShards) {
+  if (stride < 1) throw std::runtime_error("HostTier: stride");
+  node_cpus_ = numa_topology();
+  // chunk pointers never move: readers index chunks_ while a writer appends
+  chunks_.reserve(kMaxChunks);
+  pool_ = std::make_unique<ThreadPool>(threads < 1 ? 1 : threads);
+  for (auto& s : shards_) {
+    s.keys.assign(1024, kEmptyKey);
+    s.rows.assign(1024, -1);
+  }
+}
+
+HostTier::~HostTier() {
+  for (float* c : chunks_) munmap(c, (size_t)chunk_rows_ * stride_ * sizeof(float));
+}
+
+void HostTier::add_chunk() { add_chunks(1); }
+
+// map `count` chunks and first-touch them in parallel, each from a thread
+// bound to its NUMA node (round-robin over nodes)
+void HostTier::add_chunks(int count) {
+  if (chunks_.size() + (size_t)count > (size_t)kMaxChunks) throw std::runtime_error("HostTier: arena full");
+  const size_t bytes = (size_t)chunk_rows_ * stride_ * sizeof(float);
+  std::vector<std::thread> th;
+  for (int c = 0; c < count; ++c) {
+    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (p == MAP_FAILED) throw std::runtime_error("HostTier: mmap failed");
+    madvise(p, bytes, MADV_HUGEPAGE);
+    const int node = node_cpus_.empty() ? -1 : (int)(chunks_.size() % node_cpus_.size());
+    th.emplace_back([this, p, bytes, node] {
+      if (node >= 0) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        for (int cpu : node_cpus_[node]) CPU_SET(cpu, &set);
+        pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+      }
+      std::memset(p, 0, bytes);
+    });
+    chunks_.push_back(static_cast<float*>(p));
+  }
+  for (auto& t : th) t.join();
+}
+
+int64_t HostTier::alloc_row() {
+  std::lock_guard<std::mutex> lk(alloc_mu_);
+  if (!free_rows_.empty()) {
+    const int64_t r = free_rows_.back();
+    free_rows_.pop_back();
+    return r;
+  }
+  if (next_row_ >= (int64_t)chunks_.size() * chunk_rows_) add_chunk();
+  return next_row_++;
+}
+
+int64_t HostTier::find(const Shard& s, uint64_t h) const {
+  const uint64_t mask = s.keys.size() - 1;
+  for (uint64_t i = mix64(h) & mask;; i = (i + 1) & mask) {
+    const uint64_t k = s.keys[i];
+    if (k == h) return (int64_t)i;
+    if (k == kEmptyKey) return -1;
+  }
+}
+
+void HostTier::grow(Shard* s) {
+  std::vector<uint64_t> ok;
+  std::vector<int64_t> orow;
+  ok.swap(s->keys);
+  orow.swap(s->rows);
+  size_t cap = ok.size();
+  while ((double)s->live / cap > 0.35) cap *= 2;
+  s->keys.assign(cap, kEmptyKey);
+  s->rows.assign(cap, -1);
+  const uint64_t mask = cap - 1;
+  s->used = 0;
+  for (size_t j = 0; j < ok.size(); ++j) {
+    if (ok[j] == kEmptyKey || ok[j] == kTomb) continue;
+    uint64_t i = mix64(ok[j]) & mask;
+    while (s->keys[i] != kEmptyKey) i = (i + 1) & mask;
+    s->keys[i] = ok[j];
+    s->rows[i] = orow[j];
+    ++s->used;
+  }
+}
+
+int64_t HostTier::size() const {
+  int64_t n = 0;
+  for (auto& s : shards_) {
+    std::lock_guard<std::mutex> lk(s.mu);
+    n += s.live;
+  }
+  return n;
+}
+
+int64_t HostTier::memory_bytes() const {
+  int64_t b = (int64_t)chunks_.size() * chunk_rows_ * stride_ * 4;
+  for (auto& s : shards_) b += (int64_t)s.keys.size() * 16;
+  return b;
+}
+
+void HostTier::probe(const uint64_t* h, int64_t n, int64_t* rows) const {
+  pool_->parallel_range(n, [&](int, int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) {
+      const Shard& s = shards_[shard_of(h[i])];
+      std::lock_guard<std::mutex> lk(s.mu);
+      const int64_t p = find(s, h[i]);
+      rows[i] = p < 0 ? -1 : s.rows[p];
+    }
+  });
+}
+
+void HostTier::insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_new) {
+  // 1) bucket the batch by shard
+  std::vector<std::vector<int64_t>> by(kShards);
+  {
+    std::vector<int64_t> cnt(kShards, 0);
+    for (int64_t i = 0; i < n; ++i) cnt[shard_of(h[i])]++;
+    for (int si = 0; si < kShards; ++si) by[si].reserve(cnt[si]);
+    for (int64_t i = 0; i < n; ++i) by[shard_of(h[i])].push_back(i);
+  }
+  // 2) per shard (parallel): resolve present keys, collect the distinct
+  //    absent ones, size the shard's table for them once
+  std::vector<std::vector<int64_t>> fresh(kShards);  // batch index of first occurrence
+  pool_->parallel_range(kShards, [&](int, int64_t b, int64_t e) {
+    for (int64_t si = b; si < e; ++si) {
+      Shard& s = shards_[si];
+      std::lock_guard<std::mutex> lk(s.mu);
+      for (int64_t i : by[si]) {
+        const uint64_t k = h[i];
+        if (k == kEmptyKey || k == kTomb) {
+          rows[i] = -1;
+          continue;
+        }
+        const int64_t p = find(s, k);
+        rows[i] = p < 0 ? -2 : s.rows[p];
+        if (p < 0) fresh[si].push_back(i);
+      }
+      // dedup absent keys within the batch
+      auto& f = fresh[si];
+      std::sort(f.begin(), f.end(), [&](int64_t a, int64_t c) { return h[a] < h[c] || (h[a] == h[c] && a < c); });
+      f.erase(std::unique(f.begin(), f.end(), [&](int64_t a, int64_t c) { return h[a] == h[c]; }), f.end());
+      if ((double)(s.used + (int64_t)f.size()) / s.keys.size() > 0.7) {
+        s.live += (int64_t)f.size();  // grow() sizes for live
+        grow(&s);
+        s.live -= (int64_t)f.size();
+      }
+    }
+  });
+  // 3) one allocation for all new rows: recycled rows first (zeroed), then
+  //    fresh arena rows (already zero), adding first-touched chunks as needed
+  std::vector<int64_t> base(kShards + 1, 0);
+  for (int si = 0; si < kShards; ++si) base[si + 1] = base[si] + (int64_t)fresh[si].size();
+  const int64_t total = base[kShards];
+  std::vector<int64_t> alloc(total);
+  {
+    std::lock_guard<std::mutex> lk(alloc_mu_);
+    int64_t k = 0;
+    std::vector<int64_t> recycled;
+    while (k < total && !free_rows_.empty()) {
+      alloc[k++] = free_rows_.back();
+      recycled.push_back(free_rows_.back());
+      free_rows_.pop_back();
+    }
+    const int64_t need = next_row_ + (total - k);
+    const int64_t have = (int64_t)chunks_.size() * chunk_rows_;
+    if (need > have) add_chunks((int)((need - have + chunk_rows_ - 1) / chunk_rows_));
+    while (k < total) alloc[k++] = next_row_++;
+    for (int64_t r : recycled) std::memset(row_ptr(r), 0, (size_t)stride_ * sizeof(float));
+  }
+  // 4) per shard (parallel): place the new keys
+  pool_->parallel_range(kShards, [&](int, int64_t b, int64_t e) {
+    for (int64_t si = b; si < e; ++si) {
+      Shard& s = shards_[si];
+      std::lock_guard<std::mutex> lk(s.mu);
+      const uint64_t mask = s.keys.size() - 1;
+      for (size_t q = 0; q < fresh[si].size(); ++q) {
+        const uint64_t k = h[fresh[si][q]];
+        uint64_t j = mix64(k) & mask;
+        while (s.keys[j] != kEmptyKey && s.keys[j] != kTomb) j = (j + 1) & mask;
+        if (s.keys[j] == kEmptyKey) ++s.used;
+        s.keys[j] = k;
+        s.rows[j] = alloc[base[si] + (int64_t)q];
+        ++s.live;
+      }
+      for (int64_t i : by[si])
+        if (rows[i] == -2) rows[i] = s.rows[find(s, h[i])];
+    }
+  });
+  if (n_new) *n_new = total;
+}
+
+void HostTier::gather(const int64_t* rows, int64_t n, float* out, int out_stride) const {
+  const int w = std::min(out_stride, stride_);
+  pool_->parallel_range(n, [&](int, int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) {
+      float* o = out + i * out_stride;
+      if (rows[i] < 0) {
+        std::memset(o, 0, (size_t)out_stride * sizeof(float));
+        continue;
+      }
+      std::memcpy(o, row_ptr(rows[i]), (size_t)w * sizeof(float));
+      if (out_stride > w) std::memset(o + w, 0, (size_t)(out_stride - w) * sizeof(float));
+    }
+  });
+}
+
+void HostTier::scatter(const int64_t* rows, int64_t n, const float* vals, int vstride) {
+  const int w = std::min(vstride, stride_);
+  pool_->parallel_range(n, [&](int, int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i)
+      if (rows[i] >= 0) std::memcpy(row_ptr(rows[i]), vals + i * vstride, (size_t)w * sizeof(float));
+  });
+}
+
+int64_t HostTier::erase(const uint64_t* h, int64_t n) {
+  int64_t gone = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    Shard& s = shards_[shard_of(h[i])];
+    std::lock_guard<std::mutex> lk(s.mu);
+    const int64_t p = find(s, h[i]);
+    if (p < 0) continue;
+    {
+      std::lock_guard<std::mutex> lk2(alloc_mu_);
+      free_rows_.push_back(s.rows[p]);
+    }
+    s.keys[p] = kTomb;
+    s.rows[p] = -1;
+    --s.live;
+    ++gone;
+  }
+  return gone;
+}
+
+void HostTier::export_all(std::vector<uint64_t>* keys, std::vector<float>* vals) const {
+  keys->clear();
+  vals->clear();
+  for (auto& s : shards_) {
+    std::lock_guard<std::mutex> lk(s.mu);
+    for (size_t j = 0; j < s.keys.size(); ++j) {
+      if (s.keys[j] == kEmptyKey || s.keys[j] == kTomb) continue;
+      keys->push_back(s.keys[j]);
+      const float* v = row_ptr(s.rows[j]);
+      vals->insert(vals->end(), v, v + stride_);
+    }
+  }
+}
+
+void HostTier::select_ge(int col, float thr, std::vector<uint64_t>* keys, std::vector<float>* vals) const {
+  keys->clear();
+  vals->clear();
+  if (col < 0 || col >= stride_) return;
+  for (auto& s : shards_) {
+    std::lock_guard<std::mutex> lk(s.mu);
+    for (size_t j = 0; j < s.keys.size(); ++j) {
+      if (s.keys[j] == kEmptyKey || s.keys[j] == kTomb) continue;
+      const float* v = row_ptr(s.rows[j]);
+      if (v[col] >= thr) {
+        keys->push_back(s.keys[j]);
+        vals->insert(vals->end(), v, v + stride_);
+      }
+    }
+  }
+}
+
+void HostTier::clear() {
+  for (auto& s : shards_) {
+    std::lock_guard<std::mutex> lk(s.mu);
+    s.keys.assign(1024, kEmptyKey);
+    s.rows.assign(1024, -1);
+    s.used = s.live = 0;
+  }
+  std::lock_guard<std::mutex> lk(alloc_mu_);
+  free_rows_.clear();
+  next_row_ = 0;
+}
+
+// ====================================================================== SsdLog
+// record: [u64 key][u32 flags][f32 x stride]; flags bit0 = tombstone
+static constexpr int64_t kPage = 4096;
+
+SsdLog::SsdLog(const std::string& dir, int stride, int64_t segment_bytes)
+    : dir_(dir), stride_(stride), rec_bytes_(12 + 4 * stride) {
+  if (stride < 1 || rec_bytes_ > kPage) throw std::runtime_error("SsdLog: record must fit a 4 KiB page");
+  per_page_ = (int)(kPage / rec_bytes_);
+  seg_pages_ = std::max<int64_t>(1, segment_bytes / kPage);
+  mkdir(dir.c_str(), 0755);
+  if (posix_memalign(reinterpret_cast<void**>(&active_buf_), kPage, (size_t)(seg_pages_ * kPage)) != 0)
+    throw std::runtime_error("SsdLog: buffer allocation failed");
+  // replay existing segments (seg-NNNNNN.log) in id order
+  std::vector<int> ids;
+  if (DIR* d = opendir(dir.c_str())) {
+    while (dirent* e = readdir(d)) {
+      int id;
+      if (std::sscanf(e->d_name, "seg-%06d.log", &id) == 1) ids.push_back(id);
+    }
+    closedir(d);
+  }
+  std::sort(ids.begin(), ids.end());
+  for (size_t i = 0; i < ids.size(); ++i) {
+    char name[64];
+    std::snprintf(name, sizeof(name), "/seg-%06d.log", ids[i]);
+    auto s = std::make_unique<Seg>();
+    s->id = (int)segs_.size();
+    s->path = dir_ + name;
+    if (ids[i] != s->id) {  // renumber densely
+      char nn[64];
+      std::snprintf(nn, sizeof(nn), "/seg-%06d.log", s->id);
+      std::rename(s->path.c_str(), (dir_ + nn).c_str());
+      s->path = dir_ + nn;
+    }
+    s->fd = open(s->path.c_str(), O_RDWR);
+    if (s->fd < 0) throw std::runtime_error("SsdLog: cannot open " + s->path);
+    segs_.push_back(std::move(s));
+    replay(segs_.back().get());
+  }
+  open_segment();
+}
+
+SsdLog::~SsdLog() {
+  for (auto& s : segs_)
+    if (s->fd >= 0) close(s->fd);
+  std::free(active_buf_);
+}
+
+void SsdLog::replay(Seg* s) {
+  struct stat st;
+  fstat(s->fd, &st);
+  const int64_t pages = st.st_size / kPage;
+  std::vector<char> page(kPage);
+  for (int64_t p = 0; p < pages; ++p) {
+    if (pread(s->fd, page.data(), kPage, p * kPage) != kPage) break;
+    for (int r = 0; r < per_page_; ++r) {
+      const char* rec = page.data() + (int64_t)r * rec_bytes_;
+      uint64_t key;
+      uint32_t flags;
+      std::memcpy(&key, rec, 8);
+      std::memcpy(&flags, rec + 8, 4);
+      if (key == kEmptyKey) continue;  // unused slot (pages are 0xFF-filled)
+      const int64_t slot = p * per_page_ + r;
+      s->slots = std::max(s->slots, slot + 1);
+      auto it = index_.find(key);
+      if (it != index_.end()) segs_[it->second.seg]->live--;
+      if (flags & 1u) {
+        if (it != index_.end()) index_.erase(it);
+      } else {
+        index_[key] = Loc{s->id, slot};
+        s->live++;
+      }
+    }
+  }
+}
+
+void SsdLog::open_segment() {
+  auto s = std::make_unique<Seg>();
+  s->id = (int)segs_.size();
+  char name[64];
+  std::snprintf(name, sizeof(name), "/seg-%06d.log", s->id);
+  s->path = dir_ + name;
+  int fd = -1;
+  if (direct_) {
+    fd = open(s->path.c_str(), O_RDWR | O_CREAT | O_TRUNC | O_DIRECT, 0644);
+    if (fd < 0 && errno == EINVAL) direct_ = false;  // e.g. tmpfs
+  }
+  if (fd < 0) fd = open(s->path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) throw std::runtime_error("SsdLog: cannot create " + s->path);
+  s->fd = fd;
+  segs_.push_back(std::move(s));
+  std::memset(active_buf_, 0xFF, (size_t)(seg_pages_ * kPage));
+}
+
+void SsdLog::flush_pages(Seg* s, int64_t first_page, int64_t npages) {
+  if (npages <= 0) return;
+  const char* src = active_buf_ + first_page * kPage;
+  const int64_t bytes = npages * kPage;
+  int64_t done = 0;
+  while (done < bytes) {
+    const ssize_t w = pwrite(s->fd, src + done, (size_t)(bytes - done), first_page * kPage + done);
+    if (w < 0 && errno == EINVAL && direct_) {
+      // O_DIRECT refused this write: fall back to buffered IO on this fd
+      int fl = fcntl(s->fd, F_GETFL);
+      fcntl(s->fd, F_SETFL, fl & ~O_DIRECT);
+      direct_ = false;
+      continue;
+    }
+    if (w <= 0) throw std::runtime_error("SsdLog: write failed");
+    done += w;
+  }
+}
+
+void SsdLog::append(uint64_t key, const float* v, bool tomb, std::vector<std::pair<uint64_t, Loc>>* placed) {
+  Seg* s = segs_.back().get();
+  if (s->slots >= seg_pages_ * per_page_) {
+    open_segment();
+    s = segs_.back().get();
+  }
+  const int64_t slot = s->slots++;
+  char* rec = active_buf_ + page_of(slot) * kPage + (slot % per_page_) * rec_bytes_;
+  const uint32_t flags = tomb ? 1u : 0u;
+  std::memcpy(rec, &key, 8);
+  std::memcpy(rec + 8, &flags, 4);
+  if (v)
+    std::memcpy(rec + 12, v, (size_t)stride_ * 4);
+  else
+    std::memset(rec + 12, 0, (size_t)stride_ * 4);
+  placed->emplace_back(key, Loc{tomb ? -1 : s->id, slot});
+}
+
+// append records (tomb: deletions) in page-aligned batches, one pwrite per
+// touched page range of each segment
+void SsdLog::write_batch(const uint64_t* h, const float* vals, int64_t n, int vstride, bool tomb,
+                         std::vector<std::pair<uint64_t, Loc>>* placed) {
+  std::vector<float> row(stride_, 0.f);
+  int64_t i = 0;
+  while (i < n) {
+    if (segs_.back()->slots >= seg_pages_ * per_page_) open_segment();
+    Seg* s = segs_.back().get();
+    const int64_t first_page = page_of(s->slots);
+    const int64_t take = std::min<int64_t>(seg_pages_ * per_page_ - s->slots, n - i);
+    for (int64_t j = 0; j < take; ++j, ++i) {
+      if (!tomb) {
+        const int w = std::min(vstride, stride_);
+        std::memcpy(row.data(), vals + i * vstride, (size_t)w * 4);
+      }
+      append(h[i], tomb ? nullptr : row.data(), tomb, placed);
+    }
+    flush_pages(s, first_page, page_of(s->slots - 1) - first_page + 1);
+  }
+}
+
+void SsdLog::put(const uint64_t* h, const float* vals, int64_t n, int vstride) {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<std::pair<uint64_t, Loc>> placed;
+  placed.reserve(n);
+  write_batch(h, vals, n, vstride, false, &placed);
+  for (auto& kl : placed) {
+    auto it = index_.find(kl.first);
+    if (it != index_.end()) segs_[it->second.seg]->live--;
+    index_[kl.first] = kl.second;
+    segs_[kl.second.seg]->live++;
+  }
+}
+
+int64_t SsdLog::erase(const uint64_t* h, int64_t n) {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<uint64_t> dead;
+  for (int64_t i = 0; i < n; ++i) {
+    auto it = index_.find(h[i]);
+    if (it == index_.end()) continue;
+    segs_[it->second.seg]->live--;
+    index_.erase(it);
+    dead.push_back(h[i]);
+  }
+  std::vector<std::pair<uint64_t, Loc>> placed;
+  write_batch(dead.data(), nullptr, (int64_t)dead.size(), 0, true, &placed);
+  return (int64_t)dead.size();
+}
+
+void SsdLog::get(const uint64_t* h, int64_t n, uint8_t* found, float* out, int out_stride) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  const int w = std::min(out_stride, stride_);
+  const int active = segs_.back()->id;
+  char* page = nullptr;
+  if (posix_memalign(reinterpret_cast<void**>(&page), kPage, kPage) != 0) throw std::runtime_error("SsdLog: alloc");
+  int cur_seg = -1;
+  int64_t cur_page = -1;
+  for (int64_t i = 0; i < n; ++i) {
+    float* o = out + i * out_stride;
+    auto it = index_.find(h[i]);
+    if (it == index_.end()) {
+      found[i] = 0;
+      std::memset(o, 0, (size_t)out_stride * 4);
+      continue;
+    }
+    const Loc l = it->second;
+    const char* rec;
+    if (l.seg == active) {
+      rec = active_buf_ + page_of(l.slot) * kPage + (l.slot % per_page_) * rec_bytes_;
+    } else {
+      if (l.seg != cur_seg || page_of(l.slot) != cur_page) {
+        if (pread(segs_[l.seg]->fd, page, kPage, page_of(l.slot) * kPage) != kPage) {
+          std::free(page);
+          throw std::runtime_error("SsdLog: read failed");
+        }
+        cur_seg = l.seg;
+        cur_page = page_of(l.slot);
+      }
+      rec = page + (l.slot % per_page_) * rec_bytes_;
+    }
+    std::memcpy(o, rec + 12, (size_t)w * 4);
+    if (out_stride > w) std::memset(o + w, 0, (size_t)(out_stride - w) * 4);
+    found[i] = 1;
+  }
+  std::free(page);
+}
+
+std::vector<uint64_t> SsdLog::keys() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<uint64_t> out;
+  out.reserve(index_.size());
+  for (auto& kv : index_) out.push_back(kv.first);
+  return out;
+}
+
+int64_t SsdLog::disk_bytes() const {
+  int64_t b = 0;
+  for (auto& s : segs_) b += ((s->slots + per_page_ - 1) / per_page_) * kPage;
+  return b;
+}
+
+int64_t SsdLog::compact(double min_live) {
+  std::vector<uint64_t> keys;
+  std::vector<int> victims;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    const int active = segs_.back()->id;
+    for (auto& s : segs_)
+      if (s->id != active && s->fd >= 0 && s->slots > 0 && (double)s->live / (double)s->slots < min_live)
+        victims.push_back(s->id);
+    if (victims.empty()) return 0;
+    for (auto& kv : index_)
+      if (std::find(victims.begin(), victims.end(), kv.second.seg) != victims.end()) keys.push_back(kv.first);
+  }
+  // re-append the victims' live records (newest copy wins through the index)
+  std::vector<uint8_t> f(keys.size());
+  std::vector<float> v(keys.size() * stride_);
+  get(keys.data(), (int64_t)keys.size(), f.data(), v.data(), stride_);
+  put(keys.data(), v.data(), (int64_t)keys.size(), stride_);
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int id : victims) {  // now record-free: drop the file, keep the id slot
+    Seg* s = segs_[id].get();
+    close(s->fd);
+    s->fd = -1;
+    std::remove(s->path.c_str());
+    s->slots = 0;
+    s->live = 0;
+  }
+  return (int64_t)keys.size();
+}
+
+}  // namespace pbx

@@ -1,0 +1,138 @@
+// Host and SSD tiers of the HBM -> host -> SSD embedding store.
+//
+// BoxPS keeps these inside the closed libbox_ps.so (LoadSSD2Mem /
+// FeedPass staging / EndPass write-back, box_wrapper.h:1142-1183,
+// box_wrapper.cc:120-210); the open reference analogue is the PSCore SSD
+// sparse table (distributed/ps/table/ssd_sparse_table.cc).  Designed here
+// for the MI355X node: the GPU tier holds a pass's working set (up to
+// hundreds of GB of HBM per GPU), so the host tier is a staging-friendly
+// row arena and the SSD tier a log-structured segment store.
+//
+//   HostTier  64 shards of open-addressing key -> row maps (per-shard locks,
+//             so feed-pass loader threads can insert concurrently) over one
+//             chunked row arena; chunks are mmap'ed with huge-page advice and
+//             first-touched by a thread bound to the chunk's NUMA node
+//             (round-robin), so gathers into the pinned H2D staging buffer
+//             stream from local memory.  gather / scatter are multi-threaded.
+//   SsdLog    append-only segment files of fixed-size records packed into
+//             4 KiB pages, written with O_DIRECT (page-aligned batches; falls
+//             back to buffered IO where the filesystem refuses O_DIRECT);
+//             in-memory key -> (segment, slot) index, tombstone records for
+//             deletes so the index is rebuilt exactly by replaying segments;
+//             compaction rewrites segments whose live fraction is low.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../common/pbx_common.h"
+#include "runtime.h"
+
+namespace pbx {
+
+class HostTier {
+ public:
+  HostTier(int stride, int threads = 16, int64_t chunk_rows = 1 << 20);
+  ~HostTier();
+  int stride() const { return stride_; }
+  int64_t size() const;
+  int64_t memory_bytes() const;
+  int numa_nodes() const { return (int)node_cpus_.size(); }
+
+  void probe(const uint64_t* h, int64_t n, int64_t* rows) const;
+  // insert absent keys with zeroed rows (duplicates allowed); rows[i] = row of h[i]
+  void insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_new);
+  void gather(const int64_t* rows, int64_t n, float* out, int out_stride) const;
+  void scatter(const int64_t* rows, int64_t n, const float* vals, int vstride);
+  int64_t erase(const uint64_t* h, int64_t n);
+  void export_all(std::vector<uint64_t>* keys, std::vector<float>* vals) const;
+  // keys/rows whose column `col` >= thr (cold rows for the SSD spill)
+  void select_ge(int col, float thr, std::vector<uint64_t>* keys, std::vector<float>* vals) const;
+  void clear();
+
+ private:
+  struct Shard {
+    std::vector<uint64_t> keys;  // open addressing, kEmptyKey = free, kTomb = deleted
+    std::vector<int64_t> rows;
+    int64_t used = 0, live = 0;
+    mutable std::mutex mu;
+  };
+  static constexpr int kShards = 64;
+  static constexpr int kMaxChunks = 1 << 16;
+  static constexpr uint64_t kTomb = 0xFFFFFFFFFFFFFFFEULL;
+  int shard_of(uint64_t h) const { return (int)(h >> 58); }  // top 6 bits
+  int64_t find(const Shard& s, uint64_t h) const;
+  void grow(Shard* s);
+  int64_t alloc_row();
+  float* row_ptr(int64_t r) const { return chunks_[r / chunk_rows_] + (r % chunk_rows_) * stride_; }
+  void add_chunk();
+  void add_chunks(int count);
+
+  int stride_;
+  int64_t chunk_rows_;
+  std::vector<Shard> shards_;
+  std::vector<float*> chunks_;
+  std::vector<int64_t> free_rows_;
+  int64_t next_row_ = 0;
+  std::mutex alloc_mu_;
+  std::vector<std::vector<int>> node_cpus_;
+  std::unique_ptr<ThreadPool> pool_;
+};
+
+class SsdLog {
+ public:
+  SsdLog(const std::string& dir, int stride, int64_t segment_bytes = 64ll << 20);
+  ~SsdLog();
+  int stride() const { return stride_; }
+  int64_t size() const { return (int64_t)index_.size(); }
+  int64_t disk_bytes() const;
+  bool direct_io() const { return direct_; }
+  int64_t segments() const { return (int64_t)segs_.size(); }
+
+  void put(const uint64_t* h, const float* vals, int64_t n, int vstride);
+  // found[i] = 1 and out[i] = record when present
+  void get(const uint64_t* h, int64_t n, uint8_t* found, float* out, int out_stride) const;
+  int64_t erase(const uint64_t* h, int64_t n);
+  // rewrite segments whose live fraction < min_live; returns records moved
+  int64_t compact(double min_live = 0.5);
+  std::vector<uint64_t> keys() const;
+
+ private:
+  struct Seg {
+    int id;
+    int fd;
+    int64_t slots = 0;  // records written
+    int64_t live = 0;
+    std::string path;
+  };
+  struct Loc {
+    int32_t seg;
+    int64_t slot;
+  };
+  void open_segment();
+  void replay(Seg* s);
+  void append(uint64_t key, const float* v, bool tomb, std::vector<std::pair<uint64_t, Loc>>* placed);
+  void write_batch(const uint64_t* h, const float* vals, int64_t n, int vstride, bool tomb,
+                   std::vector<std::pair<uint64_t, Loc>>* placed);
+  void flush_pages(Seg* s, int64_t first_page, int64_t npages);
+  int64_t page_of(int64_t slot) const { return slot / per_page_; }
+
+  std::string dir_;
+  int stride_;
+  int rec_bytes_;
+  int per_page_;
+  int64_t seg_pages_;
+  bool direct_ = true;
+  std::vector<std::unique_ptr<Seg>> segs_;  // segs_[i]->id == i (closed segments keep their fd)
+  std::unordered_map<uint64_t, Loc> index_;
+  // the active segment is mirrored in memory (page-aligned, written through)
+  char* active_buf_ = nullptr;
+  mutable std::mutex mu_;
+};
+
+}  // namespace pbx

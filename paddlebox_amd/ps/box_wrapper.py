@@ -34,10 +34,9 @@ from ..utils.dayid import make_day_id_str
 from ..utils.log import logger
 from ..utils.timer import StageTimers
 from . import checkpoint as ckpt
-from .config import PSConfig, feature_pull_offsets, feature_push_offsets
+from .config import PSConfig, feature_pull_offsets, feature_push_offsets, row_layout
 from .cpu_table import CpuSparseTable
 from .sparse_engine import SparseEngine
-from .ssd_tier import SsdStore
 
 
 class PSAgent:
@@ -53,13 +52,15 @@ class PSAgent:
         self._parts[tid % self.n].append(torch.tensor([key], dtype=torch.int64))
 
     def add_keys(self, keys: torch.Tensor, tid: int = 0):
-        self._parts[tid % self.n].append(keys.reshape(-1).to(torch.int64).cpu())
+        # kept where they are: device keys are deduplicated on the device
+        self._parts[tid % self.n].append(keys.reshape(-1).to(torch.int64))
 
     def keys(self) -> torch.Tensor:
         allk = [t for p in self._parts for t in p]
         if not allk:
             return torch.empty(0, dtype=torch.int64)
-        k = torch.cat(allk)
+        dev = next((t.device for t in allk if t.is_cuda), allk[0].device)
+        k = torch.cat([t.to(dev) for t in allk])
         k = k[(k != 0) & (k != -1)]
         return torch.unique(k)
 
@@ -86,7 +87,7 @@ class BoxWrapper:
         self.timers = StageTimers(self.device)
         self.mode = "hbm"
         self.host: Optional[CpuSparseTable] = None
-        self.ssd: Optional[SsdStore] = None
+        self.ssd = None  # tiered.SsdTier
         self.day_id = None
         self.pass_id = 0
         self.in_pass = False
@@ -100,6 +101,7 @@ class BoxWrapper:
         self._replica = None
         self._input_table = None
         self._expand = None
+        self.tier = None  # TieredStore (GPU tiered mode)
         # AucRunner (slot-importance evaluation); None = train/test mode
         self.auc_runner = None
         BoxWrapper._instance = self
@@ -138,10 +140,15 @@ class BoxWrapper:
                                    slot_ids=[float(s) for s in self.slot_vector] or None, group=self.group,
                                    auto_insert=auto_insert)
         if self.mode == "tiered":
-            self.host = CpuSparseTable(self.cfg.embedx_dim)
+            from .tiered import HostTable, SsdTier, TieredStore
+
+            self.host = HostTable(self.cfg.embedx_dim)
             p = ssd_path or self.cfg.tier.ssd_path
             if p:
-                self.ssd = SsdStore(os.path.join(p, f"rank{self.rank:05d}"), self.host.stride)
+                self.ssd = SsdTier(os.path.join(p, f"rank{self.rank:05d}"), self.host.stride)
+            if self.device.type == "cuda":
+                self.tier = TieredStore(self.engine, self.host, self.ssd, self.cfg.sgd,
+                                        spill_unseen=self.cfg.tier.spill_unseen_days)
         if model_path:
             self.load_model(model_path)
         return 0
@@ -228,7 +235,12 @@ class BoxWrapper:
         if self.mode == "hbm":
             eng.insert_local_mixed(h)
             return
-        # tiered: host is authoritative
+        if self.tier is not None:
+            # staged into the second GPU table in the background; made live
+            # by begin_pass (overlaps the current pass's training)
+            self.tier.stage(h)
+            return
+        # tiered (CPU engine): host is authoritative
         hc = h.cpu()
         rows = self.host.probe(hc)
         miss = rows < 0
@@ -248,6 +260,9 @@ class BoxWrapper:
 
     # ---------------------------------------------------------------- pass
     def begin_pass(self):
+        if self.tier is not None:
+            with self.timers.span("begin_pass_activate"):
+                self.tier.activate()
         self.in_pass = True
         self.pass_id += 1
 
@@ -258,7 +273,11 @@ class BoxWrapper:
         if eng.check_overflow():
             raise RuntimeError("sparse key exchange overflowed its per-peer capacity this pass; "
                                "raise SparseEngine cap_factor")
-        if self.mode == "tiered":
+        if self.tier is not None:
+            # export now, D2H + host scatter + SSD spill in the background
+            with self.timers.span("end_pass_writeback"):
+                self.tier.writeback()
+        elif self.mode == "tiered":
             with self.timers.span("end_pass_writeback"):
                 h, v = eng.table.export(True)
                 self.host.assign(h.cpu(), v.cpu())
@@ -287,17 +306,44 @@ class BoxWrapper:
 
     # ---------------------------------------------------------------- model IO
     def _authoritative(self):
-        return self.host if self.mode == "tiered" else self._require_engine().table
+        if self.mode == "tiered":
+            self._sync_tiers()
+            return self.host
+        return self._require_engine().table
+
+    def _sync_tiers(self):
+        """Host tier current: finish the background write-back and, inside a
+        pass, write the live GPU rows back synchronously first."""
+        if self.tier is not None:
+            if self.in_pass:
+                self.tier.flush()
+            self.tier.wait_writeback()
+        elif self.mode == "tiered" and self.engine is not None and self.in_pass:
+            h, v = self.engine.table.export(True)
+            self.host.assign(h.cpu(), v.cpu())
+
+    def _reset_delta_live(self, hk: torch.Tensor):
+        """save_xbox reset delta_score of the saved rows in the host tier; in a
+        pass the live GPU rows must see the reset too, or the EndPass write-back
+        would restore the old scores."""
+        if self.mode != "tiered" or not self.in_pass or self.engine is None or hk.numel() == 0:
+            return
+        t = self.engine.table
+        h = hk.to(t.device)
+        rows = t.probe(h)
+        ok = rows >= 0
+        if bool(ok.any()):
+            v = t.values[rows[ok]].clone()
+            v[:, row_layout(self.cfg.embedx_dim)["delta_score"]] = 0
+            t.t.assign(rows[ok], v)
 
     def save_base(self, batch_model_path: str, xbox_model_path: str, date: str = "") -> str:
         """Full batch model + xbox base (box_wrapper.cc:1286-1305)."""
-        if self.mode == "tiered" and self.engine is not None and self.in_pass:
-            h, v = self.engine.table.export(True)
-            self.host.assign(h.cpu(), v.cpu())
         t = self._authoritative()
         n = ckpt.save_batch_model(t, batch_model_path, self.rank, date)
         sg = self.cfg.sgd
-        x = ckpt.save_xbox(t, xbox_model_path, "base", self.cfg.save, sg.nonclk_coeff, sg.clk_coeff, self.rank)
+        x = ckpt.save_xbox(t, xbox_model_path, "base", self.cfg.save, sg.nonclk_coeff, sg.clk_coeff, self.rank,
+                           on_reset=self._reset_delta_live)
         if self.rank == 0:
             ckpt.write_manifest(os.path.dirname(os.path.abspath(batch_model_path)) or ".", date=date,
                                 pass_id=self.pass_id, embedx_dim=self.cfg.embedx_dim, world=self.world,
@@ -308,7 +354,8 @@ class BoxWrapper:
     def save_delta(self, xbox_model_path: str) -> str:
         t = self._authoritative()
         sg = self.cfg.sgd
-        x = ckpt.save_xbox(t, xbox_model_path, "delta", self.cfg.save, sg.nonclk_coeff, sg.clk_coeff, self.rank)
+        x = ckpt.save_xbox(t, xbox_model_path, "delta", self.cfg.save, sg.nonclk_coeff, sg.clk_coeff, self.rank,
+                           on_reset=self._reset_delta_live)
         return f"{xbox_model_path} xbox_delta={x}"
 
     def load_model(self, model_path: str, merge: bool = False):
@@ -345,14 +392,16 @@ class BoxWrapper:
         """Preload SSD rows into host memory (LoadSSD2Mem)."""
         if self.ssd is None or self.host is None:
             return 0
-        n = 0
-        for keys, vp in list(self.ssd.segments):
-            h = torch.from_numpy(keys.copy())
-            found, vals = self.ssd.get(h)
-            self.host.insert_mixed(h[found], self.cfg.sgd)
-            self.host.assign(h[found], vals[found])
-            n += int(found.sum())
-        return n
+        if self.tier is not None:
+            self.tier.wait_writeback()
+        h = self.ssd.keys()
+        if h.numel() == 0:
+            return 0
+        found, vals = self.ssd.get(h)
+        self.host.insert_mixed(h[found], self.cfg.sgd)
+        self.host.assign(h[found], vals[found])
+        self.ssd.delete(h[found])
+        return int(found.sum())
 
     def shrink_table(self) -> int:
         t = self._authoritative()

@@ -78,9 +78,12 @@ def load_batch_model_parts(path: str, rank: Optional[int] = None) -> Tuple[np.nd
     return np.concatenate(ks), np.concatenate(vs)
 
 
-def save_xbox(table, path: str, mode: str, cfg: SaveConfig, nonclk: float, clk: float, rank: int = 0) -> int:
+def save_xbox(table, path: str, mode: str, cfg: SaveConfig, nonclk: float, clk: float, rank: int = 0,
+              on_reset=None) -> int:
     """Write the xbox text model ('base' or 'delta'); resets delta_score of
-    the saved rows (ctr_accessor.cc:121-124,153-162)."""
+    the saved rows (ctr_accessor.cc:121-124,153-162).  ``on_reset(h)`` is
+    called with the saved mixed keys (another tier holding live copies of
+    the rows applies the same reset)."""
     os.makedirs(path, exist_ok=True)
     dim = table.dim
     l = row_layout(dim)
@@ -92,6 +95,8 @@ def save_xbox(table, path: str, mode: str, cfg: SaveConfig, nonclk: float, clk: 
         vr = vk.clone()
         vr[:, l["delta_score"]] = 0
         table.assign(hk, vr)
+        if on_reset is not None:
+            on_reset(hk)
     keys = ref.unmix64(hk.cpu()).numpy().view(np.uint64)
     vv = vk.float().cpu().numpy()
     with_x = (_score(vk, nonclk, clk) >= cfg.embedx_threshold).cpu().numpy()

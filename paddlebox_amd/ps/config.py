@@ -81,6 +81,7 @@ class TierConfig:
     host_enabled: bool = True
     ssd_path: Optional[str] = None
     ssd_spill_threshold: int = 0  # features kept in host RAM before spilling
+    spill_unseen_days: float = 1.0  # host rows unseen this long move to the SSD tier at EndPass
 
 
 @dataclass

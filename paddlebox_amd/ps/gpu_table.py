@@ -29,6 +29,7 @@ class GpuSparseTable:
         self.dim = codec.DX if codec is not None else dim
         self.device = torch.device(device)
         self.load_factor = load_factor
+        self.stash_cap = stash_cap
         slots = int(math.ceil(max(capacity, 16) / load_factor))
         self._mod = _native.hip()
         with torch.cuda.device(self.device):
@@ -39,6 +40,18 @@ class GpuSparseTable:
                 assert int(self.t.stride) == codec.raw_stride
         self.layout = row_layout(self.dim)
         self._seed = 0x5EED
+
+    @staticmethod
+    def like(other: "GpuSparseTable") -> "GpuSparseTable":
+        """An empty table with exactly the geometry of ``other`` (same bucket
+        count, stash and row stride), so whole-table copies between them are
+        plain device copies."""
+        slots = int(other.t.capacity)
+        t = GpuSparseTable(other.dim, int(slots * other.load_factor), other.device, other.stash_cap,
+                           other.load_factor, other.codec)
+        if int(t.t.capacity) != slots:
+            raise RuntimeError("GpuSparseTable.like: geometry mismatch")
+        return t
 
     # -- build ------------------------------------------------------------
     def insert_mixed(self, h: torch.Tensor, sgd: SparseSGDConfig, init_embedx: bool = False,

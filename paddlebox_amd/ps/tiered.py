@@ -1,0 +1,332 @@
+"""Tiered sparse store: HBM working set <- host tier <- SSD tier.
+
+BoxPS trains a pass out of HBM while the next pass's feature values are
+staged from host memory / SSD and the previous pass's are written back
+(FeedPass / BeginPass / EndPass, box_wrapper.h:1142-1183,
+box_wrapper.cc:120-210).  MI355X design:
+
+* The live GPU table never moves (captured HIP graphs hold its addresses).
+  The next pass is staged into a second, identically shaped GPU table on a
+  side stream; ``activate`` (BeginPass) copies the rows the two passes share
+  from the live table into the staged one (their newest values) and then
+  copies the staged table over the live one device-to-device (~1 ms per
+  10 GB of HBM3E).
+* Staging runs in a background thread: host-tier probe / SSD reads /
+  gather into a pinned buffer are native and GIL-free (csrc/host/
+  tier_store.cc), then one H2D copy and the GPU insert + assign.
+* EndPass exports the live table (a device copy) and a background thread
+  moves it D2H into the host tier and spills rows unseen for
+  ``spill_unseen`` days to the log-structured SSD tier -- overlapped with the
+  next pass's training.  Staging of pass n+2 waits for write-back of pass n,
+  so every staged value is current.
+"""
+from __future__ import annotations
+
+import threading
+import time
+from typing import Optional, Tuple
+
+import torch
+
+from .. import _native
+from .config import ShrinkConfig, SparseSGDConfig, row_layout
+
+
+class HostTable:
+    """CpuSparseTable-compatible facade over the native HostTier."""
+
+    def __init__(self, dim: int, threads: int = 16, chunk_rows: int = 1 << 20, stride: Optional[int] = None):
+        self.dim = dim
+        self.layout = row_layout(dim)
+        self.stride = int(stride or self.layout["stride"])
+        self.device = torch.device("cpu")
+        self._native = _native.host().HostTier(self.stride, threads, chunk_rows)
+
+    def probe(self, h: torch.Tensor, n_dev=None) -> torch.Tensor:
+        return self._native.probe(h.reshape(-1).cpu())
+
+    def insert_mixed(self, h: torch.Tensor, sgd: SparseSGDConfig, init_embedx: bool = False, n_dev=None) -> int:
+        h = h.reshape(-1).cpu()
+        h = h[h != -1]
+        if h.numel() == 0:
+            return 0
+        before = self._native.probe(h)
+        rows, fresh = self._native.insert(h)
+        new = before < 0
+        if bool(new.any()) and (sgd.initial_range > 0 or init_embedx):
+            v = torch.zeros(int(new.sum()), self.stride)
+            if sgd.initial_range > 0:
+                v[:, 2] = (torch.rand(v.shape[0]) * 2 - 1) * sgd.initial_range
+            if init_embedx:
+                v[:, 3:3 + self.dim] = torch.rand(v.shape[0], self.dim) * sgd.mf_initial_range
+                v[:, self.layout["mf_size"]] = 1
+            self._native.scatter(rows[new], v)
+        return 0
+
+    def assign(self, h: torch.Tensor, vals: torch.Tensor):
+        rows = self.probe(h)
+        self._native.scatter(rows, vals.cpu().float())
+
+    def read(self, h: torch.Tensor) -> torch.Tensor:
+        rows = self.probe(h)
+        out = torch.empty(rows.numel(), self.stride)
+        self._native.gather(rows, out)
+        return out
+
+    def export(self, with_values: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        k, v = self._native.export_all()
+        return k, (v if with_values else None)
+
+    def erase(self, h: torch.Tensor) -> int:
+        return int(self._native.erase(h.reshape(-1).cpu()))
+
+    def size(self) -> int:
+        return int(self._native.size())
+
+    @property
+    def capacity(self) -> int:
+        return self.size()
+
+    def memory_bytes(self) -> int:
+        return int(self._native.memory_bytes())
+
+    def shrink(self, cfg: ShrinkConfig) -> int:
+        """Decay show/click, age, delete (ctr_accessor.cc:63-80) over the host tier."""
+        k, v = self.export(True)
+        if k.numel() == 0:
+            return 0
+        l = self.layout
+        v[:, 0] *= cfg.show_click_decay_rate
+        v[:, 1] *= cfg.show_click_decay_rate
+        v[:, l["unseen_days"]] += 1
+        score = (v[:, 0] - v[:, 1]) * cfg.nonclk_coeff + v[:, 1] * cfg.clk_coeff
+        keep = (score >= cfg.delete_threshold) & (v[:, l["unseen_days"]] <= cfg.delete_after_unseen_days)
+        self.erase(k[~keep])
+        self.assign(k[keep], v[keep])
+        return int((~keep).sum())
+
+    def clear(self):
+        self._native.clear()
+
+
+class SsdTier:
+    """Facade over the native log-structured SsdLog (csrc/host/tier_store.cc)."""
+
+    def __init__(self, path: str, stride: int, segment_bytes: int = 64 << 20):
+        import os
+
+        self.path = path
+        self.stride = stride
+        os.makedirs(path, exist_ok=True)
+        self._native = _native.host().SsdLog(path, stride, int(segment_bytes))
+
+    def __len__(self):
+        return int(self._native.size())
+
+    def put(self, h: torch.Tensor, v: torch.Tensor):
+        if h.numel():
+            self._native.put(h.reshape(-1).cpu(), v.cpu().float())
+
+    def get(self, h: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        return self._native.get(h.reshape(-1).cpu())
+
+    def delete(self, h: torch.Tensor):
+        if h.numel():
+            self._native.erase(h.reshape(-1).cpu())
+
+    def compact(self, min_live: float = 0.5) -> int:
+        return int(self._native.compact(min_live))
+
+    def keys(self) -> torch.Tensor:
+        return self._native.keys()
+
+    def disk_bytes(self) -> int:
+        return int(self._native.disk_bytes())
+
+    @property
+    def direct_io(self) -> bool:
+        return bool(self._native.direct_io())
+
+
+class TieredStore:
+    def __init__(self, engine, host: HostTable, ssd: Optional[SsdTier] = None, sgd: Optional[SparseSGDConfig] = None,
+                 spill_unseen: float = 1.0):
+        from .gpu_table import GpuSparseTable
+
+        self.engine = engine
+        self.host = host
+        self.ssd = ssd
+        self.sgd = sgd or engine.cfg.sgd
+        self.spill_unseen = spill_unseen
+        live = engine.table
+        self.live = live
+        if live.codec is not None:
+            raise NotImplementedError("tiered store with feature-type codecs")
+        # staged table: same geometry as the live one
+        self.stage_table = GpuSparseTable.like(live)
+        self.stream = torch.cuda.Stream(live.device)
+        self._stage_thread: Optional[threading.Thread] = None
+        self._wb_thread: Optional[threading.Thread] = None
+        self._stage_err = None
+        self._wb_err = None
+        self._wb_lock = threading.Lock()
+        # staging (pass n+1) and write-back (pass n) may run at the same time;
+        # their host/SSD sections are serialised so a spill cannot pull rows
+        # out from under a staging gather
+        self._tier_lock = threading.Lock()
+        self._staged_keys: Optional[torch.Tensor] = None
+        self._pin = {}  # reusable pinned staging buffers (pinning is slow)
+        self.stats = {"stage_s": 0.0, "writeback_s": 0.0, "activate_s": 0.0, "ssd_hits": 0, "spilled": 0,
+                      "staged_rows": 0, "new_rows": 0}
+
+    def _pinned(self, name: str, shape, dtype) -> torch.Tensor:
+        n = 1
+        for d in shape:
+            n *= int(d)
+        buf = self._pin.get(name)
+        if buf is None or buf.dtype != dtype or buf.numel() < n:
+            buf = torch.empty(max(n, 1) * 5 // 4, dtype=dtype, pin_memory=True)
+            self._pin[name] = buf
+        return buf[:n].view(*shape)
+
+    # ------------------------------------------------------------ staging (FeedPass)
+    def stage(self, h: torch.Tensor, block: bool = False):
+        """Stage the next pass's (owner-local, unique, mixed) keys into the
+        staged GPU table in the background."""
+        self.wait_stage()
+        self._stage_err = None
+        self._stage_thread = threading.Thread(target=self._stage_run, args=(h.reshape(-1).cpu().contiguous(),),
+                                              daemon=True)
+        self._stage_thread.start()
+        if block:
+            self.wait_stage()
+
+    def _stage_run(self, hc: torch.Tensor):
+        locked = False
+        try:
+            t0 = time.perf_counter()
+            self.wait_writeback()  # host values of earlier passes must be final
+            self._tier_lock.acquire()
+            locked = True
+            rows = self.host.probe(hc)
+            miss = rows < 0
+            if self.ssd is not None and bool(miss.any()):
+                found, vals = self.ssd.get(hc[miss])
+                if bool(found.any()):
+                    mk = hc[miss][found]
+                    r, _ = self.host._native.insert(mk)
+                    self.host._native.scatter(r, vals[found])
+                    self.ssd.delete(mk)
+                    self.stats["ssd_hits"] += int(mk.numel())
+                    rows = self.host.probe(hc)
+                    miss = rows < 0
+            known = ~miss
+            kh = hc[known]
+            buf = self._pinned("stage", (int(kh.numel()), self.host.stride), torch.float32)
+            self.host._native.gather(rows[known].contiguous(), buf)
+            self._tier_lock.release()
+            locked = False
+            dev = self.live.device
+            with torch.cuda.device(dev), torch.cuda.stream(self.stream):
+                st = self.stage_table
+                st.clear()
+                hd = hc.to(dev, non_blocking=True)
+                st.insert_mixed(hd, self.sgd)  # new keys get the standard GPU init
+                if kh.numel():
+                    st.assign(kh.to(dev, non_blocking=True), buf.to(dev, non_blocking=True))
+                self._staged_keys = hd
+                self.stream.synchronize()
+            self.stats["staged_rows"] += int(kh.numel())
+            self.stats["new_rows"] += int(miss.sum())
+            self.stats["stage_s"] += time.perf_counter() - t0
+        except BaseException as e:  # surfaced by wait_stage
+            self._stage_err = e
+            if locked:
+                self._tier_lock.release()
+
+    def wait_stage(self):
+        if self._stage_thread is not None:
+            self._stage_thread.join()
+            self._stage_thread = None
+        if self._stage_err is not None:
+            e, self._stage_err = self._stage_err, None
+            raise e
+
+    # ------------------------------------------------------------ BeginPass
+    def activate(self):
+        """Make the staged pass live: shared keys take the live table's newest
+        rows, then the staged table is copied over the live one."""
+        self.wait_stage()
+        if self._staged_keys is None:
+            return
+        t0 = time.perf_counter()
+        live, st = self.live, self.stage_table
+        cur = torch.cuda.current_stream(live.device)
+        cur.wait_stream(self.stream)
+        k = self._staged_keys
+        if live.size() > 0:
+            rl = live.probe(k)
+            shared = rl >= 0
+            if bool(shared.any()):
+                st.t.assign(st.probe(k[shared]), live.values[rl[shared]].contiguous())
+        live.t.copy_from(st.t)
+        self._staged_keys = None
+        torch.cuda.synchronize(live.device)
+        self.stats["activate_s"] += time.perf_counter() - t0
+
+    # ------------------------------------------------------------ EndPass
+    def writeback(self, block: bool = False):
+        """Export the live table and move it into the host tier (then spill
+        cold rows to SSD) in the background."""
+        self.wait_writeback()
+        k, v = self.live.export(True)  # device copies: the live table may change after this
+        ev = torch.cuda.Event()
+        main = torch.cuda.current_stream(self.live.device)
+        self.stream.wait_stream(main)  # the export kernel has to finish first
+        with torch.cuda.stream(self.stream):
+            kh = self._pinned("wb_keys", tuple(k.shape), k.dtype)
+            vh = self._pinned("wb_vals", tuple(v.shape), v.dtype)
+            kh.copy_(k, non_blocking=True)
+            vh.copy_(v, non_blocking=True)
+            ev.record(self.stream)
+        self._wb_err = None
+        self._wb_thread = threading.Thread(target=self._wb_run, args=(ev, kh, vh, k, v), daemon=True)
+        self._wb_thread.start()
+        if block:
+            self.wait_writeback()
+
+    def _wb_run(self, ev, kh, vh, k_dev, v_dev):
+        try:
+            t0 = time.perf_counter()
+            ev.synchronize()
+            del k_dev, v_dev
+            with self._tier_lock:
+                self._wb_locked(kh, vh)
+            self.stats["writeback_s"] += time.perf_counter() - t0
+        except BaseException as e:
+            self._wb_err = e
+
+    def _wb_locked(self, kh, vh):
+        """Host scatter of the written-back rows, then the SSD spill (holds the tier lock)."""
+        rows, _ = self.host._native.insert(kh)
+        self.host._native.scatter(rows, vh)
+        if self.ssd is not None:
+            l = self.host.layout
+            ck, cv = self.host._native.select_ge(l["unseen_days"], float(self.spill_unseen))
+            if ck.numel():
+                self.ssd.put(ck, cv)
+                self.host.erase(ck)
+                self.stats["spilled"] += int(ck.numel())
+
+    def wait_writeback(self):
+        with self._wb_lock:
+            if self._wb_thread is not None:
+                self._wb_thread.join()
+                self._wb_thread = None
+            if self._wb_err is not None:
+                e, self._wb_err = self._wb_err, None
+                raise e
+
+    def flush(self):
+        """Synchronous write-back of the live table (save in the middle of a pass)."""
+        self.writeback(block=True)

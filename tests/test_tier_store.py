@@ -1,0 +1,70 @@
+"""Native host tier (sharded open addressing over a NUMA-first-touched row
+arena) and log-structured SSD tier (csrc/host/tier_store.cc)."""
+import numpy as np
+import torch
+
+from paddlebox_amd.ops import reference as ref
+from paddlebox_amd.ps.tiered import HostTable, SsdTier
+
+STRIDE = 20
+
+
+def _keys(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.unique(ref.mix64(torch.randint(0, 1 << 40, (n,), generator=g)))
+
+
+def test_host_tier_roundtrip_growth_erase():
+    t = HostTable(8, threads=4, chunk_rows=1024)
+    h = _keys(20000, 0)  # forces shard growth and several arena chunks
+    rows, fresh = t._native.insert(h)
+    assert fresh == h.numel() and t.size() == h.numel()
+    v = torch.randn(h.numel(), STRIDE)
+    t.assign(h, v)
+    assert torch.equal(t.read(h), v)
+    # duplicates / re-insert are no-ops
+    _, fresh2 = t._native.insert(torch.cat([h[:100], h[:100]]))
+    assert fresh2 == 0
+    gone = t.erase(h[::2])
+    assert gone == h[::2].numel() and t.size() == h.numel() - gone
+    assert bool((t.probe(h[::2]) == -1).all())
+    assert torch.equal(t.read(h[1::2]), v[1::2])
+    # freed rows are reused, re-inserted keys start zeroed
+    t._native.insert(h[::2])
+    assert float(t.read(h[::2]).abs().sum()) == 0.0
+    k, vals = t.export(True)
+    assert k.numel() == h.numel()
+    cold_k, _ = t._native.select_ge(t.layout["slot"], 0.5)
+    assert cold_k.numel() == int((torch.cat([torch.zeros(h[::2].numel()), v[1::2, t.layout["slot"]]]) >= 0.5).sum())
+
+
+def test_ssd_log_put_get_erase_compact_and_replay(tmp_path):
+    d = str(tmp_path / "ssd")
+    s = SsdTier(d, STRIDE, segment_bytes=1 << 16)  # small segments: many files
+    h = _keys(5000, 1)
+    v = torch.randn(h.numel(), STRIDE)
+    s.put(h, v)
+    assert len(s) == h.numel() and s._native.segments() > 3
+    f, got = s.get(h)
+    assert bool(f.all()) and torch.equal(got, v)
+    # overwrite half, delete a quarter
+    v2 = v.clone()
+    v2[: h.numel() // 2] += 1
+    s.put(h[: h.numel() // 2], v2[: h.numel() // 2])
+    s.delete(h[-h.numel() // 4:])
+    live = h.numel() - h.numel() // 4
+    assert len(s) == live
+    f, got = s.get(h)
+    assert int(f.sum()) == live
+    assert torch.equal(got[f], v2[f])
+    moved = s.compact(0.9)
+    assert moved > 0
+    f2, got2 = s.get(h)
+    assert torch.equal(f2, f) and torch.equal(got2[f2], v2[f2])
+    # a new process rebuilds the same index by replaying the segment log
+    del s
+    s2 = SsdTier(d, STRIDE, segment_bytes=1 << 16)
+    assert len(s2) == live
+    f3, got3 = s2.get(h)
+    assert torch.equal(f3, f) and torch.equal(got3[f3], v2[f3])
+    assert set(np.asarray(s2.keys()).tolist()) == set(np.asarray(h[f]).tolist())
