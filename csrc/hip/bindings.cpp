@@ -233,6 +233,19 @@ class GpuTable {
     launch_codec_init(view(), c, ptr<int64_t>(rows), ptr<uint64_t>(h), rows.numel(), cfg, seed, init_embedx ? 1 : 0,
                       cur_stream());
   }
+  // copy another table's full state (same geometry) into this one's storage,
+  // on the current stream: the tiered store swaps a staged pass working set
+  // into the live table without moving its device addresses (captured
+  // graphs keep pointing at the live table)
+  void copy_from(const GpuTable& o) {
+    PBX_CHECK(o.nb_ == nb_ && o.stash_cap_ == stash_cap_ && o.stride_ == stride_ && o.dim_ == dim_,
+              "copy_from: table geometry differs");
+    keys_.copy_(o.keys_, true);
+    fill_.copy_(o.fill_, true);
+    values_.copy_(o.values_, true);
+    stash_keys_.copy_(o.stash_keys_, true);
+    scratch_.copy_(o.scratch_, true);
+  }
   void clear() {
     keys_.fill_(-1);
     fill_.zero_();
@@ -949,6 +962,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("codec_update", &GpuTable::codec_update)
       .def("codec_init", &GpuTable::codec_init)
       .def_property_readonly("stride", &GpuTable::stride)
+      .def("copy_from", &GpuTable::copy_from)
       .def("clear", &GpuTable::clear)
       .def_property_readonly("keys", &GpuTable::keys)
       .def_property_readonly("values", &GpuTable::values)

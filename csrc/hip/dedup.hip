@@ -314,8 +314,8 @@ void launch_dedup(const uint64_t* keys, int64_t n, bool keys_are_mixed, uint64_t
                   int32_t* scan, int32_t* uid, uint64_t* uniq_h, int32_t* seg, int32_t* u_count,
                   void* temp, size_t temp_bytes, hipStream_t s) {
   if (n <= 0) {
-    (void)hipMemsetAsync(u_count, 0, 2 * sizeof(int32_t), s);
-    (void)hipMemsetAsync(seg, 0, sizeof(int32_t), s);
+    launch_fill32(u_count, 0u, 2, s);
+    launch_fill32(seg, 0u, 1, s);
     return;
   }
   const unsigned int g = (unsigned int)((n + 255) / 256);
@@ -339,8 +339,8 @@ void launch_dedup_hash(const HashDedupArgs& a, void* temp, size_t temp_bytes, hi
   const unsigned gc = (unsigned)((cap + 255) / 256);
   hipLaunchKernelGGL(k_hash_cleanup, dim3(gc), dim3(256), 0, s, a.u_count, a.slot_of_u, a.tk, a.tu, a.cnt, cap);
   if (a.n <= 0) {
-    (void)hipMemsetAsync(a.seg, 0, sizeof(int32_t), s);
-    (void)hipMemsetAsync(a.u_count + 2, 0, sizeof(int32_t), s);
+    launch_fill32(a.seg, 0u, 1, s);
+    launch_fill32(a.u_count + 2, 0u, 1, s);
     return;
   }
   const unsigned g = (unsigned)((a.n + 255) / 256);

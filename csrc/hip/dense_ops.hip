@@ -324,7 +324,7 @@ void launch_data_norm_bwd(const float* x, const float* dy, int N, int C, const f
                           const float* scales, float eps, float* dx, float* stats, float* acc,
                           const float* scale_w, hipStream_t s) {
   if (C == 0) return;
-  (void)hipMemsetAsync(acc, 0, 2 * (size_t)C * sizeof(float), s);
+  launch_fill32(acc, 0u, 2 * (int64_t)C, s);
   const dim3 g((C + 63) / 64, (N + kDnRows - 1) / kDnRows);
   hipLaunchKernelGGL(k_dn_bwd, g, dim3(256), 0, s, x, dy, N, C, means, scales, dx, acc, scale_w);
   hipLaunchKernelGGL(k_dn_finish, dim3(nblk(C)), dim3(256), 0, s, acc, C, N, eps, stats);

@@ -225,7 +225,7 @@ int head_blocks(int B) { return (B + kRB - 1) / kRB; }
 void launch_dn_stats(const float* part, int nrows, int C, int N, float eps, float* stats, float* acc,
                      hipStream_t s) {
   if (C == 0) return;
-  (void)hipMemsetAsync(acc, 0, 2 * (size_t)C * sizeof(float), s);
+  launch_fill32(acc, 0u, 2 * (int64_t)C, s);
   launch_colsum_acc(part, nrows, 2 * C, acc, -1, nullptr, s);
   hipLaunchKernelGGL(k_dn_stats, dim3((C + 255) / 256), dim3(256), 0, s, acc, C, N, eps, stats);
 }

@@ -178,6 +178,8 @@ void launch_push_adagrad(const TableDev& t, const int64_t* rows, const float* pu
                          const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s);
 // Zero the first U rows (U from device) of a [cap, stride] buffer.
 void launch_zero_rows(float* buf, int stride, const int32_t* n_dev, int64_t cap, hipStream_t s);
+// graph-safe 32-bit fill (use instead of hipMemsetAsync in capturable code)
+void launch_fill32(void* p, uint32_t v, int64_t n_words, hipStream_t s);
 
 // ---------------------------------------------------------------- sharding
 // Unique mixed keys (sorted) -> per-owner fixed-capacity send buffer [N, C]

@@ -29,7 +29,22 @@ __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ part, 
   }
 }
 
+// 32-bit fill.  Replaces hipMemsetAsync inside captured steps: a memset
+// node of a HIP graph was observed to leave the last bytes of a buffer whose
+// size is not a multiple of 16 unwritten on replay (data_norm statistics of
+// the last columns went stale in tests/test_gpu_fluid.py).
+__global__ void k_fill32(uint32_t* __restrict__ p, uint32_t v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
 }  // namespace
+
+void launch_fill32(void* p, uint32_t v, int64_t n_words, hipStream_t s) {
+  if (n_words <= 0) return;
+  hipLaunchKernelGGL(k_fill32, dim3((unsigned)((n_words + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<uint32_t*>(p), v, n_words);
+}
 
 void launch_colsum_acc(const float* part, int R, int W, float* out, int split_col, float* out2, hipStream_t s) {
   if (R == 0 || W == 0) return;

@@ -852,8 +852,8 @@ bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const in
 
 void launch_shard_pack_hash(const uint64_t* uniq_h, const int32_t* u_count, int64_t u_cap, int nranks, int64_t cap,
                             uint64_t* send, int64_t* send_index, int32_t* ocnt, int32_t* overflow, hipStream_t s) {
-  (void)hipMemsetAsync(send, 0xFF, (size_t)nranks * cap * sizeof(uint64_t), s);  // kEmptyKey
-  (void)hipMemsetAsync(ocnt, 0, (size_t)nranks * sizeof(int32_t), s);
+  launch_fill32(send, 0xFFFFFFFFu, 2 * (int64_t)nranks * cap, s);  // kEmptyKey
+  launch_fill32(ocnt, 0u, nranks, s);
   hipLaunchKernelGGL(k_shard_pack_hash, dim3(nblk(u_cap)), dim3(256), 0, s, uniq_h, u_count, nranks, cap, send,
                      send_index, ocnt, overflow);
 }
@@ -866,7 +866,7 @@ void launch_gather_rows_by_uid(const TableDev& t, const int64_t* rows, const int
 
 void launch_zero_rows(float* buf, int stride, const int32_t* n_dev, int64_t cap, hipStream_t s) {
   (void)n_dev;
-  (void)hipMemsetAsync(buf, 0, (size_t)cap * stride * sizeof(float), s);
+  launch_fill32(buf, 0u, (int64_t)cap * stride, s);
 }
 
 void launch_shard_pack(const uint64_t* uniq_h, const int32_t* u_count, int64_t u_cap, int nranks,

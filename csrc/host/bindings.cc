@@ -295,6 +295,28 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         }
         return py::make_tuple(keys, lod, dense);
       }, py::arg("begin"), py::arg("count"), py::arg("pin") = false)
+      .def("batch_len", [](const SlotDataset& d, int64_t begin, int64_t count) {
+        return d.batch_dims(begin, count).L;
+      })
+      // fill preallocated (pinned) buffers: keys padded with -1 to keys.numel()
+      .def("build_batch_into", [](const SlotDataset& d, int64_t begin, int64_t count, Tensor keys, Tensor lod,
+                                  Tensor dense) {
+        auto dims = d.batch_dims(begin, count);
+        const int S = d.num_sparse_slots();
+        TORCH_CHECK(keys.is_contiguous() && keys.scalar_type() == torch::kInt64 && keys.numel() >= dims.L,
+                    "build_batch_into: keys buffer too small");
+        TORCH_CHECK(lod.is_contiguous() && lod.numel() == (int64_t)S * (dims.B + 1), "build_batch_into: lod");
+        TORCH_CHECK(!d.dense_width() || (dense.is_contiguous() && dense.numel() == (int64_t)dims.B * d.dense_width()),
+                    "build_batch_into: dense");
+        {
+          py::gil_scoped_release nogil;
+          d.build_batch(begin, count, keys.data_ptr<int64_t>(), lod.data_ptr<int64_t>(),
+                        d.dense_width() ? dense.data_ptr<float>() : nullptr);
+          int64_t* k = keys.data_ptr<int64_t>();
+          for (int64_t i = dims.L; i < keys.numel(); ++i) k[i] = -1;
+        }
+        return dims.L;
+      })
       .def("build_rank_offset", [](const SlotDataset& d, int64_t begin, int64_t count, int max_rank) {
         auto out = torch::empty({count, 2 * max_rank + 1}, torch::kInt32);
         d.build_rank_offset(begin, count, max_rank, out.data_ptr<int32_t>());

@@ -14,7 +14,7 @@ copy of batch i+1 (copy stream) overlaps the replay of batch i.
 from __future__ import annotations
 
 import dataclasses
-from typing import Any, Callable, List, Sequence
+from typing import Any, Callable, List, Optional, Sequence
 
 import torch
 
@@ -60,7 +60,13 @@ def clone_batch(b, device):
 
 class GraphedTrainStep:
     def __init__(self, step_fn: Callable[[Any], Any], example_batch, device, n_buffers: int = 2,
-                 warmup: int = 3, max_inflight: int = 3):
+                 warmup: int = 3, max_inflight: int = 3, warm_batches: Sequence[Any] = (),
+                 on_warm: Optional[Callable[[Any], None]] = None):
+        """``warmup`` eager runs of ``step_fn`` on the example batch precede
+        the capture (lazy allocations, kernel selection).  A trainer that must
+        not train a batch twice passes ``warmup=0`` and ``warm_batches``: real
+        batches run eagerly through the same buffers before the capture
+        (``on_warm(out)`` sees each step's outputs)."""
         self.device = torch.device(device)
         self.step_fn = step_fn
         self.fields = _tensor_fields(example_batch)
@@ -71,6 +77,11 @@ class GraphedTrainStep:
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 step_fn(self.bufs[0])
+            for hb in warm_batches:
+                self.bufs[0]._flat.copy_(hb._flat, non_blocking=True)
+                out = step_fn(self.bufs[0])
+                if on_warm is not None:
+                    on_warm(out)
         cur.wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.graphs = []

@@ -36,6 +36,26 @@ from ..utils.log import logger
 
 log = logger()
 
+# lowered ops whose kernels are shape-static and free of host syncs: a step made
+# only of these can be captured into a HIP graph (the sparse data vars reach
+# the engine only through the fused pull, which reads the padded key buffer)
+GRAPH_SAFE_OPS = {
+    "__pull_seqpool_cvm", "__fused_mlp", "data_norm", "concat", "cast", "fill_constant_batch_size_like",
+    "sigmoid", "sigmoid_cross_entropy_with_logits", "reduce_mean", "relu", "fc", "elementwise_add",
+    "elementwise_mul", "elementwise_sub", "scale", "log_loss", "mean", "reduce_sum", "tanh", "softmax",
+}
+
+
+@dataclass
+class _GraphBatch:
+    """Fixed-shape device batch of the captured step: keys padded with -1 to
+    the pass's largest batch, lod, dense slots."""
+
+    keys: torch.Tensor
+    lod: torch.Tensor
+    dense: torch.Tensor
+
+
 # sync_dense_mode (boxps_worker.cc:393-395,1191-1258)
 SYNC_NONE = 0
 SYNC_KSTEP_NODE = 1
@@ -152,6 +172,156 @@ class BoxPSWorker:
         self.timers = {"read": 0.0, "step": 0.0, "metric": 0.0, "dump": 0.0}
 
     def train_files(self) -> Dict[str, float]:
+        why = self._graph_blocker()
+        if why is None:
+            return self._train_files_graphed()
+        if self.t.use_graph:
+            log.info("train_from_dataset: running eagerly (%s)", why)
+        return self._train_files_eager()
+
+    def _graph_blocker(self) -> Optional[str]:
+        """None when the step can be captured, else the reason it cannot."""
+        t, s = self.t, self.s
+        if not t.use_graph:
+            return "graph capture disabled"
+        if s.device.type != "cuda":
+            return "not a GPU session"
+        if t.infer or t.async_dense is not None:
+            return "infer / async dense mode"
+        if t.dumper is not None or _flags.get_bool("check_nan_inf"):
+            return "dump / nan-inf check need per-step host work"
+        ds = t.dataset
+        if ds is None or not hasattr(ds, "_native"):
+            return "no in-memory slot dataset"
+        if ds.rank_offset or ds.parse_ins_id or ds.parse_logkey:
+            return "per-batch host extras (rank_offset / ins_id / logkey)"
+        if any(sy.mode not in ("none", "grad_allreduce") for sy in s.syncs):
+            return "k-step / allgather dense sync keeps host counters"
+        eng = t.box.engine if t.box is not None else None
+        if eng is None or eng.auto_insert:
+            return "engine auto-insert syncs the host"
+        bad = sorted({op.type for op in s.lowered.steps} - GRAPH_SAFE_OPS)
+        if bad:
+            return f"ops not graph-safe: {bad}"
+        return None
+
+    def _train_files_graphed(self) -> Dict[str, float]:
+        """TrainFiles with the whole step (forward, backward, sparse push,
+        dense sync, optimizer) replayed from a HIP graph per batch size.
+        The first two batches of each size run eagerly through the capture
+        buffers (real training steps that also warm the lazy state), then the
+        step is captured and every further batch is one H2D + one replay
+        (reference per-batch op loop: boxps_worker.cc:1278-1357)."""
+        from collections import Counter
+
+        from ..data.dataset import SlotBatch
+        from .graph_step import GraphedTrainStep, pack_batch
+
+        t, s, ds, box = self.t, self.s, self.t.dataset, self.t.box
+        dev = s.device
+        nat = ds._native
+        plan = ds.prepare_train()
+        S = int(nat.num_sparse_slots())
+        names, dnames, ddims = nat.sparse_slot_names(), nat.dense_slot_names(), nat.dense_slot_dims()
+        Dw = int(nat.dense_width())
+        lens = [int(nat.batch_len(b0, c)) for b0, c in plan]
+        Lcap = (max(lens + [1]) + 255) // 256 * 256
+        if Lcap > box.engine.max_keys:
+            log.info("train_from_dataset: batch keys %d exceed engine max_keys; running eagerly", Lcap)
+            return self._train_files_eager()
+        sizes = Counter(c for _, c in plan)
+        graph_B = {B for B, n in sizes.items() if n >= 3}
+        label = ds.label_name if ds.label_name in dnames else None
+
+        def host_buf(B):
+            return pack_batch(_GraphBatch(torch.empty(Lcap, dtype=torch.int64),
+                                          torch.empty(S * (B + 1), dtype=torch.int64),
+                                          torch.empty(B, Dw, dtype=torch.float32)), pin=True)
+
+        def slot_batch(keys, lod, dense, B, lod_host):
+            b = SlotBatch(keys, lod, dense, B, S, names, dnames, ddims, lod_host=lod_host)
+            if label is not None:
+                lab = b.dense_var(label)[:, 0].contiguous()
+                b.extra["label"] = lab
+                b.extra["cvm"] = torch.stack([torch.ones_like(lab), lab], 1)
+            return b
+
+        def step_fn_for(B, lod_host):
+            def fn(gb):
+                batch = slot_batch(gb.keys, gb.lod, gb.dense, B, lod_host)
+                ctx = ExecContext(s, batch, training=True)
+                s.feed_batch(ctx, batch)
+                s.step(ctx)
+                return ctx, batch
+            return fn
+
+        def metrics(out):
+            if box is not None and box.metrics.metrics:
+                box.metrics.add_batch(_FetchView(*out))
+
+        graphs, warm, ring, nused = {}, {}, {}, {}
+        t0 = time.time()
+        n_ins = 0
+        replays = 0
+        for (b0, c) in plan:
+            t_r = time.time()
+            if c in graph_B and c not in graphs:
+                hb = host_buf(c)
+                nat.build_batch_into(b0, c, hb.keys, hb.lod, hb.dense)
+                warm.setdefault(c, []).append(hb)
+                self.timers["read"] += time.time() - t_r
+                if len(warm[c]) == 2:
+                    t_s = time.time()
+                    g = GraphedTrainStep(step_fn_for(c, warm[c][1].lod.clone()), warm[c][0], dev, warmup=0,
+                                         warm_batches=warm[c], on_warm=metrics)
+                    graphs[c] = g
+                    ring[c] = [host_buf(c) for _ in range(g.n)]
+                    nused[c] = 0
+                    self.timers["step"] += time.time() - t_s
+            elif c in graphs:
+                g = graphs[c]
+                j = nused[c] % g.n
+                nused[c] += 1
+                g.ready[j].synchronize()  # the H2D that last read this pinned slot is done
+                hb = ring[c][j]
+                nat.build_batch_into(b0, c, hb.keys, hb.lod, hb.dense)
+                t_s = time.time()
+                self.timers["read"] += t_s - t_r
+                g.load(j, hb)
+                out = g.run(j)
+                replays += 1
+                metrics(out)
+                self.timers["step"] += time.time() - t_s
+            else:  # odd-sized batch: eager
+                keys, lod, dense = nat.build_batch(b0, c, True)
+                bt = slot_batch(keys.to(dev, non_blocking=True), lod.to(dev, non_blocking=True),
+                                dense.to(dev, non_blocking=True), c, lod)
+                t_s = time.time()
+                self.timers["read"] += t_s - t_r
+                ctx = ExecContext(s, bt, training=True)
+                s.feed_batch(ctx, bt)
+                s.step(ctx)
+                metrics((ctx, bt))
+                self.timers["step"] += time.time() - t_s
+            self.batches += 1
+            n_ins += c
+        # a size seen fewer than 3 times (or its warm batches) never captured
+        for c, hbs in warm.items():
+            if c in graphs:
+                continue
+            for hb in hbs:
+                bt = slot_batch(hb.keys.to(dev), hb.lod.to(dev), hb.dense.to(dev), c, hb.lod)
+                ctx = ExecContext(s, bt, training=True)
+                s.feed_batch(ctx, bt)
+                s.step(ctx)
+                metrics((ctx, bt))
+        torch.cuda.synchronize(dev)
+        el = time.time() - t0
+        return {"batches": self.batches, "instances": n_ins, "seconds": el,
+                "ins_per_sec": n_ins / el if el > 0 else 0.0, "graph_replays": replays,
+                "graph_sizes": sorted(graphs), **self.timers}
+
+    def _train_files_eager(self) -> Dict[str, float]:
         t = self.t
         s = self.s
         box = t.box
@@ -278,6 +448,14 @@ class BoxPSTrainer:
         self.print_period = print_period
         self.fetch_handler = fetch_handler
         self.desc = TrainerDesc.from_program(program)
+        # HIP-graph capture of the step (default on GPU; _pipeline_opt
+        # {"use_graph": False} or FLAGS_padbox_use_graph=0 turn it off)
+        po = program._pipeline_opt or {}
+        try:
+            flag = _flags.get("padbox_use_graph")
+        except Exception:
+            flag = None
+        self.use_graph = bool(po.get("use_graph", True)) and str(flag).lower() not in ("0", "false")
         self.box = BoxWrapper._instance
         self.group = getattr(dataset, "group", None)
         ready = dist.is_available() and dist.is_initialized()
