@@ -7,6 +7,7 @@
 #include "metrics.h"
 #include "runtime.h"
 #include "auc_runner.h"
+#include "batch_assembler.h"
 #include "tier_store.h"
 #include "slot_dataset.h"
 
@@ -301,21 +302,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       // fill preallocated (pinned) buffers: keys padded with -1 to keys.numel()
       .def("build_batch_into", [](const SlotDataset& d, int64_t begin, int64_t count, Tensor keys, Tensor lod,
                                   Tensor dense) {
-        auto dims = d.batch_dims(begin, count);
         const int S = d.num_sparse_slots();
-        TORCH_CHECK(keys.is_contiguous() && keys.scalar_type() == torch::kInt64 && keys.numel() >= dims.L,
-                    "build_batch_into: keys buffer too small");
-        TORCH_CHECK(lod.is_contiguous() && lod.numel() == (int64_t)S * (dims.B + 1), "build_batch_into: lod");
-        TORCH_CHECK(!d.dense_width() || (dense.is_contiguous() && dense.numel() == (int64_t)dims.B * d.dense_width()),
+        TORCH_CHECK(begin >= 0 && count >= 0 && begin + count <= d.size(), "build_batch_into: range");
+        TORCH_CHECK(keys.is_contiguous() && keys.scalar_type() == torch::kInt64, "build_batch_into: keys");
+        TORCH_CHECK(lod.is_contiguous() && lod.numel() == (int64_t)S * (count + 1), "build_batch_into: lod");
+        TORCH_CHECK(!d.dense_width() || (dense.is_contiguous() && dense.numel() == count * d.dense_width()),
                     "build_batch_into: dense");
-        {
-          py::gil_scoped_release nogil;
-          d.build_batch(begin, count, keys.data_ptr<int64_t>(), lod.data_ptr<int64_t>(),
-                        d.dense_width() ? dense.data_ptr<float>() : nullptr);
-          int64_t* k = keys.data_ptr<int64_t>();
-          for (int64_t i = dims.L; i < keys.numel(); ++i) k[i] = -1;
-        }
-        return dims.L;
+        py::gil_scoped_release nogil;
+        return d.build_batch_staged(begin, count, keys.data_ptr<int64_t>(), keys.numel(), lod.data_ptr<int64_t>(),
+                                    d.dense_width() ? dense.data_ptr<float>() : nullptr);
       })
       .def("build_rank_offset", [](const SlotDataset& d, int64_t begin, int64_t count, int max_rank) {
         auto out = torch::empty({count, 2 * max_rank + 1}, torch::kInt32);
@@ -398,6 +393,36 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       });
 
   // ---------------------------------------------------------------- dump
+  py::class_<BatchAssembler>(m, "BatchAssembler")
+      .def(py::init([](const SlotDataset& ds, py::list jobs, int n_slots) {
+             std::vector<BatchAssembler::Job> js;
+             for (auto item : jobs) {
+               auto t = item.cast<py::tuple>();
+               BatchAssembler::Job j;
+               j.begin = t[0].cast<int64_t>();
+               j.count = t[1].cast<int64_t>();
+               Tensor k = t[2].cast<Tensor>(), l = t[3].cast<Tensor>(), d = t[4].cast<Tensor>();
+               TORCH_CHECK(k.is_contiguous() && k.scalar_type() == torch::kInt64, "assembler: keys int64");
+               TORCH_CHECK(l.is_contiguous() && l.scalar_type() == torch::kInt64 &&
+                               l.numel() == (int64_t)ds.num_sparse_slots() * (j.count + 1), "assembler: lod");
+               TORCH_CHECK(!ds.dense_width() || (d.is_contiguous() && d.numel() == j.count * ds.dense_width()),
+                           "assembler: dense");
+               j.keys = k.data_ptr<int64_t>();
+               j.keys_cap = k.numel();
+               j.lod = l.data_ptr<int64_t>();
+               j.dense = ds.dense_width() ? d.data_ptr<float>() : nullptr;
+               j.slot = t[5].cast<int>();
+               TORCH_CHECK(j.slot < n_slots, "assembler: slot id");
+               js.push_back(j);
+             }
+             return std::make_unique<BatchAssembler>(&ds, std::move(js), n_slots);
+           }),
+           py::keep_alive<1, 2>())
+      .def("start", &BatchAssembler::start)
+      .def("next", &BatchAssembler::next, py::call_guard<py::gil_scoped_release>())
+      .def("release", &BatchAssembler::release)
+      .def("build_seconds", &BatchAssembler::build_seconds)
+      .def("wait_seconds", &BatchAssembler::wait_seconds);
   py::class_<HostTier>(m, "HostTier")
       .def(py::init<int, int, int64_t>(), py::arg("stride"), py::arg("threads") = 16,
            py::arg("chunk_rows") = 1 << 20)

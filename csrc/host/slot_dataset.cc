@@ -480,43 +480,120 @@ SlotDataset::BatchDims SlotDataset::batch_dims(int64_t begin, int64_t count) con
   return d;
 }
 
+// batch assembly pool: condition-variable workers (no OpenMP spin-waiting that
+// would steal cores from the training loop's own threads)
+static ThreadPool& assembly_pool() {
+  static ThreadPool pool([] {
+    const char* e = std::getenv("PBX_BATCH_THREADS");
+    const int n = e ? std::atoi(e) : 8;
+    return n < 1 ? 1 : n;
+  }());
+  return pool;
+}
+
 void SlotDataset::build_batch(int64_t begin, int64_t count, int64_t* keys, int64_t* lod, float* dense) const {
+  build_batch_impl(begin, count, [keys](int64_t) { return keys; }, lod, dense);
+}
+
+void SlotDataset::build_batch_impl(int64_t begin, int64_t count, const std::function<int64_t*(int64_t)>& keys_for,
+                                   int64_t* lod, float* dense) const {
   const int nu = store_.nu, nf = store_.nf;
   const int B = (int)count;
+  const int S = (int)sparse_slots_.size();
+  ThreadPool& pool = assembly_pool();
+  // record-major passes: every record's slots are contiguous in the store, so
+  // each record is read once, sequentially (a slot-major walk would stride
+  // over every record once per slot).  Pass 1 writes per-slot lengths into
+  // the lod rows; a prefix over (slot, record) turns them into offsets; pass
+  // 2 copies each record's keys to its slot-major positions.
+  pool.parallel_range(B, [&](int, int64_t bb, int64_t be) {
+    for (int64_t b = bb; b < be; ++b) {
+      const int64_t i = order_[begin + b];
+      const int64_t* off = &store_.u64_off[i * nu];
+      for (int s = 0; s < S; ++s) {
+        const int j = sparse_slots_[s];
+        lod[(int64_t)s * (B + 1) + b] = off[j + 1] - off[j];
+      }
+    }
+  });
   int64_t k = 0;
-  for (size_t s = 0; s < sparse_slots_.size(); ++s) {
-    const int j = sparse_slots_[s];
+  for (int s = 0; s < S; ++s) {
     int64_t* l = lod + (int64_t)s * (B + 1);
     for (int b = 0; b < B; ++b) {
+      const int64_t n = l[b];
       l[b] = k;
-      const int64_t i = order_[begin + b];
-      const int64_t e0 = store_.u64_off[i * nu + j], e1 = store_.u64_off[i * nu + j + 1];
-      for (int64_t e = e0; e < e1; ++e) keys[k++] = (int64_t)store_.u64[e];
+      k += n;
     }
     l[B] = k;
   }
-  if (dense && dense_width_ > 0) {
-    for (int b = 0; b < B; ++b) {
+  int64_t* keys = keys_for(k);
+  pool.parallel_range(B, [&](int, int64_t bb, int64_t be) {
+    for (int64_t b = bb; b < be; ++b) {
       const int64_t i = order_[begin + b];
-      float* row = dense + (int64_t)b * dense_width_;
-      for (const auto& d : dense_refs_) {
-        int64_t e0, e1;
-        if (d.type == 'u') {
-          e0 = store_.u64_off[i * nu + d.idx];
-          e1 = store_.u64_off[i * nu + d.idx + 1];
-        } else {
-          e0 = store_.f32_off[i * nf + d.idx];
-          e1 = store_.f32_off[i * nf + d.idx + 1];
-        }
-        for (int c = 0; c < d.dim; ++c) {
-          const int64_t e = e0 + c;
-          float v = 0.f;
-          if (e < e1) v = d.type == 'u' ? (float)store_.u64[e] : store_.f32[e];
-          row[d.col + c] = v;
-        }
+      const int64_t* off = &store_.u64_off[i * nu];
+      for (int s = 0; s < S; ++s) {
+        const int j = sparse_slots_[s];
+        int64_t* dst = keys + lod[(int64_t)s * (B + 1) + b];
+        for (int64_t e = off[j]; e < off[j + 1]; ++e) *dst++ = (int64_t)store_.u64[e];
       }
     }
+  });
+  if (dense && dense_width_ > 0) {
+    pool.parallel_range(B, [&](int, int64_t bb, int64_t be) {
+      for (int64_t b = bb; b < be; ++b) {
+        const int64_t i = order_[begin + b];
+        float* row = dense + b * dense_width_;
+        for (const auto& d : dense_refs_) {
+          int64_t e0, e1;
+          if (d.type == 'u') {
+            e0 = store_.u64_off[i * nu + d.idx];
+            e1 = store_.u64_off[i * nu + d.idx + 1];
+          } else {
+            e0 = store_.f32_off[i * nf + d.idx];
+            e1 = store_.f32_off[i * nf + d.idx + 1];
+          }
+          for (int c = 0; c < d.dim; ++c) {
+            const int64_t e = e0 + c;
+            float v = 0.f;
+            if (e < e1) v = d.type == 'u' ? (float)store_.u64[e] : store_.f32[e];
+            row[d.col + c] = v;
+          }
+        }
+      }
+    });
   }
+}
+
+int64_t SlotDataset::build_batch_staged(int64_t begin, int64_t count, int64_t* keys, int64_t keys_cap, int64_t* lod,
+                                       float* dense) const {
+  thread_local std::vector<int64_t> sk, sl;
+  thread_local std::vector<float> sd;
+  const int64_t S = (int64_t)sparse_slots_.size();
+  const int64_t nl = S * (count + 1), nd = dense ? count * dense_width_ : 0;
+  if ((int64_t)sl.size() < nl) sl.resize(nl);
+  if ((int64_t)sd.size() < nd) sd.resize(nd);
+  int64_t L = 0;
+  build_batch_impl(
+      begin, count,
+      [&](int64_t n) {
+        // lengths are known before any key is written: refuse an oversized batch
+        if (n > keys_cap) throw std::runtime_error("build_batch: batch has more keys than its buffer");
+        if ((int64_t)sk.size() < n) sk.resize(n);
+        L = n;
+        return sk.data();
+      },
+      sl.data(), nd ? sd.data() : nullptr);
+  // (thread_local names inside the pool's lambdas would resolve to the
+  // workers' own, empty, scratch: hand them this thread's pointer)
+  const int64_t* src = sk.data();
+  assembly_pool().parallel_range(keys_cap, [&](int, int64_t a, int64_t b) {
+    const int64_t e = std::min(b, L);
+    if (a < e) std::memcpy(keys + a, src + a, (e - a) * sizeof(int64_t));
+    for (int64_t i = std::max(a, L); i < b; ++i) keys[i] = -1;
+  });
+  std::memcpy(lod, sl.data(), nl * sizeof(int64_t));
+  if (nd) std::memcpy(dense, sd.data(), nd * sizeof(float));
+  return L;
 }
 
 void SlotDataset::build_rank_offset(int64_t begin, int64_t count, int max_rank, int32_t* out) const {

@@ -14,6 +14,7 @@
 // pinned staging buffers that go to HBM in a single H2D copy per tensor.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 #include <thread>
@@ -100,6 +101,21 @@ class SlotDataset {
   };
   BatchDims batch_dims(int64_t begin, int64_t count) const;
   void build_batch(int64_t begin, int64_t count, int64_t* keys, int64_t* lod, float* dense) const;
+  // build_batch into this thread's pageable scratch, then stream it into the
+  // (pinned) targets with sequential copies; keys[L..keys_cap) = -1.  Pinned
+  // host memory is write-combined: the assembly's scattered stores into it ran
+  // 4x slower than into pageable memory (measured 1.75 vs 0.43 ms per batch).
+  // Returns L; throws when L > keys_cap.
+  int64_t build_batch_staged(int64_t begin, int64_t count, int64_t* keys, int64_t keys_cap, int64_t* lod,
+                             float* dense) const;
+
+ private:
+  // keys_for(L) is called once the batch's key count is known and returns the
+  // key target (it may throw to refuse the batch)
+  void build_batch_impl(int64_t begin, int64_t count, const std::function<int64_t*(int64_t)>& keys_for,
+                        int64_t* lod, float* dense) const;
+
+ public:
   // rank_offset [B, 2*max_rank+1] for PV batches (data_feed.cu:1319-1369)
   void build_rank_offset(int64_t begin, int64_t count, int max_rank, int32_t* out) const;
 

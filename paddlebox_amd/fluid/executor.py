@@ -21,7 +21,7 @@ import torch.distributed as dist
 from ..parallel.dense import DenseArena, DenseSync, FlatAdagrad, FlatAdam, FlatMomentum, FlatSGD
 from .framework import (LoDTensor, Parameter, Program, Scope, Variable, default_main_program,
                         default_startup_program, global_scope, to_device, torch_dtype)
-from .kernels import KERNELS, Ragged
+from .kernels import KERNELS, LazyRagged, Ragged
 from .lowering import Lowered, lower
 
 
@@ -105,7 +105,9 @@ def _make_opt(spec: dict, arena: DenseArena, lr_mult: float = 1.0):
     t = spec["type"]
     lr = spec["lr"] * lr_mult
     if t == "adam":
-        return FlatAdam(arena, lr, spec.get("beta1", 0.9), spec.get("beta2", 0.999), spec.get("epsilon", 1e-8))
+        # the update kernel also zeroes the gradients (no separate fill per step)
+        return FlatAdam(arena, lr, spec.get("beta1", 0.9), spec.get("beta2", 0.999), spec.get("epsilon", 1e-8),
+                        clear_grad=arena.flat.is_cuda)
     if t == "adamw":
         return FlatAdam(arena, lr, spec.get("beta1", 0.9), spec.get("beta2", 0.999), spec.get("epsilon", 1e-8),
                         spec.get("weight_decay", 0.01))
@@ -141,6 +143,7 @@ class Session:
             self._build_optimizer(sync_mode, sync_k)
         self.data_vars = [v for v in program.global_block().vars.values() if v.is_data]
         self.box = box
+        self._one = None
 
     # -------------------------------------------------------------- params
     def _materialize(self):
@@ -237,7 +240,7 @@ class Session:
             if v.name in sparse_idx:
                 s = sparse_idx[v.name]
                 a, e = int(lh[s, 0]), int(lh[s, B])
-                ctx.set(v, Ragged(batch.keys[a:e], lod[s] - a, B, s))
+                ctx.set(v, LazyRagged(batch.keys[a:e], lod[s], a, B, s))
             elif v.name in batch.dense_names:
                 ctx.set(v, batch.dense_var(v.name))
             elif v.name in batch.extra:
@@ -279,9 +282,15 @@ class Session:
             return
         loss = ctx.get(self.program._optimize["loss"])
         loss = loss.values if isinstance(loss, Ragged) else loss
-        for a in self.arenas:
-            a.zero_grad()
-        loss.float().sum().backward()
+        for a, o in zip(self.arenas, self.opts):
+            if not getattr(o, "clear_grad", False):  # else the update kernel zeroed them last step
+                a.zero_grad()
+        if loss.dim() == 0 and loss.dtype == torch.float32:
+            if self._one is None:
+                self._one = torch.ones((), device=loss.device)
+            loss.backward(self._one)  # persistent seed: no fill kernel per step
+        else:
+            loss.float().sum().backward()
         for s, o in zip(self.syncs, self.opts):
             s.apply(o)
 

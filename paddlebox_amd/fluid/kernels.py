@@ -51,6 +51,27 @@ class Ragged:
         return self.values.shape
 
 
+class LazyRagged(Ragged):
+    """A batch slot as Ragged whose rebased offsets (``lod_row - base``) are
+    only computed when an op reads them: the fused pull consumes the batch's
+    flat keys and lod directly, so a captured step carries no per-slot
+    offset kernels."""
+
+    def __init__(self, values, lod_row, base: int, B: int, slot: int):
+        self.values, self.B, self.slot = values, B, slot
+        self._lod_row, self._base, self._offs = lod_row, base, None
+
+    @property
+    def offsets(self):
+        if self._offs is None:
+            self._offs = self._lod_row - self._base
+        return self._offs
+
+    @offsets.setter
+    def offsets(self, v):
+        self._offs = v
+
+
 def _val(x):
     return x.values if isinstance(x, Ragged) else x
 
@@ -634,6 +655,54 @@ def k_fused_seq_tensor(ctx, op):
 
 
 # ----------------------------------------------------------------- lowered dense chains
+def _tower_for(ctx, op, C: int):
+    """CtrTower bound to the session's dense storage (fc weights already in
+    the [out, in] padded layout the tower packs from) and data_norm summaries."""
+    from ..ops.ctr import DataNorm
+    from ..ops.mlp import FusedMLP
+    from ..ops.tower import CtrTower
+
+    key = ("tower", id(op))
+    t = ctx.cache.get(key)
+    if t is not None:
+        return t
+    ws = [ctx.storage(v) for v in op.inputs["W"]]
+    bs = [ctx.storage(v) for v in op.inputs["B"]]
+    mlp = FusedMLP.__new__(FusedMLP)
+    torch.nn.Module.__init__(mlp)
+    mlp.in_dim = ws[0].shape[1]
+    mlp.hidden = [w.shape[0] for w in ws]
+    mlp.w = torch.nn.ParameterList(ws)
+    mlp.b = torch.nn.ParameterList(bs)
+    mlp.w_out = ctx.storage(op.inputs["WOut"][0])
+    mlp.b_out = ctx.storage(op.inputs["BOut"][0])
+    mlp._bf16, mlp.k_split, mlp.k_split_dw = [], 512, 1024
+    mlp._ws = mlp._tw = None
+    mlp._packed = mlp.packed_by_optimizer = False
+    a = op.attrs
+    dn = DataNorm(C, epsilon=a.get("epsilon") or 1e-5, summary_decay_rate=a.get("summary_decay_rate") or 0.9999999,
+                  sync_stats=bool(a.get("sync_stats")))
+    for attr, k in (("batch_size", "BatchSize"), ("batch_sum", "BatchSum"), ("batch_square_sum", "BatchSquareSum")):
+        setattr(dn, attr, ctx.scope.get(op.inputs[k][0].name))
+    dn.stats = torch.zeros(3 * C, device=ctx.device)
+    dn.update_norm = a.get("update_norm", True) is not False
+    dn.group = ctx.group
+    t = CtrTower(mlp, dn, 0, 1, 0, 0, use_head_lin=False)
+    ctx.cache[key] = t
+    return t
+
+
+@kernel("__ctr_tower")
+def k_ctr_tower(ctx, op):
+    x = _val(ctx.get(op.inputs["X"][0])).float().contiguous()
+    label = _val(ctx.get(op.inputs["Label"][0])).float().reshape(-1).contiguous()
+    t = _tower_for(ctx, op, x.shape[1])
+    t.dn.train(ctx.training)
+    loss, pred = t(x, label)
+    ctx.set(op.outputs["Pred"][0], pred.view(-1, 1))
+    ctx.set(op.outputs["Loss"][0], loss)
+
+
 @kernel("__fused_mlp")
 def k_fused_mlp(ctx, op):
     """Lowered fc(relu)^n [-> fc(size 1)] chain on the MFMA GEMM kernels."""

@@ -12,6 +12,8 @@ by the fused MI355X kernels:
 2. ``concat([seqpool outs..., dense...], axis=1)`` consuming those outputs
    is absorbed: the fused op writes the concat buffer and the per-slot
    outputs become column views of it.
+4. (GPU) ``data_norm -> __fused_mlp -> sigmoid / log-loss / mean``  =>
+   ``__ctr_tower`` (the fused CTR tower of the DeepFM bench, ops/tower.py).
 3. (GPU) ``fc(relu) -> ... -> fc(relu) [-> fc(size=1)]`` chains  =>
    ``__fused_mlp``: bf16 MFMA GEMMs with fused bias/ReLU epilogues, a GEMV
    logit head, ReLU-mask prologues and split-K dW/db in the backward.  The
@@ -191,6 +193,60 @@ def _fuse_mlp(ops: List[Operator], fetch: set, storage: Dict[str, StorageSpec], 
     return [op for k, op in enumerate(out) if k not in removed]
 
 
+def _fuse_tower(ops: List[Operator], fetch: set, notes: List[str]):
+    """(GPU) data_norm -> __fused_mlp(+logit head) -> {sigmoid, sigmoid_cross_
+    entropy_with_logits -> reduce_mean}  =>  ``__ctr_tower``: the fused CTR
+    tower (csrc/hip/tower.hip: data_norm head, MFMA MLP with activations kept
+    on chip, sigmoid + log-loss, one backward chain with the data_norm
+    statistics)."""
+    produced_at: Dict[str, int] = {}
+    for i, op in enumerate(ops):
+        for n in op.output_arg_names:
+            produced_at[n] = i
+    cons = _consumers(ops)
+    out = list(ops)
+    removed = set()
+    for m, mop in enumerate(ops):
+        if mop.type != "__fused_mlp" or not mop.inputs.get("WOut"):
+            continue
+        xn = mop.inputs["X"][0].name
+        d = produced_at.get(xn, -1)
+        if d < 0 or ops[d].type != "data_norm" or len(cons.get(xn, [])) != 1 or xn in fetch:
+            continue
+        dop = ops[d]
+        if dop.inputs.get("scale_w") or dop.inputs.get("bias") or dop.attrs.get("slot_dim", -1) > 0:
+            continue
+        logit = mop.outputs["Out"][0].name
+        users = cons.get(logit, [])
+        if logit in fetch or len(users) != 2:
+            continue
+        types = {ops[u].type: u for u in users}
+        if set(types) != {"sigmoid", "sigmoid_cross_entropy_with_logits"}:
+            continue
+        sg, xe = ops[types["sigmoid"]], ops[types["sigmoid_cross_entropy_with_logits"]]
+        xen = xe.outputs["Out"][0].name
+        xu = cons.get(xen, [])
+        if xen in fetch or len(xu) != 1 or ops[xu[0]].type != "reduce_mean" or xe.attrs.get("normalize"):
+            continue
+        rm = ops[xu[0]]
+        if rm.attrs.get("dim") not in (None, [], [0, 1], [-1, 0]) and not rm.attrs.get("reduce_all", True):
+            continue
+        lab = xe.inputs["Label"][0].name
+        if produced_at.get(lab, -1) >= m:
+            continue
+        ins = {"X": dop.inputs["X"], "Label": xe.inputs["Label"], "W": mop.inputs["W"], "B": mop.inputs["B"],
+               "WOut": mop.inputs["WOut"], "BOut": mop.inputs["BOut"],
+               "BatchSize": dop.inputs["BatchSize"], "BatchSum": dop.inputs["BatchSum"],
+               "BatchSquareSum": dop.inputs["BatchSquareSum"]}
+        attrs = {k: dop.attrs.get(k) for k in ("epsilon", "summary_decay_rate", "sync_stats", "update_norm")}
+        fused = _synthetic(mop.block, "__ctr_tower", ins, {"Pred": sg.outputs["Out"], "Loss": rm.outputs["Out"]},
+                           attrs)
+        out[m] = fused
+        removed.update({d, types["sigmoid"], types["sigmoid_cross_entropy_with_logits"], xu[0]})
+        notes.append("data_norm + __fused_mlp + sigmoid/log-loss -> __ctr_tower")
+    return [op for k, op in enumerate(out) if k not in removed]
+
+
 def lower(program: Program, fetch_names=(), gpu: bool = True, engine_cvm_offset: int = 2,
           fuse: bool = True) -> Lowered:
     ops = list(program.global_block().ops)
@@ -202,6 +258,7 @@ def lower(program: Program, fetch_names=(), gpu: bool = True, engine_cvm_offset:
         ops = _absorb_concat(ops, notes)
         if gpu:
             ops = _fuse_mlp(ops, fetch, storage, notes)
+            ops = _fuse_tower(ops, fetch, notes)
     for op in ops:
         if op.type not in KERNELS:
             raise NotImplementedError(f"no kernel for op '{op.type}'")

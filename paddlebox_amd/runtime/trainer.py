@@ -20,6 +20,7 @@ accepted and ignored).  Per batch the worker
 """
 from __future__ import annotations
 
+import collections
 import os
 import time
 from dataclasses import dataclass, field
@@ -40,7 +41,7 @@ log = logger()
 # only of these can be captured into a HIP graph (the sparse data vars reach
 # the engine only through the fused pull, which reads the padded key buffer)
 GRAPH_SAFE_OPS = {
-    "__pull_seqpool_cvm", "__fused_mlp", "data_norm", "concat", "cast", "fill_constant_batch_size_like",
+    "__pull_seqpool_cvm", "__fused_mlp", "__ctr_tower", "data_norm", "concat", "cast", "fill_constant_batch_size_like",
     "sigmoid", "sigmoid_cross_entropy_with_logits", "reduce_mean", "relu", "fc", "elementwise_add",
     "elementwise_mul", "elementwise_sub", "scale", "log_loss", "mean", "reduce_sum", "tanh", "softmax",
 }
@@ -225,7 +226,10 @@ class BoxPSWorker:
         names, dnames, ddims = nat.sparse_slot_names(), nat.dense_slot_names(), nat.dense_slot_dims()
         Dw = int(nat.dense_width())
         lens = [int(nat.batch_len(b0, c)) for b0, c in plan]
-        Lcap = (max(lens + [1]) + 255) // 256 * 256
+        Lcap = (max(lens + [1]) + 16383) // 16384 * 16384
+        # captured steps persist across passes (per session and batch size)
+        # while their key buffer covers the pass's largest batch
+        cache = s.cache.setdefault("graphs", {})
         if Lcap > box.engine.max_keys:
             log.info("train_from_dataset: batch keys %d exceed engine max_keys; running eagerly", Lcap)
             return self._train_files_eager()
@@ -259,52 +263,81 @@ class BoxPSWorker:
             if box is not None and box.metrics.metrics:
                 box.metrics.add_batch(_FetchView(*out))
 
-        graphs, warm, ring, nused = {}, {}, {}, {}
+        graphs, warm, rings, nused = {}, {}, {}, {}
+        for B, (cL, g, rg) in cache.items():
+            if B in graph_B and cL >= Lcap:
+                graphs[B], rings[B], nused[B] = g, rg, 0
+        Lcap = max([Lcap] + [cache[B][0] for B in graphs])
+        R = 4  # pinned host batches per size in flight
+        # the pass's batch assembly runs on a native thread (csrc/host/
+        # batch_assembler.cc) into pinned buffers; ring slots are handed back
+        # once their H2D has completed
+        cached = set(graphs)
+        jobs, meta, slot_ids = [], [], {}
+        used = Counter()
+        for (b0, c) in plan:
+            sid = -1
+            if c in graph_B:
+                k = used[c]
+                used[c] += 1
+                if c not in cached and k < 2:
+                    hb, tag = host_buf(c), "warm"
+                else:
+                    r = (k - (0 if c in cached else 2)) % R
+                    ring = rings.setdefault(c, [host_buf(c) for _ in range(R)])
+                    sid = slot_ids.setdefault((c, r), len(slot_ids))
+                    hb, tag = ring[r], "ring"
+            else:
+                hb, tag = host_buf(c), "eager"
+            jobs.append((b0, c, hb.keys, hb.lod, hb.dense, sid))
+            meta.append((c, hb, tag, sid))
+        asm = _native.host().BatchAssembler(nat, jobs, len(slot_ids))
+        pending: "collections.deque" = collections.deque()
         t0 = time.time()
         n_ins = 0
         replays = 0
-        for (b0, c) in plan:
-            t_r = time.time()
-            if c in graph_B and c not in graphs:
-                hb = host_buf(c)
-                nat.build_batch_into(b0, c, hb.keys, hb.lod, hb.dense)
+        asm.start()
+        while True:
+            i = asm.next()
+            if i < 0:
+                break
+            c, hb, tag, sid = meta[i]
+            t_s = time.time()
+            if tag == "warm":
                 warm.setdefault(c, []).append(hb)
-                self.timers["read"] += time.time() - t_r
                 if len(warm[c]) == 2:
-                    t_s = time.time()
                     g = GraphedTrainStep(step_fn_for(c, warm[c][1].lod.clone()), warm[c][0], dev, warmup=0,
                                          warm_batches=warm[c], on_warm=metrics)
                     graphs[c] = g
-                    ring[c] = [host_buf(c) for _ in range(g.n)]
                     nused[c] = 0
-                    self.timers["step"] += time.time() - t_s
-            elif c in graphs:
+                    cache[c] = (Lcap, g, rings.setdefault(c, [host_buf(c) for _ in range(R)]))
+            elif tag == "ring":
                 g = graphs[c]
                 j = nused[c] % g.n
                 nused[c] += 1
-                g.ready[j].synchronize()  # the H2D that last read this pinned slot is done
-                hb = ring[c][j]
-                nat.build_batch_into(b0, c, hb.keys, hb.lod, hb.dense)
-                t_s = time.time()
-                self.timers["read"] += t_s - t_r
                 g.load(j, hb)
+                ev = torch.cuda.Event()
+                ev.record(g.copy_stream)
+                pending.append((sid, ev))
                 out = g.run(j)
                 replays += 1
                 metrics(out)
-                self.timers["step"] += time.time() - t_s
             else:  # odd-sized batch: eager
-                keys, lod, dense = nat.build_batch(b0, c, True)
-                bt = slot_batch(keys.to(dev, non_blocking=True), lod.to(dev, non_blocking=True),
-                                dense.to(dev, non_blocking=True), c, lod)
-                t_s = time.time()
-                self.timers["read"] += t_s - t_r
+                bt = slot_batch(hb.keys.to(dev, non_blocking=True), hb.lod.to(dev, non_blocking=True),
+                                hb.dense.to(dev, non_blocking=True), c, hb.lod)
                 ctx = ExecContext(s, bt, training=True)
                 s.feed_batch(ctx, bt)
                 s.step(ctx)
                 metrics((ctx, bt))
-                self.timers["step"] += time.time() - t_s
+            while pending and (len(pending) > R - 2 or pending[0][1].query()):
+                sid0, ev0 = pending.popleft()
+                ev0.synchronize()
+                asm.release(sid0)
+            self.timers["step"] += time.time() - t_s
             self.batches += 1
             n_ins += c
+        self.timers["read"] = asm.build_seconds()
+        self.timers["read_wait"] = asm.wait_seconds()
         # a size seen fewer than 3 times (or its warm batches) never captured
         for c, hbs in warm.items():
             if c in graphs:

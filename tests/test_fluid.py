@@ -87,7 +87,9 @@ def test_program_building_and_lowering(box):
     low = lower(main, gpu=True)
     steps = [op.type for op in low.steps]
     assert "__pull_seqpool_cvm" in steps and "pull_box_sparse" not in steps
-    assert "__fused_mlp" in steps and "fc" not in steps
+    # GPU: fc chain -> __fused_mlp, then data_norm + MLP + sigmoid/log-loss -> __ctr_tower
+    assert "__ctr_tower" in steps and "fc" not in steps and "data_norm" not in steps
+    assert any("__fused_mlp" in n for n in low.fusions)
     assert any("absorbed" in n for n in low.fusions)
     # CPU lowering keeps the fp32 fc ops
     assert "fc" in [op.type for op in lower(main, gpu=False).steps]

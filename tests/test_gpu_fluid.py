@@ -71,3 +71,38 @@ def test_train_from_dataset_gpu_eager_and_graph(tmp_path):
     keep = [c for c in range(eager["table"].shape[1]) if c != 14]  # "slot" field: last occurrence, racy
     torch.testing.assert_close(graphed["table"][:, keep], eager["table"][:, keep], rtol=1e-2, atol=5e-3)
     assert abs(graphed["auc"] - eager["auc"]) < 0.01
+
+
+def test_tower_lowering_matches_unfused_program(tmp_path):
+    """On the GPU the canonical program lowers to __pull_seqpool_cvm +
+    __ctr_tower; its predictions and loss match the op-by-op program (fp32
+    data_norm, fc, sigmoid, log-loss) up to the tower's bf16 GEMM inputs."""
+    from paddlebox_amd.fluid.executor import ExecContext, Session
+    from tests.test_fluid import _lines
+
+    box = _box()
+    try:
+        main, startup, slots, label, dense, pred, loss = _build()
+        ds = fluid.DatasetFactory().create_dataset("PadBoxSlotDataset")
+        ds.set_use_var([label] + slots + [dense])
+        ds.set_batch_size(128)
+        ds.add_lines(_lines(128, seed=3))
+        box.feed_pass(ds)
+        batch = ds.build_batch(0, 128).to(torch.device("cuda:0"))
+        outs = {}
+        for fuse in (True, False):
+            scope = fluid.Scope()
+            exe = fluid.Executor(fluid.CUDAPlace(0))
+            exe.run(startup, scope=scope)
+            s = Session(main, scope, torch.device("cuda:0"), fuse=fuse)
+            if fuse:
+                assert "__ctr_tower" in [op.type for op in s.lowered.steps]
+            s.training = False
+            ctx = ExecContext(s, batch, training=False)
+            s.feed_batch(ctx, batch)
+            s.forward(ctx)
+            outs[fuse] = (ctx.get(pred).detach().float().view(-1).cpu(), float(ctx.get(loss)))
+        torch.testing.assert_close(outs[True][0], outs[False][0], rtol=0, atol=2e-2)
+        assert abs(outs[True][1] - outs[False][1]) < 2e-2
+    finally:
+        BoxWrapper._instance = None
