@@ -32,6 +32,7 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from paddlebox_amd.data.synthetic import CriteoSynth  # noqa: E402
+from paddlebox_amd.models.dcn_v2 import DCNv2  # noqa: E402
 from paddlebox_amd.models.deepfm import DeepFM  # noqa: E402
 from paddlebox_amd.ops import reference as ref  # noqa: E402
 from paddlebox_amd.ops.ctr import auc_accumulate  # noqa: E402
@@ -40,6 +41,7 @@ from paddlebox_amd.ps.config import PSConfig  # noqa: E402
 from paddlebox_amd.ps.sparse_engine import SparseEngine  # noqa: E402
 
 METRIC = "samples/sec (whole node) on Criteo-1TB-shape DeepFM"
+METRIC_DCN = "samples/sec (whole node) on Criteo-1TB-shape DCN-V2 (BASELINE config 5)"
 
 
 def log(rank, *a):
@@ -72,6 +74,9 @@ def main():
                     help="after the measurement, split host time into replay / H2D load (stderr only)")
     ap.add_argument("--mlp-dtype", choices=("bf16", "fp32"), default="bf16",
                     help="bf16: fused MFMA tower (default); fp32: the reference's fp32 fc precision")
+    ap.add_argument("--model", choices=("deepfm", "dcn_v2"), default="deepfm",
+                    help="deepfm = the headline config; dcn_v2 = BASELINE config 5 (cross layers on the MFMA GEMM)")
+    ap.add_argument("--cross-layers", type=int, default=3)
     ap.add_argument("--force-collectives", action="store_true",
                     help="run the multi-GPU exchange/all-reduce path even on 1 rank (rehearsal)")
     args = ap.parse_args()
@@ -131,16 +136,22 @@ def main():
                   f"{engine.table.memory_bytes() / 2**30:.1f} GiB) in {time.time() - t0:.1f}s")
 
     hidden = tuple(int(x) for x in args.hidden.split(","))
-    model = DeepFM(engine, num_slots=S, dense_dim=13, hidden=hidden).to(device)
+    dcn = args.model == "dcn_v2"
     fp32 = args.mlp_dtype == "fp32"
+    if dcn:
+        if fp32:
+            raise SystemExit("--mlp-dtype fp32 is a DeepFM precision variant")
+        model = DCNv2(engine, num_slots=S, dense_dim=13, cross_layers=args.cross_layers, hidden=hidden).to(device)
+    else:
+        model = DeepFM(engine, num_slots=S, dense_dim=13, hidden=hidden).to(device)
     if fp32:
         model.precision = "fp32"
     C = model.dn.C
-    arena = DenseArena(model.parameters(), device, extra_grad=3 * C if multi else 0)
+    arena = DenseArena(model.parameters(), device, extra_grad=3 * C if multi and not dcn else 0)
     if multi:
         model.dn.group = dist.group.WORLD
         model.dn.sync_stats = True
-        if not fp32:
+        if not fp32 and not dcn:
             # data_norm batch statistics are summed across ranks in the SAME
             # all-reduce as the dense gradients (tail of the gradient buffer)
             model.dn.stats = arena.grad_tail(3 * C)
@@ -148,13 +159,14 @@ def main():
     # one update launch for the dense side: Adam + bf16 tower weight re-pack +
     # data_norm summary update; grads zeroed by the same kernel
     opt = FlatAdam(arena, lr=1e-3, clear_grad=True)
-    if not fp32:
+    if not fp32 and not dcn:
         opt.fuse(mlps=[model.mlp], data_norms=[model.dn])
     # the dense all-reduce runs on its own communicator and side stream, started
     # as soon as the tower's gradients are final: it overlaps the sparse push
     sync = DenseSync(arena, mode="grad_allreduce",
                      overlap_group=dist.new_group(list(range(world))) if multi else None)
-    model.tower.on_dense_grads = sync.launch
+    if not dcn:
+        model.tower.on_dense_grads = sync.launch
 
     # every pinned batch buffer is streamed to the device once up front so the
     # timed steps do not pay the driver's first-touch cost of a pinned range
@@ -283,7 +295,7 @@ def main():
         log(rank, f"[bench] loss={float(loss):.4f} actual_ctr={st[3] / max(st[4], 1):.4f} "
                   f"pred_ctr={st[2] / max(st[4], 1):.4f} overflow={overflow}")
         out = {
-            "metric": METRIC,
+            "metric": METRIC_DCN if dcn else METRIC,
             "value": round(value, 1),
             "unit": "samples/s",
             "n_gpus": world,
@@ -297,7 +309,9 @@ def main():
             "data": "synthetic (Criteo-1TB-shape: 13 dense + 26 sparse slots, 1e9-feature space, "
                     f"power-law alpha={args.alpha}), random-init weights",
             "config": {
-                "model": "DeepFM (FM + data_norm + MLP %s), embedx_dim=8, sparse Adagrad GPU PS" % args.hidden,
+                "model": ("DCN-V2 (%d full-rank cross layers + data_norm + MLP %s), embedx_dim=8, sparse Adagrad GPU PS"
+                          % (args.cross_layers, args.hidden)) if dcn else
+                         ("DeepFM (FM + data_norm + MLP %s), embedx_dim=8, sparse Adagrad GPU PS" % args.hidden),
                 "global_batch": B * world,
                 "batch_per_gpu": B,
                 "seq_len": S,

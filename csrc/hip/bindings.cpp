@@ -889,12 +889,14 @@ static void adam_flat(Tensor p, Tensor g, Tensor m, Tensor v, Tensor pows, float
 namespace pbx {
 void bind_tower(py::module& m);
 void bind_ctr(py::module& m);
+void bind_cross(py::module& m);
 }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   using namespace pbx;
   bind_tower(m);
   bind_ctr(m);
+  bind_cross(m);
   m.doc() = "PaddleBox-capability engine: hand-written gfx950 (MI355X) kernels";
   py::class_<SparseSGDConfig>(m, "SparseSGDConfig")
       .def(py::init<>())

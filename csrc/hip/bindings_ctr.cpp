@@ -312,7 +312,56 @@ std::vector<Tensor> fused_seq_tensor(const Tensor& x, const Tensor& ad, int64_t 
 
 }  // namespace
 
+// device-resident pass batch assembly (batch_ops.hip).  Every index the
+// kernels follow is checked here: order values against nrec, offset array
+// lengths, output shapes.
+int64_t batch_assemble(const Tensor& u64, const Tensor& uoff, const Tensor& f32v, const Tensor& foff,
+                       const Tensor& order, const Tensor& sparse_idx, const Tensor& drefs, int64_t nu, int64_t nf,
+                       int64_t Dw, int64_t nrec, int64_t begin, int64_t B, Tensor lod, Tensor tot, Tensor keys,
+                       Tensor dense, Tensor overflow) {
+  auto i64 = [](const Tensor& t, const char* n) {
+    CX_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kInt64,
+             std::string(n) + " must be a contiguous int64 GPU tensor");
+  };
+  i64(u64, "u64");
+  i64(uoff, "uoff");
+  i64(foff, "foff");
+  i64(order, "order");
+  i64(lod, "lod");
+  i64(tot, "tot");
+  i64(keys, "keys");
+  f32(f32v, "f32");
+  f32(dense, "dense");
+  CX_CHECK(sparse_idx.is_cuda() && sparse_idx.scalar_type() == torch::kInt32, "sparse_idx must be int32 GPU");
+  CX_CHECK(drefs.is_cuda() && drefs.scalar_type() == torch::kInt32 && drefs.is_contiguous(), "drefs int32 GPU");
+  CX_CHECK(overflow.is_cuda() && overflow.scalar_type() == torch::kInt32 && overflow.numel() >= 1, "overflow");
+  const int64_t S = sparse_idx.numel();
+  CX_CHECK(S >= 1 && S <= batch_assemble_max_slots(), "sparse slot count out of range");
+  CX_CHECK(uoff.numel() == nrec * nu + 1 && foff.numel() == nrec * nf + 1, "offset arrays do not match nrec");
+  CX_CHECK(begin >= 0 && B >= 1 && begin + B <= order.numel(), "batch range outside the pass order");
+  CX_CHECK(lod.numel() == S * (B + 1) && tot.numel() >= S, "lod / tot shape");
+  CX_CHECK(dense.numel() == B * Dw, "dense shape");
+  CX_CHECK(drefs.dim() == 2 && drefs.size(1) == 4, "drefs must be [n, 4]");
+  BatchSrc src;
+  src.u64 = P<int64_t>(u64);
+  src.uoff = P<int64_t>(uoff);
+  src.f32 = P<float>(f32v);
+  src.foff = P<int64_t>(foff);
+  src.order = P<int64_t>(order);
+  src.sparse_idx = P<int32_t>(sparse_idx);
+  src.drefs = P<int32_t>(drefs);
+  src.nu = (int)nu;
+  src.nf = (int)nf;
+  src.S = (int)S;
+  src.ndref = (int)drefs.size(0);
+  src.Dw = (int)Dw;
+  launch_batch_assemble(src, begin, (int)B, P<int64_t>(lod), P<int64_t>(tot), P<int64_t>(keys), keys.numel(),
+                        P<float>(dense), P<int32_t>(overflow), cs());
+  return keys.numel();
+}
+
 void bind_ctr(py::module& m) {
+  m.def("batch_assemble", &batch_assemble);
   m.def("spv_fwd", &spv_fwd);
   m.def("spv_bwd", &spv_bwd);
   m.def("fused_seq_tensor", &fused_seq_tensor);

@@ -181,6 +181,22 @@ void launch_zero_rows(float* buf, int stride, const int32_t* n_dev, int64_t cap,
 // graph-safe 32-bit fill (use instead of hipMemsetAsync in capturable code)
 void launch_fill32(void* p, uint32_t v, int64_t n_words, hipStream_t s);
 
+// device-resident pass (batch_ops.hip): the record store's CSR arrays + the
+// pass order on the GPU
+struct BatchSrc {
+  const int64_t* u64;   // uint64 slot values (as int64)
+  const int64_t* uoff;  // [nrec*nu + 1]
+  const float* f32;
+  const int64_t* foff;  // [nrec*nf + 1]
+  const int64_t* order;
+  const int32_t* sparse_idx;  // [S] used-uint64 index of each sparse slot
+  const int32_t* drefs;       // [ndref][4] (0=u64/1=f32, idx, dim, col)
+  int nu, nf, S, ndref, Dw;
+};
+void launch_batch_assemble(const BatchSrc& src, int64_t begin, int B, int64_t* lod, int64_t* tot, int64_t* keys,
+                           int64_t keys_cap, float* dense, int32_t* overflow, hipStream_t st);
+int batch_assemble_max_slots();
+
 // ---------------------------------------------------------------- sharding
 // Unique mixed keys (sorted) -> per-owner fixed-capacity send buffer [N, C]
 // (kEmptyKey padded) + send_index[u] = o*C + (u - start_o) + overflow flag.
@@ -226,7 +242,19 @@ void launch_data_norm_update(float* bsize, float* bsum, float* bsq, const float*
 // bf16 MFMA GEMM for the MLP (csrc/hip/gemm.hip): C[M,N] = A'[M,K] B'[K,N]
 // with A'(m,k) at A[m*lda+k] (a_kcontig) or A[k*lda+m]; B'(k,n) at
 // B[n*ldb+k] (b_kcontig) or B[k*ldb+n].
-enum GemmEpi { EPI_BIAS_RELU_BF16 = 0, EPI_BIAS_BF16 = 1, EPI_BF16 = 2, EPI_F32_SLAB = 3 };
+enum GemmEpi {
+  EPI_BIAS_RELU_BF16 = 0,
+  EPI_BIAS_BF16 = 1,
+  EPI_BF16 = 2,
+  EPI_F32_SLAB = 3,
+  // DCN-V2 cross layer x_{l+1} = x0 * (x_l W^T + b) + x_l (cross.hip):
+  //   C (f32) = x_{l+1}, out2 = z_l, outb = bf16(x_{l+1}) (nullable)
+  EPI_CROSS_FWD = 4,
+  // cross backward dX: g_l = acc + gin; with zprev: C (f32) = g_l,
+  // outb = bf16(x0 * g_l), out2 += zprev * g_l; without (layer 0):
+  // outb[m*ldx0+n] = bf16(g_l + out2)  (the gradient of x0)
+  EPI_CROSS_DX = 5
+};
 struct GemmArgs {
   const unsigned short* A = nullptr;
   const unsigned short* maskA = nullptr;  // relu' mask in A's layout (bf16), optional
@@ -240,8 +268,23 @@ struct GemmArgs {
   int epi = EPI_BF16;
   int k_per_split = 1 << 30;
   int64_t slab_stride = 0;
+  // cross epilogues (all f32 / bf16 cross buffers share ldc; x0 has ldx0)
+  const unsigned short* x0 = nullptr;
+  int ldx0 = 0;
+  const float* xin = nullptr;
+  const float* gin = nullptr;
+  const float* zprev = nullptr;
+  float* out2 = nullptr;
+  unsigned short* outb = nullptr;
 };
 void launch_gemm(const GemmArgs& g, hipStream_t s);
+// DCN-V2 cross head (cross.hip): s[m] = x[m, :N] . w ; and its backward top:
+// g[m,n] = ds[m] w[n] (f32, ld), u = bf16(x0 * g), acc = z * g, dw += sum_m ds[m] x[m,n]
+void launch_cross_dot(const float* x, int M, int N, int ld, const float* w, float* out, hipStream_t s);
+int cross_top_blocks(int M);
+void launch_cross_top_bwd(const float* x, const unsigned short* x0, int ldx0, const float* z, const float* w,
+                          const float* ds, int M, int N, int ld, float* g, unsigned short* u, float* acc, float* part,
+                          float* dw, hipStream_t s);
 void launch_slab_reduce(const float* slab, int splits, int64_t slab_stride, int M, int N, int ldc, float* dW,
                         float* db, float scale, hipStream_t s);
 void launch_gemv_out(const unsigned short* h, int M, int K, int ldh, const float* w, const float* b, float* out,

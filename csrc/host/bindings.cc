@@ -269,6 +269,31 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         if (!o.empty()) memcpy(t.data_ptr(), o.data(), o.size() * 8);
         return t;
       })
+      .def("version", &SlotDataset::version)
+      .def("dense_refs", [](const SlotDataset& d) {
+        auto v = d.dense_refs();
+        auto t = torch::empty({(int64_t)v.size() / 4, 4}, torch::kInt32);
+        if (!v.empty()) memcpy(t.data_ptr(), v.data(), v.size() * 4);
+        return t;
+      })
+      // the record store's CSR arrays copied to `device` (u64 values as int64,
+      // u64 offsets [nrec*nu+1], f32 values, f32 offsets [nrec*nf+1])
+      .def("store_to", [](const SlotDataset& d, const std::string& device) {
+        const auto& st = d.store();
+        auto dev = torch::Device(device);
+        auto copy = [&](const void* p, int64_t n, torch::ScalarType ty) {
+          if (n == 0) return torch::empty({0}, torch::TensorOptions().dtype(ty).device(dev));
+          auto view = torch::from_blob(const_cast<void*>(p), {n}, torch::TensorOptions().dtype(ty));
+          return view.to(dev, /*non_blocking=*/false, /*copy=*/true);
+        };
+        py::gil_scoped_release nogil;
+        return std::make_tuple(copy(st.u64.data(), (int64_t)st.u64.size(), torch::kInt64),
+                               copy(st.u64_off.data(), (int64_t)st.u64_off.size(), torch::kInt64),
+                               copy(st.f32.data(), (int64_t)st.f32.size(), torch::kFloat32),
+                               copy(st.f32_off.data(), (int64_t)st.f32_off.size(), torch::kInt64));
+      })
+      .def("num_u64_slots", [](const SlotDataset& d) { return d.store().nu; })
+      .def("num_f32_slots", [](const SlotDataset& d) { return d.store().nf; })
       .def("merge_by_search_id", [](SlotDataset& d) {
         auto off = d.merge_by_search_id();
         auto t = torch::empty({(int64_t)off.size()}, torch::kInt64);

@@ -46,6 +46,8 @@ void register_default_flags() {
   f.define("enable_force_hbm_recyle", "false", "release HBM pool at EndPass");
   f.define("enable_force_mem_recyle", "false", "force host memory release / disable slot pool");
   f.define("padbox_max_keys_per_batch", "0", "override engine key capacity (0 = auto)");
+  f.define("padbox_device_pass", "true", "keep the pass's record store in HBM and assemble batches on the GPU");
+  f.define("padbox_device_pass_max_gb", "64", "largest pass (GB of HBM) kept device-resident");
 }
 
 }  // namespace pbx

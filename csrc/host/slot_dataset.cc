@@ -104,6 +104,7 @@ void SlotDataset::set_slots(const std::vector<SlotDesc>& slots) {
   }
   dense_width_ = col;
   store_.reset(nu, nf);
+  ++version_;
 }
 
 std::vector<std::string> SlotDataset::sparse_slot_names() const {
@@ -400,6 +401,7 @@ int64_t SlotDataset::load_into_memory() {
   st.reset(store_.nu, store_.nf);
   load_files(files_, &st);
   store_.append(st);
+  ++version_;
   order_.resize(store_.nrec());
   std::iota(order_.begin(), order_.end(), 0);
   return store_.nrec();
@@ -415,6 +417,7 @@ void SlotDataset::preload_into_memory() {
 int64_t SlotDataset::wait_preload_done() {
   if (preload_ && preload_->joinable()) preload_->join();
   store_.append(preload_store_);
+  ++version_;
   preload_store_.reset(store_.nu, store_.nf);
   order_.resize(store_.nrec());
   std::iota(order_.begin(), order_.end(), 0);
@@ -426,6 +429,7 @@ int64_t SlotDataset::add_lines(const std::vector<std::string>& lines) {
   for (auto& l : lines) {
     if (parse_line(l.data(), l.size(), &store_)) ++ok; else ++bad_lines_;
   }
+  ++version_;
   order_.resize(store_.nrec());
   std::iota(order_.begin(), order_.end(), 0);
   return ok;
@@ -433,6 +437,7 @@ int64_t SlotDataset::add_lines(const std::vector<std::string>& lines) {
 
 void SlotDataset::release_memory() {
   store_.reset(store_.nu, store_.nf);
+  ++version_;
   order_.clear();
   store_.u64.shrink_to_fit();
   store_.f32.shrink_to_fit();
@@ -504,64 +509,71 @@ void SlotDataset::build_batch_impl(int64_t begin, int64_t count, const std::func
   // record-major passes: every record's slots are contiguous in the store, so
   // each record is read once, sequentially (a slot-major walk would stride
   // over every record once per slot).  Pass 1 writes per-slot lengths into
-  // the lod rows; a prefix over (slot, record) turns them into offsets; pass
-  // 2 copies each record's keys to its slot-major positions.
-  pool.parallel_range(B, [&](int, int64_t bb, int64_t be) {
+  // the lod rows and per-chunk slot totals; a tiny serial scan over (slot,
+  // chunk) gives every chunk its starting offset per slot; pass 2 (same static
+  // chunks) turns its lengths into offsets, copies each record's keys to its
+  // slot-major positions and fills the dense row.
+  const int T = pool.size();
+  std::vector<int64_t> csum((size_t)T * S, 0);
+  pool.parallel_range(B, [&](int t, int64_t bb, int64_t be) {
+    int64_t* cs = &csum[(size_t)t * S];
     for (int64_t b = bb; b < be; ++b) {
       const int64_t i = order_[begin + b];
       const int64_t* off = &store_.u64_off[i * nu];
       for (int s = 0; s < S; ++s) {
         const int j = sparse_slots_[s];
-        lod[(int64_t)s * (B + 1) + b] = off[j + 1] - off[j];
+        const int64_t n = off[j + 1] - off[j];
+        lod[(int64_t)s * (B + 1) + b] = n;
+        cs[s] += n;
       }
     }
   });
   int64_t k = 0;
   for (int s = 0; s < S; ++s) {
-    int64_t* l = lod + (int64_t)s * (B + 1);
-    for (int b = 0; b < B; ++b) {
-      const int64_t n = l[b];
-      l[b] = k;
+    for (int t = 0; t < T; ++t) {
+      const int64_t n = csum[(size_t)t * S + s];
+      csum[(size_t)t * S + s] = k;
       k += n;
     }
-    l[B] = k;
+    lod[(int64_t)s * (B + 1) + B] = k;
   }
   int64_t* keys = keys_for(k);
-  pool.parallel_range(B, [&](int, int64_t bb, int64_t be) {
+  const bool do_dense = dense && dense_width_ > 0;
+  pool.parallel_range(B, [&](int t, int64_t bb, int64_t be) {
+    int64_t* run = &csum[(size_t)t * S];
     for (int64_t b = bb; b < be; ++b) {
       const int64_t i = order_[begin + b];
       const int64_t* off = &store_.u64_off[i * nu];
       for (int s = 0; s < S; ++s) {
         const int j = sparse_slots_[s];
-        int64_t* dst = keys + lod[(int64_t)s * (B + 1) + b];
-        for (int64_t e = off[j]; e < off[j + 1]; ++e) *dst++ = (int64_t)store_.u64[e];
+        int64_t& l = lod[(int64_t)s * (B + 1) + b];
+        const int64_t n = l;
+        l = run[s];
+        int64_t* dst = keys + run[s];
+        const uint64_t* src = store_.u64.data() + off[j];
+        for (int64_t e = 0; e < n; ++e) dst[e] = (int64_t)src[e];
+        run[s] += n;
+      }
+      if (!do_dense) continue;
+      float* row = dense + b * dense_width_;
+      for (const auto& d : dense_refs_) {
+        int64_t e0, e1;
+        if (d.type == 'u') {
+          e0 = store_.u64_off[i * nu + d.idx];
+          e1 = store_.u64_off[i * nu + d.idx + 1];
+        } else {
+          e0 = store_.f32_off[i * nf + d.idx];
+          e1 = store_.f32_off[i * nf + d.idx + 1];
+        }
+        for (int c = 0; c < d.dim; ++c) {
+          const int64_t e = e0 + c;
+          float v = 0.f;
+          if (e < e1) v = d.type == 'u' ? (float)store_.u64[e] : store_.f32[e];
+          row[d.col + c] = v;
+        }
       }
     }
   });
-  if (dense && dense_width_ > 0) {
-    pool.parallel_range(B, [&](int, int64_t bb, int64_t be) {
-      for (int64_t b = bb; b < be; ++b) {
-        const int64_t i = order_[begin + b];
-        float* row = dense + b * dense_width_;
-        for (const auto& d : dense_refs_) {
-          int64_t e0, e1;
-          if (d.type == 'u') {
-            e0 = store_.u64_off[i * nu + d.idx];
-            e1 = store_.u64_off[i * nu + d.idx + 1];
-          } else {
-            e0 = store_.f32_off[i * nf + d.idx];
-            e1 = store_.f32_off[i * nf + d.idx + 1];
-          }
-          for (int c = 0; c < d.dim; ++c) {
-            const int64_t e = e0 + c;
-            float v = 0.f;
-            if (e < e1) v = d.type == 'u' ? (float)store_.u64[e] : store_.f32[e];
-            row[d.col + c] = v;
-          }
-        }
-      }
-    });
-  }
 }
 
 int64_t SlotDataset::build_batch_staged(int64_t begin, int64_t count, int64_t* keys, int64_t keys_cap, int64_t* lod,
@@ -594,6 +606,17 @@ int64_t SlotDataset::build_batch_staged(int64_t begin, int64_t count, int64_t* k
   std::memcpy(lod, sl.data(), nl * sizeof(int64_t));
   if (nd) std::memcpy(dense, sd.data(), nd * sizeof(float));
   return L;
+}
+
+std::vector<int32_t> SlotDataset::dense_refs() const {
+  std::vector<int32_t> out;
+  for (const auto& d : dense_refs_) {
+    out.push_back(d.type == 'u' ? 0 : 1);
+    out.push_back(d.idx);
+    out.push_back(d.dim);
+    out.push_back(d.col);
+  }
+  return out;
 }
 
 void SlotDataset::build_rank_offset(int64_t begin, int64_t count, int max_rank, int32_t* out) const {
@@ -699,6 +722,7 @@ int64_t SlotDataset::load_archive(const std::string& path, bool append) {
   if (!ok) throw std::runtime_error("truncated archive: " + path);
   if (!append) store_.reset(store_.nu, store_.nf);
   store_.append(st);
+  ++version_;
   order_.resize(store_.nrec());
   std::iota(order_.begin(), order_.end(), 0);
   return st.nrec();

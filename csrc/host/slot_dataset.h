@@ -76,7 +76,13 @@ class SlotDataset {
 
   int64_t size() const { return store_.nrec(); }
   const RecordStore& store() const { return store_; }
-  RecordStore& mutable_store() { return store_; }
+  // any non-const access may change the records: bump the store version the
+  // device-resident pass copy (data/device_pass.py) is keyed on
+  RecordStore& mutable_store() {
+    ++version_;
+    return store_;
+  }
+  uint64_t version() const { return version_; }
 
   // feed-pass keys: every feasign of sparse uint64 slots (optionally unique)
   std::vector<uint64_t> collect_keys(bool unique) const;
@@ -126,6 +132,9 @@ class SlotDataset {
   const std::vector<int>& sparse_slot_u64_index() const { return sparse_slots_; }
   std::vector<std::string> dense_slot_names() const;
   std::vector<int> dense_slot_dims() const;
+  // dense slot sources as rows (type 0 = uint64 / 1 = float, used-slot idx,
+  // width, first column) for the on-device batch builder
+  std::vector<int32_t> dense_refs() const;
 
   // binary archive ("load into disk" mode)
   void save_archive(const std::string& path) const;
@@ -159,6 +168,7 @@ class SlotDataset {
   std::unique_ptr<std::thread> preload_;
   RecordStore preload_store_;
   int64_t bad_lines_ = 0;
+  uint64_t version_ = 0;
 };
 
 }  // namespace pbx

@@ -4,7 +4,8 @@
     x0 = data_norm(x)                      fused head kernel (FM off), bf16,
                                            written into the MLP workspace
     cross:  x_{l+1} = x0 * (W_l x_l + b_l) + x_l      L full-rank layers,
-            fp32 state, bf16 MFMA GEMMs
+            fp32 state, bf16 MFMA GEMMs with the cross update fused in
+            the epilogue (CrossWorkspace, csrc/hip/bindings_cross.cpp)
     deep:   FusedMLP hidden -> 1           MFMA GEMMs, bias+ReLU fused
     logit = deep + w_c . x_L  -> fused sigmoid + logloss
 
@@ -20,15 +21,48 @@ from typing import Sequence
 import torch
 from torch import nn
 
+from .. import _native
 from ..ops.ctr import DataNorm, ctr_head, logit_logloss
-from ..ops.mlp import FusedMLP, pad8
+from ..ops.mlp import FusedMLP, _ensure_grad, pad8
 from ..ops.sparse import pull_seqpool_cvm_concat
 from ..ps.sparse_engine import SeqpoolParams, SparseEngine
+
+
+class _CrossHipFn(torch.autograd.Function):
+    """s = x_L . w_c over the cross stack on the GPU.  x0 is the MLP's bf16
+    input buffer [M, ldx0]; parameter gradients accumulate straight into
+    ``p.grad`` (dense-arena views); returns d(loss)/d(x0) as bf16 [M, ldx0]."""
+
+    @staticmethod
+    def forward(ctx, y, mod, w_c, *params):
+        xw = mod.workspace(y)
+        s = xw.forward(y, [w.detach() for w in mod.w], [b.detach() for b in mod.b], w_c.detach())
+        ctx.mod, ctx.y, ctx.w_c = mod, y, w_c
+        ctx.n_params = len(params)
+        return s
+
+    @staticmethod
+    def backward(ctx, ds):
+        mod = ctx.mod
+        dy = mod._xw.backward(ctx.y, ds.float().contiguous(), [_ensure_grad(w) for w in mod.w],
+                              [_ensure_grad(b) for b in mod.b], ctx.w_c.detach(), _ensure_grad(ctx.w_c))
+        return (dy, None, None) + (None,) * ctx.n_params
+
+
+def cross_logit(y: torch.Tensor, cross: "CrossNetV2", w_c: torch.Tensor) -> torch.Tensor:
+    """[M] = CrossNetV2(y[:, :C]) . w_c -- the HIP cross stack on a GPU
+    (y: the bf16 MLP input buffer), fp32 torch on the CPU."""
+    C = w_c.numel()
+    if y.is_cuda:
+        return _CrossHipFn.apply(y, cross, w_c, *cross.parameters(), w_c)
+    return cross(y[:, :C].float()) @ w_c
 
 
 class CrossNetV2(nn.Module):
     def __init__(self, dim: int, layers: int = 3):
         super().__init__()
+        self.dim = dim
+        self._xw = None
         self.w = nn.ParameterList()
         self.b = nn.ParameterList()
         for _ in range(layers):
@@ -37,16 +71,18 @@ class CrossNetV2(nn.Module):
             self.w.append(nn.Parameter(w * 0.1))
             self.b.append(nn.Parameter(torch.zeros(dim)))
 
+    def workspace(self, y: torch.Tensor):
+        M, ld = int(y.shape[0]), int(y.shape[1])
+        if self._xw is None or self._xw_key != (M, ld, y.device):
+            self._xw = _native.hip().CrossWorkspace(M, self.dim, len(self.w), ld, y.device.index or 0, 512)
+            self._xw_key = (M, ld, y.device)
+        return self._xw
+
     def forward(self, x0: torch.Tensor) -> torch.Tensor:
+        """fp32 reference stack (CPU path and the GPU kernels' oracle)."""
         x = x0
-        gpu = x0.is_cuda
         for w, b in zip(self.w, self.b):
-            if gpu:  # bf16 MFMA GEMM, fp32 accumulate / state
-                z = torch.nn.functional.linear(x.to(torch.bfloat16), w.to(torch.bfloat16), b.to(torch.bfloat16))
-                z = z.float()
-            else:
-                z = torch.nn.functional.linear(x, w, b)
-            x = x0 * z + x
+            x = x0 * torch.nn.functional.linear(x, w, b) + x
         return x
 
 
@@ -78,5 +114,4 @@ class DCNv2(nn.Module):
         else:
             y, _ = ctr_head(x, self.dn, S, self.Eo, self.ew_col, 0, self.Cp)
             deep = self.mlp(y)
-        xl = self.cross(y[:, : self.C].float())
-        return logit_logloss(deep, xl @ self.w_c, batch.label)
+        return logit_logloss(deep, cross_logit(y, self.cross, self.w_c), batch.label)

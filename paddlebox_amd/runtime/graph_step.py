@@ -128,6 +128,16 @@ class GraphedTrainStep:
                     getattr(dst, f).copy_(getattr(host_batch, f), non_blocking=True)
             self.ready[i].record(self.copy_stream)
 
+    def fill(self, i: int, fn: Callable[[Any], None], stream=None):
+        """Produce buffer set i on the device: ``fn(buf)`` enqueues kernels
+        that write it (on ``stream``, default the copy stream) once the
+        replay that last read it has finished."""
+        st = stream if stream is not None else self.copy_stream
+        st.wait_event(self.free[i])
+        with torch.cuda.stream(st):
+            fn(self.bufs[i])
+        self.ready[i].record(st)
+
     def run(self, i: int):
         cur = torch.cuda.current_stream(self.device)
         slot = self.step_no % self.max_inflight

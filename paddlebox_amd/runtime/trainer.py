@@ -57,6 +57,8 @@ class _GraphBatch:
     dense: torch.Tensor
 
 
+R_HOST = 4  # pinned host batches per size in flight (host-assembly path)
+
 # sync_dense_mode (boxps_worker.cc:393-395,1191-1258)
 SYNC_NONE = 0
 SYNC_KSTEP_NODE = 1
@@ -263,12 +265,19 @@ class BoxPSWorker:
             if box is not None and box.metrics.metrics:
                 box.metrics.add_batch(_FetchView(*out))
 
+        from ..data.device_pass import device_pass_for
+
+        dp = device_pass_for(ds, dev)
+        if dp is not None:
+            return self._train_device_pass(dp, plan, Lcap, cache, graph_B, S, Dw, slot_batch, step_fn_for, metrics)
         graphs, warm, rings, nused = {}, {}, {}, {}
         for B, (cL, g, rg) in cache.items():
             if B in graph_B and cL >= Lcap:
                 graphs[B], rings[B], nused[B] = g, rg, 0
+                if rg is None:  # captured by the device-pass path: no host ring yet
+                    rings[B] = [host_buf(B) for _ in range(R_HOST)]
         Lcap = max([Lcap] + [cache[B][0] for B in graphs])
-        R = 4  # pinned host batches per size in flight
+        R = R_HOST  # pinned host batches per size in flight
         # the pass's batch assembly runs on a native thread (csrc/host/
         # batch_assembler.cc) into pinned buffers; ring slots are handed back
         # once their H2D has completed
@@ -353,6 +362,71 @@ class BoxPSWorker:
         return {"batches": self.batches, "instances": n_ins, "seconds": el,
                 "ins_per_sec": n_ins / el if el > 0 else 0.0, "graph_replays": replays,
                 "graph_sizes": sorted(graphs), **self.timers}
+
+    def _train_device_pass(self, dp, plan, Lcap, cache, graph_B, S, Dw, slot_batch, step_fn_for, metrics):
+        """The graphed TrainFiles over a device-resident pass
+        (data/device_pass.py): every batch is assembled by the batch kernels
+        on the pass stream straight into the replay's input buffers, so the
+        host loop per batch is two launches + one graph replay."""
+        from .graph_step import GraphedTrainStep, pack_batch
+
+        s, dev = self.s, self.s.device
+
+        def dev_buf(B):
+            return pack_batch(_GraphBatch(torch.empty(Lcap, dtype=torch.int64), torch.empty(S * (B + 1), dtype=torch.int64),
+                                          torch.empty(B, Dw, dtype=torch.float32)), device=dev)
+
+        graphs, warm, nused = {}, {}, {}
+        for B, (cL, g, _rg) in cache.items():
+            if B in graph_B and cL >= Lcap:
+                graphs[B], nused[B] = g, 0
+        Lcap = max([Lcap] + [cache[B][0] for B in graphs])
+        t0 = time.time()
+        n_ins = replays = 0
+        for (b0, c) in plan:
+            t_s = time.time()
+            if c in graphs:
+                g = graphs[c]
+                j = nused[c] % g.n
+                nused[c] += 1
+                g.fill(j, lambda buf, b0=b0, c=c: dp.assemble(b0, c, buf.keys, buf.lod, buf.dense), dp.stream)
+                metrics(g.run(j))
+                replays += 1
+            else:
+                db = dev_buf(c)
+                dp.assemble_sync(b0, c, db.keys, db.lod, db.dense)
+                if c in graph_B:
+                    warm.setdefault(c, []).append(db)
+                    if len(warm[c]) == 2:
+                        g = GraphedTrainStep(step_fn_for(c, db.lod.cpu()), warm[c][0], dev, warmup=0,
+                                             warm_batches=warm[c], on_warm=metrics)
+                        graphs[c], nused[c] = g, 0
+                        cache[c] = (Lcap, g, None)
+                        del warm[c]
+                else:
+                    bt = slot_batch(db.keys, db.lod, db.dense, c, db.lod.cpu())
+                    ctx = ExecContext(s, bt, training=True)
+                    s.feed_batch(ctx, bt)
+                    s.step(ctx)
+                    metrics((ctx, bt))
+            self.timers["step"] += time.time() - t_s
+            self.batches += 1
+            n_ins += c
+        # a size seen once (its single warm batch) never captured: run it eagerly
+        for c, dbs in warm.items():
+            for db in dbs:
+                bt = slot_batch(db.keys, db.lod, db.dense, c, db.lod.cpu())
+                ctx = ExecContext(s, bt, training=True)
+                s.feed_batch(ctx, bt)
+                s.step(ctx)
+                metrics((ctx, bt))
+        torch.cuda.synchronize(dev)
+        if dp.overflowed():
+            raise RuntimeError("device batch assembly: a batch had more keys than the captured key buffer")
+        el = time.time() - t0
+        return {"batches": self.batches, "instances": n_ins, "seconds": el,
+                "ins_per_sec": n_ins / el if el > 0 else 0.0, "graph_replays": replays,
+                "graph_sizes": sorted(graphs), "device_pass": True, **self.timers}
 
     def _train_files_eager(self) -> Dict[str, float]:
         t = self.t

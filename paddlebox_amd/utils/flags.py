@@ -47,6 +47,8 @@ _DEFAULTS: Dict[str, str] = {
     "enable_force_hbm_recyle": "false",
     "enable_force_mem_recyle": "false",
     "padbox_max_keys_per_batch": "0",
+    "padbox_device_pass": "true",
+    "padbox_device_pass_max_gb": "64",
 }
 _py: Dict[str, str] = {k: os.environ.get("FLAGS_" + k, v) for k, v in _DEFAULTS.items()}
 

@@ -9,6 +9,7 @@ import torch
 
 import paddlebox_amd.fluid as fluid
 from paddlebox_amd.ps.box_wrapper import BoxWrapper
+from paddlebox_amd.utils.flags import set_flags
 from tests.test_fluid import DENSE, S, _build, _files
 
 pytestmark = pytest.mark.gpu
@@ -21,8 +22,9 @@ def _box():
     return b
 
 
-def _run(tmp_path, graph: bool, passes: int = 3):
+def _run(tmp_path, graph: bool, passes: int = 3, device_pass: bool = True):
     tmp_path.mkdir(parents=True, exist_ok=True)
+    set_flags({"FLAGS_padbox_device_pass": device_pass})
     box = _box()
     try:
         scope = fluid.Scope()
@@ -52,6 +54,7 @@ def _run(tmp_path, graph: bool, passes: int = 3):
               for n in ("batch_size", "batch_sum", "batch_square_sum")}
         return dict(stats=all_stats, w0=w0, w1=w1, auc=msg[0], n=msg[7], table=v[o].cpu(), dn=dn)
     finally:
+        set_flags({"FLAGS_padbox_device_pass": True})
         BoxWrapper._instance = None
 
 
@@ -61,16 +64,20 @@ def test_train_from_dataset_gpu_eager_and_graph(tmp_path):
     assert st["batches"] == 10 and st["instances"] == 640
     assert not np.allclose(eager["w0"], eager["w1"])
     assert eager["n"] == 3 * 640 and eager["auc"] > 0.55
-    graphed = _run(tmp_path / "g", graph=True)
-    gst = graphed["stats"][-1]
-    assert gst["batches"] == 10 and gst.get("graph_replays", 0) > 0
-    # same data, same order, same init: the captured step trains the same model
-    # (up to float atomics in the sparse push / column reductions, which Adam's
-    # normalised steps amplify on near-zero gradients over 30 steps)
-    np.testing.assert_allclose(graphed["w1"], eager["w1"], rtol=0, atol=5e-3)
-    keep = [c for c in range(eager["table"].shape[1]) if c != 14]  # "slot" field: last occurrence, racy
-    torch.testing.assert_close(graphed["table"][:, keep], eager["table"][:, keep], rtol=1e-2, atol=5e-3)
-    assert abs(graphed["auc"] - eager["auc"]) < 0.01
+    # graphed step fed by the device-resident pass (batches assembled on the
+    # GPU) and by the native host assembler thread (pinned ring + H2D)
+    for tag, dpass in (("g", True), ("h", False)):
+        graphed = _run(tmp_path / tag, graph=True, device_pass=dpass)
+        gst = graphed["stats"][-1]
+        assert gst["batches"] == 10 and gst.get("graph_replays", 0) > 0
+        assert bool(gst.get("device_pass", False)) == dpass
+        # same data, same order, same init: the captured step trains the same
+        # model (up to float atomics in the sparse push / column reductions,
+        # which Adam's normalised steps amplify on near-zero gradients)
+        np.testing.assert_allclose(graphed["w1"], eager["w1"], rtol=0, atol=5e-3)
+        keep = [c for c in range(eager["table"].shape[1]) if c != 14]  # "slot" field: last occurrence, racy
+        torch.testing.assert_close(graphed["table"][:, keep], eager["table"][:, keep], rtol=1e-2, atol=5e-3)
+        assert abs(graphed["auc"] - eager["auc"]) < 0.01
 
 
 def test_tower_lowering_matches_unfused_program(tmp_path):
