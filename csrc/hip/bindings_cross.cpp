@@ -1,7 +1,7 @@
-// CrossWorkspace: DCN-V2 cross network on the hand-written MFMA GEMM
-// (gemm.hip EPI_CROSS_* epilogues + cross.hip).  Persistent padded buffers,
-// all shapes checked here; the forward is L GEMMs + 1 dot, the backward
-// 1 top kernel + 3 launches per layer (dW GEMM, slab reduce, dX GEMM).
+// CrossWorkspace: DCN-V2 cross network on the LDS-DMA MFMA engine (mlp.hip,
+// MLP_EPI_CROSS_* epilogues) + cross.hip.  Persistent padded buffers, all
+// shapes checked here; forward = 1 weight cast + L GEMMs + 1 dot, backward =
+// top kernel + colsum + 2 GEMMs per layer (dW with fused db, dX).
 #include <ATen/hip/HIPContext.h>
 #include <torch/extension.h>
 
@@ -25,169 +25,184 @@ hipStream_t xs() { return at::hip::getCurrentHIPStream().stream(); }
 unsigned short* bp(const Tensor& t) { return reinterpret_cast<unsigned short*>(t.data_ptr()); }
 float* fp(const Tensor& t) { return reinterpret_cast<float*>(t.data_ptr()); }
 
+// Layout (matches the MlpWorkspace whose input it shares): D = the MLP input
+// width (multiple of 8), ld = pad64(D), ldM = pad64(M).
+//   x0 = MLP X_0 [M][ld] bf16, x0^T = MLP X_0^T [pad64(D+1)][ldM] (ones row D)
+//   W_l, W_l^T bf16 [ld][ld] (cast from the fp32 masters [D][D] every step)
+//   x_{l+1}: f32 [M][ld], bf16 [M][ld] + bf16^T [pad64(D+1)][ldM] (l+1 < L)
+//   z_l f32; backward g (f32) / u (bf16 + u^T) ping-pong pairs, acc f32
 class CrossWorkspace {
  public:
-  CrossWorkspace(int64_t M, int64_t C, int64_t L, int64_t ldx0, int device, int64_t k_split)
-      : M_(M), C_(C), L_(L), ldx0_(ldx0), ks_(k_split) {
-    CR_CHECK(M > 0 && C > 0 && L >= 1 && L <= kMaxMlpLayers, "bad shape");
-    CR_CHECK(ldx0 >= C && ldx0 % 8 == 0, "x0 row stride must be >= C and a multiple of 8");
+  CrossWorkspace(int64_t M, int64_t D, int64_t L, int device, int64_t k_split)
+      : M_(M), D_(D), L_(L), ks_(k_split) {
+    CR_CHECK(M > 0 && D > 0 && D % 8 == 0 && L >= 1 && L <= kMaxMlpLayers, "bad shape");
     CR_CHECK(k_split > 0 && k_split % 64 == 0, "k_split must be a positive multiple of 64");
-    Cp_ = (C + 7) / 8 * 8;
+    ld_ = p64(D);
+    ldM_ = p64(M);
     auto ob = torch::TensorOptions().dtype(torch::kBFloat16).device(torch::kCUDA, device);
     auto of = torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device);
     for (int l = 0; l < L; ++l) {
-      wb_.push_back(torch::zeros({Cp_, Cp_}, ob));
-      wtb_.push_back(torch::zeros({Cp_, Cp_}, ob));
-      xf_.push_back(torch::zeros({M, Cp_}, of));
-      xb_.push_back(torch::zeros({M, Cp_}, ob));
-      z_.push_back(torch::zeros({M, Cp_}, of));
+      wb_.push_back(torch::zeros({ld_, ld_}, ob));
+      wtb_.push_back(torch::zeros({ld_, ld_}, ob));
+      xf_.push_back(torch::zeros({M, ld_}, of));
+      z_.push_back(torch::zeros({M, ld_}, of));
+      if (l + 1 < L) {
+        xb_.push_back(torch::zeros({M, ld_}, ob));
+        auto t = torch::zeros({p64(D + 1), ldM_}, ob);
+        t[D].narrow(0, 0, M).fill_(1.0);  // bias ones row
+        xt_.push_back(t);
+      }
     }
     for (int i = 0; i < 2; ++i) {
-      g_.push_back(torch::zeros({M, Cp_}, of));
-      u_.push_back(torch::zeros({M, Cp_}, ob));
+      g_.push_back(torch::zeros({M, ld_}, of));
+      u_.push_back(torch::zeros({M, ld_}, ob));
+      ut_.push_back(torch::zeros({ld_, ldM_}, ob));
     }
-    acc_ = torch::zeros({M, Cp_}, of);
-    dy_ = torch::zeros({M, ldx0}, ob);
+    acc_ = torch::zeros({M, ld_}, of);
+    dy_ = torch::zeros({M, ld_}, ob);
     s_ = torch::zeros({M}, of);
-    splits_ = (M + k_split - 1) / k_split;
-    slab_ = torch::zeros({splits_, C, C + 1}, of);
-    part_ = torch::zeros({cross_top_blocks((int)M), C}, of);
+    part_ = torch::zeros({cross_top_blocks((int)M), D}, of);
   }
+  static int64_t p64(int64_t v) { return (v + 63) / 64 * 64; }
 
   Tensor forward(const Tensor& y, const std::vector<Tensor>& W, const std::vector<Tensor>& b, const Tensor& wc) {
     check_x0(y);
     CR_CHECK((int64_t)W.size() == L_ && (int64_t)b.size() == L_, "layer count");
-    CR_CHECK(wc.is_cuda() && wc.numel() == C_ && wc.scalar_type() == torch::kFloat32, "w_c");
+    CR_CHECK(wc.is_cuda() && wc.numel() == D_ && wc.scalar_type() == torch::kFloat32 && wc.is_contiguous(), "w_c");
     auto s = xs();
     CastWtBatch cb;
     cb.n = (int)L_;
     cb.tile_off[0] = 0;
     for (int l = 0; l < L_; ++l) {
       CR_CHECK(W[l].is_cuda() && W[l].is_contiguous() && W[l].scalar_type() == torch::kFloat32 &&
-                   W[l].size(0) == C_ && W[l].size(1) == C_,
-               "W must be contiguous f32 [C, C]");
-      CR_CHECK(b[l].is_cuda() && b[l].numel() == C_ && b[l].scalar_type() == torch::kFloat32, "b must be f32 [C]");
+                   W[l].size(0) == D_ && W[l].size(1) == D_,
+               "W must be contiguous f32 [D, D]");
+      CR_CHECK(b[l].is_cuda() && b[l].numel() == D_ && b[l].scalar_type() == torch::kFloat32 && b[l].is_contiguous(),
+               "b must be f32 [D]");
       cb.w[l] = fp(W[l]);
       cb.wb[l] = bp(wb_[l]);
       cb.wtb[l] = bp(wtb_[l]);
-      cb.N[l] = cb.K[l] = (int)C_;
-      cb.pN[l] = cb.pK[l] = (int)Cp_;
-      const int t = (int)((Cp_ + 31) / 32);
-      cb.tile_off[l + 1] = cb.tile_off[l] + t * t;
+      cb.N[l] = cb.K[l] = (int)D_;
+      cb.pN[l] = cb.pK[l] = (int)ld_;
+      cb.tile_off[l + 1] = cb.tile_off[l] + (int)((ld_ / 32) * (ld_ / 32));
     }
     launch_cast_wt(cb, s);
     for (int l = 0; l < L_; ++l) {
-      GemmArgs g;
+      const bool last = l + 1 == L_;
+      MlpGemmArgs g;
       g.A = l == 0 ? bp(y) : bp(xb_[l - 1]);
-      g.lda = l == 0 ? (int)ldx0_ : (int)Cp_;
+      g.lda = (int)ld_;
       g.B = bp(wb_[l]);
-      g.ldb = (int)Cp_;
+      g.ldb = (int)ld_;
       g.M = (int)M_;
-      g.N = (int)C_;
-      g.K = (int)C_;
-      g.C = fp(xf_[l]);
-      g.ldc = (int)Cp_;
+      g.N = (int)ld_;
+      g.K = (int)ld_;
+      g.C = last ? nullptr : bp(xb_[l]);
+      g.ldc = (int)ld_;
+      g.CT = last ? nullptr : bp(xt_[l]);
+      g.ldct = (int)ldM_;
+      g.ncols_valid = (int)D_;
       g.bias = fp(b[l]);
-      g.epi = EPI_CROSS_FWD;
       g.x0 = bp(y);
-      g.ldx0 = (int)ldx0_;
+      g.ldx0 = (int)ld_;
       g.xin = l == 0 ? nullptr : fp(xf_[l - 1]);
-      g.out2 = fp(z_[l]);
-      g.outb = l + 1 < L_ ? bp(xb_[l]) : nullptr;
-      launch_gemm(g, s);
+      g.fout = fp(xf_[l]);
+      g.zout = fp(z_[l]);
+      g.ldf = (int)ld_;
+      launch_mlp_gemm(g, MLP_EPI_CROSS_FWD, s);
     }
-    launch_cross_dot(fp(xf_[L_ - 1]), (int)M_, (int)C_, (int)Cp_, fp(wc), fp(s_), s);
+    launch_cross_dot(fp(xf_[L_ - 1]), (int)M_, (int)D_, (int)ld_, fp(wc), fp(s_), s);
     return s_;
   }
 
   // grads accumulate into dW[l] / db[l] / dwc (dense-arena views); returns
-  // d(loss)/d(x0) as bf16 [M, ldx0] (pad columns zero)
-  Tensor backward(const Tensor& y, const Tensor& ds, const std::vector<Tensor>& dW, const std::vector<Tensor>& db,
-                  const Tensor& wc, const Tensor& dwc) {
+  // d(loss)/d(x0) as bf16 [M, ld] (pad columns zero)
+  Tensor backward(const Tensor& y, const Tensor& yt, const Tensor& ds, const std::vector<Tensor>& dW,
+                  const std::vector<Tensor>& db, const Tensor& wc, const Tensor& dwc) {
     check_x0(y);
+    CR_CHECK(yt.is_cuda() && yt.scalar_type() == torch::kBFloat16 && yt.is_contiguous() && yt.dim() == 2 &&
+                 yt.size(0) >= D_ + 1 && yt.size(1) == ldM_,
+             "x0^T must be the MLP's bf16 [pad64(D+1), pad64(M)] transposed input");
     CR_CHECK(ds.is_cuda() && ds.numel() == M_ && ds.scalar_type() == torch::kFloat32 && ds.is_contiguous(), "ds");
     CR_CHECK((int64_t)dW.size() == L_ && (int64_t)db.size() == L_, "grad count");
     for (int l = 0; l < L_; ++l) {
-      CR_CHECK(dW[l].is_cuda() && dW[l].is_contiguous() && dW[l].numel() == C_ * C_ &&
+      CR_CHECK(dW[l].is_cuda() && dW[l].is_contiguous() && dW[l].numel() == D_ * D_ &&
                    dW[l].scalar_type() == torch::kFloat32,
-               "dW must be contiguous f32 [C, C]");
-      CR_CHECK(db[l].is_cuda() && db[l].is_contiguous() && db[l].numel() == C_ && db[l].scalar_type() == torch::kFloat32,
+               "dW must be contiguous f32 [D, D]");
+      CR_CHECK(db[l].is_cuda() && db[l].is_contiguous() && db[l].numel() == D_ && db[l].scalar_type() == torch::kFloat32,
                "db");
     }
-    CR_CHECK(dwc.is_cuda() && dwc.numel() == C_ && dwc.scalar_type() == torch::kFloat32 && dwc.is_contiguous(), "dwc");
+    CR_CHECK(wc.is_cuda() && wc.numel() == D_ && wc.is_contiguous(), "w_c");
+    CR_CHECK(dwc.is_cuda() && dwc.numel() == D_ && dwc.scalar_type() == torch::kFloat32 && dwc.is_contiguous(), "dwc");
     auto s = xs();
-    int cur = 0;  // g_/u_ ping-pong index holding g_{l+1}, u_l
-    launch_cross_top_bwd(fp(xf_[L_ - 1]), bp(y), (int)ldx0_, fp(z_[L_ - 1]), fp(wc), fp(ds), (int)M_, (int)C_,
-                         (int)Cp_, fp(g_[cur]), bp(u_[cur]), fp(acc_), fp(part_), fp(dwc), s);
+    int cur = 0;  // ping-pong index holding g_{l+1}, u_l, u_l^T
+    launch_cross_top_bwd(fp(xf_[L_ - 1]), bp(y), fp(z_[L_ - 1]), fp(wc), fp(ds), (int)M_, (int)D_, (int)ld_,
+                         fp(g_[cur]), bp(u_[cur]), bp(ut_[cur]), (int)ldM_, fp(acc_), fp(part_), fp(dwc), s);
     for (int l = (int)L_ - 1; l >= 0; --l) {
-      // dW_l = u_l^T x_l, db_l = colsum(u_l) (virtual ones column), split-K over the batch
-      GemmArgs w;
-      w.A = bp(u_[cur]);
-      w.lda = (int)Cp_;
-      w.a_kcontig = false;
-      w.B = l == 0 ? bp(y) : bp(xb_[l - 1]);
-      w.ldb = l == 0 ? (int)ldx0_ : (int)Cp_;
-      w.b_kcontig = false;
-      w.M = (int)C_;
-      w.N = (int)C_;
-      w.K = (int)M_;
-      w.ones_col_b = (int)C_;
-      w.C = fp(slab_);
-      w.ldc = (int)C_ + 1;
-      w.epi = EPI_F32_SLAB;
+      MlpGemmArgs w;  // dW_l += u_l^T [x_l | 1]   (split-K over the batch)
+      w.A = bp(ut_[cur]);
+      w.lda = (int)ldM_;
+      w.B = l == 0 ? bp(yt) : bp(xt_[l - 1]);
+      w.ldb = (int)ldM_;
+      w.M = (int)D_;
+      w.N = (int)D_ + 1;
+      w.K = (int)ldM_;
       w.k_per_split = (int)ks_;
-      w.slab_stride = C_ * (C_ + 1);
-      launch_gemm(w, s);
-      launch_slab_reduce(fp(slab_), (int)splits_, C_ * (C_ + 1), (int)C_, (int)C_, (int)C_ + 1, fp(dW[l]), fp(db[l]),
-                         1.f, s);
-      // g_l = u_l W_l + g_{l+1}
-      GemmArgs d;
+      w.dW = fp(dW[l]);
+      w.lddw = (int)D_;
+      w.db = fp(db[l]);
+      w.ncols_valid = (int)D_;
+      w.nrows_valid = (int)D_;
+      launch_mlp_gemm(w, MLP_EPI_DW, s);
+      MlpGemmArgs d;  // g_l = u_l W_l + g_{l+1}
       d.A = bp(u_[cur]);
-      d.lda = (int)Cp_;
+      d.lda = (int)ld_;
       d.B = bp(wtb_[l]);
-      d.ldb = (int)Cp_;
+      d.ldb = (int)ld_;
       d.M = (int)M_;
-      d.N = (int)C_;
-      d.K = (int)C_;
-      d.epi = EPI_CROSS_DX;
-      d.gin = fp(g_[cur]);
+      d.N = (int)ld_;
+      d.K = (int)ld_;
+      d.ncols_valid = (int)D_;
+      d.ldc = (int)ld_;
+      d.ldct = (int)ldM_;
       d.x0 = bp(y);
-      d.ldx0 = (int)ldx0_;
-      d.ldc = (int)Cp_;
-      d.out2 = fp(acc_);
+      d.ldx0 = (int)ld_;
+      d.gin = fp(g_[cur]);
+      d.accum = fp(acc_);
+      d.ldf = (int)ld_;
       if (l > 0) {
-        d.C = fp(g_[cur ^ 1]);
+        d.C = bp(u_[cur ^ 1]);
+        d.CT = bp(ut_[cur ^ 1]);
+        d.fout = fp(g_[cur ^ 1]);
         d.zprev = fp(z_[l - 1]);
-        d.outb = bp(u_[cur ^ 1]);
       } else {
-        d.C = nullptr;
-        d.zprev = nullptr;
-        d.outb = bp(dy_);
+        d.C = bp(dy_);
+        d.CT = nullptr;
       }
-      launch_gemm(d, s);
+      launch_mlp_gemm(d, MLP_EPI_CROSS_DX, s);
       cur ^= 1;
     }
     return dy_;
   }
 
-  Tensor x_out() const { return xf_[L_ - 1].narrow(1, 0, C_); }
+  Tensor x_out() const { return xf_[L_ - 1].narrow(1, 0, D_); }
 
  private:
   void check_x0(const Tensor& y) const {
     CR_CHECK(y.is_cuda() && y.scalar_type() == torch::kBFloat16 && y.is_contiguous() && y.dim() == 2 &&
-                 y.size(0) == M_ && y.size(1) == ldx0_,
-             "x0 must be the contiguous bf16 [M, ldx0] MLP input");
+                 y.size(0) == M_ && y.size(1) == ld_,
+             "x0 must be the MLP's contiguous bf16 [M, pad64(D)] input");
   }
-  int64_t M_, C_, L_, ldx0_, ks_, Cp_ = 0, splits_ = 1;
-  std::vector<Tensor> wb_, wtb_, xf_, xb_, z_, g_, u_;
-  Tensor acc_, dy_, s_, slab_, part_;
+  int64_t M_, D_, L_, ks_, ld_ = 0, ldM_ = 0;
+  std::vector<Tensor> wb_, wtb_, xf_, xb_, xt_, z_, g_, u_, ut_;
+  Tensor acc_, dy_, s_, part_;
 };
 
 }  // namespace
 
 void bind_cross(py::module& m) {
   py::class_<CrossWorkspace>(m, "CrossWorkspace")
-      .def(py::init<int64_t, int64_t, int64_t, int64_t, int, int64_t>())
+      .def(py::init<int64_t, int64_t, int64_t, int, int64_t>())
       .def("forward", &CrossWorkspace::forward)
       .def("backward", &CrossWorkspace::backward)
       .def("x_out", &CrossWorkspace::x_out);

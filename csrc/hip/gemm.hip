@@ -189,8 +189,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   for (int i = 0; i < NACC; ++i) {
     const int n = n0 + wn * 32 * NACC + i * 32 + r;
     if (n >= NB) continue;
-    const float bias =
-        (g.bias && (g.epi == EPI_BIAS_RELU_BF16 || g.epi == EPI_BIAS_BF16 || g.epi == EPI_CROSS_FWD)) ? g.bias[n] : 0.f;
+    const float bias = (g.bias && (g.epi == EPI_BIAS_RELU_BF16 || g.epi == EPI_BIAS_BF16)) ? g.bias[n] : 0.f;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int m = m0 + wm * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hh;
@@ -198,24 +197,6 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
       float v = acc[i][reg] + bias;
       if (g.epi == EPI_F32_SLAB) {
         reinterpret_cast<float*>(g.C)[(int64_t)kz * g.slab_stride + (int64_t)m * g.ldc + n] = v;
-      } else if (g.epi == EPI_CROSS_FWD) {
-        const int64_t o = (int64_t)m * g.ldc + n;
-        const float x0 = __uint_as_float(((unsigned)g.x0[(int64_t)m * g.ldx0 + n]) << 16);
-        const float xn = x0 * v + (g.xin ? g.xin[o] : x0);
-        reinterpret_cast<float*>(g.C)[o] = xn;
-        g.out2[o] = v;
-        if (g.outb) g.outb[o] = f2bf(xn);
-      } else if (g.epi == EPI_CROSS_DX) {
-        const int64_t o = (int64_t)m * g.ldc + n;
-        const float gl = v + g.gin[o];
-        if (g.zprev) {
-          const float x0 = __uint_as_float(((unsigned)g.x0[(int64_t)m * g.ldx0 + n]) << 16);
-          reinterpret_cast<float*>(g.C)[o] = gl;
-          g.outb[o] = f2bf(x0 * gl);
-          g.out2[o] += g.zprev[o] * gl;
-        } else {
-          g.outb[(int64_t)m * g.ldx0 + n] = f2bf(gl + g.out2[o]);
-        }
       } else {
         if (g.epi == EPI_BIAS_RELU_BF16) v = v > 0.f ? v : 0.f;
         reinterpret_cast<unsigned short*>(g.C)[(int64_t)m * g.ldc + n] = f2bf(v);

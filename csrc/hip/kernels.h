@@ -242,19 +242,7 @@ void launch_data_norm_update(float* bsize, float* bsum, float* bsq, const float*
 // bf16 MFMA GEMM for the MLP (csrc/hip/gemm.hip): C[M,N] = A'[M,K] B'[K,N]
 // with A'(m,k) at A[m*lda+k] (a_kcontig) or A[k*lda+m]; B'(k,n) at
 // B[n*ldb+k] (b_kcontig) or B[k*ldb+n].
-enum GemmEpi {
-  EPI_BIAS_RELU_BF16 = 0,
-  EPI_BIAS_BF16 = 1,
-  EPI_BF16 = 2,
-  EPI_F32_SLAB = 3,
-  // DCN-V2 cross layer x_{l+1} = x0 * (x_l W^T + b) + x_l (cross.hip):
-  //   C (f32) = x_{l+1}, out2 = z_l, outb = bf16(x_{l+1}) (nullable)
-  EPI_CROSS_FWD = 4,
-  // cross backward dX: g_l = acc + gin; with zprev: C (f32) = g_l,
-  // outb = bf16(x0 * g_l), out2 += zprev * g_l; without (layer 0):
-  // outb[m*ldx0+n] = bf16(g_l + out2)  (the gradient of x0)
-  EPI_CROSS_DX = 5
-};
+enum GemmEpi { EPI_BIAS_RELU_BF16 = 0, EPI_BIAS_BF16 = 1, EPI_BF16 = 2, EPI_F32_SLAB = 3 };
 struct GemmArgs {
   const unsigned short* A = nullptr;
   const unsigned short* maskA = nullptr;  // relu' mask in A's layout (bf16), optional
@@ -268,23 +256,16 @@ struct GemmArgs {
   int epi = EPI_BF16;
   int k_per_split = 1 << 30;
   int64_t slab_stride = 0;
-  // cross epilogues (all f32 / bf16 cross buffers share ldc; x0 has ldx0)
-  const unsigned short* x0 = nullptr;
-  int ldx0 = 0;
-  const float* xin = nullptr;
-  const float* gin = nullptr;
-  const float* zprev = nullptr;
-  float* out2 = nullptr;
-  unsigned short* outb = nullptr;
 };
 void launch_gemm(const GemmArgs& g, hipStream_t s);
-// DCN-V2 cross head (cross.hip): s[m] = x[m, :N] . w ; and its backward top:
-// g[m,n] = ds[m] w[n] (f32, ld), u = bf16(x0 * g), acc = z * g, dw += sum_m ds[m] x[m,n]
+// DCN-V2 cross head (cross.hip): s[m] = x[m, :N] . w ; and the top of its
+// backward: g[m,n] = ds[m] w[n] (f32), u = bf16(x0 * g) and u^T [n][ldt],
+// acc = z * g, dw[n] += sum_m ds[m] x[m,n].  x, x0, z, g, u, acc share ld.
 void launch_cross_dot(const float* x, int M, int N, int ld, const float* w, float* out, hipStream_t s);
 int cross_top_blocks(int M);
-void launch_cross_top_bwd(const float* x, const unsigned short* x0, int ldx0, const float* z, const float* w,
-                          const float* ds, int M, int N, int ld, float* g, unsigned short* u, float* acc, float* part,
-                          float* dw, hipStream_t s);
+void launch_cross_top_bwd(const float* x, const unsigned short* x0, const float* z, const float* w, const float* ds,
+                          int M, int N, int ld, float* g, unsigned short* u, unsigned short* ut, int ldt, float* acc,
+                          float* part, float* dw, hipStream_t s);
 void launch_slab_reduce(const float* slab, int splits, int64_t slab_stride, int M, int N, int ldc, float* dW,
                         float* db, float scale, hipStream_t s);
 void launch_gemv_out(const unsigned short* h, int M, int K, int ldh, const float* w, const float* b, float* out,
@@ -355,7 +336,18 @@ void launch_adam_flat(float* p, float* g, float* m, float* v, int64_t n, float l
                       bool clear_grad, hipStream_t s);
 
 // ---------------------------------------------------------------- fused MLP engine (mlp.hip)
-enum MlpEpi { MLP_EPI_FWD = 0, MLP_EPI_DX = 1, MLP_EPI_DW = 2 };
+enum MlpEpi {
+  MLP_EPI_FWD = 0,
+  MLP_EPI_DX = 1,
+  MLP_EPI_DW = 2,
+  // DCN-V2 cross layer x_{l+1} = x0 * (x_l W^T + b) + x_l: fout = x_{l+1},
+  // zout = z_l (f32 [M][ldf]); C / CT = bf16 x_{l+1} and its transpose
+  MLP_EPI_CROSS_FWD = 3,
+  // cross backward: g_l = acc + gin.  With zprev (layer l > 0): fout = g_l,
+  // accum += zprev * g_l, C / CT = bf16(x0 * g_l) (= u_{l-1});
+  // without (layer 0): C = bf16(g_l + accum), the gradient of x0
+  MLP_EPI_CROSS_DX = 4
+};
 struct MlpGemmArgs {
   const unsigned short* A = nullptr;  // [M rows][lda] k-contiguous bf16
   const unsigned short* B = nullptr;  // [N rows][ldb] k-contiguous bf16
@@ -377,6 +369,16 @@ struct MlpGemmArgs {
   float* dW = nullptr;  // [nrows_valid][lddw] fp32 (atomic accumulate)
   int lddw = 0;
   float* db = nullptr;
+  // CROSS_FWD / CROSS_DX (x0 bf16 [M][ldx0]; f32 buffers [M][ldf])
+  const unsigned short* x0 = nullptr;
+  int ldx0 = 0;
+  const float* xin = nullptr;
+  const float* gin = nullptr;
+  const float* zprev = nullptr;
+  float* fout = nullptr;
+  float* zout = nullptr;
+  float* accum = nullptr;
+  int ldf = 0;
 };
 void launch_mlp_gemm(const MlpGemmArgs& g, int epi, hipStream_t s);
 constexpr int kMaxMlpLayers = 8;

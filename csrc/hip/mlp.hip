@@ -149,6 +149,58 @@ __global__ __launch_bounds__(256) void k_gemm_nt(MlpGemmArgs g) {
       }
       continue;
     }
+    if (EPI == MLP_EPI_CROSS_FWD || EPI == MLP_EPI_CROSS_DX) {
+      // cross epilogues: every operand of the tile column is loaded before any
+      // store (restrict views; otherwise the possible aliasing serialises one
+      // load-use round trip per element), the f32 outputs are written here and
+      // acc is replaced by the bf16 output value for the shared C / C^T path
+      const bool nv = n < g.ncols_valid;
+      const float bn = (EPI == MLP_EPI_CROSS_FWD && nv) ? g.bias[n] : 0.f;
+      const unsigned short* __restrict__ x0p = g.x0;
+      const float* __restrict__ ip = EPI == MLP_EPI_CROSS_FWD ? g.xin : g.gin;
+      const float* __restrict__ zp = g.zprev;
+      float* __restrict__ ap = g.accum;
+      float* __restrict__ fo = g.fout;
+      float* __restrict__ zo = g.zout;
+      float xa[16], xb[16], xc[16], xd[16];
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int m = mb + (reg & 3) + 8 * (reg >> 2);
+        const bool ok = nv && m < g.M;
+        const int64_t of = (int64_t)m * g.ldf + n;
+        xa[reg] = ok ? bf2f(x0p[(int64_t)m * g.ldx0 + n]) : 0.f;
+        xb[reg] = (ok && ip) ? ip[of] : 0.f;
+        xc[reg] = (EPI == MLP_EPI_CROSS_DX && ok && zp) ? zp[of] : 0.f;
+        xd[reg] = (EPI == MLP_EPI_CROSS_DX && ok) ? ap[of] : 0.f;
+      }
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int m = mb + (reg & 3) + 8 * (reg >> 2);
+        const bool ok = nv && m < g.M;
+        const int64_t of = (int64_t)m * g.ldf + n;
+        float v = acc[i][reg];
+        if (EPI == MLP_EPI_CROSS_FWD) {
+          v += bn;
+          const float xn = xa[reg] * v + (ip ? xb[reg] : xa[reg]);
+          if (ok) {
+            fo[of] = xn;
+            zo[of] = v;
+          }
+          acc[i][reg] = ok ? xn : 0.f;  // zero keeps the bf16 pad columns zero
+        } else {
+          const float gl = v + xb[reg];
+          if (zp) {
+            if (ok) {
+              fo[of] = gl;
+              ap[of] = xd[reg] + xc[reg] * gl;
+            }
+            acc[i][reg] = ok ? xa[reg] * gl : 0.f;
+          } else {
+            acc[i][reg] = ok ? gl + xd[reg] : 0.f;
+          }
+        }
+      }
+    }
     float bias = 0.f;
     if (EPI == MLP_EPI_FWD && g.bias && n < g.ncols_valid) bias = g.bias[n];
 #pragma unroll
@@ -160,11 +212,11 @@ __global__ __launch_bounds__(256) void k_gemm_nt(MlpGemmArgs g) {
         float v = acc[i][grp * 4 + j] + bias;
         if (EPI == MLP_EPI_FWD) {
           if (g.relu) v = v > 0.f ? v : 0.f;
-        } else if (g.mask && m < g.M) {  // relu' of this layer's input
-          if ((short)g.mask[(int64_t)m * g.ldmask + n] <= 0) v = 0.f;
+        } else if (EPI == MLP_EPI_DX) {
+          if (g.mask && m < g.M && (short)g.mask[(int64_t)m * g.ldmask + n] <= 0) v = 0.f;  // relu' of the input
         }
         o[j] = f2bf(v);
-        if (m < g.M) g.C[(int64_t)m * g.ldc + n] = o[j];
+        if (m < g.M && g.C) g.C[(int64_t)m * g.ldc + n] = o[j];
       }
       const int m4 = mb + 8 * grp;  // 4 consecutive rows -> one 8-byte store into the transposed copy
       if (g.CT && n < g.ncols_valid && m4 < g.M) {
@@ -274,6 +326,17 @@ __global__ __launch_bounds__(256) void k_gemv_bwd(const unsigned short* __restri
 
 void launch_mlp_gemm(const MlpGemmArgs& g, int epi, hipStream_t s) {
   const int splits = (g.K + g.k_per_split - 1) / g.k_per_split;
+  if (epi == MLP_EPI_CROSS_FWD || epi == MLP_EPI_CROSS_DX) {
+    // 64 x 64 tiles: the cross epilogues move ~26 B per output element, so
+    // the work is spread over 2x the work-groups (a 128-row tile's epilogue
+    // traffic, serialised on one CU, was the kernel's critical path)
+    dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, splits);
+    if (epi == MLP_EPI_CROSS_FWD)
+      hipLaunchKernelGGL((k_gemm_nt<MLP_EPI_CROSS_FWD, 64, 64, 2>), grid, dim3(256), 0, s, g);
+    else
+      hipLaunchKernelGGL((k_gemm_nt<MLP_EPI_CROSS_DX, 64, 64, 2>), grid, dim3(256), 0, s, g);
+    return;
+  }
   if (epi == MLP_EPI_DW) {  // 64x64 tiles: dW is only ~400 x 400
     dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, splits);
     hipLaunchKernelGGL((k_gemm_nt<MLP_EPI_DW, 64, 64, 2>), grid, dim3(256), 0, s, g);

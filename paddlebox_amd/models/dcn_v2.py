@@ -29,52 +29,59 @@ from ..ps.sparse_engine import SeqpoolParams, SparseEngine
 
 
 class _CrossHipFn(torch.autograd.Function):
-    """s = x_L . w_c over the cross stack on the GPU.  x0 is the MLP's bf16
-    input buffer [M, ldx0]; parameter gradients accumulate straight into
-    ``p.grad`` (dense-arena views); returns d(loss)/d(x0) as bf16 [M, ldx0]."""
+    """s = x_L . w_c over the cross stack on the GPU.  x0 / x0^T are the MLP
+    workspace's bf16 input buffers (X_0 [M, pad64(D)], X_0^T with the ones
+    row); parameter gradients accumulate straight into ``p.grad`` (dense-arena
+    views); returns d(loss)/d(x0) as bf16 [M, pad64(D)]."""
 
     @staticmethod
-    def forward(ctx, y, mod, w_c, *params):
+    def forward(ctx, y, yt, mod, w_c, *params):
         xw = mod.workspace(y)
         s = xw.forward(y, [w.detach() for w in mod.w], [b.detach() for b in mod.b], w_c.detach())
-        ctx.mod, ctx.y, ctx.w_c = mod, y, w_c
+        ctx.mod, ctx.y, ctx.yt, ctx.w_c = mod, y, yt, w_c
         ctx.n_params = len(params)
         return s
 
     @staticmethod
     def backward(ctx, ds):
         mod = ctx.mod
-        dy = mod._xw.backward(ctx.y, ds.float().contiguous(), [_ensure_grad(w) for w in mod.w],
+        dy = mod._xw.backward(ctx.y, ctx.yt, ds.float().contiguous(), [_ensure_grad(w) for w in mod.w],
                               [_ensure_grad(b) for b in mod.b], ctx.w_c.detach(), _ensure_grad(ctx.w_c))
-        return (dy, None, None) + (None,) * ctx.n_params
+        return (dy, None, None, None) + (None,) * ctx.n_params
 
 
-def cross_logit(y: torch.Tensor, cross: "CrossNetV2", w_c: torch.Tensor) -> torch.Tensor:
-    """[M] = CrossNetV2(y[:, :C]) . w_c -- the HIP cross stack on a GPU
-    (y: the bf16 MLP input buffer), fp32 torch on the CPU."""
-    C = w_c.numel()
+def cross_logit(y: torch.Tensor, cross: "CrossNetV2", w_c: torch.Tensor,
+                yt: torch.Tensor = None) -> torch.Tensor:
+    """[M] = CrossNetV2(y[:, :D]) . w_c.  GPU: y / yt are the MLP workspace's
+    bf16 X_0 / X_0^T (the HIP cross stack); CPU: fp32 torch."""
+    D = w_c.numel()
     if y.is_cuda:
-        return _CrossHipFn.apply(y, cross, w_c, *cross.parameters(), w_c)
-    return cross(y[:, :C].float()) @ w_c
+        return _CrossHipFn.apply(y, yt, cross, w_c, *cross.parameters(), w_c)
+    return cross(y[:, :D].float()) @ w_c
 
 
 class CrossNetV2(nn.Module):
-    def __init__(self, dim: int, layers: int = 3):
+    """``dim`` (a multiple of 8 on the GPU) is the padded MLP input width;
+    features >= ``valid`` are zero padding (their weights start at zero and
+    receive zero gradients)."""
+
+    def __init__(self, dim: int, layers: int = 3, valid: int = None):
         super().__init__()
         self.dim = dim
         self._xw = None
         self.w = nn.ParameterList()
         self.b = nn.ParameterList()
         for _ in range(layers):
-            w = torch.empty(dim, dim)
-            nn.init.xavier_uniform_(w)
+            v = valid or dim
+            w = torch.zeros(dim, dim)
+            nn.init.xavier_uniform_(w[:v, :v])
             self.w.append(nn.Parameter(w * 0.1))
             self.b.append(nn.Parameter(torch.zeros(dim)))
 
     def workspace(self, y: torch.Tensor):
         M, ld = int(y.shape[0]), int(y.shape[1])
         if self._xw is None or self._xw_key != (M, ld, y.device):
-            self._xw = _native.hip().CrossWorkspace(M, self.dim, len(self.w), ld, y.device.index or 0, 512)
+            self._xw = _native.hip().CrossWorkspace(M, self.dim, len(self.w), y.device.index or 0, 1024)
             self._xw_key = (M, ld, y.device)
         return self._xw
 
@@ -99,8 +106,8 @@ class DCNv2(nn.Module):
         self.C = C
         self.Cp = pad8(C)
         self.dn = DataNorm(C) if use_data_norm else None
-        self.cross = CrossNetV2(C, cross_layers)
-        self.w_c = nn.Parameter(torch.zeros(C))
+        self.cross = CrossNetV2(self.Cp, cross_layers, valid=C)
+        self.w_c = nn.Parameter(torch.zeros(self.Cp))
         self.mlp = FusedMLP(C, hidden, 1)
         self.ew_col = 2 if self.sp.use_cvm and not self.sp.clk_filter else (1 if self.sp.use_cvm else 0)
 
@@ -111,7 +118,9 @@ class DCNv2(nn.Module):
             ws = self.mlp.workspace(B, x.device)
             y, _ = ctr_head(x, self.dn, S, self.Eo, self.ew_col, 0, self.Cp, ws.x(0), ws.xt(0))
             deep = self.mlp.forward_ws(y)
+            cross = cross_logit(y, self.cross, self.w_c, ws.xt(0))
         else:
             y, _ = ctr_head(x, self.dn, S, self.Eo, self.ew_col, 0, self.Cp)
             deep = self.mlp(y)
-        return logit_logloss(deep, cross_logit(y, self.cross, self.w_c), batch.label)
+            cross = cross_logit(y, self.cross, self.w_c)
+        return logit_logloss(deep, cross, batch.label)

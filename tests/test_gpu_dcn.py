@@ -13,8 +13,15 @@ def _rel(a, b):
     return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("M,C,L,ld", [(1000, 299, 3, 320), (4096, 64, 1, 64), (333, 131, 2, 192)])
-def test_cross_stack_matches_fp64(M, C, L, ld):
+def _p64(n):
+    return (n + 63) // 64 * 64
+
+
+@pytest.mark.parametrize("M,C,L", [(1000, 304, 3), (4096, 64, 1), (333, 136, 2)])
+def test_cross_stack_matches_fp64(M, C, L):
+    """C = the padded MLP input width D; x0 / x0^T laid out as the MLP
+    workspace's X_0 [M, pad64(D)] / X_0^T [pad64(D+1), pad64(M)] (ones row)."""
+    ld = _p64(C)
     torch.manual_seed(M + C)
     dev = torch.device("cuda:0")
     net = CrossNetV2(C, L).to(dev)
@@ -25,12 +32,15 @@ def test_cross_stack_matches_fp64(M, C, L, ld):
     w_c = torch.nn.Parameter(torch.randn(C, device=dev) * 0.3)
     y = torch.zeros(M, ld, dtype=torch.bfloat16, device=dev)
     y[:, :C] = (torch.randn(M, C, device=dev) * 0.7).to(torch.bfloat16)
+    yt = torch.zeros(_p64(C + 1), _p64(M), dtype=torch.bfloat16, device=dev)
+    yt[:C, :M] = y[:, :C].t()
+    yt[C, :M] = 1.0
     r = torch.randn(M, device=dev)
     # HIP path (grads accumulate into .grad; start from zero)
     for p in list(net.parameters()) + [w_c]:
         p.grad = torch.zeros_like(p)
     yh = y.clone().requires_grad_(True)
-    s = cross_logit(yh, net, w_c)
+    s = cross_logit(yh, net, w_c, yt)
     (s * r).sum().backward()
     # fp64 oracle
     x0 = y[:, :C].double().requires_grad_(True)
