@@ -233,6 +233,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("parse_logkey", &ParseConfig::parse_logkey)
       .def_readwrite("sample_rate", &ParseConfig::sample_rate)
       .def_readwrite("sample_seed", &ParseConfig::sample_seed);
+  py::class_<KeyAgent, std::shared_ptr<KeyAgent>>(m, "KeyAgent")
+      .def(py::init<int>(), py::arg("shards") = 64)
+      .def("add",
+           [](KeyAgent& a, const Tensor& k) {
+             req_cpu(k, "keys");
+             auto c = k.contiguous().to(torch::kInt64);
+             py::gil_scoped_release nogil;
+             a.add(reinterpret_cast<const uint64_t*>(c.data_ptr<int64_t>()), (size_t)c.numel());
+           })
+      .def("keys", [](const KeyAgent& a) { return to_tensor_u64(a.keys()); })
+      .def("size", &KeyAgent::size)
+      .def("clear", &KeyAgent::clear);
   py::class_<SlotDataset>(m, "SlotDataset")
       .def(py::init<>())
       .def("set_slots", &SlotDataset::set_slots)
@@ -269,6 +281,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         if (!o.empty()) memcpy(t.data_ptr(), o.data(), o.size() * 8);
         return t;
       })
+      .def("set_key_agent", [](SlotDataset& d, std::shared_ptr<KeyAgent> a) { d.set_key_agent(std::move(a)); },
+           py::arg("agent").none(true))
       .def("version", &SlotDataset::version)
       .def("dense_refs", [](const SlotDataset& d) {
         auto v = d.dense_refs();

@@ -361,6 +361,8 @@ int64_t SlotDataset::load_files(const std::vector<std::string>& files, RecordSto
   for (int t = 0; t < T; ++t) {
     parts[t].reset(store_.nu, store_.nf);
     th.emplace_back([&, t] {
+      std::unique_ptr<KeyAgent::Stage> stg;
+      if (agent_) stg.reset(new KeyAgent::Stage(agent_.get()));
       for (;;) {
         const size_t fi = next++;
         if (fi >= files.size()) break;
@@ -381,11 +383,13 @@ int64_t SlotDataset::load_files(const std::vector<std::string>& files, RecordSto
         char* line = nullptr;
         size_t cap = 0;
         ssize_t n;
+        const int64_t r0 = parts[t].nrec();
         while ((n = getline(&line, &cap, fp)) > 0) {
           if (n <= 1) continue;
           if (!parse_line(line, (size_t)n, &parts[t])) bad += 1;
         }
         free(line);
+        if (stg) register_keys(parts[t], r0, parts[t].nrec(), stg.get());
         if (is_pipe) pclose(fp); else fclose(fp);
       }
     });
@@ -426,8 +430,13 @@ int64_t SlotDataset::wait_preload_done() {
 
 int64_t SlotDataset::add_lines(const std::vector<std::string>& lines) {
   int64_t ok = 0;
+  const int64_t r0 = store_.nrec();
   for (auto& l : lines) {
     if (parse_line(l.data(), l.size(), &store_)) ++ok; else ++bad_lines_;
+  }
+  if (agent_) {
+    KeyAgent::Stage stg(agent_.get());
+    register_keys(store_, r0, store_.nrec(), &stg);
   }
   ++version_;
   order_.resize(store_.nrec());
@@ -443,19 +452,35 @@ void SlotDataset::release_memory() {
   store_.f32.shrink_to_fit();
 }
 
+void SlotDataset::register_keys(const RecordStore& st, int64_t r0, int64_t r1, KeyAgent::Stage* stg) const {
+  const int nu = st.nu;
+  for (int64_t i = r0; i < r1; ++i)
+    for (int j : sparse_slots_)
+      for (int64_t e = st.u64_off[i * nu + j]; e < st.u64_off[i * nu + j + 1]; ++e) stg->push(st.u64[e]);
+}
+
 std::vector<uint64_t> SlotDataset::collect_keys(bool unique) const {
-  std::vector<uint64_t> keys;
   const int64_t n = store_.nrec();
+  if (unique) {
+    // parallel registration into a sharded set (the loader-thread path)
+    KeyAgent agent;
+    const int T = std::max(1, std::min(threads_ * 2, 16));
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        KeyAgent::Stage stg(&agent);
+        register_keys(store_, n * t / T, n * (t + 1) / T, &stg);
+      });
+    for (auto& x : th) x.join();
+    return agent.keys();
+  }
+  std::vector<uint64_t> keys;
   const int nu = store_.nu;
   for (int64_t i = 0; i < n; ++i)
     for (int j : sparse_slots_) {
       const int64_t b = store_.u64_off[i * nu + j], e = store_.u64_off[i * nu + j + 1];
       keys.insert(keys.end(), store_.u64.begin() + b, store_.u64.begin() + e);
     }
-  if (unique) {
-    std::sort(keys.begin(), keys.end());
-    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
-  }
   return keys;
 }
 
@@ -723,6 +748,10 @@ int64_t SlotDataset::load_archive(const std::string& path, bool append) {
   if (!append) store_.reset(store_.nu, store_.nf);
   store_.append(st);
   ++version_;
+  if (agent_) {
+    KeyAgent::Stage stg(agent_.get());
+    register_keys(st, 0, st.nrec(), &stg);
+  }
   order_.resize(store_.nrec());
   std::iota(order_.begin(), order_.end(), 0);
   return st.nrec();

@@ -20,6 +20,8 @@
 #include <thread>
 #include <vector>
 
+#include "key_agent.h"
+
 namespace pbx {
 
 struct SlotDesc {
@@ -86,6 +88,9 @@ class SlotDataset {
 
   // feed-pass keys: every feasign of sparse uint64 slots (optionally unique)
   std::vector<uint64_t> collect_keys(bool unique) const;
+  // feed-pass agent: while set, the loader threads register the sparse
+  // feasigns of every record they parse (load / preload / add_lines / archive)
+  void set_key_agent(std::shared_ptr<KeyAgent> a) { agent_ = std::move(a); }
 
   // order of records for this pass (shuffle: Fisher-Yates with seed)
   void shuffle(uint64_t seed);
@@ -169,6 +174,8 @@ class SlotDataset {
   RecordStore preload_store_;
   int64_t bad_lines_ = 0;
   uint64_t version_ = 0;
+  std::shared_ptr<KeyAgent> agent_;
+  void register_keys(const RecordStore& st, int64_t r0, int64_t r1, KeyAgent::Stage* stg) const;
 };
 
 }  // namespace pbx

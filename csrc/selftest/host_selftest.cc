@@ -7,6 +7,7 @@
 // threads, plus the CPU sparse table and the AUC calculator.
 //
 //   host_selftest <workdir> [plugin.so]
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -53,15 +54,24 @@ static void test_dataset(const std::string& dir) {
   d.set_slots(slots());
   d.set_thread_num(4);
   d.set_filelist(files);
+  // loader threads register feasigns into the feed-pass agent concurrently
+  auto agent = std::make_shared<KeyAgent>(16);
+  d.set_key_agent(agent);
   CHECK(d.load_into_memory() == 3000);
   d.preload_into_memory();  // second pass on a background thread
   CHECK(d.wait_preload_done() == 6000);
+  d.set_key_agent(nullptr);
+  CHECK(agent->size() == 3006);
   d.shuffle(7);
   auto dims = d.batch_dims(0, 64);
   std::vector<int64_t> keys(dims.L), lod(2 * 65);
   std::vector<float> dense(64 * d.dense_width());
   d.build_batch(0, 64, keys.data(), lod.data(), dense.data());
   CHECK(dims.L == 64 * 3);
+  std::vector<int64_t> keys2(dims.L + 5), lod2(2 * 65);
+  std::vector<float> dense2(64 * d.dense_width());
+  CHECK(d.build_batch_staged(0, 64, keys2.data(), (int64_t)keys2.size(), lod2.data(), dense2.data()) == dims.L);
+  CHECK(std::equal(keys.begin(), keys.end(), keys2.begin()) && keys2[dims.L] == -1 && lod == lod2);
   CHECK(d.collect_keys(true).size() == 3006);  // s1: 3000 ids; s2/s3 add 501..506
   d.save_archive(dir + "/arch");
   SlotDataset e;

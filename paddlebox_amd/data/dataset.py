@@ -231,14 +231,37 @@ class PadBoxSlotDataset(DatasetBase):
         if not self._configured:
             self._configure()
         files = self._my_files()
-        if self.archive_mode:
-            for f in files:
-                self._native.load_archive(f, True)
-        else:
-            self._native.set_filelist(files)
-            self._native.load_into_memory()
-        if register_keys and self.box is not None:
-            self.box.feed_pass(self, self.date)
+        agent = self._open_feed_pass() if register_keys else None
+        try:
+            if self.archive_mode:
+                for f in files:
+                    self._native.load_archive(f, True)
+            else:
+                self._native.set_filelist(files)
+                self._native.load_into_memory()
+        finally:
+            self._native.set_key_agent(None)
+        if agent is not None:
+            self._close_feed_pass(agent)
+
+    def _open_feed_pass(self):
+        """BeginFeedPass: the loader threads register every parsed record's
+        feasigns into the pass agent (data_set.cc:2293-2349)."""
+        if self.box is None:
+            return None
+        agent = self.box.begin_feed_pass(self.date)
+        if agent.native is not None:
+            self._native.set_key_agent(agent.native)
+        else:  # no native agent: walk the store after the load
+            agent._collect_from = self
+        return agent
+
+    def _close_feed_pass(self, agent):
+        if getattr(agent, "_collect_from", None) is self:
+            agent.add_keys(self.collect_keys())
+        if getattr(self.box, "auc_runner", None) is not None:
+            agent.add_keys(self.box.auc_runner.prepare(self))
+        self.box.end_feed_pass(agent)
 
     def read_ins_into_memory(self):
         self.load_into_memory()
@@ -247,12 +270,17 @@ class PadBoxSlotDataset(DatasetBase):
         if not self._configured:
             self._configure()
         self._native.set_filelist(self._my_files())
+        self._preload_agent = self._open_feed_pass()
         self._native.preload_into_memory()
 
     def wait_preload_done(self, register_keys: bool = True):
-        self._native.wait_preload_done()
-        if register_keys and self.box is not None:
-            self.box.feed_pass(self, self.date)
+        try:
+            self._native.wait_preload_done()
+        finally:
+            self._native.set_key_agent(None)
+        agent, self._preload_agent = getattr(self, "_preload_agent", None), None
+        if agent is not None and register_keys:
+            self._close_feed_pass(agent)
 
     def add_lines(self, lines: List[str]) -> int:
         """Parse in-memory text lines (tests / pipe-less sources)."""

@@ -57,8 +57,8 @@ class BoxPS:
         self.box.end_pass(need_save_delta)
 
     def read_ins_into_memory(self):
-        self.dataset.load_into_memory(register_keys=False)
-        self.box.feed_pass(self.dataset, self._date)
+        # the loader threads register feasigns into the feed-pass agent
+        self.dataset.load_into_memory(register_keys=True)
 
     load_into_memory = read_ins_into_memory
 
@@ -66,8 +66,7 @@ class BoxPS:
         self.dataset.preload_into_memory()
 
     def wait_feed_pass_done(self):
-        self.dataset.wait_preload_done(register_keys=False)
-        self.box.feed_pass(self.dataset, self._date)
+        self.dataset.wait_preload_done(register_keys=True)
 
     def slots_shuffle(self, slots):
         self.dataset.slots_shuffle(slots)

@@ -33,6 +33,7 @@ from ..utils import flags as _flags
 from ..utils.dayid import make_day_id_str
 from ..utils.log import logger
 from ..utils.timer import StageTimers
+from .. import _native
 from . import checkpoint as ckpt
 from .config import PSConfig, feature_pull_offsets, feature_push_offsets, row_layout
 from .cpu_table import CpuSparseTable
@@ -40,13 +41,17 @@ from .sparse_engine import SparseEngine
 
 
 class PSAgent:
-    """Thread-sharded feed-pass key collector (boxps::PSAgentBase AddKey/AddKeys,
-    box_wrapper.cc:1185-1200)."""
+    """Feed-pass key collector (boxps::PSAgentBase AddKey/AddKeys,
+    box_wrapper.cc:1185-1200).  ``native`` is the sharded C++ key set the
+    dataset's loader threads register parsed feasigns into while a feed pass
+    is open (csrc/host/key_agent.cc); keys added from Python (device tensors
+    included) are merged at ``keys()``."""
 
     def __init__(self, n_threads: int = 30):
         self.n = n_threads
         self._parts: List[List[torch.Tensor]] = [[] for _ in range(n_threads)]
         self._lock = threading.Lock()
+        self.native = _native.host().KeyAgent(64) if _native.host_available() else None
 
     def add_key(self, key: int, tid: int = 0):
         self._parts[tid % self.n].append(torch.tensor([key], dtype=torch.int64))
@@ -57,6 +62,11 @@ class PSAgent:
 
     def keys(self) -> torch.Tensor:
         allk = [t for p in self._parts for t in p]
+        nat = self.native.keys() if self.native is not None and self.native.size() else None
+        if nat is not None:
+            if not allk:
+                return nat  # unique already, padding keys excluded
+            allk.append(nat)
         if not allk:
             return torch.empty(0, dtype=torch.int64)
         dev = next((t.device for t in allk if t.is_cuda), allk[0].device)

@@ -183,3 +183,53 @@ def test_flags_registry_env_override(monkeypatch):
     assert not flags.get_bool("check_nan_inf")
     with pytest.raises(KeyError):
         flags.set_flags({"no_such_flag": 1})
+
+
+def test_key_agent_dedups_and_loader_registers_keys(tmp_path):
+    """Feed-pass key registration by the loader threads (KeyAgent) equals a
+    walk over the loaded store (reference: AddKeys from data_set.cc merge
+    threads into the PSAgent)."""
+    import numpy as np
+
+    from paddlebox_amd import _native
+
+    ka = _native.host().KeyAgent(8)
+    ka.add(torch.tensor([5, 7, 5, 0, -1, 9, 7], dtype=torch.int64))
+    assert sorted(ka.keys().tolist()) == [5, 7, 9] and ka.size() == 3
+    big = torch.randint(1, 1 << 62, (200000,), dtype=torch.int64)
+    ka.add(big)
+    ka.add(big[:5000])
+    assert ka.size() == 3 + int(torch.unique(big).numel())
+
+    import paddlebox_amd.fluid as fluid
+    from paddlebox_amd.ps.box_wrapper import BoxWrapper
+    from tests.test_fluid import S, _build, _files
+
+    box = fluid.core.BoxWrapper(8, device="cpu", new=True)
+    try:
+        box.initialize_gpu_and_load_model(slot_vector=list(range(S)), max_keys=200000)
+        seen = {}
+        orig = box.end_feed_pass
+
+        def spy(agent=None):
+            seen["keys"] = agent.keys().clone()
+            seen["native"] = agent.native.size()
+            return orig(agent)
+
+        box.end_feed_pass = spy
+        main, startup, slots, label, dense, pred, loss = _build()
+        ds = fluid.DatasetFactory().create_dataset("PadBoxSlotDataset")
+        ds.set_use_var([label] + slots + [dense])
+        ds.set_batch_size(32)
+        ds.set_thread(3)
+        ds.set_filelist(_files(tmp_path, 3, 200))
+        boxps = fluid.core.BoxPS(ds)
+        boxps.read_ins_into_memory()
+        want = np.unique(ds.collect_keys().numpy())
+        got = np.unique(seen["keys"].numpy())
+        assert seen["native"] == got.size > 0
+        np.testing.assert_array_equal(got, want)
+        h, _ = box.engine.table.export(True)
+        assert h.numel() == want.size
+    finally:
+        BoxWrapper._instance = None
