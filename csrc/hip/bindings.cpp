@@ -848,7 +848,8 @@ static std::vector<Tensor> sigmoid_logloss(const Tensor& logit, const Tensor& la
   return {pred, loss, dz};
 }
 
-static std::vector<Tensor> logit_loss(const Tensor& a, const c10::optional<Tensor>& b, const Tensor& label) {
+static std::vector<Tensor> logit_loss(const Tensor& a, const c10::optional<Tensor>& b, const Tensor& label,
+                                      const Tensor& ws) {
   check_cuda(a, "a");
   check_cuda(label, "label");
   const int B = (int)a.numel();
@@ -861,8 +862,11 @@ static std::vector<Tensor> logit_loss(const Tensor& a, const c10::optional<Tenso
   auto pred = torch::empty({B}, a.options());
   auto dz = torch::empty({B}, a.options());
   auto loss = torch::empty({1}, a.options());
+  check_cuda(ws, "ws");
+  PBX_CHECK(ws.scalar_type() == torch::kInt32 && ws.numel() >= 1 + kLogitLossMaxBlocks && ws.is_contiguous(),
+            "logit_loss: ws must be int32 [1 + 1024] (zeroed once)");
   launch_logit_loss(ptr<float>(a), optr<float>(b), ptr<float>(label), B, ptr<float>(pred), ptr<float>(dz),
-                    ptr<float>(loss), cur_stream());
+                    ptr<float>(loss), reinterpret_cast<uint32_t*>(ws.data_ptr()), cur_stream());
   return {loss, pred, dz};
 }
 
@@ -1030,7 +1034,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fm_bwd", &fm_bwd);
   m.def("sigmoid_logloss", &sigmoid_logloss);
   m.def("auc_accumulate", &auc_accumulate);
-  m.def("logit_loss", &logit_loss, py::arg("a"), py::arg("b"), py::arg("label"));
+  m.def("logit_loss", &logit_loss, py::arg("a"), py::arg("b"), py::arg("label"), py::arg("ws"));
   m.def("adam_flat", &adam_flat, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pows"),
         py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("grad_scale"), py::arg("wd"),
         py::arg("clear_grad") = false);

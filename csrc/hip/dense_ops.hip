@@ -154,16 +154,16 @@ __global__ void k_sigmoid_logloss(const float* __restrict__ z, const float* __re
 // the chip idle for ~11 us at B=8192).  Each block writes its partial loss
 // sum; the last block to arrive (ticket counter) adds the partials in block
 // order, so the mean is deterministic, and re-arms the ticket for the next
-// launch (graph-replay safe; one loss launch in flight per device).
+// launch (graph-replay safe).  The ticket + partials live in a caller-owned
+// workspace (one per stream at the call site), so launches on different
+// streams cannot interleave on one counter.
 constexpr int kLossBlock = 256;
-constexpr int kLossMaxBlocks = 1024;
-__device__ float g_loss_part[kLossMaxBlocks];
-__device__ unsigned int g_loss_ticket;
 
 __global__ __launch_bounds__(kLossBlock) void k_logit_loss(const float* __restrict__ a, const float* __restrict__ b,
                                                            const float* __restrict__ y, int B, int per_thread,
                                                            float* __restrict__ pred, float* __restrict__ dz,
-                                                           float* __restrict__ loss_mean) {
+                                                           float* __restrict__ loss_mean, unsigned int* ticket,
+                                                           float* part) {
   __shared__ float red[kLossBlock / 64];
   __shared__ bool last;
   const float inv = 1.f / (float)B;
@@ -185,17 +185,17 @@ __global__ __launch_bounds__(kLossBlock) void k_logit_loss(const float* __restri
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int w = 0; w < kLossBlock / 64; ++w) s += red[w];
-    g_loss_part[blockIdx.x] = s;
+    part[blockIdx.x] = s;
     __threadfence();
-    last = atomicAdd(&g_loss_ticket, 1u) == gridDim.x - 1;
+    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
   }
   __syncthreads();
   if (last && threadIdx.x == 0) {
     __threadfence();
     float s = 0.f;
-    for (unsigned int k = 0; k < gridDim.x; ++k) s += __hip_atomic_load(&g_loss_part[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (unsigned int k = 0; k < gridDim.x; ++k) s += __hip_atomic_load(&part[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     loss_mean[0] = s * inv;
-    g_loss_ticket = 0u;
+    *ticket = 0u;
   }
 }
 
@@ -349,12 +349,13 @@ void launch_fm_bwd(const float* x, const float* dout, int B, int S, int D, int r
 }
 
 void launch_logit_loss(const float* a, const float* b, const float* label, int B, float* pred, float* dz,
-                       float* loss_mean, hipStream_t s) {
+                       float* loss_mean, uint32_t* ws, hipStream_t s) {
   if (B <= 0) return;
   int per_thread = 1;
-  while ((B + kLossBlock * per_thread - 1) / (kLossBlock * per_thread) > kLossMaxBlocks) per_thread *= 2;
+  while ((B + kLossBlock * per_thread - 1) / (kLossBlock * per_thread) > kLogitLossMaxBlocks) per_thread *= 2;
   const int grid = (B + kLossBlock * per_thread - 1) / (kLossBlock * per_thread);
-  hipLaunchKernelGGL(k_logit_loss, dim3(grid), dim3(kLossBlock), 0, s, a, b, label, B, per_thread, pred, dz, loss_mean);
+  hipLaunchKernelGGL(k_logit_loss, dim3(grid), dim3(kLossBlock), 0, s, a, b, label, B, per_thread, pred, dz, loss_mean,
+                     ws, reinterpret_cast<float*>(ws + 1));
 }
 
 void launch_sigmoid_logloss(const float* logit, const float* label, int B, float* pred,

@@ -320,8 +320,11 @@ void launch_sigmoid_logloss(const float* logit, const float* label, int B, float
                             float* loss_sum, float* dlogit, float grad_scale, hipStream_t s);
 
 // z = a + b (b nullable); pred = sigmoid(z), dz = (pred - y)/B, loss_mean = mean BCE.
+// ws: caller-owned uint32 [1 + kLogitLossMaxBlocks], zero before the first
+// launch (the kernel re-arms it); one workspace per stream
+constexpr int kLogitLossMaxBlocks = 1024;
 void launch_logit_loss(const float* a, const float* b, const float* label, int B, float* pred, float* dz,
-                       float* loss_mean, hipStream_t s);
+                       float* loss_mean, uint32_t* ws, hipStream_t s);
 
 // Streaming AUC histogram: table[label][bucket] += 1 and error sums
 // (stats: [abserr, sqrerr, pred_sum, label_sum, count]) in double.

@@ -260,6 +260,38 @@ __global__ void k_shrink(TableDev t, ShrinkConfig c, unsigned long long* deleted
   if (del) atomicAdd(deleted, del);
 }
 
+// Stash rows get the same decay / age / delete pass; the stash is compacted
+// in order by one thread (it holds the rare keys whose cuckoo walk failed,
+// normally none).
+__global__ void k_shrink_stash(TableDev t, ShrinkConfig c, unsigned long long* deleted) {
+  if (threadIdx.x != 0 || blockIdx.x != 0 || !t.stash_n) return;
+  const RowLayout l = make_row_layout(t.dim);
+  const int64_t row0 = (int64_t)(t.nb * kBucketSlots);
+  const uint32_t n = *t.stash_n < t.stash_cap ? *t.stash_n : t.stash_cap;
+  uint32_t w = 0;
+  unsigned long long del = 0;
+  for (uint32_t s = 0; s < n; ++s) {
+    float* v = t.values + (row0 + s) * (int64_t)t.stride;
+    v[kShow] *= c.show_click_decay_rate;
+    v[kClick] *= c.show_click_decay_rate;
+    v[l.unseen_days] += 1.f;
+    const float score = (v[kShow] - v[kClick]) * c.nonclk_coeff + v[kClick] * c.clk_coeff;
+    if (score < c.delete_threshold || v[l.unseen_days] > c.delete_after_unseen_days) {
+      ++del;
+      continue;
+    }
+    if (w != s) {
+      float* dv = t.values + (row0 + w) * (int64_t)t.stride;
+      for (int k = 0; k < t.stride; ++k) dv[k] = v[k];
+      t.stash_keys[w] = t.stash_keys[s];
+    }
+    ++w;
+  }
+  for (uint32_t s = w; s < n; ++s) t.stash_keys[s] = kEmptyKey;
+  *t.stash_n = w;
+  if (del) atomicAdd(deleted, del);
+}
+
 }  // namespace
 
 static inline unsigned int blocks_for(int64_t n, int per) {
@@ -310,6 +342,7 @@ void launch_table_assign(const TableDev& t, const int64_t* rows, const float* va
 void launch_table_shrink(const TableDev& t, const ShrinkConfig& c, unsigned long long* deleted,
                          hipStream_t s) {
   hipLaunchKernelGGL(k_shrink, dim3(blocks_for((int64_t)t.nb, 256)), dim3(256), 0, s, t, c, deleted);
+  if (t.stash_cap > 0) hipLaunchKernelGGL(k_shrink_stash, dim3(1), dim3(64), 0, s, t, c, deleted);
 }
 
 }  // namespace pbx

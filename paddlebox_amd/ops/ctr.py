@@ -233,6 +233,20 @@ def sigmoid_logloss(logit: torch.Tensor, label: torch.Tensor):
     return _SigmoidLogLoss.apply(logit, label)
 
 
+_LOSS_WS = {}
+
+
+def _loss_ws(dev: torch.device) -> torch.Tensor:
+    """Per-(device, stream) ticket + partials workspace of the loss kernel
+    (zeroed once; the kernel re-arms it): launches on different streams never
+    share a counter."""
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    ws = _LOSS_WS.get(key)
+    if ws is None:
+        ws = _LOSS_WS[key] = torch.zeros(1 + 1024, dtype=torch.int32, device=dev)
+    return ws
+
+
 class _LogitLoss(torch.autograd.Function):
     """loss, pred = BCE(sigmoid(a + b), label): the sum of the two logit parts,
     the sigmoid, the mean log-loss and its gradient in one kernel; the
@@ -244,7 +258,7 @@ class _LogitLoss(torch.autograd.Function):
         label = label.contiguous().float().view(-1)
         bb = b.contiguous().float().view(-1) if b is not None else None
         if _gpu(a):
-            loss, pred, dz = _native.hip().logit_loss(a, bb, label)
+            loss, pred, dz = _native.hip().logit_loss(a, bb, label, _loss_ws(a.device))
         else:
             z = a + bb if bb is not None else a
             pred, loss_sum, dz = ref.sigmoid_logloss(z, label, 1.0 / a.numel())

@@ -404,8 +404,10 @@ def test_logit_loss_multiblock(B):
     a = torch.randn(B, device=DEV) * 3
     b = torch.randn(B, device=DEV)
     y = (torch.rand(B, device=DEV) < 0.3).float()
+    ws = torch.zeros(1025, dtype=torch.int32, device=DEV)
     for _ in range(2):  # second launch checks the ticket re-arms
-        loss, pred, dz = hip().logit_loss(a, b, y)
+        loss, pred, dz = hip().logit_loss(a, b, y, ws)
+    assert int(ws[0]) == 0
     z = (a + b).double()
     pe = torch.sigmoid(z)
     le = torch.nn.functional.binary_cross_entropy_with_logits(z, y.double())
@@ -494,3 +496,24 @@ def test_seqpool_embed_threshold_no_cvm(ets):
     exp_rows = ref.adagrad_update(before, push, 8, eng.cfg.sgd)
     after = vals[rows]
     torch.testing.assert_close(after[:, :3], exp_rows[:, :3], rtol=2e-4, atol=2e-5)
+
+
+def test_shrink_reaches_stash_rows():
+    """Keys that overflowed the buckets into the stash are decayed / aged /
+    deleted by shrink like bucket rows (the stash is compacted)."""
+    from paddlebox_amd.ps.config import ShrinkConfig
+    from paddlebox_amd.ps.gpu_table import GpuSparseTable
+
+    t = GpuSparseTable(8, 64, DEV, stash_cap=1024, load_factor=1.0)
+    h = ref.mix64(torch.arange(1, 301, dtype=torch.int64, device=DEV))
+    t.insert_mixed(h, SparseSGDConfig())
+    assert bool((t.probe(h) >= 0).all()) and int(t.t.stash_n()) > 0
+    n0 = t.size()
+    # keep everything once: rows age by a day, nothing deleted, all still found
+    assert t.shrink(ShrinkConfig(delete_threshold=-1.0, delete_after_unseen_days=5.0)) == 0
+    assert bool((t.probe(h) >= 0).all()) and t.size() == n0
+    # rows unseen for more than 1 day go, stash included
+    deleted = t.shrink(ShrinkConfig(delete_threshold=-1.0, delete_after_unseen_days=1.5))
+    assert deleted == 300
+    assert bool((t.probe(h) < 0).all())
+    assert int(t.t.stash_n()) == 0
