@@ -77,6 +77,9 @@ def main():
     ap.add_argument("--model", choices=("deepfm", "dcn_v2"), default="deepfm",
                     help="deepfm = the headline config; dcn_v2 = BASELINE config 5 (cross layers on the MFMA GEMM)")
     ap.add_argument("--cross-layers", type=int, default=3)
+    ap.add_argument("--dense-ipc", action="store_true",
+                    help="dense gradient all-reduce on the in-house IPC mesh (one-shot, xGMI peer writes) "
+                         "instead of RCCL")
     ap.add_argument("--force-collectives", action="store_true",
                     help="run the multi-GPU exchange/all-reduce path even on 1 rank (rehearsal)")
     args = ap.parse_args()
@@ -163,8 +166,13 @@ def main():
         opt.fuse(mlps=[model.mlp], data_norms=[model.dn])
     # the dense all-reduce runs on its own communicator and side stream, started
     # as soon as the tower's gradients are final: it overlaps the sparse push
+    ipc = None
+    if args.dense_ipc and multi:
+        from paddlebox_amd.parallel.ipc import IpcMesh
+
+        ipc = IpcMesh(arena.grad.numel() * 4, device=device)
     sync = DenseSync(arena, mode="grad_allreduce",
-                     overlap_group=dist.new_group(list(range(world))) if multi else None)
+                     overlap_group=dist.new_group(list(range(world))) if multi else None, ipc=ipc)
     if not dcn:
         model.tower.on_dense_grads = sync.launch
 
@@ -317,6 +325,7 @@ def main():
                 "seq_len": S,
                 "total_features": synth.total_features,
                 "parallelism": f"dp{world}+sparse-shard{world}",
+                "dense_allreduce": "ipc-oneshot" if ipc is not None else "rccl",
                 "mlp_dtype": args.mlp_dtype,
                 "unique_keys_per_batch": round(sum(u_per_batch) / len(u_per_batch), 1),
                 "keys_per_batch": l_per_batch,

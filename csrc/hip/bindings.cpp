@@ -894,6 +894,7 @@ namespace pbx {
 void bind_tower(py::module& m);
 void bind_ctr(py::module& m);
 void bind_cross(py::module& m);
+void bind_ipc(py::module& m);
 }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -901,6 +902,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bind_tower(m);
   bind_ctr(m);
   bind_cross(m);
+  bind_ipc(m);
   m.doc() = "PaddleBox-capability engine: hand-written gfx950 (MI355X) kernels";
   py::class_<SparseSGDConfig>(m, "SparseSGDConfig")
       .def(py::init<>())

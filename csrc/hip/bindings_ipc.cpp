@@ -1,0 +1,118 @@
+// torch glue for the IPC mesh (ipc.hip): memory-handle export / import and
+// the collective launches.  Buffers are owned by the Python IpcMesh; this
+// side only holds raw pointers and checks sizes.
+#include <ATen/hip/HIPContext.h>
+#include <torch/extension.h>
+
+#include <cstring>
+#include <stdexcept>
+
+#include "kernels.h"
+
+namespace py = pybind11;
+using torch::Tensor;
+
+namespace pbx {
+namespace {
+
+#define IPC_CHECK(cond, msg)                                                 \
+  do {                                                                       \
+    if (!(cond)) throw std::runtime_error(std::string("pbx ipc: ") + msg);  \
+  } while (0)
+
+void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("pbx ipc: ") + what + ": " + hipGetErrorString(e));
+}
+
+// (handle bytes, byte offset of t inside its allocation)
+py::tuple ipc_handle(const Tensor& t) {
+  IPC_CHECK(t.is_cuda(), "tensor must be on the GPU");
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  hip_ok(hipMemGetAddressRange(&base, &size, t.data_ptr()), "hipMemGetAddressRange");
+  hipIpcMemHandle_t h;
+  hip_ok(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle");
+  const int64_t off = (int64_t)((char*)t.data_ptr() - (char*)base);
+  return py::make_tuple(py::bytes(reinterpret_cast<const char*>(&h), sizeof(h)), off);
+}
+
+int64_t ipc_open(const py::bytes& hb, int64_t off) {
+  std::string s = hb;
+  IPC_CHECK(s.size() == sizeof(hipIpcMemHandle_t), "bad handle size");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, s.data(), sizeof(h));
+  void* p = nullptr;
+  hip_ok(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  return (int64_t)((char*)p + off);
+}
+
+void ipc_close(int64_t base) { hip_ok(hipIpcCloseMemHandle(reinterpret_cast<void*>(base)), "hipIpcCloseMemHandle"); }
+
+class IpcComm {
+ public:
+  // state: own int64 [4] = epoch, arrive|depart (2 x u32), err, pad
+  IpcComm(int rank, int world, int64_t slot_bytes, const Tensor& state, int blocks)
+      : blocks_(blocks) {
+    IPC_CHECK(world >= 1 && world <= kIpcMaxRanks && rank >= 0 && rank < world, "rank / world");
+    IPC_CHECK(slot_bytes > 0 && slot_bytes % 16 == 0, "slot_bytes must be a positive multiple of 16");
+    IPC_CHECK(state.is_cuda() && state.scalar_type() == torch::kInt64 && state.numel() >= 4, "state");
+    IPC_CHECK(blocks >= 1 && blocks <= 256, "blocks");
+    std::memset(&p_, 0, sizeof(p_));
+    p_.world = world;
+    p_.rank = rank;
+    p_.slot_bytes = slot_bytes;
+    auto* st = reinterpret_cast<int64_t*>(state.data_ptr());
+    p_.epoch = reinterpret_cast<uint64_t*>(st + 0);
+    p_.arrive = reinterpret_cast<unsigned int*>(st + 1);
+    p_.depart = reinterpret_cast<unsigned int*>(st + 1) + 1;
+    p_.err = reinterpret_cast<int*>(st + 2);
+  }
+  void set_peer(int p, int64_t inbox, int64_t flags) {
+    IPC_CHECK(p >= 0 && p < p_.world && inbox && flags, "peer");
+    p_.inbox[p] = reinterpret_cast<unsigned char*>(inbox);
+    p_.flags[p] = reinterpret_cast<uint64_t*>(flags);
+  }
+  void check_ready() const {
+    for (int p = 0; p < p_.world; ++p) IPC_CHECK(p_.inbox[p] && p_.flags[p], "peer pointers not set");
+  }
+  // out = scale * sum over ranks of src (f32, <= slot_bytes)
+  void allreduce(const Tensor& src, Tensor out, double scale) {
+    check_ready();
+    IPC_CHECK(src.is_cuda() && src.scalar_type() == torch::kFloat32 && src.is_contiguous(), "src");
+    IPC_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat32 && out.is_contiguous() &&
+                  out.numel() == src.numel(), "out");
+    IPC_CHECK(((uintptr_t)src.data_ptr() & 15) == 0, "src must be 16-byte aligned");
+    const int64_t nb = src.numel() * 4;
+    IPC_CHECK(nb <= p_.slot_bytes, "tensor larger than the mesh slot");
+    launch_ipc_collective(p_, src.data_ptr(), nb, true, reinterpret_cast<float*>(out.data_ptr()), src.numel(),
+                          (float)scale, true, blocks_, at::hip::getCurrentHIPStream().stream());
+  }
+  // all-to-all of fixed slots: send [world][slot_bytes] -> this rank's inbox
+  // parity of this call (returned as the parity index; the caller views it)
+  void exchange(const Tensor& send) {
+    check_ready();
+    IPC_CHECK(send.is_cuda() && send.is_contiguous() && send.nbytes() == (size_t)(p_.world * p_.slot_bytes),
+              "send must be contiguous [world, slot_bytes]");
+    launch_ipc_collective(p_, send.data_ptr(), p_.slot_bytes, false, nullptr, 0, 1.f, false, blocks_,
+                          at::hip::getCurrentHIPStream().stream());
+  }
+
+ private:
+  IpcPeers p_;
+  int blocks_;
+};
+
+}  // namespace
+
+void bind_ipc(py::module& m) {
+  m.def("ipc_handle", &ipc_handle);
+  m.def("ipc_open", &ipc_open);
+  m.def("ipc_close", &ipc_close);
+  py::class_<IpcComm>(m, "IpcComm")
+      .def(py::init<int, int, int64_t, const Tensor&, int>())
+      .def("set_peer", &IpcComm::set_peer)
+      .def("allreduce", &IpcComm::allreduce)
+      .def("exchange", &IpcComm::exchange);
+}
+
+}  // namespace pbx

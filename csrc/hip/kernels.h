@@ -181,6 +181,21 @@ void launch_zero_rows(float* buf, int stride, const int32_t* n_dev, int64_t cap,
 // graph-safe 32-bit fill (use instead of hipMemsetAsync in capturable code)
 void launch_fill32(void* p, uint32_t v, int64_t n_words, hipStream_t s);
 
+// IPC mesh collective (ipc.hip): peer pointers of one node's ranks
+constexpr int kIpcMaxRanks = 8;
+struct IpcPeers {
+  unsigned char* inbox[kIpcMaxRanks];  // each rank's inbox [2][world][slot_bytes]
+  uint64_t* flags[kIpcMaxRanks];       // each rank's flag words [world]
+  int64_t slot_bytes;
+  int world, rank;
+  uint64_t* epoch;       // own, device
+  unsigned int* arrive;  // own, device
+  unsigned int* depart;  // own, device
+  int* err;              // own, device: 1 = a wait timed out
+};
+void launch_ipc_collective(const IpcPeers& pt, const void* send, int64_t nbytes, bool broadcast, float* out,
+                           int64_t nfloat, float scale, bool reduce, int blocks, hipStream_t s);
+
 // device-resident pass (batch_ops.hip): the record store's CSR arrays + the
 // pass order on the GPU
 struct BatchSrc {

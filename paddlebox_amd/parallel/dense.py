@@ -151,11 +151,13 @@ class DenseSync:
     """Data-parallel dense synchronisation over RCCL (or gloo on CPU)."""
 
     def __init__(self, arena: DenseArena, mode: str = "grad_allreduce", k: int = 1, group=None,
-                 overlap_group=None):
+                 overlap_group=None, ipc=None):
         """``overlap_group``: a process group of its own (own communicator) on
         which ``launch()`` runs the gradient all-reduce on a side stream, so it
         overlaps the rest of the backward (the sparse push and its key
-        all-to-all, which use the default group)."""
+        all-to-all, which use the default group).  ``ipc``: an
+        :class:`~paddlebox_amd.parallel.ipc.IpcMesh` whose one-shot all-reduce
+        replaces RCCL's ring for the gradient buffer (intra-node)."""
         self.a = arena
         self.mode = mode
         self.k = max(1, k)
@@ -164,8 +166,15 @@ class DenseSync:
         self.active = collective_active(group)
         self.steps = 0
         self.overlap_group = overlap_group
+        self.ipc = ipc
         self._stream = None
         self._launched = False
+
+    def _allreduce_grad(self, group):
+        if self.ipc is not None:
+            self.ipc.allreduce_(self.a.grad)
+        else:
+            dist.all_reduce(self.a.grad, group=group)
 
     def launch(self):
         """Start the gradient all-reduce now, on a side stream (call when the
@@ -178,7 +187,7 @@ class DenseSync:
             self._stream = torch.cuda.Stream(dev)
         self._stream.wait_stream(cur)
         with torch.cuda.stream(self._stream):
-            dist.all_reduce(self.a.grad, group=self.overlap_group if self.overlap_group is not None else self.group)
+            self._allreduce_grad(self.overlap_group if self.overlap_group is not None else self.group)
         self._launched = True
 
     def grad_scale(self) -> float:
@@ -191,7 +200,7 @@ class DenseSync:
             self._launched = False
             return
         if self.active and self.mode == "grad_allreduce":
-            dist.all_reduce(self.a.grad, group=self.group)
+            self._allreduce_grad(self.group)
 
     def apply(self, opt):
         """Sync + optimizer update for one step, every mode.
