@@ -245,6 +245,43 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("keys", [](const KeyAgent& a) { return to_tensor_u64(a.keys()); })
       .def("size", &KeyAgent::size)
       .def("clear", &KeyAgent::clear);
+  py::class_<ReplicaStore, std::shared_ptr<ReplicaStore>>(m, "ReplicaStore")
+      .def(py::init<int>())
+      .def("dim", &ReplicaStore::dim)
+      .def("size", &ReplicaStore::size)
+      .def("clear", &ReplicaStore::clear)
+      .def("add", [](ReplicaStore& r, const Tensor& v) {
+        req_cpu(v, "row");
+        auto c = v.contiguous().to(torch::kFloat32);
+        return r.add(c.data_ptr<float>(), (int)c.numel());
+      })
+      .def("data", [](const ReplicaStore& r) {
+        auto v = r.data();
+        auto t = torch::empty({(int64_t)v.size() / r.dim(), r.dim()}, torch::kFloat32);
+        if (!v.empty()) memcpy(t.data_ptr(), v.data(), v.size() * 4);
+        return t;
+      });
+  py::class_<InputIndex, std::shared_ptr<InputIndex>>(m, "InputIndex")
+      .def(py::init<int>(), py::arg("dim") = 0)
+      .def("dim", &InputIndex::dim)
+      .def("size", &InputIndex::size)
+      .def("add", [](InputIndex& t, const std::string& k, const Tensor& v) {
+        req_cpu(v, "vec");
+        auto c = v.contiguous().to(torch::kFloat32);
+        return t.add(k, c.data_ptr<float>(), (int)c.numel());
+      })
+      .def("offset", [](const InputIndex& t, const std::string& k) {
+        const uint64_t o = t.offset(k.data(), k.size());
+        return o == InputIndex::kMissing ? (int64_t)-1 : (int64_t)o;
+      })
+      .def("load_text", &InputIndex::load_text, py::call_guard<py::gil_scoped_release>())
+      .def("data", [](const InputIndex& t) {
+        auto v = t.data();
+        const int d = std::max(1, t.dim());
+        auto o = torch::empty({(int64_t)v.size() / d, d}, torch::kFloat32);
+        if (!v.empty()) memcpy(o.data_ptr(), v.data(), v.size() * 4);
+        return o;
+      });
   py::class_<SlotDataset>(m, "SlotDataset")
       .def(py::init<>())
       .def("set_slots", &SlotDataset::set_slots)
@@ -284,6 +321,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_key_agent", [](SlotDataset& d, std::shared_ptr<KeyAgent> a) { d.set_key_agent(std::move(a)); },
            py::arg("agent").none(true))
       .def("version", &SlotDataset::version)
+      .def("set_replica_cache", [](SlotDataset& d, std::shared_ptr<ReplicaStore> r) { d.set_replica_cache(r); },
+           py::arg("store").none(true))
+      .def("set_input_index", [](SlotDataset& d, std::shared_ptr<InputIndex> t) { d.set_input_index(t); },
+           py::arg("table").none(true))
+      .def("load_index_files",
+           [](const SlotDataset& d, const std::vector<std::string>& files, std::shared_ptr<InputIndex> t) {
+             py::gil_scoped_release nogil;
+             return d.load_index_files(files, t.get());
+           })
       .def("dense_refs", [](const SlotDataset& d) {
         auto v = d.dense_refs();
         auto t = torch::empty({(int64_t)v.size() / 4, 4}, torch::kInt32);

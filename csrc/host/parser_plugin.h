@@ -17,6 +17,9 @@
 //         -> number of instances emitted (0 = line dropped), < 0 = parse error
 //   void  pbx_parser_destroy(void* parser);
 //
+// (sink fields appended after `commit` are NULL-checked by a plugin that uses
+// them; plugins built against the 4-callback struct keep working.)
+//
 // For every instance the plugin calls `add_u64` / `add_f32` for the slots it
 // has values for (slot = index into the slot list given at create time; the
 // values of slots the dataset does not use are discarded by the host),
@@ -39,11 +42,27 @@ typedef struct pbx_ins_sink {
                    uint32_t rank);
   // returns 1 if the instance was kept (it has at least one sparse feasign)
   int (*commit)(void* ctx);
+  // GPU replica cache feed (reference SlotPaddleBoxDataFeedWithGpuReplicaCache):
+  // append one cache row, get its offset to store as the instance's feasign.
+  // NULL when the dataset has no replica cache attached.
+  int64_t (*add_cache)(void* ctx, const float* v, int n);
+  // input-index feed (reference InputIndexDataFeed): offset of a string key in
+  // the input table (UINT64_MAX when absent).  NULL when no table is attached.
+  uint64_t (*index_offset)(void* ctx, const char* key, int len);
 } pbx_ins_sink;
+
+// Optional 4th symbol for index files (reference ParseIndexData):
+//   int pbx_parser_parse_index(void* parser, const char* line, size_t len,
+//                              const pbx_index_sink* sink);  -> entries added
+typedef struct pbx_index_sink {
+  void* ctx;
+  void (*add_index)(void* ctx, const char* key, int key_len, const float* v, int n);
+} pbx_index_sink;
 
 typedef void* (*pbx_parser_create_fn)(int, const char* const*, const char*);
 typedef int (*pbx_parser_parse_line_fn)(void*, const char*, size_t, const pbx_ins_sink*);
 typedef void (*pbx_parser_destroy_fn)(void*);
+typedef int (*pbx_parser_parse_index_fn)(void*, const char*, size_t, const pbx_index_sink*);
 
 #ifdef __cplusplus
 }

@@ -146,6 +146,7 @@ struct SlotDataset::Plugin {
   void* parser = nullptr;
   pbx_parser_parse_line_fn parse = nullptr;
   pbx_parser_destroy_fn destroy = nullptr;
+  pbx_parser_parse_index_fn parse_index = nullptr;
   ~Plugin() {
     if (parser && destroy) destroy(parser);
     if (so) dlclose(so);
@@ -161,6 +162,8 @@ struct SinkCtx {
   bool keep_ins_id;
   bool need_sparse;
   RecordStore* st;
+  ReplicaStore* replica = nullptr;
+  const InputIndex* index = nullptr;
   std::vector<std::vector<uint64_t>> u;
   std::vector<std::vector<float>> f;
   std::string ins_id;
@@ -203,6 +206,20 @@ void sink_set_meta(void* c, const char* id, int len, uint64_t sid, uint32_t cm, 
   s->rk = rk;
 }
 
+int64_t sink_add_cache(void* c, const float* v, int n) {
+  SinkCtx* s = (SinkCtx*)c;
+  return s->replica ? s->replica->add(v, n) : -1;
+}
+
+uint64_t sink_index_offset(void* c, const char* key, int len) {
+  SinkCtx* s = (SinkCtx*)c;
+  return s->index && key && len > 0 ? s->index->offset(key, (size_t)len) : InputIndex::kMissing;
+}
+
+void index_add(void* c, const char* key, int len, const float* v, int n) {
+  if (key && len > 0) ((InputIndex*)c)->add(std::string(key, (size_t)len), v, n);
+}
+
 int sink_commit(void* c) {
   SinkCtx* s = (SinkCtx*)c;
   int ok = !(s->need_sparse && s->sparse == 0);
@@ -236,6 +253,7 @@ void SlotDataset::set_so_parser(const std::string& path) {
   auto create = (pbx_parser_create_fn)dlsym(pl->so, "pbx_parser_create");
   pl->parse = (pbx_parser_parse_line_fn)dlsym(pl->so, "pbx_parser_parse_line");
   pl->destroy = (pbx_parser_destroy_fn)dlsym(pl->so, "pbx_parser_destroy");
+  pl->parse_index = (pbx_parser_parse_index_fn)dlsym(pl->so, "pbx_parser_parse_index");  // optional
   if (!create || !pl->parse || !pl->destroy)
     throw std::runtime_error("so parser " + path + ": missing pbx_parser_{create,parse_line,destroy}");
   std::vector<const char*> names;
@@ -257,14 +275,48 @@ bool SlotDataset::parse_plugin_line(const char* line, size_t len, RecordStore* s
   ctx.keep_ins_id = parse_.parse_ins_id || parse_.parse_logkey;
   ctx.need_sparse = !sparse_slots_.empty();
   ctx.st = st;
+  ctx.replica = replica_.get();
+  ctx.index = input_index_.get();
   ctx.u.resize(store_.nu);
   ctx.f.resize(store_.nf);
   ctx.clear();
   ctx.kept = 0;
-  pbx_ins_sink sink{&ctx, sink_add_u64, sink_add_f32, sink_set_meta, sink_commit};
+  pbx_ins_sink sink{&ctx,          sink_add_u64,
+                    sink_add_f32,  sink_set_meta,
+                    sink_commit,   replica_ ? sink_add_cache : nullptr,
+                    input_index_ ? sink_index_offset : nullptr};
   const int n = plugin_->parse(plugin_->parser, line, len, &sink);
   ctx.clear();  // an instance the plugin never committed is discarded
   return n > 0 && ctx.kept > 0;
+}
+
+int64_t SlotDataset::load_index_files(const std::vector<std::string>& files, InputIndex* t) const {
+  if (!plugin_ || !plugin_->parse_index) return t->load_text(files, threads_);
+  std::atomic<size_t> next{0};
+  std::atomic<int64_t> n{0};
+  std::vector<std::thread> th;
+  const int T = std::max(1, std::min<int>(threads_, (int)files.size()));
+  for (int k = 0; k < T; ++k)
+    th.emplace_back([&] {
+      const pbx_index_sink sink{t, index_add};
+      for (;;) {
+        const size_t fi = next++;
+        if (fi >= files.size()) break;
+        FILE* fp = fopen(files[fi].c_str(), "r");
+        if (!fp) continue;
+        char* line = nullptr;
+        size_t cap = 0;
+        ssize_t len;
+        while ((len = getline(&line, &cap, fp)) > 0) {
+          const int r = plugin_->parse_index(plugin_->parser, line, (size_t)len, &sink);
+          if (r > 0) n += r;
+        }
+        free(line);
+        fclose(fp);
+      }
+    });
+  for (auto& x : th) x.join();
+  return n.load();
 }
 
 bool SlotDataset::parse_line(const char* str, size_t len, RecordStore* st) const {

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "key_agent.h"
+#include "side_tables.h"
 
 namespace pbx {
 
@@ -91,6 +92,13 @@ class SlotDataset {
   // feed-pass agent: while set, the loader threads register the sparse
   // feasigns of every record they parse (load / preload / add_lines / archive)
   void set_key_agent(std::shared_ptr<KeyAgent> a) { agent_ = std::move(a); }
+  // side tables a parser plugin fills / queries while loading (replica-cache
+  // and input-index data feeds)
+  void set_replica_cache(std::shared_ptr<ReplicaStore> r) { replica_ = std::move(r); }
+  void set_input_index(std::shared_ptr<InputIndex> t) { input_index_ = std::move(t); }
+  // index files into `t` (InputTableDataFeed): the plugin's parse_index when
+  // it has one, else "key v1 ... vD" text lines
+  int64_t load_index_files(const std::vector<std::string>& files, InputIndex* t) const;
 
   // order of records for this pass (shuffle: Fisher-Yates with seed)
   void shuffle(uint64_t seed);
@@ -175,6 +183,8 @@ class SlotDataset {
   int64_t bad_lines_ = 0;
   uint64_t version_ = 0;
   std::shared_ptr<KeyAgent> agent_;
+  std::shared_ptr<ReplicaStore> replica_;
+  std::shared_ptr<InputIndex> input_index_;
   void register_keys(const RecordStore& st, int64_t r0, int64_t r1, KeyAgent::Stage* stg) const;
 };
 

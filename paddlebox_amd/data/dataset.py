@@ -24,6 +24,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
+from ..utils import flags as _flags
 from ..utils.dayid import make_day_id_str
 
 
@@ -254,9 +255,27 @@ class PadBoxSlotDataset(DatasetBase):
             self._native.set_key_agent(agent.native)
         else:  # no native agent: walk the store after the load
             agent._collect_from = self
+        self._attach_side_tables(agent)
         return agent
 
+    def _attach_side_tables(self, agent):
+        """Replica-cache / input-index data feeds (data_feed.cc:4155-4635):
+        with FLAGS_use_gpu_replica_cache the pass gets a fresh native replica
+        store the parser plugin appends cache rows to; an input table the box
+        holds is queried for string-key offsets."""
+        h = _native.host()
+        if _flags.get_bool("use_gpu_replica_cache"):
+            agent.replica = h.ReplicaStore(int(_flags.get("gpu_replica_cache_dim")))
+            self._native.set_replica_cache(agent.replica)
+        tab = getattr(self.box, "_input_table", None)
+        if tab is not None and getattr(tab, "native", None) is not None:
+            self._native.set_input_index(tab.native)
+
     def _close_feed_pass(self, agent):
+        self._native.set_replica_cache(None)
+        self._native.set_input_index(None)
+        if getattr(agent, "replica", None) is not None:
+            self.box.replica_cache.load_native(agent.replica)
         if getattr(agent, "_collect_from", None) is self:
             agent.add_keys(self.collect_keys())
         if getattr(self.box, "auc_runner", None) is not None:
@@ -482,9 +501,17 @@ class InputTableDataset(PadBoxSlotDataset):
     def set_index_parser_files(self, files):
         self.index_files = list(files)
 
-    def load_index_into_memory(self, table):
-        for f in self.index_files:
-            table.load_text(f)
+    def load_index_into_memory(self, table=None):
+        """InputTableDataFeed: index files into the box's input table (the
+        parser plugin's parse_index when it has one, else "key v1..vD")."""
+        if not self._configured:
+            self._configure()
+        table = table if table is not None else self.box.input_table
+        if getattr(table, "native", None) is not None:
+            n = int(self._native.load_index_files(list(self.index_files), table.native))
+            table.dim = int(table.native.dim())
+            return n
+        return sum(table.load_text(f) for f in self.index_files)
 
 
 class DatasetFactory:

@@ -36,6 +36,16 @@ class GpuReplicaCache:
         self._n += a.shape[0]
         return off
 
+    def load_native(self, store):
+        """Rows a data feed appended to a native ReplicaStore during the load
+        (replica-cache data feed; offsets are the instances' feasigns)."""
+        data = store.data()
+        self.dim = int(data.shape[1])  # a pass's cache takes the feed's row width
+        self._host = [data.numpy()]
+        self._n = data.shape[0]
+        self.table = None
+        return self
+
     def to_hbm(self):
         data = np.concatenate(self._host, 0) if self._host else np.zeros((0, self.dim), np.float32)
         self.table = torch.from_numpy(data).to(self.device)
@@ -55,42 +65,86 @@ class GpuReplicaCache:
 
 
 class InputTable:
+    """String key -> dense vector table for ``lookup_input``.  Backed by the
+    native ``InputIndex`` (csrc/host/side_tables.cc) that the loader threads
+    query while parsing (input-index data feed); lookups gather from an HBM
+    copy of the rows (refreshed when rows were added) instead of a host
+    gather + H2D per call."""
+
     def __init__(self, dim: int = 0):
+        from .. import _native
+
+        self.native = _native.host().InputIndex(int(dim)) if _native.host_available() else None
+        self._py_index: Dict[str, int] = {}
+        self._py_rows: List[np.ndarray] = []
         self.dim = int(dim)
-        self.index: Dict[str, int] = {}
-        self._rows: List[np.ndarray] = []
-        self._data: Optional[np.ndarray] = None
+        self._dev: Dict[str, torch.Tensor] = {}
+        self._dev_n = -1
 
     def set_dim(self, dim: int):
         self.dim = int(dim)
+        if self.native is not None and self.native.size() == 0:
+            from .. import _native
+
+            self.native = _native.host().InputIndex(self.dim)
 
     def add_index_data(self, key: str, vec) -> int:
-        v = np.asarray(vec, dtype=np.float32).reshape(-1)
+        v = torch.as_tensor(np.asarray(vec, dtype=np.float32).reshape(-1))
+        if self.native is not None:
+            off = int(self.native.add(key, v))
+            self.dim = int(self.native.dim())
+            return off
         if self.dim == 0:
-            self.dim = v.size
-        if key in self.index:
-            return self.index[key]
-        off = len(self._rows)
-        self.index[key] = off
-        self._rows.append(v[: self.dim])
-        self._data = None
-        return off
+            self.dim = v.numel()
+        if key not in self._py_index:
+            self._py_index[key] = len(self._py_rows)
+            self._py_rows.append(v.numpy()[: self.dim])
+        return self._py_index[key]
+
+    def load_text(self, path: str, threads: int = 4) -> int:
+        if self.native is not None:
+            n = int(self.native.load_text([path], threads))
+            self.dim = int(self.native.dim())
+            return n
+        n = 0
+        with open(path) as f:
+            for line in f:
+                t = line.split()
+                if t:
+                    self.add_index_data(t[0], [float(x) for x in t[1:]])
+                    n += 1
+        return n
 
     def get_offset(self, key: str) -> int:
-        return self.index.get(key, -1)
-
-    def lookup(self, ids: torch.Tensor, size: int, device) -> torch.Tensor:
-        if self._data is None:
-            self._data = np.stack(self._rows, 0) if self._rows else np.zeros((0, self.dim), np.float32)
-        idx = ids.reshape(-1).cpu().numpy().astype(np.int64)
-        out = np.zeros((idx.size, size), np.float32)
-        ok = (idx >= 0) & (idx < self._data.shape[0])
-        w = min(size, self.dim)
-        out[ok, :w] = self._data[idx[ok], :w]
-        return torch.from_numpy(out).to(device)
+        if self.native is not None:
+            return int(self.native.offset(key))
+        return self._py_index.get(key, -1)
 
     def size(self) -> int:
-        return len(self._rows)
+        return int(self.native.size()) if self.native is not None else len(self._py_rows)
+
+    def rows(self) -> torch.Tensor:
+        if self.native is not None:
+            return self.native.data()
+        return torch.from_numpy(np.stack(self._py_rows, 0)) if self._py_rows else torch.zeros(0, max(self.dim, 1))
+
+    def lookup(self, ids: torch.Tensor, size: int, device) -> torch.Tensor:
+        device = torch.device(device)
+        n = self.size()
+        key = str(device)
+        if self._dev_n != n or key not in self._dev:
+            self._dev = {key: self.rows().to(device)}
+            self._dev_n = n
+        data = self._dev[key]
+        idx = ids.reshape(-1).to(device).long()
+        ok = (idx >= 0) & (idx < data.shape[0])
+        rows = data.index_select(0, idx.clamp(0, max(data.shape[0] - 1, 0))) if data.shape[0] else \
+            torch.zeros(idx.numel(), max(self.dim, 1), device=device)
+        rows = rows * ok.unsqueeze(1).to(rows.dtype)
+        w = min(size, rows.shape[1])
+        out = torch.zeros(idx.numel(), size, device=device)
+        out[:, :w] = rows[:, :w]
+        return out
 
 
 class _PullExtended(torch.autograd.Function):

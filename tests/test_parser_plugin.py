@@ -67,3 +67,89 @@ def test_padbox_dataset_so_parser(plugin, tmp_path):
     assert len(ds) == 20
     b = ds.build_batch(0, 8)
     assert b.keys.numel() == 8 * 26
+
+
+@pytest.fixture(scope="module")
+def side_plugin(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("plug2") / "replica_index_parser.so")
+    subprocess.run(["g++", "-O2", "-shared", "-fPIC", "-I" + os.path.join(ROOT, "csrc", "host"),
+                    os.path.join(ROOT, "csrc", "plugins", "replica_index_parser.cc"), "-o", out], check=True)
+    return out
+
+
+def test_replica_cache_and_input_index_feeds(side_plugin, tmp_path):
+    """Replica-cache and input-index data feeds (reference
+    SlotPaddleBoxDataFeedWithGpuReplicaCache / InputIndexDataFeed /
+    InputTableDataFeed): the plugin appends each instance's cache vector to
+    the pass's replica store and stores the row offset as a feasign; string
+    keys resolve to input-table offsets while parsing."""
+    from paddlebox_amd.ps.extras import GpuReplicaCache, InputTable
+
+    h = _native.host()
+    slots = [h.SlotDesc("label", "uint64", True, True, 1), h.SlotDesc("cache_off", "uint64", True, False, 1),
+             h.SlotDesc("qidx", "uint64", True, False, 1), h.SlotDesc("s0", "uint64", True, False, 1),
+             h.SlotDesc("s1", "uint64", True, False, 1)]
+    d = h.SlotDataset()
+    d.set_slots(slots)
+    d.set_so_parser(side_plugin)
+    idx_file = tmp_path / "index.txt"
+    idx_file.write_text("kA 1 2 3\nkB 4 5 6\nkA 9 9 9\n")
+    table = InputTable()
+    assert d.load_index_files([str(idx_file)], table.native) == 3
+    assert table.size() == 2 and table.get_offset("kB") == 1 and table.get_offset("kZ") == -1
+    rep = h.ReplicaStore(4)
+    d.set_replica_cache(rep)
+    d.set_input_index(table.native)
+    lines = ["1 kB 4 0.1 0.2 0.3 0.4 2 11 12 1 13", "0 kZ 3 1 2 3 1 21 1 22", "1 kA 4 5 6 7 8 1 31 1 32"]
+    assert d.add_lines(lines) == 3
+    keys, lod, dense = d.build_batch(0, 3, False)
+    L = lod.view(4, 4)  # sparse slots: cache_off, qidx, s0, s1
+    cache_keys = keys[int(L[0, 0]):int(L[0, 3])].tolist()
+    assert sorted(cache_keys) == [0, 1, 2]
+    rows = rep.data()
+    assert rows.shape == (3, 4)
+    want = {0: [0.1, 0.2, 0.3, 0.4], 1: [1, 2, 3, 0], 2: [5, 6, 7, 8]}  # short vector zero padded
+    for i, off in enumerate(cache_keys):
+        torch.testing.assert_close(rows[off], torch.tensor(want[i], dtype=torch.float32))
+    # qidx: line 0 -> kB (1), line 1 -> kZ absent (no feasign), line 2 -> kA (0)
+    assert [int(L[1, i + 1] - L[1, i]) for i in range(3)] == [1, 0, 1]
+    assert keys[int(L[1, 0]):int(L[1, 3])].tolist() == [1, 0]
+    # the BoxWrapper-side tables serve the rows: replica cache pull, lookup_input
+    rc = GpuReplicaCache(4).load_native(rep)
+    torch.testing.assert_close(rc.pull(torch.tensor(cache_keys), 4), rows[torch.tensor(cache_keys)])
+    got = table.lookup(torch.tensor([1, 0, -1]), 3, "cpu")
+    torch.testing.assert_close(got, torch.tensor([[4.0, 5, 6], [1, 2, 3], [0, 0, 0]]))
+
+
+def test_replica_cache_feed_through_the_feed_pass(side_plugin, tmp_path):
+    """FLAGS_use_gpu_replica_cache: the feed pass gives the loader a fresh
+    replica store; at EndFeedPass the box's replica cache holds its rows."""
+    import paddlebox_amd.fluid as fluid
+    from paddlebox_amd.ps.box_wrapper import BoxWrapper
+    from paddlebox_amd.utils.flags import set_flags
+
+    f = tmp_path / "part-0.txt"
+    f.write_text("\n".join(f"{i % 2} k{i} 4 {i} {i + 1} {i + 2} {i + 3} 1 {100 + i} 1 {200 + i}"
+                           for i in range(10)) + "\n")
+    box = fluid.core.BoxWrapper(8, device="cpu", new=True)
+    set_flags({"FLAGS_use_gpu_replica_cache": True, "FLAGS_gpu_replica_cache_dim": 4})
+    try:
+        box.initialize_gpu_and_load_model(slot_vector=[0, 1, 2], max_keys=10000)
+        ds = PadBoxSlotDataset(rank=0, world=1)
+        ds.set_use_var([SlotVar("label", "int64", (1,), 0), SlotVar("cache_off", "int64", (1,), 1),
+                        SlotVar("s0", "int64", (1,), 1), SlotVar("s1", "int64", (1,), 1)])
+        ds.set_so_parser_name(side_plugin)
+        ds.set_filelist([str(f)])
+        ds.set_batch_size(5)
+        ds.box = box
+        ds.load_into_memory()
+        assert len(box.replica_cache) == 10
+        b = ds.build_batch(0, 10)
+        offs = b.keys[:10]  # cache_off is the first sparse slot, one feasign per instance
+        rows = box.replica_cache.pull(offs, 4)
+        first = rows[:, 0].tolist()
+        assert sorted(first) == [float(i) for i in range(10)]
+        torch.testing.assert_close(rows[:, 1] - rows[:, 0], torch.ones(10))
+    finally:
+        set_flags({"FLAGS_use_gpu_replica_cache": False})
+        BoxWrapper._instance = None
