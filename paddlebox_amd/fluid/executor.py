@@ -144,6 +144,7 @@ class Session:
         self.data_vars = [v for v in program.global_block().vars.values() if v.is_data]
         self.box = box
         self._one = None
+        self.op_profiler = None  # runtime.op_profiler.OpProfiler in the trainer's profile mode
 
     # -------------------------------------------------------------- params
     def _materialize(self):
@@ -272,14 +273,27 @@ class Session:
 
     # -------------------------------------------------------------- run
     def forward(self, ctx: ExecContext):
+        prof = self.op_profiler
+        if prof is None:
+            for op in self.lowered.steps:
+                KERNELS[op.type](ctx, op)
+            return
         for op in self.lowered.steps:
+            t0 = prof.begin()
             KERNELS[op.type](ctx, op)
+            prof.end(op.type, t0)
+            if ctx.training:
+                names = op.output_arg_names
+                names = names() if callable(names) else names
+                prof.watch_grad(op.type + "_grad", [ctx.env[n] for n in names if n in ctx.env])
 
     def step(self, ctx: ExecContext):
         """forward + backward + dense sync + optimizer (one training batch)."""
         self.forward(ctx)
         if not (self.training and ctx.training):
             return
+        prof = self.op_profiler
+        t0 = prof.begin() if prof is not None else None
         loss = ctx.get(self.program._optimize["loss"])
         loss = loss.values if isinstance(loss, Ragged) else loss
         for a, o in zip(self.arenas, self.opts):
@@ -291,8 +305,13 @@ class Session:
             loss.backward(self._one)  # persistent seed: no fill kernel per step
         else:
             loss.float().sum().backward()
+        if prof is not None:
+            prof.end("backward (all grad ops + sparse push)", t0)
+            t0 = prof.begin()
         for s, o in zip(self.syncs, self.opts):
             s.apply(o)
+        if prof is not None:
+            prof.end("dense sync + optimizer", t0)
 
     def fetch(self, ctx: ExecContext, fetch_list, return_numpy=True):
         out = []

@@ -187,6 +187,8 @@ class BoxPSWorker:
         t, s = self.t, self.s
         if not t.use_graph:
             return "graph capture disabled"
+        if t.profile:
+            return "profile mode times every op"
         if s.device.type != "cuda":
             return "not a GPU session"
         if t.infer or t.async_dense is not None:
@@ -431,6 +433,22 @@ class BoxPSWorker:
     def _train_files_eager(self) -> Dict[str, float]:
         t = self.t
         s = self.s
+        if t.profile and s.op_profiler is None:
+            from .op_profiler import OpProfiler
+
+            s.op_profiler = OpProfiler(s.device)
+        try:
+            stats = self._train_files_eager_loop()
+        finally:
+            prof, s.op_profiler = s.op_profiler, None
+        if prof is not None:
+            stats["op_profile"] = prof.report()
+            log.info("per-op profile (%d batches):\n%s", self.batches, prof.format())
+        return stats
+
+    def _train_files_eager_loop(self) -> Dict[str, float]:
+        t = self.t
+        s = self.s
         box = t.box
         ds = t.dataset
         dev = s.device
@@ -588,6 +606,15 @@ class BoxPSTrainer:
             ddir = os.path.join(self.desc.dump_fields_path, f"rank{self.rank:03d}")
             os.makedirs(ddir, exist_ok=True)
             self.dumper = _native.host().DumpWriter(ddir, dev_id, max(1, self.desc.dump_thread_num))
+        # profile mode (reference TrainFilesWithProfiler, entered with
+        # train_from_dataset(debug=True) or TrainerDesc.profile): per-op times
+        self.profile = bool(debug or self.desc.profile)
+        if self.session.device.type == "cuda" and _flags.get_bool("enable_binding_train_cpu"):
+            from .affinity import bind_worker
+
+            lr = int(os.environ.get("LOCAL_RANK", "0"))
+            lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+            bind_worker(self.session.device, lr, lw)
         self.worker = BoxPSWorker(self)
 
     def _sync_policy(self):

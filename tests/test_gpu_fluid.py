@@ -113,3 +113,32 @@ def test_tower_lowering_matches_unfused_program(tmp_path):
         assert abs(outs[True][1] - outs[False][1]) < 2e-2
     finally:
         BoxWrapper._instance = None
+
+
+def test_profile_mode_on_gpu(tmp_path):
+    """train_from_dataset(debug=True): eager steps with every lowered op and
+    its grad op timed by HIP events."""
+    tmp_path.mkdir(parents=True, exist_ok=True)
+    box = _box()
+    try:
+        scope = fluid.Scope()
+        main, startup, slots, label, dense, pred, loss = _build()
+        exe = fluid.Executor(fluid.CUDAPlace(0))
+        exe.run(startup, scope=scope)
+        ds = fluid.DatasetFactory().create_dataset("PadBoxSlotDataset")
+        ds.set_use_var([label] + slots + [dense])
+        ds.set_batch_size(64)
+        ds.set_filelist(_files(tmp_path, 1, 320))
+        ds.disable_shuffle()
+        boxps = fluid.core.BoxPS(ds)
+        boxps.read_ins_into_memory()
+        boxps.begin_pass()
+        st = exe.train_from_dataset(main, ds, scope=scope, debug=True, print_period=1000)
+        boxps.end_pass()
+        prof = st["op_profile"]
+        assert st["batches"] == 5 and st.get("graph_replays", 0) == 0
+        assert prof["dense sync + optimizer"]["calls"] == 5
+        assert any(k.endswith("_grad") for k in prof)
+        assert all(r["ms"] >= 0 for r in prof.values())
+    finally:
+        BoxWrapper._instance = None
