@@ -12,6 +12,7 @@ from . import contrib, core, initializer, io, layers, optimizer, transpiler  # n
 from .dataset import DatasetFactory  # noqa: F401
 from .transpiler import DistributeTranspiler, DistributeTranspilerConfig  # noqa: F401
 from .executor import CompiledProgram, Executor  # noqa: F401
+from . import collective_kernels  # noqa: F401,E402  (registers the c_* op kernels)
 from .framework import (CPUPlace, CUDAPinnedPlace, CUDAPlace, LoDTensor, Parameter, ParamAttr,  # noqa: F401
                         Program, Scope, Variable, WeightNormParamAttr, cpu_places, create_lod_tensor, cuda_places,
                         default_main_program, default_startup_program, global_scope, in_dygraph_mode,

@@ -147,6 +147,60 @@ class FlatAdam:
         self.pows.copy_(sd["pows"])
 
 
+class HierarchicalAllReduce:
+    """Node-aware all-reduce: reduce-scatter inside the node (xGMI), all-reduce
+    of each shard across nodes between the ranks with the same local index,
+    all-gather inside the node.  Nodes are consecutive blocks of
+    ``local_size`` ranks (torchrun's LOCAL_WORLD_SIZE).  gloo (CPU tests)
+    has no reduce-scatter: the node reduce is an all-reduce there and each
+    rank keeps its shard."""
+
+    def __init__(self, group=None, local_size: int = 0):
+        import os
+
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        ls = int(local_size or os.environ.get("LOCAL_WORLD_SIZE", self.world))
+        if ls <= 0 or self.world % ls:
+            ls = self.world
+        self.local_size = ls
+        self.nodes = self.world // ls
+        ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.world))
+        self.node_group = self.cross_group = None
+        for n in range(self.nodes):  # every rank creates every group (collective new_group)
+            g = dist.new_group(ranks[n * ls:(n + 1) * ls])
+            if n == self.rank // ls:
+                self.node_group = g
+        for i in range(ls):
+            g = dist.new_group([ranks[n * ls + i] for n in range(self.nodes)])
+            if i == self.rank % ls:
+                self.cross_group = g
+        self.gloo = dist.get_backend(group) == "gloo"
+
+    def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
+        ls, li = self.local_size, self.rank % self.local_size
+        n = t.numel()
+        part = (n + ls - 1) // ls
+        flat = t.view(-1)
+        pad = part * ls - n
+        buf = torch.cat([flat, flat.new_zeros(pad)]) if pad else flat
+        shard = buf.new_empty(part)
+        if self.gloo:
+            tmp = buf.clone()
+            dist.all_reduce(tmp, group=self.node_group)
+            shard.copy_(tmp[li * part:(li + 1) * part])
+        else:
+            dist.reduce_scatter_tensor(shard, buf, group=self.node_group)
+        if self.nodes > 1:
+            dist.all_reduce(shard, group=self.cross_group)
+        out = buf if pad else buf.new_empty(buf.numel())
+        dist.all_gather_into_tensor(out, shard, group=self.node_group) if not self.gloo else \
+            dist.all_gather(list(out.view(ls, part)), shard, group=self.node_group)
+        flat.copy_(out[:n])
+        return t
+
+
 class DenseSync:
     """Data-parallel dense synchronisation over RCCL (or gloo on CPU)."""
 
@@ -169,6 +223,7 @@ class DenseSync:
         self.ipc = ipc
         self._stream = None
         self._launched = False
+        self.hier = HierarchicalAllReduce(group) if mode == "kstep_node" and self.active else None
 
     def _allreduce_grad(self, group):
         if self.ipc is not None:
@@ -224,15 +279,24 @@ class DenseSync:
 
     def after_step(self):
         self.steps += 1
-        if self.active and self.mode in ("kstep", "local_sgd") and self.steps % self.k == 0:
+        if self.active and self.mode in ("kstep", "local_sgd", "kstep_node") and self.steps % self.k == 0:
             self.sync_params()
 
     def sync_params(self):
-        """Parameter averaging (boxps_worker.cc:1235-1239: sum then x 1/devices)."""
-        if self.active:
+        """Parameter averaging (boxps_worker.cc:1235-1239: sum then x 1/devices).
+        ``kstep_node`` (sync_dense_mode 1 across nodes, :1211-1228): the
+        node's GPUs reduce-scatter the parameters, each shard is all-reduced
+        with the same shard of every other node, and the node all-gathers
+        the result -- the cross-node traffic is 1/local_size of the buffer
+        per GPU, in parallel over the node's GPUs."""
+        if not self.active:
+            return
+        if self.mode == "kstep_node" and self.hier is not None:
+            self.hier.allreduce_(self.a.flat)
+        else:
             dist.all_reduce(self.a.flat, group=self.group)
-            self.a.flat.mul_(1.0 / self.world)
-            self.a.notify_modified()
+        self.a.flat.mul_(1.0 / self.world)
+        self.a.notify_modified()
 
 
 class FlatSGD:

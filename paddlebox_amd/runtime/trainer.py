@@ -626,7 +626,13 @@ class BoxPSTrainer:
         if d.sync_dense_mode in (SYNC_KSTEP_ALL,):
             return "kstep", d.sync_weight_step
         if d.sync_dense_mode == SYNC_KSTEP_NODE:
-            return "none", 1  # single node: nothing crosses nodes
+            # reference SyncParam returns early on one node; across nodes the
+            # k-step parameter average is hierarchical (node reduce-scatter,
+            # cross-node shard all-reduce, node all-gather)
+            local = int(os.environ.get("LOCAL_WORLD_SIZE", self.world))
+            if local <= 0 or self.world <= local:
+                return "none", 1
+            return "kstep_node", d.sync_weight_step
         if d.sync_dense_mode == SYNC_DATA_NORM:
             return "none", 1
         return "grad_allreduce", 1
