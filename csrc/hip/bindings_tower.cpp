@@ -131,7 +131,7 @@ class TowerWorkspace {
   Tensor backward(const c10::optional<Tensor>& dloss, const Tensor& w_out, const std::vector<Tensor>& dW,
                   const std::vector<Tensor>& db, const Tensor& dw_out, const Tensor& db_out, bool need_dx,
                   const c10::optional<Tensor>& dn_part,
-                  int64_t dn_rows, double dn_eps, const c10::optional<Tensor>& dn_stats) {
+                  int64_t dn_rows, double dn_eps, const c10::optional<Tensor>& dn_stats, int64_t parts) {
     TW_CHECK((int)dW.size() == L_ && (int)db.size() == L_, "backward: layer count");
     TowerArgs a = base();
     for (int l = 0; l < L_; ++l) {
@@ -160,9 +160,12 @@ class TowerWorkspace {
       a.dn_eps = (float)dn_eps;
       a.dn_stats = OP<float>(dn_stats);
     }
+    // parts: bit 0 = dX chain (k_tower_bwd), bit 1 = dW / bias / data_norm
+    // reductions (k_tower_dw); the caller may issue them on different streams
+    // (dW overlapped with the head backward + sparse push), bwd first
     auto s = stream();
-    launch_tower_bwd(a, s);
-    launch_tower_dw(a, s);
+    if (parts & 1) launch_tower_bwd(a, s);
+    if (parts & 2) launch_tower_dw(a, s);
     return need_dx ? dx0_ : Tensor();
   }
 
@@ -301,7 +304,7 @@ void bind_tower(py::module& m) {
       .def("backward", &TowerWorkspace::backward, py::arg("dloss"), py::arg("w_out"), py::arg("dW"), py::arg("db"),
            py::arg("dw_out"),
            py::arg("db_out"), py::arg("need_dx"), py::arg("dn_part") = py::none(), py::arg("dn_rows") = 0,
-           py::arg("dn_eps") = 0.0, py::arg("dn_stats") = py::none())
+           py::arg("dn_eps") = 0.0, py::arg("dn_stats") = py::none(), py::arg("parts") = 3)
       .def("pack_regions", &TowerWorkspace::pack_regions)
       .def("x0", &TowerWorkspace::x0)
       .def("x0mp", &TowerWorkspace::x0mp)

@@ -19,6 +19,7 @@ CPU tensors run the same math in plain fp32 PyTorch.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -26,6 +27,7 @@ import torch.distributed as dist
 
 from .. import _native
 from ..parallel.comm import collective_active
+from ..parallel.dense import add_grad_producer, join_grad_producers
 from . import reference as ref
 
 
@@ -38,6 +40,8 @@ class _CtrTowerFn(torch.autograd.Function):
     def forward(ctx, x, extra, label, t: "CtrTower", *params):
         h = _native.hip()
         mlp, dn = t.mlp, t.dn
+        if x.is_cuda:
+            join_grad_producers()  # a previous dW still reading the activations (no optimizer step between)
         B = x.shape[0]
         ws = mlp.tower_workspace(B, x.device)
         mlp.ensure_packed()
@@ -80,18 +84,35 @@ class _CtrTowerFn(torch.autograd.Function):
         if gl is not None:
             gl = gl.contiguous().float().view(1)
         dn_on = dn is not None and dn.training and dn.update_norm
-        dx0 = ws.backward(gl, mlp.w_out.detach().view(-1), [w.grad for w in mlp.w], [b.grad for b in mlp.b],
-                          mlp.w_out.grad.view(-1),
-                          mlp.b_out.grad, True, t._dn_part(B, x.device) if dn_on else None,
-                          h.head_blocks(B) if dn_on else 0, dn.eps if dn is not None else 0.0,
-                          dn.stats if dn_on else None)
-        if dn_on and not getattr(dn, "stats_in_grad_bucket", False):
-            if dn.sync_stats and dn.group is not None and collective_active(dn.group):
-                dist.all_reduce(dn.stats, group=dn.group)
-        if dn_on and not dn.fused_update:
-            h.data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, dn.stats, dn.decay)
-        if t.on_dense_grads is not None:  # e.g. start the dense all-reduce, overlapped with the sparse push
-            t.on_dense_grads()
+        args = (gl, mlp.w_out.detach().view(-1), [w.grad for w in mlp.w], [b.grad for b in mlp.b],
+                mlp.w_out.grad.view(-1), mlp.b_out.grad, True, t._dn_part(B, x.device) if dn_on else None,
+                h.head_blocks(B) if dn_on else 0, dn.eps if dn is not None else 0.0, dn.stats if dn_on else None)
+
+        def dense_tail():
+            if dn_on and not getattr(dn, "stats_in_grad_bucket", False):
+                if dn.sync_stats and dn.group is not None and collective_active(dn.group):
+                    dist.all_reduce(dn.stats, group=dn.group)
+            if dn_on and not dn.fused_update:
+                h.data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, dn.stats, dn.decay)
+            if t.on_dense_grads is not None:  # e.g. start the dense all-reduce, overlapped with the sparse push
+                t.on_dense_grads()
+
+        if t.overlap_dw and x.is_cuda:
+            # dX chain on the compute stream; the dW GEMMs + bias / data_norm
+            # reductions (and whatever consumes the dense grads) on a side
+            # stream, concurrent with the head backward and the sparse push;
+            # the optimizer joins it (parallel.dense.join_grad_producers)
+            cur = torch.cuda.current_stream(x.device)
+            dx0 = ws.backward(*args, parts=1)
+            side = t._side_stream(x.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                ws.backward(*args, parts=2)
+                dense_tail()
+            add_grad_producer(side)
+        else:
+            dx0 = ws.backward(*args)
+            dense_tail()
         use_lin = t.use_head_lin and not ctx.has_extra
         dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim),
                            ctx.means, ctx.scales, dn.eps if dn is not None else 0.0, dlin_scale=gl,
@@ -114,8 +135,17 @@ class CtrTower:
         # called in the backward once every dense gradient (and data_norm
         # statistic) of the tower is final, before the sparse push runs
         self.on_dense_grads = None
+        # run the dW GEMM on a side stream, overlapped with the head backward
+        # and the sparse push (PBX_TOWER_OVERLAP_DW=0 turns it off)
+        self.overlap_dw = os.environ.get("PBX_TOWER_OVERLAP_DW", "1") != "0"
+        self._side = None
         self._part = None
         self._params = list(mlp.parameters())
+
+    def _side_stream(self, dev):
+        if self._side is None:
+            self._side = torch.cuda.Stream(dev)
+        return self._side
 
     def _dn_part(self, B, device):
         h = _native.hip()

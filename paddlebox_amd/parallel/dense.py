@@ -25,6 +25,23 @@ from ..ops import reference as ref
 from .comm import collective_active
 
 
+# Side streams still writing dense gradients (the tower's dW GEMM runs there,
+# overlapped with the head backward + sparse push).  Anything that reads the
+# gradients or rewrites the parameters joins them first.
+_GRAD_PRODUCERS: List[torch.cuda.Stream] = []
+
+
+def add_grad_producer(stream) -> None:
+    _GRAD_PRODUCERS.append(stream)
+
+
+def join_grad_producers() -> None:
+    """Make the current stream wait for every pending gradient producer."""
+    while _GRAD_PRODUCERS:
+        s = _GRAD_PRODUCERS.pop()
+        torch.cuda.current_stream(s.device).wait_stream(s)
+
+
 class DenseArena:
     def __init__(self, params: Iterable[torch.nn.Parameter], device: torch.device, extra_grad: int = 0):
         """``extra_grad`` floats are appended to the gradient buffer (not to the
@@ -73,6 +90,7 @@ class DenseArena:
         return self.grad[: self.flat.numel()]
 
     def zero_grad(self):
+        join_grad_producers()
         self.grad.zero_()
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
@@ -126,6 +144,7 @@ class FlatAdam:
         return pack, dn
 
     def step(self, grad_scale: float = 1.0):
+        join_grad_producers()
         if self.a.flat.is_cuda:
             pack, dn = self._extras()
             _native.hip().adam_fused(self.a.flat, self.a.param_grad, self.m, self.v, self.pows, self.ticket, self.lr,
@@ -236,6 +255,7 @@ class DenseSync:
         dense gradients are final); ``before_step`` joins it."""
         if not (self.active and self.mode == "grad_allreduce") or not self.a.grad.is_cuda:
             return
+        join_grad_producers()
         dev = self.a.grad.device
         cur = torch.cuda.current_stream(dev)
         if self._stream is None:
@@ -250,6 +270,7 @@ class DenseSync:
 
     def before_step(self):
         """Called after backward, before the optimizer."""
+        join_grad_producers()
         if self._launched:
             torch.cuda.current_stream(self.a.grad.device).wait_stream(self._stream)
             self._launched = False
@@ -264,6 +285,7 @@ class DenseSync:
         (``py/fluid/transpiler/collective.py:499-636``): every rank gathers all
         ranks' gradients and runs one optimizer update per gathered gradient,
         in rank order, so all replicas stay identical."""
+        join_grad_producers()
         if self.active and self.mode == "allgather":
             g = self.a.grad
             parts = [torch.empty_like(g) for _ in range(self.world)]
@@ -306,6 +328,7 @@ class FlatSGD:
         self.a, self.lr, self.wd = arena, lr, weight_decay
 
     def step(self, grad_scale: float = 1.0):
+        join_grad_producers()
         g = self.a.grad
         if self.wd:
             self.a.flat.mul_(1.0 - self.lr * self.wd)
@@ -324,6 +347,7 @@ class FlatMomentum:
         self.vel = torch.zeros_like(arena.flat)
 
     def step(self, grad_scale: float = 1.0):
+        join_grad_producers()
         g = self.a.grad if grad_scale == 1.0 else self.a.grad * grad_scale
         self.vel.mul_(self.mu).add_(g)
         upd = g.add(self.vel, alpha=self.mu) if self.nesterov else self.vel
@@ -342,6 +366,7 @@ class FlatAdagrad:
         self.acc = torch.full_like(arena.flat, float(initial_accumulator_value))
 
     def step(self, grad_scale: float = 1.0):
+        join_grad_producers()
         g = self.a.grad if grad_scale == 1.0 else self.a.grad * grad_scale
         self.acc.addcmul_(g, g)
         self.a.flat.addcdiv_(g, self.acc.sqrt().add_(self.eps), value=-self.lr)

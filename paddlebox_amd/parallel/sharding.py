@@ -26,7 +26,7 @@ import torch.distributed as dist
 from .. import _native
 from ..ops import reference as ref
 from .comm import collective_active
-from .dense import DenseArena
+from .dense import join_grad_producers, DenseArena
 
 
 def _backend(group) -> str:
@@ -84,6 +84,7 @@ class ShardedFlatAdam:
         return t[self.rank * self.shard:(self.rank + 1) * self.shard]
 
     def step(self, grad_scale: float = 1.0):
+        join_grad_producers()
         n = self.a.flat.numel()
         self._pgrad[:n].copy_(self.a.grad)
         if self.active:
