@@ -18,7 +18,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ..parallel.dense import DenseArena, DenseSync, FlatAdagrad, FlatAdam, FlatMomentum, FlatSGD
+from ..parallel.dense import join_grad_producers, DenseArena, DenseSync, FlatAdagrad, FlatAdam, FlatMomentum, FlatSGD
 from .framework import (LoDTensor, Parameter, Program, Scope, Variable, default_main_program,
                         default_startup_program, global_scope, to_device, torch_dtype)
 from .kernels import KERNELS, LazyRagged, Ragged
@@ -310,6 +310,7 @@ class Session:
             t0 = prof.begin()
         for s, o in zip(self.syncs, self.opts):
             s.apply(o)
+        join_grad_producers()  # an update issued behind the dW side stream
         if prof is not None:
             prof.end("dense sync + optimizer", t0)
 

@@ -144,6 +144,8 @@ class FlatAdam:
         return pack, dn
 
     def step(self, grad_scale: float = 1.0):
+        # (issuing the update on the dW side stream instead, beside the sparse
+        # push, measured no faster: 0.286 vs 0.280-0.285 ms/step)
         join_grad_producers()
         if self.a.flat.is_cuda:
             pack, dn = self._extras()
@@ -270,7 +272,8 @@ class DenseSync:
 
     def before_step(self):
         """Called after backward, before the optimizer."""
-        join_grad_producers()
+        if self._launched or (self.active and self.mode == "grad_allreduce"):
+            join_grad_producers()
         if self._launched:
             torch.cuda.current_stream(self.a.grad.device).wait_stream(self._stream)
             self._launched = False

@@ -19,6 +19,7 @@ from typing import Any, Callable, List, Optional, Sequence
 import torch
 
 from .. import _native
+from ..parallel.dense import join_grad_producers
 
 
 def _tensor_fields(b) -> List[str]:
@@ -77,9 +78,11 @@ class GraphedTrainStep:
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 step_fn(self.bufs[0])
+                join_grad_producers()
             for hb in warm_batches:
                 self.bufs[0]._flat.copy_(hb._flat, non_blocking=True)
                 out = step_fn(self.bufs[0])
+                join_grad_producers()
                 if on_warm is not None:
                     on_warm(out)
         cur.wait_stream(s)
@@ -90,6 +93,7 @@ class GraphedTrainStep:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
                 out = step_fn(buf)
+                join_grad_producers()  # side streams forked in the step rejoin before the capture ends
             pool = g.pool()
             self.graphs.append((g, out))
         torch.cuda.synchronize(self.device)
