@@ -162,7 +162,7 @@ def main():
     # one update launch for the dense side: Adam + bf16 tower weight re-pack +
     # data_norm summary update; grads zeroed by the same kernel
     opt = FlatAdam(arena, lr=1e-3, clear_grad=True)
-    if not fp32 and not dcn:
+    if not fp32 and getattr(model, "use_tower", False):
         opt.fuse(mlps=[model.mlp], data_norms=[model.dn])
     # the dense all-reduce runs on its own communicator and side stream, started
     # as soon as the tower's gradients are final: it overlaps the sparse push
@@ -173,7 +173,7 @@ def main():
         ipc = IpcMesh(arena.grad.numel() * 4, device=device)
     sync = DenseSync(arena, mode="grad_allreduce",
                      overlap_group=dist.new_group(list(range(world))) if multi else None, ipc=ipc)
-    if not dcn:
+    if getattr(model, "tower", None) is not None:
         model.tower.on_dense_grads = sync.launch
 
     # every pinned batch buffer is streamed to the device once up front so the

@@ -117,8 +117,11 @@ class CrossWorkspace {
 
   // grads accumulate into dW[l] / db[l] / dwc (dense-arena views); returns
   // d(loss)/d(x0) as bf16 [M, ld] (pad columns zero)
+  // dy_out (optional): a bf16 [M, ld] gradient buffer the x0 gradient is
+  // ADDED to (e.g. the fused tower's dX0, before its data_norm backward)
   Tensor backward(const Tensor& y, const Tensor& yt, const Tensor& ds, const std::vector<Tensor>& dW,
-                  const std::vector<Tensor>& db, const Tensor& wc, const Tensor& dwc) {
+                  const std::vector<Tensor>& db, const Tensor& wc, const Tensor& dwc,
+                  const c10::optional<Tensor>& dy_out) {
     check_x0(y);
     CR_CHECK(yt.is_cuda() && yt.scalar_type() == torch::kBFloat16 && yt.is_contiguous() && yt.dim() == 2 &&
                  yt.size(0) >= D_ + 1 && yt.size(1) == ldM_,
@@ -175,6 +178,13 @@ class CrossWorkspace {
         d.CT = bp(ut_[cur ^ 1]);
         d.fout = fp(g_[cur ^ 1]);
         d.zprev = fp(z_[l - 1]);
+      } else if (dy_out.has_value() && dy_out->defined()) {
+        CR_CHECK(dy_out->is_cuda() && dy_out->scalar_type() == torch::kBFloat16 && dy_out->is_contiguous() &&
+                     dy_out->dim() == 2 && dy_out->size(0) == M_ && dy_out->size(1) == ld_,
+                 "dy_out must be bf16 [M, ld]");
+        d.C = bp(*dy_out);
+        d.CT = nullptr;
+        d.add_c = 1;
       } else {
         d.C = bp(dy_);
         d.CT = nullptr;
@@ -182,7 +192,7 @@ class CrossWorkspace {
       launch_mlp_gemm(d, MLP_EPI_CROSS_DX, s);
       cur ^= 1;
     }
-    return dy_;
+    return dy_out.has_value() && dy_out->defined() ? *dy_out : dy_;
   }
 
   Tensor x_out() const { return xf_[L_ - 1].narrow(1, 0, D_); }
@@ -204,7 +214,8 @@ void bind_cross(py::module& m) {
   py::class_<CrossWorkspace>(m, "CrossWorkspace")
       .def(py::init<int64_t, int64_t, int64_t, int, int64_t>())
       .def("forward", &CrossWorkspace::forward)
-      .def("backward", &CrossWorkspace::backward)
+      .def("backward", &CrossWorkspace::backward, py::arg("y"), py::arg("yt"), py::arg("ds"), py::arg("dW"),
+           py::arg("db"), py::arg("wc"), py::arg("dwc"), py::arg("dy_out") = py::none())
       .def("x_out", &CrossWorkspace::x_out);
 }
 

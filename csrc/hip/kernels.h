@@ -397,6 +397,7 @@ struct MlpGemmArgs {
   float* zout = nullptr;
   float* accum = nullptr;
   int ldf = 0;
+  int add_c = 0;  // CROSS_DX layer 0: C += (the gradient of x0 is added to C's bf16 contents)
 };
 void launch_mlp_gemm(const MlpGemmArgs& g, int epi, hipStream_t s);
 constexpr int kMaxMlpLayers = 8;

@@ -196,7 +196,9 @@ __global__ __launch_bounds__(256) void k_gemm_nt(MlpGemmArgs g) {
             }
             acc[i][reg] = ok ? xa[reg] * gl : 0.f;
           } else {
-            acc[i][reg] = ok ? gl + xd[reg] : 0.f;
+            float v0 = gl + xd[reg];
+            if (g.add_c && ok) v0 += bf2f(g.C[(int64_t)m * g.ldc + n]);
+            acc[i][reg] = ok ? v0 : 0.f;
           }
         }
       }

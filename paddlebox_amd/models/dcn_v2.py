@@ -24,6 +24,7 @@ from torch import nn
 from .. import _native
 from ..ops.ctr import DataNorm, ctr_head, logit_logloss
 from ..ops.mlp import FusedMLP, _ensure_grad, pad8
+from ..ops.tower import CtrTower
 from ..ops.sparse import pull_seqpool_cvm_concat
 from ..ps.sparse_engine import SeqpoolParams, SparseEngine
 
@@ -57,7 +58,10 @@ def cross_logit(y: torch.Tensor, cross: "CrossNetV2", w_c: torch.Tensor,
     D = w_c.numel()
     if y.is_cuda:
         return _CrossHipFn.apply(y, yt, cross, w_c, *cross.parameters(), w_c)
-    return cross(y[:, :D].float()) @ w_c
+    yy = y[:, :D].float()
+    if yy.shape[1] < D:  # the cross width is the padded tower width
+        yy = torch.nn.functional.pad(yy, (0, D - yy.shape[1]))
+    return cross(yy) @ w_c
 
 
 class CrossNetV2(nn.Module):
@@ -95,7 +99,8 @@ class CrossNetV2(nn.Module):
 
 class DCNv2(nn.Module):
     def __init__(self, engine: SparseEngine, num_slots: int = 26, dense_dim: int = 13, cross_layers: int = 3,
-                 hidden: Sequence[int] = (512, 256), use_data_norm: bool = True, seqpool: SeqpoolParams = None):
+                 hidden: Sequence[int] = (512, 256), use_data_norm: bool = True, seqpool: SeqpoolParams = None,
+                 fused_tower: bool = True):
         super().__init__()
         self.engine = engine
         self.S = num_slots
@@ -106,14 +111,25 @@ class DCNv2(nn.Module):
         self.C = C
         self.Cp = pad8(C)
         self.dn = DataNorm(C) if use_data_norm else None
-        self.cross = CrossNetV2(self.Cp, cross_layers, valid=C)
-        self.w_c = nn.Parameter(torch.zeros(self.Cp))
         self.mlp = FusedMLP(C, hidden, 1)
         self.ew_col = 2 if self.sp.use_cvm and not self.sp.clk_filter else (1 if self.sp.use_cvm else 0)
+        # the cross stack runs inside the fused tower (csrc/hip/tower.hip
+        # head + MLP, cross GEMMs on the normalised input the head writes)
+        # when the tower's padded input width is a whole number of 64-wide
+        # GEMM k-tiles; otherwise beside the MLP workspace
+        k0 = (self.mlp.in_dim + 31) // 32 * 32
+        self.use_tower = fused_tower and k0 % 64 == 0 and len(self.mlp.hidden) <= 8
+        D = k0 if self.use_tower else self.Cp
+        self.cross = CrossNetV2(D, cross_layers, valid=C)
+        self.w_c = nn.Parameter(torch.zeros(D))
+        self.tower = CtrTower(self.mlp, self.dn, self.S, self.Eo, self.ew_col, 0, use_head_lin=False,
+                              cross=(self.cross, self.w_c)) if self.use_tower else None
 
     def forward(self, batch):
         B, S = batch.B, batch.S
         x = pull_seqpool_cvm_concat(self.engine, batch.keys, batch.lod, B, S, batch.cvm, batch.dense, self.sp)
+        if x.is_cuda and self.tower is not None:
+            return self.tower(x, batch.label)
         if x.is_cuda:
             ws = self.mlp.workspace(B, x.device)
             y, _ = ctr_head(x, self.dn, S, self.Eo, self.ew_col, 0, self.Cp, ws.x(0), ws.xt(0))

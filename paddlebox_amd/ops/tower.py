@@ -29,6 +29,7 @@ from .. import _native
 from ..parallel.comm import collective_active
 from ..parallel.dense import add_grad_producer, join_grad_producers
 from . import reference as ref
+from .mlp import _ensure_grad
 
 
 def pad32(n: int) -> int:
@@ -46,20 +47,29 @@ class _CtrTowerFn(torch.autograd.Function):
         ws = mlp.tower_workspace(B, x.device)
         mlp.ensure_packed()
         x = x.contiguous()
+        yt = t._cross_yt(B, x.device) if t.cross is not None else None
         if dn is not None:
             part = t._dn_part(B, x.device)
             _, lin, means, scales = h.head_fwd(x, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim), dn.batch_size,
-                                               dn.batch_sum, dn.batch_square_sum, y_out=ws.x0(),
+                                               dn.batch_sum, dn.batch_square_sum, y_out=ws.x0(), yT_out=yt,
                                                ymp_out=ws.x0mp(), stat_part=part)
         else:
             _, lin, means, scales = h.head_fwd(x, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim), None, None, None,
-                                               y_out=ws.x0(), ymp_out=ws.x0mp())
+                                               y_out=ws.x0(), yT_out=yt, ymp_out=ws.x0mp())
         if extra is not None:
             lin_use = extra.detach().contiguous().float().view(-1)
         elif t.use_head_lin:
             lin_use = lin
         else:
             lin_use = None
+        if t.cross is not None:
+            # DCN-V2 cross stack on the normalised input the head just wrote
+            # (x0 and its transposed copy): its logit joins the tower's loss
+            net, w_c = t.cross
+            xw = net.workspace(ws.x0())
+            s = xw.forward(ws.x0(), [w.detach() for w in net.w], [b.detach() for b in net.b], w_c.detach())
+            lin_use = s if lin_use is None else lin_use + s
+            ctx.yt = yt
         auc = t.auc
         loss, pred, dz = ws.forward(list(mlp.b), mlp.w_out.view(-1), mlp.b_out, lin_use, label.contiguous().view(-1),
                                     auc[0] if auc else None, auc[1] if auc else None, auc[2] if auc else None)
@@ -113,6 +123,13 @@ class _CtrTowerFn(torch.autograd.Function):
         else:
             dx0 = ws.backward(*args)
             dense_tail()
+        if t.cross is not None:
+            # cross backward (d logit = dz); its x0 gradient is added into the
+            # tower's dX0 before the data_norm / head backward below
+            net, w_c = t.cross
+            ds = ctx.dz if gl is None else (ctx.dz * gl).contiguous()
+            net._xw.backward(ws.x0(), ctx.yt, ds, [_ensure_grad(w) for w in net.w],
+                             [_ensure_grad(b) for b in net.b], w_c.detach(), _ensure_grad(w_c), dy_out=dx0)
         use_lin = t.use_head_lin and not ctx.has_extra
         dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim),
                            ctx.means, ctx.scales, dn.eps if dn is not None else 0.0, dlin_scale=gl,
@@ -127,8 +144,13 @@ class CtrTower:
     S slot blocks of width Eo (embed_w at ew_col, D embedx after it) followed by
     dense columns make up the input x [B, C]."""
 
-    def __init__(self, mlp, dn, S: int, Eo: int, ew_col: int, D: int, use_head_lin: bool = True):
+    def __init__(self, mlp, dn, S: int, Eo: int, ew_col: int, D: int, use_head_lin: bool = True, cross=None):
+        """``cross``: optional (CrossNetV2, w_c) whose width is the tower's
+        padded input width: a DCN-V2 cross logit computed inside the tower
+        from its normalised input and added to the MLP logit."""
         self.mlp, self.dn = mlp, dn
+        self.cross = cross
+        self._yt = None
         self.S, self.Eo, self.ew_col, self.D = S, Eo, ew_col, D
         self.use_head_lin = use_head_lin
         self.auc = None  # (table [2, T] f64, stats [5] f64, mask or None): fused AUC accumulation
@@ -141,6 +163,18 @@ class CtrTower:
         self._side = None
         self._part = None
         self._params = list(mlp.parameters())
+        if cross is not None:
+            self._params += list(cross[0].parameters()) + [cross[1]]
+
+    def _cross_yt(self, B, dev):
+        """x0^T for the cross dW GEMM: [pad64(D+1), pad64(B)] bf16, the head
+        writes rows < D, row D stays 1 (the bias row)."""
+        D = self.cross[0].dim
+        r, c = (D + 1 + 63) // 64 * 64, (B + 63) // 64 * 64
+        if self._yt is None or tuple(self._yt.shape) != (r, c):
+            self._yt = torch.zeros(r, c, dtype=torch.bfloat16, device=dev)
+            self._yt[D, :B] = 1.0
+        return self._yt
 
     def _side_stream(self, dev):
         if self._side is None:
@@ -168,6 +202,11 @@ class CtrTower:
         y, lin = ctr_head(x, self.dn, self.S, self.Eo, self.ew_col, self.D, Cp)
         deep = self.mlp(y)
         other = extra if extra is not None else (lin if self.use_head_lin else None)
+        if self.cross is not None:
+            from ..models.dcn_v2 import cross_logit
+
+            c = cross_logit(y, self.cross[0], self.cross[1])
+            other = c if other is None else other + c
         loss, pred = logit_logloss(deep, other, label)
         if self.auc is not None:
             ref.auc_accumulate(pred.detach(), label.view(-1), self.auc[0], self.auc[1], self.auc[2])

@@ -60,3 +60,59 @@ def test_cross_stack_matches_fp64(M, C, L):
         assert _rel(net.b[l].grad, bs[l].grad) < 3e-2, l
     assert _rel(yh.grad[:, :C].float(), x0.grad) < 3e-2
     assert bool((yh.grad[:, C:] == 0).all())
+
+
+def test_dcn_tower_path_matches_workspace_path():
+    """DCN-V2 with the cross stack inside the fused tower (head + MLP + loss +
+    cross on the normalised input) vs the same parameters through the MLP
+    workspace + standalone cross: same loss and gradients up to the bf16
+    operands of both (the tower's cross is 64-padded wider; the extra
+    features are zero padding)."""
+    from paddlebox_amd.data.synthetic import CriteoSynth
+    from paddlebox_amd.models.dcn_v2 import DCNv2
+    from paddlebox_amd.parallel.dense import join_grad_producers
+    from paddlebox_amd.ps.config import PSConfig
+    from paddlebox_amd.ps.sparse_engine import SparseEngine
+
+    dev = torch.device("cuda:0")
+    torch.manual_seed(3)
+    synth = CriteoSynth(total_features=20000, alpha=1.2, seed=5, device="cuda:0")
+    B = 1024
+    b = synth.batch(B)
+    eng = SparseEngine(PSConfig(embedx_dim=8), max_keys=B * 26, device=dev, auto_insert=True, capacity=100000)
+    mt = DCNv2(eng, hidden=(64, 32), cross_layers=2).to(dev)
+    mw = DCNv2(eng, hidden=(64, 32), cross_layers=2, fused_tower=False).to(dev)
+    assert mt.use_tower and not mw.use_tower
+    D = mw.cross.dim
+    with torch.no_grad():
+        mt.w_c.normal_(0, 0.3)
+        mt.w_c[mt.C:] = 0
+        mw.w_c.copy_(mt.w_c[:D])
+        for wt, ww, bt, bw in zip(mt.cross.w, mw.cross.w, mt.cross.b, mw.cross.b):
+            ww.copy_(wt[:D, :D])
+            bw.copy_(bt[:D])
+        for pt, pw in zip(mt.mlp.parameters(), mw.mlp.parameters()):
+            pw.copy_(pt)
+    mt.mlp.invalidate_pack()
+    for m in (mt, mw):
+        m.dn.training = False  # keep the data_norm summaries fixed
+    with torch.no_grad():
+        mt(b)  # auto-insert the batch's keys
+    join_grad_producers()
+    eng.test_mode = True  # pulls only: both models see the same embeddings, no push
+    res = {}
+    for tag, m in (("tower", mt), ("ws", mw)):
+        for p in m.parameters():
+            p.grad = torch.zeros_like(p)
+        loss, pred = m(b)
+        loss.backward()
+        join_grad_producers()
+        torch.cuda.synchronize()
+        res[tag] = (float(loss), m)
+    assert abs(res["tower"][0] - res["ws"][0]) < 2e-3
+    for gt, gw in [(mt.w_c.grad[:D], mw.w_c.grad)] + \
+            [(a.grad[:D, :D], c.grad) for a, c in zip(mt.cross.w, mw.cross.w)] + \
+            [(a.grad[:D], c.grad) for a, c in zip(mt.cross.b, mw.cross.b)] + \
+            [(a.grad, c.grad) for a, c in zip(mt.mlp.parameters(), mw.mlp.parameters())]:
+        if gw.abs().max() > 0:
+            assert _rel(gt, gw) < 5e-2
