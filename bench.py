@@ -77,6 +77,11 @@ def main():
     ap.add_argument("--model", choices=("deepfm", "dcn_v2"), default="deepfm",
                     help="deepfm = the headline config; dcn_v2 = BASELINE config 5 (cross layers on the MFMA GEMM)")
     ap.add_argument("--cross-layers", type=int, default=3)
+    ap.add_argument("--prefetch", dest="prefetch", action="store_true", default=False,
+                    help="pipelined pull: batch i+1's dedup + probe on a side stream beside batch i's dense "
+                         "work (measured slower on one MI355X: 0.356 vs 0.281 ms/step, see "
+                         "profiles/r2_bench_prefetch.txt)")
+    ap.add_argument("--no-prefetch", dest="prefetch", action="store_false")
     ap.add_argument("--dense-ipc", action="store_true",
                     help="dense gradient all-reduce on the in-house IPC mesh (one-shot, xGMI peer writes) "
                          "instead of RCCL")
@@ -207,7 +212,8 @@ def main():
         try:
             from paddlebox_amd.runtime.graph_step import GraphedTrainStep
 
-            graphed = GraphedTrainStep(train_step, host_batches[0], device)
+            pre = (engine, lambda b: b.keys) if (args.prefetch and engine.can_prefetch()) else None
+            graphed = GraphedTrainStep(train_step, host_batches[0], device, prefetch=pre)
             graphed.warm(host_batches, replays=args.graph_warm)
             log(rank, f"[bench] training step captured into HIP graphs ({args.graph_warm} warm replays)")
         except Exception as e:  # pragma: no cover - depends on runtime
@@ -326,6 +332,7 @@ def main():
                 "total_features": synth.total_features,
                 "parallelism": f"dp{world}+sparse-shard{world}",
                 "dense_allreduce": "ipc-oneshot" if ipc is not None else "rccl",
+                "pipelined_pull": bool(graphed is not None and graphed.prefetch is not None),
                 "mlp_dtype": args.mlp_dtype,
                 "unique_keys_per_batch": round(sum(u_per_batch) / len(u_per_batch), 1),
                 "keys_per_batch": l_per_batch,

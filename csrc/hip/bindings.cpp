@@ -73,6 +73,15 @@ class GpuTable {
     launch_table_probe(view(), ptr<uint64_t>(h), h.numel(), optr<int32_t>(n_dev), ptr<int64_t>(rows), cur_stream());
     return rows;
   }
+  // probe into a caller-owned (persistent) row buffer: graph-captured
+  // prefetches need the rows at a fixed address
+  void probe_into(const Tensor& h, const c10::optional<Tensor>& n_dev, Tensor rows) {
+    check_cuda(h, "h");
+    check_cuda(rows, "rows");
+    PBX_CHECK(rows.scalar_type() == torch::kInt64 && rows.is_contiguous() && rows.numel() >= h.numel(),
+              "probe_into: rows must be contiguous int64 with >= h.numel() entries");
+    launch_table_probe(view(), ptr<uint64_t>(h), h.numel(), optr<int32_t>(n_dev), ptr<int64_t>(rows), cur_stream());
+  }
   // Insert unique mixed keys (those not present). Returns number of keys that
   // could not be placed (0 normally).  Synchronises (build phase only).
   int64_t insert(const Tensor& h, const c10::optional<Tensor>& n_dev, const SparseSGDConfig& cfg,
@@ -957,6 +966,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("last_overflow", &GpuTable::last_overflow)
       .def("size", &GpuTable::size)
       .def("stash_n", &GpuTable::stash_n)
+      .def("probe_into", &GpuTable::probe_into)
       .def("export_all", &GpuTable::export_all)
       .def("assign", &GpuTable::assign)
       .def("shrink", &GpuTable::shrink)

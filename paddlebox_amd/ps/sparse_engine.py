@@ -71,6 +71,7 @@ class _PullSlot:
             self.ws = h.DedupWorkspace(eng.max_keys, dev.index or 0, True)
         self.occ_slot = torch.empty(eng.max_keys, dtype=torch.int32, device=dev)
         self.occ_ins = torch.empty(eng.max_keys, dtype=torch.int32, device=dev)
+        self.rows = None  # persistent probe rows of a prefetched batch
         self.gen = 0
         if eng.sharded:
             n = eng.world * eng.C
@@ -188,6 +189,7 @@ class SparseEngine:
             # ring of per-pull buffers (sort-free hash dedup everywhere: the
             # sender packs its unique keys per owner with a counting pass)
             self._slots = [_PullSlot(self) for _ in range(max(1, int(pull_ring)))]
+            self._prepared = {}  # key-buffer address -> (slot, L) of a prefetched batch
             self._next_slot = 0
             self._cur = self._slots[0]
             if self.sharded:
@@ -277,6 +279,32 @@ class SparseEngine:
                           occ_slot=sl.occ_slot, occ_ins=sl.occ_ins)
         return st
 
+    def can_prefetch(self) -> bool:
+        """Prefetched pulls need a fixed key set during training: GPU, one
+        shard, no auto-insert (keys registered at the feed pass)."""
+        return (self.is_gpu and not self.sharded and not (self.auto_insert and not self.test_mode)
+                and len(self._slots) >= 2)
+
+    def prefetch(self, keys: torch.Tensor, slot: int):
+        """Dedup + probe of a batch ahead of its pull, into pull slot ``slot``
+        (pipelined training: issued on a side stream while the previous batch
+        trains).  The batch's ``pull_seqpool_cvm`` on the same key buffer then
+        starts at the seqpool.  Buffers are persistent, so this is
+        graph-capturable."""
+        if not self.can_prefetch():
+            raise RuntimeError("prefetch needs a GPU, unsharded engine without auto-insert")
+        L = keys.numel()
+        assert L <= self.max_keys
+        sl = self._slots[slot % len(self._slots)]
+        if sl.rows is None:
+            sl.rows = torch.empty(self.max_keys, dtype=torch.int64, device=self.device)
+        sl.ws.run(keys, False)
+        self.table.t.probe_into(sl.ws.uniq_h[:L], sl.ws.u_count, sl.rows)
+        self._prepared[keys.data_ptr()] = (sl, L)
+
+    def clear_prefetch(self):
+        self._prepared.clear()
+
     def _take_slot(self) -> _PullSlot:
         sl = self._slots[self._next_slot % len(self._slots)]
         self._next_slot += 1
@@ -296,6 +324,18 @@ class SparseEngine:
         h = self._hip
         L = keys.numel()
         assert L <= self.max_keys, f"batch has {L} keys > engine max_keys {self.max_keys}"
+        pre = self._prepared.pop(keys.data_ptr(), None) if self._prepared else None
+        if pre is not None and pre[1] == L and not self.sharded:
+            sl = pre[0]
+            sl.gen += 1
+            self._cur = sl
+            if fill_occ:
+                h.fill_occurrence(lod, S, B, sl.occ_slot, sl.occ_ins)
+            ws = sl.ws
+            st = PullState(B=B, S=S, L=L, lod=lod, uid=ws.uid, perm=ws.perm, counts=ws.u_count, slot=sl,
+                           gen=sl.gen)
+            st.rows = sl.rows[:L]
+            return st
         sl = self._take_slot()
         ws = sl.ws
         ws.run(keys, False)

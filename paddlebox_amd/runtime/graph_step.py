@@ -62,7 +62,11 @@ def clone_batch(b, device):
 class GraphedTrainStep:
     def __init__(self, step_fn: Callable[[Any], Any], example_batch, device, n_buffers: int = 2,
                  warmup: int = 3, max_inflight: int = 3, warm_batches: Sequence[Any] = (),
-                 on_warm: Optional[Callable[[Any], None]] = None):
+                 on_warm: Optional[Callable[[Any], None]] = None, prefetch=None):
+        """``prefetch``: optional (engine, keys_of) -- pipelined sparse pull:
+        graph j also runs the dedup + probe of buffer j+1's keys on a side
+        stream while batch j trains (SparseEngine.prefetch, pull slot = buffer
+        index), so each step's pull starts at the seqpool."""
         """``warmup`` eager runs of ``step_fn`` on the example batch precede
         the capture (lazy allocations, kernel selection).  A trainer that must
         not train a batch twice passes ``warmup=0`` and ``warm_batches``: real
@@ -87,15 +91,37 @@ class GraphedTrainStep:
                     on_warm(out)
         cur.wait_stream(s)
         torch.cuda.synchronize(self.device)
+        self.prefetch = prefetch
+        self._side = torch.cuda.Stream(self.device) if prefetch is not None else None
+        # buffer contents versions (bumped by load / fill) and the version each
+        # buffer had when a replay prefetched it: a buffer reloaded after its
+        # prefetch is prepared again before its own replay
+        self._ver = [0] * n_buffers
+        self._pref_ver = [-1] * n_buffers
+        if prefetch is not None:
+            eng, keys_of = prefetch
+            eng.clear_prefetch()
+            eng.prefetch(keys_of(self.bufs[0]), 0)  # graph 0's pull finds buffer 0 prepared
         self.graphs = []
         pool = None
-        for buf in self.bufs:
+        n = len(self.bufs)
+        for j, buf in enumerate(self.bufs):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
+                if prefetch is not None:
+                    eng, keys_of = prefetch
+                    cap = torch.cuda.current_stream(self.device)
+                    self._side.wait_stream(cap)
+                    with torch.cuda.stream(self._side):
+                        eng.prefetch(keys_of(self.bufs[(j + 1) % n]), (j + 1) % n)
                 out = step_fn(buf)
+                if prefetch is not None:
+                    torch.cuda.current_stream(self.device).wait_stream(self._side)
                 join_grad_producers()  # side streams forked in the step rejoin before the capture ends
             pool = g.pool()
             self.graphs.append((g, out))
+        if prefetch is not None:
+            prefetch[0].clear_prefetch()
         torch.cuda.synchronize(self.device)
         self.copy_stream = torch.cuda.Stream(self.device)
         self.ready = [torch.cuda.Event() for _ in self.bufs]
@@ -118,6 +144,7 @@ class GraphedTrainStep:
     def load(self, i: int, host_batch):
         """Async H2D of a (pinned) host batch into buffer set i."""
         dst = self.bufs[i]
+        self._ver[i] += 1
         src_flat = getattr(host_batch, "_flat", None)
         with torch.cuda.stream(self.copy_stream):
             self.copy_stream.wait_event(self.free[i])
@@ -137,6 +164,7 @@ class GraphedTrainStep:
         that write it (on ``stream``, default the copy stream) once the
         replay that last read it has finished."""
         st = stream if stream is not None else self.copy_stream
+        self._ver[i] += 1
         st.wait_event(self.free[i])
         with torch.cuda.stream(st):
             fn(self.bufs[i])
@@ -148,6 +176,17 @@ class GraphedTrainStep:
         if self.step_no >= self.max_inflight:
             self.done[slot].synchronize()
         cur.wait_event(self.ready[i])
+        if self.prefetch is not None:
+            n = len(self.bufs)
+            cur.wait_event(self.ready[(i + 1) % n])  # graph i prefetches buffer i+1
+            if self._pref_ver[i] != self._ver[i]:
+                # buffer i was not prefetched with its current contents (first
+                # replay, out-of-order use, reloaded after the prefetch):
+                # prepare it now, into slot i
+                eng, keys_of = self.prefetch
+                eng.prefetch(keys_of(self.bufs[i]), i)
+                eng.clear_prefetch()
+            self._pref_ver[(i + 1) % n] = self._ver[(i + 1) % n]
         g, out = self.graphs[i]
         g.replay()
         self.free[i].record(cur)

@@ -115,3 +115,34 @@ def test_mlp_workspace_graph_replay():
     torch.cuda.synchronize()
     for p, r in zip(mlp.parameters(), ref):
         torch.testing.assert_close(p.grad, r, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("pipelined", [True, False])
+def test_prefetched_pull_graph_matches_eager(pipelined):
+    """Pipelined pull (graph j dedups + probes buffer j+1 on a side stream):
+    same training as eager steps, both with the load-ahead order (the
+    prefetch is used) and with load-then-run (each buffer is re-prepared)."""
+    eng_e, model_e, arena_e, opt_e, batches = _setup()
+    step_e = _step_fn(model_e, arena_e, opt_e)
+    for i in [0, 0, 0] + list(range(6)):  # 3 warm-up steps on the example batch
+        step_e(batches[i])
+    torch.cuda.synchronize()
+    flat_e = arena_e.flat.clone()
+    h, ve = eng_e.table.export(True)
+    eng_g, model_g, arena_g, opt_g, _ = _setup()
+    step_g = _step_fn(model_g, arena_g, opt_g)
+    g = GraphedTrainStep(step_g, batches[0], DEV, warmup=3, prefetch=(eng_g, lambda b: b.keys))
+    if pipelined:
+        g.load(0, batches[0])
+        for i in range(6):
+            if i + 1 < 6:
+                g.load((i + 1) % 2, batches[i + 1])
+            g.run(i % 2)
+    else:
+        for i in range(6):
+            g.load(i % 2, batches[i])
+            g.run(i % 2)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(arena_g.flat, flat_e, rtol=1e-3, atol=1e-4)
+    vg = eng_g.table.read(h)
+    torch.testing.assert_close(vg[:, :13], ve[:, :13], rtol=1e-3, atol=1e-4)
