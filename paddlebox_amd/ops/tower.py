@@ -36,6 +36,16 @@ def pad32(n: int) -> int:
     return (n + 31) // 32 * 32
 
 
+def _collectives_in_step() -> bool:
+    """RCCL work in the step (multi-rank or a forced-collectives rehearsal):
+    the dW side stream then only delays the dense all-reduce that overlaps
+    the sparse exchange (measured 0.478 vs 0.389 ms/step on the 1-rank
+    rehearsal), so the dW GEMM stays on the compute stream."""
+    if os.environ.get("PBX_FORCE_COLLECTIVES") == "1":
+        return True
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
 class _CtrTowerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, extra, label, t: "CtrTower", *params):
@@ -107,7 +117,7 @@ class _CtrTowerFn(torch.autograd.Function):
             if t.on_dense_grads is not None:  # e.g. start the dense all-reduce, overlapped with the sparse push
                 t.on_dense_grads()
 
-        if t.overlap_dw and x.is_cuda:
+        if t.overlap_dw and x.is_cuda and not _collectives_in_step():
             # dX chain on the compute stream; the dW GEMMs + bias / data_norm
             # reductions (and whatever consumes the dense grads) on a side
             # stream, concurrent with the head backward and the sparse push;
