@@ -21,6 +21,13 @@ namespace {
 
 constexpr int kRB = 16;  // rows per workgroup
 
+// width (elements) of the bf16 y slab; even, so the per-column arrays after
+// it stay 4-byte aligned
+__host__ __device__ inline int head_ys_width(int C, int Cp) {
+  const int w = Cp > (C + 7) / 8 * 8 + 8 ? Cp : (C + 7) / 8 * 8 + 8;
+  return (w + 1) / 2 * 2;
+}
+
 __device__ __forceinline__ unsigned short f2bf(float f) {
   // round-to-nearest-even
   unsigned int u = __float_as_uint(f);
@@ -30,8 +37,10 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
 }
 __device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(((unsigned int)h) << 16); }
 
-// dynamic LDS: xs[kRB][C] floats + s1[kRB][D]
-__global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
+// dynamic LDS: xs[kRB][C] floats + s1[kRB][D].  512 threads per 16-row
+// block: the row blocks are fixed at 16 (the tower's m-packed copy), so the
+// extra waves come from wider blocks (the staging loop is latency-bound)
+__global__ __launch_bounds__(512) void k_head_fwd(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* xs = lds;
   const int C = a.C, Cp = a.Cp;
@@ -40,21 +49,30 @@ __global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
   const int rows = min(kRB, a.B - row0);
   if (rows <= 0) return;
   unsigned short* ys = reinterpret_cast<unsigned short*>(xs + kRB * (C + a.D));  // [kRB][Cp] bf16 (for y^T)
-  // 1) stage + data_norm output (bf16, padded to Cp)
+  // per-column data_norm mean / scale, once per block (not per element)
+  float* cm = reinterpret_cast<float*>(ys + kRB * head_ys_width(C, Cp));
+  float* cs = cm + C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    if (a.bsize) {
+      const float bs = a.bsize[c];
+      cm[c] = a.bsum[c] / bs;
+      cs[c] = sqrtf(bs / a.bsq[c]);
+    } else {
+      cm[c] = 0.f;
+      cs[c] = 1.f;
+    }
+  }
+  __syncthreads();
+  // 1) stage + data_norm output (bf16, padded to Cp); r = i / Cp without an
+  // integer division (exact: i < kRB * Cp << 2^23)
+  const float inv_cp = 1.f / (float)Cp;
   for (int i = threadIdx.x; i < rows * Cp; i += blockDim.x) {
-    const int r = i / Cp, c = i - r * Cp;
+    const int r = (int)(((float)i + 0.5f) * inv_cp), c = i - r * Cp;
     float yv = 0.f;
     if (c < C) {
       const float v = a.x[(int64_t)(row0 + r) * C + c];
       xs[r * C + c] = v;
-      if (a.bsize) {
-        const float bs = a.bsize[c];
-        const float mean = a.bsum[c] / bs;
-        const float sc = sqrtf(bs / a.bsq[c]);
-        yv = (v - mean) * sc;
-      } else {
-        yv = v;
-      }
+      yv = (v - cm[c]) * cs[c];
     }
     const unsigned short yb = f2bf(yv);
     a.y[(int64_t)(row0 + r) * ldy + c] = yb;
@@ -65,9 +83,8 @@ __global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
   }
   if (blockIdx.x == 0 && a.means) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      const float bs = a.bsize[c];
-      a.means[c] = a.bsum[c] / bs;
-      a.scales[c] = sqrtf(bs / a.bsq[c]);
+      a.means[c] = cm[c];
+      a.scales[c] = cs[c];
     }
   }
   __syncthreads();
@@ -86,8 +103,7 @@ __global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
   }
   if (a.stat_part && a.means) {  // data_norm batch statistics, per-block partial row
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      const float bs = a.bsize[c];
-      const float mean = a.bsum[c] / bs;
+      const float mean = cm[c];
       float sx = 0.f, sq = 0.f;
       for (int r = 0; r < rows; ++r) {
         const float v = xs[r * C + c];
@@ -137,13 +153,18 @@ __global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
   if (r < rows && t == 0) a.lin[row0 + r] = lin;
 }
 
+// RB rows per work-group: 16 when the data_norm statistics partials are
+// produced (their [head_blocks][2C] layout), else 8 -- twice the
+// work-groups, which the latency-bound gather/scale loop needs (2 -> 4 waves
+// per SIMD at B = 8192).  The LDS layout is the kRB-row one either way.
+template <int RB>
 __global__ __launch_bounds__(256) void k_head_bwd(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int C = a.C, Cp = a.Cp, D = a.D;
-  float* xs = lds;                 // [kRB][C]
-  float* s1s = lds + kRB * C;      // [kRB][D]
-  const int row0 = blockIdx.x * kRB;
-  const int rows = min(kRB, a.B - row0);
+  float* xs = lds;                 // [RB][C]
+  float* s1s = lds + kRB * C;      // [RB][D]
+  const int row0 = blockIdx.x * RB;
+  const int rows = min(RB, a.B - row0);
   if (rows <= 0) return;
   for (int i = threadIdx.x; i < rows * C; i += blockDim.x) {
     xs[i] = a.x[(int64_t)row0 * C + i];  // rows are contiguous
@@ -157,20 +178,35 @@ __global__ __launch_bounds__(256) void k_head_bwd(HeadArgs a) {
     s1s[r * D + d] = s1;
   }
   __syncthreads();
+  // per-column scale and role (-1 plain, -2 first-order embed_w, d >= 0
+  // embedx dim d of the FM) and per-row d lin, once per block
+  float* cs = reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(xs + kRB * (C + D)) +
+                                       kRB * head_ys_width(C, Cp));
+  int* jc = reinterpret_cast<int*>(cs + C);
+  __shared__ float dls[RB];
   const int sparse_w = a.S * a.Eo;
-  for (int i = threadIdx.x; i < rows * C; i += blockDim.x) {
-    const int r = i / C, c = i - r * C;
-    const float sc = a.scales ? a.scales[c] : 1.f;
-    float g = a.dy ? bf2f(a.dy[(int64_t)(row0 + r) * (a.ldy ? a.ldy : Cp) + c]) * sc : 0.f;
-    if (c < sparse_w && a.dlin) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    cs[c] = a.scales ? a.scales[c] : 1.f;
+    int code = -1;
+    if (c < sparse_w) {
       const int j = c % a.Eo;
-      const float dl = a.dlin[row0 + r] * (a.dlin_scale ? a.dlin_scale[0] : 1.f);
-      if (j == a.ew_col) {
-        g += dl;
-      } else if (j > a.ew_col && j <= a.ew_col + D) {
-        const int d = j - a.ew_col - 1;
-        g += dl * (s1s[r * D + d] - xs[i]);
-      }
+      if (j == a.ew_col) code = -2;
+      else if (j > a.ew_col && j <= a.ew_col + D) code = j - a.ew_col - 1;
+    }
+    jc[c] = code;
+  }
+  if (threadIdx.x < rows)
+    dls[threadIdx.x] = a.dlin ? a.dlin[row0 + threadIdx.x] * (a.dlin_scale ? a.dlin_scale[0] : 1.f) : 0.f;
+  __syncthreads();
+  const int ldy = a.ldy ? a.ldy : Cp;
+  const float inv_c = 1.f / (float)C;
+  for (int i = threadIdx.x; i < rows * C; i += blockDim.x) {
+    const int r = (int)(((float)i + 0.5f) * inv_c), c = i - r * C;
+    float g = a.dy ? bf2f(a.dy[(int64_t)(row0 + r) * ldy + c]) * cs[c] : 0.f;
+    const int code = jc[c];
+    if (code != -1 && a.dlin) {
+      const float dl = dls[r];
+      g += code == -2 ? dl : dl * (s1s[r * D + code] - xs[i]);
     }
     a.dx[(int64_t)row0 * C + i] = g;
   }
@@ -203,21 +239,27 @@ __global__ void k_dn_stats(const float* __restrict__ acc, int C, int N, float ep
 }  // namespace
 
 size_t head_lds_bytes(int C, int D, int Cp) {
-  // fp32 row slab + FM sums, then the bf16 y slab for the transposed / packed write
-  const int w = Cp > (C + 7) / 8 * 8 + 8 ? Cp : (C + 7) / 8 * 8 + 8;
-  return (size_t)kRB * (C + D) * sizeof(float) + (size_t)kRB * w * sizeof(unsigned short);
+  // fp32 row slab + FM sums, the bf16 y slab for the transposed / packed
+  // write, then two per-column arrays (fwd: mean, scale; bwd: scale, role)
+  return (size_t)kRB * (C + D) * sizeof(float) + (size_t)kRB * head_ys_width(C, Cp) * sizeof(unsigned short) +
+         (size_t)2 * C * sizeof(float);
 }
 
 void launch_head_fwd(const HeadArgs& a, hipStream_t s) {
   if (a.B == 0) return;
   const unsigned g = (unsigned)((a.B + kRB - 1) / kRB);
-  hipLaunchKernelGGL(k_head_fwd, dim3(g), dim3(256), head_lds_bytes(a.C, a.D, a.Cp), s, a);
+  hipLaunchKernelGGL(k_head_fwd, dim3(g), dim3(512), head_lds_bytes(a.C, a.D, a.Cp), s, a);
 }
 
 void launch_head_bwd(const HeadArgs& a, hipStream_t s) {
   if (a.B == 0) return;
-  const unsigned g = (unsigned)((a.B + kRB - 1) / kRB);
-  hipLaunchKernelGGL(k_head_bwd, dim3(g), dim3(256), head_lds_bytes(a.C, a.D, a.Cp), s, a);
+  if (a.stat_acc) {
+    const unsigned g = (unsigned)((a.B + kRB - 1) / kRB);
+    hipLaunchKernelGGL(k_head_bwd<kRB>, dim3(g), dim3(256), head_lds_bytes(a.C, a.D, a.Cp), s, a);
+  } else {
+    const unsigned g = (unsigned)((a.B + 7) / 8);
+    hipLaunchKernelGGL(k_head_bwd<8>, dim3(g), dim3(256), head_lds_bytes(a.C, a.D, a.Cp), s, a);
+  }
 }
 
 int head_blocks(int B) { return (B + kRB - 1) / kRB; }
