@@ -18,6 +18,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from ..utils.log import logger
 from ..parallel.dense import join_grad_producers, DenseArena, DenseSync, FlatAdagrad, FlatAdam, FlatMomentum, FlatSGD
 from .framework import (LoDTensor, Parameter, Program, Scope, Variable, default_main_program,
                         default_startup_program, global_scope, to_device, torch_dtype)
@@ -29,6 +30,9 @@ def _box():
     from ..ps.box_wrapper import BoxWrapper
 
     return BoxWrapper._instance
+
+
+log = logger()
 
 
 class ExecContext:
@@ -133,6 +137,7 @@ class Session:
         cvm_off = 2
         self.lowered: Lowered = lower(program, fetch_names, gpu=device.type == "cuda", engine_cvm_offset=cvm_off,
                                       fuse=fuse)
+        self._dump_program(device)
         self.storage: Dict[str, torch.Tensor] = {}
         self.logical: Dict[str, torch.Tensor] = {}
         self._materialize()
@@ -272,8 +277,33 @@ class Session:
         ctx.B = ctx.B or B
 
     # -------------------------------------------------------------- run
+    def _dump_program(self, device):
+        """FLAGS_enable_dump_main_program (reference boxps_worker.cc:1163-1189):
+        ./device_<id>_ops_<phase>.txt with the lowered op list (after fusion),
+        the fusions applied and the parameter storage layout."""
+        from ..utils import flags as _fl
+
+        try:
+            on = _fl.get_bool("enable_dump_main_program")
+        except Exception:
+            on = False
+        if not on:
+            return
+        dev = device.index if device.type == "cuda" and device.index is not None else 0
+        phase = "train" if self.training else "test"
+        lines = [f"# lowered program: {len(self.lowered.steps)} ops, fusions: {self.lowered.fusions}"]
+        lines += [f"{i:4d} {l}" for i, l in enumerate(self.lowered.describe().splitlines())]
+        lines += [f"storage {n}: {sp.kind} {sp.shape} (logical {sp.logical})" for n, sp in self.lowered.storage.items()]
+        with open(f"./device_{dev}_ops_{phase}.txt", "w") as f:
+            f.write("\n".join(lines) + "\n")
+
     def forward(self, ctx: ExecContext):
         prof = self.op_profiler
+        if prof is None and self._print_ops():
+            for op in self.lowered.steps:
+                log.info("op %s: %s -> %s", op.type, op.input_arg_names, op.output_arg_names)
+                KERNELS[op.type](ctx, op)
+            return
         if prof is None:
             for op in self.lowered.steps:
                 KERNELS[op.type](ctx, op)
@@ -286,6 +316,17 @@ class Session:
                 names = op.output_arg_names
                 names = names() if callable(names) else names
                 prof.watch_grad(op.type + "_grad", [ctx.env[n] for n in names if n in ctx.env])
+
+    def _print_ops(self) -> bool:
+        """FLAGS_padbox_enable_print_op_debug: log every op as it runs
+        (reference boxps_worker.cc:1304-1307); eager runs only (a captured
+        step has no per-op host work)."""
+        from ..utils import flags as _fl
+
+        try:
+            return _fl.get_bool("padbox_enable_print_op_debug")
+        except Exception:
+            return False
 
     def step(self, ctx: ExecContext):
         """forward + backward + dense sync + optimizer (one training batch)."""

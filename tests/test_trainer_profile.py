@@ -44,3 +44,30 @@ def test_cpulist_parser():
     assert _parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
     assert _parse_cpulist("") == []
     assert set(os.sched_getaffinity(0))  # the binding intersects with this set
+
+
+def test_dump_main_program_and_op_debug(tmp_path, monkeypatch, caplog):
+    """FLAGS_enable_dump_main_program writes the lowered op list;
+    FLAGS_padbox_enable_print_op_debug logs each op as it runs."""
+    import numpy as np
+
+    from paddlebox_amd.utils.flags import set_flags
+
+    monkeypatch.chdir(tmp_path)
+    set_flags({"FLAGS_enable_dump_main_program": True, "FLAGS_padbox_enable_print_op_debug": True})
+    try:
+        main, startup = fluid.Program(), fluid.Program()
+        with fluid.program_guard(main, startup), fluid.unique_name.guard():
+            x = fluid.layers.data("x", shape=[3], dtype="float32")
+            y = fluid.layers.fc(x, 2, name="f")
+            z = fluid.layers.reduce_sum(y)
+        exe = fluid.Executor(fluid.CPUPlace())
+        scope = fluid.Scope()
+        exe.run(startup, scope=scope)
+        with caplog.at_level("INFO", logger="pbx"):
+            exe.run(main, feed={"x": np.ones((4, 3), np.float32)}, fetch_list=[z], scope=scope)
+        text = (tmp_path / "device_0_ops_test.txt").read_text()
+        assert "fc" in text and "reduce_sum" in text
+        assert any("op fc" in r.getMessage() for r in caplog.records)
+    finally:
+        set_flags({"FLAGS_enable_dump_main_program": False, "FLAGS_padbox_enable_print_op_debug": False})
