@@ -212,7 +212,7 @@ class PadBoxSlotDataset(DatasetBase):
 
     def _my_files(self) -> List[str]:
         """Rank-strided filelist (data_set.cc:1963-1975)."""
-        if self.disable_polling_flag or self.world == 1:
+        if self.disable_polling_flag or self.world == 1 or _flags.get_bool("padbox_dataset_disable_polling"):
             return list(self.filelist)
         return [f for i, f in enumerate(self.filelist) if i % self.world == self.rank]
 
@@ -339,11 +339,15 @@ class PadBoxSlotDataset(DatasetBase):
         self._seed += 1
         self._native.shuffle(seed if seed is not None else (self._seed * 7919 + self.rank))
 
-    def global_shuffle(self, seed: int = 0, by_search_id: bool = False):
+    def global_shuffle(self, seed: int = 0, by_search_id: Optional[bool] = None):
         """Inter-rank record shuffle (PaddleShuffler semantics,
         data_set.cc:2422-2604): destination = hash(search_id|random) % world,
-        records exchanged with all_to_all over the process group."""
-        if self.world == 1:
+        records exchanged with all_to_all over the process group.
+        FLAGS_padbox_dataset_disable_shuffle keeps records on their rank;
+        FLAGS_enable_shuffle_by_searchid picks the search-id destination."""
+        if by_search_id is None:
+            by_search_id = _flags.get_bool("enable_shuffle_by_searchid")
+        if self.world == 1 or _flags.get_bool("padbox_dataset_disable_shuffle"):
             self.local_shuffle(seed)
             return
         n = int(self._native.size())
@@ -374,7 +378,8 @@ class PadBoxSlotDataset(DatasetBase):
         """Split this rank's records into batches such that every rank runs
         the same number of batches (data_set.cc:2692-2823)."""
         if shuffle is None:
-            shuffle = not self.disable_shuffle_flag
+            # FLAGS_padbox_disable_ins_shuffle: no per-pass instance shuffle (data_set.cc:42)
+            shuffle = not self.disable_shuffle_flag and not _flags.get_bool("padbox_disable_ins_shuffle")
         if shuffle:
             self.local_shuffle()
         n = int(self._native.size())

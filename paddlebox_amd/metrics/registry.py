@@ -221,6 +221,11 @@ class MetricRegistry:
         c = m.calc
         copc = c.actual_ctr / c.predicted_ctr if c.predicted_ctr > 0 else 0.0
         res = [c.auc, c.bucket_error, c.mae, c.rmse, c.actual_ctr, c.predicted_ctr, copc, c.size]
+        if _debug_metrics():
+            # FLAGS_enable_debug_print_metrics_info (fw/fleet/metrics.cc:29)
+            _log().info("metric %s [%s phase=%s]: auc=%.6f bucket_error=%.6f mae=%.6f rmse=%.6f actual_ctr=%.6f "
+                        "predicted_ctr=%.6f copc=%.6f size=%d", name, m.method, getattr(m, "phase", -1), *res[:7],
+                        int(res[7]))
         self._reset(m)
         return res
 
@@ -251,3 +256,18 @@ class MetricRegistry:
     def _reset(self, m: Metric):
         m.calc.reset()
         m.reset_device()
+
+
+def _debug_metrics() -> bool:
+    from ..utils import flags as _fl
+
+    try:
+        return _fl.get_bool("enable_debug_print_metrics_info")
+    except Exception:
+        return False
+
+
+def _log():
+    from ..utils.log import logger
+
+    return logger()

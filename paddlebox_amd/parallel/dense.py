@@ -168,6 +168,15 @@ class FlatAdam:
         self.pows.copy_(sd["pows"])
 
 
+def _flags_get_bool(name: str) -> bool:
+    from ..utils import flags as _fl
+
+    try:
+        return _fl.get_bool(name)
+    except Exception:
+        return False
+
+
 class HierarchicalAllReduce:
     """Node-aware all-reduce: reduce-scatter inside the node (xGMI), all-reduce
     of each shard across nodes between the ranks with the same local index,
@@ -271,7 +280,13 @@ class DenseSync:
         return 1.0 / self.world if (self.mode == "grad_allreduce" and self.world > 1) else 1.0
 
     def before_step(self):
-        """Called after backward, before the optimizer."""
+        """Called after backward, before the optimizer.
+        FLAGS_enable_dense_nccl_barrier: a barrier before the (eager) dense
+        all-reduce, so its timer measures the collective alone
+        (box_wrapper.h:711-713)."""
+        if self.active and self.mode == "grad_allreduce" and not self._launched and \
+                _flags_get_bool("enable_dense_nccl_barrier") and not (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+            dist.barrier(group=self.group)
         if self._launched or (self.active and self.mode == "grad_allreduce"):
             join_grad_producers()
         if self._launched:
@@ -300,12 +315,19 @@ class DenseSync:
             return
         self.before_step()
         opt.step(self.grad_scale())
-        self.after_step()
+        self.after_step(opt)
 
-    def after_step(self):
+    def after_step(self, opt=None):
         self.steps += 1
         if self.active and self.mode in ("kstep", "local_sgd", "kstep_node") and self.steps % self.k == 0:
             self.sync_params()
+            # FLAGS_enable_sync_dense_moment: average the Adam moments with the
+            # parameters (boxps_worker.cc:464-476)
+            if opt is not None and _flags_get_bool("enable_sync_dense_moment"):
+                for buf in (getattr(opt, "m", None), getattr(opt, "v", None)):
+                    if isinstance(buf, torch.Tensor):
+                        dist.all_reduce(buf, group=self.group)
+                        buf.mul_(1.0 / self.world)
 
     def sync_params(self):
         """Parameter averaging (boxps_worker.cc:1235-1239: sum then x 1/devices).

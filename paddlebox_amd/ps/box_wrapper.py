@@ -295,6 +295,16 @@ class BoxWrapper:
                     self._spill_cold()
         if _flags.get_bool("enable_force_hbm_recyle") and self.device.type == "cuda":
             torch.cuda.empty_cache()
+        if _flags.get_bool("enable_force_mem_recyle"):
+            # release freed host memory back to the OS at the pass boundary
+            import ctypes
+            import gc
+
+            gc.collect()
+            try:
+                ctypes.CDLL("libc.so.6").malloc_trim(0)
+            except OSError:
+                pass
         self.in_pass = False
 
     def _spill_cold(self, unseen_threshold: float = 1.0):
