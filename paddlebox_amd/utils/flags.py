@@ -2,6 +2,21 @@
 
 Backed by the native registry in ``_pbx_host`` when built (so C++ components
 see the same values); otherwise a Python dict seeded from the environment.
+
+Flags accepted for compatibility whose mechanism does not exist in this
+design (documented, not silently ignored):
+
+* ``enable_pullpush_dedup_keys`` -- keys are always deduplicated: the fused
+  push (segmented merge + in-register Adagrad) is built on the dedup.
+* ``padbox_record_pool_max_size``, ``padbox_slotpool_thread_num``,
+  ``enbale_slotpool_auto_clear``, ``enable_slotpool_wait_release``,
+  ``enable_slotrecord_reset_shrink`` -- there is no SlotRecord object pool:
+  the pass lives in a columnar CSR store (``csrc/host/slot_dataset.h``).
+* ``padbox_enable_gc`` -- intermediate tensors are freed by reference
+  counting / the HIP graph's memory pool.
+* ``padbox_dataset_shuffle_thread_num`` / ``_merge_thread_num`` -- the
+  shuffle is an all_to_all over the process group; loader threads come from
+  ``set_thread``.
 """
 from __future__ import annotations
 
