@@ -5,6 +5,7 @@
 #include "cpu_ps.h"
 #include "dump.h"
 #include "metrics.h"
+#include "msg_service.h"
 #include "runtime.h"
 #include "auc_runner.h"
 #include "batch_assembler.h"
@@ -411,6 +412,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         return t;
       })
       .def("ins_ids", [](const SlotDataset& d) { return d.store().ins_id; })
+      .def("global_shuffle", &SlotDataset::global_shuffle, py::arg("svc"), py::arg("mode"), py::arg("seed"),
+           py::arg("chunk") = 4096, py::call_guard<py::gil_scoped_release>())
       .def("save_archive", &SlotDataset::save_archive)
       .def("load_archive", &SlotDataset::load_archive, py::arg("path"), py::arg("append") = true)
       .def("export_records", [](const SlotDataset& d, const Tensor& idx) {
@@ -476,6 +479,48 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         }
         return t;
       });
+
+  // ---------------------------------------------------------------- shuffle service
+  py::class_<MsgService, std::shared_ptr<MsgService>>(m, "MsgService")
+      .def(py::init<int, int>(), py::arg("rank"), py::arg("world"))
+      .def("listen", &MsgService::listen, py::arg("host"), py::arg("port") = 0)
+      .def("connect", &MsgService::connect, py::arg("endpoints"), py::arg("timeout_s") = 60.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("register_handler", [](MsgService& s, py::function fn) {
+        // the service's threads drop their copies without the GIL: release
+        // the Python object under it
+        std::shared_ptr<py::function> holder(new py::function(std::move(fn)), [](py::function* f) {
+          py::gil_scoped_acquire gil;
+          delete f;
+        });
+        return s.register_handler([holder](int src, const char* buf, int64_t len) {
+          py::gil_scoped_acquire gil;
+          (*holder)(src, py::bytes(buf ? buf : "", (size_t)len));
+        });
+      })
+      .def("unregister_consumer", &MsgService::unregister_consumer, py::call_guard<py::gil_scoped_release>())
+      .def("send_message", [](MsgService& s, int client_id, const py::bytes& data, py::object cb) {
+        std::string buf = data;
+        MsgService::Callback c;
+        if (!cb.is_none()) {
+          std::shared_ptr<py::object> holder(new py::object(cb), [](py::object* o) {
+            py::gil_scoped_acquire gil;
+            delete o;
+          });
+          c = [holder] {
+            py::gil_scoped_acquire gil;
+            (*holder)();
+          };
+        }
+        py::gil_scoped_release nogil;
+        s.send_message(client_id, buf.data(), (int64_t)buf.size(), std::move(c));
+      }, py::arg("client_id"), py::arg("data"), py::arg("callback") = py::none())
+      .def("wait_done", &MsgService::wait_done, py::call_guard<py::gil_scoped_release>())
+      .def("destroy", &MsgService::destroy, py::call_guard<py::gil_scoped_release>())
+      .def("bytes_sent", &MsgService::bytes_sent)
+      .def("messages_handled", &MsgService::messages_handled)
+      .def_property_readonly("rank", &MsgService::rank)
+      .def_property_readonly("world", &MsgService::world);
 
   // ---------------------------------------------------------------- dump
   py::class_<BatchAssembler>(m, "BatchAssembler")

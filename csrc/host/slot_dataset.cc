@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
@@ -17,6 +18,8 @@
 #include <unordered_set>
 
 #include "../common/pbx_common.h"
+#include "dump.h"
+#include "msg_service.h"
 #include "parser_plugin.h"
 #include "runtime.h"
 
@@ -807,6 +810,163 @@ int64_t SlotDataset::load_archive(const std::string& path, bool append) {
   order_.resize(store_.nrec());
   std::iota(order_.begin(), order_.end(), 0);
   return st.nrec();
+}
+
+// ---------------------------------------------------------------- shuffle
+namespace {
+template <typename T>
+void put_vec(std::string* o, const std::vector<T>& v) {
+  const uint64_t n = v.size();
+  o->append(reinterpret_cast<const char*>(&n), 8);
+  if (n) o->append(reinterpret_cast<const char*>(v.data()), n * sizeof(T));
+}
+template <typename T>
+bool get_vec(const char*& p, const char* end, std::vector<T>* v) {
+  uint64_t n;
+  if (end - p < 8) return false;
+  memcpy(&n, p, 8);
+  p += 8;
+  if ((uint64_t)(end - p) / sizeof(T) < n) return false;
+  v->resize(n);
+  if (n) memcpy(v->data(), p, n * sizeof(T));
+  p += n * sizeof(T);
+  return true;
+}
+}  // namespace
+
+void RecordStore::serialize(std::string* out) const {
+  const int32_t hdr[2] = {nu, nf};
+  out->append(reinterpret_cast<const char*>(hdr), 8);
+  put_vec(out, u64);
+  put_vec(out, u64_off);
+  put_vec(out, f32);
+  put_vec(out, f32_off);
+  put_vec(out, search_id);
+  put_vec(out, cmatch);
+  put_vec(out, rank);
+  const uint64_t ni = ins_id.size();
+  out->append(reinterpret_cast<const char*>(&ni), 8);
+  for (const auto& s : ins_id) {
+    const uint32_t l = (uint32_t)s.size();
+    out->append(reinterpret_cast<const char*>(&l), 4);
+    out->append(s);
+  }
+}
+
+bool RecordStore::parse(const char* buf, size_t len) {
+  const char* p = buf;
+  const char* end = buf + len;
+  int32_t hdr[2];
+  if (len < 8) return false;
+  memcpy(hdr, p, 8);
+  p += 8;
+  if (hdr[0] != nu || hdr[1] != nf) return false;
+  RecordStore st;
+  st.nu = nu;
+  st.nf = nf;
+  bool ok = get_vec(p, end, &st.u64) && get_vec(p, end, &st.u64_off) && get_vec(p, end, &st.f32) &&
+            get_vec(p, end, &st.f32_off) && get_vec(p, end, &st.search_id) && get_vec(p, end, &st.cmatch) &&
+            get_vec(p, end, &st.rank);
+  uint64_t ni = 0;
+  ok = ok && end - p >= 8;
+  if (ok) {
+    memcpy(&ni, p, 8);
+    p += 8;
+  }
+  for (uint64_t i = 0; ok && i < ni; ++i) {
+    uint32_t l;
+    ok = end - p >= 4;
+    if (!ok) break;
+    memcpy(&l, p, 4);
+    p += 4;
+    ok = (uint64_t)(end - p) >= l;
+    if (ok) st.ins_id.emplace_back(p, l);
+    p += ok ? l : 0;
+  }
+  ok = ok && p == end && st.u64_off.size() >= 1 && st.f32_off.size() >= 1;
+  if (ok) append(st);
+  return ok;
+}
+
+int64_t SlotDataset::global_shuffle(MsgService& svc, int mode, uint64_t seed, int64_t chunk) {
+  const int W = svc.world(), R = svc.rank();
+  if (chunk < 1) chunk = 1;
+  const RecordStore& st = store_;
+  const int64_t n = st.nrec();
+  std::vector<std::vector<int64_t>> dest((size_t)W);
+  std::mt19937_64 rng(seed * 1000003ULL + (uint64_t)R);
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t h;
+    if (mode == 1) {
+      h = mix64(st.search_id[(size_t)i]);
+    } else if (mode == 2) {
+      const std::string& id = (size_t)i < st.ins_id.size() ? st.ins_id[(size_t)i] : std::string();
+      if (id.size() < 32) throw std::runtime_error("global_shuffle: ins_id shorter than 32 bytes: " + id);
+      h = xxh64(id.data(), 32, 0);
+    } else {
+      h = rng();
+    }
+    dest[(size_t)(h % (uint64_t)W)].push_back(i);
+  }
+
+  std::mutex mu;
+  std::condition_variable cv;
+  int finished = 0;
+  bool bad = false;
+  RecordStore incoming;
+  incoming.reset(st.nu, st.nf);
+  const int sid = svc.register_handler([&](int /*src*/, const char* buf, int64_t len) {
+    if (len == 0) {  // end of this peer's stream (FIFO per peer: after its data)
+      std::lock_guard<std::mutex> g(mu);
+      ++finished;
+      cv.notify_all();
+      return;
+    }
+    RecordStore part;
+    part.reset(st.nu, st.nf);
+    const bool ok = part.parse(buf, (size_t)len);
+    std::lock_guard<std::mutex> g(mu);
+    if (ok) {
+      incoming.append(part);
+    } else {
+      bad = true;
+    }
+  });
+  // stream the outgoing records, one message per chunk
+  std::string msg;
+  for (int r = 0; r < W; ++r) {
+    if (r == R) continue;
+    const auto& idx = dest[(size_t)r];
+    for (size_t b = 0; b < idx.size(); b += (size_t)chunk) {
+      std::vector<int64_t> part(idx.begin() + b, idx.begin() + std::min(idx.size(), b + (size_t)chunk));
+      msg.clear();
+      st.select(part).serialize(&msg);
+      svc.send_message((sid << 16) | r, msg.data(), (int64_t)msg.size(), nullptr);
+    }
+  }
+  for (int r = 0; r < W; ++r)
+    if (r != R) svc.send_message((sid << 16) | r, nullptr, 0, nullptr);
+  svc.wait_done(sid);  // every message of ours handled by its receiver
+  {
+    std::unique_lock<std::mutex> g(mu);
+    cv.wait(g, [&] { return finished == W - 1; });
+  }
+  svc.unregister_consumer(sid);
+  if (bad) throw std::runtime_error("global_shuffle: malformed shuffle message");
+
+  RecordStore kept = st.select(dest[(size_t)R]);
+  kept.append(incoming);
+  store_ = std::move(kept);
+  ++version_;
+  if (agent_ && incoming.nrec()) {
+    // the feed pass keys of the records that arrived (MergeInsKeys runs after
+    // the shuffle in the reference, data_set.cc:2293-2349)
+    KeyAgent::Stage stg(agent_.get());
+    register_keys(incoming, 0, incoming.nrec(), &stg);
+  }
+  order_.resize((size_t)store_.nrec());
+  std::iota(order_.begin(), order_.end(), 0);
+  return incoming.nrec();
 }
 
 }  // namespace pbx

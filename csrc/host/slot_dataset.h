@@ -54,7 +54,13 @@ struct RecordStore {
   void reset(int nu_, int nf_);
   void append(const RecordStore& o);
   RecordStore select(const std::vector<int64_t>& idx) const;
+  // flat byte image (shuffle messages): appends to *out; parse() appends the
+  // decoded records to *this and returns false on a malformed image
+  void serialize(std::string* out) const;
+  bool parse(const char* buf, size_t len);
 };
+
+class MsgService;
 
 class SlotDataset {
  public:
@@ -148,6 +154,15 @@ class SlotDataset {
   // dense slot sources as rows (type 0 = uint64 / 1 = float, used-slot idx,
   // width, first column) for the on-device batch builder
   std::vector<int32_t> dense_refs() const;
+
+  // Inter-rank record shuffle over the message service (PaddleShuffler flow,
+  // data_set.cc:2422-2604): every record goes to rank hash % world, where
+  // hash = random (mode 0), mix64(search_id) (1, pv merge /
+  // enable_shuffle_by_searchid) or xxh64 of the first 32 ins_id bytes (2,
+  // merge_by_insid); records travel in messages of up to `chunk` records
+  // while the receivers append them, then one empty message per peer marks
+  // the end.  Returns the number of records received from peers.
+  int64_t global_shuffle(MsgService& svc, int mode, uint64_t seed, int64_t chunk = 4096);
 
   // binary archive ("load into disk" mode)
   void save_archive(const std::string& path) const;

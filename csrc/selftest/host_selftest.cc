@@ -4,7 +4,9 @@
 // runs this driver).  It drives the concurrent paths: the multi-threaded pass
 // loader (built-in parser and a dlopen'ed plugin), the async dense table
 // (concurrent pushers vs. the update thread vs. pullers), the dump writer
-// threads, plus the CPU sparse table and the AUC calculator.
+// threads, the shuffle message service (3 in-process ranks shuffling their
+// datasets over the TCP mesh at once), plus the CPU sparse table and the AUC
+// calculator.
 //
 //   host_selftest <workdir> [plugin.so]
 #include <algorithm>
@@ -13,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -21,6 +24,7 @@
 #include "host/cpu_ps.h"
 #include "host/dump.h"
 #include "host/metrics.h"
+#include "host/msg_service.h"
 #include "host/slot_dataset.h"
 
 using namespace pbx;
@@ -166,6 +170,47 @@ static void test_cpu_table_and_auc() {
   c.compute_local();
 }
 
+static void test_global_shuffle() {
+  const int W = 3;
+  std::vector<std::unique_ptr<MsgService>> svc;
+  std::vector<std::string> eps;
+  for (int r = 0; r < W; ++r) {
+    svc.emplace_back(new MsgService(r, W));
+    eps.push_back("127.0.0.1:" + std::to_string(svc[r]->listen("127.0.0.1", 0)));
+  }
+  std::vector<std::unique_ptr<SlotDataset>> ds;
+  std::vector<std::string> lines;
+  for (int r = 0; r < W; ++r) {
+    ds.emplace_back(new SlotDataset());
+    ds[r]->set_slots(slots());
+    lines.clear();
+    for (int i = 0; i < 300 + 50 * r; ++i)
+      lines.push_back("1 " + std::to_string(i & 1) + " 1 " + std::to_string(r * 10000 + i + 1) + " 1 999999");
+    ds[r]->add_lines(lines);
+  }
+  std::vector<std::thread> ts;
+  std::atomic<int64_t> moved{0};
+  for (int r = 0; r < W; ++r)
+    ts.emplace_back([&, r] {
+      svc[r]->connect(eps);
+      moved += ds[r]->global_shuffle(*svc[r], 0, 11, 23);
+    });
+  for (auto& t : ts) t.join();
+  int64_t total = 0;
+  std::vector<uint64_t> all;
+  for (int r = 0; r < W; ++r) {
+    total += ds[r]->size();
+    auto k = ds[r]->collect_keys(false);
+    all.insert(all.end(), k.begin(), k.end());
+  }
+  CHECK(total == 300 + 350 + 400);
+  CHECK(moved.load() > 0);
+  std::sort(all.begin(), all.end());
+  all.erase(std::unique(all.begin(), all.end()), all.end());
+  CHECK(all.size() == (size_t)total + 1);  // every s1 id once, plus the shared s2 feasign
+  for (auto& s : svc) s->destroy();
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: host_selftest <workdir> [plugin.so]\n");
@@ -177,6 +222,7 @@ int main(int argc, char** argv) {
   test_async_dense();
   test_dump(dir);
   test_cpu_table_and_auc();
+  test_global_shuffle();
   if (g_fail) {
     fprintf(stderr, "host_selftest: %d check(s) failed\n", g_fail);
     return 1;

@@ -339,39 +339,26 @@ class PadBoxSlotDataset(DatasetBase):
         self._seed += 1
         self._native.shuffle(seed if seed is not None else (self._seed * 7919 + self.rank))
 
-    def global_shuffle(self, seed: int = 0, by_search_id: Optional[bool] = None):
-        """Inter-rank record shuffle (PaddleShuffler semantics,
-        data_set.cc:2422-2604): destination = hash(search_id|random) % world,
-        records exchanged with all_to_all over the process group.
-        FLAGS_padbox_dataset_disable_shuffle keeps records on their rank;
-        FLAGS_enable_shuffle_by_searchid picks the search-id destination."""
+    def global_shuffle(self, seed: int = 0, by_search_id: Optional[bool] = None, chunk: int = 4096):
+        """Inter-rank record shuffle (PaddleShuffler flow,
+        data_set.cc:2422-2604): every record goes to rank hash % world --
+        hash = xxh64 of the 32-byte line id with merge_by_lineid, mix64(search_id)
+        with pv merge or FLAGS_enable_shuffle_by_searchid, random otherwise --
+        streamed natively in messages of ``chunk`` records over the shuffle
+        message service (data/shuffler.py) while the receivers append them.
+        FLAGS_padbox_dataset_disable_shuffle keeps records on their rank."""
         if by_search_id is None:
-            by_search_id = _flags.get_bool("enable_shuffle_by_searchid")
+            by_search_id = _flags.get_bool("enable_shuffle_by_searchid") or bool(self.enable_pv_merge)
         if self.world == 1 or _flags.get_bool("padbox_dataset_disable_shuffle"):
             self.local_shuffle(seed)
-            return
-        n = int(self._native.size())
-        if by_search_id:
-            from ..ops.reference import mix64
+            return 0
+        from .shuffler import get_shuffler
 
-            dest = (mix64(self._native.search_ids()) & 0x7FFFFFFF) % self.world
-        else:
-            g = torch.Generator().manual_seed(seed * 1000003 + self.rank)
-            dest = torch.randint(0, self.world, (n,), generator=g)
-        parts = [torch.nonzero(dest == r).view(-1) for r in range(self.world)]
-        payloads = [self._native.export_records(p.contiguous()) for p in parts]
-        keep = parts[self.rank]
-        # exchange the 6 tensors of each payload
-        recvs = []
-        for field_i in range(6):
-            send_list = [payloads[r][field_i] for r in range(self.world)]
-            recvs.append(_exchange(send_list, self.group))
-        self._native.replace_store_with(keep.contiguous())
-        for r in range(self.world):
-            if r == self.rank:
-                continue
-            self._native.import_records(*(recvs[f][r] for f in range(6)))
+        svc = get_shuffler(self.rank, self.world)
+        mode = 2 if self.merge_by_lineid else (1 if by_search_id else 0)
+        got = self._native.global_shuffle(svc.svc, mode, int(seed), int(chunk))
         self.local_shuffle(seed)
+        return got
 
     # -- batching -----------------------------------------------------------
     def prepare_train(self, shuffle: Optional[bool] = None) -> List[tuple]:
@@ -533,16 +520,3 @@ class DatasetFactory:
             raise ValueError(f"datafeed class {datafeed_class} does not exist")
         return self._classes[datafeed_class](**kw)
 
-
-def _exchange(tensors: List[torch.Tensor], group=None) -> List[torch.Tensor]:
-    """Variable-size all-to-all of one tensor per peer (1-D)."""
-    world = dist.get_world_size(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
-    dtype = tensors[0].dtype
-    sizes = torch.tensor([t.numel() for t in tensors], dtype=torch.int64, device=dev)
-    rsizes = torch.empty_like(sizes)
-    dist.all_to_all_single(rsizes, sizes, group=group)
-    send = torch.cat([t.reshape(-1) for t in tensors]).to(dev)
-    recv = torch.empty(int(rsizes.sum().item()), dtype=dtype, device=dev)
-    dist.all_to_all_single(recv, send, rsizes.tolist(), sizes.tolist(), group=group)
-    return list(torch.split(recv.cpu(), rsizes.tolist()))

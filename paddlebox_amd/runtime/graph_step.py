@@ -59,6 +59,20 @@ def clone_batch(b, device):
     return pack_batch(b, device)
 
 
+def _drain_collective_watchdog(settle_s: float = 0.3):
+    """Let the RCCL process group retire the eager collectives of the warm-up
+    before a capture starts: synchronize, then give its watchdog thread (100 ms
+    poll) time to drop the completed work, so it has no event left to query
+    while the capture runs."""
+    import time
+
+    import torch.distributed as dist
+
+    torch.cuda.synchronize()
+    if dist.is_available() and dist.is_initialized():
+        time.sleep(settle_s)
+
+
 class GraphedTrainStep:
     def __init__(self, step_fn: Callable[[Any], Any], example_batch, device, n_buffers: int = 2,
                  warmup: int = 3, max_inflight: int = 3, warm_batches: Sequence[Any] = (),
@@ -105,9 +119,14 @@ class GraphedTrainStep:
         self.graphs = []
         pool = None
         n = len(self.bufs)
+        _drain_collective_watchdog()
         for j, buf in enumerate(self.bufs):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            # thread_local: RCCL's watchdog thread keeps querying the events of
+            # the eager (warm-up) collectives; under the default global mode
+            # such a query from another thread invalidates the capture and
+            # kills the watchdog (hipErrorStreamCaptureUnsupported)
+            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 if prefetch is not None:
                     eng, keys_of = prefetch
                     cap = torch.cuda.current_stream(self.device)
