@@ -4,6 +4,7 @@
 #include "async_dense.h"
 #include "cpu_ps.h"
 #include "dump.h"
+#include "file_mgr.h"
 #include "metrics.h"
 #include "msg_service.h"
 #include "runtime.h"
@@ -479,6 +480,54 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         }
         return t;
       });
+
+  // ---------------------------------------------------------------- file manager
+  py::class_<FileMgr, std::unique_ptr<FileMgr, py::nodelete>>(m, "FileMgr")
+      .def("init", &FileMgr::init, py::arg("fs_name"), py::arg("fs_ugi"), py::arg("conf_path") = "",
+           py::arg("hadoop_bin") = "")
+      .def("destroy", &FileMgr::destroy)
+      .def_static("is_remote", &FileMgr::is_remote)
+      .def("remote_prefix", &FileMgr::remote_prefix)
+      .def("list_dir", &FileMgr::list_dir, py::call_guard<py::gil_scoped_release>())
+      .def("list_info", &FileMgr::list_info, py::call_guard<py::gil_scoped_release>())
+      .def("makedir", &FileMgr::makedir, py::call_guard<py::gil_scoped_release>())
+      .def("exists", &FileMgr::exists, py::call_guard<py::gil_scoped_release>())
+      .def("download", &FileMgr::download, py::call_guard<py::gil_scoped_release>())
+      .def("upload", &FileMgr::upload, py::call_guard<py::gil_scoped_release>())
+      .def("remove", &FileMgr::remove, py::call_guard<py::gil_scoped_release>())
+      .def("file_size", &FileMgr::file_size, py::call_guard<py::gil_scoped_release>())
+      .def("dus", &FileMgr::dus, py::call_guard<py::gil_scoped_release>())
+      .def("truncate", &FileMgr::truncate, py::call_guard<py::gil_scoped_release>())
+      .def("touch", &FileMgr::touch, py::call_guard<py::gil_scoped_release>())
+      .def("rename", &FileMgr::rename, py::call_guard<py::gil_scoped_release>())
+      .def("count", &FileMgr::count, py::call_guard<py::gil_scoped_release>())
+      .def("last_command", &FileMgr::last_command)
+      // whole-file read / write through the same open paths the loaders use
+      .def("read_bytes", [](const FileMgr& f, const std::string& path, const std::string& pipe) {
+        std::string out;
+        {
+          py::gil_scoped_release nogil;
+          bool is_pipe = false;
+          FILE* fp = f.open_read(path, pipe, &is_pipe);
+          if (!fp) throw std::runtime_error("cannot open " + path);
+          char buf[1 << 16];
+          size_t n;
+          while ((n = fread(buf, 1, sizeof(buf), fp)) > 0) out.append(buf, n);
+          FileMgr::close(fp, is_pipe);
+        }
+        return py::bytes(out);
+      }, py::arg("path"), py::arg("pipe_command") = "")
+      .def("write_bytes", [](const FileMgr& f, const std::string& path, const py::bytes& data) {
+        std::string d = data;
+        py::gil_scoped_release nogil;
+        bool is_pipe = false;
+        FILE* fp = f.open_write(path, &is_pipe);
+        if (!fp) throw std::runtime_error("cannot open for write " + path);
+        const bool ok = fwrite(d.data(), 1, d.size(), fp) == d.size();
+        FileMgr::close(fp, is_pipe);
+        return ok;
+      });
+  m.def("default_file_mgr", [] { return &default_file_mgr(); }, py::return_value_policy::reference);
 
   // ---------------------------------------------------------------- shuffle service
   py::class_<MsgService, std::shared_ptr<MsgService>>(m, "MsgService")

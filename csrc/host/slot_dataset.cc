@@ -19,6 +19,7 @@
 
 #include "../common/pbx_common.h"
 #include "dump.h"
+#include "file_mgr.h"
 #include "msg_service.h"
 #include "parser_plugin.h"
 #include "runtime.h"
@@ -305,7 +306,8 @@ int64_t SlotDataset::load_index_files(const std::vector<std::string>& files, Inp
       for (;;) {
         const size_t fi = next++;
         if (fi >= files.size()) break;
-        FILE* fp = fopen(files[fi].c_str(), "r");
+        bool is_pipe = false;
+        FILE* fp = default_file_mgr().open_read(files[fi], "", &is_pipe);
         if (!fp) continue;
         char* line = nullptr;
         size_t cap = 0;
@@ -315,7 +317,7 @@ int64_t SlotDataset::load_index_files(const std::vector<std::string>& files, Inp
           if (r > 0) n += r;
         }
         free(line);
-        fclose(fp);
+        FileMgr::close(fp, is_pipe);
       }
     });
   for (auto& x : th) x.join();
@@ -422,15 +424,9 @@ int64_t SlotDataset::load_files(const std::vector<std::string>& files, RecordSto
         const size_t fi = next++;
         if (fi >= files.size()) break;
         const std::string& f = files[fi];
-        FILE* fp = nullptr;
+        // local / remote (hdfs://, afs://), plain / .gz, through the converter
         bool is_pipe = false;
-        if (pipe_command_.empty() || pipe_command_ == "cat") {
-          fp = fopen(f.c_str(), "r");
-        } else {
-          const std::string cmd = pipe_command_ + " < '" + f + "'";
-          fp = popen(cmd.c_str(), "r");
-          is_pipe = true;
-        }
+        FILE* fp = default_file_mgr().open_read(f, pipe_command_, &is_pipe);
         if (!fp) {
           bad += 1;
           continue;
@@ -445,7 +441,7 @@ int64_t SlotDataset::load_files(const std::vector<std::string>& files, RecordSto
         }
         free(line);
         if (stg) register_keys(parts[t], r0, parts[t].nrec(), stg.get());
-        if (is_pipe) pclose(fp); else fclose(fp);
+        FileMgr::close(fp, is_pipe);
       }
     });
   }

@@ -7,7 +7,7 @@ ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 OUT="${SANITIZE_OUT:-/tmp/pbx_sanitize}"
 mode="${1:-all}"
 mkdir -p "$OUT"
-SRC=("$ROOT/csrc/selftest/host_selftest.cc" "$ROOT"/csrc/host/{slot_dataset,key_agent,side_tables,cpu_ps,async_dense,dump,metrics,flags,msg_service}.cc)
+SRC=("$ROOT/csrc/selftest/host_selftest.cc" "$ROOT"/csrc/host/{slot_dataset,key_agent,side_tables,cpu_ps,async_dense,dump,metrics,flags,msg_service,file_mgr}.cc)
 g++ -O1 -g -shared -fPIC -I"$ROOT/csrc/host" "$ROOT/csrc/plugins/criteo_tsv_parser.cc" -o "$OUT/criteo_tsv_parser.so"
 run() {  # name flags...
   local name=$1; shift
