@@ -38,16 +38,36 @@ class _DistOptimizer:
         self.fleet = fleet_obj
 
     def minimize(self, loss, startup_program=None, parameter_list=None, no_grad_set=None):
+        """Inner minimize, then the strategy's program rewrite: sharding ->
+        ZeRO-1 (the executor runs ShardedFlatAdam); localsgd -> LocalSGD
+        transpile; otherwise GradAllReduce with fused gradient segments
+        (``fuse_grad_size_in_num``; one segment with ``fuse_all_reduce_ops``)."""
+        from .fluid import framework as fw
+        from .fluid.transpiler.collective import GradAllReduce, LocalSGD
+
         out = self.inner_opt.minimize(loss, startup_program, parameter_list, no_grad_set)
         s = self.user_defined_strategy
+        main = loss.block.program
+        startup = startup_program or fw.default_startup_program()
+        n, r = self.fleet.worker_num(), self.fleet.worker_index()
         if s.sharding:
-            mode, k = "sharding", 1
-        elif s.localsgd:
-            mode, k = "local_sgd", int(s.localsgd_configs.get("k_steps", 1))
+            main._collective = {"mode": "sharding", "k": 1, "nranks": n, "rank": r, "strategy": "fleet"}
+            return out
+        eps = self.fleet.worker_endpoints()
+        if s.localsgd:
+            t = LocalSGD()
+            k = int(s.localsgd_configs.get("k_steps", 1))
         else:
-            mode, k = "grad_allreduce", 1
-        loss.block.program._collective = {"mode": mode, "k": k, "nranks": self.fleet.worker_num(),
-                                          "rank": self.fleet.worker_index(), "strategy": "fleet"}
+            t = GradAllReduce(nrings=max(1, int(s.nccl_comm_num)))
+            t.fuse_grad_size_in_num = (1 << 30) if s.fuse_all_reduce_ops else int(s.fuse_grad_size_in_num)
+            k = 1
+        if k > 1:
+            # k-step averaging: the executor's model-averaging sync (DenseSync
+            # local_sgd, k) -- the transpiled LocalSGD averages every step
+            main._collective = {"mode": "local_sgd", "k": k, "nranks": n, "rank": r, "strategy": "fleet"}
+            return out
+        t.transpile(startup, main, r, eps, eps[r])
+        main._collective["strategy"] = "fleet"
         return out
 
     def __getattr__(self, name):
@@ -72,6 +92,13 @@ class Fleet:
 
     def worker_num(self) -> int:
         return dist.get_world_size() if dist.is_initialized() else 1
+
+    def worker_endpoints(self):
+        eps = os.environ.get("PADDLE_TRAINER_ENDPOINTS")
+        if eps:
+            return eps.split(",")
+        host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        return [f"{host}:{6170 + i}" for i in range(self.worker_num())]
 
     def is_first_worker(self) -> bool:
         return self.worker_index() == 0

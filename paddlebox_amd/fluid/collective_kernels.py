@@ -37,6 +37,35 @@ for _r in _OPS:
     kernel(f"c_allreduce_{_r}")(lambda ctx, op, _r=_r: _allreduce(ctx, op, _r))
 
 
+@kernel("coalesce_tensor")
+def k_coalesce_tensor(ctx, op):
+    """Fused view of many tensors (coalesce_tensor_op.cc).  When the inputs
+    are consecutive fp32 slices of one buffer -- gradients in the dense arena
+    -- the fused output is a view of that span (no copy); otherwise a packed
+    copy.  The executor writes a rewritten fused value back into the inputs
+    (``ctx.cache["coalesced"]``)."""
+    xs = [_val(ctx.get(v)) for v in op.inputs["Input"]]
+    fused = _span(xs)
+    if fused is None:
+        fused = torch.cat([x.detach().reshape(-1).float() for x in xs]) if xs else torch.zeros(0)
+    out = op.outputs["FusedOutput"][0]
+    ctx.set(out, fused)
+    ctx.cache.setdefault("coalesced", {})[out.name] = [v.name for v in op.inputs["Input"]]
+
+
+def _span(xs):
+    if not xs or any(x.dtype != torch.float32 or not x.is_contiguous() for x in xs):
+        return None
+    base = xs[0]
+    ptr = base.data_ptr()
+    for x in xs:
+        if x.untyped_storage().data_ptr() != base.untyped_storage().data_ptr() or x.data_ptr() != ptr:
+            return None
+        ptr += x.numel() * 4
+    total = sum(x.numel() for x in xs)
+    return torch.as_strided(base.detach(), (total,), (1,))
+
+
 @kernel("c_allreduce_xsum")
 def k_c_allreduce_xsum(ctx, op):
     """Grouped multi-tensor all-reduce: one fused buffer (c_allreduce_x_op.cc)."""

@@ -208,6 +208,8 @@ class Session:
         world = dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
         coll = getattr(self.program, "_collective", None) or {}
         sharded = coll.get("mode") == "sharding" and spec["type"] in ("adam", "adamw")
+        if coll.get("rewritten"):
+            sync_mode, sync_k = "none", 1  # the program's own collective ops sync (transpiler rewrite)
         if sync_mode is None and coll:
             # transpiler / fleet choice (py/fluid/transpiler/collective.py modes)
             sync_mode = {"grad_allreduce": "grad_allreduce", "local_sgd": "local_sgd", "allgather": "allgather",
@@ -349,11 +351,100 @@ class Session:
         if prof is not None:
             prof.end("backward (all grad ops + sparse push)", t0)
             t0 = prof.begin()
-        for s, o in zip(self.syncs, self.opts):
-            s.apply(o)
+        lw = self.lowered
+        if lw.backward_ops or lw.optimize_ops:
+            self._transpiled_sync(ctx)
+        else:
+            for s, o in zip(self.syncs, self.opts):
+                s.apply(o)
         join_grad_producers()  # an update issued behind the dW side stream
         if prof is not None:
             prof.end("dense sync + optimizer", t0)
+
+    # ------------------------------------------------ transpiled dense sync
+    def _logical_of(self, name: str, t: torch.Tensor) -> torch.Tensor:
+        """View of a storage-layout tensor (a parameter or its gradient) in
+        the fluid (logical) layout -- same mapping as ``_refresh_logical``."""
+        spec = self.lowered.storage.get(name)
+        if spec is None or spec.kind == "plain":
+            return t.view(spec.logical) if spec is not None else t
+        if spec.kind == "t_pad":
+            K, N = spec.logical
+            return t[:N, :K].t()
+        return t[: spec.logical[0]]
+
+    def _run_role_ops(self, ctx: ExecContext, ops, bound: Dict[str, torch.Tensor]):
+        """Run transpiler ops on ``bound`` tensors, then write every rewritten
+        value back in place (kernels are functional; coalesced buffers are
+        split back into their member tensors)."""
+        for n, t in bound.items():
+            ctx.set(n, t)
+        ctx.cache["coalesced"] = {}
+        for op in ops:
+            KERNELS[op.type](ctx, op)
+        with torch.no_grad():
+            for fused, members in ctx.cache["coalesced"].items():
+                val = ctx.env.get(fused)
+                if val is None or val.dim() != 1:
+                    continue
+                off = 0
+                for m in members:
+                    dst = bound.get(m)
+                    if dst is None:
+                        continue
+                    n = dst.numel()
+                    dst.copy_(val[off:off + n].view(dst.shape))
+                    off += n
+            for n, dst in bound.items():
+                val = ctx.env.get(n)
+                if val is not None and val is not dst:
+                    dst.copy_(val.view(dst.shape) if val.numel() == dst.numel() else val)
+            # persistable outputs that are not bound (LocalSGD snapshots) live in the scope
+            blk = self.program.global_block()
+            for op in ops:
+                for n in op.output_arg_names:
+                    if n not in bound and blk.has_var(n) and blk.var(n).persistable and n in ctx.env:
+                        self.scope.set(n, ctx.env[n].detach().clone())
+
+    def _transpiled_sync(self, ctx: ExecContext):
+        """Dense sync carried by the program (GradAllReduce / LocalSGD /
+        MultiThread transpilers): backward-role ops on the @GRAD values, the
+        optimizer update(s), then optimize-role ops on the parameters."""
+        lw = self.lowered
+        grads = {}
+        for name, st in self.storage.items():
+            if isinstance(st, torch.nn.Parameter):
+                if st.grad is None:
+                    st.grad = torch.zeros_like(st)
+                grads[name + "@GRAD"] = self._logical_of(name, st.grad)
+        self._run_role_ops(ctx, lw.backward_ops, grads)
+        gather = next((op for op in lw.backward_ops if op.type == "c_allgather" and op.attrs.get("per_rank_update")),
+                      None)
+        if gather is not None:
+            # one update per gathered gradient, in rank order (all_gather mode)
+            gathered = ctx.get(gather.outputs["Out"][0])
+            members = ctx.cache["coalesced"][gather.inputs["X"][0].name]
+            per = sum(grads[m].numel() for m in members if m in grads)
+            world = max(1, gathered.numel() // max(1, per))
+            with torch.no_grad():
+                for r in range(world):
+                    part, off = gathered[r * per:(r + 1) * per], 0
+                    for m in members:
+                        g = grads.get(m)
+                        if g is None:
+                            continue
+                        g.copy_(part[off:off + g.numel()].view(g.shape))
+                        off += g.numel()
+                    for o in self.opts:
+                        o.step(1.0 / world)
+        else:
+            for s, o in zip(self.syncs, self.opts):
+                s.apply(o)
+        if lw.optimize_ops:
+            join_grad_producers()
+            params = {name: self.logical[name] for name, st in self.storage.items()
+                      if isinstance(st, torch.nn.Parameter)}
+            self._run_role_ops(ctx, lw.optimize_ops, params)
 
     def fetch(self, ctx: ExecContext, fetch_list, return_numpy=True):
         out = []
@@ -386,7 +477,9 @@ class Executor:
     @staticmethod
     def _is_startup(program: Program) -> bool:
         ops = program.global_block().ops
-        return bool(ops) and all(op.type == "init_param" for op in ops)
+        # init_param, plus the parameter snapshots a LocalSGD transpile adds
+        return bool(ops) and program._optimize is None and all(op.type in ("init_param", "assign") for op in ops) \
+            and any(op.type == "init_param" for op in ops)
 
     def run(self, program: Optional[Program] = None, feed=None, fetch_list=None, feed_var_name="feed",
             fetch_var_name="fetch", scope: Optional[Scope] = None, return_numpy=True, use_program_cache=False,
@@ -398,6 +491,10 @@ class Executor:
             ctx = ExecContext(_StartupSession(scope, self.device, program), training=False)
             for op in program.global_block().ops:
                 KERNELS[op.type](ctx, op)
+            blk = program.global_block()
+            for name, val in ctx.env.items():  # persistable outputs (snapshots) live in the scope
+                if blk.has_var(name) and blk.var(name).persistable and isinstance(val, torch.Tensor):
+                    scope.set(name, val.detach().clone())
             return []
         names = [f if isinstance(f, str) else f.name for f in (fetch_list or [])]
         s = self._session(program, scope, names)

@@ -388,6 +388,8 @@ class Program:
             blk.vars[name] = nv
             mapping[id(v)] = nv
         for op in self.global_block().ops:
+            if for_test and op.attrs.get("op_role"):
+                continue  # transpiler-inserted gradient / update sync
             ins = {k: [mapping[id(v)] for v in vs] for k, vs in op.inputs.items()}
             outs = {k: [mapping[id(v)] for v in vs] for k, vs in op.outputs.items()}
             attrs = dict(op.attrs)

@@ -47,6 +47,10 @@ class Lowered:
     steps: List[Operator]
     storage: Dict[str, StorageSpec] = field(default_factory=dict)
     fusions: List[str] = field(default_factory=list)
+    # ops a collective transpiler appended: run after backward on the @GRAD
+    # values (op_role 1) / after the optimizer update on the parameters (2)
+    backward_ops: List[Operator] = field(default_factory=list)
+    optimize_ops: List[Operator] = field(default_factory=list)
 
     def describe(self) -> str:
         return "\n".join(f"{op.type}: {op.input_arg_names} -> {op.output_arg_names}" for op in self.steps)
@@ -249,7 +253,10 @@ def _fuse_tower(ops: List[Operator], fetch: set, notes: List[str]):
 
 def lower(program: Program, fetch_names=(), gpu: bool = True, engine_cvm_offset: int = 2,
           fuse: bool = True) -> Lowered:
-    ops = list(program.global_block().ops)
+    all_ops = list(program.global_block().ops)
+    ops = [op for op in all_ops if not op.attrs.get("op_role")]
+    bwd = [op for op in all_ops if op.attrs.get("op_role") == 1]
+    opt = [op for op in all_ops if op.attrs.get("op_role") == 2]
     fetch = set(fetch_names)
     notes: List[str] = []
     storage: Dict[str, StorageSpec] = {}
@@ -259,7 +266,7 @@ def lower(program: Program, fetch_names=(), gpu: bool = True, engine_cvm_offset:
         if gpu:
             ops = _fuse_mlp(ops, fetch, storage, notes)
             ops = _fuse_tower(ops, fetch, notes)
-    for op in ops:
+    for op in ops + bwd + opt:
         if op.type not in KERNELS:
             raise NotImplementedError(f"no kernel for op '{op.type}'")
-    return Lowered(ops, storage, notes)
+    return Lowered(ops, storage, notes, bwd, opt)

@@ -111,6 +111,7 @@ def test_transpilers_and_fleet_record_modes():
     prog, start = fluid.Program(), fluid.Program()
     fluid.transpiler.GradAllReduce().transpile(start, prog, 0, "127.0.0.1:1,127.0.0.1:2", "127.0.0.1:1")
     assert prog._collective["mode"] == "grad_allreduce" and prog._collective["nranks"] == 2
+    assert prog._collective["rewritten"]
     fluid.transpiler.LocalSGD().transpile(start, prog, 1, ["a:1", "b:2"], "b:2")
     assert prog._collective["mode"] == "local_sgd" and prog._collective["rank"] == 1
     fluid.transpiler.MultiThread(trans_mode="all_gather").transpile(start, prog, 0, "a:1", "a:1")
@@ -122,3 +123,11 @@ def test_transpilers_and_fleet_record_modes():
         loss = fluid.layers.reduce_mean(fluid.layers.fc(x, 1))
         fleet_mod.fleet.distributed_optimizer(fluid.optimizer.Adam(0.01), st).minimize(loss)
     assert prog._collective["mode"] == "sharding"
+    prog2, start2 = fluid.Program(), fluid.Program()
+    with fluid.program_guard(prog2, start2):
+        x = fluid.layers.data(name="x", shape=[4], dtype="float32")
+        loss = fluid.layers.reduce_mean(fluid.layers.fc(x, 1))
+        fleet_mod.fleet.distributed_optimizer(fluid.optimizer.Adam(0.01), fleet_mod.DistributedStrategy()).minimize(loss)
+    types = [op.type for op in prog2.global_block().ops]
+    assert prog2._collective["mode"] == "grad_allreduce" and types.count("c_allreduce_sum") == 1
+    assert "coalesce_tensor" in types
