@@ -378,8 +378,10 @@ class BoxWrapper:
                            on_reset=self._reset_delta_live)
         return f"{xbox_model_path} xbox_delta={x}"
 
-    def load_model(self, model_path: str, merge: bool = False):
-        """Load a batch model (all parts); rows are routed to their owners."""
+    def load_model(self, model_path: str, merge: bool = False, update_type: str = "add", model_index: int = 0):
+        """Load a batch model (all parts); rows are routed to their owners.
+        ``merge`` combines the model with the rows already in the table
+        (``_merge_rows``, by ``update_type``); otherwise rows are replaced."""
         keys, vals = ckpt.load_batch_model_parts(model_path)
         if keys.size == 0:
             return 0
@@ -390,23 +392,69 @@ class BoxWrapper:
             mine = ref.owner_of(h, self.world) == self.rank
             h, v = h[mine], v[mine]
         t = self._authoritative()
-        if merge:
-            cur = t.read(h.to(getattr(t, "device", "cpu")))
-            v = v.to(cur.device)
-            v[:, 0:2] += cur[:, 0:2]
         dev = getattr(t, "device", torch.device("cpu"))
-        t.insert_mixed(h.to(dev), self.cfg.sgd)
-        t.assign(h.to(dev), v.to(dev).float())
+        h, v = h.to(dev), v.to(dev).float()
+        if merge and update_type != "replace":
+            found = t.probe(h) >= 0
+            cur = t.read(h).to(dev).float()
+            v = self._merge_rows(cur, v, found, update_type, int(model_index))
+        t.insert_mixed(h, self.cfg.sgd)
+        t.assign(h, v)
         return int(h.numel())
 
-    def merge_model(self, path: str):
-        return self.load_model(path, merge=True)
+    def _merge_rows(self, cur: torch.Tensor, inc: torch.Tensor, found: torch.Tensor, update_type: str,
+                    model_index: int) -> torch.Tensor:
+        """MergeModel / MergeMultiModels row rule (the closed BoxPS merge is
+        not visible; this is this engine's documented contract -- parity
+        unpinned):
 
-    def merge_multi_models(self, paths: Sequence[str], update_type: int = 0, idx: int = 0):
-        n = 0
-        for p in paths:
-            n += self.load_model(p, merge=(update_type != 0))
-        return n
+        * ``add`` (MergeModel): show / click / delta_score summed; a key the
+          table already holds keeps its weights and optimizer state, a new
+          key takes the incoming row;
+        * ``average``: show / click / delta_score summed; weights and g2sums
+          become the running mean over the merged models, ``model_index``
+          being how many models were merged before this one;
+        * ``max_show``: per key, the row with the larger show wins;
+        * ``replace``: the incoming row wins (plain load)."""
+        l = row_layout(self.cfg.embedx_dim)
+        w = min(cur.shape[1], inc.shape[1])
+        out = inc.clone()
+        f = found
+        if not bool(f.any()):
+            return out
+        c, i = cur[f][:, :w], inc[f][:, :w]
+        stats = [l["show"], l["click"], l["delta_score"]]
+        if update_type in ("add", "merge", "sum", "0"):
+            m = c.clone()
+            m[:, stats] = c[:, stats] + i[:, stats]
+        elif update_type in ("average", "avg", "1"):
+            n = float(max(0, model_index))
+            m = (c * n + i) / (n + 1.0)
+            m[:, stats] = c[:, stats] + i[:, stats]
+            m[:, l["slot"]] = c[:, l["slot"]]
+            m[:, l["unseen_days"]] = c[:, l["unseen_days"]]
+            m[:, l["mf_size"]] = torch.maximum(c[:, l["mf_size"]], i[:, l["mf_size"]])
+        elif update_type in ("max_show", "max", "2"):
+            m = torch.where((i[:, l["show"]] > c[:, l["show"]]).unsqueeze(1), i, c)
+        else:
+            raise ValueError(f"merge: unknown update_type {update_type!r} (add / average / max_show / replace)")
+        rows = out[f]
+        rows[:, :w] = m
+        out[f] = rows
+        return out
+
+    def merge_model(self, path: str):
+        """MergeModel(path): add-merge a batch model into the table."""
+        return self.load_model(path, merge=True, update_type="add")
+
+    def merge_multi_models(self, path, update_type: str = "add", model_index: int = 0):
+        """MergeMultiModels(path, update_type, model_index): merge one model of
+        a multi-model set (``model_index`` = models merged before it); a list
+        of paths merges them in order with increasing index."""
+        if isinstance(path, (list, tuple)):
+            return sum(self.load_model(p, merge=True, update_type=str(update_type), model_index=model_index + j)
+                       for j, p in enumerate(path))
+        return self.load_model(path, merge=True, update_type=str(update_type), model_index=int(model_index))
 
     def load_ssd2mem(self, date: Optional[str] = None):
         """Preload SSD rows into host memory (LoadSSD2Mem)."""

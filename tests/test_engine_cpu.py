@@ -187,3 +187,56 @@ def test_day_id():
     # 2019-08-17 00:00 UTC = day 18125; with the -8h offset -> 18124
     assert make_day_id(2019, 8, 17, fix_dayid=True) == 18125
     assert make_day_id(2019, 8, 17, fix_dayid=False) == 18124
+
+
+def test_merge_model_update_types(tmp_path):
+    """MergeModel / MergeMultiModels(path, update_type, model_index) row rules
+    (box_wrapper.h:801-815; the closed merge is not visible -- parity unpinned,
+    the engine's contract is documented in BoxWrapper._merge_rows)."""
+    from paddlebox_amd.ps.config import row_layout
+
+    box = BoxWrapper(8, device="cpu")
+    box.initialize_gpu_and_load_model(slot_vector=[1, 2, 3], max_keys=50000)
+    b = ragged_batch(32, 3, 3, 40, seed=7)
+    box.feed_pass(b.keys, "20240101")
+    sp = SeqpoolParams()
+    out = torch.zeros(b.B, b.S * 11)
+
+    def train(n):
+        box.begin_pass()
+        for _ in range(n):
+            st = box.engine.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out, 0, sp)
+            box.engine.push_seqpool_cvm(st, torch.randn_like(out), b.cvm, 0, sp, float(b.B))
+        box.end_pass()
+
+    train(2)
+    h, v1 = box.engine.table.export(True)
+    box.save_base(str(tmp_path / "m1"), str(tmp_path / "x1"), "20240101")
+    train(3)
+    v2 = box.engine.table.read(h)
+    box.save_base(str(tmp_path / "m2"), str(tmp_path / "x2"), "20240102")
+    l = row_layout(8)
+    st = [l["show"], l["click"], l["delta_score"]]
+    w = [l["embed_w"]] + list(range(l["embedx"], l["embedx"] + 8))
+
+    t = BoxWrapper(8, device="cpu")
+    t.initialize_gpu_and_load_model(slot_vector=[1, 2, 3], max_keys=50000, model_path=str(tmp_path / "m1"))
+    # add: statistics summed, weights of known keys kept
+    t.merge_model(str(tmp_path / "m2"))
+    r = t.engine.table.read(h)
+    torch.testing.assert_close(r[:, st], v1[:, st] + v2[:, st])
+    torch.testing.assert_close(r[:, w], v1[:, w])
+    # average (one model merged before): weights -> mean of the two
+    t2 = BoxWrapper(8, device="cpu")
+    t2.initialize_gpu_and_load_model(slot_vector=[1, 2, 3], max_keys=50000, model_path=str(tmp_path / "m1"))
+    assert t2.merge_multi_models(str(tmp_path / "m2"), "average", 1) == h.numel()
+    r = t2.engine.table.read(h)
+    torch.testing.assert_close(r[:, w], (v1[:, w] + v2[:, w]) / 2)
+    torch.testing.assert_close(r[:, st], v1[:, st] + v2[:, st])
+    # max_show: m2 has seen more impressions -> its rows win
+    t3 = BoxWrapper(8, device="cpu")
+    t3.initialize_gpu_and_load_model(slot_vector=[1, 2, 3], max_keys=50000, model_path=str(tmp_path / "m1"))
+    t3.merge_multi_models(str(tmp_path / "m2"), "max_show", 0)
+    torch.testing.assert_close(t3.engine.table.read(h)[:, w], v2[:, w])
+    with pytest.raises(ValueError):
+        t3.merge_multi_models(str(tmp_path / "m2"), "bogus", 0)
