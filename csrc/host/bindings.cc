@@ -413,6 +413,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         return t;
       })
       .def("ins_ids", [](const SlotDataset& d) { return d.store().ins_id; })
+      .def("batch_ext", [](SlotDataset& d, int64_t begin, int64_t count, int dim) {
+        TORCH_CHECK(begin >= 0 && count >= 0 && begin + count <= d.size() && dim > 0, "batch_ext: range");
+        auto t = torch::empty({count, dim}, torch::kFloat32);
+        d.batch_ext(begin, count, dim, t.data_ptr<float>());
+        return t;
+      })
+      .def("store_ext", [](SlotDataset& d, int64_t begin, int64_t count, int dim, int col, const Tensor& q) {
+        TORCH_CHECK(begin >= 0 && count >= 0 && begin + count <= d.size(), "store_ext: range");
+        auto qc = q.detach().to(torch::kCPU, torch::kFloat32).contiguous().view(-1);
+        TORCH_CHECK(qc.numel() == count, "store_ext: q must hold one value per batch instance");
+        d.store_ext(begin, count, dim, col, qc.data_ptr<float>());
+      })
       .def("global_shuffle", &SlotDataset::global_shuffle, py::arg("svc"), py::arg("mode"), py::arg("seed"),
            py::arg("chunk") = 4096, py::call_guard<py::gil_scoped_release>())
       .def("save_archive", &SlotDataset::save_archive)

@@ -182,7 +182,9 @@ MsgService::Handler MsgService::handler_for(uint32_t sid) {
   // a peer may start sending before this rank registered the matching
   // consumer: hold the frame until it appears
   std::unique_lock<std::mutex> g(hmu_);
-  hcv_.wait_for(g, std::chrono::seconds(300), [&] { return stop_.load() || handlers_.count(sid) > 0; });
+  // untimed wait (destroy() wakes it): a timed condition wait on the steady
+  // clock is invisible to ThreadSanitizer's mutex tracking on this toolchain
+  hcv_.wait(g, [&] { return stop_.load() || handlers_.count(sid) > 0; });
   auto it = handlers_.find(sid);
   return it == handlers_.end() ? Handler() : it->second;
 }

@@ -38,9 +38,28 @@ void RecordStore::reset(int nu_, int nf_) {
   search_id.clear();
   cmatch.clear();
   rank.clear();
+  ext.clear();
+}
+
+void RecordStore::ensure_ext(int d) {
+  const size_t want = (size_t)nrec() * (size_t)(d > 0 ? d : 0);
+  if (d != ext_dim) {
+    ext.assign(want, 0.f);
+    ext_dim = d;
+  } else if (ext.size() != want) {
+    ext.resize(want, 0.f);
+  }
 }
 
 void RecordStore::append(const RecordStore& o) {
+  const int d = std::max(ext_dim, o.ext_dim);
+  if (d > 0) {
+    ensure_ext(d);  // before the new records land: sized by the current count
+    if (o.ext_dim == d && o.ext.size() == (size_t)o.nrec() * (size_t)d)
+      ext.insert(ext.end(), o.ext.begin(), o.ext.end());
+    else
+      ext.insert(ext.end(), (size_t)o.nrec() * (size_t)d, 0.f);
+  }
   const int64_t ub = (int64_t)u64.size(), fb = (int64_t)f32.size();
   u64.insert(u64.end(), o.u64.begin(), o.u64.end());
   f32.insert(f32.end(), o.f32.begin(), o.f32.end());
@@ -55,6 +74,13 @@ void RecordStore::append(const RecordStore& o) {
 RecordStore RecordStore::select(const std::vector<int64_t>& idx) const {
   RecordStore r;
   r.reset(nu, nf);
+  const bool has_ext = ext_dim > 0 && ext.size() == (size_t)nrec() * (size_t)ext_dim;
+  if (has_ext) {
+    r.ext_dim = ext_dim;
+    r.ext.reserve(idx.size() * (size_t)ext_dim);
+    for (int64_t i : idx)
+      r.ext.insert(r.ext.end(), ext.begin() + i * ext_dim, ext.begin() + (i + 1) * ext_dim);
+  }
   for (int64_t i : idx) {
     for (int j = 0; j < nu; ++j) {
       const int64_t b = u64_off[i * nu + j], e = u64_off[i * nu + j + 1];
@@ -764,6 +790,11 @@ void SlotDataset::save_archive(const std::string& path) const {
     fwrite(&l, 4, 1, f);
     fwrite(s.data(), 1, l, f);
   }
+  const int32_t ed = store_.ext.size() == (size_t)store_.nrec() * (size_t)store_.ext_dim ? store_.ext_dim : 0;
+  if (ed > 0) {  // optional tail: extension floats (older archives end here)
+    fwrite(&ed, 4, 1, f);
+    wvec(f, store_.ext);
+  }
   fclose(f);
 }
 
@@ -794,6 +825,11 @@ int64_t SlotDataset::load_archive(const std::string& path, bool append) {
     ok = ok && (l == 0 || fread(&s[0], 1, l, f) == l);
     st.ins_id.push_back(s);
   }
+  int32_t ed = 0;
+  if (ok && fread(&ed, 4, 1, f) == 1 && ed > 0) {
+    st.ext_dim = ed;
+    ok = rvec(f, &st.ext);
+  }
   fclose(f);
   if (!ok) throw std::runtime_error("truncated archive: " + path);
   if (!append) store_.reset(store_.nu, store_.nf);
@@ -806,6 +842,24 @@ int64_t SlotDataset::load_archive(const std::string& path, bool append) {
   order_.resize(store_.nrec());
   std::iota(order_.begin(), order_.end(), 0);
   return st.nrec();
+}
+
+// ---------------------------------------------------------------- PCOC q values
+void SlotDataset::batch_ext(int64_t begin, int64_t count, int d, float* out) {
+  store_.ensure_ext(d);
+  for (int64_t i = 0; i < count; ++i) {
+    const int64_t r = order_.empty() ? begin + i : order_[(size_t)(begin + i)];
+    memcpy(out + i * d, store_.ext.data() + r * d, sizeof(float) * (size_t)d);
+  }
+}
+
+void SlotDataset::store_ext(int64_t begin, int64_t count, int d, int col, const float* q) {
+  if (col < 0 || col >= d) throw std::out_of_range("store_ext: column");
+  store_.ensure_ext(d);
+  for (int64_t i = 0; i < count; ++i) {
+    const int64_t r = order_.empty() ? begin + i : order_[(size_t)(begin + i)];
+    store_.ext[(size_t)(r * d + col)] = q[i];
+  }
 }
 
 // ---------------------------------------------------------------- shuffle
@@ -847,6 +901,9 @@ void RecordStore::serialize(std::string* out) const {
     out->append(reinterpret_cast<const char*>(&l), 4);
     out->append(s);
   }
+  const int32_t ed = ext.size() == (size_t)nrec() * (size_t)ext_dim ? ext_dim : 0;
+  out->append(reinterpret_cast<const char*>(&ed), 4);
+  if (ed > 0) put_vec(out, ext);
 }
 
 bool RecordStore::parse(const char* buf, size_t len) {
@@ -878,6 +935,16 @@ bool RecordStore::parse(const char* buf, size_t len) {
     ok = (uint64_t)(end - p) >= l;
     if (ok) st.ins_id.emplace_back(p, l);
     p += ok ? l : 0;
+  }
+  int32_t ed = 0;
+  ok = ok && end - p >= 4;
+  if (ok) {
+    memcpy(&ed, p, 4);
+    p += 4;
+  }
+  if (ok && ed > 0) {
+    st.ext_dim = ed;
+    ok = get_vec(p, end, &st.ext);
   }
   ok = ok && p == end && st.u64_off.size() >= 1 && st.f32_off.size() >= 1;
   if (ok) append(st);

@@ -50,6 +50,12 @@ struct RecordStore {
   std::vector<std::string> ins_id;
   std::vector<uint64_t> search_id;
   std::vector<uint32_t> cmatch, rank;
+  // per-record extension floats (FLAGS_padbox_slotrecord_extend_dim: PCOC q
+  // values written by store_q_value, read back by the next batch over the
+  // record; data_feed.h:195-240 trailing float[extend_dim])
+  int ext_dim = 0;
+  std::vector<float> ext;  // [nrec * ext_dim] when ext_dim > 0
+  void ensure_ext(int d);
   int64_t nrec() const { return nu ? (int64_t)(u64_off.size() - 1) / nu : (nf ? (int64_t)(f32_off.size() - 1) / nf : (int64_t)search_id.size()); }
   void reset(int nu_, int nf_);
   void append(const RecordStore& o);
@@ -163,6 +169,14 @@ class SlotDataset {
   // while the receivers append them, then one empty message per peer marks
   // the end.  Returns the number of records received from peers.
   int64_t global_shuffle(MsgService& svc, int mode, uint64_t seed, int64_t chunk = 4096);
+
+  // PCOC q values (MiniBatchGpuPack::pack_qvalue / store_qvalue,
+  // data_feed.cc:4945-4984): the extension floats of the batch's records
+  // [count, d] in batch order, and the write-back of one column from a
+  // computed q tensor.  Neither bumps the store version (the device-resident
+  // pass does not hold extension floats).
+  void batch_ext(int64_t begin, int64_t count, int d, float* out);
+  void store_ext(int64_t begin, int64_t count, int d, int col, const float* q);
 
   // binary archive ("load into disk" mode)
   void save_archive(const std::string& path) const;

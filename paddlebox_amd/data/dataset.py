@@ -62,6 +62,9 @@ class SlotBatch:
     dense_dims: List[int]
     extra: Dict[str, torch.Tensor] = field(default_factory=dict)
     lod_host: Optional[torch.Tensor] = None  # CPU copy of lod (slot boundaries without a device sync)
+    # (native dataset, begin, count, extend_dim) of the records the batch was
+    # built from: store_q_value writes PCOC q values back into them
+    src: Optional[tuple] = None
 
     def dense_var(self, name: str) -> torch.Tensor:
         col = 0
@@ -75,7 +78,8 @@ class SlotBatch:
         mv = lambda t: t.to(device, non_blocking=non_blocking) if isinstance(t, torch.Tensor) else t  # noqa: E731
         lh = self.lod if self.lod.device.type == "cpu" else self.lod_host
         return SlotBatch(mv(self.keys), mv(self.lod), mv(self.dense), self.B, self.S, self.sparse_names,
-                         self.dense_names, self.dense_dims, {k: mv(v) for k, v in self.extra.items()}, lh)
+                         self.dense_names, self.dense_dims, {k: mv(v) for k, v in self.extra.items()}, lh,
+                         self.src)
 
     # compat with the synthetic Batch used by the models
     @property
@@ -406,6 +410,11 @@ class PadBoxSlotDataset(DatasetBase):
             b.extra["ins_ids"] = self._native.batch_ins_ids(begin, count)
         if self.parse_logkey:
             b.extra["cmatch_rank"] = self._native.batch_cmatch_rank(begin, count)
+        ext = _flags.get_int("padbox_slotrecord_extend_dim")
+        if ext > 0 and count > 0:
+            # pack_qvalue: the records' q values ride with the batch
+            b.extra["q_values"] = self._native.batch_ext(begin, count, ext)
+            b.src = (self._native, begin, count, ext)
         return b
 
     def batches(self, device=None, prefetch: int = 2, shuffle: Optional[bool] = None):

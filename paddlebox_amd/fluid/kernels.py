@@ -525,9 +525,21 @@ def k_lookup_input(ctx, op):
 
 @kernel("store_q_value")
 def k_store_q_value(ctx, op):
+    """store_q_value (store_q_value_op.cc -> MiniBatchGpuPack::store_qvalue):
+    input i holds one q value per instance and is written into extension
+    float i of the batch's records, where the next batch over those records
+    (next pass / epoch) finds it in its packed q tensor."""
     qs = [_val(ctx.get(v)).detach() for v in op.inputs["Ids"]]
-    if ctx.batch is not None:
-        ctx.batch.extra["q_values"] = torch.cat([q.reshape(q.shape[0], -1) for q in qs], 1)
+    if ctx.batch is None:
+        return
+    src = getattr(ctx.batch, "src", None)
+    if src is not None:
+        native, begin, count, dim = src
+        if len(qs) != dim:
+            raise ValueError(f"store_q_value: {len(qs)} inputs for padbox_slotrecord_extend_dim={dim}")
+        for i, q in enumerate(qs):
+            native.store_ext(begin, count, dim, i, q.reshape(-1)[:count])
+    ctx.batch.extra["q_values"] = torch.cat([q.reshape(q.shape[0], -1) for q in qs], 1)
 
 
 @kernel("cvm")

@@ -46,6 +46,10 @@ GRAPH_SAFE_OPS = {
     "elementwise_mul", "elementwise_sub", "scale", "log_loss", "mean", "reduce_sum", "tanh", "softmax",
 }
 
+# transpiler-inserted dense-sync ops (run after backward / after the update):
+# all device work on the session's communicator, capturable
+GRAPH_SAFE_SYNC_OPS = {"coalesce_tensor", "c_allreduce_sum", "scale", "elementwise_sub", "assign", "c_allgather"}
+
 
 @dataclass
 class _GraphBatch:
@@ -205,7 +209,8 @@ class BoxPSWorker:
         eng = t.box.engine if t.box is not None else None
         if eng is None or eng.auto_insert:
             return "engine auto-insert syncs the host"
-        bad = sorted({op.type for op in s.lowered.steps} - GRAPH_SAFE_OPS)
+        role_ops = {op.type for op in s.lowered.backward_ops + s.lowered.optimize_ops}
+        bad = sorted(({op.type for op in s.lowered.steps} - GRAPH_SAFE_OPS) | (role_ops - GRAPH_SAFE_SYNC_OPS))
         if bad:
             return f"ops not graph-safe: {bad}"
         return None

@@ -54,7 +54,7 @@ def _worker(rank, world, port, mode, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, _train(mode, rank, world)))
+        q.put((rank, _train(mode, rank, world).detach().numpy()))  # by value: no fd sharing with an exiting worker
     finally:
         dist.barrier()
         dist.destroy_process_group()
@@ -67,7 +67,7 @@ def _run(mode, world=2):
     ps = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in ps:
         p.start()
-    out = dict(q.get(timeout=120) for _ in ps)
+    out = {r: torch.from_numpy(v) for r, v in (q.get(timeout=120) for _ in ps)}
     for p in ps:
         p.join(timeout=60)
     return out

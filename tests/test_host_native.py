@@ -233,3 +233,51 @@ def test_key_agent_dedups_and_loader_registers_keys(tmp_path):
         assert h.numel() == want.size
     finally:
         BoxWrapper._instance = None
+
+
+def test_pcoc_q_values_follow_records(tmp_path):
+    """PCOC q values (pack_qvalue / store_qvalue, data_feed.cc:4945-4984):
+    store_q_value writes one float per instance into the records' extension
+    floats; a later batch over the same records (after a reshuffle, an archive
+    round trip) carries them in its packed q tensor."""
+    import paddlebox_amd.fluid as fluid
+    from paddlebox_amd.data.dataset import PadBoxSlotDataset
+    from paddlebox_amd.fluid.kernels import KERNELS
+
+    ds = PadBoxSlotDataset(rank=0, world=1)
+    ds._native.set_slots([h.SlotDesc("label", "uint64", True, True, 1), h.SlotDesc("s", "uint64", True, False, 1)])
+    ds._configured = True
+    n = 50
+    ds.add_lines([f"1 {i % 2} 1 {1000 + i}" for i in range(n)])
+    b = ds.build_batch(0, n)
+    assert b.extra["q_values"].shape == (n, 2) and float(b.extra["q_values"].abs().sum()) == 0.0
+    # store_q_value over this batch: q0 = key-derived, q1 = 2 * q0
+    q0 = (b.keys.float() - 1000.0) / 10.0
+    prog = fluid.Program()
+    with fluid.program_guard(prog):
+        a = fluid.layers.data(name="qa", shape=[1], dtype="float32")
+        c = fluid.layers.data(name="qb", shape=[1], dtype="float32")
+        fluid.layers._store_q_value([a, c])
+    op = prog.global_block().ops[-1]
+
+    class Ctx:
+        batch = b
+        env = {"qa": q0.view(-1, 1), "qb": (2 * q0).view(-1, 1)}
+
+        def get(self, v):
+            return self.env[v if isinstance(v, str) else v.name]
+
+    KERNELS["store_q_value"](Ctx(), op)
+    ds.local_shuffle(5)
+    b2 = ds.build_batch(0, n)
+    want = (b2.keys.float() - 1000.0) / 10.0
+    torch.testing.assert_close(b2.extra["q_values"][:, 0], want)
+    torch.testing.assert_close(b2.extra["q_values"][:, 1], 2 * want)
+    # archive keeps them
+    ds._native.save_archive(str(tmp_path / "arch"))
+    ds2 = PadBoxSlotDataset(rank=0, world=1)
+    ds2._native.set_slots([h.SlotDesc("label", "uint64", True, True, 1), h.SlotDesc("s", "uint64", True, False, 1)])
+    ds2._configured = True
+    ds2._native.load_archive(str(tmp_path / "arch"), False)
+    b3 = ds2.build_batch(0, n)
+    torch.testing.assert_close(b3.extra["q_values"][:, 0], (b3.keys.float() - 1000.0) / 10.0)

@@ -75,7 +75,7 @@ def _worker(rank, world, port, q):
         batches = _batches(world)
         flat = _train(eng, model, [batches[s][rank] for s in range(STEPS)])
         h, v = eng.table.export(True)
-        q.put((rank, flat, h, v))
+        q.put((rank, flat.detach().numpy(), h.numpy(), v.detach().numpy()))  # by value: no fd sharing with an exiting worker
     finally:
         dist.barrier()
         dist.destroy_process_group()
@@ -109,7 +109,8 @@ def test_sharded_deepfm_step_matches_single_process(world):
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict((r, (f, h, v)) for r, f, h, v in (q.get(timeout=240) for _ in ps))
+    res = dict((r, (torch.from_numpy(f), torch.from_numpy(h), torch.from_numpy(v)))
+               for r, f, h, v in (q.get(timeout=240) for _ in ps))
     for p in ps:
         p.join(timeout=60)
     flat, eng = _oracle(world)
