@@ -426,7 +426,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         d.store_ext(begin, count, dim, col, qc.data_ptr<float>());
       })
       .def("global_shuffle", &SlotDataset::global_shuffle, py::arg("svc"), py::arg("mode"), py::arg("seed"),
-           py::arg("chunk") = 4096, py::call_guard<py::gil_scoped_release>())
+           py::arg("chunk") = 4096, py::arg("threads") = 1, py::call_guard<py::gil_scoped_release>())
       .def("save_archive", &SlotDataset::save_archive)
       .def("load_archive", &SlotDataset::load_archive, py::arg("path"), py::arg("append") = true)
       .def("export_records", [](const SlotDataset& d, const Tensor& idx) {

@@ -951,7 +951,7 @@ bool RecordStore::parse(const char* buf, size_t len) {
   return ok;
 }
 
-int64_t SlotDataset::global_shuffle(MsgService& svc, int mode, uint64_t seed, int64_t chunk) {
+int64_t SlotDataset::global_shuffle(MsgService& svc, int mode, uint64_t seed, int64_t chunk, int threads) {
   const int W = svc.world(), R = svc.rank();
   if (chunk < 1) chunk = 1;
   const RecordStore& st = store_;
@@ -995,18 +995,27 @@ int64_t SlotDataset::global_shuffle(MsgService& svc, int mode, uint64_t seed, in
       bad = true;
     }
   });
-  // stream the outgoing records, one message per chunk
-  std::string msg;
-  for (int r = 0; r < W; ++r) {
-    if (r == R) continue;
-    const auto& idx = dest[(size_t)r];
-    for (size_t b = 0; b < idx.size(); b += (size_t)chunk) {
-      std::vector<int64_t> part(idx.begin() + b, idx.begin() + std::min(idx.size(), b + (size_t)chunk));
-      msg.clear();
-      st.select(part).serialize(&msg);
-      svc.send_message((sid << 16) | r, msg.data(), (int64_t)msg.size(), nullptr);
-    }
-  }
+  // stream the outgoing records, one message per chunk; `threads` workers
+  // (FLAGS_padbox_dataset_shuffle_thread_num) serialize chunks in parallel,
+  // each owning whole destinations so a destination's chunks stay in order
+  std::vector<std::thread> workers;
+  const int T = std::max(1, std::min(threads, W - 1));
+  for (int t = 0; t < T; ++t)
+    workers.emplace_back([&, t] {
+      std::string msg;
+      for (int r = 0, k = 0; r < W; ++r) {
+        if (r == R) continue;
+        if (k++ % T != t) continue;
+        const auto& idx = dest[(size_t)r];
+        for (size_t b = 0; b < idx.size(); b += (size_t)chunk) {
+          std::vector<int64_t> part(idx.begin() + b, idx.begin() + std::min(idx.size(), b + (size_t)chunk));
+          msg.clear();
+          st.select(part).serialize(&msg);
+          svc.send_message((sid << 16) | r, msg.data(), (int64_t)msg.size(), nullptr);
+        }
+      }
+    });
+  for (auto& w : workers) w.join();
   for (int r = 0; r < W; ++r)
     if (r != R) svc.send_message((sid << 16) | r, nullptr, 0, nullptr);
   svc.wait_done(sid);  // every message of ours handled by its receiver

@@ -168,7 +168,7 @@ class SlotDataset {
   // merge_by_insid); records travel in messages of up to `chunk` records
   // while the receivers append them, then one empty message per peer marks
   // the end.  Returns the number of records received from peers.
-  int64_t global_shuffle(MsgService& svc, int mode, uint64_t seed, int64_t chunk = 4096);
+  int64_t global_shuffle(MsgService& svc, int mode, uint64_t seed, int64_t chunk = 4096, int threads = 1);
 
   // PCOC q values (MiniBatchGpuPack::pack_qvalue / store_qvalue,
   // data_feed.cc:4945-4984): the extension floats of the batch's records

@@ -193,7 +193,7 @@ static void test_global_shuffle() {
   for (int r = 0; r < W; ++r)
     ts.emplace_back([&, r] {
       svc[r]->connect(eps);
-      moved += ds[r]->global_shuffle(*svc[r], 0, 11, 23);
+      moved += ds[r]->global_shuffle(*svc[r], 0, 11, 23, 2);
     });
   for (auto& t : ts) t.join();
   int64_t total = 0;

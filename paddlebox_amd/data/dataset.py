@@ -360,7 +360,8 @@ class PadBoxSlotDataset(DatasetBase):
 
         svc = get_shuffler(self.rank, self.world)
         mode = 2 if self.merge_by_lineid else (1 if by_search_id else 0)
-        got = self._native.global_shuffle(svc.svc, mode, int(seed), int(chunk))
+        threads = max(1, _flags.get_int("padbox_dataset_shuffle_thread_num"))
+        got = self._native.global_shuffle(svc.svc, mode, int(seed), int(chunk), threads)
         self.local_shuffle(seed)
         return got
 

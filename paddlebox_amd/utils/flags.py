@@ -14,9 +14,10 @@ design (documented, not silently ignored):
   the pass lives in a columnar CSR store (``csrc/host/slot_dataset.h``).
 * ``padbox_enable_gc`` -- intermediate tensors are freed by reference
   counting / the HIP graph's memory pool.
-* ``padbox_dataset_shuffle_thread_num`` / ``_merge_thread_num`` -- the
-  shuffle is an all_to_all over the process group; loader threads come from
-  ``set_thread``.
+* ``padbox_dataset_merge_thread_num`` -- feed-pass keys are registered by
+  the loader threads themselves (KeyAgent); their count comes from
+  ``set_thread``.  (``padbox_dataset_shuffle_thread_num`` is live: the
+  global shuffle's serializer threads.)
 """
 from __future__ import annotations
 
