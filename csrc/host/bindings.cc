@@ -425,6 +425,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         TORCH_CHECK(qc.numel() == count, "store_ext: q must hold one value per batch instance");
         d.store_ext(begin, count, dim, col, qc.data_ptr<float>());
       })
+      .def("unroll_instances", &SlotDataset::unroll_instances, py::call_guard<py::gil_scoped_release>())
       .def("global_shuffle", &SlotDataset::global_shuffle, py::arg("svc"), py::arg("mode"), py::arg("seed"),
            py::arg("chunk") = 4096, py::arg("threads") = 1, py::call_guard<py::gil_scoped_release>())
       .def("save_archive", &SlotDataset::save_archive)

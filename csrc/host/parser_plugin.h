@@ -59,10 +59,29 @@ typedef struct pbx_index_sink {
   void (*add_index)(void* ctx, const char* key, int key_len, const float* v, int n);
 } pbx_index_sink;
 
+// Optional 5th symbol, UnrollInstance (reference ISlotParser::UnrollInstance
+// data_feed.h:1994-1998, run on the loaded pass when
+// FLAGS_padbox_dataset_enable_unrollinstance, data_set.cc:2275-2277,2825):
+//   int64_t pbx_parser_unroll(void* parser, const pbx_record_view* view,
+//                             const pbx_ins_sink* sink);
+// The plugin reads the pass's records through `view` (slot = index into the
+// slot list given at create time; unused slots read as empty) and emits the
+// pass's NEW record set through `sink` -- any number of instances per input
+// record.  Returns the number emitted (< 0 = error: the pass is kept as is).
+typedef struct pbx_record_view {
+  void* ctx;
+  int64_t n;  // records in the pass
+  int (*get_u64)(void* ctx, int64_t rec, int slot, const uint64_t** v);  // -> count
+  int (*get_f32)(void* ctx, int64_t rec, int slot, const float** v);     // -> count
+  void (*get_meta)(void* ctx, int64_t rec, const char** ins_id, int* ins_id_len, uint64_t* search_id,
+                   uint32_t* cmatch, uint32_t* rank);
+} pbx_record_view;
+
 typedef void* (*pbx_parser_create_fn)(int, const char* const*, const char*);
 typedef int (*pbx_parser_parse_line_fn)(void*, const char*, size_t, const pbx_ins_sink*);
 typedef void (*pbx_parser_destroy_fn)(void*);
 typedef int (*pbx_parser_parse_index_fn)(void*, const char*, size_t, const pbx_index_sink*);
+typedef int64_t (*pbx_parser_unroll_fn)(void*, const pbx_record_view*, const pbx_ins_sink*);
 
 #ifdef __cplusplus
 }

@@ -177,6 +177,7 @@ struct SlotDataset::Plugin {
   pbx_parser_parse_line_fn parse = nullptr;
   pbx_parser_destroy_fn destroy = nullptr;
   pbx_parser_parse_index_fn parse_index = nullptr;
+  pbx_parser_unroll_fn unroll = nullptr;
   ~Plugin() {
     if (parser && destroy) destroy(parser);
     if (so) dlclose(so);
@@ -284,6 +285,7 @@ void SlotDataset::set_so_parser(const std::string& path) {
   pl->parse = (pbx_parser_parse_line_fn)dlsym(pl->so, "pbx_parser_parse_line");
   pl->destroy = (pbx_parser_destroy_fn)dlsym(pl->so, "pbx_parser_destroy");
   pl->parse_index = (pbx_parser_parse_index_fn)dlsym(pl->so, "pbx_parser_parse_index");  // optional
+  pl->unroll = (pbx_parser_unroll_fn)dlsym(pl->so, "pbx_parser_unroll");                // optional
   if (!create || !pl->parse || !pl->destroy)
     throw std::runtime_error("so parser " + path + ": missing pbx_parser_{create,parse_line,destroy}");
   std::vector<const char*> names;
@@ -842,6 +844,73 @@ int64_t SlotDataset::load_archive(const std::string& path, bool append) {
   order_.resize(store_.nrec());
   std::iota(order_.begin(), order_.end(), 0);
   return st.nrec();
+}
+
+// ---------------------------------------------------------------- UnrollInstance
+namespace {
+struct ViewCtx {
+  const RecordStore* st;
+  const std::vector<int>* u_idx;
+  const std::vector<int>* f_idx;
+};
+int view_get_u64(void* c, int64_t rec, int slot, const uint64_t** v) {
+  const ViewCtx* x = (const ViewCtx*)c;
+  if (rec < 0 || rec >= x->st->nrec() || slot < 0 || slot >= (int)x->u_idx->size()) return 0;
+  const int j = (*x->u_idx)[slot];
+  if (j < 0) return 0;
+  const int64_t b = x->st->u64_off[rec * x->st->nu + j], e = x->st->u64_off[rec * x->st->nu + j + 1];
+  *v = x->st->u64.data() + b;
+  return (int)(e - b);
+}
+int view_get_f32(void* c, int64_t rec, int slot, const float** v) {
+  const ViewCtx* x = (const ViewCtx*)c;
+  if (rec < 0 || rec >= x->st->nrec() || slot < 0 || slot >= (int)x->f_idx->size()) return 0;
+  const int j = (*x->f_idx)[slot];
+  if (j < 0) return 0;
+  const int64_t b = x->st->f32_off[rec * x->st->nf + j], e = x->st->f32_off[rec * x->st->nf + j + 1];
+  *v = x->st->f32.data() + b;
+  return (int)(e - b);
+}
+void view_get_meta(void* c, int64_t rec, const char** id, int* id_len, uint64_t* sid, uint32_t* cm, uint32_t* rk) {
+  const ViewCtx* x = (const ViewCtx*)c;
+  const RecordStore& st = *x->st;
+  const bool has_id = (size_t)rec < st.ins_id.size();
+  *id = has_id ? st.ins_id[(size_t)rec].data() : "";
+  *id_len = has_id ? (int)st.ins_id[(size_t)rec].size() : 0;
+  *sid = st.search_id[(size_t)rec];
+  *cm = st.cmatch[(size_t)rec];
+  *rk = st.rank[(size_t)rec];
+}
+}  // namespace
+
+int64_t SlotDataset::unroll_instances() {
+  if (!plugin_ || !plugin_->unroll) return store_.nrec();  // reference default: records unchanged
+  ViewCtx vc{&store_, &u_idx_, &f_idx_};
+  const pbx_record_view view{&vc, store_.nrec(), view_get_u64, view_get_f32, view_get_meta};
+  RecordStore out;
+  out.reset(store_.nu, store_.nf);
+  SinkCtx ctx;
+  ctx.u_idx = &u_idx_;
+  ctx.f_idx = &f_idx_;
+  ctx.slots = &slots_;
+  ctx.keep_ins_id = true;
+  ctx.need_sparse = !sparse_slots_.empty();
+  ctx.st = &out;
+  ctx.u.resize(store_.nu);
+  ctx.f.resize(store_.nf);
+  ctx.clear();
+  const pbx_ins_sink sink{&ctx, sink_add_u64, sink_add_f32, sink_set_meta, sink_commit, nullptr, nullptr};
+  const int64_t n = plugin_->unroll(plugin_->parser, &view, &sink);
+  if (n < 0) return -1;
+  store_ = std::move(out);
+  ++version_;
+  if (agent_) {
+    KeyAgent::Stage stg(agent_.get());
+    register_keys(store_, 0, store_.nrec(), &stg);
+  }
+  order_.resize((size_t)store_.nrec());
+  std::iota(order_.begin(), order_.end(), 0);
+  return store_.nrec();
 }
 
 // ---------------------------------------------------------------- PCOC q values

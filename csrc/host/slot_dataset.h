@@ -178,6 +178,12 @@ class SlotDataset {
   void batch_ext(int64_t begin, int64_t count, int d, float* out);
   void store_ext(int64_t begin, int64_t count, int d, int col, const float* q);
 
+  // UnrollInstance (FLAGS_padbox_dataset_enable_unrollinstance): the parser
+  // plugin's optional pbx_parser_unroll rewrites the loaded pass (any number
+  // of instances per record).  Returns the new record count (-1: the plugin
+  // failed and the pass is unchanged); without the hook the pass is kept.
+  int64_t unroll_instances();
+
   // binary archive ("load into disk" mode)
   void save_archive(const std::string& path) const;
   int64_t load_archive(const std::string& path, bool append);

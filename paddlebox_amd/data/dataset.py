@@ -244,10 +244,19 @@ class PadBoxSlotDataset(DatasetBase):
             else:
                 self._native.set_filelist(files)
                 self._native.load_into_memory()
+            self._maybe_unroll()
         finally:
             self._native.set_key_agent(None)
         if agent is not None:
             self._close_feed_pass(agent)
+
+    def _maybe_unroll(self):
+        """FLAGS_padbox_dataset_enable_unrollinstance: the parser plugin's
+        UnrollInstance hook rewrites the loaded pass (data_set.cc:2275-2277);
+        runs while the feed-pass agent is attached so new feasigns register."""
+        if _flags.get_bool("padbox_dataset_enable_unrollinstance") and self._native.has_so_parser():
+            if self._native.unroll_instances() < 0:
+                raise RuntimeError("parser plugin UnrollInstance failed")
 
     def _open_feed_pass(self):
         """BeginFeedPass: the loader threads register every parsed record's
@@ -299,6 +308,7 @@ class PadBoxSlotDataset(DatasetBase):
     def wait_preload_done(self, register_keys: bool = True):
         try:
             self._native.wait_preload_done()
+            self._maybe_unroll()
         finally:
             self._native.set_key_agent(None)
         agent, self._preload_agent = getattr(self, "_preload_agent", None), None

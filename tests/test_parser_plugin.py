@@ -153,3 +153,86 @@ def test_replica_cache_feed_through_the_feed_pass(side_plugin, tmp_path):
     finally:
         set_flags({"FLAGS_use_gpu_replica_cache": False})
         BoxWrapper._instance = None
+
+
+UNROLL_PLUGIN = r"""
+// test plugin: lines "label k1 k2 ...": one instance with all keys in slot 1;
+// UnrollInstance splits every record into one instance per key
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "parser_plugin.h"
+extern "C" {
+void* pbx_parser_create(int, const char* const*, const char*) { return (void*)1; }
+void pbx_parser_destroy(void*) {}
+int pbx_parser_parse_line(void*, const char* line, size_t len, const pbx_ins_sink* s) {
+  char buf[512];
+  if (len >= sizeof(buf)) return -1;
+  memcpy(buf, line, len); buf[len] = 0;
+  char* p = buf;
+  uint64_t lab = strtoull(p, &p, 10);
+  s->add_u64(s->ctx, 0, &lab, 1);
+  for (;;) {
+    char* q;
+    uint64_t k = strtoull(p, &q, 10);
+    if (q == p) break;
+    p = q;
+    s->add_u64(s->ctx, 1, &k, 1);
+  }
+  char id[40];
+  int n = snprintf(id, sizeof(id), "line-%llu", (unsigned long long)lab);
+  s->set_meta(s->ctx, id, n, 0, 0, 0);
+  return s->commit(s->ctx);
+}
+int64_t pbx_parser_unroll(void*, const pbx_record_view* v, const pbx_ins_sink* s) {
+  int64_t out = 0;
+  for (int64_t r = 0; r < v->n; ++r) {
+    const uint64_t *lab, *keys;
+    if (v->get_u64(v->ctx, r, 0, &lab) != 1) return -1;
+    const int nk = v->get_u64(v->ctx, r, 1, &keys);
+    for (int i = 0; i < nk; ++i) {
+      s->add_u64(s->ctx, 0, lab, 1);
+      s->add_u64(s->ctx, 1, &keys[i], 1);
+      out += s->commit(s->ctx);
+    }
+  }
+  return out;
+}
+}
+"""
+
+
+def test_unroll_instance_hook(tmp_path):
+    """FLAGS_padbox_dataset_enable_unrollinstance + the plugin's optional
+    pbx_parser_unroll (reference ISlotParser::UnrollInstance,
+    data_feed.h:1994-1998, data_set.cc:2275-2277)."""
+    from paddlebox_amd.utils.flags import set_flags
+
+    src = tmp_path / "unroll.cc"
+    src.write_text(UNROLL_PLUGIN)
+    so = str(tmp_path / "unroll.so")
+    subprocess.run(["g++", "-O2", "-shared", "-fPIC", "-I" + os.path.join(ROOT, "csrc", "host"), str(src), "-o", so],
+                   check=True)
+    data = tmp_path / "part-0"
+    data.write_text("1 11 12 13\n0 21\n1 31 32\n")
+
+    def load(flag):
+        set_flags({"FLAGS_padbox_dataset_enable_unrollinstance": flag})
+        try:
+            ds = PadBoxSlotDataset(rank=0, world=1)
+            ds.set_use_var([SlotVar("label", "int64", (1,), 0), SlotVar("s", "int64")])
+            ds.set_so_parser_name(so)
+            ds.set_filelist([str(data)])
+            ds.load_into_memory(register_keys=False)
+            return ds
+        finally:
+            set_flags({"FLAGS_padbox_dataset_enable_unrollinstance": False})
+
+    plain = load(False)
+    assert plain.get_memory_data_size() == 3
+    un = load(True)
+    assert un.get_memory_data_size() == 6
+    keys, lod, dense = un._native.build_batch(0, 6, False)
+    assert keys.tolist() == [11, 12, 13, 21, 31, 32]
+    assert lod.tolist() == [0, 1, 2, 3, 4, 5, 6]
+    assert dense[:, 0].tolist() == [1, 1, 1, 0, 1, 1]
