@@ -149,14 +149,21 @@ __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
   float* o = a.out + (int64_t)b * a.out_stride + a.col_offset + (int64_t)s * Eo;
   if (a.use_cvm) {
     const float ls = logf(acc[0] + 1.f);
-    o[0] = ls;
     if (a.clk_filter) {
+      o[0] = ls;
 #pragma unroll
       for (int c = 2; c < E; ++c) o[c - 1] = acc[c];
     } else {
-      o[1] = logf(acc[1] + 1.f) - ls;
+      // the E floats of the row are contiguous and 4-B aligned: dwordx4
+      // stores (3 requests instead of 11 for E = 11)
+      typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+      acc[1] = logf(acc[1] + 1.f) - ls;
+      acc[0] = ls;
 #pragma unroll
-      for (int c = 2; c < E; ++c) o[c] = acc[c];
+      for (int c = 0; c + 4 <= E; c += 4)
+        *reinterpret_cast<f4u*>(o + c) = f4u{acc[c], acc[c + 1], acc[c + 2], acc[c + 3]};
+#pragma unroll
+      for (int c = E / 4 * 4; c < E; ++c) o[c] = acc[c];
     }
   } else {
 #pragma unroll
@@ -239,6 +246,34 @@ struct DoutSource {
     (void)Q;
   }
   __device__ __forceinline__ float slot(int32_t k) const { return a.slot_ids ? a.slot_ids[a.occ_slot[k]] : (float)a.occ_slot[k]; }
+  // common layout (use_cvm, no click filter, cvm_offset 2, E = 3 + D): the
+  // D + 1 embedding grads are contiguous and 4-B aligned, so they move as
+  // dwordx4 loads -- 4 memory requests per occurrence instead of 11 (the
+  // scalar gathers were ~80% of this kernel's L2 requests, PMC TCC_HIT+MISS)
+  __device__ __forceinline__ bool fast(int D) const {
+    return a.use_cvm && !a.clk_filter && a.cvm_offset == 2 && a.E == 3 + D;
+  }
+  template <int D>
+  __device__ __forceinline__ void load_fast(int32_t k, float* g) const {
+    typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+    typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+    const int b = a.occ_ins[k], s = a.occ_slot[k];
+    const f2u c = *reinterpret_cast<const f2u*>(a.cvm + (int64_t)b * 2);
+    g[0] = c.x;
+    g[1] = c.y;
+    const float* d = a.dout + (int64_t)b * a.out_stride + a.col_offset + (int64_t)s * (3 + D) + 2;
+    constexpr int N = 1 + D;
+#pragma unroll
+    for (int i = 0; i + 4 <= N; i += 4) {
+      const f4u x = *reinterpret_cast<const f4u*>(d + i);
+      g[2 + i] = x.x;
+      g[3 + i] = x.y;
+      g[4 + i] = x.z;
+      g[5 + i] = x.w;
+    }
+#pragma unroll
+    for (int i = N / 4 * 4; i < N; ++i) g[2 + i] = d[i];
+  }
 };
 
 template <int Q, typename Src>
@@ -518,7 +553,10 @@ __global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, TableD
   if (p < pv) {
     k = a.perm[p];
     u = a.uid[k];
-    src.load(k, g, Q);
+    if (src.fast(D))
+      src.template load_fast<D>(k, g);
+    else
+      src.load(k, g, Q);
   }
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
