@@ -88,18 +88,18 @@ __global__ void k_emit(const uint64_t* __restrict__ hs, const int32_t* __restric
 //              in id order (nobody needs that), which replaces a device-wide
 //              scan (two launches) with one short kernel
 //   scatter  : perm[seg[u] + rank] = occurrence
-// The table is cleaned lazily at the start of the next run (only the U
-// slots that were used), so no per-batch memset of the table.
+// The used table slots are released by k_seg_alloc (the table is not read
+// after k_hash_rank) and the per-id counts at the start of the next run, so
+// there is no per-batch memset of the table.
 // u_count = [U, n_valid, U of the previous run, segment cursor]
 constexpr int kRankItems = 4;      // occurrences per thread in k_hash_rank
 constexpr int kRankLds = 2048;     // LDS hash entries per block (load <= 0.5)
 constexpr int kSegItems = 4;       // unique ids per thread in k_seg_alloc
 
-__global__ void k_hash_cleanup(int32_t* __restrict__ u_count, const int32_t* __restrict__ slot_of_u,
-                               uint64_t* __restrict__ tk, int32_t* __restrict__ tu, int32_t* __restrict__ cnt,
-                               int64_t cap) {
+__global__ void k_hash_cleanup(int32_t* __restrict__ u_count, int32_t* __restrict__ cnt, int64_t cap) {
   // the previous run's scatter kernel saved its U into [2], so [0], [1] and
-  // the cursor [3] can be reset here
+  // the cursor [3] can be reset here; its table slots were already released
+  // by its k_seg_alloc, so only the (coalesced) per-id counts remain
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u == 0) {
     u_count[0] = 0;
@@ -107,9 +107,6 @@ __global__ void k_hash_cleanup(int32_t* __restrict__ u_count, const int32_t* __r
     u_count[3] = 0;
   }
   if (u >= cap || u >= u_count[2]) return;
-  const int32_t p = slot_of_u[u];
-  tk[p] = kEmptyKey;
-  tu[p] = -1;
   cnt[u] = 0;
 }
 
@@ -255,8 +252,12 @@ __global__ __launch_bounds__(256) void k_hash_rank(const int32_t* __restrict__ s
   }
 }
 
+// Also releases the run's hash-set slots (tk / tu are not read after
+// k_hash_rank): the random slot writes ride on this kernel's pass over the
+// ids instead of a separate cleanup pass at the start of the next run.
 __global__ __launch_bounds__(256) void k_seg_alloc(const int32_t* __restrict__ cnt, int32_t* __restrict__ u_count,
-                                                   int32_t* __restrict__ seg) {
+                                                   int32_t* __restrict__ seg, const int32_t* __restrict__ slot_of_u,
+                                                   uint64_t* __restrict__ tk, int32_t* __restrict__ tu) {
   __shared__ int32_t wsum[4];
   __shared__ int32_t base;
   const int64_t U = u_count[0];
@@ -284,7 +285,12 @@ __global__ __launch_bounds__(256) void k_seg_alloc(const int32_t* __restrict__ c
   for (int i = 0; i < w; ++i) p += wsum[i];
 #pragma unroll
   for (int t = 0; t < kSegItems; ++t) {
-    if (u0 + t < U) seg[u0 + t] = p;
+    if (u0 + t < U) {
+      seg[u0 + t] = p;
+      const int32_t sl = slot_of_u[u0 + t];
+      tk[sl] = kEmptyKey;
+      tu[sl] = -1;
+    }
     p += c[t];
   }
 }
@@ -337,7 +343,7 @@ size_t hash_dedup_temp_bytes(int64_t cap) {
 void launch_dedup_hash(const HashDedupArgs& a, void* temp, size_t temp_bytes, hipStream_t s) {
   const int64_t cap = a.cap;
   const unsigned gc = (unsigned)((cap + 255) / 256);
-  hipLaunchKernelGGL(k_hash_cleanup, dim3(gc), dim3(256), 0, s, a.u_count, a.slot_of_u, a.tk, a.tu, a.cnt, cap);
+  hipLaunchKernelGGL(k_hash_cleanup, dim3(gc), dim3(256), 0, s, a.u_count, a.cnt, cap);
   if (a.n <= 0) {
     launch_fill32(a.seg, 0u, 1, s);
     launch_fill32(a.u_count + 2, 0u, 1, s);
@@ -352,7 +358,7 @@ void launch_dedup_hash(const HashDedupArgs& a, void* temp, size_t temp_bytes, hi
   (void)temp;
   (void)temp_bytes;
   const unsigned gs = (unsigned)((a.n + 256 * kSegItems - 1) / (256 * kSegItems));  // U <= n
-  hipLaunchKernelGGL(k_seg_alloc, dim3(gs), dim3(256), 0, s, a.cnt, a.u_count, a.seg);
+  hipLaunchKernelGGL(k_seg_alloc, dim3(gs), dim3(256), 0, s, a.cnt, a.u_count, a.seg, a.slot_of_u, a.tk, a.tu);
   hipLaunchKernelGGL(k_hash_scatter, dim3(g), dim3(256), 0, s, a.uid, a.rank, a.seg, a.n, a.perm, a.u_count);
 }
 

@@ -233,6 +233,7 @@ class Session:
             self.syncs.append(DenseSync(arena, sync_mode, sync_k, self.group))
         # arena rebinding moved the storage: re-point logical views
         self._refresh_logical()
+        self._restore_optimizer_state_from_scope()
 
     # -------------------------------------------------------------- feeding
     def feed_batch(self, ctx: ExecContext, batch):
@@ -361,6 +362,57 @@ class Session:
         if prof is not None:
             prof.end("dense sync + optimizer", t0)
 
+    # ------------------------------------------------ optimizer state (checkpoints)
+    def _opt_slots(self):
+        """(param name, optimizer, element offset in its arena, storage shape)
+        for every trainable parameter with Adam state."""
+        for a, o in zip(self.arenas, self.opts):
+            if not isinstance(o, FlatAdam):
+                continue
+            base = a.flat.data_ptr()
+            for name, st in self.storage.items():
+                if isinstance(st, torch.nn.Parameter) and st.untyped_storage().data_ptr() == \
+                        a.flat.untyped_storage().data_ptr():
+                    yield name, o, (st.data_ptr() - base) // 4, st.shape
+
+    def optimizer_state(self) -> Dict[str, torch.Tensor]:
+        """Adam state under the reference's persistable names
+        (``<param>_moment1_0``, ``_moment2_0``, ``_beta1_pow_acc_0``,
+        ``_beta2_pow_acc_0``, fluid/optimizer.py AdamOptimizer), in the
+        parameters' fluid layout, so save_persistables / load_persistables
+        resume training exactly."""
+        out = {}
+        for name, o, off, shape in self._opt_slots():
+            n = int(np.prod(shape))
+            out[name + "_moment1_0"] = self._logical_of(name, o.m[off:off + n].view(shape))
+            out[name + "_moment2_0"] = self._logical_of(name, o.v[off:off + n].view(shape))
+            out[name + "_beta1_pow_acc_0"] = o.pows[0:1]
+            out[name + "_beta2_pow_acc_0"] = o.pows[1:2]
+        return out
+
+    def load_optimizer_state(self, state: Dict[str, Any]) -> int:
+        n_loaded = 0
+        with torch.no_grad():
+            for name, o, off, shape in self._opt_slots():
+                n = int(np.prod(shape))
+                for suffix, buf in (("_moment1_0", o.m), ("_moment2_0", o.v)):
+                    if name + suffix in state:
+                        dst = self._logical_of(name, buf[off:off + n].view(shape))
+                        dst.copy_(torch.as_tensor(state[name + suffix]).reshape(dst.shape).to(dst.device))
+                        n_loaded += 1
+                for i, suffix in enumerate(("_beta1_pow_acc_0", "_beta2_pow_acc_0")):
+                    if name + suffix in state:
+                        o.pows[i:i + 1].copy_(torch.as_tensor(state[name + suffix]).reshape(1).to(o.pows.device))
+        return n_loaded
+
+    def _restore_optimizer_state_from_scope(self):
+        """load_persistables before the first run stages Adam state in the
+        scope (no session yet); pick it up once the optimizers exist."""
+        names = {n for n in self.optimizer_state()}
+        staged = {n: self.scope.get(n) for n in names if n in self.scope}
+        if staged:
+            self.load_optimizer_state(staged)
+
     # ------------------------------------------------ transpiled dense sync
     def _logical_of(self, name: str, t: torch.Tensor) -> torch.Tensor:
         """View of a storage-layout tensor (a parameter or its gradient) in
@@ -464,6 +516,9 @@ class Executor:
         self.place = place
         self.device = to_device(place)
         self._sessions: Dict[tuple, Session] = {}
+
+    def sessions_for(self, program: Program) -> List[Session]:
+        return [s for k, s in self._sessions.items() if k[0] == id(program) and s.training]
 
     def _session(self, program: Program, scope: Scope, fetch_names=(), **kw) -> Session:
         key = (id(program), program._version, id(scope), tuple(sorted(fetch_names)))

@@ -84,14 +84,47 @@ def load_vars(executor, dirname: str, main_program: Optional[Program] = None, va
     return loaded
 
 
-def save_persistables(executor, dirname: str, main_program: Optional[Program] = None, filename=None):
-    program = main_program or default_main_program()
-    return save_vars(executor, dirname, program, _persistables(program), filename=filename)
+_OPT_FILE = "__optimizer_state__.safetensors"
 
 
-def load_persistables(executor, dirname: str, main_program: Optional[Program] = None, filename=None):
+def save_persistables(executor, dirname: str, main_program: Optional[Program] = None, filename=None, scope=None):
+    """Persistable variables plus the optimizer state of the executor's
+    training session for the program (Adam moments / beta powers under the
+    reference's ``<param>_moment1_0``-style names; one safetensors file)."""
     program = main_program or default_main_program()
-    return load_vars(executor, dirname, program, _persistables(program), filename=filename)
+    saved = save_vars(executor, dirname, program, _persistables(program), filename=filename, scope=scope)
+    sessions = executor.sessions_for(program) if hasattr(executor, "sessions_for") else []
+    if sessions:
+        from safetensors.numpy import save_file
+
+        st = {k: np.ascontiguousarray(_to_np(v)) for k, v in sessions[0].optimizer_state().items()}
+        if st:
+            save_file(st, os.path.join(dirname, _OPT_FILE))
+            saved += list(st)
+    return saved
+
+
+def load_persistables(executor, dirname: str, main_program: Optional[Program] = None, filename=None,
+                      scope=None):
+    """Load persistables; optimizer state goes into the live training session
+    when the program already ran, else into the scope, where the session
+    picks it up when it builds its optimizers (exact resume)."""
+    program = main_program or default_main_program()
+    loaded = load_vars(executor, dirname, program, _persistables(program), filename=filename, scope=scope)
+    p = os.path.join(dirname, _OPT_FILE)
+    if os.path.exists(p):
+        from safetensors.numpy import load_file
+
+        st = load_file(p)
+        sessions = executor.sessions_for(program) if hasattr(executor, "sessions_for") else []
+        if sessions:
+            sessions[0].load_optimizer_state(st)
+        else:
+            sc = scope or global_scope()
+            for k, a in st.items():
+                sc.set(k, torch.as_tensor(a))
+        loaded += list(st)
+    return loaded
 
 
 def save_params(executor, dirname: str, main_program: Optional[Program] = None, filename=None):

@@ -223,3 +223,58 @@ def test_xxh64_known_values():
     assert h.xxh64("", 0) == 0xEF46DB3751D8E999
     assert h.xxh64("a", 0) == 0xD24EC4F1A98C6E5B
     assert h.xxh64("abc", 0) == 0x44BC2CF5AD770999
+
+
+def _resume_run(tmp_path, files, passes_before, passes_after, ckpt=None, restore=None, device="cpu"):
+    """Train `passes_before` passes (saving sparse + dense + optimizer state
+    into `ckpt` after them), then `passes_after` more; or restore from
+    `restore` first.  Returns dense params, data_norm summaries, sparse table."""
+    BoxWrapper._instance = None
+    box = fluid.core.BoxWrapper(8, device=device, new=True)
+    box.cfg.sgd.mf_create_thresholds = 0.0
+    box.initialize_gpu_and_load_model(slot_vector=list(range(S)), max_keys=200000,
+                                      model_path=str(restore / "sparse") if restore else None)
+    scope = fluid.Scope()
+    main, startup, slots, label, dense, pred, loss = _build()
+    exe = fluid.Executor(fluid.CPUPlace() if device == "cpu" else fluid.CUDAPlace(0))
+    exe.run(startup, scope=scope)
+    if restore:
+        fluid.io.load_persistables(exe, str(restore / "dense"), main, scope=scope)
+    ds = fluid.DatasetFactory().create_dataset("PadBoxSlotDataset")
+    ds.set_use_var([label] + slots + [dense])
+    ds.set_batch_size(64)
+    ds.set_filelist(files)
+    ds.disable_shuffle()
+    boxps = fluid.core.BoxPS(ds)
+    boxps.read_ins_into_memory()
+    for i in range(passes_before + passes_after):
+        boxps.begin_pass()
+        exe.train_from_dataset(main, ds, scope=scope, fetch_list=[loss], print_period=1000)
+        boxps.end_pass()
+        if ckpt is not None and i + 1 == passes_before:
+            box.save_base(str(ckpt / "sparse"), str(ckpt / "xbox"), "20240101")
+            fluid.io.save_persistables(exe, str(ckpt / "dense"), main, scope=scope)
+    names = sorted(p.name for p in main.all_parameters())
+    dense_vals = {n: np.array(scope.get(n).detach().cpu()).copy() for n in names}
+    h, v = box.engine.table.export(True)
+    h, v = h.cpu(), v.cpu()
+    o = torch.argsort(h)
+    BoxWrapper._instance = None
+    return dense_vals, h[o], v[o]
+
+
+def test_checkpoint_resume_matches_uninterrupted(tmp_path):
+    """Save (BoxPS batch model + persistables + Adam state) after pass 1,
+    restore into a fresh wrapper / scope / executor and train pass 2: the
+    result equals training both passes without interruption."""
+    files = _files(tmp_path, 2, 200)
+    ck = tmp_path / "ck"
+    ref_dense, ref_h, ref_v = _resume_run(tmp_path, files, 1, 1, ckpt=ck)
+    assert (ck / "dense" / "__optimizer_state__.safetensors").exists()
+    res_dense, res_h, res_v = _resume_run(tmp_path, files, 0, 1, restore=ck)
+    for n in ref_dense:
+        np.testing.assert_allclose(res_dense[n], ref_dense[n], rtol=1e-5, atol=1e-6, err_msg=n)
+    assert torch.equal(res_h, ref_h)
+    l = __import__("paddlebox_amd.ps.config", fromlist=["row_layout"]).row_layout(8)
+    keep = [c for c in range(ref_v.shape[1]) if c != l["delta_score"]]  # save_base resets delta_score
+    torch.testing.assert_close(res_v[:, keep], ref_v[:, keep], rtol=1e-5, atol=1e-6)

@@ -153,3 +153,18 @@ def test_transpiled_program_captured_on_gpu(tmp_path):
     tr = _run(tmp_path / "t", graph=True, passes=1, transpile=True)
     assert tr["stats"][-1].get("graph_replays", 0) > 0
     np.testing.assert_allclose(tr["w1"], plain["w1"], rtol=0, atol=5e-3)
+
+
+def test_checkpoint_resume_on_gpu(tmp_path):
+    """Save after pass 1 (BoxPS batch model + persistables + Adam state),
+    restore into a fresh wrapper / scope and train pass 2 with the captured
+    step: equals uninterrupted training up to float atomics."""
+    from tests.test_fluid import _resume_run
+
+    files = _files(tmp_path, 2, 320)
+    ck = tmp_path / "ck"
+    ref_dense, ref_h, _ = _resume_run(tmp_path, files, 1, 1, ckpt=ck, device="cuda:0")
+    res_dense, res_h, _ = _resume_run(tmp_path, files, 0, 1, restore=ck, device="cuda:0")
+    assert torch.equal(res_h, ref_h)
+    for n in ref_dense:
+        np.testing.assert_allclose(res_dense[n], ref_dense[n], rtol=0, atol=5e-3, err_msg=n)
