@@ -1,4 +1,5 @@
 #include "dump.h"
+#include "runtime.h"
 
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -141,6 +142,14 @@ int64_t DumpWriter::dump_fields(const std::vector<std::string>& lineids, const s
                                 const std::vector<const float*>& data, const std::vector<int64_t>& widths,
                                 int64_t B, int dump_mode, int dump_interval, bool lineid_have_extend_info) {
   if (dump_interval <= 0) dump_interval = 1;
+  // FLAGS_padbox_dump_debug_lineid: dump only the line whose id starts with
+  // it (32 chars compared); FLAGS_dump_filed_same_as_aibox: field headers are
+  // the name up to its first '.' without the ":<len>" count;
+  // FLAGS_enable_print_dump_field_debug: log every dumped field
+  // (boxps_worker.cc:1777-1815)
+  const std::string debug_lid = Flags::ins().get_or("padbox_dump_debug_lineid", "");
+  const bool aibox = Flags::ins().get_bool_or("dump_filed_same_as_aibox", false);
+  const bool field_debug = Flags::ins().get_bool_or("enable_print_dump_field_debug", false);
   std::atomic<int64_t> lines{0};
   const int T = (int)fds_.size();
   std::vector<std::future<void>> fs;
@@ -156,15 +165,24 @@ int64_t DumpWriter::dump_fields(const std::vector<std::string>& lineids, const s
         if (dump_mode == 1) r = xxh64(lid.data(), lid.size(), 0);
         else if (dump_mode == 2) r = rng() & 0x7fffffff;
         if (r % (uint64_t)dump_interval != 0) continue;
+        if (!debug_lid.empty() && strncmp(lid.c_str(), debug_lid.c_str(), 32) != 0) continue;
         size_t pos = std::string::npos;
         if (lineid_have_extend_info) pos = lid.find(' ');
         s.append(lid, 0, pos == std::string::npos ? lid.size() : pos);
         for (size_t k = 0; k < names.size(); ++k) {
           const int64_t w = widths[k];
           s.push_back('\t');
-          s.append(names[k]);
-          s.push_back(':');
-          s.append(std::to_string(w));
+          if (aibox) {
+            const size_t dot = names[k].find('.');
+            s.append(names[k], 0, dot == std::string::npos ? names[k].size() : dot);
+          } else {
+            s.append(names[k]);
+            s.push_back(':');
+            s.append(std::to_string(w));
+          }
+          if (field_debug)
+            fprintf(stderr, "[pbx dump] tid=%d lineid:[%s] name=%s len=%lld\n", tid, lid.c_str(), names[k].c_str(),
+                    (long long)w);
           const float* row = data[k] + i * w;
           for (int64_t j = 0; j < w; ++j) {
             s.push_back(':');

@@ -77,11 +77,25 @@ typedef struct pbx_record_view {
                    uint32_t* cmatch, uint32_t* rank);
 } pbx_record_view;
 
+// Optional 6th symbol, whole-file parsing (reference
+// ISlotParser::ParseFileInstance, data_feed.cc:3850-3870), used for every file
+// when FLAGS_enable_ins_parser_file is set:
+//   int64_t pbx_parser_parse_file(void* parser, const char* path,
+//                                 pbx_read_fn read, void* read_ctx,
+//                                 const pbx_ins_sink* sink);
+// The plugin pulls the (decompressed / converted) file bytes with
+// read(read_ctx, buf, len) -> bytes read, 0 at end of file, and emits
+// instances through `sink`.  `path` is the file name when
+// FLAGS_enable_ins_parser_add_file_path is set, else NULL.  Returns the
+// number of instances emitted, < 0 on a parse error.
+typedef int64_t (*pbx_read_fn)(void* read_ctx, char* buf, int64_t len);
+
 typedef void* (*pbx_parser_create_fn)(int, const char* const*, const char*);
 typedef int (*pbx_parser_parse_line_fn)(void*, const char*, size_t, const pbx_ins_sink*);
 typedef void (*pbx_parser_destroy_fn)(void*);
 typedef int (*pbx_parser_parse_index_fn)(void*, const char*, size_t, const pbx_index_sink*);
 typedef int64_t (*pbx_parser_unroll_fn)(void*, const pbx_record_view*, const pbx_ins_sink*);
+typedef int64_t (*pbx_parser_parse_file_fn)(void*, const char*, pbx_read_fn, void*, const pbx_ins_sink*);
 
 #ifdef __cplusplus
 }

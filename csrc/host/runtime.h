@@ -164,6 +164,17 @@ class Flags {
     auto v = get(name);
     return v == "1" || v == "true" || v == "True";
   }
+  // non-throwing reads for code that also runs without the registered
+  // defaults (the standalone host self-test)
+  std::string get_or(const std::string& name, const std::string& def) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = vals_.find(name);
+    return it == vals_.end() ? def : it->second;
+  }
+  bool get_bool_or(const std::string& name, bool def) {
+    const auto v = get_or(name, def ? "true" : "false");
+    return v == "1" || v == "true" || v == "True";
+  }
   int64_t get_int(const std::string& name) { return std::stoll(get(name)); }
   double get_double(const std::string& name) { return std::stod(get(name)); }
   std::map<std::string, std::string> all() {

@@ -178,6 +178,7 @@ struct SlotDataset::Plugin {
   pbx_parser_destroy_fn destroy = nullptr;
   pbx_parser_parse_index_fn parse_index = nullptr;
   pbx_parser_unroll_fn unroll = nullptr;
+  pbx_parser_parse_file_fn parse_file = nullptr;
   ~Plugin() {
     if (parser && destroy) destroy(parser);
     if (so) dlclose(so);
@@ -286,6 +287,7 @@ void SlotDataset::set_so_parser(const std::string& path) {
   pl->destroy = (pbx_parser_destroy_fn)dlsym(pl->so, "pbx_parser_destroy");
   pl->parse_index = (pbx_parser_parse_index_fn)dlsym(pl->so, "pbx_parser_parse_index");  // optional
   pl->unroll = (pbx_parser_unroll_fn)dlsym(pl->so, "pbx_parser_unroll");                // optional
+  pl->parse_file = (pbx_parser_parse_file_fn)dlsym(pl->so, "pbx_parser_parse_file");    // optional
   if (!create || !pl->parse || !pl->destroy)
     throw std::runtime_error("so parser " + path + ": missing pbx_parser_{create,parse_line,destroy}");
   std::vector<const char*> names;
@@ -320,6 +322,33 @@ bool SlotDataset::parse_plugin_line(const char* line, size_t len, RecordStore* s
   const int n = plugin_->parse(plugin_->parser, line, len, &sink);
   ctx.clear();  // an instance the plugin never committed is discarded
   return n > 0 && ctx.kept > 0;
+}
+
+namespace {
+int64_t file_read(void* ctx, char* buf, int64_t len) {
+  return (int64_t)fread(buf, 1, (size_t)len, (FILE*)ctx);
+}
+}  // namespace
+
+int64_t SlotDataset::parse_plugin_file(const std::string& path, FILE* fp, RecordStore* st) const {
+  SinkCtx ctx;
+  ctx.u_idx = &u_idx_;
+  ctx.f_idx = &f_idx_;
+  ctx.slots = &slots_;
+  ctx.keep_ins_id = parse_.parse_ins_id || parse_.parse_logkey;
+  ctx.need_sparse = !sparse_slots_.empty();
+  ctx.st = st;
+  ctx.replica = replica_.get();
+  ctx.index = input_index_.get();
+  ctx.u.resize(store_.nu);
+  ctx.f.resize(store_.nf);
+  ctx.clear();
+  const pbx_ins_sink sink{&ctx,         sink_add_u64,
+                          sink_add_f32, sink_set_meta,
+                          sink_commit,  replica_ ? sink_add_cache : nullptr,
+                          input_index_ ? sink_index_offset : nullptr};
+  const bool with_path = Flags::ins().get_bool_or("enable_ins_parser_add_file_path", false);
+  return plugin_->parse_file(plugin_->parser, with_path ? path.c_str() : nullptr, file_read, fp, &sink);
 }
 
 int64_t SlotDataset::load_index_files(const std::vector<std::string>& files, InputIndex* t) const {
@@ -439,6 +468,8 @@ bool SlotDataset::parse_line(const char* str, size_t len, RecordStore* st) const
 
 int64_t SlotDataset::load_files(const std::vector<std::string>& files, RecordStore* out) {
   const int T = std::max(1, std::min<int>(threads_, (int)files.size()));
+  // FLAGS_enable_ins_parser_file: the plugin parses whole files
+  const bool file_mode = plugin_ && plugin_->parse_file && Flags::ins().get_bool_or("enable_ins_parser_file", false);
   std::vector<RecordStore> parts(T);
   std::atomic<size_t> next{0};
   std::atomic<int64_t> bad{0};
@@ -459,15 +490,19 @@ int64_t SlotDataset::load_files(const std::vector<std::string>& files, RecordSto
           bad += 1;
           continue;
         }
-        char* line = nullptr;
-        size_t cap = 0;
-        ssize_t n;
         const int64_t r0 = parts[t].nrec();
-        while ((n = getline(&line, &cap, fp)) > 0) {
-          if (n <= 1) continue;
-          if (!parse_line(line, (size_t)n, &parts[t])) bad += 1;
+        if (file_mode) {
+          if (parse_plugin_file(f, fp, &parts[t]) < 0) bad += 1;
+        } else {
+          char* line = nullptr;
+          size_t cap = 0;
+          ssize_t n;
+          while ((n = getline(&line, &cap, fp)) > 0) {
+            if (n <= 1) continue;
+            if (!parse_line(line, (size_t)n, &parts[t])) bad += 1;
+          }
+          free(line);
         }
-        free(line);
         if (stg) register_keys(parts[t], r0, parts[t].nrec(), stg.get());
         FileMgr::close(fp, is_pipe);
       }

@@ -14,6 +14,7 @@
 // pinned staging buffers that go to HBM in a single H2D copy per tensor.
 #pragma once
 #include <cstdint>
+#include <cstdio>
 #include <functional>
 #include <memory>
 #include <string>
@@ -193,6 +194,7 @@ class SlotDataset {
  private:
   struct Plugin;
   bool parse_plugin_line(const char* line, size_t len, RecordStore* st) const;
+  int64_t parse_plugin_file(const std::string& path, FILE* fp, RecordStore* st) const;
   std::shared_ptr<Plugin> plugin_;
   int64_t load_files(const std::vector<std::string>& files, RecordStore* out);
   std::vector<SlotDesc> slots_;

@@ -14,6 +14,12 @@ design (documented, not silently ignored):
   the pass lives in a columnar CSR store (``csrc/host/slot_dataset.h``).
 * ``padbox_enable_gc`` -- intermediate tensors are freed by reference
   counting / the HIP graph's memory pool.
+* ``enable_pull_box_padding_zero`` -- an empty slot always pools to zeros
+  (the fused pull writes every output row), the flag's ``true`` behaviour.
+* ``padbox_auc_runner_mode`` -- AucRunner mode is entered by
+  ``BoxWrapper.initialize_auc_runner`` (``auc_runner_mode()`` reports it).
+* ``padbox_enable_sharding_stage`` -- optimizer-state sharding is chosen by
+  the fleet strategy / ``ShardedFlatAdam``.
 * ``padbox_dataset_merge_thread_num`` -- feed-pass keys are registered by
   the loader threads themselves (KeyAgent); their count comes from
   ``set_thread``.  (``padbox_dataset_shuffle_thread_num`` is live: the

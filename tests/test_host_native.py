@@ -281,3 +281,35 @@ def test_pcoc_q_values_follow_records(tmp_path):
     ds2._native.load_archive(str(tmp_path / "arch"), False)
     b3 = ds2.build_batch(0, n)
     torch.testing.assert_close(b3.extra["q_values"][:, 0], (b3.keys.float() - 1000.0) / 10.0)
+
+
+def test_dump_debug_flags(tmp_path):
+    """FLAGS_padbox_dump_debug_lineid (only the matching line is dumped) and
+    FLAGS_dump_filed_same_as_aibox (field header = name before '.', no ':len'),
+    boxps_worker.cc:1777-1815."""
+    from paddlebox_amd.utils.flags import set_flags
+
+    ids = [f"{i:032d}" for i in range(4)]
+    mat = torch.arange(8, dtype=torch.float32).view(4, 2)
+
+    def run(sub, flags):
+        set_flags(flags)
+        try:
+            w = h.DumpWriter(str(tmp_path / sub), 0, 1)
+            w.dump_fields(ids, ["fc.tmp_0"], [mat], 0, 1, False)
+            w.flush()
+        finally:
+            set_flags({"FLAGS_padbox_dump_debug_lineid": "", "FLAGS_dump_filed_same_as_aibox": False})
+        out = []
+        for f in sorted((tmp_path / sub).rglob("*")):
+            if f.is_file():
+                out += [ln for ln in f.read_text().splitlines() if ln]
+        return out
+
+    plain = run("a", {})
+    v = lambda x: f"{x:.9f}"  # noqa: E731  (the writer's float format)
+    assert len(plain) == 4 and plain[1] == f"{ids[1]}\tfc.tmp_0:2:{v(2)}:{v(3)}"
+    one = run("b", {"FLAGS_padbox_dump_debug_lineid": ids[2]})
+    assert one == [f"{ids[2]}\tfc.tmp_0:2:{v(4)}:{v(5)}"]
+    ai = run("c", {"FLAGS_dump_filed_same_as_aibox": True})
+    assert ai[0] == f"{ids[0]}\tfc:0:{v(1)}"

@@ -236,3 +236,80 @@ def test_unroll_instance_hook(tmp_path):
     assert keys.tolist() == [11, 12, 13, 21, 31, 32]
     assert lod.tolist() == [0, 1, 2, 3, 4, 5, 6]
     assert dense[:, 0].tolist() == [1, 1, 1, 0, 1, 1]
+
+
+FILE_PLUGIN = r"""
+// whole-file parser (ParseFileInstance): reads the stream through the host's
+// read callback; lines "label k1 k2 ..."; the ins id is "<path>:<line no>"
+// when the host passes the path
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <string>
+#include "parser_plugin.h"
+extern "C" {
+void* pbx_parser_create(int, const char* const*, const char*) { return (void*)1; }
+void pbx_parser_destroy(void*) {}
+int pbx_parser_parse_line(void*, const char*, size_t, const pbx_ins_sink*) { return -1; }
+int64_t pbx_parser_parse_file(void*, const char* path, pbx_read_fn rd, void* rctx, const pbx_ins_sink* s) {
+  std::string all;
+  char buf[4096];
+  int64_t n;
+  while ((n = rd(rctx, buf, sizeof(buf))) > 0) all.append(buf, (size_t)n);
+  int64_t out = 0, lineno = 0;
+  size_t b = 0;
+  while (b < all.size()) {
+    size_t e = all.find('\n', b);
+    if (e == std::string::npos) e = all.size();
+    std::string ln = all.substr(b, e - b);
+    b = e + 1;
+    if (ln.empty()) continue;
+    char* p = &ln[0];
+    uint64_t lab = strtoull(p, &p, 10);
+    s->add_u64(s->ctx, 0, &lab, 1);
+    for (;;) {
+      char* q;
+      uint64_t k = strtoull(p, &q, 10);
+      if (q == p) break;
+      p = q;
+      s->add_u64(s->ctx, 1, &k, 1);
+    }
+    std::string id = (path ? std::string(path) : std::string("-")) + ":" + std::to_string(lineno++);
+    s->set_meta(s->ctx, id.data(), (int)id.size(), 0, 0, 0);
+    out += s->commit(s->ctx);
+  }
+  return out;
+}
+}
+"""
+
+
+def test_whole_file_parser_mode(tmp_path):
+    """FLAGS_enable_ins_parser_file (+ _add_file_path): the plugin's
+    pbx_parser_parse_file reads whole files (reference ParseFileInstance,
+    data_feed.cc:3850-3870)."""
+    from paddlebox_amd.utils.flags import set_flags
+
+    src = tmp_path / "fileparse.cc"
+    src.write_text(FILE_PLUGIN)
+    so = str(tmp_path / "fileparse.so")
+    subprocess.run(["g++", "-O2", "-shared", "-fPIC", "-I" + os.path.join(ROOT, "csrc", "host"), str(src), "-o", so],
+                   check=True)
+    f0 = tmp_path / "part-0"
+    f0.write_text("1 11 12\n0 21\n")
+    h = _native.host()
+    set_flags({"FLAGS_enable_ins_parser_file": True, "FLAGS_enable_ins_parser_add_file_path": True})
+    try:
+        d = h.SlotDataset()
+        d.set_slots([h.SlotDesc("label", "uint64", True, True, 1), h.SlotDesc("s", "uint64", True, False, 1)])
+        pc = h.ParseConfig()
+        pc.parse_ins_id = True
+        d.set_parse(pc)
+        d.set_so_parser(so)
+        d.set_filelist([str(f0)])
+        assert d.load_into_memory() == 2
+        assert d.ins_ids() == [f"{f0}:0", f"{f0}:1"]
+        keys, lod, dense = d.build_batch(0, 2, False)
+        assert keys.tolist() == [11, 12, 21]
+    finally:
+        set_flags({"FLAGS_enable_ins_parser_file": False, "FLAGS_enable_ins_parser_add_file_path": False})
