@@ -5,6 +5,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -147,6 +148,7 @@ int64_t DumpWriter::dump_fields(const std::vector<std::string>& lineids, const s
   // the name up to its first '.' without the ":<len>" count;
   // FLAGS_enable_print_dump_field_debug: log every dumped field
   // (boxps_worker.cc:1777-1815)
+  const auto t_start = std::chrono::steady_clock::now();
   const std::string debug_lid = Flags::ins().get_or("padbox_dump_debug_lineid", "");
   const bool aibox = Flags::ins().get_bool_or("dump_filed_same_as_aibox", false);
   const bool field_debug = Flags::ins().get_bool_or("enable_print_dump_field_debug", false);
@@ -204,6 +206,9 @@ int64_t DumpWriter::dump_fields(const std::vector<std::string>& lineids, const s
     }));
   }
   for (auto& f : fs) f.get();
+  if (Flags::ins().get_bool_or("enable_print_dump_info_debug", false))  // boxps_worker.cc:1849-1853
+    fprintf(stderr, "[pbx dump] ins count=%lld field=%zu span=%.3f ms\n", (long long)lines.load(), names.size(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
   return lines.load();
 }
 
