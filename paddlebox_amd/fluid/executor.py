@@ -412,6 +412,8 @@ class Session:
         staged = {n: self.scope.get(n) for n in names if n in self.scope}
         if staged:
             self.load_optimizer_state(staged)
+            for n in staged:  # consumed: a later session must not re-apply a stale checkpoint
+                self.scope._tensors.pop(n, None)
 
     # ------------------------------------------------ transpiled dense sync
     def _logical_of(self, name: str, t: torch.Tensor) -> torch.Tensor:
