@@ -46,12 +46,15 @@ class TowerWorkspace {
       : M_(M), dims_(dims), splits_(dw_splits) {
     TW_CHECK(dims.size() >= 2 && dims.size() - 1 <= (size_t)kMaxTowerLayers, "1..8 hidden layers");
     TW_CHECK(M > 0, "M > 0");
-    TW_CHECK(dw_splits == 1 || dw_splits == 2, "dw_splits in {1, 2}");
+    TW_CHECK(dw_splits == 1 || dw_splits == 2 || dw_splits == 4, "dw_splits in {1, 2, 4}");
     for (auto d : dims) TW_CHECK(d > 0 && d <= 2048, "widths in 1..2048");
     auto ob = torch::TensorOptions().dtype(torch::kBFloat16).device(torch::kCUDA, device);
     auto of = torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device);
     auto oi = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device);
     Mp_ = tower_nwg((int)M) * 32;
+    // each split walks a whole number of 4-step (64-row) ring stages; a small
+    // batch that cannot be cut in 4 falls back to 2 (always valid: Mp % 128 == 0)
+    if ((Mp_ / 16) % (4 * splits_) != 0) splits_ = 2;
     L_ = (int)dims.size() - 1;
     int64_t maxw = 0;
     for (auto d : dims) maxw = std::max(maxw, pad(d, 32));

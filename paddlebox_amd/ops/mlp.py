@@ -10,9 +10,8 @@ CPU tensors use plain fp32 PyTorch (the reference path).
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
-
 import os
+from typing import List, Optional, Sequence
 
 import torch
 from torch import nn
@@ -150,7 +149,9 @@ class FusedMLP(nn.Module):
     def tower_workspace(self, M: int, device: torch.device):
         if self._tw is None or self._tw.M != M:
             dims = [self.in_dim] + list(self.hidden)
-            self._tw = _native.hip().TowerWorkspace(M, dims, device.index or 0, 2)
+            # dW split over M (fp32 atomics between splits); PBX_TOWER_DW_SPLITS in {1, 2, 4}
+            splits = int(os.environ.get("PBX_TOWER_DW_SPLITS", "2"))
+            self._tw = _native.hip().TowerWorkspace(M, dims, device.index or 0, splits)
             self._packed = False
         return self._tw
 
