@@ -29,16 +29,10 @@ import time
 import torch
 import torch.distributed as dist
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-from paddlebox_amd.data.synthetic import CriteoSynth  # noqa: E402
-from paddlebox_amd.models.dcn_v2 import DCNv2  # noqa: E402
-from paddlebox_amd.models.deepfm import DeepFM  # noqa: E402
-from paddlebox_amd.ops import reference as ref  # noqa: E402
-from paddlebox_amd.ops.ctr import auc_accumulate  # noqa: E402
-from paddlebox_amd.parallel.dense import DenseArena, DenseSync, FlatAdam  # noqa: E402
-from paddlebox_amd.ps.config import PSConfig  # noqa: E402
-from paddlebox_amd.ps.sparse_engine import SparseEngine  # noqa: E402
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+# the package (and its HIP extension) is imported inside main(), after the
+# launcher decision: a parent that spawns one rank per GPU never loads it
 
 METRIC = "samples/sec (whole node) on Criteo-1TB-shape DeepFM"
 METRIC_DCN = "samples/sec (whole node) on Criteo-1TB-shape DCN-V2 (BASELINE config 5)"
@@ -47,6 +41,66 @@ METRIC_DCN = "samples/sec (whole node) on Criteo-1TB-shape DCN-V2 (BASELINE conf
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _visible_gpus() -> int:
+    # device_count() does not initialise the HIP runtime on this image
+    return torch.cuda.device_count()
+
+
+def launch_ranks(argv, n: int, dry: bool) -> int:
+    """``bench.py --gpus N`` started without a launcher: run one rank per GPU
+    (torch.distributed.run over 127.0.0.1) as CHILD processes of this parent,
+    which never touches the GPU itself, relay their output (rank 0 prints the
+    JSON line) and exit with the worst child return code.  Reference: one
+    worker per device, boxps_trainer.cc:53-79."""
+    import subprocess
+
+    if not dry:
+        have = _visible_gpus()
+        if n > have:
+            print(f"[bench] --gpus {n} but only {have} GPU(s) visible: refusing to measure fewer GPUs than asked",
+                  file=sys.stderr, flush=True)
+            return 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py")] + list(argv)
+    env = dict(os.environ)
+    env["PBX_BENCH_LAUNCHER"] = "bench.py-spawn"
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"[bench] launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return p.wait()
+
+
+def dry_run(args, world, rank):
+    """CPU rehearsal of the launcher contract (gloo): every rank joins the
+    group, the rank count is all-reduced and rank 0 prints the JSON line with
+    ``config.ranks_seen``.  No GPU, no model: tests the plumbing only."""
+    one = torch.ones(1)
+    if "WORLD_SIZE" in os.environ:
+        dist.init_process_group("gloo", init_method="env://")
+        dist.all_reduce(one)
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "samples/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                          "config": {"ranks_seen": int(one.item()),
+                                     "launcher": os.environ.get("PBX_BENCH_LAUNCHER", "external")}}), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
 
 def main():
@@ -87,18 +141,42 @@ def main():
                          "instead of RCCL")
     ap.add_argument("--force-collectives", action="store_true",
                     help="run the multi-GPU exchange/all-reduce path even on 1 rank (rehearsal)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo rehearsal of the multi-rank launch (no GPU, no model); prints ranks_seen")
     args = ap.parse_args()
     if args.force_collectives:
         os.environ["PBX_FORCE_COLLECTIVES"] = "1"
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher around us: start one rank per GPU ourselves
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus, args.dry_run))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    if world != args.gpus and rank == 0:
+        log(rank, f"[bench] note: --gpus {args.gpus} but the launcher started {world} ranks; measuring {world}")
+    launcher = os.environ.get("PBX_BENCH_LAUNCHER", "torchrun" if "WORLD_SIZE" in os.environ else "single")
+
+    from paddlebox_amd.data.synthetic import CriteoSynth
+    from paddlebox_amd.models.dcn_v2 import DCNv2
+    from paddlebox_amd.models.deepfm import DeepFM
+    from paddlebox_amd.ops import reference as ref
+    from paddlebox_amd.ops.ctr import auc_accumulate
+    from paddlebox_amd.parallel.dense import DenseArena, DenseSync, FlatAdam
+    from paddlebox_amd.ps.config import PSConfig
+    from paddlebox_amd.ps.sparse_engine import SparseEngine
+
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     multi = world > 1 or args.force_collectives
+    ranks_seen = 1
     if multi:
         dist.init_process_group("nccl", device_id=device)
+        seen = torch.ones(1, device=device)
+        dist.all_reduce(seen)
+        ranks_seen = int(seen.item())
 
     B = args.batch_per_gpu
     total = int(args.total_features)
@@ -331,6 +409,8 @@ def main():
                 "seq_len": S,
                 "total_features": synth.total_features,
                 "parallelism": f"dp{world}+sparse-shard{world}",
+                "ranks_seen": ranks_seen,
+                "launcher": launcher,
                 "dense_allreduce": "ipc-oneshot" if ipc is not None else "rccl",
                 "pipelined_pull": bool(graphed is not None and graphed.prefetch is not None),
                 "mlp_dtype": args.mlp_dtype,
