@@ -231,13 +231,15 @@ def main():
     else:
         model = DeepFM(engine, num_slots=S, dense_dim=13, hidden=hidden).to(device)
     if fp32:
-        model.precision = "fp32"
+        model.set_precision("fp32")
+    # the fused tower runs the whole dense side (bf16 operands, or exact fp32)
+    fused = getattr(model, "use_tower", False) and (not fp32 or model.tower.fp32)
     C = model.dn.C
     arena = DenseArena(model.parameters(), device, extra_grad=3 * C if multi and not dcn else 0)
     if multi:
         model.dn.group = dist.group.WORLD
         model.dn.sync_stats = True
-        if not fp32 and not dcn:
+        if fused and not dcn:
             # data_norm batch statistics are summed across ranks in the SAME
             # all-reduce as the dense gradients (tail of the gradient buffer)
             model.dn.stats = arena.grad_tail(3 * C)
@@ -245,7 +247,7 @@ def main():
     # one update launch for the dense side: Adam + bf16 tower weight re-pack +
     # data_norm summary update; grads zeroed by the same kernel
     opt = FlatAdam(arena, lr=1e-3, clear_grad=True)
-    if not fp32 and getattr(model, "use_tower", False):
+    if fused:
         opt.fuse(mlps=[model.mlp], data_norms=[model.dn])
     # the dense all-reduce runs on its own communicator and side stream, started
     # as soon as the tower's gradients are final: it overlaps the sparse push
@@ -269,7 +271,7 @@ def main():
     copy_stream = torch.cuda.Stream(device)
     auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
     auc_stats = torch.zeros(5, dtype=torch.float64, device=device)
-    fused_auc = getattr(model, "use_tower", False) and not fp32
+    fused_auc = fused
     if fused_auc:  # streaming AUC accumulated by the tower's loss epilogue
         model.tower.auc = (auc_table, auc_stats, None)
 

@@ -624,10 +624,13 @@ static std::vector<Tensor> head_fwd(const Tensor& x, int S, int Eo, int ew_col, 
   a.x = ptr<float>(x);
   a.B = B; a.C = C; a.Cp = Cp; a.S = S; a.Eo = Eo; a.ew_col = ew_col; a.D = D;
   Tensor y;
+  bool yf32 = false;
   if (y_out.has_value() && y_out->defined()) {
     y = *y_out;
     check_cuda(y, "y_out");
-    PBX_CHECK(y.scalar_type() == torch::kBFloat16 && y.size(0) == B && y.size(1) >= Cp, "head: y_out shape");
+    yf32 = y.scalar_type() == torch::kFloat32;
+    PBX_CHECK((yf32 || y.scalar_type() == torch::kBFloat16) && y.size(0) == B && y.size(1) >= Cp,
+              "head: y_out must be bf16 or fp32 [B, >= Cp]");
     a.ldy = (int)y.size(1);
   } else {
     y = torch::empty({B, Cp}, x.options().dtype(torch::kBFloat16));
@@ -640,9 +643,17 @@ static std::vector<Tensor> head_fwd(const Tensor& x, int S, int Eo, int ew_col, 
   }
   if (ymp_out.has_value() && ymp_out->defined()) {
     check_cuda(*ymp_out, "ymp_out");
-    PBX_CHECK(Cp % 32 == 0 && ymp_out->numel() >= (int64_t)(B + 15) / 16 * 16 * Cp, "head: ymp_out size / Cp % 32");
-    a.ymp = reinterpret_cast<unsigned short*>(ymp_out->data_ptr());
+    if (ymp_out->scalar_type() == torch::kFloat32) {
+      PBX_CHECK(yf32 && Cp % 16 == 0 && ymp_out->numel() >= (int64_t)(B + 15) / 16 * 16 * Cp,
+                "head: fp32 ymp_out needs an fp32 y_out, Cp % 16 == 0 and pad16(B) * Cp floats");
+      a.ympf = ptr<float>(*ymp_out);
+    } else {
+      PBX_CHECK(!yf32 && Cp % 32 == 0 && ymp_out->numel() >= (int64_t)(B + 15) / 16 * 16 * Cp,
+                "head: ymp_out size / Cp % 32");
+      a.ymp = reinterpret_cast<unsigned short*>(ymp_out->data_ptr());
+    }
   }
+  PBX_CHECK(!(yf32 && yT_out.has_value() && yT_out->defined()), "head: yT_out is a bf16-path output");
   if (stat_part.has_value() && stat_part->defined()) {
     check_cuda(*stat_part, "stat_part");
     PBX_CHECK(stat_part->numel() >= (int64_t)head_blocks(B) * 2 * C, "head: stat_part size");
@@ -656,7 +667,8 @@ static std::vector<Tensor> head_fwd(const Tensor& x, int S, int Eo, int ew_col, 
     a.bsize = ptr<float>(*bsize); a.bsum = ptr<float>(*bsum); a.bsq = ptr<float>(*bsq);
     a.means = ptr<float>(means); a.scales = ptr<float>(scales);
   }
-  a.y = reinterpret_cast<unsigned short*>(y.data_ptr());
+  if (yf32) a.yf = ptr<float>(y);
+  else a.y = reinterpret_cast<unsigned short*>(y.data_ptr());
   a.lin = ptr<float>(lin);
   launch_head_fwd(a, cur_stream());
   return {y, lin, means, scales};
@@ -675,8 +687,10 @@ static std::vector<Tensor> head_bwd(const Tensor& x, const c10::optional<Tensor>
   auto dx = torch::empty_like(x);
   Tensor stats, acc;
   if (dy.has_value()) {
-    PBX_CHECK(dy->scalar_type() == torch::kBFloat16 && dy->size(1) >= Cp && dy->is_contiguous(), "head: dy");
-    a.dy = reinterpret_cast<const unsigned short*>(dy->data_ptr());
+    PBX_CHECK((dy->scalar_type() == torch::kBFloat16 || dy->scalar_type() == torch::kFloat32) &&
+                  dy->size(1) >= Cp && dy->is_contiguous(), "head: dy");
+    if (dy->scalar_type() == torch::kFloat32) a.dyf = ptr<float>(*dy);
+    else a.dy = reinterpret_cast<const unsigned short*>(dy->data_ptr());
     a.ldy = (int)dy->size(1);
   }
   Tensor dl;

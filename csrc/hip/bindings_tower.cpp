@@ -42,31 +42,42 @@ void check_f32(const Tensor& t, int64_t numel, const char* what) {
 
 class TowerWorkspace {
  public:
-  TowerWorkspace(int64_t M, std::vector<int64_t> dims, int device, int64_t dw_splits)
-      : M_(M), dims_(dims), splits_(dw_splits) {
+  // fp32 = true: the exact-fp32 tower (tower32.hip, reference fc precision):
+  // fp32 activations / weights, widths padded to 16, Mp to 256
+  TowerWorkspace(int64_t M, std::vector<int64_t> dims, int device, int64_t dw_splits, bool fp32)
+      : M_(M), dims_(dims), splits_(dw_splits), fp32_(fp32) {
     TW_CHECK(dims.size() >= 2 && dims.size() - 1 <= (size_t)kMaxTowerLayers, "1..8 hidden layers");
     TW_CHECK(M > 0, "M > 0");
-    TW_CHECK(dw_splits == 1 || dw_splits == 2 || dw_splits == 4, "dw_splits in {1, 2, 4}");
-    for (auto d : dims) TW_CHECK(d > 0 && d <= 2048, "widths in 1..2048");
-    auto ob = torch::TensorOptions().dtype(torch::kBFloat16).device(torch::kCUDA, device);
+    if (fp32) TW_CHECK(dw_splits == 1 || dw_splits == 2 || dw_splits == 4 || dw_splits == 8, "dw_splits in {1,2,4,8}");
+    else TW_CHECK(dw_splits == 1 || dw_splits == 2 || dw_splits == 4, "dw_splits in {1, 2, 4}");
+    const int64_t wmax = fp32 ? kTower32MaxWidth : 2048;
+    for (auto d : dims) TW_CHECK(d > 0 && d <= wmax, "layer widths exceed the fused tower's limit");
+    auto ob = torch::TensorOptions().dtype(fp32 ? torch::kFloat32 : torch::kBFloat16).device(torch::kCUDA, device);
     auto of = torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device);
     auto oi = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device);
-    Mp_ = tower_nwg((int)M) * 32;
-    // each split walks a whole number of 4-step (64-row) ring stages; a small
-    // batch that cannot be cut in 4 falls back to 2 (always valid: Mp % 128 == 0)
-    if ((Mp_ / 16) % (4 * splits_) != 0) splits_ = 2;
+    wpad_ = fp32 ? 16 : 32;
     L_ = (int)dims.size() - 1;
     int64_t maxw = 0;
-    for (auto d : dims) maxw = std::max(maxw, pad(d, 32));
-    lds_ld_ = (int)maxw + 8;
-    TW_CHECK((size_t)2 * 32 * lds_ld_ * 2 <= 150 * 1024, "widths exceed the LDS tile budget");
-    const int64_t K0p = pad(dims[0], 32);
+    for (auto d : dims) maxw = std::max(maxw, pad(d, wpad_));
+    if (fp32) {
+      Mp_ = pad(M, 256);  // the dW splits walk whole 2-step (32-row) ring stages
+      lds_ld_ = tower32_lds_ld((int)maxw);
+      TW_CHECK((size_t)2 * 32 * lds_ld_ * 4 <= 140 * 1024, "widths exceed the fp32 LDS tile budget");
+    } else {
+      Mp_ = tower_nwg((int)M) * 32;
+      // each split walks a whole number of 4-step (64-row) ring stages; a small
+      // batch that cannot be cut in 4 falls back to 2 (always valid: Mp % 128 == 0)
+      if ((Mp_ / 16) % (4 * splits_) != 0) splits_ = 2;
+      lds_ld_ = (int)maxw + 8;
+      TW_CHECK((size_t)2 * 32 * lds_ld_ * 2 <= 150 * 1024, "widths exceed the LDS tile budget");
+    }
+    const int64_t K0p = pad(dims[0], wpad_);
     x0_ = torch::zeros({M, K0p}, ob);
     x0mp_ = torch::zeros({Mp_ * K0p}, ob);
     dx0_ = torch::zeros({M, K0p}, ob);
     int64_t boff = 0;
     for (int l = 0; l < L_; ++l) {
-      const int64_t Kp = pad(dims[l], 32), Np = pad(dims[l + 1], 32);
+      const int64_t Kp = pad(dims[l], wpad_), Np = pad(dims[l + 1], wpad_);
       wp_.push_back(torch::zeros({Np * Kp}, ob));
       wtp_.push_back(torch::zeros({Np * Kp}, ob));
       xmp_.push_back(torch::zeros({Mp_ * Np}, ob));
@@ -75,7 +86,7 @@ class TowerWorkspace {
       boff += Np;
     }
     dwout_off_ = (int)boff;
-    dbout_off_ = (int)(boff + pad(dims[L_], 32));
+    dbout_off_ = (int)(boff + pad(dims[L_], wpad_));
     bias_ld_ = dbout_off_ + 1;
     const int nwg = (int)(Mp_ / 32);
     bias_part_ = torch::zeros({nwg, bias_ld_}, of);
@@ -95,7 +106,8 @@ class TowerWorkspace {
       check_f32(W[l], dims_[l + 1] * dims_[l], "W");
       w[l] = P<float>(W[l]);
     }
-    launch_tower_pack(a, w, stream());
+    if (fp32_) launch_tower32_pack(a, w, stream());
+    else launch_tower_pack(a, w, stream());
   }
 
   std::vector<Tensor> forward(const std::vector<Tensor>& b, const Tensor& w_out, const Tensor& b_out,
@@ -125,7 +137,8 @@ class TowerWorkspace {
       a.auc_buckets = (int)(auc_table->numel() / 2);
       a.auc_mask = OP<float>(auc_mask);
     }
-    launch_tower_fwd(a, stream());
+    if (fp32_) launch_tower32_fwd(a, stream());
+    else launch_tower_fwd(a, stream());
     return {loss_, pred_, dz_};
   }
 
@@ -151,7 +164,8 @@ class TowerWorkspace {
     a.db_out = P<float>(db_out);
     a.dloss = OP<float>(dloss);
     a.need_dx0 = need_dx ? 1 : 0;
-    a.dx0 = BP(dx0_);
+    if (fp32_) a.dx0f = P<float>(dx0_);
+    else a.dx0 = BP(dx0_);
     a.lddx0 = (int)dx0_.size(1);
     if (dn_part.has_value() && dn_part->defined()) {
       TW_CHECK(dn_stats.has_value() && dn_stats->defined(), "dn_stats required with dn_part");
@@ -167,8 +181,13 @@ class TowerWorkspace {
     // reductions (k_tower_dw); the caller may issue them on different streams
     // (dW overlapped with the head backward + sparse push), bwd first
     auto s = stream();
-    if (parts & 1) launch_tower_bwd(a, s);
-    if (parts & 2) launch_tower_dw(a, s);
+    if (fp32_) {
+      if (parts & 1) launch_tower32_bwd(a, s);
+      if (parts & 2) launch_tower32_dw(a, s);
+    } else {
+      if (parts & 1) launch_tower_bwd(a, s);
+      if (parts & 2) launch_tower_dw(a, s);
+    }
     return need_dx ? dx0_ : Tensor();
   }
 
@@ -176,7 +195,7 @@ class TowerWorkspace {
   std::vector<py::tuple> pack_regions() const {
     std::vector<py::tuple> r;
     for (int l = 0; l < L_; ++l)
-      r.push_back(py::make_tuple(wp_[l], wtp_[l], dims_[l + 1], dims_[l], pad(dims_[l + 1], 32), pad(dims_[l], 32)));
+      r.push_back(py::make_tuple(wp_[l], wtp_[l], dims_[l + 1], dims_[l], pad(dims_[l + 1], wpad_), pad(dims_[l], wpad_)));
     return r;
   }
 
@@ -189,6 +208,10 @@ class TowerWorkspace {
   Tensor wtp(int l) const { return wtp_.at(l); }
   int64_t M() const { return M_; }
   int64_t Mp() const { return Mp_; }
+  int64_t K0p() const { return pad(dims_[0], wpad_); }
+  bool fp32() const { return fp32_; }
+  int64_t dw_splits() const { return splits_; }
+  int64_t lds_ld() const { return lds_ld_; }
 
  private:
   TowerArgs base() const {
@@ -197,19 +220,32 @@ class TowerWorkspace {
     a.Mp = (int)Mp_;
     a.L = L_;
     a.lds_ld = lds_ld_;
-    a.x0 = BP(x0_);
     a.ld0 = (int)x0_.size(1);
-    a.x0mp = BP(x0mp_);
+    a.f32 = fp32_ ? 1 : 0;
+    if (fp32_) {
+      a.x0f = P<float>(x0_);
+      a.x0mpf = P<float>(x0mp_);
+    } else {
+      a.x0 = BP(x0_);
+      a.x0mp = BP(x0mp_);
+    }
     for (int l = 0; l < L_; ++l) {
       TowerLayerDev& d = a.ly[l];
-      d.wp = BP(wp_[l]);
-      d.wtp = BP(wtp_[l]);
+      if (fp32_) {
+        d.wpf = P<float>(wp_[l]);
+        d.wtpf = P<float>(wtp_[l]);
+        d.xmpf = P<float>(xmp_[l]);
+        d.dzmpf = P<float>(dzmp_[l]);
+      } else {
+        d.wp = BP(wp_[l]);
+        d.wtp = BP(wtp_[l]);
+        d.xmp = BP(xmp_[l]);
+        d.dzmp = BP(dzmp_[l]);
+      }
       d.K = (int)dims_[l];
       d.N = (int)dims_[l + 1];
-      d.Kp = (int)pad(dims_[l], 32);
-      d.Np = (int)pad(dims_[l + 1], 32);
-      d.xmp = BP(xmp_[l]);
-      d.dzmp = BP(dzmp_[l]);
+      d.Kp = (int)pad(dims_[l], wpad_);
+      d.Np = (int)pad(dims_[l + 1], wpad_);
       d.bias_off = (int)boff_[l];
     }
     a.pred = P<float>(pred_);
@@ -233,6 +269,8 @@ class TowerWorkspace {
   int64_t M_, Mp_ = 0;
   std::vector<int64_t> dims_;
   int64_t splits_;
+  bool fp32_ = false;
+  int64_t wpad_ = 32;
   int L_ = 0, lds_ld_ = 0, bias_ld_ = 0, dwout_off_ = 0, dbout_off_ = 0;
   std::vector<int64_t> boff_;
   Tensor x0_, x0mp_, dx0_, bias_part_, pred_, dz_, loss_, part_, ticket_;
@@ -254,8 +292,16 @@ static void adam_fused(Tensor p, Tensor g, Tensor m, Tensor v, Tensor pows, Tens
   for (size_t i = 0; i < pack.size(); ++i) {
     const auto& t = pack[i];
     x.pack_off[i] = t[0].cast<int64_t>();
-    x.pack_wp[i] = BP(t[1].cast<Tensor>());
-    x.pack_wtp[i] = BP(t[2].cast<Tensor>());
+    auto wpt = t[1].cast<Tensor>(), wtpt = t[2].cast<Tensor>();
+    if (wpt.scalar_type() == torch::kFloat32) {  // fp32 tower region
+      x.pack_wp[i] = x.pack_wtp[i] = nullptr;
+      x.pack_wp32[i] = P<float>(wpt);
+      x.pack_wtp32[i] = P<float>(wtpt);
+    } else {
+      x.pack_wp[i] = BP(wpt);
+      x.pack_wtp[i] = BP(wtpt);
+      x.pack_wp32[i] = x.pack_wtp32[i] = nullptr;
+    }
     x.pack_N[i] = t[3].cast<int>();
     x.pack_K[i] = t[4].cast<int>();
     x.pack_Np[i] = t[5].cast<int>();
@@ -298,8 +344,8 @@ static void memcpy_h2d(Tensor dst, const Tensor& src) {
 void bind_tower(py::module& m) {
   m.def("memcpy_h2d", &memcpy_h2d, py::arg("dst"), py::arg("src"));
   py::class_<TowerWorkspace>(m, "TowerWorkspace")
-      .def(py::init<int64_t, std::vector<int64_t>, int, int64_t>(), py::arg("M"), py::arg("dims"),
-           py::arg("device"), py::arg("dw_splits") = 2)
+      .def(py::init<int64_t, std::vector<int64_t>, int, int64_t, bool>(), py::arg("M"), py::arg("dims"),
+           py::arg("device"), py::arg("dw_splits") = 2, py::arg("fp32") = false)
       .def("pack", &TowerWorkspace::pack)
       .def("forward", &TowerWorkspace::forward, py::arg("b"), py::arg("w_out"), py::arg("b_out"), py::arg("lin"),
            py::arg("label"), py::arg("auc_table") = py::none(), py::arg("auc_stats") = py::none(),
@@ -317,7 +363,11 @@ void bind_tower(py::module& m) {
       .def("wp", &TowerWorkspace::wp)
       .def("wtp", &TowerWorkspace::wtp)
       .def_property_readonly("M", &TowerWorkspace::M)
-      .def_property_readonly("Mp", &TowerWorkspace::Mp);
+      .def_property_readonly("Mp", &TowerWorkspace::Mp)
+      .def_property_readonly("K0p", &TowerWorkspace::K0p)
+      .def_property_readonly("fp32", &TowerWorkspace::fp32)
+      .def_property_readonly("dw_splits", &TowerWorkspace::dw_splits)
+      .def_property_readonly("lds_ld", &TowerWorkspace::lds_ld);
   m.def("adam_fused", &adam_fused, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pows"),
         py::arg("ticket"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("grad_scale"),
         py::arg("wd"), py::arg("clear_grad"), py::arg("pack"), py::arg("dn"));

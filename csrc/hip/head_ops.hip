@@ -74,6 +74,10 @@ __global__ __launch_bounds__(512) void k_head_fwd(HeadArgs a) {
       xs[r * C + c] = v;
       yv = (v - cm[c]) * cs[c];
     }
+    if (a.yf) {  // fp32 MLP input (fp32 tower)
+      a.yf[(int64_t)(row0 + r) * ldy + c] = yv;
+      continue;
+    }
     const unsigned short yb = f2bf(yv);
     a.y[(int64_t)(row0 + r) * ldy + c] = yb;
     if (a.yT || a.ymp) ys[r * Cp + c] = yb;
@@ -99,6 +103,21 @@ __global__ __launch_bounds__(512) void k_head_fwd(HeadArgs a) {
         p[j] = (unsigned)ys[(8 * (l >> 5) + 2 * j) * Cp + 32 * nb + (l & 31)] |
                ((unsigned)ys[(8 * (l >> 5) + 2 * j + 1) * Cp + 32 * nb + (l & 31)] << 16);
       *reinterpret_cast<uint4*>(a.ymp + ((mb * NB + nb) * 64 + l) * 8) = make_uint4(p[0], p[1], p[2], p[3]);
+    }
+  }
+  if (a.ympf) {  // MP32 copy for the fp32 tower: chunk (row0/16, nb), lane (c, g): rows 4g..4g+3, column 16nb + c
+    const int NB = Cp / 16;
+    const int64_t mb = row0 / kRB;
+    for (int i = threadIdx.x; i < NB * 64; i += blockDim.x) {
+      const int nb = i >> 6, l = i & 63;
+      const int c = 16 * nb + (l & 15), g = l >> 4;
+      float v[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = 4 * g + t;
+        v[t] = (r < rows && c < C) ? (xs[r * C + c] - cm[c]) * cs[c] : 0.f;
+      }
+      *reinterpret_cast<float4*>(a.ympf + ((mb * NB + nb) * 64 + l) * 4) = make_float4(v[0], v[1], v[2], v[3]);
     }
   }
   if (a.stat_part && a.means) {  // data_norm batch statistics, per-block partial row
@@ -202,7 +221,9 @@ __global__ __launch_bounds__(256) void k_head_bwd(HeadArgs a) {
   const float inv_c = 1.f / (float)C;
   for (int i = threadIdx.x; i < rows * C; i += blockDim.x) {
     const int r = (int)(((float)i + 0.5f) * inv_c), c = i - r * C;
-    float g = a.dy ? bf2f(a.dy[(int64_t)(row0 + r) * ldy + c]) * cs[c] : 0.f;
+    float g = a.dyf  ? a.dyf[(int64_t)(row0 + r) * ldy + c] * cs[c]
+              : a.dy ? bf2f(a.dy[(int64_t)(row0 + r) * ldy + c]) * cs[c]
+                     : 0.f;
     const int code = jc[c];
     if (code != -1 && a.dlin) {
       const float dl = dls[r];

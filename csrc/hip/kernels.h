@@ -315,6 +315,10 @@ struct HeadArgs {
   float* stat_acc = nullptr;           // [head_blocks(B), 2C] per-block partial sums (bwd)
   unsigned short* ymp = nullptr;       // optional m-packed copy of y (fwd; Cp % 32 == 0, B rows padded to 16)
   float* stat_part = nullptr;          // optional [head_blocks(B), 2C] batch-stat partials computed in fwd
+  // fp32 MLP input (the fp32 tower): used instead of y / ymp / dy when set
+  float* yf = nullptr;         // [B, ldy] fp32 out (fwd)
+  float* ympf = nullptr;       // MP32 copy of y (fwd; Cp % 16 == 0)
+  const float* dyf = nullptr;  // [B, ldy] fp32 in (bwd)
 };
 size_t head_lds_bytes(int C, int D, int Cp);
 int head_blocks(int B);
@@ -441,6 +445,11 @@ struct TowerLayerDev {
   float* dw = nullptr;             // [N][K] fp32 grad (accumulated)
   float* db = nullptr;             // [N]
   int bias_off = 0;                // column of this layer's db partials in a bias_part row
+  // fp32 tower (tower32.hip): packed fp32 weights and fp32 MP32 activations
+  const float* wpf = nullptr;   // packed W  [Np/16][Kp/16][64][4]
+  const float* wtpf = nullptr;  // packed W^T [Kp/16][Np/16][64][4]
+  float* xmpf = nullptr;        // MP32 of X_{l+1}
+  float* dzmpf = nullptr;       // MP32 of dZ_{l+1}
 };
 struct TowerArgs {
   int M = 0, Mp = 0, L = 0;
@@ -479,6 +488,11 @@ struct TowerArgs {
   float* dn_stats = nullptr;
   int dw_splits = 2;
   int debug = 0;  // timing experiments only (PBX_TOWER_DEBUG): 1 no loss reduction, 2 no dW reductions, 4 no dW GEMM
+  // fp32 tower (f32 = 1): fp32 X0 row-major / MP32, fp32 dX0; widths padded to 16
+  int f32 = 0;
+  const float* x0f = nullptr;
+  const float* x0mpf = nullptr;
+  float* dx0f = nullptr;
 };
 int tower_nwg(int M);
 size_t tower_lds_bytes(const TowerArgs& a);
@@ -487,6 +501,22 @@ void launch_tower_bwd(const TowerArgs& a, hipStream_t s);
 void launch_tower_dw(const TowerArgs& a, hipStream_t s);
 // fp32 [N][K] -> packed W / W^T (pads zero), all layers in one launch
 void launch_tower_pack(const TowerArgs& a, const float* const* w, hipStream_t s);
+
+// fp32 tower (tower32.hip): the same three launches on v_mfma_f32_16x16x4_f32
+// (exact fp32, the reference fc precision).  Layouts (floats, widths padded
+// to 16, Mp a multiple of 256):
+//  * MP32 activations Z[M][N]: 1 KB chunks [Mp/16][Np/16][64][4]; lane l,
+//    element t of chunk (mb, nb) = Z[16mb + 4(l/16) + t][16nb + l%16] -- the
+//    16x16x4 accumulator layout, and the operand fragment of the dW GEMM
+//  * packed W  [Np/16][Kp/16][64][4]: lane l, t = W[16nb + l%16][16kb + 4(l/16) + t]
+//  * packed Wt [Kp/16][Np/16][64][4]: lane l, t = W[16nb + 4(l/16) + t][16kb + l%16]
+constexpr int kTower32MaxWidth = 512;
+int tower32_lds_ld(int maxw);
+size_t tower32_lds_bytes(const TowerArgs& a);
+void launch_tower32_fwd(const TowerArgs& a, hipStream_t s);
+void launch_tower32_bwd(const TowerArgs& a, hipStream_t s);
+void launch_tower32_dw(const TowerArgs& a, hipStream_t s);
+void launch_tower32_pack(const TowerArgs& a, const float* const* w, hipStream_t s);
 
 // Flat Adam with fused extras: beta powers advanced by the last workgroup
 // (ticket), weight regions re-packed to bf16 tower layouts, data_norm
@@ -499,6 +529,8 @@ struct AdamExtras {
   int pack_N[kMaxPackRegions], pack_K[kMaxPackRegions], pack_Np[kMaxPackRegions], pack_Kp[kMaxPackRegions];
   unsigned short* pack_wp[kMaxPackRegions];
   unsigned short* pack_wtp[kMaxPackRegions];
+  float* pack_wp32[kMaxPackRegions];   // fp32 tower regions (pack_wp / pack_wtp null)
+  float* pack_wtp32[kMaxPackRegions];
   int n_dn = 0;
   const float* dn_stats[kMaxDnUpdates];
   float* dn_bsize[kMaxDnUpdates];

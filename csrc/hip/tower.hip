@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
+#include "tower_common.h"
 
 namespace pbx {
 namespace {
@@ -417,75 +418,8 @@ __global__ __launch_bounds__(256) void k_tower_dw(TowerArgs a, int ndw) {
   const int tid = threadIdx.x;
   if ((int)blockIdx.x >= ndw && (a.debug & 2)) return;
   if ((int)blockIdx.x < ndw && (a.debug & 4)) return;
-  if ((int)blockIdx.x >= ndw) {  // ---- column reductions: 32 columns x 8 row groups per block
-    __shared__ float red[2][8][32];
-    const int cl = tid & 31, rg = tid >> 5;
-    const int nbias = (a.bias_ld + 31) / 32;
-    const int rb = (int)blockIdx.x - ndw;
-    if (rb < nbias) {
-      const int col = rb * 32 + cl;
-      const int nwg = a.Mp / TBM;
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-      if (col < a.bias_ld) {
-        int r = rg;
-        for (; r + 24 < nwg; r += 32) {
-          s0 += a.bias_part[(int64_t)r * a.bias_ld + col];
-          s1 += a.bias_part[(int64_t)(r + 8) * a.bias_ld + col];
-          s2 += a.bias_part[(int64_t)(r + 16) * a.bias_ld + col];
-          s3 += a.bias_part[(int64_t)(r + 24) * a.bias_ld + col];
-        }
-        for (; r < nwg; r += 8) s0 += a.bias_part[(int64_t)r * a.bias_ld + col];
-      }
-      red[0][rg][cl] = (s0 + s1) + (s2 + s3);
-      __syncthreads();
-      if (rg == 0 && col < a.bias_ld) {
-        float s = 0.f;
-        for (int g = 0; g < 8; ++g) s += red[0][g][cl];
-        if (col == a.dbout_off) {
-          if (a.db_out) a.db_out[0] += s;
-        } else if (col >= a.dwout_off) {
-          if (a.dw_out && col - a.dwout_off < a.ly[a.L - 1].N) a.dw_out[col - a.dwout_off] += s;
-        } else {
-          for (int l = 0; l < a.L; ++l) {
-            const TowerLayerDev& ly = a.ly[l];
-            if (col >= ly.bias_off && col < ly.bias_off + ly.N) {
-              if (ly.db) ly.db[col - ly.bias_off] += s;
-              break;
-            }
-          }
-        }
-      }
-      return;
-    }
-    const int c = (rb - nbias) * 32 + cl;
-    const int C = a.dn_C;
-    float sx = 0.f, sq = 0.f, sx1 = 0.f, sq1 = 0.f;
-    if (a.dn_part && c < C) {
-      int r = rg;
-      for (; r + 8 < a.dn_rows; r += 16) {
-        sx += a.dn_part[(int64_t)r * 2 * C + c];
-        sq += a.dn_part[(int64_t)r * 2 * C + C + c];
-        sx1 += a.dn_part[(int64_t)(r + 8) * 2 * C + c];
-        sq1 += a.dn_part[(int64_t)(r + 8) * 2 * C + C + c];
-      }
-      for (; r < a.dn_rows; r += 8) {
-        sx += a.dn_part[(int64_t)r * 2 * C + c];
-        sq += a.dn_part[(int64_t)r * 2 * C + C + c];
-      }
-    }
-    red[0][rg][cl] = sx + sx1;
-    red[1][rg][cl] = sq + sq1;
-    __syncthreads();
-    if (rg == 0 && a.dn_part && c < C) {
-      float tx = 0.f, tq = 0.f;
-      for (int g = 0; g < 8; ++g) {
-        tx += red[0][g][cl];
-        tq += red[1][g][cl];
-      }
-      a.dn_stats[c] = 1.f;
-      a.dn_stats[C + c] = tx / (float)a.M;
-      a.dn_stats[2 * C + c] = tq / (float)a.M + a.dn_eps;
-    }
+  if ((int)blockIdx.x >= ndw) {  // ---- column reductions (tower_common.h)
+    tower_col_reduce(a, (int)blockIdx.x - ndw, TBM);
     return;
   }
   __shared__ __attribute__((aligned(16))) u16 smem[DW_NST * DW_STAGE];
@@ -656,6 +590,11 @@ __global__ __launch_bounds__(256) void k_adam_fused(float* __restrict__ p, float
         const int64_t i = e0 + k - off;
         if (i < 0 || i >= cnt || e0 + k >= n) continue;
         const int nn = (int)(i / K), kk = (int)(i % K);
+        if (x.pack_wp32[r]) {  // fp32 tower
+          x.pack_wp32[r][tower_wp32_index(nn, kk, x.pack_Kp[r])] = pa[k];
+          x.pack_wtp32[r][tower_wtp32_index(nn, kk, x.pack_Np[r])] = pa[k];
+          continue;
+        }
         const u16 bv = f2bf(pa[k]);
         x.pack_wp[r][wp_index(nn, kk, x.pack_Kp[r])] = bv;
         x.pack_wtp[r][wtp_index(nn, kk, x.pack_Np[r])] = bv;

@@ -71,14 +71,22 @@ class DeepFM(nn.Module):
         # the per-layer GEMM path (mlp.hip) for comparison
         self.tower = CtrTower(self.mlp, self.dn, self.S, self.Eo, self.ew_col, self.D, use_head_lin=True)
         self.use_tower = True
-        # "fp32": the reference's precision (fluid fc = fp32 GEMMs): fp32
-        # data_norm / FM kernels and fp32 library GEMMs for the MLP
+        # "fp32": the reference's precision (fluid fc = fp32 GEMMs): the
+        # exact-fp32 fused tower (tower32.hip, v_mfma_f32_16x16x4_f32); layer
+        # widths above its LDS budget fall back to fp32 library GEMMs
         self.precision = "bf16"
+
+    def set_precision(self, precision: str):
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(precision)
+        self.precision = precision
+        self.tower.fp32 = precision == "fp32" and self.mlp.tower_fp32_ok()
+        self.mlp.invalidate_pack()
 
     def forward(self, batch):
         B, S = batch.B, batch.S
         x = pull_seqpool_cvm_concat(self.engine, batch.keys, batch.lod, B, S, batch.cvm, batch.dense, self.sp)
-        if self.precision == "fp32" and x.is_cuda:
+        if self.precision == "fp32" and x.is_cuda and not (self.use_tower and self.tower.fp32):
             return self._forward_fp32(x, batch.label)
         if self.use_tower or not x.is_cuda:
             return self.tower(x, batch.label)

@@ -146,14 +146,24 @@ class FusedMLP(nn.Module):
         self.packed_by_optimizer = False
 
     # ---- fused tower path (csrc/hip/tower.hip)
-    def tower_workspace(self, M: int, device: torch.device):
-        if self._tw is None or self._tw.M != M:
+    def tower_workspace(self, M: int, device: torch.device, fp32: bool = False):
+        """Persistent buffers of the fused tower for batch M.  fp32=True is the
+        exact-fp32 tower (csrc/hip/tower32.hip, the reference fc precision),
+        else the bf16-operand tower (csrc/hip/tower.hip)."""
+        if self._tw is None or self._tw.M != M or bool(self._tw.fp32) != bool(fp32):
             dims = [self.in_dim] + list(self.hidden)
-            # dW split over M (fp32 atomics between splits); PBX_TOWER_DW_SPLITS in {1, 2, 4}
-            splits = int(os.environ.get("PBX_TOWER_DW_SPLITS", "2"))
-            self._tw = _native.hip().TowerWorkspace(M, dims, device.index or 0, splits)
+            # dW split over M (fp32 atomics between splits)
+            if fp32:
+                splits = int(os.environ.get("PBX_TOWER32_DW_SPLITS", "8"))
+            else:
+                splits = int(os.environ.get("PBX_TOWER_DW_SPLITS", "2"))
+            self._tw = _native.hip().TowerWorkspace(M, dims, device.index or 0, splits, bool(fp32))
             self._packed = False
         return self._tw
+
+    def tower_fp32_ok(self) -> bool:
+        """The fp32 tower keeps two 32-row fp32 tiles in LDS: widths <= 512."""
+        return max([self.in_dim] + list(self.hidden)) <= 512
 
     def ensure_packed(self):
         if not self._packed or not self.packed_by_optimizer:

@@ -1,8 +1,9 @@
 """CTR dense tower: fused head (data_norm + first-order/FM) + MLP + loss as
 one autograd node, on the three-launch HIP tower (csrc/hip/tower.hip).
 
-Forward  : k_head_fwd (data_norm -> bf16 MLP input in row-major and m-packed
-           layouts, lin = first-order + FM, data_norm batch-stat partials)
+Forward  : k_head_fwd (data_norm -> MLP input (bf16, or fp32 for the fp32 tower)
+           in row-major and m-packed layouts, lin = first-order + FM,
+           data_norm batch-stat partials)
            k_tower_fwd (all ReLU layers, output GEMV, sigmoid, log-loss,
            d loss/d logit, AUC histogram)
 Backward : k_tower_bwd (dX chain) + k_tower_dw (grouped dW GEMM, bias /
@@ -54,17 +55,18 @@ class _CtrTowerFn(torch.autograd.Function):
         if x.is_cuda:
             join_grad_producers()  # a previous dW still reading the activations (no optimizer step between)
         B = x.shape[0]
-        ws = mlp.tower_workspace(B, x.device)
+        ws = mlp.tower_workspace(B, x.device, fp32=t.fp32)
         mlp.ensure_packed()
         x = x.contiguous()
         yt = t._cross_yt(B, x.device) if t.cross is not None else None
+        Cp = ws.K0p  # MLP input width: padded to 32 (bf16 tower) / 16 (fp32 tower)
         if dn is not None:
             part = t._dn_part(B, x.device)
-            _, lin, means, scales = h.head_fwd(x, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim), dn.batch_size,
+            _, lin, means, scales = h.head_fwd(x, t.S, t.Eo, t.ew_col, t.D, Cp, dn.batch_size,
                                                dn.batch_sum, dn.batch_square_sum, y_out=ws.x0(), yT_out=yt,
                                                ymp_out=ws.x0mp(), stat_part=part)
         else:
-            _, lin, means, scales = h.head_fwd(x, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim), None, None, None,
+            _, lin, means, scales = h.head_fwd(x, t.S, t.Eo, t.ew_col, t.D, Cp, None, None, None,
                                                y_out=ws.x0(), yT_out=yt, ymp_out=ws.x0mp())
         if extra is not None:
             lin_use = extra.detach().contiguous().float().view(-1)
@@ -141,7 +143,7 @@ class _CtrTowerFn(torch.autograd.Function):
             net._xw.backward(ws.x0(), ctx.yt, ds, [_ensure_grad(w) for w in net.w],
                              [_ensure_grad(b) for b in net.b], w_c.detach(), _ensure_grad(w_c), dy_out=dx0)
         use_lin = t.use_head_lin and not ctx.has_extra
-        dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, pad32(mlp.in_dim),
+        dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, ws.K0p,
                            ctx.means, ctx.scales, dn.eps if dn is not None else 0.0, dlin_scale=gl,
                            want_stats=False)
         d_extra = (ctx.dz * gl if gl is not None else ctx.dz.clone()) if ctx.has_extra else None
@@ -154,10 +156,16 @@ class CtrTower:
     S slot blocks of width Eo (embed_w at ew_col, D embedx after it) followed by
     dense columns make up the input x [B, C]."""
 
-    def __init__(self, mlp, dn, S: int, Eo: int, ew_col: int, D: int, use_head_lin: bool = True, cross=None):
+    def __init__(self, mlp, dn, S: int, Eo: int, ew_col: int, D: int, use_head_lin: bool = True, cross=None,
+                 fp32: bool = False):
         """``cross``: optional (CrossNetV2, w_c) whose width is the tower's
         padded input width: a DCN-V2 cross logit computed inside the tower
-        from its normalised input and added to the MLP logit."""
+        from its normalised input and added to the MLP logit.
+        ``fp32``: run the exact-fp32 tower (tower32.hip) instead of the
+        bf16-operand one (the reference's fp32 fc precision)."""
+        if fp32 and cross is not None:
+            raise ValueError("the fp32 tower does not carry the DCN-V2 cross stack")
+        self.fp32 = bool(fp32)
         self.mlp, self.dn = mlp, dn
         self.cross = cross
         self._yt = None

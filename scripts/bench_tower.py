@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--M", type=int, default=8192)
     ap.add_argument("--dims", type=str, default="304,400,400,400")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--fp32", action="store_true", help="exact-fp32 tower (tower32.hip)")
     args = ap.parse_args()
     dims = [int(d) for d in args.dims.split(",")]
     dev = torch.device("cuda:0")
@@ -31,9 +32,9 @@ def main():
     mlp = FusedMLP(dims[0], dims[1:], 1).to(dev)
     arena = DenseArena(mlp.parameters(), dev)
     opt = FlatAdam(arena, lr=1e-3, clear_grad=True).fuse(mlps=[mlp])
-    ws = mlp.tower_workspace(args.M, dev)
+    ws = mlp.tower_workspace(args.M, dev, fp32=args.fp32)
     mlp.ensure_packed()
-    ws.x0()[:, :dims[0]] = torch.randn(args.M, dims[0], device=dev).to(torch.bfloat16)
+    ws.x0()[:, :dims[0]] = torch.randn(args.M, dims[0], device=dev).to(ws.x0().dtype)
     lin = torch.randn(args.M, device=dev)
     label = (torch.rand(args.M, device=dev) < 0.3).float()
     gl = torch.ones(1, device=dev)
@@ -41,15 +42,17 @@ def main():
     def fwd():
         ws.forward(list(mlp.b), mlp.w_out.view(-1), mlp.b_out, lin, label)
 
-    def bwd():
+    def bwd(parts=3):
         ws.backward(gl, mlp.w_out.detach().view(-1), [w.grad for w in mlp.w], [b.grad for b in mlp.b],
-                    mlp.w_out.grad.view(-1), mlp.b_out.grad, True)
+                    mlp.w_out.grad.view(-1), mlp.b_out.grad, True, parts=parts)
 
     def step():
         opt.step()
 
     flops = 2 * args.M * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
-    for name, fn, fl in (("forward", fwd, flops), ("backward", bwd, 2 * flops), ("adam+pack", step, 0)):
+    mlp.ensure_grads()
+    for name, fn, fl in (("forward", fwd, flops), ("backward", bwd, 2 * flops), ("dX chain", lambda: bwd(1), flops),
+                         ("dW", lambda: bwd(2), flops), ("adam+pack", step, 0)):
         for _ in range(5):
             fn()
         torch.cuda.synchronize()
