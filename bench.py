@@ -136,9 +136,15 @@ def main():
                          "work (measured slower on one MI355X: 0.356 vs 0.281 ms/step, see "
                          "profiles/r2_bench_prefetch.txt)")
     ap.add_argument("--no-prefetch", dest="prefetch", action="store_false")
-    ap.add_argument("--dense-ipc", action="store_true",
-                    help="dense gradient all-reduce on the in-house IPC mesh (one-shot, xGMI peer writes) "
-                         "instead of RCCL")
+    ap.add_argument("--dense", choices=("ipc", "rccl"), default="ipc",
+                    help="multi-rank dense gradient all-reduce: the in-house IPC mesh (xGMI peer writes, "
+                         "two-phase; self-tested, falls back to RCCL) or RCCL")
+    ap.add_argument("--sparse-exchange", choices=("ipc", "rccl"), default="ipc",
+                    help="multi-rank sparse key/value/grad exchange: IPC mesh (self-tested, falls back to RCCL) "
+                         "or RCCL all_to_all")
+    ap.add_argument("--same-gpu", action="store_true",
+                    help="rehearsal: every rank on cuda:0 with a gloo control plane (all in-step collectives "
+                         "then run on the IPC meshes); exercises the N-GPU step on one GPU")
     ap.add_argument("--force-collectives", action="store_true",
                     help="run the multi-GPU exchange/all-reduce path even on 1 rank (rehearsal)")
     ap.add_argument("--dry-run", action="store_true",
@@ -168,13 +174,19 @@ def main():
     from paddlebox_amd.ps.config import PSConfig
     from paddlebox_amd.ps.sparse_engine import SparseEngine
 
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    gpu_index = 0 if args.same_gpu else local_rank
+    torch.cuda.set_device(gpu_index)
+    device = torch.device("cuda", gpu_index)
     multi = world > 1 or args.force_collectives
     ranks_seen = 1
+    # control-plane tensors live where the backend wants them
+    cdev = torch.device("cpu") if args.same_gpu else device
     if multi:
-        dist.init_process_group("nccl", device_id=device)
-        seen = torch.ones(1, device=device)
+        if args.same_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
+        seen = torch.ones(1, device=cdev)
         dist.all_reduce(seen)
         ranks_seen = int(seen.item())
 
@@ -199,14 +211,14 @@ def main():
         # exchange exactly by distinct keys per owner, max over batches and ranks
         from paddlebox_amd.ps.sparse_engine import exchange_capacity_for
 
-        xc = torch.tensor([exchange_capacity_for([hb.keys.to(device) for hb in host_batches], world)], device=device)
+        xc = torch.tensor([exchange_capacity_for([hb.keys.to(device) for hb in host_batches], world)], device=cdev)
         dist.all_reduce(xc, op=dist.ReduceOp.MAX)
         xcap = int(xc.item())
         log(rank, f"[bench] key exchange capacity {xcap} per peer (heuristic bound would be "
                   f"{int(math.ceil(B * S / world * 1.25)) + 64})")
     engine = SparseEngine(cfg, max_keys=B * S, device=device, capacity=synth.total_features,
                           slot_ids=[float(s + 1) for s in range(S)], auto_insert=args.no_prefill,
-                          exchange_capacity=xcap)
+                          exchange_capacity=xcap, exchange=args.sparse_exchange)
 
     t0 = time.time()
     if not args.no_prefill:
@@ -252,12 +264,24 @@ def main():
     # the dense all-reduce runs on its own communicator and side stream, started
     # as soon as the tower's gradients are final: it overlaps the sparse push
     ipc = None
-    if args.dense_ipc and multi:
-        from paddlebox_amd.parallel.ipc import IpcMesh
+    if multi and (args.dense == "ipc" or args.same_gpu):
+        from paddlebox_amd.parallel.ipc import IpcMesh, IpcMeshError
 
-        ipc = IpcMesh(arena.grad.numel() * 4, device=device)
+        try:
+            ipc = IpcMesh(arena.grad.numel() * 4, device=device)
+            if not ipc.self_test():
+                ipc.close()
+                ipc = None
+                log(rank, "[bench] dense IPC mesh self-test failed; RCCL all-reduce")
+        except IpcMeshError as e:
+            ipc = None
+            log(rank, f"[bench] dense IPC mesh unavailable ({e}); RCCL all-reduce")
+    if multi and args.same_gpu and (ipc is None or engine.exchange_mode != "ipc"):
+        raise SystemExit("--same-gpu needs the IPC meshes (RCCL cannot run two ranks on one GPU)")
+    # RCCL dense all-reduce: its own communicator, so it overlaps the sparse
+    # exchange; the IPC meshes are independent of each other by construction
     sync = DenseSync(arena, mode="grad_allreduce",
-                     overlap_group=dist.new_group(list(range(world))) if multi else None, ipc=ipc)
+                     overlap_group=dist.new_group(list(range(world))) if (multi and ipc is None) else None, ipc=ipc)
     if getattr(model, "tower", None) is not None:
         model.tower.on_dense_grads = sync.launch
 
@@ -354,7 +378,7 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t_start
     if multi:
-        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        t = torch.tensor([dt], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     log(rank, f"[bench] host enqueue {t_enq / args.steps * 1e3:.4f} ms/step, wall {dt / args.steps * 1e3:.4f} ms/step")
@@ -381,7 +405,9 @@ def main():
                 tw = time.perf_counter() - t0w
                 log(rank, f"[bench] host-diag {name} window {w}: host {th / args.steps * 1e3:.4f} "
                           f"wall {tw / args.steps * 1e3:.4f} ms/step")
-    overflow = engine.check_overflow()
+    overflow = engine.check_overflow()  # also raises if an IPC exchange timed out
+    if ipc is not None:
+        ipc.check()
     samples = B * world * args.steps
     value = samples / dt
     if rank == 0:
@@ -413,7 +439,9 @@ def main():
                 "parallelism": f"dp{world}+sparse-shard{world}",
                 "ranks_seen": ranks_seen,
                 "launcher": launcher,
-                "dense_allreduce": "ipc-oneshot" if ipc is not None else "rccl",
+                "dense_allreduce": ("ipc" if ipc is not None else "rccl") if multi else "none",
+                "sparse_exchange": engine.exchange_mode,
+                "same_gpu_rehearsal": bool(args.same_gpu),
                 "pipelined_pull": bool(graphed is not None and graphed.prefetch is not None),
                 "mlp_dtype": args.mlp_dtype,
                 "unique_keys_per_batch": round(sum(u_per_batch) / len(u_per_batch), 1),

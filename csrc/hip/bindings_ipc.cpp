@@ -51,15 +51,19 @@ void ipc_close(int64_t base) { hip_ok(hipIpcCloseMemHandle(reinterpret_cast<void
 class IpcComm {
  public:
   // state: own int64 [4] = epoch, arrive|depart (2 x u32), err, pad
-  IpcComm(int rank, int world, int64_t slot_bytes, const Tensor& state, int blocks)
+  IpcComm(int rank, int world, int64_t slot_bytes, const Tensor& state, int blocks, int depth, int64_t spin_limit)
       : blocks_(blocks) {
     IPC_CHECK(world >= 1 && world <= kIpcMaxRanks && rank >= 0 && rank < world, "rank / world");
     IPC_CHECK(slot_bytes > 0 && slot_bytes % 16 == 0, "slot_bytes must be a positive multiple of 16");
     IPC_CHECK(state.is_cuda() && state.scalar_type() == torch::kInt64 && state.numel() >= 4, "state");
     IPC_CHECK(blocks >= 1 && blocks <= 256, "blocks");
+    IPC_CHECK(depth >= 2 && depth <= 16, "depth in 2..16");
+    IPC_CHECK(spin_limit > 0, "spin_limit");
     std::memset(&p_, 0, sizeof(p_));
     p_.world = world;
     p_.rank = rank;
+    p_.depth = depth;
+    p_.spin_limit = spin_limit;
     p_.slot_bytes = slot_bytes;
     auto* st = reinterpret_cast<int64_t*>(state.data_ptr());
     p_.epoch = reinterpret_cast<uint64_t*>(st + 0);
@@ -75,26 +79,53 @@ class IpcComm {
   void check_ready() const {
     for (int p = 0; p < p_.world; ++p) IPC_CHECK(p_.inbox[p] && p_.flags[p], "peer pointers not set");
   }
-  // out = scale * sum over ranks of src (f32, <= slot_bytes)
-  void allreduce(const Tensor& src, Tensor out, double scale) {
+  // out = scale * sum over ranks of src (f32, in place allowed).  One-shot up
+  // to one slot; two-phase (reduce-scatter + all-gather) needs ceil(n/W)
+  // floats per slot.
+  void allreduce(const Tensor& src, Tensor out, double scale, bool two_phase) {
     check_ready();
     IPC_CHECK(src.is_cuda() && src.scalar_type() == torch::kFloat32 && src.is_contiguous(), "src");
     IPC_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat32 && out.is_contiguous() &&
                   out.numel() == src.numel(), "out");
-    IPC_CHECK(((uintptr_t)src.data_ptr() & 15) == 0, "src must be 16-byte aligned");
-    const int64_t nb = src.numel() * 4;
-    IPC_CHECK(nb <= p_.slot_bytes, "tensor larger than the mesh slot");
-    launch_ipc_collective(p_, src.data_ptr(), nb, true, reinterpret_cast<float*>(out.data_ptr()), src.numel(),
-                          (float)scale, true, blocks_, at::hip::getCurrentHIPStream().stream());
+    IPC_CHECK(((uintptr_t)src.data_ptr() & 15) == 0 && ((uintptr_t)out.data_ptr() & 15) == 0,
+              "src / out must be 16-byte aligned");
+    const int64_t n = src.numel();
+    const int W = p_.world;
+    if (two_phase) {
+      const int64_t cs = ((n + W - 1) / W + 3) / 4 * 4;
+      IPC_CHECK(cs * 4 <= p_.slot_bytes, "two-phase chunk larger than the mesh slot");
+    } else {
+      IPC_CHECK(n * 4 <= p_.slot_bytes, "tensor larger than the mesh slot");
+    }
+    launch_ipc_allreduce(p_, reinterpret_cast<const float*>(src.data_ptr()),
+                         reinterpret_cast<float*>(out.data_ptr()), n, (float)scale, two_phase, blocks_,
+                         at::hip::getCurrentHIPStream().stream());
   }
-  // all-to-all of fixed slots: send [world][slot_bytes] -> this rank's inbox
-  // parity of this call (returned as the parity index; the caller views it)
-  void exchange(const Tensor& send) {
+  // all-to-all: send [world, slot_bytes] (contiguous, any dtype) -> dst (same
+  // shape); counts / rcounts: optional device int32 [world]
+  void exchange(const Tensor& send, Tensor dst, const c10::optional<Tensor>& counts, int64_t rec_bytes,
+                bool fill_tail, const c10::optional<Tensor>& rcounts) {
     check_ready();
     IPC_CHECK(send.is_cuda() && send.is_contiguous() && send.nbytes() == (size_t)(p_.world * p_.slot_bytes),
               "send must be contiguous [world, slot_bytes]");
-    launch_ipc_collective(p_, send.data_ptr(), p_.slot_bytes, false, nullptr, 0, 1.f, false, blocks_,
-                          at::hip::getCurrentHIPStream().stream());
+    IPC_CHECK(dst.is_cuda() && dst.is_contiguous() && dst.nbytes() == (size_t)(p_.world * p_.slot_bytes),
+              "dst must be contiguous [world, slot_bytes]");
+    IPC_CHECK(((uintptr_t)send.data_ptr() & 15) == 0 && ((uintptr_t)dst.data_ptr() & 15) == 0,
+              "send / dst must be 16-byte aligned");
+    IPC_CHECK(rec_bytes > 0 && rec_bytes <= p_.slot_bytes, "rec_bytes");
+    const int32_t* c = nullptr;
+    int32_t* rc = nullptr;
+    if (counts.has_value() && counts->defined()) {
+      IPC_CHECK(counts->is_cuda() && counts->scalar_type() == torch::kInt32 && counts->numel() >= p_.world, "counts");
+      c = reinterpret_cast<const int32_t*>(counts->data_ptr());
+    }
+    if (rcounts.has_value() && rcounts->defined()) {
+      IPC_CHECK(rcounts->is_cuda() && rcounts->scalar_type() == torch::kInt32 && rcounts->numel() >= p_.world,
+                "rcounts");
+      rc = reinterpret_cast<int32_t*>(rcounts->data_ptr());
+    }
+    launch_ipc_exchange(p_, send.data_ptr(), dst.data_ptr(), c, rec_bytes, fill_tail, rc, blocks_,
+                        at::hip::getCurrentHIPStream().stream());
   }
 
  private:
@@ -109,10 +140,13 @@ void bind_ipc(py::module& m) {
   m.def("ipc_open", &ipc_open);
   m.def("ipc_close", &ipc_close);
   py::class_<IpcComm>(m, "IpcComm")
-      .def(py::init<int, int, int64_t, const Tensor&, int>())
+      .def(py::init<int, int, int64_t, const Tensor&, int, int, int64_t>(), py::arg("rank"), py::arg("world"),
+           py::arg("slot_bytes"), py::arg("state"), py::arg("blocks"), py::arg("depth"), py::arg("spin_limit"))
       .def("set_peer", &IpcComm::set_peer)
-      .def("allreduce", &IpcComm::allreduce)
-      .def("exchange", &IpcComm::exchange);
+      .def("allreduce", &IpcComm::allreduce, py::arg("src"), py::arg("out"), py::arg("scale"),
+           py::arg("two_phase"))
+      .def("exchange", &IpcComm::exchange, py::arg("send"), py::arg("dst"), py::arg("counts"), py::arg("rec_bytes"),
+           py::arg("fill_tail"), py::arg("rcounts"));
 }
 
 }  // namespace pbx

@@ -78,8 +78,11 @@ class TowerWorkspace {
     int64_t boff = 0;
     for (int l = 0; l < L_; ++l) {
       const int64_t Kp = pad(dims[l], wpad_), Np = pad(dims[l + 1], wpad_);
-      wp_.push_back(torch::zeros({Np * Kp}, ob));
-      wtp_.push_back(torch::zeros({Np * Kp}, ob));
+      // fp32: 8 KB of slack -- the tower32 weight pipeline loads up to 8
+      // k-groups past a block's last fragment (values unused)
+      const int64_t slack = fp32 ? 2048 : 0;
+      wp_.push_back(torch::zeros({Np * Kp + slack}, ob));
+      wtp_.push_back(torch::zeros({Np * Kp + slack}, ob));
       xmp_.push_back(torch::zeros({Mp_ * Np}, ob));
       dzmp_.push_back(torch::zeros({Mp_ * Np}, ob));
       boff_.push_back(boff);
@@ -137,6 +140,7 @@ class TowerWorkspace {
       a.auc_buckets = (int)(auc_table->numel() / 2);
       a.auc_mask = OP<float>(auc_mask);
     }
+    if (stamps_.defined()) a.stamps = reinterpret_cast<long long*>(stamps_.data_ptr());
     if (fp32_) launch_tower32_fwd(a, stream());
     else launch_tower_fwd(a, stream());
     return {loss_, pred_, dz_};
@@ -209,6 +213,8 @@ class TowerWorkspace {
   int64_t M() const { return M_; }
   int64_t Mp() const { return Mp_; }
   int64_t K0p() const { return pad(dims_[0], wpad_); }
+  // timing experiments: per-wave s_memtime stamps of the fp32 forward
+  void set_stamps(const Tensor& t) { stamps_ = t; }
   bool fp32() const { return fp32_; }
   int64_t dw_splits() const { return splits_; }
   int64_t lds_ld() const { return lds_ld_; }
@@ -273,7 +279,7 @@ class TowerWorkspace {
   int64_t wpad_ = 32;
   int L_ = 0, lds_ld_ = 0, bias_ld_ = 0, dwout_off_ = 0, dbout_off_ = 0;
   std::vector<int64_t> boff_;
-  Tensor x0_, x0mp_, dx0_, bias_part_, pred_, dz_, loss_, part_, ticket_;
+  Tensor x0_, x0mp_, dx0_, bias_part_, pred_, dz_, loss_, part_, ticket_, stamps_;
   std::vector<Tensor> wp_, wtp_, xmp_, dzmp_;
 };
 
@@ -355,6 +361,7 @@ void bind_tower(py::module& m) {
            py::arg("db_out"), py::arg("need_dx"), py::arg("dn_part") = py::none(), py::arg("dn_rows") = 0,
            py::arg("dn_eps") = 0.0, py::arg("dn_stats") = py::none(), py::arg("parts") = 3)
       .def("pack_regions", &TowerWorkspace::pack_regions)
+      .def("set_stamps", &TowerWorkspace::set_stamps)
       .def("x0", &TowerWorkspace::x0)
       .def("x0mp", &TowerWorkspace::x0mp)
       .def("xmp", &TowerWorkspace::xmp)

@@ -1,24 +1,36 @@
-// In-house IPC mesh collective for one node (xGMI peer-to-peer writes).
+// In-house IPC mesh collectives for the GPUs of one node (xGMI peer writes).
 //
-// Every rank owns an inbox (2 parities x W slots x slot_bytes) and a flag
-// word per source rank, both exported with hipIpcGetMemHandle and mapped by
-// every peer.  One kernel per collective, graph-capturable and host-sync
-// free:
-//   1. put:    the grid writes its payload (slot p of the send buffer, or the
-//              whole buffer for a broadcast) straight into peer p's inbox
-//              slot [parity][rank] -- one pass over xGMI, no staging;
-//   2. signal: every block fences at system scope and arrives on a local
-//              counter; the last block publishes the epoch into each peer's
-//              flag word [rank] (system-scope release store);
-//   3. wait:   every block waits (bounded spin, acquire loads) until all W
-//              flags of its own inbox carry the epoch;
-//   4. reduce: (all-reduce) out = scale * sum over the W slots.
+// Every rank owns an inbox [depth][2][W][slot_bytes] and 2W flag words, both
+// exported with hipIpcGetMemHandle and mapped by every peer.  One kernel per
+// collective, graph-capturable and free of host synchronisation:
+//   put     the grid writes its payload straight into peer p's inbox slot
+//           [e % depth][phase][me] (one pass over xGMI);
+//   signal  every block fences at system scope and arrives on a local
+//           counter; the last block publishes (epoch << 24 | count) into each
+//           peer's flag word [phase][me] (system-scope release store);
+//   wait    every block polls (bounded, acquire loads) until all W flags of
+//           its own inbox carry the epoch; the counts ride along.
+// Collectives:
+//   exchange   all-to-all of per-peer records: only counts[p] records of slot
+//              p travel (the sparse step's keys / values / gradients, sized by
+//              the unique keys per owner, not by the padded capacity); the
+//              receiver learns the counts from the flags, copies the valid
+//              records to its destination buffer, writes the counts to
+//              rcounts and may fill the rest with 0xFF bytes (= -1 keys);
+//   allreduce  one-shot (W copies summed by every rank, latency-bound sizes)
+//              or two-phase (reduce-scatter + all-gather: each rank moves
+//              2(W-1)/W of the buffer instead of W-1 times it).
 // The epoch lives in device memory and is advanced by the last block to
-// leave, so replays of a captured graph keep counting.  Parity
-// double-buffering makes inbox reuse safe: a peer can only write parity
-// (e+2)%2 after it saw this rank's epoch e+1 flag, which is published after
-// this rank finished reading epoch e.  A spin that exceeds its bound sets
-// err[0] = 1 and the kernel exits (a lost peer cannot hang the GPU).
+// leave, so replays of a captured graph keep counting.  A call uses inbox
+// slot epoch % depth and consumes it inside the launch (the reduce, or the
+// exchange's copy-out into the caller's buffer).  A peer writes the same slot
+// again only at epoch e + depth, after it saw this rank's flag of epoch
+// e + depth - 1, which this rank publishes in a later launch -- so no slot is
+// overwritten while it is read, whatever the caller does between calls.
+// Failure: a wait that exceeds its bound sets the sticky err word, poisons the
+// result (NaN sums / zero counts and -1 keys) and later launches skip their
+// waits, so a lost peer fails every rank fast instead of hanging the GPU or
+// training silently on stale slots; IpcMesh.check() raises on the host.
 // Reference: the in-process c_mixallgather / heter_comm peer copies
 // (c_mixallgather_op.cc:221-327, heter_comm_inl.h:273-490).
 #include <hip/hip_runtime.h>
@@ -28,6 +40,9 @@
 namespace pbx {
 namespace {
 
+constexpr int kCountBits = 24;
+constexpr uint64_t kCountMask = (1ull << kCountBits) - 1;
+
 __device__ __forceinline__ uint64_t ld_acquire_sys(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -35,62 +50,72 @@ __device__ __forceinline__ void st_release_sys(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(256) void k_ipc_collective(IpcPeers pt, const unsigned char* __restrict__ send,
-                                                        int64_t nbytes, int broadcast, float* out, int64_t nfloat,
-                                                        float scale, int reduce) {
-  __shared__ uint64_t s_epoch;
-  __shared__ int s_last;
-  const int W = pt.world, me = pt.rank;
-  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(pt.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  __syncthreads();
-  const uint64_t epoch = s_epoch;
-  const int par = (int)(epoch & 1);
-  const int64_t slot = pt.slot_bytes;
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nth = (int64_t)gridDim.x * blockDim.x;
-  // 1. put (16-byte vectors + a byte tail; slot_bytes is a multiple of 16)
-  const int64_t nv = nbytes >> 4;
-  for (int p = 0; p < W; ++p) {
-    const unsigned char* sb = send + (broadcast ? 0 : p * slot);
-    unsigned char* db = pt.inbox[p] + ((int64_t)par * W + me) * slot;
-    const uint4* src = reinterpret_cast<const uint4*>(sb);
-    uint4* dst = reinterpret_cast<uint4*>(db);
-    for (int64_t i = tid; i < nv; i += nth) dst[i] = src[i];
-    if (tid < (nbytes & 15)) db[(nv << 4) + tid] = sb[(nv << 4) + tid];
-  }
-  // 2. signal
+__device__ __forceinline__ unsigned char* slot_ptr(const IpcPeers& pt, int owner, int slot, int phase, int src) {
+  const int64_t s = pt.slot_bytes;
+  const int W = pt.world;
+  return pt.inbox[owner] + ((((int64_t)slot * 2 + phase) * W + src) * s);
+}
+
+// grid-strided copy of n bytes (16-B vectors + byte tail; both ends 16-B aligned)
+__device__ __forceinline__ void put_bytes(unsigned char* dst, const unsigned char* src, int64_t n, int64_t tid,
+                                          int64_t nth) {
+  const int64_t nv = n >> 4;
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  for (int64_t i = tid; i < nv; i += nth) d4[i] = s4[i];
+  if (tid < (n & 15)) dst[(nv << 4) + tid] = src[(nv << 4) + tid];
+}
+
+// last-arriving block publishes flag value (epoch, count[p]) to every peer
+__device__ __forceinline__ void signal(const IpcPeers& pt, uint64_t epoch, int phase, const int32_t* counts,
+                                       int* s_last, int64_t max_count = 0) {
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned int a = atomicAdd(pt.arrive, 1u) + 1u;
-    s_last = (a % gridDim.x) == 0;
+    *s_last = (a % gridDim.x) == 0;
   }
   __syncthreads();
-  if (s_last && threadIdx.x < W) st_release_sys(pt.flags[threadIdx.x] + me, epoch);
-  // 3. wait for every source's flag in this rank's inbox
-  if (threadIdx.x < W) {
-    const uint64_t* f = pt.flags[me] + threadIdx.x;
+  if (*s_last && (int)threadIdx.x < pt.world) {
+    const int p = threadIdx.x;
+    int64_t cn = counts ? (int64_t)counts[p] : 0;
+    cn = cn < 0 ? 0 : (cn > max_count ? max_count : cn);  // an overflowing sender sends (and announces) a full slot
+    const uint64_t c = (uint64_t)cn & kCountMask;
+    st_release_sys(pt.flags[p] + phase * pt.world + pt.rank, (epoch << kCountBits) | c);
+  }
+}
+
+// wait for all W flags of phase; returns false (and sets err) on timeout.
+// The received counts land in s_cnt[src].
+__device__ __forceinline__ bool wait_all(const IpcPeers& pt, uint64_t epoch, int phase, int* s_cnt, int* s_ok) {
+  if (threadIdx.x == 0) *s_ok = 1;
+  __syncthreads();
+  if ((int)threadIdx.x < pt.world) {
+    const uint64_t* f = pt.flags[pt.rank] + phase * pt.world + threadIdx.x;
+    const bool dead = __hip_atomic_load(pt.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    uint64_t v = ld_acquire_sys(f);
     int64_t spins = 0;
-    while (ld_acquire_sys(f) < epoch) {
+    while (!dead && (v >> kCountBits) < epoch) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > (int64_t)1 << 24) {
-        pt.err[0] = 1;
+      if (++spins > pt.spin_limit) {
+        atomicExch(pt.err, 1);
         break;
       }
+      v = ld_acquire_sys(f);
+    }
+    if ((v >> kCountBits) < epoch) {
+      *s_ok = 0;
+      s_cnt[threadIdx.x] = 0;
+    } else {
+      s_cnt[threadIdx.x] = (int)(v & kCountMask);
     }
   }
   __syncthreads();
-  // 4. reduce the W slots of this parity
-  if (reduce) {
-    const float* base = reinterpret_cast<const float*>(pt.inbox[me] + (int64_t)par * W * slot);
-    const int64_t fs = slot / 4;
-    for (int64_t i = tid; i < nfloat; i += nth) {
-      float s = 0.f;
-      for (int p = 0; p < W; ++p) s += __builtin_nontemporal_load(base + p * fs + i);
-      out[i] = s * scale;
-    }
-  }
-  // the last block to leave advances the epoch for the next launch
+  return *s_ok != 0;
+}
+
+// the last block to leave advances the epoch for the next launch
+__device__ __forceinline__ void depart(const IpcPeers& pt, uint64_t epoch) {
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
@@ -99,13 +124,113 @@ __global__ __launch_bounds__(256) void k_ipc_collective(IpcPeers pt, const unsig
   }
 }
 
+__global__ __launch_bounds__(256) void k_ipc_exchange(IpcPeers pt, const unsigned char* __restrict__ send,
+                                                      unsigned char* __restrict__ dst, const int32_t* counts,
+                                                      int64_t rec_bytes, int fill_tail, int32_t* rcounts) {
+  __shared__ uint64_t s_epoch;
+  __shared__ int s_last, s_ok;
+  __shared__ int s_cnt[kIpcMaxRanks];
+  const int W = pt.world, me = pt.rank;
+  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(pt.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __syncthreads();
+  const uint64_t epoch = s_epoch;
+  const int sl = (int)(epoch % (uint64_t)pt.depth);
+  const int64_t slot = pt.slot_bytes;  // bytes per source
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nth = (int64_t)gridDim.x * blockDim.x;
+  for (int p = 0; p < W; ++p) {
+    int64_t n = counts ? (int64_t)counts[p] * rec_bytes : slot;
+    n = n < 0 ? 0 : (n > slot ? slot : n);
+    put_bytes(slot_ptr(pt, p, sl, 0, me), send + p * slot, n, tid, nth);
+  }
+  signal(pt, epoch, 0, counts, &s_last, slot / rec_bytes);
+  const bool ok = wait_all(pt, epoch, 0, s_cnt, &s_ok);
+  // receiver side: the valid records of every source slot are copied out of
+  // the inbox into dst (so the slot is free when this launch ends), counts
+  // out, unused tails filled (keys -> -1)
+  for (int src = 0; src < W; ++src) {
+    int64_t have = counts ? (ok ? (int64_t)s_cnt[src] * rec_bytes : 0) : (ok ? slot : 0);
+    have = have < slot ? have : slot;
+    if (rcounts && tid == 0) rcounts[src] = ok ? (counts ? s_cnt[src] : (int)(slot / rec_bytes)) : 0;
+    unsigned char* d = dst + src * slot;
+    put_bytes(d, slot_ptr(pt, me, sl, 0, src), have, tid, nth);
+    if (fill_tail || !ok) {
+      if ((have & 7) == 0) {  // 8-B records (keys): word stores
+        uint64_t* d8 = reinterpret_cast<uint64_t*>(d);
+        for (int64_t i = (have >> 3) + tid; i < (slot >> 3); i += nth) d8[i] = ~0ull;
+      } else {
+        for (int64_t i = have + tid; i < slot; i += nth) d[i] = 0xFF;
+      }
+    }
+  }
+  depart(pt, epoch);
+}
+
+__global__ __launch_bounds__(256) void k_ipc_allreduce(IpcPeers pt, const float* __restrict__ src, float* out,
+                                                       int64_t n, float scale, int two_phase) {
+  __shared__ uint64_t s_epoch;
+  __shared__ int s_last, s_ok;
+  __shared__ int s_cnt[kIpcMaxRanks];
+  const int W = pt.world, me = pt.rank;
+  if (threadIdx.x == 0) s_epoch = __hip_atomic_load(pt.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __syncthreads();
+  const uint64_t epoch = s_epoch;
+  const int sl = (int)(epoch % (uint64_t)pt.depth);
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nth = (int64_t)gridDim.x * blockDim.x;
+  const float qnan = __int_as_float(0x7fc00000);
+  if (!two_phase) {
+    for (int p = 0; p < W; ++p)
+      put_bytes(slot_ptr(pt, p, sl, 0, me), reinterpret_cast<const unsigned char*>(src), n * 4, tid, nth);
+    signal(pt, epoch, 0, nullptr, &s_last);
+    const bool ok = wait_all(pt, epoch, 0, s_cnt, &s_ok);
+    for (int64_t i = tid; i < n; i += nth) {
+      float s = 0.f;
+      for (int p = 0; p < W; ++p) s += __builtin_nontemporal_load(reinterpret_cast<const float*>(slot_ptr(pt, me, sl, 0, p)) + i);
+      out[i] = ok ? s * scale : qnan;
+    }
+    depart(pt, epoch);
+    return;
+  }
+  // two-phase: chunk q (cs floats, 16-B multiple) is reduced by rank q
+  const int64_t cs = ((n + W - 1) / W + 3) / 4 * 4;
+  const int64_t mine0 = me * cs, mine1 = (me + 1) * cs < n ? (me + 1) * cs : n;
+  for (int p = 0; p < W; ++p) {
+    const int64_t a0 = p * cs, a1 = (p + 1) * cs < n ? (p + 1) * cs : n;
+    if (a1 > a0)
+      put_bytes(slot_ptr(pt, p, sl, 0, me), reinterpret_cast<const unsigned char*>(src + a0), (a1 - a0) * 4, tid,
+                nth);
+  }
+  signal(pt, epoch, 0, nullptr, &s_last);
+  bool ok = wait_all(pt, epoch, 0, s_cnt, &s_ok);
+  // reduce my chunk and push each reduced element to every peer's gather area
+  for (int64_t i = tid; i < mine1 - mine0; i += nth) {
+    float s = 0.f;
+    for (int p = 0; p < W; ++p) s += __builtin_nontemporal_load(reinterpret_cast<const float*>(slot_ptr(pt, me, sl, 0, p)) + i);
+    s = ok ? s * scale : qnan;
+    for (int p = 0; p < W; ++p) reinterpret_cast<float*>(slot_ptr(pt, p, sl, 1, me))[i] = s;
+  }
+  signal(pt, epoch, 1, nullptr, &s_last);
+  ok = wait_all(pt, epoch, 1, s_cnt, &s_ok) && ok;
+  for (int64_t i = tid; i < n; i += nth) {
+    const int q = (int)(i / cs);
+    const float v = __builtin_nontemporal_load(reinterpret_cast<const float*>(slot_ptr(pt, me, sl, 1, q)) + (i - q * cs));
+    out[i] = ok ? v : qnan;
+  }
+  depart(pt, epoch);
+}
+
 }  // namespace
 
-void launch_ipc_collective(const IpcPeers& pt, const void* send, int64_t nbytes, bool broadcast, float* out,
-                           int64_t nfloat, float scale, bool reduce, int blocks, hipStream_t s) {
-  hipLaunchKernelGGL(k_ipc_collective, dim3(blocks), dim3(256), 0, s, pt,
-                     reinterpret_cast<const unsigned char*>(send), nbytes, broadcast ? 1 : 0, out, nfloat, scale,
-                     reduce ? 1 : 0);
+void launch_ipc_exchange(const IpcPeers& pt, const void* send, void* dst, const int32_t* counts, int64_t rec_bytes,
+                         bool fill_tail, int32_t* rcounts, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(k_ipc_exchange, dim3(blocks), dim3(256), 0, s, pt, reinterpret_cast<const unsigned char*>(send),
+                     reinterpret_cast<unsigned char*>(dst), counts, rec_bytes, fill_tail ? 1 : 0, rcounts);
+}
+
+void launch_ipc_allreduce(const IpcPeers& pt, const float* src, float* out, int64_t n, float scale, bool two_phase,
+                          int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(k_ipc_allreduce, dim3(blocks), dim3(256), 0, s, pt, src, out, n, scale, two_phase ? 1 : 0);
 }
 
 }  // namespace pbx

@@ -181,20 +181,28 @@ void launch_zero_rows(float* buf, int stride, const int32_t* n_dev, int64_t cap,
 // graph-safe 32-bit fill (use instead of hipMemsetAsync in capturable code)
 void launch_fill32(void* p, uint32_t v, int64_t n_words, hipStream_t s);
 
-// IPC mesh collective (ipc.hip): peer pointers of one node's ranks
+// IPC mesh collectives (ipc.hip): peer pointers of one node's ranks
 constexpr int kIpcMaxRanks = 8;
 struct IpcPeers {
-  unsigned char* inbox[kIpcMaxRanks];  // each rank's inbox [2][world][slot_bytes]
-  uint64_t* flags[kIpcMaxRanks];       // each rank's flag words [world]
+  unsigned char* inbox[kIpcMaxRanks];  // each rank's inbox [depth][2][world][slot_bytes]
+  uint64_t* flags[kIpcMaxRanks];       // each rank's flag words [2][world] = epoch << 24 | count
   int64_t slot_bytes;
-  int world, rank;
+  int world, rank, depth;  // depth = inbox slots (a call uses slot epoch % depth)
+  int64_t spin_limit;    // s_sleep(2) polls before a wait gives up (sticky err)
   uint64_t* epoch;       // own, device
   unsigned int* arrive;  // own, device
   unsigned int* depart;  // own, device
-  int* err;              // own, device: 1 = a wait timed out
+  int* err;              // own, device: 1 = a wait timed out (sticky)
 };
-void launch_ipc_collective(const IpcPeers& pt, const void* send, int64_t nbytes, bool broadcast, float* out,
-                           int64_t nfloat, float scale, bool reduce, int blocks, hipStream_t s);
+// send / dst [world][slot_bytes]; counts (device [world], nullable = whole
+// slots) of rec_bytes records go to each peer; the received records land in
+// dst, rcounts (device [world], nullable) gets the received counts and
+// fill_tail writes 0xFF over the rest of each dst slot
+void launch_ipc_exchange(const IpcPeers& pt, const void* send, void* dst, const int32_t* counts, int64_t rec_bytes,
+                         bool fill_tail, int32_t* rcounts, int blocks, hipStream_t s);
+// out = scale * sum over ranks of src (n floats; out may alias src)
+void launch_ipc_allreduce(const IpcPeers& pt, const float* src, float* out, int64_t n, float scale, bool two_phase,
+                          int blocks, hipStream_t s);
 
 // device-resident pass (batch_ops.hip): the record store's CSR arrays + the
 // pass order on the GPU
@@ -490,6 +498,7 @@ struct TowerArgs {
   int debug = 0;  // timing experiments only (PBX_TOWER_DEBUG): 1 no loss reduction, 2 no dW reductions, 4 no dW GEMM
   // fp32 tower (f32 = 1): fp32 X0 row-major / MP32, fp32 dX0; widths padded to 16
   int f32 = 0;
+  long long* stamps = nullptr;  // timing experiments only: per-wave s_memtime stamps (fp32 fwd)
   const float* x0f = nullptr;
   const float* x0mpf = nullptr;
   float* dx0f = nullptr;

@@ -44,62 +44,73 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 
 // acc{0,1} += A{0,1}(16 rows x 16 KG, LDS) x B (packed fragments bfr[g * 64]).
 // A0/A1: this lane's row pointer (+4 * (lane / 16)); TWO = both 16-row halves.
-// Fragments are prefetched PF groups ahead; each workgroup starts at its own
-// group (rot) so the CUs of an XCD do not queue on the same L2 lines.
+// Software pipeline, unrolled by 4 k-groups with NAMED registers: the weight
+// fragments b0..b3 are each re-loaded right after the MFMAs that consumed
+// them (4 groups = 32 MFMAs ahead) and the A fragments alternate between two
+// register sets, so nothing is copied between registers at the loop edge (a
+// rotated ring made hipcc move registers and drain vmcnt(0) every 4 groups).
+// Addressing is pointer increments only: the loads run up to 8 groups past
+// the end (the packed weights carry 8 KB of slack, the LDS tile 64 floats),
+// so the loop needs no clamping or index arithmetic -- the first version's
+// per-group scalar index math (~20 SALU between MFMA clusters) cost ~40% of
+// the MFMA rate (timing experiments, profiles/r3_tower32_notes.txt).
 template <bool TWO>
 __device__ __forceinline__ void mma32(const float* __restrict__ A0, const float* __restrict__ A1,
-                                      const f32x4* __restrict__ bfr, int KG, int rot, f32x4& acc0, f32x4& acc1) {
-  rot = rot % KG;
-  const int flast = rot == 0 ? KG - 1 : rot - 1;
-  auto adv = [&](int f) { return f + 1 == KG ? 0 : f + 1; };
-  int fi = rot, fc = rot, issued = 0;
-  f32x4 q[PF];
+                                      const f32x4* __restrict__ bp, int KG, f32x4& acc0, f32x4& acc1) {
+  auto step = [&](const f32x4& a0, const f32x4& a1, const f32x4& b) {
 #pragma unroll
-  for (int p = 0; p < PF; ++p) {
-    q[p] = bfr[(int64_t)(issued < KG ? fi : flast) * 64];
-    fi = adv(fi);
-    ++issued;
-  }
-  f32x4 a0 = *reinterpret_cast<const f32x4*>(A0 + 16 * fc);
-  f32x4 a1 = TWO ? *reinterpret_cast<const f32x4*>(A1 + 16 * fc) : a0;
-  const int KM = KG - KG % PF;
-  for (int k0 = 0; k0 < KM; k0 += PF) {
-#pragma unroll
-    for (int p = 0; p < PF; ++p) {
-      fc = adv(fc);
-      const int fn = (k0 + p + 1 < KG) ? fc : flast;
-      const f32x4 n0 = *reinterpret_cast<const f32x4*>(A0 + 16 * fn);
-      const f32x4 n1 = TWO ? *reinterpret_cast<const f32x4*>(A1 + 16 * fn) : n0;
-      const f32x4 b = q[p];
-      q[p] = bfr[(int64_t)(issued < KG ? fi : flast) * 64];
-      fi = adv(fi);
-      ++issued;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        acc0 = mfma4(a0[t], b[t], acc0);
-        if (TWO) acc1 = mfma4(a1[t], b[t], acc1);
-      }
-      a0 = n0;
-      a1 = n1;
+    for (int t = 0; t < 4; ++t) {
+      acc0 = mfma4(a0[t], b[t], acc0);
+      if (TWO) acc1 = mfma4(a1[t], b[t], acc1);
     }
+  };
+  auto lda = [](const float* p, int g) { return *reinterpret_cast<const f32x4*>(p + 16 * g); };
+  f32x4 b0 = bp[0], b1 = bp[64], b2 = bp[128], b3 = bp[192];
+  f32x4 e0 = lda(A0, 0), e1 = TWO ? lda(A1, 0) : e0;  // A of even groups
+  f32x4 o0, o1;                                       // A of odd groups
+  const int KM = KG & ~3;
+  for (int k = 0; k < KM; k += 4) {
+    o0 = lda(A0, 1);
+    if (TWO) o1 = lda(A1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    step(e0, e1, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    b0 = bp[256];
+    e0 = lda(A0, 2);
+    if (TWO) e1 = lda(A1, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    step(o0, o1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    b1 = bp[320];
+    o0 = lda(A0, 3);
+    if (TWO) o1 = lda(A1, 3);
+    __builtin_amdgcn_sched_barrier(0);
+    step(e0, e1, b2);
+    __builtin_amdgcn_sched_barrier(0);
+    b2 = bp[384];
+    e0 = lda(A0, 4);
+    if (TWO) e1 = lda(A1, 4);
+    __builtin_amdgcn_sched_barrier(0);
+    step(o0, o1, b3);
+    __builtin_amdgcn_sched_barrier(0);
+    b3 = bp[448];
+    bp += 256;
+    A0 += 64;
+    if (TWO) A1 += 64;
   }
-#pragma unroll
-  for (int p = 0; p < PF; ++p) {  // tail: KG % PF groups already in the ring
-    if (KM + p < KG) {
-      fc = adv(fc);
-      const int fn = (KM + p + 1 < KG) ? fc : flast;
-      const f32x4 n0 = *reinterpret_cast<const f32x4*>(A0 + 16 * fn);
-      const f32x4 n1 = TWO ? *reinterpret_cast<const f32x4*>(A1 + 16 * fn) : n0;
-      const f32x4 b = q[p];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        acc0 = mfma4(a0[t], b[t], acc0);
-        if (TWO) acc1 = mfma4(a1[t], b[t], acc1);
-      }
-      a0 = n0;
-      a1 = n1;
-    }
+  // tail: KG % 4 groups, their fragments already loaded (b0.., e)
+  const int rem = KG - KM;
+  if (rem > 0) {
+    o0 = lda(A0, 1);
+    if (TWO) o1 = lda(A1, 1);
+    step(e0, e1, b0);
   }
+  if (rem > 1) {
+    e0 = lda(A0, 2);
+    if (TWO) e1 = lda(A1, 2);
+    step(o0, o1, b1);
+  }
+  if (rem > 2) step(e0, e1, b2);
 }
 
 // Work split of one layer over the 8 waves: NB column blocks, each a "pair"
@@ -113,20 +124,25 @@ __device__ __forceinline__ void for_units(int NB, int w, F&& f) {
   for (int j = w; j < 2 * r; j += NW) f(NW * q + (j >> 1), j & 1);
 }
 
-template <typename Epi>
+// One unit: the epilogue's own global operands (bias, ReLU mask) are fetched
+// by pre(nb, half) BEFORE the MFMA chain, so their latency hides under it
+// instead of stalling the epilogue of both waves of a SIMD at once.
+template <typename Pre, typename Epi>
 __device__ __forceinline__ void run_unit(const float* src, int ldl, const f32x4* wbase, int KG, int nb, int half,
-                                         int lane, int rot, Epi&& epi) {
+                                         int lane, Pre&& pre, Epi&& epi) {
   const int c = lane & 15, g = lane >> 4;
   const f32x4* bfr = wbase + (int64_t)nb * KG * 64 + lane;
   f32x4 acc0 = (f32x4){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
   if (half < 0) {
-    mma32<true>(src + c * ldl + 4 * g, src + (16 + c) * ldl + 4 * g, bfr, KG, rot, acc0, acc1);
-    epi(acc0, nb, 0);
-    epi(acc1, nb, 1);
+    const f32x4 p0 = pre(nb, 0), p1 = pre(nb, 1);
+    mma32<true>(src + c * ldl + 4 * g, src + (16 + c) * ldl + 4 * g, bfr, KG, acc0, acc1);
+    epi(acc0, nb, 0, p0);
+    epi(acc1, nb, 1, p1);
   } else {
+    const f32x4 p0 = pre(nb, half);
     const float* A = src + (16 * half + c) * ldl + 4 * g;
-    mma32<false>(A, A, bfr, KG, rot, acc0, acc1);
-    epi(acc0, nb, half);
+    mma32<false>(A, A, bfr, KG, acc0, acc1);
+    epi(acc0, nb, half, p0);
   }
 }
 
@@ -137,6 +153,11 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
   const int m0 = blockIdx.x * BM;
   float* src = lds32;
   float* dst = lds32 + BM * ldl;
+  // waves 4-7 share SIMDs with 0-3 and lose every arbitration at equal
+  // priority (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+  long long* stp = a.stamps ? a.stamps + ((int64_t)blockIdx.x * NW + w) * 8 : nullptr;
+  if (stp && lane == 0) stp[0] = __builtin_amdgcn_s_memtime();
   {  // stage the X0 tile (zero rows past M)
     const int c4n = a.ly[0].Kp / 4;
     for (int i = tid; i < BM * c4n; i += NT) {
@@ -147,16 +168,18 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
     }
   }
   __syncthreads();
-  const int rot = (int)blockIdx.x * 5;
   for (int l = 0; l < a.L; ++l) {
     const TowerLayerDev& ly = a.ly[l];
     const int NB = ly.Np / 16, KG = ly.Kp / 16;
     const f32x4* wp = reinterpret_cast<const f32x4*>(ly.wpf);
     const int c = lane & 15, g = lane >> 4;
     for_units(NB, w, [&](int nb, int half) {
-      run_unit(src, ldl, wp, KG, nb, half, lane, rot, [&](const f32x4& acc, int nbb, int mb) {
+      run_unit(src, ldl, wp, KG, nb, half, lane, [&](int nbb, int) {
         const int n = nbb * 16 + c;
-        const float bias = n < ly.N ? ly.bias[n] : 0.f;
+        return (f32x4){n < ly.N ? ly.bias[n] : 0.f, 0.f, 0.f, 0.f};
+      }, [&](const f32x4& acc, int nbb, int mb, const f32x4& pb) {
+        const int n = nbb * 16 + c;
+        const float bias = pb[0];
         f32x4 o;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -167,7 +190,9 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
         *reinterpret_cast<f32x4*>(ly.xmpf + mp32(m0 / 16 + mb, NB, nbb) + lane * 4) = o;
       });
     });
+    if (stp && lane == 0) stp[1 + 2 * l] = __builtin_amdgcn_s_memtime();
     __syncthreads();
+    if (stp && lane == 0) stp[2 + 2 * l] = __builtin_amdgcn_s_memtime();
     float* t = src;
     src = dst;
     dst = t;
@@ -206,6 +231,7 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
       }
     }
   }
+  if (stp && lane == 0) stp[7] = __builtin_amdgcn_s_memtime();
   if (lane == 0) {
     red[w][0] = sl;
     red[w][1] = s_ae;
@@ -263,6 +289,7 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
   float* src = lds32;
   float* dst = lds32 + BM * ldl;
   float* bp = a.bias_part + (int64_t)blockIdx.x * a.bias_ld;
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
   const float gl = a.dloss ? a.dloss[0] : 1.f;
   if (tid < BM) gs[tid] = (m0 + tid < a.M) ? a.dz[m0 + tid] * gl : 0.f;
   __syncthreads();
@@ -313,7 +340,6 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
     }
     __syncthreads();
   }
-  const int rot = (int)blockIdx.x * 5;
   // dX_i = dZ_{i+1} W_i  (i = L-1 .. 0); dZ_i = dX_i . relu'(X_i) for i >= 1
   for (int i = a.L - 1; i >= 0; --i) {
     if (i == 0 && !a.need_dx0) break;
@@ -325,9 +351,10 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
       const TowerLayerDev& prev = a.ly[i - 1];
       const int PNB = prev.Np / 16;
       for_units(KB, w, [&](int kb, int half) {
-        run_unit(src, ldl, wtp, NG, kb, half, lane, rot, [&](const f32x4& acc, int kbb, int mb) {
+        run_unit(src, ldl, wtp, NG, kb, half, lane, [&](int kbb, int mb) {
+          return *reinterpret_cast<const f32x4*>(prev.xmpf + mp32(m0 / 16 + mb, PNB, kbb) + lane * 4);
+        }, [&](const f32x4& acc, int kbb, int mb, const f32x4& x4) {
           const int64_t off = mp32(m0 / 16 + mb, PNB, kbb) + lane * 4;
-          const f32x4 x4 = *reinterpret_cast<const f32x4*>(prev.xmpf + off);
           f32x4 o;
           float s = 0.f;
 #pragma unroll
@@ -344,7 +371,8 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
       });
     } else {
       for_units(KB, w, [&](int kb, int half) {
-        run_unit(src, ldl, wtp, NG, kb, half, lane, rot, [&](const f32x4& acc, int kbb, int mb) {
+        run_unit(src, ldl, wtp, NG, kb, half, lane, [&](int, int) { return (f32x4){0.f, 0.f, 0.f, 0.f}; },
+                 [&](const f32x4& acc, int kbb, int mb, const f32x4&) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) dst[(16 * mb + 4 * g + t) * ldl + kbb * 16 + c] = acc[t];
         });
@@ -548,7 +576,8 @@ int tower32_lds_ld(int maxw) {
   return (maxw + 3) / 4 * 4;
 }
 
-size_t tower32_lds_bytes(const TowerArgs& a) { return (size_t)2 * BM * a.lds_ld * sizeof(float); }
+// + 64 floats: the A-operand loads run up to 4 k-groups past a row's end
+size_t tower32_lds_bytes(const TowerArgs& a) { return ((size_t)2 * BM * a.lds_ld + 64) * sizeof(float); }
 
 static void allow_big_lds32() {
   static const bool once = [] {

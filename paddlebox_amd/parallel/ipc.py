@@ -2,24 +2,30 @@
 (``csrc/hip/ipc.hip``): peer-to-peer writes over xGMI into IPC-mapped inboxes,
 one kernel per collective, no host synchronisation, graph-capturable.
 
-* ``allreduce_(t)`` -- one-shot all-reduce: every rank writes its whole
-  buffer into every peer's inbox and sums the W copies locally.  For the
-  ~2 MB dense arena this is one xGMI hop (7 links in parallel on MI355X)
-  instead of a 2(W-1)-step ring, which is latency-bound at that size.
-* ``exchange(send)`` -- all-to-all of fixed-size slots (the key / value
-  exchange of the sharded sparse step with per-peer capacity): slot p of
-  ``send`` lands in peer p's inbox; returns this rank's inbox view
-  ``[world, slot_bytes]`` (valid until the second-next collective).
+* ``allreduce_(t)`` -- one-shot all-reduce (every rank writes its whole
+  buffer into every peer's inbox and sums the W copies: one xGMI hop, for
+  latency-bound sizes) or two-phase (reduce-scatter + all-gather: each rank
+  moves 2(W-1)/W of the buffer over its 7 links in parallel instead of W-1
+  copies; the default above 256 KB).
+* ``exchange(send, dst, counts=...)`` -- all-to-all of per-peer record slots
+  (the key / value / gradient exchange of the sharded sparse step): only
+  ``counts[p]`` records of slot p travel, the receiver copies them into
+  ``dst``, gets the counts in ``rcounts`` and, with ``fill_tail``, -1 keys
+  past them.  The inbox slot is consumed inside the launch, so nothing the
+  caller does between collectives can race a peer's next write.
 
 Reference: the c_mixallgather / heter_comm peer copies
 (``c_mixallgather_op.cc:221-327``, ``heter_comm_inl.h:273-490``); here the
 memory handles are exchanged once over the process group and every later
 call is a single kernel.  Every rank must issue the same sequence of
-collectives (as with RCCL).  A peer that never arrives makes the wait time
-out (``error()`` turns true) instead of hanging the GPU.
+collectives on a mesh (as with RCCL).  A peer that never arrives makes the
+wait time out: the sticky error poisons the results (NaN sums, empty
+exchanges) and :meth:`check` raises on the host, instead of hanging the GPU
+or training on stale slots.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -27,9 +33,18 @@ import torch.distributed as dist
 
 from .. import _native
 
+# s_sleep(2) polls (~55 ns each) before a wait gives up: ~3.7 s by default, so
+# a peer that is seconds late at a pass boundary does not trip it
+DEFAULT_SPIN_LIMIT = int(os.environ.get("PBX_IPC_SPIN_LIMIT", str(1 << 26)))
+
+
+class IpcMeshError(RuntimeError):
+    pass
+
 
 class IpcMesh:
-    def __init__(self, slot_bytes: int, group=None, device=None, blocks: int = 32):
+    def __init__(self, slot_bytes: int, group=None, device=None, blocks: int = 32, depth: int = 2,
+                 spin_limit: Optional[int] = None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -37,50 +52,120 @@ class IpcMesh:
             raise ValueError("IpcMesh spans the GPUs of one node (<= 8 ranks)")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.slot_bytes = (int(slot_bytes) + 15) // 16 * 16
+        self.depth = int(depth)
         h = _native.hip()
         W = self.world
-        self.inbox = torch.zeros(2 * W * self.slot_bytes, dtype=torch.uint8, device=self.device)
-        self.flags = torch.zeros(W, dtype=torch.int64, device=self.device)
+        self.inbox = torch.zeros(self.depth * 2 * W * self.slot_bytes, dtype=torch.uint8, device=self.device)
+        self.flags = torch.zeros(2 * W, dtype=torch.int64, device=self.device)
         self.state = torch.zeros(4, dtype=torch.int64, device=self.device)
-        self.comm = h.IpcComm(self.rank, W, self.slot_bytes, self.state, int(blocks))
-        mine = (h.ipc_handle(self.inbox), h.ipc_handle(self.flags))
+        self.comm = h.IpcComm(self.rank, W, self.slot_bytes, self.state, int(blocks), self.depth,
+                              int(spin_limit or DEFAULT_SPIN_LIMIT))
+        self._opened = []
+        # no rank may raise between the collectives below (a peer would block
+        # in them forever): failures are recorded and agreed on at the end
+        err = None
+        try:
+            mine = (h.ipc_handle(self.inbox), h.ipc_handle(self.flags))
+        except Exception as e:  # pragma: no cover - depends on the driver
+            mine, err = None, f"export: {e!r}"
         allh = [None] * W
         if W > 1:
             dist.all_gather_object(allh, mine, group=group)
         else:
             allh = [mine]
-        self._opened = []
         for p in range(W):
+            if err is not None:
+                break
             if p == self.rank:
                 self.comm.set_peer(p, self.inbox.data_ptr(), self.flags.data_ptr())
                 continue
-            (ih, io), (fh, fo) = allh[p]
-            ip = h.ipc_open(ih, io)
-            fp = h.ipc_open(fh, fo)
-            self._opened += [ip - io, fp - fo]
-            self.comm.set_peer(p, ip, fp)
+            if allh[p] is None:
+                err = f"rank {p} could not export its inbox"
+                break
+            try:
+                (ih, io), (fh, fo) = allh[p]
+                ip = h.ipc_open(ih, io)
+                self._opened.append(ip - io)
+                fp = h.ipc_open(fh, fo)
+                self._opened.append(fp - fo)
+                self.comm.set_peer(p, ip, fp)
+            except Exception as e:  # pragma: no cover - depends on the driver
+                err = f"open peer {p}: {e!r}"
         torch.cuda.synchronize(self.device)
         if W > 1:
-            dist.barrier(group=group)
-        self._calls = 0
+            bad = self._all_min(0 if err else 1) == 0
+        else:
+            bad = err is not None
+        if bad:
+            self.close()
+            raise IpcMeshError(f"IPC mesh setup failed on some rank (this rank: {err or 'ok'})")
 
-    def allreduce_(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
+    def _all_min(self, v: int) -> int:
+        t = torch.tensor([int(v)], dtype=torch.int32)
+        if dist.get_backend(self.group) == "nccl":
+            t = t.to(self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return int(t.item())
+
+    def allreduce_(self, t: torch.Tensor, average: bool = False, two_phase: Optional[bool] = None) -> torch.Tensor:
         """In-place sum (or mean) over the ranks of a contiguous f32 tensor."""
-        self.comm.allreduce(t, t, 1.0 / self.world if average else 1.0)
-        self._calls += 1
+        if two_phase is None:
+            two_phase = self.world > 2 and t.numel() * 4 > (256 << 10)
+        self.comm.allreduce(t, t, 1.0 / self.world if average else 1.0, bool(two_phase))
         return t
 
-    def exchange(self, send: torch.Tensor) -> torch.Tensor:
-        """send: [world, slot_bytes] (any dtype, contiguous); returns the
-        received slots as a uint8 view [world, slot_bytes] of the inbox."""
-        self.comm.exchange(send)
-        self._calls += 1
-        par = self._calls & 1  # epoch e = calls, parity e & 1
-        W, sb = self.world, self.slot_bytes
-        return self.inbox[par * W * sb:(par + 1) * W * sb].view(W, sb)
+    def exchange(self, send: torch.Tensor, dst: Optional[torch.Tensor] = None, counts: Optional[torch.Tensor] = None,
+                 rec_bytes: int = 16, fill_tail: bool = False, rcounts: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """send / dst: [world, slot_bytes] bytes (any dtype, contiguous).  Slot
+        p of send goes to peer p (its first counts[p] records of rec_bytes,
+        or the whole slot); dst receives slot q from peer q.  Returns dst."""
+        if dst is None:
+            dst = torch.empty_like(send)
+        self.comm.exchange(send, dst, counts, int(rec_bytes), bool(fill_tail), rcounts)
+        return dst
 
     def error(self) -> bool:
+        """True once any wait on this mesh timed out (device read: syncs)."""
         return bool(int(self.state[2].item()) != 0)
+
+    def check(self):
+        """Raise if a collective on this mesh failed (call outside the hot
+        loop: at pass ends, checkpoints and the end of a benchmark)."""
+        if self.world > 1 and self.error():
+            raise IpcMeshError(f"IPC mesh rank {self.rank}: a peer did not arrive within the spin bound; "
+                               "results since then are poisoned (NaN / empty)")
+
+    def self_test(self, agree: bool = True) -> bool:
+        """Exchange known patterns with every peer (both phases, several
+        slots) and verify them on the host.  agree=True all-reduces the
+        verdict over the process group, so every rank takes the same
+        fallback decision."""
+        W, sb = self.world, self.slot_bytes
+        ok = True
+        n = min(sb // 8, 4096)
+        for it in range(2 * self.depth):
+            send = torch.full((W, sb // 8), -7, dtype=torch.int64, device=self.device)
+            cnt = torch.empty(W, dtype=torch.int32, device=self.device)
+            for p in range(W):
+                c = max(1, (n * (p + 1 + it)) // (W + 2 * self.depth))
+                cnt[p] = c
+                send[p, :c] = (self.rank << 40) + (p << 32) + it * 1000 + torch.arange(c, device=self.device)
+            rc = torch.zeros(W, dtype=torch.int32, device=self.device)
+            recv = self.exchange(send, None, cnt, 8, True, rc).view(torch.int64).view(W, sb // 8)
+            torch.cuda.synchronize(self.device)
+            for src in range(W):
+                c = max(1, (n * (self.rank + 1 + it)) // (W + 2 * self.depth))
+                want = (src << 40) + (self.rank << 32) + it * 1000 + torch.arange(c, device=self.device)
+                ok &= int(rc[src]) == c and bool((recv[src, :c] == want).all()) and bool((recv[src, c:] == -1).all())
+            na = max(4, min(1000, sb // 4))
+            t = torch.arange(na, dtype=torch.float32, device=self.device) + self.rank
+            self.allreduce_(t, two_phase=bool(it & 1))
+            want = torch.arange(na, dtype=torch.float32, device=self.device) * W + W * (W - 1) / 2
+            ok &= bool(torch.allclose(t, want))
+        ok &= not self.error()
+        if agree and W > 1:
+            ok = self._all_min(1 if ok else 0) == 1
+        return ok
 
     def close(self):
         h = _native.hip()

@@ -22,6 +22,7 @@ MI355X design points
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -29,7 +30,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
-from ..parallel.comm import Comm, default_comm
+from ..parallel.comm import Comm, TorchDistComm, default_comm
 from ..ops import reference as ref
 from .config import PSConfig, SparseSGDConfig, padded, pull_width, push_width
 from .cpu_table import CpuSparseTable
@@ -81,6 +82,7 @@ class _PullSlot:
             self.recv = torch.empty(n, dtype=torch.int64, device=dev)
             self.send_index = torch.empty(eng.max_keys, dtype=torch.int64, device=dev)
             self.ocnt = torch.zeros(eng.world, dtype=torch.int32, device=dev)
+            self.rcnt = torch.zeros(eng.world, dtype=torch.int32, device=dev)  # keys received per peer (IPC)
             self.resp = torch.empty(n, eng.P, device=dev)
             self.resp_back = torch.empty(n, eng.P, device=dev)
             self.rows_r = None
@@ -144,7 +146,12 @@ class SparseEngine:
         comm: Optional[Comm] = None,
         pull_ring: int = 2,
         exchange_capacity: Optional[int] = None,
+        exchange: Optional[str] = None,
     ):
+        """``exchange`` (sharded GPU engines): "ipc" = the in-house xGMI peer-
+        write mesh (parallel/ipc.py; default, self-tested at construction with
+        a fallback to RCCL), "rccl" = torch.distributed all_to_all_single.
+        PBX_SPARSE_EXCHANGE overrides the default."""
         self.cfg = cfg
         self.dim = cfg.embedx_dim
         self.E = pull_width(self.dim)
@@ -162,6 +169,8 @@ class SparseEngine:
         self.auto_insert = auto_insert
         self.test_mode = False
         self.is_gpu = self.device.type == "cuda"
+        self.xmesh = None  # IPC meshes of the sharded exchange (GPU, see _setup_exchange)
+        self.exchange_mode = "rccl" if self.sharded else "none"
         shard_cap = int(math.ceil(capacity / self.world)) if self.world > 1 else capacity
         # non-default feature types (int16 embedx, expand block, SparseAdam):
         # rows go through the codec kernels (ps/feature_types.py)
@@ -186,6 +195,8 @@ class SparseEngine:
                     self.C = (int(exchange_capacity) + 63) // 64 * 64
                 else:
                     self.C = int(math.ceil(self.max_keys / self.world * cap_factor)) + 64
+            if self.sharded:
+                self._setup_exchange(exchange or os.environ.get("PBX_SPARSE_EXCHANGE", "ipc"))
             # ring of per-pull buffers (sort-free hash dedup everywhere: the
             # sender packs its unique keys per owner with a counting pass)
             self._slots = [_PullSlot(self) for _ in range(max(1, int(pull_ring)))]
@@ -213,6 +224,44 @@ class SparseEngine:
         self._seed = 1234
 
     # ------------------------------------------------------------------ build
+    def _setup_exchange(self, mode: str):
+        """Sparse key / value / gradient exchange transport.  "ipc": three
+        IPC meshes (one per record kind, so each received view is a contiguous
+        [world * C] array) moving only the valid records of each peer slot;
+        self-tested on every rank, all ranks fall back to RCCL together if any
+        rank's test fails (e.g. no peer access between the GPUs)."""
+        self.exchange_mode = "rccl"
+        if mode != "ipc" or not isinstance(self.comm, TorchDistComm) or self.world > 8:
+            return
+        from ..parallel.ipc import IpcMesh, IpcMeshError
+
+        meshes = []
+        try:
+            for rec in (8, self.P * 4, self.Q * 4):
+                meshes.append(IpcMesh(self.C * rec, group=self.group, device=self.device))
+        except IpcMeshError as e:
+            for m in meshes:
+                m.close()
+            print(f"[sparse] IPC exchange unavailable ({e}); using RCCL all_to_all", flush=True)
+            return
+        ok = True
+        for m in meshes:
+            ok = m.self_test(agree=True) and ok
+        if not ok:
+            for m in meshes:
+                m.close()
+            print("[sparse] IPC exchange self-test failed on some rank; using RCCL all_to_all", flush=True)
+            return
+        self.xmesh = meshes
+        self.exchange_mode = "ipc"
+        dev = self.device
+        self._rcnt = torch.zeros(self.world, dtype=torch.int32, device=dev)
+
+    def check_exchange(self):
+        """Raise if an IPC exchange timed out (outside the hot loop)."""
+        for m in self.xmesh or ():
+            m.check()
+
     def is_gpu_device(self) -> bool:
         return self.device.type == "cuda"
 
@@ -349,7 +398,13 @@ class SparseEngine:
             return st
         # sharded: pack per-owner, exchange keys, owner-side dedup/probe/gather
         h.shard_pack_hash(ws.uniq_h, ws.u_count, self.world, self.C, sl.send, sl.send_index, sl.ocnt, self.overflow)
-        self.comm.all_to_all_single(sl.recv, sl.send)
+        if self.xmesh is not None:
+            # only the valid keys of each peer slot travel; the receiver
+            # fills the rest of its slots with -1 (padding for the dedup)
+            self.xmesh[0].exchange(sl.send.view(self.world, -1), sl.recv.view(self.world, -1), sl.ocnt, 8, True,
+                                   sl.rcnt)
+        else:
+            self.comm.all_to_all_single(sl.recv, sl.send)
         sl.ws_r.run(sl.recv, True)
         rows_r = self.table.probe(sl.ws_r.uniq_h, sl.ws_r.u_count)
         if self.auto_insert and not self.test_mode:
@@ -363,7 +418,12 @@ class SparseEngine:
             self.table.t.codec_pull(self.codec.native(), rows_r, sl.ws_r.uid, None, sl.resp.shape[0], sl.resp)
         else:
             self.table.t.gather_rows_by_uid(rows_r, sl.ws_r.uid, sl.resp)
-        self.comm.all_to_all_single(sl.resp_back, sl.resp)
+        if self.xmesh is not None:
+            # answers: as many rows to each peer as it sent keys
+            self.xmesh[1].exchange(sl.resp.view(self.world, -1), sl.resp_back.view(self.world, -1), sl.rcnt,
+                                   self.P * 4, False, None)
+        else:
+            self.comm.all_to_all_single(sl.resp_back, sl.resp)
         st.send_index = sl.send_index[:L]
         st.rows_r = rows_r
         return st
@@ -412,8 +472,17 @@ class SparseEngine:
         h.push_merge(dout, col_offset, cvm.contiguous(), sp.cvm_offset, sp.use_cvm, sp.clk_filter, self.E,
                      ws.perm[:L], ws.uid, sl.occ_slot, sl.occ_ins, self._slot_ids(st.S),
                      ws.u_count[1:], self.push_send, st.send_index, float(bs_scale), self.dim, ets)
-        self.comm.all_to_all_single(self.push_recv, self.push_send)
-        self._owner_update(sl, st.rows_r, self.push_recv)
+        self._owner_update(sl, st.rows_r, self._push_exchange(sl))
+
+    def _push_exchange(self, sl: _PullSlot) -> torch.Tensor:
+        """Merged gradient records to the key owners (same per-peer counts as
+        the keys of this pull)."""
+        if self.xmesh is not None:
+            self.xmesh[2].exchange(self.push_send.view(self.world, -1), self.push_recv.view(self.world, -1), sl.ocnt,
+                                   self.Q * 4, False, None)
+        else:
+            self.comm.all_to_all_single(self.push_recv, self.push_send)
+        return self.push_recv
 
     def _owner_update(self, sl: _PullSlot, rows_r: torch.Tensor, recv: torch.Tensor):
         """Owner side of the push: each unique key got at most one merged record
@@ -441,6 +510,7 @@ class SparseEngine:
         return self.slot_ids
 
     def check_overflow(self) -> bool:
+        self.check_exchange()
         if self.sharded and self.is_gpu:
             return bool(self.overflow.item())
         return False
@@ -521,8 +591,7 @@ class SparseEngine:
         idx = st.send_index
         ok = idx >= 0
         self.push_send[idx[ok]] = merged[ok]
-        self.comm.all_to_all_single(self.push_recv, self.push_send)
-        self._owner_update(sl, st.rows_r, self.push_recv)
+        self._owner_update(sl, st.rows_r, self._push_exchange(sl))
 
     # ------------------------------------------------------------------ CPU path
     def _cpu_pull_seqpool(self, keys, lod, B, S, out, col_offset, sp: SeqpoolParams) -> PullState:

@@ -88,3 +88,54 @@ def test_ipc_mesh_allreduce_and_exchange_two_processes():
         assert not isinstance(errs, str), errs
         assert not err_flag, f"rank {rank}: a wait timed out"
         assert max(errs) == 0.0, (rank, errs)
+
+
+def _timeout_worker(rank, world, port, q):
+    try:
+        import torch.distributed as dist
+
+        from paddlebox_amd.parallel.ipc import IpcMesh, IpcMeshError
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        mesh = IpcMesh(4096, device=dev, blocks=4, spin_limit=1 << 14)  # ~1 ms bound
+        t = torch.ones(256, device=dev)
+        mesh.allreduce_(t)  # both ranks: fine
+        torch.cuda.synchronize(dev)
+        ok_first = bool(torch.all(t == world)) and not mesh.error()
+        if rank == 0:  # rank 1 never joins this one: rank 0 must time out, not hang
+            mesh.allreduce_(t)
+            torch.cuda.synchronize(dev)
+        dist.barrier()
+        poisoned = bool(torch.isnan(t).all()) if rank == 0 else True
+        raised = False
+        try:
+            mesh.check()
+        except IpcMeshError:
+            raised = True
+        q.put((rank, ok_first, poisoned, raised))
+        mesh.close()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), False, False))
+
+
+def test_ipc_mesh_lost_peer_times_out_and_poisons():
+    """a wait that gives up must not let training continue on a
+    stale slot: the sum is NaN, the error is sticky and check() raises."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, _free_port()
+    ps = [ctx.Process(target=_timeout_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = dict((o[0], o[1:]) for o in (q.get(timeout=180) for _ in range(world)))
+    for p in ps:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert out[0][0] is True and out[1][0] is True, out
+    assert out[0][1] and out[0][2], out  # rank 0: NaN result, check() raised
+    assert out[1][2] is False, out       # rank 1 saw no failure of its own
