@@ -452,14 +452,17 @@ def main():
         }
         print(json.dumps(out), flush=True)
     if multi:
-        # the captured graphs hold RCCL work: tearing the communicator down
-        # under them can block, so leave the process without it once every
-        # rank is done (output is flushed above)
         dist.barrier()
         torch.cuda.synchronize()
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        if ipc is None or engine.exchange_mode != "ipc":
+            # the captured graphs hold RCCL work: tearing the communicator
+            # down under them can block, so leave the process without it once
+            # every rank is done (output is flushed above)
+            os._exit(0)
+        # no RCCL in the step (IPC meshes): a normal exit, so profilers flush
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -315,12 +315,18 @@ struct DedupWorkspace {
     temp = torch::empty({(int64_t)temp_bytes}, torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, device));
   }
   // keys: int64 tensor (n <= cap).  Results live in this workspace.
-  void run(const Tensor& keys, bool mixed) {
+  // zero (optional, hash mode): int32 counters zeroed by the first launch
+  void run(const Tensor& keys, bool mixed, const c10::optional<Tensor>& zero) {
     check_cuda(keys, "keys");
     const int64_t n = keys.numel();
     PBX_CHECK(n <= cap, "dedup: more keys than workspace capacity");
     if (hash) {
       HashDedupArgs a;
+      if (zero.has_value() && zero->defined()) {
+        PBX_CHECK(zero->is_cuda() && zero->scalar_type() == torch::kInt32 && zero->numel() <= 256, "dedup zero");
+        a.zero_extra = ptr<int32_t>(*zero);
+        a.zero_n = (int)zero->numel();
+      }
       a.keys = ptr<uint64_t>(keys);
       a.n = n; a.cap = cap; a.mixed = mixed ? 1 : 0;
       a.tk = ptr<uint64_t>(tk); a.tu = ptr<int32_t>(tu); a.tmask = tmask;
@@ -461,8 +467,10 @@ static void shard_pack(const Tensor& uniq_h, const Tensor& u_count, int nranks, 
                     ptr<uint64_t>(send), ptr<int64_t>(send_index), ptr<int32_t>(overflow), cur_stream());
 }
 
+// prezeroed: ocnt was zeroed by an earlier launch (the dedup's) and the send
+// slots' tails need no -1 fill (the IPC exchange fills them at the receiver)
 static void shard_pack_hash(const Tensor& uniq_h, const Tensor& u_count, int nranks, int64_t cap, Tensor send,
-                            Tensor send_index, Tensor ocnt, Tensor overflow) {
+                            Tensor send_index, Tensor ocnt, Tensor overflow, bool prezeroed) {
   check_cuda(uniq_h, "uniq_h");
   check_cuda(send, "send");
   PBX_CHECK(send.numel() == nranks * cap, "send shape");
@@ -471,7 +479,7 @@ static void shard_pack_hash(const Tensor& uniq_h, const Tensor& u_count, int nra
   PBX_CHECK(send_index.numel() >= uniq_h.numel(), "send_index too short");
   launch_shard_pack_hash(ptr<uint64_t>(uniq_h), ptr<int32_t>(u_count), uniq_h.numel(), nranks, cap,
                          ptr<uint64_t>(send), ptr<int64_t>(send_index), ptr<int32_t>(ocnt), ptr<int32_t>(overflow),
-                         cur_stream());
+                         prezeroed, cur_stream());
 }
 
 static void gather_by_uid(const Tensor& src, const Tensor& uid, Tensor out, int width) {
@@ -1005,7 +1013,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("nbuckets", &GpuTable::nbuckets);
   py::class_<DedupWorkspace>(m, "DedupWorkspace")
       .def(py::init<int64_t, int, bool>(), py::arg("cap"), py::arg("device"), py::arg("hash") = true)
-      .def("run", &DedupWorkspace::run, py::arg("keys"), py::arg("mixed") = false)
+      .def("run", &DedupWorkspace::run, py::arg("keys"), py::arg("mixed") = false, py::arg("zero") = py::none())
       .def_readonly("hash", &DedupWorkspace::hash)
       .def_readonly("cap", &DedupWorkspace::cap)
       .def_readonly("h_sorted", &DedupWorkspace::h_sorted)
@@ -1039,7 +1047,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bs_scale"), py::arg("dim"), py::arg("embed_thres_size") = 0);
   m.def("push_merge_records", &push_merge_records);
   m.def("shard_pack", &shard_pack);
-  m.def("shard_pack_hash", &shard_pack_hash);
+  m.def("shard_pack_hash", &shard_pack_hash, py::arg("uniq_h"), py::arg("u_count"), py::arg("nranks"), py::arg("cap"),
+        py::arg("send"), py::arg("send_index"), py::arg("ocnt"), py::arg("overflow"), py::arg("prezeroed") = false);
   m.def("gather_by_uid", &gather_by_uid);
   m.def("data_norm_fwd", &data_norm_fwd);
   m.def("data_norm_bwd", &data_norm_bwd);

@@ -96,7 +96,8 @@ constexpr int kRankItems = 4;      // occurrences per thread in k_hash_rank
 constexpr int kRankLds = 2048;     // LDS hash entries per block (load <= 0.5)
 constexpr int kSegItems = 4;       // unique ids per thread in k_seg_alloc
 
-__global__ void k_hash_cleanup(int32_t* __restrict__ u_count, int32_t* __restrict__ cnt, int64_t cap) {
+__global__ void k_hash_cleanup(int32_t* __restrict__ u_count, int32_t* __restrict__ cnt, int64_t cap,
+                               int32_t* __restrict__ zero_extra, int zero_n) {
   // the previous run's scatter kernel saved its U into [2], so [0], [1] and
   // the cursor [3] can be reset here; its table slots were already released
   // by its k_seg_alloc, so only the (coalesced) per-id counts remain
@@ -106,6 +107,7 @@ __global__ void k_hash_cleanup(int32_t* __restrict__ u_count, int32_t* __restric
     u_count[1] = 0;
     u_count[3] = 0;
   }
+  if (u < zero_n) zero_extra[u] = 0;  // a consumer's counters, zeroed here instead of by a launch of their own
   if (u >= cap || u >= u_count[2]) return;
   cnt[u] = 0;
 }
@@ -343,7 +345,7 @@ size_t hash_dedup_temp_bytes(int64_t cap) {
 void launch_dedup_hash(const HashDedupArgs& a, void* temp, size_t temp_bytes, hipStream_t s) {
   const int64_t cap = a.cap;
   const unsigned gc = (unsigned)((cap + 255) / 256);
-  hipLaunchKernelGGL(k_hash_cleanup, dim3(gc), dim3(256), 0, s, a.u_count, a.cnt, cap);
+  hipLaunchKernelGGL(k_hash_cleanup, dim3(gc), dim3(256), 0, s, a.u_count, a.cnt, cap, a.zero_extra, a.zero_n);
   if (a.n <= 0) {
     launch_fill32(a.seg, 0u, 1, s);
     launch_fill32(a.u_count + 2, 0u, 1, s);

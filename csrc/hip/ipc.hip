@@ -114,6 +114,30 @@ __device__ __forceinline__ bool wait_all(const IpcPeers& pt, uint64_t epoch, int
   return *s_ok != 0;
 }
 
+// out[i0 .. i1) = scale * sum over the W source slots (float4 body + tail);
+// NaN when a wait failed
+__device__ __forceinline__ void reduce_slots(const IpcPeers& pt, int sl, int phase, int W, int64_t i0, int64_t i1,
+                                             float* out, float scale, bool ok, int64_t tid, int64_t nth) {
+  const float qnan = __int_as_float(0x7fc00000);
+  const int64_t n = i1 - i0;
+  const bool vec = ((reinterpret_cast<uintptr_t>(out + i0) & 15) == 0);
+  const int64_t n4 = vec ? n / 4 : 0;
+  for (int64_t i4 = tid; i4 < n4; i4 += nth) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = 0; p < W; ++p) {
+      const float4 v = reinterpret_cast<const float4*>(slot_ptr(pt, pt.rank, sl, phase, p))[i4];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    reinterpret_cast<float4*>(out + i0)[i4] =
+        ok ? make_float4(s.x * scale, s.y * scale, s.z * scale, s.w * scale) : make_float4(qnan, qnan, qnan, qnan);
+  }
+  for (int64_t i = n4 * 4 + tid; i < n; i += nth) {
+    float s = 0.f;
+    for (int p = 0; p < W; ++p) s += reinterpret_cast<const float*>(slot_ptr(pt, pt.rank, sl, phase, p))[i];
+    out[i0 + i] = ok ? s * scale : qnan;
+  }
+}
+
 // the last block to leave advances the epoch for the next launch
 __device__ __forceinline__ void depart(const IpcPeers& pt, uint64_t epoch) {
   __syncthreads();
@@ -184,11 +208,7 @@ __global__ __launch_bounds__(256) void k_ipc_allreduce(IpcPeers pt, const float*
       put_bytes(slot_ptr(pt, p, sl, 0, me), reinterpret_cast<const unsigned char*>(src), n * 4, tid, nth);
     signal(pt, epoch, 0, nullptr, &s_last);
     const bool ok = wait_all(pt, epoch, 0, s_cnt, &s_ok);
-    for (int64_t i = tid; i < n; i += nth) {
-      float s = 0.f;
-      for (int p = 0; p < W; ++p) s += __builtin_nontemporal_load(reinterpret_cast<const float*>(slot_ptr(pt, me, sl, 0, p)) + i);
-      out[i] = ok ? s * scale : qnan;
-    }
+    reduce_slots(pt, sl, 0, W, 0, n, out, scale, ok, tid, nth);
     depart(pt, epoch);
     return;
   }
@@ -203,19 +223,30 @@ __global__ __launch_bounds__(256) void k_ipc_allreduce(IpcPeers pt, const float*
   }
   signal(pt, epoch, 0, nullptr, &s_last);
   bool ok = wait_all(pt, epoch, 0, s_cnt, &s_ok);
-  // reduce my chunk and push each reduced element to every peer's gather area
-  for (int64_t i = tid; i < mine1 - mine0; i += nth) {
-    float s = 0.f;
-    for (int p = 0; p < W; ++p) s += __builtin_nontemporal_load(reinterpret_cast<const float*>(slot_ptr(pt, me, sl, 0, p)) + i);
-    s = ok ? s * scale : qnan;
-    for (int p = 0; p < W; ++p) reinterpret_cast<float*>(slot_ptr(pt, p, sl, 1, me))[i] = s;
+  // reduce my chunk and push each reduced float4 to every peer's gather area
+  // (chunks are multiples of 4 floats; the last one may be short)
+  const int64_t mc = mine1 - mine0;
+  for (int64_t i4 = tid; i4 < (mc + 3) / 4; i4 += nth) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = 0; p < W; ++p) {
+      const float4 v = reinterpret_cast<const float4*>(slot_ptr(pt, me, sl, 0, p))[i4];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    s = ok ? make_float4(s.x * scale, s.y * scale, s.z * scale, s.w * scale) : make_float4(qnan, qnan, qnan, qnan);
+    for (int p = 0; p < W; ++p) reinterpret_cast<float4*>(slot_ptr(pt, p, sl, 1, me))[i4] = s;
   }
   signal(pt, epoch, 1, nullptr, &s_last);
   ok = wait_all(pt, epoch, 1, s_cnt, &s_ok) && ok;
-  for (int64_t i = tid; i < n; i += nth) {
-    const int q = (int)(i / cs);
-    const float v = __builtin_nontemporal_load(reinterpret_cast<const float*>(slot_ptr(pt, me, sl, 1, q)) + (i - q * cs));
-    out[i] = ok ? v : qnan;
+  for (int q = 0; q < W; ++q) {  // gather: chunk q of every rank's result into out
+    const int64_t a0 = q * cs, a1 = (q + 1) * cs < n ? (q + 1) * cs : n;
+    if (a1 <= a0) continue;
+    const float* g = reinterpret_cast<const float*>(slot_ptr(pt, me, sl, 1, q));
+    if (ok) {
+      put_bytes(reinterpret_cast<unsigned char*>(out + a0), reinterpret_cast<const unsigned char*>(g),
+                (a1 - a0) * 4, tid, nth);
+    } else {
+      for (int64_t i = a0 + tid; i < a1; i += nth) out[i] = qnan;
+    }
   }
   depart(pt, epoch);
 }

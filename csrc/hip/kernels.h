@@ -88,6 +88,8 @@ struct HashDedupArgs {
   uint64_t* uniq_h = nullptr;
   int32_t* seg = nullptr;  // [cap+1]
   int32_t* u_count = nullptr;
+  int32_t* zero_extra = nullptr;  // optional: zeroed by the first launch (e.g. the shard pack's per-owner counts)
+  int zero_n = 0;
 };
 size_t hash_dedup_temp_bytes(int64_t cap);
 void launch_dedup_hash(const HashDedupArgs& a, void* temp, size_t temp_bytes, hipStream_t s);
@@ -233,7 +235,8 @@ void launch_gather_by_uid(const float* src, int src_stride, const int32_t* uid, 
 // fixed-capacity segments of send [nranks*cap] (kEmptyKey padded) and
 // send_index[u]; ocnt [nranks] scratch; overflow flag is sticky.
 void launch_shard_pack_hash(const uint64_t* uniq_h, const int32_t* u_count, int64_t u_cap, int nranks, int64_t cap,
-                            uint64_t* send, int64_t* send_index, int32_t* ocnt, int32_t* overflow, hipStream_t s);
+                            uint64_t* send, int64_t* send_index, int32_t* ocnt, int32_t* overflow, bool prezeroed,
+                            hipStream_t s);
 // out[j] = pull head of table row rows[uid[j]] (zeros if uid/row < 0);
 // out_stride % 4 == 0 and <= table stride.
 void launch_gather_rows_by_uid(const TableDev& t, const int64_t* rows, const int32_t* uid, int64_t n, float* out,

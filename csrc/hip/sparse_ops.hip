@@ -889,9 +889,12 @@ bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const in
 }
 
 void launch_shard_pack_hash(const uint64_t* uniq_h, const int32_t* u_count, int64_t u_cap, int nranks, int64_t cap,
-                            uint64_t* send, int64_t* send_index, int32_t* ocnt, int32_t* overflow, hipStream_t s) {
-  launch_fill32(send, 0xFFFFFFFFu, 2 * (int64_t)nranks * cap, s);  // kEmptyKey
-  launch_fill32(ocnt, 0u, nranks, s);
+                            uint64_t* send, int64_t* send_index, int32_t* ocnt, int32_t* overflow, bool prezeroed,
+                            hipStream_t s) {
+  if (!prezeroed) {
+    launch_fill32(send, 0xFFFFFFFFu, 2 * (int64_t)nranks * cap, s);  // kEmptyKey
+    launch_fill32(ocnt, 0u, nranks, s);
+  }
   hipLaunchKernelGGL(k_shard_pack_hash, dim3(nblk(u_cap)), dim3(256), 0, s, uniq_h, u_count, nranks, cap, send,
                      send_index, ocnt, overflow);
 }

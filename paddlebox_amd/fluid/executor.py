@@ -14,6 +14,8 @@ from __future__ import annotations
 
 from typing import Any, Dict, List, Optional, Sequence
 
+import warnings
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -364,45 +366,70 @@ class Session:
 
     # ------------------------------------------------ optimizer state (checkpoints)
     def _opt_slots(self):
-        """(param name, optimizer, element offset in its arena, storage shape)
-        for every trainable parameter with Adam state."""
+        """(param name, optimizer, element offset in its arena, storage shape,
+        full-arena m, full-arena v) for every trainable parameter with Adam
+        state.  ShardedFlatAdam's moments are all-gathered (collective: every
+        rank must call this); an optimizer without exportable state warns
+        instead of silently dropping it from the checkpoint."""
+        from ..parallel.sharding import ShardedFlatAdam
+
         for a, o in zip(self.arenas, self.opts):
-            if not isinstance(o, FlatAdam):
+            if isinstance(o, FlatAdam):
+                m, v = o.m, o.v
+            elif isinstance(o, ShardedFlatAdam):
+                m, v = o.gather_moments()
+            else:
+                if not isinstance(o, FlatSGD):  # SGD has no state to lose
+                    warnings.warn(f"optimizer {type(o).__name__} has no exportable state: "
+                                  "save_persistables writes the parameters only", RuntimeWarning)
                 continue
             base = a.flat.data_ptr()
             for name, st in self.storage.items():
                 if isinstance(st, torch.nn.Parameter) and st.untyped_storage().data_ptr() == \
                         a.flat.untyped_storage().data_ptr():
-                    yield name, o, (st.data_ptr() - base) // 4, st.shape
+                    yield name, o, (st.data_ptr() - base) // 4, st.shape, m, v
 
     def optimizer_state(self) -> Dict[str, torch.Tensor]:
         """Adam state under the reference's persistable names
         (``<param>_moment1_0``, ``_moment2_0``, ``_beta1_pow_acc_0``,
         ``_beta2_pow_acc_0``, fluid/optimizer.py AdamOptimizer), in the
         parameters' fluid layout, so save_persistables / load_persistables
-        resume training exactly."""
+        resume training exactly.
+
+        Beta powers: the reference initialises the accumulators to beta and
+        multiplies after each update (optimizer.py:2518-2523), so after t steps
+        they hold beta^(t+1); FlatAdam's ``pows`` hold beta^t (multiplied
+        before use).  The boundary converts both ways."""
         out = {}
-        for name, o, off, shape in self._opt_slots():
+        for name, o, off, shape, m, v in self._opt_slots():
             n = int(np.prod(shape))
-            out[name + "_moment1_0"] = self._logical_of(name, o.m[off:off + n].view(shape))
-            out[name + "_moment2_0"] = self._logical_of(name, o.v[off:off + n].view(shape))
-            out[name + "_beta1_pow_acc_0"] = o.pows[0:1]
-            out[name + "_beta2_pow_acc_0"] = o.pows[1:2]
+            out[name + "_moment1_0"] = self._logical_of(name, m[off:off + n].view(shape))
+            out[name + "_moment2_0"] = self._logical_of(name, v[off:off + n].view(shape))
+            out[name + "_beta1_pow_acc_0"] = o.pows[0:1] * o.b1
+            out[name + "_beta2_pow_acc_0"] = o.pows[1:2] * o.b2
         return out
 
     def load_optimizer_state(self, state: Dict[str, Any]) -> int:
+        from ..parallel.sharding import ShardedFlatAdam
+
         n_loaded = 0
+        touched = {}
         with torch.no_grad():
-            for name, o, off, shape in self._opt_slots():
+            for name, o, off, shape, m, v in self._opt_slots():
                 n = int(np.prod(shape))
-                for suffix, buf in (("_moment1_0", o.m), ("_moment2_0", o.v)):
+                for suffix, buf in (("_moment1_0", m), ("_moment2_0", v)):
                     if name + suffix in state:
                         dst = self._logical_of(name, buf[off:off + n].view(shape))
                         dst.copy_(torch.as_tensor(state[name + suffix]).reshape(dst.shape).to(dst.device))
                         n_loaded += 1
-                for i, suffix in enumerate(("_beta1_pow_acc_0", "_beta2_pow_acc_0")):
+                        touched[id(o)] = (o, m, v)
+                for i, (suffix, beta) in enumerate((("_beta1_pow_acc_0", o.b1), ("_beta2_pow_acc_0", o.b2))):
                     if name + suffix in state:
-                        o.pows[i:i + 1].copy_(torch.as_tensor(state[name + suffix]).reshape(1).to(o.pows.device))
+                        acc = torch.as_tensor(state[name + suffix], dtype=torch.float32).reshape(1)
+                        o.pows[i:i + 1].copy_((acc / beta).to(o.pows.device))
+            for o, m, v in touched.values():
+                if isinstance(o, ShardedFlatAdam):
+                    o.scatter_moments(m, v)
         return n_loaded
 
     def _restore_optimizer_state_from_scope(self):

@@ -43,7 +43,7 @@ class IpcMeshError(RuntimeError):
 
 
 class IpcMesh:
-    def __init__(self, slot_bytes: int, group=None, device=None, blocks: int = 32, depth: int = 2,
+    def __init__(self, slot_bytes: int, group=None, device=None, blocks: Optional[int] = None, depth: int = 2,
                  spin_limit: Optional[int] = None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -55,6 +55,11 @@ class IpcMesh:
         self.depth = int(depth)
         h = _native.hip()
         W = self.world
+        if blocks is None:
+            # ~64 KB of payload per workgroup: enough 16-B streams in flight
+            # to fill 7 xGMI links (and the local copy-out), without hundreds
+            # of flag pollers on small collectives
+            blocks = max(16, min(256, (W * self.slot_bytes) >> 16))
         self.inbox = torch.zeros(self.depth * 2 * W * self.slot_bytes, dtype=torch.uint8, device=self.device)
         self.flags = torch.zeros(2 * W, dtype=torch.int64, device=self.device)
         self.state = torch.zeros(4, dtype=torch.int64, device=self.device)

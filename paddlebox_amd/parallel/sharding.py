@@ -106,6 +106,26 @@ class ShardedFlatAdam:
             all_gather_flat(self._pflat, p.clone(), self.group)
         self.a.flat.copy_(self._pflat[:n])
 
+    def gather_moments(self):
+        """Full-arena (m, v) assembled from every rank's shard (collective)."""
+        n = self.a.flat.numel()
+        if not self.active:
+            return self.m[:n].clone(), self.v[:n].clone()
+        out = []
+        for part in (self.m, self.v):
+            full = torch.empty(self.padded, device=part.device)
+            all_gather_flat(full, part, self.group)
+            out.append(full[:n])
+        return out[0], out[1]
+
+    def scatter_moments(self, m_full: torch.Tensor, v_full: torch.Tensor):
+        """Inverse of gather_moments: keep this rank's slice of full-arena moments."""
+        n = self.a.flat.numel()
+        for part, full in ((self.m, m_full), (self.v, v_full)):
+            pad = torch.zeros(self.padded, device=part.device)
+            pad[:n] = full.reshape(-1)[:n].to(part.device)
+            part.copy_(self._slice(pad))
+
     def state_dict(self):
         return {"m": self.m, "v": self.v, "pows": self.pows, "rank": self.rank, "world": self.world}
 

@@ -387,7 +387,10 @@ class SparseEngine:
             return st
         sl = self._take_slot()
         ws = sl.ws
-        ws.run(keys, False)
+        # IPC exchange: the shard pack's per-owner counters are zeroed by the
+        # dedup's first launch (no fill launches of their own)
+        ipc = self.sharded and self.xmesh is not None
+        ws.run(keys, False, sl.ocnt if ipc else None)
         if fill_occ:
             h.fill_occurrence(lod, S, B, sl.occ_slot, sl.occ_ins)
         st = PullState(B=B, S=S, L=L, lod=lod, uid=ws.uid, perm=ws.perm, counts=ws.u_count, slot=sl, gen=sl.gen)
@@ -397,7 +400,8 @@ class SparseEngine:
                 self._auto_insert(st, L)
             return st
         # sharded: pack per-owner, exchange keys, owner-side dedup/probe/gather
-        h.shard_pack_hash(ws.uniq_h, ws.u_count, self.world, self.C, sl.send, sl.send_index, sl.ocnt, self.overflow)
+        h.shard_pack_hash(ws.uniq_h, ws.u_count, self.world, self.C, sl.send, sl.send_index, sl.ocnt, self.overflow,
+                          ipc)
         if self.xmesh is not None:
             # only the valid keys of each peer slot travel; the receiver
             # fills the rest of its slots with -1 (padding for the dedup)
