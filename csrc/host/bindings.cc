@@ -578,6 +578,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         s.send_message(client_id, buf.data(), (int64_t)buf.size(), std::move(c));
       }, py::arg("client_id"), py::arg("data"), py::arg("callback") = py::none())
       .def("wait_done", &MsgService::wait_done, py::call_guard<py::gil_scoped_release>())
+      .def("broken_peers", &MsgService::broken_peers)
       .def("destroy", &MsgService::destroy, py::call_guard<py::gil_scoped_release>())
       .def("bytes_sent", &MsgService::bytes_sent)
       .def("messages_handled", &MsgService::messages_handled)

@@ -172,10 +172,19 @@ int MsgService::register_handler(Handler h) {
 }
 
 void MsgService::unregister_consumer(int sid) {
-  wait_done(sid);
+  // waits for our messages like wait_done, but never throws: a caller
+  // unwinding from a failed shuffle must still be able to drop its handler
+  {
+    std::unique_lock<std::mutex> g(hmu_);
+    hcv_.wait(g, [&] {
+      auto it = pending_.find((uint32_t)sid);
+      return stop_.load() || it == pending_.end() || it->second <= 0;
+    });
+  }
   std::lock_guard<std::mutex> g(hmu_);
   handlers_.erase((uint32_t)sid);
   pending_.erase((uint32_t)sid);
+  failed_.erase((uint32_t)sid);
 }
 
 MsgService::Handler MsgService::handler_for(uint32_t sid) {
@@ -197,6 +206,59 @@ void MsgService::finish_one(uint32_t sid, Callback& cb) {
   hcv_.notify_all();
 }
 
+void MsgService::fail_peer(int peer, const char* why) {
+  Peer& p = *peers_[peer];
+  std::vector<uint32_t> lost;  // sid of every frame that will never be acknowledged
+  {
+    std::lock_guard<std::mutex> g(p.mu);
+    if (p.broken) return;
+    p.broken = true;
+    for (auto& f : p.queue) lost.push_back(f.sid);
+    p.queue.clear();
+    for (auto& e : p.inflight) lost.push_back(e.second.first);
+    p.inflight.clear();
+  }
+  p.cv.notify_all();
+  if (!stop_.load())
+    fprintf(stderr, "[pbx msg] rank %d: peer %d lost (%s), %zu message(s) failed\n", rank_, peer, why, lost.size());
+  std::vector<LossListener> ls;
+  {
+    std::lock_guard<std::mutex> g(hmu_);
+    for (uint32_t sid : lost) {
+      auto it = pending_.find(sid);
+      if (it != pending_.end()) --it->second;
+      if (!failed_.count(sid)) failed_[sid] = "message to rank " + std::to_string(peer) + " failed: " + why;
+    }
+    for (auto& e : listeners_) ls.push_back(e.second);
+    hcv_.notify_all();
+  }
+  // listeners (e.g. a shuffle waiting for this peer's end-of-stream message)
+  // run with none of this service's locks held
+  for (auto& f : ls) f(peer);
+}
+
+int MsgService::add_loss_listener(LossListener f) {
+  std::lock_guard<std::mutex> g(hmu_);
+  const int id = next_listener_++;
+  listeners_[id] = std::move(f);
+  return id;
+}
+
+void MsgService::remove_loss_listener(int id) {
+  std::lock_guard<std::mutex> g(hmu_);
+  listeners_.erase(id);
+}
+
+std::vector<int> MsgService::broken_peers() {
+  std::vector<int> out;
+  for (int i = 0; i < world_; ++i) {
+    if (i == rank_) continue;
+    std::lock_guard<std::mutex> g(peers_[i]->mu);
+    if (peers_[i]->broken) out.push_back(i);
+  }
+  return out;
+}
+
 void MsgService::send_message(int client_id, const char* buf, int64_t len, Callback cb) {
   const uint32_t sid = (uint32_t)client_id >> 16;
   const int dest = client_id & 0xffff;
@@ -216,10 +278,22 @@ void MsgService::send_message(int client_id, const char* buf, int64_t len, Callb
   if (!connected_) throw std::runtime_error("MsgService::send_message: not connected");
   Peer& p = *peers_[dest];
   Frame f{sid, 0, std::string(buf ? buf : "", buf ? (size_t)len : 0), std::move(cb)};
+  bool broken;
   {
     std::lock_guard<std::mutex> g(p.mu);
-    f.seq = p.next_seq++;
-    p.queue.push_back(std::move(f));
+    broken = p.broken;
+    if (!broken) {
+      f.seq = p.next_seq++;
+      p.queue.push_back(std::move(f));
+    }
+  }
+  if (broken) {
+    {
+      std::lock_guard<std::mutex> g(hmu_);
+      --pending_[sid];
+      hcv_.notify_all();
+    }
+    throw std::runtime_error("MsgService::send_message: rank " + std::to_string(dest) + " is lost");
   }
   p.cv.notify_one();
 }
@@ -228,8 +302,10 @@ void MsgService::wait_done(int sid) {
   std::unique_lock<std::mutex> g(hmu_);
   hcv_.wait(g, [&] {
     auto it = pending_.find((uint32_t)sid);
-    return stop_.load() || it == pending_.end() || it->second == 0;
+    return stop_.load() || it == pending_.end() || it->second <= 0;
   });
+  auto f = failed_.find((uint32_t)sid);
+  if (f != failed_.end()) throw std::runtime_error("MsgService::wait_done(" + std::to_string(sid) + "): " + f->second);
 }
 
 void MsgService::sender_loop(int peer) {
@@ -246,7 +322,7 @@ void MsgService::sender_loop(int peer) {
     }
     FrameHeader h{kMagic, f.sid, f.seq, (int64_t)f.payload.size()};
     if (!write_all(p.out_fd, &h, sizeof(h)) || !write_all(p.out_fd, f.payload.data(), f.payload.size())) {
-      if (!stop_.load()) fprintf(stderr, "[pbx msg] rank %d: send to %d failed\n", rank_, peer);
+      fail_peer(peer, "send failed");
       return;
     }
     bytes_sent_ += (int64_t)(sizeof(h) + f.payload.size());
@@ -267,6 +343,8 @@ void MsgService::acker_loop(int peer) {
     }
     finish_one(e.first, e.second);
   }
+  // acknowledgements stopped: unless we are shutting down, the peer is gone
+  if (!stop_.load()) fail_peer(peer, "connection closed");
 }
 
 void MsgService::receiver_loop(int peer) {
@@ -281,6 +359,7 @@ void MsgService::receiver_loop(int peer) {
     buf.resize((size_t)h.len);
     if (h.len && !read_all(p.in_fd, &buf[0], (size_t)h.len)) return;
     Handler fn = handler_for(h.sid);
+    if (stop_.load()) return;
     if (fn) {
       fn(peer, h.len ? buf.data() : nullptr, h.len);
     } else if (!stop_.load()) {
@@ -288,8 +367,9 @@ void MsgService::receiver_loop(int peer) {
               (long long)h.len);
     }
     ++handled_;
-    if (!write_all(p.in_fd, &h.seq, sizeof(h.seq))) return;
+    if (!write_all(p.in_fd, &h.seq, sizeof(h.seq))) break;
   }
+  if (!stop_.load()) fail_peer(peer, "inbound stream ended");
 }
 
 void MsgService::destroy() {

@@ -13,7 +13,12 @@
 //    target service's handler and then acknowledges the frame;
 //  * a callback fires when the peer has ACKNOWLEDGED (handled) the message,
 //    and wait_done(sid) blocks until every message sent by that service has
-//    been handled on its destination.
+//    been handled on its destination;
+//  * a peer whose socket fails (process died, connection reset) is marked
+//    broken: its queued and in-flight frames are completed as FAILED (no
+//    callback), further sends to it throw, and wait_done(sid) throws once the
+//    service has no message left pending -- a lost peer fails the shuffle on
+//    every rank instead of hanging it.
 //
 // Payloads are copied at send time, so the caller may reuse its buffer as soon
 // as send_message returns (the reference clears its archive right after
@@ -53,9 +58,18 @@ class MsgService {
   // their consumers in the same order agree on them (as in the reference)
   int register_handler(Handler h);
   void unregister_consumer(int sid);
-  // client_id = (sid << 16) | dest_rank; len 0 is a legal (end-marker) message
+  // client_id = (sid << 16) | dest_rank; len 0 is a legal (end-marker) message.
+  // Throws if the destination peer is broken.
   void send_message(int client_id, const char* buf, int64_t len, Callback cb);
+  // Blocks until nothing sent by sid is pending; throws if any of its
+  // messages failed (broken peer).
   void wait_done(int sid);
+  // ranks whose connection failed (empty when healthy)
+  std::vector<int> broken_peers();
+  // called (from a service thread, no service lock held) when a peer is lost
+  using LossListener = std::function<void(int peer)>;
+  int add_loss_listener(LossListener f);
+  void remove_loss_listener(int id);
   void destroy();
 
   int rank() const { return rank_; }
@@ -77,6 +91,7 @@ class MsgService {
     std::deque<Frame> queue;
     std::map<uint64_t, std::pair<uint32_t, Callback>> inflight;  // seq -> (sid, cb)
     uint64_t next_seq = 0;
+    bool broken = false;  // guarded by mu
     std::thread sender, acker, receiver;
   };
   void sender_loop(int peer);
@@ -84,6 +99,8 @@ class MsgService {
   void receiver_loop(int peer);
   Handler handler_for(uint32_t sid);
   void finish_one(uint32_t sid, Callback& cb);
+  // mark a peer broken and fail everything queued / in flight to it
+  void fail_peer(int peer, const char* why);
 
   int rank_, world_;
   int listen_fd_ = -1;
@@ -96,6 +113,9 @@ class MsgService {
   std::map<uint32_t, Handler> handlers_;
   uint32_t next_sid_ = 1;
   std::map<uint32_t, int64_t> pending_;  // sid -> messages not yet acknowledged
+  std::map<uint32_t, std::string> failed_;  // sid -> first failure
+  std::map<int, LossListener> listeners_;
+  int next_listener_ = 1;
 
   std::atomic<int64_t> bytes_sent_{0}, handled_{0};
 };

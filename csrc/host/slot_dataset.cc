@@ -1080,12 +1080,26 @@ int64_t SlotDataset::global_shuffle(MsgService& svc, int mode, uint64_t seed, in
   std::condition_variable cv;
   int finished = 0;
   bool bad = false;
+  std::vector<char> lost_peer((size_t)W, 0), done_peer((size_t)W, 0);  // lost connections, end markers seen
+  std::string send_err;
   RecordStore incoming;
   incoming.reset(st.nu, st.nf);
-  const int sid = svc.register_handler([&](int /*src*/, const char* buf, int64_t len) {
+  const int lid = svc.add_loss_listener([&](int peer) {
+    std::lock_guard<std::mutex> g(mu);
+    lost_peer[(size_t)peer] = 1;
+    cv.notify_all();
+  });
+  // a peer lost before its end marker arrived: its records never will (mu held)
+  auto lost_unfinished = [&]() {
+    for (int r = 0; r < W; ++r)
+      if (lost_peer[(size_t)r] && !done_peer[(size_t)r]) return r;
+    return -1;
+  };
+  const int sid = svc.register_handler([&](int src, const char* buf, int64_t len) {
     if (len == 0) {  // end of this peer's stream (FIFO per peer: after its data)
       std::lock_guard<std::mutex> g(mu);
       ++finished;
+      if (src >= 0 && src < W) done_peer[(size_t)src] = 1;
       cv.notify_all();
       return;
     }
@@ -1115,19 +1129,37 @@ int64_t SlotDataset::global_shuffle(MsgService& svc, int mode, uint64_t seed, in
           std::vector<int64_t> part(idx.begin() + b, idx.begin() + std::min(idx.size(), b + (size_t)chunk));
           msg.clear();
           st.select(part).serialize(&msg);
-          svc.send_message((sid << 16) | r, msg.data(), (int64_t)msg.size(), nullptr);
+          try {
+            svc.send_message((sid << 16) | r, msg.data(), (int64_t)msg.size(), nullptr);
+          } catch (const std::exception& e) {  // destination lost: stop sending to it
+            std::lock_guard<std::mutex> g(mu);
+            if (send_err.empty()) send_err = e.what();
+            break;
+          }
         }
       }
     });
   for (auto& w : workers) w.join();
-  for (int r = 0; r < W; ++r)
-    if (r != R) svc.send_message((sid << 16) | r, nullptr, 0, nullptr);
-  svc.wait_done(sid);  // every message of ours handled by its receiver
-  {
-    std::unique_lock<std::mutex> g(mu);
-    cv.wait(g, [&] { return finished == W - 1; });
+  std::string err;
+  try {
+    for (int r = 0; r < W; ++r)
+      if (r != R) svc.send_message((sid << 16) | r, nullptr, 0, nullptr);
+    svc.wait_done(sid);  // every message of ours handled by its receiver (throws if a peer was lost)
+  } catch (const std::exception& e) {
+    err = e.what();
   }
+  {
+    const std::vector<int> already = svc.broken_peers();  // lost before the listener existed
+    std::unique_lock<std::mutex> g(mu);
+    for (int r : already) lost_peer[(size_t)r] = 1;
+    cv.wait(g, [&] { return finished == W - 1 || lost_unfinished() >= 0; });
+    if (err.empty() && !send_err.empty()) err = send_err;
+    const int lu = lost_unfinished();
+    if (err.empty() && lu >= 0) err = "rank " + std::to_string(lu) + " was lost before finishing its stream";
+  }
+  svc.remove_loss_listener(lid);
   svc.unregister_consumer(sid);
+  if (!err.empty()) throw std::runtime_error("global_shuffle: " + err);
   if (bad) throw std::runtime_error("global_shuffle: malformed shuffle message");
 
   RecordStore kept = st.select(dest[(size_t)R]);

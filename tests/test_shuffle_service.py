@@ -147,3 +147,74 @@ def test_global_shuffle_three_ranks(mode):
         if mode == "lineid":
             for i in ids:
                 assert h.xxh64(i[:32], 0) % world == r
+
+
+def _kill_worker(rank, W, q_in, q_out):
+    import os as _os
+
+    from paddlebox_amd import _native as nat
+
+    hh = nat.host()
+    svc = hh.MsgService(rank, W)
+    q_out.put(("port", rank, svc.listen("127.0.0.1", 0)))
+    eps = q_in.get(timeout=60)
+    svc.connect(eps, 30.0)
+    seen = [0]
+
+    def on_receive(src, data):
+        seen[0] += 1
+        if rank == W - 1 and seen[0] == 3:  # the victim dies abruptly mid-shuffle
+            _os._exit(3)
+
+    sid = svc.register_handler(on_receive)
+    err = None
+    try:
+        for k in range(200):
+            for d in range(W):
+                if d != rank:
+                    svc.send_message((sid << 16) | d, b"x" * 65536)
+        for d in range(W):
+            if d != rank:
+                svc.send_message((sid << 16) | d, b"")
+        svc.wait_done(sid)
+    except RuntimeError as e:
+        err = str(e)
+    q_out.put(("done", rank, err, list(svc.broken_peers())))
+    svc.unregister_consumer(sid)
+    svc.destroy()
+
+
+def test_msg_service_lost_peer_fails_fast():
+    """a peer that dies mid-shuffle must fail the survivors'
+    wait_done with an error naming it, not hang them forever."""
+    import time
+
+    W = 3
+    ctx = mp.get_context("spawn")
+    q_in = [ctx.Queue() for _ in range(W)]
+    q_out = ctx.Queue()
+    ps = [ctx.Process(target=_kill_worker, args=(r, W, q_in[r], q_out)) for r in range(W)]
+    for p in ps:
+        p.start()
+    ports = {}
+    while len(ports) < W:
+        kind, r, port = q_out.get(timeout=60)
+        ports[r] = port
+    eps = [f"127.0.0.1:{ports[r]}" for r in range(W)]
+    for q in q_in:
+        q.put(eps)
+    t0 = time.time()
+    res = {}
+    while len(res) < W - 1:
+        kind, r, err, broken = q_out.get(timeout=90)
+        res[r] = (err, broken)
+    for p in ps:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert ps[W - 1].exitcode == 3
+    for r in range(W - 1):
+        err, broken = res[r]
+        assert err is not None and "rank 2" in err, res
+        assert W - 1 in broken, res
+    assert time.time() - t0 < 60
