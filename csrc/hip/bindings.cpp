@@ -168,6 +168,39 @@ class GpuTable {
                                    ptr<int32_t>(perm), ptr<int32_t>(seg), ptr<int32_t>(cnt), ptr<int32_t>(n_dev),
                                    rows.numel(), cfg, seed, cur_stream());
   }
+  // owner side of the sharded pull, one launch: rows[i] = row of h[i] (-1 if
+  // absent) and out[i] = its pull record; h may hold -1 padding (skipped)
+  void probe_gather(const Tensor& h, Tensor rows, Tensor out) {
+    check_cuda(h, "h");
+    check_cuda(rows, "rows");
+    check_cuda(out, "out");
+    PBX_CHECK(rows.scalar_type() == torch::kInt64 && rows.is_contiguous() && rows.numel() >= h.numel(),
+              "probe_gather: rows");
+    PBX_CHECK(out.dim() == 2 && out.is_contiguous() && out.size(0) >= h.numel() && out.size(1) % 4 == 0 &&
+                  out.size(1) <= stride_,
+              "probe_gather: out must be contiguous [>= n, stride % 4 == 0, <= row stride]");
+    launch_probe_gather(view(), ptr<uint64_t>(h), h.numel(), ptr<int64_t>(rows), ptr<float>(out), (int)out.size(1),
+                        cur_stream());
+  }
+  // owner side of the sharded push without a dedup of the received keys
+  // (entries sharing a row elect a leader through a per-row lock word, see
+  // launch_owner_push); rec is modified (records summed into the leaders').
+  // False if not vectorisable for this dim / record stride.
+  bool owner_push(const Tensor& rows, Tensor rec, const SparseSGDConfig& cfg, uint64_t seed) {
+    check_cuda(rows, "rows");
+    check_cuda(rec, "rec");
+    const int64_t n = rows.numel();
+    PBX_CHECK(rec.dim() == 2 && rec.is_contiguous() && rec.size(0) >= n && rec.size(1) >= push_width(dim_),
+              "owner_push: rec");
+    PBX_CHECK(n < (int64_t)INT32_MAX, "owner_push: too many records");
+    if (!lock_.defined()) {
+      auto opt4 = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device_);
+      lock_ = torch::full({values_.size(0)}, -1, opt4);  // free; every apply resets what it took
+    }
+    if (!lead_.defined() || lead_.numel() < n) lead_ = torch::empty({n}, lock_.options());
+    return launch_owner_push(view(), ptr<int64_t>(rows), ptr<float>(rec), (int)rec.size(1), n, ptr<int32_t>(lock_),
+                             ptr<int32_t>(lead_), cfg, seed, cur_stream());
+  }
   // single-shard push: merge per unique key + Adagrad in one pass (acc: all-zero
   // scratch [>= U_cap, stride], kept zero; inc: [>= ceil(n/64)] int32 scratch)
   bool push_merge_apply(const Tensor& dout, int col_offset, const Tensor& cvm, bool use_cvm, bool clk_filter, int E,
@@ -277,6 +310,7 @@ class GpuTable {
   int64_t stash_cap_;
   int64_t last_overflow_ = 0;
   Tensor keys_, fill_, values_, stash_keys_, scratch_;
+  Tensor lock_, lead_;  // owner_push: per-row leader word (-1 = free), per-record leader
 };
 
 // --------------------------------------------------------------- dedup
@@ -997,6 +1031,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("gather_rows_by_uid", &GpuTable::gather_rows_by_uid)
       .def("push_adagrad_seg", &GpuTable::push_adagrad_seg)
       .def("push_merge_apply", &GpuTable::push_merge_apply)
+      .def("probe_gather", &GpuTable::probe_gather)
+      .def("owner_push", &GpuTable::owner_push)
       .def("codec_pull", &GpuTable::codec_pull, py::arg("codec"), py::arg("rows"), py::arg("uid"), py::arg("n_dev"),
            py::arg("n"), py::arg("out"))
       .def("codec_update", &GpuTable::codec_update)

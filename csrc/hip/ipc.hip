@@ -5,11 +5,12 @@
 // collective, graph-capturable and free of host synchronisation:
 //   put     the grid writes its payload straight into peer p's inbox slot
 //           [e % depth][phase][me] (one pass over xGMI);
-//   signal  every block fences at system scope and arrives on a local
-//           counter; the last block publishes (epoch << 24 | count) into each
-//           peer's flag word [phase][me] (system-scope release store);
-//   wait    every block polls (bounded, acquire loads) until all W flags of
-//           its own inbox carry the epoch; the counts ride along.
+//   signal  every block drains its puts, one lane releases at system scope and
+//           arrives on a local counter; the last block publishes
+//           (epoch << 24 | count) into each peer's flag word [phase][me];
+//   wait    every block polls (bounded, relaxed system-scope loads) until all
+//           W flags of its own inbox carry the epoch, then acquires once; the
+//           counts ride along.
 // Collectives:
 //   exchange   all-to-all of per-peer records: only counts[p] records of slot
 //              p travel (the sparse step's keys / values / gradients, sized by
@@ -43,13 +44,6 @@ namespace {
 constexpr int kCountBits = 24;
 constexpr uint64_t kCountMask = (1ull << kCountBits) - 1;
 
-__device__ __forceinline__ uint64_t ld_acquire_sys(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void st_release_sys(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 __device__ __forceinline__ unsigned char* slot_ptr(const IpcPeers& pt, int owner, int slot, int phase, int src) {
   const int64_t s = pt.slot_bytes;
   const int W = pt.world;
@@ -66,12 +60,19 @@ __device__ __forceinline__ void put_bytes(unsigned char* dst, const unsigned cha
   if (tid < (n & 15)) dst[(nv << 4) + tid] = src[(nv << 4) + tid];
 }
 
-// last-arriving block publishes flag value (epoch, count[p]) to every peer
+// Publish: every wave drains its own puts (vmcnt 0), the workgroup meets at
+// a barrier, ONE lane issues the system-scope release (write-back of the
+// XCD's L2, for puts that went through it) and arrives on the local counter;
+// the last-arriving block then stores (epoch, count[p]) into each peer's
+// flag word with a relaxed system-scope store.  One release per block, not
+// one per thread (MI355X_MICROARCH.md, valid forms: producer).
 __device__ __forceinline__ void signal(const IpcPeers& pt, uint64_t epoch, int phase, const int32_t* counts,
                                        int* s_last, int64_t max_count = 0) {
-  __threadfence_system();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned int a = atomicAdd(pt.arrive, 1u) + 1u;
     *s_last = (a % gridDim.x) == 0;
   }
@@ -81,19 +82,22 @@ __device__ __forceinline__ void signal(const IpcPeers& pt, uint64_t epoch, int p
     int64_t cn = counts ? (int64_t)counts[p] : 0;
     cn = cn < 0 ? 0 : (cn > max_count ? max_count : cn);  // an overflowing sender sends (and announces) a full slot
     const uint64_t c = (uint64_t)cn & kCountMask;
-    st_release_sys(pt.flags[p] + phase * pt.world + pt.rank, (epoch << kCountBits) | c);
+    __hip_atomic_store(pt.flags[p] + phase * pt.world + pt.rank, (epoch << kCountBits) | c, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
-// wait for all W flags of phase; returns false (and sets err) on timeout.
-// The received counts land in s_cnt[src].
+// Wait for all W flags of phase: relaxed system-scope polls (no cache
+// invalidation per poll), then ONE system-scope acquire per block before
+// anything reads the inbox (the consumer form of the same table).  Returns
+// false (and sets the sticky err) on timeout; the counts land in s_cnt[src].
 __device__ __forceinline__ bool wait_all(const IpcPeers& pt, uint64_t epoch, int phase, int* s_cnt, int* s_ok) {
   if (threadIdx.x == 0) *s_ok = 1;
   __syncthreads();
   if ((int)threadIdx.x < pt.world) {
     const uint64_t* f = pt.flags[pt.rank] + phase * pt.world + threadIdx.x;
     const bool dead = __hip_atomic_load(pt.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    uint64_t v = ld_acquire_sys(f);
+    uint64_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     int64_t spins = 0;
     while (!dead && (v >> kCountBits) < epoch) {
       __builtin_amdgcn_s_sleep(2);
@@ -101,7 +105,7 @@ __device__ __forceinline__ bool wait_all(const IpcPeers& pt, uint64_t epoch, int
         atomicExch(pt.err, 1);
         break;
       }
-      v = ld_acquire_sys(f);
+      v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if ((v >> kCountBits) < epoch) {
       *s_ok = 0;
@@ -110,8 +114,21 @@ __device__ __forceinline__ bool wait_all(const IpcPeers& pt, uint64_t epoch, int
       s_cnt[threadIdx.x] = (int)(v & kCountMask);
     }
   }
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
   return *s_ok != 0;
+}
+
+// the last block to leave advances the epoch for the next launch
+__device__ __forceinline__ void depart(const IpcPeers& pt, uint64_t epoch) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int d = atomicAdd(pt.depart, 1u) + 1u;
+    if ((d % gridDim.x) == 0) __hip_atomic_store(pt.epoch, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // out[i0 .. i1) = scale * sum over the W source slots (float4 body + tail);
@@ -138,15 +155,6 @@ __device__ __forceinline__ void reduce_slots(const IpcPeers& pt, int sl, int pha
   }
 }
 
-// the last block to leave advances the epoch for the next launch
-__device__ __forceinline__ void depart(const IpcPeers& pt, uint64_t epoch) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const unsigned int d = atomicAdd(pt.depart, 1u) + 1u;
-    if ((d % gridDim.x) == 0) __hip_atomic_store(pt.epoch, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
 
 __global__ __launch_bounds__(256) void k_ipc_exchange(IpcPeers pt, const unsigned char* __restrict__ send,
                                                       unsigned char* __restrict__ dst, const int32_t* counts,

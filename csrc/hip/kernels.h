@@ -26,6 +26,16 @@ struct TableDev {
 // rows[i] = row id of h[i] or -1.  n_dev (optional) = device-side count.
 void launch_table_probe(const TableDev& t, const uint64_t* h, int64_t n, const int32_t* n_dev,
                         int64_t* rows, hipStream_t s);
+// Owner side of the sharded pull: rows[i] = row of h[i] (or -1) and out[i] =
+// its pull record (zero padded to out_stride floats), no dedup needed.
+void launch_probe_gather(const TableDev& t, const uint64_t* h, int64_t n, int64_t* rows, float* out, int out_stride,
+                         hipStream_t s);
+// Owner side of the sharded push without a dedup of the received keys:
+// entries with the same table row elect a leader through lock[row] (int32,
+// -1 = free, reset by the apply), the others add their record into the
+// leader's (slot field excepted); then each leader applies sparse Adagrad.
+bool launch_owner_push(const TableDev& t, const int64_t* rows, float* rec, int rec_stride, int64_t n,
+                       int32_t* lock, int32_t* lead, const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s);
 // Insert unique keys h[i] whose rows[i] < 0.  Overflowing keys are appended to
 // ovf_keys (count in ovf_n) for launch_table_resolve_overflow.
 void launch_table_insert(const TableDev& t, const uint64_t* h, int64_t n, const int32_t* n_dev,

@@ -615,6 +615,48 @@ __global__ __launch_bounds__(256) void k_push_finish(TableDev t, const int64_t* 
   if (r >= 0) adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
 }
 
+// Owner-side push of the sharded step, no dedup of the received keys.  Pass
+// 1: every received entry with a row elects a leader among the entries of
+// that row (first CAS on lock[row] wins) and adds its merged gradient record
+// into the leader's (the slot field is kept from the leader); pass 2: each
+// leader applies Adagrad to the row and frees the lock.  A key asked by k
+// peers costs k-1 record atomics instead of a sort or hash dedup of W*C keys.
+template <int D>
+__global__ __launch_bounds__(256) void k_owner_push_elect(const int64_t* __restrict__ rows, float* __restrict__ rec,
+                                                          int rec_stride, int64_t n, int32_t* __restrict__ lock,
+                                                          int32_t* __restrict__ lead) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int64_t r = rows[e];
+  if (r < 0) {
+    lead[e] = -1;
+    return;
+  }
+  const int32_t old = atomicCAS(&lock[r], -1, (int32_t)e);
+  const int32_t l = old == -1 ? (int32_t)e : old;
+  lead[e] = l;
+  if (l == (int32_t)e) return;
+  constexpr int Q = RowF<D>::kQ;
+  const float* src = rec + e * (int64_t)rec_stride;
+  float* dst = rec + (int64_t)l * rec_stride;
+#pragma unroll
+  for (int c = 1; c < Q; ++c) atomicAdd(&dst[c], src[c]);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_owner_push_apply(TableDev t, const int64_t* __restrict__ rows,
+                                                          const float* __restrict__ rec, int rec_stride, int64_t n,
+                                                          int32_t* __restrict__ lock, const int32_t* __restrict__ lead,
+                                                          SparseSGDConfig cfg, uint64_t seed) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n || lead[e] != (int32_t)e) return;
+  const int64_t r = rows[e];
+  float g[RowF<D>::kQ4 * 4];
+  load_push<D>(rec + e * (int64_t)rec_stride, g);
+  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
+  lock[r] = -1;
+}
+
 // ---------------------------------------------------------------- sharding helpers
 __device__ __forceinline__ int64_t owner_lower_bound(const uint64_t* h, int64_t U, uint32_t o, uint32_t N) {
   int64_t lo = 0, hi = U;
@@ -863,6 +905,24 @@ bool launch_push_adagrad_seg(const TableDev& t, const int64_t* rows, const float
   else
     return false;
   return true;
+}
+
+bool launch_owner_push(const TableDev& t, const int64_t* rows, float* rec, int rec_stride, int64_t n, int32_t* lock,
+                       int32_t* lead, const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s) {
+  if (n <= 0) return true;
+  const dim3 g(nblk(n)), b(256);
+#define PBX_OWNER_PUSH(D)                                                                                  \
+  if (t.dim == D && vec_push_ok<D>(t, rec_stride)) {                                                       \
+    hipLaunchKernelGGL(k_owner_push_elect<D>, g, b, 0, s, rows, rec, rec_stride, n, lock, lead);           \
+    hipLaunchKernelGGL(k_owner_push_apply<D>, g, b, 0, s, t, rows, rec, rec_stride, n, lock, lead, cfg, seed); \
+    return true;                                                                                           \
+  }
+  PBX_OWNER_PUSH(8)
+  PBX_OWNER_PUSH(16)
+  PBX_OWNER_PUSH(4)
+  PBX_OWNER_PUSH(32)
+#undef PBX_OWNER_PUSH
+  return false;
 }
 
 bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const int64_t* rows, int32_t* inc,

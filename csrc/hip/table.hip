@@ -86,6 +86,60 @@ __global__ __launch_bounds__(256) void k_probe(TableDev t, const uint64_t* __res
   if (j == 0 && blk + g < nn) rows[blk + g] = r;
 }
 
+// Owner side of the sharded pull in one launch: probe every received key (one
+// 16-lane group per key, as k_probe) and copy its pull record (P floats,
+// zero padded to out_stride) straight into the answer buffer -- no dedup of
+// the received keys (a key asked by several peers is simply read twice).
+__global__ __launch_bounds__(256) void k_probe_gather(TableDev t, const uint64_t* __restrict__ h, int64_t n,
+                                                      int64_t* __restrict__ rows, float* __restrict__ out,
+                                                      int out_stride) {
+  __shared__ uint64_t q[16];
+  const int64_t blk = (int64_t)blockIdx.x * 16;
+  if (blk >= n) return;
+  if (threadIdx.x < 16) q[threadIdx.x] = (blk + threadIdx.x < n) ? h[blk + threadIdx.x] : kEmptyKey;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int sub = lane >> 4;
+  const int j = lane & 15;
+  const int g = threadIdx.x >> 4;
+  const uint64_t key = q[g];
+  int64_t r = -1;
+  if (key != kEmptyKey) {
+    const uint64_t b1 = bucket1(key, t.nb);
+    const uint64_t k1 = t.keys[b1 * kBucketSlots + j];
+    uint64_t m = (__ballot(k1 == key) >> (sub * 16)) & 0xFFFFull;
+    if (m) {
+      r = (int64_t)(b1 * kBucketSlots) + (__ffsll((long long)m) - 1);
+    } else {
+      const uint64_t b2 = bucket2(key, t.nb);
+      const uint64_t k2 = t.keys[b2 * kBucketSlots + j];
+      m = (__ballot(k2 == key) >> (sub * 16)) & 0xFFFFull;
+      if (m) {
+        r = (int64_t)(b2 * kBucketSlots) + (__ffsll((long long)m) - 1);
+      } else {
+        const uint32_t sn = t.stash_n ? *t.stash_n : 0u;
+        const uint32_t lim = sn < t.stash_cap ? sn : t.stash_cap;
+        int64_t found = -1;
+        for (uint32_t s = j; s < lim; s += 16)
+          if (t.stash_keys[s] == key) found = (int64_t)(t.nb * kBucketSlots) + s;
+        for (int off = 8; off > 0; off >>= 1) {
+          long long o = __shfl_xor((long long)found, off, 16);
+          found = found > o ? found : o;
+        }
+        r = found;
+      }
+    }
+  }
+  const int64_t e = blk + g;
+  if (e >= n) return;
+  if (j == 0) rows[e] = r;
+  if (key == kEmptyKey) return;  // exchange padding: nobody reads its record
+  // the group's 16 lanes copy the record (pull head = the row's first P floats)
+  const int P = kPullHead + t.dim;
+  float* o = out + e * (int64_t)out_stride;
+  for (int c = j; c < out_stride; c += 16) o[c] = (r >= 0 && c < P) ? t.values[r * (int64_t)t.stride + c] : 0.f;
+}
+
 __global__ void k_insert(TableDev t, const uint64_t* __restrict__ h, int64_t n, const int32_t* n_dev,
                          const int64_t* __restrict__ rows, SparseSGDConfig cfg, uint64_t seed,
                          int init_embedx, uint64_t* ovf, uint32_t* ovf_n) {
@@ -303,6 +357,12 @@ void launch_table_probe(const TableDev& t, const uint64_t* h, int64_t n, const i
                         int64_t* rows, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_probe, dim3(blocks_for(n, 16)), dim3(256), 0, s, t, h, n, n_dev, rows);
+}
+
+void launch_probe_gather(const TableDev& t, const uint64_t* h, int64_t n, int64_t* rows, float* out, int out_stride,
+                         hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_probe_gather, dim3(blocks_for(n, 16)), dim3(256), 0, s, t, h, n, rows, out, out_stride);
 }
 
 void launch_table_insert(const TableDev& t, const uint64_t* h, int64_t n, const int32_t* n_dev,

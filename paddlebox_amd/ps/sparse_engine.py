@@ -83,6 +83,7 @@ class _PullSlot:
             self.send_index = torch.empty(eng.max_keys, dtype=torch.int64, device=dev)
             self.ocnt = torch.zeros(eng.world, dtype=torch.int32, device=dev)
             self.rcnt = torch.zeros(eng.world, dtype=torch.int32, device=dev)  # keys received per peer (IPC)
+            self.rows_recv = torch.empty(n, dtype=torch.int64, device=dev)  # table row per received key
             self.resp = torch.empty(n, eng.P, device=dev)
             self.resp_back = torch.empty(n, eng.P, device=dev)
             self.rows_r = None
@@ -409,6 +410,17 @@ class SparseEngine:
                                    sl.rcnt)
         else:
             self.comm.all_to_all_single(sl.recv, sl.send)
+        if self.codec is None:
+            # owner answers in one launch: probe + record copy per received
+            # key, no dedup (a key asked by several peers is read twice)
+            rows_r = sl.rows_recv
+            self.table.t.probe_gather(sl.recv, rows_r, sl.resp)
+            if self.auto_insert and not self.test_mode:
+                miss = (rows_r < 0) & (sl.recv != -1)
+                if bool(miss.any()):
+                    self.table.insert_mixed(torch.unique(sl.recv[miss]), self.cfg.sgd)
+                    self.table.t.probe_gather(sl.recv, rows_r, sl.resp)
+            return self._answer(sl, st, L, rows_r)
         sl.ws_r.run(sl.recv, True)
         rows_r = self.table.probe(sl.ws_r.uniq_h, sl.ws_r.u_count)
         if self.auto_insert and not self.test_mode:
@@ -418,10 +430,10 @@ class SparseEngine:
                 self.table.insert_mixed(sl.ws_r.uniq_h[:U][miss], self.cfg.sgd)
                 rows_r = self.table.probe(sl.ws_r.uniq_h, sl.ws_r.u_count)
         # owner answers straight from the table rows (no intermediate pull buffer)
-        if self.codec is not None:
-            self.table.t.codec_pull(self.codec.native(), rows_r, sl.ws_r.uid, None, sl.resp.shape[0], sl.resp)
-        else:
-            self.table.t.gather_rows_by_uid(rows_r, sl.ws_r.uid, sl.resp)
+        self.table.t.codec_pull(self.codec.native(), rows_r, sl.ws_r.uid, None, sl.resp.shape[0], sl.resp)
+        return self._answer(sl, st, L, rows_r)
+
+    def _answer(self, sl: _PullSlot, st: PullState, L: int, rows_r: torch.Tensor) -> PullState:
         if self.xmesh is not None:
             # answers: as many rows to each peer as it sent keys
             self.xmesh[1].exchange(sl.resp.view(self.world, -1), sl.resp_back.view(self.world, -1), sl.rcnt,
@@ -489,13 +501,19 @@ class SparseEngine:
         return self.push_recv
 
     def _owner_update(self, sl: _PullSlot, rows_r: torch.Tensor, recv: torch.Tensor):
-        """Owner side of the push: each unique key got at most one merged record
-        per sender; merge them and apply sparse Adagrad in one kernel."""
+        """Owner side of the push: each key got at most one merged record per
+        sender.  Plain rows: rows_r holds the row of every received entry;
+        the entries of one row elect a leader that sums the others' records
+        and applies sparse Adagrad (two launches, no dedup).  Codec rows (or
+        a dim without the vector kernels): dedup the received keys, merge,
+        then the codec / generic update."""
         self._seed += 1
         ws = sl.ws_r
-        if self.codec is None and self.table.t.push_adagrad_seg(rows_r, recv, ws.perm, ws.seg, ws.cnt, ws.u_count,
-                                                                self._sgd_native, self._seed):
-            return
+        if self.codec is None:
+            if self.table.t.owner_push(rows_r, recv, self._sgd_native, self._seed):
+                return
+            ws.run(sl.recv, True)
+            rows_r = self.table.probe(ws.uniq_h, ws.u_count)
         self.push_merged.zero_()
         self._hip.push_merge_records(recv, ws.perm, ws.uid, ws.u_count[1:], self.xdim, self.push_merged)
         self._update_rows(rows_r, self.push_merged, ws.u_count)

@@ -1,0 +1,31 @@
+"""Per-step kernel breakdown of a rocprofv3 kernel trace: the last --steps
+training steps (delimited by an anchor kernel, default the tower forward),
+average time per kernel name and the launch count per step."""
+import argparse
+import collections
+import csv
+
+ap = argparse.ArgumentParser()
+ap.add_argument("trace")
+ap.add_argument("--anchor", default="k_tower_fwd")
+ap.add_argument("--steps", type=int, default=10)
+a = ap.parse_args()
+rows = list(csv.DictReader(open(a.trace)))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if a.anchor in r["Kernel_Name"]]
+idx = idx[-(a.steps + 1):]
+agg = collections.defaultdict(float)
+cnt = collections.Counter()
+busy = 0.0
+for s, e in zip(idx[:-1], idx[1:]):
+    for r in rows[s:e]:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        n = r["Kernel_Name"].replace("pbx::(anonymous namespace)::", "").replace("void ", "").split("(")[0][:60]
+        agg[n] += d
+        cnt[n] += 1
+        busy += d
+n = len(idx) - 1
+span = (int(rows[idx[-1]]["Start_Timestamp"]) - int(rows[idx[0]]["Start_Timestamp"])) / 1e3 / n
+print(f"steps={n} wall/step={span:.1f}us kernel-busy/step={busy / n:.1f}us launches/step={sum(cnt.values()) / n:.1f}")
+for k, v in sorted(agg.items(), key=lambda kv: -kv[1]):
+    print(f"{k:60s} {cnt[k] / n:5.1f}x {v / n:8.1f}us")
