@@ -174,6 +174,9 @@ def main():
     from paddlebox_amd.ps.config import PSConfig
     from paddlebox_amd.ps.sparse_engine import SparseEngine
 
+    if args.same_gpu:
+        # all ranks' spinning IPC collectives share one GPU's workgroup slots
+        os.environ.setdefault("PBX_IPC_MAX_BLOCKS", str(max(8, 256 // max(1, world))))
     gpu_index = 0 if args.same_gpu else local_rank
     torch.cuda.set_device(gpu_index)
     device = torch.device("cuda", gpu_index)

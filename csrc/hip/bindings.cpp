@@ -479,6 +479,51 @@ static void push_merge(const Tensor& dout, int col_offset, const Tensor& cvm, in
   launch_push_merge(a, cur_stream());
 }
 
+// Sharded push, fused: per-unique merged records written straight into their
+// send slots (send[send_index[u]]); acc = all-zero straddle scratch [>= U_cap,
+// stride] (kept zero), inc = [>= ceil(n/64)] int32 scratch.  False when the
+// dim / layout has no fused instantiation (caller: zero + push_merge).
+static bool push_merge_send(const Tensor& dout, int col_offset, const Tensor& cvm, bool use_cvm, bool clk_filter,
+                            int E, const Tensor& perm, const Tensor& uid, const Tensor& occ_slot, const Tensor& occ_ins,
+                            const Tensor& slot_ids, const Tensor& n_valid, Tensor acc, Tensor inc, Tensor send,
+                            const Tensor& send_index, float bs_scale, int dim, int embed_thres_size) {
+  check_cuda(dout, "dout");
+  check_cuda(cvm, "cvm");
+  check_cuda(acc, "acc");
+  check_cuda(send, "send");
+  check_cuda(send_index, "send_index");
+  if (cvm.dim() != 2 || cvm.size(1) != 2 || E != 3 + dim) return false;
+  PBX_CHECK(acc.dim() == 2 && acc.is_contiguous() && acc.size(0) >= perm.numel(), "push_merge_send: acc rows");
+  PBX_CHECK(send.dim() == 2 && send.is_contiguous(), "push_merge_send: send");
+  PBX_CHECK(send_index.scalar_type() == torch::kInt64 && send_index.numel() >= perm.numel(),
+            "push_merge_send: send_index");
+  PBX_CHECK(inc.numel() * 64 >= perm.numel(), "push_merge_send: inc too small");
+  PushMergeArgs a;
+  a.dout = ptr<float>(dout);
+  a.out_stride = (int)dout.size(1);
+  a.col_offset = col_offset;
+  a.cvm = ptr<float>(cvm);
+  a.cvm_offset = 2;
+  a.use_cvm = use_cvm;
+  a.clk_filter = clk_filter;
+  a.E = E;
+  a.perm = ptr<int32_t>(perm);
+  a.uid = ptr<int32_t>(uid);
+  a.occ_slot = ptr<int32_t>(occ_slot);
+  a.occ_ins = ptr<int32_t>(occ_ins);
+  a.slot_ids = ptr<float>(slot_ids);
+  a.n_valid = ptr<int32_t>(n_valid);
+  a.n = perm.numel();
+  a.push = ptr<float>(acc);
+  a.push_stride = (int)acc.size(1);
+  a.push_index = nullptr;
+  a.bs_scale = bs_scale;
+  a.dim = dim;
+  a.embed_thres_size = use_cvm ? 0 : embed_thres_size;
+  return launch_push_merge_send(a, dim, ptr<float>(send), (int)send.size(1), ptr<int64_t>(send_index),
+                                ptr<int32_t>(inc), cur_stream());
+}
+
 static void push_merge_records(const Tensor& rec, const Tensor& perm, const Tensor& uid, const Tensor& n_valid,
                                int dim, Tensor out) {
   check_cuda(rec, "rec");
@@ -1081,6 +1126,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("use_cvm"), py::arg("clk_filter"), py::arg("E"), py::arg("perm"), py::arg("uid"), py::arg("occ_slot"),
         py::arg("occ_ins"), py::arg("slot_ids"), py::arg("n_valid"), py::arg("push"), py::arg("push_index"),
         py::arg("bs_scale"), py::arg("dim"), py::arg("embed_thres_size") = 0);
+  m.def("push_merge_send", &push_merge_send);
   m.def("push_merge_records", &push_merge_records);
   m.def("shard_pack", &shard_pack);
   m.def("shard_pack_hash", &shard_pack_hash, py::arg("uniq_h"), py::arg("u_count"), py::arg("nranks"), py::arg("cap"),

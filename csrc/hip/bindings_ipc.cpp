@@ -56,7 +56,9 @@ class IpcComm {
     IPC_CHECK(world >= 1 && world <= kIpcMaxRanks && rank >= 0 && rank < world, "rank / world");
     IPC_CHECK(slot_bytes > 0 && slot_bytes % 16 == 0, "slot_bytes must be a positive multiple of 16");
     IPC_CHECK(state.is_cuda() && state.scalar_type() == torch::kInt64 && state.numel() >= 4, "state");
-    IPC_CHECK(blocks >= 1 && blocks <= 256, "blocks");
+    // power of two: the last block is found by counter % grid, and the
+    // 32-bit counters wrap
+    IPC_CHECK(blocks >= 1 && blocks <= 1024 && (blocks & (blocks - 1)) == 0, "blocks must be a power of two <= 1024");
     IPC_CHECK(depth >= 2 && depth <= 16, "depth in 2..16");
     IPC_CHECK(spin_limit > 0, "spin_limit");
     std::memset(&p_, 0, sizeof(p_));

@@ -50,13 +50,24 @@ __device__ __forceinline__ unsigned char* slot_ptr(const IpcPeers& pt, int owner
   return pt.inbox[owner] + ((((int64_t)slot * 2 + phase) * W + src) * s);
 }
 
-// grid-strided copy of n bytes (16-B vectors + byte tail; both ends 16-B aligned)
+// grid-strided copy of n bytes (16-B vectors + byte tail; both ends 16-B
+// aligned).  Four independent 16-B loads are in flight per lane before their
+// stores: a copy loop with one load per iteration waits a full (remote)
+// memory latency per 16 B and runs at a fraction of the link / HBM rate.
 __device__ __forceinline__ void put_bytes(unsigned char* dst, const unsigned char* src, int64_t n, int64_t tid,
                                           int64_t nth) {
   const int64_t nv = n >> 4;
   const uint4* s4 = reinterpret_cast<const uint4*>(src);
   uint4* d4 = reinterpret_cast<uint4*>(dst);
-  for (int64_t i = tid; i < nv; i += nth) d4[i] = s4[i];
+  int64_t i = tid;
+  for (; i + 3 * nth < nv; i += 4 * nth) {
+    const uint4 a = s4[i], b = s4[i + nth], c = s4[i + 2 * nth], d = s4[i + 3 * nth];
+    d4[i] = a;
+    d4[i + nth] = b;
+    d4[i + 2 * nth] = c;
+    d4[i + 3 * nth] = d;
+  }
+  for (; i < nv; i += nth) d4[i] = s4[i];
   if (tid < (n & 15)) dst[(nv << 4) + tid] = src[(nv << 4) + tid];
 }
 

@@ -264,6 +264,11 @@ bool launch_push_adagrad_seg(const TableDev& t, const int64_t* rows, const float
 // instantiation (caller falls back to launch_push_merge + launch_push_adagrad).
 bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const int64_t* rows, int32_t* inc,
                              const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s);
+// Sharded push: the same merge, each unique's summed record written to
+// send[send_index[u]] (rows with send_index -1 dropped); a.push / a.push_stride
+// = the all-zero straddle accumulator [>= U_cap rows]; no memset of send.
+bool launch_push_merge_send(const PushMergeArgs& a, int dim, float* send, int send_stride, const int64_t* send_index,
+                            int32_t* inc, hipStream_t s);
 
 // ---------------------------------------------------------------- dense ops
 void launch_data_norm_fwd(const float* x, int N, int C, const float* bsize, const float* bsum,

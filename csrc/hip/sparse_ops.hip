@@ -534,11 +534,38 @@ __global__ __launch_bounds__(256) void k_push_adagrad_seg(TableDev t, const int6
 // occurrence files u in inc[] for k_push_finish, which applies it and
 // re-zeroes acc[u]: no merged-record buffer, no memset, one read of dout.
 // (Reference: PushMergeCopy + PushSparseGPU, box_wrapper.cu:417-512.)
-template <int D>
-__global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, TableDev t, const int64_t* __restrict__ rows,
-                                                          float* __restrict__ acc, int acc_stride,
-                                                          int32_t* __restrict__ inc, float neg_bs,
-                                                          SparseSGDConfig cfg, uint64_t seed) {
+// What a completed run (one unique key's summed push record) turns into:
+// the single-shard step applies Adagrad to the key's table row; the sharded
+// step writes the record into the key's slot of the send buffer (no memset of
+// the send buffer, no atomics for the runs that fit in a wave).
+struct ApplyEmit {
+  TableDev t;
+  const int64_t* rows;
+  SparseSGDConfig cfg;
+  uint64_t seed;
+  template <int D>
+  __device__ __forceinline__ void emit(int32_t u, const float* rec) const {
+    const int64_t r = rows[u];
+    if (r >= 0) adagrad_row<D>(t.values + r * (int64_t)t.stride, rec, cfg, seed, r);
+  }
+};
+struct SendEmit {
+  float* send;
+  int stride;
+  const int64_t* index;  // send row per unique (-1: dropped on overflow)
+  template <int D>
+  __device__ __forceinline__ void emit(int32_t u, const float* rec) const {
+    const int64_t j = index[u];
+    if (j < 0) return;
+    float4* d = reinterpret_cast<float4*>(send + j * (int64_t)stride);
+#pragma unroll
+    for (int i = 0; i < RowF<D>::kQ4; ++i) d[i] = make_float4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
+  }
+};
+
+template <int D, class Emit>
+__global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, Emit em, float* __restrict__ acc,
+                                                          int acc_stride, int32_t* __restrict__ inc, float neg_bs) {
   constexpr int Q = 3 + D;
   const PushMergeArgs& a = src.a;
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -586,8 +613,7 @@ __global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, TableD
   for (int c = 2; c < Q; ++c) rec[kPushEmbedG + (c - 2)] = g[c] * neg_bs;
   const bool straddle = (u == u_last && cont_next) || (u == u_first && cont_prev);
   if (!straddle) {
-    const int64_t r = rows[u];
-    if (r >= 0) adagrad_row<D>(t.values + r * (int64_t)t.stride, rec, cfg, seed, r);
+    em.template emit<D>(u, rec);
     return;
   }
   float* dst = acc + (int64_t)u * acc_stride;
@@ -596,11 +622,9 @@ __global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, TableD
   for (int c = 1; c < RowF<D>::kQ; ++c) atomicAdd(&dst[c], rec[c]);
 }
 
-template <int D>
-__global__ __launch_bounds__(256) void k_push_finish(TableDev t, const int64_t* __restrict__ rows,
-                                                     float* __restrict__ acc, int acc_stride,
-                                                     const int32_t* __restrict__ inc, const int32_t* n_valid,
-                                                     SparseSGDConfig cfg, uint64_t seed) {
+template <int D, class Emit>
+__global__ __launch_bounds__(256) void k_push_finish(Emit em, float* __restrict__ acc, int acc_stride,
+                                                     const int32_t* __restrict__ inc, const int32_t* n_valid) {
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= ((int64_t)*n_valid + 63) / 64) return;
   const int32_t u = inc[w];
@@ -611,8 +635,7 @@ __global__ __launch_bounds__(256) void k_push_finish(TableDev t, const int64_t* 
   float4* a4 = reinterpret_cast<float4*>(ap);
 #pragma unroll
   for (int i = 0; i < RowF<D>::kQ4; ++i) a4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  const int64_t r = rows[u];
-  if (r >= 0) adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
+  em.template emit<D>(u, g);
 }
 
 // Owner-side push of the sharded step, no dedup of the received keys.  Pass
@@ -932,19 +955,42 @@ bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const in
   const dim3 g(nblk(a.n)), gf(nblk((a.n + 63) / 64)), b(256);
   DoutSource src{a};
   const float neg_bs = -a.bs_scale;
-#define PBX_MERGE_APPLY(D)                                                                                   \
-  if (vec_push_ok<D>(t, a.push_stride)) {                                                                    \
-    hipLaunchKernelGGL(k_push_merge_apply<D>, g, b, 0, s, src, t, rows, a.push, a.push_stride, inc, neg_bs,  \
-                       cfg, seed);                                                                           \
-    hipLaunchKernelGGL(k_push_finish<D>, gf, b, 0, s, t, rows, a.push, a.push_stride, inc, a.n_valid, cfg,   \
-                       seed);                                                                                \
-    return true;                                                                                             \
+  const ApplyEmit em{t, rows, cfg, seed};
+#define PBX_MERGE_APPLY(D)                                                                                    \
+  if (vec_push_ok<D>(t, a.push_stride)) {                                                                     \
+    hipLaunchKernelGGL((k_push_merge_apply<D, ApplyEmit>), g, b, 0, s, src, em, a.push, a.push_stride, inc,   \
+                       neg_bs);                                                                               \
+    hipLaunchKernelGGL((k_push_finish<D, ApplyEmit>), gf, b, 0, s, em, a.push, a.push_stride, inc, a.n_valid); \
+    return true;                                                                                              \
   }
   PBX_MERGE_APPLY(8)
   PBX_MERGE_APPLY(16)
   PBX_MERGE_APPLY(4)
   PBX_MERGE_APPLY(32)
 #undef PBX_MERGE_APPLY
+  return false;
+}
+
+bool launch_push_merge_send(const PushMergeArgs& a, int dim, float* send, int send_stride, const int64_t* send_index,
+                            int32_t* inc, hipStream_t s) {
+  if (a.cvm_offset != 2 || a.n_valid == nullptr || a.E != 3 + dim || send_stride % 4 != 0) return false;
+  if (a.n <= 0) return true;
+  const dim3 g(nblk(a.n)), gf(nblk((a.n + 63) / 64)), b(256);
+  DoutSource src{a};
+  const float neg_bs = -a.bs_scale;
+  const SendEmit em{send, send_stride, send_index};
+#define PBX_MERGE_SEND(D)                                                                                     \
+  if (dim == D && send_stride >= RowF<D>::kQ4 * 4 && a.push_stride >= RowF<D>::kQ4 * 4 && a.push_stride % 4 == 0) { \
+    hipLaunchKernelGGL((k_push_merge_apply<D, SendEmit>), g, b, 0, s, src, em, a.push, a.push_stride, inc,    \
+                       neg_bs);                                                                               \
+    hipLaunchKernelGGL((k_push_finish<D, SendEmit>), gf, b, 0, s, em, a.push, a.push_stride, inc, a.n_valid);  \
+    return true;                                                                                              \
+  }
+  PBX_MERGE_SEND(8)
+  PBX_MERGE_SEND(16)
+  PBX_MERGE_SEND(4)
+  PBX_MERGE_SEND(32)
+#undef PBX_MERGE_SEND
   return false;
 }
 

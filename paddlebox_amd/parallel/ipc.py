@@ -56,10 +56,17 @@ class IpcMesh:
         h = _native.hip()
         W = self.world
         if blocks is None:
-            # ~64 KB of payload per workgroup: enough 16-B streams in flight
-            # to fill 7 xGMI links (and the local copy-out), without hundreds
-            # of flag pollers on small collectives
-            blocks = max(16, min(256, (W * self.slot_bytes) >> 16))
+            # ~16 KB of payload per workgroup (4 x 16 B in flight per lane:
+            # about one pass of the unrolled copy loop), so the puts and the
+            # copy-out are not latency-bound; 16..256 workgroups
+            # (PBX_IPC_MAX_BLOCKS caps it: every workgroup of every rank's
+            # collective must be resident at once -- the waits spin -- which
+            # matters when several ranks share one GPU, see bench --same-gpu)
+            cap = int(os.environ.get("PBX_IPC_MAX_BLOCKS", "256"))
+            blocks = max(min(16, cap), min(cap, (W * self.slot_bytes) >> 14))
+        # power of two: the arrive / depart counters find the last block by
+        # count % grid and wrap at 2^32
+        blocks = 1 << max(0, int(blocks).bit_length() - 1)
         self.inbox = torch.zeros(self.depth * 2 * W * self.slot_bytes, dtype=torch.uint8, device=self.device)
         self.flags = torch.zeros(2 * W, dtype=torch.int64, device=self.device)
         self.state = torch.zeros(4, dtype=torch.int64, device=self.device)

@@ -210,6 +210,9 @@ class SparseEngine:
                 self.push_send = torch.empty(n, self.Q, device=self.device)
                 self.push_recv = torch.empty(n, self.Q, device=self.device)
                 self.push_merged = torch.empty(n, self.Q, device=self.device)
+                # fused merge straddle scratch (all-zero between steps) + per-wave run owners
+                self.push_acc = torch.zeros(self.max_keys, self.Q, device=self.device)
+                self.push_inc = torch.empty((self.max_keys + 63) // 64 + 1, dtype=torch.int32, device=self.device)
             else:
                 self.push_buf = torch.empty(self.max_keys, self.Q, device=self.device)
                 if self.codec is not None:  # decoded pull records of the batch's unique keys
@@ -483,6 +486,14 @@ class SparseEngine:
                          ws.u_count[1:], push[:L], None, float(bs_scale), self.dim, ets)
             self._seed += 1
             self._update_rows(st.rows, push[:L], ws.u_count)
+            return
+        if (sp.cvm_offset == 2 and cvm.shape[1] == 2 and self.codec is None
+                and h.push_merge_send(dout, col_offset, cvm.contiguous(), sp.use_cvm, sp.clk_filter, self.E,
+                                      ws.perm[:L], ws.uid, sl.occ_slot, sl.occ_ins, self._slot_ids(st.S),
+                                      ws.u_count[1:], self.push_acc, self.push_inc, self.push_send, st.send_index,
+                                      float(bs_scale), self.dim, ets)):
+            # merged records went straight into their send slots
+            self._owner_update(sl, st.rows_r, self._push_exchange(sl))
             return
         self.push_send.zero_()
         h.push_merge(dout, col_offset, cvm.contiguous(), sp.cvm_offset, sp.use_cvm, sp.clk_filter, self.E,
