@@ -147,6 +147,9 @@ def main():
                          "then run on the IPC meshes); exercises the N-GPU step on one GPU")
     ap.add_argument("--force-collectives", action="store_true",
                     help="run the multi-GPU exchange/all-reduce path even on 1 rank (rehearsal)")
+    ap.add_argument("--dedup", choices=("on", "off"), default="on",
+                    help="FLAGS_enable_pullpush_dedup_keys: off = single-shard step without a key dedup "
+                         "(per-occurrence probe + leader-elected push merge)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank launch (no GPU, no model); prints ranks_seen")
     args = ap.parse_args()
@@ -221,7 +224,7 @@ def main():
                   f"{int(math.ceil(B * S / world * 1.25)) + 64})")
     engine = SparseEngine(cfg, max_keys=B * S, device=device, capacity=synth.total_features,
                           slot_ids=[float(s + 1) for s in range(S)], auto_insert=args.no_prefill,
-                          exchange_capacity=xcap, exchange=args.sparse_exchange)
+                          exchange_capacity=xcap, exchange=args.sparse_exchange, dedup=args.dedup == "on")
 
     t0 = time.time()
     if not args.no_prefill:
@@ -446,6 +449,7 @@ def main():
                 "sparse_exchange": engine.exchange_mode,
                 "same_gpu_rehearsal": bool(args.same_gpu),
                 "pipelined_pull": bool(graphed is not None and graphed.prefetch is not None),
+                "key_dedup": bool(engine.dedup),
                 "mlp_dtype": args.mlp_dtype,
                 "unique_keys_per_batch": round(sum(u_per_batch) / len(u_per_batch), 1),
                 "keys_per_batch": l_per_batch,

@@ -3,6 +3,8 @@
 #include <ATen/hip/HIPContext.h>
 #include <torch/extension.h>
 
+#include <cstring>
+
 #include <stdexcept>
 
 #include "kernels.h"
@@ -182,6 +184,98 @@ class GpuTable {
     launch_probe_gather(view(), ptr<uint64_t>(h), h.numel(), ptr<int64_t>(rows), ptr<float>(out), (int)out.size(1),
                         cur_stream());
   }
+  // no-dedup pull: rows[k] = row of raw feasign keys[k] (-1: padding / absent)
+  void probe_raw(const Tensor& keys, Tensor rows) {
+    check_cuda(keys, "keys");
+    check_cuda(rows, "rows");
+    PBX_CHECK(keys.scalar_type() == torch::kInt64 && keys.is_contiguous(), "probe_raw: keys must be int64");
+    PBX_CHECK(rows.scalar_type() == torch::kInt64 && rows.is_contiguous() && rows.numel() >= keys.numel(),
+              "probe_raw: rows");
+    launch_probe_raw(view(), ptr<int64_t>(keys), keys.numel(), ptr<int64_t>(rows), cur_stream());
+  }
+  Tensor& owner_lock() {
+    if (!lock_.defined()) {
+      auto opt4 = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device_);
+      lock_ = torch::full({values_.size(0)}, -1, opt4);  // free; every apply resets what it took
+    }
+    return lock_;
+  }
+  Tensor& lead_buf(int64_t n) {
+    if (!lead_.defined() || lead_.numel() < n) lead_ = torch::empty({n}, owner_lock().options());
+    return lead_;
+  }
+  // no-dedup push (one record per occurrence, merged per row by leader
+  // election, then Adagrad); acc: all-zero scratch [>= n, stride], kept zero.
+  // False if not vectorisable for this dim / layout.
+  bool push_occ(const Tensor& dout, int col_offset, const Tensor& cvm, bool use_cvm, bool clk_filter, int E,
+                const Tensor& occ_slot, const Tensor& occ_ins, const Tensor& slot_ids, const Tensor& rows, Tensor acc,
+                float bs_scale, const SparseSGDConfig& cfg, uint64_t seed, int embed_thres_size) {
+    check_cuda(dout, "dout");
+    check_cuda(cvm, "cvm");
+    check_cuda(rows, "rows");
+    check_cuda(acc, "acc");
+    const int64_t n = rows.numel();
+    if (cvm.dim() != 2 || cvm.size(1) != 2 || E != 3 + dim_) return false;
+    PBX_CHECK(acc.dim() == 2 && acc.is_contiguous() && acc.size(0) >= n * kOccRep, "push_occ: acc rows (kOccRep x n)");
+    PBX_CHECK(occ_slot.numel() >= n && occ_ins.numel() >= n, "push_occ: occurrence maps");
+    PBX_CHECK(n < (int64_t)INT32_MAX, "push_occ: too many occurrences");
+    PBX_CHECK(values_.size(0) < (int64_t)0xFFFFFFFFll, "push_occ: table rows must fit 32 bits");
+    PushMergeArgs a;
+    a.dout = ptr<float>(dout);
+    a.out_stride = (int)dout.size(1);
+    a.col_offset = col_offset;
+    a.cvm = ptr<float>(cvm);
+    a.cvm_offset = 2;
+    a.use_cvm = use_cvm;
+    a.clk_filter = clk_filter;
+    a.E = E;
+    a.perm = nullptr;
+    a.uid = nullptr;
+    a.occ_slot = ptr<int32_t>(occ_slot);
+    a.occ_ins = ptr<int32_t>(occ_ins);
+    a.slot_ids = ptr<float>(slot_ids);
+    a.n_valid = nullptr;
+    a.n = n;
+    a.push = ptr<float>(acc);
+    a.push_stride = (int)acc.size(1);
+    a.push_index = nullptr;
+    a.bs_scale = bs_scale;
+    a.dim = dim_;
+    a.embed_thres_size = use_cvm ? 0 : embed_thres_size;
+    return launch_push_occ(a, view(), ptr<int64_t>(rows), ptr<int32_t>(owner_lock()), ptr<int32_t>(lead_buf(n)), cfg,
+                           seed, cur_stream());
+  }
+  // streaming checkpoint of this table (ckpt.hip / ckpt_saver.cpp): kind 0 =
+  // numpy batch model (keys_path / vals_path), 1 = xbox text (keys_path);
+  // mode 0 all / 1 base / 2 delta.  Returns (rows, chunks, gpu_s, write_s,
+  // total_s, saved mixed keys (int64 CPU tensor) or None).
+  py::tuple save_stream(int kind, int mode, bool reset_delta, float base_threshold, float delta_threshold,
+                        float delta_keep_days, float nonclk_coeff, float clk_coeff, float embedx_threshold,
+                        const std::string& keys_path, const std::string& vals_path, int64_t chunk_rows, int threads,
+                        bool collect) {
+    SaveSelect sel;
+    sel.mode = mode;
+    sel.reset_delta = reset_delta ? 1 : 0;
+    sel.base_threshold = base_threshold;
+    sel.delta_threshold = delta_threshold;
+    sel.delta_keep_days = delta_keep_days;
+    sel.nonclk_coeff = nonclk_coeff;
+    sel.clk_coeff = clk_coeff;
+    std::vector<uint64_t> mixed;
+    SaveStats st;
+    {
+      py::gil_scoped_release nogil;
+      st = stream_save_table(view(), values_.size(0), kind, sel, embedx_threshold, keys_path, vals_path, chunk_rows,
+                             threads, collect ? &mixed : nullptr, device_, cur_stream());
+    }
+    py::object keys = py::none();
+    if (collect) {
+      auto k = torch::empty({(int64_t)mixed.size()}, torch::TensorOptions().dtype(torch::kInt64));
+      if (!mixed.empty()) std::memcpy(k.data_ptr(), mixed.data(), mixed.size() * sizeof(uint64_t));
+      keys = py::cast(k);
+    }
+    return py::make_tuple(st.rows, st.chunks, st.gpu_s, st.write_s, st.total_s, keys);
+  }
   // owner side of the sharded push without a dedup of the received keys
   // (entries sharing a row elect a leader through a per-row lock word, see
   // launch_owner_push); rec is modified (records summed into the leaders').
@@ -193,13 +287,8 @@ class GpuTable {
     PBX_CHECK(rec.dim() == 2 && rec.is_contiguous() && rec.size(0) >= n && rec.size(1) >= push_width(dim_),
               "owner_push: rec");
     PBX_CHECK(n < (int64_t)INT32_MAX, "owner_push: too many records");
-    if (!lock_.defined()) {
-      auto opt4 = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device_);
-      lock_ = torch::full({values_.size(0)}, -1, opt4);  // free; every apply resets what it took
-    }
-    if (!lead_.defined() || lead_.numel() < n) lead_ = torch::empty({n}, lock_.options());
-    return launch_owner_push(view(), ptr<int64_t>(rows), ptr<float>(rec), (int)rec.size(1), n, ptr<int32_t>(lock_),
-                             ptr<int32_t>(lead_), cfg, seed, cur_stream());
+    return launch_owner_push(view(), ptr<int64_t>(rows), ptr<float>(rec), (int)rec.size(1), n,
+                             ptr<int32_t>(owner_lock()), ptr<int32_t>(lead_buf(n)), cfg, seed, cur_stream());
   }
   // single-shard push: merge per unique key + Adagrad in one pass (acc: all-zero
   // scratch [>= U_cap, stride], kept zero; inc: [>= ceil(n/64)] int32 scratch)
@@ -387,7 +476,7 @@ static void fill_occurrence(const Tensor& lod, int S, int B, Tensor occ_slot, Te
   launch_fill_occurrence(ptr<int64_t>(lod), S, B, ptr<int32_t>(occ_slot), ptr<int32_t>(occ_ins), cur_stream());
 }
 
-static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_index, const Tensor& uid,
+static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_index, const c10::optional<Tensor>& uid,
                             const Tensor& lod, int S, int B, int E, Tensor out, int col_offset, bool use_cvm,
                             int cvm_offset, bool clk_filter, float pad_value, bool need_filter, float show_coeff,
                             float clk_coeff, float threshold, int quant_ratio, bool embed_threshold_filter,
@@ -395,16 +484,19 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
                             int dense_col, const c10::optional<Tensor>& occ_slot,
                             const c10::optional<Tensor>& occ_ins) {
   check_cuda(src, "src");
-  check_cuda(uid, "uid");
   check_cuda(lod, "lod");
   check_cuda(out, "out");
   PBX_CHECK(src.dim() == 2 && src.size(1) >= E, "src width < E");
+  // uid None: record index = occurrence index (no-dedup pull; the caller
+  // sizes the occurrence maps to its key buffer -- no device read here, the
+  // call is graph-captured)
+  const int64_t L = uid.has_value() && uid->defined() ? uid->numel() : 0;
   PBX_CHECK(out.dim() == 2 && out.size(0) == B, "out shape");
   SeqpoolCvmArgs a;
   a.src = ptr<float>(src);
   a.src_stride = (int)src.size(1);
   a.src_index = optr<int64_t>(src_index);
-  a.uid = ptr<int32_t>(uid);
+  a.uid = optr<int32_t>(uid);
   a.lod = ptr<int64_t>(lod);
   a.S = S;
   a.B = B;
@@ -427,7 +519,7 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
   PBX_CHECK(col_offset + (int64_t)S * seqpool_cvm_out_width(a) <= out.size(1), "out too narrow");
   if (occ_slot.has_value() && occ_slot->defined()) {  // occurrence map written by the same launch
     PBX_CHECK(occ_ins.has_value() && occ_ins->defined(), "occ_ins required with occ_slot");
-    PBX_CHECK(occ_slot->numel() >= uid.numel() && occ_ins->numel() >= uid.numel(), "occ buffers too small");
+    PBX_CHECK(occ_slot->numel() >= L && occ_ins->numel() >= L, "occ buffers too small");
     a.occ_slot = ptr<int32_t>(*occ_slot);
     a.occ_ins = ptr<int32_t>(*occ_ins);
   }
@@ -1077,6 +1169,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("push_adagrad_seg", &GpuTable::push_adagrad_seg)
       .def("push_merge_apply", &GpuTable::push_merge_apply)
       .def("probe_gather", &GpuTable::probe_gather)
+      .def("probe_raw", &GpuTable::probe_raw)
+      .def("save_stream", &GpuTable::save_stream)
+      .def_property_readonly_static("occ_replicas", [](py::object) { return kOccRep; })
+      .def("push_occ", &GpuTable::push_occ)
       .def("owner_push", &GpuTable::owner_push)
       .def("codec_pull", &GpuTable::codec_pull, py::arg("codec"), py::arg("rows"), py::arg("uid"), py::arg("n_dev"),
            py::arg("n"), py::arg("out"))

@@ -3,6 +3,9 @@
 // csrc/hip/bindings.cpp calls these with raw pointers + the current stream.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
 #include <cstddef>
 #include <cstdint>
 
@@ -267,6 +270,46 @@ bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const in
 // Sharded push: the same merge, each unique's summed record written to
 // send[send_index[u]] (rows with send_index -1 dropped); a.push / a.push_stride
 // = the all-zero straddle accumulator [>= U_cap rows]; no memset of send.
+// No-dedup single-shard push: rows[k] = table row of occurrence k (a.n of
+// them); a.push / a.push_stride = all-zero accumulator [>= kOccRep * n rows]
+// (kept zero); lock = per-table-row int32 (-1 = free), lead = [n] scratch.
+constexpr int kOccRep = 8;
+bool launch_push_occ(const PushMergeArgs& a, const TableDev& t, const int64_t* rows, int32_t* lock, int32_t* lead,
+                     const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s);
+// Streaming checkpoint (ckpt.hip / ckpt_saver.cpp).  mode 0 = every row
+// (batch model), 1 = xbox base, 2 = xbox delta (ctr_accessor.cc:102-170).
+struct SaveSelect {
+  int mode = 0;
+  int reset_delta = 0;
+  float base_threshold = 0.f;
+  float delta_threshold = 0.f;
+  float delta_keep_days = 16.f;
+  float nonclk_coeff = 0.1f;
+  float clk_coeff = 1.f;
+};
+// Compact the selected rows of flat row range [r0, r1) (buckets then stash)
+// into okeys (unmixed feasigns) / ovals (stride floats per row) at
+// positions atomically taken from *count; resets delta_score if asked.
+void launch_save_chunk(const TableDev& t, int64_t r0, int64_t r1, const SaveSelect& sel, uint64_t* okeys,
+                       float* ovals, unsigned long long* count, hipStream_t s);
+struct SaveStats {
+  int64_t rows = 0;
+  int64_t chunks = 0;
+  double gpu_s = 0, write_s = 0, total_s = 0;
+};
+// Host driver: walks the table in chunks of chunk_rows row slots through two
+// device buffers and pinned host buffers into writer threads.  kind 0: numpy
+// batch model (keys_path .npy uint64 [N], vals_path .npy f32 [N, stride]);
+// kind 1: xbox text (keys_path, "feasign\tslot unseen delta show click
+// embed_w g2sum [embedx.. embedx_g2sum]", embedx only when score >=
+// embedx_threshold and mf_size != 0).  saved_mixed (optional): the mixed keys
+// of the saved rows are appended (for tiers that mirror the delta reset).
+SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, const SaveSelect& sel,
+                            float embedx_threshold, const std::string& keys_path, const std::string& vals_path,
+                            int64_t chunk_rows, int threads, std::vector<uint64_t>* saved_mixed, int device,
+                            hipStream_t s);
+// Probe raw feasigns (mixed in the kernel, -1 = padding -> row -1).
+void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows, hipStream_t s);
 bool launch_push_merge_send(const PushMergeArgs& a, int dim, float* send, int send_stride, const int64_t* send_index,
                             int32_t* inc, hipStream_t s);
 

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
       a.occ_slot[k] = s;
       a.occ_ins[k] = b;
     }
-    const int32_t u = a.uid[k];
+    const int32_t u = a.uid ? a.uid[k] : (int32_t)k;
     if (u < 0) continue;
     const int64_t ri = a.src_index ? a.src_index[u] : (int64_t)u;
     if (ri < 0) continue;
@@ -198,7 +198,7 @@ __global__ void k_seqpool_cvm_generic(SeqpoolCvmArgs a) {
   for (int c = 0; c < E; ++c) {
     float acc = a.pad_value;
     for (int64_t k = st; k < en; ++k) {
-      const int32_t u = a.uid[k];
+      const int32_t u = a.uid ? a.uid[k] : (int32_t)k;
       if (u < 0) continue;
       const int64_t ri = a.src_index ? a.src_index[u] : (int64_t)u;
       if (ri < 0) continue;
@@ -638,6 +638,112 @@ __global__ __launch_bounds__(256) void k_push_finish(Emit em, float* __restrict_
   em.template emit<D>(u, g);
 }
 
+// No-dedup push (FLAGS_enable_pullpush_dedup_keys=false, single shard): the
+// pull probed every occurrence, rows[k] is occurrence k's table row.  No
+// sort, hash or scan of the keys at all (reference: the atomic push merge of
+// box_wrapper.cu:1040-1047 + the PS-side merge of duplicate keys).
+// Pass 1 aggregates in LDS first: a workgroup's occurrences are slot-major
+// neighbours, so a popular key shows up many times in one workgroup; its
+// records are summed with LDS atomics in an open-addressing table keyed by
+// row (2 slots per thread, so it never fills), and only each distinct row of
+// the workgroup goes to global memory: one CAS on lock[row] elects the row's
+// leader (first workgroup representative wins), then one set of fp32 atomics
+// into the leader's accumulator.  The accumulator has kOccRep replicas,
+// picked by workgroup, so the hottest keys of a power-law batch (present in
+// every workgroup) spread their atomics over 8 lines instead of serialising
+// on one.  Pass 2: each leader sums and re-zeroes its replicas, applies
+// Adagrad and frees the lock.
+template <int D>
+struct OccCfg {
+  static constexpr int kThreads = D <= 8 ? 1024 : (D <= 16 ? 512 : 256);  // LDS table <= ~112 KB
+  static constexpr int kSlots = 2 * kThreads;
+};
+template <int D>
+__global__ __launch_bounds__(OccCfg<D>::kThreads) void k_push_occ_elect(DoutSource src, const int64_t* __restrict__ rows,
+                                                                int64_t n, float* __restrict__ acc, int acc_stride,
+                                                                int32_t* __restrict__ lock,
+                                                                int32_t* __restrict__ lead, float neg_bs) {
+  constexpr int Q = 3 + D;
+  constexpr int QP = RowF<D>::kQ4 * 4;
+  constexpr int NS = OccCfg<D>::kSlots;
+  constexpr int NT = OccCfg<D>::kThreads;
+  __shared__ unsigned int skey[NS];
+  __shared__ int srep[NS];
+  __shared__ float sacc[NS * QP];
+  for (int i = threadIdx.x; i < NS; i += NT) {
+    skey[i] = 0xFFFFFFFFu;
+    srep[i] = 0x7FFFFFFF;
+  }
+  for (int i = threadIdx.x; i < NS * QP; i += NT) sacc[i] = 0.f;
+  __syncthreads();
+  const int64_t k = (int64_t)blockIdx.x * NT + threadIdx.x;
+  const int64_t r = k < n ? rows[k] : -1;
+  if (k < n) lead[k] = -1;
+  if (r >= 0) {
+    float g[Q];
+    if (src.fast(D))
+      src.template load_fast<D>((int32_t)k, g);
+    else
+      src.load((int32_t)k, g, Q);
+    const unsigned int key = (unsigned int)r;
+    unsigned int h = (unsigned int)(((uint64_t)key * 0x9E3779B97F4A7C15ull) >> 40) & (NS - 1);
+    for (;;) {
+      const unsigned int prev = atomicCAS(&skey[h], 0xFFFFFFFFu, key);
+      if (prev == 0xFFFFFFFFu || prev == key) break;
+      h = (h + 1) & (NS - 1);
+    }
+    atomicMin(&srep[h], (int)k);
+    float* a = sacc + h * QP;
+    a[kPushSlot] = src.slot((int32_t)k);  // same slot for every occurrence of a row
+    atomicAdd(&a[kPushShow], g[0]);
+    atomicAdd(&a[kPushClick], g[1]);
+#pragma unroll
+    for (int c = 2; c < Q; ++c) atomicAdd(&a[kPushEmbedG + (c - 2)], g[c] * neg_bs);
+  }
+  __syncthreads();
+  const int rep_i = (int)(blockIdx.x % kOccRep);
+  for (int i = threadIdx.x; i < NS; i += NT) {
+    const unsigned int key = skey[i];
+    if (key == 0xFFFFFFFFu) continue;
+    const int rep = srep[i];
+    const int32_t old = atomicCAS(&lock[key], -1, rep);
+    const int32_t l = old == -1 ? rep : old;
+    if (l == rep) lead[rep] = rep;
+    float* dst = acc + ((int64_t)l * kOccRep + rep_i) * acc_stride;
+    const float* a = sacc + i * QP;
+    if (l == rep) dst[kPushSlot] = a[kPushSlot];  // only the leader's replica carries the slot
+#pragma unroll
+    for (int c = 1; c < RowF<D>::kQ; ++c) atomicAdd(&dst[c], a[c]);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_push_occ_apply(TableDev t, const int64_t* __restrict__ rows, int64_t n,
+                                                        float* __restrict__ acc, int acc_stride,
+                                                        int32_t* __restrict__ lock, const int32_t* __restrict__ lead,
+                                                        SparseSGDConfig cfg, uint64_t seed) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n || lead[k] != (int32_t)k) return;
+  const int64_t r = rows[k];
+  constexpr int QP = RowF<D>::kQ4 * 4;
+  float g[QP];
+#pragma unroll
+  for (int c = 0; c < QP; ++c) g[c] = 0.f;
+#pragma unroll
+  for (int q = 0; q < kOccRep; ++q) {
+    float* ap = acc + (k * kOccRep + q) * (int64_t)acc_stride;
+    float x[QP];
+    load_push<D>(ap, x);
+#pragma unroll
+    for (int c = 0; c < QP; ++c) g[c] += x[c];
+    float4* a4 = reinterpret_cast<float4*>(ap);
+#pragma unroll
+    for (int i = 0; i < RowF<D>::kQ4; ++i) a4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
+  lock[r] = -1;
+}
+
 // Owner-side push of the sharded step, no dedup of the received keys.  Pass
 // 1: every received entry with a row elects a leader among the entries of
 // that row (first CAS on lock[row] wins) and adds its merged gradient record
@@ -968,6 +1074,29 @@ bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const in
   PBX_MERGE_APPLY(4)
   PBX_MERGE_APPLY(32)
 #undef PBX_MERGE_APPLY
+  return false;
+}
+
+bool launch_push_occ(const PushMergeArgs& a, const TableDev& t, const int64_t* rows, int32_t* lock, int32_t* lead,
+                     const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s) {
+  if (a.cvm_offset != 2 || a.E != 3 + t.dim) return false;
+  if (a.n <= 0) return true;
+  const dim3 g(nblk(a.n)), b(256);
+  DoutSource src{a};
+  const float neg_bs = -a.bs_scale;
+#define PBX_PUSH_OCC(D)                                                                                          \
+  if (vec_push_ok<D>(t, a.push_stride)) {                                                                        \
+    constexpr int T = OccCfg<D>::kThreads;                                                                      \
+    hipLaunchKernelGGL(k_push_occ_elect<D>, dim3((unsigned)((a.n + T - 1) / T)), dim3(T), 0, s, src, rows, a.n,  \
+                       a.push, a.push_stride, lock, lead, neg_bs);                                               \
+    hipLaunchKernelGGL(k_push_occ_apply<D>, g, b, 0, s, t, rows, a.n, a.push, a.push_stride, lock, lead, cfg, seed); \
+    return true;                                                                                                 \
+  }
+  PBX_PUSH_OCC(8)
+  PBX_PUSH_OCC(16)
+  PBX_PUSH_OCC(4)
+  PBX_PUSH_OCC(32)
+#undef PBX_PUSH_OCC
   return false;
 }
 

@@ -42,19 +42,9 @@ __device__ void init_row(const TableDev& t, int64_t row, uint64_t key, const Spa
   }
 }
 
-__global__ __launch_bounds__(256) void k_probe(TableDev t, const uint64_t* __restrict__ h, int64_t n,
-                                               const int32_t* n_dev, int64_t* __restrict__ rows) {
-  __shared__ uint64_t q[16];
-  const int64_t nn = n_dev ? (int64_t)*n_dev : n;
-  const int64_t blk = (int64_t)blockIdx.x * 16;
-  if (blk >= nn) return;
-  if (threadIdx.x < 16) q[threadIdx.x] = (blk + threadIdx.x < nn) ? h[blk + threadIdx.x] : kEmptyKey;
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int sub = lane >> 4;  // query group within the wave
-  const int j = lane & 15;
-  const int g = threadIdx.x >> 4;
-  const uint64_t key = q[g];
+// Row of mixed key `key` (kEmptyKey: -1) for the 16-lane group (sub, j) of
+// the wave: bucket 1, bucket 2, then the (normally empty) stash.
+__device__ __forceinline__ int64_t probe_group(const TableDev& t, uint64_t key, int sub, int j) {
   int64_t r = -1;
   if (key != kEmptyKey) {
     const uint64_t b1 = bucket1(key, t.nb);
@@ -83,6 +73,28 @@ __global__ __launch_bounds__(256) void k_probe(TableDev t, const uint64_t* __res
       }
     }
   }
+  return r;
+}
+
+// MIX: the queries are raw feasigns (-1 = padding) mixed here, so a batch's
+// occurrences are probed straight from its key buffer (no-dedup pull).
+template <bool MIX>
+__global__ __launch_bounds__(256) void k_probe(TableDev t, const uint64_t* __restrict__ h, int64_t n,
+                                               const int32_t* n_dev, int64_t* __restrict__ rows) {
+  __shared__ uint64_t q[16];
+  const int64_t nn = n_dev ? (int64_t)*n_dev : n;
+  const int64_t blk = (int64_t)blockIdx.x * 16;
+  if (blk >= nn) return;
+  if (threadIdx.x < 16) {
+    uint64_t k = (blk + threadIdx.x < nn) ? h[blk + threadIdx.x] : kEmptyKey;
+    if (MIX && k != kEmptyKey) k = mix64(k);
+    q[threadIdx.x] = k;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 15;
+  const int g = threadIdx.x >> 4;
+  const int64_t r = probe_group(t, q[g], lane >> 4, j);
   if (j == 0 && blk + g < nn) rows[blk + g] = r;
 }
 
@@ -103,33 +115,7 @@ __global__ __launch_bounds__(256) void k_probe_gather(TableDev t, const uint64_t
   const int j = lane & 15;
   const int g = threadIdx.x >> 4;
   const uint64_t key = q[g];
-  int64_t r = -1;
-  if (key != kEmptyKey) {
-    const uint64_t b1 = bucket1(key, t.nb);
-    const uint64_t k1 = t.keys[b1 * kBucketSlots + j];
-    uint64_t m = (__ballot(k1 == key) >> (sub * 16)) & 0xFFFFull;
-    if (m) {
-      r = (int64_t)(b1 * kBucketSlots) + (__ffsll((long long)m) - 1);
-    } else {
-      const uint64_t b2 = bucket2(key, t.nb);
-      const uint64_t k2 = t.keys[b2 * kBucketSlots + j];
-      m = (__ballot(k2 == key) >> (sub * 16)) & 0xFFFFull;
-      if (m) {
-        r = (int64_t)(b2 * kBucketSlots) + (__ffsll((long long)m) - 1);
-      } else {
-        const uint32_t sn = t.stash_n ? *t.stash_n : 0u;
-        const uint32_t lim = sn < t.stash_cap ? sn : t.stash_cap;
-        int64_t found = -1;
-        for (uint32_t s = j; s < lim; s += 16)
-          if (t.stash_keys[s] == key) found = (int64_t)(t.nb * kBucketSlots) + s;
-        for (int off = 8; off > 0; off >>= 1) {
-          long long o = __shfl_xor((long long)found, off, 16);
-          found = found > o ? found : o;
-        }
-        r = found;
-      }
-    }
-  }
+  const int64_t r = probe_group(t, key, sub, j);
   const int64_t e = blk + g;
   if (e >= n) return;
   if (j == 0) rows[e] = r;
@@ -356,7 +342,13 @@ static inline unsigned int blocks_for(int64_t n, int per) {
 void launch_table_probe(const TableDev& t, const uint64_t* h, int64_t n, const int32_t* n_dev,
                         int64_t* rows, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_probe, dim3(blocks_for(n, 16)), dim3(256), 0, s, t, h, n, n_dev, rows);
+  hipLaunchKernelGGL(k_probe<false>, dim3(blocks_for(n, 16)), dim3(256), 0, s, t, h, n, n_dev, rows);
+}
+
+void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_probe<true>, dim3(blocks_for(n, 16)), dim3(256), 0, s, t,
+                     reinterpret_cast<const uint64_t*>(keys), n, nullptr, rows);
 }
 
 void launch_probe_gather(const TableDev& t, const uint64_t* h, int64_t n, int64_t* rows, float* out, int out_stride,

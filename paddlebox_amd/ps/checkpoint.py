@@ -17,6 +17,11 @@ semantics reproduced here are the PSCore CTR accessor's
 
 Layout: ``<path>/part-<rank>.keys.npy``, ``.vals.npy``, ``meta.json``;
 xbox ``<path>/part-<rank>.txt``.
+
+GPU tables (plain layout) are written by the native streaming saver
+(``GpuTable.save_stream``: chunked device compaction -> pinned ring -> writer
+threads, bounded HBM); CPU tables, codec layouts and PBX_SAVE_STREAM=0 use the
+export-based writer below.  Both produce the same files.
 """
 from __future__ import annotations
 
@@ -49,18 +54,56 @@ def select_rows(h: torch.Tensor, v: torch.Tensor, dim: int, mode: str, cfg: Save
     return keep
 
 
+# Streaming native saver (csrc/hip/ckpt.hip + ckpt_saver.cpp) for plain-
+# layout GPU tables: the table is walked in chunks of this many row slots
+# through two device buffers (2 x chunk x (8 + 4*stride) B of HBM, ~190 MB at
+# the default) and pinned host buffers into writer threads -- no device copy
+# of the table, no Python loop over rows.
+STREAM_CHUNK_ROWS = int(os.environ.get("PBX_SAVE_CHUNK_ROWS", str(1 << 22)))
+STREAM_THREADS = int(os.environ.get("PBX_SAVE_THREADS", str(min(16, os.cpu_count() or 4))))
+last_save_stats: dict = {}
+
+
+def _streamable(table) -> bool:
+    t = getattr(table, "t", None)
+    return (t is not None and hasattr(t, "save_stream") and getattr(table, "codec", None) is None
+            and os.environ.get("PBX_SAVE_STREAM", "1") != "0")
+
+
+def _stream(table, kind: int, mode: int, reset: bool, cfg: Optional[SaveConfig], nonclk: float, clk: float,
+            keys_path: str, vals_path: str = "", collect: bool = False):
+    cfg = cfg or SaveConfig()
+    with torch.cuda.device(table.device):
+        rows, chunks, gpu_s, write_s, total_s, keys = table.t.save_stream(
+            kind, mode, reset, float(cfg.base_threshold), float(cfg.delta_threshold), float(cfg.delta_keep_days),
+            float(nonclk), float(clk), float(cfg.embedx_threshold), keys_path, vals_path, STREAM_CHUNK_ROWS,
+            STREAM_THREADS, collect)
+    last_save_stats.clear()
+    last_save_stats.update(rows=rows, chunks=chunks, gpu_s=gpu_s, write_s=write_s, total_s=total_s, native=True)
+    return int(rows), keys
+
+
+def _write_meta(path: str, dim: int, stride: int, date):
+    meta = {"format": FORMAT, "dim": dim, "stride": stride, "layout": row_layout(dim), "date": date}
+    with open(os.path.join(path, "meta.json"), "w") as f:
+        json.dump(meta, f)
+
+
 def save_batch_model(table, path: str, rank: int = 0, date: Optional[str] = None) -> int:
     os.makedirs(path, exist_ok=True)
+    if _streamable(table):
+        n, _ = _stream(table, 0, 0, False, None, 0.0, 0.0, os.path.join(path, f"part-{rank:05d}.keys.npy"),
+                       os.path.join(path, f"part-{rank:05d}.vals.npy"))
+        if rank == 0:
+            _write_meta(path, table.dim, int(table.t.stride), date)
+        return n
     h, v = table.export(True)
     keys = ref.unmix64(h.cpu()).numpy().view(np.uint64)
     vals = v.float().cpu().numpy()
     np.save(os.path.join(path, f"part-{rank:05d}.keys.npy"), keys, allow_pickle=False)
     np.save(os.path.join(path, f"part-{rank:05d}.vals.npy"), vals, allow_pickle=False)
     if rank == 0:
-        meta = {"format": FORMAT, "dim": table.dim, "stride": int(vals.shape[1]) if vals.ndim == 2 else 0,
-                "layout": row_layout(table.dim), "date": date}
-        with open(os.path.join(path, "meta.json"), "w") as f:
-            json.dump(meta, f)
+        _write_meta(path, table.dim, int(vals.shape[1]) if vals.ndim == 2 else 0, date)
     return int(keys.shape[0])
 
 
@@ -87,6 +130,13 @@ def save_xbox(table, path: str, mode: str, cfg: SaveConfig, nonclk: float, clk: 
     os.makedirs(path, exist_ok=True)
     dim = table.dim
     l = row_layout(dim)
+    fn = os.path.join(path, f"part-{rank:05d}.txt")
+    if _streamable(table):
+        n, saved = _stream(table, 1, 1 if mode == "base" else 2, True, cfg, nonclk, clk, fn,
+                           collect=on_reset is not None)
+        if on_reset is not None and saved is not None and saved.numel():
+            on_reset(saved.to(table.device))
+        return n
     h, v = table.export(True)
     keep = select_rows(h, v, dim, mode, cfg, nonclk, clk)
     hk, vk = h[keep], v[keep]
@@ -100,7 +150,6 @@ def save_xbox(table, path: str, mode: str, cfg: SaveConfig, nonclk: float, clk: 
     keys = ref.unmix64(hk.cpu()).numpy().view(np.uint64)
     vv = vk.float().cpu().numpy()
     with_x = (_score(vk, nonclk, clk) >= cfg.embedx_threshold).cpu().numpy()
-    fn = os.path.join(path, f"part-{rank:05d}.txt")
     with open(fn, "w") as f:
         for i in range(keys.shape[0]):
             row = vv[i]

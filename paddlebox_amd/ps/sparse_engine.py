@@ -74,6 +74,8 @@ class _PullSlot:
         self.occ_ins = torch.empty(eng.max_keys, dtype=torch.int32, device=dev)
         self.rows = None  # persistent probe rows of a prefetched batch
         self.gen = 0
+        # no-dedup pull: table row of every key occurrence
+        self.rows_occ = None if eng.dedup else torch.empty(eng.max_keys, dtype=torch.int64, device=dev)
         if eng.sharded:
             n = eng.world * eng.C
             with torch.cuda.device(dev):
@@ -148,11 +150,19 @@ class SparseEngine:
         pull_ring: int = 2,
         exchange_capacity: Optional[int] = None,
         exchange: Optional[str] = None,
+        dedup: Optional[bool] = None,
     ):
         """``exchange`` (sharded GPU engines): "ipc" = the in-house xGMI peer-
         write mesh (parallel/ipc.py; default, self-tested at construction with
         a fallback to RCCL), "rccl" = torch.distributed all_to_all_single.
-        PBX_SPARSE_EXCHANGE overrides the default."""
+        PBX_SPARSE_EXCHANGE overrides the default.
+
+        ``dedup`` (FLAGS_enable_pullpush_dedup_keys, default true): false =
+        the single-shard GPU step probes every key occurrence and merges the
+        push per table row by leader election (probe, seqpool, push elect,
+        push apply: four launches, no key dedup at all -- the reference's
+        no-dedup pull/push, box_wrapper.cu:1049-1060).  Sharded engines,
+        feature-type codecs and dims without vector kernels keep the dedup."""
         self.cfg = cfg
         self.dim = cfg.embedx_dim
         self.E = pull_width(self.dim)
@@ -175,6 +185,10 @@ class SparseEngine:
         shard_cap = int(math.ceil(capacity / self.world)) if self.world > 1 else capacity
         # non-default feature types (int16 embedx, expand block, SparseAdam):
         # rows go through the codec kernels (ps/feature_types.py)
+        if dedup is None:
+            from ..utils import flags as _flags
+
+            dedup = _flags.get_bool("enable_pullpush_dedup_keys")
         self.codec = FeatureCodec.from_config(cfg)
         if self.codec is not None and not self.is_gpu_device():
             if self.codec.kind != 0:
@@ -198,6 +212,8 @@ class SparseEngine:
                     self.C = int(math.ceil(self.max_keys / self.world * cap_factor)) + 64
             if self.sharded:
                 self._setup_exchange(exchange or os.environ.get("PBX_SPARSE_EXCHANGE", "ipc"))
+            # no-dedup single-shard step (see the docstring)
+            self.dedup = bool(dedup) or self.sharded or self.codec is not None or self.dim not in (4, 8, 16, 32)
             # ring of per-pull buffers (sort-free hash dedup everywhere: the
             # sender packs its unique keys per owner with a counting pass)
             self._slots = [_PullSlot(self) for _ in range(max(1, int(pull_ring)))]
@@ -221,8 +237,12 @@ class SparseEngine:
                 # (kept all-zero between steps) and per-wave run owners
                 self.push_acc = torch.zeros(self.max_keys, self.Q, device=self.device)
                 self.push_inc = torch.empty((self.max_keys + 63) // 64 + 1, dtype=torch.int32, device=self.device)
+                if not self.dedup:  # per-occurrence accumulators, kOccRep replicas each (kept all-zero)
+                    self.push_acc_occ = torch.zeros(self.max_keys * int(self.table.t.occ_replicas), self.Q,
+                                                    device=self.device)
         else:
             self.table = CpuSparseTable(self.dim)
+            self.dedup = True
         self.slot_ids = torch.tensor(slot_ids if slot_ids is not None else [], dtype=torch.float32,
                                      device=self.device)
         self._seed = 1234
@@ -312,10 +332,12 @@ class SparseEngine:
             if dense is not None:
                 out[:, dense_col:dense_col + dense.shape[1]] = dense
             return st
+        h = self._hip
+        if not self.dedup and sp.cvm_offset == 2:
+            return self._pull_nodedup(keys, lod, B, S, out, col_offset, sp, dense, dense_col)
         # the occurrence map is written by the seqpool launch itself
         st = self._pull_common(keys, lod, B, S, fill_occ=False)
         sl = st.slot
-        h = self._hip
         if not self.sharded and self.codec is not None:
             self.table.t.codec_pull(self.codec.native(), st.rows, None, sl.ws.u_count, st.L, self.pull_buf)
             src, src_index = self.pull_buf, None
@@ -332,11 +354,36 @@ class SparseEngine:
                           occ_slot=sl.occ_slot, occ_ins=sl.occ_ins)
         return st
 
+    def _pull_nodedup(self, keys, lod, B, S, out, col_offset, sp, dense, dense_col) -> PullState:
+        """No-dedup pull: probe every occurrence, pool straight from the rows."""
+        h = self._hip
+        L = keys.numel()
+        assert L <= self.max_keys, f"batch has {L} keys > engine max_keys {self.max_keys}"
+        sl = self._take_slot()
+        rows = sl.rows_occ[:L]
+        self.table.t.probe_raw(keys, rows)
+        if self.auto_insert and not self.test_mode:
+            miss = (rows < 0) & (keys != -1)
+            if bool(miss.any()):
+                self.table.insert_mixed(torch.unique(ref.mix64(keys[miss])), self.cfg.sgd)
+                self.table.t.probe_raw(keys, rows)
+        if dense is not None:
+            dense = dense.contiguous().float()
+        h.seqpool_cvm_fwd(self.table.values, rows, None, lod, S, B, self.E, out, col_offset, sp.use_cvm,
+                          sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter, sp.show_coeff, sp.clk_coeff,
+                          sp.threshold, sp.quant_ratio, sp.embed_threshold_filter, sp.embed_threshold,
+                          sp.embed_thres_size if not sp.use_cvm else 0, dense, dense_col,
+                          occ_slot=sl.occ_slot, occ_ins=sl.occ_ins)
+        st = PullState(B=B, S=S, L=L, lod=lod, slot=sl, gen=sl.gen)
+        st.rows = rows
+        st.extra["nodedup"] = True
+        return st
+
     def can_prefetch(self) -> bool:
         """Prefetched pulls need a fixed key set during training: GPU, one
         shard, no auto-insert (keys registered at the feed pass)."""
         return (self.is_gpu and not self.sharded and not (self.auto_insert and not self.test_mode)
-                and len(self._slots) >= 2)
+                and len(self._slots) >= 2 and self.dedup)
 
     def prefetch(self, keys: torch.Tensor, slot: int):
         """Dedup + probe of a batch ahead of its pull, into pull slot ``slot``
@@ -469,6 +516,13 @@ class SparseEngine:
         L = st.L
         dout = dout.contiguous()
         ets = 0 if sp.use_cvm else sp.embed_thres_size
+        if st.extra.get("nodedup"):
+            self._seed += 1
+            if not self.table.t.push_occ(dout, col_offset, cvm.contiguous(), sp.use_cvm, sp.clk_filter, self.E,
+                                         sl.occ_slot, sl.occ_ins, self._slot_ids(st.S), st.rows, self.push_acc_occ,
+                                         float(bs_scale), self._sgd_native, self._seed, ets):
+                raise RuntimeError("no-dedup push needs cvm_offset 2 with a [B, 2] cvm (use the dedup path)")
+            return
         if not self.sharded:
             if sp.cvm_offset == 2 and cvm.shape[1] == 2 and self.codec is None:
                 self._seed += 1
