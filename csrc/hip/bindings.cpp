@@ -1133,7 +1133,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("clk_coeff", &ShrinkConfig::clk_coeff);
   py::class_<CodecDev>(m, "Codec")
       .def(py::init([](int kind, int D, int De, float qscale, float beta1, float beta2, float eps) {
-             PBX_CHECK(kind >= 0 && kind <= 2, "codec kind 0/1/2");
+             PBX_CHECK(kind >= 0 && kind <= 3, "codec kind 0/1/2/3");
              PBX_CHECK(D >= 1 && De >= 0 && D + De <= 256, "codec dims");
              return make_codec(kind, D, De, qscale, beta1, beta2, eps);
            }),
@@ -1148,6 +1148,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("mf", &CodecDev::mf)
       .def_readonly("eg2", &CodecDev::eg2)
       .def_readonly("adam", &CodecDev::adam)
+      .def_readonly("xsz", &CodecDev::xsz)
+      // kind 3: bitmap (int32 device tensor, kept alive by the caller) of
+      // the slot ids whose new features get De columns
+      .def("set_expand_slots",
+           [](CodecDev& c, const Tensor& bm) {
+             check_cuda(bm, "bitmap");
+             PBX_CHECK(bm.scalar_type() == torch::kInt32 && bm.is_contiguous(), "bitmap must be int32");
+             c.vslots = reinterpret_cast<const uint32_t*>(bm.data_ptr());
+             c.vslot_bits = (int)bm.numel() * 32;
+           })
       .def_readonly("extra", &CodecDev::extra)
       .def_property_readonly("storage_dim", [](const CodecDev& c) { return c.Wx + c.We; });
   py::class_<GpuTable>(m, "GpuTable")

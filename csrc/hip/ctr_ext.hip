@@ -1,16 +1,20 @@
 // CTR op family beyond the DeepFM hot path, hand-written for gfx950.
 //
-//   k_sgemm          fp32 batched GEMM with arbitrary operand strides, bias
-//                    (+scale) and accumulate epilogues: batch_fc (all three
-//                    layouts), scaled_fc, and their backward GEMMs.
+//   k_mgemm          fp32 batched GEMM on v_mfma_f32_16x16x4_f32 (exact fp32
+//                    products, the reference fc precision) with arbitrary
+//                    operand strides staged through LDS, bias (+scale) and
+//                    accumulate epilogues: batch_fc (all three layouts),
+//                    scaled_fc, and their backward GEMMs.
 //                    (reference: batch_fc_op.cu:34-567, scaled_fc_op.cu:39-342
 //                    -- cuBLAS batched/fp16 GEMMs plus separate bias kernels)
 //   k_i8_quant / k_i8_gemm
 //                    scaled_int8fc: clip/expand quantisation and an int8 MFMA
 //                    GEMM (v_mfma_i32_32x32x32_i8, exact int32 accumulation)
 //                    with the dequantising epilogue (scaled_int8fc_op.cu:38-440)
-//   k_ra_*           rank_attention forward, the reference's gather-form input
-//                    gradient and the per-block parameter gradient
+//   k_ra_*           rank_attention as grouped MFMA GEMMs over the R*R
+//                    parameter blocks with gather-on-load: forward, the
+//                    reference's gather-form input gradient and the per-block
+//                    parameter gradient (pairs found by a parallel ballot scan)
 //                    (rank_attention.cu.h:28-190, rank_attention_op.cu:30-392)
 //   k_cvm_*          cvm op (cvm_op.cu:29-70)
 //   k_mdn_*          masked_data_norm (masked_data_norm_op.cu:39-290)
@@ -29,20 +33,29 @@ inline unsigned nblk(int64_t n, int per = 256) {
 }
 
 // ---------------------------------------------------------------- fp32 batched GEMM
-// 64x64 output tile per 256-thread block, K step 16, each thread a 4x4 block.
-__global__ __launch_bounds__(256) void k_sgemm(SgemmArgs g) {
-  __shared__ float As[16][64 + 4];
-  __shared__ float Bs[16][64 + 4];
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// One 64x64 output tile per 256-thread block: 4 waves of 32x32, each 2x2
+// v_mfma_f32_16x16x4 tiles; K staged through LDS 16 at a time (k-major, rows
+// padded to 68 floats).  16x16x4 operand layout: lane l feeds A[l%16][l/16]
+// and B[l/16][l%16]; accumulator register r is C[4(l/16)+r][l%16].
+__global__ __launch_bounds__(256) void k_mgemm(SgemmArgs g) {
+  __shared__ float As[16][68];
+  __shared__ float Bs[16][68];
   const int b = blockIdx.z;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
-  const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  const int fr = lane & 15, fk = lane >> 4;
   const float* A = g.A + (int64_t)b * g.sA;
   const float* Bm = g.B + (int64_t)b * g.sB;
-  float acc[4][4];
+  f32x4 acc[2][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   for (int k0 = 0; k0 < g.K; k0 += 16) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -55,34 +68,34 @@ __global__ __launch_bounds__(256) void k_sgemm(SgemmArgs g) {
     }
     __syncthreads();
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      const float4 av = *reinterpret_cast<const float4*>(&As[kk][ty * 4]);
-      const float4 bv = *reinterpret_cast<const float4*>(&Bs[kk][tx * 4]);
-      const float a4[4] = {av.x, av.y, av.z, av.w};
-      const float b4[4] = {bv.x, bv.y, bv.z, bv.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] += a4[i] * b4[j];
+    for (int kk = 0; kk < 16; kk += 4) {
+      const float a0 = As[kk + fk][wm + fr], a1 = As[kk + fk][wm + 16 + fr];
+      const float b0 = Bs[kk + fk][wn + fr], b1 = Bs[kk + fk][wn + 16 + fr];
+      acc[0][0] = mfma4(a0, b0, acc[0][0]);
+      acc[0][1] = mfma4(a0, b1, acc[0][1]);
+      acc[1][0] = mfma4(a1, b0, acc[1][0]);
+      acc[1][1] = mfma4(a1, b1, acc[1][1]);
     }
     __syncthreads();
   }
   float* C = g.C + (int64_t)b * g.sC;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + ty * 4 + i;
-    if (m >= g.M) continue;
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + tx * 4 + j;
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn + j * 16 + fr;
       if (n >= g.N) continue;
-      float v = g.alpha * acc[i][j];
-      if (g.bias) v += g.bias[(int64_t)b * g.sBias + n] * g.bias_scale;
-      float* dst = C + (int64_t)m * g.ldc + n;
-      if (g.accumulate) v += *dst;
-      *dst = v;
+      const float bv = g.bias ? g.bias[(int64_t)b * g.sBias + n] * g.bias_scale : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + i * 16 + 4 * fk + r;
+        if (m >= g.M) continue;
+        float v = g.alpha * acc[i][j][r] + bv;
+        float* dst = C + (int64_t)m * g.ldc + n;
+        if (g.accumulate) v += *dst;
+        *dst = v;
+      }
     }
-  }
 }
 
 // column sums of a [batch][M][N] strided matrix into out[batch][N] (+=): bias
@@ -132,31 +145,49 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 // y[m][n] = acc(qx[m] . qwt[n]) * scale + bias[n]; qx [M][Kp], qwt [N][Kp]
-// int8 with Kp % 32 == 0 (zero padded).  One wave per 32x32 tile, 4 waves
-// per block (64x64); lane l feeds 16 consecutive k of row/col l%32.
+// int8 with Kp % 32 == 0 (zero padded).  64x64 tile per block, 4 waves of
+// 32x32; the A and B panels move through LDS 64 k at a time (one 16-B load
+// per lane per operand, rows padded to 80 B), then each wave feeds
+// v_mfma_i32_32x32x32_i8 from LDS: lane l takes 16 consecutive k of row l%32.
 __global__ __launch_bounds__(256) void k_i8_gemm(const signed char* __restrict__ qx,
                                                  const signed char* __restrict__ qwt, int M, int N, int Kp,
                                                  float scale, const float* __restrict__ bias, float* __restrict__ y,
                                                  int ldy) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int m0 = blockIdx.y * 64 + (w >> 1) * 32, n0 = blockIdx.x * 64 + (w & 1) * 32;
+  constexpr int LDR = 80;  // bytes per LDS row (64 k + pad)
+  __shared__ __attribute__((aligned(16))) signed char As[64 * LDR];
+  __shared__ __attribute__((aligned(16))) signed char Bs[64 * LDR];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int bm = blockIdx.y * 64, bn = blockIdx.x * 64;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
   const int r = lane & 31, h = lane >> 5;
-  const int am = min(m0 + r, M - 1), bn = min(n0 + r, N - 1);
-  const signed char* ap = qx + (int64_t)am * Kp + 16 * h;
-  const signed char* bp = qwt + (int64_t)bn * Kp + 16 * h;
+  // staging: thread t moves 16 B of row t/4, k bytes 16*(t%4)
+  const int sr = t >> 2, sk = (t & 3) * 16;
+  const int am = min(bm + sr, M - 1), an = min(bn + sr, N - 1);
   i32x16 acc = {0};
-  for (int k = 0; k < Kp; k += 32) {
-    const i32x4 a = *reinterpret_cast<const i32x4*>(ap + k);
-    const i32x4 b = *reinterpret_cast<const i32x4*>(bp + k);
-    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+  for (int k0 = 0; k0 < Kp; k0 += 64) {
+    i32x4 av = {0, 0, 0, 0}, bv = {0, 0, 0, 0};
+    if (k0 + sk < Kp) {
+      av = *reinterpret_cast<const i32x4*>(qx + (int64_t)am * Kp + k0 + sk);
+      bv = *reinterpret_cast<const i32x4*>(qwt + (int64_t)an * Kp + k0 + sk);
+    }
+    __syncthreads();
+    *reinterpret_cast<i32x4*>(As + sr * LDR + sk) = av;
+    *reinterpret_cast<i32x4*>(Bs + sr * LDR + sk) = bv;
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 64; ks += 32) {
+      const i32x4 a = *reinterpret_cast<const i32x4*>(As + (wm + r) * LDR + ks + 16 * h);
+      const i32x4 b = *reinterpret_cast<const i32x4*>(Bs + (wn + r) * LDR + ks + 16 * h);
+      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+    }
   }
-  const int n = n0 + r;
+  const int n = bn + wn + r;
   if (n >= N) return;
-  const float bv = bias ? bias[n] : 0.f;
+  const float bvv = bias ? bias[n] : 0.f;
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) {
-    const int m = m0 + 8 * (reg >> 2) + 4 * h + (reg & 3);
-    if (m < M) y[(int64_t)m * ldy + n] = (float)acc[reg] * scale + bv;
+    const int m = bm + wm + 8 * (reg >> 2) + 4 * h + (reg & 3);
+    if (m < M) y[(int64_t)m * ldy + n] = (float)acc[reg] * scale + bvv;
   }
 }
 
@@ -172,114 +203,161 @@ __device__ __forceinline__ int ra_block(const int* ro, int ld, int i, int k, int
   return lower * R + faster;
 }
 
-// out[i][p] = sum_k x[idx_k] . W[blk_k][:, p].  Block: 64 instances x 64
-// columns; W_b is staged through LDS 32 rows at a time for every block b
-// that occurs in the tile; each thread holds 16 outputs of one instance.
+// Grouped-GEMM form of rank_attention.  For a tile of 64 instances and a
+// parameter block b, A_b[i][c] = sum of x[idx_k] over the pairs k of
+// instance i that use block b (gather-sum on load), so
+//   out = sum_b A_b W_b,   R_b = dout W_b^T (dexp rows of the pairs of b),
+//   dW_b = X_b^T dout_b over the pairs of b,
+// each an MFMA GEMM (v_mfma_f32_16x16x4_f32, exact fp32) with the operand
+// panels gathered into LDS 16 deep.  Only the blocks present in a tile are
+// visited (a 64-bit mask over the <= 64 blocks).
+template <int R>
+__device__ __forceinline__ unsigned long long ra_tile_blocks(const int* ro, int ld, int i0, int B, int (*sblk)[64],
+                                                             int (*sidx)[64], unsigned long long* used) {
+  const int t = threadIdx.x;
+  if (t == 0) *used = 0ull;
+  __syncthreads();
+  if (t < 64) {
+    const int i = i0 + t;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      int idx = -1;
+      const int b = i < B ? ra_block(ro, ld, i, k, R, &idx) : -1;
+      sblk[k][t] = (b >= 0 && idx < B) ? b : -1;
+      sidx[k][t] = idx;
+      if (sblk[k][t] >= 0) atomicOr(used, 1ull << b);
+    }
+  }
+  __syncthreads();
+  return *used;
+}
+
 template <int R>
 __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, const int* __restrict__ ro, int ld,
                                                 const float* __restrict__ W, int B, int C, int P,
                                                 float* __restrict__ out) {
-  __shared__ float Ws[32][64];
-  __shared__ int used[64];
-  const int t = threadIdx.x, ii = t & 63, g = t >> 6;
-  const int i = blockIdx.x * 64 + ii;
-  const int p0 = blockIdx.y * 64 + g * 16;
-  float acc[16];
+  __shared__ float As[16][68];  // [c][instance]
+  __shared__ float Ws[16][68];  // [c][p]
+  __shared__ int sblk[R][64], sidx[R][64];
+  __shared__ unsigned long long used;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int i0 = blockIdx.x * 64, p0 = blockIdx.y * 64;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32, fr = lane & 15, fk = lane >> 4;
+  unsigned long long mask = ra_tile_blocks<R>(ro, ld, i0, B, sblk, sidx, &used);
+  f32x4 acc[2][2];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-  int blk[R], idx[R];
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-  for (int k = 0; k < R; ++k) blk[k] = (i < B) ? ra_block(ro, ld, i, k, R, &idx[k]) : -1;
-  if (t < 64) used[t] = 0;
-  __syncthreads();
-  if (g == 0)
-#pragma unroll
-    for (int k = 0; k < R; ++k)
-      if (blk[k] >= 0) used[blk[k]] = 1;
-  __syncthreads();
-  for (int b = 0; b < R * R; ++b) {
-    if (!used[b]) continue;  // block-uniform
-    for (int c0 = 0; c0 < C; c0 += 32) {
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  while (mask) {
+    const int b = __ffsll((long long)mask) - 1;
+    mask &= mask - 1;
+    for (int c0 = 0; c0 < C; c0 += 16) {
       __syncthreads();
-      for (int e = t; e < 32 * 64; e += 256) {
-        const int cc = e >> 6, pp = e & 63;
-        const int c = c0 + cc, p = blockIdx.y * 64 + pp;
-        Ws[cc][pp] = (c < C && p < P) ? W[((int64_t)b * C + c) * P + p] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = t + 256 * j, ii = e & 63, cc = e >> 6, c = c0 + cc;
+        float a = 0.f;
+        if (c < C) {
+#pragma unroll
+          for (int k = 0; k < R; ++k)
+            if (sblk[k][ii] == b) a += x[(int64_t)sidx[k][ii] * C + c];
+        }
+        As[cc][ii] = a;
+        const int p = p0 + ii;
+        Ws[cc][ii] = (c < C && p < P) ? W[((int64_t)b * C + c) * P + p] : 0.f;
       }
       __syncthreads();
 #pragma unroll
-      for (int k = 0; k < R; ++k) {
-        if (blk[k] != b) continue;
-        const float* xr = x + (int64_t)idx[k] * C + c0;
-        const int cn = min(32, C - c0);
-        for (int cc = 0; cc < cn; ++cc) {
-          const float xv = xr[cc];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) acc[j] += xv * Ws[cc][g * 16 + j];
-        }
+      for (int kk = 0; kk < 16; kk += 4) {
+        const float a0 = As[kk + fk][wm + fr], a1 = As[kk + fk][wm + 16 + fr];
+        const float b0 = Ws[kk + fk][wn + fr], b1 = Ws[kk + fk][wn + 16 + fr];
+        acc[0][0] = mfma4(a0, b0, acc[0][0]);
+        acc[0][1] = mfma4(a0, b1, acc[0][1]);
+        acc[1][0] = mfma4(a1, b0, acc[1][0]);
+        acc[1][1] = mfma4(a1, b1, acc[1][1]);
       }
     }
   }
-  if (i >= B) return;
 #pragma unroll
-  for (int j = 0; j < 16; ++j)
-    if (p0 + j < P) out[(int64_t)i * P + p0 + j] = acc[j];
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int p = p0 + wn + j * 16 + fr;
+      if (p >= P) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = i0 + wm + i * 16 + 4 * fk + r;
+        if (m < B) out[(int64_t)m * P + p] = acc[i][j][r];
+      }
+    }
 }
 
-// dexp[j][k][c] = valid(j,k) ? sum_p dout[j][p] W[blk(j,k)][c][p] : 0
+// dexp[j][k][c] = valid(j,k) ? sum_p dout[j][p] W[blk(j,k)][c][p] : 0.  Per
+// tile (64 instances x 64 c) and present block b: R_b = dout_tile W_b^T on
+// MFMA, scattered to the (j, k) rows whose pair uses b.
 template <int R>
 __global__ __launch_bounds__(256) void k_ra_dexp(const float* __restrict__ dout, const int* __restrict__ ro, int ld,
                                                  const float* __restrict__ W, int B, int C, int P,
                                                  float* __restrict__ dexp) {
-  __shared__ float Ws[64][33];  // [c][p chunk]
-  __shared__ int used[64];
-  const int t = threadIdx.x, jj = t & 63, g = t >> 6;
-  const int j = blockIdx.x * 64 + jj;
-  const int c0 = blockIdx.y * 64 + g * 16;
-  int blk[R], idx[R];
+  __shared__ float Ds[16][68];  // [p][instance]
+  __shared__ float Ws[16][68];  // [p][c]
+  __shared__ int sblk[R][64], sidx[R][64];
+  __shared__ unsigned long long used;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int j0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32, fr = lane & 15, fk = lane >> 4;
+  unsigned long long mask = ra_tile_blocks<R>(ro, ld, j0, B, sblk, sidx, &used);
+  // rows of invalid pairs are zero
+  for (int e = t; e < 64 * R * 64; e += 256) {
+    const int cc = e & 63, jk = e >> 6, jj = jk / R, k = jk % R;
+    const int j = j0 + jj, c = c0 + cc;
+    if (j < B && c < C && sblk[k][jj] < 0) dexp[((int64_t)j * R + k) * C + c] = 0.f;
+  }
+  while (mask) {
+    const int b = __ffsll((long long)mask) - 1;
+    mask &= mask - 1;
+    f32x4 acc[2][2];
 #pragma unroll
-  for (int k = 0; k < R; ++k) blk[k] = (j < B) ? ra_block(ro, ld, j, k, R, &idx[k]) : -1;
-  if (t < 64) used[t] = 0;
-  __syncthreads();
-  if (g == 0)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int k = 0; k < R; ++k)
-      if (blk[k] >= 0) used[blk[k]] = 1;
-  __syncthreads();
-  float acc[R][16];
-#pragma unroll
-  for (int k = 0; k < R; ++k)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[k][q] = 0.f;
-  for (int b = 0; b < R * R; ++b) {
-    if (!used[b]) continue;
-    for (int pc = 0; pc < P; pc += 32) {
+      for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int q0 = 0; q0 < P; q0 += 16) {
       __syncthreads();
-      for (int e = t; e < 64 * 32; e += 256) {
-        const int cc = e >> 5, pp = e & 31;
-        const int c = blockIdx.y * 64 + cc, p = pc + pp;
-        Ws[cc][pp] = (c < C && p < P) ? W[((int64_t)b * C + c) * P + p] : 0.f;
+#pragma unroll
+      for (int jj4 = 0; jj4 < 4; ++jj4) {
+        const int e = t + 256 * jj4, ii = e & 63, pp = e >> 6, p = q0 + pp;
+        const int j = j0 + ii, c = c0 + ii;
+        Ds[pp][ii] = (j < B && p < P) ? dout[(int64_t)j * P + p] : 0.f;
+        Ws[pp][ii] = (c < C && p < P) ? W[((int64_t)b * C + c) * P + p] : 0.f;
       }
       __syncthreads();
 #pragma unroll
-      for (int k = 0; k < R; ++k) {
-        if (blk[k] != b) continue;
-        const float* dr = dout + (int64_t)j * P + pc;
-        const int pn = min(32, P - pc);
-        for (int pp = 0; pp < pn; ++pp) {
-          const float dv = dr[pp];
-#pragma unroll
-          for (int q = 0; q < 16; ++q) acc[k][q] += dv * Ws[g * 16 + q][pp];
-        }
+      for (int kk = 0; kk < 16; kk += 4) {
+        const float a0 = Ds[kk + fk][wm + fr], a1 = Ds[kk + fk][wm + 16 + fr];
+        const float b0 = Ws[kk + fk][wn + fr], b1 = Ws[kk + fk][wn + 16 + fr];
+        acc[0][0] = mfma4(a0, b0, acc[0][0]);
+        acc[0][1] = mfma4(a0, b1, acc[0][1]);
+        acc[1][0] = mfma4(a1, b0, acc[1][0]);
+        acc[1][1] = mfma4(a1, b1, acc[1][1]);
       }
     }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn) {
+        const int c = c0 + wn + jn * 16 + fr;
+        if (c >= C) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int jj = wm + i * 16 + 4 * fk + r, j = j0 + jj;
+          if (j >= B) continue;
+#pragma unroll
+          for (int k = 0; k < R; ++k)
+            if (sblk[k][jj] == b) dexp[((int64_t)j * R + k) * C + c] = acc[i][jn][r];
+        }
+      }
   }
-  if (j >= B) return;
-#pragma unroll
-  for (int k = 0; k < R; ++k)
-#pragma unroll
-    for (int q = 0; q < 16; ++q)
-      if (c0 + q < C) dexp[((int64_t)j * R + k) * C + c0 + q] = acc[k][q];
 }
 
 // dx[i][c] = sum_t dexp[ro[i][2t+2]][rank_i - 1][c]   (reference gather form,
@@ -302,67 +380,82 @@ __global__ void k_ra_dx(const float* __restrict__ dexp, const int* __restrict__ 
 }
 
 // dW[b][c][p] += sum over valid pairs (j,k) with blk = b of x[idx][c] dout[j][p].
-// Grid: (c tiles of 64, p tiles of 64, R*R * splits).  Pairs of the split's
-// instance range are scanned in chunks of 32, staged through LDS.
+// Grid: (c tiles of 64, p tiles of 64, R*R * splits).  The split's instances
+// are scanned 256/R at a time, one (j, k) pair per thread; the pairs of
+// block b are compacted with a wave ballot + LDS offsets, then consumed 16 at
+// a time as the K dimension of a 64x64 MFMA tile (X rows and dout rows
+// gathered into LDS).
 __global__ __launch_bounds__(256) void k_ra_dw(const float* __restrict__ x, const float* __restrict__ dout,
                                                const int* __restrict__ ro, int ld, int B, int C, int P, int R,
                                                int per_split, float* __restrict__ dW) {
-  __shared__ float xs[32][64];
-  __shared__ float ds[32][64];
-  __shared__ int cnt;
+  __shared__ float Xs[16][68];  // [pair][c]
+  __shared__ float Ds[16][68];  // [pair][p]
+  __shared__ int pj[256], px[256];
+  __shared__ int wcnt[4];
   const int b = blockIdx.z % (R * R), split = blockIdx.z / (R * R);
   const int c0 = blockIdx.x * 64, p0 = blockIdx.y * 64;
-  const int t = threadIdx.x, tc = t & 15, tp = t >> 4;  // 4 c x 4 p per thread
-  float acc[4][4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32, fr = lane & 15, fk = lane >> 4;
+  f32x4 acc[2][2];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[a][q] = 0.f;
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int j_beg = split * per_split, j_end = min(B, j_beg + per_split);
-  __shared__ int pj[32], px[32];
-  for (int jb = j_beg; jb < j_end; jb += 32 / R > 0 ? 32 / R : 1) {
-    const int jn = min(j_end, jb + (32 / R > 0 ? 32 / R : 1));
-    if (t == 0) {
-      int n = 0;
-      for (int j = jb; j < jn; ++j)
-        for (int k = 0; k < R; ++k) {
-          int idx;
-          if (ra_block(ro, ld, j, k, R, &idx) == b && idx < B) {
-            pj[n] = j;
-            px[n] = idx;
-            ++n;
-          }
-        }
-      cnt = n;
-    }
+  const int per = 256 / R;  // instances per scan step
+  for (int jb = j_beg; jb < j_end; jb += per) {
+    // ---- parallel pair scan: thread t checks pair (jb + t / R, t % R)
+    const int jj = t / R, k = t % R, j = jb + jj;
+    int idx = -1;
+    const bool ok = jj < per && j < j_end && ra_block(ro, ld, j, k, R, &idx) == b && idx < B;
+    const unsigned long long m = __ballot(ok);
+    if (lane == 0) wcnt[w] = __popcll(m);
     __syncthreads();
-    const int n = cnt;
-    for (int e = t; e < n * 64; e += 256) {
-      const int r = e >> 6, q = e & 63;
-      xs[r][q] = (c0 + q < C) ? x[(int64_t)px[r] * C + c0 + q] : 0.f;
-      ds[r][q] = (p0 + q < P) ? dout[(int64_t)pj[r] * P + p0 + q] : 0.f;
-    }
-    __syncthreads();
-    for (int r = 0; r < n; ++r) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const float xv = xs[r][tc * 4 + a];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[a][q] += xv * ds[r][tp * 4 + q];
-      }
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int c = c0 + tc * 4 + a;
-    if (c >= C) continue;
+    int off = 0, n = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int p = p0 + tp * 4 + q;
-      if (p < P && acc[a][q] != 0.f) atomicAdd(&dW[((int64_t)b * C + c) * P + p], acc[a][q]);
+      off += q < w ? wcnt[q] : 0;
+      n += wcnt[q];
+    }
+    if (ok) {
+      const int pos = off + __popcll(m & ((1ull << lane) - 1ull));
+      pj[pos] = j;
+      px[pos] = idx;
+    }
+    __syncthreads();
+    // ---- dW tile += X_pairs^T dout_pairs, 16 pairs per LDS stage
+    for (int q0 = 0; q0 < n; q0 += 16) {
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const int e = t + 256 * e4, cc = e & 63, pr = e >> 6, q = q0 + pr;
+        Xs[pr][cc] = (q < n && c0 + cc < C) ? x[(int64_t)px[q] * C + c0 + cc] : 0.f;
+        Ds[pr][cc] = (q < n && p0 + cc < P) ? dout[(int64_t)pj[q] * P + p0 + cc] : 0.f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < 16; kk += 4) {
+        const float a0 = Xs[kk + fk][wm + fr], a1 = Xs[kk + fk][wm + 16 + fr];
+        const float b0 = Ds[kk + fk][wn + fr], b1 = Ds[kk + fk][wn + 16 + fr];
+        acc[0][0] = mfma4(a0, b0, acc[0][0]);
+        acc[0][1] = mfma4(a0, b1, acc[0][1]);
+        acc[1][0] = mfma4(a1, b0, acc[1][0]);
+        acc[1][1] = mfma4(a1, b1, acc[1][1]);
+      }
+      __syncthreads();
     }
   }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const int p = p0 + wn + jn * 16 + fr;
+      if (p >= P) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = c0 + wm + i * 16 + 4 * fk + r;
+        if (c < C && acc[i][jn][r] != 0.f) atomicAdd(&dW[((int64_t)b * C + c) * P + p], acc[i][jn][r]);
+      }
+    }
 }
 
 // ---------------------------------------------------------------- cvm op
@@ -577,7 +670,7 @@ __global__ void k_mdn_stats(const float* __restrict__ part, int rows, int C, flo
 void launch_sgemm(const SgemmArgs& g, hipStream_t s) {
   if (g.M == 0 || g.N == 0 || g.batch == 0) return;
   dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, g.batch);
-  hipLaunchKernelGGL(k_sgemm, grid, dim3(256), 0, s, g);
+  hipLaunchKernelGGL(k_mgemm, grid, dim3(256), 0, s, g);
 }
 
 void launch_colsum_strided(const float* x, int batch, int M, int N, int64_t sb, int64_t ld, float* out, int64_t so,

@@ -6,6 +6,13 @@
 //   kind 1  int16 embedx (+expand), Adagrad     value = q * pull_embedx_scale
 //   kind 2  fp32 embedx (+expand), SparseAdam   per-element moments, per-row
 //                                               beta powers (w and x separately)
+//   kind 3  variable: one fp32 block of max(D, De) columns of which the
+//           row's stored size (0, D or De) is live; a feature is created
+//           with De columns when its slot is pulled into an expand output
+//           (codec bitmap), else D.  Pull zeroes columns past the size and
+//           reports it; push updates only the live columns (reference
+//           PullCopyVariable / PushMergeCopyVariable, box_wrapper.cu:
+//           271-322,714-875: embedx_size per feature, total_dims flags)
 //
 // and an optional expand block (NNCross / extended pull: De extra columns
 // pulled next to embedx, pull_box_extended_sparse).  Rows keep the standard
@@ -25,6 +32,7 @@ __device__ __forceinline__ float clampf(float x, float lo, float hi) { return x 
 
 // one embedding column j < D + De of row v (embedx then expand)
 __device__ __forceinline__ float load_col(const CodecDev& c, const float* v, int j) {
+  if (c.kind == 3) return v[kEmbedx + j];
   if (c.kind == 1) {
     const int16_t* q = reinterpret_cast<const int16_t*>(v + kEmbedx);
     const int w = j < c.D ? j : 2 * c.Wx + (j - c.D);
@@ -34,6 +42,10 @@ __device__ __forceinline__ float load_col(const CodecDev& c, const float* v, int
 }
 
 __device__ __forceinline__ void store_col(const CodecDev& c, float* v, int j, float x) {
+  if (c.kind == 3) {
+    v[kEmbedx + j] = x;
+    return;
+  }
   if (c.kind == 1) {
     int16_t* q = reinterpret_cast<int16_t*>(v + kEmbedx);
     const int w = j < c.D ? j : 2 * c.Wx + (j - c.D);
@@ -52,7 +64,8 @@ __global__ __launch_bounds__(256) void k_codec_pull(TableDev t, CodecDev c, cons
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nn) return;
   float* o = out + i * out_stride;
-  const int W = 3 + c.D + c.De;
+  const int DXv = c.kind == 3 ? c.Wx : c.D + c.De;
+  const int W = 3 + DXv;
   int64_t r = -1;
   if (uid) {
     const int32_t u = uid[i];
@@ -60,15 +73,28 @@ __global__ __launch_bounds__(256) void k_codec_pull(TableDev t, CodecDev c, cons
   } else {
     r = rows[i];
   }
+  const bool size_col = c.kind == 3 && out_stride > W;  // variable: the size rides in column W
   if (r < 0) {
     for (int j = 0; j < W; ++j) o[j] = 0.f;
+    if (size_col) o[W] = 0.f;
     return;
   }
   const float* v = t.values + r * (int64_t)t.stride;
   o[0] = v[kShow];
   o[1] = v[kClick];
   o[2] = v[kEmbedW];
+  if (c.kind == 3) {
+    const int xs = (int)v[c.xsz];
+    for (int j = 0; j < DXv; ++j) o[3 + j] = j < xs ? v[kEmbedx + j] : 0.f;
+    if (size_col) o[W] = (float)xs;
+    return;
+  }
   for (int j = 0; j < c.D + c.De; ++j) o[3 + j] = load_col(c, v, j);
+}
+
+__device__ __forceinline__ bool expand_slot(const CodecDev& c, float slot) {
+  const int s = (int)slot;
+  return c.vslots && s >= 0 && s < c.vslot_bits && ((c.vslots[s >> 5] >> (s & 31)) & 1u);
 }
 
 // SparseAdam step of n values w[j] (j through col()) with moments m/v and
@@ -88,7 +114,7 @@ __global__ __launch_bounds__(256) void k_codec_update(TableDev t, CodecDev c, co
   if (r < 0) return;
   float* v = t.values + r * (int64_t)t.stride;
   const float* g = push + u * push_stride;
-  const int DX = c.D + c.De;
+  const int DX = c.kind == 3 ? c.Wx : c.D + c.De;
   const float slot = g[kPushSlot], g_show = g[kPushShow], g_click = g[kPushClick];
   v[c.slot] = slot;
   const float show = v[kShow] + g_show;
@@ -155,8 +181,24 @@ __global__ __launch_bounds__(256) void k_codec_update(TableDev t, CodecDev c, co
     if (cfg.nonclk_coeff * (show - click) + cfg.clk_coeff * click >= cfg.mf_create_thresholds) {
       v[c.mf] = 1.f;
       const uint64_t salt = seed ^ (uint64_t)r * 0x9E3779B97F4A7C15ULL;
-      for (int j = 0; j < DX; ++j) store_col(c, v, j, hash_uniform(salt, j) * cfg.mf_initial_range);
+      const int nc = c.kind == 3 ? (expand_slot(c, slot) ? c.De : c.D) : DX;
+      if (c.kind == 3) v[c.xsz] = (float)nc;
+      for (int j = 0; j < nc; ++j) store_col(c, v, j, hash_uniform(salt, j) * cfg.mf_initial_range);
     }
+    return;
+  }
+  if (c.kind == 3) {  // variable: one Adagrad group over the live columns
+    const int xs = (int)v[c.xsz];
+    if (xs <= 0) return;
+    const float g2 = v[c.xg2];
+    const float ratio = mf_lr * sqrtf(cfg.mf_initial_g2sum / (cfg.mf_initial_g2sum + g2));
+    float add = 0.f;
+    for (int j = 0; j < xs; ++j) {
+      const float sg = g[kPushEmbedxG + j] / scale;
+      v[kEmbedx + j] = clampf(v[kEmbedx + j] + sg * ratio, cfg.mf_min_bound, cfg.mf_max_bound);
+      add += sg * sg;
+    }
+    v[c.xg2] = g2 + add / (float)xs;
     return;
   }
   // embedx and expand are two Adagrad groups with their own g2sum
@@ -185,7 +227,7 @@ __global__ void k_codec_init(TableDev t, CodecDev c, const int64_t* __restrict__
   const int64_t r = rows[i];
   if (r < 0) return;
   float* v = t.values + r * (int64_t)t.stride;
-  const int DX = c.D + c.De;
+  const int DX = c.kind == 3 ? c.D : c.D + c.De;  // variable: created with D columns
   if (c.kind == 2) {
     float* st = v + c.adam;
     st[2] = c.beta1;
@@ -195,6 +237,7 @@ __global__ void k_codec_init(TableDev t, CodecDev c, const int64_t* __restrict__
   }
   if (init_embedx) {  // same draws as the table insert's init_row
     v[c.mf] = 1.f;
+    if (c.kind == 3) v[c.xsz] = (float)c.D;
     for (int j = 0; j < DX; ++j) store_col(c, v, j, hash_uniform(keys[i], seed + 1 + j) * cfg.mf_initial_range);
   }
 }

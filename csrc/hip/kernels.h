@@ -676,7 +676,12 @@ struct CodecDev {
   int g2 = 0, xg2 = 0, delta = 0, slot = 0, unseen = 0, mf = 0;
   int eg2 = 0;   // expand g2sum (Adagrad, De > 0)
   int adam = 0;  // first SparseAdam state word
+  int xsz = 0;   // kind 3: the row's embedding size (0, D or De) as a float
   int extra = 0;  // floats after the standard tail
+  // kind 3: bitmap over slot ids of the slots whose features are created
+  // with De columns (the slots pulled into an expand output)
+  const uint32_t* vslots = nullptr;
+  int vslot_bits = 0;
 };
 // fills storage widths and field offsets for (kind, D, De)
 inline CodecDev make_codec(int kind, int D, int De, float qscale, float beta1, float beta2, float eps) {
@@ -684,8 +689,9 @@ inline CodecDev make_codec(int kind, int D, int De, float qscale, float beta1, f
   c.kind = kind;
   c.D = D;
   c.De = De;
-  c.Wx = kind == 1 ? (D + 1) / 2 : D;
-  c.We = kind == 1 ? (De + 1) / 2 : De;
+  // kind 3 (variable): one block of max(D, De) columns, the first `size` live
+  c.Wx = kind == 1 ? (D + 1) / 2 : (kind == 3 ? (D > De ? D : De) : D);
+  c.We = kind == 1 ? (De + 1) / 2 : (kind == 3 ? 0 : De);
   c.qscale = qscale;
   c.beta1 = beta1;
   c.beta2 = beta2;
@@ -699,7 +705,9 @@ inline CodecDev make_codec(int kind, int D, int De, float qscale, float beta1, f
   c.mf = l.mf_size;
   int used = l.mf_size + 1;
   c.eg2 = used;
-  if (De > 0) used += 1;
+  if (De > 0 && kind != 3) used += 1;
+  c.xsz = used;
+  if (kind == 3) used += 1;
   c.adam = used;
   if (kind == 2) used += 6 + 2 * (D + De);
   c.extra = used - (l.mf_size + 1);

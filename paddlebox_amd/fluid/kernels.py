@@ -495,7 +495,8 @@ def k_fused_seqpool_cvm(ctx, op):
 @kernel("pull_box_extended_sparse")
 def k_pull_box_extended_sparse(ctx, op):
     keys, lod, B, S = _sparse_inputs(ctx, op.inputs["Ids"])
-    recs, ext = ctx.box.pull_extended(keys, lod, B, S, op.attrs["emb_size"], op.attrs["emb_extended_size"])
+    recs, ext = ctx.box.pull_extended(keys, lod, B, S, op.attrs["emb_size"], op.attrs["emb_extended_size"],
+                                      op.attrs.get("mask"))
     lod2 = lod.view(S, B + 1)
     mask = op.attrs.get("mask") or [3] * S
     oi = ei = 0

@@ -152,7 +152,11 @@ class BoxWrapper:
         if self.mode == "tiered":
             from .tiered import HostTable, SsdTier, TieredStore
 
-            self.host = HostTable(self.cfg.embedx_dim)
+            codec = getattr(self.engine, "codec", None)
+            # feature-type codecs: the host / SSD tiers keep the canonical fp32
+            # rows the GPU table exports (re-encoded when staged back)
+            self.host = (HostTable(codec.DX, stride=codec.canon_width) if codec is not None
+                         else HostTable(self.cfg.embedx_dim))
             p = ssd_path or self.cfg.tier.ssd_path
             if p:
                 self.ssd = SsdTier(os.path.join(p, f"rank{self.rank:05d}"), self.host.stride)
@@ -544,9 +548,14 @@ class BoxWrapper:
             self._input_table = InputTable(self.input_table_dim)
         return self._input_table
 
-    def pull_extended(self, keys, lod, B, S, emb_size: int, ext_size: int):
+    def pull_extended(self, keys, lod, B, S, emb_size: int, ext_size: int, mask=None):
         """pull_box_extended_sparse: (records [L, emb_size], expand [L, ext_size])."""
         eng = self._require_engine()
+        if getattr(eng, "codec", None) is not None and eng.codec.kind == 3:
+            # variable feature type: per-feature size, one output per slot
+            from .extras import pull_extended_var
+
+            return pull_extended_var(eng, keys, lod, B, S, emb_size, ext_size, mask)
         if getattr(eng, "codec", None) is not None and eng.codec.De >= ext_size:
             # GPU PS rows carry the expand block: one pull / push for both
             from .extras import pull_extended_codec

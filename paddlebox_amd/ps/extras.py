@@ -19,6 +19,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from ..ops import reference as ref
+
 
 class GpuReplicaCache:
     def __init__(self, dim: int, device=None):
@@ -201,6 +203,82 @@ class _PullExtendedCodec(torch.autograd.Function):
             gm[:, ctx.E:ctx.E + gex.shape[1]] = gex.float()
         ctx.eng.push_records(ctx.st, gm, 2, ctx.bs)
         return (None,) * 9
+
+
+class _PullExtendedVar(torch.autograd.Function):
+    """pull_box_extended_sparse with the variable feature type (codec kind
+    3): every feature has its own embedding size (D or De, set at creation
+    by the slot it was created from).  Each slot is pulled into ONE output:
+    the expand output when the slot has one (mask bit 1), else the embedx
+    output; columns past the feature's size read as zero.  The push takes
+    the cvm / embed_w gradients from that output and the embedding gradients
+    only when the feature's size matches the output (reference
+    PullCopyVariable / PushMergeCopyVariable, box_wrapper.cu:271-322,
+    714-875, total_dims bit 0 = size D, bit 1 = size De)."""
+
+    @staticmethod
+    def forward(ctx, anchor, keys, lod, eng, B, S, emb_size, ext_size, bs_scale, route):
+        recs, st = eng.pull_records(keys, lod, B, S, with_expand=True)
+        c = eng.codec
+        DX = c.DX
+        xs = recs[:, 3 + DX]
+        slot_of_occ, _ = ref.occurrence_map(lod.cpu(), S, B)
+        slot_of_occ = slot_of_occ.to(keys.device)
+        to_ex = route.to(keys.device)[slot_of_occ.long()]
+        ctx.eng, ctx.st, ctx.bs, ctx.DX = eng, st, bs_scale, DX
+        ctx.save_for_backward(xs, to_ex, slot_of_occ)
+
+        def cols(n):
+            out = recs[:, :min(n, 3 + DX)]
+            return torch.nn.functional.pad(out, (0, n - out.shape[1])) if n > out.shape[1] else out
+
+        out = cols(emb_size).clone()
+        ex = cols(ext_size).clone()
+        # a slot writes only its own output (the other one stays zero)
+        out[to_ex] = 0
+        ex[~to_ex] = 0
+        # embedding columns beyond the output's dim: embedx output shows D
+        if emb_size > 3 + c.D:
+            out[:, 3 + c.D:] = 0
+        return out, ex
+
+    @staticmethod
+    def backward(ctx, g, gex):
+        xs, to_ex, slot_of_occ = ctx.saved_tensors
+        c = ctx.eng.codec
+        L = ctx.st.L
+        gm = torch.zeros(L, 3 + ctx.DX, device=xs.device, dtype=torch.float32)
+        if g is None:
+            g = torch.zeros(L, 3, device=xs.device)
+        if gex is None:
+            gex = torch.zeros(L, 3, device=xs.device)
+        g, gex = g.float(), gex.float()
+        head_x = torch.nn.functional.pad(g[:, :3], (0, max(0, 3 - g.shape[1])))
+        head_e = torch.nn.functional.pad(gex[:, :3], (0, max(0, 3 - gex.shape[1])))
+        gm[:, :3] = torch.where(to_ex.unsqueeze(1), head_e, head_x)
+        we = min(c.De, gex.shape[1] - 3)
+        wx = min(c.D, g.shape[1] - 3)
+        if we > 0:
+            sel = to_ex & (xs == c.De)
+            gm[sel, 3:3 + we] = gex[sel, 3:3 + we]
+        if wx > 0:
+            sel = (~to_ex) & (xs == c.D)
+            gm[sel, 3:3 + wx] = g[sel, 3:3 + wx]
+        ctx.eng.push_records(ctx.st, gm, 2, ctx.bs, slot_of_occ)
+        return (None,) * 10
+
+
+def pull_extended_var(eng, keys, lod, B, S, emb_size: int, ext_size: int, mask=None):
+    """Variable feature type pull (see _PullExtendedVar).  mask[s] as in
+    _pull_box_extended_sparse: bit 1 = slot s has an expand output."""
+    from ..ops.sparse import _anchor
+
+    mask = list(mask) if mask else [3] * S
+    route = torch.tensor([bool(m & 2) for m in mask[:S]] + [False] * max(0, S - len(mask)), dtype=torch.bool)
+    ids = tuple(int(x) for x, r in zip(eng._slot_ids(S)[:S].tolist(), route.tolist()) if r)
+    if getattr(eng.codec, "_vslot_ids", None) != sorted(set(ids)):
+        eng.codec.set_expand_slots(ids)
+    return _PullExtendedVar.apply(_anchor(keys.device), keys, lod, eng, B, S, emb_size, ext_size, float(B), route)
 
 
 def pull_extended_codec(eng, keys, lod, B, S, emb_size: int, ext_size: int):

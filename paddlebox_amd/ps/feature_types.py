@@ -23,35 +23,43 @@ import torch
 
 from .config import PSConfig, SparseSGDConfig, row_layout
 
-KIND_FP32, KIND_INT16, KIND_ADAM = 0, 1, 2
+KIND_FP32, KIND_INT16, KIND_ADAM, KIND_VAR = 0, 1, 2, 3
 
 
 class FeatureCodec:
     def __init__(self, kind: int, D: int, De: int = 0, qscale: float = 1.0, beta1: float = 0.9,
                  beta2: float = 0.999, eps: float = 1e-8):
-        if kind not in (KIND_FP32, KIND_INT16, KIND_ADAM):
+        if kind not in (KIND_FP32, KIND_INT16, KIND_ADAM, KIND_VAR):
             raise ValueError(f"feature codec kind {kind}")
+        if kind == KIND_VAR and De <= 0:
+            raise ValueError("the variable feature type needs expand_embed_dim > 0")
         self.kind, self.D, self.De = int(kind), int(D), int(De)
         self.qscale, self.beta1, self.beta2, self.eps = float(qscale), float(beta1), float(beta2), float(eps)
         q = kind == KIND_INT16
-        self.Wx = (D + 1) // 2 if q else D
-        self.We = (De + 1) // 2 if q else De
+        var = kind == KIND_VAR
+        # variable: one block of max(D, De) columns; the row's size field says
+        # how many are live (0 before creation, then D or De)
+        self.Wx = (D + 1) // 2 if q else (max(D, De) if var else D)
+        self.We = (De + 1) // 2 if q else (0 if var else De)
         self.storage_dim = self.Wx + self.We
         sl = row_layout(self.storage_dim)
         self.raw = sl
         used = sl["mf_size"] + 1
         self.eg2 = used
-        used += 1 if De > 0 else 0
+        used += 1 if De > 0 and not var else 0
+        self.xsz = used
+        used += 1 if var else 0
         self.adam = used
         used += 6 + 2 * (D + De) if kind == KIND_ADAM else 0
         self.extra = used - (sl["mf_size"] + 1)
         self.raw_stride = ((sl["mf_size"] + 1 + self.extra) + 3) & ~3 if self.extra else sl["stride"]
         # canonical (IO) layout: fp32 embedx+expand as one block, then the
         # codec state copied verbatim
-        self.DX = D + De
+        self.DX = max(D, De) if var else D + De
         self.canon = row_layout(self.DX)
         self.canon_width = self.canon["stride"] + self.extra
         self._native = None
+        self.device = None  # set by the engine (variable slot bitmap lives there)
 
     @staticmethod
     def from_config(cfg: PSConfig) -> Optional["FeatureCodec"]:
@@ -60,6 +68,8 @@ class FeatureCodec:
         opt = getattr(cfg, "sparse_optimizer", "adagrad")
         kind = KIND_ADAM if opt == "adam" else (KIND_INT16 if cfg.feature_type == 1 else KIND_FP32)
         De = int(cfg.expand_embed_dim or 0)
+        if cfg.feature_type == 2 and opt != "adam":
+            kind = KIND_VAR
         if kind == KIND_FP32 and De == 0 and not getattr(cfg, "force_codec", False):
             return None
         return FeatureCodec(kind, cfg.embedx_dim, De, cfg.pull_embedx_scale, getattr(cfg, "adam_beta1", 0.9),
@@ -72,14 +82,36 @@ class FeatureCodec:
             self._native = _native.hip().Codec(self.kind, self.D, self.De, self.qscale, self.beta1, self.beta2,
                                                self.eps)
             assert self._native.storage_dim == self.storage_dim and self._native.extra == self.extra
+            if self.kind == KIND_VAR:
+                self._vslots = None
+                self.set_expand_slots([])
         return self._native
+
+    def set_expand_slots(self, slot_ids):
+        """Variable feature type: the slot ids whose new features are created
+        with De columns (the slots pulled into an expand output)."""
+        import torch as _t
+
+        ids = [int(s) for s in slot_ids]
+        nbits = max([64] + [s + 1 for s in ids])
+        bm = _t.zeros((nbits + 31) // 32, dtype=_t.int64)
+        for s in ids:
+            bm[s >> 5] |= 1 << (s & 31)
+        bm = ((bm + (1 << 31)) % (1 << 32) - (1 << 31)).to(_t.int32)  # two's complement words
+        dev = getattr(self, "device", None) or _t.device("cuda", _t.cuda.current_device())
+        self._vslots = bm.to(dev)
+        self._vslot_ids = sorted(set(ids))
+        self.native().set_expand_slots(self._vslots)
 
     # ------------------------------------------------------------ row IO
     _TAIL = ("embed_g2sum", "embedx_g2sum", "delta_score", "slot", "unseen_days", "mf_size")
 
     def _emb_raw(self, raw: torch.Tensor):
-        """(embedx [n, D], expand [n, De]) fp32 views/copies of raw rows."""
+        """(embedx [n, D], expand [n, De]) fp32 views/copies of raw rows
+        (variable: the whole block, and an empty second part)."""
         blk = raw[:, 3:3 + self.storage_dim]
+        if self.kind == KIND_VAR:
+            return blk, blk[:, :0]
         if self.kind == KIND_INT16:
             q = blk.contiguous().view(torch.int16).float() * self.qscale
             return q[:, :self.D], q[:, 2 * self.Wx:2 * self.Wx + self.De]
@@ -91,8 +123,8 @@ class FeatureCodec:
         out = torch.zeros(n, self.canon_width, dtype=torch.float32, device=raw.device)
         out[:, :3] = raw[:, :3]
         ex, ee = self._emb_raw(raw)
-        out[:, 3:3 + self.D] = ex
-        out[:, 3 + self.D:3 + self.DX] = ee
+        out[:, 3:3 + ex.shape[1]] = ex
+        out[:, 3 + ex.shape[1]:3 + self.DX] = ee
         for f in self._TAIL:
             out[:, self.canon[f]] = raw[:, self.raw[f]]
         if self.extra:
@@ -109,7 +141,9 @@ class FeatureCodec:
         raw = torch.zeros(n, self.raw_stride, dtype=torch.float32, device=canon.device)
         raw[:, :3] = canon[:, :3]
         ex, ee = canon[:, 3:3 + self.D], canon[:, 3 + self.D:3 + self.DX]
-        if self.kind == KIND_INT16:
+        if self.kind == KIND_VAR:
+            raw[:, 3:3 + self.DX] = canon[:, 3:3 + self.DX]
+        elif self.kind == KIND_INT16:
             q = torch.zeros(n, 2 * self.storage_dim, dtype=torch.int16, device=canon.device)
             q[:, :self.D] = self.quantize(ex).to(torch.int16)
             q[:, 2 * self.Wx:2 * self.Wx + self.De] = self.quantize(ee).to(torch.int16)
@@ -141,6 +175,8 @@ class FeatureCodec:
         x = v[:, 3:3 + DX]
         gx = push[:, 4:4 + DX] / scale.unsqueeze(1)
         sg = push[:, 3] / scale
+        if self.kind == KIND_VAR:
+            return self._update_var_ref(v, push, cfg, gs, sg, scale, slot)
         if self.kind == KIND_ADAM:
             st = v[:, c["stride"] + (self.adam - self.raw["mf_size"] - 1):]
             b1, b2 = self.beta1, self.beta2
@@ -187,11 +223,34 @@ class FeatureCodec:
             v[:, gi] = g2x + (gg * gg).sum(1) / nj
         return v
 
+    def _update_var_ref(self, v, push, cfg, gs, sg, scale, slot):
+        c = self.canon
+        lr = torch.full_like(gs, cfg.learning_rate)
+        mf_lr = torch.full_like(gs, cfg.mf_learning_rate)
+        if cfg.use_feature_lr:
+            msk = slot != cfg.nodeid_slot
+            lr = torch.where(msk, torch.full_like(lr, cfg.feature_learning_rate), lr)
+            mf_lr = torch.where(msk, torch.full_like(lr, cfg.feature_learning_rate), mf_lr)
+        g2 = v[:, c["embed_g2sum"]]
+        ratio = lr * torch.sqrt(cfg.initial_g2sum / (cfg.initial_g2sum + g2))
+        v[:, 2] = (v[:, 2] + sg * ratio).clamp(cfg.min_bound, cfg.max_bound)
+        v[:, c["embed_g2sum"]] = g2 + sg * sg
+        xs = v[:, c["stride"] + (self.xsz - self.raw["mf_size"] - 1)].long()
+        live = torch.arange(self.DX, device=v.device).unsqueeze(0) < xs.unsqueeze(1)
+        gx = push[:, 4:4 + self.DX] / scale.unsqueeze(1) * live
+        g2x = v[:, c["embedx_g2sum"]]
+        rx = (mf_lr * torch.sqrt(cfg.mf_initial_g2sum / (cfg.mf_initial_g2sum + g2x))).unsqueeze(1)
+        x = v[:, 3:3 + self.DX]
+        nx = torch.where(live, (x + gx * rx).clamp(cfg.mf_min_bound, cfg.mf_max_bound), x)
+        v[:, 3:3 + self.DX] = nx
+        v[:, c["embedx_g2sum"]] = torch.where(xs > 0, g2x + (gx * gx).sum(1) / xs.clamp(min=1), g2x)
+        return v
+
     def memory_per_row(self) -> int:
         return self.raw_stride * 4
 
     def __repr__(self) -> str:
-        names = {0: "fp32-adagrad", 1: "int16-adagrad", 2: "fp32-adam"}
+        names = {0: "fp32-adagrad", 1: "int16-adagrad", 2: "fp32-adam", 3: "variable-adagrad"}
         return (f"FeatureCodec({names[self.kind]}, D={self.D}, De={self.De}, scale={self.qscale:g}, "
                 f"row={self.raw_stride * 4}B)")
 
@@ -201,4 +260,4 @@ def quant_scale_for(bound: float) -> float:
     return float(bound) / 32767.0 if bound > 0 else 1.0
 
 
-__all__ = ["FeatureCodec", "KIND_FP32", "KIND_INT16", "KIND_ADAM", "quant_scale_for"]
+__all__ = ["FeatureCodec", "KIND_FP32", "KIND_INT16", "KIND_ADAM", "KIND_VAR", "quant_scale_for"]

@@ -196,7 +196,9 @@ class SparseEngine:
             self.codec = None  # CPU: the expand block is served by ps.extras.ExpandEmbedding
         self.xdim = self.codec.DX if self.codec is not None else self.dim
         if self.codec is not None:
-            self.P = padded(3 + self.xdim)
+            self.codec.device = self.device
+            # variable feature type: one more pull column carries the row's size
+            self.P = padded((4 if self.codec.kind == 3 else 3) + self.xdim)
             self.Q = padded(4 + self.xdim)
         if self.is_gpu:
             self.table = GpuSparseTable(self.dim, shard_cap, self.device, codec=self.codec)
@@ -631,6 +633,8 @@ class SparseEngine:
             idx = sl.send_index[:L][sl.ws.uid[:L].long().clamp(min=0)]
             ok = (sl.ws.uid[:L] >= 0) & (idx >= 0)
             recs = torch.where(ok.unsqueeze(1), sl.resp_back[idx.clamp(min=0)], torch.zeros((), device=self.device))
+        if with_expand and self.codec is not None and self.codec.kind == 3:
+            W += 1  # variable: [show, click, embed_w, block[max(D, De)], size]
         return recs[:, :W], st
 
     def push_records(self, st: PullState, grads: torch.Tensor, cvm_cols: int, bs_scale: float,

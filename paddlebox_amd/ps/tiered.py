@@ -14,6 +14,9 @@ box_wrapper.cc:120-210).  MI355X design:
 * Staging runs in a background thread: host-tier probe / SSD reads /
   gather into a pinned buffer are native and GIL-free (csrc/host/
   tier_store.cc), then one H2D copy and the GPU insert + assign.
+* Feature-type codecs (int16, SparseAdam, expand, variable) are tiered in
+  their canonical fp32 layout (``FeatureCodec.decode`` / ``encode``): the
+  host and SSD tiers never see the packed device encoding.
 * EndPass exports the live table (a device copy) and a background thread
   moves it D2H into the host tier and spills rows unseen for
   ``spill_unseen`` days to the log-structured SSD tier -- overlapped with the
@@ -161,7 +164,13 @@ class TieredStore:
         live = engine.table
         self.live = live
         if live.codec is not None:
-            raise NotImplementedError("tiered store with feature-type codecs")
+            # codec rows (int16 / SparseAdam / expand / variable) travel in the
+            # canonical fp32 layout: export decodes, assign re-encodes, and the
+            # host tier's unseen_days column is the canonical one
+            c = live.codec
+            if host.stride != c.canon_width or host.dim != c.DX:
+                raise ValueError(f"tiered store with {c!r}: the host tier must hold canonical rows "
+                                 f"(HostTable({c.DX}, stride={c.canon_width}))")
         # staged table: same geometry as the live one
         self.stage_table = GpuSparseTable.like(live)
         self.stream = torch.cuda.Stream(live.device)

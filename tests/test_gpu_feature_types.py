@@ -201,3 +201,57 @@ def test_extended_pull_push_codec():
     push[:, 12:] = ge * (-float(B))
     exp = eng.codec.update_ref(before, push, cfg.sgd)
     torch.testing.assert_close(eng.table.read(hk).cpu(), exp, rtol=1e-5, atol=1e-6)
+
+
+def test_variable_feature_pull_push():
+    """Variable feature type (codec kind 3, reference PullCopyVariable /
+    PushMergeCopyVariable): features of the expand slot are created with De
+    columns, the others with D; each slot reads / writes only its own output
+    and the update touches only the feature's live columns."""
+    from paddlebox_amd.ps.extras import pull_extended_var
+    from paddlebox_amd.ps.feature_types import KIND_VAR
+
+    D, De, B, S = 8, 16, 32, 2
+    cfg = PSConfig(embedx_dim=D, expand_embed_dim=De, feature_type=2)
+    cfg.sgd.mf_create_thresholds = 0.0
+    cfg.sgd.mf_initial_range = 0.01
+    eng = _engine(cfg, B, S)
+    c = eng.codec
+    assert c.kind == KIND_VAR and c.DX == De
+    g = torch.Generator().manual_seed(5)
+    keys = torch.randperm(10000, generator=g)[: B * S].to(torch.int64) + 1  # all distinct
+    lod = torch.cat([torch.arange(B + 1), torch.arange(B, 2 * B + 1)]).to(torch.int64)
+    keys, lod = keys.to(DEV), lod.to(DEV)
+    mask = [1, 2]  # slot 0 -> embedx output, slot 1 -> expand output
+    eng.register_keys(keys, init_embedx=False)
+    hk = ref.mix64(keys)
+    size_col = c.canon["stride"] + (c.xsz - c.raw["mf_size"] - 1)
+    # pass 1: nothing created yet -> zero embeddings; the push creates them
+    out, ex = pull_extended_var(eng, keys, lod, B, S, 3 + D, 3 + De, mask)
+    assert out.shape == (B * S, 3 + D) and ex.shape == (B * S, 3 + De)
+    assert float(out[B:].abs().sum()) == 0 and float(ex[:B].abs().sum()) == 0
+    assert float(out[:B, 3:].abs().sum()) == 0 and float(ex[B:, 3:].abs().sum()) == 0
+    torch.autograd.backward([out, ex], [torch.randn(out.shape, generator=g).to(DEV),
+                                        torch.randn(ex.shape, generator=g).to(DEV)])
+    before = eng.table.read(hk).cpu()
+    sizes = before[:, size_col]
+    assert torch.equal(sizes[:B], torch.full((B,), float(D)))
+    assert torch.equal(sizes[B:], torch.full((B,), float(De)))
+    assert float(before[:B, 3 + D:3 + De].abs().sum()) == 0  # past the size: untouched zeros
+    assert float(before[B:, 3:3 + De].abs().sum()) > 0
+    # pass 2: pull values masked by size, push against the oracle
+    out, ex = pull_extended_var(eng, keys, lod, B, S, 3 + D, 3 + De, mask)
+    torch.testing.assert_close(out[:B].cpu(), before[:B, :3 + D], rtol=0, atol=0)
+    torch.testing.assert_close(ex[B:].cpu(), before[B:, :3 + De], rtol=0, atol=0)
+    go = torch.randn(B * S, 3 + D, generator=g)
+    ge = torch.randn(B * S, 3 + De, generator=g)
+    torch.autograd.backward([out, ex], [go.to(DEV), ge.to(DEV)])
+    push = torch.zeros(B * S, 4 + De)
+    push[:, 0] = torch.tensor([1.0] * B + [2.0] * B)
+    push[:B, 1:3] = go[:B, :2]
+    push[:B, 3:4 + D] = go[:B, 2:3 + D] * (-float(B))
+    push[B:, 1:3] = ge[B:, :2]
+    push[B:, 3:4 + De] = ge[B:, 2:3 + De] * (-float(B))
+    exp = c.update_ref(before, push, cfg.sgd)
+    after = eng.table.read(hk).cpu()
+    torch.testing.assert_close(after, exp, rtol=1e-5, atol=1e-6)

@@ -106,3 +106,40 @@ def test_tiered_matches_hbm_oracle(tmp_path, use_ssd, overlap):
             assert st["spilled"] > 0 and st["ssd_hits"] > 0 and len(tb.ssd) > 0
     finally:
         BoxWrapper._instance = None
+
+
+@pytest.mark.parametrize("ftype,opt", [(1, "adagrad"), (0, "adam")])
+def test_tiered_codec_matches_hbm_oracle(tmp_path, ftype, opt):
+    """Feature-type codecs through the tiers: int16 rows
+    and SparseAdam rows are staged / written back / spilled to SSD in their
+    canonical fp32 layout and train exactly like the all-in-HBM table."""
+
+    def box_codec(mode, capacity, ssd=None):
+        box = BoxWrapper(8, feature_type=ftype, pull_embedx_scale=2.0 ** -12, device=DEV)
+        box.cfg.sparse_optimizer = opt
+        box.cfg.sgd.mf_create_thresholds = 0.0
+        box.cfg.sgd.mf_initial_range = 0.0
+        box.cfg.tier.spill_unseen_days = 0.0
+        box.initialize_gpu_and_load_model(slot_vector=list(range(1, S + 1)), max_keys=B * S * 4,
+                                          capacity=capacity, mode=mode, ssd_path=ssd)
+        assert box.engine.codec is not None
+        return box
+
+    try:
+        ob = box_codec("hbm", 100000)
+        h = _train(ob, overlap=False)
+        exp = ob.engine.table.read(h.to(DEV)).cpu()
+    finally:
+        BoxWrapper._instance = None
+    try:
+        tb = box_codec("tiered", 2400, ssd=str(tmp_path / "ssd"))
+        assert tb.tier is not None and tb.host.stride == tb.engine.codec.canon_width
+        h2 = _train(tb, overlap=True)
+        assert torch.equal(h, h2)
+        got = _tier_rows(tb, h)
+        keep = [c for c in range(exp.shape[1]) if c != tb.host.layout["slot"]]
+        torch.testing.assert_close(got[:, keep], exp[:, keep], rtol=1e-5, atol=1e-6)
+        st = tb.tier.stats
+        assert st["spilled"] > 0 and st["ssd_hits"] > 0
+    finally:
+        BoxWrapper._instance = None
