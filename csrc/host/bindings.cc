@@ -667,6 +667,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         t.export_all(&k, &v);
         return py::make_tuple(to_tensor_u64(k), to_tensor_f(v, t.stride()));
       })
+      .def("shrink", &HostTier::shrink, py::arg("decay"), py::arg("unseen_col"), py::arg("nonclk_coeff"),
+           py::arg("clk_coeff"), py::arg("delete_threshold"), py::arg("max_unseen"),
+           py::call_guard<py::gil_scoped_release>())
       .def("select_ge", [](const HostTier& t, int col, float thr) {
         std::vector<uint64_t> k;
         std::vector<float> v;

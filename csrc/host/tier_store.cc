@@ -314,6 +314,39 @@ void HostTier::select_ge(int col, float thr, std::vector<uint64_t>* keys, std::v
   }
 }
 
+int64_t HostTier::shrink(float decay, int unseen_col, float nonclk_coeff, float clk_coeff, float delete_threshold,
+                         float max_unseen) {
+  if (unseen_col < 2 || unseen_col >= stride_) throw std::runtime_error("HostTier::shrink: unseen column");
+  std::vector<std::vector<int64_t>> freed(kShards);
+  std::atomic<int64_t> gone{0};
+  pool_->parallel_range(kShards, [&](int, int64_t b, int64_t e) {
+    for (int64_t si = b; si < e; ++si) {
+      Shard& s = shards_[si];
+      std::lock_guard<std::mutex> lk(s.mu);
+      int64_t g = 0;
+      for (size_t j = 0; j < s.keys.size(); ++j) {
+        if (s.keys[j] == kEmptyKey || s.keys[j] == kTomb) continue;
+        float* v = row_ptr(s.rows[j]);
+        v[0] *= decay;
+        v[1] *= decay;
+        v[unseen_col] += 1.f;
+        const float score = (v[0] - v[1]) * nonclk_coeff + v[1] * clk_coeff;
+        if (score < delete_threshold || v[unseen_col] > max_unseen) {
+          freed[si].push_back(s.rows[j]);
+          s.keys[j] = kTomb;
+          s.rows[j] = -1;
+          --s.live;
+          ++g;
+        }
+      }
+      gone += g;
+    }
+  });
+  std::lock_guard<std::mutex> lk(alloc_mu_);
+  for (auto& f : freed) free_rows_.insert(free_rows_.end(), f.begin(), f.end());
+  return gone.load();
+}
+
 void HostTier::clear() {
   for (auto& s : shards_) {
     std::lock_guard<std::mutex> lk(s.mu);
@@ -578,6 +611,44 @@ int64_t SsdLog::compact(double min_live) {
   get(keys.data(), (int64_t)keys.size(), f.data(), v.data(), stride_);
   put(keys.data(), v.data(), (int64_t)keys.size(), stride_);
   std::lock_guard<std::mutex> lk(mu_);
+  // Tombstones in a victim may still shadow an older put of the same key in
+  // a segment that survives (replay would resurrect it): carry forward every
+  // victim tombstone whose key is still absent when some older segment
+  // survives the compaction.
+  {
+    std::vector<uint64_t> carry;
+    char* page = nullptr;
+    if (posix_memalign(reinterpret_cast<void**>(&page), kPage, kPage) != 0) throw std::runtime_error("SsdLog: alloc");
+    for (int id : victims) {
+      bool older = false;
+      for (auto& s : segs_)
+        if (s->id < id && s->fd >= 0 && std::find(victims.begin(), victims.end(), s->id) == victims.end()) {
+          older = true;
+          break;
+        }
+      if (!older) continue;
+      Seg* s = segs_[id].get();
+      const int64_t pages = s->slots > 0 ? page_of(s->slots - 1) + 1 : 0;
+      for (int64_t p = 0; p < pages; ++p) {
+        if (pread(s->fd, page, kPage, p * kPage) != kPage) break;
+        for (int r = 0; r < per_page_; ++r) {
+          const char* rec = page + (int64_t)r * rec_bytes_;
+          uint64_t key;
+          uint32_t flags;
+          std::memcpy(&key, rec, 8);
+          std::memcpy(&flags, rec + 8, 4);
+          if (key != kEmptyKey && (flags & 1u) && index_.find(key) == index_.end()) carry.push_back(key);
+        }
+      }
+    }
+    free(page);
+    std::sort(carry.begin(), carry.end());
+    carry.erase(std::unique(carry.begin(), carry.end()), carry.end());
+    if (!carry.empty()) {
+      std::vector<std::pair<uint64_t, Loc>> placed;
+      write_batch(carry.data(), nullptr, (int64_t)carry.size(), 0, true, &placed);
+    }
+  }
   for (int id : victims) {  // now record-free: drop the file, keep the id slot
     Seg* s = segs_[id].get();
     close(s->fd);

@@ -53,6 +53,12 @@ class HostTier {
   void export_all(std::vector<uint64_t>* keys, std::vector<float>* vals) const;
   // keys/rows whose column `col` >= thr (cold rows for the SSD spill)
   void select_ge(int col, float thr, std::vector<uint64_t>* keys, std::vector<float>* vals) const;
+  // end-of-day shrink over every row, in parallel over the shards
+  // (ctr_accessor.cc:63-80): show/click *= decay, unseen_days += 1, delete
+  // rows with score < delete_threshold or unseen_days > max_unseen.
+  // Column indices: show 0, click 1, unseen_col.  Returns rows deleted.
+  int64_t shrink(float decay, int unseen_col, float nonclk_coeff, float clk_coeff, float delete_threshold,
+                 float max_unseen);
   void clear();
 
  private:

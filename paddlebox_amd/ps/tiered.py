@@ -94,19 +94,11 @@ class HostTable:
         return int(self._native.memory_bytes())
 
     def shrink(self, cfg: ShrinkConfig) -> int:
-        """Decay show/click, age, delete (ctr_accessor.cc:63-80) over the host tier."""
-        k, v = self.export(True)
-        if k.numel() == 0:
-            return 0
-        l = self.layout
-        v[:, 0] *= cfg.show_click_decay_rate
-        v[:, 1] *= cfg.show_click_decay_rate
-        v[:, l["unseen_days"]] += 1
-        score = (v[:, 0] - v[:, 1]) * cfg.nonclk_coeff + v[:, 1] * cfg.clk_coeff
-        keep = (score >= cfg.delete_threshold) & (v[:, l["unseen_days"]] <= cfg.delete_after_unseen_days)
-        self.erase(k[~keep])
-        self.assign(k[keep], v[keep])
-        return int((~keep).sum())
+        """Decay show/click, age, delete (ctr_accessor.cc:63-80) over the host
+        tier, natively and in place (HostTier::shrink: parallel over shards)."""
+        return int(self._native.shrink(float(cfg.show_click_decay_rate), int(self.layout["unseen_days"]),
+                                       float(cfg.nonclk_coeff), float(cfg.clk_coeff), float(cfg.delete_threshold),
+                                       float(cfg.delete_after_unseen_days)))
 
     def clear(self):
         self._native.clear()

@@ -68,3 +68,60 @@ def test_ssd_log_put_get_erase_compact_and_replay(tmp_path):
     f3, got3 = s2.get(h)
     assert torch.equal(f3, f) and torch.equal(got3[f3], v2[f3])
     assert set(np.asarray(s2.keys()).tolist()) == set(np.asarray(h[f]).tolist())
+
+
+def test_ssd_compaction_keeps_tombstones_that_shadow_survivors(tmp_path):
+    """a tombstone living in a compacted (victim) segment must not
+    vanish while an older surviving segment still holds the key's previous
+    put -- otherwise a reopen replays the old record and the key comes back."""
+    d = str(tmp_path / "ssd")
+    stride = 4
+    per_seg = (4096 // (12 + 4 * stride)) * 2  # records per 2-page segment
+    s = SsdTier(d, stride, segment_bytes=2 * 4096)
+    k_old = torch.arange(1, per_seg + 1, dtype=torch.int64)  # fills segment 0
+    s.put(k_old, torch.ones(per_seg, stride))
+    victim_keys = torch.arange(10_000, 10_000 + per_seg // 2, dtype=torch.int64)
+    s.put(victim_keys, torch.full((victim_keys.numel(), stride), 2.0))  # segment 1
+    gone = k_old[5:6]
+    s.delete(gone)  # tombstone in segment 1; segment 0 still holds the old put
+    s.put(victim_keys, torch.full((victim_keys.numel(), stride), 3.0))  # segment 1 -> mostly dead
+    assert s._native.segments() >= 3
+    moved = s.compact(0.5)  # segment 1 is a victim, segment 0 (live ~100%) survives
+    assert moved > 0
+    f, _ = s.get(gone)
+    assert not bool(f.any())
+    del s
+    s2 = SsdTier(d, stride, segment_bytes=2 * 4096)
+    f, _ = s2.get(gone)
+    assert not bool(f.any()), "deleted key resurrected by replay after compaction"
+    f, v = s2.get(victim_keys)
+    assert bool(f.all()) and bool((v == 3.0).all())
+    f, _ = s2.get(k_old[6:])
+    assert bool(f.all())
+
+
+def test_host_tier_native_shrink_matches_rule():
+    from paddlebox_amd.ps.config import ShrinkConfig
+
+    t = HostTable(8, threads=4, chunk_rows=1024)
+    h = _keys(5000, 3)
+    t._native.insert(h)
+    g = torch.Generator().manual_seed(9)
+    v = torch.zeros(h.numel(), t.stride)
+    v[:, 0] = torch.rand(h.numel(), generator=g) * 5
+    v[:, 1] = v[:, 0] * torch.rand(h.numel(), generator=g) * 0.5
+    l = t.layout
+    v[:, l["unseen_days"]] = torch.randint(0, 40, (h.numel(),), generator=g).float()
+    t.assign(h, v)
+    cfg = ShrinkConfig(show_click_decay_rate=0.9, delete_threshold=0.8, delete_after_unseen_days=30.0)
+    exp = v.clone()
+    exp[:, 0] *= 0.9
+    exp[:, 1] *= 0.9
+    exp[:, l["unseen_days"]] += 1
+    score = (exp[:, 0] - exp[:, 1]) * cfg.nonclk_coeff + exp[:, 1] * cfg.clk_coeff
+    keep = (score >= cfg.delete_threshold) & (exp[:, l["unseen_days"]] <= cfg.delete_after_unseen_days)
+    gone = t.shrink(cfg)
+    assert gone == int((~keep).sum()) > 0
+    assert t.size() == int(keep.sum())
+    assert bool((t.probe(h[~keep]) == -1).all())
+    torch.testing.assert_close(t.read(h[keep]), exp[keep])
