@@ -128,6 +128,9 @@ def main():
                     help="after the measurement, split host time into replay / H2D load (stderr only)")
     ap.add_argument("--mlp-dtype", choices=("bf16", "fp32"), default="bf16",
                     help="bf16: fused MFMA tower (default); fp32: the reference's fp32 fc precision")
+    ap.add_argument("--secondary-dtype", choices=("auto", "fp32", "bf16", "none"), default="auto",
+                    help="after the headline measurement, time the same K steps at this MLP precision in the same "
+                         "run and report it in config (auto: fp32 when the headline is bf16 DeepFM)")
     ap.add_argument("--model", choices=("deepfm", "dcn_v2"), default="deepfm",
                     help="deepfm = the headline config; dcn_v2 = BASELINE config 5 (cross layers on the MFMA GEMM)")
     ap.add_argument("--cross-layers", type=int, default=3)
@@ -239,179 +242,214 @@ def main():
         log(rank, f"[bench] prefilled {n_ins} features on rank0 (table size {engine.table.size()}, "
                   f"{engine.table.memory_bytes() / 2**30:.1f} GiB) in {time.time() - t0:.1f}s")
 
+    def measure(mlp_dtype: str, primary: bool):
+        """Build the model at this MLP precision over the shared sparse engine,
+        capture the step, run W warmup + K timed steps; returns the timings."""
+        hidden = tuple(int(x) for x in args.hidden.split(","))
+        dcn = args.model == "dcn_v2"
+        fp32 = mlp_dtype == "fp32"
+        if dcn:
+            if fp32:
+                raise SystemExit("--mlp-dtype fp32 is a DeepFM precision variant")
+            model = DCNv2(engine, num_slots=S, dense_dim=13, cross_layers=args.cross_layers, hidden=hidden).to(device)
+        else:
+            model = DeepFM(engine, num_slots=S, dense_dim=13, hidden=hidden).to(device)
+        if fp32:
+            model.set_precision("fp32")
+        # the fused tower runs the whole dense side (bf16 operands, or exact fp32)
+        fused = getattr(model, "use_tower", False) and (not fp32 or model.tower.fp32)
+        C = model.dn.C
+        arena = DenseArena(model.parameters(), device, extra_grad=3 * C if multi and not dcn else 0)
+        if multi:
+            model.dn.group = dist.group.WORLD
+            model.dn.sync_stats = True
+            if fused and not dcn:
+                # data_norm batch statistics are summed across ranks in the SAME
+                # all-reduce as the dense gradients (tail of the gradient buffer)
+                model.dn.stats = arena.grad_tail(3 * C)
+                model.dn.stats_in_grad_bucket = True
+        # one update launch for the dense side: Adam + bf16 tower weight re-pack +
+        # data_norm summary update; grads zeroed by the same kernel
+        opt = FlatAdam(arena, lr=1e-3, clear_grad=True)
+        if fused:
+            opt.fuse(mlps=[model.mlp], data_norms=[model.dn])
+        # the dense all-reduce runs on its own communicator and side stream, started
+        # as soon as the tower's gradients are final: it overlaps the sparse push
+        ipc = None
+        if multi and (args.dense == "ipc" or args.same_gpu):
+            from paddlebox_amd.parallel.ipc import IpcMesh, IpcMeshError
+
+            try:
+                ipc = IpcMesh(arena.grad.numel() * 4, device=device)
+                if not ipc.self_test():
+                    ipc.close()
+                    ipc = None
+                    log(rank, "[bench] dense IPC mesh self-test failed; RCCL all-reduce")
+            except IpcMeshError as e:
+                ipc = None
+                log(rank, f"[bench] dense IPC mesh unavailable ({e}); RCCL all-reduce")
+        if multi and args.same_gpu and (ipc is None or engine.exchange_mode != "ipc"):
+            raise SystemExit("--same-gpu needs the IPC meshes (RCCL cannot run two ranks on one GPU)")
+        # RCCL dense all-reduce: its own communicator, so it overlaps the sparse
+        # exchange; the IPC meshes are independent of each other by construction
+        sync = DenseSync(arena, mode="grad_allreduce",
+                         overlap_group=dist.new_group(list(range(world))) if (multi and ipc is None) else None, ipc=ipc)
+        if getattr(model, "tower", None) is not None:
+            model.tower.on_dense_grads = sync.launch
+
+        # every pinned batch buffer is streamed to the device once up front so the
+        # timed steps do not pay the driver's first-touch cost of a pinned range
+        scratch = torch.empty_like(host_batches[0]._flat, device=device)
+        for hb in host_batches:
+            scratch.copy_(hb._flat, non_blocking=True)
+        torch.cuda.synchronize()
+        del scratch
+        copy_stream = torch.cuda.Stream(device)
+        auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
+        auc_stats = torch.zeros(5, dtype=torch.float64, device=device)
+        fused_auc = fused
+        if fused_auc:  # streaming AUC accumulated by the tower's loss epilogue
+            model.tower.auc = (auc_table, auc_stats, None)
+
+        one = torch.ones((), device=device)  # persistent d loss / d loss: no fill kernel per step
+
+        def train_step(b):
+            loss, pred = model(b)
+            loss.backward(one)
+            sync.before_step()
+            opt.step(sync.grad_scale())
+            if not fused_auc:
+                auc_accumulate(pred, b.label, auc_table, auc_stats)
+            return loss.detach()
+
+        nb = len(host_batches)
+        graphed = None
+        if args.graph:
+            try:
+                from paddlebox_amd.runtime.graph_step import GraphedTrainStep
+
+                pre = (engine, lambda b: b.keys) if (args.prefetch and engine.can_prefetch()) else None
+                graphed = GraphedTrainStep(train_step, host_batches[0], device, prefetch=pre)
+                graphed.warm(host_batches, replays=args.graph_warm)
+                log(rank, f"[bench] training step captured into HIP graphs ({args.graph_warm} warm replays)")
+            except Exception as e:  # pragma: no cover - depends on runtime
+                log(rank, f"[bench] graph capture failed ({e!r}); running eagerly")
+                graphed = None
+
+        if graphed is not None:
+            graphed.load(0, host_batches[0])
+
+            def run(i):
+                graphed.load((i + 1) % graphed.n, host_batches[(i + 1) % nb])
+                return graphed.run(i % graphed.n)
+        else:
+            def fetch(i):
+                with torch.cuda.stream(copy_stream):
+                    b = host_batches[i % nb].to(device, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(copy_stream)
+                return b, ev
+
+            pending = [fetch(0)]
+
+            def run(i):
+                b, ev = pending.pop()
+                pending.append(fetch(i + 1))
+                torch.cuda.current_stream().wait_event(ev)
+                for t in (b.keys, b.lod, b.dense, b.label, b.cvm):
+                    t.record_stream(torch.cuda.current_stream())
+                return train_step(b)
+
+        if primary and args.trace_steps and graphed is not None:
+            # diagnostics: per-step host time of the H2D load and the replay
+            tl, tr = [], []
+            for i in range(args.trace_steps):
+                t0 = time.perf_counter()
+                graphed.load((i + 1) % graphed.n, host_batches[(i + 1) % nb])
+                t1 = time.perf_counter()
+                graphed.run(i % graphed.n)
+                tr.append(time.perf_counter() - t1)
+                tl.append(t1 - t0)
+            torch.cuda.synchronize()
+            log(rank, "[bench] trace load us: " + " ".join(f"{x * 1e6:.0f}" for x in tl))
+            log(rank, "[bench] trace run  us: " + " ".join(f"{x * 1e6:.0f}" for x in tr))
+        for i in range(args.warmup):
+            run(i)
+        torch.cuda.synchronize()
+        if multi:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        loss = None
+        for i in range(args.steps):
+            loss = run(args.warmup + i)
+        t_enq = time.perf_counter() - t_start
+        torch.cuda.synchronize()
+        if multi:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t_start
+        if multi:
+            t = torch.tensor([dt], device=cdev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        log(rank, f"[bench] host enqueue {t_enq / args.steps * 1e3:.4f} ms/step, wall {dt / args.steps * 1e3:.4f} ms/step")
+        # diagnostics only (after the measurement): further windows of K steps
+        for w in range(args.diag_windows if primary else 0):
+            torch.cuda.synchronize()
+            t0w = time.perf_counter()
+            for i in range(args.steps):
+                run(args.warmup + args.steps * (w + 1) + i)
+            torch.cuda.synchronize()
+            log(rank, f"[bench] diag window {w}: {(time.perf_counter() - t0w) / args.steps * 1e3:.4f} ms/step")
+        if primary and args.host_diag and graphed is not None:
+            # where the host time of a step goes: replay alone, H2D load alone, both
+            for name, fn in (("replay", lambda i: graphed.graphs[i % 2][0].replay()),
+                             ("load", lambda i: graphed.load(i % 2, host_batches[i % nb])),
+                             ("load+run", lambda i: run(i))):
+                for w in range(3):
+                    torch.cuda.synchronize()
+                    t0w = time.perf_counter()
+                    for i in range(args.steps):
+                        fn(i)
+                    th = time.perf_counter() - t0w
+                    torch.cuda.synchronize()
+                    tw = time.perf_counter() - t0w
+                    log(rank, f"[bench] host-diag {name} window {w}: host {th / args.steps * 1e3:.4f} "
+                              f"wall {tw / args.steps * 1e3:.4f} ms/step")
+
+        res = dict(dt=dt, t_enq=t_enq, loss=float(loss) if loss is not None else float("nan"),
+                   auc_stats=auc_stats.clone(), ipc=ipc,
+                   prefetch=bool(graphed is not None and graphed.prefetch is not None), fused=fused)
+        # free this precision's graphs / model before the next measurement
+        del graphed, model, opt, arena, sync
+        return res
+
     hidden = tuple(int(x) for x in args.hidden.split(","))
     dcn = args.model == "dcn_v2"
-    fp32 = args.mlp_dtype == "fp32"
-    if dcn:
-        if fp32:
-            raise SystemExit("--mlp-dtype fp32 is a DeepFM precision variant")
-        model = DCNv2(engine, num_slots=S, dense_dim=13, cross_layers=args.cross_layers, hidden=hidden).to(device)
-    else:
-        model = DeepFM(engine, num_slots=S, dense_dim=13, hidden=hidden).to(device)
-    if fp32:
-        model.set_precision("fp32")
-    # the fused tower runs the whole dense side (bf16 operands, or exact fp32)
-    fused = getattr(model, "use_tower", False) and (not fp32 or model.tower.fp32)
-    C = model.dn.C
-    arena = DenseArena(model.parameters(), device, extra_grad=3 * C if multi and not dcn else 0)
-    if multi:
-        model.dn.group = dist.group.WORLD
-        model.dn.sync_stats = True
-        if fused and not dcn:
-            # data_norm batch statistics are summed across ranks in the SAME
-            # all-reduce as the dense gradients (tail of the gradient buffer)
-            model.dn.stats = arena.grad_tail(3 * C)
-            model.dn.stats_in_grad_bucket = True
-    # one update launch for the dense side: Adam + bf16 tower weight re-pack +
-    # data_norm summary update; grads zeroed by the same kernel
-    opt = FlatAdam(arena, lr=1e-3, clear_grad=True)
-    if fused:
-        opt.fuse(mlps=[model.mlp], data_norms=[model.dn])
-    # the dense all-reduce runs on its own communicator and side stream, started
-    # as soon as the tower's gradients are final: it overlaps the sparse push
-    ipc = None
-    if multi and (args.dense == "ipc" or args.same_gpu):
-        from paddlebox_amd.parallel.ipc import IpcMesh, IpcMeshError
+    res = measure(args.mlp_dtype, True)
+    dt, t_enq, loss, auc_stats, ipc = res["dt"], res["t_enq"], res["loss"], res["auc_stats"], res["ipc"]
+    overflow_1 = engine.check_overflow()
+    if ipc is not None:
+        ipc.check()
+    second = None
+    sec_dtype = args.secondary_dtype
+    if sec_dtype == "auto":
+        sec_dtype = "fp32" if (args.mlp_dtype == "bf16" and not dcn) else "none"
+    if sec_dtype != "none" and sec_dtype != args.mlp_dtype:
+        # same run, same sparse engine: the other MLP precision's step time
+        # (the reference fc computes in fp32 / TF32; the headline is bf16)
+        if ipc is not None:
+            ipc.close()
+        import gc
 
-        try:
-            ipc = IpcMesh(arena.grad.numel() * 4, device=device)
-            if not ipc.self_test():
-                ipc.close()
-                ipc = None
-                log(rank, "[bench] dense IPC mesh self-test failed; RCCL all-reduce")
-        except IpcMeshError as e:
-            ipc = None
-            log(rank, f"[bench] dense IPC mesh unavailable ({e}); RCCL all-reduce")
-    if multi and args.same_gpu and (ipc is None or engine.exchange_mode != "ipc"):
-        raise SystemExit("--same-gpu needs the IPC meshes (RCCL cannot run two ranks on one GPU)")
-    # RCCL dense all-reduce: its own communicator, so it overlaps the sparse
-    # exchange; the IPC meshes are independent of each other by construction
-    sync = DenseSync(arena, mode="grad_allreduce",
-                     overlap_group=dist.new_group(list(range(world))) if (multi and ipc is None) else None, ipc=ipc)
-    if getattr(model, "tower", None) is not None:
-        model.tower.on_dense_grads = sync.launch
+        gc.collect()
+        torch.cuda.empty_cache()
+        second = measure(sec_dtype, False)
+        ipc = second["ipc"]
+        log(rank, f"[bench] {sec_dtype} MLP: {second['dt'] / args.steps * 1e3:.4f} ms/step")
 
-    # every pinned batch buffer is streamed to the device once up front so the
-    # timed steps do not pay the driver's first-touch cost of a pinned range
-    scratch = torch.empty_like(host_batches[0]._flat, device=device)
-    for hb in host_batches:
-        scratch.copy_(hb._flat, non_blocking=True)
-    torch.cuda.synchronize()
-    del scratch
-    copy_stream = torch.cuda.Stream(device)
-    auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
-    auc_stats = torch.zeros(5, dtype=torch.float64, device=device)
-    fused_auc = fused
-    if fused_auc:  # streaming AUC accumulated by the tower's loss epilogue
-        model.tower.auc = (auc_table, auc_stats, None)
-
-    one = torch.ones((), device=device)  # persistent d loss / d loss: no fill kernel per step
-
-    def train_step(b):
-        loss, pred = model(b)
-        loss.backward(one)
-        sync.before_step()
-        opt.step(sync.grad_scale())
-        if not fused_auc:
-            auc_accumulate(pred, b.label, auc_table, auc_stats)
-        return loss.detach()
-
-    nb = len(host_batches)
-    graphed = None
-    if args.graph:
-        try:
-            from paddlebox_amd.runtime.graph_step import GraphedTrainStep
-
-            pre = (engine, lambda b: b.keys) if (args.prefetch and engine.can_prefetch()) else None
-            graphed = GraphedTrainStep(train_step, host_batches[0], device, prefetch=pre)
-            graphed.warm(host_batches, replays=args.graph_warm)
-            log(rank, f"[bench] training step captured into HIP graphs ({args.graph_warm} warm replays)")
-        except Exception as e:  # pragma: no cover - depends on runtime
-            log(rank, f"[bench] graph capture failed ({e!r}); running eagerly")
-            graphed = None
-
-    if graphed is not None:
-        graphed.load(0, host_batches[0])
-
-        def run(i):
-            graphed.load((i + 1) % graphed.n, host_batches[(i + 1) % nb])
-            return graphed.run(i % graphed.n)
-    else:
-        def fetch(i):
-            with torch.cuda.stream(copy_stream):
-                b = host_batches[i % nb].to(device, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(copy_stream)
-            return b, ev
-
-        pending = [fetch(0)]
-
-        def run(i):
-            b, ev = pending.pop()
-            pending.append(fetch(i + 1))
-            torch.cuda.current_stream().wait_event(ev)
-            for t in (b.keys, b.lod, b.dense, b.label, b.cvm):
-                t.record_stream(torch.cuda.current_stream())
-            return train_step(b)
-
-    if args.trace_steps and graphed is not None:
-        # diagnostics: per-step host time of the H2D load and the replay
-        tl, tr = [], []
-        for i in range(args.trace_steps):
-            t0 = time.perf_counter()
-            graphed.load((i + 1) % graphed.n, host_batches[(i + 1) % nb])
-            t1 = time.perf_counter()
-            graphed.run(i % graphed.n)
-            tr.append(time.perf_counter() - t1)
-            tl.append(t1 - t0)
-        torch.cuda.synchronize()
-        log(rank, "[bench] trace load us: " + " ".join(f"{x * 1e6:.0f}" for x in tl))
-        log(rank, "[bench] trace run  us: " + " ".join(f"{x * 1e6:.0f}" for x in tr))
-    for i in range(args.warmup):
-        run(i)
-    torch.cuda.synchronize()
-    if multi:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    loss = None
-    for i in range(args.steps):
-        loss = run(args.warmup + i)
-    t_enq = time.perf_counter() - t_start
-    torch.cuda.synchronize()
-    if multi:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t_start
-    if multi:
-        t = torch.tensor([dt], device=cdev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    log(rank, f"[bench] host enqueue {t_enq / args.steps * 1e3:.4f} ms/step, wall {dt / args.steps * 1e3:.4f} ms/step")
-    # diagnostics only (after the measurement): further windows of K steps
-    for w in range(args.diag_windows):
-        torch.cuda.synchronize()
-        t0w = time.perf_counter()
-        for i in range(args.steps):
-            run(args.warmup + args.steps * (w + 1) + i)
-        torch.cuda.synchronize()
-        log(rank, f"[bench] diag window {w}: {(time.perf_counter() - t0w) / args.steps * 1e3:.4f} ms/step")
-    if args.host_diag and graphed is not None:
-        # where the host time of a step goes: replay alone, H2D load alone, both
-        for name, fn in (("replay", lambda i: graphed.graphs[i % 2][0].replay()),
-                         ("load", lambda i: graphed.load(i % 2, host_batches[i % nb])),
-                         ("load+run", lambda i: run(i))):
-            for w in range(3):
-                torch.cuda.synchronize()
-                t0w = time.perf_counter()
-                for i in range(args.steps):
-                    fn(i)
-                th = time.perf_counter() - t0w
-                torch.cuda.synchronize()
-                tw = time.perf_counter() - t0w
-                log(rank, f"[bench] host-diag {name} window {w}: host {th / args.steps * 1e3:.4f} "
-                          f"wall {tw / args.steps * 1e3:.4f} ms/step")
-    overflow = engine.check_overflow()  # also raises if an IPC exchange timed out
+    overflow = engine.check_overflow() or overflow_1  # also raises if an IPC exchange timed out
     if ipc is not None:
         ipc.check()
     samples = B * world * args.steps
@@ -448,9 +486,14 @@ def main():
                 "dense_allreduce": ("ipc" if ipc is not None else "rccl") if multi else "none",
                 "sparse_exchange": engine.exchange_mode,
                 "same_gpu_rehearsal": bool(args.same_gpu),
-                "pipelined_pull": bool(graphed is not None and graphed.prefetch is not None),
+                "pipelined_pull": res["prefetch"],
                 "key_dedup": bool(engine.dedup),
                 "mlp_dtype": args.mlp_dtype,
+                **({f"{sec_dtype}_ms_per_step": round(second["dt"] / args.steps * 1e3, 4),
+                    f"{sec_dtype}_samples_per_s": round(B * world * args.steps / second["dt"], 1),
+                    f"{sec_dtype}_mlp": ("exact fp32 products on v_mfma_f32_16x16x4_f32 (the reference fc "
+                                         "precision), same run, same sparse engine")}
+                   if second is not None else {}),
                 "unique_keys_per_batch": round(sum(u_per_batch) / len(u_per_batch), 1),
                 "keys_per_batch": l_per_batch,
                 "u_over_l": round(u_over_l, 4),

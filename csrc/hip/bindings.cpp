@@ -338,7 +338,8 @@ class GpuTable {
     codec_check(c);
     check_cuda(rows, "rows");
     check_cuda(out, "out");
-    PBX_CHECK(out.dim() == 2 && out.size(0) >= n && out.size(1) >= 3 + c.D + c.De, "codec_pull: out shape");
+    const int need = 3 + (c.kind == 3 ? c.Wx : c.D + c.De);  // variable: one block of max(D, De)
+    PBX_CHECK(out.dim() == 2 && out.size(0) >= n && out.size(1) >= need, "codec_pull: out shape");
     if (uid.has_value() && uid->defined()) PBX_CHECK(uid->numel() >= n, "codec_pull: uid");
     else PBX_CHECK(rows.numel() >= n, "codec_pull: rows");
     launch_codec_pull(view(), c, ptr<int64_t>(rows), optr<int32_t>(uid), optr<int32_t>(n_dev), n, ptr<float>(out),
@@ -350,7 +351,7 @@ class GpuTable {
     codec_check(c);
     check_cuda(rows, "rows");
     check_cuda(push, "push");
-    PBX_CHECK(push.dim() == 2 && push.size(0) >= rows.numel() && push.size(1) >= 4 + c.D + c.De,
+    PBX_CHECK(push.dim() == 2 && push.size(0) >= rows.numel() && push.size(1) >= 4 + (c.kind == 3 ? c.Wx : c.D + c.De),
               "codec_update: push record width");
     launch_codec_update(view(), c, ptr<int64_t>(rows), ptr<float>(push), (int)push.size(1), optr<int32_t>(n_dev),
                         rows.numel(), cfg, seed, cur_stream());

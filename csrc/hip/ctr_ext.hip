@@ -22,6 +22,8 @@
 //   k_colsum_rows    ordered column reduction of per-block partial rows
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace pbx {
@@ -41,10 +43,16 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // v_mfma_f32_16x16x4 tiles; K staged through LDS 16 at a time (k-major, rows
 // padded to 68 floats).  16x16x4 operand layout: lane l feeds A[l%16][l/16]
 // and B[l/16][l%16]; accumulator register r is C[4(l/16)+r][l%16].
+// Split-K (g.ksplit > 1, small M x N with long K such as the dW GEMMs of
+// batch_fc): blockIdx.z = batch * ksplit + slice, each slice adds its partial
+// product with fp32 atomics into C (zeroed by the launcher unless
+// accumulating); slice 0 adds the bias.
 __global__ __launch_bounds__(256) void k_mgemm(SgemmArgs g) {
   __shared__ float As[16][68];
   __shared__ float Bs[16][68];
-  const int b = blockIdx.z;
+  const int b = blockIdx.z / g.ksplit, ks = blockIdx.z % g.ksplit;
+  const int kper = ((g.K + g.ksplit - 1) / g.ksplit + 15) / 16 * 16;
+  const int kbeg = ks * kper, kend = min(g.K, kbeg + kper);
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
@@ -56,15 +64,15 @@ __global__ __launch_bounds__(256) void k_mgemm(SgemmArgs g) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < g.K; k0 += 16) {
+  for (int k0 = kbeg; k0 < kend; k0 += 16) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int e = t + 256 * j;
       const int mm = e & 63, kk = e >> 6;
       const int gm = m0 + mm, gk = k0 + kk;
-      As[kk][mm] = (gm < g.M && gk < g.K) ? A[(int64_t)gm * g.rsA + (int64_t)gk * g.csA] : 0.f;
+      As[kk][mm] = (gm < g.M && gk < kend) ? A[(int64_t)gm * g.rsA + (int64_t)gk * g.csA] : 0.f;
       const int gn = n0 + mm;
-      Bs[kk][mm] = (gn < g.N && gk < g.K) ? Bm[(int64_t)gk * g.rsB + (int64_t)gn * g.csB] : 0.f;
+      Bs[kk][mm] = (gn < g.N && gk < kend) ? Bm[(int64_t)gk * g.rsB + (int64_t)gn * g.csB] : 0.f;
     }
     __syncthreads();
 #pragma unroll
@@ -85,39 +93,52 @@ __global__ __launch_bounds__(256) void k_mgemm(SgemmArgs g) {
     for (int j = 0; j < 2; ++j) {
       const int n = n0 + wn + j * 16 + fr;
       if (n >= g.N) continue;
-      const float bv = g.bias ? g.bias[(int64_t)b * g.sBias + n] * g.bias_scale : 0.f;
+      const float bv = (g.bias && ks == 0) ? g.bias[(int64_t)b * g.sBias + n] * g.bias_scale : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm + i * 16 + 4 * fk + r;
         if (m >= g.M) continue;
         float v = g.alpha * acc[i][j][r] + bv;
         float* dst = C + (int64_t)m * g.ldc + n;
-        if (g.accumulate) v += *dst;
-        *dst = v;
+        if (g.ksplit > 1) {
+          atomicAdd(dst, v);
+        } else {
+          if (g.accumulate) v += *dst;
+          *dst = v;
+        }
       }
     }
 }
 
 // column sums of a [batch][M][N] strided matrix into out[batch][N] (+=): bias
-// gradients of batch_fc / scaled_fc.  One thread per (batch, column).
-__global__ void k_colsum_strided(const float* __restrict__ x, int batch, int M, int N, int64_t sb, int64_t ld,
-                                 float* __restrict__ out, int64_t so, int accumulate) {
+// gradients of batch_fc / scaled_fc.  Block = 64 columns x 4 row phases over
+// a slice of kColSlice rows; the 4 phases meet in LDS and one fp32 atomic
+// per column adds the slice (out zeroed first unless accumulating): enough
+// workgroups for M in the thousands instead of one serial thread per column.
+constexpr int kColSlice = 512;
+__global__ __launch_bounds__(256) void k_colsum_strided(const float* __restrict__ x, int batch, int M, int N, int64_t sb,
+                                                        int64_t ld, float* __restrict__ out, int64_t so) {
+  __shared__ float part[4][64];
+  const int b = blockIdx.z;
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+  const int m0 = blockIdx.y * kColSlice, m1 = min(M, m0 + kColSlice);
+  float s = 0.f;
+  if (n < N) {
+    const float* p = x + (int64_t)b * sb + n;
+    for (int m = m0 + ph; m < m1; m += 4) s += p[(int64_t)m * ld];
+  }
+  part[ph][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ph == 0 && n < N) {
+    const float t = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+    atomicAdd(out + (int64_t)b * so + n, t);
+  }
+}
+
+__global__ void k_zero_strided(float* __restrict__ out, int batch, int N, int64_t so) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)batch * N) return;
-  const int b = (int)(t / N), n = (int)(t % N);
-  const float* p = x + (int64_t)b * sb + n;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int m = 0;
-  for (; m + 3 < M; m += 4) {
-    s0 += p[(int64_t)m * ld];
-    s1 += p[(int64_t)(m + 1) * ld];
-    s2 += p[(int64_t)(m + 2) * ld];
-    s3 += p[(int64_t)(m + 3) * ld];
-  }
-  for (; m < M; ++m) s0 += p[(int64_t)m * ld];
-  const float s = (s0 + s1) + (s2 + s3);
-  float* o = out + (int64_t)b * so + n;
-  *o = accumulate ? *o + s : s;
+  out[(t / N) * so + (t % N)] = 0.f;
 }
 
 // ---------------------------------------------------------------- int8 fc
@@ -211,6 +232,13 @@ __device__ __forceinline__ int ra_block(const int* ro, int ld, int i, int k, int
 // each an MFMA GEMM (v_mfma_f32_16x16x4_f32, exact fp32) with the operand
 // panels gathered into LDS 16 deep.  Only the blocks present in a tile are
 // visited (a 64-bit mask over the <= 64 blocks).
+// blocks b with b % gridDim.z == blockIdx.z
+__device__ __forceinline__ unsigned long long ra_group_mask(int R) {
+  unsigned long long m = 0ull;
+  for (int b = (int)blockIdx.z; b < R * R; b += (int)gridDim.z) m |= 1ull << b;
+  return m;
+}
+
 template <int R>
 __device__ __forceinline__ unsigned long long ra_tile_blocks(const int* ro, int ld, int i0, int B, int (*sblk)[64],
                                                              int (*sidx)[64], unsigned long long* used) {
@@ -243,7 +271,8 @@ __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, con
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i0 = blockIdx.x * 64, p0 = blockIdx.y * 64;
   const int wm = (w >> 1) * 32, wn = (w & 1) * 32, fr = lane & 15, fk = lane >> 4;
-  unsigned long long mask = ra_tile_blocks<R>(ro, ld, i0, B, sblk, sidx, &used);
+  // grid.z splits the parameter blocks of a tile over workgroups (b % gz == z)
+  unsigned long long mask = ra_tile_blocks<R>(ro, ld, i0, B, sblk, sidx, &used) & ra_group_mask(R);
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -288,7 +317,11 @@ __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, con
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = i0 + wm + i * 16 + 4 * fk + r;
-        if (m < B) out[(int64_t)m * P + p] = acc[i][j][r];
+        if (m >= B) continue;
+        if (gridDim.z > 1)
+          atomicAdd(&out[(int64_t)m * P + p], acc[i][j][r]);  // out zeroed by the launcher
+        else
+          out[(int64_t)m * P + p] = acc[i][j][r];
       }
     }
 }
@@ -307,9 +340,9 @@ __global__ __launch_bounds__(256) void k_ra_dexp(const float* __restrict__ dout,
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int j0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
   const int wm = (w >> 1) * 32, wn = (w & 1) * 32, fr = lane & 15, fk = lane >> 4;
-  unsigned long long mask = ra_tile_blocks<R>(ro, ld, j0, B, sblk, sidx, &used);
-  // rows of invalid pairs are zero
-  for (int e = t; e < 64 * R * 64; e += 256) {
+  unsigned long long mask = ra_tile_blocks<R>(ro, ld, j0, B, sblk, sidx, &used) & ra_group_mask(R);
+  // rows of invalid pairs are zero (written once, by group 0)
+  for (int e = t; blockIdx.z == 0 && e < 64 * R * 64; e += 256) {
     const int cc = e & 63, jk = e >> 6, jj = jk / R, k = jk % R;
     const int j = j0 + jj, c = c0 + cc;
     if (j < B && c < C && sblk[k][jj] < 0) dexp[((int64_t)j * R + k) * C + c] = 0.f;
@@ -667,17 +700,39 @@ __global__ void k_mdn_stats(const float* __restrict__ part, int rows, int C, flo
 
 }  // namespace
 
-void launch_sgemm(const SgemmArgs& g, hipStream_t s) {
-  if (g.M == 0 || g.N == 0 || g.batch == 0) return;
-  dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, g.batch);
+__global__ void k_zero_mat(float* __restrict__ C, int batch, int M, int N, int64_t sC, int64_t ldc) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)batch * M * N) return;
+  const int64_t b = t / ((int64_t)M * N), r = t % ((int64_t)M * N);
+  C[b * sC + (r / N) * ldc + (r % N)] = 0.f;
+}
+
+void launch_sgemm(const SgemmArgs& g0, hipStream_t s) {
+  if (g0.M == 0 || g0.N == 0 || g0.batch == 0) return;
+  SgemmArgs g = g0;
+  // fewer output tiles than ~2 waves of workgroups over 256 CUs and a long K:
+  // split K (each slice >= 256 deep)
+  const int64_t tiles = (int64_t)((g.N + 63) / 64) * ((g.M + 63) / 64) * g.batch;
+  g.ksplit = 1;
+  if (tiles < 512 && g.K >= 512) {
+    const int64_t want = (1024 + tiles - 1) / tiles;
+    g.ksplit = (int)std::max<int64_t>(1, std::min<int64_t>(want, g.K / 256));
+  }
+  if (g.ksplit > 1 && !g.accumulate)
+    hipLaunchKernelGGL(k_zero_mat, dim3(nblk((int64_t)g.batch * g.M * g.N)), dim3(256), 0, s, g.C, g.batch, g.M,
+                       g.N, g.sC, g.ldc);
+  dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, g.batch * g.ksplit);
   hipLaunchKernelGGL(k_mgemm, grid, dim3(256), 0, s, g);
 }
 
 void launch_colsum_strided(const float* x, int batch, int M, int N, int64_t sb, int64_t ld, float* out, int64_t so,
                            bool accumulate, hipStream_t s) {
   if (batch * N == 0) return;
-  hipLaunchKernelGGL(k_colsum_strided, dim3(nblk((int64_t)batch * N)), dim3(256), 0, s, x, batch, M, N, sb, ld, out,
-                     so, accumulate ? 1 : 0);
+  if (!accumulate)
+    hipLaunchKernelGGL(k_zero_strided, dim3(nblk((int64_t)batch * N)), dim3(256), 0, s, out, batch, N, so);
+  if (M == 0) return;
+  hipLaunchKernelGGL(k_colsum_strided, dim3((N + 63) / 64, (M + kColSlice - 1) / kColSlice, batch), dim3(256), 0, s,
+                     x, batch, M, N, sb, ld, out, so);
 }
 
 void launch_i8_quant(const float* x, int R, int C, int ldo, float expand, float clip, float range, bool transpose,
@@ -692,6 +747,14 @@ void launch_i8_gemm(const signed char* qx, const signed char* qwt, int M, int N,
   if (M == 0 || N == 0) return;
   hipLaunchKernelGGL(k_i8_gemm, dim3((N + 63) / 64, (M + 63) / 64), dim3(256), 0, s, qx, qwt, M, N, Kp, scale, bias,
                      y, ldy);
+}
+
+// workgroups per tile that split its parameter blocks: aim for ~2 waves of
+// workgroups over the 256 CUs
+static int ra_groups(int tiles, int R) {
+  int gz = (512 + tiles - 1) / (tiles > 0 ? tiles : 1);
+  gz = gz < 1 ? 1 : (gz > R * R ? R * R : gz);
+  return gz;
 }
 
 #define PBX_RA_DISPATCH(KER, GRID, ...)                                       \
@@ -709,13 +772,17 @@ void launch_i8_gemm(const signed char* qx, const signed char* qwt, int M, int N,
 void launch_rank_attention_fwd(const float* x, const int* ro, int ld, const float* W, int B, int C, int P, int R,
                                float* out, hipStream_t s) {
   if (B == 0) return;
-  PBX_RA_DISPATCH(k_ra_fwd, dim3((B + 63) / 64, (P + 63) / 64), x, ro, ld, W, B, C, P, out);
+  const int tiles = ((B + 63) / 64) * ((P + 63) / 64);
+  const int gz = ra_groups(tiles, R);
+  if (gz > 1) (void)hipMemsetAsync(out, 0, (size_t)B * P * sizeof(float), s);
+  PBX_RA_DISPATCH(k_ra_fwd, dim3((B + 63) / 64, (P + 63) / 64, gz), x, ro, ld, W, B, C, P, out);
 }
 
 void launch_rank_attention_bwd(const float* x, const float* dout, const int* ro, int ld, const float* W, int B, int C,
                                int P, int R, float* dexp, float* dx, float* dW, hipStream_t s) {
   if (B == 0) return;
-  PBX_RA_DISPATCH(k_ra_dexp, dim3((B + 63) / 64, (C + 63) / 64), dout, ro, ld, W, B, C, P, dexp);
+  const int gz = ra_groups(((B + 63) / 64) * ((C + 63) / 64), R);
+  PBX_RA_DISPATCH(k_ra_dexp, dim3((B + 63) / 64, (C + 63) / 64, gz), dout, ro, ld, W, B, C, P, dexp);
   hipLaunchKernelGGL(k_ra_dx, dim3(nblk((int64_t)B * C)), dim3(256), 0, s, dexp, ro, ld, B, C, R, dx);
   const int splits = B > 4096 ? 8 : (B > 512 ? 4 : 1);
   const int per = (B + splits - 1) / splits;

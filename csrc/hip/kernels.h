@@ -629,6 +629,7 @@ struct SgemmArgs {
   int64_t sC = 0, ldc = 0, sBias = 0;
   float bias_scale = 1.f, alpha = 1.f;
   int accumulate = 0;
+  int ksplit = 1;  // set by launch_sgemm: K slices per output tile (fp32 atomics)
 };
 void launch_sgemm(const SgemmArgs& g, hipStream_t s);
 void launch_colsum_strided(const float* x, int batch, int M, int N, int64_t sb, int64_t ld, float* out, int64_t so,

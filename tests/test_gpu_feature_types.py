@@ -231,8 +231,10 @@ def test_variable_feature_pull_push():
     assert out.shape == (B * S, 3 + D) and ex.shape == (B * S, 3 + De)
     assert float(out[B:].abs().sum()) == 0 and float(ex[:B].abs().sum()) == 0
     assert float(out[:B, 3:].abs().sum()) == 0 and float(ex[B:, 3:].abs().sum()) == 0
-    torch.autograd.backward([out, ex], [torch.randn(out.shape, generator=g).to(DEV),
-                                        torch.randn(ex.shape, generator=g).to(DEV)])
+    g1, g2 = torch.randn(out.shape, generator=g), torch.randn(ex.shape, generator=g)
+    g1[:, :2] = g1[:, :2].abs() + 1  # show / click (cvm inputs) > 0: score passes the create threshold
+    g2[:, :2] = g2[:, :2].abs() + 1
+    torch.autograd.backward([out, ex], [g1.to(DEV), g2.to(DEV)])
     before = eng.table.read(hk).cpu()
     sizes = before[:, size_col]
     assert torch.equal(sizes[:B], torch.full((B,), float(D)))
