@@ -96,6 +96,7 @@ class BoxWrapper:
         self.metrics = MetricRegistry(group)
         self.timers = StageTimers(self.device)
         self.mode = "hbm"
+        self.use_afs_api = False  # init_afs_api configured the remote file client
         self.host: Optional[CpuSparseTable] = None
         self.ssd = None  # tiered.SsdTier
         self.day_id = None
@@ -568,10 +569,18 @@ class BoxWrapper:
             self._expand = ExpandEmbedding(self._require_engine(), dim)
         return self._expand.pull(keys, lod, B, S, emb_size, ext_size)
 
-    def init_afs_api(self, fs_name: str = "", fs_user: str = "", pass_wd: str = "", conf_path: str = ""):
+    def init_afs_api(self, fs_name: str = "", fs_user: str = "", pass_wd: str = "", conf_path: str = "",
+                     hadoop_bin: str = ""):
+        """Configure the process-wide file client (reference InitAfsAPI,
+        box_wrapper.h:721-734: fs_ugi = "user,passwd"): model save/load paths
+        and the pass loaders' hdfs:// / afs:// files then go through it."""
         from ..utils.fs import BoxFileMgr
 
         self.fs = BoxFileMgr()
+        ugi = f"{fs_user},{pass_wd}" if (fs_user or pass_wd) else ""
+        if not self.fs.init(fs_name, ugi, conf_path, hadoop_bin=hadoop_bin):
+            raise RuntimeError("Called AFSAPI Init Interface Failed.")
+        self.use_afs_api = True
         return 0
 
     def print_device_info(self) -> str:

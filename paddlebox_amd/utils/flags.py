@@ -6,8 +6,8 @@ see the same values); otherwise a Python dict seeded from the environment.
 Flags accepted for compatibility whose mechanism does not exist in this
 design (documented, not silently ignored):
 
-* ``enable_pullpush_dedup_keys`` -- keys are always deduplicated: the fused
-  push (segmented merge + in-register Adagrad) is built on the dedup.
+* ``enable_pullpush_dedup_keys`` -- live: false selects the single-shard GPU step
+  without a key dedup (per-occurrence probe + leader-elected push merge).
 * ``padbox_record_pool_max_size``, ``padbox_slotpool_thread_num``,
   ``enbale_slotpool_auto_clear``, ``enable_slotpool_wait_release``,
   ``enable_slotrecord_reset_shrink`` -- there is no SlotRecord object pool:

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--hbm-cap", type=float, default=4e6)
     ap.add_argument("--ssd", type=str, default="")
     ap.add_argument("--mode", choices=("tiered", "hbm"), default="tiered")
+    ap.add_argument("--spill-unseen", type=float, default=1.0,
+                    help="write-back spills host rows unseen for >= this many days to SSD (0: every written-back row)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -38,7 +40,7 @@ def main():
     S = synth.S
     cap = int(args.hbm_cap) if args.mode == "tiered" else int(args.features)
     box = BoxWrapper(8, device=dev)
-    box.cfg.tier.spill_unseen_days = 1.0
+    box.cfg.tier.spill_unseen_days = args.spill_unseen
     box.initialize_gpu_and_load_model(slot_vector=list(range(1, S + 1)), max_keys=args.batch * S, capacity=cap,
                                       mode=args.mode, ssd_path=args.ssd or None)
     model = DeepFM(box.engine, num_slots=S, dense_dim=13, hidden=(400, 400, 400)).to(dev)
@@ -84,6 +86,11 @@ def main():
         "host_rows": box.host.size() if box.host is not None else 0,
         "ssd_rows": len(box.ssd) if box.ssd is not None else 0,
         "tier_stats": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()},
+        # staging of pass p+1 and write-back of pass p-1 run during pass p's training:
+        # the part of their time the training hid
+        "stage_s_total": round(st.get("stage_s", 0.0), 3),
+        "train_s_total": round(sum(r["train_ms"] for r in rows) / 1e3, 3),
+        "ssd_direct_io": bool(box.ssd.direct_io) if box.ssd is not None else None,
     }
     print(json.dumps(out), flush=True)
 

@@ -313,3 +313,29 @@ def test_dump_debug_flags(tmp_path):
     assert one == [f"{ids[2]}\tfc.tmp_0:2:{v(4)}:{v(5)}"]
     ai = run("c", {"FLAGS_dump_filed_same_as_aibox": True})
     assert ai[0] == f"{ids[0]}\tfc:0:{v(1)}"
+
+
+def test_init_afs_api_configures_the_file_client(tmp_path):
+    """init_afs_api ignored its arguments.  It now configures the
+    process-wide native client (reference InitAfsAPI, box_wrapper.h:721-734:
+    fs_ugi = "user,passwd") that model IO and the pass loaders use."""
+    from paddlebox_amd.ps.box_wrapper import BoxWrapper
+
+    box = BoxWrapper(8, device="cpu")
+    try:
+        fake = tmp_path / "hadoop"
+        fake.write_text("#!/bin/sh\necho \"$@\" >> " + str(tmp_path / "calls.txt") + "\n")
+        fake.chmod(0o755)
+        assert box.init_afs_api("afs://nn.example:9000", "alice", "s3cret", "/etc/hadoop",
+                                hadoop_bin=str(fake)) == 0
+        assert box.use_afs_api
+        pre = box.fs._m.remote_prefix()
+        assert "fs.default.name=" in pre and "afs://nn.example:9000" in pre
+        assert "hadoop.job.ugi=" in pre and "alice,s3cret" in pre
+        assert "--config" in pre and "/etc/hadoop" in pre
+        box.fs.makedir("afs://nn.example:9000/user/alice/model")
+        calls = (tmp_path / "calls.txt").read_text()
+        assert "-mkdir" in calls and "alice,s3cret" in calls and "/user/alice/model" in calls
+    finally:
+        box.fs.destory()
+        BoxWrapper._instance = None
