@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256) void k_mgemm(SgemmArgs g) {
 // a slice of kColSlice rows; the 4 phases meet in LDS and one fp32 atomic
 // per column adds the slice (out zeroed first unless accumulating): enough
 // workgroups for M in the thousands instead of one serial thread per column.
-constexpr int kColSlice = 512;
+constexpr int kColSlice = 128;
 __global__ __launch_bounds__(256) void k_colsum_strided(const float* __restrict__ x, int batch, int M, int N, int64_t sb,
                                                         int64_t ld, float* __restrict__ out, int64_t so) {
   __shared__ float part[4][64];
