@@ -304,7 +304,9 @@ def main():
             scratch.copy_(hb._flat, non_blocking=True)
         torch.cuda.synchronize()
         del scratch
-        copy_stream = torch.cuda.Stream(device)
+        from paddlebox_amd.runtime.streams import side_stream
+
+        copy_stream = side_stream(device, "graph_copy")
         auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
         auc_stats = torch.zeros(5, dtype=torch.float64, device=device)
         fused_auc = fused

@@ -196,7 +196,9 @@ class CtrTower:
 
     def _side_stream(self, dev):
         if self._side is None:
-            self._side = torch.cuda.Stream(dev)
+            from ..runtime.streams import side_stream
+
+            self._side = side_stream(dev, "tower_dw")
         return self._side
 
     def _dn_part(self, B, device):

@@ -270,7 +270,9 @@ class DenseSync:
         dev = self.a.grad.device
         cur = torch.cuda.current_stream(dev)
         if self._stream is None:
-            self._stream = torch.cuda.Stream(dev)
+            from ..runtime.streams import side_stream
+
+            self._stream = side_stream(dev, "dense_sync")
         self._stream.wait_stream(cur)
         with torch.cuda.stream(self._stream):
             self._allreduce_grad(self.overlap_group if self.overlap_group is not None else self.group)

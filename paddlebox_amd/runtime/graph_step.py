@@ -18,6 +18,8 @@ from typing import Any, Callable, List, Optional, Sequence
 
 import torch
 
+from .streams import side_stream
+
 from .. import _native
 from ..parallel.dense import join_grad_producers
 
@@ -91,7 +93,7 @@ class GraphedTrainStep:
         self.fields = _tensor_fields(example_batch)
         self.bufs = [clone_batch(example_batch, self.device) for _ in range(n_buffers)]
         cur = torch.cuda.current_stream(self.device)
-        s = torch.cuda.Stream(self.device)
+        s = side_stream(self.device, "graph_warmup")
         s.wait_stream(cur)
         with torch.cuda.stream(s):
             for _ in range(warmup):
@@ -106,7 +108,7 @@ class GraphedTrainStep:
         cur.wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.prefetch = prefetch
-        self._side = torch.cuda.Stream(self.device) if prefetch is not None else None
+        self._side = side_stream(self.device, "graph_prefetch") if prefetch is not None else None
         # buffer contents versions (bumped by load / fill) and the version each
         # buffer had when a replay prefetched it: a buffer reloaded after its
         # prefetch is prepared again before its own replay
@@ -142,7 +144,7 @@ class GraphedTrainStep:
         if prefetch is not None:
             prefetch[0].clear_prefetch()
         torch.cuda.synchronize(self.device)
-        self.copy_stream = torch.cuda.Stream(self.device)
+        self.copy_stream = side_stream(self.device, "graph_copy")
         self.ready = [torch.cuda.Event() for _ in self.bufs]
         self.free = [torch.cuda.Event() for _ in self.bufs]
         for e in self.free:
