@@ -200,6 +200,17 @@ class GpuTable {
     }
     return lock_;
   }
+  // per-row scratch of the table dedup (launch_table_dedup): occurrence
+  // counts (kept all-zero between batches) and the batch's unique id of a row
+  std::pair<int32_t*, int32_t*> dedup_rows() {
+    if (!cnt_row_.defined()) {
+      PBX_CHECK(values_.size(0) < (int64_t)INT32_MAX, "table dedup: table rows must fit int32");
+      auto opt4 = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device_);
+      cnt_row_ = torch::zeros({values_.size(0)}, opt4);
+      uid_row_ = torch::empty({values_.size(0)}, opt4);
+    }
+    return {ptr<int32_t>(cnt_row_), ptr<int32_t>(uid_row_)};
+  }
   Tensor& lead_buf(int64_t n) {
     if (!lead_.defined() || lead_.numel() < n) lead_ = torch::empty({n}, owner_lock().options());
     return lead_;
@@ -401,6 +412,7 @@ class GpuTable {
   int64_t last_overflow_ = 0;
   Tensor keys_, fill_, values_, stash_keys_, scratch_;
   Tensor lock_, lead_;  // owner_push: per-row leader word (-1 = free), per-record leader
+  Tensor cnt_row_, uid_row_;  // table dedup scratch (dedup_rows)
 };
 
 // --------------------------------------------------------------- dedup
@@ -465,6 +477,27 @@ struct DedupWorkspace {
     launch_dedup(ptr<uint64_t>(keys), n, mixed, ptr<uint64_t>(h_tmp), ptr<uint64_t>(h_sorted), ptr<int32_t>(idx_tmp),
                  ptr<int32_t>(perm), ptr<int32_t>(flags), ptr<int32_t>(scan), ptr<int32_t>(uid), ptr<uint64_t>(uniq_h),
                  ptr<int32_t>(seg), ptr<int32_t>(u_count), temp.data_ptr(), temp_bytes, cur_stream());
+    last_n = n;
+  }
+  // Single-shard dedup through the GPU table (launch_table_dedup): keys are
+  // raw feasigns; rows_u[u] = table row of unique u (st.rows), rows_occ the
+  // row of every occurrence.  Same uid / perm / seg / u_count contract.
+  Tensor rows_u, rows_occ;
+  void run_table(const Tensor& keys, GpuTable& t) {
+    check_cuda(keys, "keys");
+    const int64_t n = keys.numel();
+    PBX_CHECK(n <= cap, "dedup: more keys than workspace capacity");
+    PBX_CHECK(keys.scalar_type() == torch::kInt64 && keys.is_contiguous(), "run_table: keys must be int64");
+    if (!rows_u.defined()) {
+      auto o8 = perm.options().dtype(torch::kInt64);
+      rows_u = torch::empty({cap}, o8);
+      rows_occ = torch::empty({cap}, o8);
+      if (!rank.defined()) rank = torch::empty({cap}, perm.options());
+    }
+    auto rc = t.dedup_rows();
+    launch_table_dedup(t.view(), ptr<int64_t>(keys), n, ptr<int64_t>(rows_occ), ptr<int32_t>(rank), rc.first,
+                       rc.second, ptr<int64_t>(rows_u), ptr<int32_t>(uid), ptr<int32_t>(perm), ptr<int32_t>(seg),
+                       ptr<int32_t>(u_count), cur_stream());
     last_n = n;
   }
   int64_t last_n = 0;
@@ -1202,6 +1235,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<DedupWorkspace>(m, "DedupWorkspace")
       .def(py::init<int64_t, int, bool>(), py::arg("cap"), py::arg("device"), py::arg("hash") = true)
       .def("run", &DedupWorkspace::run, py::arg("keys"), py::arg("mixed") = false, py::arg("zero") = py::none())
+      .def("run_table", &DedupWorkspace::run_table)
+      .def_readonly("rows_u", &DedupWorkspace::rows_u)
+      .def_readonly("rows_occ", &DedupWorkspace::rows_occ)
       .def_readonly("hash", &DedupWorkspace::hash)
       .def_readonly("cap", &DedupWorkspace::cap)
       .def_readonly("h_sorted", &DedupWorkspace::h_sorted)

@@ -308,6 +308,14 @@ SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, con
                             float embedx_threshold, const std::string& keys_path, const std::string& vals_path,
                             int64_t chunk_rows, int threads, std::vector<uint64_t>* saved_mixed, int device,
                             hipStream_t s);
+// Single-shard dedup through the table itself: rows_occ[i] = row of raw key
+// keys[i] (-1: padding / absent), rows_u[u] = row of unique u, uid / perm /
+// seg / u_count as the hash dedup (u_count = [U, n_valid, -, cursor]).
+// cnt_row / uid_row: int32 per table row; cnt_row all-zero between calls
+// (re-zeroed by the call), uid_row needs no reset.
+void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows_occ, int32_t* rank,
+                        int32_t* cnt_row, int32_t* uid_row, int64_t* rows_u, int32_t* uid, int32_t* perm, int32_t* seg,
+                        int32_t* u_count, hipStream_t s);
 // Probe raw feasigns (mixed in the kernel, -1 = padding -> row -1).
 void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows, hipStream_t s);
 bool launch_push_merge_send(const PushMergeArgs& a, int dim, float* send, int send_stride, const int64_t* send_index,

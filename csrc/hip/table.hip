@@ -98,6 +98,176 @@ __global__ __launch_bounds__(256) void k_probe(TableDev t, const uint64_t* __res
   if (j == 0 && blk + g < nn) rows[blk + g] = r;
 }
 
+// Per-thread probe of one mixed key (8 x 16-B loads per bucket line, all in
+// flight at once): the table dedup below probes 4 keys per thread, so many
+// independent bucket reads overlap instead of one 16-lane group per key.
+__device__ __forceinline__ int64_t probe_thread(const TableDev& t, uint64_t key) {
+  if (key == kEmptyKey) return -1;
+#pragma unroll
+  for (int which = 0; which < 2; ++which) {
+    const uint64_t b = which == 0 ? bucket1(key, t.nb) : bucket2(key, t.nb);
+    const uint4* p = reinterpret_cast<const uint4*>(t.keys + b * kBucketSlots);
+    uint4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = p[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t k0 = (uint64_t)v[j].x | ((uint64_t)v[j].y << 32);
+      const uint64_t k1 = (uint64_t)v[j].z | ((uint64_t)v[j].w << 32);
+      if (k0 == key) return (int64_t)(b * kBucketSlots) + 2 * j;
+      if (k1 == key) return (int64_t)(b * kBucketSlots) + 2 * j + 1;
+    }
+  }
+  const uint32_t sn = t.stash_n ? *t.stash_n : 0u;
+  const uint32_t lim = sn < t.stash_cap ? sn : t.stash_cap;
+  for (uint32_t s = 0; s < lim; ++s)
+    if (t.stash_keys[s] == key) return (int64_t)(t.nb * kBucketSlots) + s;
+  return -1;
+}
+
+// Table dedup of a single-shard batch (the pass-resident table row IS the
+// unique id): one launch probes every occurrence and ranks it
+// within its row -- per block, occurrences are counted per row in an LDS
+// hash, then ONE global atomicAdd per distinct row per block on cnt_row[row]
+// returns the block's base; the block that finds the count at 0 owns the
+// row's unique id (one global atomic per block allocates the block's new
+// ids).  k_table_seg turns the counts into run starts (and re-zeroes them),
+// k_table_scatter writes perm.  Replaces the scratch-hash insert, rank and
+// cleanup plus the separate probe of the unique keys.
+constexpr int kTdItems = 1;
+constexpr int kTdLds = 512;
+__global__ __launch_bounds__(256) void k_table_rank(TableDev t, const uint64_t* __restrict__ keys, int64_t n,
+                                                    int64_t* __restrict__ rows_occ, int32_t* __restrict__ rank,
+                                                    int32_t* __restrict__ cnt_row, int32_t* __restrict__ uid_row,
+                                                    int64_t* __restrict__ rows_u, int32_t* __restrict__ u_count) {
+  __shared__ int32_t lkey[kTdLds];
+  __shared__ int32_t lcnt[kTdLds];
+  __shared__ int32_t lnew[kTdLds];
+  __shared__ int32_t nvalid_blk, nnew_blk, base_blk;
+  for (int e = threadIdx.x; e < kTdLds; e += blockDim.x) {
+    lkey[e] = -1;
+    lcnt[e] = 0;
+  }
+  if (threadIdx.x == 0) {
+    nvalid_blk = 0;
+    nnew_blk = 0;
+  }
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * (blockDim.x * kTdItems);
+  int64_t row[kTdItems];
+  int pos[kTdItems], lr[kTdItems];
+  int nv = 0;
+#pragma unroll
+  for (int it = 0; it < kTdItems; ++it) {
+    const int64_t i = i0 + it * blockDim.x + threadIdx.x;
+    const uint64_t k = i < n ? keys[i] : kEmptyKey;
+    row[it] = probe_thread(t, k == kEmptyKey ? kEmptyKey : mix64(k));
+    nv += row[it] >= 0;  // n_valid = occurrences placed in perm (absent keys are skipped like padding)
+  }
+#pragma unroll
+  for (int it = 0; it < kTdItems; ++it) {
+    pos[it] = -1;
+    if (row[it] < 0) continue;
+    const int32_t r = (int32_t)row[it];
+    unsigned e = ((unsigned)r * 2654435761u) & (kTdLds - 1);
+    for (;;) {
+      const int32_t old = atomicCAS(&lkey[e], -1, r);
+      if (old == -1 || old == r) break;
+      e = (e + 1) & (kTdLds - 1);
+    }
+    pos[it] = (int)e;
+    lr[it] = atomicAdd(&lcnt[e], 1);
+  }
+  if (nv) atomicAdd(&nvalid_blk, nv);
+  __syncthreads();
+  for (int e = threadIdx.x; e < kTdLds; e += blockDim.x) {
+    const int32_t r = lkey[e];
+    lnew[e] = -1;
+    if (r < 0) continue;
+    const int32_t base = atomicAdd(&cnt_row[r], lcnt[e]);
+    lcnt[e] = base;  // the block's base rank within row r
+    if (base == 0) lnew[e] = atomicAdd(&nnew_blk, 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    base_blk = nnew_blk ? atomicAdd(&u_count[0], nnew_blk) : 0;
+    if (nvalid_blk) atomicAdd(&u_count[1], nvalid_blk);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kTdLds; e += blockDim.x) {
+    if (lnew[e] < 0) continue;
+    const int32_t u = base_blk + lnew[e];
+    uid_row[lkey[e]] = u;
+    rows_u[u] = lkey[e];
+  }
+#pragma unroll
+  for (int it = 0; it < kTdItems; ++it) {
+    const int64_t i = i0 + it * blockDim.x + threadIdx.x;
+    if (i >= n) continue;
+    rows_occ[i] = row[it];
+    rank[i] = pos[it] >= 0 ? lcnt[pos[it]] + lr[it] : -1;
+  }
+}
+
+// run starts: block exclusive scan of the per-row counts of the block's
+// unique ids + one cursor atomic per block (runs contiguous, not id-ordered);
+// the row counts are re-zeroed for the next batch
+constexpr int kTdSegItems = 4;
+__global__ __launch_bounds__(256) void k_table_seg(const int64_t* __restrict__ rows_u, int32_t* __restrict__ cnt_row,
+                                                   int32_t* __restrict__ u_count, int32_t* __restrict__ seg) {
+  __shared__ int32_t wsum[4];
+  __shared__ int32_t base;
+  const int64_t U = u_count[0];
+  const int64_t b0 = (int64_t)blockIdx.x * (blockDim.x * kTdSegItems);
+  if (b0 >= U) return;  // block-uniform
+  const int64_t u0 = b0 + (int64_t)threadIdx.x * kTdSegItems;
+  int c[kTdSegItems];
+  int tot = 0;
+#pragma unroll
+  for (int it = 0; it < kTdSegItems; ++it) {
+    c[it] = 0;
+    if (u0 + it < U) {
+      const int64_t r = rows_u[u0 + it];
+      c[it] = cnt_row[r];
+      cnt_row[r] = 0;
+    }
+    tot += c[it];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = tot;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) base = atomicAdd(&u_count[3], wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+  __syncthreads();
+  int p = base + x - tot;
+  for (int i = 0; i < w; ++i) p += wsum[i];
+#pragma unroll
+  for (int it = 0; it < kTdSegItems; ++it) {
+    if (u0 + it < U) seg[u0 + it] = p;
+    p += c[it];
+  }
+}
+
+__global__ void k_table_scatter(const int64_t* __restrict__ rows_occ, const int32_t* __restrict__ rank,
+                                const int32_t* __restrict__ uid_row, const int32_t* __restrict__ seg, int64_t n,
+                                int32_t* __restrict__ uid, int32_t* __restrict__ perm) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows_occ[i];
+  if (r < 0) {
+    uid[i] = -1;
+    return;
+  }
+  const int32_t u = uid_row[r];
+  uid[i] = u;
+  perm[seg[u] + rank[i]] = (int32_t)i;
+}
+
 // Owner side of the sharded pull in one launch: probe every received key (one
 // 16-lane group per key, as k_probe) and copy its pull record (P floats,
 // zero padded to out_stride) straight into the answer buffer -- no dedup of
@@ -349,6 +519,19 @@ void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t
   if (n <= 0) return;
   hipLaunchKernelGGL(k_probe<true>, dim3(blocks_for(n, 16)), dim3(256), 0, s, t,
                      reinterpret_cast<const uint64_t*>(keys), n, nullptr, rows);
+}
+
+void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows_occ, int32_t* rank,
+                        int32_t* cnt_row, int32_t* uid_row, int64_t* rows_u, int32_t* uid, int32_t* perm, int32_t* seg,
+                        int32_t* u_count, hipStream_t s) {
+  launch_fill32(u_count, 0u, 4, s);  // [U, n_valid, -, segment cursor]
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_table_rank, dim3(blocks_for(n, 256 * kTdItems)), dim3(256), 0, s, t,
+                     reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, uid_row, rows_u, u_count);
+  hipLaunchKernelGGL(k_table_seg, dim3(blocks_for(n, 256 * kTdSegItems)), dim3(256), 0, s, rows_u, cnt_row, u_count,
+                     seg);
+  hipLaunchKernelGGL(k_table_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_occ, rank, uid_row, seg, n, uid,
+                     perm);
 }
 
 void launch_probe_gather(const TableDev& t, const uint64_t* h, int64_t n, int64_t* rows, float* out, int out_stride,

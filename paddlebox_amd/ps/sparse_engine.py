@@ -216,6 +216,9 @@ class SparseEngine:
                 self._setup_exchange(exchange or os.environ.get("PBX_SPARSE_EXCHANGE", "ipc"))
             # no-dedup single-shard step (see the docstring)
             self.dedup = bool(dedup) or self.sharded or self.codec is not None or self.dim not in (4, 8, 16, 32)
+            # single shard: dedup through the table itself (the row is the
+            # unique id): probe + rank in one launch, no scratch hash table
+            self.table_dedup = not self.sharded and os.environ.get("PBX_TABLE_DEDUP", "0") == "1"
             # ring of per-pull buffers (sort-free hash dedup everywhere: the
             # sender packs its unique keys per owner with a counting pass)
             self._slots = [_PullSlot(self) for _ in range(max(1, int(pull_ring)))]
@@ -245,6 +248,7 @@ class SparseEngine:
         else:
             self.table = CpuSparseTable(self.dim)
             self.dedup = True
+            self.table_dedup = False
         self.slot_ids = torch.tensor(slot_ids if slot_ids is not None else [], dtype=torch.float32,
                                      device=self.device)
         self._seed = 1234
@@ -400,8 +404,12 @@ class SparseEngine:
         sl = self._slots[slot % len(self._slots)]
         if sl.rows is None:
             sl.rows = torch.empty(self.max_keys, dtype=torch.int64, device=self.device)
-        sl.ws.run(keys, False)
-        self.table.t.probe_into(sl.ws.uniq_h[:L], sl.ws.u_count, sl.rows)
+        if self.table_dedup:
+            sl.ws.run_table(keys, self.table.t)
+            sl.rows = sl.ws.rows_u
+        else:
+            sl.ws.run(keys, False)
+            self.table.t.probe_into(sl.ws.uniq_h[:L], sl.ws.u_count, sl.rows)
         self._prepared[keys.data_ptr()] = (sl, L)
 
     def clear_prefetch(self):
@@ -440,6 +448,19 @@ class SparseEngine:
             return st
         sl = self._take_slot()
         ws = sl.ws
+        if self.table_dedup:
+            ws.run_table(keys, self.table.t)
+            if fill_occ:
+                h.fill_occurrence(lod, S, B, sl.occ_slot, sl.occ_ins)
+            st = PullState(B=B, S=S, L=L, lod=lod, uid=ws.uid, perm=ws.perm, counts=ws.u_count, slot=sl,
+                           gen=sl.gen)
+            st.rows = ws.rows_u[:L]
+            if self.auto_insert and not self.test_mode:
+                miss = (ws.rows_occ[:L] < 0) & (keys.reshape(-1) != -1)
+                if bool(miss.any()):
+                    self.table.insert_mixed(torch.unique(ref.mix64(keys.reshape(-1)[miss])), self.cfg.sgd)
+                    ws.run_table(keys, self.table.t)
+            return st
         # IPC exchange: the shard pack's per-owner counters are zeroed by the
         # dedup's first launch (no fill launches of their own)
         ipc = self.sharded and self.xmesh is not None
