@@ -287,7 +287,7 @@ class BoxWrapper:
         eng = self._require_engine()
         if eng.check_overflow():
             raise RuntimeError("sparse key exchange overflowed its per-peer capacity this pass; "
-                               "raise SparseEngine cap_factor")
+                               "raise SparseEngine cap_factor (or leave it unset: worst-case slots never overflow)")
         if self.tier is not None:
             # export now, D2H + host scatter + SSD spill in the background
             with self.timers.span("end_pass_writeback"):

@@ -144,7 +144,7 @@ class SparseEngine:
         capacity: int = 1 << 20,
         slot_ids: Optional[List[float]] = None,
         group=None,
-        cap_factor: float = 1.25,
+        cap_factor: Optional[float] = None,
         auto_insert: bool = False,
         comm: Optional[Comm] = None,
         pull_ring: int = 2,
@@ -206,12 +206,18 @@ class SparseEngine:
             self._sgd_native = cfg.sgd.to_native(self._hip)
             if self.sharded:
                 # per-peer exchange slots: exact when the pass's batches were
-                # pre-scanned (exchange_capacity_for), else a heuristic bound
-                # with a sticky device-side overflow flag
+                # pre-scanned (exchange_capacity_for); otherwise the worst case
+                # (every key of a batch owned by one peer), so the exchange can
+                # never overflow -- only counts[p] records of a slot travel over
+                # the IPC mesh, so the large slots cost HBM (~1 GB at 8 ranks and
+                # 213K keys per batch, nothing on 288 GB) but no bandwidth.
+                # cap_factor restores a smaller heuristic slot (sticky overflow flag).
                 if exchange_capacity is not None:
                     self.C = (int(exchange_capacity) + 63) // 64 * 64
-                else:
+                elif cap_factor is not None:
                     self.C = int(math.ceil(self.max_keys / self.world * cap_factor)) + 64
+                else:
+                    self.C = (self.max_keys + 63) // 64 * 64
             if self.sharded:
                 self._setup_exchange(exchange or os.environ.get("PBX_SPARSE_EXCHANGE", "ipc"))
             # no-dedup single-shard step (see the docstring)
