@@ -130,7 +130,7 @@ def main():
                     help="bf16: fused MFMA tower (default); fp32: the reference's fp32 fc precision")
     ap.add_argument("--secondary-dtype", choices=("auto", "fp32", "bf16", "none"), default="auto",
                     help="after the headline measurement, time the same K steps at this MLP precision in the same "
-                         "run and report it in config (auto: fp32 when the headline is bf16 DeepFM)")
+                         "run and report it in config (auto: fp32 when the headline is bf16 DeepFM on one GPU)")
     ap.add_argument("--model", choices=("deepfm", "dcn_v2"), default="deepfm",
                     help="deepfm = the headline config; dcn_v2 = BASELINE config 5 (cross layers on the MFMA GEMM)")
     ap.add_argument("--cross-layers", type=int, default=3)
@@ -437,7 +437,8 @@ def main():
     second = None
     sec_dtype = args.secondary_dtype
     if sec_dtype == "auto":
-        sec_dtype = "fp32" if (args.mlp_dtype == "bf16" and not dcn) else "none"
+        # one GPU: the driver's headline run; the N-GPU scaling runs keep one measurement
+        sec_dtype = "fp32" if (args.mlp_dtype == "bf16" and not dcn and world == 1) else "none"
     if sec_dtype != "none" and sec_dtype != args.mlp_dtype:
         # same run, same sparse engine: the other MLP precision's step time
         # (the reference fc computes in fp32 / TF32; the headline is bf16)
