@@ -224,7 +224,7 @@ class SparseEngine:
             self.dedup = bool(dedup) or self.sharded or self.codec is not None or self.dim not in (4, 8, 16, 32)
             # single shard: dedup through the table itself (the row is the
             # unique id): probe + rank in one launch, no scratch hash table
-            self.table_dedup = not self.sharded and os.environ.get("PBX_TABLE_DEDUP", "0") == "1"
+            self.table_dedup = not self.sharded and os.environ.get("PBX_TABLE_DEDUP", "1") != "0"
             # ring of per-pull buffers (sort-free hash dedup everywhere: the
             # sender packs its unique keys per owner with a counting pass)
             self._slots = [_PullSlot(self) for _ in range(max(1, int(pull_ring)))]
