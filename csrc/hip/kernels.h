@@ -564,7 +564,8 @@ struct TowerArgs {
   float dn_eps = 0.f;
   float* dn_stats = nullptr;
   int dw_splits = 2;
-  int debug = 0;  // timing experiments only (PBX_TOWER_DEBUG): 1 no loss reduction, 2 no dW reductions, 4 no dW GEMM
+  int debug = 0;  // timing experiments only (PBX_TOWER_DEBUG): 1 no loss reduction, 2 no dW reductions, 4 no dW GEMM,
+                  // 8 no fwd m-packed stores, 16 no output layer / loss
   // fp32 tower (f32 = 1): fp32 X0 row-major / MP32, fp32 dX0; widths padded to 16
   int f32 = 0;
   long long* stamps = nullptr;  // timing experiments only: per-wave s_memtime stamps (fp32 fwd)

@@ -117,7 +117,7 @@ __device__ __forceinline__ int64_t mp_off(int mb, int NB, int nb, int lane_p) {
 }
 
 __device__ __forceinline__ void fwd_epilogue(const f32x16& acc, const TowerLayerDev& ly, int nb, int m0, u16* dst,
-                                             int ldl, int lane) {
+                                             int ldl, int lane, bool mp = true) {
   const int c = lane & 31, h = lane >> 5;
   const int n = nb * 32 + c;
   const float bias = n < ly.N ? ly.bias[n] : 0.f;
@@ -135,7 +135,7 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16& acc, const TowerLayer
     uint2 pk;
     pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
     pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
-    *reinterpret_cast<uint2*>(ly.xmp + mp_off(m0 / 16 + (q >> 1), NB, nb, c + 32 * (q & 1)) + 4 * h) = pk;
+    if (mp) *reinterpret_cast<uint2*>(ly.xmp + mp_off(m0 / 16 + (q >> 1), NB, nb, c + 32 * (q & 1)) + 4 * h) = pk;
   }
 }
 
@@ -146,6 +146,14 @@ __global__ __launch_bounds__(TNT) void k_tower_fwd(TowerArgs a) {
   const int m0 = blockIdx.x * TBM;
   u16* src = lds;
   u16* dst = lds + TBM * ldl;
+  // loss-tail inputs and the output-layer weights, loaded ahead of the layers
+  const int NL = a.ly[a.L - 1].N;
+  TowerRowIn rin{0.f, 0.f, 0.f, 0.f};
+  if (w < 2) rin = tower_row_in(a, m0, lane, TBM);
+  constexpr int WO = 8;
+  float wo[WO];
+#pragma unroll
+  for (int j = 0; j < WO; ++j) wo[j] = lane + 64 * j < NL ? a.w_out[lane + 64 * j] : 0.f;
   {  // stage the X0 tile (row-major, zero rows past M)
     const int c8n = a.ly[0].Kp / 8;
     for (int i = tid; i < TBM * c8n; i += TNT) {
@@ -167,106 +175,78 @@ __global__ __launch_bounds__(TNT) void k_tower_fwd(TowerArgs a) {
       const bf16x8* w0p = wp + (int64_t)nb0 * KS * 64 + lane;
       if (two) mma_pair<true>(src, ldl, w0p, wp + (int64_t)nb1 * KS * 64 + lane, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
       else mma_pair<false>(src, ldl, w0p, w0p, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
-      fwd_epilogue(acc0, ly, nb0, m0, dst, ldl, lane);
-      if (two) fwd_epilogue(acc1, ly, nb1, m0, dst, ldl, lane);
+      const bool mp = !(a.debug & 8);
+      fwd_epilogue(acc0, ly, nb0, m0, dst, ldl, lane, mp);
+      if (two) fwd_epilogue(acc1, ly, nb1, m0, dst, ldl, lane, mp);
     }
     __syncthreads();
     u16* t = src;
     src = dst;
     dst = t;
   }
-  // output layer + sigmoid + log-loss (+ AUC), 4 rows per wave
-  __shared__ float red[TNW][6];
-  const int NL = a.ly[a.L - 1].N;
-  const float inv = 1.f / (float)a.M;
-  float sl = 0.f, s_ae = 0.f, s_se = 0.f, s_ps = 0.f, s_ls = 0.f, s_cnt = 0.f;
-  for (int rr = 0; rr < TBM / TNW; ++rr) {
-    const int r = w * (TBM / TNW) + rr;
-    const int m = m0 + r;
-    float s = 0.f;
-    for (int k = lane; k < NL; k += 64) s += bf2f(src[r * ldl + k]) * a.w_out[k];
+  if (a.debug & 16) return;
+  // output layer: 4 rows per wave, independent accumulations, w_out from
+  // registers; the logits meet in LDS for the loss tail
+  __shared__ float zrow[TBM];
+  {
+    constexpr int RPW = TBM / TNW;
+    float s[RPW];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0 && m < a.M) {
-      const float z = s + (a.b_out ? a.b_out[0] : 0.f) + (a.lin ? a.lin[m] : 0.f);
-      const float y = a.label[m];
-      const float p = 1.f / (1.f + __expf(-z));
-      a.pred[m] = p;
-      a.dz[m] = (p - y) * inv;
-      sl += fmaxf(z, 0.f) - z * y + log1pf(__expf(-fabsf(z)));
-      if (a.auc_table && (!a.auc_mask || a.auc_mask[m] != 0.f)) {
-        const int lab = y > 0.5f ? 1 : 0;
-        const int T = a.auc_buckets;
-        int pos = (int)(p * T);
-        pos = pos < 0 ? 0 : (pos > T - 1 ? T - 1 : pos);
-        atomicAdd(&a.auc_table[lab * T + pos], 1.0);
-        const float d = p - (float)lab;
-        s_ae += fabsf(d);
-        s_se += d * d;
-        s_ps += p;
-        s_ls += (float)lab;
-        s_cnt += 1.f;
+    for (int rr = 0; rr < RPW; ++rr) s[rr] = 0.f;
+#pragma unroll
+    for (int j = 0; j < WO; ++j) {
+      const int k = lane + 64 * j;
+      if (k < NL) {
+#pragma unroll
+        for (int rr = 0; rr < RPW; ++rr) s[rr] += bf2f(src[(w * RPW + rr) * ldl + k]) * wo[j];
       }
     }
-  }
-  if (lane == 0) {
-    red[w][0] = sl;
-    red[w][1] = s_ae;
-    red[w][2] = s_se;
-    red[w][3] = s_ps;
-    red[w][4] = s_ls;
-    red[w][5] = s_cnt;
+    for (int k = lane + 64 * WO; k < NL; k += 64) {  // widths past 512
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) s[rr] += bf2f(src[(w * RPW + rr) * ldl + k]) * a.w_out[k];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) s[rr] += __shfl_xor(s[rr], off);
+    if (lane < RPW) {
+      float mine = s[0];
+#pragma unroll
+      for (int rr = 1; rr < RPW; ++rr) mine = lane == rr ? s[rr] : mine;
+      zrow[w * RPW + lane] = mine;
+    }
   }
   __syncthreads();
-  __shared__ bool last;
-  if (a.debug & 1) return;
-  if (tid == 0) {
-    // hand-off without fences (MI355X_MICROARCH.md, valid-forms table row 1):
-    // one lane stores the partials write-through (sc1), waits for them, then
-    // adds to the ticket; the last adder reads them back with sc1 loads
-    float* pp = a.part + (int64_t)blockIdx.x * 8;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      float s = 0.f;
-      for (int v = 0; v < TNW; ++v) s += red[v][i];
-      __hip_atomic_store(&pp[i], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last && w == 0) {  // deterministic: fixed lane -> partial assignment and tree
-    float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (unsigned int k = lane; k < gridDim.x; k += 64) {
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-        acc[i] += __hip_atomic_load(&a.part[(int64_t)k * 8 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-      for (int off = 32; off > 0; off >>= 1) acc[i] += __shfl_xor(acc[i], off);
-    if (lane == 0) {
-      a.loss[0] = acc[0] * inv;
-      if (a.auc_stats && acc[5] > 0.f) {
-        for (int i = 0; i < 5; ++i) a.auc_stats[i] += (double)acc[1 + i];
-      }
-      *a.ticket = 0u;
-    }
-  }
+  tower_loss_tail(a, zrow, rin, m0, w, lane, TBM);
 }
 
 // dZ epilogue of the backward chain for output block kb of layer i: mask with
 // relu'(X_i) (read from X_i's m-packed copy at exactly the accumulator's
 // positions), write the LDS tile, the m-packed dZ_i and the column sums.
-__device__ __forceinline__ void bwd_epilogue(const f32x16& acc, const TowerLayerDev& prev, int kb, int m0, u16* dst,
-                                             int ldl, float* bp, int lane) {
+// The relu' masks are loaded before the block's MMA loop (bwd_mask) so their
+// latency hides under it.
+struct BwdMask {
+  uint2 v[4];
+};
+__device__ __forceinline__ BwdMask bwd_mask(const TowerLayerDev& prev, int kb, int m0, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  const int NB = prev.Np / 32;
+  BwdMask mk;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    mk.v[q] = *reinterpret_cast<const uint2*>(prev.xmp + mp_off(m0 / 16 + (q >> 1), NB, kb, c + 32 * (q & 1)) + 4 * h);
+  return mk;
+}
+
+__device__ __forceinline__ void bwd_epilogue(const f32x16& acc, const TowerLayerDev& prev, const BwdMask& mk, int kb,
+                                             int m0, u16* dst, int ldl, float* bp, int lane) {
   const int c = lane & 31, h = lane >> 5;
   const int NB = prev.Np / 32;
   float cs = 0.f;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int64_t off = mp_off(m0 / 16 + (q >> 1), NB, kb, c + 32 * (q & 1)) + 4 * h;
-    const uint2 xm = *reinterpret_cast<const uint2*>(prev.xmp + off);
+    const uint2 xm = mk.v[q];
     const u16 xs[4] = {(u16)(xm.x & 0xffff), (u16)(xm.x >> 16), (u16)(xm.y & 0xffff), (u16)(xm.y >> 16)};
     u16 o[4];
 #pragma unroll
@@ -355,12 +335,17 @@ __global__ __launch_bounds__(TNT) void k_tower_bwd(TowerArgs a) {
       const int kb1 = kb0 + TNW;
       const bool two = kb1 < KB;
       f32x16 acc0 = (f32x16){0}, acc1 = (f32x16){0};
+      BwdMask mk0, mk1;
+      if (i > 0) {
+        mk0 = bwd_mask(a.ly[i - 1], kb0, m0, lane);
+        if (two) mk1 = bwd_mask(a.ly[i - 1], kb1, m0, lane);
+      }
       const bf16x8* w0p = wtp + (int64_t)kb0 * NS * 64 + lane;
       if (two) mma_pair<true>(src, ldl, w0p, wtp + (int64_t)kb1 * NS * 64 + lane, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
       else mma_pair<false>(src, ldl, w0p, w0p, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
       if (i > 0) {
-        bwd_epilogue(acc0, a.ly[i - 1], kb0, m0, dst, ldl, bp, lane);
-        if (two) bwd_epilogue(acc1, a.ly[i - 1], kb1, m0, dst, ldl, bp, lane);
+        bwd_epilogue(acc0, a.ly[i - 1], mk0, kb0, m0, dst, ldl, bp, lane);
+        if (two) bwd_epilogue(acc1, a.ly[i - 1], mk1, kb1, m0, dst, ldl, bp, lane);
       } else {
         const int c = lane & 31, h = lane >> 5;
 #pragma unroll

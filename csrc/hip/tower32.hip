@@ -158,6 +158,14 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
   if (w >= 4) __builtin_amdgcn_s_setprio(1);
   long long* stp = a.stamps ? a.stamps + ((int64_t)blockIdx.x * NW + w) * 8 : nullptr;
   if (stp && lane == 0) stp[0] = __builtin_amdgcn_s_memtime();
+  // loss-tail inputs and the output-layer weights, loaded ahead of the layers
+  const int NL = a.ly[a.L - 1].N;
+  TowerRowIn rin{0.f, 0.f, 0.f, 0.f};
+  if (w < 2) rin = tower_row_in(a, m0, lane, BM);
+  constexpr int WO = 8;
+  float wo[WO];
+#pragma unroll
+  for (int j = 0; j < WO; ++j) wo[j] = lane + 64 * j < NL ? a.w_out[lane + 64 * j] : 0.f;
   {  // stage the X0 tile (zero rows past M)
     const int c4n = a.ly[0].Kp / 4;
     for (int i = tid; i < BM * c4n; i += NT) {
@@ -197,83 +205,40 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
     src = dst;
     dst = t;
   }
-  // output layer + sigmoid + log-loss (+ AUC), 4 rows per wave
-  __shared__ float red[NW][6];
-  const int NL = a.ly[a.L - 1].N;
-  const float inv = 1.f / (float)a.M;
-  float sl = 0.f, s_ae = 0.f, s_se = 0.f, s_ps = 0.f, s_ls = 0.f, s_cnt = 0.f;
-  for (int rr = 0; rr < BM / NW; ++rr) {
-    const int r = w * (BM / NW) + rr;
-    const int m = m0 + r;
-    float s = 0.f;
-    for (int k = lane; k < NL; k += 64) s += src[r * ldl + k] * a.w_out[k];
+  // output layer: 4 rows per wave, independent accumulations, w_out from
+  // registers; the logits meet in LDS for the loss tail
+  __shared__ float zrow[BM];
+  {
+    constexpr int RPW = BM / NW;
+    float s[RPW];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0 && m < a.M) {
-      const float z = s + (a.b_out ? a.b_out[0] : 0.f) + (a.lin ? a.lin[m] : 0.f);
-      const float y = a.label[m];
-      const float p = 1.f / (1.f + __expf(-z));
-      a.pred[m] = p;
-      a.dz[m] = (p - y) * inv;
-      sl += fmaxf(z, 0.f) - z * y + log1pf(__expf(-fabsf(z)));
-      if (a.auc_table && (!a.auc_mask || a.auc_mask[m] != 0.f)) {
-        const int lab = y > 0.5f ? 1 : 0;
-        const int T = a.auc_buckets;
-        int pos = (int)(p * T);
-        pos = pos < 0 ? 0 : (pos > T - 1 ? T - 1 : pos);
-        atomicAdd(&a.auc_table[lab * T + pos], 1.0);
-        const float d = p - (float)lab;
-        s_ae += fabsf(d);
-        s_se += d * d;
-        s_ps += p;
-        s_ls += (float)lab;
-        s_cnt += 1.f;
+    for (int rr = 0; rr < RPW; ++rr) s[rr] = 0.f;
+#pragma unroll
+    for (int j = 0; j < WO; ++j) {
+      const int k = lane + 64 * j;
+      if (k < NL) {
+#pragma unroll
+        for (int rr = 0; rr < RPW; ++rr) s[rr] += src[(w * RPW + rr) * ldl + k] * wo[j];
       }
+    }
+    for (int k = lane + 64 * WO; k < NL; k += 64) {  // widths past 512
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) s[rr] += src[(w * RPW + rr) * ldl + k] * a.w_out[k];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) s[rr] += __shfl_xor(s[rr], off);
+    if (lane < RPW) {
+      float mine = s[0];
+#pragma unroll
+      for (int rr = 1; rr < RPW; ++rr) mine = lane == rr ? s[rr] : mine;
+      zrow[w * RPW + lane] = mine;
     }
   }
   if (stp && lane == 0) stp[7] = __builtin_amdgcn_s_memtime();
-  if (lane == 0) {
-    red[w][0] = sl;
-    red[w][1] = s_ae;
-    red[w][2] = s_se;
-    red[w][3] = s_ps;
-    red[w][4] = s_ls;
-    red[w][5] = s_cnt;
-  }
   __syncthreads();
-  __shared__ bool last;
-  if (tid == 0) {
-    // sc1 partial stores + ticket; the last arriver reads them back with sc1
-    // loads (MI355X_MICROARCH.md valid-forms table, row 1)
-    float* pp = a.part + (int64_t)blockIdx.x * 8;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      float s = 0.f;
-      for (int v = 0; v < NW; ++v) s += red[v][i];
-      __hip_atomic_store(&pp[i], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last && w == 0) {
-    float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (unsigned int k = lane; k < gridDim.x; k += 64) {
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-        acc[i] += __hip_atomic_load(&a.part[(int64_t)k * 8 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-      for (int off = 32; off > 0; off >>= 1) acc[i] += __shfl_xor(acc[i], off);
-    if (lane == 0) {
-      a.loss[0] = acc[0] * inv;
-      if (a.auc_stats && acc[5] > 0.f) {
-        for (int i = 0; i < 5; ++i) a.auc_stats[i] += (double)acc[1 + i];
-      }
-      *a.ticket = 0u;
-    }
-  }
+  tower_loss_tail(a, zrow, rin, m0, w, lane, BM);
 }
 
 __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {

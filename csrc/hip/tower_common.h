@@ -84,6 +84,104 @@ __device__ inline void tower_col_reduce(const TowerArgs& a, int rb, int tbm) {
   }
 }
 
+// Per-row inputs of the loss tail, loaded by waves 0 and 1 (lane r = row r)
+// at kernel start so that their latency hides under the layer loop.
+struct TowerRowIn {
+  float lin, y, mask, bout;
+};
+__device__ inline TowerRowIn tower_row_in(const TowerArgs& a, int m0, int lane, int rows) {
+  TowerRowIn r{0.f, 0.f, 0.f, 0.f};
+  const int m = m0 + lane;
+  r.bout = a.b_out ? a.b_out[0] : 0.f;
+  if (lane < rows && m < a.M) {
+    r.lin = a.lin ? a.lin[m] : 0.f;
+    r.y = a.label[m];
+    r.mask = (a.auc_table && (!a.auc_mask || a.auc_mask[m] != 0.f)) ? 1.f : 0.f;
+  }
+  return r;
+}
+
+// Loss tail of the forward launches, once zrow[r] (the output-layer GEMV of
+// row r) is in LDS and the workgroup has synchronised.  One lane per row:
+// wave 0 computes the loss / AUC partial sums and runs the cross-workgroup
+// ticket; wave 1 stores pred / dz and adds the AUC histogram, so the drain
+// before wave 0's ticket waits only for its own six partial stores.  The
+// last workgroup reduces the partials in a fixed lane order and tree
+// (deterministic).  Semantics: sigmoid + log_loss (phi/kernels/gpu/log_loss_kernel.cu),
+// auc histogram (phi/kernels/gpu/auc_kernel.cu:25-80).
+__device__ inline void tower_loss_tail(const TowerArgs& a, const float* zrow, const TowerRowIn& in, int m0, int w,
+                                       int lane, int rows) {
+  if (w > 1) return;
+  const int m = m0 + lane;
+  const bool valid = lane < rows && m < a.M;
+  const float inv = 1.f / (float)a.M;
+  float z = 0.f, p = 0.f;
+  if (valid) {
+    z = zrow[lane] + in.bout + in.lin;
+    p = 1.f / (1.f + __expf(-z));
+  }
+  if (w == 1) {
+    if (valid) {
+      a.pred[m] = p;
+      a.dz[m] = (p - in.y) * inv;
+      if (in.mask != 0.f) {
+        const int lab = in.y > 0.5f ? 1 : 0;
+        const int T = a.auc_buckets;
+        int pos = (int)(p * T);
+        pos = pos < 0 ? 0 : (pos > T - 1 ? T - 1 : pos);
+        atomicAdd(&a.auc_table[lab * T + pos], 1.0);
+      }
+    }
+    return;
+  }
+  float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (valid) {
+    v[0] = fmaxf(z, 0.f) - z * in.y + log1pf(__expf(-fabsf(z)));
+    if (in.mask != 0.f) {
+      const float d = p - (in.y > 0.5f ? 1.f : 0.f);
+      v[1] = fabsf(d);
+      v[2] = d * d;
+      v[3] = p;
+      v[4] = in.y > 0.5f ? 1.f : 0.f;
+      v[5] = 1.f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[i] += __shfl_xor(v[i], off);
+  if (a.debug & 1) return;
+  int last = 0;
+  if (lane == 0) {
+    // hand-off without fences (MI355X_MICROARCH.md, valid-forms table row 1):
+    // write-through (sc1) partial stores, drained, then the ticket; the last
+    // adder reads them back with sc1 loads
+    float* pp = a.part + (int64_t)blockIdx.x * 8;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) __hip_atomic_store(&pp[i], v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
+  }
+  last = __shfl(last, 0);
+  if (!last) return;
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (unsigned int k = lane; k < gridDim.x; k += 64) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+      acc[i] += __hip_atomic_load(&a.part[(int64_t)k * 8 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+    for (int off = 32; off > 0; off >>= 1) acc[i] += __shfl_xor(acc[i], off);
+  if (lane == 0) {
+    a.loss[0] = acc[0] * inv;
+    if (a.auc_stats && acc[5] > 0.f) {
+      for (int i = 0; i < 5; ++i) a.auc_stats[i] += (double)acc[1 + i];
+    }
+    *a.ticket = 0u;
+  }
+}
+
 // Workgroup index -> work id such that consecutive work ids land on one XCD
 // (blocks are dealt to the 8 XCDs round-robin; speed only, never correctness).
 __device__ inline int xcd_work_id(int block, int n) {
