@@ -482,22 +482,28 @@ struct DedupWorkspace {
   // Single-shard dedup through the GPU table (launch_table_dedup): keys are
   // raw feasigns; rows_u[u] = table row of unique u (st.rows), rows_occ the
   // row of every occurrence.  Same uid / perm / seg / u_count contract.
+  // rows_given: rows_occ[:n] already holds the rows (probed by the split
+  // pull); keys then only give n.
   Tensor rows_u, rows_occ;
-  void run_table(const Tensor& keys, GpuTable& t) {
+  Tensor& table_rows_occ() {
+    if (!rows_u.defined()) {
+      auto o8 = perm.options().dtype(torch::kInt64);
+      rows_u = torch::empty({cap}, o8);
+      rows_occ = torch::full({cap}, -1, o8);  // kept all -1 between split pulls (k_table_scatter resets it)
+      if (!rank.defined()) rank = torch::empty({cap}, perm.options());
+    }
+    return rows_occ;
+  }
+  void run_table(const Tensor& keys, GpuTable& t, bool rows_given) {
     check_cuda(keys, "keys");
     const int64_t n = keys.numel();
     PBX_CHECK(n <= cap, "dedup: more keys than workspace capacity");
     PBX_CHECK(keys.scalar_type() == torch::kInt64 && keys.is_contiguous(), "run_table: keys must be int64");
-    if (!rows_u.defined()) {
-      auto o8 = perm.options().dtype(torch::kInt64);
-      rows_u = torch::empty({cap}, o8);
-      rows_occ = torch::empty({cap}, o8);
-      if (!rank.defined()) rank = torch::empty({cap}, perm.options());
-    }
+    table_rows_occ();
     auto rc = t.dedup_rows();
     launch_table_dedup(t.view(), ptr<int64_t>(keys), n, ptr<int64_t>(rows_occ), ptr<int32_t>(rank), rc.first,
                        rc.second, ptr<int64_t>(rows_u), ptr<int32_t>(uid), ptr<int32_t>(perm), ptr<int32_t>(seg),
-                       ptr<int32_t>(u_count), cur_stream());
+                       ptr<int32_t>(u_count), rows_given, cur_stream());
     last_n = n;
   }
   int64_t last_n = 0;
@@ -516,7 +522,8 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
                             float clk_coeff, float threshold, int quant_ratio, bool embed_threshold_filter,
                             float embed_threshold, int embed_thres_size, const c10::optional<Tensor>& dense,
                             int dense_col, const c10::optional<Tensor>& occ_slot,
-                            const c10::optional<Tensor>& occ_ins) {
+                            const c10::optional<Tensor>& occ_ins, const c10::optional<Tensor>& probe_keys,
+                            GpuTable* probe_table, const c10::optional<Tensor>& rows_out) {
   check_cuda(src, "src");
   check_cuda(lod, "lod");
   check_cuda(out, "out");
@@ -565,6 +572,21 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
     a.dense = ptr<float>(*dense);
     a.dense_dim = (int)dense->size(1);
     a.dense_col = dense_col;
+  }
+  if (probe_keys.has_value() && probe_keys->defined()) {  // fused probe of the split pull
+    PBX_CHECK(probe_table != nullptr && rows_out.has_value() && rows_out->defined(),
+              "fused probe needs the table and rows_out");
+    check_cuda(*probe_keys, "probe_keys");
+    PBX_CHECK(probe_keys->scalar_type() == torch::kInt64 && probe_keys->is_contiguous(), "probe_keys: int64");
+    PBX_CHECK(rows_out->scalar_type() == torch::kInt64 && rows_out->numel() >= probe_keys->numel(), "rows_out");
+    PBX_CHECK(!uid.has_value() || !uid->defined(), "fused probe replaces uid / src_index");
+    PBX_CHECK(a.src_stride % 4 == 0 && (E == 11 || E == 12 || E == 19 || E == 35),
+              "fused probe: vectorised record widths only");
+    PBX_CHECK(!occ_slot.has_value() || !occ_slot->defined() || occ_slot->numel() >= probe_keys->numel(),
+              "occ buffers too small");
+    a.probe_keys = reinterpret_cast<const uint64_t*>(probe_keys->data_ptr<int64_t>());
+    a.probe_t = probe_table->view();
+    a.rows_out = ptr<int64_t>(*rows_out);
   }
   launch_seqpool_cvm_fwd(a, cur_stream());
 }
@@ -1235,7 +1257,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<DedupWorkspace>(m, "DedupWorkspace")
       .def(py::init<int64_t, int, bool>(), py::arg("cap"), py::arg("device"), py::arg("hash") = true)
       .def("run", &DedupWorkspace::run, py::arg("keys"), py::arg("mixed") = false, py::arg("zero") = py::none())
-      .def("run_table", &DedupWorkspace::run_table)
+      .def("run_table", &DedupWorkspace::run_table, py::arg("keys"), py::arg("table"), py::arg("rows_given") = false)
+      .def("table_rows_occ", &DedupWorkspace::table_rows_occ)
       .def_readonly("rows_u", &DedupWorkspace::rows_u)
       .def_readonly("rows_occ", &DedupWorkspace::rows_occ)
       .def_readonly("hash", &DedupWorkspace::hash)
@@ -1264,7 +1287,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("show_coeff"), py::arg("clk_coeff"), py::arg("threshold"), py::arg("quant_ratio"),
         py::arg("embed_threshold_filter"), py::arg("embed_threshold"), py::arg("embed_thres_size"),
         py::arg("dense") = py::none(), py::arg("dense_col") = 0, py::arg("occ_slot") = py::none(),
-        py::arg("occ_ins") = py::none());
+        py::arg("occ_ins") = py::none(), py::arg("probe_keys") = py::none(),
+        py::arg("probe_table") = static_cast<GpuTable*>(nullptr), py::arg("rows_out") = py::none());
   m.def("push_merge", &push_merge, py::arg("dout"), py::arg("col_offset"), py::arg("cvm"), py::arg("cvm_offset"),
         py::arg("use_cvm"), py::arg("clk_filter"), py::arg("E"), py::arg("perm"), py::arg("uid"), py::arg("occ_slot"),
         py::arg("occ_ins"), py::arg("slot_ids"), py::arg("n_valid"), py::arg("push"), py::arg("push_index"),

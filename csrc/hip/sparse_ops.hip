@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
+#include "table_probe.h"
 
 namespace pbx {
 namespace {
@@ -97,6 +98,20 @@ __device__ __forceinline__ void load_row(const float* __restrict__ p, float* v) 
   }
 }
 
+// record index of occurrence k: probed from its feasign (fused probe of the
+// split pull, also recorded in rows_out) or read through uid / src_index
+__device__ __forceinline__ int64_t seqpool_record(const SeqpoolCvmArgs& a, int64_t k) {
+  if (a.probe_keys) {
+    const uint64_t kk = a.probe_keys[k];
+    const int64_t r = table_probe_thread(a.probe_t, kk == kEmptyKey ? kEmptyKey : mix64(kk));
+    a.rows_out[k] = r;
+    return r;
+  }
+  const int32_t u = a.uid ? a.uid[k] : (int32_t)k;
+  if (u < 0) return -1;
+  return a.src_index ? a.src_index[u] : (int64_t)u;
+}
+
 template <int E>
 __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -117,9 +132,7 @@ __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
       a.occ_slot[k] = s;
       a.occ_ins[k] = b;
     }
-    const int32_t u = a.uid ? a.uid[k] : (int32_t)k;
-    if (u < 0) continue;
-    const int64_t ri = a.src_index ? a.src_index[u] : (int64_t)u;
+    const int64_t ri = seqpool_record(a, k);
     if (ri < 0) continue;
     float v[E];
     load_row<E>(a.src + ri * (int64_t)a.src_stride, v);

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
+#include "table_probe.h"
 
 namespace pbx {
 
@@ -98,32 +99,8 @@ __global__ __launch_bounds__(256) void k_probe(TableDev t, const uint64_t* __res
   if (j == 0 && blk + g < nn) rows[blk + g] = r;
 }
 
-// Per-thread probe of one mixed key (8 x 16-B loads per bucket line, all in
-// flight at once): the table dedup below probes 4 keys per thread, so many
-// independent bucket reads overlap instead of one 16-lane group per key.
-__device__ __forceinline__ int64_t probe_thread(const TableDev& t, uint64_t key) {
-  if (key == kEmptyKey) return -1;
-#pragma unroll
-  for (int which = 0; which < 2; ++which) {
-    const uint64_t b = which == 0 ? bucket1(key, t.nb) : bucket2(key, t.nb);
-    const uint4* p = reinterpret_cast<const uint4*>(t.keys + b * kBucketSlots);
-    uint4 v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = p[j];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint64_t k0 = (uint64_t)v[j].x | ((uint64_t)v[j].y << 32);
-      const uint64_t k1 = (uint64_t)v[j].z | ((uint64_t)v[j].w << 32);
-      if (k0 == key) return (int64_t)(b * kBucketSlots) + 2 * j;
-      if (k1 == key) return (int64_t)(b * kBucketSlots) + 2 * j + 1;
-    }
-  }
-  const uint32_t sn = t.stash_n ? *t.stash_n : 0u;
-  const uint32_t lim = sn < t.stash_cap ? sn : t.stash_cap;
-  for (uint32_t s = 0; s < lim; ++s)
-    if (t.stash_keys[s] == key) return (int64_t)(t.nb * kBucketSlots) + s;
-  return -1;
-}
+// Per-thread probe: table_probe.h (shared with the fused probe of the seqpool).
+__device__ __forceinline__ int64_t probe_thread(const TableDev& t, uint64_t key) { return table_probe_thread(t, key); }
 
 // Table dedup of a single-shard batch (the pass-resident table row IS the
 // unique id): one launch probes every occurrence and ranks it
@@ -134,8 +111,12 @@ __device__ __forceinline__ int64_t probe_thread(const TableDev& t, uint64_t key)
 // ids).  k_table_seg turns the counts into run starts (and re-zeroes them),
 // k_table_scatter writes perm.  Replaces the scratch-hash insert, rank and
 // cleanup plus the separate probe of the unique keys.
+// PROBE = false: rows_occ already holds every occurrence's row (the split
+// pull probed it on the critical stream; this dedup runs on a side stream
+// under the dense forward).
 constexpr int kTdItems = 1;
 constexpr int kTdLds = 512;
+template <bool PROBE>
 __global__ __launch_bounds__(256) void k_table_rank(TableDev t, const uint64_t* __restrict__ keys, int64_t n,
                                                     int64_t* __restrict__ rows_occ, int32_t* __restrict__ rank,
                                                     int32_t* __restrict__ cnt_row, int32_t* __restrict__ uid_row,
@@ -160,8 +141,12 @@ __global__ __launch_bounds__(256) void k_table_rank(TableDev t, const uint64_t* 
 #pragma unroll
   for (int it = 0; it < kTdItems; ++it) {
     const int64_t i = i0 + it * blockDim.x + threadIdx.x;
-    const uint64_t k = i < n ? keys[i] : kEmptyKey;
-    row[it] = probe_thread(t, k == kEmptyKey ? kEmptyKey : mix64(k));
+    if (PROBE) {
+      const uint64_t k = i < n ? keys[i] : kEmptyKey;
+      row[it] = probe_thread(t, k == kEmptyKey ? kEmptyKey : mix64(k));
+    } else {
+      row[it] = i < n ? rows_occ[i] : -1;
+    }
     nv += row[it] >= 0;  // n_valid = occurrences placed in perm (absent keys are skipped like padding)
   }
 #pragma unroll
@@ -204,7 +189,7 @@ __global__ __launch_bounds__(256) void k_table_rank(TableDev t, const uint64_t* 
   for (int it = 0; it < kTdItems; ++it) {
     const int64_t i = i0 + it * blockDim.x + threadIdx.x;
     if (i >= n) continue;
-    rows_occ[i] = row[it];
+    if (PROBE) rows_occ[i] = row[it];
     rank[i] = pos[it] >= 0 ? lcnt[pos[it]] + lr[it] : -1;
   }
 }
@@ -253,12 +238,15 @@ __global__ __launch_bounds__(256) void k_table_seg(const int64_t* __restrict__ r
   }
 }
 
-__global__ void k_table_scatter(const int64_t* __restrict__ rows_occ, const int32_t* __restrict__ rank,
+// reset_rows: rows_occ is handed back all -1 (the split pull's fused probe
+// writes only the occurrences inside the lod, so the padding must read -1)
+__global__ void k_table_scatter(int64_t* __restrict__ rows_occ, const int32_t* __restrict__ rank,
                                 const int32_t* __restrict__ uid_row, const int32_t* __restrict__ seg, int64_t n,
-                                int32_t* __restrict__ uid, int32_t* __restrict__ perm) {
+                                int32_t* __restrict__ uid, int32_t* __restrict__ perm, int reset_rows) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t r = rows_occ[i];
+  if (reset_rows && r >= 0) rows_occ[i] = -1;
   if (r < 0) {
     uid[i] = -1;
     return;
@@ -523,15 +511,19 @@ void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t
 
 void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows_occ, int32_t* rank,
                         int32_t* cnt_row, int32_t* uid_row, int64_t* rows_u, int32_t* uid, int32_t* perm, int32_t* seg,
-                        int32_t* u_count, hipStream_t s) {
+                        int32_t* u_count, bool rows_given, hipStream_t s) {
   launch_fill32(u_count, 0u, 4, s);  // [U, n_valid, -, segment cursor]
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_table_rank, dim3(blocks_for(n, 256 * kTdItems)), dim3(256), 0, s, t,
-                     reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, uid_row, rows_u, u_count);
+  if (rows_given)
+    hipLaunchKernelGGL(k_table_rank<false>, dim3(blocks_for(n, 256 * kTdItems)), dim3(256), 0, s, t,
+                       reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, uid_row, rows_u, u_count);
+  else
+    hipLaunchKernelGGL(k_table_rank<true>, dim3(blocks_for(n, 256 * kTdItems)), dim3(256), 0, s, t,
+                       reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, uid_row, rows_u, u_count);
   hipLaunchKernelGGL(k_table_seg, dim3(blocks_for(n, 256 * kTdSegItems)), dim3(256), 0, s, rows_u, cnt_row, u_count,
                      seg);
   hipLaunchKernelGGL(k_table_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_occ, rank, uid_row, seg, n, uid,
-                     perm);
+                     perm, rows_given ? 1 : 0);
 }
 
 void launch_probe_gather(const TableDev& t, const uint64_t* h, int64_t n, int64_t* rows, float* out, int out_stride,

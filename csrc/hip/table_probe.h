@@ -1,0 +1,38 @@
+// Device-side probe of the bucketized cuckoo table (table.hip layout), shared
+// by the table kernels and the fused probe of the split pull's seqpool.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace pbx {
+
+// Per-thread probe of one mixed key (8 x 16-B loads per bucket line, all in
+// flight at once): used where every thread owns one occurrence (the table
+// dedup, the split pull's seqpool), so many independent bucket reads overlap
+// instead of one 16-lane group per key.
+__device__ __forceinline__ int64_t table_probe_thread(const TableDev& t, uint64_t key) {
+  if (key == kEmptyKey) return -1;
+#pragma unroll
+  for (int which = 0; which < 2; ++which) {
+    const uint64_t b = which == 0 ? fast_range64(key, t.nb) : fast_range64(rehash64(key), t.nb);
+    const uint4* p = reinterpret_cast<const uint4*>(t.keys + b * kBucketSlots);
+    uint4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = p[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t k0 = (uint64_t)v[j].x | ((uint64_t)v[j].y << 32);
+      const uint64_t k1 = (uint64_t)v[j].z | ((uint64_t)v[j].w << 32);
+      if (k0 == key) return (int64_t)(b * kBucketSlots) + 2 * j;
+      if (k1 == key) return (int64_t)(b * kBucketSlots) + 2 * j + 1;
+    }
+  }
+  const uint32_t sn = t.stash_n ? *t.stash_n : 0u;
+  const uint32_t lim = sn < t.stash_cap ? sn : t.stash_cap;
+  for (uint32_t s = 0; s < lim; ++s)
+    if (t.stash_keys[s] == key) return (int64_t)(t.nb * kBucketSlots) + s;
+  return -1;
+}
+
+}  // namespace pbx

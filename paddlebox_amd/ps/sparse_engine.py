@@ -36,6 +36,7 @@ from .config import PSConfig, SparseSGDConfig, padded, pull_width, push_width
 from .cpu_table import CpuSparseTable
 from .feature_types import FeatureCodec
 from .gpu_table import GpuSparseTable
+from ..runtime.streams import side_stream
 
 
 @dataclass
@@ -225,6 +226,12 @@ class SparseEngine:
             # single shard: dedup through the table itself (the row is the
             # unique id): probe + rank in one launch, no scratch hash table
             self.table_dedup = not self.sharded and os.environ.get("PBX_TABLE_DEDUP", "1") != "0"
+            # ... split off the critical path (_pull_split, PBX_SPLIT_PULL=1):
+            # measured slower on one MI355X (same-box interleaved A/B, 3 reps:
+            # 0.283 vs 0.263-0.268 ms/step, profiles/r3_s2_split_pull_ab.txt) --
+            # the side-stream dedup's atomics slow the concurrent head / tower
+            # forward more than the overlap saves -- so it stays opt-in
+            self.split_pull = os.environ.get("PBX_SPLIT_PULL", "0") == "1"
             # ring of per-pull buffers (sort-free hash dedup everywhere: the
             # sender packs its unique keys per owner with a counting pass)
             self._slots = [_PullSlot(self) for _ in range(max(1, int(pull_ring)))]
@@ -255,6 +262,7 @@ class SparseEngine:
             self.table = CpuSparseTable(self.dim)
             self.dedup = True
             self.table_dedup = False
+        self._pending_dedup = None
         self.slot_ids = torch.tensor(slot_ids if slot_ids is not None else [], dtype=torch.float32,
                                      device=self.device)
         self._seed = 1234
@@ -347,6 +355,9 @@ class SparseEngine:
         h = self._hip
         if not self.dedup and sp.cvm_offset == 2:
             return self._pull_nodedup(keys, lod, B, S, out, col_offset, sp, dense, dense_col)
+        if (self.table_dedup and self.split_pull and self.codec is None
+                and keys.data_ptr() not in self._prepared):
+            return self._pull_split(keys, lod, B, S, out, col_offset, sp, dense, dense_col)
         # the occurrence map is written by the seqpool launch itself
         st = self._pull_common(keys, lod, B, S, fill_occ=False)
         sl = st.slot
@@ -390,6 +401,70 @@ class SparseEngine:
         st.rows = rows
         st.extra["nodedup"] = True
         return st
+
+    def _pull_split(self, keys, lod, B, S, out, col_offset, sp, dense, dense_col) -> PullState:
+        """Single-shard pull with the dedup split off the critical path: one
+        launch probes every occurrence and pools straight from its table row
+        (the seqpool's fused probe, which also records the rows); the table
+        dedup (per-row ranks, run starts, perm) that only the push needs runs
+        on a side stream, overlapping the dense forward, and the push joins
+        it.  The reference orders DedupKeysAndFillIdx before PullSparseGPU
+        (box_wrapper_impl.h:152-155); here the dense step never waits for it."""
+        h = self._hip
+        keys = keys.reshape(-1)
+        L = keys.numel()
+        assert L <= self.max_keys, f"batch has {L} keys > engine max_keys {self.max_keys}"
+        self._join_dedup()
+        sl = self._take_slot()
+        ws = sl.ws
+        rows = ws.table_rows_occ()[:L]  # all -1 outside the lod between pulls
+        if dense is not None:
+            dense = dense.contiguous().float()
+
+        def pool():
+            h.seqpool_cvm_fwd(self.table.values, None, None, lod, S, B, self.E, out, col_offset, sp.use_cvm,
+                              sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter, sp.show_coeff,
+                              sp.clk_coeff, sp.threshold, sp.quant_ratio, sp.embed_threshold_filter,
+                              sp.embed_threshold, sp.embed_thres_size if not sp.use_cvm else 0, dense, dense_col,
+                              occ_slot=sl.occ_slot, occ_ins=sl.occ_ins, probe_keys=keys, probe_table=self.table.t,
+                              rows_out=rows)
+
+        pool()
+        if self.auto_insert and not self.test_mode:
+            miss = (rows < 0) & (keys != -1)
+            if bool(miss.any()):
+                self.table.insert_mixed(torch.unique(ref.mix64(keys[miss])), self.cfg.sgd)
+                pool()
+        st = PullState(B=B, S=S, L=L, lod=lod, uid=ws.uid, perm=ws.perm, counts=ws.u_count, slot=sl, gen=sl.gen)
+        st.rows = ws.rows_u[:L]
+        if self.test_mode:
+            rows.fill_(-1)  # no push, no dedup: restore the all -1 invariant here
+            return st
+        cur = torch.cuda.current_stream(self.device)
+        # the tower's dW stream: a process gets GPU_MAX_HW_QUEUES (4) hardware
+        # queues, and a fifth stream lands on the batch-copy queue, where the
+        # next batch's H2D DMA blocks this dedup (measured 0.35 vs 0.26 ms per
+        # step); the dedup finishes long before the dW GEMM is issued there
+        side = side_stream(self.device, "tower_dw")
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            ws.run_table(keys, self.table.t, True)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        st.extra["dedup_event"] = ev
+        self._pending_dedup = ev
+        return st
+
+    def _join_dedup(self, st: Optional[PullState] = None):
+        """Make the current stream wait for a split pull's side-stream dedup
+        (the push of that batch, or the next pull if the push never ran)."""
+        ev = st.extra.pop("dedup_event", None) if st is not None else None
+        if ev is None:
+            ev = self._pending_dedup
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            if ev is self._pending_dedup:
+                self._pending_dedup = None
 
     def can_prefetch(self) -> bool:
         """Prefetched pulls need a fixed key set during training: GPU, one
@@ -540,6 +615,8 @@ class SparseEngine:
         if not self.is_gpu:
             return self._cpu_push(st, dout, cvm, col_offset, sp, bs_scale)
         sl = self._check_slot(st)
+        if "dedup_event" in st.extra:
+            self._join_dedup(st)
         ws = sl.ws
         h = self._hip
         L = st.L

@@ -29,3 +29,17 @@ span = (int(rows[idx[-1]]["Start_Timestamp"]) - int(rows[idx[0]]["Start_Timestam
 print(f"steps={n} wall/step={span:.1f}us kernel-busy/step={busy / n:.1f}us launches/step={sum(cnt.values()) / n:.1f}")
 for k, v in sorted(agg.items(), key=lambda kv: -kv[1]):
     print(f"{k:60s} {cnt[k] / n:5.1f}x {v / n:8.1f}us")
+
+# timeline of the last full step: start offset / duration per kernel (gaps show
+# launch latency, overlap shows the side streams)
+s, e = idx[-2], idx[-1]
+t0 = int(rows[s]["Start_Timestamp"])
+# include the kernels of the same step launched before the anchor
+prev = idx[-3] if len(idx) >= 3 else s
+print("\ntimeline (us from the anchor of the last step; negative = before it):")
+for r in rows[prev:e]:
+    st = (int(r["Start_Timestamp"]) - t0) / 1e3
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    n = r["Kernel_Name"].replace("pbx::(anonymous namespace)::", "").replace("void ", "").split("(")[0][:50]
+    if st > -200:
+        print(f"  {st:8.1f} {st + d:8.1f} {d:7.1f}  {n}")

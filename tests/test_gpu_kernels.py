@@ -517,3 +517,40 @@ def test_shrink_reaches_stash_rows():
     assert deleted == 300
     assert bool((t.probe(h) < 0).all())
     assert int(t.t.stash_n()) == 0
+
+
+def test_split_pull_matches_inline_dedup():
+    """Split pull (fused probe in the seqpool, table dedup on a side stream
+    joined by the push) == the inline table dedup, over batches of different
+    sizes in -1 padded key buffers (the rows buffer must read -1 outside the
+    lod on every pull)."""
+    synth = CriteoSynth(total_features=30000, alpha=1.2, seed=11, device=DEV)
+    batches = [synth.batch(n) for n in (512, 128, 384, 256)]
+    engs = []
+    for split in (True, False):
+        torch.manual_seed(0)
+        e = _engine()
+        e.split_pull = split
+        for b in batches:
+            e.register_keys(b.keys, init_embedx=True)
+        engs.append(e)
+    allk = torch.cat([b.keys.reshape(-1) for b in batches])
+    h = torch.unique(ref.mix64(allk[allk != -1]))
+    engs[1].table.assign(h, engs[0].table.read(h))
+    sp = SeqpoolParams()
+    for it in range(6):
+        b = batches[it % len(batches)]
+        pad = torch.full((97,), -1, dtype=torch.int64, device=DEV)
+        keys = torch.cat([b.keys.reshape(-1), pad])
+        outs = []
+        for e in engs:
+            out = torch.zeros(b.B, b.S * 11, device=DEV)
+            st = e.pull_seqpool_cvm(keys, b.lod, b.B, b.S, out, 0, sp)
+            dout = torch.sin(out * 7.0 + it) * 0.01
+            e.push_seqpool_cvm(st, dout, b.cvm, 0, sp, float(b.B))
+            outs.append(out)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(outs[0], outs[1], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(engs[0].table.read(h), engs[1].table.read(h), rtol=1e-5, atol=1e-6)
+    rows = engs[0]._slots[0].ws.table_rows_occ()
+    assert bool((rows == -1).all()), "rows buffer not handed back all -1"
