@@ -103,6 +103,17 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+
+def _build_summary() -> dict:
+    """Provenance of the loaded gfx950 libraries (build stamp vs this tree's sources)."""
+    from paddlebox_amd import _native
+
+    bi = _native.build_info()
+    st = bi["stamp"] or {}
+    return {"sources": st.get("sources"), "sources_match_tree": bi["matches_tree"], "hipcc": st.get("hipcc"),
+            "built_at": st.get("built_at")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -497,6 +508,7 @@ def main():
                     f"{sec_dtype}_mlp": ("exact fp32 products on v_mfma_f32_16x16x4_f32 (the reference fc "
                                          "precision), same run, same sparse engine")}
                    if second is not None else {}),
+                "native_build": _build_summary(),
                 "unique_keys_per_batch": round(sum(u_per_batch) / len(u_per_batch), 1),
                 "keys_per_batch": l_per_batch,
                 "u_over_l": round(u_over_l, 4),

@@ -79,3 +79,47 @@ def so_paths():
         if mod is not None:
             out[name] = os.path.abspath(mod.__file__)
     return out
+
+
+# ---------------------------------------------------------------- build provenance
+_SRC_DIRS = ("csrc",)
+_SRC_SUFFIXES = (".hip", ".cpp", ".cc", ".h")
+
+
+def sources_digest(root: str = None) -> str:
+    """sha256 over the native sources (path + bytes, sorted): what the in-tree
+    libraries must have been built from."""
+    import hashlib
+
+    root = root or os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    h = hashlib.sha256()
+    files = []
+    for d in _SRC_DIRS:
+        for dp, _, fns in os.walk(os.path.join(root, d)):
+            files += [os.path.join(dp, f) for f in fns if f.endswith(_SRC_SUFFIXES)]
+    for f in sorted(files):
+        h.update(os.path.relpath(f, root).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_info() -> dict:
+    """Provenance of the loaded libraries: the stamp written by the build
+    (__graft_entry__.build: sources digest, hipcc version, arch, time) and
+    whether the sources in this tree still match it (False = stale binary)."""
+    import json
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    info = {"stamp": None, "sources_now": None, "matches_tree": None}
+    try:
+        with open(os.path.join(here, "_build_info.json")) as f:
+            info["stamp"] = json.load(f)
+    except (OSError, ValueError):
+        return info
+    try:
+        info["sources_now"] = sources_digest()
+        info["matches_tree"] = info["sources_now"] == info["stamp"].get("sources")
+    except OSError:
+        pass
+    return info
