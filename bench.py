@@ -104,6 +104,21 @@ def dry_run(args, world, rank):
 
 
 
+
+def graph_steps_for(steps: int, warmup: int, requested: int = 0) -> int:
+    """Steps per captured graph: every timed and warmup step still runs in
+    full; only the graph-launch boundary (and the wait on the batch copy) is
+    paid once per K steps instead of once per step."""
+    if requested > 0:
+        if steps % requested or warmup % requested:
+            raise SystemExit(f"--graph-steps {requested} must divide --steps {steps} and --warmup {warmup}")
+        return requested
+    for k in range(8, 0, -1):
+        if steps % k == 0 and warmup % k == 0:
+            return k
+    return 1
+
+
 def _build_summary() -> dict:
     """Provenance of the loaded gfx950 libraries (build stamp vs this tree's sources)."""
     from paddlebox_amd import _native
@@ -131,6 +146,9 @@ def main():
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--diag-windows", type=int, default=0,
                     help="after the measurement, time this many more K-step windows (stderr only)")
+    ap.add_argument("--graph-steps", type=int, default=1,
+                    help="training steps per captured HIP graph (0 = auto: the largest k <= 8 dividing both --steps "
+                         "and --warmup).  Default 1: K = 5 / 8 measured no faster (profiles/r3_s2_multistep_graph.txt)")
     ap.add_argument("--graph-warm", type=int, default=32,
                     help="load+replay cycles run right after capture (runtime warm-up, part of graph setup)")
     ap.add_argument("--trace-steps", type=int, default=0,
@@ -336,13 +354,15 @@ def main():
             return loss.detach()
 
         nb = len(host_batches)
+        K = graph_steps_for(args.steps, args.warmup, args.graph_steps)
         graphed = None
         if args.graph:
             try:
                 from paddlebox_amd.runtime.graph_step import GraphedTrainStep
 
                 pre = (engine, lambda b: b.keys) if (args.prefetch and engine.can_prefetch()) else None
-                graphed = GraphedTrainStep(train_step, host_batches[0], device, prefetch=pre)
+                graphed = GraphedTrainStep(train_step, host_batches[0], device, prefetch=pre,
+                                           steps_per_graph=K if pre is None else 1)
                 graphed.warm(host_batches, replays=args.graph_warm)
                 log(rank, f"[bench] training step captured into HIP graphs ({args.graph_warm} warm replays)")
             except Exception as e:  # pragma: no cover - depends on runtime
@@ -350,12 +370,19 @@ def main():
                 graphed = None
 
         if graphed is not None:
-            graphed.load(0, host_batches[0])
+            K = graphed.K  # run(i) trains group i: steps i*K .. i*K+K-1
+
+            def group(i):
+                return host_batches[i % nb] if K == 1 else [host_batches[(i * K + k) % nb] for k in range(K)]
+
+            graphed.load(0, group(0))
 
             def run(i):
-                graphed.load((i + 1) % graphed.n, host_batches[(i + 1) % nb])
+                graphed.load((i + 1) % graphed.n, group(i + 1))
                 return graphed.run(i % graphed.n)
         else:
+            K = 1
+
             def fetch(i):
                 with torch.cuda.stream(copy_stream):
                     b = host_batches[i % nb].to(device, non_blocking=True)
@@ -373,7 +400,7 @@ def main():
                     t.record_stream(torch.cuda.current_stream())
                 return train_step(b)
 
-        if primary and args.trace_steps and graphed is not None:
+        if primary and args.trace_steps and graphed is not None and K == 1:
             # diagnostics: per-step host time of the H2D load and the replay
             tl, tr = [], []
             for i in range(args.trace_steps):
@@ -386,7 +413,9 @@ def main():
             torch.cuda.synchronize()
             log(rank, "[bench] trace load us: " + " ".join(f"{x * 1e6:.0f}" for x in tl))
             log(rank, "[bench] trace run  us: " + " ".join(f"{x * 1e6:.0f}" for x in tr))
-        for i in range(args.warmup):
+        # K divides both counts (graph_steps_for): exactly W warmup and K timed steps
+        wg, sg = args.warmup // K, args.steps // K
+        for i in range(wg):
             run(i)
         torch.cuda.synchronize()
         if multi:
@@ -394,8 +423,8 @@ def main():
         torch.cuda.synchronize()
         t_start = time.perf_counter()
         loss = None
-        for i in range(args.steps):
-            loss = run(args.warmup + i)
+        for i in range(sg):
+            loss = run(wg + i)
         t_enq = time.perf_counter() - t_start
         torch.cuda.synchronize()
         if multi:
@@ -411,11 +440,11 @@ def main():
         for w in range(args.diag_windows if primary else 0):
             torch.cuda.synchronize()
             t0w = time.perf_counter()
-            for i in range(args.steps):
-                run(args.warmup + args.steps * (w + 1) + i)
+            for i in range(sg):
+                run(wg + sg * (w + 1) + i)
             torch.cuda.synchronize()
             log(rank, f"[bench] diag window {w}: {(time.perf_counter() - t0w) / args.steps * 1e3:.4f} ms/step")
-        if primary and args.host_diag and graphed is not None:
+        if primary and args.host_diag and graphed is not None and K == 1:
             # where the host time of a step goes: replay alone, H2D load alone, both
             for name, fn in (("replay", lambda i: graphed.graphs[i % 2][0].replay()),
                              ("load", lambda i: graphed.load(i % 2, host_batches[i % nb])),
@@ -431,7 +460,7 @@ def main():
                     log(rank, f"[bench] host-diag {name} window {w}: host {th / args.steps * 1e3:.4f} "
                               f"wall {tw / args.steps * 1e3:.4f} ms/step")
 
-        res = dict(dt=dt, t_enq=t_enq, loss=float(loss) if loss is not None else float("nan"),
+        res = dict(dt=dt, t_enq=t_enq, graph_steps=K, loss=float(loss) if loss is not None else float("nan"),
                    auc_stats=auc_stats.clone(), ipc=ipc,
                    prefetch=bool(graphed is not None and graphed.prefetch is not None), fused=fused)
         # free this precision's graphs / model before the next measurement
@@ -501,6 +530,7 @@ def main():
                 "sparse_exchange": engine.exchange_mode,
                 "same_gpu_rehearsal": bool(args.same_gpu),
                 "pipelined_pull": res["prefetch"],
+                "steps_per_graph": res.get("graph_steps", 1),
                 "key_dedup": bool(engine.dedup),
                 "mlp_dtype": args.mlp_dtype,
                 **({f"{sec_dtype}_ms_per_step": round(second["dt"] / args.steps * 1e3, 4),

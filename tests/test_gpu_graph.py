@@ -146,3 +146,29 @@ def test_prefetched_pull_graph_matches_eager(pipelined):
     torch.testing.assert_close(arena_g.flat, flat_e, rtol=1e-3, atol=1e-4)
     vg = eng_g.table.read(h)
     torch.testing.assert_close(vg[:, :13], ve[:, :13], rtol=1e-3, atol=1e-4)
+
+
+def test_multistep_graph_matches_eager():
+    """steps_per_graph = 2: each replay trains two batches (two buffer sets
+    of two), identical to eager training on the same sequence."""
+    eng_e, model_e, arena_e, opt_e, batches = _setup()
+    step_e = _step_fn(model_e, arena_e, opt_e)
+    for _ in range(3):
+        step_e(batches[0])
+    seq = [batches[i % 6] for i in range(1, 9)]
+    for b in seq:
+        step_e(b)
+    torch.cuda.synchronize()
+    flat_e = arena_e.flat.clone()
+    h, ve = eng_e.table.export(True)
+    eng_g, model_g, arena_g, opt_g, _ = _setup()
+    step_g = _step_fn(model_g, arena_g, opt_g)
+    g = GraphedTrainStep(step_g, batches[0], DEV, warmup=3, steps_per_graph=2)
+    assert g.n == 2 and len(g.bufs) == 4
+    for j in range(4):
+        g.load(j % 2, seq[2 * j:2 * j + 2])
+        g.run(j % 2)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(arena_g.flat, flat_e, rtol=1e-3, atol=1e-4)
+    vg = eng_g.table.read(h)
+    torch.testing.assert_close(vg[:, :13], ve[:, :13], rtol=1e-3, atol=1e-4)
