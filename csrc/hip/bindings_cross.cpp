@@ -1,10 +1,15 @@
-// CrossWorkspace: DCN-V2 cross network on the LDS-DMA MFMA engine (mlp.hip,
-// MLP_EPI_CROSS_* epilogues) + cross.hip.  Persistent padded buffers, all
-// shapes checked here; forward = 1 weight cast + L GEMMs + 1 dot, backward =
-// top kernel + colsum + 2 GEMMs per layer (dW with fused db, dX).
+// CrossWorkspace: DCN-V2 cross network.  Default (the 32-row tile fits in
+// LDS): forward = weight pack + ONE launch for all layers and the w_c dot
+// (tower.hip k_cross_fwd), backward = ONE launch for the top + dX chain
+// (k_cross_bwd) + one dW GEMM per layer + the w_c column sum.  Fallback
+// (PBX_CROSS_FUSED=0 or wide D): the per-layer LDS-DMA MFMA GEMMs (mlp.hip,
+// MLP_EPI_CROSS_* epilogues) + cross.hip: forward = 1 weight cast + L GEMMs +
+// 1 dot, backward = top kernel + colsum + 2 GEMMs per layer.  Persistent
+// padded buffers, all shapes checked here.
 #include <ATen/hip/HIPContext.h>
 #include <torch/extension.h>
 
+#include <cstdlib>
 #include <stdexcept>
 
 #include "kernels.h"
@@ -58,6 +63,19 @@ class CrossWorkspace {
       u_.push_back(torch::zeros({M, ld_}, ob));
       ut_.push_back(torch::zeros({ld_, ldM_}, ob));
     }
+    // fused forward (k_cross_fwd) when its 32-row tile fits in LDS
+    np_ = (D + 31) / 32 * 32;
+    kp_ = (D + 15) / 16 * 16;
+    const char* fe = getenv("PBX_CROSS_FUSED");
+    fused_ = (!fe || atoi(fe) != 0) && cross_fwd_lds_bytes((int)np_, (int)kp_) > 0;
+    if (fused_) {
+      for (int l = 0; l < L; ++l) {
+        wp_.push_back(torch::zeros({np_ * kp_}, ob));
+        wtp_.push_back(torch::zeros({np_ * np_}, ob));
+        utl_.push_back(torch::zeros({ld_, ldM_}, ob));  // u_l^T for the dW GEMMs after the chain
+      }
+      partb_ = torch::zeros({cross_bwd_blocks((int)M), D}, of);
+    }
     acc_ = torch::zeros({M, ld_}, of);
     dy_ = torch::zeros({M, ld_}, ob);
     s_ = torch::zeros({M}, of);
@@ -85,6 +103,36 @@ class CrossWorkspace {
       cb.N[l] = cb.K[l] = (int)D_;
       cb.pN[l] = cb.pK[l] = (int)ld_;
       cb.tile_off[l + 1] = cb.tile_off[l] + (int)((ld_ / 32) * (ld_ / 32));
+    }
+    if (fused_) {  // one launch for the whole stack + the w_c dot (weights packed for it and the fused backward)
+      const float* wl[kMaxMlpLayers];
+      unsigned short* wpl[kMaxMlpLayers];
+      unsigned short* wtpl[kMaxMlpLayers];
+      CrossFwdArgs a;
+      a.x0 = bp(y);
+      a.ldx0 = (int)ld_;
+      for (int l = 0; l < L_; ++l) {
+        wl[l] = fp(W[l]);
+        wpl[l] = bp(wp_[l]);
+        wtpl[l] = bp(wtp_[l]);
+        a.wp[l] = bp(wp_[l]);
+        a.bias[l] = fp(b[l]);
+        a.z[l] = fp(z_[l]);
+        a.xt[l] = l + 1 < L_ ? bp(xt_[l]) : nullptr;
+      }
+      launch_cross_pack(wl, wpl, wtpl, (int)L_, (int)D_, (int)kp_, (int)np_, s);
+      a.ldt = (int)ldM_;
+      a.xlast = fp(xf_[L_ - 1]);
+      a.ldf = (int)ld_;
+      a.wc = fp(wc);
+      a.s = fp(s_);
+      a.M = (int)M_;
+      a.D = (int)D_;
+      a.L = (int)L_;
+      a.Np = (int)np_;
+      a.Kp = (int)kp_;
+      launch_cross_fwd(a, s);
+      return s_;
     }
     launch_cast_wt(cb, s);
     for (int l = 0; l < L_; ++l) {
@@ -138,6 +186,7 @@ class CrossWorkspace {
     CR_CHECK(wc.is_cuda() && wc.numel() == D_ && wc.is_contiguous(), "w_c");
     CR_CHECK(dwc.is_cuda() && dwc.numel() == D_ && dwc.scalar_type() == torch::kFloat32 && dwc.is_contiguous(), "dwc");
     auto s = xs();
+    if (fused_) return backward_fused(y, yt, ds, dW, db, wc, dwc, dy_out, s);
     int cur = 0;  // ping-pong index holding g_{l+1}, u_l, u_l^T
     launch_cross_top_bwd(fp(xf_[L_ - 1]), bp(y), fp(z_[L_ - 1]), fp(wc), fp(ds), (int)M_, (int)D_, (int)ld_,
                          fp(g_[cur]), bp(u_[cur]), bp(ut_[cur]), (int)ldM_, fp(acc_), fp(part_), fp(dwc), s);
@@ -195,7 +244,61 @@ class CrossWorkspace {
     return dy_out.has_value() && dy_out->defined() ? *dy_out : dy_;
   }
 
+  // one launch for top + dX chain (k_cross_bwd), then the dW GEMMs of all
+  // layers from the u_l^T it wrote, then the w_c column sum
+  Tensor backward_fused(const Tensor& y, const Tensor& yt, const Tensor& ds, const std::vector<Tensor>& dW,
+                        const std::vector<Tensor>& db, const Tensor& wc, const Tensor& dwc,
+                        const c10::optional<Tensor>& dy_out, hipStream_t s) {
+    const bool add = dy_out.has_value() && dy_out->defined();
+    if (add)
+      CR_CHECK(dy_out->is_cuda() && dy_out->scalar_type() == torch::kBFloat16 && dy_out->is_contiguous() &&
+                   dy_out->dim() == 2 && dy_out->size(0) == M_ && dy_out->size(1) == ld_,
+               "dy_out must be bf16 [M, ld]");
+    CrossBwdArgs a;
+    a.x0 = bp(y);
+    a.ldx0 = (int)ld_;
+    for (int l = 0; l < L_; ++l) {
+      a.wtp[l] = bp(wtp_[l]);
+      a.z[l] = fp(z_[l]);
+      a.ut[l] = bp(utl_[l]);
+    }
+    a.xlast = fp(xf_[L_ - 1]);
+    a.ldf = (int)ld_;
+    a.ds = fp(ds);
+    a.wc = fp(wc);
+    a.ldt = (int)ldM_;
+    a.dy = add ? bp(*dy_out) : bp(dy_);
+    a.ldy = (int)ld_;
+    a.add_dy = add ? 1 : 0;
+    a.part = fp(partb_);
+    a.M = (int)M_;
+    a.D = (int)D_;
+    a.L = (int)L_;
+    a.Np = (int)np_;
+    launch_cross_bwd(a, s);
+    for (int l = (int)L_ - 1; l >= 0; --l) {
+      MlpGemmArgs w;  // dW_l += u_l^T [x_l | 1]   (split-K over the batch)
+      w.A = bp(utl_[l]);
+      w.lda = (int)ldM_;
+      w.B = l == 0 ? bp(yt) : bp(xt_[l - 1]);
+      w.ldb = (int)ldM_;
+      w.M = (int)D_;
+      w.N = (int)D_ + 1;
+      w.K = (int)ldM_;
+      w.k_per_split = (int)ks_;
+      w.dW = fp(dW[l]);
+      w.lddw = (int)D_;
+      w.db = fp(db[l]);
+      w.ncols_valid = (int)D_;
+      w.nrows_valid = (int)D_;
+      launch_mlp_gemm(w, MLP_EPI_DW, s);
+    }
+    launch_colsum_acc(fp(partb_), cross_bwd_blocks((int)M_), (int)D_, fp(dwc), -1, nullptr, s);
+    return add ? *dy_out : dy_;
+  }
+
   Tensor x_out() const { return xf_[L_ - 1].narrow(1, 0, D_); }
+  bool fused() const { return fused_; }
 
  private:
   void check_x0(const Tensor& y) const {
@@ -203,9 +306,10 @@ class CrossWorkspace {
                  y.size(0) == M_ && y.size(1) == ld_,
              "x0 must be the MLP's contiguous bf16 [M, pad64(D)] input");
   }
-  int64_t M_, D_, L_, ks_, ld_ = 0, ldM_ = 0;
-  std::vector<Tensor> wb_, wtb_, xf_, xb_, xt_, z_, g_, u_, ut_;
-  Tensor acc_, dy_, s_, part_;
+  int64_t M_, D_, L_, ks_, ld_ = 0, ldM_ = 0, np_ = 0, kp_ = 0;
+  bool fused_ = false;
+  std::vector<Tensor> wb_, wtb_, xf_, xb_, xt_, z_, g_, u_, ut_, wp_, wtp_, utl_;
+  Tensor acc_, dy_, s_, part_, partb_;
 };
 
 }  // namespace
@@ -216,7 +320,8 @@ void bind_cross(py::module& m) {
       .def("forward", &CrossWorkspace::forward)
       .def("backward", &CrossWorkspace::backward, py::arg("y"), py::arg("yt"), py::arg("ds"), py::arg("dW"),
            py::arg("db"), py::arg("wc"), py::arg("dwc"), py::arg("dy_out") = py::none())
-      .def("x_out", &CrossWorkspace::x_out);
+      .def("x_out", &CrossWorkspace::x_out)
+      .def_property_readonly("fused_forward", [](const CrossWorkspace& w) { return w.fused(); });
 }
 
 }  // namespace pbx

@@ -497,6 +497,56 @@ struct CastWtBatch {  // all layers' fp32 -> bf16 (W, W^T) casts in one launch
   int n = 0;
 };
 void launch_cast_wt(const CastWtBatch& c, hipStream_t s);
+// DCN-V2 cross stack forward fused into one launch (tower.hip k_cross_fwd):
+// per 32-row tile x_0 and x_l stay in LDS (bf16 MFMA operand + fp32
+// residual) across all L layers, the packed bf16 weights stream from L2
+// (tower wp layout, Np = pad32(D), Kp = pad16(D)), and only what the
+// backward reads goes to HBM: z_l (f32), x_{l+1}^T (bf16, l < L-1), x_L (f32)
+// and s = x_L . w_c.  Same epilogue as MLP_EPI_CROSS_FWD.
+struct CrossFwdArgs {
+  const unsigned short* x0 = nullptr;  // [M][ldx0] bf16
+  int ldx0 = 0;
+  const unsigned short* wp[kMaxMlpLayers] = {};
+  const float* bias[kMaxMlpLayers] = {};
+  float* z[kMaxMlpLayers] = {};          // [M][ldf]
+  unsigned short* xt[kMaxMlpLayers] = {};  // [>= D+1][ldt] (l < L-1) or null
+  int ldt = 0;
+  float* xlast = nullptr;  // [M][ldf]
+  int ldf = 0;
+  const float* wc = nullptr;
+  float* s = nullptr;  // [M]
+  int M = 0, D = 0, L = 0, Np = 0, Kp = 0;
+};
+size_t cross_fwd_lds_bytes(int Np, int Kp);  // 0 if the tile does not fit in LDS
+void launch_cross_fwd(const CrossFwdArgs& a, hipStream_t s);
+// fp32 W_l [D][D] -> packed bf16 W_l (tower wp layout, Kp) and, when wtp is
+// given, packed W_l^T (tower wtp layout, Np = pad32(D)); pad entries untouched
+void launch_cross_pack(const float* const* w, unsigned short* const* wp, unsigned short* const* wtp, int L, int D,
+                       int Kp, int Np, hipStream_t s);
+// DCN-V2 cross backward chain fused into one launch (tower.hip k_cross_bwd):
+// per 32-row tile g (f32), the dx_0 accumulator (f32) and u = bf16(x_0 * g)
+// stay in LDS across the layers; top (g_L = ds w_c), dX chain
+// g_l = u_l W_l + g_{l+1}, dx_0 = g_0 + sum_l z_l * g_{l+1} -> dy (bf16),
+// u_l^T (bf16) for the dW GEMMs and per-tile dw_c partials.  Same math as
+// k_cross_top_bwd + MLP_EPI_CROSS_DX.
+struct CrossBwdArgs {
+  const unsigned short* x0 = nullptr;  // [M][ldx0] bf16
+  int ldx0 = 0;
+  const unsigned short* wtp[kMaxMlpLayers] = {};
+  const float* z[kMaxMlpLayers] = {};  // [M][ldf]
+  const float* xlast = nullptr;        // x_L [M][ldf]
+  int ldf = 0;
+  const float* ds = nullptr;  // [M]
+  const float* wc = nullptr;  // [D]
+  unsigned short* ut[kMaxMlpLayers] = {};  // u_l^T [>= D][ldt]
+  int ldt = 0;
+  unsigned short* dy = nullptr;  // [M][ldy]
+  int ldy = 0, add_dy = 0;
+  float* part = nullptr;  // [ceil(M/32)][D] dw_c partials
+  int M = 0, D = 0, L = 0, Np = 0;
+};
+void launch_cross_bwd(const CrossBwdArgs& a, hipStream_t s);
+int cross_bwd_blocks(int M);
 void launch_mlp_gemv_fwd(const unsigned short* h, int M, int K, int ld, const float* w, const float* b, float* out,
                          hipStream_t s);
 int mlp_gemv_bwd_blocks(int M);

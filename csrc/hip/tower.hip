@@ -514,16 +514,19 @@ __global__ void k_tower_pack(TowerArgs a, PackJob j) {
 }
 
 // ---------------------------------------------------------------- Adam (+ extras)
+// Grid-stride over float4 groups with a capped grid: the beta-power ticket
+// below is one same-address returning atomic per workgroup, and ~1700 of
+// them (one group per thread) serialised at the memory side for several us.
 __global__ __launch_bounds__(256) void k_adam_fused(float* __restrict__ p, float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                     float lr, float b1, float b2, float eps, float* pows, float gs,
                                                     float wd, int clear_grad, AdamExtras x) {
-  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const float b1pow = pows[0] * b1, b2pow = pows[1] * b2;  // powers of this step
   const float lr_t = lr * sqrtf(1.f - b2pow) / (1.f - b1pow);
   const float epst = eps * sqrtf(1.f - b2pow);
-  const int64_t e0 = i4 * 4;
-  if (e0 < n) {
+  const int64_t stride4 = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i4 * 4 < n; i4 += stride4) {
+    const int64_t e0 = i4 * 4;
     float pa[4], ga[4], ma[4], va[4];
     const bool full = e0 + 4 <= n;
     if (full) {
@@ -574,7 +577,7 @@ __global__ __launch_bounds__(256) void k_adam_fused(float* __restrict__ p, float
       for (int k = 0; k < 4; ++k) {
         const int64_t i = e0 + k - off;
         if (i < 0 || i >= cnt || e0 + k >= n) continue;
-        const int nn = (int)(i / K), kk = (int)(i % K);
+        const int nn = (int)((uint32_t)i / (uint32_t)K), kk = (int)((uint32_t)i - (uint32_t)nn * (uint32_t)K);
         if (x.pack_wp32[r]) {  // fp32 tower
           x.pack_wp32[r][tower_wp32_index(nn, kk, x.pack_Kp[r])] = pa[k];
           x.pack_wtp32[r][tower_wtp32_index(nn, kk, x.pack_Np[r])] = pa[k];
@@ -589,12 +592,12 @@ __global__ __launch_bounds__(256) void k_adam_fused(float* __restrict__ p, float
   // data_norm summaries: bsize = bsize*decay + stats0, ...
   for (int d = 0; d < x.n_dn; ++d) {
     const int C = x.dn_C[d];
-    if (i4 < C) {
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
       const float* st = x.dn_stats[d];
       const float dec = x.dn_decay[d];
-      x.dn_bsize[d][i4] = x.dn_bsize[d][i4] * dec + st[i4];
-      x.dn_bsum[d][i4] = x.dn_bsum[d][i4] * dec + st[C + i4];
-      x.dn_bsq[d][i4] = x.dn_bsq[d][i4] * dec + st[2 * C + i4];
+      x.dn_bsize[d][c] = x.dn_bsize[d][c] * dec + st[c];
+      x.dn_bsum[d][c] = x.dn_bsum[d][c] * dec + st[C + c];
+      x.dn_bsq[d][c] = x.dn_bsq[d][c] * dec + st[2 * C + c];
     }
   }
   // the last workgroup to finish publishes the new beta powers
@@ -608,6 +611,252 @@ __global__ __launch_bounds__(256) void k_adam_fused(float* __restrict__ p, float
   }
 }
 
+
+// ---------------------------------------------------------------- DCN-V2 cross forward
+// x_{l+1} = x_0 * (x_l W_l^T + b_l) + x_l for l < L, then s = x_L . w_c,
+// one 512-thread workgroup per 32-row tile (kernels.h CrossFwdArgs).
+__device__ __forceinline__ int cross_ldl(int P) { return P + 8; }
+__device__ __forceinline__ int cross_ldf(int P) { return P + 4; }
+
+__global__ __launch_bounds__(TNT) void k_cross_fwd(CrossFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) u16 lds[];
+  const int P = a.Np > a.Kp ? a.Np : a.Kp;
+  const int ldl = cross_ldl(P), ldf = cross_ldf(P);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int m0 = blockIdx.x * TBM;
+  u16* x0b = lds;
+  u16* src = x0b + TBM * ldl;
+  u16* dst = src + TBM * ldl;
+  float* fsrc = reinterpret_cast<float*>(dst + TBM * ldl);
+  float* fdst = fsrc + TBM * ldf;
+  constexpr int WO = 8;
+  float wo[WO];
+#pragma unroll
+  for (int j = 0; j < WO; ++j) wo[j] = lane + 64 * j < a.D ? a.wc[lane + 64 * j] : 0.f;
+  {  // stage x_0: bf16 (epilogue operand + first A operand) and its fp32 residual
+    const int c8n = a.Kp / 8;
+    for (int i = tid; i < TBM * c8n; i += TNT) {
+      const int r = i / c8n, c = i - r * c8n;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (m0 + r < a.M) v = *reinterpret_cast<const uint4*>(a.x0 + (int64_t)(m0 + r) * a.ldx0 + c * 8);
+      *reinterpret_cast<uint4*>(x0b + r * ldl + c * 8) = v;
+      *reinterpret_cast<uint4*>(src + r * ldl + c * 8) = v;
+      const unsigned int vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) fsrc[r * ldf + c * 8 + e] = bf2f((u16)((vw[e >> 1] >> (16 * (e & 1))) & 0xffff));
+    }
+  }
+  __syncthreads();
+  const int NB = a.Np / 32, KS = a.Kp / 16;
+  for (int l = 0; l < a.L; ++l) {
+    const bf16x8* wp = reinterpret_cast<const bf16x8*>(a.wp[l]);
+    const bool last = l + 1 == a.L;
+    auto epi = [&](const f32x16& acc, int nb) {
+      const int c = lane & 31, h = lane >> 5;
+      const int n = nb * 32 + c;
+      const bool nv = n < a.D;
+      const float bn = nv ? a.bias[l][n] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        u16 o[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int r = 8 * q + 4 * h + t;
+          const int m = m0 + r;
+          const float z = acc[q * 4 + t] + bn;
+          const float xn = nv ? bf2f(x0b[r * ldl + n]) * z + fsrc[r * ldf + n] : 0.f;
+          fdst[r * ldf + n] = xn;
+          o[t] = f2bf(xn);
+          dst[r * ldl + n] = o[t];
+          if (nv && m < a.M) {
+            a.z[l][(int64_t)m * a.ldf + n] = z;
+            if (last) a.xlast[(int64_t)m * a.ldf + n] = xn;
+          }
+          if (m >= a.M) o[t] = 0;
+        }
+        if (!last && nv && a.xt[l]) {  // x_{l+1}^T: 4 consecutive rows of column n, one 8-B store
+          uint2 pk;
+          pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
+          pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
+          *reinterpret_cast<uint2*>(a.xt[l] + (int64_t)n * a.ldt + m0 + 8 * q + 4 * h) = pk;
+        }
+      }
+    };
+    for (int nb0 = w; nb0 < NB; nb0 += 2 * TNW) {
+      const int nb1 = nb0 + TNW;
+      const bool two = nb1 < NB;
+      f32x16 acc0 = (f32x16){0}, acc1 = (f32x16){0};
+      const bf16x8* w0p = wp + (int64_t)nb0 * KS * 64 + lane;
+      if (two) mma_pair<true>(src, ldl, w0p, wp + (int64_t)nb1 * KS * 64 + lane, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      else mma_pair<false>(src, ldl, w0p, w0p, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      epi(acc0, nb0);
+      if (two) epi(acc1, nb1);
+    }
+    __syncthreads();
+    u16* t = src;
+    src = dst;
+    dst = t;
+    float* tf = fsrc;
+    fsrc = fdst;
+    fdst = tf;
+  }
+  // s = x_L . w_c from the fp32 tile, 4 rows per wave
+  constexpr int RPW = TBM / TNW;
+  float sv[RPW];
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) sv[rr] = 0.f;
+#pragma unroll
+  for (int j = 0; j < WO; ++j) {
+    const int k = lane + 64 * j;
+    if (k < a.D) {
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) sv[rr] += fsrc[(w * RPW + rr) * ldf + k] * wo[j];
+    }
+  }
+  for (int k = lane + 64 * WO; k < a.D; k += 64) {
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) sv[rr] += fsrc[(w * RPW + rr) * ldf + k] * a.wc[k];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) sv[rr] += __shfl_xor(sv[rr], off);
+  if (lane < RPW) {
+    float mine = sv[0];
+#pragma unroll
+    for (int rr = 1; rr < RPW; ++rr) mine = lane == rr ? sv[rr] : mine;
+    const int m = m0 + w * RPW + lane;
+    if (m < a.M) a.s[m] = mine;
+  }
+}
+
+struct CrossPackJob {
+  const float* w[kMaxMlpLayers];
+  u16* wp[kMaxMlpLayers];
+  u16* wtp[kMaxMlpLayers];
+};
+
+__global__ void k_cross_pack(CrossPackJob j, int L, int D, int Kp, int Np) {
+  const int64_t per = (int64_t)D * D;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= per * L) return;
+  const int l = (int)(e / per);
+  const int64_t i = e - (int64_t)l * per;
+  const int n = (int)(i / D), k = (int)(i - (int64_t)n * D);
+  const u16 v = f2bf(j.w[l][i]);
+  j.wp[l][wp_index(n, k, Kp)] = v;
+  if (j.wtp[l]) j.wtp[l][wtp_index(n, k, Np)] = v;
+}
+
+// ---------------------------------------------------------------- DCN-V2 cross backward chain
+__global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) u16 lds[];
+  const int P = a.Np;
+  const int ldl = cross_ldl(P), ldf = cross_ldf(P);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int m0 = blockIdx.x * TBM;
+  u16* x0b = lds;
+  u16* src = x0b + TBM * ldl;
+  u16* dst = src + TBM * ldl;
+  float* gs = reinterpret_cast<float*>(dst + TBM * ldl);  // g_{l+1}, updated in place
+  float* as = gs + TBM * ldf;                             // sum_l z_l * g_{l+1}
+  __shared__ float dss[TBM];
+  if (tid < TBM) dss[tid] = m0 + tid < a.M ? a.ds[m0 + tid] : 0.f;
+  {
+    const int c8n = P / 8;
+    for (int i = tid; i < TBM * c8n; i += TNT) {
+      const int r = i / c8n, c = i - r * c8n;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (m0 + r < a.M) v = *reinterpret_cast<const uint4*>(a.x0 + (int64_t)(m0 + r) * a.ldx0 + c * 8);
+      *reinterpret_cast<uint4*>(x0b + r * ldl + c * 8) = v;
+    }
+  }
+  __syncthreads();
+  const int L = a.L;
+  // top: g_L = ds w_c, u_{L-1} = bf16(x_0 g_L), acc = z_{L-1} g_L; dw_c partial = sum_m ds x_L
+  for (int i = tid; i < TBM * P; i += TNT) {
+    const int r = i / P, n = i - r * P;
+    const int m = m0 + r;
+    const bool ok = n < a.D && m < a.M;
+    const float g = ok ? dss[r] * a.wc[n] : 0.f;
+    gs[r * ldf + n] = g;
+    src[r * ldl + n] = ok ? f2bf(bf2f(x0b[r * ldl + n]) * g) : (u16)0;
+    as[r * ldf + n] = ok ? a.z[L - 1][(int64_t)m * a.ldf + n] * g : 0.f;
+  }
+  for (int n = tid; n < a.D; n += TNT) {
+    float p = 0.f;
+    for (int r = 0; r < TBM && m0 + r < a.M; ++r) p += dss[r] * a.xlast[(int64_t)(m0 + r) * a.ldf + n];
+    a.part[(int64_t)blockIdx.x * a.D + n] = p;
+  }
+  __syncthreads();
+  // u_{L-1}^T: four rows of one column per 8-B store
+  auto store_ut = [&](const u16* u, u16* ut) {
+    for (int i = tid; i < a.D * (TBM / 4); i += TNT) {
+      const int n = i / (TBM / 4), j = i - n * (TBM / 4);
+      u16 o[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] = m0 + 4 * j + t < a.M ? u[(4 * j + t) * ldl + n] : (u16)0;
+      uint2 pk;
+      pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
+      pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
+      *reinterpret_cast<uint2*>(ut + (int64_t)n * a.ldt + m0 + 4 * j) = pk;
+    }
+  };
+  store_ut(src, a.ut[L - 1]);
+  const int NB = P / 32, NS = P / 16;
+  for (int l = L - 1; l >= 0; --l) {
+    const bf16x8* wtp = reinterpret_cast<const bf16x8*>(a.wtp[l]);
+    auto epi = [&](const f32x16& acc, int kb, const float* zp) {
+      const int c = lane & 31, h = lane >> 5;
+      const int k = kb * 32 + c;
+      const bool kv = k < a.D;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int r = 8 * q + 4 * h + t;
+          const int m = m0 + r;
+          const float gl = acc[q * 4 + t] + gs[r * ldf + k];
+          if (l > 0) {
+            gs[r * ldf + k] = kv ? gl : 0.f;
+            as[r * ldf + k] += kv ? zp[q * 4 + t] * gl : 0.f;
+            dst[r * ldl + k] = kv ? f2bf(bf2f(x0b[r * ldl + k]) * gl) : (u16)0;
+          } else if (kv && m < a.M) {
+            float v0 = gl + as[r * ldf + k];
+            u16* d = a.dy + (int64_t)m * a.ldy + k;
+            if (a.add_dy) v0 += bf2f(*d);
+            *d = f2bf(v0);
+          }
+        }
+      }
+    };
+    for (int kb0 = w; kb0 < NB; kb0 += 2 * TNW) {
+      const int kb1 = kb0 + TNW;
+      const bool two = kb1 < NB;
+      // z_{l-1} at the accumulator positions, loaded ahead of the MMA loop
+      float z0[16], z1[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int r = 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
+        const int m = m0 + r;
+        const int k0 = kb0 * 32 + (lane & 31), k1 = kb1 * 32 + (lane & 31);
+        z0[e] = (l > 0 && m < a.M && k0 < a.D) ? a.z[l - 1][(int64_t)m * a.ldf + k0] : 0.f;
+        z1[e] = (l > 0 && two && m < a.M && k1 < a.D) ? a.z[l - 1][(int64_t)m * a.ldf + k1] : 0.f;
+      }
+      f32x16 acc0 = (f32x16){0}, acc1 = (f32x16){0};
+      const bf16x8* w0p = wtp + (int64_t)kb0 * NS * 64 + lane;
+      if (two) mma_pair<true>(src, ldl, w0p, wtp + (int64_t)kb1 * NS * 64 + lane, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      else mma_pair<false>(src, ldl, w0p, w0p, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      epi(acc0, kb0, z0);
+      if (two) epi(acc1, kb1, z1);
+    }
+    __syncthreads();
+    if (l > 0) store_ut(dst, a.ut[l - 1]);
+    u16* t = src;
+    src = dst;
+    dst = t;
+  }
+}
 }  // namespace
 
 int tower_nwg(int M) { return ((M + kMpAlign - 1) / kMpAlign * kMpAlign) / TBM; }
@@ -627,6 +876,54 @@ static void allow_big_lds() {
     return true;
   }();
   (void)once;
+}
+
+
+size_t cross_fwd_lds_bytes(int Np, int Kp) {
+  const int P = Np > Kp ? Np : Kp;
+  const size_t b = (size_t)3 * TBM * (P + 8) * sizeof(u16) + (size_t)2 * TBM * (P + 4) * sizeof(float);
+  return b <= (size_t)150 * 1024 ? b : 0;
+}
+
+void launch_cross_fwd(const CrossFwdArgs& a, hipStream_t s) {
+  if (a.M == 0) return;
+  static const bool once = [] {
+    if (hipFuncSetAttribute((const void*)k_cross_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) !=
+        hipSuccess)
+      (void)hipGetLastError();
+    return true;
+  }();
+  (void)once;
+  hipLaunchKernelGGL(k_cross_fwd, dim3((unsigned)((a.M + TBM - 1) / TBM)), dim3(TNT), cross_fwd_lds_bytes(a.Np, a.Kp),
+                     s, a);
+}
+
+void launch_cross_pack(const float* const* w, unsigned short* const* wp, unsigned short* const* wtp, int L, int D,
+                       int Kp, int Np, hipStream_t s) {
+  CrossPackJob j;
+  for (int l = 0; l < L; ++l) {
+    j.w[l] = w[l];
+    j.wp[l] = wp[l];
+    j.wtp[l] = wtp ? wtp[l] : nullptr;
+  }
+  const int64_t n = (int64_t)D * D * L;
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_cross_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, j, L, D, Kp, Np);
+}
+
+int cross_bwd_blocks(int M) { return (M + TBM - 1) / TBM; }
+
+void launch_cross_bwd(const CrossBwdArgs& a, hipStream_t s) {
+  if (a.M == 0) return;
+  static const bool once = [] {
+    if (hipFuncSetAttribute((const void*)k_cross_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) !=
+        hipSuccess)
+      (void)hipGetLastError();
+    return true;
+  }();
+  (void)once;
+  hipLaunchKernelGGL(k_cross_bwd, dim3((unsigned)cross_bwd_blocks(a.M)), dim3(TNT), cross_fwd_lds_bytes(a.Np, a.Np),
+                     s, a);
 }
 
 void launch_tower_fwd(const TowerArgs& a, hipStream_t s) {
@@ -663,13 +960,25 @@ void launch_tower_pack(const TowerArgs& a, const float* const* w, hipStream_t s)
   hipLaunchKernelGGL(k_tower_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, j);
 }
 
+static int adam_max_blocks() {
+  static const int v = [] {
+    const char* e = getenv("PBX_ADAM_MAX_BLOCKS");
+    return e ? atoi(e) : 512;
+  }();
+  return v > 0 ? v : 512;
+}
+
 void launch_adam_fused(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
                        float* pows, float grad_scale, float weight_decay, bool clear_grad, const AdamExtras& x,
                        hipStream_t s) {
   int64_t n4 = (n + 3) / 4;
   for (int d = 0; d < x.n_dn; ++d) n4 = n4 > x.dn_C[d] ? n4 : x.dn_C[d];
   if (n4 == 0) return;
-  hipLaunchKernelGGL(k_adam_fused, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2,
+  // <= 2 workgroups per CU (grid-stride loop inside): few ticket atomics
+  int64_t blocks = (n4 + 255) / 256;
+  const int64_t cap = (int64_t)adam_max_blocks();
+  blocks = blocks < cap ? blocks : cap;
+  hipLaunchKernelGGL(k_adam_fused, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2,
                      eps, pows, grad_scale, weight_decay, clear_grad ? 1 : 0, x);
 }
 

@@ -17,10 +17,14 @@ def _p64(n):
     return (n + 63) // 64 * 64
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("M,C,L", [(1000, 304, 3), (4096, 64, 1), (333, 136, 2)])
-def test_cross_stack_matches_fp64(M, C, L):
+def test_cross_stack_matches_fp64(M, C, L, fused, monkeypatch):
     """C = the padded MLP input width D; x0 / x0^T laid out as the MLP
-    workspace's X_0 [M, pad64(D)] / X_0^T [pad64(D+1), pad64(M)] (ones row)."""
+    workspace's X_0 [M, pad64(D)] / X_0^T [pad64(D+1), pad64(M)] (ones row).
+    fused: the one-launch forward (tower.hip k_cross_fwd) vs the per-layer
+    GEMMs (PBX_CROSS_FUSED=0)."""
+    monkeypatch.setenv("PBX_CROSS_FUSED", "1" if fused else "0")
     ld = _p64(C)
     torch.manual_seed(M + C)
     dev = torch.device("cuda:0")
@@ -41,6 +45,7 @@ def test_cross_stack_matches_fp64(M, C, L):
         p.grad = torch.zeros_like(p)
     yh = y.clone().requires_grad_(True)
     s = cross_logit(yh, net, w_c, yt)
+    assert net._xw.fused_forward == fused
     (s * r).sum().backward()
     # fp64 oracle
     x0 = y[:, :C].double().requires_grad_(True)
