@@ -773,20 +773,33 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
   }
   __syncthreads();
   const int L = a.L;
-  // top: g_L = ds w_c, u_{L-1} = bf16(x_0 g_L), acc = z_{L-1} g_L; dw_c partial = sum_m ds x_L
-  for (int i = tid; i < TBM * P; i += TNT) {
-    const int r = i / P, n = i - r * P;
-    const int m = m0 + r;
-    const bool ok = n < a.D && m < a.M;
-    const float g = ok ? dss[r] * a.wc[n] : 0.f;
-    gs[r * ldf + n] = g;
-    src[r * ldl + n] = ok ? f2bf(bf2f(x0b[r * ldl + n]) * g) : (u16)0;
-    as[r * ldf + n] = ok ? a.z[L - 1][(int64_t)m * a.ldf + n] * g : 0.f;
-  }
-  for (int n = tid; n < a.D; n += TNT) {
+  // top, one column per thread (z_{L-1} and x_L rows read coalesced, 8 rows
+  // of loads in flight): g_L = ds w_c, u_{L-1} = bf16(x_0 g_L),
+  // acc = z_{L-1} g_L, and the tile's dw_c partial sum_m ds x_L
+  for (int n = tid; n < P; n += TNT) {
+    const bool nv = n < a.D;
+    const float wcn = nv ? a.wc[n] : 0.f;
     float p = 0.f;
-    for (int r = 0; r < TBM && m0 + r < a.M; ++r) p += dss[r] * a.xlast[(int64_t)(m0 + r) * a.ldf + n];
-    a.part[(int64_t)blockIdx.x * a.D + n] = p;
+    for (int r0 = 0; r0 < TBM; r0 += 8) {
+      float zv[8], xv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int m = m0 + r0 + e;
+        const bool ok = nv && m < a.M;
+        zv[e] = ok ? a.z[L - 1][(int64_t)m * a.ldf + n] : 0.f;
+        xv[e] = ok ? a.xlast[(int64_t)m * a.ldf + n] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int r = r0 + e;
+        const float g = dss[r] * wcn;
+        gs[r * ldf + n] = g;
+        src[r * ldl + n] = nv ? f2bf(bf2f(x0b[r * ldl + n]) * g) : (u16)0;
+        as[r * ldf + n] = zv[e] * g;
+        p += dss[r] * xv[e];
+      }
+    }
+    if (nv) a.part[(int64_t)blockIdx.x * a.D + n] = p;
   }
   __syncthreads();
   // u_{L-1}^T: four rows of one column per 8-B store

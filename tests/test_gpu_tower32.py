@@ -157,7 +157,11 @@ def test_tower32_fused_adam_repack():
         runs.append((arena.flat.clone(), [m._tw.wp(i).clone() for i in range(len(m.w))],
                      [m._tw.wtp(i).clone() for i in range(len(m.w))], m))
     a, b = runs
-    assert torch.allclose(a[0], b[0], rtol=1e-5, atol=1e-6)
+    # two unfused runs already differ by up to ~2e-6 here (the dW split sums
+    # in nondeterministic order and Adam's m / sqrt(v) amplifies it for
+    # near-zero grads, scripts/diag_t32_adam.py): the update is compared at
+    # that tolerance, the re-pack exactly below
+    assert torch.allclose(a[0], b[0], rtol=1e-5, atol=1e-5)
     m = b[3]
     m._tw.pack([w.detach() for w in m.w])
     torch.cuda.synchronize()
