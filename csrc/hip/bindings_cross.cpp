@@ -1,7 +1,8 @@
 // CrossWorkspace: DCN-V2 cross network.  Default (the 32-row tile fits in
 // LDS): forward = weight pack + ONE launch for all layers and the w_c dot
 // (tower.hip k_cross_fwd), backward = ONE launch for the top + dX chain
-// (k_cross_bwd) + one dW GEMM per layer + the w_c column sum.  Fallback
+// (k_cross_bwd) + ONE grouped dW launch for all layers, db and dw_c
+// (tower.hip k_tower_dw on m-packed operands).  Fallback
 // (PBX_CROSS_FUSED=0 or wide D): the per-layer LDS-DMA MFMA GEMMs (mlp.hip,
 // MLP_EPI_CROSS_* epilogues) + cross.hip: forward = 1 weight cast + L GEMMs +
 // 1 dot, backward = top kernel + colsum + 2 GEMMs per layer.  Persistent
@@ -69,12 +70,15 @@ class CrossWorkspace {
     const char* fe = getenv("PBX_CROSS_FUSED");
     fused_ = (!fe || atoi(fe) != 0) && cross_fwd_lds_bytes((int)np_, (int)kp_) > 0;
     if (fused_) {
+      mp_ = (M + 127) / 128 * 128;  // the grouped dW launch walks M in 128-row stages
       for (int l = 0; l < L; ++l) {
         wp_.push_back(torch::zeros({np_ * kp_}, ob));
         wtp_.push_back(torch::zeros({np_ * np_}, ob));
-        utl_.push_back(torch::zeros({ld_, ldM_}, ob));  // u_l^T for the dW GEMMs after the chain
+        xmp_.push_back(torch::zeros({mp_ * np_}, ob));  // m-packed x_l (dW B operand)
+        ump_.push_back(torch::zeros({mp_ * np_}, ob));  // m-packed u_l (dW A operand)
       }
-      partb_ = torch::zeros({cross_bwd_blocks((int)M), D}, of);
+      bias_ld_ = L * np_ + (D + 31) / 32 * 32;
+      biasp_ = torch::zeros({mp_ / 32, bias_ld_}, of);
     }
     acc_ = torch::zeros({M, ld_}, of);
     dy_ = torch::zeros({M, ld_}, ob);
@@ -118,10 +122,9 @@ class CrossWorkspace {
         a.wp[l] = bp(wp_[l]);
         a.bias[l] = fp(b[l]);
         a.z[l] = fp(z_[l]);
-        a.xt[l] = l + 1 < L_ ? bp(xt_[l]) : nullptr;
+        a.xmp[l] = bp(xmp_[l]);
       }
       launch_cross_pack(wl, wpl, wtpl, (int)L_, (int)D_, (int)kp_, (int)np_, s);
-      a.ldt = (int)ldM_;
       a.xlast = fp(xf_[L_ - 1]);
       a.ldf = (int)ld_;
       a.wc = fp(wc);
@@ -244,11 +247,13 @@ class CrossWorkspace {
     return dy_out.has_value() && dy_out->defined() ? *dy_out : dy_;
   }
 
-  // one launch for top + dX chain (k_cross_bwd), then the dW GEMMs of all
-  // layers from the u_l^T it wrote, then the w_c column sum
+  // one launch for the top + dX chain (k_cross_bwd), then ONE grouped dW
+  // launch over all layers (k_tower_dw on the m-packed u_l / x_l) whose extra
+  // workgroups reduce the db and dw_c column partials
   Tensor backward_fused(const Tensor& y, const Tensor& yt, const Tensor& ds, const std::vector<Tensor>& dW,
                         const std::vector<Tensor>& db, const Tensor& wc, const Tensor& dwc,
                         const c10::optional<Tensor>& dy_out, hipStream_t s) {
+    (void)yt;
     const bool add = dy_out.has_value() && dy_out->defined();
     if (add)
       CR_CHECK(dy_out->is_cuda() && dy_out->scalar_type() == torch::kBFloat16 && dy_out->is_contiguous() &&
@@ -260,40 +265,44 @@ class CrossWorkspace {
     for (int l = 0; l < L_; ++l) {
       a.wtp[l] = bp(wtp_[l]);
       a.z[l] = fp(z_[l]);
-      a.ut[l] = bp(utl_[l]);
+      a.ump[l] = bp(ump_[l]);
     }
     a.xlast = fp(xf_[L_ - 1]);
     a.ldf = (int)ld_;
     a.ds = fp(ds);
     a.wc = fp(wc);
-    a.ldt = (int)ldM_;
     a.dy = add ? bp(*dy_out) : bp(dy_);
     a.ldy = (int)ld_;
     a.add_dy = add ? 1 : 0;
-    a.part = fp(partb_);
+    a.bias_part = fp(biasp_);
+    a.bias_ld = (int)bias_ld_;
     a.M = (int)M_;
     a.D = (int)D_;
     a.L = (int)L_;
     a.Np = (int)np_;
     launch_cross_bwd(a, s);
-    for (int l = (int)L_ - 1; l >= 0; --l) {
-      MlpGemmArgs w;  // dW_l += u_l^T [x_l | 1]   (split-K over the batch)
-      w.A = bp(utl_[l]);
-      w.lda = (int)ldM_;
-      w.B = l == 0 ? bp(yt) : bp(xt_[l - 1]);
-      w.ldb = (int)ldM_;
-      w.M = (int)D_;
-      w.N = (int)D_ + 1;
-      w.K = (int)ldM_;
-      w.k_per_split = (int)ks_;
-      w.dW = fp(dW[l]);
-      w.lddw = (int)D_;
-      w.db = fp(db[l]);
-      w.ncols_valid = (int)D_;
-      w.nrows_valid = (int)D_;
-      launch_mlp_gemm(w, MLP_EPI_DW, s);
+    TowerArgs t;
+    t.M = (int)M_;
+    t.Mp = (int)mp_;
+    t.L = (int)L_;
+    t.x0mp = bp(xmp_[0]);
+    for (int l = 0; l < L_; ++l) {
+      TowerLayerDev& d = t.ly[l];
+      d.N = d.K = (int)D_;
+      d.Np = d.Kp = (int)np_;
+      d.dzmp = bp(ump_[l]);
+      d.xmp = l + 1 < L_ ? bp(xmp_[l + 1]) : nullptr;  // X_{l+1}: the B operand of layer l+1
+      d.dw = fp(dW[l]);
+      d.db = fp(db[l]);
+      d.bias_off = (int)(l * np_);
     }
-    launch_colsum_acc(fp(partb_), cross_bwd_blocks((int)M_), (int)D_, fp(dwc), -1, nullptr, s);
+    t.bias_part = fp(biasp_);
+    t.bias_ld = (int)bias_ld_;
+    t.dwout_off = (int)(L_ * np_);
+    t.dbout_off = (int)bias_ld_;  // no output-layer bias here
+    t.dw_out = fp(dwc);
+    t.dw_splits = 2;
+    launch_tower_dw(t, s);
     return add ? *dy_out : dy_;
   }
 
@@ -306,10 +315,10 @@ class CrossWorkspace {
                  y.size(0) == M_ && y.size(1) == ld_,
              "x0 must be the MLP's contiguous bf16 [M, pad64(D)] input");
   }
-  int64_t M_, D_, L_, ks_, ld_ = 0, ldM_ = 0, np_ = 0, kp_ = 0;
+  int64_t M_, D_, L_, ks_, ld_ = 0, ldM_ = 0, np_ = 0, kp_ = 0, mp_ = 0, bias_ld_ = 0;
   bool fused_ = false;
-  std::vector<Tensor> wb_, wtb_, xf_, xb_, xt_, z_, g_, u_, ut_, wp_, wtp_, utl_;
-  Tensor acc_, dy_, s_, part_, partb_;
+  std::vector<Tensor> wb_, wtb_, xf_, xb_, xt_, z_, g_, u_, ut_, wp_, wtp_, xmp_, ump_;
+  Tensor acc_, dy_, s_, part_, biasp_;
 };
 
 }  // namespace

@@ -501,16 +501,15 @@ void launch_cast_wt(const CastWtBatch& c, hipStream_t s);
 // per 32-row tile x_0 and x_l stay in LDS (bf16 MFMA operand + fp32
 // residual) across all L layers, the packed bf16 weights stream from L2
 // (tower wp layout, Np = pad32(D), Kp = pad16(D)), and only what the
-// backward reads goes to HBM: z_l (f32), x_{l+1}^T (bf16, l < L-1), x_L (f32)
-// and s = x_L . w_c.  Same epilogue as MLP_EPI_CROSS_FWD.
+// backward reads goes to HBM: z_l (f32), m-packed x_l (bf16, the dW GEMM
+// operand), x_L (f32) and s = x_L . w_c.  Same epilogue as MLP_EPI_CROSS_FWD.
 struct CrossFwdArgs {
   const unsigned short* x0 = nullptr;  // [M][ldx0] bf16
   int ldx0 = 0;
   const unsigned short* wp[kMaxMlpLayers] = {};
   const float* bias[kMaxMlpLayers] = {};
-  float* z[kMaxMlpLayers] = {};          // [M][ldf]
-  unsigned short* xt[kMaxMlpLayers] = {};  // [>= D+1][ldt] (l < L-1) or null
-  int ldt = 0;
+  float* z[kMaxMlpLayers] = {};            // [M][ldf]
+  unsigned short* xmp[kMaxMlpLayers] = {};  // m-packed x_l, l < L (tower MP layout, NB = Np/32): dW B operand
   float* xlast = nullptr;  // [M][ldf]
   int ldf = 0;
   const float* wc = nullptr;
@@ -527,8 +526,9 @@ void launch_cross_pack(const float* const* w, unsigned short* const* wp, unsigne
 // per 32-row tile g (f32), the dx_0 accumulator (f32) and u = bf16(x_0 * g)
 // stay in LDS across the layers; top (g_L = ds w_c), dX chain
 // g_l = u_l W_l + g_{l+1}, dx_0 = g_0 + sum_l z_l * g_{l+1} -> dy (bf16),
-// u_l^T (bf16) for the dW GEMMs and per-tile dw_c partials.  Same math as
-// k_cross_top_bwd + MLP_EPI_CROSS_DX.
+// m-packed u_l for the grouped dW launch (k_tower_dw over the cross layers)
+// and per-tile db / dw_c partials.  Same math as k_cross_top_bwd +
+// MLP_EPI_CROSS_DX.
 struct CrossBwdArgs {
   const unsigned short* x0 = nullptr;  // [M][ldx0] bf16
   int ldx0 = 0;
@@ -538,11 +538,13 @@ struct CrossBwdArgs {
   int ldf = 0;
   const float* ds = nullptr;  // [M]
   const float* wc = nullptr;  // [D]
-  unsigned short* ut[kMaxMlpLayers] = {};  // u_l^T [>= D][ldt]
-  int ldt = 0;
+  unsigned short* ump[kMaxMlpLayers] = {};  // m-packed u_l (dW GEMM A operand)
   unsigned short* dy = nullptr;  // [M][ldy]
   int ldy = 0, add_dy = 0;
-  float* part = nullptr;  // [ceil(M/32)][D] dw_c partials
+  // per-tile column partials [Mp/32][bias_ld]: db_l at l*Np (sum of u_l),
+  // dw_c at L*Np (sum of ds x_L) -- reduced by the grouped dW launch
+  float* bias_part = nullptr;
+  int bias_ld = 0;
   int M = 0, D = 0, L = 0, Np = 0;
 };
 void launch_cross_bwd(const CrossBwdArgs& a, hipStream_t s);

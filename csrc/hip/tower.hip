@@ -648,6 +648,17 @@ __global__ __launch_bounds__(TNT) void k_cross_fwd(CrossFwdArgs a) {
   }
   __syncthreads();
   const int NB = a.Np / 32, KS = a.Kp / 16;
+  // m-packed x_0 (the layer-0 dW operand): 8 rows of one column = 16 B
+  for (int i = tid; i < a.Np * (TBM / 8); i += TNT) {
+    const int n = i / (TBM / 8), g8 = i - n * (TBM / 8);
+    unsigned int pk[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      pk[e] = (unsigned)x0b[(8 * g8 + 2 * e) * ldl + n] | ((unsigned)x0b[(8 * g8 + 2 * e + 1) * ldl + n] << 16);
+    const int r0 = 8 * g8;
+    *reinterpret_cast<uint4*>(a.xmp[0] + mp_off(m0 / 16 + r0 / 16, NB, n >> 5, (n & 31) + 32 * ((r0 & 15) >> 3))) =
+        make_uint4(pk[0], pk[1], pk[2], pk[3]);
+  }
   for (int l = 0; l < a.L; ++l) {
     const bf16x8* wp = reinterpret_cast<const bf16x8*>(a.wp[l]);
     const bool last = l + 1 == a.L;
@@ -674,11 +685,11 @@ __global__ __launch_bounds__(TNT) void k_cross_fwd(CrossFwdArgs a) {
           }
           if (m >= a.M) o[t] = 0;
         }
-        if (!last && nv && a.xt[l]) {  // x_{l+1}^T: 4 consecutive rows of column n, one 8-B store
+        if (!last) {  // m-packed x_{l+1} (tower fwd_epilogue layout)
           uint2 pk;
           pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
           pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
-          *reinterpret_cast<uint2*>(a.xt[l] + (int64_t)n * a.ldt + m0 + 8 * q + 4 * h) = pk;
+          *reinterpret_cast<uint2*>(a.xmp[l + 1] + mp_off(m0 / 16 + (q >> 1), NB, nb, c + 32 * (q & 1)) + 4 * h) = pk;
         }
       }
     };
@@ -776,10 +787,12 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
   // top, one column per thread (z_{L-1} and x_L rows read coalesced, 8 rows
   // of loads in flight): g_L = ds w_c, u_{L-1} = bf16(x_0 g_L),
   // acc = z_{L-1} g_L, and the tile's dw_c partial sum_m ds x_L
+  const int NB = P / 32, NS = P / 16;
+  float* bpart = a.bias_part + (int64_t)blockIdx.x * a.bias_ld;
   for (int n = tid; n < P; n += TNT) {
     const bool nv = n < a.D;
     const float wcn = nv ? a.wc[n] : 0.f;
-    float p = 0.f;
+    float p = 0.f, du = 0.f;
     for (int r0 = 0; r0 < TBM; r0 += 8) {
       float zv[8], xv[8];
 #pragma unroll
@@ -789,51 +802,49 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
         zv[e] = ok ? a.z[L - 1][(int64_t)m * a.ldf + n] : 0.f;
         xv[e] = ok ? a.xlast[(int64_t)m * a.ldf + n] : 0.f;
       }
+      u16 uo[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int r = r0 + e;
         const float g = dss[r] * wcn;
         gs[r * ldf + n] = g;
-        src[r * ldl + n] = nv ? f2bf(bf2f(x0b[r * ldl + n]) * g) : (u16)0;
+        uo[e] = nv ? f2bf(bf2f(x0b[r * ldl + n]) * g) : (u16)0;
+        src[r * ldl + n] = uo[e];
+        du += bf2f(uo[e]);
         as[r * ldf + n] = zv[e] * g;
         p += dss[r] * xv[e];
       }
+      // m-packed u_{L-1}: these 8 rows of column n are 16 contiguous bytes
+      *reinterpret_cast<uint4*>(a.ump[L - 1] + mp_off(m0 / 16 + r0 / 16, NB, n >> 5, (n & 31) + 32 * ((r0 & 15) >> 3))) =
+          make_uint4((unsigned)uo[0] | ((unsigned)uo[1] << 16), (unsigned)uo[2] | ((unsigned)uo[3] << 16),
+                     (unsigned)uo[4] | ((unsigned)uo[5] << 16), (unsigned)uo[6] | ((unsigned)uo[7] << 16));
     }
-    if (nv) a.part[(int64_t)blockIdx.x * a.D + n] = p;
+    bpart[(L - 1) * P + n] = du;
+    if (nv) bpart[L * P + n] = p;
   }
   __syncthreads();
-  // u_{L-1}^T: four rows of one column per 8-B store
-  auto store_ut = [&](const u16* u, u16* ut) {
-    for (int i = tid; i < a.D * (TBM / 4); i += TNT) {
-      const int n = i / (TBM / 4), j = i - n * (TBM / 4);
-      u16 o[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) o[t] = m0 + 4 * j + t < a.M ? u[(4 * j + t) * ldl + n] : (u16)0;
-      uint2 pk;
-      pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
-      pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
-      *reinterpret_cast<uint2*>(ut + (int64_t)n * a.ldt + m0 + 4 * j) = pk;
-    }
-  };
-  store_ut(src, a.ut[L - 1]);
-  const int NB = P / 32, NS = P / 16;
   for (int l = L - 1; l >= 0; --l) {
     const bf16x8* wtp = reinterpret_cast<const bf16x8*>(a.wtp[l]);
     auto epi = [&](const f32x16& acc, int kb, const float* zp) {
       const int c = lane & 31, h = lane >> 5;
       const int k = kb * 32 + c;
       const bool kv = k < a.D;
+      float cs = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        u16 o[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int r = 8 * q + 4 * h + t;
           const int m = m0 + r;
           const float gl = acc[q * 4 + t] + gs[r * ldf + k];
+          o[t] = 0;
           if (l > 0) {
             gs[r * ldf + k] = kv ? gl : 0.f;
             as[r * ldf + k] += kv ? zp[q * 4 + t] * gl : 0.f;
-            dst[r * ldl + k] = kv ? f2bf(bf2f(x0b[r * ldl + k]) * gl) : (u16)0;
+            o[t] = kv ? f2bf(bf2f(x0b[r * ldl + k]) * gl) : (u16)0;
+            dst[r * ldl + k] = o[t];
+            cs += bf2f(o[t]);
           } else if (kv && m < a.M) {
             float v0 = gl + as[r * ldf + k];
             u16* d = a.dy + (int64_t)m * a.ldy + k;
@@ -841,6 +852,16 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
             *d = f2bf(v0);
           }
         }
+        if (l > 0) {  // m-packed u_{l-1}
+          uint2 pk;
+          pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
+          pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
+          *reinterpret_cast<uint2*>(a.ump[l - 1] + mp_off(m0 / 16 + (q >> 1), NB, kb, c + 32 * (q & 1)) + 4 * h) = pk;
+        }
+      }
+      if (l > 0) {  // db_{l-1} partial: column sum of the tile's u_{l-1}
+        cs += __shfl_xor(cs, 32);
+        if (h == 0) bpart[(l - 1) * P + k] = cs;
       }
     };
     for (int kb0 = w; kb0 < NB; kb0 += 2 * TNW) {
@@ -864,7 +885,6 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
       if (two) epi(acc1, kb1, z1);
     }
     __syncthreads();
-    if (l > 0) store_ut(dst, a.ut[l - 1]);
     u16* t = src;
     src = dst;
     dst = t;

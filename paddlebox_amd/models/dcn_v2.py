@@ -18,6 +18,8 @@ from __future__ import annotations
 
 from typing import Sequence
 
+import os
+
 import torch
 from torch import nn
 
@@ -85,7 +87,9 @@ class CrossNetV2(nn.Module):
     def workspace(self, y: torch.Tensor):
         M, ld = int(y.shape[0]), int(y.shape[1])
         if self._xw is None or self._xw_key != (M, ld, y.device):
-            self._xw = _native.hip().CrossWorkspace(M, self.dim, len(self.w), y.device.index or 0, 1024)
+            # batch rows per split-K slice of the dW GEMMs (PBX_CROSS_KSPLIT, multiple of 64)
+            ks = int(os.environ.get("PBX_CROSS_KSPLIT", "1024"))
+            self._xw = _native.hip().CrossWorkspace(M, self.dim, len(self.w), y.device.index or 0, ks)
             self._xw_key = (M, ld, y.device)
         return self._xw
 
