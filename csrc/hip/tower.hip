@@ -793,15 +793,17 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
     const bool nv = n < a.D;
     const float wcn = nv ? a.wc[n] : 0.f;
     float p = 0.f, du = 0.f;
-    for (int r0 = 0; r0 < TBM; r0 += 8) {
-      float zv[8], xv[8];
+    // all 32 rows' z / x_L loads in flight at once (64 per thread, before any use)
+    float zv[TBM], xv[TBM];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int m = m0 + r0 + e;
-        const bool ok = nv && m < a.M;
-        zv[e] = ok ? a.z[L - 1][(int64_t)m * a.ldf + n] : 0.f;
-        xv[e] = ok ? a.xlast[(int64_t)m * a.ldf + n] : 0.f;
-      }
+    for (int e = 0; e < TBM; ++e) {
+      const int m = m0 + e;
+      const bool ok = nv && m < a.M;
+      zv[e] = ok ? a.z[L - 1][(int64_t)m * a.ldf + n] : 0.f;
+      xv[e] = ok ? a.xlast[(int64_t)m * a.ldf + n] : 0.f;
+    }
+#pragma unroll
+    for (int r0 = 0; r0 < TBM; r0 += 8) {
       u16 uo[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -811,8 +813,8 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
         uo[e] = nv ? f2bf(bf2f(x0b[r * ldl + n]) * g) : (u16)0;
         src[r * ldl + n] = uo[e];
         du += bf2f(uo[e]);
-        as[r * ldf + n] = zv[e] * g;
-        p += dss[r] * xv[e];
+        as[r * ldf + n] = zv[r] * g;
+        p += dss[r] * xv[r];
       }
       // m-packed u_{L-1}: these 8 rows of column n are 16 contiguous bytes
       *reinterpret_cast<uint4*>(a.ump[L - 1] + mp_off(m0 / 16 + r0 / 16, NB, n >> 5, (n & 31) + 32 * ((r0 & 15) >> 3))) =

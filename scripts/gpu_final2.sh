@@ -1,0 +1,16 @@
+#!/bin/bash
+# GPU box: whole GPU suite, smoke(), driver-style bench (defaults and 20/5), step kernel trace
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_final.log 2>&1
+rc=$?
+tail -1 gpurun_out/pytest_final.log
+if [ $rc -ne 0 ]; then grep -E "FAILED|Error" gpurun_out/pytest_final.log | head -20; exit $rc; fi
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_final.log 2>&1 || { echo smoke failed; tail -20 gpurun_out/smoke_final.log; exit 2; }
+tail -1 gpurun_out/smoke_final.log
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/b_final.json 2> gpurun_out/b_final.err || { echo "bench failed"; tail -30 gpurun_out/b_final.err; exit 3; }
+cat gpurun_out/b_final.json
+timeout -k 10 400 python -u bench.py > gpurun_out/b_final_def.json 2> gpurun_out/b_final_def.err || { echo "bench failed"; tail -30 gpurun_out/b_final_def.err; exit 3; }
+grep -o '"ms_per_step": [0-9.]*\|"fp32_ms_per_step": [0-9.]*\|"steps": [0-9]*' gpurun_out/b_final_def.json | tr '\n' ' '; echo
+bash scripts/gpu_step_trace.sh final | head -16
