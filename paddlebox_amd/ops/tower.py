@@ -119,6 +119,7 @@ class _CtrTowerFn(torch.autograd.Function):
             if t.on_dense_grads is not None:  # e.g. start the dense all-reduce, overlapped with the sparse push
                 t.on_dense_grads()
 
+        deferred_dw = None
         if t.overlap_dw and x.is_cuda and not _collectives_in_step():
             # dX chain on the compute stream; the dW GEMMs + bias / data_norm
             # reductions (and whatever consumes the dense grads) on a side
@@ -126,12 +127,11 @@ class _CtrTowerFn(torch.autograd.Function):
             # the optimizer joins it (parallel.dense.join_grad_producers)
             cur = torch.cuda.current_stream(x.device)
             dx0 = ws.backward(*args, parts=1)
-            side = t._side_stream(x.device)
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                ws.backward(*args, parts=2)
-                dense_tail()
-            add_grad_producer(side)
+            deferred_dw = torch.cuda.Event()
+            deferred_dw.record(cur)
+            if not t.dw_after_head:
+                _launch_dw(t, ws, args, dense_tail, x.device, deferred_dw)
+                deferred_dw = None
         else:
             dx0 = ws.backward(*args)
             dense_tail()
@@ -146,8 +146,25 @@ class _CtrTowerFn(torch.autograd.Function):
         dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, ws.K0p,
                            ctx.means, ctx.scales, dn.eps if dn is not None else 0.0, dlin_scale=gl,
                            want_stats=False)
+        if deferred_dw is not None:
+            # issued after the head backward (and the cross backward): both
+            # depend only on the dX chain, and a dW launch enqueued first
+            # fills the CUs and starves the head's workgroups (fp32 tower:
+            # head_bwd 13 -> 95 us beside k_t32_dw, profiles/r3_s2_dw_after_head.txt)
+            _launch_dw(t, ws, args, dense_tail, x.device, deferred_dw)
         d_extra = (ctx.dz * gl if gl is not None else ctx.dz.clone()) if ctx.has_extra else None
         return (dx, d_extra, None, None) + (None,) * (len(t._params))
+
+
+def _launch_dw(t, ws, args, dense_tail, device, after: "torch.cuda.Event"):
+    """The tower's dW GEMM + reductions and the dense tail on its side stream,
+    ordered after the dX chain (event ``after``) only."""
+    side = t._side_stream(device)
+    side.wait_event(after)
+    with torch.cuda.stream(side):
+        ws.backward(*args, parts=2)
+        dense_tail()
+    add_grad_producer(side)
 
 
 class CtrTower:
@@ -178,6 +195,8 @@ class CtrTower:
         # run the dW GEMM on a side stream, overlapped with the head backward
         # and the sparse push (PBX_TOWER_OVERLAP_DW=0 turns it off)
         self.overlap_dw = os.environ.get("PBX_TOWER_OVERLAP_DW", "1") != "0"
+        # ... enqueued after the head backward (PBX_DW_AFTER_HEAD=0: right after the dX chain)
+        self.dw_after_head = os.environ.get("PBX_DW_AFTER_HEAD", "1") != "0"
         self._side = None
         self._part = None
         self._params = list(mlp.parameters())
