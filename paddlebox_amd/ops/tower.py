@@ -195,8 +195,13 @@ class CtrTower:
         # run the dW GEMM on a side stream, overlapped with the head backward
         # and the sparse push (PBX_TOWER_OVERLAP_DW=0 turns it off)
         self.overlap_dw = os.environ.get("PBX_TOWER_OVERLAP_DW", "1") != "0"
-        # ... enqueued after the head backward (PBX_DW_AFTER_HEAD=0: right after the dX chain)
-        self.dw_after_head = os.environ.get("PBX_DW_AFTER_HEAD", "1") != "0"
+        # ... enqueued after the head backward, or right after the dX chain.
+        # Measured (profiles/r3_s2_dw_after_head.txt): after the head for
+        # DeepFM (0.255 vs 0.278 ms/step), right after the dX chain with a
+        # DCN-V2 cross stack, whose long backward then hides the dW (0.399 vs
+        # 0.410).  PBX_DW_AFTER_HEAD=1/0 forces either.
+        env = os.environ.get("PBX_DW_AFTER_HEAD")
+        self.dw_after_head = (env != "0") if env is not None else cross is None
         self._side = None
         self._part = None
         self._params = list(mlp.parameters())
