@@ -114,9 +114,7 @@ __device__ __forceinline__ int64_t probe_thread(const TableDev& t, uint64_t key)
 // PROBE = false: rows_occ already holds every occurrence's row (the split
 // pull probed it on the critical stream; this dedup runs on a side stream
 // under the dense forward).
-constexpr int kTdItems = 1;
-constexpr int kTdLds = 512;
-template <bool PROBE>
+template <bool PROBE, int kTdItems, int kTdLds = 512 * kTdItems>  // LDS hash at load factor <= 1/2
 __global__ __launch_bounds__(256) void k_table_rank(TableDev t, const uint64_t* __restrict__ keys, int64_t n,
                                                     int64_t* __restrict__ rows_occ, int32_t* __restrict__ rank,
                                                     int32_t* __restrict__ cnt_row, int32_t* __restrict__ uid_row,
@@ -514,12 +512,27 @@ void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64
                         int32_t* u_count, bool rows_given, hipStream_t s) {
   launch_fill32(u_count, 0u, 4, s);  // [U, n_valid, -, segment cursor]
   if (n <= 0) return;
-  if (rows_given)
-    hipLaunchKernelGGL(k_table_rank<false>, dim3(blocks_for(n, 256 * kTdItems)), dim3(256), 0, s, t,
-                       reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, uid_row, rows_u, u_count);
-  else
-    hipLaunchKernelGGL(k_table_rank<true>, dim3(blocks_for(n, 256 * kTdItems)), dim3(256), 0, s, t,
-                       reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, uid_row, rows_u, u_count);
+  // occurrences per thread (PBX_TD_ITEMS 1 / 2 / 4): more probes in flight
+  // per thread and fewer workgroups (fewer same-address u_count atomics);
+  // same-box A/B 0.252-0.257 (2) vs 0.258-0.262 (1) vs 0.262-0.267 (4) ms/step
+  static const int items = [] {
+    const char* e = getenv("PBX_TD_ITEMS");
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 4) ? v : 2;
+  }();
+#define PBX_TD_LAUNCH(PR, IT)                                                                                  \
+  hipLaunchKernelGGL((k_table_rank<PR, IT>), dim3(blocks_for(n, 256 * IT)), dim3(256), 0, s, t,              \
+                     reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, uid_row, rows_u, u_count)
+  if (rows_given) {
+    if (items == 4) PBX_TD_LAUNCH(false, 4);
+    else if (items == 2) PBX_TD_LAUNCH(false, 2);
+    else PBX_TD_LAUNCH(false, 1);
+  } else {
+    if (items == 4) PBX_TD_LAUNCH(true, 4);
+    else if (items == 2) PBX_TD_LAUNCH(true, 2);
+    else PBX_TD_LAUNCH(true, 1);
+  }
+#undef PBX_TD_LAUNCH
   hipLaunchKernelGGL(k_table_seg, dim3(blocks_for(n, 256 * kTdSegItems)), dim3(256), 0, s, rows_u, cnt_row, u_count,
                      seg);
   hipLaunchKernelGGL(k_table_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_occ, rank, uid_row, seg, n, uid,
