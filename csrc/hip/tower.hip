@@ -40,7 +40,8 @@ typedef unsigned short u16;
 constexpr int TBM = 32;   // rows per workgroup (fwd / bwd)
 constexpr int TNT = 512;  // threads per workgroup (8 waves, 2 per SIMD)
 constexpr int TNW = TNT / 64;
-constexpr int PF = 8;     // weight-fragment prefetch depth (k-steps)
+constexpr int PF = 6;     // default weight-fragment prefetch depth (k-steps; PBX_TOWER_PF picks 4 / 6 / 8;
+                          // same-box A/B 0.2515-0.2528 ms/step at 6 vs 0.2543-0.2660 at 8)
 constexpr int kMpAlign = 128;
 
 __device__ __forceinline__ u16 f2bf(float f) {
@@ -59,7 +60,7 @@ __device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float(((unsigned
 // The steady-state loop is branch-free (prefetch addresses are clamped, TWO
 // is a template parameter) so hipcc keeps counted vmcnt waits across the
 // ring instead of draining it every step.
-template <bool TWO>
+template <bool TWO, int PF>
 __device__ __forceinline__ void mma_pair(const u16* __restrict__ As, int ldl, const bf16x8* __restrict__ w0,
                                          const bf16x8* __restrict__ w1, int KS, int rot, f32x16& acc0,
                                          f32x16& acc1, int lane) {
@@ -139,6 +140,7 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16& acc, const TowerLayer
   }
 }
 
+template <int PFv>
 __global__ __launch_bounds__(TNT) void k_tower_fwd(TowerArgs a) {
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
   const int ldl = a.lds_ld;
@@ -173,8 +175,8 @@ __global__ __launch_bounds__(TNT) void k_tower_fwd(TowerArgs a) {
       const bool two = nb1 < NB;
       f32x16 acc0 = (f32x16){0}, acc1 = (f32x16){0};
       const bf16x8* w0p = wp + (int64_t)nb0 * KS * 64 + lane;
-      if (two) mma_pair<true>(src, ldl, w0p, wp + (int64_t)nb1 * KS * 64 + lane, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
-      else mma_pair<false>(src, ldl, w0p, w0p, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      if (two) mma_pair<true, PFv>(src, ldl, w0p, wp + (int64_t)nb1 * KS * 64 + lane, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      else mma_pair<false, PFv>(src, ldl, w0p, w0p, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
       const bool mp = !(a.debug & 8);
       fwd_epilogue(acc0, ly, nb0, m0, dst, ldl, lane, mp);
       if (two) fwd_epilogue(acc1, ly, nb1, m0, dst, ldl, lane, mp);
@@ -266,6 +268,7 @@ __device__ __forceinline__ void bwd_epilogue(const f32x16& acc, const TowerLayer
   if (h == 0) bp[prev.bias_off + kb * 32 + c] = cs;
 }
 
+template <int PFv>
 __global__ __launch_bounds__(TNT) void k_tower_bwd(TowerArgs a) {
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
   __shared__ float gs[TBM];
@@ -341,8 +344,8 @@ __global__ __launch_bounds__(TNT) void k_tower_bwd(TowerArgs a) {
         if (two) mk1 = bwd_mask(a.ly[i - 1], kb1, m0, lane);
       }
       const bf16x8* w0p = wtp + (int64_t)kb0 * NS * 64 + lane;
-      if (two) mma_pair<true>(src, ldl, w0p, wtp + (int64_t)kb1 * NS * 64 + lane, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
-      else mma_pair<false>(src, ldl, w0p, w0p, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      if (two) mma_pair<true, PFv>(src, ldl, w0p, wtp + (int64_t)kb1 * NS * 64 + lane, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      else mma_pair<false, PFv>(src, ldl, w0p, w0p, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
       if (i > 0) {
         bwd_epilogue(acc0, a.ly[i - 1], mk0, kb0, m0, dst, ldl, bp, lane);
         if (two) bwd_epilogue(acc1, a.ly[i - 1], mk1, kb1, m0, dst, ldl, bp, lane);
@@ -618,6 +621,7 @@ __global__ __launch_bounds__(256) void k_adam_fused(float* __restrict__ p, float
 __device__ __forceinline__ int cross_ldl(int P) { return P + 8; }
 __device__ __forceinline__ int cross_ldf(int P) { return P + 4; }
 
+template <int PFv>
 __global__ __launch_bounds__(TNT) void k_cross_fwd(CrossFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
   const int P = a.Np > a.Kp ? a.Np : a.Kp;
@@ -698,8 +702,8 @@ __global__ __launch_bounds__(TNT) void k_cross_fwd(CrossFwdArgs a) {
       const bool two = nb1 < NB;
       f32x16 acc0 = (f32x16){0}, acc1 = (f32x16){0};
       const bf16x8* w0p = wp + (int64_t)nb0 * KS * 64 + lane;
-      if (two) mma_pair<true>(src, ldl, w0p, wp + (int64_t)nb1 * KS * 64 + lane, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
-      else mma_pair<false>(src, ldl, w0p, w0p, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      if (two) mma_pair<true, PFv>(src, ldl, w0p, wp + (int64_t)nb1 * KS * 64 + lane, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      else mma_pair<false, PFv>(src, ldl, w0p, w0p, KS, (int)blockIdx.x * 5, acc0, acc1, lane);
       epi(acc0, nb0);
       if (two) epi(acc1, nb1);
     }
@@ -760,6 +764,7 @@ __global__ void k_cross_pack(CrossPackJob j, int L, int D, int Kp, int Np) {
 }
 
 // ---------------------------------------------------------------- DCN-V2 cross backward chain
+template <int PFv>
 __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
   const int P = a.Np;
@@ -881,8 +886,8 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
       }
       f32x16 acc0 = (f32x16){0}, acc1 = (f32x16){0};
       const bf16x8* w0p = wtp + (int64_t)kb0 * NS * 64 + lane;
-      if (two) mma_pair<true>(src, ldl, w0p, wtp + (int64_t)kb1 * NS * 64 + lane, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
-      else mma_pair<false>(src, ldl, w0p, w0p, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      if (two) mma_pair<true, PFv>(src, ldl, w0p, wtp + (int64_t)kb1 * NS * 64 + lane, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
+      else mma_pair<false, PFv>(src, ldl, w0p, w0p, NS, (int)blockIdx.x * 5, acc0, acc1, lane);
       epi(acc0, kb0, z0);
       if (two) epi(acc1, kb1, z1);
     }
@@ -898,20 +903,41 @@ int tower_nwg(int M) { return ((M + kMpAlign - 1) / kMpAlign * kMpAlign) / TBM; 
 
 size_t tower_lds_bytes(const TowerArgs& a) { return (size_t)2 * TBM * a.lds_ld * sizeof(u16); }
 
-static void allow_big_lds() {
+static int tower_pf() {
+  static const int v = [] {
+    const char* e = getenv("PBX_TOWER_PF");
+    const int x = e ? atoi(e) : PF;
+    return (x == 4 || x == 8) ? x : 6;
+  }();
+  return v;
+}
+
+// dynamic LDS above 64 KB must be opted into per kernel instantiation (static
+// LDS of the kernels is < 1 KB); clear the runtime's sticky last-error if the
+// call is refused
+static void big_lds(const void* f) {
+  if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
+    (void)hipGetLastError();
+}
+template <int P>
+static void allow_big_lds_pf() {
   static const bool once = [] {
-    // dynamic LDS above 64 KB must be opted into (static LDS of the kernels
-    // is < 1 KB); clear the runtime's sticky last-error if the call is refused
-    if (hipFuncSetAttribute((const void*)k_tower_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) !=
-        hipSuccess)
-      (void)hipGetLastError();
-    if (hipFuncSetAttribute((const void*)k_tower_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) !=
-        hipSuccess)
-      (void)hipGetLastError();
+    big_lds((const void*)k_tower_fwd<P>);
+    big_lds((const void*)k_tower_bwd<P>);
+    big_lds((const void*)k_cross_fwd<P>);
+    big_lds((const void*)k_cross_bwd<P>);
     return true;
   }();
   (void)once;
 }
+#define PBX_PF_DISPATCH(KERN, GRID, LDS, STREAM, ARG)                                                       \
+  do {                                                                                                     \
+    switch (tower_pf()) {                                                                                  \
+      case 4: allow_big_lds_pf<4>(); hipLaunchKernelGGL(KERN<4>, GRID, dim3(TNT), LDS, STREAM, ARG); break; \
+      case 6: allow_big_lds_pf<6>(); hipLaunchKernelGGL(KERN<6>, GRID, dim3(TNT), LDS, STREAM, ARG); break; \
+      default: allow_big_lds_pf<8>(); hipLaunchKernelGGL(KERN<8>, GRID, dim3(TNT), LDS, STREAM, ARG); break; \
+    }                                                                                                      \
+  } while (0)
 
 
 size_t cross_fwd_lds_bytes(int Np, int Kp) {
@@ -922,15 +948,7 @@ size_t cross_fwd_lds_bytes(int Np, int Kp) {
 
 void launch_cross_fwd(const CrossFwdArgs& a, hipStream_t s) {
   if (a.M == 0) return;
-  static const bool once = [] {
-    if (hipFuncSetAttribute((const void*)k_cross_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) !=
-        hipSuccess)
-      (void)hipGetLastError();
-    return true;
-  }();
-  (void)once;
-  hipLaunchKernelGGL(k_cross_fwd, dim3((unsigned)((a.M + TBM - 1) / TBM)), dim3(TNT), cross_fwd_lds_bytes(a.Np, a.Kp),
-                     s, a);
+  PBX_PF_DISPATCH(k_cross_fwd, dim3((unsigned)((a.M + TBM - 1) / TBM)), cross_fwd_lds_bytes(a.Np, a.Kp), s, a);
 }
 
 void launch_cross_pack(const float* const* w, unsigned short* const* wp, unsigned short* const* wtp, int L, int D,
@@ -950,27 +968,17 @@ int cross_bwd_blocks(int M) { return (M + TBM - 1) / TBM; }
 
 void launch_cross_bwd(const CrossBwdArgs& a, hipStream_t s) {
   if (a.M == 0) return;
-  static const bool once = [] {
-    if (hipFuncSetAttribute((const void*)k_cross_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) !=
-        hipSuccess)
-      (void)hipGetLastError();
-    return true;
-  }();
-  (void)once;
-  hipLaunchKernelGGL(k_cross_bwd, dim3((unsigned)cross_bwd_blocks(a.M)), dim3(TNT), cross_fwd_lds_bytes(a.Np, a.Np),
-                     s, a);
+  PBX_PF_DISPATCH(k_cross_bwd, dim3((unsigned)cross_bwd_blocks(a.M)), cross_fwd_lds_bytes(a.Np, a.Np), s, a);
 }
 
 void launch_tower_fwd(const TowerArgs& a, hipStream_t s) {
   if (a.M == 0) return;
-  allow_big_lds();
-  hipLaunchKernelGGL(k_tower_fwd, dim3(a.Mp / TBM), dim3(TNT), tower_lds_bytes(a), s, a);
+  PBX_PF_DISPATCH(k_tower_fwd, dim3(a.Mp / TBM), tower_lds_bytes(a), s, a);
 }
 
 void launch_tower_bwd(const TowerArgs& a, hipStream_t s) {
   if (a.M == 0) return;
-  allow_big_lds();
-  hipLaunchKernelGGL(k_tower_bwd, dim3(a.Mp / TBM), dim3(TNT), tower_lds_bytes(a), s, a);
+  PBX_PF_DISPATCH(k_tower_bwd, dim3(a.Mp / TBM), tower_lds_bytes(a), s, a);
 }
 
 void launch_tower_dw(const TowerArgs& a, hipStream_t s) {
