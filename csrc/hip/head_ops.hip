@@ -14,6 +14,8 @@
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace pbx {
@@ -278,8 +280,16 @@ void launch_head_bwd(const HeadArgs& a, hipStream_t s) {
     const unsigned g = (unsigned)((a.B + kRB - 1) / kRB);
     hipLaunchKernelGGL(k_head_bwd<kRB>, dim3(g), dim3(256), head_lds_bytes(a.C, a.D, a.Cp), s, a);
   } else {
-    const unsigned g = (unsigned)((a.B + 7) / 8);
-    hipLaunchKernelGGL(k_head_bwd<8>, dim3(g), dim3(256), head_lds_bytes(a.C, a.D, a.Cp), s, a);
+    // rows per workgroup without the statistics (PBX_HEAD_BWD_RB 4 / 8)
+    static const int rb = [] {
+      const char* e = getenv("PBX_HEAD_BWD_RB");
+      return (e && atoi(e) == 4) ? 4 : 8;
+    }();
+    const unsigned g = (unsigned)((a.B + rb - 1) / rb);
+    if (rb == 4)
+      hipLaunchKernelGGL(k_head_bwd<4>, dim3(g), dim3(256), head_lds_bytes(a.C, a.D, a.Cp), s, a);
+    else
+      hipLaunchKernelGGL(k_head_bwd<8>, dim3(g), dim3(256), head_lds_bytes(a.C, a.D, a.Cp), s, a);
   }
 }
 

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void k_table_rank(TableDev t, const uint64_t* 
 // run starts: block exclusive scan of the per-row counts of the block's
 // unique ids + one cursor atomic per block (runs contiguous, not id-ordered);
 // the row counts are re-zeroed for the next batch
-constexpr int kTdSegItems = 4;
+template <int kTdSegItems>
 __global__ __launch_bounds__(256) void k_table_seg(const int64_t* __restrict__ rows_u, int32_t* __restrict__ cnt_row,
                                                    int32_t* __restrict__ u_count, int32_t* __restrict__ seg) {
   __shared__ int32_t wsum[4];
@@ -533,8 +533,19 @@ void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64
     else PBX_TD_LAUNCH(true, 1);
   }
 #undef PBX_TD_LAUNCH
-  hipLaunchKernelGGL(k_table_seg, dim3(blocks_for(n, 256 * kTdSegItems)), dim3(256), 0, s, rows_u, cnt_row, u_count,
-                     seg);
+  // unique ids per thread of the run-start scan (PBX_TD_SEG_ITEMS 1 / 2 / 4);
+  // same-box A/B: 0.250-0.259 ms/step at 1 vs 0.255-0.262 at 4
+  static const int seg_items = [] {
+    const char* e = getenv("PBX_TD_SEG_ITEMS");
+    const int v = e ? atoi(e) : 1;
+    return (v == 2 || v == 4) ? v : 1;
+  }();
+  if (seg_items == 1)
+    hipLaunchKernelGGL(k_table_seg<1>, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_u, cnt_row, u_count, seg);
+  else if (seg_items == 2)
+    hipLaunchKernelGGL(k_table_seg<2>, dim3(blocks_for(n, 512)), dim3(256), 0, s, rows_u, cnt_row, u_count, seg);
+  else
+    hipLaunchKernelGGL(k_table_seg<4>, dim3(blocks_for(n, 1024)), dim3(256), 0, s, rows_u, cnt_row, u_count, seg);
   hipLaunchKernelGGL(k_table_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_occ, rank, uid_row, seg, n, uid,
                      perm, rows_given ? 1 : 0);
 }
