@@ -492,6 +492,9 @@ class Session:
         MultiThread transpilers): backward-role ops on the @GRAD values, the
         optimizer update(s), then optimize-role ops on the parameters."""
         lw = self.lowered
+        # the backward-role ops read the gradients: wait for the side streams
+        # still producing them (the tower's dW runs beside the sparse push)
+        join_grad_producers()
         grads = {}
         for name, st in self.storage.items():
             if isinstance(st, torch.nn.Parameter):

@@ -160,6 +160,9 @@ class AsyncDense:
             off += n
 
     def push(self, summary_stats: Optional[List[torch.Tensor]] = None):
+        from ..parallel.dense import join_grad_producers
+
+        join_grad_producers()  # .cpu() syncs the compute stream only, not the dW side stream
         parts = [a.grad.detach().float().cpu() for a in self.arenas]
         for i, t in enumerate(self.summ):
             st = summary_stats[i] if summary_stats and i < len(summary_stats) else torch.zeros(t.numel())
