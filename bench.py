@@ -66,7 +66,7 @@ def launch_ranks(argv, n: int, dry: bool) -> int:
     worker per device, boxps_trainer.cc:53-79."""
     import subprocess
 
-    if not dry:
+    if not dry and "--same-gpu" not in argv:  # the same-GPU rehearsal runs every rank on cuda:0
         have = _visible_gpus()
         if n > have:
             print(f"[bench] --gpus {n} but only {have} GPU(s) visible: refusing to measure fewer GPUs than asked",
