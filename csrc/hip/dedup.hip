@@ -12,6 +12,8 @@
 // device (no host sync, graph-capturable; padding keys == kEmptyKey sort last
 // and are excluded).
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <hipcub/hipcub.hpp>
 
 #include "kernels.h"
@@ -92,9 +94,9 @@ __global__ void k_emit(const uint64_t* __restrict__ hs, const int32_t* __restric
 // after k_hash_rank) and the per-id counts at the start of the next run, so
 // there is no per-batch memset of the table.
 // u_count = [U, n_valid, U of the previous run, segment cursor]
-constexpr int kRankItems = 4;      // occurrences per thread in k_hash_rank
-constexpr int kRankLds = 2048;     // LDS hash entries per block (load <= 0.5)
-constexpr int kSegItems = 4;       // unique ids per thread in k_seg_alloc
+// occurrences per thread in k_hash_rank (LDS hash at load <= 0.5) and unique
+// ids per thread in k_seg_alloc: template parameters, picked at launch
+// (PBX_HASH_RANK_ITEMS 1/2/4, PBX_HASH_SEG_ITEMS 1/2/4)
 
 __global__ void k_hash_cleanup(int32_t* __restrict__ u_count, int32_t* __restrict__ cnt, int64_t cap,
                                int32_t* __restrict__ zero_extra, int zero_n) {
@@ -211,6 +213,7 @@ __global__ __launch_bounds__(256) void k_hash_insert(const uint64_t* __restrict_
   }
 }
 
+template <int kRankItems, int kRankLds = 512 * kRankItems>
 __global__ __launch_bounds__(256) void k_hash_rank(const int32_t* __restrict__ slot, const int32_t* __restrict__ tu,
                                                    int64_t n, int32_t* __restrict__ uid, int32_t* __restrict__ cnt,
                                                    int32_t* __restrict__ rank) {
@@ -257,6 +260,7 @@ __global__ __launch_bounds__(256) void k_hash_rank(const int32_t* __restrict__ s
 // Also releases the run's hash-set slots (tk / tu are not read after
 // k_hash_rank): the random slot writes ride on this kernel's pass over the
 // ids instead of a separate cleanup pass at the start of the next run.
+template <int kSegItems>
 __global__ __launch_bounds__(256) void k_seg_alloc(const int32_t* __restrict__ cnt, int32_t* __restrict__ u_count,
                                                    int32_t* __restrict__ seg, const int32_t* __restrict__ slot_of_u,
                                                    uint64_t* __restrict__ tk, int32_t* __restrict__ tu) {
@@ -355,12 +359,25 @@ void launch_dedup_hash(const HashDedupArgs& a, void* temp, size_t temp_bytes, hi
   const unsigned gi = (unsigned)((a.n + 256 * kInsItems - 1) / (256 * kInsItems));
   hipLaunchKernelGGL(k_hash_insert, dim3(gi), dim3(256), 0, s, a.keys, a.n, a.mixed, a.tk, a.tu, a.tmask, a.slot,
                      a.slot_of_u, a.uniq_h, a.u_count);
-  const unsigned gr = (unsigned)((a.n + 256 * kRankItems - 1) / (256 * kRankItems));
-  hipLaunchKernelGGL(k_hash_rank, dim3(gr), dim3(256), 0, s, a.slot, a.tu, a.n, a.uid, a.cnt, a.rank);
+  auto env_items = [](const char* name, int dflt) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : dflt;
+    return (v == 1 || v == 2 || v == 4) ? v : dflt;
+  };
+  static const int ri = env_items("PBX_HASH_RANK_ITEMS", 4), si = env_items("PBX_HASH_SEG_ITEMS", 4);
+  const unsigned gr = (unsigned)((a.n + 256 * ri - 1) / (256 * ri));
+  if (ri == 1) hipLaunchKernelGGL(k_hash_rank<1>, dim3(gr), dim3(256), 0, s, a.slot, a.tu, a.n, a.uid, a.cnt, a.rank);
+  else if (ri == 2) hipLaunchKernelGGL(k_hash_rank<2>, dim3(gr), dim3(256), 0, s, a.slot, a.tu, a.n, a.uid, a.cnt, a.rank);
+  else hipLaunchKernelGGL(k_hash_rank<4>, dim3(gr), dim3(256), 0, s, a.slot, a.tu, a.n, a.uid, a.cnt, a.rank);
   (void)temp;
   (void)temp_bytes;
-  const unsigned gs = (unsigned)((a.n + 256 * kSegItems - 1) / (256 * kSegItems));  // U <= n
-  hipLaunchKernelGGL(k_seg_alloc, dim3(gs), dim3(256), 0, s, a.cnt, a.u_count, a.seg, a.slot_of_u, a.tk, a.tu);
+  const unsigned gs = (unsigned)((a.n + 256 * si - 1) / (256 * si));  // U <= n
+  if (si == 1)
+    hipLaunchKernelGGL(k_seg_alloc<1>, dim3(gs), dim3(256), 0, s, a.cnt, a.u_count, a.seg, a.slot_of_u, a.tk, a.tu);
+  else if (si == 2)
+    hipLaunchKernelGGL(k_seg_alloc<2>, dim3(gs), dim3(256), 0, s, a.cnt, a.u_count, a.seg, a.slot_of_u, a.tk, a.tu);
+  else
+    hipLaunchKernelGGL(k_seg_alloc<4>, dim3(gs), dim3(256), 0, s, a.cnt, a.u_count, a.seg, a.slot_of_u, a.tk, a.tu);
   hipLaunchKernelGGL(k_hash_scatter, dim3(g), dim3(256), 0, s, a.uid, a.rank, a.seg, a.n, a.perm, a.u_count);
 }
 
