@@ -205,7 +205,7 @@ def main():
     from paddlebox_amd.models.deepfm import DeepFM
     from paddlebox_amd.ops import reference as ref
     from paddlebox_amd.ops.ctr import auc_accumulate
-    from paddlebox_amd.parallel.dense import DenseArena, DenseSync, FlatAdam
+    from paddlebox_amd.parallel.dense import DenseArena, DenseSync, FlatAdam, join_grad_producers
     from paddlebox_amd.ps.config import PSConfig
     from paddlebox_amd.ps.sparse_engine import SparseEngine
 
@@ -323,7 +323,14 @@ def main():
         # exchange; the IPC meshes are independent of each other by construction
         sync = DenseSync(arena, mode="grad_allreduce",
                          overlap_group=dist.new_group(list(range(world))) if (multi and ipc is None) else None, ipc=ipc)
-        if getattr(model, "tower", None) is not None:
+        # PBX_ADAM_ON_SIDE=1 (one rank): the Adam update is issued from the tower's
+        # dense-grads hook on the dW side stream, beside the sparse push, instead
+        # of after the push on the compute stream (joined at the end of the step)
+        adam_side = (not multi) and os.environ.get("PBX_ADAM_ON_SIDE", "0") == "1" and \
+            getattr(model, "tower", None) is not None
+        if adam_side:
+            model.tower.on_dense_grads = lambda: opt.step(1.0, join=False)
+        elif getattr(model, "tower", None) is not None:
             model.tower.on_dense_grads = sync.launch
 
         # every pinned batch buffer is streamed to the device once up front so the
@@ -347,8 +354,11 @@ def main():
         def train_step(b):
             loss, pred = model(b)
             loss.backward(one)
-            sync.before_step()
-            opt.step(sync.grad_scale())
+            if adam_side:
+                join_grad_producers()  # the side stream ran the update
+            else:
+                sync.before_step()
+                opt.step(sync.grad_scale())
             if not fused_auc:
                 auc_accumulate(pred, b.label, auc_table, auc_stats)
             return loss.detach()

@@ -143,10 +143,13 @@ class FlatAdam:
               for d in self._fuse_dns if d.training and d.update_norm]
         return pack, dn
 
-    def step(self, grad_scale: float = 1.0):
+    def step(self, grad_scale: float = 1.0, join: bool = True):
         # (issuing the update on the dW side stream instead, beside the sparse
-        # push, measured no faster: 0.286 vs 0.280-0.285 ms/step)
-        join_grad_producers()
+        # push, measured no faster: 0.286 vs 0.280-0.285 ms/step; bench.py
+        # PBX_ADAM_ON_SIDE re-measures it).  join=False: the caller is on the
+        # stream that produced the gradients
+        if join:
+            join_grad_producers()
         if self.a.flat.is_cuda:
             pack, dn = self._extras()
             _native.hip().adam_fused(self.a.flat, self.a.param_grad, self.m, self.v, self.pows, self.ticket, self.lr,
