@@ -510,7 +510,13 @@ void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t
 void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows_occ, int32_t* rank,
                         int32_t* cnt_row, int32_t* uid_row, int64_t* rows_u, int32_t* uid, int32_t* perm, int32_t* seg,
                         int32_t* u_count, bool rows_given, hipStream_t s) {
-  launch_fill32(u_count, 0u, 4, s);  // [U, n_valid, -, segment cursor]
+  // [U, n_valid, -, segment cursor] = 0 (PBX_FILL_MEMSET=1: a memset node instead of the fill kernel)
+  static const bool memset_fill = [] {
+    const char* e = getenv("PBX_FILL_MEMSET");
+    return e && atoi(e) == 1;
+  }();
+  if (memset_fill) (void)hipMemsetAsync(u_count, 0, 4 * sizeof(int32_t), s);
+  else launch_fill32(u_count, 0u, 4, s);
   if (n <= 0) return;
   // occurrences per thread (PBX_TD_ITEMS 1 / 2 / 4): more probes in flight
   // per thread and fewer workgroups (fewer same-address u_count atomics);
