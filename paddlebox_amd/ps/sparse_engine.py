@@ -232,6 +232,8 @@ class SparseEngine:
             # the side-stream dedup's atomics slow the concurrent head / tower
             # forward more than the overlap saves -- so it stays opt-in
             self.split_pull = os.environ.get("PBX_SPLIT_PULL", "0") == "1"
+            # table dedup: the seqpool reads each occurrence's row directly
+            self.seqpool_rows_occ = os.environ.get("PBX_SEQPOOL_ROWS_OCC", "1") != "0"
             # ring of per-pull buffers (sort-free hash dedup everywhere: the
             # sender packs its unique keys per owner with a counting pass)
             self._slots = [_PullSlot(self) for _ in range(max(1, int(pull_ring)))]
@@ -368,9 +370,15 @@ class SparseEngine:
             src, src_index = self.table.values, st.rows
         else:
             src, src_index = sl.resp_back, sl.send_index
+        uid = sl.ws.uid
+        if (st.extra.get("rows_occ") is not None and self.seqpool_rows_occ and not self.sharded
+                and self.codec is None):
+            # table dedup: the occurrence's row is known directly (one dependent
+            # load less per occurrence than uid -> rows_u)
+            src_index, uid = st.extra["rows_occ"], None
         if dense is not None:
             dense = dense.contiguous().float()
-        h.seqpool_cvm_fwd(src, src_index, sl.ws.uid, lod, S, B, self.E, out, col_offset, sp.use_cvm,
+        h.seqpool_cvm_fwd(src, src_index, uid, lod, S, B, self.E, out, col_offset, sp.use_cvm,
                           sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter, sp.show_coeff, sp.clk_coeff,
                           sp.threshold, sp.quant_ratio, sp.embed_threshold_filter, sp.embed_threshold,
                           sp.embed_thres_size if not sp.use_cvm else 0, dense, dense_col,
@@ -536,6 +544,7 @@ class SparseEngine:
             st = PullState(B=B, S=S, L=L, lod=lod, uid=ws.uid, perm=ws.perm, counts=ws.u_count, slot=sl,
                            gen=sl.gen)
             st.rows = ws.rows_u[:L]
+            st.extra["rows_occ"] = ws.rows_occ[:L]
             if self.auto_insert and not self.test_mode:
                 miss = (ws.rows_occ[:L] < 0) & (keys.reshape(-1) != -1)
                 if bool(miss.any()):
