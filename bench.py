@@ -10,7 +10,9 @@ Criteo-1TB-shape"): 26 sparse slots over a 1e9-feature space (Criteo-1TB
 per-slot cardinalities scaled to 1B, power-law id popularity), 13 dense
 features, 8-dim embedx (+show/click/embed_w = 11-wide pull records), sparse
 Adagrad in the GPU parameter server, DeepFM (FM + data_norm + MLP 400-400-400)
-with bf16 MFMA GEMMs and fused Adam.  The feature table is pre-populated with
+with the MLP in exact fp32 (the reference's fc precision) on fp32 MFMA and fused
+Adam; the same run also times the bf16-MFMA tower and DCN-V2 (BASELINE config 5)
+as secondaries in ``config``.  The feature table is pre-populated with
 all 1e9 features (random-init weights, as if a base model was loaded) and
 sharded across GPUs by hash; keys are exchanged with all-to-all each step.
 Weak scaling: the per-GPU batch is fixed.  Each timed step = H2D of the batch
@@ -155,11 +157,16 @@ def main():
                     help="before warmup, print per-step host time of load / replay for this many steps (stderr)")
     ap.add_argument("--host-diag", action="store_true",
                     help="after the measurement, split host time into replay / H2D load (stderr only)")
-    ap.add_argument("--mlp-dtype", choices=("bf16", "fp32"), default="bf16",
-                    help="bf16: fused MFMA tower (default); fp32: the reference's fp32 fc precision")
+    ap.add_argument("--mlp-dtype", choices=("bf16", "fp32"), default="fp32",
+                    help="fp32: the reference's fp32 fc precision (default headline, exact fp32 MFMA tower); "
+                         "bf16: the bf16 MFMA tower")
     ap.add_argument("--secondary-dtype", choices=("auto", "fp32", "bf16", "none"), default="auto",
                     help="after the headline measurement, time the same K steps at this MLP precision in the same "
-                         "run and report it in config (auto: fp32 when the headline is bf16 DeepFM on one GPU)")
+                         "run and report it in config (auto: the other precision when the headline is DeepFM on "
+                         "one GPU)")
+    ap.add_argument("--secondary-dcn", choices=("auto", "on", "off"), default="auto",
+                    help="also time DCN-V2 (BASELINE config 5, bf16 MLP) in the same run over the same sparse "
+                         "engine and report it in config (auto: on for the one-GPU DeepFM headline)")
     ap.add_argument("--model", choices=("deepfm", "dcn_v2"), default="deepfm",
                     help="deepfm = the headline config; dcn_v2 = BASELINE config 5 (cross layers on the MFMA GEMM)")
     ap.add_argument("--cross-layers", type=int, default=3)
@@ -271,15 +278,15 @@ def main():
         log(rank, f"[bench] prefilled {n_ins} features on rank0 (table size {engine.table.size()}, "
                   f"{engine.table.memory_bytes() / 2**30:.1f} GiB) in {time.time() - t0:.1f}s")
 
-    def measure(mlp_dtype: str, primary: bool):
+    def measure(mlp_dtype: str, primary: bool, model_name: str = args.model):
         """Build the model at this MLP precision over the shared sparse engine,
         capture the step, run W warmup + K timed steps; returns the timings."""
         hidden = tuple(int(x) for x in args.hidden.split(","))
-        dcn = args.model == "dcn_v2"
+        dcn = model_name == "dcn_v2"
         fp32 = mlp_dtype == "fp32"
         if dcn:
             if fp32:
-                raise SystemExit("--mlp-dtype fp32 is a DeepFM precision variant")
+                raise SystemExit("DCN-V2 (BASELINE config 5) is a bf16-MLP config: run it with --mlp-dtype bf16")
             model = DCNv2(engine, num_slots=S, dense_dim=13, cross_layers=args.cross_layers, hidden=hidden).to(device)
         else:
             model = DeepFM(engine, num_slots=S, dense_dim=13, hidden=hidden).to(device)
@@ -479,6 +486,8 @@ def main():
 
     hidden = tuple(int(x) for x in args.hidden.split(","))
     dcn = args.model == "dcn_v2"
+    if dcn and args.mlp_dtype == "fp32":
+        args.mlp_dtype = "bf16"  # config 5 names a bf16 MLP
     res = measure(args.mlp_dtype, True)
     dt, t_enq, loss, auc_stats, ipc = res["dt"], res["t_enq"], res["loss"], res["auc_stats"], res["ipc"]
     overflow_1 = engine.check_overflow()
@@ -488,19 +497,33 @@ def main():
     sec_dtype = args.secondary_dtype
     if sec_dtype == "auto":
         # one GPU: the driver's headline run; the N-GPU scaling runs keep one measurement
-        sec_dtype = "fp32" if (args.mlp_dtype == "bf16" and not dcn and world == 1) else "none"
-    if sec_dtype != "none" and sec_dtype != args.mlp_dtype:
-        # same run, same sparse engine: the other MLP precision's step time
-        # (the reference fc computes in fp32 / TF32; the headline is bf16)
+        sec_dtype = ("bf16" if args.mlp_dtype == "fp32" else "fp32") if (not dcn and world == 1) else "none"
+    if dcn:
+        sec_dtype = "none"
+
+    def _release():
+        nonlocal ipc
         if ipc is not None:
             ipc.close()
+            ipc = None
         import gc
 
         gc.collect()
         torch.cuda.empty_cache()
+
+    if sec_dtype != "none" and sec_dtype != args.mlp_dtype:
+        # same run, same sparse engine: the other MLP precision's step time
+        _release()
         second = measure(sec_dtype, False)
         ipc = second["ipc"]
         log(rank, f"[bench] {sec_dtype} MLP: {second['dt'] / args.steps * 1e3:.4f} ms/step")
+    dcn_res = None
+    if args.secondary_dcn == "on" or (args.secondary_dcn == "auto" and not dcn and world == 1):
+        # BASELINE config 5 (DCN-V2, bf16 MLP) over the same sparse engine
+        _release()
+        dcn_res = measure("bf16", False, "dcn_v2")
+        ipc = dcn_res["ipc"]
+        log(rank, f"[bench] DCN-V2: {dcn_res['dt'] / args.steps * 1e3:.4f} ms/step")
 
     overflow = engine.check_overflow() or overflow_1  # also raises if an IPC exchange timed out
     if ipc is not None:
@@ -546,8 +569,15 @@ def main():
                 **({f"{sec_dtype}_ms_per_step": round(second["dt"] / args.steps * 1e3, 4),
                     f"{sec_dtype}_samples_per_s": round(B * world * args.steps / second["dt"], 1),
                     f"{sec_dtype}_mlp": ("exact fp32 products on v_mfma_f32_16x16x4_f32 (the reference fc "
-                                         "precision), same run, same sparse engine")}
+                                         "precision)" if sec_dtype == "fp32" else "bf16 operands on bf16 MFMA, fp32 "
+                                         "accumulate") + ", same run, same sparse engine"}
                    if second is not None else {}),
+                **({"dcn_v2_ms_per_step": round(dcn_res["dt"] / args.steps * 1e3, 4),
+                    "dcn_v2_samples_per_s": round(B * world * args.steps / dcn_res["dt"], 1),
+                    "dcn_v2_model": "DCN-V2 (%d full-rank cross layers + data_norm + MLP %s, bf16 MFMA), BASELINE "
+                                    "config 5 shape on one GPU, same run, same sparse engine"
+                                    % (args.cross_layers, args.hidden)}
+                   if dcn_res is not None else {}),
                 "native_build": _build_summary(),
                 "unique_keys_per_batch": round(sum(u_per_batch) / len(u_per_batch), 1),
                 "keys_per_batch": l_per_batch,

@@ -115,6 +115,9 @@ class IpcComm {
     IPC_CHECK(((uintptr_t)send.data_ptr() & 15) == 0 && ((uintptr_t)dst.data_ptr() & 15) == 0,
               "send / dst must be 16-byte aligned");
     IPC_CHECK(rec_bytes > 0 && rec_bytes <= p_.slot_bytes, "rec_bytes");
+    // per-peer record counts travel in the flag word's count field (ipc.hip kIpcCountBits)
+    IPC_CHECK(p_.slot_bytes / rec_bytes < ((int64_t)1 << kIpcCountBits),
+              "slot holds more records than the flag word's count field can announce");
     const int32_t* c = nullptr;
     int32_t* rc = nullptr;
     if (counts.has_value() && counts->defined()) {

@@ -188,8 +188,21 @@ __global__ __launch_bounds__(256) void k_codec_update(TableDev t, CodecDev c, co
     return;
   }
   if (c.kind == 3) {  // variable: one Adagrad group over the live columns
-    const int xs = (int)v[c.xsz];
+    int xs = (int)v[c.xsz];
     if (xs <= 0) return;
+    // a row's size follows its slot: rows pre-populated with init_embedx
+    // (k_codec_init knows no slot and creates D columns) that turn out to
+    // belong to an expand slot are re-created at their first push with De
+    // columns (fresh draws, fresh g2sum), as a push-created row would be
+    const int want = expand_slot(c, slot) ? c.De : c.D;
+    if (xs != want) {
+      const uint64_t salt = seed ^ (uint64_t)r * 0x9E3779B97F4A7C15ULL;
+      for (int j = 0; j < want; ++j) store_col(c, v, j, hash_uniform(salt, j) * cfg.mf_initial_range);
+      for (int j = want; j < c.Wx; ++j) store_col(c, v, j, 0.f);
+      v[c.xsz] = (float)want;
+      v[c.xg2] = 0.f;
+      return;
+    }
     const float g2 = v[c.xg2];
     const float ratio = mf_lr * sqrtf(cfg.mf_initial_g2sum / (cfg.mf_initial_g2sum + g2));
     float add = 0.f;

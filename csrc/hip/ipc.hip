@@ -7,7 +7,7 @@
 //           [e % depth][phase][me] (one pass over xGMI);
 //   signal  every block drains its puts, one lane releases at system scope and
 //           arrives on a local counter; the last block publishes
-//           (epoch << 24 | count) into each peer's flag word [phase][me];
+//           (epoch << 28 | count) into each peer's flag word [phase][me];
 //   wait    every block polls (bounded, relaxed system-scope loads) until all
 //           W flags of its own inbox carry the epoch, then acquires once; the
 //           counts ride along.
@@ -41,7 +41,9 @@
 namespace pbx {
 namespace {
 
-constexpr int kCountBits = 24;
+// flag word = epoch << kCountBits | count: 2^28 records per peer slot (the
+// host refuses bigger slots), 36 epoch bits (~6.9e10 collectives)
+constexpr int kCountBits = kIpcCountBits;
 constexpr uint64_t kCountMask = (1ull << kCountBits) - 1;
 
 __device__ __forceinline__ unsigned char* slot_ptr(const IpcPeers& pt, int owner, int slot, int phase, int src) {

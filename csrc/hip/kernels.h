@@ -204,9 +204,10 @@ void launch_fill32(void* p, uint32_t v, int64_t n_words, hipStream_t s);
 
 // IPC mesh collectives (ipc.hip): peer pointers of one node's ranks
 constexpr int kIpcMaxRanks = 8;
+constexpr int kIpcCountBits = 28;  // flag word count field (ipc.hip)
 struct IpcPeers {
   unsigned char* inbox[kIpcMaxRanks];  // each rank's inbox [depth][2][world][slot_bytes]
-  uint64_t* flags[kIpcMaxRanks];       // each rank's flag words [2][world] = epoch << 24 | count
+  uint64_t* flags[kIpcMaxRanks];       // each rank's flag words [2][world] = epoch << kIpcCountBits | count
   int64_t slot_bytes;
   int world, rank, depth;  // depth = inbox slots (a call uses slot epoch % depth)
   int64_t spin_limit;    // s_sleep(2) polls before a wait gives up (sticky err)

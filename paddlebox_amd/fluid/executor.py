@@ -409,7 +409,10 @@ class Session:
             out[name + "_beta2_pow_acc_0"] = o.pows[1:2] * o.b2
         return out
 
-    def load_optimizer_state(self, state: Dict[str, Any]) -> int:
+    def load_optimizer_state(self, state: Dict[str, Any], reference_pows: bool = True) -> int:
+        """``reference_pows``: the beta-pow accumulators hold beta^(t+1) (the
+        reference convention, what optimizer_state writes); False for files
+        written before io.save_persistables recorded the convention (beta^t)."""
         from ..parallel.sharding import ShardedFlatAdam
 
         n_loaded = 0
@@ -426,7 +429,7 @@ class Session:
                 for i, (suffix, beta) in enumerate((("_beta1_pow_acc_0", o.b1), ("_beta2_pow_acc_0", o.b2))):
                     if name + suffix in state:
                         acc = torch.as_tensor(state[name + suffix], dtype=torch.float32).reshape(1)
-                        o.pows[i:i + 1].copy_((acc / beta).to(o.pows.device))
+                        o.pows[i:i + 1].copy_((acc / beta if reference_pows else acc).to(o.pows.device))
             for o, m, v in touched.values():
                 if isinstance(o, ShardedFlatAdam):
                     o.scatter_moments(m, v)
@@ -438,7 +441,9 @@ class Session:
         names = {n for n in self.optimizer_state()}
         staged = {n: self.scope.get(n) for n in names if n in self.scope}
         if staged:
-            self.load_optimizer_state(staged)
+            conv = self.scope.get("@beta_pow_convention@") if "@beta_pow_convention@" in self.scope else None
+            self.load_optimizer_state(staged, reference_pows=conv is None or bool(int(conv)))
+            self.scope._tensors.pop("@beta_pow_convention@", None)
             for n in staged:  # consumed: a later session must not re-apply a stale checkpoint
                 self.scope._tensors.pop(n, None)
 

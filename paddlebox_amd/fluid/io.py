@@ -99,7 +99,9 @@ def save_persistables(executor, dirname: str, main_program: Optional[Program] = 
 
         st = {k: np.ascontiguousarray(_to_np(v)) for k, v in sessions[0].optimizer_state().items()}
         if st:
-            save_file(st, os.path.join(dirname, _OPT_FILE))
+            # format marker: beta-pow accumulators hold beta^(t+1) (the
+            # reference convention); files without it hold beta^t
+            save_file(st, os.path.join(dirname, _OPT_FILE), metadata={"beta_pow_convention": "reference"})
             saved += list(st)
     return saved
 
@@ -113,16 +115,22 @@ def load_persistables(executor, dirname: str, main_program: Optional[Program] = 
     loaded = load_vars(executor, dirname, program, _persistables(program), filename=filename, scope=scope)
     p = os.path.join(dirname, _OPT_FILE)
     if os.path.exists(p):
+        from safetensors import safe_open
         from safetensors.numpy import load_file
 
         st = load_file(p)
+        with safe_open(p, "np") as f:
+            meta = f.metadata() or {}
+        # written before the format marker existed: raw beta^t powers
+        ref_pows = meta.get("beta_pow_convention") == "reference"
         sessions = executor.sessions_for(program) if hasattr(executor, "sessions_for") else []
         if sessions:
-            sessions[0].load_optimizer_state(st)
+            sessions[0].load_optimizer_state(st, reference_pows=ref_pows)
         else:
             sc = scope or global_scope()
             for k, a in st.items():
                 sc.set(k, torch.as_tensor(a))
+            sc.set("@beta_pow_convention@", torch.tensor(1 if ref_pows else 0))
         loaded += list(st)
     return loaded
 

@@ -93,6 +93,11 @@ class GpuSparseTable:
     def values(self) -> torch.Tensor:
         return self.t.values
 
+    @property
+    def rows(self) -> int:
+        """Value rows (slots + stash): the index space of a table row."""
+        return int(self.t.values.shape[0])
+
     def export(self, with_values: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
         k, v = self.t.export_all(with_values)
         if with_values and self.codec is not None:

@@ -1,4 +1,4 @@
-"""Per-batch sparse pipeline: dedup -> (key all-to-all) -> probe -> pull ->
+"""Per-batch sparse pipeline: dedup -> (key exchange) -> probe -> pull ->
 fused seqpool+CVM, and the mirror push path with fused sparse Adagrad.
 
 This is the engine behind ``pull_box_sparse``/``push_box_sparse`` and
@@ -7,17 +7,30 @@ pull, ``:373-522`` push; BoxPS ``PullSparseGPU/PushSparseGPU`` closed).
 
 MI355X design points
 --------------------
-* No host synchronisation per batch: the unique count lives on the device
-  and every kernel is launched for the static upper bound, so a whole training
-  step can be captured in one HIP graph.
-* Sorting by ``h = mix64(key)`` makes the unique list come out grouped by owner
-  GPU (``owner = floor(h*N/2^64)`` is monotone in h): the key all-to-all needs no
-  partition pass.  The exchange uses fixed per-peer capacity ``C`` so
-  ``all_to_all_single`` has static equal splits (graph-capturable, one RCCL
-  call per direction, ragged bytes padded to C).  Overflow (a peer receiving
-  more than C uniques -- needs adversarial keys) is flagged on the device and
-  checked at pass end.
-* One GPU (world=1): the forward reads value rows straight out of the table.
+* No host synchronisation per batch: unique counts live on the device and
+  every kernel is launched for the static upper bound, so a whole training
+  step is captured in one HIP graph.
+* One shard (world = 1, the default): the dedup runs THROUGH the table -- the
+  pass-resident table row is the unique id.  ``k_table_rank`` probes every
+  occurrence (LDS-staged bucket, wave ballot) and ranks first occurrences,
+  ``k_table_seg`` / ``k_table_scatter`` build the per-unique occurrence
+  segments; the fused seqpool+CVM reads each occurrence's row directly.  The
+  push is one wave-segmented merge with the Adagrad update in registers
+  (``k_push_merge_apply``) plus ``k_push_finish`` for runs that straddle waves.
+  ``dedup=False`` (FLAGS_enable_pullpush_dedup_keys) probes per occurrence and
+  merges the push by leader election per table row instead.
+* Sharded (world > 1): the sender dedups with the sort-free hash dedup
+  (``dedup.hip``: insert, rank, segment, scatter) and packs its unique keys
+  per owner (``owner = floor(h * N / 2^64)``, ``h = mix64(key)``).  The
+  exchange runs on the in-house IPC mesh (``parallel/ipc.py``: one kernel per
+  exchange, only ``counts[p]`` records of each peer slot travel, worst-case or
+  pre-scanned exact slots, so nothing is dropped) or, as the fallback, on RCCL
+  ``all_to_all_single`` with fixed per-peer slots (heuristic slot size, sticky
+  device overflow flag checked at pass end).  The owner probes and gathers in
+  one launch, answers, and applies the pushed gradients with a leader-elected
+  per-row Adagrad (no owner-side dedup).
+* Feature-type codecs (int16 embedx, expand block, variable, SparseAdam) run
+  through the codec kernels of ``feature_ops.hip`` on the hash-dedup path.
 """
 from __future__ import annotations
 
@@ -110,6 +123,16 @@ class PullState:
     slot: Optional[_PullSlot] = None  # GPU: the buffers this pull used
     gen: int = 0
     extra: dict = field(default_factory=dict)
+
+
+TABLE_DEDUP_MAX_ROWS = (1 << 31) - 1
+
+
+def table_dedup_fits(table_rows: int) -> bool:
+    """The single-shard table dedup (table.hip k_table_rank) keys its LDS hash
+    and per-row scratch by int32 row; past INT32_MAX rows the engine falls
+    back to the sort-free hash dedup (dedup.hip), which carries int64 rows."""
+    return int(table_rows) < TABLE_DEDUP_MAX_ROWS
 
 
 def exchange_capacity_for(key_batches, world: int, comm: Optional[Comm] = None) -> int:
@@ -213,19 +236,23 @@ class SparseEngine:
                 # the IPC mesh, so the large slots cost HBM (~1 GB at 8 ranks and
                 # 213K keys per batch, nothing on 288 GB) but no bandwidth.
                 # cap_factor restores a smaller heuristic slot (sticky overflow flag).
-                if exchange_capacity is not None:
-                    self.C = (int(exchange_capacity) + 63) // 64 * 64
-                elif cap_factor is not None:
-                    self.C = int(math.ceil(self.max_keys / self.world * cap_factor)) + 64
-                else:
-                    self.C = (self.max_keys + 63) // 64 * 64
-            if self.sharded:
-                self._setup_exchange(exchange or os.environ.get("PBX_SPARSE_EXCHANGE", "ipc"))
+                # The worst-case slot only pays on the IPC mesh; RCCL's
+                # all_to_all_single always moves whole slots, so it keeps the
+                # heuristic slot (1.25 x the even share, sticky overflow flag).
+                xmode = exchange or os.environ.get("PBX_SPARSE_EXCHANGE", "ipc")
+                self.C = self._exchange_slot(exchange_capacity, cap_factor, self._ipc_candidate(xmode))
+                self._setup_exchange(xmode)
+                if self.exchange_mode != "ipc" and exchange_capacity is None and cap_factor is None:
+                    self.C = self._exchange_slot(None, None, False)
             # no-dedup single-shard step (see the docstring)
             self.dedup = bool(dedup) or self.sharded or self.codec is not None or self.dim not in (4, 8, 16, 32)
             # single shard: dedup through the table itself (the row is the
             # unique id): probe + rank in one launch, no scratch hash table
-            self.table_dedup = not self.sharded and os.environ.get("PBX_TABLE_DEDUP", "1") != "0"
+            # ... for tables up to INT32_MAX rows (its LDS hash and per-row
+            # scratch hold int32 rows); bigger single-GPU tables (~2^31+ slots,
+            # ~190+ GB at the default layout) take the hash dedup instead
+            self.table_dedup = (not self.sharded and os.environ.get("PBX_TABLE_DEDUP", "1") != "0"
+                                and table_dedup_fits(self.table.rows))
             # ... split off the critical path (_pull_split, PBX_SPLIT_PULL=1):
             # measured slower on one MI355X (same-box interleaved A/B, 3 reps:
             # 0.283 vs 0.263-0.268 ms/step, profiles/r3_s2_split_pull_ab.txt) --
@@ -270,6 +297,21 @@ class SparseEngine:
         self._seed = 1234
 
     # ------------------------------------------------------------------ build
+    def _ipc_candidate(self, mode: str) -> bool:
+        return mode == "ipc" and isinstance(self.comm, TorchDistComm) and self.world <= 8
+
+    def _exchange_slot(self, exact: Optional[int], cap_factor: Optional[float], ipc: bool) -> int:
+        """Per-peer exchange slot (records): exact when the pass was
+        pre-scanned (exchange_capacity_for); the worst case (every key of a
+        batch owned by one peer) on the IPC mesh, where only the valid records
+        of a slot travel; otherwise the heuristic ``cap_factor`` share."""
+        if exact is not None:
+            return (int(exact) + 63) // 64 * 64
+        if cap_factor is None and ipc:
+            return (self.max_keys + 63) // 64 * 64
+        f = 1.25 if cap_factor is None else float(cap_factor)
+        return min((self.max_keys + 63) // 64 * 64, int(math.ceil(self.max_keys / self.world * f)) + 64)
+
     def _setup_exchange(self, mode: str):
         """Sparse key / value / gradient exchange transport.  "ipc": three
         IPC meshes (one per record kind, so each received view is a contiguous
@@ -277,7 +319,7 @@ class SparseEngine:
         self-tested on every rank, all ranks fall back to RCCL together if any
         rank's test fails (e.g. no peer access between the GPUs)."""
         self.exchange_mode = "rccl"
-        if mode != "ipc" or not isinstance(self.comm, TorchDistComm) or self.world > 8:
+        if not self._ipc_candidate(mode):
             return
         from ..parallel.ipc import IpcMesh, IpcMeshError
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box driver: runs steps in order; continues past plain test failures
 # (pytest rc=1) but stops at anything that looks like a fault/abort/timeout.
-# usage: scripts/gpu_round.sh "<step1 cmd>" "<step2 cmd>" ...
+# usage: scripts/gpu/steps.sh "<step1 cmd>" "<step2 cmd>" ...
 mkdir -p gpurun_out
 i=0
 for cmd in "$@"; do

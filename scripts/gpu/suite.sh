@@ -13,6 +13,6 @@ timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/b_final.
 cat gpurun_out/b_final.json
 timeout -k 10 400 python -u bench.py > gpurun_out/b_final_def.json 2> gpurun_out/b_final_def.err || { echo "bench failed"; tail -30 gpurun_out/b_final_def.err; exit 3; }
 grep -o '"ms_per_step": [0-9.]*\|"fp32_ms_per_step": [0-9.]*\|"steps": [0-9]*' gpurun_out/b_final_def.json | tr '\n' ' '; echo
-bash scripts/gpu_step_trace.sh final | head -16
+bash scripts/gpu/step_trace.sh final | head -16
 timeout -k 10 400 python -u bench.py --model dcn_v2 --steps 200 --warmup 50 --secondary-dtype none > gpurun_out/b_final_dcn.json 2> gpurun_out/b_final_dcn.err || { echo "dcn bench failed"; tail -30 gpurun_out/b_final_dcn.err; exit 3; }
 grep -h "wall" gpurun_out/b_final_dcn.err

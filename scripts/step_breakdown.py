@@ -9,8 +9,17 @@ ap = argparse.ArgumentParser()
 ap.add_argument("trace")
 ap.add_argument("--anchor", default="k_tower_fwd")
 ap.add_argument("--steps", type=int, default=10)
+ap.add_argument("--copies", default=None, help="rocprofv3 memory_copy_trace.csv: shown in the timeline")
 a = ap.parse_args()
 rows = list(csv.DictReader(open(a.trace)))
+copies = []
+if a.copies:
+    try:
+        for r in csv.DictReader(open(a.copies)):
+            copies.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                           "copy " + r.get("Direction", "?") + " " + r.get("Size", r.get("Bytes", "")) + "B"))
+    except OSError:
+        copies = []
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if a.anchor in r["Kernel_Name"]]
 idx = idx[-(a.steps + 1):]
@@ -37,9 +46,13 @@ t0 = int(rows[s]["Start_Timestamp"])
 # include the kernels of the same step launched before the anchor
 prev = idx[-3] if len(idx) >= 3 else s
 print("\ntimeline (us from the anchor of the last step; negative = before it):")
-for r in rows[prev:e]:
-    st = (int(r["Start_Timestamp"]) - t0) / 1e3
-    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-    n = r["Kernel_Name"].replace("pbx::(anonymous namespace)::", "").replace("void ", "").split("(")[0][:50]
+ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+       r["Kernel_Name"].replace("pbx::(anonymous namespace)::", "").replace("void ", "").split("(")[0][:50])
+      for r in rows[prev:e]]
+lo, hi = ev[0][0], int(rows[e]["Start_Timestamp"])
+ev += [c for c in copies if lo <= c[0] < hi]
+for b0, b1, n in sorted(ev):
+    st = (b0 - t0) / 1e3
+    d = (b1 - b0) / 1e3
     if st > -200:
         print(f"  {st:8.1f} {st + d:8.1f} {d:7.1f}  {n}")

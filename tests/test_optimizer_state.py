@@ -68,3 +68,37 @@ def test_beta_pow_accumulators_follow_reference_convention(box, tmp_path):
     # round trip of the state just exported restores the powers exactly
     s.load_optimizer_state({k: np.asarray(v) for k, v in st.items()})
     assert float(opt.pows[0]) == pytest.approx(opt.b1 ** steps, rel=1e-6)
+
+
+def test_optimizer_file_records_pow_convention(box, tmp_path):
+    """save_persistables marks its optimizer file with the beta-pow convention;
+    a file without the marker (written before it existed) holds raw beta^t
+    powers and loads without the beta^(t+1) conversion."""
+    from safetensors import safe_open
+    from safetensors.numpy import save_file
+
+    from paddlebox_amd.fluid import io as fio
+
+    s = _session(box, tmp_path)
+    opt = s.opts[0]
+    pows = opt.pows.clone()
+    d = tmp_path / "ckpt"
+    d.mkdir()
+    st = {k: np.ascontiguousarray(np.asarray(v)) for k, v in s.optimizer_state().items()}
+    save_file(st, str(d / "marked.safetensors"), metadata={"beta_pow_convention": "reference"})
+    with safe_open(str(d / "marked.safetensors"), "np") as f:
+        assert f.metadata()["beta_pow_convention"] == "reference"
+    # legacy layout: the raw powers under the same names, no marker
+    legacy = dict(st)
+    for k in legacy:
+        if k.endswith("_beta1_pow_acc_0"):
+            legacy[k] = pows[0:1].numpy().copy()
+        elif k.endswith("_beta2_pow_acc_0"):
+            legacy[k] = pows[1:2].numpy().copy()
+    opt.pows.fill_(0.5)
+    s.load_optimizer_state(legacy, reference_pows=False)
+    torch.testing.assert_close(opt.pows, pows)
+    opt.pows.fill_(0.5)
+    s.load_optimizer_state(st, reference_pows=True)
+    torch.testing.assert_close(opt.pows, pows)
+    assert fio._OPT_FILE.endswith(".safetensors")
