@@ -208,11 +208,8 @@ def main():
     launcher = os.environ.get("PBX_BENCH_LAUNCHER", "torchrun" if "WORLD_SIZE" in os.environ else "single")
 
     from paddlebox_amd.data.synthetic import CriteoSynth
-    from paddlebox_amd.models.dcn_v2 import DCNv2
-    from paddlebox_amd.models.deepfm import DeepFM
     from paddlebox_amd.ops import reference as ref
-    from paddlebox_amd.ops.ctr import auc_accumulate
-    from paddlebox_amd.parallel.dense import DenseArena, DenseSync, FlatAdam, join_grad_producers
+    from paddlebox_amd.runtime.ctr_step import CtrTrainStep
     from paddlebox_amd.ps.config import PSConfig
     from paddlebox_amd.ps.sparse_engine import SparseEngine
 
@@ -283,62 +280,17 @@ def main():
         capture the step, run W warmup + K timed steps; returns the timings."""
         hidden = tuple(int(x) for x in args.hidden.split(","))
         dcn = model_name == "dcn_v2"
-        fp32 = mlp_dtype == "fp32"
-        if dcn:
-            if fp32:
-                raise SystemExit("DCN-V2 (BASELINE config 5) is a bf16-MLP config: run it with --mlp-dtype bf16")
-            model = DCNv2(engine, num_slots=S, dense_dim=13, cross_layers=args.cross_layers, hidden=hidden).to(device)
-        else:
-            model = DeepFM(engine, num_slots=S, dense_dim=13, hidden=hidden).to(device)
-        if fp32:
-            model.set_precision("fp32")
-        # the fused tower runs the whole dense side (bf16 operands, or exact fp32)
-        fused = getattr(model, "use_tower", False) and (not fp32 or model.tower.fp32)
-        C = model.dn.C
-        arena = DenseArena(model.parameters(), device, extra_grad=3 * C if multi and not dcn else 0)
-        if multi:
-            model.dn.group = dist.group.WORLD
-            model.dn.sync_stats = True
-            if fused and not dcn:
-                # data_norm batch statistics are summed across ranks in the SAME
-                # all-reduce as the dense gradients (tail of the gradient buffer)
-                model.dn.stats = arena.grad_tail(3 * C)
-                model.dn.stats_in_grad_bucket = True
-        # one update launch for the dense side: Adam + bf16 tower weight re-pack +
-        # data_norm summary update; grads zeroed by the same kernel
-        opt = FlatAdam(arena, lr=1e-3, clear_grad=True)
-        if fused:
-            opt.fuse(mlps=[model.mlp], data_norms=[model.dn])
-        # the dense all-reduce runs on its own communicator and side stream, started
-        # as soon as the tower's gradients are final: it overlaps the sparse push
-        ipc = None
-        if multi and (args.dense == "ipc" or args.same_gpu):
-            from paddlebox_amd.parallel.ipc import IpcMesh, IpcMeshError
-
-            try:
-                ipc = IpcMesh(arena.grad.numel() * 4, device=device)
-                if not ipc.self_test():
-                    ipc.close()
-                    ipc = None
-                    log(rank, "[bench] dense IPC mesh self-test failed; RCCL all-reduce")
-            except IpcMeshError as e:
-                ipc = None
-                log(rank, f"[bench] dense IPC mesh unavailable ({e}); RCCL all-reduce")
-        if multi and args.same_gpu and (ipc is None or engine.exchange_mode != "ipc"):
-            raise SystemExit("--same-gpu needs the IPC meshes (RCCL cannot run two ranks on one GPU)")
-        # RCCL dense all-reduce: its own communicator, so it overlaps the sparse
-        # exchange; the IPC meshes are independent of each other by construction
-        sync = DenseSync(arena, mode="grad_allreduce",
-                         overlap_group=dist.new_group(list(range(world))) if (multi and ipc is None) else None, ipc=ipc)
-        # PBX_ADAM_ON_SIDE=1 (one rank): the Adam update is issued from the tower's
-        # dense-grads hook on the dW side stream, beside the sparse push, instead
-        # of after the push on the compute stream (joined at the end of the step)
-        adam_side = (not multi) and os.environ.get("PBX_ADAM_ON_SIDE", "0") == "1" and \
-            getattr(model, "tower", None) is not None
-        if adam_side:
-            model.tower.on_dense_grads = lambda: opt.step(1.0, join=False)
-        elif getattr(model, "tower", None) is not None:
-            model.tower.on_dense_grads = sync.launch
+        if dcn and mlp_dtype == "fp32":
+            raise SystemExit("DCN-V2 (BASELINE config 5) is a bf16-MLP config: run it with --mlp-dtype bf16")
+        auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
+        auc_stats = torch.zeros(5, dtype=torch.float64, device=device)
+        # the model, dense arena + fused Adam, the dense all-reduce (IPC mesh
+        # launched from the tower's dense-grads hook, RCCL fallback) and the
+        # data_norm statistics in the gradient bucket: runtime/ctr_step.py
+        step = CtrTrainStep(engine, model_name, mlp_dtype, num_slots=S, dense_dim=13, hidden=hidden,
+                            cross_layers=args.cross_layers, multi=multi, dense=args.dense, same_gpu=args.same_gpu,
+                            fused_auc=(auc_table, auc_stats), log=lambda m: log(rank, "[bench] dense " + m))
+        model, opt, arena, sync, ipc, fused = step.model, step.opt, step.arena, step.sync, step.ipc, step.fused
 
         # every pinned batch buffer is streamed to the device once up front so the
         # timed steps do not pay the driver's first-touch cost of a pinned range
@@ -350,25 +302,7 @@ def main():
         from paddlebox_amd.runtime.streams import side_stream
 
         copy_stream = side_stream(device, "graph_copy")
-        auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
-        auc_stats = torch.zeros(5, dtype=torch.float64, device=device)
-        fused_auc = fused
-        if fused_auc:  # streaming AUC accumulated by the tower's loss epilogue
-            model.tower.auc = (auc_table, auc_stats, None)
-
-        one = torch.ones((), device=device)  # persistent d loss / d loss: no fill kernel per step
-
-        def train_step(b):
-            loss, pred = model(b)
-            loss.backward(one)
-            if adam_side:
-                join_grad_producers()  # the side stream ran the update
-            else:
-                sync.before_step()
-                opt.step(sync.grad_scale())
-            if not fused_auc:
-                auc_accumulate(pred, b.label, auc_table, auc_stats)
-            return loss.detach()
+        train_step = step.train_step
 
         nb = len(host_batches)
         K = graph_steps_for(args.steps, args.warmup, args.graph_steps)
@@ -481,7 +415,7 @@ def main():
                    auc_stats=auc_stats.clone(), ipc=ipc,
                    prefetch=bool(graphed is not None and graphed.prefetch is not None), fused=fused)
         # free this precision's graphs / model before the next measurement
-        del graphed, model, opt, arena, sync
+        del graphed, model, opt, arena, sync, step
         return res
 
     hidden = tuple(int(x) for x in args.hidden.split(","))

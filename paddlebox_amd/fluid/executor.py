@@ -14,6 +14,7 @@ from __future__ import annotations
 
 from typing import Any, Dict, List, Optional, Sequence
 
+import os
 import warnings
 
 import numpy as np
@@ -219,8 +220,22 @@ class Session:
             sync_k = int(coll.get("k", sync_k))
         if sync_mode is None:
             sync_mode = "grad_allreduce" if world > 1 else "none"
-        for lr_mult, ps in groups.items():
-            arena = DenseArena(ps, self.device)
+        arenas = [(lr_mult, DenseArena(ps, self.device)) for lr_mult, ps in groups.items()]
+        # One process per GPU: the dense gradient all-reduce, the transpiled
+        # c_allreduce_sum ops and data_norm sync_stats of this session run on a
+        # self-tested IPC mesh of the group (one collective kernel, side
+        # stream, graph-capturable), RCCL when the mesh is unavailable
+        # (PBX_DENSE_IPC=0 forces RCCL).  Collective: every rank builds it.
+        self.ipc = None
+        if world > 1 and self.device.type == "cuda" and arenas and os.environ.get("PBX_DENSE_IPC", "1") != "0":
+            from ..parallel.comm import register_group_mesh
+            from ..runtime.ctr_step import make_ipc_mesh
+
+            nbytes = max(max(a.grad.numel() for _, a in arenas) * 4, 1 << 20)
+            self.ipc = make_ipc_mesh(nbytes, self.device, group=self.group,
+                                     log=lambda m: log.warning("fluid dense sync: %s", m))
+            register_group_mesh(self.group, self.ipc)
+        for lr_mult, arena in arenas:
             self.arenas.append(arena)
             if sharded:
                 # ZeRO-1: reduce-scatter grads, Adam on this rank's slice, all-gather params
@@ -232,10 +247,26 @@ class Session:
                 self.syncs.append(DenseSync(arena, "none", 1, self.group))
                 continue
             self.opts.append(_make_opt(spec, arena, lr_mult))
-            self.syncs.append(DenseSync(arena, sync_mode, sync_k, self.group))
+            self.syncs.append(DenseSync(arena, sync_mode, sync_k, self.group,
+                                        ipc=self.ipc if sync_mode == "grad_allreduce" else None))
         # arena rebinding moved the storage: re-point logical views
         self._refresh_logical()
         self._restore_optimizer_state_from_scope()
+
+    def on_tower_grads(self, tower):
+        """The fused tower's dense gradients (and data_norm statistics) are
+        final: start the gradient all-reduce of every arena that holds only
+        this tower's parameters on its side stream now, so it overlaps the
+        head backward and the sparse push (the reference's dense sync hook,
+        box_wrapper.h:686-719, boxps_worker.cc:1216-1236); ``before_step``
+        joins it.  Arenas with other parameters sync after the backward."""
+        own = getattr(self, "_early_sync", None)
+        if own is None:
+            tp = {p.data_ptr() for p in tower._params}
+            own = self._early_sync = [all(p.data_ptr() in tp for p in a.params) for a in self.arenas]
+        for s, early in zip(self.syncs, own):
+            if early and s.ipc is not None:
+                s.launch()
 
     # -------------------------------------------------------------- feeding
     def feed_batch(self, ctx: ExecContext, batch):

@@ -560,8 +560,19 @@ def k_data_norm(ctx, op):
     bias = ctx.param(op.inputs["bias"][0]) if op.inputs.get("bias") else None
     training = ctx.training and not a.get("is_test")
     y = ctr_ops._DataNorm.apply(x, bsize, bsum, bsq, sw, bias, a["epsilon"], a["summary_decay_rate"],
-                                ctx.group if a.get("sync_stats") else None, a.get("update_norm", True), training)
+                                _stats_group(ctx) if a.get("sync_stats") else None, a.get("update_norm", True), training)
     ctx.set(op.outputs["Y"][0], y)
+
+
+def _stats_group(ctx):
+    """The process group data_norm-family statistics are summed over when the
+    op asks for sync_stats: the session's group, and for the default group
+    (ctx.group None) the WORLD handle -- None would mean "no sync"."""
+    if ctx.group is not None:
+        return ctx.group
+    import torch.distributed as dist
+
+    return dist.group.WORLD if dist.is_available() and dist.is_initialized() else None
 
 
 @kernel("masked_data_norm")
@@ -574,7 +585,7 @@ def k_masked_data_norm(ctx, op):
     bias = ctx.param(op.inputs["bias"][0]) if op.inputs.get("bias") else None
     training = ctx.training and not a.get("is_test")
     y = ctr_ext.masked_data_norm(x, mask, bsize, bsum, bsq, sw, bias, a["epsilon"], a["summary_decay_rate"],
-                                 ctx.group if a.get("sync_stats") else None, a.get("update_norm", True), training)
+                                 _stats_group(ctx) if a.get("sync_stats") else None, a.get("update_norm", True), training)
     ctx.set(op.outputs["Y"][0], y)
 
 
@@ -584,7 +595,7 @@ def k_cross_norm_hadamard(ctx, op):
     summary = ctx.scope.get(op.inputs["SummaryInput"][0].name)
     a = op.attrs
     y = ctr_ext.cross_norm_hadamard(x, summary, a["fields_num"], a["embed_dim"], a["epsilon"],
-                                    a["summary_decay_rate"], ctx.group if a.get("sync_stats") else None,
+                                    a["summary_decay_rate"], _stats_group(ctx) if a.get("sync_stats") else None,
                                     ctx.training)
     ctx.set(op.outputs["Out"][0], y)
 
@@ -699,8 +710,10 @@ def _tower_for(ctx, op, C: int):
         setattr(dn, attr, ctx.scope.get(op.inputs[k][0].name))
     dn.stats = torch.zeros(3 * C, device=ctx.device)
     dn.update_norm = a.get("update_norm", True) is not False
-    dn.group = ctx.group
+    dn.group = _stats_group(ctx)
     t = CtrTower(mlp, dn, 0, 1, 0, 0, use_head_lin=False)
+    if ctx.training and hasattr(ctx.s, "on_tower_grads"):
+        t.on_dense_grads = lambda: ctx.s.on_tower_grads(t)
     ctx.cache[key] = t
     return t
 

@@ -10,7 +10,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
-from ..parallel.comm import collective_active
+from ..parallel.comm import allreduce_sum, collective_active
 from . import reference as ref
 
 
@@ -42,8 +42,8 @@ class _DataNorm(torch.autograd.Function):
             dx, stats = ref.data_norm_bwd(x, dy, means, scales, ctx.eps, scale_w)
         if ctx.group is not None and collective_active(ctx.group):
             # one fused all-reduce of [3, C] (reference does 3 separate ones,
-            # data_norm_op.cu:203-230)
-            dist.all_reduce(stats, group=ctx.group)
+            # data_norm_op.cu:203-230); the group's IPC mesh when registered
+            allreduce_sum(stats, ctx.group)
         if ctx.update and ctx.training:
             if _gpu(x):
                 _native.hip().data_norm_update(bsize, bsum, bsq, stats, ctx.decay)
@@ -156,7 +156,7 @@ class _CtrHead(torch.autograd.Function):
                 _, stats = ref.data_norm_bwd(x, x, ctx.means, ctx.scales, dn.eps)
         if dn is not None and dn.training and dn.update_norm:
             if dn.sync_stats and dn.group is not None and collective_active(dn.group):
-                dist.all_reduce(stats, group=dn.group)
+                allreduce_sum(stats, dn.group)
             if _gpu(x):
                 _native.hip().data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, stats, dn.decay)
             else:

@@ -27,7 +27,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
-from ..parallel.comm import collective_active
+from ..parallel.comm import allreduce_sum, collective_active
 from ..parallel.dense import add_grad_producer, join_grad_producers
 from . import reference as ref
 from .mlp import _ensure_grad
@@ -113,7 +113,7 @@ class _CtrTowerFn(torch.autograd.Function):
         def dense_tail():
             if dn_on and not getattr(dn, "stats_in_grad_bucket", False):
                 if dn.sync_stats and dn.group is not None and collective_active(dn.group):
-                    dist.all_reduce(dn.stats, group=dn.group)
+                    allreduce_sum(dn.stats, dn.group)  # the group's IPC mesh when registered
             if dn_on and not dn.fused_update:
                 h.data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, dn.stats, dn.decay)
             if t.on_dense_grads is not None:  # e.g. start the dense all-reduce, overlapped with the sparse push

@@ -171,3 +171,41 @@ def run_ranks(world: int, fn):
     if errs:
         raise errs[0]
     return outs
+
+
+# ------------------------------------------------------------------ dense IPC meshes per group
+# A training session that set up a self-tested IPC mesh for its process group
+# (fluid Session, runtime.ctr_step) registers it here; the in-step sums of
+# that group -- c_allreduce_sum, data_norm sync_stats, the dense gradient
+# all-reduce -- then run as one IPC collective kernel instead of an RCCL call.
+_GROUP_MESH = {}
+
+
+def _gkey(group):
+    if group is None or (dist.is_available() and group is dist.group.WORLD):
+        return None  # the default group under either name
+    return id(group)
+
+
+def register_group_mesh(group, mesh) -> None:
+    if mesh is None:
+        _GROUP_MESH.pop(_gkey(group), None)
+    else:
+        _GROUP_MESH[_gkey(group)] = mesh
+
+
+def group_mesh(group=None):
+    return _GROUP_MESH.get(_gkey(group))
+
+
+def allreduce_sum(t, group=None) -> str:
+    """In-place sum of ``t`` over ``group``: the group's IPC mesh when one is
+    registered and ``t`` is a contiguous fp32 GPU tensor that fits its slot,
+    else torch.distributed.  Returns the transport used ("ipc" / "dist")."""
+    m = group_mesh(group)
+    if m is not None and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and \
+            t.numel() * 4 <= m.slot_bytes:
+        m.allreduce_(t)
+        return "ipc"
+    dist.all_reduce(t, group=group)
+    return "dist"

@@ -1,0 +1,140 @@
+"""The data-parallel CTR training step on one rank, as bench.py times it.
+
+One object builds, over a shared :class:`~paddlebox_amd.ps.sparse_engine.SparseEngine`:
+
+* the model (DeepFM or DCN-V2) at its MLP precision (exact fp32 or bf16 tower);
+* the dense arena, one fused Adam launch (with the tower weight re-pack and the
+  data_norm summary update folded in);
+* on several ranks, the dense gradient all-reduce: the in-house IPC mesh
+  (self-tested, one collective kernel, side stream, launched from the tower's
+  dense-grads hook so it overlaps the sparse push) with RCCL as the fallback,
+  and the data_norm batch statistics riding in the same all-reduce (tail of the
+  gradient buffer);
+* ``train_step(batch)``: forward, backward (sparse push with fused Adagrad
+  inside the pull's backward), dense sync, Adam -- capturable into one HIP
+  graph (runtime/graph_step.py).
+
+Reference: the BoxPSWorker step, ``boxps_worker.cc:1191-1258`` (dense sync
+modes) and ``:1296-1324`` (op loop); the dense sync hook
+``box_wrapper.h:686-719``.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from ..parallel.dense import DenseArena, DenseSync, FlatAdam, join_grad_producers
+
+
+def make_ipc_mesh(nbytes: int, device, group=None, log=None):
+    """A self-tested IPC mesh of ``nbytes`` per slot, or None (caller falls
+    back to RCCL).  Collective over ``group``: every rank must call it."""
+    from ..parallel.ipc import IpcMesh, IpcMeshError
+
+    try:
+        m = IpcMesh(nbytes, group=group, device=device)
+    except IpcMeshError as e:
+        if log:
+            log(f"IPC mesh unavailable ({e}); RCCL all-reduce")
+        return None
+    if not m.self_test(agree=True):
+        m.close()
+        if log:
+            log("IPC mesh self-test failed; RCCL all-reduce")
+        return None
+    return m
+
+
+class CtrTrainStep:
+    def __init__(self, engine, model_name: str = "deepfm", precision: str = "fp32", num_slots: int = 26,
+                 dense_dim: int = 13, hidden: Sequence[int] = (400, 400, 400), cross_layers: int = 3,
+                 multi: bool = False, dense: str = "ipc", same_gpu: bool = False, lr: float = 1e-3,
+                 fused_auc: Optional[tuple] = None, log=None):
+        """``multi``: data-parallel over the default process group (dense
+        all-reduce + synced data_norm statistics).  ``dense``: "ipc" (the IPC
+        mesh, RCCL fallback) or "rccl".  ``same_gpu``: every rank on one GPU
+        (rehearsal): the IPC mesh is mandatory.  ``fused_auc``: (table, stats)
+        accumulated by the tower's loss epilogue."""
+        from ..models.dcn_v2 import DCNv2
+        from ..models.deepfm import DeepFM
+
+        device = engine.device
+        self.device = device
+        dcn = model_name == "dcn_v2"
+        fp32 = precision == "fp32"
+        if dcn:
+            if fp32:
+                raise ValueError("DCN-V2 (BASELINE config 5) is a bf16-MLP config")
+            model = DCNv2(engine, num_slots=num_slots, dense_dim=dense_dim, cross_layers=cross_layers,
+                          hidden=tuple(hidden)).to(device)
+        else:
+            model = DeepFM(engine, num_slots=num_slots, dense_dim=dense_dim, hidden=tuple(hidden)).to(device)
+        if fp32:
+            model.set_precision("fp32")
+        self.model = model
+        # the fused tower runs the whole dense side (bf16 operands, or exact fp32)
+        self.fused = getattr(model, "use_tower", False) and (not fp32 or model.tower.fp32)
+        C = model.dn.C
+        self.arena = DenseArena(model.parameters(), device, extra_grad=3 * C if multi and not dcn else 0)
+        if multi:
+            model.dn.group = dist.group.WORLD
+            model.dn.sync_stats = True
+            if self.fused and not dcn:
+                # data_norm batch statistics are summed across ranks in the SAME
+                # all-reduce as the dense gradients (tail of the gradient buffer)
+                model.dn.stats = self.arena.grad_tail(3 * C)
+                model.dn.stats_in_grad_bucket = True
+        # one update launch for the dense side: Adam + tower weight re-pack +
+        # data_norm summary update; grads zeroed by the same kernel
+        self.opt = FlatAdam(self.arena, lr=lr, clear_grad=True)
+        if self.fused:
+            self.opt.fuse(mlps=[model.mlp], data_norms=[model.dn])
+        self.ipc = None
+        if multi and (dense == "ipc" or same_gpu):
+            self.ipc = make_ipc_mesh(self.arena.grad.numel() * 4, device, log=log)
+        if multi and same_gpu and (self.ipc is None or engine.exchange_mode != "ipc"):
+            raise RuntimeError("same-GPU ranks need the IPC meshes (RCCL cannot run two ranks on one GPU)")
+        # RCCL fallback: the gradient all-reduce stays on the default group and
+        # runs in the step's order (no second communicator running concurrently
+        # inside the captured graph: two RCCL communicators in flight on one
+        # stream set can deadlock)
+        self.sync = DenseSync(self.arena, mode="grad_allreduce", ipc=self.ipc)
+        tower = getattr(model, "tower", None)
+        # PBX_ADAM_ON_SIDE=1 (one rank): the Adam update is issued from the
+        # tower's dense-grads hook on the dW side stream (measured no faster)
+        self.adam_side = (not multi) and os.environ.get("PBX_ADAM_ON_SIDE", "0") == "1" and tower is not None
+        if self.adam_side:
+            tower.on_dense_grads = lambda: self.opt.step(1.0, join=False)
+        elif tower is not None and (self.ipc is not None or not multi):
+            # start the IPC all-reduce as soon as the tower's gradients are final
+            tower.on_dense_grads = self.sync.launch
+        self.fused_auc = fused_auc is not None and self.fused
+        if self.fused_auc:
+            tower.auc = (fused_auc[0], fused_auc[1], None)
+        self._auc = fused_auc
+        self.one = torch.ones((), device=device)  # persistent d loss / d loss: no fill kernel per step
+
+    def __call__(self, b):
+        return self.train_step(b)
+
+    def train_step(self, b):
+        from ..ops.ctr import auc_accumulate
+
+        loss, pred = self.model(b)
+        loss.backward(self.one)
+        if self.adam_side:
+            join_grad_producers()  # the side stream ran the update
+        else:
+            self.sync.before_step()
+            self.opt.step(self.sync.grad_scale())
+        if self._auc is not None and not self.fused_auc:
+            auc_accumulate(pred, b.label, self._auc[0], self._auc[1])
+        return loss.detach()
+
+    def close(self):
+        if self.ipc is not None:
+            self.ipc.close()
+            self.ipc = None
