@@ -263,7 +263,16 @@ class GpuTable {
   py::tuple save_stream(int kind, int mode, bool reset_delta, float base_threshold, float delta_threshold,
                         float delta_keep_days, float nonclk_coeff, float clk_coeff, float embedx_threshold,
                         const std::string& keys_path, const std::string& vals_path, int64_t chunk_rows, int threads,
-                        bool collect) {
+                        bool collect, std::vector<int64_t> decode_map, float decode_scale, int out_dim) {
+    SaveDecode dec;
+    PBX_CHECK(decode_map.size() <= (size_t)kSaveMaxCols, "save_stream: decoded row wider than kSaveMaxCols");
+    dec.n = (int)decode_map.size();
+    dec.scale = decode_scale;
+    for (size_t i = 0; i < decode_map.size(); ++i) {
+      PBX_CHECK(decode_map[i] >= -(int64_t)(2 * values_.size(1)) - 2 && decode_map[i] < values_.size(1),
+                "save_stream: decode map column out of the row");
+      dec.map[i] = (int16_t)decode_map[i];
+    }
     SaveSelect sel;
     sel.mode = mode;
     sel.reset_delta = reset_delta ? 1 : 0;
@@ -276,8 +285,8 @@ class GpuTable {
     SaveStats st;
     {
       py::gil_scoped_release nogil;
-      st = stream_save_table(view(), values_.size(0), kind, sel, embedx_threshold, keys_path, vals_path, chunk_rows,
-                             threads, collect ? &mixed : nullptr, device_, cur_stream());
+      st = stream_save_table(view(), values_.size(0), kind, sel, dec, out_dim, embedx_threshold, keys_path,
+                             vals_path, chunk_rows, threads, collect ? &mixed : nullptr, device_, cur_stream());
     }
     py::object keys = py::none();
     if (collect) {

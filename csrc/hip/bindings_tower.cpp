@@ -8,6 +8,7 @@
 #include <stdexcept>
 
 #include "kernels.h"
+#include "tower32_sched.h"
 
 namespace py = pybind11;
 using torch::Tensor;
@@ -62,7 +63,13 @@ class TowerWorkspace {
     if (fp32) {
       Mp_ = pad(M, 256);  // the dW splits walk whole 2-step (32-row) ring stages
       lds_ld_ = tower32_lds_ld((int)maxw);
-      TW_CHECK((size_t)2 * 32 * lds_ld_ * 4 <= 140 * 1024, "widths exceed the fp32 LDS tile budget");
+      bool part = false;  // wave-stream remainder scratch (tower32.hip): some column count not a multiple of 128
+      for (auto d : dims) part = part || (pad(d, 16) / 16) % 8 != 0;
+      int64_t nbias = 0;
+      for (size_t l = 1; l < dims.size(); ++l) nbias += pad(dims[l], 16);
+      TW_CHECK(tower32_lds_bytes_for(lds_ld_, part, 0) + kTower32BwdStatic <= kTower32LdsTotal &&
+                   tower32_lds_bytes_for(lds_ld_, part, (int)nbias) + 512 <= kTower32LdsTotal,
+               "widths exceed the fp32 LDS tile budget");
     } else {
       Mp_ = tower_nwg((int)M) * 32;
       // each split walks a whole number of 4-step (64-row) ring stages; a small
@@ -78,11 +85,14 @@ class TowerWorkspace {
     int64_t boff = 0;
     for (int l = 0; l < L_; ++l) {
       const int64_t Kp = pad(dims[l], wpad_), Np = pad(dims[l + 1], wpad_);
-      // fp32: 8 KB of slack -- the tower32 weight pipeline loads up to 8
-      // k-groups past a block's last fragment (values unused)
-      const int64_t slack = fp32 ? 2048 : 0;
-      wp_.push_back(torch::zeros({Np * Kp + slack}, ob));
-      wtp_.push_back(torch::zeros({Np * Kp + slack}, ob));
+      // fp32: the wave-stream layout (tower32_sched.h: per-wave streams,
+      // segments padded to the ring depth) + slack for the weight ring, which
+      // loads kT32Ring k-groups (1 KB each) past a stream's end
+      const int64_t slack = 256 * 2 * kT32Ring;
+      const int64_t n_wp = fp32 ? t32_stream_groups((int)(Np / 16), (int)(Kp / 16)) * 256 + slack : Np * Kp;
+      const int64_t n_wtp = fp32 ? t32_stream_groups((int)(Kp / 16), (int)(Np / 16)) * 256 + slack : Np * Kp;
+      wp_.push_back(torch::zeros({n_wp}, ob));
+      wtp_.push_back(torch::zeros({n_wtp}, ob));
       xmp_.push_back(torch::zeros({Mp_ * Np}, ob));
       dzmp_.push_back(torch::zeros({Mp_ * Np}, ob));
       boff_.push_back(boff);

@@ -15,8 +15,8 @@ namespace pbx {
 namespace {
 
 __global__ __launch_bounds__(256) void k_save_chunk(TableDev t, int64_t r0, int64_t r1, SaveSelect sel,
-                                                    uint64_t* __restrict__ okeys, float* __restrict__ ovals,
-                                                    unsigned long long* __restrict__ count) {
+                                                    SaveDecode dec, uint64_t* __restrict__ okeys,
+                                                    float* __restrict__ ovals, unsigned long long* __restrict__ count) {
   const RowLayout l = make_row_layout(t.dim);
   const int64_t total = (int64_t)t.nb * kBucketSlots;
   const uint32_t sn = t.stash_n ? (*t.stash_n < t.stash_cap ? *t.stash_n : t.stash_cap) : 0u;
@@ -54,22 +54,31 @@ __global__ __launch_bounds__(256) void k_save_chunk(TableDev t, int64_t r0, int6
     const unsigned long long o = wbase + __popcll(m & ((1ull << lane) - 1ull));
     okeys[o] = unmix64(key);
     float* v = t.values + row * (int64_t)t.stride;
-    const float4* s4 = reinterpret_cast<const float4*>(v);
-    float4* d4 = reinterpret_cast<float4*>(ovals + (int64_t)o * t.stride);
-    for (int c = 0; c < t.stride / 4; ++c) d4[c] = s4[c];
+    if (dec.n == 0) {
+      const float4* s4 = reinterpret_cast<const float4*>(v);
+      float4* d4 = reinterpret_cast<float4*>(ovals + (int64_t)o * t.stride);
+      for (int c = 0; c < t.stride / 4; ++c) d4[c] = s4[c];
+    } else {  // codec table: decoded canonical row (reset applied below, on the stored row and the copy)
+      float* d = ovals + (int64_t)o * dec.n;
+      const int16_t* q = reinterpret_cast<const int16_t*>(v + kEmbedx);
+      for (int c = 0; c < dec.n; ++c) {
+        const int m = dec.map[c];
+        d[c] = m >= 0 ? v[m] : (m == -1 ? 0.f : (float)q[-2 - m] * dec.scale);
+      }
+    }
     if (sel.reset_delta) v[l.delta_score] = 0.f;
   }
 }
 
 }  // namespace
 
-void launch_save_chunk(const TableDev& t, int64_t r0, int64_t r1, const SaveSelect& sel, uint64_t* okeys,
-                       float* ovals, unsigned long long* count, hipStream_t s) {
+void launch_save_chunk(const TableDev& t, int64_t r0, int64_t r1, const SaveSelect& sel, const SaveDecode& dec,
+                       uint64_t* okeys, float* ovals, unsigned long long* count, hipStream_t s) {
   if (r1 <= r0) return;
   const int64_t n = r1 - r0;
   int blocks = (int)((n + 255) / 256);
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(k_save_chunk, dim3(blocks), dim3(256), 0, s, t, r0, r1, sel, okeys, ovals, count);
+  hipLaunchKernelGGL(k_save_chunk, dim3(blocks), dim3(256), 0, s, t, r0, r1, sel, dec, okeys, ovals, count);
 }
 
 }  // namespace pbx

@@ -129,16 +129,18 @@ void format_rows(const HostBuf& b, int64_t i0, int64_t i1, int dim, int stride, 
 }  // namespace
 
 SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, const SaveSelect& sel,
-                            float embedx_threshold, const std::string& keys_path, const std::string& vals_path,
-                            int64_t chunk_rows, int threads, std::vector<uint64_t>* saved_mixed, int device,
-                            hipStream_t s) {
+                            const SaveDecode& dec, int out_dim, float embedx_threshold, const std::string& keys_path,
+                            const std::string& vals_path, int64_t chunk_rows, int threads,
+                            std::vector<uint64_t>* saved_mixed, int device, hipStream_t s) {
   using clk = std::chrono::steady_clock;
   const auto t_start = clk::now();
   SaveStats st;
   if (chunk_rows < 1024) chunk_rows = 1024;
   if (threads < 1) threads = 1;
-  const int stride = t.stride;
-  const RowLayout l = make_row_layout(t.dim);
+  // output rows: stored (plain layout) or decoded canonical (codec tables)
+  const int stride = dec.n > 0 ? dec.n : t.stride;
+  const int odim = dec.n > 0 ? out_dim : t.dim;
+  const RowLayout l = make_row_layout(odim);
   CK(hipSetDevice(device));
   // ---- buffers
   struct Dev {
@@ -212,7 +214,7 @@ SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, con
             ws.emplace_back([&, w]() {
               outs[w].clear();
               outs[w].reserve((size_t)(b.n / T + 1) * 160);
-              format_rows(b, b.n * w / T, b.n * (w + 1) / T, t.dim, stride, l, sel, embedx_threshold, outs[w]);
+              format_rows(b, b.n * w / T, b.n * (w + 1) / T, odim, stride, l, sel, embedx_threshold, outs[w]);
             });
           }
           for (auto& th : ws) th.join();
@@ -245,7 +247,7 @@ SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, con
       Dev& d = dev[c & 1];
       const auto t0 = clk::now();
       CK(hipMemsetAsync(d.count, 0, sizeof(unsigned long long), s));
-      launch_save_chunk(t, r0, r1, sel, d.keys, d.vals, d.count, s);
+      launch_save_chunk(t, r0, r1, sel, dec, d.keys, d.vals, d.count, s);
       CK(hipGetLastError());
       unsigned long long n = 0;
       CK(hipMemcpyAsync(&n, d.count, sizeof(n), hipMemcpyDeviceToHost, s));

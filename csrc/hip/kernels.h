@@ -294,11 +294,23 @@ struct SaveSelect {
   float nonclk_coeff = 0.1f;
   float clk_coeff = 1.f;
 };
+// Output row of a save: the table row as stored (n = 0), or a decoded row of
+// n floats (feature-type codec tables: the canonical fp32 layout of
+// ps/feature_types.py FeatureCodec.decode) -- map[j] >= 0: stored float
+// column, -1: zero, <= -2: int16 element (-2 - map[j]) of the row's
+// embedding block (stored from float column 3) times scale.
+constexpr int kSaveMaxCols = 192;
+struct SaveDecode {
+  int n = 0;
+  float scale = 1.f;
+  int16_t map[kSaveMaxCols];
+};
 // Compact the selected rows of flat row range [r0, r1) (buckets then stash)
-// into okeys (unmixed feasigns) / ovals (stride floats per row) at
-// positions atomically taken from *count; resets delta_score if asked.
-void launch_save_chunk(const TableDev& t, int64_t r0, int64_t r1, const SaveSelect& sel, uint64_t* okeys,
-                       float* ovals, unsigned long long* count, hipStream_t s);
+// into okeys (unmixed feasigns) / ovals (out_stride floats per row: stride,
+// or dec.n when decoding) at positions atomically taken from *count; resets
+// delta_score if asked.
+void launch_save_chunk(const TableDev& t, int64_t r0, int64_t r1, const SaveSelect& sel, const SaveDecode& dec,
+                       uint64_t* okeys, float* ovals, unsigned long long* count, hipStream_t s);
 struct SaveStats {
   int64_t rows = 0;
   int64_t chunks = 0;
@@ -311,10 +323,12 @@ struct SaveStats {
 // embed_w g2sum [embedx.. embedx_g2sum]", embedx only when score >=
 // embedx_threshold and mf_size != 0).  saved_mixed (optional): the mixed keys
 // of the saved rows are appended (for tiers that mirror the delta reset).
+// dec.n > 0: rows are decoded to the canonical layout of embedding width
+// out_dim (text and .npy use it).
 SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, const SaveSelect& sel,
-                            float embedx_threshold, const std::string& keys_path, const std::string& vals_path,
-                            int64_t chunk_rows, int threads, std::vector<uint64_t>* saved_mixed, int device,
-                            hipStream_t s);
+                            const SaveDecode& dec, int out_dim, float embedx_threshold, const std::string& keys_path,
+                            const std::string& vals_path, int64_t chunk_rows, int threads,
+                            std::vector<uint64_t>* saved_mixed, int device, hipStream_t s);
 // Single-shard dedup through the table itself: rows_occ[i] = row of raw key
 // keys[i] (-1: padding / absent), rows_u[u] = row of unique u, uid / perm /
 // seg / u_count as the hash dedup (u_count = [U, n_valid, -, cursor]).
@@ -590,6 +604,7 @@ struct TowerLayerDev {
 struct TowerArgs {
   int M = 0, Mp = 0, L = 0;
   int lds_ld = 0;  // LDS row stride in elements (max padded width + 8)
+  int t32_part = 0;  // fp32 tower: LDS scratch of the wave-stream remainder partials present (set by the launcher)
   const unsigned short* x0 = nullptr;  // row-major input [M][ld0] (>= Kp_0 cols, pad cols 0)
   int ld0 = 0;
   const unsigned short* x0mp = nullptr;  // MP(X0)
@@ -624,7 +639,8 @@ struct TowerArgs {
   float* dn_stats = nullptr;
   int dw_splits = 2;
   int debug = 0;  // timing experiments only (PBX_TOWER_DEBUG): 1 no loss reduction, 2 no dW reductions, 4 no dW GEMM,
-                  // 8 no fwd m-packed stores, 16 no output layer / loss
+                  // 8 no fwd m-packed stores, 16 no output layer / loss, 32 fp32 tower: no s_setprio on waves 4-7,
+                  // 64 fp32 fwd/bwd: no weight loads in the k-loop
   // fp32 tower (f32 = 1): fp32 X0 row-major / MP32, fp32 dX0; widths padded to 16
   int f32 = 0;
   long long* stamps = nullptr;  // timing experiments only: per-wave s_memtime stamps (fp32 fwd)
@@ -649,8 +665,11 @@ void launch_tower_pack(const TowerArgs& a, const float* const* w, hipStream_t s)
 //  * packed W  [Np/16][Kp/16][64][4]: lane l, t = W[16nb + l%16][16kb + 4(l/16) + t]
 //  * packed Wt [Kp/16][Np/16][64][4]: lane l, t = W[16nb + 4(l/16) + t][16kb + l%16]
 constexpr int kTower32MaxWidth = 512;
+constexpr size_t kTower32LdsTotal = 160 * 1024;  // LDS per CU
+constexpr size_t kTower32BwdStatic = 8704;       // k_t32_bwd's static LDS (gs + csum), rounded up
 int tower32_lds_ld(int maxw);
 size_t tower32_lds_bytes(const TowerArgs& a);
+size_t tower32_lds_bytes_for(int lds_ld, bool part, int bias_floats);
 void launch_tower32_fwd(const TowerArgs& a, hipStream_t s);
 void launch_tower32_bwd(const TowerArgs& a, hipStream_t s);
 void launch_tower32_dw(const TowerArgs& a, hipStream_t s);

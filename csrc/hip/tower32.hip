@@ -42,110 +42,192 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// acc{0,1} += A{0,1}(16 rows x 16 KG, LDS) x B (packed fragments bfr[g * 64]).
-// A0/A1: this lane's row pointer (+4 * (lane / 16)); TWO = both 16-row halves.
-// Software pipeline, unrolled by 4 k-groups with NAMED registers: the weight
-// fragments b0..b3 are each re-loaded right after the MFMAs that consumed
-// them (4 groups = 32 MFMAs ahead) and the A fragments alternate between two
-// register sets, so nothing is copied between registers at the loop edge (a
-// rotated ring made hipcc move registers and drain vmcnt(0) every 4 groups).
-// Addressing is pointer increments only: the loads run up to 8 groups past
-// the end (the packed weights carry 8 KB of slack, the LDS tile 64 floats),
-// so the loop needs no clamping or index arithmetic -- the first version's
-// per-group scalar index math (~20 SALU between MFMA clusters) cost ~40% of
-// the MFMA rate (timing experiments, profiles/r3_tower32_notes.txt).
-template <bool TWO>
-__device__ __forceinline__ void mma32(const float* __restrict__ A0, const float* __restrict__ A1,
-                                      const f32x4* __restrict__ bp, int KG, f32x4& acc0, f32x4& acc1) {
+// The weight ring: kT32Ring k-groups of B fragments in flight per wave (one
+// dwordx4 per lane each), in named registers (an 8-deep ring, with segments
+// padded to 8, measured slower: 92.9 vs 87.9 us forward).
+struct Ring {
+  f32x4 b0, b1, b2, b3, b4, b5, b6, b7;
+};
+static_assert(kT32Ring == 4 || kT32Ring == 8, "t32_seg is written for a 4- or 8-slot ring");
+
+// acc{0,1} += A{0,1}(16 rows x 16 n k-groups, LDS) x B (the wave's weight
+// stream at bp): one segment of the wave's stream, led by p pad groups up to
+// a multiple of kT32Ring (tower32_sched.h).  Each ring slot is re-loaded
+// right after its 8 MFMAs with the k-group kT32Ring ahead IN THE STREAM --
+// across the segment's end into the next segment (next unit, or the
+// remainder range), so a unit starts with its first fragments in flight
+// instead of cold.  The pads keep every refill in stream order (slot 0
+// first): in-order vmcnt then covers exactly the oldest load, and no
+// register moves are needed (a rotating ring made hipcc copy registers and
+// drain vmcnt(0)).  A fragments are loaded one k-group ahead; sched_barriers
+// pin the order so hipcc keeps the loads in flight.
+// Timing experiment (TowerArgs.debug 64, its own instantiation XP = 64): no
+// weight loads in the loop (stale ring).
+template <int XP>
+__device__ __forceinline__ void t32_seg(Ring& rg, const f32x4*& bp, const float* A0, const float* A1, int n,
+                                        f32x4& acc0, f32x4& acc1) {
+  constexpr int R = kT32Ring;
   auto step = [&](const f32x4& a0, const f32x4& a1, const f32x4& b) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       acc0 = mfma4(a0[t], b[t], acc0);
-      if (TWO) acc1 = mfma4(a1[t], b[t], acc1);
+      acc1 = mfma4(a1[t], b[t], acc1);
     }
   };
-  auto lda = [](const float* p, int g) { return *reinterpret_cast<const f32x4*>(p + 16 * g); };
-  f32x4 b0 = bp[0], b1 = bp[64], b2 = bp[128], b3 = bp[192];
-  f32x4 e0 = lda(A0, 0), e1 = TWO ? lda(A1, 0) : e0;  // A of even groups
-  f32x4 o0, o1;                                       // A of odd groups
-  const int KM = KG & ~3;
-  for (int k = 0; k < KM; k += 4) {
-    o0 = lda(A0, 1);
-    if (TWO) o1 = lda(A1, 1);
+  constexpr bool noB = XP & 64;
+  auto lda = [](const float* p, int g, const f32x4&) { return *reinterpret_cast<const f32x4*>(p + 16 * g); };
+  // first block, always run (n >= 1): slots 0 .. p-1 hold pad groups, slots
+  // p .. R-1 the segment's first R - p groups; every slot is refilled in
+  // order (the refills stay on the straight path, only the MFMAs are
+  // conditional), so at least R loads follow whatever was issued before the
+  // segment (hipcc's vmcnt for the epilogue operands counts on it)
+  const int p = (R - (n & (R - 1))) & (R - 1);
+  f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = e0;  // A of even groups
+  f32x4 o0 = e0, o1 = e0;                    // A of odd groups
+  {
+    const float* a0p = A0 - 16 * p;
+    const float* a1p = A1 - 16 * p;
+#define T32_FIRST(S, B)                                       \
+  if (p <= S) {                                               \
+    e0 = lda(a0p, S, e0);                                     \
+    e1 = lda(a1p, S, e1);                                     \
+    step(e0, e1, B);                                          \
+  }                                                           \
+  __builtin_amdgcn_sched_barrier(0);                          \
+  if constexpr (!noB) B = bp[(R + S) * 64];                   \
+  __builtin_amdgcn_sched_barrier(0);
+    T32_FIRST(0, rg.b0)
+    T32_FIRST(1, rg.b1)
+    T32_FIRST(2, rg.b2)
+    if constexpr (R == 8) {
+      T32_FIRST(3, rg.b3)
+      T32_FIRST(4, rg.b4)
+      T32_FIRST(5, rg.b5)
+      T32_FIRST(6, rg.b6)
+      e0 = lda(a0p, 7, e0);
+      e1 = lda(a1p, 7, e1);
+      step(e0, e1, rg.b7);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!noB) rg.b7 = bp[(R + 7) * 64];
+    } else {
+      e0 = lda(a0p, 3, e0);
+      e1 = lda(a1p, 3, e1);
+      step(e0, e1, rg.b3);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!noB) rg.b3 = bp[(R + 3) * 64];
+    }
     __builtin_amdgcn_sched_barrier(0);
-    step(e0, e1, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    b0 = bp[256];
-    e0 = lda(A0, 2);
-    if (TWO) e1 = lda(A1, 2);
-    __builtin_amdgcn_sched_barrier(0);
-    step(o0, o1, b1);
-    __builtin_amdgcn_sched_barrier(0);
-    b1 = bp[320];
-    o0 = lda(A0, 3);
-    if (TWO) o1 = lda(A1, 3);
-    __builtin_amdgcn_sched_barrier(0);
-    step(e0, e1, b2);
-    __builtin_amdgcn_sched_barrier(0);
-    b2 = bp[384];
-    e0 = lda(A0, 4);
-    if (TWO) e1 = lda(A1, 4);
-    __builtin_amdgcn_sched_barrier(0);
-    step(o0, o1, b3);
-    __builtin_amdgcn_sched_barrier(0);
-    b3 = bp[448];
-    bp += 256;
-    A0 += 64;
-    if (TWO) A1 += 64;
+#undef T32_FIRST
+    bp += R * 64;
+    A0 += 16 * (R - p);
+    A1 += 16 * (R - p);
   }
-  // tail: KG % 4 groups, their fragments already loaded (b0.., e)
-  const int rem = KG - KM;
-  if (rem > 0) {
-    o0 = lda(A0, 1);
-    if (TWO) o1 = lda(A1, 1);
-    step(e0, e1, b0);
+  const int nb = (n - (R - p)) / R;  // whole blocks left
+  e0 = lda(A0, 0, e0);
+  e1 = lda(A1, 0, e1);
+#define T32_SLOT(S, B, CUR0, CUR1, NXT0, NXT1) \
+  NXT0 = lda(A0, S + 1, NXT0);                 \
+  NXT1 = lda(A1, S + 1, NXT1);                 \
+  __builtin_amdgcn_sched_barrier(0);           \
+  step(CUR0, CUR1, B);                         \
+  __builtin_amdgcn_sched_barrier(0);           \
+  if constexpr (!noB) B = bp[(R + S) * 64];
+  for (int k = 0; k < nb; ++k) {
+    T32_SLOT(0, rg.b0, e0, e1, o0, o1)
+    T32_SLOT(1, rg.b1, o0, o1, e0, e1)
+    T32_SLOT(2, rg.b2, e0, e1, o0, o1)
+    T32_SLOT(3, rg.b3, o0, o1, e0, e1)
+    if constexpr (R == 8) {
+      T32_SLOT(4, rg.b4, e0, e1, o0, o1)
+      T32_SLOT(5, rg.b5, o0, o1, e0, e1)
+      T32_SLOT(6, rg.b6, e0, e1, o0, o1)
+      T32_SLOT(7, rg.b7, o0, o1, e0, e1)
+    }
+    bp += R * 64;
+    A0 += 16 * R;
+    A1 += 16 * R;
   }
-  if (rem > 1) {
-    e0 = lda(A0, 2);
-    if (TWO) e1 = lda(A1, 2);
-    step(o0, o1, b1);
-  }
-  if (rem > 2) step(e0, e1, b2);
+#undef T32_SLOT
 }
 
-// Work split of one layer over the 8 waves: NB column blocks, each a "pair"
-// unit (both 16-row halves, sharing every weight fragment).  Full rounds go
-// pair-wise; the remainder is dealt as single (block, half) items so that the
-// 4 SIMDs (waves w and w + 4 share one) end within one item of each other.
-template <typename F>
-__device__ __forceinline__ void for_units(int NB, int w, F&& f) {
-  const int q = NB / NW, r = NB % NW;
-  for (int i = 0; i < q; ++i) f(w + NW * i, -1);
-  for (int j = w; j < 2 * r; j += NW) f(NW * q + (j >> 1), j & 1);
-}
+// LDS scratch of the remainder partial sums: [8 waves][2 segments][2 halves][64 lanes][4]
+constexpr int kPartFloats = 8 * 2 * 2 * 256;
 
-// One unit: the epilogue's own global operands (bias, ReLU mask) are fetched
-// by pre(nb, half) BEFORE the MFMA chain, so their latency hides under it
-// instead of stalling the epilogue of both waves of a SIMD at once.
-template <typename Pre, typename Epi>
-__device__ __forceinline__ void run_unit(const float* src, int ldl, const f32x4* wbase, int KG, int nb, int half,
-                                         int lane, Pre&& pre, Epi&& epi) {
+// Workgroup barrier for LDS only: the global stores / loads in flight (MP32
+// copies, the next unit's weight fragments) are NOT drained (a
+// __syncthreads() fence would wait vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// One layer of the wave-stream schedule (tower_common.h): this wave's full
+// units (epi(acc, col, half, pre) after each; pre(col, half) is fetched before
+// its MFMA chain so the load hides under it), then its remainder range, whose
+// K-partial sums go to LDS.  t32_layer_rem (after an LDS barrier) reduces the
+// remainder blocks in wave order -- deterministic -- and applies epi.
+template <int XP, typename Pre, typename Epi>
+__device__ __forceinline__ void t32_layer(const float* src, int ldl, const f32x4* wl, int ncol, int ng, int w,
+                                          int lane, float* part, Pre&& pre, Epi&& epi) {
   const int c = lane & 15, g = lane >> 4;
-  const f32x4* bfr = wbase + (int64_t)nb * KG * 64 + lane;
-  f32x4 acc0 = (f32x4){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-  if (half < 0) {
-    const f32x4 p0 = pre(nb, 0), p1 = pre(nb, 1);
-    mma32<true>(src + c * ldl + 4 * g, src + (16 + c) * ldl + 4 * g, bfr, KG, acc0, acc1);
-    epi(acc0, nb, 0, p0);
-    epi(acc1, nb, 1, p1);
-  } else {
-    const f32x4 p0 = pre(nb, half);
-    const float* A = src + (16 * half + c) * ldl + 4 * g;
-    mma32<false>(A, A, bfr, KG, acc0, acc1);
-    epi(acc0, nb, half, p0);
+  const T32Sched s = t32_sched(ncol, ng);
+  const f32x4* bp = wl + t32_wave_off(s, ng, w) * 64 + lane;
+  Ring rg;
+  rg.b0 = bp[0];
+  rg.b1 = bp[64];
+  rg.b2 = bp[128];
+  rg.b3 = bp[192];
+  if constexpr (kT32Ring == 8) {
+    rg.b4 = bp[256];
+    rg.b5 = bp[320];
+    rg.b6 = bp[384];
+    rg.b7 = bp[448];
+  }
+  const float* A0 = src + c * ldl + 4 * g;
+  const float* A1 = A0 + 16 * ldl;
+  for (int i = 0; i < s.q; ++i) {
+    const int col = 8 * i + w;
+    const f32x4 p0 = pre(col, 0), p1 = pre(col, 1);
+    __builtin_amdgcn_sched_barrier(0);  // issue the epilogue operands before the chain
+    f32x4 acc0 = (f32x4){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    t32_seg<XP>(rg, bp, A0, A1, ng, acc0, acc1);
+    epi(acc0, col, 0, p0);
+    epi(acc1, col, 1, p1);
+  }
+  if (s.R == 0) return;
+  const int lo = t32_rem_lo(s, w), hi = t32_rem_lo(s, w + 1);
+  int seg = 0;
+  for (int f = lo; f < hi; ++seg) {
+    const int j = f / ng, g0 = f - j * ng;
+    const int len = min(ng - g0, hi - f);
+    f32x4 acc0 = (f32x4){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    t32_seg<XP>(rg, bp, A0 + 16 * g0, A1 + 16 * g0, len, acc0, acc1);
+    float* sl = part + ((w * 2 + seg) * 2) * 256 + lane * 4;
+    *reinterpret_cast<f32x4*>(sl) = acc0;
+    *reinterpret_cast<f32x4*>(sl + 256) = acc1;
+    f += len;
   }
 }
 
+template <typename Pre, typename Epi>
+__device__ __forceinline__ void t32_layer_rem(int ncol, int ng, int w, int lane, const float* part, Pre&& pre,
+                                              Epi&& epi) {
+  const T32Sched s = t32_sched(ncol, ng);
+  if (w >= s.R) return;
+  const int j = w, col = 8 * s.q + j;
+  const f32x4 p0 = pre(col, 0), p1 = pre(col, 1);
+  const int wa = t32_rem_wave(s, j * ng), wb = t32_rem_wave(s, (j + 1) * ng - 1);
+  f32x4 s0 = (f32x4){0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  for (int ww = wa; ww <= wb; ++ww) {
+    const int lo = t32_rem_lo(s, ww);
+    if (lo == t32_rem_lo(s, ww + 1)) continue;  // empty range
+    const int seg = j - lo / ng;
+    const float* sl = part + ((ww * 2 + seg) * 2) * 256 + lane * 4;
+    s0 += *reinterpret_cast<const f32x4*>(sl);
+    s1 += *reinterpret_cast<const f32x4*>(sl + 256);
+  }
+  epi(s0, col, 0, p0);
+  epi(s1, col, 1, p1);
+}
+
+template <int XP>
 __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds32[];
   const int ldl = a.lds_ld;
@@ -155,7 +237,7 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
   float* dst = lds32 + BM * ldl;
   // waves 4-7 share SIMDs with 0-3 and lose every arbitration at equal
   // priority (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+  if (w >= 4 && !(a.debug & 32)) __builtin_amdgcn_s_setprio(1);
   long long* stp = a.stamps ? a.stamps + ((int64_t)blockIdx.x * NW + w) * 8 : nullptr;
   if (stp && lane == 0) stp[0] = __builtin_amdgcn_s_memtime();
   // loss-tail inputs and the output-layer weights, loaded ahead of the layers
@@ -176,30 +258,41 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
     }
   }
   __syncthreads();
+  float* part = lds32 + 2 * BM * ldl + 64;  // remainder partial sums
+  // every layer's bias in LDS (at its bias_off): the epilogues then depend
+  // on no global load, so hipcc has no reason to drain the weight ring
+  float* sbias = part + (a.t32_part ? kPartFloats : 0);
+  for (int l = 0; l < a.L; ++l) {
+    const TowerLayerDev& ly = a.ly[l];
+    for (int n = tid; n < ly.Np; n += NT) sbias[ly.bias_off + n] = n < ly.N ? ly.bias[n] : 0.f;
+  }
+  __syncthreads();
   for (int l = 0; l < a.L; ++l) {
     const TowerLayerDev& ly = a.ly[l];
     const int NB = ly.Np / 16, KG = ly.Kp / 16;
     const f32x4* wp = reinterpret_cast<const f32x4*>(ly.wpf);
     const int c = lane & 15, g = lane >> 4;
-    for_units(NB, w, [&](int nb, int half) {
-      run_unit(src, ldl, wp, KG, nb, half, lane, [&](int nbb, int) {
-        const int n = nbb * 16 + c;
-        return (f32x4){n < ly.N ? ly.bias[n] : 0.f, 0.f, 0.f, 0.f};
-      }, [&](const f32x4& acc, int nbb, int mb, const f32x4& pb) {
-        const int n = nbb * 16 + c;
-        const float bias = pb[0];
-        f32x4 o;
+    const float* lb = sbias + ly.bias_off;
+    auto pre = [&](int nbb, int) { return (f32x4){lb[nbb * 16 + c], 0.f, 0.f, 0.f}; };
+    auto epi = [&](const f32x4& acc, int nbb, int mb, const f32x4& pb) {
+      const int n = nbb * 16 + c;
+      const float bias = pb[0];
+      f32x4 o;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const float v = acc[t] + bias;
-          o[t] = v > 0.f ? v : 0.f;
-          dst[(16 * mb + 4 * g + t) * ldl + n] = o[t];
-        }
-        *reinterpret_cast<f32x4*>(ly.xmpf + mp32(m0 / 16 + mb, NB, nbb) + lane * 4) = o;
-      });
-    });
+      for (int t = 0; t < 4; ++t) {
+        const float v = acc[t] + bias;
+        o[t] = v > 0.f ? v : 0.f;
+        dst[(16 * mb + 4 * g + t) * ldl + n] = o[t];
+      }
+      *reinterpret_cast<f32x4*>(ly.xmpf + mp32(m0 / 16 + mb, NB, nbb) + lane * 4) = o;
+    };
+    t32_layer<XP>(src, ldl, wp, NB, KG, w, lane, part, pre, epi);
     if (stp && lane == 0) stp[1 + 2 * l] = __builtin_amdgcn_s_memtime();
-    __syncthreads();
+    lds_barrier();
+    if (NB % 8) {
+      t32_layer_rem(NB, KG, w, lane, part, pre, epi);
+      lds_barrier();
+    }
     if (stp && lane == 0) stp[2 + 2 * l] = __builtin_amdgcn_s_memtime();
     float* t = src;
     src = dst;
@@ -241,6 +334,7 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
   tower_loss_tail(a, zrow, rin, m0, w, lane, BM);
 }
 
+template <int XP>
 __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds32[];
   __shared__ float gs[BM];
@@ -254,7 +348,8 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
   float* src = lds32;
   float* dst = lds32 + BM * ldl;
   float* bp = a.bias_part + (int64_t)blockIdx.x * a.bias_ld;
-  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+  float* part = lds32 + 2 * BM * ldl + 64;  // remainder partial sums
+  if (w >= 4 && !(a.debug & 32)) __builtin_amdgcn_s_setprio(1);
   const float gl = a.dloss ? a.dloss[0] : 1.f;
   if (tid < BM) gs[tid] = (m0 + tid < a.M) ? a.dz[m0 + tid] * gl : 0.f;
   __syncthreads();
@@ -315,38 +410,43 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
     if (i > 0) {
       const TowerLayerDev& prev = a.ly[i - 1];
       const int PNB = prev.Np / 16;
-      for_units(KB, w, [&](int kb, int half) {
-        run_unit(src, ldl, wtp, NG, kb, half, lane, [&](int kbb, int mb) {
-          return *reinterpret_cast<const f32x4*>(prev.xmpf + mp32(m0 / 16 + mb, PNB, kbb) + lane * 4);
-        }, [&](const f32x4& acc, int kbb, int mb, const f32x4& x4) {
-          const int64_t off = mp32(m0 / 16 + mb, PNB, kbb) + lane * 4;
-          f32x4 o;
-          float s = 0.f;
+      auto pre = [&](int kbb, int mb) {
+        return *reinterpret_cast<const f32x4*>(prev.xmpf + mp32(m0 / 16 + mb, PNB, kbb) + lane * 4);
+      };
+      auto epi = [&](const f32x4& acc, int kbb, int mb, const f32x4& x4) {
+        const int64_t off = mp32(m0 / 16 + mb, PNB, kbb) + lane * 4;
+        f32x4 o;
+        float s = 0.f;
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            o[t] = x4[t] > 0.f ? acc[t] : 0.f;
-            s += o[t];
-            dst[(16 * mb + 4 * g + t) * ldl + kbb * 16 + c] = o[t];
-          }
-          *reinterpret_cast<f32x4*>(prev.dzmpf + off) = o;
-          s += __shfl_xor(s, 16);
-          s += __shfl_xor(s, 32);
-          if (g == 0) cs[mb][kbb * 16 + c] = s;
-        });
-      });
-    } else {
-      for_units(KB, w, [&](int kb, int half) {
-        run_unit(src, ldl, wtp, NG, kb, half, lane, [&](int, int) { return (f32x4){0.f, 0.f, 0.f, 0.f}; },
-                 [&](const f32x4& acc, int kbb, int mb, const f32x4&) {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) dst[(16 * mb + 4 * g + t) * ldl + kbb * 16 + c] = acc[t];
-        });
-      });
-    }
-    __syncthreads();
-    if (i > 0) {
-      const TowerLayerDev& prev = a.ly[i - 1];
+        for (int t = 0; t < 4; ++t) {
+          o[t] = x4[t] > 0.f ? acc[t] : 0.f;
+          s += o[t];
+          dst[(16 * mb + 4 * g + t) * ldl + kbb * 16 + c] = o[t];
+        }
+        *reinterpret_cast<f32x4*>(prev.dzmpf + off) = o;
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        if (g == 0) cs[mb][kbb * 16 + c] = s;
+      };
+      t32_layer<XP>(src, ldl, wtp, KB, NG, w, lane, part, pre, epi);
+      lds_barrier();
+      if (KB % 8) {
+        t32_layer_rem(KB, NG, w, lane, part, pre, epi);
+        lds_barrier();
+      }
       for (int col = tid; col < prev.Np; col += NT) bp[prev.bias_off + col] = cs[0][col] + cs[1][col];
+    } else {
+      auto pre = [&](int, int) { return (f32x4){0.f, 0.f, 0.f, 0.f}; };
+      auto epi = [&](const f32x4& acc, int kbb, int mb, const f32x4&) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) dst[(16 * mb + 4 * g + t) * ldl + kbb * 16 + c] = acc[t];
+      };
+      t32_layer<XP>(src, ldl, wtp, KB, NG, w, lane, part, pre, epi);
+      lds_barrier();
+      if (KB % 8) {
+        t32_layer_rem(KB, NG, w, lane, part, pre, epi);
+        lds_barrier();
+      }
     }
     float* t = src;
     src = dst;
@@ -504,8 +604,8 @@ __global__ void k_t32_pack(TowerArgs a, Pack32Job j) {
   const int64_t i = e - j.off[l];
   const int n = (int)(i / ly.K), k = (int)(i % ly.K);
   const float v = j.w[l][i];
-  const_cast<float*>(ly.wpf)[tower_wp32_index(n, k, ly.Kp)] = v;
-  const_cast<float*>(ly.wtpf)[tower_wtp32_index(n, k, ly.Np)] = v;
+  const_cast<float*>(ly.wpf)[tower_wp32_index(n, k, ly.Np, ly.Kp)] = v;
+  const_cast<float*>(ly.wtpf)[tower_wtp32_index(n, k, ly.Np, ly.Kp)] = v;
 }
 
 }  // namespace
@@ -541,17 +641,37 @@ int tower32_lds_ld(int maxw) {
   return (maxw + 3) / 4 * 4;
 }
 
-// + 64 floats: the A-operand loads run up to 4 k-groups past a row's end
-size_t tower32_lds_bytes(const TowerArgs& a) { return ((size_t)2 * BM * a.lds_ld + 64) * sizeof(float); }
+// + 64 floats: the A-operand loads run one k-group past a row's end; then the
+// remainder partial sums of the wave-stream schedule when a layer has column
+// blocks past a multiple of 8 (fwd: Np / 16, bwd: Kp / 16)
+bool tower32_needs_part(const TowerArgs& a) {
+  for (int l = 0; l < a.L; ++l)
+    if ((a.ly[l].Np / 16) % 8 || (a.ly[l].Kp / 16) % 8) return true;
+  return false;
+}
+size_t tower32_lds_bytes_for(int lds_ld, bool part, int bias_floats) {
+  return ((size_t)2 * BM * lds_ld + 64 + (part ? kPartFloats : 0) + bias_floats) * sizeof(float);
+}
+// forward: + the layers' biases
+static size_t fwd_lds_bytes(const TowerArgs& a) {
+  return tower32_lds_bytes_for(a.lds_ld, a.t32_part != 0, a.ly[a.L - 1].bias_off + a.ly[a.L - 1].Np);
+}
+size_t tower32_lds_bytes(const TowerArgs& a) { return tower32_lds_bytes_for(a.lds_ld, tower32_needs_part(a), 0); }
 
+template <int XP>
+static void allow_big_lds32_xp() {
+  // 160 KB per CU minus each kernel's static LDS (zrow; gs + csum)
+  if (hipFuncSetAttribute((const void*)k_t32_fwd<XP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          kTower32LdsTotal - 512) != hipSuccess)
+    (void)hipGetLastError();
+  if (hipFuncSetAttribute((const void*)k_t32_bwd<XP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          kTower32LdsTotal - kTower32BwdStatic) != hipSuccess)
+    (void)hipGetLastError();
+}
 static void allow_big_lds32() {
   static const bool once = [] {
-    if (hipFuncSetAttribute((const void*)k_t32_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) !=
-        hipSuccess)
-      (void)hipGetLastError();
-    if (hipFuncSetAttribute((const void*)k_t32_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 140 * 1024) !=
-        hipSuccess)
-      (void)hipGetLastError();
+    allow_big_lds32_xp<0>();
+    allow_big_lds32_xp<64>();
     return true;
   }();
   (void)once;
@@ -560,13 +680,20 @@ static void allow_big_lds32() {
 void launch_tower32_fwd(const TowerArgs& a, hipStream_t s) {
   if (a.M == 0) return;
   allow_big_lds32();
-  hipLaunchKernelGGL(k_t32_fwd, dim3(a.Mp / BM), dim3(NT), tower32_lds_bytes(a), s, a);
+  TowerArgs b = a;
+  b.t32_part = tower32_needs_part(a) ? 1 : 0;
+  // timing experiments (TowerArgs.debug 64 / 128) run their own instantiations
+  if (a.debug & 64) hipLaunchKernelGGL(k_t32_fwd<64>, dim3(a.Mp / BM), dim3(NT), fwd_lds_bytes(b), s, b);
+  else hipLaunchKernelGGL(k_t32_fwd<0>, dim3(a.Mp / BM), dim3(NT), fwd_lds_bytes(b), s, b);
 }
 
 void launch_tower32_bwd(const TowerArgs& a, hipStream_t s) {
   if (a.M == 0) return;
   allow_big_lds32();
-  hipLaunchKernelGGL(k_t32_bwd, dim3(a.Mp / BM), dim3(NT), tower32_lds_bytes(a), s, a);
+  TowerArgs b = a;
+  b.t32_part = tower32_needs_part(a) ? 1 : 0;
+  if (a.debug & 64) hipLaunchKernelGGL(k_t32_bwd<64>, dim3(a.Mp / BM), dim3(NT), tower32_lds_bytes(b), s, b);
+  else hipLaunchKernelGGL(k_t32_bwd<0>, dim3(a.Mp / BM), dim3(NT), tower32_lds_bytes(b), s, b);
 }
 
 void launch_tower32_dw(const TowerArgs& a, hipStream_t s) {

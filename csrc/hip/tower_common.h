@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
+#include "tower32_sched.h"
 
 namespace pbx {
 
@@ -202,13 +203,15 @@ __device__ __forceinline__ unsigned tower_lds_addr(const void* p) {
   return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
 }
 
-// fp32 tower packed-weight index maps (kernels.h layout comment): element
-// W[n][k] in packed W (forward B operand) and packed W^T (backward B operand)
-__device__ __forceinline__ int64_t tower_wp32_index(int n, int k, int Kp) {
-  return ((int64_t)((n >> 4) * (Kp >> 4) + (k >> 4)) * 64 + (n & 15) + 16 * ((k & 15) >> 2)) * 4 + (k & 3);
+// fp32 tower wave-stream schedule: tower32_sched.h
+// element W[n][k] in packed W (forward B operand: column block n / 16,
+// k-group k / 16; lane (n % 16) + 16 ((k % 16) / 4), component k % 4) and in
+// packed W^T (backward B operand: column block k / 16, k-group n / 16)
+__device__ __forceinline__ int64_t tower_wp32_index(int n, int k, int Np, int Kp) {
+  return (t32_group_pos(Np >> 4, Kp >> 4, n >> 4, k >> 4) * 64 + (n & 15) + 16 * ((k & 15) >> 2)) * 4 + (k & 3);
 }
-__device__ __forceinline__ int64_t tower_wtp32_index(int n, int k, int Np) {
-  return ((int64_t)((k >> 4) * (Np >> 4) + (n >> 4)) * 64 + (k & 15) + 16 * ((n & 15) >> 2)) * 4 + (n & 3);
+__device__ __forceinline__ int64_t tower_wtp32_index(int n, int k, int Np, int Kp) {
+  return (t32_group_pos(Kp >> 4, Np >> 4, k >> 4, n >> 4) * 64 + (k & 15) + 16 * ((n & 15) >> 2)) * 4 + (n & 3);
 }
 
 }  // namespace pbx

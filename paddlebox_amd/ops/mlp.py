@@ -162,8 +162,13 @@ class FusedMLP(nn.Module):
         return self._tw
 
     def tower_fp32_ok(self) -> bool:
-        """The fp32 tower keeps two 32-row fp32 tiles in LDS: widths <= 512."""
-        return max([self.in_dim] + list(self.hidden)) <= 512
+        """The fp32 tower keeps two 32-row fp32 tiles in LDS, plus the
+        remainder partial sums of its wave-stream schedule when a width is not
+        a multiple of 128: widths <= 464, or <= 512 when all are multiples of
+        128 (bindings_tower.cpp checks the exact budget)."""
+        ws = [self.in_dim] + list(self.hidden)
+        p16 = [(w + 15) // 16 * 16 for w in ws]
+        return max(ws) <= 464 or (max(ws) <= 512 and all(p % 128 == 0 for p in p16))
 
     def ensure_packed(self):
         if not self._packed or not self.packed_by_optimizer:

@@ -24,6 +24,7 @@ import threading
 import time
 from typing import Dict, List, Optional, Sequence
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -365,7 +366,7 @@ class BoxWrapper:
     def save_base(self, batch_model_path: str, xbox_model_path: str, date: str = "") -> str:
         """Full batch model + xbox base (box_wrapper.cc:1286-1305)."""
         t = self._authoritative()
-        n = ckpt.save_batch_model(t, batch_model_path, self.rank, date)
+        n = ckpt.save_batch_model(t, batch_model_path, self.rank, date, world=self.world)
         sg = self.cfg.sgd
         x = ckpt.save_xbox(t, xbox_model_path, "base", self.cfg.save, sg.nonclk_coeff, sg.clk_coeff, self.rank,
                            on_reset=self._reset_delta_live)
@@ -384,28 +385,76 @@ class BoxWrapper:
         return f"{xbox_model_path} xbox_delta={x}"
 
     def load_model(self, model_path: str, merge: bool = False, update_type: str = "add", model_index: int = 0):
-        """Load a batch model (all parts); rows are routed to their owners.
+        """Load a batch model, streamed: parts are memory-mapped and walked in
+        chunks (ckpt.LOAD_CHUNK_ROWS), so host RAM stays at ~2 chunks per rank
+        whatever the model size (reference: the PS loads model_path per node,
+        box_wrapper.cc:1201-1242).
+        * one rank: every part, chunk by chunk;
+        * parts written by a job of this world size (meta "world"): each rank
+          reads only its own part -- it holds exactly the keys the rank owns;
+        * otherwise each rank reads parts rank, rank + W, ... and routes the
+          rows of every chunk to their owners with one bounded all-to-all per
+          round (chunk / W rows per rank per round).
         ``merge`` combines the model with the rows already in the table
-        (``_merge_rows``, by ``update_type``); otherwise rows are replaced."""
-        keys, vals = ckpt.load_batch_model_parts(model_path)
-        if keys.size == 0:
+        (``_merge_rows``, by ``update_type``); otherwise rows are replaced.
+        Returns the number of rows this rank loaded."""
+        meta = ckpt.read_meta(model_path)
+        parts = ckpt.list_parts(model_path)
+        if not parts:
             return 0
-        k = torch.from_numpy(keys.view("int64").copy())
-        v = torch.from_numpy(vals)
-        h = ref.mix64(k)
-        if self.world > 1:
-            mine = ref.owner_of(h, self.world) == self.rank
-            h, v = h[mine], v[mine]
         t = self._authoritative()
         dev = getattr(t, "device", torch.device("cpu"))
-        h, v = h.to(dev), v.to(dev).float()
-        if merge and update_type != "replace":
-            found = t.probe(h) >= 0
-            cur = t.read(h).to(dev).float()
-            v = self._merge_rows(cur, v, found, update_type, int(model_index))
-        t.insert_mixed(h, self.cfg.sgd)
-        t.assign(h, v)
-        return int(h.numel())
+        chunk = max(1, int(ckpt.LOAD_CHUNK_ROWS))
+        loaded = 0
+
+        def apply(h: torch.Tensor, v: torch.Tensor) -> int:
+            if h.numel() == 0:
+                return 0
+            h, v = h.to(dev), v.to(dev).float()
+            if merge and update_type != "replace":
+                found = t.probe(h) >= 0
+                cur = t.read(h).to(dev).float()
+                v = self._merge_rows(cur, v, found, update_type, int(model_index))
+            t.insert_mixed(h, self.cfg.sgd)
+            t.assign(h, v)
+            return int(h.numel())
+
+        def mixed(keys: np.ndarray) -> torch.Tensor:
+            return ref.mix64(torch.from_numpy(keys.view("int64").copy()))
+
+        if self.world == 1 or int(meta.get("world", -1)) == self.world:
+            mine = parts if self.world == 1 else [p for p in parts if p == self.rank]
+            for p in mine:
+                for k, v in ckpt.iter_part_chunks(model_path, p, chunk):
+                    loaded += apply(mixed(k), torch.from_numpy(v))
+            return loaded
+        # route rows to owners: rounds of chunk / W rows per rank
+        W, me = self.world, self.rank
+        per = max(1, chunk // W)
+        my_parts = parts[me::W]
+        gdev = self.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        n_rounds = sum((ckpt.part_rows(model_path, p) + per - 1) // per for p in my_parts)
+        nr = torch.tensor([n_rounds], dtype=torch.int64, device=gdev)
+        dist.all_reduce(nr, op=dist.ReduceOp.MAX, group=self.group)
+        stride = int(meta.get("stride") or np.load(os.path.join(model_path, f"part-{parts[0]:05d}.vals.npy"),
+                                                   mmap_mode="r", allow_pickle=False).shape[1])
+        src = (c for p in my_parts for c in ckpt.iter_part_chunks(model_path, p, per))
+        for _ in range(int(nr.item())):
+            k, v = next(src, (np.zeros(0, np.uint64), np.zeros((0, stride), np.float32)))
+            h, vt = mixed(k), torch.from_numpy(v).reshape(-1, stride)
+            owner = ref.owner_of(h, W)
+            order = torch.argsort(owner, stable=True)
+            h, vt = h[order], vt[order]
+            counts = torch.bincount(owner, minlength=W)
+            rcd = torch.empty(W, dtype=torch.int64, device=gdev)
+            dist.all_to_all_single(rcd, counts.to(gdev), group=self.group)
+            sc, rcl = counts.tolist(), rcd.cpu().tolist()
+            hk = torch.empty(int(sum(rcl)), dtype=torch.int64, device=gdev)
+            dist.all_to_all_single(hk, h.to(gdev), rcl, sc, group=self.group)
+            rv = torch.empty(int(sum(rcl)), stride, dtype=torch.float32, device=gdev)
+            dist.all_to_all_single(rv, vt.to(gdev), rcl, sc, group=self.group)
+            loaded += apply(hk, rv)
+        return loaded
 
     def _merge_rows(self, cur: torch.Tensor, inc: torch.Tensor, found: torch.Tensor, update_type: str,
                     model_index: int) -> torch.Tensor:

@@ -18,10 +18,12 @@ semantics reproduced here are the PSCore CTR accessor's
 Layout: ``<path>/part-<rank>.keys.npy``, ``.vals.npy``, ``meta.json``;
 xbox ``<path>/part-<rank>.txt``.
 
-GPU tables (plain layout) are written by the native streaming saver
-(``GpuTable.save_stream``: chunked device compaction -> pinned ring -> writer
-threads, bounded HBM); CPU tables, codec layouts and PBX_SAVE_STREAM=0 use the
-export-based writer below.  Both produce the same files.
+GPU tables are written by the native streaming saver (``GpuTable.save_stream``:
+chunked device compaction -> pinned ring -> writer threads, bounded HBM);
+feature-type codec tables (int16 / variable / SparseAdam) are decoded to their
+canonical fp32 rows on the device in the same pass.  CPU tables and
+PBX_SAVE_STREAM=0 use the export-based writer below.  Both produce the same
+files.
 """
 from __future__ import annotations
 
@@ -66,36 +68,54 @@ last_save_stats: dict = {}
 
 def _streamable(table) -> bool:
     t = getattr(table, "t", None)
-    return (t is not None and hasattr(t, "save_stream") and getattr(table, "codec", None) is None
-            and os.environ.get("PBX_SAVE_STREAM", "1") != "0")
+    return t is not None and hasattr(t, "save_stream") and os.environ.get("PBX_SAVE_STREAM", "1") != "0"
+
+
+def _decode_args(table):
+    """(column map, scale, embedding width) of a codec table's canonical rows;
+    an empty map = rows as stored."""
+    c = getattr(table, "codec", None)
+    if c is None:
+        return [], 1.0, 0
+    return c.save_map(), float(c.qscale), int(c.DX)
+
+
+def _out_stride(table) -> int:
+    c = getattr(table, "codec", None)
+    return int(c.canon_width) if c is not None else int(table.t.stride)
 
 
 def _stream(table, kind: int, mode: int, reset: bool, cfg: Optional[SaveConfig], nonclk: float, clk: float,
             keys_path: str, vals_path: str = "", collect: bool = False):
     cfg = cfg or SaveConfig()
+    dmap, dscale, ddim = _decode_args(table)
     with torch.cuda.device(table.device):
         rows, chunks, gpu_s, write_s, total_s, keys = table.t.save_stream(
             kind, mode, reset, float(cfg.base_threshold), float(cfg.delta_threshold), float(cfg.delta_keep_days),
             float(nonclk), float(clk), float(cfg.embedx_threshold), keys_path, vals_path, STREAM_CHUNK_ROWS,
-            STREAM_THREADS, collect)
+            STREAM_THREADS, collect, dmap, dscale, ddim)
     last_save_stats.clear()
     last_save_stats.update(rows=rows, chunks=chunks, gpu_s=gpu_s, write_s=write_s, total_s=total_s, native=True)
     return int(rows), keys
 
 
-def _write_meta(path: str, dim: int, stride: int, date):
+def _write_meta(path: str, dim: int, stride: int, date, world: Optional[int] = None):
     meta = {"format": FORMAT, "dim": dim, "stride": stride, "layout": row_layout(dim), "date": date}
+    if world is not None:
+        # parts written by `world` owner-sharded ranks: part r holds exactly the
+        # keys that rank r of a same-sized job owns (load fast path)
+        meta["world"] = int(world)
     with open(os.path.join(path, "meta.json"), "w") as f:
         json.dump(meta, f)
 
 
-def save_batch_model(table, path: str, rank: int = 0, date: Optional[str] = None) -> int:
+def save_batch_model(table, path: str, rank: int = 0, date: Optional[str] = None, world: Optional[int] = None) -> int:
     os.makedirs(path, exist_ok=True)
     if _streamable(table):
         n, _ = _stream(table, 0, 0, False, None, 0.0, 0.0, os.path.join(path, f"part-{rank:05d}.keys.npy"),
                        os.path.join(path, f"part-{rank:05d}.vals.npy"))
         if rank == 0:
-            _write_meta(path, table.dim, int(table.t.stride), date)
+            _write_meta(path, table.dim, _out_stride(table), date, world)
         return n
     h, v = table.export(True)
     keys = ref.unmix64(h.cpu()).numpy().view(np.uint64)
@@ -103,7 +123,7 @@ def save_batch_model(table, path: str, rank: int = 0, date: Optional[str] = None
     np.save(os.path.join(path, f"part-{rank:05d}.keys.npy"), keys, allow_pickle=False)
     np.save(os.path.join(path, f"part-{rank:05d}.vals.npy"), vals, allow_pickle=False)
     if rank == 0:
-        _write_meta(path, table.dim, int(vals.shape[1]) if vals.ndim == 2 else 0, date)
+        _write_meta(path, table.dim, int(vals.shape[1]) if vals.ndim == 2 else 0, date, world)
     return int(keys.shape[0])
 
 
@@ -121,6 +141,40 @@ def load_batch_model_parts(path: str, rank: Optional[int] = None) -> Tuple[np.nd
     return np.concatenate(ks), np.concatenate(vs)
 
 
+# Streaming load: parts are memory-mapped and walked in chunks of this many
+# rows, so a rank's host RAM for a load stays at ~2 chunks whatever the model
+# size (a 1e9-row model is ~90 GB of parts).
+LOAD_CHUNK_ROWS = int(os.environ.get("PBX_LOAD_CHUNK_ROWS", str(1 << 22)))
+
+
+def read_meta(path: str) -> dict:
+    fn = os.path.join(path, "meta.json")
+    if not os.path.exists(fn):
+        return {}
+    with open(fn) as f:
+        return json.load(f)
+
+
+def list_parts(path: str):
+    """Part ids of a batch model directory, ascending."""
+    return sorted(int(f[5:10]) for f in os.listdir(path) if f.startswith("part-") and f.endswith(".keys.npy"))
+
+
+def part_rows(path: str, part: int) -> int:
+    return int(np.load(os.path.join(path, f"part-{part:05d}.keys.npy"), mmap_mode="r", allow_pickle=False).shape[0])
+
+
+def iter_part_chunks(path: str, part: int, chunk_rows: int):
+    """(feasigns uint64 [n], rows f32 [n, stride]) chunks of one part, read
+    through read-only memory maps (allow_pickle=False): only the chunk being
+    yielded is resident."""
+    k = np.load(os.path.join(path, f"part-{part:05d}.keys.npy"), mmap_mode="r", allow_pickle=False)
+    v = np.load(os.path.join(path, f"part-{part:05d}.vals.npy"), mmap_mode="r", allow_pickle=False)
+    for a in range(0, k.shape[0], max(1, int(chunk_rows))):
+        b = min(k.shape[0], a + int(chunk_rows))
+        yield np.array(k[a:b]), np.array(v[a:b], dtype=np.float32)
+
+
 def save_xbox(table, path: str, mode: str, cfg: SaveConfig, nonclk: float, clk: float, rank: int = 0,
               on_reset=None) -> int:
     """Write the xbox text model ('base' or 'delta'); resets delta_score of
@@ -128,7 +182,9 @@ def save_xbox(table, path: str, mode: str, cfg: SaveConfig, nonclk: float, clk: 
     called with the saved mixed keys (another tier holding live copies of
     the rows applies the same reset)."""
     os.makedirs(path, exist_ok=True)
-    dim = table.dim
+    # rows are canonical: a codec table's embedding block is embedx + expand
+    codec = getattr(table, "codec", None)
+    dim = int(codec.DX) if codec is not None else table.dim
     l = row_layout(dim)
     fn = os.path.join(path, f"part-{rank:05d}.txt")
     if _streamable(table):

@@ -132,6 +132,28 @@ class FeatureCodec:
             out[:, self.canon["stride"]:] = raw[:, b:b + self.extra]
         return out
 
+    def save_map(self):
+        """Column map of ``decode`` for the native streaming saver
+        (csrc/hip/ckpt.hip SaveDecode): per canonical column, the stored float
+        column (>= 0), -1 for zero, or -2 - e for int16 element e of the
+        embedding block (times qscale)."""
+        m = [-1] * self.canon_width
+        m[0], m[1], m[2] = 0, 1, 2
+        for j in range(self.DX):
+            if self.kind == KIND_VAR:
+                src = 3 + j
+            elif self.kind == KIND_INT16:
+                src = -2 - (j if j < self.D else 2 * self.Wx + (j - self.D))
+            else:
+                src = 3 + j if j < self.D else 3 + self.Wx + (j - self.D)
+            m[3 + j] = src
+        for f in self._TAIL:
+            m[self.canon[f]] = self.raw[f]
+        b = self.raw["mf_size"] + 1
+        for e in range(self.extra):
+            m[self.canon["stride"] + e] = b + e
+        return m
+
     def quantize(self, x: torch.Tensor) -> torch.Tensor:
         return torch.clamp(torch.round(x / self.qscale), -32768, 32767)
 

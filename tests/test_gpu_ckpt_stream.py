@@ -102,3 +102,82 @@ def test_stream_save_bounded_and_fast(tmp_path):
     assert 2 * ckpt.STREAM_CHUNK_ROWS * (8 + 4 * stride) <= 1 << 30
     k = np.load(str(tmp_path / "big" / "part-00000.keys.npy"), mmap_mode="r", allow_pickle=False)
     assert k.shape == (n,) and int(np.asarray(k[:1000]).min()) >= 1
+
+
+def _codec_table(kind, De, n=30000, seed=5):
+    """A feature-type codec table (int16 embedx / SparseAdam / variable) with
+    randomised statistics, written through the canonical (decoded) rows."""
+    from paddlebox_amd.ps.feature_types import FeatureCodec
+
+    codec = FeatureCodec(kind, 8, De, qscale=1.0 / 512)
+    codec.device = DEV
+    g = torch.Generator().manual_seed(seed)
+    t = GpuSparseTable(8, n, DEV, stash_cap=64, codec=codec)
+    keys = torch.unique(torch.randint(1, 1 << 62, (n,), generator=g))
+    h = ref.mix64(keys).to(DEV)
+    t.insert_mixed(h, SparseSGDConfig(), init_embedx=True)
+    l = codec.canon
+    k, v = t.export(True)
+    v = v.clone()
+    gg = torch.Generator(device=DEV).manual_seed(seed + 1)
+    v[:, 0] = torch.rand(v.shape[0], device=DEV, generator=gg) * 30
+    v[:, 1] = v[:, 0] * torch.rand(v.shape[0], device=DEV, generator=gg) * 0.3
+    v[:, 3:3 + codec.DX] = (torch.rand(v.shape[0], codec.DX, device=DEV, generator=gg) - 0.5) * 0.1
+    v[:, l["delta_score"]] = torch.rand(v.shape[0], device=DEV, generator=gg)
+    v[:, l["unseen_days"]] = torch.randint(0, 30, (v.shape[0],), device=DEV, generator=gg).float()
+    v[:, l["slot"]] = torch.randint(1, 40, (v.shape[0],), device=DEV, generator=gg).float()
+    v[:, l["mf_size"]] = (torch.rand(v.shape[0], device=DEV, generator=gg) < 0.8).float()
+    if codec.extra:  # codec state: any values survive the round trip verbatim
+        v[:, l["stride"]:] = torch.rand(v.shape[0], codec.extra, device=DEV, generator=gg)
+    t.assign(k, v)
+    return t
+
+
+CODECS = [(1, 0), (1, 4), (2, 0), (3, 12)]  # (kind, expand dim): int16, int16 + expand, SparseAdam, variable
+
+
+@pytest.mark.parametrize("kind,De", CODECS)
+def test_codec_batch_model_stream_round_trip(tmp_path, small_chunks, monkeypatch, kind, De):
+    """Codec tables stream through the native saver too (VERDICT r3 #6c): rows
+    decoded on the device to the canonical layout equal the export writer's,
+    and load back into an empty table of the same codec bit-exactly."""
+    t = _codec_table(kind, De)
+    n = ckpt.save_batch_model(t, str(tmp_path / "native"), 0)
+    assert ckpt.last_save_stats.get("native") and ckpt.last_save_stats["chunks"] > 5
+    monkeypatch.setenv("PBX_SAVE_STREAM", "0")
+    m = ckpt.save_batch_model(t, str(tmp_path / "py"), 0)
+    assert n == m == t.size()
+    ka, va = ckpt.load_batch_model_parts(str(tmp_path / "native"))
+    kb, vb = ckpt.load_batch_model_parts(str(tmp_path / "py"))
+    oa, ob = np.argsort(ka), np.argsort(kb)
+    assert np.array_equal(ka[oa], kb[ob])
+    assert np.array_equal(va[oa], vb[ob])
+    # round trip into a fresh table of the same codec
+    u = GpuSparseTable.like(t)
+    h = ref.mix64(torch.from_numpy(ka.view(np.int64).copy())).to(DEV)
+    u.insert_mixed(h, SparseSGDConfig())
+    u.assign(h, torch.from_numpy(va).to(DEV))
+    k0, v0 = t.export(True)
+    k1, v1 = u.export(True)
+    o0, o1 = torch.argsort(k0), torch.argsort(k1)
+    assert torch.equal(k0[o0], k1[o1])
+    torch.testing.assert_close(v1[o1], v0[o0], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("kind,De", CODECS)
+def test_codec_xbox_stream_matches_export(tmp_path, small_chunks, monkeypatch, kind, De):
+    cfg = SaveConfig(base_threshold=1.5, delta_threshold=0.25, delta_keep_days=16, embedx_threshold=10.0)
+    a = _codec_table(kind, De, seed=9)
+    b = _twin(a)
+    na = ckpt.save_xbox(a, str(tmp_path / "native"), "base", cfg, 0.1, 1.0, 0)
+    assert ckpt.last_save_stats.get("native")
+    monkeypatch.setenv("PBX_SAVE_STREAM", "0")
+    nb = ckpt.save_xbox(b, str(tmp_path / "py"), "base", cfg, 0.1, 1.0, 0)
+    assert na == nb > 0
+    la = open(tmp_path / "native" / "part-00000.txt").read().splitlines()
+    lb = open(tmp_path / "py" / "part-00000.txt").read().splitlines()
+    assert sorted(la) == sorted(lb)
+    ka, va = a.export(True)
+    kb, vb = b.export(True)
+    oa, ob = torch.argsort(ka), torch.argsort(kb)
+    torch.testing.assert_close(va[oa], vb[ob], rtol=0, atol=0)

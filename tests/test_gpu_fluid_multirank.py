@@ -90,7 +90,7 @@ def _train(fluid, files, batch, rank, W, transpile):
     box.initialize_gpu_and_load_model(slot_vector=list(range(S)), max_keys=60000)
     scope = fluid.Scope()
     main, startup, slots, label, dense, loss = _build(fluid)
-    main._pipeline_opt = dict(main._pipeline_opt or {}, use_graph=True)
+    main._pipeline_opt = dict(main._pipeline_opt or {}, use_graph=os.environ.get("PBX_TEST_FLUID_GRAPH", "1") == "1")
     if transpile:
         eps = [f"127.0.0.1:{6170 + r}" for r in range(W)]
         fluid.transpiler.GradAllReduce().transpile(startup, main, rank, eps, eps[rank])

@@ -91,9 +91,10 @@ def _worker(rank, W, port, B, steps, q):
                              on_warm=lambda out: losses.append(float(out)))
         for i in range(1, steps):
             g.load(i % g.n, hbs[i])
-            losses.append(g.run(i % g.n))
-        torch.cuda.synchronize()
-        losses = [float(x) for x in losses]
+            out = g.run(i % g.n)
+            torch.cuda.synchronize()
+            losses.append(float(out))  # the graphs' loss outputs share the tower's workspace scalar
+
         dn = step.model.dn
         res = dict(flat=step.arena.flat.cpu(), dn=torch.stack([dn.batch_size, dn.batch_sum, dn.batch_square_sum]).cpu(),
                    keys=None, vals=None, losses=losses, ovf=eng.check_overflow())
@@ -135,7 +136,7 @@ def _oracle(W, B, steps):
         join_grad_producers()
         model.dn.stats.mul_(W)  # W ranks' normalised statistics, summed (module docstring)
         step.opt.step(1.0)
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
     torch.cuda.synchronize()
     dn = model.dn
     return dict(flat=step.arena.flat.cpu(), dn=torch.stack([dn.batch_size, dn.batch_sum, dn.batch_square_sum]).cpu(),

@@ -80,7 +80,8 @@ def test_tower32_matches_fp32(B, hidden):
     assert float(tg.auc[0].sum()) == float(tc.auc[0].sum()) == B
 
 
-@pytest.mark.parametrize("M,dims", [(300, [304, 64, 48]), (8192, [304, 400, 400, 400]), (1000, [64, 136, 96])])
+@pytest.mark.parametrize("M,dims", [(300, [304, 64, 48]), (8192, [304, 400, 400, 400]), (1000, [64, 136, 96]),
+                                    (700, [128, 256, 512])])
 def test_tower32_kernels_exact(M, dims):
     """k_t32_fwd/bwd/dw against fp64 math on the kernels' own stored
     activations (ReLU masks agree), checking every MP32 buffer."""
