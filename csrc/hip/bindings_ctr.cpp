@@ -62,6 +62,39 @@ void sgemm(const Tensor& A, const Tensor& B, Tensor C, const c10::optional<Tenso
   launch_sgemm(g, cs());
 }
 
+// scaled_fc's fp16 GEMM (launch_hgemm): C [M, ldc] fp32 from strided fp32
+// A [M x K] (rsA, csA) and B [K x N] (rsB, csB) with the reference rounding
+void hgemm(const Tensor& A, const Tensor& B, Tensor C, const c10::optional<Tensor>& bias, int64_t M, int64_t N,
+           int64_t K, std::vector<int64_t> a_strides, std::vector<int64_t> b_strides, int64_t ldc, double a_scale,
+           double b_scale, double alpha, double bias_scale, double out_scale, int64_t ksplit) {
+  f32(A, "A");
+  f32(B, "B");
+  f32(C, "C");
+  CX_CHECK(a_strides.size() == 2 && b_strides.size() == 2, "strides are (row, col)");
+  HgemmArgs g;
+  g.A = P<float>(A);
+  g.B = P<float>(B);
+  g.C = P<float>(C);
+  g.bias = OP<float>(bias);
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.rsA = a_strides[0]; g.csA = a_strides[1];
+  g.rsB = b_strides[0]; g.csB = b_strides[1];
+  g.ldc = ldc;
+  g.a_scale = (float)a_scale; g.b_scale = (float)b_scale; g.alpha = (float)alpha;
+  g.bias_scale = (float)bias_scale; g.out_scale = (float)out_scale;
+  g.ksplit = (int)std::max<int64_t>(1, std::min<int64_t>(ksplit, (K + 31) / 32));
+  CX_CHECK((M - 1) * g.rsA + (K - 1) * g.csA < A.numel(), "A too small for its strides");
+  CX_CHECK((K - 1) * g.rsB + (N - 1) * g.csB < B.numel(), "B too small for its strides");
+  CX_CHECK((M - 1) * ldc + N - 1 < C.numel(), "C too small");
+  if (g.bias) CX_CHECK(bias->numel() >= N, "bias");
+  Tensor ws;
+  if (g.ksplit > 1) {
+    ws = torch::empty({M * N}, C.options());
+    g.ws = P<float>(ws);
+  }
+  launch_hgemm(g, cs());
+}
+
 void colsum_strided(const Tensor& x, int64_t batch, int64_t M, int64_t N, int64_t sb, int64_t ld, Tensor out,
                     int64_t so, bool accumulate) {
   f32(x, "x");
@@ -369,6 +402,7 @@ void bind_ctr(py::module& m) {
         py::arg("K"), py::arg("batch"), py::arg("a_strides"), py::arg("b_strides"), py::arg("sC"), py::arg("ldc"),
         py::arg("sBias") = 0, py::arg("bias_scale") = 1.0, py::arg("alpha") = 1.0, py::arg("accumulate") = false);
   m.def("colsum_strided", &colsum_strided);
+  m.def("hgemm", &hgemm);
   m.def("int8_fc", &int8_fc);
   m.def("rank_attention_fwd", &rank_attention_fwd);
   m.def("rank_attention_bwd", &rank_attention_bwd);

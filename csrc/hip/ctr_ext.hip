@@ -110,6 +110,100 @@ __global__ __launch_bounds__(256) void k_mgemm(SgemmArgs g) {
     }
 }
 
+// ---------------------------------------------------------------- scaled_fc fp16 GEMM
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+// One 64x64 output tile per 256-thread block: 4 waves of 32x32, each 2x2
+// v_mfma_f32_16x16x32_f16 tiles.  K steps of 32: the fp32 operands are read
+// with arbitrary strides, scaled, rounded to fp16 and written to LDS k-minor
+// ([row][k], rows padded to 40 halves) so every lane reads its 8-element
+// fragment with one 16-B LDS read; the next K step's operands are loaded into
+// registers while the current one is multiplied.  16x16x32 layout: lane l
+// feeds A[l%16][8(l/16)+j] and B[8(l/16)+j][l%16]; accumulator register r is
+// C[4(l/16)+r][l%16].
+constexpr int kHPad = 40;
+__device__ __forceinline__ float h16_epi(float acc, float bv, const HgemmArgs& g) {
+  _Float16 v = (_Float16)((float)(_Float16)g.alpha * acc);
+  if (g.bias) v = (_Float16)((float)v + (float)(_Float16)((float)(_Float16)bv * (float)(_Float16)g.bias_scale));
+  float y = (float)v * g.out_scale;
+  return __builtin_isinf(y) ? __int_as_float(0x7fc00000) : y;
+}
+
+__global__ __launch_bounds__(256) void k_hgemm(HgemmArgs g) {
+  __shared__ __attribute__((aligned(16))) _Float16 As[64 * kHPad];
+  __shared__ __attribute__((aligned(16))) _Float16 Bs[64 * kHPad];
+  const int ks = blockIdx.z;
+  const int kper = ((g.K + g.ksplit - 1) / g.ksplit + 31) / 32 * 32;
+  const int kbeg = ks * kper, kend = min(g.K, kbeg + kper);
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  const int fr = lane & 15, fk = lane >> 4;
+  // staging: thread t covers row / column (t & 63), k = 8 (t >> 6) .. + 7
+  const int sr = t & 63, sk = (t >> 6) * 8;
+  float ra[8], rb[8];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int gk = k0 + sk + j;
+      const int gm = m0 + sr, gn = n0 + sr;
+      ra[j] = (gm < g.M && gk < kend) ? g.A[(int64_t)gm * g.rsA + (int64_t)gk * g.csA] : 0.f;
+      rb[j] = (gn < g.N && gk < kend) ? g.B[(int64_t)gk * g.rsB + (int64_t)gn * g.csB] : 0.f;
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (kbeg < kend) load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += 32) {
+    h16x8 ha, hb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ha[j] = (_Float16)(ra[j] * g.a_scale);
+      hb[j] = (_Float16)(rb[j] * g.b_scale);
+    }
+    __syncthreads();  // the previous step's reads of As / Bs are done
+    *reinterpret_cast<h16x8*>(&As[sr * kHPad + sk]) = ha;
+    *reinterpret_cast<h16x8*>(&Bs[sr * kHPad + sk]) = hb;
+    __syncthreads();
+    if (k0 + 32 < kend) load(k0 + 32);  // next step in flight under the MFMAs
+    const h16x8 a0 = *reinterpret_cast<const h16x8*>(&As[(wm + fr) * kHPad + 8 * fk]);
+    const h16x8 a1 = *reinterpret_cast<const h16x8*>(&As[(wm + 16 + fr) * kHPad + 8 * fk]);
+    const h16x8 b0 = *reinterpret_cast<const h16x8*>(&Bs[(wn + fr) * kHPad + 8 * fk]);
+    const h16x8 b1 = *reinterpret_cast<const h16x8*>(&Bs[(wn + 16 + fr) * kHPad + 8 * fk]);
+    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b1, acc[1][1], 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn + j * 16 + fr;
+      if (n >= g.N) continue;
+      const float bv = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + i * 16 + 4 * fk + r;
+        if (m >= g.M) continue;
+        if (g.ksplit > 1)
+          atomicAdd(&g.ws[(int64_t)m * g.N + n], acc[i][j][r]);
+        else
+          g.C[(int64_t)m * g.ldc + n] = h16_epi(acc[i][j][r], bv, g);
+      }
+    }
+}
+
+// split-K second pass: the fp16 epilogue over the fp32 sums
+__global__ void k_hgemm_epi(HgemmArgs g) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)g.M * g.N) return;
+  const int m = (int)(e / g.N), n = (int)(e % g.N);
+  g.C[(int64_t)m * g.ldc + n] = h16_epi(g.ws[e], g.bias ? g.bias[n] : 0.f, g);
+}
+
 // column sums of a [batch][M][N] strided matrix into out[batch][N] (+=): bias
 // gradients of batch_fc / scaled_fc.  Block = 64 columns x 4 row phases over
 // a slice of kColSlice rows; the 4 phases meet in LDS and one fp32 atomic
@@ -723,6 +817,19 @@ void launch_sgemm(const SgemmArgs& g0, hipStream_t s) {
                        g.N, g.sC, g.ldc);
   dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, g.batch * g.ksplit);
   hipLaunchKernelGGL(k_mgemm, grid, dim3(256), 0, s, g);
+}
+
+void launch_hgemm(const HgemmArgs& g0, hipStream_t s) {
+  if (g0.M == 0 || g0.N == 0) return;
+  HgemmArgs g = g0;
+  if (g.ksplit > 1) {
+    (void)hipMemsetAsync(g.ws, 0, (size_t)g.M * g.N * sizeof(float), s);
+  } else {
+    g.ksplit = 1;
+  }
+  dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, g.ksplit);
+  hipLaunchKernelGGL(k_hgemm, grid, dim3(256), 0, s, g);
+  if (g.ksplit > 1) hipLaunchKernelGGL(k_hgemm_epi, dim3(nblk((int64_t)g.M * g.N)), dim3(256), 0, s, g);
 }
 
 void launch_colsum_strided(const float* x, int batch, int M, int N, int64_t sb, int64_t ld, float* out, int64_t so,

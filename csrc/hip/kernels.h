@@ -719,6 +719,26 @@ struct SgemmArgs {
   int ksplit = 1;  // set by launch_sgemm: K slices per output tile (fp32 atomics)
 };
 void launch_sgemm(const SgemmArgs& g, hipStream_t s);
+// scaled_fc's fp16 GEMMs with the reference's rounding points
+// (scaled_fc_op.cu:144-330): operands a_scale * A, b_scale * B rounded to
+// fp16, fp32-accumulated MFMA (v_mfma_f32_16x16x32_f16), then
+//   v = fp16(alpha16 * acc); if bias: v = fp16(v + fp16(fp16(bias) * bs16));
+//   C = float(v) * out_scale, inf -> NaN
+// (alpha16 / bs16 = the fp16 values of alpha / bias_scale).  Split-K adds
+// fp32 partials into the zeroed scratch ws (M x N per batch) and a second
+// pass applies the fp16 epilogue.
+struct HgemmArgs {
+  const float* A = nullptr;
+  const float* B = nullptr;
+  float* C = nullptr;
+  const float* bias = nullptr;
+  float* ws = nullptr;
+  int M = 0, N = 0, K = 0;
+  int64_t rsA = 0, csA = 0, rsB = 0, csB = 0, ldc = 0;
+  float a_scale = 1.f, b_scale = 1.f, alpha = 1.f, bias_scale = 1.f, out_scale = 1.f;
+  int ksplit = 1;
+};
+void launch_hgemm(const HgemmArgs& g, hipStream_t s);
 void launch_colsum_strided(const float* x, int batch, int M, int N, int64_t sb, int64_t ld, float* out, int64_t so,
                            bool accumulate, hipStream_t s);
 void launch_i8_quant(const float* x, int R, int C, int ldo, float expand, float clip, float range, bool transpose,

@@ -773,31 +773,74 @@ def _fc_backward_hip(x, W, dy):
     return dx, dW, db
 
 
+def scaled_fc_reference(x, W, b, in_scale, bias_scale):
+    """The reference forward's arithmetic (scaled_fc_op.cu:144-227) in torch:
+    fp16 operands, fp32-accumulated GEMM scaled by fp16(in_scale) and rounded
+    to fp16, + fp16(fp16(bias) * fp16(bias_scale)) in fp16, then fp32 * 1/in_scale
+    with inf -> NaN."""
+    h = torch.float16
+    acc = x.to(h).float() @ W.to(h).float()
+    v = (float(torch.tensor(in_scale, dtype=h)) * acc).to(h)
+    bb = (b.reshape(-1).to(h).float() * float(torch.tensor(bias_scale, dtype=h))).to(h)
+    v = (v.float() + bb.float().reshape(1, -1)).to(h)
+    y = v.float() * (1.0 / in_scale)
+    return torch.where(torch.isinf(y), torch.full_like(y, float("nan")), y)
+
+
 class _ScaledFc(torch.autograd.Function):
-    """scaled_fc (operators/scaled_fc_op.cu:144-330): y = x@W + bias*bs/is
-    (the reference's fp16 scaling is numerically transparent in bf16/fp32);
-    reference gradients: dx = dy W^T, dW = x^T dy, db = colsum(dy).
-    GPU tensors run k_sgemm with the scaled bias fused into the epilogue."""
+    """scaled_fc (operators/scaled_fc_op.cu:144-330) with the reference's
+    fp16 arithmetic on fp16 MFMA (csrc/hip/ctr_ext.hip k_hgemm):
+      forward  y = fp32(fp16(fp16(in_scale) * x16 @ W16) + fp16(b16 * bs16)) / in_scale
+      backward d16 = fp16(dy * grad_scale / in_scale);
+               dx = fp32(fp16(fp16(in_scale) * d16 @ W16^T)) / grad_scale,
+               dW = fp32(fp16(fp16(in_scale) * x16^T @ d16)) / grad_scale,
+               db = colsum(dy) (fp32);  inf -> NaN on every cast back.
+    CPU tensors run the same arithmetic in torch."""
 
     @staticmethod
     def forward(ctx, x, W, b, in_scale, bias_scale, grad_scale):
         ctx.save_for_backward(x, W)
         ctx.bshape = b.shape
+        ctx.sc = (in_scale, grad_scale)
         if x.is_cuda:
             N, K = x.shape
             O = W.shape[1]
-            return _sg(x, W, x.new_empty(N, O), N, O, K, 1, (0, K, 1), (0, O, 1), 0, O, b.reshape(-1), 0,
-                       bias_scale / in_scale)
-        return x @ W + b.reshape(1, -1) * (bias_scale / in_scale)
+            y = x.new_empty(N, O)
+            _native.hip().hgemm(x, W, y, b.reshape(-1), N, O, K, [K, 1], [O, 1], O, 1.0, 1.0, in_scale, bias_scale,
+                                1.0 / in_scale, 1)
+            return y
+        return scaled_fc_reference(x, W, b, in_scale, bias_scale)
 
     @staticmethod
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
+        in_scale, gs = ctx.sc
+        dy = dy.float().contiguous()
+        N, K = x.shape
+        O = W.shape[1]
         if x.is_cuda:
-            dx, dW, db = _fc_backward_hip(x, W, dy)
-        else:
-            dx, dW, db = dy @ W.t(), x.t() @ dy, dy.sum(0)
-        return dx, dW, db.reshape(ctx.bshape), None, None, None
+            h = _native.hip()
+            dx = x.new_empty(N, K)
+            # dx [N, K] = d16 [N, O] @ W16^T: B[o][k] = W[k][o]
+            h.hgemm(dy, W, dx, None, N, K, O, [O, 1], [1, O], K, gs / in_scale, 1.0, in_scale, 1.0, 1.0 / gs, 1)
+            dW = W.new_empty(K, O)
+            # dW [K, O] = x16^T [K, N] @ d16 [N, O]: A[k][n] = x[n][k]; split over N
+            h.hgemm(x, dy, dW, None, K, O, N, [1, K], [O, 1], O, 1.0, gs / in_scale, in_scale, 1.0, 1.0 / gs,
+                    max(1, min(16, N // 512)))
+            db = W.new_empty(O)
+            h.colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
+            return dx, dW, db.reshape(ctx.bshape), None, None, None
+        hf = torch.float16
+        a16 = float(torch.tensor(in_scale, dtype=hf))
+        d16 = (dy * (gs / in_scale)).to(hf).float()
+
+        def back(v):
+            y = (a16 * v).to(hf).float() * (1.0 / gs)
+            return torch.where(torch.isinf(y), torch.full_like(y, float("nan")), y)
+
+        dx = back(d16 @ W.to(hf).float().t())
+        dW = back(x.to(hf).float().t() @ d16)
+        return dx, dW, dy.sum(0).reshape(ctx.bshape), None, None, None
 
 
 def scaled_fc(x, W, b, in_scale, bias_scale, grad_scale=256.0):

@@ -1,5 +1,6 @@
 """Microbenchmarks of the CTR GEMM ops at CTR shapes:
-batch_fc (slot-batched fp32 MFMA GEMM), scaled_fc, rank_attention (grouped
+batch_fc (slot-batched fp32 MFMA GEMM), scaled_fc (fp16 MFMA, the reference's
+fp16 rounding chain), rank_attention (grouped
 MFMA GEMMs with gather-on-load) and scaled_int8fc (int8 MFMA, LDS-staged),
 forward and forward+backward, timed with HIP events over many iterations.
 A torch.matmul (hipBLASLt) fp32 GEMM of the same FLOP shape is printed next
@@ -85,13 +86,18 @@ def main():
         report(f"rank_attention_R{R}", [B, R, C, Pp], 2.0 * B * R * C * Pp, lambda: cx.rank_attention(x, ro, W, R),
                lambda: cx.rank_attention(x, ro, W, R).backward(d), lambda: xr @ wr, it)
 
-    # scaled_int8fc (forward only in the reference: no backward op)
+    # scaled_int8fc: int8 MFMA forward, fp32 straight-through backward
+    # (scaled_int8fc_op.cu:290-440 registers both)
     N, K, O = 8192, 512, 512
-    x, W, bb = torch.randn(N, K, device=DEV), torch.randn(K, O, device=DEV) * 0.2, torch.randn(O, device=DEV)
+    x = torch.randn(N, K, device=DEV).requires_grad_()
+    W = (torch.randn(K, O, device=DEV) * 0.2).requires_grad_()
+    bb = torch.randn(O, device=DEV).requires_grad_()
+    d = torch.randn(N, O, device=DEV)
+    xr, wr = x.detach(), W.detach()
     at = dict(input_expand_factor=10.0, input_clip_factor=3.0, weight_expand_factor=40.0, weight_clip_factor=5.0,
               int8_range=127.0)
     report("scaled_int8fc", [N, K, O], 2.0 * N * K * O, lambda: cx.scaled_int8fc(x, W, bb, at),
-           lambda: cx.scaled_int8fc(x, W, bb, at), lambda: x @ W, it)
+           lambda: cx.scaled_int8fc(x, W, bb, at).backward(d), lambda: xr @ wr, it)
 
 
 if __name__ == "__main__":

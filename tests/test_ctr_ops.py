@@ -49,7 +49,19 @@ def test_scaled_fc_and_int8fc():
     W = torch.randn(9, 5, generator=g)
     b = torch.randn(1, 5, generator=g)
     y = cx.scaled_fc(x, W, b, 4.0, 2.0)
-    torch.testing.assert_close(y, x @ W + b * 0.5)
+    # the reference's fp16 arithmetic (scaled_fc_op.cu): fp16-close to the fp32 product
+    torch.testing.assert_close(y, x @ W + b * 0.5, rtol=4e-3, atol=1e-2)
+    torch.testing.assert_close(y, cx.scaled_fc_reference(x, W, b, 4.0, 2.0), rtol=0, atol=0)
+    # values past fp16 range come back NaN (inf -> NaN on the cast back)
+    assert torch.isnan(cx.scaled_fc(x * 1e4, W, b, 4.0, 2.0)).any()
+    xr = x.clone().requires_grad_()
+    Wr = W.clone().requires_grad_()
+    br = b.clone().requires_grad_()
+    cx.scaled_fc(xr, Wr, br, 4.0, 2.0, grad_scale=256.0).sum().backward()
+    d = torch.ones(7, 5)
+    torch.testing.assert_close(xr.grad, d @ W.t(), rtol=4e-3, atol=1e-2)
+    torch.testing.assert_close(Wr.grad, x.t() @ d, rtol=4e-3, atol=1e-2)
+    torch.testing.assert_close(br.grad, d.sum(0, keepdim=True))
     a = dict(input_expand_factor=16.0, input_clip_factor=2.0, weight_expand_factor=32.0, weight_clip_factor=3.0,
              int8_range=127.0)
     y8 = cx.scaled_int8fc(x, W, b, a)
