@@ -124,7 +124,8 @@ Tensor int8_fc(const Tensor& x, const Tensor& W, const Tensor& b, double ie, dou
   return y;
 }
 
-Tensor rank_attention_fwd(const Tensor& x, const Tensor& ro, const Tensor& W, int64_t R) {
+// returns (out, bucket): bucket = the rank permutation + tile table the backward reuses
+std::vector<Tensor> rank_attention_fwd(const Tensor& x, const Tensor& ro, const Tensor& W, int64_t R) {
   f32(x, "x");
   f32(W, "W");
   CX_CHECK(ro.is_cuda() && ro.scalar_type() == torch::kInt32 && ro.dim() == 2 && ro.size(1) >= 2 * R + 1,
@@ -134,22 +135,25 @@ Tensor rank_attention_fwd(const Tensor& x, const Tensor& ro, const Tensor& W, in
   CX_CHECK(W.size(0) == R * R * C, "W must be [R*R*C, P]");
   auto xc = x.contiguous(), Wc = W.contiguous(), roc = ro.contiguous();
   auto out = torch::empty({B, P_}, x.options());
+  auto bucket = torch::empty({rank_attention_bucket_ints(B, (int)R)}, roc.options());
   launch_rank_attention_fwd(P<float>(xc), P<int>(roc), (int)roc.size(1), P<float>(Wc), B, C, P_, (int)R,
-                            P<float>(out), cs());
-  return out;
+                            P<int>(bucket), P<float>(out), cs());
+  return {out, bucket};
 }
 
 std::vector<Tensor> rank_attention_bwd(const Tensor& x, const Tensor& ro, const Tensor& W, const Tensor& dout,
-                                       int64_t R) {
+                                       const Tensor& bucket, int64_t R) {
   f32(x, "x");
   f32(dout, "dout");
+  CX_CHECK(bucket.scalar_type() == torch::kInt32 && bucket.numel() == rank_attention_bucket_ints((int)x.size(0), (int)R),
+           "bucket must come from rank_attention_fwd with the same B and R");
   const int B = (int)x.size(0), C = (int)x.size(1), P_ = (int)W.size(1);
   auto xc = x.contiguous(), Wc = W.contiguous(), roc = ro.contiguous(), dc = dout.contiguous();
   auto dexp = torch::empty({B, R, C}, x.options());
   auto dx = torch::empty_like(xc);
   auto dW = torch::zeros_like(Wc);
   launch_rank_attention_bwd(P<float>(xc), P<float>(dc), P<int>(roc), (int)roc.size(1), P<float>(Wc), B, C, P_,
-                            (int)R, P<float>(dexp), P<float>(dx), P<float>(dW), cs());
+                            (int)R, P<int>(bucket), P<float>(dexp), P<float>(dx), P<float>(dW), cs());
   return {dx, dW};
 }
 

@@ -307,183 +307,286 @@ __global__ __launch_bounds__(256) void k_i8_gemm(const signed char* __restrict__
 }
 
 // ---------------------------------------------------------------- rank_attention
-// rank_offset row i: [rank_i, (rank_k, index_k) for k < R]; a pair (i, k) is
-// valid when rank_i >= 1 and rank_k >= 1; its parameter block is
-// (rank_i - 1) * R + (rank_k - 1) of W [R*R][C][P].
-__device__ __forceinline__ int ra_block(const int* ro, int ld, int i, int k, int R, int* idx) {
-  const int lower = ro[(int64_t)i * ld] - 1;
-  const int faster = ro[(int64_t)i * ld + 2 * k + 1] - 1;
-  *idx = ro[(int64_t)i * ld + 2 * k + 2];
-  if (lower < 0 || faster < 0 || *idx < 0) return -1;
-  return lower * R + faster;
-}
+// Rank-bucketed rank_attention.  An instance i of rank r = rank_i - 1 uses
+// only the R parameter blocks W[r*R + f] (f = faster rank of a peer), and they
+// sit contiguously: W_r = W[r*R*C : (r+1)*R*C] viewed as [R*C, P].  With
+//   A_i[f*C + c] = sum over valid peers k of i with faster_k = f of x[idx_k][c]
+// the op is, per rank r over the instances of that rank,
+//   out_i = A_i W_r,   G_i = dout_i W_r^T (the dexp rows),   dW_r = sum_i A_i^T dout_i
+// -- dense GEMMs (K = R*C for out / G, K = the rank's instances for dW) that
+// never visit a block an instance does not use.  k_ra_bucket counting-sorts
+// the instances by rank once (stable, one workgroup); the forward keeps the
+// permutation + tile table for the backward.  Exact fp32 (v_mfma_f32_16x16x4_f32).
+// A pair (i, k) is valid when rank_i in 1..R, faster_k + 1 in 1..R and
+// 0 <= idx_k < B; invalid pairs contribute nothing and get zero dexp rows.
+constexpr int kRaT = 32;  // instances per tile
+constexpr int kRaBucketThreads = 1024;
+constexpr int kRaSeg = 256;  // dW: peer tables staged per segment of instances
 
-// Grouped-GEMM form of rank_attention.  For a tile of 64 instances and a
-// parameter block b, A_b[i][c] = sum of x[idx_k] over the pairs k of
-// instance i that use block b (gather-sum on load), so
-//   out = sum_b A_b W_b,   R_b = dout W_b^T (dexp rows of the pairs of b),
-//   dW_b = X_b^T dout_b over the pairs of b,
-// each an MFMA GEMM (v_mfma_f32_16x16x4_f32, exact fp32) with the operand
-// panels gathered into LDS 16 deep.  Only the blocks present in a tile are
-// visited (a 64-bit mask over the <= 64 blocks).
-// blocks b with b % gridDim.z == blockIdx.z
-__device__ __forceinline__ unsigned long long ra_group_mask(int R) {
-  unsigned long long m = 0ull;
-  for (int b = (int)blockIdx.z; b < R * R; b += (int)gridDim.z) m |= 1ull << b;
-  return m;
-}
+__device__ __forceinline__ int ra_bucket_of(int rank, int R) { return (rank >= 1 && rank <= R) ? rank - 1 : R; }
 
+// meta (ints, after perm[B]): [0, R+1) count, [R+1, 2R+2) base, [2R+2, 3R+4) tile prefix
 template <int R>
-__device__ __forceinline__ unsigned long long ra_tile_blocks(const int* ro, int ld, int i0, int B, int (*sblk)[64],
-                                                             int (*sidx)[64], unsigned long long* used) {
-  const int t = threadIdx.x;
-  if (t == 0) *used = 0ull;
-  __syncthreads();
-  if (t < 64) {
-    const int i = i0 + t;
+__global__ __launch_bounds__(kRaBucketThreads) void k_ra_bucket(const int* __restrict__ ro, int ld, int B,
+                                                                int* __restrict__ perm, int* __restrict__ meta) {
+  constexpr int Q = R + 1;
+  __shared__ int wsum[kRaBucketThreads / 64][Q];
+  __shared__ int tot[Q];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int chunk = (B + kRaBucketThreads - 1) / kRaBucketThreads;
+  const int i0 = min(B, t * chunk), i1 = min(B, i0 + chunk);
+  int cnt[Q];
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-      int idx = -1;
-      const int b = i < B ? ra_block(ro, ld, i, k, R, &idx) : -1;
-      sblk[k][t] = (b >= 0 && idx < B) ? b : -1;
-      sidx[k][t] = idx;
-      if (sblk[k][t] >= 0) atomicOr(used, 1ull << b);
+  for (int q = 0; q < Q; ++q) cnt[q] = 0;
+  for (int i = i0; i < i1; ++i) {
+    const int b = ra_bucket_of(ro[(int64_t)i * ld], R);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) cnt[q] += b == q;
+  }
+  int off[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    int v = cnt[q];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int u = __shfl_up(v, d);
+      if (lane >= d) v += u;
     }
+    off[q] = v - cnt[q];
+    if (lane == 63) wsum[w][q] = v;
   }
   __syncthreads();
-  return *used;
+  if (t < Q) {
+    int s = 0;
+    for (int ww = 0; ww < kRaBucketThreads / 64; ++ww) {
+      const int v = wsum[ww][t];
+      wsum[ww][t] = s;
+      s += v;
+    }
+    tot[t] = s;
+  }
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    off[q] += wsum[w][q] + base;
+    base += tot[q];
+  }
+  for (int i = i0; i < i1; ++i) {
+    const int b = ra_bucket_of(ro[(int64_t)i * ld], R);
+    int pos = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (b == q) pos = off[q]++;
+    perm[pos] = i;
+  }
+  if (t == 0) {
+    int bs = 0, tp = 0;
+    for (int q = 0; q < Q; ++q) {
+      meta[q] = tot[q];
+      meta[Q + q] = bs;
+      meta[2 * Q + q] = tp;
+      bs += tot[q];
+      tp += (tot[q] + kRaT - 1) / kRaT;
+    }
+    meta[3 * Q] = tp;
+  }
 }
 
+// tile x of the bucketed order -> (bucket, first sorted position, instances)
+template <int R>
+__device__ __forceinline__ bool ra_tile(const int* __restrict__ meta, int x, int* q, int* start, int* n) {
+  constexpr int Q = R + 1;
+  if (x >= meta[3 * Q]) return false;
+  int b = 0;
+  while (b < R && x >= meta[2 * Q + b + 1]) ++b;
+  const int lt = x - meta[2 * Q + b];
+  *q = b;
+  *start = meta[Q + b] + lt * kRaT;
+  *n = min(kRaT, meta[b] - lt * kRaT);
+  return true;
+}
+
+// the valid peers of instance i as (faster, idx), faster = -1 if invalid
+template <int R>
+__device__ __forceinline__ void ra_peers(const int* __restrict__ ro, int ld, int i, int B, int* pf, int* px) {
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    int f = -1, id = 0;
+    if (i >= 0) {
+      f = ro[(int64_t)i * ld + 2 * k + 1] - 1;
+      id = ro[(int64_t)i * ld + 2 * k + 2];
+      if (f >= R || id < 0 || id >= B) f = -1;
+    }
+    pf[k] = f;
+    px[k] = f >= 0 ? id : 0;
+  }
+}
+
+// out rows of one tile (32 instances of rank q) x 64 outputs; K = R*C in
+// chunks of 64, the next chunk's gathered A and W_q rows held in registers
+// while the current one runs on MFMA.
 template <int R>
 __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, const int* __restrict__ ro, int ld,
                                                 const float* __restrict__ W, int B, int C, int P,
+                                                const int* __restrict__ perm, const int* __restrict__ meta,
                                                 float* __restrict__ out) {
-  __shared__ float As[16][68];  // [c][instance]
-  __shared__ float Ws[16][68];  // [c][p]
-  __shared__ int sblk[R][64], sidx[R][64];
-  __shared__ unsigned long long used;
+  constexpr int KC = 64;
+  __shared__ float As[KC][kRaT + 4];  // [k][instance]
+  __shared__ float Ws[KC][68];        // [k][p]
+  __shared__ int sperm[kRaT];
+  int q, start, n;
+  if (!ra_tile<R>(meta, blockIdx.x, &q, &start, &n)) return;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int i0 = blockIdx.x * 64, p0 = blockIdx.y * 64;
-  const int wm = (w >> 1) * 32, wn = (w & 1) * 32, fr = lane & 15, fk = lane >> 4;
-  // grid.z splits the parameter blocks of a tile over workgroups (b % gz == z)
-  unsigned long long mask = ra_tile_blocks<R>(ro, ld, i0, B, sblk, sidx, &used) & ra_group_mask(R);
-  f32x4 acc[2][2];
+  const int p0 = blockIdx.y * 64;
+  if (t < kRaT) sperm[t] = t < n ? perm[start + t] : -1;
+  __syncthreads();
+  if (q == R) {  // instances without a valid rank: zero rows
+    for (int e = t; e < n * 64; e += 256) {
+      const int p = p0 + (e & 63);
+      if (p < P) out[(int64_t)sperm[e >> 6] * P + p] = 0.f;
+    }
+    return;
+  }
+  const int KT = R * C;
+  const float* Wq = W + (int64_t)q * KT * P;
+  // A staging: instance ii = t & 31, k rows ka .. ka + 7
+  const int ii = t & 31, ka = (t >> 5) * 8;
+  int pf[R], px[R];
+  ra_peers<R>(ro, ld, sperm[ii], B, pf, px);
+  // W staging: column p = t & 63, k rows (t >> 6) + 4 j
+  const int wp = t & 63, wr = t >> 6;
+  float ra[8], rw[16];
+  auto load = [&](int kc) {
+    int kg = kc + ka, f = kg / C, c = kg - f * C;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 8; ++j) {
+      float a = 0.f;
+      if (kg < KT) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  while (mask) {
-    const int b = __ffsll((long long)mask) - 1;
-    mask &= mask - 1;
-    for (int c0 = 0; c0 < C; c0 += 16) {
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int e = t + 256 * j, ii = e & 63, cc = e >> 6, c = c0 + cc;
-        float a = 0.f;
-        if (c < C) {
-#pragma unroll
-          for (int k = 0; k < R; ++k)
-            if (sblk[k][ii] == b) a += x[(int64_t)sidx[k][ii] * C + c];
-        }
-        As[cc][ii] = a;
-        const int p = p0 + ii;
-        Ws[cc][ii] = (c < C && p < P) ? W[((int64_t)b * C + c) * P + p] : 0.f;
+        for (int k = 0; k < R; ++k)
+          if (pf[k] == f) a += x[(int64_t)px[k] * C + c];
       }
-      __syncthreads();
+      ra[j] = a;
+      ++kg;
+      if (++c == C) { c = 0; ++f; }
+    }
 #pragma unroll
-      for (int kk = 0; kk < 16; kk += 4) {
-        const float a0 = As[kk + fk][wm + fr], a1 = As[kk + fk][wm + 16 + fr];
-        const float b0 = Ws[kk + fk][wn + fr], b1 = Ws[kk + fk][wn + 16 + fr];
-        acc[0][0] = mfma4(a0, b0, acc[0][0]);
-        acc[0][1] = mfma4(a0, b1, acc[0][1]);
-        acc[1][0] = mfma4(a1, b0, acc[1][0]);
-        acc[1][1] = mfma4(a1, b1, acc[1][1]);
-      }
+    for (int j = 0; j < 16; ++j) {
+      const int r = kc + wr + 4 * j;
+      rw[j] = (r < KT && p0 + wp < P) ? Wq[(int64_t)r * P + p0 + wp] : 0.f;
+    }
+  };
+  const int fr = lane & 15, fk = lane >> 4, mi = (w & 1) * 16, nb = (w >> 1) * 32;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int kc = 0; kc < KT; kc += KC) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) As[ka + j][ii] = ra[j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) Ws[wr + 4 * j][wp] = rw[j];
+    __syncthreads();
+    if (kc + KC < KT) load(kc + KC);
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 4) {
+      const float a = As[kk + fk][mi + fr];
+      acc0 = mfma4(a, Ws[kk + fk][nb + fr], acc0);
+      acc1 = mfma4(a, Ws[kk + fk][nb + 16 + fr], acc1);
     }
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int p = p0 + wn + j * 16 + fr;
-      if (p >= P) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = i0 + wm + i * 16 + 4 * fk + r;
-        if (m >= B) continue;
-        if (gridDim.z > 1)
-          atomicAdd(&out[(int64_t)m * P + p], acc[i][j][r]);  // out zeroed by the launcher
-        else
-          out[(int64_t)m * P + p] = acc[i][j][r];
-      }
-    }
+  for (int r = 0; r < 4; ++r) {
+    const int m = mi + 4 * fk + r;
+    if (m >= n) continue;
+    const int64_t row = (int64_t)sperm[m] * P;
+    if (p0 + nb + fr < P) out[row + p0 + nb + fr] = acc0[r];
+    if (p0 + nb + 16 + fr < P) out[row + p0 + nb + 16 + fr] = acc1[r];
+  }
 }
 
-// dexp[j][k][c] = valid(j,k) ? sum_p dout[j][p] W[blk(j,k)][c][p] : 0.  Per
-// tile (64 instances x 64 c) and present block b: R_b = dout_tile W_b^T on
-// MFMA, scattered to the (j, k) rows whose pair uses b.
+// dexp[j][k][c] = valid(j,k) ? G_j[faster_k*C + c] : 0, G_j = dout_j W_q^T.
+// Tile: 32 instances x 64 columns of R*C; K = P.  Grid.y == 0 also writes
+// the zero rows of invalid pairs.
 template <int R>
 __global__ __launch_bounds__(256) void k_ra_dexp(const float* __restrict__ dout, const int* __restrict__ ro, int ld,
                                                  const float* __restrict__ W, int B, int C, int P,
+                                                 const int* __restrict__ perm, const int* __restrict__ meta,
                                                  float* __restrict__ dexp) {
-  __shared__ float Ds[16][68];  // [p][instance]
-  __shared__ float Ws[16][68];  // [p][c]
-  __shared__ int sblk[R][64], sidx[R][64];
-  __shared__ unsigned long long used;
+  constexpr int KC = 64;
+  __shared__ float Ds[KC][kRaT + 4];  // [p][instance]
+  __shared__ float Ws[KC][68];        // [p][column]
+  __shared__ int sperm[kRaT], spf[R][kRaT];
+  int q, start, n;
+  if (!ra_tile<R>(meta, blockIdx.x, &q, &start, &n)) return;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int j0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
-  const int wm = (w >> 1) * 32, wn = (w & 1) * 32, fr = lane & 15, fk = lane >> 4;
-  unsigned long long mask = ra_tile_blocks<R>(ro, ld, j0, B, sblk, sidx, &used) & ra_group_mask(R);
-  // rows of invalid pairs are zero (written once, by group 0)
-  for (int e = t; blockIdx.z == 0 && e < 64 * R * 64; e += 256) {
-    const int cc = e & 63, jk = e >> 6, jj = jk / R, k = jk % R;
-    const int j = j0 + jj, c = c0 + cc;
-    if (j < B && c < C && sblk[k][jj] < 0) dexp[((int64_t)j * R + k) * C + c] = 0.f;
+  const int n0 = blockIdx.y * 64, KT = R * C;
+  if (t < kRaT) {
+    const int i = t < n ? perm[start + t] : -1;
+    sperm[t] = i;
+    int pf[R], px[R];
+    ra_peers<R>(ro, ld, (q < R) ? i : -1, B, pf, px);
+#pragma unroll
+    for (int k = 0; k < R; ++k) spf[k][t] = pf[k];
   }
-  while (mask) {
-    const int b = __ffsll((long long)mask) - 1;
-    mask &= mask - 1;
-    f32x4 acc[2][2];
+  __syncthreads();
+  if (blockIdx.y == 0) {  // zero rows of invalid pairs (every pair of a rank-less instance)
+    for (int e = t; e < n * R * C; e += 256) {
+      const int jj = e / (R * C), rem = e - jj * R * C, k = rem / C;
+      if (spf[k][jj] < 0) dexp[(int64_t)sperm[jj] * R * C + rem] = 0.f;
+    }
+  }
+  if (q == R) return;
+  const float* Wq = W + (int64_t)q * KT * P;
+  const int ii = t & 31, pa = (t >> 5) * 8;    // dout staging: instance ii, p .. p + 7
+  const int wn = t >> 2, wpa = (t & 3) * 16;   // W staging: column wn, p .. p + 15
+  const int64_t drow = sperm[ii] >= 0 ? (int64_t)sperm[ii] * P : -1;
+  float rd[8], rw[16];
+  auto load = [&](int pc) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int q0 = 0; q0 < P; q0 += 16) {
-      __syncthreads();
-#pragma unroll
-      for (int jj4 = 0; jj4 < 4; ++jj4) {
-        const int e = t + 256 * jj4, ii = e & 63, pp = e >> 6, p = q0 + pp;
-        const int j = j0 + ii, c = c0 + ii;
-        Ds[pp][ii] = (j < B && p < P) ? dout[(int64_t)j * P + p] : 0.f;
-        Ws[pp][ii] = (c < C && p < P) ? W[((int64_t)b * C + c) * P + p] : 0.f;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int kk = 0; kk < 16; kk += 4) {
-        const float a0 = Ds[kk + fk][wm + fr], a1 = Ds[kk + fk][wm + 16 + fr];
-        const float b0 = Ws[kk + fk][wn + fr], b1 = Ws[kk + fk][wn + 16 + fr];
-        acc[0][0] = mfma4(a0, b0, acc[0][0]);
-        acc[0][1] = mfma4(a0, b1, acc[0][1]);
-        acc[1][0] = mfma4(a1, b0, acc[1][0]);
-        acc[1][1] = mfma4(a1, b1, acc[1][1]);
-      }
+    for (int j = 0; j < 8; ++j) {
+      const int p = pc + pa + j;
+      rd[j] = (drow >= 0 && p < P) ? dout[drow + p] : 0.f;
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 16; ++j) {
+      const int p = pc + wpa + j;
+      rw[j] = (n0 + wn < KT && p < P) ? Wq[(int64_t)(n0 + wn) * P + p] : 0.f;
+    }
+  };
+  const int fr = lane & 15, fk = lane >> 4, mi = (w & 1) * 16, nb = (w >> 1) * 32;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int pc = 0; pc < P; pc += KC) {
+    __syncthreads();
 #pragma unroll
-      for (int jn = 0; jn < 2; ++jn) {
-        const int c = c0 + wn + jn * 16 + fr;
-        if (c >= C) continue;
+    for (int j = 0; j < 8; ++j) Ds[pa + j][ii] = rd[j];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int jj = wm + i * 16 + 4 * fk + r, j = j0 + jj;
-          if (j >= B) continue;
+    for (int j = 0; j < 16; ++j) Ws[wpa + j][wn] = rw[j];
+    __syncthreads();
+    if (pc + KC < P) load(pc + KC);
 #pragma unroll
-          for (int k = 0; k < R; ++k)
-            if (sblk[k][jj] == b) dexp[((int64_t)j * R + k) * C + c] = acc[i][jn][r];
-        }
-      }
+    for (int kk = 0; kk < KC; kk += 4) {
+      const float a = Ds[kk + fk][mi + fr];
+      acc0 = mfma4(a, Ws[kk + fk][nb + fr], acc0);
+      acc1 = mfma4(a, Ws[kk + fk][nb + 16 + fr], acc1);
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int col = n0 + nb + 16 * h + fr;
+    if (col >= KT) continue;
+    const int f = col / C, c = col - f * C;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mi + 4 * fk + r;
+      if (m >= n) continue;
+      const float v = h ? acc1[r] : acc0[r];
+      float* d = dexp + (int64_t)sperm[m] * R * C + c;
+#pragma unroll
+      for (int k = 0; k < R; ++k)
+        if (spf[k][m] == f) d[k * C] = v;
+    }
   }
 }
 
@@ -506,61 +609,78 @@ __global__ void k_ra_dx(const float* __restrict__ dexp, const int* __restrict__ 
   dx[t] = s;
 }
 
-// dW[b][c][p] += sum over valid pairs (j,k) with blk = b of x[idx][c] dout[j][p].
-// Grid: (c tiles of 64, p tiles of 64, R*R * splits).  The split's instances
-// are scanned 256/R at a time, one (j, k) pair per thread; the pairs of
-// block b are compacted with a wave ballot + LDS offsets, then consumed 16 at
-// a time as the K dimension of a 64x64 MFMA tile (X rows and dout rows
-// gathered into LDS).
+// dW_q[m][p] += sum over a split of rank q's instances i of A_i[m] dout_i[p].
+// Grid: (64-row tiles of R*C, 64-column tiles of P, R * splits).  Peer
+// tables of kRaSeg instances at a time in LDS; the K loop takes 32 instances
+// per stage, the next stage's gathered rows prefetched into registers.
+template <int R>
 __global__ __launch_bounds__(256) void k_ra_dw(const float* __restrict__ x, const float* __restrict__ dout,
-                                               const int* __restrict__ ro, int ld, int B, int C, int P, int R,
-                                               int per_split, float* __restrict__ dW) {
-  __shared__ float Xs[16][68];  // [pair][c]
-  __shared__ float Ds[16][68];  // [pair][p]
-  __shared__ int pj[256], px[256];
-  __shared__ int wcnt[4];
-  const int b = blockIdx.z % (R * R), split = blockIdx.z / (R * R);
-  const int c0 = blockIdx.x * 64, p0 = blockIdx.y * 64;
+                                               const int* __restrict__ ro, int ld, int B, int C, int P,
+                                               const int* __restrict__ perm, const int* __restrict__ meta, int splits,
+                                               float* __restrict__ dW) {
+  constexpr int Q = R + 1, KC = 32;
+  __shared__ float Xs[KC][68];  // [instance][m]
+  __shared__ float Ds[KC][68];  // [instance][p]
+  __shared__ int sinst[kRaSeg], spf[R][kRaSeg], spx[R][kRaSeg];
+  const int q = blockIdx.z / splits, s = blockIdx.z % splits;
+  const int cnt = meta[q], per = (cnt + splits - 1) / splits;
+  const int beg = meta[Q + q] + s * per, end = meta[Q + q] + min(cnt, (s + 1) * per);
+  if (beg >= end) return;
+  const int KT = R * C;
+  const int m0 = blockIdx.x * 64, p0 = blockIdx.y * 64;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wm = (w >> 1) * 32, wn = (w & 1) * 32, fr = lane & 15, fk = lane >> 4;
+  const int tm = t & 63, tr = t >> 6;  // staging: column tm, instance rows tr + 4 j
+  const int mg = m0 + tm, f = mg < KT ? mg / C : -2, c = mg - (mg / C) * C;
+  const bool pok = p0 + tm < P;
+  const int fr = lane & 15, fk = lane >> 4, wm = (w >> 1) * 32, wn = (w & 1) * 32;
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int j_beg = split * per_split, j_end = min(B, j_beg + per_split);
-  const int per = 256 / R;  // instances per scan step
-  for (int jb = j_beg; jb < j_end; jb += per) {
-    // ---- parallel pair scan: thread t checks pair (jb + t / R, t % R)
-    const int jj = t / R, k = t % R, j = jb + jj;
-    int idx = -1;
-    const bool ok = jj < per && j < j_end && ra_block(ro, ld, j, k, R, &idx) == b && idx < B;
-    const unsigned long long m = __ballot(ok);
-    if (lane == 0) wcnt[w] = __popcll(m);
+  float rx[8], rd[8];
+  for (int sg = beg; sg < end; sg += kRaSeg) {
+    const int sn = min(kRaSeg, end - sg);
     __syncthreads();
-    int off = 0, n = 0;
+    if (t < sn) {
+      const int i = perm[sg + t];
+      int pf[R], px[R];
+      ra_peers<R>(ro, ld, i, B, pf, px);
+      sinst[t] = i;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      off += q < w ? wcnt[q] : 0;
-      n += wcnt[q];
-    }
-    if (ok) {
-      const int pos = off + __popcll(m & ((1ull << lane) - 1ull));
-      pj[pos] = j;
-      px[pos] = idx;
-    }
-    __syncthreads();
-    // ---- dW tile += X_pairs^T dout_pairs, 16 pairs per LDS stage
-    for (int q0 = 0; q0 < n; q0 += 16) {
-#pragma unroll
-      for (int e4 = 0; e4 < 4; ++e4) {
-        const int e = t + 256 * e4, cc = e & 63, pr = e >> 6, q = q0 + pr;
-        Xs[pr][cc] = (q < n && c0 + cc < C) ? x[(int64_t)px[q] * C + c0 + cc] : 0.f;
-        Ds[pr][cc] = (q < n && p0 + cc < P) ? dout[(int64_t)pj[q] * P + p0 + cc] : 0.f;
+      for (int k = 0; k < R; ++k) {
+        spf[k][t] = pf[k];
+        spx[k][t] = px[k];
       }
+    }
+    __syncthreads();
+    auto load = [&](int k0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int u = k0 + tr + 4 * j;
+        float a = 0.f, d = 0.f;
+        if (u < sn) {
+#pragma unroll
+          for (int k = 0; k < R; ++k)
+            if (spf[k][u] == f) a += x[(int64_t)spx[k][u] * C + c];
+          if (pok) d = dout[(int64_t)sinst[u] * P + p0 + tm];
+        }
+        rx[j] = a;
+        rd[j] = d;
+      }
+    };
+    load(0);
+    for (int k0 = 0; k0 < sn; k0 += KC) {
       __syncthreads();
 #pragma unroll
-      for (int kk = 0; kk < 16; kk += 4) {
+      for (int j = 0; j < 8; ++j) {
+        Xs[tr + 4 * j][tm] = rx[j];
+        Ds[tr + 4 * j][tm] = rd[j];
+      }
+      __syncthreads();
+      if (k0 + KC < sn) load(k0 + KC);
+#pragma unroll
+      for (int kk = 0; kk < KC; kk += 4) {
         const float a0 = Xs[kk + fk][wm + fr], a1 = Xs[kk + fk][wm + 16 + fr];
         const float b0 = Ds[kk + fk][wn + fr], b1 = Ds[kk + fk][wn + 16 + fr];
         acc[0][0] = mfma4(a0, b0, acc[0][0]);
@@ -568,9 +688,9 @@ __global__ __launch_bounds__(256) void k_ra_dw(const float* __restrict__ x, cons
         acc[1][0] = mfma4(a1, b0, acc[1][0]);
         acc[1][1] = mfma4(a1, b1, acc[1][1]);
       }
-      __syncthreads();
     }
   }
+  float* dWq = dW + (int64_t)q * KT * P;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -579,8 +699,8 @@ __global__ __launch_bounds__(256) void k_ra_dw(const float* __restrict__ x, cons
       if (p >= P) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int c = c0 + wm + i * 16 + 4 * fk + r;
-        if (c < C && acc[i][jn][r] != 0.f) atomicAdd(&dW[((int64_t)b * C + c) * P + p], acc[i][jn][r]);
+        const int m = m0 + wm + i * 16 + 4 * fk + r;
+        if (m < KT && acc[i][jn][r] != 0.f) atomicAdd(&dWq[(int64_t)m * P + p], acc[i][jn][r]);
       }
     }
 }
@@ -856,45 +976,45 @@ void launch_i8_gemm(const signed char* qx, const signed char* qwt, int M, int N,
                      y, ldy);
 }
 
-// workgroups per tile that split its parameter blocks: aim for ~2 waves of
-// workgroups over the 256 CUs
-static int ra_groups(int tiles, int R) {
-  int gz = (512 + tiles - 1) / (tiles > 0 ? tiles : 1);
-  gz = gz < 1 ? 1 : (gz > R * R ? R * R : gz);
-  return gz;
-}
-
-#define PBX_RA_DISPATCH(KER, GRID, ...)                                       \
-  switch (R) {                                                                \
-    case 1: hipLaunchKernelGGL(KER<1>, GRID, dim3(256), 0, s, __VA_ARGS__); break; \
-    case 2: hipLaunchKernelGGL(KER<2>, GRID, dim3(256), 0, s, __VA_ARGS__); break; \
-    case 3: hipLaunchKernelGGL(KER<3>, GRID, dim3(256), 0, s, __VA_ARGS__); break; \
-    case 4: hipLaunchKernelGGL(KER<4>, GRID, dim3(256), 0, s, __VA_ARGS__); break; \
-    case 5: hipLaunchKernelGGL(KER<5>, GRID, dim3(256), 0, s, __VA_ARGS__); break; \
-    case 6: hipLaunchKernelGGL(KER<6>, GRID, dim3(256), 0, s, __VA_ARGS__); break; \
-    case 7: hipLaunchKernelGGL(KER<7>, GRID, dim3(256), 0, s, __VA_ARGS__); break; \
-    default: hipLaunchKernelGGL(KER<8>, GRID, dim3(256), 0, s, __VA_ARGS__); break; \
+#define PBX_RA_DISPATCH(KER, GRID, BLOCK, ...)                                       \
+  switch (R) {                                                                       \
+    case 1: hipLaunchKernelGGL(KER<1>, GRID, dim3(BLOCK), 0, s, __VA_ARGS__); break; \
+    case 2: hipLaunchKernelGGL(KER<2>, GRID, dim3(BLOCK), 0, s, __VA_ARGS__); break; \
+    case 3: hipLaunchKernelGGL(KER<3>, GRID, dim3(BLOCK), 0, s, __VA_ARGS__); break; \
+    case 4: hipLaunchKernelGGL(KER<4>, GRID, dim3(BLOCK), 0, s, __VA_ARGS__); break; \
+    case 5: hipLaunchKernelGGL(KER<5>, GRID, dim3(BLOCK), 0, s, __VA_ARGS__); break; \
+    case 6: hipLaunchKernelGGL(KER<6>, GRID, dim3(BLOCK), 0, s, __VA_ARGS__); break; \
+    case 7: hipLaunchKernelGGL(KER<7>, GRID, dim3(BLOCK), 0, s, __VA_ARGS__); break; \
+    default: hipLaunchKernelGGL(KER<8>, GRID, dim3(BLOCK), 0, s, __VA_ARGS__); break; \
   }
 
+int rank_attention_bucket_ints(int B, int R) { return B + 3 * (R + 1) + 1; }
+
+// upper bound on the tiles of the bucketed order: every bucket may end in a partial tile
+static int ra_max_tiles(int B, int R) { return (B + kRaT - 1) / kRaT + R + 1; }
+
 void launch_rank_attention_fwd(const float* x, const int* ro, int ld, const float* W, int B, int C, int P, int R,
-                               float* out, hipStream_t s) {
+                               int* bucket, float* out, hipStream_t s) {
   if (B == 0) return;
-  const int tiles = ((B + 63) / 64) * ((P + 63) / 64);
-  const int gz = ra_groups(tiles, R);
-  if (gz > 1) (void)hipMemsetAsync(out, 0, (size_t)B * P * sizeof(float), s);
-  PBX_RA_DISPATCH(k_ra_fwd, dim3((B + 63) / 64, (P + 63) / 64, gz), x, ro, ld, W, B, C, P, out);
+  int* perm = bucket;
+  int* meta = bucket + B;
+  PBX_RA_DISPATCH(k_ra_bucket, dim3(1), kRaBucketThreads, ro, ld, B, perm, meta);
+  PBX_RA_DISPATCH(k_ra_fwd, dim3(ra_max_tiles(B, R), (P + 63) / 64), 256, x, ro, ld, W, B, C, P, perm, meta, out);
 }
 
 void launch_rank_attention_bwd(const float* x, const float* dout, const int* ro, int ld, const float* W, int B, int C,
-                               int P, int R, float* dexp, float* dx, float* dW, hipStream_t s) {
+                               int P, int R, const int* bucket, float* dexp, float* dx, float* dW, hipStream_t s) {
   if (B == 0) return;
-  const int gz = ra_groups(((B + 63) / 64) * ((C + 63) / 64), R);
-  PBX_RA_DISPATCH(k_ra_dexp, dim3((B + 63) / 64, (C + 63) / 64, gz), dout, ro, ld, W, B, C, P, dexp);
+  const int* perm = bucket;
+  const int* meta = bucket + B;
+  PBX_RA_DISPATCH(k_ra_dexp, dim3(ra_max_tiles(B, R), (R * C + 63) / 64), 256, dout, ro, ld, W, B, C, P, perm, meta,
+                  dexp);
   hipLaunchKernelGGL(k_ra_dx, dim3(nblk((int64_t)B * C)), dim3(256), 0, s, dexp, ro, ld, B, C, R, dx);
-  const int splits = B > 4096 ? 8 : (B > 512 ? 4 : 1);
-  const int per = (B + splits - 1) / splits;
-  hipLaunchKernelGGL(k_ra_dw, dim3((C + 63) / 64, (P + 63) / 64, R * R * splits), dim3(256), 0, s, x, dout, ro, ld, B,
-                     C, P, R, per, dW);
+  // ~128 instances per split at an even rank mix; dW zeroed by the caller
+  int splits = (B + R * 128 - 1) / (R * 128);
+  splits = splits < 1 ? 1 : (splits > 64 ? 64 : splits);
+  PBX_RA_DISPATCH(k_ra_dw, dim3((R * C + 63) / 64, (P + 63) / 64, R * splits), 256, x, dout, ro, ld, B, C, P, perm,
+                  meta, splits, dW);
 }
 
 void launch_cvm_fwd(const float* x, int64_t n, int W, bool use_cvm, float* y, hipStream_t s) {

@@ -745,11 +745,15 @@ void launch_i8_quant(const float* x, int R, int C, int ldo, float expand, float 
                      signed char* out, hipStream_t s);
 void launch_i8_gemm(const signed char* qx, const signed char* qwt, int M, int N, int Kp, float scale,
                     const float* bias, float* y, int ldy, hipStream_t s);
+// rank_attention, rank-bucketed (ctr_ext.hip): the forward counting-sorts the
+// instances by rank into `bucket` (rank_attention_bucket_ints(B, R) ints:
+// permutation + tile table), which the backward reuses.
+int rank_attention_bucket_ints(int B, int R);
 void launch_rank_attention_fwd(const float* x, const int* ro, int ld, const float* W, int B, int C, int P, int R,
-                               float* out, hipStream_t s);
-// dexp: scratch [B][R][C]; dx overwritten; dW accumulated (atomics)
+                               int* bucket, float* out, hipStream_t s);
+// dexp: scratch [B][R][C]; dx overwritten; dW accumulated (atomics: zero it first)
 void launch_rank_attention_bwd(const float* x, const float* dout, const int* ro, int ld, const float* W, int B, int C,
-                               int P, int R, float* dexp, float* dx, float* dW, hipStream_t s);
+                               int P, int R, const int* bucket, float* dexp, float* dx, float* dW, hipStream_t s);
 void launch_cvm_fwd(const float* x, int64_t n, int W, bool use_cvm, float* y, hipStream_t s);
 void launch_cvm_bwd(const float* dy, const float* cvm, int64_t n, int W, bool use_cvm, int cvm_rows, float* dx,
                     hipStream_t s);

@@ -634,8 +634,8 @@ def _rank_gather(x, rank_offset, W, max_rank):
         faster = ro[:, 2 * k + 1] - 1
         raw = ro[:, 2 * k + 2]
         idx = raw.clamp(0, B - 1)
-        ok = (lower >= 0) & (faster >= 0) & (raw >= 0) & (raw < B)
-        blk = (lower.clamp(min=0) * R + faster.clamp(min=0))
+        ok = (lower >= 0) & (lower < R) & (faster >= 0) & (faster < R) & (raw >= 0) & (raw < B)
+        blk = torch.where(ok, lower * R + faster, torch.zeros_like(lower))
         xs.append(x[idx] * ok.unsqueeze(1).to(x.dtype))
         ws.append(blk)
         valid.append(ok)
@@ -656,23 +656,27 @@ def rank_attention(x: torch.Tensor, rank_offset: torch.Tensor, W: torch.Tensor, 
 
 
 class _RankAttentionHip(torch.autograd.Function):
-    """GPU rank_attention: k_ra_fwd stages each used W block through LDS for
-    a 64-instance tile; backward = k_ra_dexp (per-peer input gradient),
-    k_ra_dx (the reference's gather-form merge, rank_attention.cu.h:120-190)
-    and k_ra_dw (per-block parameter gradient)."""
+    """GPU rank_attention, rank-bucketed (csrc/hip/ctr_ext.hip): k_ra_bucket
+    counting-sorts the instances by their own rank; an instance of rank r uses
+    only W_r = W[r*R*C:(r+1)*R*C], so each rank's tiles are dense GEMMs with
+    the peer rows gathered on load -- k_ra_fwd (out = A W_r), k_ra_dexp
+    (dout W_r^T scattered to the per-peer rows), k_ra_dx (the reference's
+    gather-form merge, rank_attention.cu.h:120-190) and k_ra_dw (A^T dout per
+    rank, split over instances)."""
 
     @staticmethod
     def forward(ctx, x, ro, W, R):
         h = _native.hip()
-        ctx.save_for_backward(x, ro, W)
+        out, bucket = h.rank_attention_fwd(x, ro, W.contiguous(), R)
+        ctx.save_for_backward(x, ro, W, bucket)
         ctx.R = R
-        return h.rank_attention_fwd(x, ro, W.contiguous(), R)
+        return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, ro, W = ctx.saved_tensors
+        x, ro, W, bucket = ctx.saved_tensors
         h = _native.hip()
-        dx, dW = h.rank_attention_bwd(x, ro, W.contiguous(), dout.contiguous(), ctx.R)
+        dx, dW = h.rank_attention_bwd(x, ro, W.contiguous(), dout.contiguous(), bucket, ctx.R)
         return dx, None, dW, None
 
 

@@ -2,14 +2,18 @@
 import torch
 
 
-def page_view_ranks(n_pv: int, R: int, gen: torch.Generator) -> torch.Tensor:
+def page_view_ranks(n_pv: int, R: int, gen: torch.Generator, p_single: float = 0.0) -> torch.Tensor:
     """rank_offset [ins, 2R+1] for n_pv page views of 1..R+1 ads each: an ad
     shown at rank r <= R lists every ad of its page view with rank <= R at
     slot r'-1 as (r', instance index); ranks > R are -1 (the layout the
-    reference's rank_attention test builds, test_rank_attention_op.py:109)."""
+    reference's rank_attention test builds, test_rank_attention_op.py:109).
+    A page view holds a single ad with probability ``p_single`` (skews the
+    instances towards rank 1)."""
     rows = []
     for _ in range(n_pv):
         n = int(torch.randint(1, R + 2, (1,), generator=gen))
+        if p_single and float(torch.rand(1, generator=gen)) < p_single:
+            n = 1
         ranks = (torch.randperm(n, generator=gen) + 1).tolist()
         start = len(rows)
         for r in ranks:

@@ -49,6 +49,25 @@ def test_rank_attention_gpu(R):
     _close(wg.grad, wc.grad, rtol=1e-4, atol=1e-3)
 
 
+def test_rank_attention_gpu_skewed_ranks():
+    """Most instances have rank 1 (one bucket spans several dW segments and
+    splits; B is not a tile multiple); page views larger than R give rank-less
+    instances."""
+    g = torch.Generator().manual_seed(11)
+    R, C, P = 8, 64, 64
+    ro = page_view_ranks(2400, R, g, p_single=0.85)
+    B = ro.shape[0]
+    (xc, xg), (wc, wg) = _pair(torch.rand(B, C, generator=g), torch.rand(R * R * C, P, generator=g))
+    yc = cx.rank_attention(xc, ro, wc, R)
+    yg = cx.rank_attention(xg, ro.to(DEV), wg, R)
+    _close(yg, yc, atol=1e-3)
+    d = torch.randn(B, P, generator=g)
+    yc.backward(d.double())
+    yg.backward(d.to(DEV))
+    _close(xg.grad, xc.grad, atol=1e-3)
+    _close(wg.grad, wc.grad, rtol=1e-4, atol=2e-3)
+
+
 @pytest.mark.parametrize("mode", ["default", "transpose", "batchcount"])
 def test_batch_fc_gpu(mode):
     g = torch.Generator().manual_seed(5)
