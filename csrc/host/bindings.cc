@@ -673,7 +673,33 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("select_ge", [](const HostTier& t, int col, float thr) {
         std::vector<uint64_t> k;
         std::vector<float> v;
-        t.select_ge(col, thr, &k, &v);
+        {
+          py::gil_scoped_release g;
+          t.select_ge(col, thr, &k, &v);
+        }
+        return py::make_tuple(to_tensor_u64(k), to_tensor_f(v, t.stride()));
+      })
+      .def("stamp", [](HostTier& t, const Tensor& rows, int64_t epoch) {
+        auto rc = rows.contiguous();
+        py::gil_scoped_release g;
+        t.stamp(rc.data_ptr<int64_t>(), rc.numel(), (uint32_t)epoch);
+      })
+      .def("epochs", [](const HostTier& t, const Tensor& rows) {
+        auto rc = rows.contiguous();
+        auto out = torch::empty({rc.numel()}, torch::kInt64);
+        for (int64_t i = 0; i < rc.numel(); ++i) {
+          const int64_t r = rc.data_ptr<int64_t>()[i];
+          out.data_ptr<int64_t>()[i] = r < 0 ? -1 : (int64_t)t.epoch_of_row(r);
+        }
+        return out;
+      })
+      .def("spill_oldest", [](HostTier& t, int64_t keep_rows) {
+        std::vector<uint64_t> k;
+        std::vector<float> v;
+        {
+          py::gil_scoped_release g;
+          t.spill_oldest(keep_rows, &k, &v);
+        }
         return py::make_tuple(to_tensor_u64(k), to_tensor_f(v, t.stride()));
       })
       .def("clear", &HostTier::clear);

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <map>
 #include <memory>
 #include <sstream>
 #include <stdexcept>
@@ -58,6 +59,7 @@ HostTier::HostTier(int stride, int threads, int64_t chunk_rows)
   node_cpus_ = numa_topology();
   // chunk pointers never move: readers index chunks_ while a writer appends
   chunks_.reserve(kMaxChunks);
+  epochs_.reserve(kMaxChunks);
   pool_ = std::make_unique<ThreadPool>(threads < 1 ? 1 : threads);
   for (auto& s : shards_) {
     s.keys.assign(1024, kEmptyKey);
@@ -92,6 +94,7 @@ void HostTier::add_chunks(int count) {
       std::memset(p, 0, bytes);
     });
     chunks_.push_back(static_cast<float*>(p));
+    epochs_.emplace_back(new uint32_t[chunk_rows_]());
   }
   for (auto& t : th) t.join();
 }
@@ -299,21 +302,95 @@ void HostTier::export_all(std::vector<uint64_t>* keys, std::vector<float>* vals)
   }
 }
 
+void HostTier::extract(const std::function<bool(int64_t, const float*)>& pred, bool erase,
+                       std::vector<uint64_t>* keys, std::vector<float>* vals) {
+  std::vector<std::vector<uint64_t>> lk(kShards);
+  std::vector<std::vector<float>> lv(kShards);
+  std::vector<std::vector<int64_t>> freed(kShards);
+  pool_->parallel_range(kShards, [&](int, int64_t b, int64_t e) {
+    for (int64_t si = b; si < e; ++si) {
+      Shard& s = shards_[si];
+      std::lock_guard<std::mutex> g(s.mu);
+      for (size_t j = 0; j < s.keys.size(); ++j) {
+        if (s.keys[j] == kEmptyKey || s.keys[j] == kTomb) continue;
+        const int64_t r = s.rows[j];
+        const float* v = row_ptr(r);
+        if (!pred(r, v)) continue;
+        lk[si].push_back(s.keys[j]);
+        lv[si].insert(lv[si].end(), v, v + stride_);
+        if (erase) {
+          freed[si].push_back(r);
+          s.keys[j] = kTomb;
+          s.rows[j] = -1;
+          --s.live;
+        }
+      }
+    }
+  });
+  keys->clear();
+  vals->clear();
+  size_t n = 0;
+  for (auto& k : lk) n += k.size();
+  keys->reserve(n);
+  vals->reserve(n * stride_);
+  for (int si = 0; si < kShards; ++si) {
+    keys->insert(keys->end(), lk[si].begin(), lk[si].end());
+    vals->insert(vals->end(), lv[si].begin(), lv[si].end());
+  }
+  if (erase) {
+    std::lock_guard<std::mutex> g(alloc_mu_);
+    for (auto& f : freed) free_rows_.insert(free_rows_.end(), f.begin(), f.end());
+  }
+}
+
 void HostTier::select_ge(int col, float thr, std::vector<uint64_t>* keys, std::vector<float>* vals) const {
   keys->clear();
   vals->clear();
   if (col < 0 || col >= stride_) return;
-  for (auto& s : shards_) {
-    std::lock_guard<std::mutex> lk(s.mu);
-    for (size_t j = 0; j < s.keys.size(); ++j) {
-      if (s.keys[j] == kEmptyKey || s.keys[j] == kTomb) continue;
-      const float* v = row_ptr(s.rows[j]);
-      if (v[col] >= thr) {
-        keys->push_back(s.keys[j]);
-        vals->insert(vals->end(), v, v + stride_);
-      }
+  const_cast<HostTier*>(this)->extract([&](int64_t, const float* v) { return v[col] >= thr; }, false, keys, vals);
+}
+
+void HostTier::stamp(const int64_t* rows, int64_t n, uint32_t epoch) {
+  pool_->parallel_range(n, [&](int, int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i)
+      if (rows[i] >= 0) epochs_[rows[i] / chunk_rows_][rows[i] % chunk_rows_] = epoch;
+  });
+}
+
+int64_t HostTier::spill_oldest(int64_t keep_rows, std::vector<uint64_t>* keys, std::vector<float>* vals) {
+  keys->clear();
+  vals->clear();
+  const int64_t need = size() - (keep_rows < 0 ? 0 : keep_rows);
+  if (need <= 0) return 0;
+  // pass histogram over the live rows
+  std::vector<std::map<uint32_t, int64_t>> hs(kShards);
+  pool_->parallel_range(kShards, [&](int, int64_t b, int64_t e) {
+    for (int64_t si = b; si < e; ++si) {
+      const Shard& s = shards_[si];
+      std::lock_guard<std::mutex> g(s.mu);
+      for (size_t j = 0; j < s.keys.size(); ++j)
+        if (s.keys[j] != kEmptyKey && s.keys[j] != kTomb) hs[si][epoch_of_row(s.rows[j])]++;
     }
+  });
+  std::map<uint32_t, int64_t> h;
+  for (auto& m : hs)
+    for (auto& kv : m) h[kv.first] += kv.second;
+  // boundary pass T: every row of an older pass goes, then `quota` rows of T
+  uint32_t T = 0;
+  int64_t below = 0;
+  for (auto& kv : h) {
+    T = kv.first;
+    if (below + kv.second >= need) break;
+    below += kv.second;
   }
+  std::atomic<int64_t> quota{need - below};
+  extract(
+      [&](int64_t r, const float*) {
+        const uint32_t e = epoch_of_row(r);
+        return e < T || (e == T && quota.fetch_sub(1, std::memory_order_relaxed) > 0);
+      },
+      true, keys, vals);
+  return (int64_t)keys->size();
 }
 
 int64_t HostTier::shrink(float decay, int unseen_col, float nonclk_coeff, float clk_coeff, float delete_threshold,
@@ -359,6 +436,10 @@ void HostTier::clear() {
   std::lock_guard<std::mutex> lk(alloc_mu_);
   free_rows_.clear();
   next_row_ = 0;
+  // insert() relies on never-used arena rows being zero: release the arena
+  for (float* c : chunks_) munmap(c, (size_t)chunk_rows_ * stride_ * sizeof(float));
+  chunks_.clear();
+  epochs_.clear();
 }
 
 // ====================================================================== SsdLog

@@ -24,6 +24,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -53,6 +54,13 @@ class HostTier {
   void export_all(std::vector<uint64_t>* keys, std::vector<float>* vals) const;
   // keys/rows whose column `col` >= thr (cold rows for the SSD spill)
   void select_ge(int col, float thr, std::vector<uint64_t>* keys, std::vector<float>* vals) const;
+  // pass stamps: every arena row carries the id of the pass that last wrote
+  // it (write-back / SSD reload); spill_oldest removes the rows of the oldest
+  // passes (whole passes, then part of the boundary pass) until at most
+  // keep_rows remain, returning them for the SSD tier.  Parallel over shards.
+  void stamp(const int64_t* rows, int64_t n, uint32_t epoch);
+  int64_t spill_oldest(int64_t keep_rows, std::vector<uint64_t>* keys, std::vector<float>* vals);
+  uint32_t epoch_of_row(int64_t r) const { return epochs_[r / chunk_rows_][r % chunk_rows_]; }
   // end-of-day shrink over every row, in parallel over the shards
   // (ctr_accessor.cc:63-80): show/click *= decay, unseen_days += 1, delete
   // rows with score < delete_threshold or unseen_days > max_unseen.
@@ -78,11 +86,15 @@ class HostTier {
   float* row_ptr(int64_t r) const { return chunks_[r / chunk_rows_] + (r % chunk_rows_) * stride_; }
   void add_chunk();
   void add_chunks(int count);
+  // rows matching pred(row, values), in shard order; erased from the tier when `erase`
+  void extract(const std::function<bool(int64_t, const float*)>& pred, bool erase, std::vector<uint64_t>* keys,
+               std::vector<float>* vals);
 
   int stride_;
   int64_t chunk_rows_;
   std::vector<Shard> shards_;
   std::vector<float*> chunks_;
+  std::vector<std::unique_ptr<uint32_t[]>> epochs_;  // one stamp per arena row, chunked like chunks_
   std::vector<int64_t> free_rows_;
   int64_t next_row_ = 0;
   std::mutex alloc_mu_;

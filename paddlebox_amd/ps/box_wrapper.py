@@ -164,7 +164,8 @@ class BoxWrapper:
                 self.ssd = SsdTier(os.path.join(p, f"rank{self.rank:05d}"), self.host.stride)
             if self.device.type == "cuda":
                 self.tier = TieredStore(self.engine, self.host, self.ssd, self.cfg.sgd,
-                                        spill_unseen=self.cfg.tier.spill_unseen_days)
+                                        spill_unseen=self.cfg.tier.spill_unseen_days,
+                                        host_cap_rows=self.cfg.tier.ssd_spill_threshold)
         if model_path:
             self.load_model(model_path)
         return 0
@@ -297,8 +298,13 @@ class BoxWrapper:
             with self.timers.span("end_pass_writeback"):
                 h, v = eng.table.export(True)
                 self.host.assign(h.cpu(), v.cpu())
+                self.host.stamp_keys(h.cpu(), self.pass_id)
                 if self.ssd is not None:
                     self._spill_cold()
+                    cap = int(self.cfg.tier.ssd_spill_threshold)
+                    if cap > 0:
+                        ck, cv = self.host._native.spill_oldest(cap)
+                        self.ssd.put(ck, cv)
         if _flags.get_bool("enable_force_hbm_recyle") and self.device.type == "cuda":
             torch.cuda.empty_cache()
         if _flags.get_bool("enable_force_mem_recyle"):

@@ -80,7 +80,7 @@ class TierConfig:
     load_factor: float = 0.8
     host_enabled: bool = True
     ssd_path: Optional[str] = None
-    ssd_spill_threshold: int = 0  # features kept in host RAM before spilling
+    ssd_spill_threshold: int = 0  # host-tier row cap: rows of the oldest passes spill to SSD beyond it (0 = off)
     spill_unseen_days: float = 1.0  # host rows unseen this long move to the SSD tier at EndPass
 
 

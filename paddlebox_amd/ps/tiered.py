@@ -18,10 +18,12 @@ box_wrapper.cc:120-210).  MI355X design:
   their canonical fp32 layout (``FeatureCodec.decode`` / ``encode``): the
   host and SSD tiers never see the packed device encoding.
 * EndPass exports the live table (a device copy) and a background thread
-  moves it D2H into the host tier and spills rows unseen for
-  ``spill_unseen`` days to the log-structured SSD tier -- overlapped with the
-  next pass's training.  Staging of pass n+2 waits for write-back of pass n,
-  so every staged value is current.
+  moves it D2H into the host tier and spills to the log-structured SSD tier
+  -- overlapped with the next pass's training.  Two spill rules: rows unseen
+  for ``spill_unseen`` days, and a host-tier row cap (``host_cap_rows``):
+  every host row carries the id of the pass that last wrote it, and the rows
+  of the oldest passes move to SSD until the cap holds.  Staging of pass n+2
+  waits for write-back of pass n, so every staged value is current.
 """
 from __future__ import annotations
 
@@ -69,6 +71,10 @@ class HostTable:
     def assign(self, h: torch.Tensor, vals: torch.Tensor):
         rows = self.probe(h)
         self._native.scatter(rows, vals.cpu().float())
+
+    def stamp_keys(self, h: torch.Tensor, epoch: int):
+        """Pass stamp of the rows of h (the spill_oldest order)."""
+        self._native.stamp(self.probe(h), int(epoch))
 
     def read(self, h: torch.Tensor) -> torch.Tensor:
         rows = self.probe(h)
@@ -145,7 +151,7 @@ class SsdTier:
 
 class TieredStore:
     def __init__(self, engine, host: HostTable, ssd: Optional[SsdTier] = None, sgd: Optional[SparseSGDConfig] = None,
-                 spill_unseen: float = 1.0):
+                 spill_unseen: float = 1.0, host_cap_rows: int = 0):
         from .gpu_table import GpuSparseTable
 
         self.engine = engine
@@ -153,6 +159,8 @@ class TieredStore:
         self.ssd = ssd
         self.sgd = sgd or engine.cfg.sgd
         self.spill_unseen = spill_unseen
+        self.host_cap_rows = int(host_cap_rows)
+        self.epoch = 0  # pass stamp of host rows: write-back count
         live = engine.table
         self.live = live
         if live.codec is not None:
@@ -177,8 +185,8 @@ class TieredStore:
         self._tier_lock = threading.Lock()
         self._staged_keys: Optional[torch.Tensor] = None
         self._pin = {}  # reusable pinned staging buffers (pinning is slow)
-        self.stats = {"stage_s": 0.0, "writeback_s": 0.0, "activate_s": 0.0, "ssd_hits": 0, "spilled": 0,
-                      "staged_rows": 0, "new_rows": 0}
+        self.stats = {"stage_s": 0.0, "writeback_s": 0.0, "activate_s": 0.0, "spill_s": 0.0, "ssd_hits": 0,
+                      "spilled": 0, "spilled_cap": 0, "staged_rows": 0, "new_rows": 0, "host_rows_staged": 0}
 
     def _pinned(self, name: str, shape, dtype) -> torch.Tensor:
         n = 1
@@ -217,6 +225,7 @@ class TieredStore:
                     mk = hc[miss][found]
                     r, _ = self.host._native.insert(mk)
                     self.host._native.scatter(r, vals[found])
+                    self.host._native.stamp(r, self.epoch)  # reloaded for the coming pass: newest
                     self.ssd.delete(mk)
                     self.stats["ssd_hits"] += int(mk.numel())
                     rows = self.host.probe(hc)
@@ -238,6 +247,7 @@ class TieredStore:
                 self._staged_keys = hd
                 self.stream.synchronize()
             self.stats["staged_rows"] += int(kh.numel())
+            self.stats["host_rows_staged"] += int(kh.numel())
             self.stats["new_rows"] += int(miss.sum())
             self.stats["stage_s"] += time.perf_counter() - t0
         except BaseException as e:  # surfaced by wait_stage
@@ -309,15 +319,26 @@ class TieredStore:
 
     def _wb_locked(self, kh, vh):
         """Host scatter of the written-back rows, then the SSD spill (holds the tier lock)."""
+        self.epoch += 1
         rows, _ = self.host._native.insert(kh)
         self.host._native.scatter(rows, vh)
+        self.host._native.stamp(rows, self.epoch)
         if self.ssd is not None:
             l = self.host.layout
-            ck, cv = self.host._native.select_ge(l["unseen_days"], float(self.spill_unseen))
-            if ck.numel():
-                self.ssd.put(ck, cv)
-                self.host.erase(ck)
-                self.stats["spilled"] += int(ck.numel())
+            t0 = time.perf_counter()
+            if self.spill_unseen >= 0:
+                ck, cv = self.host._native.select_ge(l["unseen_days"], float(self.spill_unseen))
+                if ck.numel():
+                    self.ssd.put(ck, cv)
+                    self.host.erase(ck)
+                    self.stats["spilled"] += int(ck.numel())
+            if self.host_cap_rows > 0:
+                ck, cv = self.host._native.spill_oldest(self.host_cap_rows)
+                if ck.numel():
+                    self.ssd.put(ck, cv)
+                    self.stats["spilled"] += int(ck.numel())
+                    self.stats["spilled_cap"] += int(ck.numel())
+            self.stats["spill_s"] += time.perf_counter() - t0
 
     def wait_writeback(self):
         with self._wb_lock:

@@ -1,10 +1,23 @@
 #!/usr/bin/env python3
-"""Scaled-down tiered-store run (BASELINE config 4 shape): DeepFM passes over
-a feature space larger than the HBM cap, HBM <- host (<- SSD) staging of the
-next pass overlapped with training, write-back overlapped with the next pass.
-Prints per-pass timings and the tier statistics (stderr) and one JSON line.
+"""BASELINE config 4 shape: the graph-captured fp32 DeepFM step (bench.py's
+CtrTrainStep) trained pass by pass over a feature space much larger than the
+HBM table, through the HBM <- host <- SSD tiers:
 
-    python scripts/tier_bench.py --passes 6 --steps 40 --features 5e7 --hbm-cap 4e6 [--ssd DIR]
+* every pass's batches are generated on the GPU before timing (synthetic
+  Criteo-shaped, power-law ids) and fed to the captured step device-to-device;
+* FeedPass of pass p+1 stages its working set (host probe, SSD reload, gather,
+  H2D, insert into the second GPU table) in the background while pass p trains;
+* EndPass exports the live table and writes it back (D2H, host scatter, pass
+  stamps, SSD spill of the oldest passes beyond ``--host-cap`` rows) in the
+  background while pass p+1 trains;
+* ``--mode hbm`` trains the same passes from one all-in-HBM table for the
+  reference point.
+
+Per pass (stderr): begin/train/end times and whether the background staging /
+write-back finished inside the training window.  One JSON line on stdout.
+
+    python scripts/tier_bench.py --mode tiered --passes 5 --steps 1000 \\
+        --features 1e9 --hbm-cap 6e7 --host-cap 1e8 --ssd /tmp/pbx_ssd
 """
 import argparse
 import json
@@ -17,79 +30,110 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from paddlebox_amd.data.synthetic import CriteoSynth  # noqa: E402
-from paddlebox_amd.models.deepfm import DeepFM  # noqa: E402
-from paddlebox_amd.parallel.dense import DenseArena, FlatAdam  # noqa: E402
 from paddlebox_amd.ps.box_wrapper import BoxWrapper  # noqa: E402
+from paddlebox_amd.runtime.ctr_step import CtrTrainStep  # noqa: E402
+from paddlebox_amd.runtime.graph_step import GraphedTrainStep, pack_batch  # noqa: E402
+
+
+def log(msg):
+    print(msg, file=sys.stderr, flush=True)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--passes", type=int, default=6)
-    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--passes", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--batch", type=int, default=8192)
-    ap.add_argument("--features", type=float, default=5e7)
-    ap.add_argument("--hbm-cap", type=float, default=4e6)
+    ap.add_argument("--features", type=float, default=1e9)
+    ap.add_argument("--hbm-cap", type=float, default=6e7)
+    ap.add_argument("--host-cap", type=float, default=0, help="host-tier rows before the oldest passes spill to SSD")
     ap.add_argument("--ssd", type=str, default="")
     ap.add_argument("--mode", choices=("tiered", "hbm"), default="tiered")
-    ap.add_argument("--spill-unseen", type=float, default=1.0,
-                    help="write-back spills host rows unseen for >= this many days to SSD (0: every written-back row)")
+    ap.add_argument("--spill-unseen", type=float, default=-1.0,
+                    help="also spill host rows unseen for >= this many days (-1: off)")
+    ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     synth = CriteoSynth(total_features=int(args.features), alpha=1.05, seed=7, device=str(dev))
     S = synth.S
-    cap = int(args.hbm_cap) if args.mode == "tiered" else int(args.features)
     box = BoxWrapper(8, device=dev)
     box.cfg.tier.spill_unseen_days = args.spill_unseen
+    box.cfg.tier.ssd_spill_threshold = int(args.host_cap)
+    # hbm mode: a table sized for every key the passes touch
+    cap = int(args.hbm_cap) if args.mode == "tiered" else int(args.hbm_cap) * args.passes
     box.initialize_gpu_and_load_model(slot_vector=list(range(1, S + 1)), max_keys=args.batch * S, capacity=cap,
-                                      mode=args.mode, ssd_path=args.ssd or None)
-    model = DeepFM(box.engine, num_slots=S, dense_dim=13, hidden=(400, 400, 400)).to(dev)
-    arena = DenseArena(model.parameters(), dev)
-    opt = FlatAdam(arena, lr=1e-3, clear_grad=True).fuse(mlps=[model.mlp], data_norms=[model.dn])
-    one = torch.ones((), device=dev)
-    passes = [[synth.batch(args.batch) for _ in range(args.steps)] for _ in range(args.passes)]
+                                      mode=args.mode, ssd_path=(args.ssd or None) if args.mode == "tiered" else None)
+    t0 = time.perf_counter()
+    passes = []
+    for p in range(args.passes):
+        passes.append([pack_batch(synth.batch(args.batch), device=dev) for _ in range(args.steps)])
     keys = [torch.cat([b.keys for b in bs]) for bs in passes]
+    torch.cuda.synchronize()
+    log(f"[tier] generated {args.passes} x {args.steps} batches in {time.perf_counter() - t0:.1f} s")
+    torch.manual_seed(0)
+    step = CtrTrainStep(box.engine, "deepfm", args.precision, num_slots=S, hidden=(400, 400, 400))
+    rows, bg = [], []
     t_all = time.perf_counter()
     box.feed_pass(keys[0])
-    rows = []
+    g = None
     for p in range(args.passes):
+        st0 = dict(box.tier.stats) if box.tier is not None else {}
         t0 = time.perf_counter()
         box.begin_pass()
         t1 = time.perf_counter()
         if p + 1 < args.passes:
             box.feed_pass(keys[p + 1])  # staged in the background while this pass trains
         t2 = time.perf_counter()
-        for b in passes[p]:
-            loss, _ = model(b)
-            loss.backward(one)
-            opt.step()
+        bs = passes[p]
+        if g is None:
+            # capture once (the live table never moves); the warm step trains batch 0
+            g = GraphedTrainStep(step.train_step, bs[0], dev, warmup=0, warm_batches=[bs[0]])
+            first = 1
+        else:
+            first = 0
+        g.load(first % g.n, bs[first])
+        for i in range(first, len(bs)):
+            if i + 1 < len(bs):
+                g.load((i + 1) % g.n, bs[i + 1])
+            g.run(i % g.n)
         torch.cuda.synchronize()
         t3 = time.perf_counter()
+        # did the background work of this window finish while the pass trained?
+        stage_done = box.tier is None or box.tier._stage_thread is None or not box.tier._stage_thread.is_alive()
+        wb_done = box.tier is None or box.tier._wb_thread is None or not box.tier._wb_thread.is_alive()
         box.end_pass()
         t4 = time.perf_counter()
-        rows.append(dict(pass_id=p, begin_pass_ms=(t1 - t0) * 1e3, feed_call_ms=(t2 - t1) * 1e3,
-                         train_ms=(t3 - t2) * 1e3, end_pass_ms=(t4 - t3) * 1e3,
-                         live_rows=box.engine.table.size()))
-        print("[tier]", json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in rows[-1].items()}),
-              file=sys.stderr, flush=True)
+        st1 = dict(box.tier.stats) if box.tier is not None else {}
+        d = {k: st1[k] - st0.get(k, 0) for k in st1}
+        r = dict(pass_id=p, begin_pass_ms=(t1 - t0) * 1e3, feed_call_ms=(t2 - t1) * 1e3, train_ms=(t3 - t2) * 1e3,
+                 end_pass_ms=(t4 - t3) * 1e3, live_rows=box.engine.table.size(),
+                 stage_done_in_pass=stage_done, writeback_done_in_pass=wb_done,
+                 host_rows=box.host.size() if box.host is not None else 0,
+                 ssd_rows=len(box.ssd) if box.ssd is not None else 0)
+        r.update({f"d_{k}": v for k, v in d.items()})
+        rows.append(r)
+        log("[tier] " + json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
     if box.tier is not None:
         box.tier.wait_writeback()
     wall = time.perf_counter() - t_all
     st = dict(box.tier.stats) if box.tier is not None else {}
+    steady = rows[1:] if len(rows) > 1 else rows
+    train_s = sum(r["train_ms"] for r in rows) / 1e3
     out = {
-        "mode": args.mode, "passes": args.passes, "steps_per_pass": args.steps, "batch": args.batch,
-        "features": int(args.features), "hbm_cap_rows": cap, "wall_s": round(wall, 3),
-        "samples_per_s": round(args.passes * args.steps * args.batch / wall, 1),
-        "train_ms_mean": round(sum(r["train_ms"] for r in rows[1:]) / max(1, len(rows) - 1), 2),
-        "begin_pass_ms_mean": round(sum(r["begin_pass_ms"] for r in rows[1:]) / max(1, len(rows) - 1), 2),
-        "end_pass_ms_mean": round(sum(r["end_pass_ms"] for r in rows[1:]) / max(1, len(rows) - 1), 2),
+        "mode": args.mode, "precision": args.precision, "passes": args.passes, "steps_per_pass": args.steps,
+        "batch": args.batch, "features": int(args.features), "hbm_cap_rows": cap, "host_cap_rows": int(args.host_cap),
+        "wall_s": round(wall, 3), "samples_per_s": round(args.passes * args.steps * args.batch / wall, 1),
+        "train_only_samples_per_s": round(args.passes * args.steps * args.batch / train_s, 1),
+        "train_ms_per_step": round(sum(r["train_ms"] for r in steady) / (len(steady) * args.steps), 4),
+        "begin_pass_ms_mean": round(sum(r["begin_pass_ms"] for r in steady) / len(steady), 2),
+        "end_pass_ms_mean": round(sum(r["end_pass_ms"] for r in steady) / len(steady), 2),
+        "live_rows_mean": int(sum(r["live_rows"] for r in rows) / len(rows)),
         "host_rows": box.host.size() if box.host is not None else 0,
         "ssd_rows": len(box.ssd) if box.ssd is not None else 0,
+        "stage_hidden_passes": sum(1 for r in rows if r["stage_done_in_pass"]),
+        "writeback_hidden_passes": sum(1 for r in rows if r["writeback_done_in_pass"]),
         "tier_stats": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()},
-        # staging of pass p+1 and write-back of pass p-1 run during pass p's training:
-        # the part of their time the training hid
-        "stage_s_total": round(st.get("stage_s", 0.0), 3),
-        "train_s_total": round(sum(r["train_ms"] for r in rows) / 1e3, 3),
         "ssd_direct_io": bool(box.ssd.direct_io) if box.ssd is not None else None,
     }
     print(json.dumps(out), flush=True)

@@ -125,3 +125,39 @@ def test_host_tier_native_shrink_matches_rule():
     assert t.size() == int(keep.sum())
     assert bool((t.probe(h[~keep]) == -1).all())
     torch.testing.assert_close(t.read(h[keep]), exp[keep])
+
+
+def test_host_tier_spill_oldest_passes_first():
+    """spill_oldest moves whole older passes first, then part of the boundary
+    pass, and returns exactly the removed rows with their values."""
+    t = HostTable(8, threads=4, chunk_rows=1024)
+    passes = [_keys(3000, 10 + p) for p in range(3)]
+    vals = {}
+    for p, h in enumerate(passes, start=1):
+        rows, _ = t._native.insert(h)
+        v = torch.randn(h.numel(), STRIDE)
+        t._native.scatter(rows, v)
+        t._native.stamp(rows, p)
+        for k, row in zip(h.tolist(), v):
+            vals[k] = row
+    union = torch.unique(torch.cat(passes))
+    total = t.size()
+    assert total == union.numel()
+    ep = t._native.epochs(t.probe(union))
+    n1 = int((ep == 1).sum())
+    keep = total - n1 - 500  # all of pass 1's surviving rows + 500 of pass 2's
+    k, v = t._native.spill_oldest(keep)
+    assert k.numel() == n1 + 500 and t.size() == keep
+    kep = dict(zip(union.tolist(), ep.tolist()))
+    spilled_ep = torch.tensor([kep[x] for x in k.tolist()])
+    assert int((spilled_ep == 1).sum()) == n1 and int((spilled_ep == 2).sum()) == 500
+    for i, x in enumerate(k.tolist()):
+        assert torch.equal(v[i], vals[x])
+    assert bool((t.probe(k) == -1).all())
+    # under the cap: nothing moves
+    k2, _ = t._native.spill_oldest(keep)
+    assert k2.numel() == 0
+    # clear releases the arena: re-inserted keys start from zero rows
+    t.clear()
+    t._native.insert(passes[0])
+    assert float(t.read(passes[0]).abs().sum()) == 0.0
