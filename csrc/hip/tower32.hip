@@ -465,10 +465,12 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
 }
 
 // ---------------------------------------------------------------- grouped dW
-constexpr int DSTEPS = 2;               // m16 steps per ring stage
-constexpr int DNST = 3;                 // ring stages (48 KB: two dW workgroups per CU leave room for the
-                                        // head backward that runs beside them on the compute stream)
-constexpr int DSTAGE = DSTEPS * 8 * 256;  // floats per stage: 8 chunks of 1 KB per step (4 dZ, 4 X)
+// Ring of NS stages of DS m16 steps each (8 KB of dZ + X chunks per step).
+// Stage s+NS-1 is issued while stage s is consumed, so NS-1 stages (the
+// latency budget) are in flight.  Variants (PBX_T32_DW_RING = DSxNS):
+// 2x3 (48 KB, two workgroups per CU beside the head backward), 1x6 (48 KB,
+// deeper in time), 2x4 (64 KB), 2x5 (80 KB).
+constexpr int kDwStep = 8 * 256;  // floats per m16 step: 8 chunks of 1 KB (4 dZ, 4 X)
 
 __device__ __forceinline__ int dw32_tiles(const TowerLayerDev& ly) {
   return ((ly.Np / 16 + 3) / 4) * ((ly.Kp / 16 + 3) / 4);
@@ -479,13 +481,28 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// wait until at most `ahead` stages of 2*DS loads are outstanding
+template <int DS>
+__device__ __forceinline__ void wait_stages(int ahead) {
+  switch (ahead) {
+    case 0: wait_vm<0>(); break;
+    case 1: wait_vm<2 * DS>(); break;
+    case 2: wait_vm<4 * DS>(); break;
+    case 3: wait_vm<6 * DS>(); break;
+    default: wait_vm<8 * DS>(); break;
+  }
+}
+
+template <int DS, int NS>
 __global__ __launch_bounds__(256) void k_t32_dw(TowerArgs a, int ndw) {
+  static_assert(NS >= 3 && NS - 2 <= 4, "wait_stages covers up to 4 stages ahead");
+  constexpr int DSTEPS = DS, DNST = NS, DSTAGE = DS * kDwStep;
   const int tid = threadIdx.x;
   if ((int)blockIdx.x >= ndw) {
     tower_col_reduce(a, (int)blockIdx.x - ndw, BM);
     return;
   }
-  __shared__ __attribute__((aligned(16))) float smem[DNST * DSTAGE];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int S = a.dw_splits;
   int t, split;
   if (S == 8) {
@@ -541,10 +558,8 @@ __global__ __launch_bounds__(256) void k_t32_dw(TowerArgs a, int ndw) {
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   for (int p = 0; p < DNST - 1 && p < nstage; ++p) issue(p, p);
   for (int s = 0; s < nstage; ++s) {
-    const int ahead = min(DNST - 2, nstage - 1 - s);
-    if (ahead >= 2) wait_vm<4 * DSTEPS>();
-    else if (ahead == 1) wait_vm<2 * DSTEPS>();
-    else wait_vm<0>();
+    // stages s .. s + ahead are outstanding; stage s must have landed
+    wait_stages<DSTEPS>(min(DNST - 2, nstage - 1 - s));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (s + DNST - 1 < nstage) issue((s + DNST - 1) % DNST, s + DNST - 1);
@@ -702,7 +717,39 @@ void launch_tower32_dw(const TowerArgs& a, hipStream_t s) {
   for (int l = 0; l < a.L; ++l) tiles += ((a.ly[l].Np / 16 + 3) / 4) * ((a.ly[l].Kp / 16 + 3) / 4);
   const int ndw = tiles * a.dw_splits;
   const int nred = (a.bias_ld + 31) / 32 + (a.dn_part ? (a.dn_C + 31) / 32 : 0);
-  hipLaunchKernelGGL(k_t32_dw, dim3(ndw + nred), dim3(256), 0, s, a, ndw);
+  static const int ring = [] {
+    const char* e = getenv("PBX_T32_DW_RING");
+    return e ? atoi(e) : 23;  // DS * 10 + NS
+  }();
+  const dim3 g(ndw + nred), b(256);
+  switch (ring) {
+    case 16: {
+      static const bool big = hipFuncSetAttribute((const void*)k_t32_dw<1, 6>,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 6 * kDwStep * 4) ==
+                              hipSuccess;
+      (void)big;
+      hipLaunchKernelGGL((k_t32_dw<1, 6>), g, b, 6 * kDwStep * 4, s, a, ndw);
+      break;
+    }
+    case 24: {
+      static const bool big = hipFuncSetAttribute((const void*)k_t32_dw<2, 4>,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 8 * kDwStep * 4) ==
+                              hipSuccess;
+      (void)big;
+      hipLaunchKernelGGL((k_t32_dw<2, 4>), g, b, 8 * kDwStep * 4, s, a, ndw);
+      break;
+    }
+    case 25: {
+      static const bool big = hipFuncSetAttribute((const void*)k_t32_dw<2, 5>,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 10 * kDwStep * 4) ==
+                              hipSuccess;
+      (void)big;
+      hipLaunchKernelGGL((k_t32_dw<2, 5>), g, b, 10 * kDwStep * 4, s, a, ndw);
+      break;
+    }
+    default:
+      hipLaunchKernelGGL((k_t32_dw<2, 3>), g, b, 6 * kDwStep * 4, s, a, ndw);
+  }
 }
 
 void launch_tower32_pack(const TowerArgs& a, const float* const* w, hipStream_t s) {
