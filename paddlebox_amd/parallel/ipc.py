@@ -18,7 +18,12 @@ Reference: the c_mixallgather / heter_comm peer copies
 (``c_mixallgather_op.cc:221-327``, ``heter_comm_inl.h:273-490``); here the
 memory handles are exchanged once over the process group and every later
 call is a single kernel.  Every rank must issue the same sequence of
-collectives on a mesh (as with RCCL).  A peer that never arrives makes the
+collectives on a mesh (as with RCCL).  The launches of one mesh are
+serialised on the mesh's own stream (forked from and joined back into the
+caller's stream): a launch reads the mesh epoch from device memory, so two
+collectives of one mesh in flight at once -- e.g. a data_norm statistics
+all-reduce on the tower's dW stream and a transpiled c_allreduce_sum on the
+compute stream -- would run under the same epoch.  A peer that never arrives makes the
 wait time out: the sticky error poisons the results (NaN sums, empty
 exchanges) and :meth:`check` raises on the host, instead of hanging the GPU
 or training on stale slots.
@@ -72,6 +77,7 @@ class IpcMesh:
         self.state = torch.zeros(4, dtype=torch.int64, device=self.device)
         self.comm = h.IpcComm(self.rank, W, self.slot_bytes, self.state, int(blocks), self.depth,
                               int(spin_limit or DEFAULT_SPIN_LIMIT))
+        self.stream = torch.cuda.Stream(self.device)  # every launch of this mesh, in issue order
         self._opened = []
         # no rank may raise between the collectives below (a peer would block
         # in them forever): failures are recorded and agreed on at the end
@@ -123,8 +129,30 @@ class IpcMesh:
         """In-place sum (or mean) over the ranks of a contiguous f32 tensor."""
         if two_phase is None:
             two_phase = self.world > 2 and t.numel() * 4 > (256 << 10)
-        self.comm.allreduce(t, t, 1.0 / self.world if average else 1.0, bool(two_phase))
+        with self._serial():
+            self.comm.allreduce(t, t, 1.0 / self.world if average else 1.0, bool(two_phase))
         return t
+
+    class _Serial:
+        def __init__(self, mesh):
+            self.m = mesh
+
+        def __enter__(self):
+            self.cur = torch.cuda.current_stream(self.m.device)
+            self.fork = self.cur != self.m.stream
+            if self.fork:
+                self.m.stream.wait_stream(self.cur)
+                self.ctx = torch.cuda.stream(self.m.stream)
+                self.ctx.__enter__()
+
+        def __exit__(self, *exc):
+            if self.fork:
+                self.ctx.__exit__(*exc)
+                self.cur.wait_stream(self.m.stream)
+            return False
+
+    def _serial(self):
+        return IpcMesh._Serial(self)
 
     def exchange(self, send: torch.Tensor, dst: Optional[torch.Tensor] = None, counts: Optional[torch.Tensor] = None,
                  rec_bytes: int = 16, fill_tail: bool = False, rcounts: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -133,7 +161,8 @@ class IpcMesh:
         or the whole slot); dst receives slot q from peer q.  Returns dst."""
         if dst is None:
             dst = torch.empty_like(send)
-        self.comm.exchange(send, dst, counts, int(rec_bytes), bool(fill_tail), rcounts)
+        with self._serial():
+            self.comm.exchange(send, dst, counts, int(rec_bytes), bool(fill_tail), rcounts)
         return dst
 
     def error(self) -> bool:
