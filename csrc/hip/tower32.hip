@@ -603,6 +603,150 @@ __global__ __launch_bounds__(256) void k_t32_dw(TowerArgs a, int ndw) {
   }
 }
 
+// Register-streamed dW (PBX_T32_DW_RING=0, the default when the split's
+// steps divide evenly): each wave owns the whole 64x64 tile for every 4th m16
+// step of its split (K split inside the workgroup), so its operands go
+// L2 -> VGPRs with global_load_dwordx4 -- a chunk's fragment order IS the
+// MFMA operand order -- in a ring of R steps: no LDS staging and no barrier
+// in the loop, and R-1 steps (8 loads each) in flight per wave.  The four
+// partial tiles meet in LDS at the end; one fp32 atomic per output element
+// and workgroup, as in k_t32_dw.
+// one wave's K loop of k_t32_dw_reg over a tile with VN x VK valid 16-blocks
+// (only valid chunks are loaded and multiplied: fixed load count per step)
+// NST > 0: the step count is NST and the loop is unrolled completely -- a
+// loop header merges the load-ordering state of its two edges and hipcc then
+// waits for all but the newest step there (1 step in flight per R)
+template <int R, int VN, int VK, int NST>
+__device__ __forceinline__ void dw_reg_loop(const float* const* pa, const float* const* pb, int64_t sA, int64_t sB,
+                                            int nsteps_rt, f32x4 (&acc)[4][4]) {
+  const int nsteps = NST > 0 ? NST : nsteps_rt;
+  f32x4 ring[R][VN + VK];
+  auto load = [&](f32x4* slot, int st) {
+    const int64_t oa = (int64_t)st * 4 * sA, ob = (int64_t)st * 4 * sB;
+#pragma unroll
+    for (int i = 0; i < VN; ++i) slot[i] = *reinterpret_cast<const f32x4*>(pa[i] + oa);
+#pragma unroll
+    for (int j = 0; j < VK; ++j) slot[VN + j] = *reinterpret_cast<const f32x4*>(pb[j] + ob);
+  };
+#pragma unroll
+  for (int p = 0; p < R - 1; ++p) load(ring[p], p);
+#pragma unroll NST > 0 ? NST / R : 1
+  for (int s0 = 0; s0 < nsteps; s0 += R) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      // the step R-1 ahead (the tail re-reads the last step: no branch around loads)
+      load(ring[(r + R - 1) % R], min(s0 + r + R - 1, nsteps - 1));
+      // pin the ring: the loads stay R-1 steps ahead of their MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+      const f32x4* c = ring[r];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < VN; ++i)
+#pragma unroll
+          for (int j = 0; j < VK; ++j) acc[i][j] = mfma4(c[i][q], c[VN + j][q], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(256, 2) void k_t32_dw_reg(TowerArgs a, int ndw) {
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= ndw) {
+    tower_col_reduce(a, (int)blockIdx.x - ndw, BM);
+    return;
+  }
+  __shared__ f32x4 red[4][16][64];  // 64 KB: the waves' partial tiles
+  const int S = a.dw_splits;
+  int t, split;
+  if (S == 8) {
+    split = (int)blockIdx.x & 7;  // one M split per XCD (see k_t32_dw)
+    t = (int)blockIdx.x >> 3;
+  } else {
+    const int wid = xcd_work_id((int)blockIdx.x, ndw);
+    t = wid / S;
+    split = wid % S;
+  }
+  int l = 0;
+  for (; l < a.L; ++l) {
+    const int nt = dw32_tiles(a.ly[l]);
+    if (t < nt) break;
+    t -= nt;
+  }
+  const TowerLayerDev& ly = a.ly[l];
+  const int NBn = ly.Np / 16, NBk = ly.Kp / 16;
+  const int tk_n = (NBk + 3) / 4;
+  const int tn = t / tk_n, tk = t % tk_n;
+  const int vn = min(4, NBn - tn * 4), vk = min(4, NBk - tk * 4);  // valid 16-blocks of the tile
+  const float* Amp = ly.dzmpf;
+  const float* Bmp = l == 0 ? a.x0mpf : a.ly[l - 1].xmpf;
+  const int lane = tid & 63, w = tid >> 6;
+  const int64_t sA = (int64_t)NBn * 256, sB = (int64_t)NBk * 256;
+  // chunk pointers of this wave's first step (invalid blocks re-read the last valid one: uniform load counts)
+  const int per = a.Mp / 16 / S;
+  const int64_t m0 = (int64_t)split * per + w;
+  const float* pa[4];
+  const float* pb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pa[i] = Amp + m0 * sA + (int64_t)min(tn * 4 + i, NBn - 1) * 256 + lane * 4;
+    pb[i] = Bmp + m0 * sB + (int64_t)min(tk * 4 + i, NBk - 1) * 256 + lane * 4;
+  }
+  const int nsteps = per / 4;  // multiple of R (host check)
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // the valid block counts select a branch-free loop (branches between the
+  // MFMAs make hipcc wait for every older load, not just the oldest step's)
+#define PBX_DW_REG(VN, VK)                                                   \
+  if (nsteps == 16) dw_reg_loop<R, VN, VK, 16>(pa, pb, sA, sB, nsteps, acc); \
+  else dw_reg_loop<R, VN, VK, 0>(pa, pb, sA, sB, nsteps, acc)
+  switch (vn * 4 + vk) {
+    case 5: PBX_DW_REG(1, 1); break;
+    case 6: PBX_DW_REG(1, 2); break;
+    case 7: PBX_DW_REG(1, 3); break;
+    case 8: PBX_DW_REG(1, 4); break;
+    case 9: PBX_DW_REG(2, 1); break;
+    case 10: PBX_DW_REG(2, 2); break;
+    case 11: PBX_DW_REG(2, 3); break;
+    case 12: PBX_DW_REG(2, 4); break;
+    case 13: PBX_DW_REG(3, 1); break;
+    case 14: PBX_DW_REG(3, 2); break;
+    case 15: PBX_DW_REG(3, 3); break;
+    case 16: PBX_DW_REG(3, 4); break;
+    case 17: PBX_DW_REG(4, 1); break;
+    case 18: PBX_DW_REG(4, 2); break;
+    case 19: PBX_DW_REG(4, 3); break;
+    default: PBX_DW_REG(4, 4); break;
+  }
+#undef PBX_DW_REG
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[w][i * 4 + j][lane] = acc[i][j];
+  __syncthreads();
+  // wave w sums row-block i = w of the four partials: lane (c, g) register q -> dW[16 nb + 4g + q][16 kb + c]
+  if (w >= vn) return;
+  const int c = lane & 15, g = lane >> 4;
+  const int nb = tn * 4 + w;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j >= vk) continue;
+    const int k = (tk * 4 + j) * 16 + c;
+    const f32x4 v = red[0][w * 4 + j][lane] + red[1][w * 4 + j][lane] + red[2][w * 4 + j][lane] +
+                    red[3][w * 4 + j][lane];
+    if (k >= ly.K) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = nb * 16 + 4 * g + q;
+      if (n < ly.N) atomicAdd(&ly.dw[(int64_t)n * ly.K + k], v[q]);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- weight packing (index maps: tower_common.h)
 
 struct Pack32Job {
@@ -719,10 +863,18 @@ void launch_tower32_dw(const TowerArgs& a, hipStream_t s) {
   const int nred = (a.bias_ld + 31) / 32 + (a.dn_part ? (a.dn_C + 31) / 32 : 0);
   static const int ring = [] {
     const char* e = getenv("PBX_T32_DW_RING");
-    return e ? atoi(e) : 23;  // DS * 10 + NS
+    return e ? atoi(e) : 0;  // 0: register-streamed (ring of 4 steps); else DS * 10 + NS of the LDS ring
   }();
   const dim3 g(ndw + nred), b(256);
-  switch (ring) {
+  // the register-streamed kernel needs every wave's step count to divide by its ring
+  const bool reg_ok = (a.Mp / 16) % (a.dw_splits * 4 * 4) == 0;  // ring 4 (ring 2 divides whenever 4 does)
+  switch (ring == 0 && !reg_ok ? 23 : ring) {
+    case 0:
+      hipLaunchKernelGGL((k_t32_dw_reg<4>), g, b, 0, s, a, ndw);
+      break;
+    case 2:
+      hipLaunchKernelGGL((k_t32_dw_reg<2>), g, b, 0, s, a, ndw);
+      break;
     case 16: {
       static const bool big = hipFuncSetAttribute((const void*)k_t32_dw<1, 6>,
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 6 * kDwStep * 4) ==
