@@ -493,12 +493,13 @@ struct DedupWorkspace {
   // row of every occurrence.  Same uid / perm / seg / u_count contract.
   // rows_given: rows_occ[:n] already holds the rows (probed by the split
   // pull); keys then only give n.
-  Tensor rows_u, rows_occ;
+  Tensor rows_u, rows_occ, u_acc;
   Tensor& table_rows_occ() {
     if (!rows_u.defined()) {
       auto o8 = perm.options().dtype(torch::kInt64);
       rows_u = torch::empty({cap}, o8);
       rows_occ = torch::full({cap}, -1, o8);  // kept all -1 between split pulls (k_table_scatter resets it)
+      u_acc = torch::zeros({4}, perm.options());  // the dedup's private counters (zero between dedups)
       if (!rank.defined()) rank = torch::empty({cap}, perm.options());
     }
     return rows_occ;
@@ -512,7 +513,7 @@ struct DedupWorkspace {
     auto rc = t.dedup_rows();
     launch_table_dedup(t.view(), ptr<int64_t>(keys), n, ptr<int64_t>(rows_occ), ptr<int32_t>(rank), rc.first,
                        rc.second, ptr<int64_t>(rows_u), ptr<int32_t>(uid), ptr<int32_t>(perm), ptr<int32_t>(seg),
-                       ptr<int32_t>(u_count), rows_given, cur_stream());
+                       ptr<int32_t>(u_count), ptr<int32_t>(u_acc), rows_given, cur_stream());
     last_n = n;
   }
   int64_t last_n = 0;

@@ -111,6 +111,9 @@ __device__ __forceinline__ int64_t probe_thread(const TableDev& t, uint64_t key)
 // ids).  k_table_seg turns the counts into run starts (and re-zeroes them),
 // k_table_scatter writes perm.  Replaces the scratch-hash insert, rank and
 // cleanup plus the separate probe of the unique keys.
+// The counters [U, n_valid, -, segment cursor] accumulate in a private block
+// (acc) that k_table_scatter publishes to u_count and re-zeroes, so a dedup
+// needs no fill launch before it (acc is zero between dedups by construction).
 // PROBE = false: rows_occ already holds every occurrence's row (the split
 // pull probed it on the critical stream; this dedup runs on a side stream
 // under the dense forward).
@@ -240,8 +243,13 @@ __global__ __launch_bounds__(256) void k_table_seg(const int64_t* __restrict__ r
 // writes only the occurrences inside the lod, so the padding must read -1)
 __global__ void k_table_scatter(int64_t* __restrict__ rows_occ, const int32_t* __restrict__ rank,
                                 const int32_t* __restrict__ uid_row, const int32_t* __restrict__ seg, int64_t n,
-                                int32_t* __restrict__ uid, int32_t* __restrict__ perm, int reset_rows) {
+                                int32_t* __restrict__ uid, int32_t* __restrict__ perm, int reset_rows,
+                                int32_t* __restrict__ acc, int32_t* __restrict__ u_count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 4) {  // publish the counters, leave the accumulator zero for the next dedup
+    u_count[i] = acc[i];
+    acc[i] = 0;
+  }
   if (i >= n) return;
   const int64_t r = rows_occ[i];
   if (reset_rows && r >= 0) rows_occ[i] = -1;
@@ -509,15 +517,11 @@ void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t
 
 void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows_occ, int32_t* rank,
                         int32_t* cnt_row, int32_t* uid_row, int64_t* rows_u, int32_t* uid, int32_t* perm, int32_t* seg,
-                        int32_t* u_count, bool rows_given, hipStream_t s) {
-  // [U, n_valid, -, segment cursor] = 0 (PBX_FILL_MEMSET=1: a memset node instead of the fill kernel)
-  static const bool memset_fill = [] {
-    const char* e = getenv("PBX_FILL_MEMSET");
-    return e && atoi(e) == 1;
-  }();
-  if (memset_fill) (void)hipMemsetAsync(u_count, 0, 4 * sizeof(int32_t), s);
-  else launch_fill32(u_count, 0u, 4, s);
-  if (n <= 0) return;
+                        int32_t* u_count, int32_t* acc, bool rows_given, hipStream_t s) {
+  if (n <= 0) {  // no scatter to publish the counters: [U, n_valid, -, cursor] = 0
+    launch_fill32(reinterpret_cast<uint32_t*>(u_count), 0u, 4, s);
+    return;
+  }
   // occurrences per thread (PBX_TD_ITEMS 1 / 2 / 4): more probes in flight
   // per thread and fewer workgroups (fewer same-address u_count atomics);
   // same-box A/B 0.252-0.257 (2) vs 0.258-0.262 (1) vs 0.262-0.267 (4) ms/step
@@ -528,7 +532,7 @@ void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64
   }();
 #define PBX_TD_LAUNCH(PR, IT)                                                                                  \
   hipLaunchKernelGGL((k_table_rank<PR, IT>), dim3(blocks_for(n, 256 * IT)), dim3(256), 0, s, t,              \
-                     reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, uid_row, rows_u, u_count)
+                     reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, uid_row, rows_u, acc)
   if (rows_given) {
     if (items == 4) PBX_TD_LAUNCH(false, 4);
     else if (items == 2) PBX_TD_LAUNCH(false, 2);
@@ -547,13 +551,13 @@ void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64
     return (v == 2 || v == 4) ? v : 1;
   }();
   if (seg_items == 1)
-    hipLaunchKernelGGL(k_table_seg<1>, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_u, cnt_row, u_count, seg);
+    hipLaunchKernelGGL(k_table_seg<1>, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_u, cnt_row, acc, seg);
   else if (seg_items == 2)
-    hipLaunchKernelGGL(k_table_seg<2>, dim3(blocks_for(n, 512)), dim3(256), 0, s, rows_u, cnt_row, u_count, seg);
+    hipLaunchKernelGGL(k_table_seg<2>, dim3(blocks_for(n, 512)), dim3(256), 0, s, rows_u, cnt_row, acc, seg);
   else
-    hipLaunchKernelGGL(k_table_seg<4>, dim3(blocks_for(n, 1024)), dim3(256), 0, s, rows_u, cnt_row, u_count, seg);
+    hipLaunchKernelGGL(k_table_seg<4>, dim3(blocks_for(n, 1024)), dim3(256), 0, s, rows_u, cnt_row, acc, seg);
   hipLaunchKernelGGL(k_table_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_occ, rank, uid_row, seg, n, uid,
-                     perm, rows_given ? 1 : 0);
+                     perm, rows_given ? 1 : 0, acc, u_count);
 }
 
 void launch_probe_gather(const TableDev& t, const uint64_t* h, int64_t n, int64_t* rows, float* out, int out_stride,
