@@ -18,12 +18,14 @@ Reference: the c_mixallgather / heter_comm peer copies
 (``c_mixallgather_op.cc:221-327``, ``heter_comm_inl.h:273-490``); here the
 memory handles are exchanged once over the process group and every later
 call is a single kernel.  Every rank must issue the same sequence of
-collectives on a mesh (as with RCCL).  The launches of one mesh are
-serialised on the mesh's own stream (forked from and joined back into the
-caller's stream): a launch reads the mesh epoch from device memory, so two
-collectives of one mesh in flight at once -- e.g. a data_norm statistics
-all-reduce on the tower's dW stream and a transpiled c_allreduce_sum on the
-compute stream -- would run under the same epoch.  A peer that never arrives makes the
+collectives on a mesh (as with RCCL).  A launch reads the mesh epoch from
+device memory, so two collectives of one mesh must never be in flight at once:
+a mesh built with ``stream=<name>`` issues every launch on that named side
+stream (forked from and joined back into the caller's stream), which orders
+them -- the dense mesh uses the tower's dW stream, where the gradient
+all-reduce, a data_norm statistics all-reduce and a transpiled
+c_allreduce_sum issued from the compute stream then queue in issue order.
+The sparse exchange meshes are only ever issued from one stream and skip it.  A peer that never arrives makes the
 wait time out: the sticky error poisons the results (NaN sums, empty
 exchanges) and :meth:`check` raises on the host, instead of hanging the GPU
 or training on stale slots.
@@ -49,7 +51,7 @@ class IpcMeshError(RuntimeError):
 
 class IpcMesh:
     def __init__(self, slot_bytes: int, group=None, device=None, blocks: Optional[int] = None, depth: int = 2,
-                 spin_limit: Optional[int] = None):
+                 spin_limit: Optional[int] = None, stream: Optional[str] = None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -77,7 +79,13 @@ class IpcMesh:
         self.state = torch.zeros(4, dtype=torch.int64, device=self.device)
         self.comm = h.IpcComm(self.rank, W, self.slot_bytes, self.state, int(blocks), self.depth,
                               int(spin_limit or DEFAULT_SPIN_LIMIT))
-        self.stream = torch.cuda.Stream(self.device)  # every launch of this mesh, in issue order
+        # every launch of this mesh in issue order on one named side stream (or the caller's)
+        if stream is not None:
+            from ..runtime.streams import side_stream
+
+            self.stream = side_stream(self.device, stream)
+        else:
+            self.stream = None
         self._opened = []
         # no rank may raise between the collectives below (a peer would block
         # in them forever): failures are recorded and agreed on at the end
@@ -139,7 +147,7 @@ class IpcMesh:
 
         def __enter__(self):
             self.cur = torch.cuda.current_stream(self.m.device)
-            self.fork = self.cur != self.m.stream
+            self.fork = self.m.stream is not None and self.cur != self.m.stream
             if self.fork:
                 self.m.stream.wait_stream(self.cur)
                 self.ctx = torch.cuda.stream(self.m.stream)

@@ -35,7 +35,9 @@ def make_ipc_mesh(nbytes: int, device, group=None, log=None):
     from ..parallel.ipc import IpcMesh, IpcMeshError
 
     try:
-        m = IpcMesh(nbytes, group=group, device=device)
+        # dense collectives (gradient all-reduce, data_norm statistics,
+        # c_allreduce_sum) queue on the tower's dW stream, in issue order
+        m = IpcMesh(nbytes, group=group, device=device, stream="tower_dw")
     except IpcMeshError as e:
         if log:
             log(f"IPC mesh unavailable ({e}); RCCL all-reduce")
