@@ -146,6 +146,42 @@ def test_tiered_mode_with_ssd(tmp_path):
     torch.testing.assert_close(got[:, 0], host_rows[:, 0] * box.cfg.shrink.show_click_decay_rate)
 
 
+def test_tiered_host_cap_spills_oldest_pass(tmp_path):
+    """With a host-tier row cap (TierConfig.ssd_spill_threshold) the rows of
+    the oldest written-back passes move to SSD and come back, values intact,
+    when a later pass needs them."""
+    box = BoxWrapper(8, device="cpu")
+    box.cfg.tier.spill_unseen_days = 1e9  # only the cap spills
+    box.initialize_gpu_and_load_model(slot_vector=[1, 2], max_keys=50000, mode="tiered",
+                                      ssd_path=str(tmp_path / "ssd"))
+    eng = box.engine
+    sp = SeqpoolParams()
+    batches = []
+    for p in range(3):
+        b = ragged_batch(16, 2, 2, 20, seed=10 + p)
+        b.keys += p * 10**6  # disjoint passes
+        batches.append(b)
+    u = [torch.unique(ref.mix64(b.keys)) for b in batches]
+    box.cfg.tier.ssd_spill_threshold = int(u[1].numel() + u[2].numel())  # room for the two newest passes
+    for b in batches:
+        box.feed_pass(b.keys)
+        box.begin_pass()
+        out = torch.zeros(b.B, b.S * 11)
+        st = eng.pull_seqpool_cvm(b.keys, b.lod, b.B, b.S, out, 0, sp)
+        eng.push_seqpool_cvm(st, torch.randn_like(out), b.cvm, 0, sp, float(b.B))
+        if b is batches[0]:
+            first = eng.table.read(u[0]).clone()
+        box.end_pass()
+    assert box.host.size() == u[1].numel() + u[2].numel()
+    assert len(box.ssd) == u[0].numel()  # pass 0 was the oldest
+    assert bool((box.host.probe(u[0]) < 0).all())
+    # pass 0's keys come back from SSD with the values they were written back with
+    box.feed_pass(batches[0].keys)
+    got = box.engine.table.read(u[0])
+    assert got[:, 0].sum() > 0
+    torch.testing.assert_close(got[:, :3], first[:, :3])
+
+
 def test_metric_registry_kinds():
     box = BoxWrapper(8, device="cpu")
     box.initialize_gpu_and_load_model(max_keys=1000)
