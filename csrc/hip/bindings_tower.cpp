@@ -93,6 +93,19 @@ class TowerWorkspace {
       const int64_t n_wtp = fp32 ? t32_stream_groups((int)(Kp / 16), (int)(Np / 16)) * 256 + slack : Np * Kp;
       wp_.push_back(torch::zeros({n_wp}, ob));
       wtp_.push_back(torch::zeros({n_wtp}, ob));
+      if (fp32) {
+        // group position of every (column block, k-group) of the wave-stream
+        // layout, for the per-step re-pack in the fused Adam (the closed form
+        // walks the schedule: ~100s of integer ops per element)
+        const int nb = (int)(Np / 16), kb = (int)(Kp / 16);
+        auto pos = torch::empty({(int64_t)nb * kb}, torch::kInt32), posT = torch::empty({(int64_t)kb * nb}, torch::kInt32);
+        for (int c = 0; c < nb; ++c)
+          for (int g = 0; g < kb; ++g) pos.data_ptr<int>()[c * kb + g] = (int)t32_group_pos(nb, kb, c, g);
+        for (int c = 0; c < kb; ++c)
+          for (int g = 0; g < nb; ++g) posT.data_ptr<int>()[c * nb + g] = (int)t32_group_pos(kb, nb, c, g);
+        pos_.push_back(pos.to(x0_.device()));
+        posT_.push_back(posT.to(x0_.device()));
+      }
       xmp_.push_back(torch::zeros({Mp_ * Np}, ob));
       dzmp_.push_back(torch::zeros({Mp_ * Np}, ob));
       boff_.push_back(boff);
@@ -209,7 +222,9 @@ class TowerWorkspace {
   std::vector<py::tuple> pack_regions() const {
     std::vector<py::tuple> r;
     for (int l = 0; l < L_; ++l)
-      r.push_back(py::make_tuple(wp_[l], wtp_[l], dims_[l + 1], dims_[l], pad(dims_[l + 1], wpad_), pad(dims_[l], wpad_)));
+      r.push_back(py::make_tuple(wp_[l], wtp_[l], dims_[l + 1], dims_[l], pad(dims_[l + 1], wpad_), pad(dims_[l], wpad_),
+                                 fp32_ ? py::object(py::cast(pos_[l])) : py::object(py::none()),
+                                 fp32_ ? py::object(py::cast(posT_[l])) : py::object(py::none())));
     return r;
   }
 
@@ -291,6 +306,7 @@ class TowerWorkspace {
   std::vector<int64_t> boff_;
   Tensor x0_, x0mp_, dx0_, bias_part_, pred_, dz_, loss_, part_, ticket_, stamps_;
   std::vector<Tensor> wp_, wtp_, xmp_, dzmp_;
+  std::vector<Tensor> pos_, posT_;  // fp32: wave-stream group position per (column block, k-group), W and W^T
 };
 
 // Adam over the flat arena + fused extras (see kernels.h AdamExtras).
@@ -317,6 +333,11 @@ static void adam_fused(Tensor p, Tensor g, Tensor m, Tensor v, Tensor pows, Tens
       x.pack_wp[i] = BP(wpt);
       x.pack_wtp[i] = BP(wtpt);
       x.pack_wp32[i] = x.pack_wtp32[i] = nullptr;
+    }
+    x.pack_pos32[i] = x.pack_posT32[i] = nullptr;
+    if (t.size() >= 9 && !t[7].is_none()) {
+      x.pack_pos32[i] = P<int>(t[7].cast<Tensor>());
+      x.pack_posT32[i] = P<int>(t[8].cast<Tensor>());
     }
     x.pack_N[i] = t[3].cast<int>();
     x.pack_K[i] = t[4].cast<int>();

@@ -688,6 +688,9 @@ struct AdamExtras {
   unsigned short* pack_wtp[kMaxPackRegions];
   float* pack_wp32[kMaxPackRegions];   // fp32 tower regions (pack_wp / pack_wtp null)
   float* pack_wtp32[kMaxPackRegions];
+  // fp32: group position tables [Np/16][Kp/16] and [Kp/16][Np/16] (tower_wp32_index_pos)
+  const int* pack_pos32[kMaxPackRegions];
+  const int* pack_posT32[kMaxPackRegions];
   int n_dn = 0;
   const float* dn_stats[kMaxDnUpdates];
   float* dn_bsize[kMaxDnUpdates];

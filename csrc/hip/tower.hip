@@ -582,8 +582,13 @@ __global__ __launch_bounds__(256) void k_adam_fused(float* __restrict__ p, float
         if (i < 0 || i >= cnt || e0 + k >= n) continue;
         const int nn = (int)((uint32_t)i / (uint32_t)K), kk = (int)((uint32_t)i - (uint32_t)nn * (uint32_t)K);
         if (x.pack_wp32[r]) {  // fp32 tower
-          x.pack_wp32[r][tower_wp32_index(nn, kk, x.pack_Np[r], x.pack_Kp[r])] = pa[k];
-          x.pack_wtp32[r][tower_wtp32_index(nn, kk, x.pack_Np[r], x.pack_Kp[r])] = pa[k];
+          if (x.pack_pos32[r]) {
+            x.pack_wp32[r][tower_wp32_index_pos(x.pack_pos32[r], nn, kk, x.pack_Kp[r])] = pa[k];
+            x.pack_wtp32[r][tower_wtp32_index_pos(x.pack_posT32[r], nn, kk, x.pack_Np[r])] = pa[k];
+          } else {
+            x.pack_wp32[r][tower_wp32_index(nn, kk, x.pack_Np[r], x.pack_Kp[r])] = pa[k];
+            x.pack_wtp32[r][tower_wtp32_index(nn, kk, x.pack_Np[r], x.pack_Kp[r])] = pa[k];
+          }
           continue;
         }
         const u16 bv = f2bf(pa[k]);

@@ -603,8 +603,8 @@ __global__ __launch_bounds__(256) void k_t32_dw(TowerArgs a, int ndw) {
   }
 }
 
-// Register-streamed dW (PBX_T32_DW_RING=0, the default when the split's
-// steps divide evenly): each wave owns the whole 64x64 tile for every 4th m16
+// Register-streamed dW (PBX_T32_DW_RING=0; measured slower than the LDS ring,
+// kept for the A/B): each wave owns the whole 64x64 tile for every 4th m16
 // step of its split (K split inside the workgroup), so its operands go
 // L2 -> VGPRs with global_load_dwordx4 -- a chunk's fragment order IS the
 // MFMA operand order -- in a ring of R steps: no LDS staging and no barrier
@@ -863,7 +863,10 @@ void launch_tower32_dw(const TowerArgs& a, hipStream_t s) {
   const int nred = (a.bias_ld + 31) / 32 + (a.dn_part ? (a.dn_C + 31) / 32 : 0);
   static const int ring = [] {
     const char* e = getenv("PBX_T32_DW_RING");
-    return e ? atoi(e) : 0;  // 0: register-streamed (ring of 4 steps); else DS * 10 + NS of the LDS ring
+    // DS * 10 + NS of the LDS ring (default 2x3), 0 / 2: the register-streamed
+    // kernel with a ring of 4 / 2 steps.  Same box, tower dW alone: 2x3
+    // 99.9 us, 1x6 106.9, reg-4 116.7, reg-2 110.3 (profiles/r4_dw_variants.txt)
+    return e ? atoi(e) : 23;
   }();
   const dim3 g(ndw + nred), b(256);
   // the register-streamed kernel needs every wave's step count to divide by its ring

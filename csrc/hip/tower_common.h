@@ -213,5 +213,12 @@ __device__ __forceinline__ int64_t tower_wp32_index(int n, int k, int Np, int Kp
 __device__ __forceinline__ int64_t tower_wtp32_index(int n, int k, int Np, int Kp) {
   return (t32_group_pos(Kp >> 4, Np >> 4, k >> 4, n >> 4) * 64 + (k & 15) + 16 * ((n & 15) >> 2)) * 4 + (n & 3);
 }
+// the same through precomputed group positions (pos [Np/16][Kp/16], posT [Kp/16][Np/16])
+__device__ __forceinline__ int64_t tower_wp32_index_pos(const int* pos, int n, int k, int Kp) {
+  return ((int64_t)pos[(n >> 4) * (Kp >> 4) + (k >> 4)] * 64 + (n & 15) + 16 * ((k & 15) >> 2)) * 4 + (k & 3);
+}
+__device__ __forceinline__ int64_t tower_wtp32_index_pos(const int* posT, int n, int k, int Np) {
+  return ((int64_t)posT[(k >> 4) * (Np >> 4) + (n >> 4)] * 64 + (k & 15) + 16 * ((n & 15) >> 2)) * 4 + (n & 3);
+}
 
 }  // namespace pbx

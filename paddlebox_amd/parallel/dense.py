@@ -137,8 +137,9 @@ class FlatAdam:
         for mlp in self._fuse_mlps:
             if mlp._tw is None:
                 continue  # the tower packs on its first forward
-            for (wp, wtp, N, K, Np, Kp), w in zip(mlp._tw.pack_regions(), mlp.w):
-                pack.append(((w.data_ptr() - base) // 4, wp, wtp, N, K, Np, Kp))
+            for reg, w in zip(mlp._tw.pack_regions(), mlp.w):
+                wp, wtp, N, K, Np, Kp, pos, posT = reg
+                pack.append(((w.data_ptr() - base) // 4, wp, wtp, N, K, Np, Kp, pos, posT))
         dn = [(d.stats, d.batch_size, d.batch_sum, d.batch_square_sum, d.decay)
               for d in self._fuse_dns if d.training and d.update_norm]
         return pack, dn

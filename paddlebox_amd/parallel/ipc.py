@@ -49,6 +49,10 @@ class IpcMeshError(RuntimeError):
     pass
 
 
+_TRACE = os.environ.get("PBX_IPC_TRACE", "0") == "1"
+_N_MESHES = [0]
+
+
 class IpcMesh:
     def __init__(self, slot_bytes: int, group=None, device=None, blocks: Optional[int] = None, depth: int = 2,
                  spin_limit: Optional[int] = None, stream: Optional[str] = None):
@@ -60,6 +64,9 @@ class IpcMesh:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.slot_bytes = (int(slot_bytes) + 15) // 16 * 16
         self.depth = int(depth)
+        self.mesh_id = _N_MESHES[0]
+        _N_MESHES[0] += 1
+        self.calls = 0
         h = _native.hip()
         W = self.world
         if blocks is None:
@@ -137,7 +144,7 @@ class IpcMesh:
         """In-place sum (or mean) over the ranks of a contiguous f32 tensor."""
         if two_phase is None:
             two_phase = self.world > 2 and t.numel() * 4 > (256 << 10)
-        with self._serial():
+        with self._serial("allreduce"):
             self.comm.allreduce(t, t, 1.0 / self.world if average else 1.0, bool(two_phase))
         return t
 
@@ -159,7 +166,15 @@ class IpcMesh:
                 self.cur.wait_stream(self.m.stream)
             return False
 
-    def _serial(self):
+    def _serial(self, op: str = ""):
+        self.calls += 1
+        if _TRACE:
+            import sys
+            import traceback
+
+            where = " <- ".join(f"{f.name}:{f.lineno}" for f in traceback.extract_stack(limit=6)[:-2][::-1])
+            print(f"[ipc r{self.rank} m{self.mesh_id}] {op} #{self.calls} stream={torch.cuda.current_stream(self.device).stream_id} "
+                  f"capturing={torch.cuda.is_current_stream_capturing()} {where}", file=sys.stderr, flush=True)
         return IpcMesh._Serial(self)
 
     def exchange(self, send: torch.Tensor, dst: Optional[torch.Tensor] = None, counts: Optional[torch.Tensor] = None,
@@ -169,7 +184,7 @@ class IpcMesh:
         or the whole slot); dst receives slot q from peer q.  Returns dst."""
         if dst is None:
             dst = torch.empty_like(send)
-        with self._serial():
+        with self._serial("exchange"):
             self.comm.exchange(send, dst, counts, int(rec_bytes), bool(fill_tail), rcounts)
         return dst
 

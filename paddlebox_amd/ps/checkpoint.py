@@ -141,9 +141,10 @@ def load_batch_model_parts(path: str, rank: Optional[int] = None) -> Tuple[np.nd
     return np.concatenate(ks), np.concatenate(vs)
 
 
-# Streaming load: parts are memory-mapped and walked in chunks of this many
-# rows, so a rank's host RAM for a load stays at ~2 chunks whatever the model
-# size (a 1e9-row model is ~90 GB of parts).
+# Streaming load: parts are read in chunks of this many rows (positioned reads
+# past the .npy header, no memory map: a mapping keeps every page it touched
+# resident), so a rank's host RAM for a load stays at ~2 chunks whatever the
+# model size (a 1e9-row model is ~90 GB of parts).
 LOAD_CHUNK_ROWS = int(os.environ.get("PBX_LOAD_CHUNK_ROWS", str(1 << 22)))
 
 
@@ -160,19 +161,50 @@ def list_parts(path: str):
     return sorted(int(f[5:10]) for f in os.listdir(path) if f.startswith("part-") and f.endswith(".keys.npy"))
 
 
+def _npy_layout(fn: str):
+    """(shape, dtype, data offset) of a .npy file, from its header only
+    (numpy.lib.format: no pickle is ever read; object arrays are refused)."""
+    with open(fn, "rb") as f:
+        version = np.lib.format.read_magic(f)
+        if version == (1, 0):
+            shape, fortran, dtype = np.lib.format.read_array_header_1_0(f)
+        else:
+            shape, fortran, dtype = np.lib.format.read_array_header_2_0(f)
+        if fortran or dtype.hasobject:
+            raise ValueError(f"{fn}: not a C-order plain array")
+        return shape, dtype, f.tell()
+
+
 def part_rows(path: str, part: int) -> int:
-    return int(np.load(os.path.join(path, f"part-{part:05d}.keys.npy"), mmap_mode="r", allow_pickle=False).shape[0])
+    return int(_npy_layout(os.path.join(path, f"part-{part:05d}.keys.npy"))[0][0])
 
 
 def iter_part_chunks(path: str, part: int, chunk_rows: int):
     """(feasigns uint64 [n], rows f32 [n, stride]) chunks of one part, read
-    through read-only memory maps (allow_pickle=False): only the chunk being
-    yielded is resident."""
-    k = np.load(os.path.join(path, f"part-{part:05d}.keys.npy"), mmap_mode="r", allow_pickle=False)
-    v = np.load(os.path.join(path, f"part-{part:05d}.vals.npy"), mmap_mode="r", allow_pickle=False)
-    for a in range(0, k.shape[0], max(1, int(chunk_rows))):
-        b = min(k.shape[0], a + int(chunk_rows))
-        yield np.array(k[a:b]), np.array(v[a:b], dtype=np.float32)
+    with positioned reads of the raw array data: only the chunk being yielded
+    is resident (and the page cache's copy, which the kernel may drop)."""
+    kf = os.path.join(path, f"part-{part:05d}.keys.npy")
+    vf = os.path.join(path, f"part-{part:05d}.vals.npy")
+    (n,), kd, ko = _npy_layout(kf)
+    vshape, vd, vo = _npy_layout(vf)
+    if vshape[0] != n:
+        raise ValueError(f"part {part}: {n} keys but {vshape[0]} value rows")
+    width = int(np.prod(vshape[1:])) if len(vshape) > 1 else 1
+    step = max(1, int(chunk_rows))
+    with open(kf, "rb") as fk, open(vf, "rb") as fv:
+        for a in range(0, n, step):
+            b = min(n, a + step)
+            fk.seek(ko + a * kd.itemsize)
+            k = np.fromfile(fk, dtype=kd, count=b - a)
+            fv.seek(vo + a * width * vd.itemsize)
+            v = np.fromfile(fv, dtype=vd, count=(b - a) * width).reshape((b - a,) + tuple(vshape[1:]))
+            try:  # the chunk is consumed: let the page cache drop it
+                os.posix_fadvise(fk.fileno(), ko + a * kd.itemsize, (b - a) * kd.itemsize, os.POSIX_FADV_DONTNEED)
+                os.posix_fadvise(fv.fileno(), vo + a * width * vd.itemsize, (b - a) * width * vd.itemsize,
+                                 os.POSIX_FADV_DONTNEED)
+            except (AttributeError, OSError):
+                pass
+            yield k.astype(np.uint64, copy=False), v.astype(np.float32, copy=False)
 
 
 def save_xbox(table, path: str, mode: str, cfg: SaveConfig, nonclk: float, clk: float, rank: int = 0,
