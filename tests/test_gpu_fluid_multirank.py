@@ -120,6 +120,10 @@ def _train(fluid, files, batch, rank, W, transpile):
 
 
 def _worker(rank, W, port, d, transpile, q):
+    import faulthandler
+    import sys
+
+    faulthandler.dump_traceback_later(90, exit=False, file=sys.stderr)  # a stuck rank shows where
     try:
         import torch.distributed as dist
 
@@ -167,8 +171,9 @@ def test_fluid_two_ranks_match_union_oracle(tmp_path, monkeypatch, transpile):
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
+    errs = {r: res[r] for r in range(W) if isinstance(res.get(r), str)}
+    assert not errs, "\n".join(f"rank {r}: {e}" for r, e in errs.items())
     for r in range(W):
-        assert not isinstance(res[r], str), res[r]
         assert res[r][3]["ipc"], "the session did not set up its IPC mesh"
     # oracle: one rank, the union file, W*B batches, statistics x W
     h = _native.hip()
