@@ -394,7 +394,7 @@ __global__ __launch_bounds__(256) void k_push_adagrad(TableDev t, const int64_t*
   if (v[l.mf_size] == 0.f) {
     if (cfg.nonclk_coeff * (show - click) + cfg.clk_coeff * click >= cfg.mf_create_thresholds) {
       v[l.mf_size] = 1.f;
-      const uint64_t salt = seed ^ (uint64_t)r * 0x9E3779B97F4A7C15ULL;
+      const uint64_t salt = seed ^ table_row_key(t, r) * 0x9E3779B97F4A7C15ULL;
       for (int d = 0; d < t.dim; ++d) v[kEmbedx + d] = hash_uniform(salt, d) * cfg.mf_initial_range;
     }
   } else {
@@ -424,7 +424,7 @@ struct RowF {
 
 template <int D>
 __device__ __forceinline__ void adagrad_row(float* __restrict__ row, const float* g, const SparseSGDConfig& cfg,
-                                            uint64_t seed, int64_t r) {
+                                            uint64_t seed, uint64_t rkey) {
   using L = RowF<D>;
   float v[L::kStride];
   float4* r4 = reinterpret_cast<float4*>(row);
@@ -457,7 +457,7 @@ __device__ __forceinline__ void adagrad_row(float* __restrict__ row, const float
   if (v[L::kMf] == 0.f) {
     if (cfg.nonclk_coeff * (show - click) + cfg.clk_coeff * click >= cfg.mf_create_thresholds) {
       v[L::kMf] = 1.f;
-      const uint64_t salt = seed ^ (uint64_t)r * 0x9E3779B97F4A7C15ULL;
+      const uint64_t salt = seed ^ rkey * 0x9E3779B97F4A7C15ULL;
 #pragma unroll
       for (int d = 0; d < D; ++d) v[kEmbedx + d] = hash_uniform(salt, d) * cfg.mf_initial_range;
     }
@@ -504,7 +504,7 @@ __global__ __launch_bounds__(256) void k_push_adagrad_v(TableDev t, const int64_
   if (r < 0) return;
   float g[RowF<D>::kQ4 * 4];
   load_push<D>(push + u * push_stride, g);
-  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
+  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, table_row_key(t, r));
 }
 
 // Owner side of the sharded push: the records of unique u (at most one per
@@ -535,7 +535,7 @@ __global__ __launch_bounds__(256) void k_push_adagrad_seg(TableDev t, const int6
 #pragma unroll
     for (int c = 1; c < QP; ++c) g[c] += x[c];
   }
-  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
+  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, table_row_key(t, r));
 }
 
 // Single-shard push, merge + Adagrad in one pass over the batch gradients.
@@ -559,7 +559,7 @@ struct ApplyEmit {
   template <int D>
   __device__ __forceinline__ void emit(int32_t u, const float* rec) const {
     const int64_t r = rows[u];
-    if (r >= 0) adagrad_row<D>(t.values + r * (int64_t)t.stride, rec, cfg, seed, r);
+    if (r >= 0) adagrad_row<D>(t.values + r * (int64_t)t.stride, rec, cfg, seed, table_row_key(t, r));
   }
 };
 struct SendEmit {
@@ -753,7 +753,7 @@ __global__ __launch_bounds__(256) void k_push_occ_apply(TableDev t, const int64_
 #pragma unroll
     for (int i = 0; i < RowF<D>::kQ4; ++i) a4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
+  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, table_row_key(t, r));
   lock[r] = -1;
 }
 
@@ -795,7 +795,7 @@ __global__ __launch_bounds__(256) void k_owner_push_apply(TableDev t, const int6
   const int64_t r = rows[e];
   float g[RowF<D>::kQ4 * 4];
   load_push<D>(rec + e * (int64_t)rec_stride, g);
-  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, r);
+  adagrad_row<D>(t.values + r * (int64_t)t.stride, g, cfg, seed, table_row_key(t, r));
   lock[r] = -1;
 }
 

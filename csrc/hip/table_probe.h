@@ -35,4 +35,13 @@ __device__ __forceinline__ int64_t table_probe_thread(const TableDev& t, uint64_
   return -1;
 }
 
+// The key stored at row r (bucket slots, then the stash).  Lazy embedx
+// creation draws a row's initial values from its key, not its row index, so a
+// key gets the same values whichever shard and row hold it (an N-rank run
+// equals the one-rank run on the union batch).
+__device__ __forceinline__ uint64_t table_row_key(const TableDev& t, int64_t r) {
+  const int64_t total = (int64_t)t.nb * kBucketSlots;
+  return r < total ? t.keys[r] : t.stash_keys[r - total];
+}
+
 }  // namespace pbx

@@ -116,7 +116,9 @@ def _train(fluid, files, batch, rank, W, transpile):
     sess = exe.sessions_for(main)[0]
     info = dict(ipc=sess.ipc is not None, replays=stats.get("graph_replays", 0) if isinstance(stats, dict) else 0)
     BoxWrapper._instance = None
-    return out, h.cpu(), v.cpu(), info
+    # numpy, not torch: a torch tensor crosses the result queue as a shared fd
+    # that dies with the worker process
+    return out, h.cpu().numpy(), v.cpu().numpy(), info
 
 
 def _worker(rank, W, port, d, transpile, q):
@@ -135,8 +137,10 @@ def _worker(rank, W, port, d, transpile, q):
         torch.cuda.set_device(0)
         paths, _ = _write_files(d, W) if rank == 0 else (None, None)
         dist.barrier()
+        # every rank gets the whole filelist and reads its rank stride of it
+        # (data_set.cc:1963-1975): rank r trains rank-r.txt
         paths = [os.path.join(d, f"rank-{r}.txt") for r in range(W)]
-        out = _train(fluid, [paths[rank]], B, rank, W, transpile)
+        out = _train(fluid, paths, B, rank, W, transpile)
         dist.barrier()
         q.put((rank, out))
         dist.destroy_process_group()
@@ -181,6 +185,9 @@ def test_fluid_two_ranks_match_union_oracle(tmp_path, monkeypatch, transpile):
     monkeypatch.setattr(h, "data_norm_update", lambda bs, bsum, bsq, st, dec: orig(bs, bsum, bsq, st * W, dec))
     _, union = _write_files(d, W)
     o_dense, o_h, o_v, _ = _train(fluid, [union], W * B, 0, 1, False)
+    o_h, o_v = torch.from_numpy(o_h), torch.from_numpy(o_v)
+    for r in range(W):
+        res[r] = (res[r][0], torch.from_numpy(res[r][1]), torch.from_numpy(res[r][2]), res[r][3])
     for n, a in o_dense.items():
         for r in range(W):
             np.testing.assert_allclose(res[r][0][n], a, rtol=2e-4, atol=2e-5, err_msg=f"rank {r} {n}")

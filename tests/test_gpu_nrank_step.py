@@ -21,6 +21,7 @@ summary update.  Reference step: boxps_worker.cc:1191-1258.
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
@@ -103,7 +104,8 @@ def _worker(rank, W, port, B, steps, q):
         eng.check_exchange()
         step.ipc.check()
         dist.barrier()
-        q.put((rank, res))
+        # numpy, not torch: a torch tensor crosses the queue as a shared fd that dies with the worker
+        q.put((rank, {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in res.items()}))
         step.close()
         for m in eng.xmesh:
             m.close()
@@ -166,6 +168,7 @@ def test_nrank_graphed_deepfm_step_matches_union_oracle(W):
                 p.kill()
     for r in range(W):
         assert not isinstance(res[r], str), res[r]
+        res[r] = {k: (torch.from_numpy(v) if isinstance(v, np.ndarray) else v) for k, v in res[r].items()}
         assert res[r]["ovf"] is False
     orc = _oracle(W, B, steps)
     # every replica holds the same dense parameters (one-shot all-reduce: same
