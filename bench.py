@@ -170,6 +170,10 @@ def main():
     ap.add_argument("--model", choices=("deepfm", "dcn_v2"), default="deepfm",
                     help="deepfm = the headline config; dcn_v2 = BASELINE config 5 (cross layers on the MFMA GEMM)")
     ap.add_argument("--cross-layers", type=int, default=3)
+    ap.add_argument("--pipeline", dest="pipeline", action="store_true", default=False,
+                    help="pipelined pull with the whole sparse front: each graph pools the next batch (dedup + "
+                         "seqpool) right after its sparse push, under its dW GEMM (3 batch buffers)")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false")
     ap.add_argument("--prefetch", dest="prefetch", action="store_true", default=False,
                     help="pipelined pull: batch i+1's dedup + probe on a side stream beside batch i's dense "
                          "work (measured slower on one MI355X: 0.356 vs 0.281 ms/step, see "
@@ -260,7 +264,8 @@ def main():
                   f"{int(math.ceil(B * S / world * 1.25)) + 64})")
     engine = SparseEngine(cfg, max_keys=B * S, device=device, capacity=synth.total_features,
                           slot_ids=[float(s + 1) for s in range(S)], auto_insert=args.no_prefill,
-                          exchange_capacity=xcap, exchange=args.sparse_exchange, dedup=args.dedup == "on")
+                          exchange_capacity=xcap, exchange=args.sparse_exchange, dedup=args.dedup == "on",
+                          pull_ring=3 if args.pipeline else 2)
 
     t0 = time.time()
     if not args.no_prefill:
@@ -312,8 +317,12 @@ def main():
                 from paddlebox_amd.runtime.graph_step import GraphedTrainStep
 
                 pre = (engine, lambda b: b.keys) if (args.prefetch and engine.can_prefetch()) else None
+                pipe = None
+                if args.pipeline and pre is None and engine.can_prefetch() and engine.table_dedup:
+                    pipe = (lambda b, j: step.prefetch(b, j), step.set_next, engine.clear_prefetch)
                 graphed = GraphedTrainStep(train_step, host_batches[0], device, prefetch=pre,
-                                           steps_per_graph=K if pre is None else 1)
+                                           steps_per_graph=K if (pre is None and pipe is None) else 1,
+                                           n_buffers=3 if pipe is not None else 2, pipeline=pipe)
                 graphed.warm(host_batches, replays=args.graph_warm)
                 log(rank, f"[bench] training step captured into HIP graphs ({args.graph_warm} warm replays)")
             except Exception as e:  # pragma: no cover - depends on runtime
@@ -326,10 +335,14 @@ def main():
             def group(i):
                 return host_batches[i % nb] if K == 1 else [host_batches[(i * K + k) % nb] for k in range(K)]
 
-            graphed.load(0, group(0))
+            # buffers in flight ahead of the replay: graph i of a pipelined
+            # step also reads buffer i+1, so its copy is issued a step earlier
+            ahead = 2 if graphed.pipeline is not None else 1
+            for a in range(ahead):
+                graphed.load(a % graphed.n, group(a))
 
             def run(i):
-                graphed.load((i + 1) % graphed.n, group(i + 1))
+                graphed.load((i + ahead) % graphed.n, group(i + ahead))
                 return graphed.run(i % graphed.n)
         else:
             K = 1
@@ -413,7 +426,8 @@ def main():
 
         res = dict(dt=dt, t_enq=t_enq, graph_steps=K, loss=float(loss) if loss is not None else float("nan"),
                    auc_stats=auc_stats.clone(), ipc=ipc,
-                   prefetch=bool(graphed is not None and graphed.prefetch is not None), fused=fused)
+                   prefetch=bool(graphed is not None and graphed.prefetch is not None),
+                   pipeline=bool(graphed is not None and graphed.pipeline is not None), fused=fused)
         # free this precision's graphs / model before the next measurement
         del graphed, model, opt, arena, sync, step
         return res
@@ -497,6 +511,7 @@ def main():
                 "sparse_exchange": engine.exchange_mode,
                 "same_gpu_rehearsal": bool(args.same_gpu),
                 "pipelined_pull": res["prefetch"],
+                "pipelined_front": res.get("pipeline", False),
                 "steps_per_graph": res.get("graph_steps", 1),
                 "key_dedup": bool(engine.dedup),
                 "mlp_dtype": args.mlp_dtype,

@@ -27,7 +27,7 @@ from .. import _native
 from ..ops.ctr import DataNorm, ctr_head, logit_logloss
 from ..ops.mlp import FusedMLP, _ensure_grad, pad8
 from ..ops.tower import CtrTower
-from ..ops.sparse import pull_seqpool_cvm_concat
+from ..ops.sparse import prefetch_seqpool_cvm_concat, pull_seqpool_cvm_concat
 from ..ps.sparse_engine import SeqpoolParams, SparseEngine
 
 
@@ -128,6 +128,12 @@ class DCNv2(nn.Module):
         self.w_c = nn.Parameter(torch.zeros(D))
         self.tower = CtrTower(self.mlp, self.dn, self.S, self.Eo, self.ew_col, 0, use_head_lin=False,
                               cross=(self.cross, self.w_c)) if self.use_tower else None
+
+    def prefetch(self, batch, slot: int) -> bool:
+        """Pool the NEXT batch now (after this step's sparse push), so its
+        step starts at the data_norm head (ops/sparse.py)."""
+        return prefetch_seqpool_cvm_concat(self.engine, batch.keys, batch.lod, batch.B, batch.S, batch.dense, self.sp,
+                                           slot)
 
     def forward(self, batch):
         B, S = batch.B, batch.S

@@ -24,7 +24,7 @@ from torch import nn
 
 from ..ops.ctr import DataNorm, ctr_head, fm_interaction, logit_logloss
 from ..ops.mlp import FusedMLP, pad8
-from ..ops.sparse import pull_seqpool_cvm_concat
+from ..ops.sparse import prefetch_seqpool_cvm_concat, pull_seqpool_cvm_concat
 from ..ops.tower import CtrTower
 from ..ps.sparse_engine import SeqpoolParams, SparseEngine
 
@@ -82,6 +82,12 @@ class DeepFM(nn.Module):
         self.precision = precision
         self.tower.fp32 = precision == "fp32" and self.mlp.tower_fp32_ok()
         self.mlp.invalidate_pack()
+
+    def prefetch(self, batch, slot: int) -> bool:
+        """Pool the NEXT batch now (after this step's sparse push), so its
+        step starts at the data_norm head (ops/sparse.py)."""
+        return prefetch_seqpool_cvm_concat(self.engine, batch.keys, batch.lod, batch.B, batch.S, batch.dense, self.sp,
+                                           slot)
 
     def forward(self, batch):
         B, S = batch.B, batch.S

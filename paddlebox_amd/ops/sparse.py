@@ -39,7 +39,9 @@ class _PullSeqpoolCvmConcat(torch.autograd.Function):
         E = engine.E
         Eo = sp.out_width(E)
         Dd = 0 if dense is None else dense.shape[1]
-        out = torch.empty(B, S * Eo + Dd, dtype=torch.float32, device=keys.device)
+        out = engine.prepared_output(keys)  # pooled ahead by prefetch_seqpool_cvm_concat
+        if out is None or tuple(out.shape) != (B, S * Eo + Dd):
+            out = torch.empty(B, S * Eo + Dd, dtype=torch.float32, device=keys.device)
         # the dense features are written by the same launch (no concat copy)
         st = engine.pull_seqpool_cvm(keys, lod, B, S, out, 0, sp, dense=dense if Dd else None, dense_col=S * Eo)
         ctx.engine, ctx.st, ctx.sp, ctx.bs_scale = engine, st, sp, bs_scale
@@ -65,6 +67,15 @@ def pull_seqpool_cvm_concat(engine: SparseEngine, keys: torch.Tensor, lod: torch
     sp = sp or SeqpoolParams()
     bs = float(B if bs_scale is None else bs_scale)
     return _PullSeqpoolCvmConcat.apply(_anchor(keys.device), dense, keys, lod, cvm, engine, B, S, sp, bs)
+
+
+def prefetch_seqpool_cvm_concat(engine: SparseEngine, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int,
+                                dense: Optional[torch.Tensor] = None, sp: Optional[SeqpoolParams] = None,
+                                slot: int = 0) -> bool:
+    """Pool a batch ahead of its step (SparseEngine.prefetch_pull): the
+    step's pull_seqpool_cvm_concat on the same key buffer then launches
+    nothing.  Returns False when the engine cannot prepare pulls."""
+    return engine.prefetch_pull(keys, lod, B, S, sp or SeqpoolParams(), dense, slot)
 
 
 class _PullBoxSparse(torch.autograd.Function):

@@ -87,6 +87,7 @@ class _PullSlot:
         self.occ_slot = torch.empty(eng.max_keys, dtype=torch.int32, device=dev)
         self.occ_ins = torch.empty(eng.max_keys, dtype=torch.int32, device=dev)
         self.rows = None  # persistent probe rows of a prefetched batch
+        self.pre_out = None  # persistent pooled output of a prefetched seqpool (prefetch_pull)
         self.gen = 0
         # no-dedup pull: table row of every key occurrence
         self.rows_occ = None if eng.dedup else torch.empty(eng.max_keys, dtype=torch.int64, device=dev)
@@ -265,6 +266,7 @@ class SparseEngine:
             # sender packs its unique keys per owner with a counting pass)
             self._slots = [_PullSlot(self) for _ in range(max(1, int(pull_ring)))]
             self._prepared = {}  # key-buffer address -> (slot, L) of a prefetched batch
+            self._prepared_out = {}  # key-buffer address -> pooled output of a prefetch_pull
             self._next_slot = 0
             self._cur = self._slots[0]
             if self.sharded:
@@ -397,6 +399,10 @@ class SparseEngine:
                 out[:, dense_col:dense_col + dense.shape[1]] = dense
             return st
         h = self._hip
+        pre_out = self._prepared_out.pop(keys.data_ptr(), None) if (not self.sharded and self._prepared_out) else None
+        if pre_out is not None and pre_out is out and col_offset == 0:
+            # prefetch_pull already pooled this batch into out: only the pull state
+            return self._pull_common(keys, lod, B, S, fill_occ=False)
         if not self.dedup and sp.cvm_offset == 2:
             return self._pull_nodedup(keys, lod, B, S, out, col_offset, sp, dense, dense_col)
         if (self.table_dedup and self.split_pull and self.codec is None
@@ -543,8 +549,49 @@ class SparseEngine:
             self.table.t.probe_into(sl.ws.uniq_h[:L], sl.ws.u_count, sl.rows)
         self._prepared[keys.data_ptr()] = (sl, L)
 
+    def prefetch_pull(self, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int, sp: "SeqpoolParams",
+                      dense: Optional[torch.Tensor] = None, slot: int = 0) -> bool:
+        """Dedup + probe AND the fused seqpool + CVM (+ dense columns) of a
+        batch ahead of its training step, into pull slot ``slot`` and its
+        persistent output buffer.  Issued after the previous step's sparse
+        push (the pooled values must include that update) on the compute
+        stream, it runs under the previous step's dW GEMM; the batch's own
+        pull then returns the buffer with no launch at all.  False when the
+        engine cannot prepare pulls (sharded, codec rows, auto-insert)."""
+        if not (self.can_prefetch() and self.table_dedup and self.codec is None):
+            return False
+        L = keys.numel()
+        assert L <= self.max_keys
+        sl = self._slots[slot % len(self._slots)]
+        ws = sl.ws
+        ws.run_table(keys, self.table.t)
+        sl.rows = ws.rows_u
+        Eo = sp.out_width(self.E)
+        Dd = 0 if dense is None else int(dense.shape[1])
+        shape = (B, S * Eo + Dd)
+        if sl.pre_out is None or tuple(sl.pre_out.shape) != shape:
+            sl.pre_out = torch.empty(shape, dtype=torch.float32, device=self.device)
+        if self.seqpool_rows_occ:
+            src_index, uid = ws.rows_occ[:L], None
+        else:
+            src_index, uid = ws.rows_u, ws.uid
+        self._hip.seqpool_cvm_fwd(self.table.values, src_index, uid, lod, S, B, self.E, sl.pre_out, 0, sp.use_cvm,
+                                  sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter, sp.show_coeff,
+                                  sp.clk_coeff, sp.threshold, sp.quant_ratio, sp.embed_threshold_filter,
+                                  sp.embed_threshold, sp.embed_thres_size if not sp.use_cvm else 0,
+                                  dense.contiguous().float() if dense is not None else None, S * Eo,
+                                  occ_slot=sl.occ_slot, occ_ins=sl.occ_ins)
+        self._prepared[keys.data_ptr()] = (sl, L)
+        self._prepared_out[keys.data_ptr()] = sl.pre_out
+        return True
+
+    def prepared_output(self, keys: torch.Tensor) -> Optional[torch.Tensor]:
+        """The pooled output a prefetch_pull left for this key buffer (or None)."""
+        return self._prepared_out.get(keys.data_ptr()) if self.is_gpu and not self.sharded else None
+
     def clear_prefetch(self):
         self._prepared.clear()
+        self._prepared_out.clear()
 
     def _take_slot(self) -> _PullSlot:
         sl = self._slots[self._next_slot % len(self._slots)]

@@ -118,6 +118,18 @@ class CtrTrainStep:
             tower.auc = (fused_auc[0], fused_auc[1], None)
         self._auc = fused_auc
         self.one = torch.ones((), device=device)  # persistent d loss / d loss: no fill kernel per step
+        # pipelined pull: the next batch (and its pull slot) to pool right
+        # after this step's sparse push, under this step's dW GEMM
+        self.next_batch = None
+        self.next_slot = 0
+
+    def set_next(self, batch, slot: int = 0):
+        """Batch to prefetch (pool) at the end of each train_step (None: off)."""
+        self.next_batch, self.next_slot = batch, int(slot)
+
+    def prefetch(self, batch, slot: int) -> bool:
+        pre = getattr(self.model, "prefetch", None)
+        return bool(pre(batch, slot)) if pre is not None else False
 
     def __call__(self, b):
         return self.train_step(b)
@@ -127,6 +139,10 @@ class CtrTrainStep:
 
         loss, pred = self.model(b)
         loss.backward(self.one)
+        if self.next_batch is not None:
+            # the sparse push is on this stream already: pool the next batch
+            # now, beside the dW GEMM on the tower's side stream
+            self.prefetch(self.next_batch, self.next_slot)
         if self.adam_side:
             join_grad_producers()  # the side stream ran the update
         else:

@@ -78,7 +78,8 @@ def _drain_collective_watchdog(settle_s: float = 0.3):
 class GraphedTrainStep:
     def __init__(self, step_fn: Callable[[Any], Any], example_batch, device, n_buffers: int = 2,
                  warmup: int = 3, max_inflight: int = 3, warm_batches: Sequence[Any] = (),
-                 on_warm: Optional[Callable[[Any], None]] = None, prefetch=None, steps_per_graph: int = 1):
+                 on_warm: Optional[Callable[[Any], None]] = None, prefetch=None, steps_per_graph: int = 1,
+                 pipeline=None):
         """``steps_per_graph`` K > 1: each graph holds K consecutive training
         steps over K batch buffers (``load`` then takes K host batches and
         ``run`` trains all K).  Inside one graph consecutive steps are
@@ -92,7 +93,15 @@ class GraphedTrainStep:
         graph j also runs the dedup + probe of buffer j+1's keys on a side
         stream while batch j trains (SparseEngine.prefetch, pull slot = buffer
         index), so each step's pull starts at the seqpool."""
-        """``warmup`` eager runs of ``step_fn`` on the example batch precede
+        """``pipeline``: optional (prep, set_next[, clear]) -- pipelined pull with the
+        whole front: graph j pools buffer j+1 (dedup + seqpool) at the end of
+        its own step, after the sparse push, under the dW GEMM
+        (CtrTrainStep.set_next / prefetch); ``prep(buf, j)`` pools buffer j
+        eagerly when its graph finds it unprepared, ``set_next(buf, j)`` tells
+        the step what to pool (None: nothing), ``clear()`` drops the engine's
+        host-side prepared entries.  Load buffers two steps ahead:
+        graph j waits for buffer j+1's copy.
+        ``warmup`` eager runs of ``step_fn`` on the example batch precede
         the capture (lazy allocations, kernel selection).  A trainer that must
         not train a batch twice passes ``warmup=0`` and ``warm_batches``: real
         batches run eagerly through the same buffers before the capture
@@ -101,12 +110,17 @@ class GraphedTrainStep:
         self.step_fn = step_fn
         self.fields = _tensor_fields(example_batch)
         self.K = max(1, int(steps_per_graph))
-        if self.K > 1 and prefetch is not None:
+        if self.K > 1 and (prefetch is not None or pipeline is not None):
             raise ValueError("steps_per_graph > 1 does not combine with the pipelined pull")
+        if prefetch is not None and pipeline is not None:
+            raise ValueError("prefetch and pipeline are alternatives")
+        self.pipeline = pipeline
         self.bufs = [clone_batch(example_batch, self.device) for _ in range(n_buffers * self.K)]
         cur = torch.cuda.current_stream(self.device)
         s = side_stream(self.device, "graph_warmup")
         s.wait_stream(cur)
+        if pipeline is not None:
+            pipeline[1](None, 0)  # eager warm-up steps pool nothing ahead
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 step_fn(self.bufs[0])
@@ -130,6 +144,8 @@ class GraphedTrainStep:
             eng, keys_of = prefetch
             eng.clear_prefetch()
             eng.prefetch(keys_of(self.bufs[0]), 0)  # graph 0's pull finds buffer 0 prepared
+        if pipeline is not None:
+            pipeline[0](self.bufs[0], 0)  # graph 0's pull finds buffer 0 pooled
         self.graphs = []
         pool = None
         n = n_buffers
@@ -140,6 +156,8 @@ class GraphedTrainStep:
             # the eager (warm-up) collectives; under the default global mode
             # such a query from another thread invalidates the capture and
             # kills the watchdog (hipErrorStreamCaptureUnsupported)
+            if pipeline is not None:
+                pipeline[1](self.bufs[(j + 1) % n], (j + 1) % n)  # graph j pools buffer j+1 after its push
             with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 if prefetch is not None:
                     eng, keys_of = prefetch
@@ -156,6 +174,10 @@ class GraphedTrainStep:
             self.graphs.append((g, out))
         if prefetch is not None:
             prefetch[0].clear_prefetch()
+        if pipeline is not None:
+            pipeline[1](None, 0)
+            if len(pipeline) > 2:
+                pipeline[2]()  # the host-side prepared entries only steer captures
         torch.cuda.synchronize(self.device)
         self.copy_stream = side_stream(self.device, "graph_copy")
         self.ready = [torch.cuda.Event() for _ in range(n_buffers)]
@@ -218,6 +240,15 @@ class GraphedTrainStep:
         if self.step_no >= self.max_inflight:
             self.done[slot].synchronize()
         cur.wait_event(self.ready[i])
+        if self.pipeline is not None:
+            n = len(self.bufs)
+            cur.wait_event(self.ready[(i + 1) % n])  # graph i pools buffer i+1
+            if self._pref_ver[i] != self._ver[i]:
+                # buffer i was not pooled by the previous replay with its
+                # current contents: pool it now
+                self.pipeline[0](self.bufs[i], i)
+                self.pipeline[2]() if len(self.pipeline) > 2 else None
+            self._pref_ver[(i + 1) % n] = self._ver[(i + 1) % n]
         if self.prefetch is not None:
             n = len(self.bufs)
             cur.wait_event(self.ready[(i + 1) % n])  # graph i prefetches buffer i+1
