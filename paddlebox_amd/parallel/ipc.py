@@ -22,9 +22,10 @@ collectives on a mesh (as with RCCL).  A launch reads the mesh epoch from
 device memory, so two collectives of one mesh must never be in flight at once:
 a mesh built with ``stream=<name>`` issues every launch on that named side
 stream (forked from and joined back into the caller's stream), which orders
-them -- the dense mesh uses the tower's dW stream, where the gradient
-all-reduce, a data_norm statistics all-reduce and a transpiled
-c_allreduce_sum issued from the compute stream then queue in issue order.
+them -- the dense mesh uses the dense-sync stream, where the gradient
+all-reduce (DenseSync.launch issues there), a data_norm statistics
+all-reduce from the tower's dW stream and a transpiled c_allreduce_sum from
+the compute stream then queue in issue order.
 The sparse exchange meshes are only ever issued from one stream and skip it.  A peer that never arrives makes the
 wait time out: the sticky error poisons the results (NaN sums, empty
 exchanges) and :meth:`check` raises on the host, instead of hanging the GPU

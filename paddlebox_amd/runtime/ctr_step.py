@@ -36,8 +36,11 @@ def make_ipc_mesh(nbytes: int, device, group=None, log=None):
 
     try:
         # dense collectives (gradient all-reduce, data_norm statistics,
-        # c_allreduce_sum) queue on the tower's dW stream, in issue order
-        m = IpcMesh(nbytes, group=group, device=device, stream="tower_dw")
+        # c_allreduce_sum) queue on the dense-sync side stream, in issue order
+        # (DenseSync.launch issues there itself: no fork on the hot path; a
+        # fork from the tower's dW stream back into it, inside a captured
+        # graph, crashed the capture)
+        m = IpcMesh(nbytes, group=group, device=device, stream="dense_sync")
     except IpcMeshError as e:
         if log:
             log(f"IPC mesh unavailable ({e}); RCCL all-reduce")
