@@ -24,7 +24,7 @@ from torch import nn
 
 from ..ops.ctr import DataNorm, ctr_head, fm_interaction, logit_logloss
 from ..ops.mlp import FusedMLP, pad8
-from ..ops.sparse import prefetch_seqpool_cvm_concat, pull_seqpool_cvm_concat
+from ..ops.sparse import prefetch_pool_seqpool_cvm_concat, prefetch_seqpool_cvm_concat, pull_seqpool_cvm_concat
 from ..ops.tower import CtrTower
 from ..ps.sparse_engine import SeqpoolParams, SparseEngine
 
@@ -88,6 +88,11 @@ class DeepFM(nn.Module):
         step starts at the data_norm head (ops/sparse.py)."""
         return prefetch_seqpool_cvm_concat(self.engine, batch.keys, batch.lod, batch.B, batch.S, batch.dense, self.sp,
                                            slot)
+
+    def prefetch_pool(self, batch, slot: int) -> bool:
+        """The pooling half of prefetch (its dedup issued earlier: engine.prefetch_dedup)."""
+        return prefetch_pool_seqpool_cvm_concat(self.engine, batch.keys, batch.lod, batch.B, batch.S, batch.dense,
+                                                self.sp, slot)
 
     def forward(self, batch):
         B, S = batch.B, batch.S

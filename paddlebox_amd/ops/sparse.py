@@ -78,6 +78,15 @@ def prefetch_seqpool_cvm_concat(engine: SparseEngine, keys: torch.Tensor, lod: t
     return engine.prefetch_pull(keys, lod, B, S, sp or SeqpoolParams(), dense, slot)
 
 
+def prefetch_pool_seqpool_cvm_concat(engine: SparseEngine, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int,
+                                     dense: Optional[torch.Tensor] = None, sp: Optional[SeqpoolParams] = None,
+                                     slot: int = 0) -> bool:
+    """The pooling half of prefetch_seqpool_cvm_concat, after an
+    ``engine.prefetch_dedup(keys, slot)`` issued earlier (e.g. on a side
+    stream beside the previous step's push)."""
+    return engine.prefetch_pool(keys, lod, B, S, sp or SeqpoolParams(), dense, slot)
+
+
 class _PullBoxSparse(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor: torch.Tensor, keys: torch.Tensor, lod: torch.Tensor, engine: SparseEngine, B: int,

@@ -129,6 +129,8 @@ class _CtrTowerFn(torch.autograd.Function):
             dx0 = ws.backward(*args, parts=1)
             deferred_dw = torch.cuda.Event()
             deferred_dw.record(cur)
+            if t.on_dx_done is not None:  # e.g. the next batch's key dedup on a side stream
+                t.on_dx_done(deferred_dw)
             if not t.dw_after_head:
                 _launch_dw(t, ws, args, dense_tail, x.device, deferred_dw)
                 deferred_dw = None
@@ -192,6 +194,10 @@ class CtrTower:
         # called in the backward once every dense gradient (and data_norm
         # statistic) of the tower is final, before the sparse push runs
         self.on_dense_grads = None
+        # called with an event on the compute stream once the dX chain is
+        # enqueued (the tower's big MFMA kernels are then behind it): work that
+        # should overlap the dW / head backward / sparse push forks from it
+        self.on_dx_done = None
         # run the dW GEMM on a side stream, overlapped with the head backward
         # and the sparse push (PBX_TOWER_OVERLAP_DW=0 turns it off)
         self.overlap_dw = os.environ.get("PBX_TOWER_OVERLAP_DW", "1") != "0"

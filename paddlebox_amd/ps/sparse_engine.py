@@ -549,6 +549,9 @@ class SparseEngine:
             self.table.t.probe_into(sl.ws.uniq_h[:L], sl.ws.u_count, sl.rows)
         self._prepared[keys.data_ptr()] = (sl, L)
 
+    def can_prefetch_pull(self) -> bool:
+        return self.can_prefetch() and self.table_dedup and self.codec is None
+
     def prefetch_pull(self, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int, sp: "SeqpoolParams",
                       dense: Optional[torch.Tensor] = None, slot: int = 0) -> bool:
         """Dedup + probe AND the fused seqpool + CVM (+ dense columns) of a
@@ -558,14 +561,32 @@ class SparseEngine:
         stream, it runs under the previous step's dW GEMM; the batch's own
         pull then returns the buffer with no launch at all.  False when the
         engine cannot prepare pulls (sharded, codec rows, auto-insert)."""
-        if not (self.can_prefetch() and self.table_dedup and self.codec is None):
+        if not self.prefetch_dedup(keys, slot):
+            return False
+        return self.prefetch_pool(keys, lod, B, S, sp, dense, slot)
+
+    def prefetch_dedup(self, keys: torch.Tensor, slot: int = 0) -> bool:
+        """The key half of prefetch_pull (table dedup + probe into the slot):
+        depends on the keys only, so it may run on a side stream beside the
+        previous step's sparse push."""
+        if not self.can_prefetch_pull():
+            return False
+        assert keys.numel() <= self.max_keys
+        sl = self._slots[slot % len(self._slots)]
+        sl.ws.run_table(keys, self.table.t)
+        sl.rows = sl.ws.rows_u
+        return True
+
+    def prefetch_pool(self, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int, sp: "SeqpoolParams",
+                      dense: Optional[torch.Tensor] = None, slot: int = 0) -> bool:
+        """The value half of prefetch_pull: the fused seqpool of the slot's
+        deduplicated batch into its persistent output (after prefetch_dedup
+        and after every push the values must include, in stream order)."""
+        if not self.can_prefetch_pull():
             return False
         L = keys.numel()
-        assert L <= self.max_keys
         sl = self._slots[slot % len(self._slots)]
         ws = sl.ws
-        ws.run_table(keys, self.table.t)
-        sl.rows = ws.rows_u
         Eo = sp.out_width(self.E)
         Dd = 0 if dense is None else int(dense.shape[1])
         shape = (B, S * Eo + Dd)

@@ -125,10 +125,33 @@ class CtrTrainStep:
         # after this step's sparse push, under this step's dW GEMM
         self.next_batch = None
         self.next_slot = 0
+        self._dedup_ev = None
+        # the next batch's key dedup runs on its own side stream, forked once
+        # this step's dX chain is enqueued (beside the head backward, the dW
+        # GEMM and the sparse push); its pooling follows the push on this
+        # stream.  PBX_SPLIT_PREFETCH=0: both halves after the push.
+        self.split_prefetch = (os.environ.get("PBX_SPLIT_PREFETCH", "1") != "0" and tower is not None
+                               and hasattr(model, "prefetch_pool"))
+        if self.split_prefetch:
+            tower.on_dx_done = self._dedup_next
 
     def set_next(self, batch, slot: int = 0):
         """Batch to prefetch (pool) at the end of each train_step (None: off)."""
         self.next_batch, self.next_slot = batch, int(slot)
+
+    def _dedup_next(self, after):
+        nb = self.next_batch
+        if nb is None or not self.engine.can_prefetch_pull():
+            return
+        from .streams import side_stream
+
+        st = side_stream(self.device, "graph_prefetch")
+        st.wait_event(after)
+        with torch.cuda.stream(st):
+            self.engine.prefetch_dedup(nb.keys, self.next_slot)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        self._dedup_ev = ev
 
     def prefetch(self, batch, slot: int) -> bool:
         pre = getattr(self.model, "prefetch", None)
@@ -145,7 +168,12 @@ class CtrTrainStep:
         if self.next_batch is not None:
             # the sparse push is on this stream already: pool the next batch
             # now, beside the dW GEMM on the tower's side stream
-            self.prefetch(self.next_batch, self.next_slot)
+            if self._dedup_ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(self._dedup_ev)
+                self._dedup_ev = None
+                self.model.prefetch_pool(self.next_batch, self.next_slot)
+            else:
+                self.prefetch(self.next_batch, self.next_slot)
         if self.adam_side:
             join_grad_producers()  # the side stream ran the update
         else:
