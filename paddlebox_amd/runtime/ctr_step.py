@@ -68,6 +68,7 @@ class CtrTrainStep:
 
         device = engine.device
         self.device = device
+        self.engine = engine
         dcn = model_name == "dcn_v2"
         fp32 = precision == "fp32"
         if dcn:
