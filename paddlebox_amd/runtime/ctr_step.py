@@ -130,8 +130,10 @@ class CtrTrainStep:
         # the next batch's key dedup runs on its own side stream, forked once
         # this step's dX chain is enqueued (beside the head backward, the dW
         # GEMM and the sparse push); its pooling follows the push on this
-        # stream.  PBX_SPLIT_PREFETCH=0: both halves after the push.
-        self.split_prefetch = (os.environ.get("PBX_SPLIT_PREFETCH", "1") != "0" and tower is not None
+        # stream.  Off by default (PBX_SPLIT_PREFETCH=1 turns it on): the
+        # dedup grabs the CUs ahead of the head backward and delays the dW
+        # start (0.413 vs 0.398 ms/step, profiles/r4_pipeline_ab.txt)
+        self.split_prefetch = (os.environ.get("PBX_SPLIT_PREFETCH", "0") == "1" and tower is not None
                                and hasattr(model, "prefetch_pool"))
         if self.split_prefetch:
             tower.on_dx_done = self._dedup_next
