@@ -902,8 +902,22 @@ void launch_tower32_dw(const TowerArgs& a, hipStream_t s) {
       hipLaunchKernelGGL((k_t32_dw<2, 5>), g, b, 10 * kDwStep * 4, s, a, ndw);
       break;
     }
-    default:
-      hipLaunchKernelGGL((k_t32_dw<2, 3>), g, b, 6 * kDwStep * 4, s, a, ndw);
+    default: {
+      // PBX_T32_DW_LDS: LDS bytes a 2x3 workgroup reserves (>= its 48 KB ring).
+      // More caps the dW workgroups per CU (160 KB / bytes) and leaves LDS for
+      // the sparse kernels running beside it (the table dedup needs 12 KB)
+      static const int lds = [] {
+        const char* e = getenv("PBX_T32_DW_LDS");
+        const int v = e ? atoi(e) : 0;
+        return v > 6 * kDwStep * 4 ? (v < 150 * 1024 ? v : 150 * 1024) : 6 * kDwStep * 4;
+      }();
+      if (lds > 64 * 1024) {
+        static const bool big = hipFuncSetAttribute((const void*)k_t32_dw<2, 3>,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+        (void)big;
+      }
+      hipLaunchKernelGGL((k_t32_dw<2, 3>), g, b, lds, s, a, ndw);
+    }
   }
 }
 
