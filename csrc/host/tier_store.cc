@@ -506,12 +506,12 @@ void SsdLog::replay(Seg* s) {
       if (key == kEmptyKey) continue;  // unused slot (pages are 0xFF-filled)
       const int64_t slot = p * per_page_ + r;
       s->slots = std::max(s->slots, slot + 1);
-      auto it = index_.find(key);
-      if (it != index_.end()) segs_[it->second.seg]->live--;
       if (flags & 1u) {
-        if (it != index_.end()) index_.erase(it);
+        const int32_t old = index_.erase(key);
+        if (old >= 0) segs_[old]->live--;
       } else {
-        index_[key] = Loc{s->id, slot};
+        const int32_t old = index_.set(key, Loc{s->id, slot});
+        if (old >= 0) segs_[old]->live--;
         s->live++;
       }
     }
@@ -555,42 +555,36 @@ void SsdLog::flush_pages(Seg* s, int64_t first_page, int64_t npages) {
   }
 }
 
-void SsdLog::append(uint64_t key, const float* v, bool tomb, std::vector<std::pair<uint64_t, Loc>>* placed) {
-  Seg* s = segs_.back().get();
-  if (s->slots >= seg_pages_ * per_page_) {
-    open_segment();
-    s = segs_.back().get();
-  }
-  const int64_t slot = s->slots++;
-  char* rec = active_buf_ + page_of(slot) * kPage + (slot % per_page_) * rec_bytes_;
-  const uint32_t flags = tomb ? 1u : 0u;
-  std::memcpy(rec, &key, 8);
-  std::memcpy(rec + 8, &flags, 4);
-  if (v)
-    std::memcpy(rec + 12, v, (size_t)stride_ * 4);
-  else
-    std::memset(rec + 12, 0, (size_t)stride_ * 4);
-  placed->emplace_back(key, Loc{tomb ? -1 : s->id, slot});
-}
-
 // append records (tomb: deletions) in page-aligned batches, one pwrite per
 // touched page range of each segment
 void SsdLog::write_batch(const uint64_t* h, const float* vals, int64_t n, int vstride, bool tomb,
                          std::vector<std::pair<uint64_t, Loc>>* placed) {
-  std::vector<float> row(stride_, 0.f);
+  const int w = std::min(vstride, stride_);
   int64_t i = 0;
   while (i < n) {
     if (segs_.back()->slots >= seg_pages_ * per_page_) open_segment();
     Seg* s = segs_.back().get();
-    const int64_t first_page = page_of(s->slots);
-    const int64_t take = std::min<int64_t>(seg_pages_ * per_page_ - s->slots, n - i);
-    for (int64_t j = 0; j < take; ++j, ++i) {
-      if (!tomb) {
-        const int w = std::min(vstride, stride_);
-        std::memcpy(row.data(), vals + i * vstride, (size_t)w * 4);
+    const int64_t slot0 = s->slots;
+    const int64_t first_page = page_of(slot0);
+    const int64_t take = std::min<int64_t>(seg_pages_ * per_page_ - slot0, n - i);
+    // records land in consecutive slots: pack them in parallel
+#pragma omp parallel for schedule(static) if (take > 65536)
+    for (int64_t j = 0; j < take; ++j) {
+      const int64_t slot = slot0 + j;
+      char* rec = active_buf_ + page_of(slot) * kPage + (slot % per_page_) * rec_bytes_;
+      const uint32_t flags = tomb ? 1u : 0u;
+      std::memcpy(rec, h + i + j, 8);
+      std::memcpy(rec + 8, &flags, 4);
+      if (tomb) {
+        std::memset(rec + 12, 0, (size_t)stride_ * 4);
+      } else {
+        std::memcpy(rec + 12, vals + (i + j) * vstride, (size_t)w * 4);
+        if (w < stride_) std::memset(rec + 12 + (size_t)w * 4, 0, (size_t)(stride_ - w) * 4);
       }
-      append(h[i], tomb ? nullptr : row.data(), tomb, placed);
     }
+    for (int64_t j = 0; j < take; ++j) placed->emplace_back(h[i + j], Loc{tomb ? -1 : s->id, slot0 + j});
+    s->slots += take;
+    i += take;
     flush_pages(s, first_page, page_of(s->slots - 1) - first_page + 1);
   }
 }
@@ -601,9 +595,8 @@ void SsdLog::put(const uint64_t* h, const float* vals, int64_t n, int vstride) {
   placed.reserve(n);
   write_batch(h, vals, n, vstride, false, &placed);
   for (auto& kl : placed) {
-    auto it = index_.find(kl.first);
-    if (it != index_.end()) segs_[it->second.seg]->live--;
-    index_[kl.first] = kl.second;
+    const int32_t old = index_.set(kl.first, kl.second);
+    if (old >= 0) segs_[old]->live--;
     segs_[kl.second.seg]->live++;
   }
 }
@@ -612,10 +605,9 @@ int64_t SsdLog::erase(const uint64_t* h, int64_t n) {
   std::lock_guard<std::mutex> lk(mu_);
   std::vector<uint64_t> dead;
   for (int64_t i = 0; i < n; ++i) {
-    auto it = index_.find(h[i]);
-    if (it == index_.end()) continue;
-    segs_[it->second.seg]->live--;
-    index_.erase(it);
+    const int32_t old = index_.erase(h[i]);
+    if (old < 0) continue;
+    segs_[old]->live--;
     dead.push_back(h[i]);
   }
   std::vector<std::pair<uint64_t, Loc>> placed;
@@ -641,13 +633,13 @@ void SsdLog::get(const uint64_t* h, int64_t n, uint8_t* found, float* out, int o
   std::vector<Want> want;
   for (int64_t i = 0; i < n; ++i) {
     float* o = out + i * out_stride;
-    auto it = index_.find(h[i]);
-    if (it == index_.end()) {
+    const Loc* it = index_.find(h[i]);
+    if (it == nullptr) {
       found[i] = 0;
       std::memset(o, 0, (size_t)out_stride * 4);
       continue;
     }
-    const Loc l = it->second;
+    const Loc l = *it;
     found[i] = 1;
     if (l.seg == active) {
       const char* rec = active_buf_ + page_of(l.slot) * kPage + (l.slot % per_page_) * rec_bytes_;
@@ -726,7 +718,7 @@ std::vector<uint64_t> SsdLog::keys() const {
   std::lock_guard<std::mutex> lk(mu_);
   std::vector<uint64_t> out;
   out.reserve(index_.size());
-  for (auto& kv : index_) out.push_back(kv.first);
+  index_.for_each([&](uint64_t k, const Loc&) { out.push_back(k); });
   return out;
 }
 
@@ -746,8 +738,9 @@ int64_t SsdLog::compact(double min_live) {
       if (s->id != active && s->fd >= 0 && s->slots > 0 && (double)s->live / (double)s->slots < min_live)
         victims.push_back(s->id);
     if (victims.empty()) return 0;
-    for (auto& kv : index_)
-      if (std::find(victims.begin(), victims.end(), kv.second.seg) != victims.end()) keys.push_back(kv.first);
+    index_.for_each([&](uint64_t k, const Loc& l) {
+      if (std::find(victims.begin(), victims.end(), l.seg) != victims.end()) keys.push_back(k);
+    });
   }
   // re-append the victims' live records (newest copy wins through the index)
   std::vector<uint8_t> f(keys.size());
@@ -781,7 +774,7 @@ int64_t SsdLog::compact(double min_live) {
           uint32_t flags;
           std::memcpy(&key, rec, 8);
           std::memcpy(&flags, rec + 8, 4);
-          if (key != kEmptyKey && (flags & 1u) && index_.find(key) == index_.end()) carry.push_back(key);
+          if (key != kEmptyKey && (flags & 1u) && index_.find(key) == nullptr) carry.push_back(key);
         }
       }
     }

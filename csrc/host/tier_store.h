@@ -102,12 +102,97 @@ class HostTier {
   std::unique_ptr<ThreadPool> pool_;
 };
 
+// key -> record location of the SSD log: open addressing over flat arrays
+// (linear probing, backward-shift deletion, load <= 1/2).  A node-based map
+// costs an allocation per record, which dominated a multi-million-row spill.
+class LocIndex {
+ public:
+  struct Loc {
+    int32_t seg;
+    int64_t slot;
+  };
+  LocIndex() { rehash(1024); }
+  int64_t size() const { return n_; }
+  const Loc* find(uint64_t k) const {
+    for (uint64_t i = home(k);; i = (i + 1) & mask_) {
+      if (keys_[i] == k) return &locs_[i];
+      if (keys_[i] == kEmptyKey) return nullptr;
+    }
+  }
+  // insert or overwrite; returns the previous location's segment (-1: new key)
+  int32_t set(uint64_t k, Loc l) {
+    if ((n_ + 1) * 2 > (int64_t)keys_.size()) rehash(keys_.size() * 2);
+    for (uint64_t i = home(k);; i = (i + 1) & mask_) {
+      if (keys_[i] == k) {
+        const int32_t old = locs_[i].seg;
+        locs_[i] = l;
+        return old;
+      }
+      if (keys_[i] == kEmptyKey) {
+        keys_[i] = k;
+        locs_[i] = l;
+        ++n_;
+        return -1;
+      }
+    }
+  }
+  // returns the erased location's segment (-1: absent)
+  int32_t erase(uint64_t k) {
+    uint64_t i = home(k);
+    for (;; i = (i + 1) & mask_) {
+      if (keys_[i] == k) break;
+      if (keys_[i] == kEmptyKey) return -1;
+    }
+    const int32_t old = locs_[i].seg;
+    // backward shift: pull later members of the probe chain into the hole
+    uint64_t j = i;
+    for (;;) {
+      j = (j + 1) & mask_;
+      if (keys_[j] == kEmptyKey) break;
+      const uint64_t h = home(keys_[j]);
+      const bool movable = (i <= j) ? (h <= i || h > j) : (h <= i && h > j);
+      if (movable) {
+        keys_[i] = keys_[j];
+        locs_[i] = locs_[j];
+        i = j;
+      }
+    }
+    keys_[i] = kEmptyKey;
+    --n_;
+    return old;
+  }
+  template <class F>
+  void for_each(F f) const {
+    for (size_t i = 0; i < keys_.size(); ++i)
+      if (keys_[i] != kEmptyKey) f(keys_[i], locs_[i]);
+  }
+
+ private:
+  uint64_t home(uint64_t k) const { return (k ^ (k >> 29) ^ (k >> 47)) * 0x9E3779B97F4A7C15ULL >> 7 & mask_; }
+  void rehash(size_t cap) {
+    std::vector<uint64_t> ok;
+    std::vector<Loc> ol;
+    ok.swap(keys_);
+    ol.swap(locs_);
+    keys_.assign(cap, kEmptyKey);
+    locs_.resize(cap);
+    mask_ = cap - 1;
+    n_ = 0;
+    for (size_t i = 0; i < ok.size(); ++i)
+      if (ok[i] != kEmptyKey) set(ok[i], ol[i]);
+  }
+  std::vector<uint64_t> keys_;
+  std::vector<Loc> locs_;
+  uint64_t mask_ = 0;
+  int64_t n_ = 0;
+};
+
 class SsdLog {
  public:
   SsdLog(const std::string& dir, int stride, int64_t segment_bytes = 64ll << 20);
   ~SsdLog();
   int stride() const { return stride_; }
-  int64_t size() const { return (int64_t)index_.size(); }
+  int64_t size() const { return index_.size(); }
   int64_t disk_bytes() const;
   bool direct_io() const { return direct_; }
   int64_t segments() const { return (int64_t)segs_.size(); }
@@ -128,13 +213,9 @@ class SsdLog {
     int64_t live = 0;
     std::string path;
   };
-  struct Loc {
-    int32_t seg;
-    int64_t slot;
-  };
+  using Loc = LocIndex::Loc;
   void open_segment();
   void replay(Seg* s);
-  void append(uint64_t key, const float* v, bool tomb, std::vector<std::pair<uint64_t, Loc>>* placed);
   void write_batch(const uint64_t* h, const float* vals, int64_t n, int vstride, bool tomb,
                    std::vector<std::pair<uint64_t, Loc>>* placed);
   void flush_pages(Seg* s, int64_t first_page, int64_t npages);
@@ -147,7 +228,7 @@ class SsdLog {
   int64_t seg_pages_;
   bool direct_ = true;
   std::vector<std::unique_ptr<Seg>> segs_;  // segs_[i]->id == i (closed segments keep their fd)
-  std::unordered_map<uint64_t, Loc> index_;
+  LocIndex index_;
   // the active segment is mirrored in memory (page-aligned, written through)
   char* active_buf_ = nullptr;
   mutable std::mutex mu_;
