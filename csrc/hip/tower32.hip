@@ -905,10 +905,13 @@ void launch_tower32_dw(const TowerArgs& a, hipStream_t s) {
     default: {
       // PBX_T32_DW_LDS: LDS bytes a 2x3 workgroup reserves (>= its 48 KB ring).
       // More caps the dW workgroups per CU (160 KB / bytes) and leaves LDS for
-      // the sparse kernels running beside it (the table dedup needs 12 KB)
+      // the sparse kernels running beside it (the table dedup needs 12 KB).
+      // Default 64 KB: two per CU -- the dW alone is slower (110 vs 100 us)
+      // but the pipelined step beside it faster (0.383 vs 0.397 ms/step;
+      // 80 KB 0.404), profiles/r4_dw_lds_ab.txt
       static const int lds = [] {
         const char* e = getenv("PBX_T32_DW_LDS");
-        const int v = e ? atoi(e) : 0;
+        const int v = e ? atoi(e) : 64 * 1024;
         return v > 6 * kDwStep * 4 ? (v < 150 * 1024 ? v : 150 * 1024) : 6 * kDwStep * 4;
       }();
       if (lds > 64 * 1024) {
