@@ -266,7 +266,8 @@ def main():
     engine = SparseEngine(cfg, max_keys=B * S, device=device, capacity=synth.total_features,
                           slot_ids=[float(s + 1) for s in range(S)], auto_insert=args.no_prefill,
                           exchange_capacity=xcap, exchange=args.sparse_exchange, dedup=args.dedup == "on",
-                          pull_ring=3 if args.pipeline != "off" else 2)
+                          pull_ring=(3 * graph_steps_for(args.steps, args.warmup, args.graph_steps)
+                                     if args.pipeline != "off" else 2))
 
     t0 = time.time()
     if not args.no_prefill:
@@ -323,7 +324,7 @@ def main():
                 if want_pipe and pre is None and engine.can_prefetch() and engine.table_dedup:
                     pipe = (lambda b, j: step.prefetch(b, j), step.set_next, engine.clear_prefetch)
                 graphed = GraphedTrainStep(train_step, host_batches[0], device, prefetch=pre,
-                                           steps_per_graph=K if (pre is None and pipe is None) else 1,
+                                           steps_per_graph=K if pre is None else 1,
                                            n_buffers=3 if pipe is not None else 2, pipeline=pipe)
                 graphed.warm(host_batches, replays=args.graph_warm)
                 log(rank, f"[bench] training step captured into HIP graphs ({args.graph_warm} warm replays)")

@@ -99,8 +99,10 @@ class GraphedTrainStep:
         (CtrTrainStep.set_next / prefetch); ``prep(buf, j)`` pools buffer j
         eagerly when its graph finds it unprepared, ``set_next(buf, j)`` tells
         the step what to pool (None: nothing), ``clear()`` drops the engine's
-        host-side prepared entries.  Load buffers two steps ahead:
-        graph j waits for buffer j+1's copy.
+        host-side prepared entries.  Load buffers two graphs ahead: graph j
+        waits for buffer set j+1's copy.  With K steps per graph, step k
+        pools step k+1's batch inside the graph and the last step pools the
+        next graph's first (pull slot = batch buffer index: n_buffers * K).
         ``warmup`` eager runs of ``step_fn`` on the example batch precede
         the capture (lazy allocations, kernel selection).  A trainer that must
         not train a batch twice passes ``warmup=0`` and ``warm_batches``: real
@@ -110,7 +112,7 @@ class GraphedTrainStep:
         self.step_fn = step_fn
         self.fields = _tensor_fields(example_batch)
         self.K = max(1, int(steps_per_graph))
-        if self.K > 1 and (prefetch is not None or pipeline is not None):
+        if self.K > 1 and prefetch is not None:
             raise ValueError("steps_per_graph > 1 does not combine with the pipelined pull")
         if prefetch is not None and pipeline is not None:
             raise ValueError("prefetch and pipeline are alternatives")
@@ -146,6 +148,7 @@ class GraphedTrainStep:
             eng.prefetch(keys_of(self.bufs[0]), 0)  # graph 0's pull finds buffer 0 prepared
         if pipeline is not None:
             pipeline[0](self.bufs[0], 0)  # graph 0's pull finds buffer 0 pooled
+        nK = n_buffers * self.K  # batch buffers (= pull slots of the pipeline)
         self.graphs = []
         pool = None
         n = n_buffers
@@ -156,8 +159,6 @@ class GraphedTrainStep:
             # the eager (warm-up) collectives; under the default global mode
             # such a query from another thread invalidates the capture and
             # kills the watchdog (hipErrorStreamCaptureUnsupported)
-            if pipeline is not None:
-                pipeline[1](self.bufs[(j + 1) % n], (j + 1) % n)  # graph j pools buffer j+1 after its push
             with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 if prefetch is not None:
                     eng, keys_of = prefetch
@@ -166,6 +167,10 @@ class GraphedTrainStep:
                     with torch.cuda.stream(self._side):
                         eng.prefetch(keys_of(self.bufs[(j + 1) % n]), (j + 1) % n)
                 for k in range(self.K):
+                    if pipeline is not None:
+                        # step b pools buffer b+1 after its push (across graphs: the next graph's first)
+                        b1 = (j * self.K + k + 1) % nK
+                        pipeline[1](self.bufs[b1], b1)
                     out = step_fn(self.bufs[j * self.K + k])
                     join_grad_producers()  # side streams forked in the step rejoin (before the capture ends)
                 if prefetch is not None:
@@ -244,9 +249,9 @@ class GraphedTrainStep:
             n = len(self.bufs)
             cur.wait_event(self.ready[(i + 1) % n])  # graph i pools buffer i+1
             if self._pref_ver[i] != self._ver[i]:
-                # buffer i was not pooled by the previous replay with its
-                # current contents: pool it now
-                self.pipeline[0](self.bufs[i], i)
+                # buffer set i's first batch was not pooled by the previous
+                # replay with its current contents: pool it now
+                self.pipeline[0](self.bufs[i * self.K], i * self.K)
                 self.pipeline[2]() if len(self.pipeline) > 2 else None
             self._pref_ver[(i + 1) % n] = self._ver[(i + 1) % n]
         if self.prefetch is not None:

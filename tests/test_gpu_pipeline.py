@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 
 
-def _setup(seed_batches=7):
+def _setup(seed_batches=7, ring=3):
     from paddlebox_amd.data.synthetic import CriteoSynth
     from paddlebox_amd.ops import reference as ref
     from paddlebox_amd.ps.config import PSConfig
@@ -23,43 +23,54 @@ def _setup(seed_batches=7):
     bs = [synth.batch(512) for _ in range(8)]
     S = bs[0].S
     eng = SparseEngine(PSConfig(embedx_dim=8), max_keys=512 * S, device=DEV, capacity=300_000,
-                       slot_ids=[float(s + 1) for s in range(S)], pull_ring=3)
+                       slot_ids=[float(s + 1) for s in range(S)], pull_ring=ring)
     allk = torch.cat([b.keys for b in bs])
     eng.insert_local_mixed(torch.unique(ref.mix64(allk[allk != -1])).to(DEV), init_embedx=True)
     hbs = [pack_batch(b, pin=True) for b in bs]
     return eng, hbs, S
 
 
-def _train(pipeline: bool, precision: str):
+def _train(pipeline: bool, precision: str, K: int = 1):
     from paddlebox_amd.runtime.ctr_step import CtrTrainStep
     from paddlebox_amd.runtime.graph_step import GraphedTrainStep
 
-    eng, hbs, S = _setup()
+    eng, hbs, S = _setup(ring=3 * K)
     torch.manual_seed(0)
     step = CtrTrainStep(eng, "deepfm", precision, num_slots=S, hidden=(64, 64, 64))
     pipe = (lambda b, j: step.prefetch(b, j), step.set_next, eng.clear_prefetch) if pipeline else None
     losses = []
     g = GraphedTrainStep(step.train_step, hbs[0], DEV, warmup=0, warm_batches=[hbs[0]],
                          on_warm=lambda out: losses.append(float(out)), n_buffers=3 if pipeline else 2,
-                         pipeline=pipe)
-    ahead = 2 if pipeline else 1
-    for a in range(1, 1 + ahead):
-        g.load(a % g.n, hbs[a])
-    for i in range(1, len(hbs)):
-        if i + ahead < len(hbs):
-            g.load((i + ahead) % g.n, hbs[i + ahead])
-        out = g.run(i % g.n)
-        torch.cuda.synchronize()
-        losses.append(float(out))
+                         pipeline=pipe, steps_per_graph=K)
+    if K == 1:
+        ahead = 2 if pipeline else 1
+        for a in range(1, 1 + ahead):
+            g.load(a % g.n, hbs[a])
+        for i in range(1, len(hbs)):
+            if i + ahead < len(hbs):
+                g.load((i + ahead) % g.n, hbs[i + ahead])
+            out = g.run(i % g.n)
+            torch.cuda.synchronize()
+            losses.append(float(out))
+    else:  # batches 1.. in groups of K (the graph returns its last step's loss)
+        groups = [hbs[1 + q * K:1 + (q + 1) * K] for q in range((len(hbs) - 1) // K)]
+        for a in range(min(2, len(groups))):
+            g.load(a % g.n, groups[a])
+        for q in range(len(groups)):
+            if q + 2 < len(groups):
+                g.load((q + 2) % g.n, groups[q + 2])
+            out = g.run(q % g.n)
+            torch.cuda.synchronize()
+            losses.append(float(out))
     hk, v = eng.table.export(True)
     o = torch.argsort(hk)
     return step.arena.flat.cpu(), losses, hk[o].cpu(), v[o].cpu()
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_pipelined_front_matches_plain_graphed_step(precision):
-    f0, l0, k0, v0 = _train(False, precision)
-    f1, l1, k1, v1 = _train(True, precision)
+@pytest.mark.parametrize("precision,K", [("fp32", 1), ("bf16", 1), ("fp32", 2)])
+def test_pipelined_front_matches_plain_graphed_step(precision, K):
+    f0, l0, k0, v0 = _train(False, precision, K)
+    f1, l1, k1, v1 = _train(True, precision, K)
     assert l1 == pytest.approx(l0, rel=1e-6, abs=1e-7)
     torch.testing.assert_close(f1, f0, rtol=1e-6, atol=1e-7)
     assert torch.equal(k1, k0)
