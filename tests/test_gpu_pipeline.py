@@ -54,11 +54,12 @@ def _train(pipeline: bool, precision: str, K: int = 1):
             losses.append(float(out))
     else:  # batches 1.. in groups of K (the graph returns its last step's loss)
         groups = [hbs[1 + q * K:1 + (q + 1) * K] for q in range((len(hbs) - 1) // K)]
-        for a in range(min(2, len(groups))):
+        ahead = 2 if pipeline else 1
+        for a in range(min(ahead, len(groups))):
             g.load(a % g.n, groups[a])
         for q in range(len(groups)):
-            if q + 2 < len(groups):
-                g.load((q + 2) % g.n, groups[q + 2])
+            if q + ahead < len(groups):
+                g.load((q + ahead) % g.n, groups[q + ahead])
             out = g.run(q % g.n)
             torch.cuda.synchronize()
             losses.append(float(out))
