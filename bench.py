@@ -331,6 +331,9 @@ def main():
             except Exception as e:  # pragma: no cover - depends on runtime
                 log(rank, f"[bench] graph capture failed ({e!r}); running eagerly")
                 graphed = None
+                # no pooling ahead in the eager loop: forget what the capture prepared
+                step.set_next(None)
+                engine.clear_prefetch()
 
         if graphed is not None:
             K = graphed.K  # run(i) trains group i: steps i*K .. i*K+K-1

@@ -246,8 +246,8 @@ class GraphedTrainStep:
             self.done[slot].synchronize()
         cur.wait_event(self.ready[i])
         if self.pipeline is not None:
-            n = len(self.bufs)
-            cur.wait_event(self.ready[(i + 1) % n])  # graph i pools buffer i+1
+            n = len(self.graphs)
+            cur.wait_event(self.ready[(i + 1) % n])  # graph i pools buffer set i+1's first batch
             if self._pref_ver[i] != self._ver[i]:
                 # buffer set i's first batch was not pooled by the previous
                 # replay with its current contents: pool it now

@@ -72,7 +72,9 @@ def _train(pipeline: bool, precision: str, K: int = 1):
 def test_pipelined_front_matches_plain_graphed_step(precision, K):
     f0, l0, k0, v0 = _train(False, precision, K)
     f1, l1, k1, v1 = _train(True, precision, K)
-    assert l1 == pytest.approx(l0, rel=1e-6, abs=1e-7)
-    torch.testing.assert_close(f1, f0, rtol=1e-6, atol=1e-7)
+    # the dW split-K atomics sum in any order: fp32-rounding-level differences
+    rt, at = (1e-6, 1e-7) if precision == "fp32" else (1e-4, 1e-5)
+    assert l1 == pytest.approx(l0, rel=rt, abs=at)
+    torch.testing.assert_close(f1, f0, rtol=rt, atol=at)
     assert torch.equal(k1, k0)
-    torch.testing.assert_close(v1, v0, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(v1, v0, rtol=rt, atol=at)
