@@ -110,10 +110,14 @@ def dry_run(args, world, rank):
 def graph_steps_for(steps: int, warmup: int, requested: int = 0) -> int:
     """Steps per captured graph: every timed and warmup step still runs in
     full; only the graph-launch boundary (and the wait on the batch copy) is
-    paid once per K steps instead of once per step."""
+    paid once per K steps instead of once per step.  requested -1 (default):
+    2 when it divides the timed steps, else 1 (a warmup remainder runs
+    eagerly)."""
+    if requested < 0:
+        return 2 if steps % 2 == 0 else 1
     if requested > 0:
-        if steps % requested or warmup % requested:
-            raise SystemExit(f"--graph-steps {requested} must divide --steps {steps} and --warmup {warmup}")
+        if steps % requested:
+            raise SystemExit(f"--graph-steps {requested} must divide --steps {steps}")
         return requested
     for k in range(8, 0, -1):
         if steps % k == 0 and warmup % k == 0:
@@ -148,9 +152,10 @@ def main():
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--diag-windows", type=int, default=0,
                     help="after the measurement, time this many more K-step windows (stderr only)")
-    ap.add_argument("--graph-steps", type=int, default=1,
+    ap.add_argument("--graph-steps", type=int, default=-1,
                     help="training steps per captured HIP graph (0 = auto: the largest k <= 8 dividing both --steps "
-                         "and --warmup).  Default 1: K = 5 / 8 measured no faster (profiles/r3_s2_multistep_graph.txt)")
+                         "and --warmup).  Default -1: 2 when it divides --steps (pipelined fp32 step 0.371 vs 0.393 "
+                         "ms at K = 1, 0.377 at K = 5, profiles/r4_graph_steps_ab.txt), else 1")
     ap.add_argument("--graph-warm", type=int, default=32,
                     help="load+replay cycles run right after capture (runtime warm-up, part of graph setup)")
     ap.add_argument("--trace-steps", type=int, default=0,
@@ -387,6 +392,13 @@ def main():
         wg, sg = args.warmup // K, args.steps // K
         for i in range(wg):
             run(i)
+        if graphed is not None and args.warmup % K:
+            # the warmup remainder (W not a multiple of K) as eager steps; the
+            # next replay's batch is pooled again after their pushes
+            step.set_next(None)
+            for r in range(args.warmup % K):
+                train_step(host_batches[(wg * K + r) % nb].to(device))
+            graphed.invalidate_prefetch()
         torch.cuda.synchronize()
         if multi:
             dist.barrier()

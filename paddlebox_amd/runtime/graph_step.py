@@ -226,6 +226,11 @@ class GraphedTrainStep:
                         getattr(dst, f).copy_(getattr(hb, f), non_blocking=True)
             self.ready[i].record(self.copy_stream)
 
+    def invalidate_prefetch(self):
+        """Work outside the graphs changed the table (eager steps): every
+        buffer set is pooled / prepared again before its next replay."""
+        self._pref_ver = [-1] * len(self._pref_ver)
+
     def fill(self, i: int, fn: Callable[[Any], None], stream=None):
         """Produce buffer set i on the device: ``fn(buf)`` enqueues kernels
         that write it (on ``stream``, default the copy stream) once the
