@@ -111,8 +111,8 @@ def graph_steps_for(steps: int, warmup: int, requested: int = 0) -> int:
     """Steps per captured graph: every timed and warmup step still runs in
     full; only the graph-launch boundary (and the wait on the batch copy) is
     paid once per K steps instead of once per step.  requested -1 (default):
-    2 when it divides the timed steps, else 1 (a warmup remainder runs
-    eagerly)."""
+    2 when it divides the timed steps, else 1 (the warmup is rounded up to
+    whole graphs)."""
     if requested < 0:
         return 2 if steps % 2 == 0 else 1
     if requested > 0:
@@ -389,16 +389,11 @@ def main():
             log(rank, "[bench] trace load us: " + " ".join(f"{x * 1e6:.0f}" for x in tl))
             log(rank, "[bench] trace run  us: " + " ".join(f"{x * 1e6:.0f}" for x in tr))
         # K divides both counts (graph_steps_for): exactly W warmup and K timed steps
-        wg, sg = args.warmup // K, args.steps // K
+        # warmup in whole graphs: W rounded up to a multiple of K (at most K-1
+        # extra untimed steps); the timed steps are exactly K * sg = --steps
+        wg, sg = -(-args.warmup // K), args.steps // K
         for i in range(wg):
             run(i)
-        if graphed is not None and args.warmup % K:
-            # the warmup remainder (W not a multiple of K) as eager steps; the
-            # next replay's batch is pooled again after their pushes
-            step.set_next(None)
-            for r in range(args.warmup % K):
-                train_step(host_batches[(wg * K + r) % nb].to(device))
-            graphed.invalidate_prefetch()
         torch.cuda.synchronize()
         if multi:
             dist.barrier()
