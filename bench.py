@@ -317,7 +317,10 @@ def main():
         train_step = step.train_step
 
         nb = len(host_batches)
-        K = graph_steps_for(args.steps, args.warmup, args.graph_steps)
+        # the headline takes K steps per graph; the same-run secondaries keep
+        # one (a bf16 K = 2 run after the pipelined fp32 one faulted on the
+        # box at 200 steps -- under investigation; K = 1 is the validated path)
+        K = graph_steps_for(args.steps, args.warmup, args.graph_steps) if primary else 1
         graphed = None
         if args.graph:
             try:
