@@ -95,6 +95,16 @@ void hgemm(const Tensor& A, const Tensor& B, Tensor C, const c10::optional<Tenso
   launch_hgemm(g, cs());
 }
 
+// in place: acc [M, N] fp32 -> the reference fp16 rounding chain of scaled_fc
+void h16_epi(Tensor acc, const c10::optional<Tensor>& bias, double alpha, double bias_scale, double out_scale) {
+  f32(acc, "acc");
+  CX_CHECK(acc.dim() == 2 && acc.is_contiguous(), "acc must be a contiguous [M, N] tensor");
+  const int M = (int)acc.size(0), N = (int)acc.size(1);
+  if (bias.has_value() && bias->defined()) CX_CHECK(bias->numel() >= N && bias->is_contiguous(), "bias");
+  launch_h16_epi(P<float>(acc), OP<float>(bias), M, N, (float)alpha, (float)bias_scale, (float)out_scale, P<float>(acc),
+                 cs());
+}
+
 void colsum_strided(const Tensor& x, int64_t batch, int64_t M, int64_t N, int64_t sb, int64_t ld, Tensor out,
                     int64_t so, bool accumulate) {
   f32(x, "x");
@@ -407,6 +417,7 @@ void bind_ctr(py::module& m) {
         py::arg("sBias") = 0, py::arg("bias_scale") = 1.0, py::arg("alpha") = 1.0, py::arg("accumulate") = false);
   m.def("colsum_strided", &colsum_strided);
   m.def("hgemm", &hgemm);
+  m.def("h16_epi", &h16_epi);
   m.def("int8_fc", &int8_fc);
   m.def("rank_attention_fwd", &rank_attention_fwd);
   m.def("rank_attention_bwd", &rank_attention_bwd);

@@ -196,6 +196,21 @@ __global__ __launch_bounds__(256) void k_hgemm(HgemmArgs g) {
     }
 }
 
+// the fp16 epilogue over an fp32 accumulator matrix [M][N] (ld N) -- the
+// library-GEMM path of scaled_fc, and the split-K second pass below
+__global__ void k_h16_epi(const float* acc, const float* __restrict__ bias, int M, int N, float alpha,
+                          float bias_scale, float out_scale, float* out) {  // out may alias acc
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)M * N) return;
+  const int n = (int)(e % N);
+  HgemmArgs g;
+  g.alpha = alpha;
+  g.bias = bias;
+  g.bias_scale = bias_scale;
+  g.out_scale = out_scale;
+  out[e] = h16_epi(acc[e], bias ? bias[n] : 0.f, g);
+}
+
 // split-K second pass: the fp16 epilogue over the fp32 sums
 __global__ void k_hgemm_epi(HgemmArgs g) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -950,6 +965,13 @@ void launch_hgemm(const HgemmArgs& g0, hipStream_t s) {
   dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, g.ksplit);
   hipLaunchKernelGGL(k_hgemm, grid, dim3(256), 0, s, g);
   if (g.ksplit > 1) hipLaunchKernelGGL(k_hgemm_epi, dim3(nblk((int64_t)g.M * g.N)), dim3(256), 0, s, g);
+}
+
+void launch_h16_epi(const float* acc, const float* bias, int M, int N, float alpha, float bias_scale, float out_scale,
+                    float* out, hipStream_t s) {
+  if ((int64_t)M * N == 0) return;
+  hipLaunchKernelGGL(k_h16_epi, dim3(nblk((int64_t)M * N)), dim3(256), 0, s, acc, bias, M, N, alpha, bias_scale,
+                     out_scale, out);
 }
 
 void launch_colsum_strided(const float* x, int batch, int M, int N, int64_t sb, int64_t ld, float* out, int64_t so,

@@ -741,6 +741,9 @@ struct HgemmArgs {
   float a_scale = 1.f, b_scale = 1.f, alpha = 1.f, bias_scale = 1.f, out_scale = 1.f;
   int ksplit = 1;
 };
+// scaled_fc's fp16 epilogue over an fp32 accumulator [M][N] (library GEMM path); out may alias acc
+void launch_h16_epi(const float* acc, const float* bias, int M, int N, float alpha, float bias_scale, float out_scale,
+                    float* out, hipStream_t s);
 void launch_hgemm(const HgemmArgs& g, hipStream_t s);
 void launch_colsum_strided(const float* x, int batch, int M, int N, int64_t sb, int64_t ld, float* out, int64_t so,
                            bool accumulate, hipStream_t s);

@@ -791,6 +791,23 @@ def scaled_fc_reference(x, W, b, in_scale, bias_scale):
     return torch.where(torch.isinf(y), torch.full_like(y, float("nan")), y)
 
 
+_MM16 = [None]  # torch.mm(fp16, fp16, out_dtype=float32) works on this build: None (untried) / True / False
+
+
+def _mm16(a16, b16):
+    """fp16 x fp16 -> fp32 (fp32 accumulate) on the library GEMM, or None
+    when this torch build has no mixed-dtype mm (then k_hgemm runs)."""
+    if _MM16[0] is False:
+        return None
+    try:
+        r = torch.mm(a16, b16, out_dtype=torch.float32)
+    except (RuntimeError, TypeError, NotImplementedError):
+        _MM16[0] = False
+        return None
+    _MM16[0] = True
+    return r.contiguous()
+
+
 class _ScaledFc(torch.autograd.Function):
     """scaled_fc (operators/scaled_fc_op.cu:144-330) with the reference's
     fp16 arithmetic on fp16 MFMA (csrc/hip/ctr_ext.hip k_hgemm):
@@ -809,6 +826,10 @@ class _ScaledFc(torch.autograd.Function):
         if x.is_cuda:
             N, K = x.shape
             O = W.shape[1]
+            acc = _mm16(x.half(), W.half())
+            if acc is not None:  # library fp16 GEMM (fp32 accumulate) + the fp16 epilogue
+                _native.hip().h16_epi(acc, b.reshape(-1).contiguous(), in_scale, bias_scale, 1.0 / in_scale)
+                return acc
             y = x.new_empty(N, O)
             _native.hip().hgemm(x, W, y, b.reshape(-1), N, O, K, [K, 1], [O, 1], O, 1.0, 1.0, in_scale, bias_scale,
                                 1.0 / in_scale, 1)
@@ -822,6 +843,17 @@ class _ScaledFc(torch.autograd.Function):
         dy = dy.float().contiguous()
         N, K = x.shape
         O = W.shape[1]
+        if x.is_cuda and _MM16[0] is not False:
+            h = _native.hip()
+            d16 = (dy * (gs / in_scale)).half()
+            dxa = _mm16(d16, W.half().t())
+            dWa = _mm16(x.half().t(), d16) if dxa is not None else None
+            if dWa is not None:
+                h.h16_epi(dxa, None, in_scale, 1.0, 1.0 / gs)
+                h.h16_epi(dWa, None, in_scale, 1.0, 1.0 / gs)
+                db = W.new_empty(O)
+                h.colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
+                return dxa, dWa, db.reshape(ctx.bshape), None, None, None
         if x.is_cuda:
             h = _native.hip()
             dx = x.new_empty(N, K)
