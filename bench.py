@@ -292,6 +292,7 @@ def main():
         capture the step, run W warmup + K timed steps; returns the timings."""
         hidden = tuple(int(x) for x in args.hidden.split(","))
         dcn = model_name == "dcn_v2"
+        engine.clear_prefetch()  # nothing a previous measurement prepared steers this one's capture
         if dcn and mlp_dtype == "fp32":
             raise SystemExit("DCN-V2 (BASELINE config 5) is a bf16-MLP config: run it with --mlp-dtype bf16")
         auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)

@@ -448,7 +448,7 @@ __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, con
                                                 float* __restrict__ out) {
   constexpr int KC = 64;
   __shared__ float As[KC][kRaT + 4];  // [k][instance]
-  __shared__ float Ws[KC][68];        // [k][p]
+  __shared__ __attribute__((aligned(16))) float Ws[KC][68];  // [k][p]
   __shared__ int sperm[kRaT];
   int q, start, n;
   if (!ra_tile<R>(meta, blockIdx.x, &q, &start, &n)) return;
@@ -469,11 +469,43 @@ __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, con
   const int ii = t & 31, ka = (t >> 5) * 8;
   int pf[R], px[R];
   ra_peers<R>(ro, ld, sperm[ii], B, pf, px);
-  // W staging: column p = t & 63, k rows (t >> 6) + 4 j
+  // W staging: column p = t & 63, k rows (t >> 6) + 4 j (scalar), or
+  // columns 4 (t & 15) .. +3, k rows (t >> 4) + 16 j (float4)
   const int wp = t & 63, wr = t >> 6;
+  const int wq = (t & 15) * 4, wr4 = t >> 4;
+  // C % 8 == 0: a thread's 8 consecutive k rows lie in one peer block (one
+  // faster rank f) and one aligned 32-byte run of each matching peer's x
+  // row -- two float4 loads per matching peer instead of R predicated
+  // scalar loads per row.  P % 4 == 0: W rows by float4.
+  const bool vec = (C % 8) == 0 && (P % 4) == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W)) & 15) == 0;
   float ra[8], rw[16];
   auto load = [&](int kc) {
-    int kg = kc + ka, f = kg / C, c = kg - f * C;
+    int kg = kc + ka;
+    if (vec) {
+      float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+      if (kg < KT) {
+        const int f = kg / C, c = kg - f * C;
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+          if (pf[k] == f) {
+            const float4* xp = reinterpret_cast<const float4*>(x + (int64_t)px[k] * C + c);
+            const float4 v0 = xp[0], v1 = xp[1];
+            a0.x += v0.x; a0.y += v0.y; a0.z += v0.z; a0.w += v0.w;
+            a1.x += v1.x; a1.y += v1.y; a1.z += v1.z; a1.w += v1.w;
+          }
+      }
+      ra[0] = a0.x; ra[1] = a0.y; ra[2] = a0.z; ra[3] = a0.w;
+      ra[4] = a1.x; ra[5] = a1.y; ra[6] = a1.z; ra[7] = a1.w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = kc + wr4 + 16 * j;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < KT && p0 + wq < P) v = *reinterpret_cast<const float4*>(Wq + (int64_t)r * P + p0 + wq);
+        rw[4 * j] = v.x; rw[4 * j + 1] = v.y; rw[4 * j + 2] = v.z; rw[4 * j + 3] = v.w;
+      }
+      return;
+    }
+    int f = kg / C, c = kg - f * C;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float a = 0.f;
@@ -499,8 +531,15 @@ __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, con
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 8; ++j) As[ka + j][ii] = ra[j];
+    if (vec) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) Ws[wr + 4 * j][wp] = rw[j];
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<float4*>(&Ws[wr4 + 16 * j][wq]) =
+            make_float4(rw[4 * j], rw[4 * j + 1], rw[4 * j + 2], rw[4 * j + 3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) Ws[wr + 4 * j][wp] = rw[j];
+    }
     __syncthreads();
     if (kc + KC < KT) load(kc + KC);
 #pragma unroll
