@@ -154,6 +154,10 @@ class _CtrTowerFn(torch.autograd.Function):
             # fills the CUs and starves the head's workgroups (fp32 tower:
             # head_bwd 13 -> 95 us beside k_t32_dw, profiles/r3_s2_dw_after_head.txt)
             _launch_dw(t, ws, args, dense_tail, x.device, deferred_dw)
+        if t.on_head_done is not None:  # e.g. the next batch's key dedup beside the sparse push
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(x.device))
+            t.on_head_done(ev)
         d_extra = (ctx.dz * gl if gl is not None else ctx.dz.clone()) if ctx.has_extra else None
         return (dx, d_extra, None, None) + (None,) * (len(t._params))
 
@@ -198,6 +202,7 @@ class CtrTower:
         # enqueued (the tower's big MFMA kernels are then behind it): work that
         # should overlap the dW / head backward / sparse push forks from it
         self.on_dx_done = None
+        self.on_head_done = None
         # run the dW GEMM on a side stream, overlapped with the head backward
         # and the sparse push (PBX_TOWER_OVERLAP_DW=0 turns it off)
         self.overlap_dw = os.environ.get("PBX_TOWER_OVERLAP_DW", "1") != "0"

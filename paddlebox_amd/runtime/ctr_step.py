@@ -127,16 +127,21 @@ class CtrTrainStep:
         self.next_batch = None
         self.next_slot = 0
         self._dedup_ev = None
-        # the next batch's key dedup runs on its own side stream, forked once
-        # this step's dX chain is enqueued (beside the head backward, the dW
-        # GEMM and the sparse push); its pooling follows the push on this
-        # stream.  Off by default (PBX_SPLIT_PREFETCH=1 turns it on): the
-        # dedup grabs the CUs ahead of the head backward and delays the dW
-        # start (0.413 vs 0.398 ms/step, profiles/r4_pipeline_ab.txt)
-        self.split_prefetch = (os.environ.get("PBX_SPLIT_PREFETCH", "0") == "1" and tower is not None
-                               and hasattr(model, "prefetch_pool"))
+        # the next batch's key dedup on its own side stream (PBX_SPLIT_PREFETCH):
+        #   1: forked once this step's dX chain is enqueued -- it grabs the CUs
+        #      ahead of the head backward and delays the dW start (0.413 vs
+        #      0.398 ms/step, profiles/r4_pipeline_ab.txt);
+        #   2: forked after the head backward, so it runs beside the sparse
+        #      push and the dW GEMM (both wait on nothing it produces);
+        # its pooling follows the push on this stream.  0 (default): the dedup
+        # runs after the push on this stream.
+        mode = os.environ.get("PBX_SPLIT_PREFETCH", "0")
+        self.split_prefetch = mode in ("1", "2") and tower is not None and hasattr(model, "prefetch_pool")
         if self.split_prefetch:
-            tower.on_dx_done = self._dedup_next
+            if mode == "1":
+                tower.on_dx_done = self._dedup_next
+            else:
+                tower.on_head_done = self._dedup_next
 
     def set_next(self, batch, slot: int = 0):
         """Batch to prefetch (pool) at the end of each train_step (None: off)."""

@@ -68,9 +68,13 @@ def _train(pipeline: bool, precision: str, K: int = 1):
     return step.arena.flat.cpu(), losses, hk[o].cpu(), v[o].cpu()
 
 
-@pytest.mark.parametrize("precision,K", [("fp32", 1), ("bf16", 1), ("fp32", 2)])
-def test_pipelined_front_matches_plain_graphed_step(precision, K):
+@pytest.mark.parametrize("precision,K,split", [("fp32", 1, "0"), ("bf16", 1, "0"), ("fp32", 2, "0"), ("fp32", 1, "2"),
+                                               ("fp32", 2, "1")])
+def test_pipelined_front_matches_plain_graphed_step(precision, K, split, monkeypatch):
+    # split: the next batch's key dedup on its own stream (PBX_SPLIT_PREFETCH,
+    # forked at the dX chain (1) or after the head backward (2))
     f0, l0, k0, v0 = _train(False, precision, K)
+    monkeypatch.setenv("PBX_SPLIT_PREFETCH", split)
     f1, l1, k1, v1 = _train(True, precision, K)
     # the dW split-K atomics sum in any order: fp32-rounding-level differences
     rt, at = (1e-6, 1e-7) if precision == "fp32" else (1e-4, 1e-5)
