@@ -139,13 +139,21 @@ __global__ __launch_bounds__(256) void k_table_rank(TableDev t, const uint64_t* 
   int64_t row[kTdItems];
   int pos[kTdItems], lr[kTdItems];
   int nv = 0;
+  if (PROBE) {
+    // every item's bucket lines in flight together (table_probe_thread_n)
+    uint64_t q[kTdItems];
+#pragma unroll
+    for (int it = 0; it < kTdItems; ++it) {
+      const int64_t i = i0 + it * blockDim.x + threadIdx.x;
+      const uint64_t k = i < n ? keys[i] : kEmptyKey;
+      q[it] = k == kEmptyKey ? kEmptyKey : mix64(k);
+    }
+    table_probe_thread_n<kTdItems>(t, q, row);
+  }
 #pragma unroll
   for (int it = 0; it < kTdItems; ++it) {
-    const int64_t i = i0 + it * blockDim.x + threadIdx.x;
-    if (PROBE) {
-      const uint64_t k = i < n ? keys[i] : kEmptyKey;
-      row[it] = probe_thread(t, k == kEmptyKey ? kEmptyKey : mix64(k));
-    } else {
+    if (!PROBE) {
+      const int64_t i = i0 + it * blockDim.x + threadIdx.x;
       row[it] = i < n ? rows_occ[i] : -1;
     }
     nv += row[it] >= 0;  // n_valid = occurrences placed in perm (absent keys are skipped like padding)
