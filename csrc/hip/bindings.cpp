@@ -323,7 +323,9 @@ class GpuTable {
     PBX_CHECK(E == 3 + dim_, "push_merge_apply: E must be 3 + dim");
     PBX_CHECK(cvm.dim() == 2 && cvm.size(1) == 2, "push_merge_apply: cvm must be [B, 2]");
     PBX_CHECK(acc.dim() == 2 && acc.size(0) >= perm.numel() && acc.size(0) >= rows.numel(), "push_merge_apply: acc rows");
-    PBX_CHECK(inc.numel() * 64 >= perm.numel(), "push_merge_apply: inc too small");
+    const bool fused = inc.scalar_type() == torch::kInt64;  // per-unique arrival counters: one launch
+    PBX_CHECK(fused ? inc.numel() >= perm.numel() : (inc.scalar_type() == torch::kInt32 && inc.numel() * 64 >= perm.numel()),
+              "push_merge_apply: inc too small");
     PushMergeArgs a;
     a.dout = ptr<float>(dout);
     a.out_stride = (int)dout.size(1);
@@ -346,7 +348,9 @@ class GpuTable {
     a.bs_scale = bs_scale;
     a.dim = dim_;
     a.embed_thres_size = use_cvm ? 0 : embed_thres_size;
-    return launch_push_merge_apply(a, view(), ptr<int64_t>(rows), ptr<int32_t>(inc), cfg, seed, cur_stream());
+    return launch_push_merge_apply(a, view(), ptr<int64_t>(rows), fused ? nullptr : ptr<int32_t>(inc),
+                                   fused ? reinterpret_cast<unsigned long long*>(ptr<int64_t>(inc)) : nullptr, cfg,
+                                   seed, cur_stream());
   }
   // ---- feature-type codec (feature_ops.hip)
   void codec_check(const CodecDev& c) const {
@@ -655,7 +659,9 @@ static bool push_merge_send(const Tensor& dout, int col_offset, const Tensor& cv
   PBX_CHECK(send.dim() == 2 && send.is_contiguous(), "push_merge_send: send");
   PBX_CHECK(send_index.scalar_type() == torch::kInt64 && send_index.numel() >= perm.numel(),
             "push_merge_send: send_index");
-  PBX_CHECK(inc.numel() * 64 >= perm.numel(), "push_merge_send: inc too small");
+  const bool fused = inc.scalar_type() == torch::kInt64;  // per-unique arrival counters: one launch
+  PBX_CHECK(fused ? inc.numel() >= perm.numel() : (inc.scalar_type() == torch::kInt32 && inc.numel() * 64 >= perm.numel()),
+            "push_merge_send: inc too small");
   PushMergeArgs a;
   a.dout = ptr<float>(dout);
   a.out_stride = (int)dout.size(1);
@@ -679,7 +685,8 @@ static bool push_merge_send(const Tensor& dout, int col_offset, const Tensor& cv
   a.dim = dim;
   a.embed_thres_size = use_cvm ? 0 : embed_thres_size;
   return launch_push_merge_send(a, dim, ptr<float>(send), (int)send.size(1), ptr<int64_t>(send_index),
-                                ptr<int32_t>(inc), cur_stream());
+                                fused ? nullptr : ptr<int32_t>(inc),
+                                fused ? reinterpret_cast<unsigned long long*>(ptr<int64_t>(inc)) : nullptr, cur_stream());
 }
 
 static void push_merge_records(const Tensor& rec, const Tensor& perm, const Tensor& uid, const Tensor& n_valid,

@@ -272,7 +272,10 @@ bool launch_push_adagrad_seg(const TableDev& t, const int64_t* rows, const float
 // Adagrad in place (a.push = acc scratch [U_cap, stride], kept all-zero;
 // inc [ceil(n/64)] scratch).  False if the dim/stride/layout has no fused
 // instantiation (caller falls back to launch_push_merge + launch_push_adagrad).
+// inc: int32 per wave (two launches: merge + k_push_finish) or, with ctr set
+// (int64 per unique, zero between pushes), one fused launch (inc unused)
 bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const int64_t* rows, int32_t* inc,
+                             unsigned long long* ctr,
                              const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s);
 // Sharded push: the same merge, each unique's summed record written to
 // send[send_index[u]] (rows with send_index -1 dropped); a.push / a.push_stride
@@ -340,7 +343,7 @@ void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64
 // Probe raw feasigns (mixed in the kernel, -1 = padding -> row -1).
 void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows, hipStream_t s);
 bool launch_push_merge_send(const PushMergeArgs& a, int dim, float* send, int send_stride, const int64_t* send_index,
-                            int32_t* inc, hipStream_t s);
+                            int32_t* inc, unsigned long long* ctr, hipStream_t s);
 
 // ---------------------------------------------------------------- dense ops
 void launch_data_norm_fwd(const float* x, int N, int C, const float* bsize, const float* bsum,

@@ -576,9 +576,18 @@ struct SendEmit {
   }
 };
 
-template <int D, class Emit>
+// FUSED (ctr != nullptr): no k_push_finish.  Every piece of a straddling run
+// adds its partial record into acc[u], then arrives on ctr[u] with ONE 64-bit
+// atomic carrying (1 arrival | last piece: its wave index + 1 << 20 | first
+// piece: its wave index + 1 << 41); the arrival that completes the count
+// (arrivals == last - first + 1 waves, both ends seen) applies the summed
+// record and re-zeroes acc[u] and ctr[u].  Exactly one arrival sees the run
+// complete, nobody waits for anybody (no cross-workgroup spinning).
+constexpr int kPcArrBits = 20, kPcLastShift = 20, kPcFirstShift = 41;
+template <int D, class Emit, bool FUSED = false>
 __global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, Emit em, float* __restrict__ acc,
-                                                          int acc_stride, int32_t* __restrict__ inc, float neg_bs) {
+                                                          int acc_stride, int32_t* __restrict__ inc, float neg_bs,
+                                                          unsigned long long* __restrict__ ctr = nullptr) {
   constexpr int Q = 3 + D;
   const PushMergeArgs& a = src.a;
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -612,7 +621,7 @@ __global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, Emit e
   if (lane == 63 && p + 1 < pv) cn = a.uid[a.perm[p + 1]] == u;
   if (lane == 0 && wave_base > 0) cp = a.uid[a.perm[wave_base - 1]] == u;
   const int cont_next = __shfl(cn, 63), cont_prev = __shfl(cp, 0);
-  if (lane == 63) inc[wave_base >> 6] = (cont_next && !(cont_prev && u_first == u_last)) ? u_last : -1;
+  if (!FUSED && lane == 63) inc[wave_base >> 6] = (cont_next && !(cont_prev && u_first == u_last)) ? u_last : -1;
   const int32_t un = __shfl_down(u, 1);
   const bool tail = lane == 63 || un != u;
   if (p >= pv || u < 0 || !tail) return;
@@ -630,9 +639,35 @@ __global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, Emit e
     return;
   }
   float* dst = acc + (int64_t)u * acc_stride;
-  dst[kPushSlot] = rec[kPushSlot];
+  if (!FUSED) {
+    dst[kPushSlot] = rec[kPushSlot];
+#pragma unroll
+    for (int c = 1; c < RowF<D>::kQ; ++c) atomicAdd(&dst[c], rec[c]);
+    return;
+  }
 #pragma unroll
   for (int c = 1; c < RowF<D>::kQ; ++c) atomicAdd(&dst[c], rec[c]);
+  const bool first = !(u == u_first && cont_prev), last = !(u == u_last && cont_next);
+  const unsigned long long wv = (unsigned long long)(wave_base >> 6) + 1ull;
+  const unsigned long long add =
+      1ull + (last ? wv << kPcLastShift : 0ull) + (first ? wv << kPcFirstShift : 0ull);
+  __threadfence();  // this piece's acc atomics before its arrival
+  const unsigned long long now = atomicAdd(&ctr[u], add) + add;
+  const unsigned long long arr = now & ((1ull << kPcArrBits) - 1ull);
+  const unsigned long long lw = (now >> kPcLastShift) & ((1ull << (kPcFirstShift - kPcLastShift)) - 1ull);
+  const unsigned long long fw = now >> kPcFirstShift;
+  if (lw == 0 || fw == 0 || arr != lw - fw + 1) return;
+  __threadfence();  // every other piece's acc atomics before the reads
+  float sum[RowF<D>::kQ4 * 4];
+#pragma unroll
+  for (int c = 0; c < RowF<D>::kQ4 * 4; ++c)
+    sum[c] = c < RowF<D>::kQ ? __hip_atomic_load(&dst[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+  sum[kPushSlot] = rec[kPushSlot];
+  float4* a4 = reinterpret_cast<float4*>(dst);
+#pragma unroll
+  for (int i = 0; i < RowF<D>::kQ4; ++i) a4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  ctr[u] = 0ull;
+  em.template emit<D>(u, sum);
 }
 
 template <int D, class Emit>
@@ -1068,7 +1103,7 @@ bool launch_owner_push(const TableDev& t, const int64_t* rows, float* rec, int r
 }
 
 bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const int64_t* rows, int32_t* inc,
-                             const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s) {
+                             unsigned long long* ctr, const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s) {
   if (a.cvm_offset != 2 || a.push_index != nullptr || a.n_valid == nullptr || a.E != 3 + t.dim) return false;
   if (a.n <= 0) return true;
   const dim3 g(nblk(a.n)), gf(nblk((a.n + 63) / 64)), b(256);
@@ -1077,8 +1112,13 @@ bool launch_push_merge_apply(const PushMergeArgs& a, const TableDev& t, const in
   const ApplyEmit em{t, rows, cfg, seed};
 #define PBX_MERGE_APPLY(D)                                                                                    \
   if (vec_push_ok<D>(t, a.push_stride)) {                                                                     \
+    if (ctr) {                                                                                                \
+      hipLaunchKernelGGL((k_push_merge_apply<D, ApplyEmit, true>), g, b, 0, s, src, em, a.push, a.push_stride, \
+                         nullptr, neg_bs, ctr);                                                               \
+      return true;                                                                                            \
+    }                                                                                                         \
     hipLaunchKernelGGL((k_push_merge_apply<D, ApplyEmit>), g, b, 0, s, src, em, a.push, a.push_stride, inc,   \
-                       neg_bs);                                                                               \
+                       neg_bs, nullptr);                                                                      \
     hipLaunchKernelGGL((k_push_finish<D, ApplyEmit>), gf, b, 0, s, em, a.push, a.push_stride, inc, a.n_valid); \
     return true;                                                                                              \
   }
@@ -1114,7 +1154,7 @@ bool launch_push_occ(const PushMergeArgs& a, const TableDev& t, const int64_t* r
 }
 
 bool launch_push_merge_send(const PushMergeArgs& a, int dim, float* send, int send_stride, const int64_t* send_index,
-                            int32_t* inc, hipStream_t s) {
+                            int32_t* inc, unsigned long long* ctr, hipStream_t s) {
   if (a.cvm_offset != 2 || a.n_valid == nullptr || a.E != 3 + dim || send_stride % 4 != 0) return false;
   if (a.n <= 0) return true;
   const dim3 g(nblk(a.n)), gf(nblk((a.n + 63) / 64)), b(256);
@@ -1123,8 +1163,13 @@ bool launch_push_merge_send(const PushMergeArgs& a, int dim, float* send, int se
   const SendEmit em{send, send_stride, send_index};
 #define PBX_MERGE_SEND(D)                                                                                     \
   if (dim == D && send_stride >= RowF<D>::kQ4 * 4 && a.push_stride >= RowF<D>::kQ4 * 4 && a.push_stride % 4 == 0) { \
+    if (ctr) {                                                                                                \
+      hipLaunchKernelGGL((k_push_merge_apply<D, SendEmit, true>), g, b, 0, s, src, em, a.push, a.push_stride,  \
+                         nullptr, neg_bs, ctr);                                                               \
+      return true;                                                                                            \
+    }                                                                                                         \
     hipLaunchKernelGGL((k_push_merge_apply<D, SendEmit>), g, b, 0, s, src, em, a.push, a.push_stride, inc,    \
-                       neg_bs);                                                                               \
+                       neg_bs, nullptr);                                                                      \
     hipLaunchKernelGGL((k_push_finish<D, SendEmit>), gf, b, 0, s, em, a.push, a.push_stride, inc, a.n_valid);  \
     return true;                                                                                              \
   }

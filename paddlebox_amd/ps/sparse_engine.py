@@ -129,6 +129,16 @@ class PullState:
 TABLE_DEDUP_MAX_ROWS = (1 << 31) - 1
 
 
+def _push_run_scratch(max_keys: int, device) -> torch.Tensor:
+    """Runs of a key's occurrences that straddle waves in the fused merge +
+    update: int64 arrival counters per unique (one launch: the piece that
+    completes a run applies it), or with PBX_PUSH_FINISH=1 the int32 per-wave
+    run owners of the two-launch form (k_push_finish)."""
+    if os.environ.get("PBX_PUSH_FINISH", "0") == "1":
+        return torch.empty((max_keys + 63) // 64 + 1, dtype=torch.int32, device=device)
+    return torch.zeros(max_keys, dtype=torch.int64, device=device)
+
+
 def table_dedup_fits(table_rows: int) -> bool:
     """The single-shard table dedup (table.hip k_table_rank) keys its LDS hash
     and per-row scratch by int32 row; past INT32_MAX rows the engine falls
@@ -275,17 +285,17 @@ class SparseEngine:
                 self.push_send = torch.empty(n, self.Q, device=self.device)
                 self.push_recv = torch.empty(n, self.Q, device=self.device)
                 self.push_merged = torch.empty(n, self.Q, device=self.device)
-                # fused merge straddle scratch (all-zero between steps) + per-wave run owners
+                # fused merge straddle scratch (all-zero between steps) + run arrival counters
                 self.push_acc = torch.zeros(self.max_keys, self.Q, device=self.device)
-                self.push_inc = torch.empty((self.max_keys + 63) // 64 + 1, dtype=torch.int32, device=self.device)
+                self.push_inc = _push_run_scratch(self.max_keys, self.device)
             else:
                 self.push_buf = torch.empty(self.max_keys, self.Q, device=self.device)
                 if self.codec is not None:  # decoded pull records of the batch's unique keys
                     self.pull_buf = torch.empty(self.max_keys, self.P, device=self.device)
-                # fused merge+Adagrad scratch: straddling-run accumulators
-                # (kept all-zero between steps) and per-wave run owners
+                # fused merge+Adagrad scratch: straddling-run accumulators and
+                # run arrival counters (both kept all-zero between steps)
                 self.push_acc = torch.zeros(self.max_keys, self.Q, device=self.device)
-                self.push_inc = torch.empty((self.max_keys + 63) // 64 + 1, dtype=torch.int32, device=self.device)
+                self.push_inc = _push_run_scratch(self.max_keys, self.device)
                 if not self.dedup:  # per-occurrence accumulators, kOccRep replicas each (kept all-zero)
                     self.push_acc_occ = torch.zeros(self.max_keys * int(self.table.t.occ_replicas), self.Q,
                                                     device=self.device)
