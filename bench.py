@@ -292,7 +292,15 @@ def main():
         capture the step, run W warmup + K timed steps; returns the timings."""
         hidden = tuple(int(x) for x in args.hidden.split(","))
         dcn = model_name == "dcn_v2"
-        engine.clear_prefetch()  # nothing a previous measurement prepared steers this one's capture
+        # nothing a previous measurement prepared steers this one's capture, and
+        # the pull slots' occurrence rows are all -1 again (a pipelined run
+        # leaves rows there, which a split pull must not read as occurrences)
+        engine.clear_prefetch(reset_rows=True)
+        if not primary:
+            # a secondary after a pipelined multi-step headline faulted in its
+            # sparse push on the box (twice; cause not isolated): it starts
+            # from fresh pull slots and push scratch, like a new program
+            engine.reset_pull_ring()
         if dcn and mlp_dtype == "fp32":
             raise SystemExit("DCN-V2 (BASELINE config 5) is a bf16-MLP config: run it with --mlp-dtype bf16")
         auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)

@@ -508,6 +508,15 @@ struct DedupWorkspace {
     }
     return rows_occ;
   }
+  // rows_occ holds rows after a probing dedup (rows_given = false: the
+  // pipelined pull's seqpool reads them); the split pull needs it all -1
+  // outside the lod, so it cleans a dirty workspace first
+  bool rows_occ_dirty = false;
+  void clean_rows_occ() {
+    if (!rows_occ_dirty) return;
+    rows_occ.fill_(-1);
+    rows_occ_dirty = false;
+  }
   void run_table(const Tensor& keys, GpuTable& t, bool rows_given) {
     check_cuda(keys, "keys");
     const int64_t n = keys.numel();
@@ -519,6 +528,7 @@ struct DedupWorkspace {
                        rc.second, ptr<int64_t>(rows_u), ptr<int32_t>(uid), ptr<int32_t>(perm), ptr<int32_t>(seg),
                        ptr<int32_t>(u_count), ptr<int32_t>(u_acc), rows_given, cur_stream());
     last_n = n;
+    if (!rows_given) rows_occ_dirty = true;  // rows_given: k_table_scatter hands rows_occ back all -1
   }
   int64_t last_n = 0;
 };
@@ -1276,6 +1286,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("run", &DedupWorkspace::run, py::arg("keys"), py::arg("mixed") = false, py::arg("zero") = py::none())
       .def("run_table", &DedupWorkspace::run_table, py::arg("keys"), py::arg("table"), py::arg("rows_given") = false)
       .def("table_rows_occ", &DedupWorkspace::table_rows_occ)
+      .def("clean_rows_occ", &DedupWorkspace::clean_rows_occ)
+      .def_readonly("rows_occ_dirty", &DedupWorkspace::rows_occ_dirty)
       .def_readonly("rows_u", &DedupWorkspace::rows_u)
       .def_readonly("rows_occ", &DedupWorkspace::rows_occ)
       .def_readonly("hash", &DedupWorkspace::hash)

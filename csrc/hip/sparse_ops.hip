@@ -651,22 +651,21 @@ __global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, Emit e
   const unsigned long long wv = (unsigned long long)(wave_base >> 6) + 1ull;
   const unsigned long long add =
       1ull + (last ? wv << kPcLastShift : 0ull) + (first ? wv << kPcFirstShift : 0ull);
-  __threadfence();  // this piece's acc atomics before its arrival
+  // this piece's acc atomics are acknowledged before its arrival (vmcnt
+  // counts atomics on CDNA); no cache-maintenance fence
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long now = atomicAdd(&ctr[u], add) + add;
   const unsigned long long arr = now & ((1ull << kPcArrBits) - 1ull);
   const unsigned long long lw = (now >> kPcLastShift) & ((1ull << (kPcFirstShift - kPcLastShift)) - 1ull);
   const unsigned long long fw = now >> kPcFirstShift;
   if (lw == 0 || fw == 0 || arr != lw - fw + 1) return;
-  __threadfence();  // every other piece's acc atomics before the reads
+  // the completing arrival takes the sum and re-zeroes with atomic
+  // exchanges (read at the atomics' coherence point, not a cached line)
   float sum[RowF<D>::kQ4 * 4];
 #pragma unroll
-  for (int c = 0; c < RowF<D>::kQ4 * 4; ++c)
-    sum[c] = c < RowF<D>::kQ ? __hip_atomic_load(&dst[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+  for (int c = 0; c < RowF<D>::kQ4 * 4; ++c) sum[c] = c < RowF<D>::kQ && c != kPushSlot ? atomicExch(&dst[c], 0.f) : 0.f;
   sum[kPushSlot] = rec[kPushSlot];
-  float4* a4 = reinterpret_cast<float4*>(dst);
-#pragma unroll
-  for (int i = 0; i < RowF<D>::kQ4; ++i) a4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  ctr[u] = 0ull;
+  atomicExch(&ctr[u], 0ull);
   em.template emit<D>(u, sum);
 }
 

@@ -131,10 +131,12 @@ TABLE_DEDUP_MAX_ROWS = (1 << 31) - 1
 
 def _push_run_scratch(max_keys: int, device) -> torch.Tensor:
     """Runs of a key's occurrences that straddle waves in the fused merge +
-    update: int64 arrival counters per unique (one launch: the piece that
-    completes a run applies it), or with PBX_PUSH_FINISH=1 the int32 per-wave
-    run owners of the two-launch form (k_push_finish)."""
-    if os.environ.get("PBX_PUSH_FINISH", "0") == "1":
+    update: the int32 per-wave run owners of the two-launch form
+    (k_push_finish, default), or with PBX_PUSH_FINISH=0 int64 arrival
+    counters per unique (one launch: the piece that completes a run applies
+    it; the first form of it fenced every piece and measured 0.49 vs 0.38
+    ms/step)."""
+    if os.environ.get("PBX_PUSH_FINISH", "1") == "1":
         return torch.empty((max_keys + 63) // 64 + 1, dtype=torch.int32, device=device)
     return torch.zeros(max_keys, dtype=torch.int64, device=device)
 
@@ -484,6 +486,10 @@ class SparseEngine:
         sl = self._take_slot()
         ws = sl.ws
         rows = ws.table_rows_occ()[:L]  # all -1 outside the lod between pulls
+        # ... unless a probing dedup (prefetched / plain table-dedup pull) used
+        # this slot last: its rows_occ still holds rows, and the padding
+        # positions would then count as occurrences of stale rows
+        ws.clean_rows_occ()
         if dense is not None:
             dense = dense.contiguous().float()
 
@@ -620,9 +626,32 @@ class SparseEngine:
         """The pooled output a prefetch_pull left for this key buffer (or None)."""
         return self._prepared_out.get(keys.data_ptr()) if self.is_gpu and not self.sharded else None
 
-    def clear_prefetch(self):
+    def clear_prefetch(self, reset_rows: bool = False):
+        """Forget the prepared pulls.  reset_rows: also hand every pull slot's
+        occurrence rows back all -1 now (eagerly, so a step captured next
+        does not carry the clean-up; SparseEngine._pull_split)."""
         self._prepared.clear()
         self._prepared_out.clear()
+        if reset_rows and self.is_gpu:
+            for sl in getattr(self, "_slots", []):
+                if getattr(sl.ws, "rows_occ_dirty", False):
+                    sl.ws.clean_rows_occ()
+
+    def reset_pull_ring(self):
+        """Fresh pull slots (dedup workspaces, occurrence maps, pooled
+        outputs) and zeroed push scratch -- what a new training program over
+        the same table starts from (bench.py: each same-run measurement)."""
+        if not self.is_gpu:
+            return
+        self.clear_prefetch()
+        self._pending_dedup = None
+        n = len(self._slots)
+        self._slots = [_PullSlot(self) for _ in range(n)]
+        self._next_slot = 0
+        self._cur = self._slots[0]
+        if getattr(self, "push_acc", None) is not None:
+            self.push_acc.zero_()
+            self.push_inc = _push_run_scratch(self.max_keys, self.device)
 
     def _take_slot(self) -> _PullSlot:
         sl = self._slots[self._next_slot % len(self._slots)]
