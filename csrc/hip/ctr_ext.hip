@@ -350,13 +350,32 @@ __global__ __launch_bounds__(kRaBucketThreads) void k_ra_bucket(const int* __res
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int chunk = (B + kRaBucketThreads - 1) / kRaBucketThreads;
   const int i0 = min(B, t * chunk), i1 = min(B, i0 + chunk);
+  // up to kPre ranks per thread are loaded once, all in flight together, and
+  // kept for the scatter pass (a serial load per instance and pass made this
+  // one-workgroup kernel latency bound: ~11 us at B = 5k)
+  constexpr int kPre = 8;
+  const bool pre = chunk <= kPre;
+  int bk[kPre];
+#pragma unroll
+  for (int j = 0; j < kPre; ++j) bk[j] = (pre && i0 + j < i1) ? ro[(int64_t)(i0 + j) * ld] : 0;
+#pragma unroll
+  for (int j = 0; j < kPre; ++j) bk[j] = ra_bucket_of(bk[j], R);
   int cnt[Q];
 #pragma unroll
   for (int q = 0; q < Q; ++q) cnt[q] = 0;
-  for (int i = i0; i < i1; ++i) {
-    const int b = ra_bucket_of(ro[(int64_t)i * ld], R);
+  if (pre) {
 #pragma unroll
-    for (int q = 0; q < Q; ++q) cnt[q] += b == q;
+    for (int j = 0; j < kPre; ++j)
+      if (i0 + j < i1) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) cnt[q] += bk[j] == q;
+      }
+  } else {
+    for (int i = i0; i < i1; ++i) {
+      const int b = ra_bucket_of(ro[(int64_t)i * ld], R);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) cnt[q] += b == q;
+    }
   }
   int off[Q];
 #pragma unroll
@@ -387,13 +406,25 @@ __global__ __launch_bounds__(kRaBucketThreads) void k_ra_bucket(const int* __res
     off[q] += wsum[w][q] + base;
     base += tot[q];
   }
-  for (int i = i0; i < i1; ++i) {
-    const int b = ra_bucket_of(ro[(int64_t)i * ld], R);
-    int pos = 0;
+  if (pre) {
 #pragma unroll
-    for (int q = 0; q < Q; ++q)
-      if (b == q) pos = off[q]++;
-    perm[pos] = i;
+    for (int j = 0; j < kPre; ++j) {
+      if (i0 + j >= i1) continue;
+      int pos = 0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (bk[j] == q) pos = off[q]++;
+      perm[pos] = i0 + j;
+    }
+  } else {
+    for (int i = i0; i < i1; ++i) {
+      const int b = ra_bucket_of(ro[(int64_t)i * ld], R);
+      int pos = 0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (b == q) pos = off[q]++;
+      perm[pos] = i;
+    }
   }
   if (t == 0) {
     int bs = 0, tp = 0;
@@ -439,14 +470,16 @@ __device__ __forceinline__ void ra_peers(const int* __restrict__ ro, int ld, int
 }
 
 // out rows of one tile (32 instances of rank q) x 64 outputs; K = R*C in
-// chunks of 64, the next chunk's gathered A and W_q rows held in registers
-// while the current one runs on MFMA.
-template <int R>
+// chunks of KC, the next chunk's gathered A and W_q rows held in registers
+// while the current one runs on MFMA.  KC = 128 when the gathers vectorise
+// (half the chunk round trips of KC = 64: the loop is load-latency bound).
+template <int R, int KC>
 __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, const int* __restrict__ ro, int ld,
                                                 const float* __restrict__ W, int B, int C, int P,
                                                 const int* __restrict__ perm, const int* __restrict__ meta,
                                                 float* __restrict__ out) {
-  constexpr int KC = 64;
+  constexpr int AK = KC / 8;   // A elements per thread: instance t & 31, k rows ka .. ka + AK - 1
+  constexpr int WN = KC / 4;   // W elements per thread
   __shared__ float As[KC][kRaT + 4];  // [k][instance]
   __shared__ __attribute__((aligned(16))) float Ws[KC][68];  // [k][p]
   __shared__ int sperm[kRaT];
@@ -465,39 +498,44 @@ __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, con
   }
   const int KT = R * C;
   const float* Wq = W + (int64_t)q * KT * P;
-  // A staging: instance ii = t & 31, k rows ka .. ka + 7
-  const int ii = t & 31, ka = (t >> 5) * 8;
+  const int ii = t & 31, ka = (t >> 5) * AK;
   int pf[R], px[R];
   ra_peers<R>(ro, ld, sperm[ii], B, pf, px);
   // W staging: column p = t & 63, k rows (t >> 6) + 4 j (scalar), or
   // columns 4 (t & 15) .. +3, k rows (t >> 4) + 16 j (float4)
   const int wp = t & 63, wr = t >> 6;
   const int wq = (t & 15) * 4, wr4 = t >> 4;
-  // C % 8 == 0: a thread's 8 consecutive k rows lie in one peer block (one
-  // faster rank f) and one aligned 32-byte run of each matching peer's x
-  // row -- two float4 loads per matching peer instead of R predicated
-  // scalar loads per row.  P % 4 == 0: W rows by float4.
-  const bool vec = (C % 8) == 0 && (P % 4) == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W)) & 15) == 0;
-  float ra[8], rw[16];
+  // C % AK == 0: a thread's AK consecutive k rows lie in one peer block (one
+  // faster rank f) and one aligned run of each matching peer's x row --
+  // AK / 4 float4 loads per matching peer instead of R predicated scalar
+  // loads per row.  P % 4 == 0: W rows by float4.
+  const bool vec = (C % AK) == 0 && (P % 4) == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W)) & 15) == 0;
+  float ra[AK], rw[WN];
   auto load = [&](int kc) {
     int kg = kc + ka;
     if (vec) {
-      float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+      float4 av[AK / 4];
+#pragma unroll
+      for (int v = 0; v < AK / 4; ++v) av[v] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (kg < KT) {
         const int f = kg / C, c = kg - f * C;
 #pragma unroll
         for (int k = 0; k < R; ++k)
           if (pf[k] == f) {
             const float4* xp = reinterpret_cast<const float4*>(x + (int64_t)px[k] * C + c);
-            const float4 v0 = xp[0], v1 = xp[1];
-            a0.x += v0.x; a0.y += v0.y; a0.z += v0.z; a0.w += v0.w;
-            a1.x += v1.x; a1.y += v1.y; a1.z += v1.z; a1.w += v1.w;
+#pragma unroll
+            for (int v = 0; v < AK / 4; ++v) {
+              const float4 xv = xp[v];
+              av[v].x += xv.x; av[v].y += xv.y; av[v].z += xv.z; av[v].w += xv.w;
+            }
           }
       }
-      ra[0] = a0.x; ra[1] = a0.y; ra[2] = a0.z; ra[3] = a0.w;
-      ra[4] = a1.x; ra[5] = a1.y; ra[6] = a1.z; ra[7] = a1.w;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int v = 0; v < AK / 4; ++v) {
+        ra[4 * v] = av[v].x; ra[4 * v + 1] = av[v].y; ra[4 * v + 2] = av[v].z; ra[4 * v + 3] = av[v].w;
+      }
+#pragma unroll
+      for (int j = 0; j < WN / 4; ++j) {
         const int r = kc + wr4 + 16 * j;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (r < KT && p0 + wq < P) v = *reinterpret_cast<const float4*>(Wq + (int64_t)r * P + p0 + wq);
@@ -507,7 +545,7 @@ __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, con
     }
     int f = kg / C, c = kg - f * C;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < AK; ++j) {
       float a = 0.f;
       if (kg < KT) {
 #pragma unroll
@@ -519,7 +557,7 @@ __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, con
       if (++c == C) { c = 0; ++f; }
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < WN; ++j) {
       const int r = kc + wr + 4 * j;
       rw[j] = (r < KT && p0 + wp < P) ? Wq[(int64_t)r * P + p0 + wp] : 0.f;
     }
@@ -530,15 +568,15 @@ __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, con
   for (int kc = 0; kc < KT; kc += KC) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 8; ++j) As[ka + j][ii] = ra[j];
+    for (int j = 0; j < AK; ++j) As[ka + j][ii] = ra[j];
     if (vec) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < WN / 4; ++j)
         *reinterpret_cast<float4*>(&Ws[wr4 + 16 * j][wq]) =
             make_float4(rw[4 * j], rw[4 * j + 1], rw[4 * j + 2], rw[4 * j + 3]);
     } else {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) Ws[wr + 4 * j][wp] = rw[j];
+      for (int j = 0; j < WN; ++j) Ws[wr + 4 * j][wp] = rw[j];
     }
     __syncthreads();
     if (kc + KC < KT) load(kc + KC);
@@ -1049,6 +1087,21 @@ void launch_i8_gemm(const signed char* qx, const signed char* qwt, int M, int N,
     default: hipLaunchKernelGGL(KER<8>, GRID, dim3(BLOCK), 0, s, __VA_ARGS__); break; \
   }
 
+template <int KC>
+static void ra_fwd_launch(int R, dim3 g, hipStream_t s, const float* x, const int* ro, int ld, const float* W, int B,
+                          int C, int P, const int* perm, const int* meta, float* out) {
+  switch (R) {
+    case 1: hipLaunchKernelGGL((k_ra_fwd<1, KC>), g, dim3(256), 0, s, x, ro, ld, W, B, C, P, perm, meta, out); break;
+    case 2: hipLaunchKernelGGL((k_ra_fwd<2, KC>), g, dim3(256), 0, s, x, ro, ld, W, B, C, P, perm, meta, out); break;
+    case 3: hipLaunchKernelGGL((k_ra_fwd<3, KC>), g, dim3(256), 0, s, x, ro, ld, W, B, C, P, perm, meta, out); break;
+    case 4: hipLaunchKernelGGL((k_ra_fwd<4, KC>), g, dim3(256), 0, s, x, ro, ld, W, B, C, P, perm, meta, out); break;
+    case 5: hipLaunchKernelGGL((k_ra_fwd<5, KC>), g, dim3(256), 0, s, x, ro, ld, W, B, C, P, perm, meta, out); break;
+    case 6: hipLaunchKernelGGL((k_ra_fwd<6, KC>), g, dim3(256), 0, s, x, ro, ld, W, B, C, P, perm, meta, out); break;
+    case 7: hipLaunchKernelGGL((k_ra_fwd<7, KC>), g, dim3(256), 0, s, x, ro, ld, W, B, C, P, perm, meta, out); break;
+    default: hipLaunchKernelGGL((k_ra_fwd<8, KC>), g, dim3(256), 0, s, x, ro, ld, W, B, C, P, perm, meta, out); break;
+  }
+}
+
 int rank_attention_bucket_ints(int B, int R) { return B + 3 * (R + 1) + 1; }
 
 // upper bound on the tiles of the bucketed order: every bucket may end in a partial tile
@@ -1060,7 +1113,12 @@ void launch_rank_attention_fwd(const float* x, const int* ro, int ld, const floa
   int* perm = bucket;
   int* meta = bucket + B;
   PBX_RA_DISPATCH(k_ra_bucket, dim3(1), kRaBucketThreads, ro, ld, B, perm, meta);
-  PBX_RA_DISPATCH(k_ra_fwd, dim3(ra_max_tiles(B, R), (P + 63) / 64), 256, x, ro, ld, W, B, C, P, perm, meta, out);
+  const dim3 gf(ra_max_tiles(B, R), (P + 63) / 64);
+  const bool wide = C % 16 == 0 && P % 4 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W)) & 15) == 0;
+  if (wide)
+    ra_fwd_launch<128>(R, gf, s, x, ro, ld, W, B, C, P, perm, meta, out);
+  else
+    ra_fwd_launch<64>(R, gf, s, x, ro, ld, W, B, C, P, perm, meta, out);
 }
 
 void launch_rank_attention_bwd(const float* x, const float* dout, const int* ro, int ld, const float* W, int B, int C,

@@ -808,6 +808,22 @@ def _mm16(a16, b16):
     return r.contiguous()
 
 
+def _half_of(W: torch.Tensor) -> torch.Tensor:
+    """fp16 copy of a weight, cached on the tensor until it is modified in
+    place (its version counter moves) -- one cast per optimizer step, not
+    per forward."""
+    key = (W._version, W.data_ptr(), tuple(W.shape))
+    c = getattr(W, "_pbx_half", None)
+    if c is not None and c[0] == key:
+        return c[1]
+    W16 = W.detach().half()
+    try:
+        W._pbx_half = (key, W16)
+    except (AttributeError, RuntimeError):
+        pass
+    return W16
+
+
 class _ScaledFc(torch.autograd.Function):
     """scaled_fc (operators/scaled_fc_op.cu:144-330) with the reference's
     fp16 arithmetic on fp16 MFMA (csrc/hip/ctr_ext.hip k_hgemm):
@@ -820,20 +836,25 @@ class _ScaledFc(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W, b, in_scale, bias_scale, grad_scale):
-        ctx.save_for_backward(x, W)
         ctx.bshape = b.shape
         ctx.sc = (in_scale, grad_scale)
+        ctx.half_ops = False
         if x.is_cuda:
             N, K = x.shape
             O = W.shape[1]
-            acc = _mm16(x.half(), W.half())
+            x16, W16 = x.half(), _half_of(W)
+            acc = _mm16(x16, W16)
             if acc is not None:  # library fp16 GEMM (fp32 accumulate) + the fp16 epilogue
-                _native.hip().h16_epi(acc, b.reshape(-1).contiguous(), in_scale, bias_scale, 1.0 / in_scale)
+                _native.hip().h16_epi(acc, b.reshape(-1), in_scale, bias_scale, 1.0 / in_scale)
+                ctx.save_for_backward(x16, W16)  # the backward's fp16 operands, cast once
+                ctx.half_ops = True
                 return acc
+            ctx.save_for_backward(x, W)
             y = x.new_empty(N, O)
             _native.hip().hgemm(x, W, y, b.reshape(-1), N, O, K, [K, 1], [O, 1], O, 1.0, 1.0, in_scale, bias_scale,
                                 1.0 / in_scale, 1)
             return y
+        ctx.save_for_backward(x, W)
         return scaled_fc_reference(x, W, b, in_scale, bias_scale)
 
     @staticmethod
@@ -843,17 +864,18 @@ class _ScaledFc(torch.autograd.Function):
         dy = dy.float().contiguous()
         N, K = x.shape
         O = W.shape[1]
-        if x.is_cuda and _MM16[0] is not False:
+        if ctx.half_ops:  # x, W are the forward's fp16 casts
             h = _native.hip()
             d16 = (dy * (gs / in_scale)).half()
-            dxa = _mm16(d16, W.half().t())
-            dWa = _mm16(x.half().t(), d16) if dxa is not None else None
+            dxa = _mm16(d16, W.t())
+            dWa = _mm16(x.t(), d16) if dxa is not None else None
             if dWa is not None:
                 h.h16_epi(dxa, None, in_scale, 1.0, 1.0 / gs)
                 h.h16_epi(dWa, None, in_scale, 1.0, 1.0 / gs)
                 db = W.new_empty(O)
                 h.colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
                 return dxa, dWa, db.reshape(ctx.bshape), None, None, None
+            x, W = x.float(), W.float()  # fp16 values are exact in fp32: the kernel path below recasts
         if x.is_cuda:
             h = _native.hip()
             dx = x.new_empty(N, K)
