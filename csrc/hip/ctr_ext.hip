@@ -211,6 +211,26 @@ __global__ void k_h16_epi(const float* acc, const float* __restrict__ bias, int 
   out[e] = h16_epi(acc[e], bias ? bias[n] : 0.f, g);
 }
 
+// vector form (N % 4 == 0, M * N < 2^31): four columns per thread, 32-bit
+// index math (the 64-bit modulo per element dominated the scalar form)
+__global__ __launch_bounds__(256) void k_h16_epi4(const float* acc, const float* __restrict__ bias, int M, int N,
+                                                  float alpha, float bias_scale, float out_scale, float* out) {
+  const int e4 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total4 = (M * N) >> 2;
+  if (e4 >= total4) return;
+  const int n = (e4 << 2) % N;
+  HgemmArgs g;
+  g.alpha = alpha;
+  g.bias = bias;
+  g.bias_scale = bias_scale;
+  g.out_scale = out_scale;
+  const float4 a = reinterpret_cast<const float4*>(acc)[e4];
+  float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (bias) b = *reinterpret_cast<const float4*>(bias + n);
+  reinterpret_cast<float4*>(out)[e4] =
+      make_float4(h16_epi(a.x, b.x, g), h16_epi(a.y, b.y, g), h16_epi(a.z, b.z, g), h16_epi(a.w, b.w, g));
+}
+
 // split-K second pass: the fp16 epilogue over the fp32 sums
 __global__ void k_hgemm_epi(HgemmArgs g) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1047,6 +1067,13 @@ void launch_hgemm(const HgemmArgs& g0, hipStream_t s) {
 void launch_h16_epi(const float* acc, const float* bias, int M, int N, float alpha, float bias_scale, float out_scale,
                     float* out, hipStream_t s) {
   if ((int64_t)M * N == 0) return;
+  const bool al = ((reinterpret_cast<uintptr_t>(acc) | reinterpret_cast<uintptr_t>(out) |
+                    reinterpret_cast<uintptr_t>(bias)) & 15) == 0;
+  if (N % 4 == 0 && (int64_t)M * N < (int64_t)INT32_MAX && al) {
+    hipLaunchKernelGGL(k_h16_epi4, dim3((unsigned)((((int64_t)M * N) / 4 + 255) / 256)), dim3(256), 0, s, acc, bias, M,
+                       N, alpha, bias_scale, out_scale, out);
+    return;
+  }
   hipLaunchKernelGGL(k_h16_epi, dim3(nblk((int64_t)M * N)), dim3(256), 0, s, acc, bias, M, N, alpha, bias_scale,
                      out_scale, out);
 }
