@@ -105,6 +105,26 @@ void h16_epi(Tensor acc, const c10::optional<Tensor>& bias, double alpha, double
                  cs());
 }
 
+// scaled_fc fused fp16 GEMM (forward / dx): out [M, Nd] = h16_epi(fp16(A * a_scale) @ Bk^T),
+// Bk fp16 [Nd, Kd] contiguous.  Returns an undefined tensor when the shapes do not fit the kernel.
+Tensor sfc(const Tensor& A, const Tensor& Bk, const c10::optional<Tensor>& bias, double a_scale, double alpha,
+           double bias_scale, double out_scale) {
+  f32(A, "A");
+  CX_CHECK(A.dim() == 2 && A.is_contiguous(), "A must be a contiguous [M, Kd] tensor");
+  CX_CHECK(Bk.is_cuda() && Bk.scalar_type() == torch::kHalf && Bk.dim() == 2 && Bk.is_contiguous() &&
+               Bk.size(1) == A.size(1), "Bk must be a contiguous fp16 [Nd, Kd] tensor");
+  const int M = (int)A.size(0), Kd = (int)A.size(1), Nd = (int)Bk.size(0);
+  if (bias.has_value() && bias->defined()) {
+    f32(*bias, "bias");
+    CX_CHECK(bias->numel() >= Nd && bias->is_contiguous(), "bias");
+  }
+  auto out = torch::empty({M, Nd}, A.options());
+  if (!launch_sfc(P<float>(A), static_cast<const void*>(Bk.data_ptr<at::Half>()), M, Nd, Kd, (float)a_scale,
+                  OP<float>(bias), (float)alpha, (float)bias_scale, (float)out_scale, P<float>(out), cs()))
+    return Tensor();
+  return out;
+}
+
 void colsum_strided(const Tensor& x, int64_t batch, int64_t M, int64_t N, int64_t sb, int64_t ld, Tensor out,
                     int64_t so, bool accumulate) {
   f32(x, "x");
@@ -418,6 +438,7 @@ void bind_ctr(py::module& m) {
   m.def("colsum_strided", &colsum_strided);
   m.def("hgemm", &hgemm);
   m.def("h16_epi", &h16_epi);
+  m.def("sfc", &sfc);
   m.def("int8_fc", &int8_fc);
   m.def("rank_attention_fwd", &rank_attention_fwd);
   m.def("rank_attention_bwd", &rank_attention_bwd);

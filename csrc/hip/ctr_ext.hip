@@ -231,6 +231,110 @@ __global__ __launch_bounds__(256) void k_h16_epi4(const float* acc, const float*
       make_float4(h16_epi(a.x, b.x, g), h16_epi(a.y, b.y, g), h16_epi(a.z, b.z, g), h16_epi(a.w, b.w, g));
 }
 
+// ---------------------------------------------------------------- scaled_fc fused fp16 GEMM
+// out[M][Nd] = h16_epi( fp16(A * a_scale) [M][Kd] @ Bk^T ) with Bk fp16 [Nd][Kd]
+// (k-minor: the weight's cached fp16 copy) -- scaled_fc's forward (A = x,
+// Bk = W16^T) and its dx (A = dy, a_scale = grad_scale / in_scale, Bk = W16)
+// in ONE launch: the fp32 -> fp16 cast happens in the A staging and the
+// reference's fp16 epilogue in the store, so no fp16 copy of A and no fp32
+// accumulator matrix go through HBM.  64 x 80 tiles (80 = 5 x 16 divides the
+// 400-wide CTR layers), 4 waves of 16 rows x 80 columns, v_mfma_f32_16x16x32_f16;
+// K in chunks of 64, double-buffered in LDS (41 KB: 3 workgroups per CU), the
+// next chunk's global loads in flight under the current chunk's MFMAs.  The
+// tiles of one row block are consecutive work ids of one XCD, so the A rows
+// come from HBM once and from that XCD's L2 for the other 4 column tiles.
+constexpr int kSfcBM = 64, kSfcBN = 80, kSfcKC = 64, kSfcPad = 72;  // LDS row: 64 k + 8 (bank spread)
+__device__ __forceinline__ int sfc_xcd_id(int block, int n) {
+  const int q = n / 8, rr = n % 8, xcd = block % 8;
+  return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + block / 8;
+}
+__global__ __launch_bounds__(256) void k_sfc(const float* __restrict__ A, const _Float16* __restrict__ Bk, int M,
+                                             int Nd, int Kd, float a_scale, const float* __restrict__ bias,
+                                             float alpha, float bias_scale, float out_scale, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) _Float16 As[2][kSfcBM * kSfcPad];
+  __shared__ __attribute__((aligned(16))) _Float16 Bs[2][kSfcBN * kSfcPad];
+  const int ntn = (Nd + kSfcBN - 1) / kSfcBN, ntiles = ntn * ((M + kSfcBM - 1) / kSfcBM);
+  const int wid = sfc_xcd_id((int)blockIdx.x, ntiles);
+  const int m0 = (wid / ntn) * kSfcBM, n0 = (wid % ntn) * kSfcBN;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  // A staging: row t >> 2, k 16 (t & 3) .. + 15 (four float4, two 16-B LDS writes)
+  const int ar = t >> 2, ak = (t & 3) * 16;
+  const int64_t arow = (int64_t)min(m0 + ar, M - 1) * Kd;
+  const bool arow_ok = m0 + ar < M;
+  float4 ra[4];
+  _Float16 __attribute__((ext_vector_type(8))) rb[3];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int k = k0 + ak + 4 * v;
+      ra[v] = (arow_ok && k < Kd) ? *reinterpret_cast<const float4*>(A + arow + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int idx = t + 256 * i, n = idx >> 3, k = k0 + (idx & 7) * 8;
+      h16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (idx < kSfcBN * 8 && n0 + n < Nd && k < Kd) z = *reinterpret_cast<const h16x8*>(Bk + (int64_t)(n0 + n) * Kd + k);
+      rb[i] = z;
+    }
+  };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      h16x8 v;
+      const float4 x0 = ra[2 * h], x1 = ra[2 * h + 1];
+      v[0] = (_Float16)(x0.x * a_scale); v[1] = (_Float16)(x0.y * a_scale);
+      v[2] = (_Float16)(x0.z * a_scale); v[3] = (_Float16)(x0.w * a_scale);
+      v[4] = (_Float16)(x1.x * a_scale); v[5] = (_Float16)(x1.y * a_scale);
+      v[6] = (_Float16)(x1.z * a_scale); v[7] = (_Float16)(x1.w * a_scale);
+      *reinterpret_cast<h16x8*>(&As[buf][ar * kSfcPad + ak + 8 * h]) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int idx = t + 256 * i;
+      if (idx < kSfcBN * 8) *reinterpret_cast<h16x8*>(&Bs[buf][(idx >> 3) * kSfcPad + (idx & 7) * 8]) = rb[i];
+    }
+  };
+  f32x4 acc[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int nch = (Kd + kSfcKC - 1) / kSfcKC;
+  load(0);
+  stage(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nch) load((c + 1) * kSfcKC);  // in flight under this chunk's MFMAs
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const h16x8 a = *reinterpret_cast<const h16x8*>(&As[buf][(16 * w + fr) * kSfcPad + 32 * s2 + 8 * fk]);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const h16x8 b = *reinterpret_cast<const h16x8*>(&Bs[buf][(16 * j + fr) * kSfcPad + 32 * s2 + 8 * fk]);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[j], 0, 0, 0);
+      }
+    }
+    if (c + 1 < nch) stage(buf ^ 1);  // the other buffer was last read before the previous barrier
+    __syncthreads();
+  }
+  HgemmArgs g;
+  g.alpha = alpha;
+  g.bias = bias;
+  g.bias_scale = bias_scale;
+  g.out_scale = out_scale;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int n = n0 + 16 * j + fr;
+    if (n >= Nd) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + 16 * w + 4 * fk + r;
+      if (m < M) out[(int64_t)m * Nd + n] = h16_epi(acc[j][r], bv, g);
+    }
+  }
+}
+
 // split-K second pass: the fp16 epilogue over the fp32 sums
 __global__ void k_hgemm_epi(HgemmArgs g) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1076,6 +1180,17 @@ void launch_h16_epi(const float* acc, const float* bias, int M, int N, float alp
   }
   hipLaunchKernelGGL(k_h16_epi, dim3(nblk((int64_t)M * N)), dim3(256), 0, s, acc, bias, M, N, alpha, bias_scale,
                      out_scale, out);
+}
+
+bool launch_sfc(const float* A, const void* Bk_, int M, int Nd, int Kd, float a_scale, const float* bias,
+                float alpha, float bias_scale, float out_scale, float* out, hipStream_t s) {
+  const _Float16* Bk = static_cast<const _Float16*>(Bk_);
+  if ((Kd % 8) != 0 || ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(Bk)) & 15) != 0) return false;
+  if ((int64_t)M * Nd == 0) return true;
+  const int tiles = ((Nd + kSfcBN - 1) / kSfcBN) * ((M + kSfcBM - 1) / kSfcBM);
+  hipLaunchKernelGGL(k_sfc, dim3(tiles), dim3(256), 0, s, A, Bk, M, Nd, Kd, a_scale, bias, alpha, bias_scale, out_scale,
+                     out);
+  return true;
 }
 
 void launch_colsum_strided(const float* x, int batch, int M, int N, int64_t sb, int64_t ld, float* out, int64_t so,

@@ -745,6 +745,10 @@ struct HgemmArgs {
   int ksplit = 1;
 };
 // scaled_fc's fp16 epilogue over an fp32 accumulator [M][N] (library GEMM path); out may alias acc
+// scaled_fc fused fp16 GEMM: out = h16_epi(fp16(A * a_scale) @ Bk^T), Bk fp16 [Nd][Kd]
+// (false: Kd % 8 != 0 or misaligned operands -- the caller takes the library path)
+bool launch_sfc(const float* A, const void* Bk_, int M, int Nd, int Kd, float a_scale, const float* bias,
+                float alpha, float bias_scale, float out_scale, float* out, hipStream_t s);
 void launch_h16_epi(const float* acc, const float* bias, int M, int N, float alpha, float bias_scale, float out_scale,
                     float* out, hipStream_t s);
 void launch_hgemm(const HgemmArgs& g, hipStream_t s);

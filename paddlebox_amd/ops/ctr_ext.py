@@ -808,17 +808,18 @@ def _mm16(a16, b16):
     return r.contiguous()
 
 
-def _half_of(W: torch.Tensor) -> torch.Tensor:
-    """fp16 copy of a weight, cached on the tensor until it is modified in
-    place (its version counter moves) -- one cast per optimizer step, not
-    per forward."""
+def _half_of(W: torch.Tensor, transposed: bool = False) -> torch.Tensor:
+    """fp16 copy of a weight (transposed: of W^T, contiguous), cached on the
+    tensor until it is modified in place (its version counter moves) -- one
+    cast per optimizer step, not per forward."""
     key = (W._version, W.data_ptr(), tuple(W.shape))
-    c = getattr(W, "_pbx_half", None)
+    attr = "_pbx_half_t" if transposed else "_pbx_half"
+    c = getattr(W, attr, None)
     if c is not None and c[0] == key:
         return c[1]
-    W16 = W.detach().half()
+    W16 = (W.detach().t() if transposed else W.detach()).contiguous().half()
     try:
-        W._pbx_half = (key, W16)
+        setattr(W, attr, (key, W16))
     except (AttributeError, RuntimeError):
         pass
     return W16
@@ -839,9 +840,16 @@ class _ScaledFc(torch.autograd.Function):
         ctx.bshape = b.shape
         ctx.sc = (in_scale, grad_scale)
         ctx.half_ops = False
+        ctx.fused = False
         if x.is_cuda:
             N, K = x.shape
             O = W.shape[1]
+            # one launch: the x cast, fp16 MFMA GEMM and fp16 epilogue fused (k_sfc)
+            y = _native.hip().sfc(x, _half_of(W, True), b.reshape(-1), 1.0, in_scale, bias_scale, 1.0 / in_scale)
+            if y is not None:
+                ctx.save_for_backward(x, W)
+                ctx.fused = True
+                return y
             x16, W16 = x.half(), _half_of(W)
             acc = _mm16(x16, W16)
             if acc is not None:  # library fp16 GEMM (fp32 accumulate) + the fp16 epilogue
@@ -864,6 +872,17 @@ class _ScaledFc(torch.autograd.Function):
         dy = dy.float().contiguous()
         N, K = x.shape
         O = W.shape[1]
+        if ctx.fused:
+            h = _native.hip()
+            # dx = fp16(dy * gs / in_scale) @ W16^T in one launch (k_sfc, Bk = W16 [K, O])
+            dx = h.sfc(dy, _half_of(W), None, gs / in_scale, in_scale, 1.0, 1.0 / gs)
+            d16 = (dy * (gs / in_scale)).half()
+            dWa = _mm16(x.half().t(), d16) if dx is not None else None
+            if dWa is not None:
+                h.h16_epi(dWa, None, in_scale, 1.0, 1.0 / gs)
+                db = W.new_empty(O)
+                h.colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
+                return dx, dWa, db.reshape(ctx.bshape), None, None, None
         if ctx.half_ops:  # x, W are the forward's fp16 casts
             h = _native.hip()
             d16 = (dy * (gs / in_scale)).half()

@@ -92,9 +92,11 @@ def test_batch_fc_gpu(mode):
         _close(a.grad, b.grad, atol=1e-3)
 
 
-@pytest.mark.parametrize("shape", [(300, 130, 65), (1, 1, 1), (4096, 512, 256), (2053, 33, 97)])
+@pytest.mark.parametrize("shape", [(300, 130, 65), (1, 1, 1), (4096, 512, 256), (2053, 33, 97), (1000, 200, 130),
+                                   (777, 400, 400), (65, 8, 8)])
 def test_scaled_fc_gpu(shape):
-    """fp16 MFMA (k_hgemm) against the same fp16 rounding chain in torch: the
+    """fp16 MFMA (k_sfc when K % 8 == 0, else the library fp16 GEMM / k_hgemm)
+    against the same fp16 rounding chain in torch: the
     products differ only in fp32 accumulation order, so results agree to one
     fp16 ulp; the fp32 bias gradient is exact up to summation order."""
     N, K, O = shape
