@@ -880,7 +880,7 @@ class _ScaledFc(torch.autograd.Function):
             dWa = _mm16(x.half().t(), d16) if dx is not None else None
             if dWa is not None:
                 h.h16_epi(dWa, None, in_scale, 1.0, 1.0 / gs)
-                db = W.new_empty(O)
+                db = dy.new_empty(O)
                 h.colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
                 return dx, dWa, db.reshape(ctx.bshape), None, None, None
         if ctx.half_ops:  # x, W are the forward's fp16 casts
@@ -891,7 +891,7 @@ class _ScaledFc(torch.autograd.Function):
             if dWa is not None:
                 h.h16_epi(dxa, None, in_scale, 1.0, 1.0 / gs)
                 h.h16_epi(dWa, None, in_scale, 1.0, 1.0 / gs)
-                db = W.new_empty(O)
+                db = dy.new_empty(O)
                 h.colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
                 return dxa, dWa, db.reshape(ctx.bshape), None, None, None
             x, W = x.float(), W.float()  # fp16 values are exact in fp32: the kernel path below recasts
