@@ -84,6 +84,11 @@ class _PullSlot:
         h = eng._hip
         with torch.cuda.device(dev):
             self.ws = h.DedupWorkspace(eng.max_keys, dev.index or 0, True)
+            if getattr(eng, "table_dedup", False):
+                # allocate (and -1 / zero fill) the table-dedup buffers now: a
+                # slot first used inside a graph capture would otherwise record
+                # those fills into the graph and replay them every step
+                self.ws.table_rows_occ()
         self.occ_slot = torch.empty(eng.max_keys, dtype=torch.int32, device=dev)
         self.occ_ins = torch.empty(eng.max_keys, dtype=torch.int32, device=dev)
         self.rows = None  # persistent probe rows of a prefetched batch
