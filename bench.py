@@ -342,7 +342,8 @@ def main():
                     pipe = (lambda b, j: step.prefetch(b, j), step.set_next, engine.clear_prefetch)
                 graphed = GraphedTrainStep(train_step, host_batches[0], device, prefetch=pre,
                                            steps_per_graph=K if pre is None else 1,
-                                           n_buffers=3 if pipe is not None else 2, pipeline=pipe)
+                                           n_buffers=3 if pipe is not None else 2, pipeline=pipe,
+                                           join_each_step=not step.adam_overlap)
                 graphed.warm(host_batches, replays=args.graph_warm)
                 log(rank, f"[bench] training step captured into HIP graphs ({args.graph_warm} warm replays)")
             except Exception as e:  # pragma: no cover - depends on runtime

@@ -28,7 +28,7 @@ import torch.distributed as dist
 
 from .. import _native
 from ..parallel.comm import allreduce_sum, collective_active
-from ..parallel.dense import add_grad_producer, join_grad_producers
+from ..parallel.dense import add_grad_producer, join_grad_producers, pop_pre_head_event
 from . import reference as ref
 from .mlp import _ensure_grad
 
@@ -52,11 +52,19 @@ class _CtrTowerFn(torch.autograd.Function):
     def forward(ctx, x, extra, label, t: "CtrTower", *params):
         h = _native.hip()
         mlp, dn = t.mlp, t.dn
-        if x.is_cuda:
+        pre_head = pop_pre_head_event(id(t)) if x.is_cuda else None
+        if pre_head is not None:
+            # overlapped optimizer: the previous step's dW (which reads this
+            # head's output buffers) and data_norm update are done; its Adam
+            # may still run on the side stream -- joined below, before the
+            # tower reads the weights
+            torch.cuda.current_stream(x.device).wait_event(pre_head)
+        elif x.is_cuda:
             join_grad_producers()  # a previous dW still reading the activations (no optimizer step between)
         B = x.shape[0]
         ws = mlp.tower_workspace(B, x.device, fp32=t.fp32)
-        mlp.ensure_packed()
+        if pre_head is None:
+            mlp.ensure_packed()
         x = x.contiguous()
         yt = t._cross_yt(B, x.device) if t.cross is not None else None
         Cp = ws.K0p  # MLP input width: padded to 32 (bf16 tower) / 16 (fp32 tower)
@@ -82,6 +90,9 @@ class _CtrTowerFn(torch.autograd.Function):
             s = xw.forward(ws.x0(), [w.detach() for w in net.w], [b.detach() for b in net.b], w_c.detach())
             lin_use = s if lin_use is None else lin_use + s
             ctx.yt = yt
+        if pre_head is not None:
+            join_grad_producers()
+            mlp.ensure_packed()
         auc = t.auc
         loss, pred, dz = ws.forward(list(mlp.b), mlp.w_out.view(-1), mlp.b_out, lin_use, label.contiguous().view(-1),
                                     auc[0] if auc else None, auc[1] if auc else None, auc[2] if auc else None)

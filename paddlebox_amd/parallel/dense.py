@@ -35,11 +35,27 @@ def add_grad_producer(stream) -> None:
     _GRAD_PRODUCERS.append(stream)
 
 
+# Overlapped optimizer (CtrTrainStep adam_overlap): the side stream records an
+# event once the data_norm summaries are updated (before its Adam); the next
+# step's head may start after that event instead of after the whole side
+# stream.  Keyed by the tower; any full join makes the events moot.
+_PRE_HEAD: Dict[int, "torch.cuda.Event"] = {}
+
+
+def set_pre_head_event(key: int, ev) -> None:
+    _PRE_HEAD[key] = ev
+
+
+def pop_pre_head_event(key: int):
+    return _PRE_HEAD.pop(key, None)
+
+
 def join_grad_producers() -> None:
     """Make the current stream wait for every pending gradient producer."""
     while _GRAD_PRODUCERS:
         s = _GRAD_PRODUCERS.pop()
         torch.cuda.current_stream(s.device).wait_stream(s)
+    _PRE_HEAD.clear()
 
 
 class DenseArena:

@@ -96,8 +96,17 @@ class CtrTrainStep:
         # one update launch for the dense side: Adam + tower weight re-pack +
         # data_norm summary update; grads zeroed by the same kernel
         self.opt = FlatAdam(self.arena, lr=lr, clear_grad=True)
+        tower = getattr(model, "tower", None)
+        # PBX_ADAM_OVERLAP=1 (one rank, fused tower): the update runs on the dW
+        # side stream after the data_norm summary update, and the NEXT step's
+        # head (data_norm + concat) starts once that summary update is done --
+        # only the tower forward waits for Adam (the step boundary no longer
+        # serialises head_fwd behind the optimizer)
+        self.adam_overlap = (not multi and self.fused and tower is not None
+                             and os.environ.get("PBX_ADAM_OVERLAP", "0") == "1")
         if self.fused:
-            self.opt.fuse(mlps=[model.mlp], data_norms=[model.dn])
+            # the overlap keeps the data_norm update out of the Adam launch
+            self.opt.fuse(mlps=[model.mlp], data_norms=[] if self.adam_overlap else [model.dn])
         self.ipc = None
         if multi and (dense == "ipc" or same_gpu):
             self.ipc = make_ipc_mesh(self.arena.grad.numel() * 4, device, log=log)
@@ -108,11 +117,13 @@ class CtrTrainStep:
         # inside the captured graph: two RCCL communicators in flight on one
         # stream set can deadlock)
         self.sync = DenseSync(self.arena, mode="grad_allreduce", ipc=self.ipc)
-        tower = getattr(model, "tower", None)
         # PBX_ADAM_ON_SIDE=1 (one rank): the Adam update is issued from the
         # tower's dense-grads hook on the dW side stream (measured no faster)
-        self.adam_side = (not multi) and os.environ.get("PBX_ADAM_ON_SIDE", "0") == "1" and tower is not None
-        if self.adam_side:
+        self.adam_side = ((not multi) and os.environ.get("PBX_ADAM_ON_SIDE", "0") == "1" and tower is not None
+                          and not self.adam_overlap)
+        if self.adam_overlap:
+            tower.on_dense_grads = self._side_update
+        elif self.adam_side:
             tower.on_dense_grads = lambda: self.opt.step(1.0, join=False)
         elif tower is not None and (self.ipc is not None or not multi):
             # start the IPC all-reduce as soon as the tower's gradients are final
@@ -142,6 +153,16 @@ class CtrTrainStep:
                 tower.on_dx_done = self._dedup_next
             else:
                 tower.on_head_done = self._dedup_next
+
+    def _side_update(self):
+        """On the dW side stream, after the data_norm summary update: mark the
+        point the next step's head may start from, then Adam."""
+        from ..parallel.dense import set_pre_head_event
+
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        set_pre_head_event(id(self.model.tower), ev)
+        self.opt.step(1.0, join=False)
 
     def set_next(self, batch, slot: int = 0):
         """Batch to prefetch (pool) at the end of each train_step (None: off)."""
@@ -182,7 +203,9 @@ class CtrTrainStep:
                 self.model.prefetch_pool(self.next_batch, self.next_slot)
             else:
                 self.prefetch(self.next_batch, self.next_slot)
-        if self.adam_side:
+        if self.adam_overlap:
+            pass  # the side stream runs the update; the next forward joins it after its head
+        elif self.adam_side:
             join_grad_producers()  # the side stream ran the update
         else:
             self.sync.before_step()

@@ -79,7 +79,7 @@ class GraphedTrainStep:
     def __init__(self, step_fn: Callable[[Any], Any], example_batch, device, n_buffers: int = 2,
                  warmup: int = 3, max_inflight: int = 3, warm_batches: Sequence[Any] = (),
                  on_warm: Optional[Callable[[Any], None]] = None, prefetch=None, steps_per_graph: int = 1,
-                 pipeline=None):
+                 pipeline=None, join_each_step: bool = True):
         """``steps_per_graph`` K > 1: each graph holds K consecutive training
         steps over K batch buffers (``load`` then takes K host batches and
         ``run`` trains all K).  Inside one graph consecutive steps are
@@ -172,7 +172,11 @@ class GraphedTrainStep:
                         b1 = (j * self.K + k + 1) % nK
                         pipeline[1](self.bufs[b1], b1)
                     out = step_fn(self.bufs[j * self.K + k])
-                    join_grad_producers()  # side streams forked in the step rejoin (before the capture ends)
+                    if join_each_step or k == self.K - 1:
+                        # side streams forked in the step rejoin (before the capture
+                        # ends; join_each_step=False: a step's side work may run on
+                        # under the next step of the same graph, which joins it)
+                        join_grad_producers()
                 if prefetch is not None:
                     torch.cuda.current_stream(self.device).wait_stream(self._side)
             pool = g.pool()

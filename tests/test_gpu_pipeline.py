@@ -41,7 +41,7 @@ def _train(pipeline: bool, precision: str, K: int = 1):
     losses = []
     g = GraphedTrainStep(step.train_step, hbs[0], DEV, warmup=0, warm_batches=[hbs[0]],
                          on_warm=lambda out: losses.append(float(out)), n_buffers=3 if pipeline else 2,
-                         pipeline=pipe, steps_per_graph=K)
+                         pipeline=pipe, steps_per_graph=K, join_each_step=not step.adam_overlap)
     if K == 1:
         ahead = 2 if pipeline else 1
         for a in range(1, 1 + ahead):
@@ -68,13 +68,18 @@ def _train(pipeline: bool, precision: str, K: int = 1):
     return step.arena.flat.cpu(), losses, hk[o].cpu(), v[o].cpu()
 
 
-@pytest.mark.parametrize("precision,K,split", [("fp32", 1, "0"), ("bf16", 1, "0"), ("fp32", 2, "0"), ("fp32", 1, "2"),
-                                               ("fp32", 2, "1")])
-def test_pipelined_front_matches_plain_graphed_step(precision, K, split, monkeypatch):
+@pytest.mark.parametrize("precision,K,split,overlap", [("fp32", 1, "0", "0"), ("bf16", 1, "0", "0"),
+                                                       ("fp32", 2, "0", "0"), ("fp32", 1, "2", "0"),
+                                                       ("fp32", 2, "1", "0"), ("fp32", 2, "0", "1"),
+                                                       ("bf16", 2, "0", "1")])
+def test_pipelined_front_matches_plain_graphed_step(precision, K, split, overlap, monkeypatch):
     # split: the next batch's key dedup on its own stream (PBX_SPLIT_PREFETCH,
-    # forked at the dX chain (1) or after the head backward (2))
+    # forked at the dX chain (1) or after the head backward (2)); overlap:
+    # Adam on the dW side stream, the next head not waiting for it
+    # (PBX_ADAM_OVERLAP, the step's side work joined by the next step)
     f0, l0, k0, v0 = _train(False, precision, K)
     monkeypatch.setenv("PBX_SPLIT_PREFETCH", split)
+    monkeypatch.setenv("PBX_ADAM_OVERLAP", overlap)
     f1, l1, k1, v1 = _train(True, precision, K)
     # the dW split-K atomics sum in any order: fp32-rounding-level differences
     rt, at = (1e-6, 1e-7) if precision == "fp32" else (1e-4, 1e-5)
