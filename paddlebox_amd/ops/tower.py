@@ -131,7 +131,7 @@ class _CtrTowerFn(torch.autograd.Function):
                 t.on_dense_grads()
 
         deferred_dw = None
-        if t.overlap_dw and x.is_cuda and not _collectives_in_step():
+        if t.overlap_dw and x.is_cuda and (t.overlap_dw_collectives or not _collectives_in_step()):
             # dX chain on the compute stream; the dW GEMMs + bias / data_norm
             # reductions (and whatever consumes the dense grads) on a side
             # stream, concurrent with the head backward and the sparse push;
@@ -217,6 +217,11 @@ class CtrTower:
         # run the dW GEMM on a side stream, overlapped with the head backward
         # and the sparse push (PBX_TOWER_OVERLAP_DW=0 turns it off)
         self.overlap_dw = os.environ.get("PBX_TOWER_OVERLAP_DW", "1") != "0"
+        # with collectives in the step the dW stays on the compute stream
+        # (an RCCL all-reduce on a side stream delayed the sparse exchange) --
+        # unless the owner sets this: its dense all-reduce is an IPC mesh
+        # launched from the dW stream (CtrTrainStep)
+        self.overlap_dw_collectives = False
         # ... enqueued after the head backward, or right after the dX chain.
         # Measured (profiles/r3_s2_dw_after_head.txt): after the head for
         # DeepFM (0.255 vs 0.278 ms/step), right after the dX chain with a

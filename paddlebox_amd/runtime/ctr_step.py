@@ -128,6 +128,11 @@ class CtrTrainStep:
         elif tower is not None and (self.ipc is not None or not multi):
             # start the IPC all-reduce as soon as the tower's gradients are final
             tower.on_dense_grads = self.sync.launch
+            # multi-rank with the IPC dense mesh: the dW GEMM (and the all-reduce
+            # it launches) may run on the side stream beside the head backward
+            # and the sparse push exchange (PBX_OVERLAP_DW_IPC=1)
+            tower.overlap_dw_collectives = (multi and self.ipc is not None
+                                            and os.environ.get("PBX_OVERLAP_DW_IPC", "0") == "1")
         self.fused_auc = fused_auc is not None and self.fused
         if self.fused_auc:
             tower.auc = (fused_auc[0], fused_auc[1], None)
