@@ -338,7 +338,11 @@ def main():
                 pre = (engine, lambda b: b.keys) if (args.prefetch and engine.can_prefetch()) else None
                 pipe = None
                 want_pipe = args.pipeline == "on" or (args.pipeline == "auto" and mlp_dtype == "fp32" and not dcn)
-                if want_pipe and pre is None and engine.can_prefetch() and engine.table_dedup:
+                # multi-rank: the sharded prefetch (exchanges inside the graphs)
+                # stays opt-in until measured (PBX_SHARDED_PIPELINE=1)
+                pipe_ok = engine.can_prefetch_pull() and (
+                    not engine.sharded or os.environ.get("PBX_SHARDED_PIPELINE", "0") == "1")
+                if want_pipe and pre is None and pipe_ok:
                     pipe = (lambda b, j: step.prefetch(b, j), step.set_next, engine.clear_prefetch)
                 graphed = GraphedTrainStep(train_step, host_batches[0], device, prefetch=pre,
                                            steps_per_graph=K if pre is None else 1,

@@ -416,7 +416,7 @@ class SparseEngine:
                 out[:, dense_col:dense_col + dense.shape[1]] = dense
             return st
         h = self._hip
-        pre_out = self._prepared_out.pop(keys.data_ptr(), None) if (not self.sharded and self._prepared_out) else None
+        pre_out = self._prepared_out.pop(keys.data_ptr(), None) if self._prepared_out else None
         if pre_out is not None and pre_out is out and col_offset == 0:
             # prefetch_pull already pooled this batch into out: only the pull state
             return self._pull_common(keys, lod, B, S, fill_occ=False)
@@ -571,6 +571,12 @@ class SparseEngine:
         self._prepared[keys.data_ptr()] = (sl, L)
 
     def can_prefetch_pull(self) -> bool:
+        if self.sharded:
+            # the whole sharded pull (dedup, key / answer exchanges on the IPC
+            # meshes, owner probe + gather, pooling) ahead of its step: IPC
+            # meshes only (capturable, no RCCL inside the graphs), fixed keys
+            return (self.is_gpu and self.xmesh is not None and self.codec is None and self.dedup
+                    and not (self.auto_insert and not self.test_mode) and len(self._slots) >= 2)
         return self.can_prefetch() and self.table_dedup and self.codec is None
 
     def prefetch_pull(self, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int, sp: "SeqpoolParams",
@@ -582,9 +588,41 @@ class SparseEngine:
         stream, it runs under the previous step's dW GEMM; the batch's own
         pull then returns the buffer with no launch at all.  False when the
         engine cannot prepare pulls (sharded, codec rows, auto-insert)."""
+        if self.sharded:
+            return self._prefetch_pull_sharded(keys, lod, B, S, sp, dense, slot)
         if not self.prefetch_dedup(keys, slot):
             return False
         return self.prefetch_pool(keys, lod, B, S, sp, dense, slot)
+
+    def _prefetch_pull_sharded(self, keys, lod, B, S, sp, dense, slot) -> bool:
+        """Sharded prefetch_pull: the complete pull of the next batch into pull
+        slot ``slot`` -- sender dedup, key exchange, owner probe + gather,
+        answer exchange, fused seqpool/CVM into the slot's persistent output.
+        Issued after this step's push (and its owner-side update) in stream
+        order on every rank, so every owner answers with the updated rows."""
+        if not self.can_prefetch_pull():
+            return False
+        keys = keys.reshape(-1)
+        L = keys.numel()
+        assert L <= self.max_keys
+        sl = self._slots[slot % len(self._slots)]
+        sl.gen += 1
+        st = self._pull_into_slot(sl, keys, lod, B, S, fill_occ=False)
+        Eo = sp.out_width(self.E)
+        Dd = 0 if dense is None else int(dense.shape[1])
+        shape = (B, S * Eo + Dd)
+        if sl.pre_out is None or tuple(sl.pre_out.shape) != shape:
+            sl.pre_out = torch.empty(shape, dtype=torch.float32, device=self.device)
+        self._hip.seqpool_cvm_fwd(sl.resp_back, sl.send_index, sl.ws.uid, lod, S, B, self.E, sl.pre_out, 0,
+                                  sp.use_cvm, sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter,
+                                  sp.show_coeff, sp.clk_coeff, sp.threshold, sp.quant_ratio,
+                                  sp.embed_threshold_filter, sp.embed_threshold,
+                                  sp.embed_thres_size if not sp.use_cvm else 0,
+                                  dense.contiguous().float() if dense is not None else None, S * Eo,
+                                  occ_slot=sl.occ_slot, occ_ins=sl.occ_ins)
+        self._prepared[keys.data_ptr()] = (sl, L, st)
+        self._prepared_out[keys.data_ptr()] = sl.pre_out
+        return True
 
     def prefetch_dedup(self, keys: torch.Tensor, slot: int = 0) -> bool:
         """The key half of prefetch_pull (table dedup + probe into the slot):
@@ -629,7 +667,7 @@ class SparseEngine:
 
     def prepared_output(self, keys: torch.Tensor) -> Optional[torch.Tensor]:
         """The pooled output a prefetch_pull left for this key buffer (or None)."""
-        return self._prepared_out.get(keys.data_ptr()) if self.is_gpu and not self.sharded else None
+        return self._prepared_out.get(keys.data_ptr()) if self.is_gpu else None
 
     def clear_prefetch(self, reset_rows: bool = False):
         """Forget the prepared pulls.  reset_rows: also hand every pull slot's
@@ -678,6 +716,12 @@ class SparseEngine:
         L = keys.numel()
         assert L <= self.max_keys, f"batch has {L} keys > engine max_keys {self.max_keys}"
         pre = self._prepared.pop(keys.data_ptr(), None) if self._prepared else None
+        if pre is not None and pre[1] == L and self.sharded and len(pre) > 2:
+            # prefetch_pull ran the whole sharded pull (exchanges included)
+            # into this slot: its state is the pull state
+            st = pre[2]
+            self._cur = pre[0]
+            return st
         if pre is not None and pre[1] == L and not self.sharded:
             sl = pre[0]
             sl.gen += 1
@@ -689,7 +733,11 @@ class SparseEngine:
                            gen=sl.gen)
             st.rows = sl.rows[:L]
             return st
-        sl = self._take_slot()
+        return self._pull_into_slot(self._take_slot(), keys, lod, B, S, fill_occ)
+
+    def _pull_into_slot(self, sl: _PullSlot, keys, lod, B, S, fill_occ: bool) -> PullState:
+        h = self._hip
+        L = keys.numel()
         ws = sl.ws
         if self.table_dedup:
             ws.run_table(keys, self.table.t)

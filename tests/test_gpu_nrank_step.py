@@ -60,8 +60,10 @@ def _union_keys(union):
     return torch.unique(ref.mix64(allk[allk != -1]))
 
 
-def _worker(rank, W, port, B, steps, q):
+def _worker(rank, W, port, B, steps, q, mode="plain"):
     try:
+        if mode == "overlap_dw":
+            os.environ["PBX_OVERLAP_DW_IPC"] = "1"
         import torch.distributed as dist
 
         from paddlebox_amd.ops import reference as ref
@@ -78,7 +80,8 @@ def _worker(rank, W, port, B, steps, q):
         per_rank, union = _data(W, B, steps)
         S = union[0].S
         eng = SparseEngine(_cfg(), max_keys=B * S, device=dev, capacity=400_000, comm=TorchDistComm(),
-                           exchange="ipc", exchange_capacity=B * S, slot_ids=[float(s + 1) for s in range(S)])
+                           exchange="ipc", exchange_capacity=B * S, slot_ids=[float(s + 1) for s in range(S)],
+                           pull_ring=3)
         assert eng.exchange_mode == "ipc", eng.exchange_mode
         h = _union_keys(union)
         eng.insert_local_mixed(h[ref.owner_of(h, W) == rank].to(dev), init_embedx=True)
@@ -88,10 +91,21 @@ def _worker(rank, W, port, B, steps, q):
         hbs = [pack_batch(per_rank[i][rank], pin=True) for i in range(steps)]
         losses = []
         # step 0 eagerly through the graph's buffers, then the captured replays
+        pipe = None
+        if mode == "pipeline":
+            # sharded pipelined front: each step pulls the next batch (dedup,
+            # both exchanges, owner gather, pooling) right after its own push
+            assert eng.can_prefetch_pull()
+            pipe = (lambda b, j: step.prefetch(b, j), step.set_next, eng.clear_prefetch)
         g = GraphedTrainStep(step.train_step, hbs[0], dev, warmup=0, warm_batches=[hbs[0]],
-                             on_warm=lambda out: losses.append(float(out)))
+                             on_warm=lambda out: losses.append(float(out)), n_buffers=3 if pipe else 2,
+                             pipeline=pipe)
+        ahead = 2 if pipe else 1
+        for a in range(1, min(1 + ahead, steps)):
+            g.load(a % g.n, hbs[a])
         for i in range(1, steps):
-            g.load(i % g.n, hbs[i])
+            if i + ahead < steps:
+                g.load((i + ahead) % g.n, hbs[i + ahead])
             out = g.run(i % g.n)
             torch.cuda.synchronize()
             losses.append(float(out))  # the graphs' loss outputs share the tower's workspace scalar
@@ -145,15 +159,19 @@ def _oracle(W, B, steps):
                 eng=eng, losses=losses)
 
 
-@pytest.mark.parametrize("W", [2, 4])
-def test_nrank_graphed_deepfm_step_matches_union_oracle(W):
+@pytest.mark.parametrize("W,mode", [(2, "plain"), (4, "plain"), (2, "overlap_dw"), (2, "pipeline"),
+                                    (4, "pipeline")])
+def test_nrank_graphed_deepfm_step_matches_union_oracle(W, mode):
+    """mode: plain graphed step; overlap_dw = the dW GEMM and its IPC dense
+    all-reduce on the side stream (PBX_OVERLAP_DW_IPC); pipeline = the sharded
+    pipelined front (SparseEngine prefetch_pull with the exchanges inside)."""
     from paddlebox_amd.ops import reference as ref
 
-    B, steps = 256, 3
+    B, steps = 256, 4 if mode == "pipeline" else 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, W, port, B, steps, q)) for r in range(W)]
+    ps = [ctx.Process(target=_worker, args=(r, W, port, B, steps, q, mode)) for r in range(W)]
     for p in ps:
         p.start()
     res = {}
