@@ -308,9 +308,24 @@ def main():
         # the model, dense arena + fused Adam, the dense all-reduce (IPC mesh
         # launched from the tower's dense-grads hook, RCCL fallback) and the
         # data_norm statistics in the gradient bucket: runtime/ctr_step.py
+        # the pipelined front (next batch pooled after the push): fp32 DeepFM by
+        # default; multi-rank it runs the sharded pull with its IPC exchanges
+        # inside the graphs and pairs with the dW GEMM + IPC dense all-reduce
+        # on the side stream (rehearsal 0.526 -> 0.434 ms/step with both,
+        # either alone no faster: profiles/r4_sharded_pipeline_ab.txt);
+        # PBX_SHARDED_PIPELINE=0 turns the multi-rank form off
+        want_pipe = args.pipeline == "on" or (args.pipeline == "auto" and mlp_dtype == "fp32" and not dcn)
+        pipe_ok = args.graph and engine.can_prefetch_pull() and (
+            not engine.sharded or os.environ.get("PBX_SHARDED_PIPELINE", "1") == "1")
+        use_pipe = want_pipe and pipe_ok and not (args.prefetch and engine.can_prefetch())
+        set_ov = use_pipe and engine.sharded and "PBX_OVERLAP_DW_IPC" not in os.environ
+        if set_ov:
+            os.environ["PBX_OVERLAP_DW_IPC"] = "1"  # read by CtrTrainStep's constructor only
         step = CtrTrainStep(engine, model_name, mlp_dtype, num_slots=S, dense_dim=13, hidden=hidden,
                             cross_layers=args.cross_layers, multi=multi, dense=args.dense, same_gpu=args.same_gpu,
                             fused_auc=(auc_table, auc_stats), log=lambda m: log(rank, "[bench] dense " + m))
+        if set_ov:
+            del os.environ["PBX_OVERLAP_DW_IPC"]
         model, opt, arena, sync, ipc, fused = step.model, step.opt, step.arena, step.sync, step.ipc, step.fused
 
         # every pinned batch buffer is streamed to the device once up front so the
@@ -337,12 +352,7 @@ def main():
 
                 pre = (engine, lambda b: b.keys) if (args.prefetch and engine.can_prefetch()) else None
                 pipe = None
-                want_pipe = args.pipeline == "on" or (args.pipeline == "auto" and mlp_dtype == "fp32" and not dcn)
-                # multi-rank: the sharded prefetch (exchanges inside the graphs)
-                # stays opt-in until measured (PBX_SHARDED_PIPELINE=1)
-                pipe_ok = engine.can_prefetch_pull() and (
-                    not engine.sharded or os.environ.get("PBX_SHARDED_PIPELINE", "0") == "1")
-                if want_pipe and pre is None and pipe_ok:
+                if use_pipe and pre is None:
                     pipe = (lambda b, j: step.prefetch(b, j), step.set_next, engine.clear_prefetch)
                 graphed = GraphedTrainStep(train_step, host_batches[0], device, prefetch=pre,
                                            steps_per_graph=K if pre is None else 1,
