@@ -318,7 +318,11 @@ def main():
         pipe_ok = args.graph and engine.can_prefetch_pull() and (
             not engine.sharded or os.environ.get("PBX_SHARDED_PIPELINE", "1") == "1")
         use_pipe = want_pipe and pipe_ok and not (args.prefetch and engine.can_prefetch())
-        set_ov = use_pipe and engine.sharded and "PBX_OVERLAP_DW_IPC" not in os.environ
+        # (not in the same-GPU rehearsal: its W processes' spinning collectives
+        # share one GPU's CU slots, and two concurrent meshes per process ran
+        # into the IPC wait bound there)
+        set_ov = (use_pipe and engine.sharded and not args.same_gpu
+                  and "PBX_OVERLAP_DW_IPC" not in os.environ)
         if set_ov:
             os.environ["PBX_OVERLAP_DW_IPC"] = "1"  # read by CtrTrainStep's constructor only
         step = CtrTrainStep(engine, model_name, mlp_dtype, num_slots=S, dense_dim=13, hidden=hidden,
