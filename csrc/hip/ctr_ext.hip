@@ -1257,7 +1257,9 @@ void launch_rank_attention_fwd(const float* x, const int* ro, int ld, const floa
   PBX_RA_DISPATCH(k_ra_bucket, dim3(1), kRaBucketThreads, ro, ld, B, perm, meta);
   const dim3 gf(ra_max_tiles(B, R), (P + 63) / 64);
   const bool wide = C % 16 == 0 && P % 4 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W)) & 15) == 0;
-  if (wide)
+  if (wide && C % 32 == 0 && R * C >= 512)
+    ra_fwd_launch<256>(R, gf, s, x, ro, ld, W, B, C, P, perm, meta, out);  // 2 chunk round trips at R*C = 512
+  else if (wide)
     ra_fwd_launch<128>(R, gf, s, x, ro, ld, W, B, C, P, perm, meta, out);
   else
     ra_fwd_launch<64>(R, gf, s, x, ro, ld, W, B, C, P, perm, meta, out);
