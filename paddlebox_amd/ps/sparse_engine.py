@@ -608,6 +608,13 @@ class SparseEngine:
         sl = self._slots[slot % len(self._slots)]
         sl.gen += 1
         st = self._pull_into_slot(sl, keys, lod, B, S, fill_occ=False)
+        self._pool_sharded(sl, st, keys, lod, B, S, sp, dense)
+        return True
+
+    def _pool_sharded(self, sl: _PullSlot, st: PullState, keys, lod, B, S, sp, dense):
+        """Fused seqpool/CVM of a prefetched sharded pull into the slot's
+        persistent output; the pull state is kept for the batch's own step."""
+        L = keys.numel()
         Eo = sp.out_width(self.E)
         Dd = 0 if dense is None else int(dense.shape[1])
         shape = (B, S * Eo + Dd)
@@ -622,7 +629,6 @@ class SparseEngine:
                                   occ_slot=sl.occ_slot, occ_ins=sl.occ_ins)
         self._prepared[keys.data_ptr()] = (sl, L, st)
         self._prepared_out[keys.data_ptr()] = sl.pre_out
-        return True
 
     def prefetch_dedup(self, keys: torch.Tensor, slot: int = 0) -> bool:
         """The key half of prefetch_pull (table dedup + probe into the slot):
@@ -632,6 +638,11 @@ class SparseEngine:
             return False
         assert keys.numel() <= self.max_keys
         sl = self._slots[slot % len(self._slots)]
+        if self.sharded:
+            # the sender dedup only (keys -> uniques, per-owner counts); the
+            # pack, both exchanges and the pooling follow in prefetch_pool
+            self._hash_dedup(sl, keys.reshape(-1))
+            return True
         sl.ws.run_table(keys, self.table.t)
         sl.rows = sl.ws.rows_u
         return True
@@ -645,6 +656,11 @@ class SparseEngine:
             return False
         L = keys.numel()
         sl = self._slots[slot % len(self._slots)]
+        if self.sharded:
+            sl.gen += 1
+            st = self._sharded_after_dedup(sl, L, lod, B, S)
+            self._pool_sharded(sl, st, keys, lod, B, S, sp, dense)
+            return True
         ws = sl.ws
         Eo = sp.out_width(self.E)
         Dd = 0 if dense is None else int(dense.shape[1])
@@ -753,18 +769,31 @@ class SparseEngine:
                     self.table.insert_mixed(torch.unique(ref.mix64(keys.reshape(-1)[miss])), self.cfg.sgd)
                     ws.run_table(keys, self.table.t)
             return st
-        # IPC exchange: the shard pack's per-owner counters are zeroed by the
-        # dedup's first launch (no fill launches of their own)
-        ipc = self.sharded and self.xmesh is not None
-        ws.run(keys, False, sl.ocnt if ipc else None)
+        self._hash_dedup(sl, keys)
         if fill_occ:
             h.fill_occurrence(lod, S, B, sl.occ_slot, sl.occ_ins)
-        st = PullState(B=B, S=S, L=L, lod=lod, uid=ws.uid, perm=ws.perm, counts=ws.u_count, slot=sl, gen=sl.gen)
         if not self.sharded:
+            st = PullState(B=B, S=S, L=L, lod=lod, uid=ws.uid, perm=ws.perm, counts=ws.u_count, slot=sl,
+                           gen=sl.gen)
             st.rows = self.table.probe(ws.uniq_h[:L], ws.u_count)
             if self.auto_insert and not self.test_mode:
                 self._auto_insert(st, L)
             return st
+        return self._sharded_after_dedup(sl, L, lod, B, S)
+
+    def _hash_dedup(self, sl: _PullSlot, keys):
+        # IPC exchange: the shard pack's per-owner counters are zeroed by the
+        # dedup's first launch (no fill launches of their own)
+        ipc = self.sharded and self.xmesh is not None
+        sl.ws.run(keys, False, sl.ocnt if ipc else None)
+
+    def _sharded_after_dedup(self, sl: _PullSlot, L: int, lod, B: int, S: int) -> PullState:
+        """Sharded pull after the sender dedup: pack per owner, key exchange,
+        owner probe + gather, answer exchange."""
+        h = self._hip
+        ws = sl.ws
+        ipc = self.xmesh is not None
+        st = PullState(B=B, S=S, L=L, lod=lod, uid=ws.uid, perm=ws.perm, counts=ws.u_count, slot=sl, gen=sl.gen)
         # sharded: pack per-owner, exchange keys, owner-side dedup/probe/gather
         h.shard_pack_hash(ws.uniq_h, ws.u_count, self.world, self.C, sl.send, sl.send_index, sl.ocnt, self.overflow,
                           ipc)

@@ -151,12 +151,17 @@ class CtrTrainStep:
         #      push and the dW GEMM (both wait on nothing it produces);
         # its pooling follows the push on this stream.  0 (default): the dedup
         # runs after the push on this stream.
+        #   3: forked at the START of the step onto the tower's dW stream (idle
+        #      until this step's dX chain is done), beside the head and tower
+        #      forward / backward -- for the sharded step, whose dedup + exchange
+        #      chain after the push is far longer than the dW GEMM
         mode = os.environ.get("PBX_SPLIT_PREFETCH", "0")
-        self.split_prefetch = mode in ("1", "2") and tower is not None and hasattr(model, "prefetch_pool")
+        self.split_mode = mode if mode in ("1", "2", "3") else "0"
+        self.split_prefetch = self.split_mode != "0" and tower is not None and hasattr(model, "prefetch_pool")
         if self.split_prefetch:
             if mode == "1":
                 tower.on_dx_done = self._dedup_next
-            else:
+            elif mode == "2":
                 tower.on_head_done = self._dedup_next
 
     def _side_update(self):
@@ -194,9 +199,28 @@ class CtrTrainStep:
     def __call__(self, b):
         return self.train_step(b)
 
+    def _dedup_next_early(self):
+        """Split mode 3: the next batch's key dedup on the tower's dW stream,
+        issued before this step's forward (the stream is idle until the dX
+        chain; the dW launch queues behind the dedup)."""
+        nb = self.next_batch
+        if nb is None or not self.engine.can_prefetch_pull():
+            return
+        join_grad_producers()  # the forward's own join below then finds nothing to wait for
+        cur = torch.cuda.current_stream(self.device)
+        st = self.model.tower._side_stream(self.device)
+        st.wait_stream(cur)
+        with torch.cuda.stream(st):
+            self.engine.prefetch_dedup(nb.keys, self.next_slot)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        self._dedup_ev = ev
+
     def train_step(self, b):
         from ..ops.ctr import auc_accumulate
 
+        if self.split_prefetch and self.split_mode == "3":
+            self._dedup_next_early()
         loss, pred = self.model(b)
         loss.backward(self.one)
         if self.next_batch is not None:

@@ -62,8 +62,10 @@ def _union_keys(union):
 
 def _worker(rank, W, port, B, steps, q, mode="plain"):
     try:
-        if mode in ("overlap_dw", "both"):
+        if mode in ("overlap_dw", "both", "both_split3"):
             os.environ["PBX_OVERLAP_DW_IPC"] = "1"
+        if mode == "both_split3":
+            os.environ["PBX_SPLIT_PREFETCH"] = "3"
         import torch.distributed as dist
 
         from paddlebox_amd.ops import reference as ref
@@ -92,7 +94,7 @@ def _worker(rank, W, port, B, steps, q, mode="plain"):
         losses = []
         # step 0 eagerly through the graph's buffers, then the captured replays
         pipe = None
-        if mode in ("pipeline", "both"):
+        if mode in ("pipeline", "both", "both_split3"):
             # sharded pipelined front: each step pulls the next batch (dedup,
             # both exchanges, owner gather, pooling) right after its own push
             assert eng.can_prefetch_pull()
@@ -160,14 +162,14 @@ def _oracle(W, B, steps):
 
 
 @pytest.mark.parametrize("W,mode", [(2, "plain"), (4, "plain"), (2, "overlap_dw"), (2, "pipeline"),
-                                    (4, "pipeline"), (2, "both")])
+                                    (4, "pipeline"), (2, "both"), (2, "both_split3"), (4, "both_split3")])
 def test_nrank_graphed_deepfm_step_matches_union_oracle(W, mode):
     """mode: plain graphed step; overlap_dw = the dW GEMM and its IPC dense
     all-reduce on the side stream (PBX_OVERLAP_DW_IPC); pipeline = the sharded
     pipelined front (SparseEngine prefetch_pull with the exchanges inside)."""
     from paddlebox_amd.ops import reference as ref
 
-    B, steps = 256, 4 if mode in ("pipeline", "both") else 3
+    B, steps = 256, 4 if mode in ("pipeline", "both", "both_split3") else 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -71,7 +71,7 @@ def _train(pipeline: bool, precision: str, K: int = 1):
 @pytest.mark.parametrize("precision,K,split,overlap", [("fp32", 1, "0", "0"), ("bf16", 1, "0", "0"),
                                                        ("fp32", 2, "0", "0"), ("fp32", 1, "2", "0"),
                                                        ("fp32", 2, "1", "0"), ("fp32", 2, "0", "1"),
-                                                       ("bf16", 2, "0", "1")])
+                                                       ("bf16", 2, "0", "1"), ("fp32", 2, "3", "0")])
 def test_pipelined_front_matches_plain_graphed_step(precision, K, split, overlap, monkeypatch):
     # split: the next batch's key dedup on its own stream (PBX_SPLIT_PREFETCH,
     # forked at the dX chain (1) or after the head backward (2)); overlap:
