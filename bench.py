@@ -199,6 +199,8 @@ def main():
     ap.add_argument("--dedup", choices=("on", "off"), default="on",
                     help="FLAGS_enable_pullpush_dedup_keys: off = single-shard step without a key dedup "
                          "(per-occurrence probe + leader-elected push merge)")
+    ap.add_argument("--trace-timed", action="store_true",
+                    help="diagnostics: host time of every replay inside the timed window")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank launch (no GPU, no model); prints ranks_seen")
     args = ap.parse_args()
@@ -431,9 +433,19 @@ def main():
         torch.cuda.synchronize()
         t_start = time.perf_counter()
         loss = None
+        tt = [] if (primary and args.trace_timed) else None
         for i in range(sg):
             loss = run(wg + i)
+            if tt is not None:
+                tt.append(time.perf_counter())
         t_enq = time.perf_counter() - t_start
+        if tt is not None:
+            torch.cuda.synchronize()
+            t_end = time.perf_counter()
+            marks = [t_start] + tt
+            log(rank, "[bench] timed-window host us per replay: "
+                + " ".join(f"{(b - a) * 1e6:.0f}" for a, b in zip(marks, marks[1:]))
+                + f" | drain {(t_end - marks[-1]) * 1e6:.0f}")
         torch.cuda.synchronize()
         if multi:
             dist.barrier()
