@@ -199,6 +199,8 @@ def main():
     ap.add_argument("--dedup", choices=("on", "off"), default="on",
                     help="FLAGS_enable_pullpush_dedup_keys: off = single-shard step without a key dedup "
                          "(per-occurrence probe + leader-elected push merge)")
+    ap.add_argument("--gc-off", type=int, default=1,
+                    help="1: Python's cyclic GC disabled inside the timed window (collected just before)")
     ap.add_argument("--trace-timed", action="store_true",
                     help="diagnostics: host time of every replay inside the timed window")
     ap.add_argument("--dry-run", action="store_true",
@@ -431,6 +433,20 @@ def main():
         if multi:
             dist.barrier()
         torch.cuda.synchronize()
+        import gc
+
+        gcev = []
+        if primary and args.trace_timed:
+            def _gc_cb(phase, info, _ev=gcev):
+                _ev.append((phase, info.get("generation"), time.perf_counter()))
+            gc.callbacks.append(_gc_cb)
+        # Python's cyclic GC off inside the timed window (as timeit does): a
+        # generation-2 pass over the graphs' / model's objects blocks the host
+        # for ~10 ms, longer than the few replays it keeps queued
+        gc.collect()
+        gc_was = gc.isenabled()
+        if args.gc_off:
+            gc.disable()
         t_start = time.perf_counter()
         loss = None
         tt = [] if (primary and args.trace_timed) else None
@@ -439,6 +455,12 @@ def main():
             if tt is not None:
                 tt.append(time.perf_counter())
         t_enq = time.perf_counter() - t_start
+        if gc_was:
+            gc.enable()
+        if gcev:
+            gc.callbacks.pop()
+            log(rank, "[bench] gc in timed window: " + " ".join(
+                f"{ph[0]}{gen}@{(t - t_start) * 1e6:.0f}" for ph, gen, t in gcev if t >= t_start))
         if tt is not None:
             torch.cuda.synchronize()
             t_end = time.perf_counter()
