@@ -387,8 +387,12 @@ def main():
             for a in range(ahead):
                 graphed.load(a % graphed.n, group(a))
 
+            load_marks = []
+
             def run(i):
                 graphed.load((i + ahead) % graphed.n, group(i + ahead))
+                if args.trace_timed:
+                    load_marks.append(time.perf_counter())
                 return graphed.run(i % graphed.n)
         else:
             K = 1
@@ -450,6 +454,8 @@ def main():
         t_start = time.perf_counter()
         loss = None
         tt = [] if (primary and args.trace_timed) else None
+        if tt is not None and graphed is not None:
+            graphed.trace = []
         for i in range(sg):
             loss = run(wg + i)
             if tt is not None:
@@ -468,6 +474,14 @@ def main():
             log(rank, "[bench] timed-window host us per replay: "
                 + " ".join(f"{(b - a) * 1e6:.0f}" for a, b in zip(marks, marks[1:]))
                 + f" | drain {(t_end - marks[-1]) * 1e6:.0f}")
+            if graphed is not None and graphed.trace:
+                tr = graphed.trace[-len(tt):]
+                log(rank, "[bench] timed-window throttle-wait/rest us: "
+                    + " ".join(f"{a * 1e6:.0f}/{b * 1e6:.0f}" for a, b in tr))
+            lm = load_marks[-len(tt):] if graphed is not None else []
+            if lm:
+                log(rank, "[bench] timed-window load us: "
+                    + " ".join(f"{(l - a) * 1e6:.0f}" for a, l in zip(marks, lm)))
         torch.cuda.synchronize()
         if multi:
             dist.barrier()

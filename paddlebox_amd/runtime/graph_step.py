@@ -248,11 +248,17 @@ class GraphedTrainStep:
             fn(self.bufs[i])
         self.ready[i].record(st)
 
+    trace = None  # diagnostics: a list to collect (throttle wait, rest of run) host seconds per replay
+
     def run(self, i: int):
+        import time as _t
+
+        t0 = _t.perf_counter() if self.trace is not None else 0.0
         cur = torch.cuda.current_stream(self.device)
         slot = self.step_no % self.max_inflight
         if self.step_no >= self.max_inflight:
             self.done[slot].synchronize()
+        t1 = _t.perf_counter() if self.trace is not None else 0.0
         cur.wait_event(self.ready[i])
         if self.pipeline is not None:
             n = len(self.graphs)
@@ -279,6 +285,8 @@ class GraphedTrainStep:
         self.free[i].record(cur)
         self.done[slot].record(cur)
         self.step_no += 1
+        if self.trace is not None:
+            self.trace.append((t1 - t0, _t.perf_counter() - t1))
         return out
 
     def warm(self, host_batches: Sequence[Any], replays: int = 32):
