@@ -199,6 +199,9 @@ def main():
     ap.add_argument("--dedup", choices=("on", "off"), default="on",
                     help="FLAGS_enable_pullpush_dedup_keys: off = single-shard step without a key dedup "
                          "(per-occurrence probe + leader-elected push merge)")
+    ap.add_argument("--inputs", choices=("host", "hbm"), default="host",
+                    help="hbm: the pass's packed batches are kept in HBM and each step copies its batch into the "
+                         "graph inputs device-to-device (host: a pinned host-to-device DMA per step)")
     ap.add_argument("--gc-off", type=int, default=1,
                     help="1: Python's cyclic GC disabled inside the timed window (collected just before)")
     ap.add_argument("--trace-timed", action="store_true",
@@ -366,6 +369,8 @@ def main():
                                            steps_per_graph=K if pre is None else 1,
                                            n_buffers=3 if pipe is not None else 2, pipeline=pipe,
                                            join_each_step=not step.adam_overlap)
+                if args.inputs == "hbm":
+                    graphed.stage_inputs(host_batches)
                 graphed.warm(host_batches, replays=args.graph_warm)
                 log(rank, f"[bench] training step captured into HIP graphs ({args.graph_warm} warm replays)")
             except Exception as e:  # pragma: no cover - depends on runtime
