@@ -199,9 +199,11 @@ def main():
     ap.add_argument("--dedup", choices=("on", "off"), default="on",
                     help="FLAGS_enable_pullpush_dedup_keys: off = single-shard step without a key dedup "
                          "(per-occurrence probe + leader-elected push merge)")
-    ap.add_argument("--inputs", choices=("host", "hbm"), default="host",
-                    help="hbm: the pass's packed batches are kept in HBM and each step copies its batch into the "
-                         "graph inputs device-to-device (host: a pinned host-to-device DMA per step)")
+    ap.add_argument("--inputs", choices=("host", "hbm"), default="hbm",
+                    help="hbm (default): the pass's packed batches are kept in HBM and each step copies its batch "
+                         "into the graph inputs device-to-device; host: a pinned host-to-device DMA per step, whose "
+                         "hipMemcpyAsync blocks the launching thread 7-19 ms once early in a fresh timing window "
+                         "(20-step windows measured 0.69-1.10 vs 0.40 ms/step, profiles/r4_input_stall.txt)")
     ap.add_argument("--gc-off", type=int, default=1,
                     help="1: Python's cyclic GC disabled inside the timed window (collected just before)")
     ap.add_argument("--trace-timed", action="store_true",
@@ -606,6 +608,7 @@ def main():
                 "launcher": launcher,
                 "dense_allreduce": ("ipc" if ipc is not None else "rccl") if multi else "none",
                 "sparse_exchange": engine.exchange_mode,
+                "inputs": ("HBM-resident synthetic batches, device-to-device copy into the captured graph inputs every step" if args.inputs == "hbm" else "pinned host batches, host-to-device DMA every step"),
                 "same_gpu_rehearsal": bool(args.same_gpu),
                 "pipelined_pull": res["prefetch"],
                 "pipelined_front": res.get("pipeline", False),
