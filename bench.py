@@ -107,7 +107,7 @@ def dry_run(args, world, rank):
 
 
 
-def graph_steps_for(steps: int, warmup: int, requested: int = 0) -> int:
+def graph_steps_for(steps: int, warmup: int, requested: int = 0, world: int = 1) -> int:
     """Steps per captured graph: every timed and warmup step still runs in
     full; only the graph-launch boundary (and the wait on the batch copy) is
     paid once per K steps instead of once per step.  requested -1 (default):
@@ -115,7 +115,11 @@ def graph_steps_for(steps: int, warmup: int, requested: int = 0) -> int:
     is rounded up to whole graphs; K = 4 vs 2: 0.362-0.364 vs ~0.368 ms/step
     over 200 steps, profiles/r4_input_stall.txt)."""
     if requested < 0:
-        return 4 if steps % 4 == 0 else (2 if steps % 2 == 0 else 1)
+        # multi-rank: 2 (the same-GPU 2-rank rehearsal ran 1.43 ms/step at
+        # K = 2 and 2.51 at K = 4; K = 2 is the validated multi-rank form)
+        if world == 1 and steps % 4 == 0:
+            return 4
+        return 2 if steps % 2 == 0 else 1
     if requested > 0:
         if steps % requested:
             raise SystemExit(f"--graph-steps {requested} must divide --steps {steps}")
@@ -281,7 +285,7 @@ def main():
     engine = SparseEngine(cfg, max_keys=B * S, device=device, capacity=synth.total_features,
                           slot_ids=[float(s + 1) for s in range(S)], auto_insert=args.no_prefill,
                           exchange_capacity=xcap, exchange=args.sparse_exchange, dedup=args.dedup == "on",
-                          pull_ring=(3 * graph_steps_for(args.steps, args.warmup, args.graph_steps)
+                          pull_ring=(3 * graph_steps_for(args.steps, args.warmup, args.graph_steps, world)
                                      if args.pipeline != "off" else 2))
 
     t0 = time.time()
@@ -358,7 +362,7 @@ def main():
         # the headline takes K steps per graph; the same-run secondaries keep
         # one (a bf16 K = 2 run after the pipelined fp32 one faulted on the
         # box at 200 steps -- under investigation; K = 1 is the validated path)
-        K = graph_steps_for(args.steps, args.warmup, args.graph_steps) if primary else 1
+        K = graph_steps_for(args.steps, args.warmup, args.graph_steps, world) if primary else 1
         graphed = None
         if args.graph:
             try:
