@@ -454,6 +454,8 @@ def main():
         if multi:
             dist.barrier()
         torch.cuda.synchronize()
+        if graphed is not None:
+            graphed.drained()
         import gc
 
         gcev = []

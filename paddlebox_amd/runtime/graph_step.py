@@ -273,6 +273,11 @@ class GraphedTrainStep:
 
     trace = None  # diagnostics: a list to collect (throttle wait, rest of run) host seconds per replay
 
+    def drained(self):
+        """The caller synchronised the device: every replay has finished, so
+        the next max_inflight replays need no host-side throttle wait."""
+        self.step_no = 0
+
     def run(self, i: int):
         import time as _t
 
