@@ -44,6 +44,12 @@ class GpuTable {
     const RowLayout l = make_row_layout(dim);
     // codec state (feature_ops.hip) follows the standard tail
     stride_ = extra > 0 ? ((l.mf_size + 1 + extra) + 3) & ~3 : l.stride;
+    // a plain row's first padding word (after the layout's last field) holds
+    // the table dedup's per-row occurrence counter -- zero between dedups, so
+    // invisible to every reader -- on the row's own page instead of a
+    // separate table-sized array (PBX_TD_INROW=0: the separate array)
+    const char* inrow = getenv("PBX_TD_INROW");
+    pad_col_ = (extra == 0 && stride_ > l.mf_size + 1 && !(inrow && inrow[0] == '0')) ? l.mf_size + 1 : -1;
     nb_ = (uint64_t)((capacity + kBucketSlots - 1) / kBucketSlots);
     if (nb_ < 1) nb_ = 1;
     stash_cap_ = stash_cap;
@@ -202,14 +208,16 @@ class GpuTable {
   }
   // per-row scratch of the table dedup (launch_table_dedup): occurrence
   // counts (kept all-zero between batches) and the batch's unique id of a row
-  std::pair<int32_t*, int32_t*> dedup_rows() {
-    if (!cnt_row_.defined()) {
+  // (cnt base, cnt stride in int32 words, uid_row)
+  std::tuple<int32_t*, int64_t, int32_t*> dedup_rows() {
+    if (!uid_row_.defined()) {
       PBX_CHECK(values_.size(0) < (int64_t)INT32_MAX, "table dedup: table rows must fit int32");
       auto opt4 = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device_);
-      cnt_row_ = torch::zeros({values_.size(0)}, opt4);
+      if (pad_col_ < 0) cnt_row_ = torch::zeros({values_.size(0)}, opt4);
       uid_row_ = torch::empty({values_.size(0)}, opt4);
     }
-    return {ptr<int32_t>(cnt_row_), ptr<int32_t>(uid_row_)};
+    if (pad_col_ >= 0) return {reinterpret_cast<int32_t*>(ptr<float>(values_)) + pad_col_, (int64_t)stride_, ptr<int32_t>(uid_row_)};
+    return {ptr<int32_t>(cnt_row_), (int64_t)1, ptr<int32_t>(uid_row_)};
   }
   Tensor& lead_buf(int64_t n) {
     if (!lead_.defined() || lead_.numel() < n) lead_ = torch::empty({n}, owner_lock().options());
@@ -426,6 +434,7 @@ class GpuTable {
   Tensor keys_, fill_, values_, stash_keys_, scratch_;
   Tensor lock_, lead_;  // owner_push: per-row leader word (-1 = free), per-record leader
   Tensor cnt_row_, uid_row_;  // table dedup scratch (dedup_rows)
+  int pad_col_ = -1;          // in-row dedup counter column (-1: cnt_row_)
 };
 
 // --------------------------------------------------------------- dedup
@@ -524,9 +533,9 @@ struct DedupWorkspace {
     PBX_CHECK(keys.scalar_type() == torch::kInt64 && keys.is_contiguous(), "run_table: keys must be int64");
     table_rows_occ();
     auto rc = t.dedup_rows();
-    launch_table_dedup(t.view(), ptr<int64_t>(keys), n, ptr<int64_t>(rows_occ), ptr<int32_t>(rank), rc.first,
-                       rc.second, ptr<int64_t>(rows_u), ptr<int32_t>(uid), ptr<int32_t>(perm), ptr<int32_t>(seg),
-                       ptr<int32_t>(u_count), ptr<int32_t>(u_acc), rows_given, cur_stream());
+    launch_table_dedup(t.view(), ptr<int64_t>(keys), n, ptr<int64_t>(rows_occ), ptr<int32_t>(rank), std::get<0>(rc),
+                       std::get<1>(rc), std::get<2>(rc), ptr<int64_t>(rows_u), ptr<int32_t>(uid), ptr<int32_t>(perm),
+                       ptr<int32_t>(seg), ptr<int32_t>(u_count), ptr<int32_t>(u_acc), rows_given, cur_stream());
     last_n = n;
     if (!rows_given) rows_occ_dirty = true;  // rows_given: k_table_scatter hands rows_occ back all -1
   }

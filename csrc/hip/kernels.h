@@ -338,8 +338,9 @@ SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, con
 // cnt_row / uid_row: int32 per table row; cnt_row all-zero between calls
 // (re-zeroed by the call), uid_row needs no reset.
 void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows_occ, int32_t* rank,
-                        int32_t* cnt_row, int32_t* uid_row, int64_t* rows_u, int32_t* uid, int32_t* perm, int32_t* seg,
-                        int32_t* u_count, int32_t* acc, bool rows_given, hipStream_t s);
+                        int32_t* cnt_row, int64_t cnt_rs, int32_t* uid_row, int64_t* rows_u, int32_t* uid,
+                        int32_t* perm, int32_t* seg, int32_t* u_count, int32_t* acc, bool rows_given,
+                        hipStream_t s);
 // Probe raw feasigns (mixed in the kernel, -1 = padding -> row -1).
 void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows, hipStream_t s);
 bool launch_push_merge_send(const PushMergeArgs& a, int dim, float* send, int send_stride, const int64_t* send_index,

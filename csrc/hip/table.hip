@@ -120,7 +120,8 @@ __device__ __forceinline__ int64_t probe_thread(const TableDev& t, uint64_t key)
 template <bool PROBE, int kTdItems, int kTdLds = 512 * kTdItems>  // LDS hash at load factor <= 1/2
 __global__ __launch_bounds__(256) void k_table_rank(TableDev t, const uint64_t* __restrict__ keys, int64_t n,
                                                     int64_t* __restrict__ rows_occ, int32_t* __restrict__ rank,
-                                                    int32_t* __restrict__ cnt_row, int32_t* __restrict__ uid_row,
+                                                    int32_t* __restrict__ cnt_row, int64_t cnt_rs,
+                                                    int32_t* __restrict__ uid_row,
                                                     int64_t* __restrict__ rows_u, int32_t* __restrict__ u_count) {
   __shared__ int32_t lkey[kTdLds];
   __shared__ int32_t lcnt[kTdLds];
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(256) void k_table_rank(TableDev t, const uint64_t* 
     const int32_t r = lkey[e];
     lnew[e] = -1;
     if (r < 0) continue;
-    const int32_t base = atomicAdd(&cnt_row[r], lcnt[e]);
+    const int32_t base = atomicAdd(&cnt_row[(int64_t)r * cnt_rs], lcnt[e]);
     lcnt[e] = base;  // the block's base rank within row r
     if (base == 0) lnew[e] = atomicAdd(&nnew_blk, 1);
   }
@@ -208,7 +209,8 @@ __global__ __launch_bounds__(256) void k_table_rank(TableDev t, const uint64_t* 
 // the row counts are re-zeroed for the next batch
 template <int kTdSegItems>
 __global__ __launch_bounds__(256) void k_table_seg(const int64_t* __restrict__ rows_u, int32_t* __restrict__ cnt_row,
-                                                   int32_t* __restrict__ u_count, int32_t* __restrict__ seg) {
+                                                   int64_t cnt_rs, int32_t* __restrict__ u_count,
+                                                   int32_t* __restrict__ seg) {
   __shared__ int32_t wsum[4];
   __shared__ int32_t base;
   const int64_t U = u_count[0];
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(256) void k_table_seg(const int64_t* __restrict__ r
   for (int it = 0; it < kTdSegItems; ++it) {
     c[it] = 0;
     if (u0 + it < U) {
-      const int64_t r = rows_u[u0 + it];
+      const int64_t r = rows_u[u0 + it] * cnt_rs;
       c[it] = cnt_row[r];
       cnt_row[r] = 0;
     }
@@ -524,8 +526,9 @@ void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t
 }
 
 void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows_occ, int32_t* rank,
-                        int32_t* cnt_row, int32_t* uid_row, int64_t* rows_u, int32_t* uid, int32_t* perm, int32_t* seg,
-                        int32_t* u_count, int32_t* acc, bool rows_given, hipStream_t s) {
+                        int32_t* cnt_row, int64_t cnt_rs, int32_t* uid_row, int64_t* rows_u, int32_t* uid,
+                        int32_t* perm, int32_t* seg, int32_t* u_count, int32_t* acc, bool rows_given,
+                        hipStream_t s) {
   if (n <= 0) {  // no scatter to publish the counters: [U, n_valid, -, cursor] = 0
     launch_fill32(reinterpret_cast<uint32_t*>(u_count), 0u, 4, s);
     return;
@@ -540,7 +543,7 @@ void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64
   }();
 #define PBX_TD_LAUNCH(PR, IT)                                                                                  \
   hipLaunchKernelGGL((k_table_rank<PR, IT>), dim3(blocks_for(n, 256 * IT)), dim3(256), 0, s, t,              \
-                     reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, uid_row, rows_u, acc)
+                     reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, cnt_rs, uid_row, rows_u, acc)
   if (rows_given) {
     if (items == 4) PBX_TD_LAUNCH(false, 4);
     else if (items == 2) PBX_TD_LAUNCH(false, 2);
@@ -559,11 +562,11 @@ void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64
     return (v == 2 || v == 4) ? v : 1;
   }();
   if (seg_items == 1)
-    hipLaunchKernelGGL(k_table_seg<1>, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_u, cnt_row, acc, seg);
+    hipLaunchKernelGGL(k_table_seg<1>, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_u, cnt_row, cnt_rs, acc, seg);
   else if (seg_items == 2)
-    hipLaunchKernelGGL(k_table_seg<2>, dim3(blocks_for(n, 512)), dim3(256), 0, s, rows_u, cnt_row, acc, seg);
+    hipLaunchKernelGGL(k_table_seg<2>, dim3(blocks_for(n, 512)), dim3(256), 0, s, rows_u, cnt_row, cnt_rs, acc, seg);
   else
-    hipLaunchKernelGGL(k_table_seg<4>, dim3(blocks_for(n, 1024)), dim3(256), 0, s, rows_u, cnt_row, acc, seg);
+    hipLaunchKernelGGL(k_table_seg<4>, dim3(blocks_for(n, 1024)), dim3(256), 0, s, rows_u, cnt_row, cnt_rs, acc, seg);
   hipLaunchKernelGGL(k_table_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_occ, rank, uid_row, seg, n, uid,
                      perm, rows_given ? 1 : 0, acc, u_count);
 }
