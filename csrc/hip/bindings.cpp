@@ -44,12 +44,16 @@ class GpuTable {
     const RowLayout l = make_row_layout(dim);
     // codec state (feature_ops.hip) follows the standard tail
     stride_ = extra > 0 ? ((l.mf_size + 1 + extra) + 3) & ~3 : l.stride;
-    // a plain row's first padding word (after the layout's last field) holds
-    // the table dedup's per-row occurrence counter -- zero between dedups, so
-    // invisible to every reader -- on the row's own page instead of a
-    // separate table-sized array (PBX_TD_INROW=0: the separate array)
+    // PBX_TD_INROW=1: a plain row's first padding word (after the layout's
+    // last field) holds the table dedup's per-row occurrence counter -- zero
+    // between dedups -- on the row's own page instead of a separate
+    // table-sized array.  Opt-in: a dedup running CONCURRENTLY with a push
+    // (PBX_SPLIT_PREFETCH modes) races the push's whole-row float4 stores and
+    // faulted; never combined with them.
     const char* inrow = getenv("PBX_TD_INROW");
-    pad_col_ = (extra == 0 && stride_ > l.mf_size + 1 && !(inrow && inrow[0] == '0')) ? l.mf_size + 1 : -1;
+    const char* split = getenv("PBX_SPLIT_PREFETCH");
+    const bool split_on = split && split[0] != '\0' && split[0] != '0';
+    pad_col_ = (extra == 0 && stride_ > l.mf_size + 1 && inrow && inrow[0] == '1' && !split_on) ? l.mf_size + 1 : -1;
     nb_ = (uint64_t)((capacity + kBucketSlots - 1) / kBucketSlots);
     if (nb_ < 1) nb_ = 1;
     stash_cap_ = stash_cap;
