@@ -530,16 +530,23 @@ struct DedupWorkspace {
     rows_occ.fill_(-1);
     rows_occ_dirty = false;
   }
-  void run_table(const Tensor& keys, GpuTable& t, bool rows_given) {
+  // defer_scatter: the per-occurrence scatter (uid, perm) and the counter
+  // publish are left to the seqpool launch that follows (seqpool_cvm_fwd
+  // scatter_ws = this workspace)
+  const int32_t* sc_uid_row = nullptr;
+  void run_table(const Tensor& keys, GpuTable& t, bool rows_given, bool defer_scatter = false) {
     check_cuda(keys, "keys");
     const int64_t n = keys.numel();
     PBX_CHECK(n <= cap, "dedup: more keys than workspace capacity");
     PBX_CHECK(keys.scalar_type() == torch::kInt64 && keys.is_contiguous(), "run_table: keys must be int64");
     table_rows_occ();
     auto rc = t.dedup_rows();
+    PBX_CHECK(!(defer_scatter && rows_given), "run_table: a deferred scatter needs the probing dedup");
     launch_table_dedup(t.view(), ptr<int64_t>(keys), n, ptr<int64_t>(rows_occ), ptr<int32_t>(rank), std::get<0>(rc),
                        std::get<1>(rc), std::get<2>(rc), ptr<int64_t>(rows_u), ptr<int32_t>(uid), ptr<int32_t>(perm),
-                       ptr<int32_t>(seg), ptr<int32_t>(u_count), ptr<int32_t>(u_acc), rows_given, cur_stream());
+                       ptr<int32_t>(seg), ptr<int32_t>(u_count), ptr<int32_t>(u_acc), rows_given, cur_stream(),
+                       !(defer_scatter && n > 0));
+    sc_uid_row = (defer_scatter && n > 0) ? std::get<2>(rc) : nullptr;
     last_n = n;
     if (!rows_given) rows_occ_dirty = true;  // rows_given: k_table_scatter hands rows_occ back all -1
   }
@@ -560,7 +567,8 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
                             float embed_threshold, int embed_thres_size, const c10::optional<Tensor>& dense,
                             int dense_col, const c10::optional<Tensor>& occ_slot,
                             const c10::optional<Tensor>& occ_ins, const c10::optional<Tensor>& probe_keys,
-                            GpuTable* probe_table, const c10::optional<Tensor>& rows_out) {
+                            GpuTable* probe_table, const c10::optional<Tensor>& rows_out,
+                            DedupWorkspace* scatter_ws) {
   check_cuda(src, "src");
   check_cuda(lod, "lod");
   check_cuda(out, "out");
@@ -595,6 +603,21 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
   a.embed_threshold = embed_threshold;
   a.embed_thres_size = embed_thres_size;
   PBX_CHECK(col_offset + (int64_t)S * seqpool_cvm_out_width(a) <= out.size(1), "out too narrow");
+  if (scatter_ws != nullptr && scatter_ws->sc_uid_row != nullptr) {
+    // the deferred table-dedup scatter of scatter_ws rides on this launch:
+    // occurrence k's row must be read directly (src_index = rows_occ, no uid)
+    PBX_CHECK(!(uid.has_value() && uid->defined()) && a.src_index == scatter_ws->rows_occ.data_ptr<int64_t>(),
+              "fused scatter: src_index must be the workspace's rows_occ and uid None");
+    PBX_CHECK(E == 11 || E == 12 || E == 19 || E == 35, "fused scatter: needs a specialised seqpool width");
+    a.sc_uid_row = scatter_ws->sc_uid_row;
+    a.sc_seg = ptr<int32_t>(scatter_ws->seg);
+    a.sc_rank = ptr<int32_t>(scatter_ws->rank);
+    a.sc_uid = ptr<int32_t>(scatter_ws->uid);
+    a.sc_perm = ptr<int32_t>(scatter_ws->perm);
+    a.sc_acc = ptr<int32_t>(scatter_ws->u_acc);
+    a.sc_u_count = ptr<int32_t>(scatter_ws->u_count);
+    scatter_ws->sc_uid_row = nullptr;  // one pooling per dedup
+  }
   if (occ_slot.has_value() && occ_slot->defined()) {  // occurrence map written by the same launch
     PBX_CHECK(occ_ins.has_value() && occ_ins->defined(), "occ_ins required with occ_slot");
     PBX_CHECK(occ_slot->numel() >= L && occ_ins->numel() >= L, "occ buffers too small");
@@ -1297,7 +1320,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<DedupWorkspace>(m, "DedupWorkspace")
       .def(py::init<int64_t, int, bool>(), py::arg("cap"), py::arg("device"), py::arg("hash") = true)
       .def("run", &DedupWorkspace::run, py::arg("keys"), py::arg("mixed") = false, py::arg("zero") = py::none())
-      .def("run_table", &DedupWorkspace::run_table, py::arg("keys"), py::arg("table"), py::arg("rows_given") = false)
+      .def("run_table", &DedupWorkspace::run_table, py::arg("keys"), py::arg("table"), py::arg("rows_given") = false,
+           py::arg("defer_scatter") = false)
       .def("table_rows_occ", &DedupWorkspace::table_rows_occ)
       .def("clean_rows_occ", &DedupWorkspace::clean_rows_occ)
       .def_readonly("rows_occ_dirty", &DedupWorkspace::rows_occ_dirty)
@@ -1330,7 +1354,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("embed_threshold_filter"), py::arg("embed_threshold"), py::arg("embed_thres_size"),
         py::arg("dense") = py::none(), py::arg("dense_col") = 0, py::arg("occ_slot") = py::none(),
         py::arg("occ_ins") = py::none(), py::arg("probe_keys") = py::none(),
-        py::arg("probe_table") = static_cast<GpuTable*>(nullptr), py::arg("rows_out") = py::none());
+        py::arg("probe_table") = static_cast<GpuTable*>(nullptr), py::arg("rows_out") = py::none(),
+        py::arg("scatter_ws") = static_cast<DedupWorkspace*>(nullptr));
   m.def("push_merge", &push_merge, py::arg("dout"), py::arg("col_offset"), py::arg("cvm"), py::arg("cvm_offset"),
         py::arg("use_cvm"), py::arg("clk_filter"), py::arg("E"), py::arg("perm"), py::arg("uid"), py::arg("occ_slot"),
         py::arg("occ_ins"), py::arg("slot_ids"), py::arg("n_valid"), py::arg("push"), py::arg("push_index"),

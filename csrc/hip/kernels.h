@@ -155,6 +155,17 @@ struct SeqpoolCvmArgs {
   const uint64_t* probe_keys = nullptr;
   TableDev probe_t;
   int64_t* rows_out = nullptr;
+  // optional fused table-dedup scatter (launch_table_dedup with
+  // do_scatter = false before it): for every occurrence k with a row,
+  // uid[k] = uid_row[row], perm[seg[uid] + rank[k]] = k; threads 0..3
+  // publish the dedup counters (u_count = acc, acc = 0)
+  const int32_t* sc_uid_row = nullptr;
+  const int32_t* sc_seg = nullptr;
+  const int32_t* sc_rank = nullptr;
+  int32_t* sc_uid = nullptr;
+  int32_t* sc_perm = nullptr;
+  int32_t* sc_acc = nullptr;
+  int32_t* sc_u_count = nullptr;
 };
 int seqpool_cvm_out_width(const SeqpoolCvmArgs& a);
 void launch_seqpool_cvm_fwd(const SeqpoolCvmArgs& a, hipStream_t s);
@@ -340,7 +351,7 @@ SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, con
 void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows_occ, int32_t* rank,
                         int32_t* cnt_row, int64_t cnt_rs, int32_t* uid_row, int64_t* rows_u, int32_t* uid,
                         int32_t* perm, int32_t* seg, int32_t* u_count, int32_t* acc, bool rows_given,
-                        hipStream_t s);
+                        hipStream_t s, bool do_scatter = true);
 // Probe raw feasigns (mixed in the kernel, -1 = padding -> row -1).
 void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows, hipStream_t s);
 bool launch_push_merge_send(const PushMergeArgs& a, int dim, float* send, int send_stride, const int64_t* send_index,

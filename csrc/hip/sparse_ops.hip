@@ -115,6 +115,10 @@ __device__ __forceinline__ int64_t seqpool_record(const SeqpoolCvmArgs& a, int64
 template <int E>
 __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a.sc_perm && t < 4) {  // fused dedup scatter: publish the counters, leave acc zero
+    a.sc_u_count[t] = a.sc_acc[t];
+    a.sc_acc[t] = 0;
+  }
   if (t >= (int64_t)a.S * a.B) return;
   // instance-major so a wave writes contiguous output rows
   const int b = (int)(t / a.S), s = (int)(t % a.S);
@@ -133,6 +137,15 @@ __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
       a.occ_ins[k] = b;
     }
     const int64_t ri = seqpool_record(a, k);
+    if (a.sc_perm) {  // fused table-dedup scatter (k_table_scatter's per-occurrence work)
+      if (ri >= 0) {
+        const int32_t u = a.sc_uid_row[ri];
+        a.sc_uid[k] = u;
+        a.sc_perm[a.sc_seg[u] + a.sc_rank[k]] = (int32_t)k;
+      } else {
+        a.sc_uid[k] = -1;
+      }
+    }
     if (ri < 0) continue;
     float v[E];
     load_row<E>(a.src + ri * (int64_t)a.src_stride, v);

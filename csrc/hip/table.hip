@@ -528,7 +528,7 @@ void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t
 void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows_occ, int32_t* rank,
                         int32_t* cnt_row, int64_t cnt_rs, int32_t* uid_row, int64_t* rows_u, int32_t* uid,
                         int32_t* perm, int32_t* seg, int32_t* u_count, int32_t* acc, bool rows_given,
-                        hipStream_t s) {
+                        hipStream_t s, bool do_scatter) {
   if (n <= 0) {  // no scatter to publish the counters: [U, n_valid, -, cursor] = 0
     launch_fill32(reinterpret_cast<uint32_t*>(u_count), 0u, 4, s);
     return;
@@ -567,6 +567,7 @@ void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64
     hipLaunchKernelGGL(k_table_seg<2>, dim3(blocks_for(n, 512)), dim3(256), 0, s, rows_u, cnt_row, cnt_rs, acc, seg);
   else
     hipLaunchKernelGGL(k_table_seg<4>, dim3(blocks_for(n, 1024)), dim3(256), 0, s, rows_u, cnt_row, cnt_rs, acc, seg);
+  if (!do_scatter) return;  // the caller's seqpool launch scatters (SeqpoolCvmArgs.sc_*)
   hipLaunchKernelGGL(k_table_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_occ, rank, uid_row, seg, n, uid,
                      perm, rows_given ? 1 : 0, acc, u_count);
 }

@@ -643,9 +643,15 @@ class SparseEngine:
             # pack, both exchanges and the pooling follow in prefetch_pool
             self._hash_dedup(sl, keys.reshape(-1))
             return True
-        sl.ws.run_table(keys, self.table.t)
+        sl.ws.run_table(keys, self.table.t, False, self._fuse_scatter())
         sl.rows = sl.ws.rows_u
         return True
+
+    def _fuse_scatter(self) -> bool:
+        """Leave the table dedup's scatter to the prefetched pooling launch
+        (PBX_FUSED_SCATTER=1): one launch less on the step's sparse chain."""
+        return (self.seqpool_rows_occ and self.codec is None and self.E in (11, 12, 19, 35)
+                and os.environ.get("PBX_FUSED_SCATTER", "0") == "1")
 
     def prefetch_pool(self, keys: torch.Tensor, lod: torch.Tensor, B: int, S: int, sp: "SeqpoolParams",
                       dense: Optional[torch.Tensor] = None, slot: int = 0) -> bool:
@@ -676,7 +682,7 @@ class SparseEngine:
                                   sp.clk_coeff, sp.threshold, sp.quant_ratio, sp.embed_threshold_filter,
                                   sp.embed_threshold, sp.embed_thres_size if not sp.use_cvm else 0,
                                   dense.contiguous().float() if dense is not None else None, S * Eo,
-                                  occ_slot=sl.occ_slot, occ_ins=sl.occ_ins)
+                                  occ_slot=sl.occ_slot, occ_ins=sl.occ_ins, scatter_ws=ws)
         self._prepared[keys.data_ptr()] = (sl, L)
         self._prepared_out[keys.data_ptr()] = sl.pre_out
         return True

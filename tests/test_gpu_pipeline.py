@@ -68,11 +68,13 @@ def _train(pipeline: bool, precision: str, K: int = 1):
     return step.arena.flat.cpu(), losses, hk[o].cpu(), v[o].cpu()
 
 
-@pytest.mark.parametrize("precision,K,split,overlap", [("fp32", 1, "0", "0"), ("bf16", 1, "0", "0"),
-                                                       ("fp32", 2, "0", "0"), ("fp32", 1, "2", "0"),
-                                                       ("fp32", 2, "1", "0"), ("fp32", 2, "0", "1"),
-                                                       ("bf16", 2, "0", "1"), ("fp32", 2, "3", "0")])
-def test_pipelined_front_matches_plain_graphed_step(precision, K, split, overlap, monkeypatch):
+@pytest.mark.parametrize("precision,K,split,overlap,fs", [("fp32", 1, "0", "0", "0"), ("bf16", 1, "0", "0", "0"),
+                                                          ("fp32", 2, "0", "0", "0"), ("fp32", 1, "2", "0", "0"),
+                                                          ("fp32", 2, "1", "0", "0"), ("fp32", 2, "0", "1", "0"),
+                                                          ("bf16", 2, "0", "1", "0"), ("fp32", 2, "3", "0", "0"),
+                                                          ("fp32", 1, "0", "0", "1"), ("fp32", 2, "0", "0", "1"),
+                                                          ("fp32", 2, "2", "0", "1")])
+def test_pipelined_front_matches_plain_graphed_step(precision, K, split, overlap, fs, monkeypatch):
     # split: the next batch's key dedup on its own stream (PBX_SPLIT_PREFETCH,
     # forked at the dX chain (1) or after the head backward (2)); overlap:
     # Adam on the dW side stream, the next head not waiting for it
@@ -80,6 +82,7 @@ def test_pipelined_front_matches_plain_graphed_step(precision, K, split, overlap
     f0, l0, k0, v0 = _train(False, precision, K)
     monkeypatch.setenv("PBX_SPLIT_PREFETCH", split)
     monkeypatch.setenv("PBX_ADAM_OVERLAP", overlap)
+    monkeypatch.setenv("PBX_FUSED_SCATTER", fs)  # the dedup scatter inside the prefetched pooling launch
     f1, l1, k1, v1 = _train(True, precision, K)
     # the dW split-K atomics sum in any order: fp32-rounding-level differences
     rt, at = (1e-6, 1e-7) if precision == "fp32" else (1e-4, 1e-5)
