@@ -530,6 +530,26 @@ __global__ __launch_bounds__(256) void k_adam_fused(float* __restrict__ p, float
   const int64_t stride4 = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i4 * 4 < n; i4 += stride4) {
     const int64_t e0 = i4 * 4;
+    // fp32 tower re-pack destinations of this group, looked up BEFORE the
+    // update (their position-table loads then overlap the p/g/m/v loads
+    // instead of starting after the arithmetic); -1: not a packed weight
+    int64_t dwp[4] = {-1, -1, -1, -1}, dwt[4] = {-1, -1, -1, -1};
+    int rsel = -1;
+    for (int r = 0; r < x.n_pack; ++r) {
+      const int64_t off = x.pack_off[r];
+      const int64_t cnt = (int64_t)x.pack_N[r] * x.pack_K[r];
+      if (e0 + 3 < off || e0 >= off + cnt || !x.pack_wp32[r] || !x.pack_pos32[r]) continue;
+      rsel = r;
+      const int K = x.pack_K[r];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t i = e0 + k - off;
+        if (i < 0 || i >= cnt || e0 + k >= n) continue;
+        const int nn = (int)((uint32_t)i / (uint32_t)K), kk = (int)((uint32_t)i - (uint32_t)nn * (uint32_t)K);
+        dwp[k] = tower_wp32_index_pos(x.pack_pos32[r], nn, kk, x.pack_Kp[r]);
+        dwt[k] = tower_wtp32_index_pos(x.pack_posT32[r], nn, kk, x.pack_Np[r]);
+      }
+    }
     float pa[4], ga[4], ma[4], va[4];
     const bool full = e0 + 4 <= n;
     if (full) {
@@ -570,8 +590,17 @@ __global__ __launch_bounds__(256) void k_adam_fused(float* __restrict__ p, float
         if (clear_grad) g[e0 + k] = 0.f;
       }
     }
-    // bf16 tower copies of weight regions
+    if (rsel >= 0) {  // fp32 tower copies (destinations resolved above)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (dwp[k] >= 0) {
+          x.pack_wp32[rsel][dwp[k]] = pa[k];
+          x.pack_wtp32[rsel][dwt[k]] = pa[k];
+        }
+    }
+    // bf16 tower copies of weight regions (and fp32 ones without position tables)
     for (int r = 0; r < x.n_pack; ++r) {
+      if (r == rsel) continue;
       const int64_t off = x.pack_off[r];
       const int K = x.pack_K[r];
       const int64_t cnt = (int64_t)x.pack_N[r] * K;
