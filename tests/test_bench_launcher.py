@@ -7,6 +7,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -47,3 +49,36 @@ def test_refuses_more_gpus_than_visible():
     p = _run(["--gpus", "64", "--steps", "1", "--warmup", "0"])
     assert p.returncode != 0
     assert "refusing" in p.stderr
+
+
+def test_graph_steps_default_and_explicit():
+    """Steps per captured graph: 4 on one rank / 2 multi-rank when they divide
+    the timed steps, an explicit K must divide them."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("pbx_bench", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert b.graph_steps_for(20, 5, -1) == 4
+    assert b.graph_steps_for(200, 50, -1, world=1) == 4
+    assert b.graph_steps_for(20, 5, -1, world=8) == 2
+    assert b.graph_steps_for(30, 5, -1) == 2
+    assert b.graph_steps_for(21, 5, -1) == 1
+    assert b.graph_steps_for(48, 20, 3) == 3
+    with pytest.raises(SystemExit):
+        b.graph_steps_for(20, 5, 3)
+
+
+def test_push_run_scratch_forms(monkeypatch):
+    """The fused push's straddling-run scratch: int32 per-wave owners (two
+    launches, default) or int64 per-unique arrival counters (PBX_PUSH_FINISH=0)."""
+    import torch
+
+    from paddlebox_amd.ps.sparse_engine import _push_run_scratch
+
+    monkeypatch.delenv("PBX_PUSH_FINISH", raising=False)
+    t = _push_run_scratch(1000, "cpu")
+    assert t.dtype == torch.int32 and t.numel() == (1000 + 63) // 64 + 1
+    monkeypatch.setenv("PBX_PUSH_FINISH", "0")
+    t = _push_run_scratch(1000, "cpu")
+    assert t.dtype == torch.int64 and t.numel() == 1000 and int(t.abs().sum()) == 0
