@@ -448,6 +448,9 @@ def main():
         # warmup in whole graphs: W rounded up to a multiple of K (at most K-1
         # extra untimed steps); the timed steps are exactly K * sg = --steps
         wg, sg = -(-args.warmup // K), args.steps // K
+        import gc
+
+        gc.collect()
         for i in range(wg):
             run(i)
         torch.cuda.synchronize()
@@ -465,8 +468,9 @@ def main():
             gc.callbacks.append(_gc_cb)
         # Python's cyclic GC off inside the timed window (as timeit does): a
         # generation-2 pass over the graphs' / model's objects blocks the host
-        # for ~10 ms, longer than the few replays it keeps queued
-        gc.collect()
+        # for ~10 ms, longer than the few replays it keeps queued.  The
+        # collection itself runs before the warmup replays (a collection right
+        # before the window idles the GPU for tens of ms first)
         gc_was = gc.isenabled()
         if args.gc_off:
             gc.disable()
