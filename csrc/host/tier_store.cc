@@ -192,14 +192,19 @@ void HostTier::probe(const uint64_t* h, int64_t n, int64_t* rows) const {
 }
 
 void HostTier::insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_new) {
-  // 1) bucket the batch by shard
-  std::vector<std::vector<int64_t>> by(kShards);
-  {
-    std::vector<int64_t> cnt(kShards, 0);
-    for (int64_t i = 0; i < n; ++i) cnt[shard_of(h[i])]++;
-    for (int si = 0; si < kShards; ++si) by[si].reserve(cnt[si]);
-    for (int64_t i = 0; i < n; ++i) by[shard_of(h[i])].push_back(i);
-  }
+  // 1) bucket the batch by shard: each worker its contiguous range (the
+  //    per-shard lists of all workers, in worker order, keep batch order)
+  const int T = std::max(1, pool_->size());
+  std::vector<std::vector<std::vector<int64_t>>> loc(T, std::vector<std::vector<int64_t>>(kShards));
+  pool_->parallel_range(n, [&](int tid, int64_t b, int64_t e) {
+    auto& L = loc[tid];
+    for (auto& v : L) v.reserve((size_t)((e - b) / kShards + 16));
+    for (int64_t i = b; i < e; ++i) L[shard_of(h[i])].push_back(i);
+  });
+  auto for_shard = [&](int64_t si, auto&& f) {
+    for (int t = 0; t < T; ++t)
+      for (int64_t i : loc[t][si]) f(i);
+  };
   // 2) per shard (parallel): resolve present keys, collect the distinct
   //    absent ones, size the shard's table for them once
   std::vector<std::vector<int64_t>> fresh(kShards);  // batch index of first occurrence
@@ -207,16 +212,16 @@ void HostTier::insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_ne
     for (int64_t si = b; si < e; ++si) {
       Shard& s = shards_[si];
       std::lock_guard<std::mutex> lk(s.mu);
-      for (int64_t i : by[si]) {
+      for_shard(si, [&](int64_t i) {
         const uint64_t k = h[i];
         if (k == kEmptyKey || k == kTomb) {
           rows[i] = -1;
-          continue;
+          return;
         }
         const int64_t p = find(s, k);
         rows[i] = p < 0 ? -2 : s.rows[p];
         if (p < 0) fresh[si].push_back(i);
-      }
+      });
       // dedup absent keys within the batch
       auto& f = fresh[si];
       std::sort(f.begin(), f.end(), [&](int64_t a, int64_t c) { return h[a] < h[c] || (h[a] == h[c] && a < c); });
@@ -264,8 +269,9 @@ void HostTier::insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_ne
         s.rows[j] = alloc[base[si] + (int64_t)q];
         ++s.live;
       }
-      for (int64_t i : by[si])
+      for_shard(si, [&](int64_t i) {
         if (rows[i] == -2) rows[i] = s.rows[find(s, h[i])];
+      });
     }
   });
   if (n_new) *n_new = total;
