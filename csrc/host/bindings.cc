@@ -671,13 +671,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("clk_coeff"), py::arg("delete_threshold"), py::arg("max_unseen"),
            py::call_guard<py::gil_scoped_release>())
       .def("select_ge", [](const HostTier& t, int col, float thr) {
-        std::vector<uint64_t> k;
-        std::vector<float> v;
+        // the selected rows land straight in the returned tensors (filled by
+        // the tier's workers, no intermediate vectors)
+        Tensor k, v;
         {
           py::gil_scoped_release g;
-          t.select_ge(col, thr, &k, &v);
+          t.select_ge_to(col, thr, [&](size_t n) {
+            k = torch::empty({(int64_t)n}, torch::kInt64);
+            v = torch::empty({(int64_t)n, (int64_t)t.stride()}, torch::kFloat32);
+            return std::make_pair(reinterpret_cast<uint64_t*>(k.data_ptr<int64_t>()), v.data_ptr<float>());
+          });
         }
-        return py::make_tuple(to_tensor_u64(k), to_tensor_f(v, t.stride()));
+        return py::make_tuple(k, v);
       })
       .def("stamp", [](HostTier& t, const Tensor& rows, int64_t epoch) {
         auto rc = rows.contiguous();
@@ -694,13 +699,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         return out;
       })
       .def("spill_oldest", [](HostTier& t, int64_t keep_rows) {
-        std::vector<uint64_t> k;
-        std::vector<float> v;
+        Tensor k, v;
         {
           py::gil_scoped_release g;
-          t.spill_oldest(keep_rows, &k, &v);
+          t.spill_oldest_to(keep_rows, [&](size_t n) {
+            k = torch::empty({(int64_t)n}, torch::kInt64);
+            v = torch::empty({(int64_t)n, (int64_t)t.stride()}, torch::kFloat32);
+            return std::make_pair(reinterpret_cast<uint64_t*>(k.data_ptr<int64_t>()), v.data_ptr<float>());
+          });
         }
-        return py::make_tuple(to_tensor_u64(k), to_tensor_f(v, t.stride()));
+        return py::make_tuple(k, v);
       })
       .def("clear", &HostTier::clear);
   py::class_<SsdLog>(m, "SsdLog")

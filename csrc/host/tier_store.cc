@@ -335,9 +335,21 @@ void HostTier::export_all(std::vector<uint64_t>* keys, std::vector<float>* vals)
 
 void HostTier::extract(const std::function<bool(int64_t, const float*)>& pred, bool erase,
                        std::vector<uint64_t>* keys, std::vector<float>* vals) {
+  extract_to(pred, erase, [&](size_t n) {
+    keys->resize(n);
+    vals->resize(n * (size_t)stride_);
+    return std::make_pair(keys->data(), vals->data());
+  });
+}
+
+void HostTier::extract_to(const std::function<bool(int64_t, const float*)>& pred, bool erase,
+                          const OutAlloc& alloc) {
+  // pass 1 (parallel over shards, each under its lock): select, tombstone,
+  // remember the selected rows; pass 2: every shard copies its rows straight
+  // into its slice of the output (one allocation, no per-row vector growth
+  // and no concatenation copy)
   std::vector<std::vector<uint64_t>> lk(kShards);
-  std::vector<std::vector<float>> lv(kShards);
-  std::vector<std::vector<int64_t>> freed(kShards);
+  std::vector<std::vector<int64_t>> lr(kShards);
   pool_->parallel_range(kShards, [&](int, int64_t b, int64_t e) {
     for (int64_t si = b; si < e; ++si) {
       Shard& s = shards_[si];
@@ -345,12 +357,10 @@ void HostTier::extract(const std::function<bool(int64_t, const float*)>& pred, b
       for (size_t j = 0; j < s.keys.size(); ++j) {
         if (s.keys[j] == kEmptyKey || s.keys[j] == kTomb) continue;
         const int64_t r = s.rows[j];
-        const float* v = row_ptr(r);
-        if (!pred(r, v)) continue;
+        if (!pred(r, row_ptr(r))) continue;
         lk[si].push_back(s.keys[j]);
-        lv[si].insert(lv[si].end(), v, v + stride_);
+        lr[si].push_back(r);
         if (erase) {
-          freed[si].push_back(r);
           s.keys[j] = kTomb;
           s.rows[j] = -1;
           --s.live;
@@ -358,19 +368,21 @@ void HostTier::extract(const std::function<bool(int64_t, const float*)>& pred, b
       }
     }
   });
-  keys->clear();
-  vals->clear();
-  size_t n = 0;
-  for (auto& k : lk) n += k.size();
-  keys->reserve(n);
-  vals->reserve(n * stride_);
-  for (int si = 0; si < kShards; ++si) {
-    keys->insert(keys->end(), lk[si].begin(), lk[si].end());
-    vals->insert(vals->end(), lv[si].begin(), lv[si].end());
-  }
+  std::vector<size_t> off(kShards + 1, 0);
+  for (int si = 0; si < kShards; ++si) off[si + 1] = off[si] + lk[si].size();
+  const size_t n = off[kShards];
+  const auto out = alloc(n);
+  pool_->parallel_range(kShards, [&](int, int64_t b, int64_t e) {
+    for (int64_t si = b; si < e; ++si) {
+      std::copy(lk[si].begin(), lk[si].end(), out.first + off[si]);
+      float* dst = out.second + off[si] * (size_t)stride_;
+      for (size_t q = 0; q < lr[si].size(); ++q)
+        std::memcpy(dst + q * (size_t)stride_, row_ptr(lr[si][q]), (size_t)stride_ * sizeof(float));
+    }
+  });
   if (erase) {
     std::lock_guard<std::mutex> g(alloc_mu_);
-    for (auto& f : freed) free_rows_.insert(free_rows_.end(), f.begin(), f.end());
+    for (auto& f : lr) free_rows_.insert(free_rows_.end(), f.begin(), f.end());
   }
 }
 
@@ -379,6 +391,14 @@ void HostTier::select_ge(int col, float thr, std::vector<uint64_t>* keys, std::v
   vals->clear();
   if (col < 0 || col >= stride_) return;
   const_cast<HostTier*>(this)->extract([&](int64_t, const float* v) { return v[col] >= thr; }, false, keys, vals);
+}
+
+void HostTier::select_ge_to(int col, float thr, const OutAlloc& alloc) const {
+  if (col < 0 || col >= stride_) {
+    alloc(0);
+    return;
+  }
+  const_cast<HostTier*>(this)->extract_to([&](int64_t, const float* v) { return v[col] >= thr; }, false, alloc);
 }
 
 void HostTier::stamp(const int64_t* rows, int64_t n, uint32_t epoch) {
@@ -391,21 +411,44 @@ void HostTier::stamp(const int64_t* rows, int64_t n, uint32_t epoch) {
 int64_t HostTier::spill_oldest(int64_t keep_rows, std::vector<uint64_t>* keys, std::vector<float>* vals) {
   keys->clear();
   vals->clear();
+  return spill_oldest_to(keep_rows, [&](size_t n) {
+    keys->resize(n);
+    vals->resize(n * (size_t)stride_);
+    return std::make_pair(keys->data(), vals->data());
+  });
+}
+
+int64_t HostTier::spill_oldest_to(int64_t keep_rows, const OutAlloc& alloc) {
   const int64_t need = size() - (keep_rows < 0 ? 0 : keep_rows);
-  if (need <= 0) return 0;
-  // pass histogram over the live rows
+  if (need <= 0) {
+    alloc(0);
+    return 0;
+  }
+  // pass histogram over the live rows: small pass ids in a flat array per
+  // shard (the common case), larger ones in a map
+  constexpr uint32_t kFlat = 4096;
+  std::vector<std::vector<int64_t>> hf(kShards, std::vector<int64_t>(kFlat, 0));
   std::vector<std::map<uint32_t, int64_t>> hs(kShards);
   pool_->parallel_range(kShards, [&](int, int64_t b, int64_t e) {
     for (int64_t si = b; si < e; ++si) {
       const Shard& s = shards_[si];
       std::lock_guard<std::mutex> g(s.mu);
       for (size_t j = 0; j < s.keys.size(); ++j)
-        if (s.keys[j] != kEmptyKey && s.keys[j] != kTomb) hs[si][epoch_of_row(s.rows[j])]++;
+        if (s.keys[j] != kEmptyKey && s.keys[j] != kTomb) {
+          const uint32_t ep = epoch_of_row(s.rows[j]);
+          if (ep < kFlat)
+            hf[si][ep]++;
+          else
+            hs[si][ep]++;
+        }
     }
   });
   std::map<uint32_t, int64_t> h;
-  for (auto& m : hs)
-    for (auto& kv : m) h[kv.first] += kv.second;
+  for (int si = 0; si < kShards; ++si) {
+    for (uint32_t ep = 0; ep < kFlat; ++ep)
+      if (hf[si][ep]) h[ep] += hf[si][ep];
+    for (auto& kv : hs[si]) h[kv.first] += kv.second;
+  }
   // boundary pass T: every row of an older pass goes, then `quota` rows of T
   uint32_t T = 0;
   int64_t below = 0;
@@ -415,13 +458,20 @@ int64_t HostTier::spill_oldest(int64_t keep_rows, std::vector<uint64_t>* keys, s
     below += kv.second;
   }
   std::atomic<int64_t> quota{need - below};
-  extract(
+  // the boundary pass taken whole: no per-row quota atomic (8M contended
+  // fetch_subs were a large part of a spill)
+  const bool whole = need - below >= h[T];
+  size_t got = 0;
+  extract_to(
       [&](int64_t r, const float*) {
         const uint32_t e = epoch_of_row(r);
-        return e < T || (e == T && quota.fetch_sub(1, std::memory_order_relaxed) > 0);
+        return e < T || (e == T && (whole || quota.fetch_sub(1, std::memory_order_relaxed) > 0));
       },
-      true, keys, vals);
-  return (int64_t)keys->size();
+      true, [&](size_t n) {
+        got = n;
+        return alloc(n);
+      });
+  return (int64_t)got;
 }
 
 int64_t HostTier::shrink(float decay, int unseen_col, float nonclk_coeff, float clk_coeff, float delete_threshold,

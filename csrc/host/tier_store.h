@@ -60,6 +60,10 @@ class HostTier {
   // keep_rows remain, returning them for the SSD tier.  Parallel over shards.
   void stamp(const int64_t* rows, int64_t n, uint32_t epoch);
   int64_t spill_oldest(int64_t keep_rows, std::vector<uint64_t>* keys, std::vector<float>* vals);
+  // output buffers for n selected rows (keys [n], vals [n * stride]), filled in parallel
+  using OutAlloc = std::function<std::pair<uint64_t*, float*>(size_t)>;
+  int64_t spill_oldest_to(int64_t keep_rows, const OutAlloc& alloc);
+  void select_ge_to(int col, float thr, const OutAlloc& alloc) const;
   uint32_t epoch_of_row(int64_t r) const { return epochs_[r / chunk_rows_][r % chunk_rows_]; }
   // end-of-day shrink over every row, in parallel over the shards
   // (ctr_accessor.cc:63-80): show/click *= decay, unseen_days += 1, delete
@@ -89,6 +93,7 @@ class HostTier {
   // rows matching pred(row, values), in shard order; erased from the tier when `erase`
   void extract(const std::function<bool(int64_t, const float*)>& pred, bool erase, std::vector<uint64_t>* keys,
                std::vector<float>* vals);
+  void extract_to(const std::function<bool(int64_t, const float*)>& pred, bool erase, const OutAlloc& alloc);
 
   int stride_;
   int64_t chunk_rows_;
