@@ -684,7 +684,12 @@ void SsdLog::put(const uint64_t* h, const float* vals, int64_t n, int vstride) {
   std::vector<std::pair<uint64_t, Loc>> placed;
   placed.reserve(n);
   write_batch(h, vals, n, vstride, false, &placed);
-  for (auto& kl : placed) {
+  index_.reserve_more((int64_t)placed.size());
+  const size_t np = placed.size();
+  constexpr size_t kAhead = 16;  // the index is random access: prefetch ahead
+  for (size_t i = 0; i < np; ++i) {
+    if (i + kAhead < np) index_.prefetch(placed[i + kAhead].first);
+    const auto& kl = placed[i];
     const int32_t old = index_.set(kl.first, kl.second);
     if (old >= 0) segs_[old]->live--;
     segs_[kl.second.seg]->live++;

@@ -171,6 +171,18 @@ class LocIndex {
     for (size_t i = 0; i < keys_.size(); ++i)
       if (keys_[i] != kEmptyKey) f(keys_[i], locs_[i]);
   }
+  // grow once for n more keys instead of doubling inside a long insert run
+  void reserve_more(int64_t n) {
+    size_t cap = keys_.size();
+    while ((n_ + n + 1) * 2 > (int64_t)cap) cap *= 2;
+    if (cap != keys_.size()) rehash(cap);
+  }
+  // hide the two cache misses of a later set()/find() of k
+  void prefetch(uint64_t k) const {
+    const uint64_t i = home(k);
+    __builtin_prefetch(&keys_[i], 1);
+    __builtin_prefetch(&locs_[i], 1);
+  }
 
  private:
   uint64_t home(uint64_t k) const { return (k ^ (k >> 29) ^ (k >> 47)) * 0x9E3779B97F4A7C15ULL >> 7 & mask_; }
