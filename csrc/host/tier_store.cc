@@ -110,6 +110,16 @@ int64_t HostTier::alloc_row() {
   return next_row_++;
 }
 
+namespace {
+using KeyIdx = std::pair<uint64_t, int64_t>;  // (key, batch index)
+constexpr size_t kAhead = 12;                  // prefetch distance of the shard lookups (miss-bound)
+template <class S>
+inline void prefetch_slot(const S& s, uint64_t j) {
+  __builtin_prefetch(&s.keys[j]);
+  __builtin_prefetch(&s.rows[j]);
+}
+}  // namespace
+
 int64_t HostTier::find(const Shard& s, uint64_t h) const {
   const uint64_t mask = s.keys.size() - 1;
   for (uint64_t i = mix64(h) & mask;; i = (i + 1) & mask) {
@@ -172,21 +182,27 @@ void HostTier::probe(const uint64_t* h, int64_t n, int64_t* rows) const {
   // key across the pool's threads made a 14M-key probe take 3.6 s on 8 cores,
   // 4x an insert of the same keys).  Each worker buckets its contiguous range
   // by shard, then each shard resolves all of its keys under one lock.
-  std::vector<std::vector<std::vector<int64_t>>> loc(T, std::vector<std::vector<int64_t>>(kShards));
+  // (key, batch index) pairs: the per-shard pass then never re-reads h[] at
+  // random, and the prefetch of a later key's home slot does not stall on it
+  std::vector<std::vector<std::vector<KeyIdx>>> loc(T, std::vector<std::vector<KeyIdx>>(kShards));
   pool_->parallel_range(n, [&](int tid, int64_t b, int64_t e) {
     auto& L = loc[tid];
     for (auto& v : L) v.reserve((size_t)((e - b) / kShards + 16));
-    for (int64_t i = b; i < e; ++i) L[shard_of(h[i])].push_back(i);
+    for (int64_t i = b; i < e; ++i) L[shard_of(h[i])].emplace_back(h[i], i);
   });
   pool_->parallel_range(kShards, [&](int, int64_t sb, int64_t se) {
     for (int64_t si = sb; si < se; ++si) {
       const Shard& s = shards_[si];
       std::lock_guard<std::mutex> lk(s.mu);
-      for (int t = 0; t < T; ++t)
-        for (int64_t i : loc[t][si]) {
-          const int64_t p = find(s, h[i]);
-          rows[i] = p < 0 ? -1 : s.rows[p];
+      const uint64_t pmask = s.keys.size() - 1;
+      for (int t = 0; t < T; ++t) {
+        const auto& L = loc[t][si];
+        for (size_t q = 0; q < L.size(); ++q) {
+          if (q + kAhead < L.size()) prefetch_slot(s, mix64(L[q + kAhead].first) & pmask);
+          const int64_t p = find(s, L[q].first);
+          rows[L[q].second] = p < 0 ? -1 : s.rows[p];
         }
+      }
     }
   });
 }
@@ -195,46 +211,44 @@ void HostTier::insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_ne
   // 1) bucket the batch by shard: each worker its contiguous range (the
   //    per-shard lists of all workers, in worker order, keep batch order)
   const int T = std::max(1, pool_->size());
-  std::vector<std::vector<std::vector<int64_t>>> loc(T, std::vector<std::vector<int64_t>>(kShards));
+  std::vector<std::vector<std::vector<KeyIdx>>> loc(T, std::vector<std::vector<KeyIdx>>(kShards));
   pool_->parallel_range(n, [&](int tid, int64_t b, int64_t e) {
     auto& L = loc[tid];
     for (auto& v : L) v.reserve((size_t)((e - b) / kShards + 16));
-    for (int64_t i = b; i < e; ++i) L[shard_of(h[i])].push_back(i);
+    for (int64_t i = b; i < e; ++i) L[shard_of(h[i])].emplace_back(h[i], i);
   });
-  auto for_shard = [&](int64_t si, auto&& f) {
-    for (int t = 0; t < T; ++t)
-      for (int64_t i : loc[t][si]) f(i);
-  };
   // 2) per shard (parallel): resolve present keys, collect the distinct
   //    absent ones, size the shard's table for them once
-  std::vector<std::vector<int64_t>> fresh(kShards);  // batch index of first occurrence
+  std::vector<std::vector<KeyIdx>> fresh(kShards);  // (key, batch index of first occurrence)
   pool_->parallel_range(kShards, [&](int, int64_t b, int64_t e) {
     for (int64_t si = b; si < e; ++si) {
       Shard& s = shards_[si];
       std::lock_guard<std::mutex> lk(s.mu);
-      for_shard(si, [&](int64_t i) {
-        const uint64_t k = h[i];
-        if (k == kEmptyKey || k == kTomb) {
-          rows[i] = -1;
-          return;
-        }
-        const int64_t p = find(s, k);
-        rows[i] = p < 0 ? -2 : s.rows[p];
-        if (p < 0) fresh[si].push_back(i);
-      });
-      // dedup absent keys within the batch: sort (key, first index) pairs
-      // in place (an index sort comparing through h[] missed the cache on
-      // every comparison: most of a 14M-new-key insert)
       auto& f = fresh[si];
-      {
-        std::vector<std::pair<uint64_t, int64_t>> kp(f.size());
-        for (size_t q = 0; q < f.size(); ++q) kp[q] = {h[f[q]], f[q]};
-        std::sort(kp.begin(), kp.end());
-        size_t w = 0;
-        for (size_t q = 0; q < kp.size(); ++q)
-          if (q == 0 || kp[q].first != kp[q - 1].first) f[w++] = kp[q].second;
-        f.resize(w);
+      const uint64_t pmask = s.keys.size() - 1;
+      for (int t = 0; t < T; ++t) {
+        const auto& L = loc[t][si];
+        for (size_t q = 0; q < L.size(); ++q) {
+          if (q + kAhead < L.size()) prefetch_slot(s, mix64(L[q + kAhead].first) & pmask);
+          const uint64_t k = L[q].first;
+          const int64_t i = L[q].second;
+          if (k == kEmptyKey || k == kTomb) {
+            rows[i] = -1;
+            continue;
+          }
+          const int64_t p = find(s, k);
+          rows[i] = p < 0 ? -2 : s.rows[p];
+          if (p < 0) f.emplace_back(k, i);
+        }
       }
+      // dedup absent keys within the batch: sort the (key, first index)
+      // pairs (an index sort comparing through h[] missed the cache on
+      // every comparison: most of a 14M-new-key insert)
+      std::sort(f.begin(), f.end());
+      size_t w = 0;
+      for (size_t q = 0; q < f.size(); ++q)
+        if (q == 0 || f[q].first != f[q - 1].first) f[w++] = f[q];
+      f.resize(w);
       if ((double)(s.used + (int64_t)f.size()) / s.keys.size() > 0.7) {
         s.live += (int64_t)f.size();  // grow() sizes for live
         grow(&s);
@@ -270,7 +284,7 @@ void HostTier::insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_ne
       std::lock_guard<std::mutex> lk(s.mu);
       const uint64_t mask = s.keys.size() - 1;
       for (size_t q = 0; q < fresh[si].size(); ++q) {
-        const uint64_t k = h[fresh[si][q]];
+        const uint64_t k = fresh[si][q].first;
         uint64_t j = mix64(k) & mask;
         while (s.keys[j] != kEmptyKey && s.keys[j] != kTomb) j = (j + 1) & mask;
         if (s.keys[j] == kEmptyKey) ++s.used;
@@ -278,9 +292,9 @@ void HostTier::insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_ne
         s.rows[j] = alloc[base[si] + (int64_t)q];
         ++s.live;
       }
-      for_shard(si, [&](int64_t i) {
-        if (rows[i] == -2) rows[i] = s.rows[find(s, h[i])];
-      });
+      for (int t = 0; t < T; ++t)
+        for (const auto& ki : loc[t][si])
+          if (rows[ki.second] == -2) rows[ki.second] = s.rows[find(s, ki.first)];
     }
   });
   if (n_new) *n_new = total;
