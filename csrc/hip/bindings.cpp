@@ -1346,6 +1346,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("dz", &MlpWorkspace::dz)
       .def("dx0", &MlpWorkspace::dx0)
       .def_property_readonly("M", &MlpWorkspace::M);
+  m.attr("kSaveMaxCols") = kSaveMaxCols;
   m.def("fill_occurrence", &fill_occurrence);
   m.def("seqpool_cvm_fwd", &seqpool_cvm_fwd, py::arg("src"), py::arg("src_index"), py::arg("uid"), py::arg("lod"),
         py::arg("S"), py::arg("B"), py::arg("E"), py::arg("out"), py::arg("col_offset"), py::arg("use_cvm"),

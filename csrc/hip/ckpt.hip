@@ -35,13 +35,7 @@ __global__ __launch_bounds__(256) void k_save_chunk(TableDev t, int64_t r0, int6
       } else {
         key = t.stash_keys[row - total];
       }
-      take = key != kEmptyKey;
-      if (take && sel.mode != 0) {
-        const float* v = t.values + row * (int64_t)t.stride;
-        const float score = (v[kShow] - v[kClick]) * sel.nonclk_coeff + v[kClick] * sel.clk_coeff;
-        take = score >= sel.base_threshold && v[l.unseen_days] <= sel.delta_keep_days;
-        if (take && sel.mode == 2) take = v[l.delta_score] >= sel.delta_threshold;
-      }
+      take = key != kEmptyKey && save_keep(sel, t.values + row * (int64_t)t.stride, l);
     }
     // wave compaction: one counter add per wave
     const uint64_t m = __ballot(take);

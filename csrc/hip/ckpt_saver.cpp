@@ -44,87 +44,11 @@ namespace {
                                                    hipGetErrorString(e_));                   \
   } while (0)
 
-constexpr size_t kNpyHeader = 128;
-
-std::string npy_header(const char* descr, int64_t n, int64_t cols) {
-  char dict[128];
-  if (cols > 0)
-    snprintf(dict, sizeof(dict), "{'descr': '%s', 'fortran_order': False, 'shape': (%lld, %lld), }", descr,
-             (long long)n, (long long)cols);
-  else
-    snprintf(dict, sizeof(dict), "{'descr': '%s', 'fortran_order': False, 'shape': (%lld,), }", descr,
-             (long long)n);
-  std::string d(dict);
-  const size_t body = kNpyHeader - 10;  // magic(6) + version(2) + length(2)
-  if (d.size() + 1 > body) throw std::runtime_error("stream_save: npy header too long");
-  d.append(body - 1 - d.size(), ' ');
-  d.push_back('\n');
-  std::string h("\x93NUMPY\x01\x00", 8);
-  h.push_back((char)(body & 0xff));
-  h.push_back((char)(body >> 8));
-  return h + d;
-}
-
-struct File {
-  FILE* f = nullptr;
-  explicit File(const std::string& p) {
-    f = fopen(p.c_str(), "wb");
-    if (!f) throw std::runtime_error("stream_save: cannot open " + p);
-    setvbuf(f, nullptr, _IOFBF, 1 << 22);
-  }
-  ~File() {
-    if (f) fclose(f);
-  }
-  void write(const void* p, size_t n) {
-    if (n && fwrite(p, 1, n, f) != n) throw std::runtime_error("stream_save: write failed");
-  }
-  void close() {
-    if (f && fclose(f) != 0) {
-      f = nullptr;
-      throw std::runtime_error("stream_save: close failed");
-    }
-    f = nullptr;
-  }
-};
-
 struct HostBuf {
   uint64_t* keys = nullptr;
   float* vals = nullptr;
   int64_t n = 0;
 };
-
-// one xbox text line per row (same bytes as the Python writer's
-// f"{key}\t" + " ".join(f"{x:.6g}") + "\n")
-void format_rows(const HostBuf& b, int64_t i0, int64_t i1, int dim, int stride, const RowLayout& l,
-                 const SaveSelect& sel, float embedx_threshold, std::string& out) {
-  char tmp[48];
-  auto put = [&](float x) {
-    auto r = std::to_chars(tmp, tmp + sizeof(tmp), (double)x, std::chars_format::general, 6);
-    out.append(tmp, r.ptr);
-  };
-  for (int64_t i = i0; i < i1; ++i) {
-    const float* v = b.vals + i * (int64_t)stride;
-    auto r = std::to_chars(tmp, tmp + sizeof(tmp), (unsigned long long)b.keys[i]);
-    out.append(tmp, r.ptr);
-    out.push_back('\t');
-    const float head[7] = {v[l.slot], v[l.unseen_days], v[l.delta_score], v[kShow], v[kClick], v[kEmbedW],
-                           v[l.embed_g2sum]};
-    for (int c = 0; c < 7; ++c) {
-      if (c) out.push_back(' ');
-      put(head[c]);
-    }
-    const float score = (v[kShow] - v[kClick]) * sel.nonclk_coeff + v[kClick] * sel.clk_coeff;
-    if (score >= embedx_threshold && v[l.mf_size] != 0.f) {
-      for (int d = 0; d < dim; ++d) {
-        out.push_back(' ');
-        put(v[kEmbedx + d]);
-      }
-      out.push_back(' ');
-      put(v[l.embedx_g2sum]);
-    }
-    out.push_back('\n');
-  }
-}
 
 }  // namespace
 
@@ -177,9 +101,9 @@ SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, con
     CK(hipHostMalloc(&h.vals, chunk_rows * (size_t)stride * sizeof(float), hipHostMallocDefault));
   }
   // ---- files
-  std::unique_ptr<File> fk(new File(keys_path)), fv;
+  std::unique_ptr<SaveFile> fk(new SaveFile(keys_path)), fv;
   if (kind == 0) {
-    fv.reset(new File(vals_path));
+    fv.reset(new SaveFile(vals_path));
     fk->write(npy_header("<u8", 0, 0).data(), kNpyHeader);
     fv->write(npy_header("<f4", 0, stride).data(), kNpyHeader);
   }
@@ -214,7 +138,8 @@ SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, con
             ws.emplace_back([&, w]() {
               outs[w].clear();
               outs[w].reserve((size_t)(b.n / T + 1) * 160);
-              format_rows(b, b.n * w / T, b.n * (w + 1) / T, odim, stride, l, sel, embedx_threshold, outs[w]);
+              format_xbox_rows(b.keys, b.vals, b.n * w / T, b.n * (w + 1) / T, odim, stride, l, sel, embedx_threshold,
+                               outs[w]);
             });
           }
           for (auto& th : ws) th.join();
@@ -286,10 +211,8 @@ SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, con
   if (!werr.empty()) throw std::runtime_error(werr);
   if (kind == 0) {  // patch the shapes into the fixed-length headers
     for (int i = 0; i < 2; ++i) {
-      File* f = i == 0 ? fk.get() : fv.get();
-      const std::string h = i == 0 ? npy_header("<u8", st.rows, 0) : npy_header("<f4", st.rows, stride);
-      if (fseek(f->f, 0, SEEK_SET) != 0) throw std::runtime_error("stream_save: seek failed");
-      f->write(h.data(), kNpyHeader);
+      SaveFile* f = i == 0 ? fk.get() : fv.get();
+      f->rewrite_head(i == 0 ? npy_header("<u8", st.rows, 0) : npy_header("<f4", st.rows, stride));
     }
     fv->close();
   }

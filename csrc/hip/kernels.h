@@ -10,6 +10,7 @@
 #include <cstdint>
 
 #include "../common/pbx_common.h"
+#include "../common/ckpt_format.h"
 
 namespace pbx {
 
@@ -299,21 +300,12 @@ bool launch_push_occ(const PushMergeArgs& a, const TableDev& t, const int64_t* r
                      const SparseSGDConfig& cfg, uint64_t seed, hipStream_t s);
 // Streaming checkpoint (ckpt.hip / ckpt_saver.cpp).  mode 0 = every row
 // (batch model), 1 = xbox base, 2 = xbox delta (ctr_accessor.cc:102-170).
-struct SaveSelect {
-  int mode = 0;
-  int reset_delta = 0;
-  float base_threshold = 0.f;
-  float delta_threshold = 0.f;
-  float delta_keep_days = 16.f;
-  float nonclk_coeff = 0.1f;
-  float clk_coeff = 1.f;
-};
 // Output row of a save: the table row as stored (n = 0), or a decoded row of
 // n floats (feature-type codec tables: the canonical fp32 layout of
 // ps/feature_types.py FeatureCodec.decode) -- map[j] >= 0: stored float
 // column, -1: zero, <= -2: int16 element (-2 - map[j]) of the row's
 // embedding block (stored from float column 3) times scale.
-constexpr int kSaveMaxCols = 192;
+constexpr int kSaveMaxCols = 1024;  // 2 KB of kernel arguments
 struct SaveDecode {
   int n = 0;
   float scale = 1.f;

@@ -11,6 +11,7 @@
 #include "auc_runner.h"
 #include "batch_assembler.h"
 #include "tier_store.h"
+#include "tier_save.h"
 #include "slot_dataset.h"
 
 namespace py = pybind11;
@@ -643,6 +644,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         }
         return py::make_tuple(rows, fresh);
       })
+      .def("insert_fresh", [](HostTier& t, const Tensor& h) {
+        // (rows, fresh): fresh[i] = h[i] was absent before the call
+        auto hc = h.contiguous();
+        auto rows = torch::empty({hc.numel()}, torch::kInt64);
+        auto fresh = torch::zeros({hc.numel()}, torch::kUInt8);
+        {
+          py::gil_scoped_release g;
+          int64_t n_new = 0;
+          t.insert(reinterpret_cast<const uint64_t*>(hc.data_ptr<int64_t>()), hc.numel(), rows.data_ptr<int64_t>(),
+                   &n_new, fresh.data_ptr<uint8_t>());
+        }
+        return py::make_tuple(rows, fresh.to(torch::kBool));
+      })
       .def("gather", [](const HostTier& t, const Tensor& rows, Tensor out) {
         TORCH_CHECK(out.is_contiguous() && out.dim() == 2 && out.size(0) >= rows.numel() &&
                     out.scalar_type() == torch::kFloat32, "gather: out [n, stride] f32");
@@ -742,7 +756,38 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         return s.erase(reinterpret_cast<const uint64_t*>(hc.data_ptr<int64_t>()), hc.numel());
       })
       .def("compact", &SsdLog::compact, py::arg("min_live") = 0.5, py::call_guard<py::gil_scoped_release>())
+      .def("shrink", &SsdLog::shrink, py::arg("decay"), py::arg("unseen_col"), py::arg("nonclk_coeff"),
+           py::arg("clk_coeff"), py::arg("delete_threshold"), py::arg("max_unseen"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("live_permille", &SsdLog::live_fraction_permille)
       .def("keys", [](const SsdLog& s) { return to_tensor_u64(s.keys()); });
+  m.def(
+      "save_tiers",
+      [](HostTier* host, SsdLog* ssd, int kind, int mode, bool reset, float base_thr, float delta_thr,
+         float keep_days, float nonclk, float clk, float embedx_thr, int dim, const std::string& keys_path,
+         const std::string& vals_path, int threads, bool collect) {
+        SaveSelect sel;
+        sel.mode = mode;
+        sel.reset_delta = reset ? 1 : 0;
+        sel.base_threshold = base_thr;
+        sel.delta_threshold = delta_thr;
+        sel.delta_keep_days = keep_days;
+        sel.nonclk_coeff = nonclk;
+        sel.clk_coeff = clk;
+        std::vector<uint64_t> saved;
+        TierSaveStats st;
+        {
+          py::gil_scoped_release g;
+          st = save_tiers(host, ssd, kind, sel, dim, embedx_thr, keys_path, vals_path, threads,
+                          collect ? &saved : nullptr);
+        }
+        py::object keys = collect ? py::object(py::cast(to_tensor_u64(saved))) : py::object(py::none());
+        return py::make_tuple(st.rows, st.host_rows, st.ssd_rows, st.total_s, keys);
+      },
+      py::arg("host"), py::arg("ssd"), py::arg("kind"), py::arg("mode"), py::arg("reset"), py::arg("base_threshold"),
+      py::arg("delta_threshold"), py::arg("delta_keep_days"), py::arg("nonclk_coeff"), py::arg("clk_coeff"),
+      py::arg("embedx_threshold"), py::arg("dim"), py::arg("keys_path"), py::arg("vals_path"), py::arg("threads"),
+      py::arg("collect"));
   py::class_<AucRunner>(m, "AucRunner")
       .def(py::init<int, int, uint64_t>(), py::arg("pool_size"), py::arg("threads") = 4, py::arg("seed") = 0)
       .def("set_eval_slots", &AucRunner::set_eval_slots)

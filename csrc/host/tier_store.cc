@@ -207,7 +207,7 @@ void HostTier::probe(const uint64_t* h, int64_t n, int64_t* rows) const {
   });
 }
 
-void HostTier::insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_new) {
+void HostTier::insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_new, uint8_t* fresh_out) {
   // 1) bucket the batch by shard: each worker its contiguous range (the
   //    per-shard lists of all workers, in worker order, keep batch order)
   const int T = std::max(1, pool_->size());
@@ -276,6 +276,8 @@ void HostTier::insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_ne
     if (need > have) add_chunks((int)((need - have + chunk_rows_ - 1) / chunk_rows_));
     while (k < total) alloc[k++] = next_row_++;
     for (int64_t r : recycled) std::memset(row_ptr(r), 0, (size_t)stride_ * sizeof(float));
+    const uint32_t ep = cur_epoch_.load(std::memory_order_relaxed);
+    for (int64_t r : alloc) epochs_[r / chunk_rows_][r % chunk_rows_] = ep;
   }
   // 4) per shard (parallel): place the new keys
   pool_->parallel_range(kShards, [&](int, int64_t b, int64_t e) {
@@ -293,8 +295,11 @@ void HostTier::insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_ne
         ++s.live;
       }
       for (int t = 0; t < T; ++t)
-        for (const auto& ki : loc[t][si])
-          if (rows[ki.second] == -2) rows[ki.second] = s.rows[find(s, ki.first)];
+        for (const auto& ki : loc[t][si]) {
+          const bool was_absent = rows[ki.second] == -2;
+          if (fresh_out) fresh_out[ki.second] = was_absent ? 1 : 0;
+          if (was_absent) rows[ki.second] = s.rows[find(s, ki.first)];
+        }
     }
   });
   if (n_new) *n_new = total;
@@ -425,6 +430,9 @@ void HostTier::select_ge_to(int col, float thr, const OutAlloc& alloc) const {
 }
 
 void HostTier::stamp(const int64_t* rows, int64_t n, uint32_t epoch) {
+  uint32_t cur = cur_epoch_.load(std::memory_order_relaxed);
+  while (epoch > cur && !cur_epoch_.compare_exchange_weak(cur, epoch)) {
+  }
   pool_->parallel_range(n, [&](int, int64_t b, int64_t e) {
     for (int64_t i = b; i < e; ++i)
       if (rows[i] >= 0) epochs_[rows[i] / chunk_rows_][rows[i] % chunk_rows_] = epoch;
@@ -530,6 +538,21 @@ int64_t HostTier::shrink(float decay, int unseen_col, float nonclk_coeff, float 
   return gone.load();
 }
 
+void HostTier::visit(int s0, int s1, const std::function<void(int, uint64_t, float*)>& fn) {
+  s0 = std::max(0, s0);
+  s1 = std::min(kShards, s1);
+  if (s1 <= s0) return;
+  pool_->parallel_range(s1 - s0, [&](int, int64_t b, int64_t e) {
+    for (int64_t q = b; q < e; ++q) {
+      const int si = s0 + (int)q;
+      Shard& s = shards_[si];
+      std::lock_guard<std::mutex> lk(s.mu);
+      for (size_t j = 0; j < s.keys.size(); ++j)
+        if (s.keys[j] != kEmptyKey && s.keys[j] != kTomb) fn(si, s.keys[j], row_ptr(s.rows[j]));
+    }
+  });
+}
+
 void HostTier::clear() {
   for (auto& s : shards_) {
     std::lock_guard<std::mutex> lk(s.mu);
@@ -540,6 +563,7 @@ void HostTier::clear() {
   std::lock_guard<std::mutex> lk(alloc_mu_);
   free_rows_.clear();
   next_row_ = 0;
+  cur_epoch_ = 0;
   // insert() relies on never-used arena rows being zero: release the arena
   for (float* c : chunks_) munmap(c, (size_t)chunk_rows_ * stride_ * sizeof(float));
   chunks_.clear();
@@ -904,6 +928,104 @@ int64_t SsdLog::compact(double min_live) {
     s->live = 0;
   }
   return (int64_t)keys.size();
+}
+
+int64_t SsdLog::rewrite(const std::function<int(uint64_t, float*)>& fn, const std::function<void()>& after_run) {
+  std::lock_guard<std::mutex> lk(mu_);
+  constexpr int64_t kRunPages = 8192;  // 32 MiB per read
+  char* buf = nullptr;
+  if (posix_memalign(reinterpret_cast<void**>(&buf), kPage, (size_t)(kRunPages * kPage)) != 0)
+    throw std::runtime_error("SsdLog: alloc");
+  std::unique_ptr<char, decltype(&std::free)> guard(buf, &std::free);
+  const int active = segs_.back()->id;
+  int64_t deleted = 0;
+  std::vector<uint8_t> dirty;
+  for (auto& sp : segs_) {
+    Seg* s = sp.get();
+    if (s->slots == 0 || (s->fd < 0 && s->id != active)) continue;
+    const int64_t pages = page_of(s->slots - 1) + 1;
+    for (int64_t p0 = 0; p0 < pages; p0 += kRunPages) {
+      const int64_t np = std::min(kRunPages, pages - p0);
+      // the active segment is edited in its write-through mirror
+      char* base = s->id == active ? active_buf_ + p0 * kPage : buf;
+      if (s->id != active) {
+        const ssize_t want = (ssize_t)(np * kPage);
+        if (pread(s->fd, buf, (size_t)want, p0 * kPage) != want) throw std::runtime_error("SsdLog: read failed");
+      }
+      dirty.assign((size_t)np, 0);
+      for (int64_t p = 0; p < np; ++p) {
+        for (int r = 0; r < per_page_; ++r) {
+          const int64_t slot = (p0 + p) * per_page_ + r;
+          if (slot >= s->slots) break;
+          char* rec = base + p * kPage + (int64_t)r * rec_bytes_;
+          uint64_t key;
+          uint32_t flags;
+          std::memcpy(&key, rec, 8);
+          std::memcpy(&flags, rec + 8, 4);
+          if (key == kEmptyKey || (flags & 1u)) continue;
+          const Loc* l = index_.find(key);
+          if (l == nullptr || l->seg != s->id || l->slot != slot) continue;  // superseded record
+          const int act = fn(key, reinterpret_cast<float*>(rec + 12));
+          if (act == kModified) {
+            dirty[p] = 1;
+          } else if (act == kDelete) {
+            flags = 1u;
+            std::memcpy(rec + 8, &flags, 4);
+            std::memset(rec + 12, 0, (size_t)stride_ * 4);
+            index_.erase(key);
+            s->live--;
+            ++deleted;
+            dirty[p] = 1;
+          }
+        }
+      }
+      // write the dirty pages back, one pwrite per consecutive range
+      for (int64_t p = 0; p < np;) {
+        if (!dirty[p]) {
+          ++p;
+          continue;
+        }
+        int64_t q = p;
+        while (q < np && dirty[q]) ++q;
+        if (s->id == active) {
+          flush_pages(s, p0 + p, q - p);
+        } else {
+          const int64_t bytes = (q - p) * kPage;
+          int64_t done = 0;
+          while (done < bytes) {
+            const ssize_t w = pwrite(s->fd, buf + p * kPage + done, (size_t)(bytes - done), (p0 + p) * kPage + done);
+            if (w <= 0) throw std::runtime_error("SsdLog: write failed");
+            done += w;
+          }
+        }
+        p = q;
+      }
+      if (after_run) after_run();
+    }
+  }
+  return deleted;
+}
+
+int64_t SsdLog::shrink(float decay, int unseen_col, float nonclk_coeff, float clk_coeff, float delete_threshold,
+                       float max_unseen) {
+  if (unseen_col < 2 || unseen_col >= stride_) throw std::runtime_error("SsdLog::shrink: unseen column");
+  return rewrite([&](uint64_t, float* v) {
+    v[0] *= decay;
+    v[1] *= decay;
+    v[unseen_col] += 1.f;
+    const float score = (v[0] - v[1]) * nonclk_coeff + v[1] * clk_coeff;
+    return (score < delete_threshold || v[unseen_col] > max_unseen) ? (int)kDelete : (int)kModified;
+  });
+}
+
+int64_t SsdLog::live_fraction_permille() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  int64_t slots = 0, live = 0;
+  for (auto& s : segs_) {
+    slots += s->slots;
+    live += s->live;
+  }
+  return slots ? live * 1000 / slots : 1000;
 }
 
 }  // namespace pbx

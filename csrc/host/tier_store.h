@@ -47,7 +47,8 @@ class HostTier {
 
   void probe(const uint64_t* h, int64_t n, int64_t* rows) const;
   // insert absent keys with zeroed rows (duplicates allowed); rows[i] = row of h[i]
-  void insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_new);
+  // fresh (optional, [n]): 1 where h[i] was absent before this call
+  void insert(const uint64_t* h, int64_t n, int64_t* rows, int64_t* n_new, uint8_t* fresh = nullptr);
   void gather(const int64_t* rows, int64_t n, float* out, int out_stride) const;
   void scatter(const int64_t* rows, int64_t n, const float* vals, int vstride);
   int64_t erase(const uint64_t* h, int64_t n);
@@ -72,6 +73,12 @@ class HostTier {
   int64_t shrink(float decay, int unseen_col, float nonclk_coeff, float clk_coeff, float delete_threshold,
                  float max_unseen);
   void clear();
+  // every live row of shards [s0, s1), shards in parallel on the pool, each
+  // under its lock and visited by one thread: fn(shard, key, row) may modify
+  // the row in place (saves, delta reset)
+  static constexpr int kNumShards = 64;
+  void visit(int s0, int s1, const std::function<void(int, uint64_t, float*)>& fn);
+  int threads() const { return pool_->size(); }
 
  private:
   struct Shard {
@@ -80,7 +87,7 @@ class HostTier {
     int64_t used = 0, live = 0;
     mutable std::mutex mu;
   };
-  static constexpr int kShards = 64;
+  static constexpr int kShards = kNumShards;
   static constexpr int kMaxChunks = 1 << 16;
   static constexpr uint64_t kTomb = 0xFFFFFFFFFFFFFFFEULL;
   int shard_of(uint64_t h) const { return (int)(h >> 58); }  // top 6 bits
@@ -102,6 +109,10 @@ class HostTier {
   std::vector<std::unique_ptr<uint32_t[]>> epochs_;  // one stamp per arena row, chunked like chunks_
   std::vector<int64_t> free_rows_;
   int64_t next_row_ = 0;
+  // newest pass stamp seen: rows entering by insert() carry it, so a row
+  // loaded / assigned outside a write-back does not look like the oldest
+  // pass to spill_oldest (nor inherit a recycled row's stamp)
+  std::atomic<uint32_t> cur_epoch_{0};
   std::mutex alloc_mu_;
   std::vector<std::vector<int>> node_cpus_;
   std::unique_ptr<ThreadPool> pool_;
@@ -220,6 +231,19 @@ class SsdLog {
   int64_t erase(const uint64_t* h, int64_t n);
   // rewrite segments whose live fraction < min_live; returns records moved
   int64_t compact(double min_live = 0.5);
+  // In-place pass over every live record, segment by segment (sequential
+  // reads of up to 32 MiB): fn(key, values) returns kKeep, kModified (its
+  // page is written back in place) or kDelete (the record becomes a
+  // tombstone in place and leaves the index -- replay stays exact: no later
+  // segment holds the key).  after_run() runs after each read run, so a
+  // consumer can flush what fn collected.  Returns the records deleted.
+  enum : int { kKeep = 0, kModified = 1, kDelete = 2 };
+  int64_t rewrite(const std::function<int(uint64_t, float*)>& fn, const std::function<void()>& after_run = {});
+  // end-of-day shrink of every SSD record (HostTier::shrink's rule, applied
+  // eagerly through rewrite); returns rows deleted
+  int64_t shrink(float decay, int unseen_col, float nonclk_coeff, float clk_coeff, float delete_threshold,
+                 float max_unseen);
+  int64_t live_fraction_permille() const;
   std::vector<uint64_t> keys() const;
 
  private:

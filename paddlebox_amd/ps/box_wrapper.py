@@ -338,9 +338,17 @@ class BoxWrapper:
 
     # ---------------------------------------------------------------- model IO
     def _authoritative(self):
+        """The table model IO and shrink act on: the GPU table (hbm), or in
+        tiered mode the host + SSD tiers as one table (``TierView``: every
+        feature, cold SSD rows included), made current first."""
         if self.mode == "tiered":
             self._sync_tiers()
-            return self.host
+            from .tiered import TierView
+
+            v = getattr(self, "_tier_view", None)
+            if v is None or v.host is not self.host or v.ssd is not self.ssd:
+                v = self._tier_view = TierView(self.host, self.ssd)
+            return v
         return self._require_engine().table
 
     def _sync_tiers(self):
@@ -532,8 +540,15 @@ class BoxWrapper:
         return int(found.sum())
 
     def shrink_table(self) -> int:
+        """ShrinkTable (box_wrapper.h:638): decay show/click, age, delete
+        (ctr_accessor.cc:63-80) over the whole table -- in tiered mode the
+        host tier and every SSD record.  Inside a pass the live GPU rows are
+        shrunk by the same rule, so the next write-back keeps the result."""
         t = self._authoritative()
-        return t.shrink(self.cfg.shrink)
+        gone = t.shrink(self.cfg.shrink)
+        if self.mode == "tiered" and self.in_pass and self.engine is not None:
+            self.engine.table.shrink(self.cfg.shrink)
+        return gone
 
     def shrink_resource(self):
         if self.device.type == "cuda":

@@ -66,9 +66,24 @@ STREAM_THREADS = int(os.environ.get("PBX_SAVE_THREADS", str(min(16, os.cpu_count
 last_save_stats: dict = {}
 
 
+def _save_max_cols() -> int:
+    from .. import _native
+
+    return int(getattr(_native.hip(), "kSaveMaxCols", 192))
+
+
 def _streamable(table) -> bool:
     t = getattr(table, "t", None)
-    return t is not None and hasattr(t, "save_stream") and os.environ.get("PBX_SAVE_STREAM", "1") != "0"
+    if t is None or not hasattr(t, "save_stream") or os.environ.get("PBX_SAVE_STREAM", "1") == "0":
+        return False
+    c = getattr(table, "codec", None)
+    # the device-side decode map is a kernel argument of kSaveMaxCols entries:
+    # wider canonical rows (e.g. SparseAdam at large dims) take the export path
+    return c is None or int(c.canon_width) <= _save_max_cols()
+
+
+def _tiered(table) -> bool:
+    return hasattr(table, "save_tiers") and os.environ.get("PBX_SAVE_STREAM", "1") != "0"
 
 
 def _decode_args(table):
@@ -111,6 +126,14 @@ def _write_meta(path: str, dim: int, stride: int, date, world: Optional[int] = N
 
 def save_batch_model(table, path: str, rank: int = 0, date: Optional[str] = None, world: Optional[int] = None) -> int:
     os.makedirs(path, exist_ok=True)
+    if _tiered(table):  # host + SSD tiers, natively streamed
+        n, _ = table.save_tiers(0, 0, False, None, 0.0, 0.0, os.path.join(path, f"part-{rank:05d}.keys.npy"),
+                                os.path.join(path, f"part-{rank:05d}.vals.npy"))
+        last_save_stats.clear()
+        last_save_stats.update(table.last_save)
+        if rank == 0:
+            _write_meta(path, table.dim, int(table.stride), date, world)
+        return n
     if _streamable(table):
         n, _ = _stream(table, 0, 0, False, None, 0.0, 0.0, os.path.join(path, f"part-{rank:05d}.keys.npy"),
                        os.path.join(path, f"part-{rank:05d}.vals.npy"))
@@ -219,6 +242,14 @@ def save_xbox(table, path: str, mode: str, cfg: SaveConfig, nonclk: float, clk: 
     dim = int(codec.DX) if codec is not None else table.dim
     l = row_layout(dim)
     fn = os.path.join(path, f"part-{rank:05d}.txt")
+    if _tiered(table):
+        n, saved = table.save_tiers(1, 1 if mode == "base" else 2, True, cfg, nonclk, clk, fn,
+                                    collect=on_reset is not None)
+        last_save_stats.clear()
+        last_save_stats.update(table.last_save)
+        if on_reset is not None and saved is not None and saved.numel():
+            on_reset(saved)
+        return n
     if _streamable(table):
         n, saved = _stream(table, 1, 1 if mode == "base" else 2, True, cfg, nonclk, clk, fn,
                            collect=on_reset is not None)

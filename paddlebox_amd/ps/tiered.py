@@ -149,6 +149,112 @@ class SsdTier:
         return bool(self._native.direct_io())
 
 
+class TierView:
+    """The tiered sparse model as one table: the host tier plus the SSD log.
+
+    Every key lives in exactly one tier (staging and ``promote`` move SSD rows
+    to the host, spills move host rows to SSD, write-back drops the SSD copy
+    of a key that re-enters the host), so BoxWrapper's model IO and shrink see
+    the whole table -- SaveBase / SaveDelta / load / ShrinkTable over every
+    feature, as the reference PS does (box_wrapper.cc:1286-1318,
+    box_wrapper.h:638; accessor rules ctr_accessor.cc:63-170).
+
+    * saves stream natively (``save_tiers``, csrc/host/tier_save.cc): host
+      shards under their locks, then the SSD log segment by segment; the xbox
+      delta_score reset is applied in place in both tiers;
+    * shrink applies the accessor rule to both tiers (SSD records rewritten in
+      place, deleted ones become tombstones) and compacts the log when under
+      half of it is live;
+    * point operations (probe / read / insert / assign, used by model loads
+      and merges) first promote the keys' SSD rows into the host tier."""
+
+    def __init__(self, host: HostTable, ssd: Optional[SsdTier] = None):
+        self.host = host
+        self.ssd = ssd
+        self.dim = host.dim
+        self.stride = host.stride
+        self.device = torch.device("cpu")
+        self.codec = None  # rows are canonical fp32 in both tiers
+
+    def _ssd_live(self) -> bool:
+        return self.ssd is not None and len(self.ssd) > 0
+
+    def promote(self, h: torch.Tensor) -> int:
+        """Move the SSD rows of keys h into the host tier; returns how many."""
+        if not self._ssd_live():
+            return 0
+        h = h.reshape(-1).cpu()
+        miss = h[self.host.probe(h) < 0]
+        if miss.numel() == 0:
+            return 0
+        found, vals = self.ssd.get(miss)
+        if not bool(found.any()):
+            return 0
+        mk = miss[found]
+        rows, _ = self.host._native.insert(mk)
+        self.host._native.scatter(rows, vals[found])
+        self.ssd.delete(mk)
+        return int(mk.numel())
+
+    def probe(self, h: torch.Tensor, n_dev=None) -> torch.Tensor:
+        self.promote(h)
+        return self.host.probe(h)
+
+    def read(self, h: torch.Tensor) -> torch.Tensor:
+        self.promote(h)
+        return self.host.read(h)
+
+    def insert_mixed(self, h: torch.Tensor, sgd: SparseSGDConfig, init_embedx: bool = False, n_dev=None) -> int:
+        self.promote(h)
+        return self.host.insert_mixed(h, sgd, init_embedx)
+
+    def assign(self, h: torch.Tensor, vals: torch.Tensor):
+        self.promote(h)
+        self.host.assign(h, vals)
+
+    def export(self, with_values: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        """Every row of both tiers, in memory (small tables and tests; saves
+        stream instead)."""
+        k, v = self.host.export(with_values)
+        if not self._ssd_live():
+            return k, v
+        sk = self.ssd.keys()
+        if not with_values:
+            return torch.cat([k, sk]), None
+        _, sv = self.ssd.get(sk)
+        return torch.cat([k, sk]), torch.cat([v, sv])
+
+    def size(self) -> int:
+        return self.host.size() + (len(self.ssd) if self.ssd is not None else 0)
+
+    def shrink(self, cfg: ShrinkConfig) -> int:
+        gone = self.host.shrink(cfg)
+        if self._ssd_live():
+            gone += int(self.ssd._native.shrink(float(cfg.show_click_decay_rate), int(self.host.layout["unseen_days"]),
+                                                float(cfg.nonclk_coeff), float(cfg.clk_coeff),
+                                                float(cfg.delete_threshold), float(cfg.delete_after_unseen_days)))
+            if int(self.ssd._native.live_permille()) < 500:
+                self.ssd.compact(0.5)
+        return gone
+
+    def save_tiers(self, kind: int, mode: int, reset: bool, cfg, nonclk: float, clk: float, keys_path: str,
+                   vals_path: str = "", collect: bool = False):
+        """Native streaming save over both tiers: (rows, mixed keys saved or None)."""
+        import os
+
+        from .config import SaveConfig
+
+        cfg = cfg or SaveConfig()
+        threads = min(16, os.cpu_count() or 4)
+        rows, host_rows, ssd_rows, secs, keys = _native.host().save_tiers(
+            self.host._native, self.ssd._native if self.ssd is not None else None, int(kind), int(mode), bool(reset),
+            float(cfg.base_threshold), float(cfg.delta_threshold), float(cfg.delta_keep_days), float(nonclk),
+            float(clk), float(cfg.embedx_threshold), int(self.dim), keys_path, vals_path, threads, bool(collect))
+        self.last_save = {"rows": int(rows), "host_rows": int(host_rows), "ssd_rows": int(ssd_rows),
+                          "total_s": float(secs), "native": True}
+        return int(rows), keys
+
+
 class TieredStore:
     def __init__(self, engine, host: HostTable, ssd: Optional[SsdTier] = None, sgd: Optional[SparseSGDConfig] = None,
                  spill_unseen: float = 1.0, host_cap_rows: int = 0):
@@ -320,9 +426,14 @@ class TieredStore:
     def _wb_locked(self, kh, vh):
         """Host scatter of the written-back rows, then the SSD spill (holds the tier lock)."""
         self.epoch += 1
-        rows, _ = self.host._native.insert(kh)
+        rows, fresh = self.host._native.insert_fresh(kh)
         self.host._native.scatter(rows, vh)
         self.host._native.stamp(rows, self.epoch)
+        if self.ssd is not None and len(self.ssd) > 0 and bool(fresh.any()):
+            # a key re-entering the host tier may still have a copy on SSD
+            # (spilled by an earlier write-back while its pass was live):
+            # the host row is newer -- one tier per key
+            self.ssd.delete(kh[fresh])
         if self.ssd is not None:
             l = self.host.layout
             t0 = time.perf_counter()

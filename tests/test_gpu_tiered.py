@@ -143,3 +143,52 @@ def test_tiered_codec_matches_hbm_oracle(tmp_path, ftype, opt):
         assert st["spilled"] > 0 and st["ssd_hits"] > 0
     finally:
         BoxWrapper._instance = None
+
+
+def test_tiered_save_load_shrink_cover_ssd(tmp_path):
+    """VERDICT r4 item 1 on the GPU tier: with most rows on SSD (every
+    written-back row spills), SaveBase writes every feature, the batch model
+    loads back into an all-in-HBM table equal to the oracle, the xbox base row
+    sets agree, and ShrinkTable ages / deletes the SSD rows like the oracle."""
+    import numpy as np
+
+    from paddlebox_amd.ps import checkpoint as ck
+
+    try:
+        ob = _box("hbm", 100000)
+        h = _train(ob, overlap=False)
+        exp = ob.engine.table.read(h.to(DEV)).cpu()
+    finally:
+        BoxWrapper._instance = None
+    try:
+        tb = _box("tiered", 2400, ssd=str(tmp_path / "ssd"))
+        _train(tb, overlap=True)
+        tb.tier.wait_writeback()
+        assert len(tb.ssd) >= 0.3 * h.numel()
+        slot = tb.host.layout["slot"]
+        keep = [c for c in range(exp.shape[1]) if c != slot]
+        tb.save_base(str(tmp_path / "t_batch"), str(tmp_path / "t_xbox"))
+        assert ck.last_save_stats["ssd_rows"] > 0
+        ob.save_base(str(tmp_path / "o_batch"), str(tmp_path / "o_xbox"))
+        tk = np.load(str(tmp_path / "t_batch" / "part-00000.keys.npy"), allow_pickle=False)
+        assert tk.shape[0] == h.numel()
+        tx, _ = ck.load_xbox_text(str(tmp_path / "t_xbox" / "part-00000.txt"), 8)
+        ox, _ = ck.load_xbox_text(str(tmp_path / "o_xbox" / "part-00000.txt"), 8)
+        assert np.array_equal(np.sort(tx), np.sort(ox))
+        BoxWrapper._instance = None
+        lb = _box("hbm", 100000)
+        assert lb.load_model(str(tmp_path / "t_batch")) == h.numel()
+        got = lb.engine.table.read(h.to(DEV)).cpu()
+        torch.testing.assert_close(got[:, keep], exp[:, keep], rtol=1e-5, atol=1e-6)
+        # shrink over host + SSD vs the HBM oracle's shrink
+        for b in (tb, ob):
+            b.cfg.shrink.delete_threshold = 0.5
+        g1, g2 = tb.shrink_table(), ob.shrink_table()
+        assert g1 == g2 > 0
+        th, tv = tb._authoritative().export(True)
+        oh, ov = ob.engine.table.export(True)
+        assert torch.equal(torch.sort(th).values, torch.sort(oh.cpu()).values)
+        to, oo = torch.argsort(th), torch.argsort(oh.cpu())
+        torch.testing.assert_close(tv[to][:, keep], ov.cpu()[oo][:, keep], rtol=1e-5, atol=1e-6)
+    finally:
+        BoxWrapper._instance = None
