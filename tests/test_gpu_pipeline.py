@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 
 
-def _setup(seed_batches=7, ring=3):
+def _setup(seed_batches=7, ring=3, n_batches=8):
     from paddlebox_amd.data.synthetic import CriteoSynth
     from paddlebox_amd.ops import reference as ref
     from paddlebox_amd.ps.config import PSConfig
@@ -20,7 +20,7 @@ def _setup(seed_batches=7, ring=3):
     from paddlebox_amd.runtime.graph_step import pack_batch
 
     synth = CriteoSynth(total_features=200_000, alpha=1.1, seed=seed_batches, device="cpu")
-    bs = [synth.batch(512) for _ in range(8)]
+    bs = [synth.batch(512) for _ in range(n_batches)]
     S = bs[0].S
     eng = SparseEngine(PSConfig(embedx_dim=8), max_keys=512 * S, device=DEV, capacity=300_000,
                        slot_ids=[float(s + 1) for s in range(S)], pull_ring=ring)
@@ -30,11 +30,21 @@ def _setup(seed_batches=7, ring=3):
     return eng, hbs, S
 
 
-def _train(pipeline: bool, precision: str, K: int = 1):
+def _train(pipeline: bool, precision: str, K: int = 1, n_batches: int = 8):
+    eng, hbs, S = _setup(ring=3 * K, n_batches=n_batches)
+    flat, losses = _run(eng, hbs, S, pipeline, precision, K)
+    hk, v = eng.table.export(True)
+    o = torch.argsort(hk)
+    return flat, losses, hk[o].cpu(), v[o].cpu()
+
+
+def _run(eng, hbs, S, pipeline: bool, precision: str, K: int = 1):
+    """One training program over the engine: warm batch 0 eagerly, then the
+    rest of the batches through the graphed step (K steps per graph)."""
     from paddlebox_amd.runtime.ctr_step import CtrTrainStep
     from paddlebox_amd.runtime.graph_step import GraphedTrainStep
 
-    eng, hbs, S = _setup(ring=3 * K)
+    eng.clear_prefetch(reset_rows=True)
     torch.manual_seed(0)
     step = CtrTrainStep(eng, "deepfm", precision, num_slots=S, hidden=(64, 64, 64))
     pipe = (lambda b, j: step.prefetch(b, j), step.set_next, eng.clear_prefetch) if pipeline else None
@@ -63,12 +73,13 @@ def _train(pipeline: bool, precision: str, K: int = 1):
             out = g.run(q % g.n)
             torch.cuda.synchronize()
             losses.append(float(out))
-    hk, v = eng.table.export(True)
-    o = torch.argsort(hk)
-    return step.arena.flat.cpu(), losses, hk[o].cpu(), v[o].cpu()
+    flat = step.arena.flat.cpu()
+    del g, step
+    return flat, losses
 
 
-@pytest.mark.parametrize("precision,K,split,overlap,fs", [("fp32", 1, "0", "0", "0"), ("bf16", 1, "0", "0", "0"),
+@pytest.mark.parametrize("precision,K,split,overlap,fs", [("fp32", 3, "0", "0", "0"), ("fp32", 4, "0", "0", "0"),
+                                                          ("fp32", 1, "0", "0", "0"), ("bf16", 1, "0", "0", "0"),
                                                           ("fp32", 2, "0", "0", "0"), ("fp32", 1, "2", "0", "0"),
                                                           ("fp32", 2, "1", "0", "0"), ("fp32", 2, "0", "1", "0"),
                                                           ("bf16", 2, "0", "1", "0"), ("fp32", 2, "3", "0", "0"),
@@ -79,14 +90,37 @@ def test_pipelined_front_matches_plain_graphed_step(precision, K, split, overlap
     # forked at the dX chain (1) or after the head backward (2)); overlap:
     # Adam on the dW side stream, the next head not waiting for it
     # (PBX_ADAM_OVERLAP, the step's side work joined by the next step)
-    f0, l0, k0, v0 = _train(False, precision, K)
+    nb = 1 + 3 * K if K > 2 else 8  # K = 3, 4 (bench's default): three graphs of K steps
+    f0, l0, k0, v0 = _train(False, precision, K, nb)
     monkeypatch.setenv("PBX_SPLIT_PREFETCH", split)
     monkeypatch.setenv("PBX_ADAM_OVERLAP", overlap)
     monkeypatch.setenv("PBX_FUSED_SCATTER", fs)  # the dedup scatter inside the prefetched pooling launch
-    f1, l1, k1, v1 = _train(True, precision, K)
+    f1, l1, k1, v1 = _train(True, precision, K, nb)
     # the dW split-K atomics sum in any order: fp32-rounding-level differences
     rt, at = (1e-6, 1e-7) if precision == "fp32" else (1e-4, 1e-5)
     assert l1 == pytest.approx(l0, rel=rt, abs=at)
     torch.testing.assert_close(f1, f0, rtol=rt, atol=at)
     assert torch.equal(k1, k0)
     torch.testing.assert_close(v1, v0, rtol=rt, atol=at)
+
+
+def test_pipelined_program_then_plain_multistep_on_same_engine():
+    """bench.py runs a pipelined K = 4 fp32 program and then
+    other programs (bf16 K = 2, plain) over the SAME engine.  No pull-ring
+    reset between them: the second program must train exactly like a fresh
+    plain sequence (fp32 K = 1 then bf16 K = 1) from the same initial state."""
+    eng, hbs, S = _setup(ring=12, n_batches=13)
+    _, la = _run(eng, hbs, S, True, "fp32", 4)
+    fb, lb = _run(eng, hbs, S, False, "bf16", 2)
+    ha, va = eng.table.export(True)
+    del eng
+    ref_eng, hbs2, _ = _setup(ring=12, n_batches=13)
+    _, lc = _run(ref_eng, hbs2, S, False, "fp32", 1)
+    fd, ld = _run(ref_eng, hbs2, S, False, "bf16", 1)
+    hr, vr = ref_eng.table.export(True)
+    assert la == pytest.approx(lc[:1] + lc[4::4], rel=1e-5, abs=1e-6)
+    assert lb == pytest.approx(ld[:1] + ld[2::2], rel=2e-3, abs=1e-4)
+    torch.testing.assert_close(fb, fd, rtol=2e-3, atol=1e-4)
+    oa, orr = torch.argsort(ha), torch.argsort(hr)
+    assert torch.equal(ha[oa], hr[orr])
+    torch.testing.assert_close(va[oa], vr[orr], rtol=2e-3, atol=1e-4)
