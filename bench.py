@@ -310,11 +310,6 @@ def main():
         # the pull slots' occurrence rows are all -1 again (a pipelined run
         # leaves rows there, which a split pull must not read as occurrences)
         engine.clear_prefetch(reset_rows=True)
-        if not primary:
-            # a secondary after a pipelined multi-step headline faulted in its
-            # sparse push on the box (twice; cause not isolated): it starts
-            # from fresh pull slots and push scratch, like a new program
-            engine.reset_pull_ring()
         if dcn and mlp_dtype == "fp32":
             raise SystemExit("DCN-V2 (BASELINE config 5) is a bf16-MLP config: run it with --mlp-dtype bf16")
         auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
@@ -359,10 +354,10 @@ def main():
         train_step = step.train_step
 
         nb = len(host_batches)
-        # the headline takes K steps per graph; the same-run secondaries keep
-        # one (a bf16 K = 2 run after the pipelined fp32 one faulted on the
-        # box at 200 steps -- under investigation; K = 1 is the validated path)
-        K = graph_steps_for(args.steps, args.warmup, args.graph_steps, world) if primary else 1
+        # every measurement (headline and same-run secondaries) takes K steps
+        # per graph over the same engine (tests/test_gpu_pipeline.py: a
+        # pipelined K = 4 program followed by a plain K = 2 one)
+        K = graph_steps_for(args.steps, args.warmup, args.graph_steps, world)
         graphed = None
         if args.graph:
             try:
@@ -539,6 +534,9 @@ def main():
                     log(rank, f"[bench] host-diag {name} window {w}: host {th / args.steps * 1e3:.4f} "
                               f"wall {tw / args.steps * 1e3:.4f} ms/step")
 
+        # the kernels' index guards (skipped + recorded, never followed) must
+        # not have tripped anywhere in this measurement
+        engine.check_guards()
         res = dict(dt=dt, t_enq=t_enq, graph_steps=K, loss=float(loss) if loss is not None else float("nan"),
                    auc_stats=auc_stats.clone(), ipc=ipc,
                    prefetch=bool(graphed is not None and graphed.prefetch is not None),

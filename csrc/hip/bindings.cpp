@@ -65,6 +65,7 @@ class GpuTable {
     values_ = torch::zeros({(int64_t)nb_ * kBucketSlots + stash_cap_, stride_}, optf);
     stash_keys_ = torch::full({std::max<int64_t>(stash_cap_, 1)}, -1, opt8);
     scratch_ = torch::zeros({8}, opt8);  // [stash_n, ovf_n, fail_n, count, cursor...]
+    err_ = torch::zeros({1}, opt4);       // guard bits (TableDev::err), sticky until clear_error
   }
   TableDev view() const {
     TableDev t;
@@ -77,8 +78,12 @@ class GpuTable {
     t.stash_cap = (uint32_t)stash_cap_;
     t.stride = stride_;
     t.dim = dim_;
+    t.err = ptr<int32_t>(err_);
     return t;
   }
+  // guard bits the kernels recorded (a device read: call outside captures)
+  int64_t error_bits() const { return err_.cpu().item<int32_t>(); }
+  void clear_error() { err_.zero_(); }
   Tensor probe(const Tensor& h, const c10::optional<Tensor>& n_dev) {
     check_cuda(h, "h");
     auto rows = torch::empty({h.numel()}, h.options().dtype(torch::kInt64));
@@ -360,6 +365,7 @@ class GpuTable {
     a.bs_scale = bs_scale;
     a.dim = dim_;
     a.embed_thres_size = use_cvm ? 0 : embed_thres_size;
+    a.err = ptr<int32_t>(err_);
     return launch_push_merge_apply(a, view(), ptr<int64_t>(rows), fused ? nullptr : ptr<int32_t>(inc),
                                    fused ? reinterpret_cast<unsigned long long*>(ptr<int64_t>(inc)) : nullptr, cfg,
                                    seed, cur_stream());
@@ -435,7 +441,7 @@ class GpuTable {
   uint64_t nb_;
   int64_t stash_cap_;
   int64_t last_overflow_ = 0;
-  Tensor keys_, fill_, values_, stash_keys_, scratch_;
+  Tensor keys_, fill_, values_, stash_keys_, scratch_, err_;
   Tensor lock_, lead_;  // owner_push: per-row leader word (-1 = free), per-record leader
   Tensor cnt_row_, uid_row_;  // table dedup scratch (dedup_rows)
   int pad_col_ = -1;          // in-row dedup counter column (-1: cnt_row_)
@@ -1288,6 +1294,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("last_overflow", &GpuTable::last_overflow)
       .def("size", &GpuTable::size)
       .def("stash_n", &GpuTable::stash_n)
+      .def("error_bits", &GpuTable::error_bits)
+      .def("clear_error", &GpuTable::clear_error)
       .def("probe_into", &GpuTable::probe_into)
       .def("export_all", &GpuTable::export_all)
       .def("assign", &GpuTable::assign)

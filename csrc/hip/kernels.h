@@ -25,7 +25,14 @@ struct TableDev {
   uint32_t stash_cap = 0;
   int stride = 16;  // floats per row
   int dim = 8;      // embedx dim
+  // sticky guard bits (device int32): an index a kernel is about to follow
+  // that lies outside its buffer -- a table row past the table, a unique id
+  // past the batch -- is skipped and recorded here instead of becoming a
+  // wild access; SparseEngine.check_overflow raises on it (bits: 1 table row
+  // of a push, 2 dedup unique id, 4 dedup perm slot, 8 push occurrence / id)
+  int32_t* err = nullptr;
 };
+PBX_HD int64_t table_rows(const TableDev& t) { return (int64_t)t.nb * kBucketSlots + (int64_t)t.stash_cap; }
 
 // rows[i] = row id of h[i] or -1.  n_dev (optional) = device-side count.
 void launch_table_probe(const TableDev& t, const uint64_t* h, int64_t n, const int32_t* n_dev,
@@ -198,6 +205,7 @@ struct PushMergeArgs {
   float bs_scale = 1.f;              // multiply embed grads by -bs_scale
   int dim = 8;
   int embed_thres_size = 0;          // use_cvm = 0: leading embed columns dropped from the output
+  int32_t* err = nullptr;            // guard bits (TableDev::err)
 };
 void launch_push_merge(const PushMergeArgs& a, hipStream_t s);
 // Owner-side merge of received push records rec[j] (j over n entries) keyed by

@@ -572,7 +572,12 @@ struct ApplyEmit {
   template <int D>
   __device__ __forceinline__ void emit(int32_t u, const float* rec) const {
     const int64_t r = rows[u];
-    if (r >= 0) adagrad_row<D>(t.values + r * (int64_t)t.stride, rec, cfg, seed, table_row_key(t, r));
+    if (r < 0) return;
+    if (r >= table_rows(t)) {  // corrupted row: recorded, never written
+      if (t.err) atomicOr(t.err, 1);
+      return;
+    }
+    adagrad_row<D>(t.values + r * (int64_t)t.stride, rec, cfg, seed, table_row_key(t, r));
   }
 };
 struct SendEmit {
@@ -614,7 +619,14 @@ __global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, Emit e
   for (int c = 0; c < Q; ++c) g[c] = 0.f;
   if (p < pv) {
     k = a.perm[p];
-    u = a.uid[k];
+    u = (k >= 0 && k < a.n) ? a.uid[k] : -2;
+    if (u < -1 || u >= a.n) {  // an occurrence / unique id outside the batch
+      if (a.err) atomicOr(a.err, 8);
+      u = -1;
+      k = -1;
+    }
+  }
+  if (k >= 0) {
     if (src.fast(D))
       src.template load_fast<D>(k, g);
     else
@@ -631,8 +643,12 @@ __global__ __launch_bounds__(256) void k_push_merge_apply(DoutSource src, Emit e
   }
   const int32_t u_first = __shfl(u, 0), u_last = __shfl(u, 63);
   int cn = 0, cp = 0;
-  if (lane == 63 && p + 1 < pv) cn = a.uid[a.perm[p + 1]] == u;
-  if (lane == 0 && wave_base > 0) cp = a.uid[a.perm[wave_base - 1]] == u;
+  auto uid_at = [&](int64_t q) {
+    const int32_t kq = a.perm[q];
+    return (kq >= 0 && kq < a.n) ? a.uid[kq] : -1;
+  };
+  if (lane == 63 && p + 1 < pv) cn = uid_at(p + 1) == u && u >= 0;
+  if (lane == 0 && wave_base > 0) cp = uid_at(wave_base - 1) == u && u >= 0;
   const int cont_next = __shfl(cn, 63), cont_prev = __shfl(cp, 0);
   if (!FUSED && lane == 63) inc[wave_base >> 6] = (cont_next && !(cont_prev && u_first == u_last)) ? u_last : -1;
   const int32_t un = __shfl_down(u, 1);

@@ -254,7 +254,8 @@ __global__ __launch_bounds__(256) void k_table_seg(const int64_t* __restrict__ r
 __global__ void k_table_scatter(int64_t* __restrict__ rows_occ, const int32_t* __restrict__ rank,
                                 const int32_t* __restrict__ uid_row, const int32_t* __restrict__ seg, int64_t n,
                                 int32_t* __restrict__ uid, int32_t* __restrict__ perm, int reset_rows,
-                                int32_t* __restrict__ acc, int32_t* __restrict__ u_count) {
+                                int32_t* __restrict__ acc, int32_t* __restrict__ u_count,
+                                const int64_t* __restrict__ rows_u, int32_t* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < 4) {  // publish the counters, leave the accumulator zero for the next dedup
     u_count[i] = acc[i];
@@ -268,8 +269,21 @@ __global__ void k_table_scatter(int64_t* __restrict__ rows_occ, const int32_t* _
     return;
   }
   const int32_t u = uid_row[r];
+  // a row whose dedup counter was not zero at the dedup's start has no unique
+  // id of this batch (its uid_row entry is stale): skipped and recorded
+  if (u < 0 || u >= n) {
+    uid[i] = -1;
+    if (err) atomicOr(err, 2);
+    return;
+  }
+  const int64_t q = (int64_t)seg[u] + rank[i];
+  if (q < 0 || q >= n || rows_u[u] != r) {
+    uid[i] = -1;
+    if (err) atomicOr(err, 4);
+    return;
+  }
   uid[i] = u;
-  perm[seg[u] + rank[i]] = (int32_t)i;
+  perm[q] = (int32_t)i;
 }
 
 // Owner side of the sharded pull in one launch: probe every received key (one
@@ -569,7 +583,7 @@ void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64
     hipLaunchKernelGGL(k_table_seg<4>, dim3(blocks_for(n, 1024)), dim3(256), 0, s, rows_u, cnt_row, cnt_rs, acc, seg);
   if (!do_scatter) return;  // the caller's seqpool launch scatters (SeqpoolCvmArgs.sc_*)
   hipLaunchKernelGGL(k_table_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, s, rows_occ, rank, uid_row, seg, n, uid,
-                     perm, rows_given ? 1 : 0, acc, u_count);
+                     perm, rows_given ? 1 : 0, acc, u_count, rows_u, t.err);
 }
 
 void launch_probe_gather(const TableDev& t, const uint64_t* h, int64_t n, int64_t* rows, float* out, int out_stride,

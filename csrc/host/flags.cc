@@ -48,6 +48,9 @@ void register_default_flags() {
   f.define("padbox_max_keys_per_batch", "0", "override engine key capacity (0 = auto)");
   f.define("padbox_device_pass", "true", "keep the pass's record store in HBM and assemble batches on the GPU");
   f.define("padbox_device_pass_max_gb", "64", "largest pass (GB of HBM) kept device-resident");
+  f.define("padbox_fc_precision", "fp32", "fluid fc chains: fp32 (exact, reference) or bf16 MFMA operands");
+  f.define("padbox_train_steps_per_graph", "0", "graphed train loop: training steps per HIP graph (0 = auto)");
+  f.define("padbox_pipelined_front", "true", "graphed train loop: pool the next batch after the sparse push");
 }
 
 }  // namespace pbx

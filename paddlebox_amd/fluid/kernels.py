@@ -679,6 +679,14 @@ def k_fused_seq_tensor(ctx, op):
 
 
 # ----------------------------------------------------------------- lowered dense chains
+def _fc_fp32() -> bool:
+    """FLAGS_padbox_fc_precision: fp32 (default, the reference fc precision,
+    python/paddle/fluid/layers/nn.py:243) or bf16 MFMA operands."""
+    from ..utils import flags as _flags
+
+    return _flags.get("padbox_fc_precision").lower() != "bf16"
+
+
 def _tower_for(ctx, op, C: int):
     """CtrTower bound to the session's dense storage (fc weights already in
     the [out, in] padded layout the tower packs from) and data_norm summaries."""
@@ -711,7 +719,9 @@ def _tower_for(ctx, op, C: int):
     dn.stats = torch.zeros(3 * C, device=ctx.device)
     dn.update_norm = a.get("update_norm", True) is not False
     dn.group = _stats_group(ctx)
-    t = CtrTower(mlp, dn, 0, 1, 0, 0, use_head_lin=False)
+    # the reference fc precision by default (FLAGS_padbox_fc_precision):
+    # the lowering only forms the tower when the fp32 tower takes its widths
+    t = CtrTower(mlp, dn, 0, 1, 0, 0, use_head_lin=False, fp32=_fc_fp32())
     if ctx.training and hasattr(ctx.s, "on_tower_grads"):
         t.on_dense_grads = lambda: ctx.s.on_tower_grads(t)
     ctx.cache[key] = t
@@ -732,15 +742,18 @@ def k_ctr_tower(ctx, op):
 @kernel("__fused_mlp")
 def k_fused_mlp(ctx, op):
     """Lowered fc(relu)^n [-> fc(size 1)] chain on the MFMA GEMM kernels."""
-    from ..ops.mlp import fused_mlp
+    from ..ops.mlp import fused_mlp, fused_mlp_fp32
 
     x = _val(ctx.get(op.inputs["X"][0]))
     ws = [ctx.storage(v) for v in op.inputs["W"]]
     bs = [ctx.storage(v) for v in op.inputs["B"]]
     wo = ctx.storage(op.inputs["WOut"][0]) if op.inputs.get("WOut") else None
     bo = ctx.storage(op.inputs["BOut"][0]) if op.inputs.get("BOut") else None
-    cache = ctx.cache.setdefault(id(op), [])
-    y = fused_mlp(x, ws, bs, wo, bo, cache)
+    if _fc_fp32():  # the reference fc precision: library fp32 GEMMs
+        y = fused_mlp_fp32(x, ws, bs, wo, bo)
+    else:
+        cache = ctx.cache.setdefault(id(op), [])
+        y = fused_mlp(x, ws, bs, wo, bo, cache)
     if wo is not None:
         y = y.view(-1, 1)
     else:

@@ -15,10 +15,18 @@ by the fused MI355X kernels:
 4. (GPU) ``data_norm -> __fused_mlp -> sigmoid / log-loss / mean``  =>
    ``__ctr_tower`` (the fused CTR tower of the DeepFM bench, ops/tower.py).
 3. (GPU) ``fc(relu) -> ... -> fc(relu) [-> fc(size=1)]`` chains  =>
-   ``__fused_mlp``: bf16 MFMA GEMMs with fused bias/ReLU epilogues, a GEMV
-   logit head, ReLU-mask prologues and split-K dW/db in the backward.  The
-   fc weights of a fused chain are stored ``[out, in]`` (padded to 8) in the
-   dense arena; the scope exposes the logical ``[in, out]`` view.
+   ``__fused_mlp``: at the reference fc precision (fp32, default) one
+   library fp32 GEMM per layer with the gradients accumulated into the arena;
+   with FLAGS_padbox_fc_precision=bf16, bf16 MFMA GEMMs with fused bias/ReLU
+   epilogues, a GEMV logit head, ReLU-mask prologues and split-K dW/db in the
+   backward.  The fc weights of a fused chain are stored ``[out, in]``
+   (padded to 8) in the dense arena; the scope exposes the logical
+   ``[in, out]`` view.
+
+The tower (4) runs the exact-fp32 MFMA tower (csrc/hip/tower32.hip) at fp32
+and the bf16-operand tower at bf16; at fp32 it is formed only when the fp32
+tower's LDS budget takes the chain's widths (ops/mlp.py tower_fp32_fits),
+otherwise the chain stays on the fp32 ``__fused_mlp``.
 """
 from __future__ import annotations
 
@@ -197,7 +205,7 @@ def _fuse_mlp(ops: List[Operator], fetch: set, storage: Dict[str, StorageSpec], 
     return [op for k, op in enumerate(out) if k not in removed]
 
 
-def _fuse_tower(ops: List[Operator], fetch: set, notes: List[str]):
+def _fuse_tower(ops: List[Operator], fetch: set, notes: List[str], fp32: bool = True):
     """(GPU) data_norm -> __fused_mlp(+logit head) -> {sigmoid, sigmoid_cross_
     entropy_with_logits -> reduce_mean}  =>  ``__ctr_tower``: the fused CTR
     tower (csrc/hip/tower.hip: data_norm head, MFMA MLP with activations kept
@@ -238,6 +246,12 @@ def _fuse_tower(ops: List[Operator], fetch: set, notes: List[str]):
         lab = xe.inputs["Label"][0].name
         if produced_at.get(lab, -1) >= m:
             continue
+        if fp32:
+            from ..ops.mlp import tower_fp32_fits
+
+            widths = [mop.inputs["W"][0].shape[0]] + [w.shape[1] for w in mop.inputs["W"]]
+            if not tower_fp32_fits([pad8(w) for w in widths]):
+                continue
         ins = {"X": dop.inputs["X"], "Label": xe.inputs["Label"], "W": mop.inputs["W"], "B": mop.inputs["B"],
                "WOut": mop.inputs["WOut"], "BOut": mop.inputs["BOut"],
                "BatchSize": dop.inputs["BatchSize"], "BatchSum": dop.inputs["BatchSum"],
@@ -264,8 +278,10 @@ def lower(program: Program, fetch_names=(), gpu: bool = True, engine_cvm_offset:
         ops = _fuse_pull_seqpool(ops, fetch, engine_cvm_offset, notes)
         ops = _absorb_concat(ops, notes)
         if gpu:
+            from .kernels import _fc_fp32
+
             ops = _fuse_mlp(ops, fetch, storage, notes)
-            ops = _fuse_tower(ops, fetch, notes)
+            ops = _fuse_tower(ops, fetch, notes, fp32=_fc_fp32())
     for op in ops + bwd + opt:
         if op.type not in KERNELS:
             raise NotImplementedError(f"no kernel for op '{op.type}'")

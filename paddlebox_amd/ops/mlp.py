@@ -112,6 +112,65 @@ def fused_mlp(x: torch.Tensor, ws: Sequence[torch.Tensor], bs: Sequence[torch.Te
     return _MLPFn.apply(x.contiguous(), list(ws), list(bs), w_out, b_out, cache, k_split, *params)
 
 
+class _MLP32Fn(torch.autograd.Function):
+    """Exact-fp32 fc(relu) chain on library fp32 GEMMs (the reference fc
+    precision, python/paddle/fluid/layers/nn.py:243 -> mul / matmul) for the
+    lowered chains the fused fp32 tower does not take.  Same contract as
+    _MLPFn: W [N, K] storage (K zero padded), gradients accumulated straight
+    into ``p.grad`` (dense-arena views)."""
+
+    @staticmethod
+    def forward(ctx, x, ws, bs, w_out, b_out, *params):
+        hs = [x]
+        cur = x
+        for w, b in zip(ws, bs):
+            cur = torch.relu(torch.addmm(b.detach(), cur, w.detach().t()))
+            hs.append(cur)
+        ctx.ws, ctx.bs, ctx.w_out, ctx.b_out, ctx.hs = ws, bs, w_out, b_out, hs
+        ctx.x_needs_grad = x.requires_grad
+        ctx.n_params = len(params)
+        if w_out is not None:
+            return torch.addmm(b_out.detach(), cur, w_out.detach().t()).view(-1)
+        return cur
+
+    @staticmethod
+    def backward(ctx, dout):
+        hs = ctx.hs
+        if ctx.w_out is not None:
+            g = dout.float().reshape(-1, 1)
+            _ensure_grad(ctx.w_out).add_(g.t() @ hs[-1])
+            _ensure_grad(ctx.b_out).add_(g.sum(0))
+            dh = g @ ctx.w_out.detach()
+        else:
+            dh = dout.float()
+        for i in reversed(range(len(ctx.ws))):
+            dh = dh * (hs[i + 1] > 0)
+            _ensure_grad(ctx.ws[i]).add_(dh.t() @ hs[i])
+            _ensure_grad(ctx.bs[i]).add_(dh.sum(0))
+            if i > 0 or ctx.x_needs_grad:
+                dh = dh @ ctx.ws[i].detach()
+        ctx.hs = None
+        dx = dh if ctx.x_needs_grad else None
+        return (dx,) + (None,) * (4 + ctx.n_params)
+
+
+def fused_mlp_fp32(x: torch.Tensor, ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor],
+                   w_out: Optional[torch.Tensor], b_out: Optional[torch.Tensor]) -> torch.Tensor:
+    """fp32 twin of fused_mlp: x [M, K0] zero-padded to ws[0].shape[1]."""
+    x = x.float()
+    if x.shape[1] != ws[0].shape[1]:
+        x = torch.nn.functional.pad(x, (0, ws[0].shape[1] - x.shape[1]))
+    params = list(ws) + list(bs) + ([w_out, b_out] if w_out is not None else [])
+    return _MLP32Fn.apply(x.contiguous(), list(ws), list(bs), w_out, b_out, *params)
+
+
+def tower_fp32_fits(widths: Sequence[int]) -> bool:
+    """The exact-fp32 tower's LDS budget (FusedMLP.tower_fp32_ok) for the
+    padded layer widths [in, hidden...]."""
+    p16 = [(w + 15) // 16 * 16 for w in widths]
+    return max(widths) <= 464 or (max(widths) <= 512 and all(p % 128 == 0 for p in p16))
+
+
 class FusedMLP(nn.Module):
     def __init__(self, in_dim: int, hidden: Sequence[int], out_dim: int = 1):
         super().__init__()
@@ -166,9 +225,7 @@ class FusedMLP(nn.Module):
         remainder partial sums of its wave-stream schedule when a width is not
         a multiple of 128: widths <= 464, or <= 512 when all are multiples of
         128 (bindings_tower.cpp checks the exact budget)."""
-        ws = [self.in_dim] + list(self.hidden)
-        p16 = [(w + 15) // 16 * 16 for w in ws]
-        return max(ws) <= 464 or (max(ws) <= 512 and all(p % 128 == 0 for p in p16))
+        return tower_fp32_fits([self.in_dim] + list(self.hidden))
 
     def ensure_packed(self):
         if not self._packed or not self.packed_by_optimizer:

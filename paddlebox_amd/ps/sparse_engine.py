@@ -948,8 +948,23 @@ class SparseEngine:
             self.slot_ids = torch.arange(S, dtype=torch.float32, device=self.device)
         return self.slot_ids
 
+    GUARD_BITS = {1: "push: table row outside the table", 2: "dedup: row without a unique id of its batch",
+                  4: "dedup: perm slot outside the batch", 8: "push: occurrence / unique id outside the batch"}
+
+    def check_guards(self):
+        """Raise if a kernel met an out-of-range index (skipped, not followed:
+        TableDev::err).  A device read: call outside graph captures."""
+        if not self.is_gpu:
+            return
+        bits = int(self.table.t.error_bits())
+        if bits:
+            self.table.t.clear_error()
+            what = "; ".join(v for b, v in self.GUARD_BITS.items() if bits & b)
+            raise RuntimeError(f"sparse engine index guard tripped (bits {bits:#x}): {what}")
+
     def check_overflow(self) -> bool:
         self.check_exchange()
+        self.check_guards()
         if self.sharded and self.is_gpu:
             return bool(self.overflow.item())
         return False

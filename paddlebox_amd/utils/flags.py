@@ -20,6 +20,15 @@ design (documented, not silently ignored):
   ``BoxWrapper.initialize_auc_runner`` (``auc_runner_mode()`` reports it).
 * ``padbox_enable_sharding_stage`` -- optimizer-state sharding is chosen by
   the fleet strategy / ``ShardedFlatAdam``.
+* ``padbox_fc_precision`` (this engine's, not the reference's) -- operand
+  precision of the fluid ``fc`` chains the lowering fuses: ``fp32`` (default,
+  the reference fc precision: the exact-fp32 MFMA tower, or library fp32
+  GEMMs for chains the tower does not take) or ``bf16`` (bf16 MFMA operands,
+  fp32 accumulate).
+* ``padbox_train_steps_per_graph`` / ``padbox_pipelined_front`` (this
+  engine's) -- the graphed ``train_from_dataset`` loop: training steps per
+  captured HIP graph (0 = auto) and the pipelined front (each step pools the
+  next batch right after its sparse push).
 * ``padbox_dataset_merge_thread_num`` -- feed-pass keys are registered by
   the loader threads themselves (KeyAgent); their count comes from
   ``set_thread``.  (``padbox_dataset_shuffle_thread_num`` is live: the
@@ -71,6 +80,9 @@ _DEFAULTS: Dict[str, str] = {
     "padbox_max_keys_per_batch": "0",
     "padbox_device_pass": "true",
     "padbox_device_pass_max_gb": "64",
+    "padbox_fc_precision": "fp32",
+    "padbox_train_steps_per_graph": "0",
+    "padbox_pipelined_front": "true",
 }
 _py: Dict[str, str] = {k: os.environ.get("FLAGS_" + k, v) for k, v in _DEFAULTS.items()}
 
