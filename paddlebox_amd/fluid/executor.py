@@ -153,6 +153,38 @@ class Session:
         self.box = box
         self._one = None
         self.op_profiler = None  # runtime.op_profiler.OpProfiler in the trainer's profile mode
+        # pipelined front (graphed train loop): (batch, pull slot) pooled right
+        # after this step's sparse push, so the next step starts at the dense head
+        self._next = None
+
+    # -------------------------------------------------------------- pipelined front
+    def pipeline_pull_op(self):
+        """The program's single fused pull op when the pipelined front applies
+        (a GPU engine that can prepare pulls, the pull's dense columns are data
+        variables of the batch), else None."""
+        pulls = [op for op in self.lowered.steps if op.type == "__pull_seqpool_cvm"]
+        eng = getattr(self.box, "engine", None) if self.box is not None else None
+        if len(pulls) != 1 or eng is None or not eng.can_prefetch_pull() or not self.training:
+            return None
+        data = {v.name for v in self.data_vars}
+        if any(v.name not in data for v in pulls[0].inputs.get("Dense", [])):
+            return None
+        return pulls[0]
+
+    def set_next(self, batch, slot: int = 0):
+        """Batch to pool at the end of each step (None: none)."""
+        self._next = None if batch is None else (batch, int(slot))
+
+    def prefetch(self, batch, slot: int) -> bool:
+        """Pool ``batch`` for its step now, into pull slot ``slot``."""
+        from .kernels import prefetch_pull_op
+
+        op = self.pipeline_pull_op()
+        if op is None:
+            return False
+        ctx = ExecContext(self, batch, training=True)
+        self.feed_batch(ctx, batch)
+        return prefetch_pull_op(ctx, op, slot)
 
     # -------------------------------------------------------------- params
     def _materialize(self):
@@ -382,6 +414,10 @@ class Session:
             loss.backward(self._one)  # persistent seed: no fill kernel per step
         else:
             loss.float().sum().backward()
+        if self._next is not None:
+            # the sparse push is on this stream already: pool the next batch
+            # now, beside the tower's dW GEMM on its side stream
+            self.prefetch(*self._next)
         if prof is not None:
             prof.end("backward (all grad ops + sparse push)", t0)
             t0 = prof.begin()

@@ -457,9 +457,9 @@ def k_pull_box_sparse(ctx, op):
         ctx.set(v, Ragged(recs[a:e], lod2[s] - a, B, s))
 
 
-@kernel("__pull_seqpool_cvm")
-def k_pull_seqpool_cvm(ctx, op):
-    """Lowered pull_box_sparse -> fused_seqpool_cvm (-> concat) chain."""
+def _pull_op_args(ctx, op):
+    """(keys, lod, B, S, SeqpoolParams, dense or None) of a __pull_seqpool_cvm
+    op over the batch bound to ctx."""
     keys, lod, B, S = _sparse_inputs(ctx, op.inputs["Ids"])
     a = op.attrs
     sp = SeqpoolParams(use_cvm=a["use_cvm"], cvm_offset=a["cvm_offset"], clk_filter=a["clk_filter"],
@@ -467,10 +467,25 @@ def k_pull_seqpool_cvm(ctx, op):
                        clk_coeff=a["clk_coeff"], threshold=a["threshold"], quant_ratio=a["quant_ratio"],
                        embed_threshold_filter=a["embed_threshold_filter"], embed_threshold=a["embed_threshold"],
                        embed_thres_size=a["embed_thres_size"])
-    cvm = _val(ctx.get(op.inputs["CVM"][0])).float().contiguous()
     dense = None
     if op.inputs.get("Dense"):
         dense = torch.cat([_val(ctx.get(v)).float().reshape(B, -1) for v in op.inputs["Dense"]], 1)
+    return keys, lod, B, S, sp, dense
+
+
+def prefetch_pull_op(ctx, op, slot: int) -> bool:
+    """Pool the batch bound to ctx for a __pull_seqpool_cvm op ahead of its
+    step (the pipelined front: SparseEngine.prefetch_pull into pull slot
+    ``slot``); that step's pull then launches nothing."""
+    keys, lod, B, S, sp, dense = _pull_op_args(ctx, op)
+    return sparse_ops.prefetch_seqpool_cvm_concat(ctx.engine, keys, lod, B, S, dense, sp, slot)
+
+
+@kernel("__pull_seqpool_cvm")
+def k_pull_seqpool_cvm(ctx, op):
+    """Lowered pull_box_sparse -> fused_seqpool_cvm (-> concat) chain."""
+    keys, lod, B, S, sp, dense = _pull_op_args(ctx, op)
+    cvm = _val(ctx.get(op.inputs["CVM"][0])).float().contiguous()
     out = sparse_ops.pull_seqpool_cvm_concat(ctx.engine, keys, lod, B, S, cvm, dense, sp)
     Eo = sp.out_width(ctx.engine.E)
     for s, v in enumerate(op.outputs["Out"]):

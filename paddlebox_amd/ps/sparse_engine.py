@@ -702,6 +702,12 @@ class SparseEngine:
                 if getattr(sl.ws, "rows_occ_dirty", False):
                     sl.ws.clean_rows_occ()
 
+    def ensure_pull_ring(self, n: int):
+        """At least ``n`` pull slots (the pipelined front keys slots by batch
+        buffer: n_buffers x steps per graph).  Not inside a graph capture."""
+        if self.is_gpu and len(self._slots) < n:
+            self._slots += [_PullSlot(self) for _ in range(n - len(self._slots))]
+
     def reset_pull_ring(self):
         """Fresh pull slots (dedup workspaces, occurrence maps, pooled
         outputs) and zeroed push scratch -- what a new training program over

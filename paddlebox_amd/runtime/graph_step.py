@@ -258,17 +258,20 @@ class GraphedTrainStep:
         buffer set is pooled / prepared again before its next replay."""
         self._pref_ver = [-1] * len(self._pref_ver)
 
-    def fill(self, i: int, fn: Callable[[Any], None], stream=None):
+    def fill(self, i: int, fn, stream=None):
         """Produce buffer set i on the device: ``fn(buf)`` enqueues kernels
         that write it (on ``stream``, default the copy stream) once the
-        replay that last read it has finished."""
-        if self.K > 1:
-            raise ValueError("fill() serves single-step graphs")
+        replay that last read it has finished.  With K steps per graph
+        ``fn`` is a sequence of K such callables, one per batch buffer."""
+        fns = list(fn) if self.K > 1 else [fn]
+        if len(fns) != self.K:
+            raise ValueError(f"fill needs {self.K} producers per buffer set")
         st = stream if stream is not None else self.copy_stream
         self._ver[i] += 1
         st.wait_event(self.free[i])
         with torch.cuda.stream(st):
-            fn(self.bufs[i])
+            for k, f in enumerate(fns):
+                f(self.bufs[i * self.K + k])
         self.ready[i].record(st)
 
     trace = None  # diagnostics: a list to collect (throttle wait, rest of run) host seconds per replay

@@ -282,7 +282,8 @@ class BoxPSWorker:
             return self._train_device_pass(dp, plan, Lcap, cache, graph_B, S, Dw, slot_batch, step_fn_for, metrics)
         graphs, warm, rings, nused = {}, {}, {}, {}
         for B, (cL, g, rg) in cache.items():
-            if B in graph_B and cL >= Lcap:
+            # the host-assembly loop replays single-step, non-pipelined graphs
+            if B in graph_B and cL >= Lcap and g.K == 1 and g.pipeline is None:
                 graphs[B], rings[B], nused[B] = g, rg, 0
                 if rg is None:  # captured by the device-pass path: no host ring yet
                     rings[B] = [host_buf(B) for _ in range(R_HOST)]
@@ -373,70 +374,170 @@ class BoxPSWorker:
                 "ins_per_sec": n_ins / el if el > 0 else 0.0, "graph_replays": replays,
                 "graph_sizes": sorted(graphs), **self.timers}
 
+    # metric kinds accumulated by device kernels only (capturable inside a
+    # multi-step graph); the others pull predictions to the host per batch
+    DEVICE_METRICS = {"AucCalculator", "MaskAucCalculator", "MultiMaskAucCalculator"}
+
+    def _metrics_in_graph(self) -> bool:
+        box = self.t.box
+        ms = list(box.metrics.metrics.values()) if box is not None else []
+        return all(m.method in self.DEVICE_METRICS and not m.sample_scale_var and m.phase == -1 for m in ms)
+
+    def _steps_per_graph(self, metrics_in_graph: bool) -> int:
+        """FLAGS_padbox_train_steps_per_graph (0 = auto: 4 on one rank, 2 on
+        several -- bench.py's measured choice -- when every metric can be
+        accumulated inside the graph, else 1)."""
+        k = _flags.get_int("padbox_train_steps_per_graph")
+        if k <= 0:
+            k = (4 if self.t.world == 1 else 2) if metrics_in_graph else 1
+        return k if metrics_in_graph else 1
+
     def _train_device_pass(self, dp, plan, Lcap, cache, graph_B, S, Dw, slot_batch, step_fn_for, metrics):
         """The graphed TrainFiles over a device-resident pass
         (data/device_pass.py): every batch is assembled by the batch kernels
         on the pass stream straight into the replay's input buffers, so the
-        host loop per batch is two launches + one graph replay."""
+        host loop per batch is a few launches + one graph replay.
+
+        The step is the one bench.py times (runtime/graph_step.py):
+        * K training steps per captured graph (FLAGS_padbox_train_steps_per_graph,
+          metrics accumulated inside the graph);
+        * the pipelined front (FLAGS_padbox_pipelined_front): each step pools
+          the next batch right after its sparse push, beside the tower's dW
+          GEMM, so the next step starts at the dense head.  Buffer sets are
+          filled two graphs ahead of their replay (graph j pools set j+1).
+        Reference hot loop: boxps_worker.cc:1278-1357."""
         from .graph_step import GraphedTrainStep, pack_batch
 
-        s, dev = self.s, self.s.device
+        s, dev, box = self.s, self.s.device, self.t.box
+        eng = box.engine
+        in_graph = self._metrics_in_graph()
+        K = self._steps_per_graph(in_graph)
+        pipe_on = _flags.get_bool("padbox_pipelined_front") and s.pipeline_pull_op() is not None
+        n_buf = 3 if pipe_on else 2
 
         def dev_buf(B):
             return pack_batch(_GraphBatch(torch.empty(Lcap, dtype=torch.int64), torch.empty(S * (B + 1), dtype=torch.int64),
                                           torch.empty(B, Dw, dtype=torch.float32)), device=dev)
 
-        graphs, warm, nused = {}, {}, {}
+        def step_for(c, lod_host):
+            fn = step_fn_for(c, lod_host)
+            if not in_graph:
+                return fn
+
+            def fn_m(gb):
+                out = fn(gb)
+                metrics(out)  # device histogram kernels, captured with the step
+                return out
+            return fn_m
+
+        def pipe_for(c, lod_host):
+            if not pipe_on:
+                return None
+
+            def as_batch(buf):
+                return slot_batch(buf.keys, buf.lod, buf.dense, c, lod_host)
+
+            return (lambda buf, j: s.prefetch(as_batch(buf), j),
+                    lambda buf, j: s.set_next(None if buf is None else as_batch(buf), j),
+                    eng.clear_prefetch)
+
+        graphs, warm, state, queue = {}, {}, {}, {}
         for B, (cL, g, _rg) in cache.items():
-            if B in graph_B and cL >= Lcap:
-                graphs[B], nused[B] = g, 0
+            if (B in graph_B and cL >= Lcap and g.K == K and (g.pipeline is not None) == pipe_on
+                    and getattr(g, "metrics_in_graph", False) == in_graph):
+                graphs[B] = g
         Lcap = max([Lcap] + [cache[B][0] for B in graphs])
         t0 = time.time()
         n_ins = replays = 0
+
+        def invalidate_others(c):
+            # a step of another size (or an eager one, c = None) changed the
+            # table after a graph pooled its next buffer set: that set is
+            # pooled again before its replay
+            for c2, g2 in graphs.items():
+                if c2 != c:
+                    g2.invalidate_prefetch()
+
+        def run_one(c):
+            nonlocal replays
+            g, st = graphs[c], state[c]
+            out = g.run(st[1] % g.n)
+            st[1] += 1
+            replays += g.K
+            if not in_graph:
+                metrics(out)
+            invalidate_others(c)
+
+        def fill_group(c, grp):
+            g, st = graphs[c], state.setdefault(c, [0, 0])
+            fns = [lambda buf, b0=b0, c=c: dp.assemble(b0, c, buf.keys, buf.lod, buf.dense) for b0 in grp]
+            g.fill(st[0] % g.n, fns if g.K > 1 else fns[0], dp.stream)
+            st[0] += 1
+            lag = 2 if g.pipeline is not None else 1  # graph j pools set j+1: fill it first
+            while st[0] - st[1] >= lag:
+                run_one(c)
+
+        def eager(db, c):
+            bt = slot_batch(db.keys, db.lod, db.dense, c, db.lod.cpu())
+            ctx = ExecContext(s, bt, training=True)
+            s.feed_batch(ctx, bt)
+            s.step(ctx)
+            metrics((ctx, bt))
+            invalidate_others(None)
+
         for (b0, c) in plan:
             t_s = time.time()
             if c in graphs:
-                g = graphs[c]
-                j = nused[c] % g.n
-                nused[c] += 1
-                g.fill(j, lambda buf, b0=b0, c=c: dp.assemble(b0, c, buf.keys, buf.lod, buf.dense), dp.stream)
-                metrics(g.run(j))
-                replays += 1
+                q = queue.setdefault(c, [])
+                q.append(b0)
+                if len(q) == graphs[c].K:
+                    fill_group(c, list(q))
+                    q.clear()
             else:
                 db = dev_buf(c)
                 dp.assemble_sync(b0, c, db.keys, db.lod, db.dense)
                 if c in graph_B:
                     warm.setdefault(c, []).append(db)
                     if len(warm[c]) == 2:
-                        g = GraphedTrainStep(step_fn_for(c, db.lod.cpu()), warm[c][0], dev, warmup=0,
-                                             warm_batches=warm[c], on_warm=metrics)
-                        graphs[c], nused[c] = g, 0
+                        lh = db.lod.cpu()
+                        if pipe_on:
+                            eng.ensure_pull_ring(n_buf * K)
+                        g = GraphedTrainStep(step_for(c, lh), warm[c][0], dev, warmup=0, warm_batches=warm[c],
+                                             on_warm=None if in_graph else metrics, n_buffers=n_buf,
+                                             pipeline=pipe_for(c, lh), steps_per_graph=K)
+                        g.metrics_in_graph = in_graph
+                        invalidate_others(c)
+                        graphs[c] = g
                         cache[c] = (Lcap, g, None)
                         del warm[c]
                 else:
-                    bt = slot_batch(db.keys, db.lod, db.dense, c, db.lod.cpu())
-                    ctx = ExecContext(s, bt, training=True)
-                    s.feed_batch(ctx, bt)
-                    s.step(ctx)
-                    metrics((ctx, bt))
+                    eager(db, c)
             self.timers["step"] += time.time() - t_s
             self.batches += 1
             n_ins += c
-        # a size seen once (its single warm batch) never captured: run it eagerly
+        # the graphs' filled sets not yet replayed, then the batches short of a
+        # whole graph and the sizes seen once (never captured) run eagerly
+        for c, g in graphs.items():
+            st = state.get(c, [0, 0])
+            while st[1] < st[0]:
+                run_one(c)
+        for c, q in queue.items():
+            for b0 in q:
+                db = dev_buf(c)
+                dp.assemble_sync(b0, c, db.keys, db.lod, db.dense)
+                eager(db, c)
         for c, dbs in warm.items():
             for db in dbs:
-                bt = slot_batch(db.keys, db.lod, db.dense, c, db.lod.cpu())
-                ctx = ExecContext(s, bt, training=True)
-                s.feed_batch(ctx, bt)
-                s.step(ctx)
-                metrics((ctx, bt))
+                eager(db, c)
         torch.cuda.synchronize(dev)
         if dp.overflowed():
             raise RuntimeError("device batch assembly: a batch had more keys than the captured key buffer")
+        eng.check_guards()
         el = time.time() - t0
         return {"batches": self.batches, "instances": n_ins, "seconds": el,
                 "ins_per_sec": n_ins / el if el > 0 else 0.0, "graph_replays": replays,
-                "graph_sizes": sorted(graphs), "device_pass": True, **self.timers}
+                "graph_sizes": sorted(graphs), "device_pass": True, "steps_per_graph": K,
+                "pipelined_front": pipe_on, **self.timers}
 
     def _train_files_eager(self) -> Dict[str, float]:
         t = self.t

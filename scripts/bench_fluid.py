@@ -8,6 +8,12 @@ by the native loader).  Prints one JSON line with samples/s of a steady-state
 pass (stderr: per-pass stats).
 
     python scripts/bench_fluid.py [--batches 40] [--passes 3] [--no-graph]
+        [--features 1e9] [--no-prefill] [--fc-precision fp32|bf16]
+        [--steps-per-graph K] [--no-pipeline]
+
+The table is pre-populated with all --features features (as bench.py does:
+random-init rows, as if a base model was loaded), so the fluid step runs
+against the same 1e9-row HBM table as the headline.
 """
 import argparse
 import json
@@ -77,7 +83,16 @@ def main():
     ap.add_argument("--passes", type=int, default=3)
     ap.add_argument("--features", type=float, default=1e9)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-prefill", action="store_true")
+    ap.add_argument("--fc-precision", choices=("fp32", "bf16"), default="fp32")
+    ap.add_argument("--steps-per-graph", type=int, default=0)
+    ap.add_argument("--no-pipeline", action="store_true")
     args = ap.parse_args()
+    from paddlebox_amd.utils.flags import set_flags
+
+    set_flags({"FLAGS_padbox_fc_precision": args.fc_precision,
+               "FLAGS_padbox_train_steps_per_graph": args.steps_per_graph,
+               "FLAGS_padbox_pipelined_front": not args.no_pipeline})
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     t0 = time.time()
@@ -85,7 +100,18 @@ def main():
     lines = lines_from(synth, args.batch, args.batches)
     print(f"[fluid] generated {len(lines)} lines in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     box = fluid.core.BoxWrapper(8, device="cuda:0", new=True)
-    box.initialize_gpu_and_load_model(slot_vector=list(range(S)), max_keys=args.batch * S, capacity=20_000_000)
+    cap = int(args.features) if not args.no_prefill else 20_000_000
+    box.initialize_gpu_and_load_model(slot_vector=list(range(S)), max_keys=args.batch * S, capacity=cap)
+    if not args.no_prefill:
+        from paddlebox_amd.ops import reference as ref
+
+        t2 = time.time()
+        for chunk in synth.all_keys_chunks(1 << 26):
+            box.engine.insert_local_mixed(ref.mix64(chunk), init_embedx=True)
+        torch.cuda.synchronize()
+        print(f"[fluid] prefilled {box.engine.table.size()} features "
+              f"({box.engine.table.memory_bytes() / 2**30:.1f} GiB) in {time.time() - t2:.1f}s", file=sys.stderr,
+              flush=True)
     main_p, startup, slots, label, dense, pred, loss = build((400, 400, 400))
     main_p._pipeline_opt = dict(main_p._pipeline_opt or {}, use_graph=not args.no_graph)
     exe = fluid.Executor(fluid.CUDAPlace(0))
@@ -113,7 +139,10 @@ def main():
            "value": round(last["ins_per_sec"], 1), "unit": "samples/s", "n_gpus": 1,
            "ms_per_step": round(last["seconds"] / max(1, last["batches"]) * 1e3, 4),
            "batches": last["batches"], "batch": args.batch, "graph": not args.no_graph,
-           "graph_replays": last.get("graph_replays", 0), "auc": box.get_metric_msg("auc")[0]}
+           "graph_replays": last.get("graph_replays", 0), "auc": box.get_metric_msg("auc")[0],
+           "fc_precision": args.fc_precision, "steps_per_graph": last.get("steps_per_graph", 1),
+           "pipelined_front": last.get("pipelined_front", False), "table_rows": box.engine.table.size(),
+           "step_s": round(last.get("step", 0.0), 4)}
     print(json.dumps(out), flush=True)
 
 
