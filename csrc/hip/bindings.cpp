@@ -540,18 +540,21 @@ struct DedupWorkspace {
   // publish are left to the seqpool launch that follows (seqpool_cvm_fwd
   // scatter_ws = this workspace)
   const int32_t* sc_uid_row = nullptr;
-  void run_table(const Tensor& keys, GpuTable& t, bool rows_given, bool defer_scatter = false) {
+  // stage (launch_table_dedup): 0 all, 1 probe + rank, 2 run starts + scatter
+  // of the stage-1 call before it on the same keys (may be another stream)
+  void run_table(const Tensor& keys, GpuTable& t, bool rows_given, bool defer_scatter = false, int stage = 0) {
     check_cuda(keys, "keys");
     const int64_t n = keys.numel();
     PBX_CHECK(n <= cap, "dedup: more keys than workspace capacity");
     PBX_CHECK(keys.scalar_type() == torch::kInt64 && keys.is_contiguous(), "run_table: keys must be int64");
+    PBX_CHECK(stage >= 0 && stage <= 2 && !(stage != 0 && defer_scatter), "run_table: stage");
     table_rows_occ();
     auto rc = t.dedup_rows();
     PBX_CHECK(!(defer_scatter && rows_given), "run_table: a deferred scatter needs the probing dedup");
     launch_table_dedup(t.view(), ptr<int64_t>(keys), n, ptr<int64_t>(rows_occ), ptr<int32_t>(rank), std::get<0>(rc),
                        std::get<1>(rc), std::get<2>(rc), ptr<int64_t>(rows_u), ptr<int32_t>(uid), ptr<int32_t>(perm),
                        ptr<int32_t>(seg), ptr<int32_t>(u_count), ptr<int32_t>(u_acc), rows_given, cur_stream(),
-                       !(defer_scatter && n > 0));
+                       !(defer_scatter && n > 0), stage);
     sc_uid_row = (defer_scatter && n > 0) ? std::get<2>(rc) : nullptr;
     last_n = n;
     if (!rows_given) rows_occ_dirty = true;  // rows_given: k_table_scatter hands rows_occ back all -1
@@ -631,13 +634,15 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
     a.occ_ins = ptr<int32_t>(*occ_ins);
   }
   if (dense.has_value() && dense->defined()) {
-    check_cuda(*dense, "dense");
+    PBX_CHECK(dense->is_cuda(), "dense must be a GPU tensor");
     PBX_CHECK(dense->dim() == 2 && dense->size(0) == B && dense->scalar_type() == torch::kFloat32,
               "dense must be f32 [B, Dd]");
     PBX_CHECK(S > 0 && dense_col >= 0 && dense_col + dense->size(1) <= out.size(1), "dense columns out of range");
+    PBX_CHECK(dense->stride(1) == 1 || dense->size(1) == 1, "dense: rows must be unit-stride");
     a.dense = ptr<float>(*dense);
     a.dense_dim = (int)dense->size(1);
     a.dense_col = dense_col;
+    a.dense_stride = (int)dense->stride(0);  // a column slice of the batch's dense block: read in place
   }
   if (probe_keys.has_value() && probe_keys->defined()) {  // fused probe of the split pull
     PBX_CHECK(probe_table != nullptr && rows_out.has_value() && rows_out->defined(),
@@ -1329,7 +1334,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(py::init<int64_t, int, bool>(), py::arg("cap"), py::arg("device"), py::arg("hash") = true)
       .def("run", &DedupWorkspace::run, py::arg("keys"), py::arg("mixed") = false, py::arg("zero") = py::none())
       .def("run_table", &DedupWorkspace::run_table, py::arg("keys"), py::arg("table"), py::arg("rows_given") = false,
-           py::arg("defer_scatter") = false)
+           py::arg("defer_scatter") = false, py::arg("stage") = 0)
       .def("table_rows_occ", &DedupWorkspace::table_rows_occ)
       .def("clean_rows_occ", &DedupWorkspace::clean_rows_occ)
       .def_readonly("rows_occ_dirty", &DedupWorkspace::rows_occ_dirty)

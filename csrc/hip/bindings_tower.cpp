@@ -148,12 +148,17 @@ class TowerWorkspace {
     }
     check_f32(w_out, dims_[L_], "w_out");
     check_f32(b_out, 1, "b_out");
-    check_f32(label, M_, "label");
+    // the label may be a column view of the batch's dense block: [M] or
+    // [M, 1] with any row stride (read strided by the loss tail, no copy)
+    TW_CHECK(label.is_cuda() && label.scalar_type() == torch::kFloat32 && label.numel() == M_ &&
+                 (label.dim() == 1 || (label.dim() == 2 && label.size(1) == 1)),
+             "label: f32 GPU [M] / [M, 1]");
     a.w_out = P<float>(w_out);
     a.b_out = P<float>(b_out);
     if (lin.has_value() && lin->defined()) check_f32(*lin, M_, "lin");
     a.lin = OP<float>(lin);
     a.label = P<float>(label);
+    a.label_stride = (int)label.stride(0);
     if (auc_table.has_value() && auc_table->defined()) {
       TW_CHECK(auc_table->scalar_type() == torch::kFloat64 && auc_stats.has_value() &&
                    auc_stats->scalar_type() == torch::kFloat64 && auc_stats->numel() >= 5,

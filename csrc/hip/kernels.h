@@ -153,6 +153,7 @@ struct SeqpoolCvmArgs {
   const float* dense = nullptr;
   int dense_dim = 0;
   int dense_col = 0;
+  int dense_stride = 0;  // floats between dense rows (0: dense_dim; a column slice of a wider block)
   // optional occurrence map (occ_slot[k] = s, occ_ins[k] = b) written as the
   // keys are walked, so the push needs no separate fill launch
   int32_t* occ_slot = nullptr;
@@ -351,7 +352,11 @@ SaveStats stream_save_table(const TableDev& t, int64_t total_rows, int kind, con
 void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows_occ, int32_t* rank,
                         int32_t* cnt_row, int64_t cnt_rs, int32_t* uid_row, int64_t* rows_u, int32_t* uid,
                         int32_t* perm, int32_t* seg, int32_t* u_count, int32_t* acc, bool rows_given,
-                        hipStream_t s, bool do_scatter = true);
+                        hipStream_t s, bool do_scatter = true, int stage = 0);
+// stage: 0 = the whole dedup; 1 = the probe + rank launch only (rows_occ /
+// rows_u / per-row counts ready: what the pooling needs); 2 = run starts +
+// scatter only (uid / perm / u_count: what the push needs), which may then
+// run on a side stream beside the pooling
 // Probe raw feasigns (mixed in the kernel, -1 = padding -> row -1).
 void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows, hipStream_t s);
 bool launch_push_merge_send(const PushMergeArgs& a, int dim, float* send, int send_stride, const int64_t* send_index,
@@ -627,7 +632,8 @@ struct TowerArgs {
   const float* w_out = nullptr;  // [N_L]
   const float* b_out = nullptr;  // [1]
   const float* lin = nullptr;    // [M] extra logit part (first-order + FM), nullable
-  const float* label = nullptr;  // [M]
+  const float* label = nullptr;  // [M], element m at label[m * label_stride]
+  int label_stride = 1;          // a label column of the batch's dense block (no copy)
   float* pred = nullptr;         // [M]
   float* dz = nullptr;           // [M] d(mean loss)/d logit
   float* loss = nullptr;         // [1] mean loss

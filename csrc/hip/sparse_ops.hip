@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
   // instance-major so a wave writes contiguous output rows
   const int b = (int)(t / a.S), s = (int)(t % a.S);
   if (s == 0 && a.dense) {
-    const float* src = a.dense + (int64_t)b * a.dense_dim;
+    const float* src = a.dense + (int64_t)b * (a.dense_stride ? a.dense_stride : a.dense_dim);
     float* dst = a.out + (int64_t)b * a.out_stride + a.dense_col;
     for (int c = 0; c < a.dense_dim; ++c) dst[c] = src[c];
   }
@@ -205,7 +205,7 @@ __global__ void k_seqpool_cvm_generic(SeqpoolCvmArgs a) {
   const int b = (int)(t / a.S), s = (int)(t % a.S);
   const int E = a.E;
   if (s == 0 && a.dense) {
-    const float* src = a.dense + (int64_t)b * a.dense_dim;
+    const float* src = a.dense + (int64_t)b * (a.dense_stride ? a.dense_stride : a.dense_dim);
     float* dst = a.out + (int64_t)b * a.out_stride + a.dense_col;
     for (int c = 0; c < a.dense_dim; ++c) dst[c] = src[c];
   }

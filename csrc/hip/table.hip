@@ -542,9 +542,9 @@ void launch_probe_raw(const TableDev& t, const int64_t* keys, int64_t n, int64_t
 void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64_t* rows_occ, int32_t* rank,
                         int32_t* cnt_row, int64_t cnt_rs, int32_t* uid_row, int64_t* rows_u, int32_t* uid,
                         int32_t* perm, int32_t* seg, int32_t* u_count, int32_t* acc, bool rows_given,
-                        hipStream_t s, bool do_scatter) {
+                        hipStream_t s, bool do_scatter, int stage) {
   if (n <= 0) {  // no scatter to publish the counters: [U, n_valid, -, cursor] = 0
-    launch_fill32(reinterpret_cast<uint32_t*>(u_count), 0u, 4, s);
+    if (stage != 1) launch_fill32(reinterpret_cast<uint32_t*>(u_count), 0u, 4, s);
     return;
   }
   // occurrences per thread (PBX_TD_ITEMS 1 / 2 / 4): more probes in flight
@@ -558,16 +558,19 @@ void launch_table_dedup(const TableDev& t, const int64_t* keys, int64_t n, int64
 #define PBX_TD_LAUNCH(PR, IT)                                                                                  \
   hipLaunchKernelGGL((k_table_rank<PR, IT>), dim3(blocks_for(n, 256 * IT)), dim3(256), 0, s, t,              \
                      reinterpret_cast<const uint64_t*>(keys), n, rows_occ, rank, cnt_row, cnt_rs, uid_row, rows_u, acc)
-  if (rows_given) {
-    if (items == 4) PBX_TD_LAUNCH(false, 4);
-    else if (items == 2) PBX_TD_LAUNCH(false, 2);
-    else PBX_TD_LAUNCH(false, 1);
-  } else {
-    if (items == 4) PBX_TD_LAUNCH(true, 4);
-    else if (items == 2) PBX_TD_LAUNCH(true, 2);
-    else PBX_TD_LAUNCH(true, 1);
+  if (stage != 2) {
+    if (rows_given) {
+      if (items == 4) PBX_TD_LAUNCH(false, 4);
+      else if (items == 2) PBX_TD_LAUNCH(false, 2);
+      else PBX_TD_LAUNCH(false, 1);
+    } else {
+      if (items == 4) PBX_TD_LAUNCH(true, 4);
+      else if (items == 2) PBX_TD_LAUNCH(true, 2);
+      else PBX_TD_LAUNCH(true, 1);
+    }
   }
 #undef PBX_TD_LAUNCH
+  if (stage == 1) return;
   // unique ids per thread of the run-start scan (PBX_TD_SEG_ITEMS 1 / 2 / 4);
   // same-box A/B: 0.250-0.259 ms/step at 1 vs 0.255-0.262 at 4
   static const int seg_items = [] {

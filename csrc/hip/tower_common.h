@@ -96,7 +96,7 @@ __device__ inline TowerRowIn tower_row_in(const TowerArgs& a, int m0, int lane, 
   r.bout = a.b_out ? a.b_out[0] : 0.f;
   if (lane < rows && m < a.M) {
     r.lin = a.lin ? a.lin[m] : 0.f;
-    r.y = a.label[m];
+    r.y = a.label[(int64_t)m * a.label_stride];
     r.mask = (a.auc_table && (!a.auc_mask || a.auc_mask[m] != 0.f)) ? 1.f : 0.f;
   }
   return r;

@@ -47,6 +47,9 @@ class ExecContext:
         self.batch = batch
         self.training = training
         self.B = B
+        # metrics a kernel already accumulated for this batch (the fused
+        # tower's AUC histogram): the registry skips them
+        self.fused_metrics = set()
 
     # session passthroughs
     @property
@@ -170,6 +173,51 @@ class Session:
         if any(v.name not in data for v in pulls[0].inputs.get("Dense", [])):
             return None
         return pulls[0]
+
+    def fuse_towers(self, metrics=None, optimizer: bool = True):
+        """Fold each fused tower's per-step side work into launches the step
+        already has (the form bench.py times, runtime/ctr_step.py): the
+        tower weight re-pack and the data_norm summary update into the fused
+        Adam launch of the arena holding the tower, and an AucCalculator over
+        the tower's prediction / label into the tower's loss tail.  For
+        loops where the optimizer is the only writer of the weights between
+        steps (the graphed train loop re-packs at each pass start)."""
+        from ..parallel.dense import FlatAdam
+
+        for key, t in list(self.cache.items()):
+            if not (isinstance(key, tuple) and key and key[0] == "tower"):
+                continue
+            if optimizer and not getattr(t, "_opt_fused", False) and self.training:
+                for a, o in zip(self.arenas, self.opts):
+                    fs = a.flat.untyped_storage().data_ptr()
+                    if isinstance(o, FlatAdam) and all(w.untyped_storage().data_ptr() == fs for w in t.mlp.w):
+                        o.fuse(mlps=list(o._fuse_mlps) + [t.mlp],
+                               data_norms=list(o._fuse_dns) + ([t.dn] if t.dn is not None else []))
+                        t._opt_fused = True
+                        break
+            if metrics is not None and t.auc is not None and (
+                    metrics.metrics.get(getattr(t, "auc_metric", None)) is not getattr(t, "auc_metric_obj", None)):
+                t.auc = t.auc_metric = t.auc_metric_obj = None  # the metric was re-registered: bind the new one
+            if metrics is not None and t.auc is None:
+                pred, label = getattr(t, "io", (None, None))
+                for name, m in metrics.metrics.items():
+                    if (m.method == "AucCalculator" and not m.mask_var and m.phase == -1 and not m.sample_scale_var
+                            and m.pred_var == pred and m.label_var == label
+                            and getattr(m, "fused_tower", None) is None):
+                        tab, st = metrics._dev_tables(m, self.device)
+                        t.auc = (tab, st, None)
+                        t.auc_metric, t.auc_metric_obj = name, m
+                        m.fused_tower = t
+                        break
+
+    def repack_towers(self):
+        """Eager re-pack of every fused tower workspace (start of a graphed
+        pass: a checkpoint load or scope write since the last optimizer step
+        is not seen by captured steps that rely on the optimizer's re-pack)."""
+        for key, t in list(self.cache.items()):
+            if isinstance(key, tuple) and key and key[0] == "tower":
+                for tw in t.mlp.tower_workspaces():
+                    tw.pack([w.detach() for w in t.mlp.w])
 
     def set_next(self, batch, slot: int = 0):
         """Batch to pool at the end of each step (None: none)."""

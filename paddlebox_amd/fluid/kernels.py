@@ -469,7 +469,10 @@ def _pull_op_args(ctx, op):
                        embed_thres_size=a["embed_thres_size"])
     dense = None
     if op.inputs.get("Dense"):
-        dense = torch.cat([_val(ctx.get(v)).float().reshape(B, -1) for v in op.inputs["Dense"]], 1)
+        ds = [_val(ctx.get(v)).float().reshape(B, -1) for v in op.inputs["Dense"]]
+        # one dense variable (a column slice of the batch's dense block) is
+        # read in place by the seqpool launch: no concat copy
+        dense = ds[0] if len(ds) == 1 else torch.cat(ds, 1)
     return keys, lod, B, S, sp, dense
 
 
@@ -479,6 +482,20 @@ def prefetch_pull_op(ctx, op, slot: int) -> bool:
     ``slot``); that step's pull then launches nothing."""
     keys, lod, B, S, sp, dense = _pull_op_args(ctx, op)
     return sparse_ops.prefetch_seqpool_cvm_concat(ctx.engine, keys, lod, B, S, dense, sp, slot)
+
+
+@kernel("__cvm_show_click")
+def k_cvm_show_click(ctx, op):
+    """[B, 2] (show = 1, click = label): a persistent buffer per batch size,
+    its click column copied from the label (lowering._fuse_cvm)."""
+    lab = _val(ctx.get(op.inputs["Label"][0]))
+    B = int(lab.shape[0])
+    key = ("cvm_show_click", id(op), B, lab.device)
+    buf = ctx.cache.get(key)
+    if buf is None:
+        buf = ctx.cache[key] = torch.ones(B, 2, dtype=torch.float32, device=lab.device)
+    buf[:, 1].copy_(lab.reshape(B, -1)[:, 0])
+    ctx.set(op.outputs["Out"][0], buf)
 
 
 @kernel("__pull_seqpool_cvm")
@@ -737,6 +754,7 @@ def _tower_for(ctx, op, C: int):
     # the reference fc precision by default (FLAGS_padbox_fc_precision):
     # the lowering only forms the tower when the fp32 tower takes its widths
     t = CtrTower(mlp, dn, 0, 1, 0, 0, use_head_lin=False, fp32=_fc_fp32())
+    t.io = (op.outputs["Pred"][0].name, op.inputs["Label"][0].name)  # Session.fuse_towers binds metrics by name
     if ctx.training and hasattr(ctx.s, "on_tower_grads"):
         t.on_dense_grads = lambda: ctx.s.on_tower_grads(t)
     ctx.cache[key] = t
@@ -746,10 +764,14 @@ def _tower_for(ctx, op, C: int):
 @kernel("__ctr_tower")
 def k_ctr_tower(ctx, op):
     x = _val(ctx.get(op.inputs["X"][0])).float().contiguous()
-    label = _val(ctx.get(op.inputs["Label"][0])).float().reshape(-1).contiguous()
+    label = _val(ctx.get(op.inputs["Label"][0])).float()
+    if not (label.dim() == 2 and label.shape[1] == 1) and not label.dim() == 1:
+        label = label.reshape(-1).contiguous()  # else a [B, 1] column view: the tower reads it strided
     t = _tower_for(ctx, op, x.shape[1])
     t.dn.train(ctx.training)
     loss, pred = t(x, label)
+    if t.auc is not None and getattr(t, "auc_metric", None):
+        ctx.fused_metrics.add(t.auc_metric)  # histogram added by the tower's loss tail
     ctx.set(op.outputs["Pred"][0], pred.view(-1, 1))
     ctx.set(op.outputs["Loss"][0], loss)
 

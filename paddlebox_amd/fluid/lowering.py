@@ -143,6 +143,40 @@ def _absorb_concat(ops: List[Operator], notes: List[str]):
     return [op for k, op in enumerate(ops) if k not in removed]
 
 
+def _fuse_cvm(ops: List[Operator], fetch: set, notes: List[str]):
+    """``concat([fill_constant_batch_size_like(1.0, [-1, 1]), cast(label ->
+    float32)], axis=1)`` -- the canonical program's show/click CVM input --
+    => ``__cvm_show_click``: a persistent [B, 2] buffer whose show column is
+    1 once and whose click column is copied from the label each step (one
+    launch instead of a fill, a cast and a concat)."""
+    produced_at: Dict[str, int] = {}
+    for i, op in enumerate(ops):
+        for n in op.output_arg_names:
+            produced_at[n] = i
+    cons = _consumers(ops)
+    out = list(ops)
+    removed = set()
+    for k, op in enumerate(ops):
+        if op.type != "concat" or op.attrs.get("axis", 0) not in (1, -1) or len(op.inputs["X"]) != 2:
+            continue
+        sn, cn = op.inputs["X"][0].name, op.inputs["X"][1].name
+        i, j = produced_at.get(sn, -1), produced_at.get(cn, -1)
+        if i < 0 or j < 0 or sn in fetch or cn in fetch:
+            continue
+        fo, co = ops[i], ops[j]
+        if fo.type != "fill_constant_batch_size_like" or co.type != "cast":
+            continue
+        if float(fo.attrs.get("value", 0)) != 1.0 or list(fo.attrs.get("shape", [])) != [-1, 1] \
+                or fo.attrs.get("dtype") not in ("float32", None) or co.attrs.get("out_dtype") != "float32":
+            continue
+        if len(cons.get(sn, [])) != 1 or len(cons.get(cn, [])) != 1:
+            continue
+        out[k] = _synthetic(op.block, "__cvm_show_click", {"Label": co.inputs["X"]}, {"Out": op.outputs["Out"]}, {})
+        removed.update({i, j})
+        notes.append("fill_constant(1) + cast(label) + concat -> __cvm_show_click")
+    return [op for q, op in enumerate(out) if q not in removed]
+
+
 def _fc_ok(op: Operator) -> bool:
     return (op.type == "fc" and op.attrs.get("in_num_col_dims", 1) == 1 and len(op.inputs["Input"]) == 1
             and bool(op.inputs.get("Bias")) and len(op.inputs["W"][0].shape) == 2)
@@ -280,6 +314,7 @@ def lower(program: Program, fetch_names=(), gpu: bool = True, engine_cvm_offset:
         if gpu:
             from .kernels import _fc_fp32
 
+            ops = _fuse_cvm(ops, fetch, notes)
             ops = _fuse_mlp(ops, fetch, storage, notes)
             ops = _fuse_tower(ops, fetch, notes, fp32=_fc_fp32())
     for op in ops + bwd + opt:

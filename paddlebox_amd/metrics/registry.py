@@ -113,9 +113,14 @@ class MetricRegistry:
     # -- accumulation ---------------------------------------------------
     def add_batch(self, fetch: Dict[str, torch.Tensor]):
         """Accumulate every registered metric of the current phase from the
-        batch's named tensors (preds, labels, masks, cmatch_rank, uids)."""
-        for m in self.metrics.values():
+        batch's named tensors (preds, labels, masks, cmatch_rank, uids).
+        Metrics a kernel already accumulated for this batch (``fetch.
+        fused_metrics``: the fused tower's AUC) are skipped."""
+        done = getattr(fetch, "fused_metrics", ())
+        for name, m in self.metrics.items():
             if m.phase != -1 and m.phase != self.phase:
+                continue
+            if name in done:
                 continue
             self._add(m, fetch)
 

@@ -208,17 +208,29 @@ class FusedMLP(nn.Module):
     def tower_workspace(self, M: int, device: torch.device, fp32: bool = False):
         """Persistent buffers of the fused tower for batch M.  fp32=True is the
         exact-fp32 tower (csrc/hip/tower32.hip, the reference fc precision),
-        else the bf16-operand tower (csrc/hip/tower.hip)."""
-        if self._tw is None or self._tw.M != M or bool(self._tw.fp32) != bool(fp32):
+        else the bf16-operand tower (csrc/hip/tower.hip).  One workspace per
+        (M, precision), kept for the module's lifetime: a HIP graph captured
+        at one batch size keeps its workspace's addresses while steps of
+        another size (a pass's last partial batch) use their own."""
+        tws = self.__dict__.setdefault("_tws", {})
+        key = (int(M), bool(fp32))
+        tw = tws.get(key)
+        if tw is None:
             dims = [self.in_dim] + list(self.hidden)
             # dW split over M (fp32 atomics between splits)
             if fp32:
                 splits = int(os.environ.get("PBX_TOWER32_DW_SPLITS", "8"))
             else:
                 splits = int(os.environ.get("PBX_TOWER_DW_SPLITS", "2"))
-            self._tw = _native.hip().TowerWorkspace(M, dims, device.index or 0, splits, bool(fp32))
+            tw = tws[key] = _native.hip().TowerWorkspace(M, dims, device.index or 0, splits, bool(fp32))
+        if self._tw is not tw:
+            self._tw = tw
             self._packed = False
         return self._tw
+
+    def tower_workspaces(self):
+        """Every workspace of this MLP (the fused Adam re-packs all of them)."""
+        return list(self.__dict__.get("_tws", {}).values())
 
     def tower_fp32_ok(self) -> bool:
         """The fp32 tower keeps two 32-row fp32 tiles in LDS, plus the
@@ -228,7 +240,11 @@ class FusedMLP(nn.Module):
         return tower_fp32_fits([self.in_dim] + list(self.hidden))
 
     def ensure_packed(self):
-        if not self._packed or not self.packed_by_optimizer:
+        """Pack the current workspace's tower weights unless the optimizer
+        keeps them packed.  With several batch-size workspaces the forward
+        always packs its own: an optimizer launch captured before a
+        workspace existed does not re-pack it."""
+        if not self._packed or not self.packed_by_optimizer or len(self.__dict__.get("_tws", {})) > 1:
             self._tw.pack([w.detach() for w in self.w])
             self._packed = True
 

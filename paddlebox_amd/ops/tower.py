@@ -94,7 +94,9 @@ class _CtrTowerFn(torch.autograd.Function):
             join_grad_producers()
             mlp.ensure_packed()
         auc = t.auc
-        loss, pred, dz = ws.forward(list(mlp.b), mlp.w_out.view(-1), mlp.b_out, lin_use, label.contiguous().view(-1),
+        # a [B] / [B, 1] label may be a strided column view (read in place)
+        lab = label if label.dtype == torch.float32 and label.dim() in (1, 2) else label.float().contiguous().view(-1)
+        loss, pred, dz = ws.forward(list(mlp.b), mlp.w_out.view(-1), mlp.b_out, lin_use, lab,
                                     auc[0] if auc else None, auc[1] if auc else None, auc[2] if auc else None)
         ctx.t, ctx.ws = t, ws
         ctx.save_for_backward(x)

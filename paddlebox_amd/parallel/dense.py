@@ -131,6 +131,8 @@ class FlatAdam:
         self.ticket = torch.zeros(1, dtype=torch.int32, device=arena.flat.device)
         self._fuse_mlps, self._fuse_dns = [], []
 
+    MAX_PACK_REGIONS = 8  # kernels.h kMaxPackRegions
+
     def fuse(self, mlps=(), data_norms=()):
         """Let the update kernel also (a) re-pack the bf16 tower copies of
         these MLPs' weights and (b) apply these data_norm layers' summary
@@ -151,11 +153,20 @@ class FlatAdam:
         base = self.a.flat.data_ptr()
         pack = []
         for mlp in self._fuse_mlps:
-            if mlp._tw is None:
-                continue  # the tower packs on its first forward
-            for reg, w in zip(mlp._tw.pack_regions(), mlp.w):
-                wp, wtp, N, K, Np, Kp, pos, posT = reg
-                pack.append(((w.data_ptr() - base) // 4, wp, wtp, N, K, Np, Kp, pos, posT))
+            if not mlp.packed_by_optimizer:
+                continue  # its forward packs (too many workspaces for the launch)
+            # the tower packs on its first forward; every batch size's
+            # workspace keeps its own packed copy, all re-packed here
+            tws = mlp.tower_workspaces() if hasattr(mlp, "tower_workspaces") else (
+                [mlp._tw] if mlp._tw is not None else [])
+            regs = [((w.data_ptr() - base) // 4,) + tuple(reg) for tw in tws for reg, w in zip(tw.pack_regions(), mlp.w)]
+            if len(pack) + len(regs) > self.MAX_PACK_REGIONS:
+                # more batch sizes than one launch re-packs: this MLP's forward
+                # packs its current workspace from now on (always correct)
+                mlp.packed_by_optimizer = False
+                mlp.invalidate_pack()
+                continue
+            pack += regs
         dn = [(d.stats, d.batch_size, d.batch_sum, d.batch_square_sum, d.decay)
               for d in self._fuse_dns if d.training and d.update_norm]
         return pack, dn

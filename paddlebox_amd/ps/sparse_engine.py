@@ -134,6 +134,16 @@ class PullState:
 TABLE_DEDUP_MAX_ROWS = (1 << 31) - 1
 
 
+def _dense_rows(dense: torch.Tensor) -> torch.Tensor:
+    """Dense columns for the fused seqpool launch, read in place when they are
+    a unit-stride column slice of the batch's dense block (the launch takes
+    the row stride), copied otherwise."""
+    dense = dense.float()
+    if dense.dim() == 2 and (dense.stride(1) == 1 or dense.shape[1] == 1):
+        return dense
+    return dense.contiguous()
+
+
 def _push_run_scratch(max_keys: int, device) -> torch.Tensor:
     """Runs of a key's occurrences that straddle waves in the fused merge +
     update: the int32 per-wave run owners of the two-launch form
@@ -442,7 +452,7 @@ class SparseEngine:
             # load less per occurrence than uid -> rows_u)
             src_index, uid = st.extra["rows_occ"], None
         if dense is not None:
-            dense = dense.contiguous().float()
+            dense = _dense_rows(dense)
         h.seqpool_cvm_fwd(src, src_index, uid, lod, S, B, self.E, out, col_offset, sp.use_cvm,
                           sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter, sp.show_coeff, sp.clk_coeff,
                           sp.threshold, sp.quant_ratio, sp.embed_threshold_filter, sp.embed_threshold,
@@ -464,7 +474,7 @@ class SparseEngine:
                 self.table.insert_mixed(torch.unique(ref.mix64(keys[miss])), self.cfg.sgd)
                 self.table.t.probe_raw(keys, rows)
         if dense is not None:
-            dense = dense.contiguous().float()
+            dense = _dense_rows(dense)
         h.seqpool_cvm_fwd(self.table.values, rows, None, lod, S, B, self.E, out, col_offset, sp.use_cvm,
                           sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter, sp.show_coeff, sp.clk_coeff,
                           sp.threshold, sp.quant_ratio, sp.embed_threshold_filter, sp.embed_threshold,
@@ -496,7 +506,7 @@ class SparseEngine:
         # positions would then count as occurrences of stale rows
         ws.clean_rows_occ()
         if dense is not None:
-            dense = dense.contiguous().float()
+            dense = _dense_rows(dense)
 
         def pool():
             h.seqpool_cvm_fwd(self.table.values, None, None, lod, S, B, self.E, out, col_offset, sp.use_cvm,
@@ -625,7 +635,7 @@ class SparseEngine:
                                   sp.show_coeff, sp.clk_coeff, sp.threshold, sp.quant_ratio,
                                   sp.embed_threshold_filter, sp.embed_threshold,
                                   sp.embed_thres_size if not sp.use_cvm else 0,
-                                  dense.contiguous().float() if dense is not None else None, S * Eo,
+                                  _dense_rows(dense) if dense is not None else None, S * Eo,
                                   occ_slot=sl.occ_slot, occ_ins=sl.occ_ins)
         self._prepared[keys.data_ptr()] = (sl, L, st)
         self._prepared_out[keys.data_ptr()] = sl.pre_out
@@ -643,9 +653,30 @@ class SparseEngine:
             # pack, both exchanges and the pooling follow in prefetch_pool
             self._hash_dedup(sl, keys.reshape(-1))
             return True
-        sl.ws.run_table(keys, self.table.t, False, self._fuse_scatter())
+        if self._finish_side():
+            # the pooling needs only the probe + rank launch (rows_occ); the
+            # run starts + scatter (uid / perm / counters) are the next push's:
+            # they run on a side stream beside the pooling, joined with the
+            # step's other side work (parallel.dense grad producers)
+            from ..parallel.dense import add_grad_producer
+
+            sl.ws.run_table(keys, self.table.t, False, False, 1)
+            cur = torch.cuda.current_stream(self.device)
+            side = side_stream(self.device, "td_finish")
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                sl.ws.run_table(keys, self.table.t, False, False, 2)
+            add_grad_producer(side)
+        else:
+            sl.ws.run_table(keys, self.table.t, False, self._fuse_scatter())
         sl.rows = sl.ws.rows_u
         return True
+
+    def _finish_side(self) -> bool:
+        """PBX_TD_FINISH_SIDE=1: the prefetched table dedup's run starts +
+        scatter on a side stream beside the pooling (not with the fused
+        scatter, which the pooling launch itself performs)."""
+        return os.environ.get("PBX_TD_FINISH_SIDE", "0") == "1" and not self._fuse_scatter()
 
     def _fuse_scatter(self) -> bool:
         """Leave the table dedup's scatter to the prefetched pooling launch
@@ -681,7 +712,7 @@ class SparseEngine:
                                   sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter, sp.show_coeff,
                                   sp.clk_coeff, sp.threshold, sp.quant_ratio, sp.embed_threshold_filter,
                                   sp.embed_threshold, sp.embed_thres_size if not sp.use_cvm else 0,
-                                  dense.contiguous().float() if dense is not None else None, S * Eo,
+                                  _dense_rows(dense) if dense is not None else None, S * Eo,
                                   occ_slot=sl.occ_slot, occ_ins=sl.occ_ins, scatter_ws=ws)
         self._prepared[keys.data_ptr()] = (sl, L)
         self._prepared_out[keys.data_ptr()] = sl.pre_out

@@ -299,6 +299,7 @@ class GraphedTrainStep:
                 # replay with its current contents: pool it now
                 self.pipeline[0](self.bufs[i * self.K], i * self.K)
                 self.pipeline[2]() if len(self.pipeline) > 2 else None
+                join_grad_producers()  # side-stream parts of that pooling (PBX_TD_FINISH_SIDE)
             self._pref_ver[(i + 1) % n] = self._ver[(i + 1) % n]
         if self.prefetch is not None:
             n = len(self.bufs)

@@ -41,7 +41,7 @@ log = logger()
 # only of these can be captured into a HIP graph (the sparse data vars reach
 # the engine only through the fused pull, which reads the padded key buffer)
 GRAPH_SAFE_OPS = {
-    "__pull_seqpool_cvm", "__fused_mlp", "__ctr_tower", "data_norm", "concat", "cast", "fill_constant_batch_size_like",
+    "__pull_seqpool_cvm", "__fused_mlp", "__ctr_tower", "__cvm_show_click", "data_norm", "concat", "cast", "fill_constant_batch_size_like",
     "sigmoid", "sigmoid_cross_entropy_with_logits", "reduce_mean", "relu", "fc", "elementwise_add",
     "elementwise_mul", "elementwise_sub", "scale", "log_loss", "mean", "reduce_sum", "tanh", "softmax",
 }
@@ -112,6 +112,7 @@ class _FetchView(dict):
     def __init__(self, ctx: ExecContext, batch):
         super().__init__()
         self.ctx, self.batch = ctx, batch
+        self.fused_metrics = ctx.fused_metrics
 
     def __missing__(self, name):
         if name == "__cmatch_rank__" and self.batch is not None and "cmatch_rank" in self.batch.extra:
@@ -248,6 +249,11 @@ class BoxPSWorker:
         sizes = Counter(c for _, c in plan)
         graph_B = {B for B, n in sizes.items() if n >= 3}
         label = ds.label_name if ds.label_name in dnames else None
+        # the label / cvm extras only feed data variables of those names that
+        # are not dense slots (the canonical program builds its cvm from the
+        # label with its own ops): otherwise not built, two launches a step less
+        if label is not None and not any(v.name in ("label", "cvm") and v.name not in dnames for v in s.data_vars):
+            label = None
 
         def host_buf(B):
             return pack_batch(_GraphBatch(torch.empty(Lcap, dtype=torch.int64),
@@ -410,6 +416,12 @@ class BoxPSWorker:
 
         s, dev, box = self.s, self.s.device, self.t.box
         eng = box.engine
+        # the fused towers' side work rides in launches the step has anyway
+        # (weight re-pack + data_norm update in Adam, AUC in the loss tail);
+        # the optimizer is this loop's only weight writer, so one eager
+        # re-pack at the pass start covers checkpoint loads between passes
+        s.fuse_towers(box.metrics)
+        s.repack_towers()
         in_graph = self._metrics_in_graph()
         K = self._steps_per_graph(in_graph)
         pipe_on = _flags.get_bool("padbox_pipelined_front") and s.pipeline_pull_op() is not None
@@ -420,7 +432,12 @@ class BoxPSWorker:
                                           torch.empty(B, Dw, dtype=torch.float32)), device=dev)
 
         def step_for(c, lod_host):
-            fn = step_fn_for(c, lod_host)
+            fn0 = step_fn_for(c, lod_host)
+
+            def fn(gb):
+                out = fn0(gb)
+                s.fuse_towers(box.metrics)  # host-only: a tower first built by this step (before the capture)
+                return out
             if not in_graph:
                 return fn
 
@@ -559,6 +576,8 @@ class BoxPSWorker:
         t = self.t
         s = self.s
         box = t.box
+        if box is not None:
+            s.fuse_towers(box.metrics, optimizer=False)  # keep a fused-tower AUC bound to the current metric
         ds = t.dataset
         dev = s.device
         desc = t.desc

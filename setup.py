@@ -23,6 +23,24 @@ def rel(p):
     return os.path.relpath(p, ROOT)
 
 
+def _drop_stale_hip_objects():
+    """torch's ninja build gives hipcc no depfile, so a .hip object is rebuilt
+    only when the .hip itself changes -- not when a header it includes does.
+    A struct change in kernels.h (e.g. a field added to TowerArgs) then leaves
+    objects compiled with the old layout next to callers built with the new
+    one: kernel arguments read at shifted offsets, a GPU memory fault.  Drop
+    every HIP object older than the newest header before building."""
+    headers = glob.glob(os.path.join(ROOT, "csrc", "hip", "*.h")) + glob.glob(os.path.join(ROOT, "csrc", "common", "*.h"))
+    if not headers:
+        return
+    newest = max(os.path.getmtime(h) for h in headers)
+    for obj in glob.glob(os.path.join(ROOT, "build", "temp.*", "csrc", "hip", "*.o")):
+        if os.path.getmtime(obj) < newest:
+            os.remove(obj)
+
+
+_drop_stale_hip_objects()
+
 hip_sources = sorted(glob.glob(os.path.join(ROOT, "csrc", "hip", "*.hip"))) + sorted(
     glob.glob(os.path.join(ROOT, "csrc", "hip", "*.cpp"))
 )

@@ -124,3 +124,19 @@ def test_pipelined_program_then_plain_multistep_on_same_engine():
     oa, orr = torch.argsort(ha), torch.argsort(hr)
     assert torch.equal(ha[oa], hr[orr])
     torch.testing.assert_close(va[oa], vr[orr], rtol=2e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("K,overlap", [(1, "0"), (4, "0"), (4, "1")])
+def test_dedup_finish_on_side_stream_matches_plain(K, overlap, monkeypatch):
+    """PBX_TD_FINISH_SIDE=1: the prefetched dedup's run starts + scatter run
+    on a side stream beside the pooling (joined with the step's side work);
+    with and without Adam on the dW stream (PBX_ADAM_OVERLAP)."""
+    nb = 1 + 3 * K if K > 2 else 8
+    f0, l0, k0, v0 = _train(False, "fp32", K, nb)
+    monkeypatch.setenv("PBX_TD_FINISH_SIDE", "1")
+    monkeypatch.setenv("PBX_ADAM_OVERLAP", overlap)
+    f1, l1, k1, v1 = _train(True, "fp32", K, nb)
+    assert l1 == pytest.approx(l0, rel=1e-6, abs=1e-7)
+    torch.testing.assert_close(f1, f0, rtol=1e-6, atol=1e-7)
+    assert torch.equal(k1, k0)
+    torch.testing.assert_close(v1, v0, rtol=1e-6, atol=1e-7)
