@@ -160,6 +160,24 @@ class Session:
         # after this step's sparse push, so the next step starts at the dense head
         self._next = None
 
+    def close(self):
+        """Release the session's IPC mesh (each session's mesh stayed
+        registered and mapped forever): unregistered when it is the group's
+        current one, then closed.  A mesh shared from another session is left
+        to its owner."""
+        ipc, self.ipc = getattr(self, "ipc", None), None
+        if ipc is None or not getattr(self, "_owns_ipc", False):
+            return
+        from ..parallel.comm import group_mesh, register_group_mesh
+
+        if group_mesh(self.group) is ipc:
+            register_group_mesh(self.group, None)
+        for s in self.syncs:
+            if getattr(s, "ipc", None) is ipc:
+                s.ipc = None
+        ipc.close()
+        self._owns_ipc = False
+
     # -------------------------------------------------------------- pipelined front
     def pipeline_pull_op(self):
         """The program's single fused pull op when the pipelined front applies
@@ -199,10 +217,10 @@ class Session:
                     metrics.metrics.get(getattr(t, "auc_metric", None)) is not getattr(t, "auc_metric_obj", None)):
                 t.auc = t.auc_metric = t.auc_metric_obj = None  # the metric was re-registered: bind the new one
             if metrics is not None and t.auc is None:
-                pred, label = getattr(t, "io", (None, None))
+                pred, labels = getattr(t, "io", (None, ()))
                 for name, m in metrics.metrics.items():
                     if (m.method == "AucCalculator" and not m.mask_var and m.phase == -1 and not m.sample_scale_var
-                            and m.pred_var == pred and m.label_var == label
+                            and m.pred_var == pred and m.label_var in labels
                             and getattr(m, "fused_tower", None) is None):
                         tab, st = metrics._dev_tables(m, self.device)
                         t.auc = (tab, st, None)
@@ -307,14 +325,26 @@ class Session:
         # stream, graph-capturable), RCCL when the mesh is unavailable
         # (PBX_DENSE_IPC=0 forces RCCL).  Collective: every rank builds it.
         self.ipc = None
+        self._owns_ipc = False
         if world > 1 and self.device.type == "cuda" and arenas and os.environ.get("PBX_DENSE_IPC", "1") != "0":
-            from ..parallel.comm import register_group_mesh
+            from ..parallel.comm import group_mesh, register_group_mesh
             from ..runtime.ctr_step import make_ipc_mesh
 
             nbytes = max(max(a.grad.numel() for _, a in arenas) * 4, 1 << 20)
-            self.ipc = make_ipc_mesh(nbytes, self.device, group=self.group,
-                                     log=lambda m: log.warning("fluid dense sync: %s", m))
-            register_group_mesh(self.group, self.ipc)
+            live = group_mesh(self.group)
+            if live is not None and getattr(live, "slot_bytes", 0) >= nbytes and live.device == self.device:
+                # another session's mesh of this group serves this one too (the
+                # same decision on every rank: sizes come from the program)
+                self.ipc = live
+            else:
+                self.ipc = make_ipc_mesh(nbytes, self.device, group=self.group,
+                                         log=lambda m: log.warning("fluid dense sync: %s", m))
+                self._owns_ipc = self.ipc is not None
+                if self.ipc is not None:
+                    # the group's collectives (c_allreduce_sum, data_norm
+                    # sync_stats) use the newest mesh; an older, smaller one
+                    # stays alive for the session that owns it
+                    register_group_mesh(self.group, self.ipc)
         for lr_mult, arena in arenas:
             self.arenas.append(arena)
             if sharded:
@@ -731,6 +761,9 @@ class Executor:
         return trainer.run()
 
     def close(self):
+        for sess in self._sessions.values():
+            if hasattr(sess, "close"):
+                sess.close()
         self._sessions.clear()
 
 

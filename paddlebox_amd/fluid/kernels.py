@@ -754,7 +754,8 @@ def _tower_for(ctx, op, C: int):
     # the reference fc precision by default (FLAGS_padbox_fc_precision):
     # the lowering only forms the tower when the fp32 tower takes its widths
     t = CtrTower(mlp, dn, 0, 1, 0, 0, use_head_lin=False, fp32=_fc_fp32())
-    t.io = (op.outputs["Pred"][0].name, op.inputs["Label"][0].name)  # Session.fuse_towers binds metrics by name
+    # Session.fuse_towers binds an AUC metric by these names
+    t.io = (op.outputs["Pred"][0].name, {op.inputs["Label"][0].name, a.get("label_alias") or ""} - {""})
     if ctx.training and hasattr(ctx.s, "on_tower_grads"):
         t.on_dense_grads = lambda: ctx.s.on_tower_grads(t)
     ctx.cache[key] = t

@@ -169,10 +169,12 @@ def _fuse_cvm(ops: List[Operator], fetch: set, notes: List[str]):
         if float(fo.attrs.get("value", 0)) != 1.0 or list(fo.attrs.get("shape", [])) != [-1, 1] \
                 or fo.attrs.get("dtype") not in ("float32", None) or co.attrs.get("out_dtype") != "float32":
             continue
-        if len(cons.get(sn, [])) != 1 or len(cons.get(cn, [])) != 1:
+        if len(cons.get(sn, [])) != 1:
             continue
         out[k] = _synthetic(op.block, "__cvm_show_click", {"Label": co.inputs["X"]}, {"Out": op.outputs["Out"]}, {})
-        removed.update({i, j})
+        removed.add(i)
+        if len(cons.get(cn, [])) == 1:
+            removed.add(j)  # else the float label also feeds the loss: the cast stays
         notes.append("fill_constant(1) + cast(label) + concat -> __cvm_show_click")
     return [op for q, op in enumerate(out) if q not in removed]
 
@@ -291,6 +293,10 @@ def _fuse_tower(ops: List[Operator], fetch: set, notes: List[str], fp32: bool = 
                "BatchSize": dop.inputs["BatchSize"], "BatchSum": dop.inputs["BatchSum"],
                "BatchSquareSum": dop.inputs["BatchSquareSum"]}
         attrs = {k: dop.attrs.get(k) for k in ("epsilon", "summary_decay_rate", "sync_stats", "update_norm")}
+        lp = produced_at.get(lab, -1)
+        if lp >= 0 and ops[lp].type == "cast" and ops[lp].attrs.get("out_dtype") == "float32":
+            # a metric over the uncast label is the same AUC (Session.fuse_towers)
+            attrs["label_alias"] = ops[lp].inputs["X"][0].name
         fused = _synthetic(mop.block, "__ctr_tower", ins, {"Pred": sg.outputs["Out"], "Loss": rm.outputs["Out"]},
                            attrs)
         out[m] = fused

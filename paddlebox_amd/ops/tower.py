@@ -84,7 +84,11 @@ class _CtrTowerFn(torch.autograd.Function):
             lin_use = None
         if t.cross is not None:
             # DCN-V2 cross stack on the normalised input the head just wrote
-            # (x0 and its transposed copy): its logit joins the tower's loss
+            # (x0 and its transposed copy): its logit joins the tower's loss.
+            # Its weights are updated by the overlapped Adam too: join it first
+            # (the cross forward read net.w / w_c under the update)
+            if pre_head is not None:
+                join_grad_producers()
             net, w_c = t.cross
             xw = net.workspace(ws.x0())
             s = xw.forward(ws.x0(), [w.detach() for w in net.w], [b.detach() for b in net.b], w_c.detach())
@@ -123,6 +127,13 @@ class _CtrTowerFn(torch.autograd.Function):
                 mlp.w_out.grad.view(-1), mlp.b_out.grad, True, t._dn_part(B, x.device) if dn_on else None,
                 h.head_blocks(B) if dn_on else 0, dn.eps if dn is not None else 0.0, dn.stats if dn_on else None)
 
+        # with a DCN-V2 cross stack the dense gradients are final only after
+        # the cross backward below: a dense tail that runs before it (dW
+        # launched right after the dX chain, or no dW overlap) must not yet
+        # fire on_dense_grads (the all-reduce / overlapped Adam would read the
+        # cross weights' gradients unfinished)
+        hook = {"after_cross": False}
+
         def dense_tail():
             if dn_on and not getattr(dn, "stats_in_grad_bucket", False):
                 if dn.sync_stats and dn.group is not None and collective_active(dn.group):
@@ -130,7 +141,10 @@ class _CtrTowerFn(torch.autograd.Function):
             if dn_on and not dn.fused_update:
                 h.data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, dn.stats, dn.decay)
             if t.on_dense_grads is not None:  # e.g. start the dense all-reduce, overlapped with the sparse push
-                t.on_dense_grads()
+                if t.cross is not None and not hook["after_cross"]:
+                    hook["pending"] = True
+                else:
+                    t.on_dense_grads()
 
         deferred_dw = None
         if t.overlap_dw and x.is_cuda and (t.overlap_dw_collectives or not _collectives_in_step()):
@@ -157,6 +171,21 @@ class _CtrTowerFn(torch.autograd.Function):
             ds = ctx.dz if gl is None else (ctx.dz * gl).contiguous()
             net._xw.backward(ws.x0(), ctx.yt, ds, [_ensure_grad(w) for w in net.w],
                              [_ensure_grad(b) for b in net.b], w_c.detach(), _ensure_grad(w_c), dy_out=dx0)
+            hook["after_cross"] = True
+            if hook.get("pending"):
+                # the dense tail already ran (on the dW side stream, or inline):
+                # fire the hook where it ran, once the cross gradients are final
+                cur = torch.cuda.current_stream(x.device)
+                if t._side is not None and t.overlap_dw and x.is_cuda and deferred_dw is None and \
+                        (t.overlap_dw_collectives or not _collectives_in_step()):
+                    done = torch.cuda.Event()
+                    done.record(cur)
+                    side = t._side_stream(x.device)
+                    side.wait_event(done)
+                    with torch.cuda.stream(side):
+                        t.on_dense_grads()
+                else:
+                    t.on_dense_grads()
         use_lin = t.use_head_lin and not ctx.has_extra
         dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, ws.K0p,
                            ctx.means, ctx.scales, dn.eps if dn is not None else 0.0, dlin_scale=gl,

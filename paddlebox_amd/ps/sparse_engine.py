@@ -293,6 +293,7 @@ class SparseEngine:
             # sender packs its unique keys per owner with a counting pass)
             self._slots = [_PullSlot(self) for _ in range(max(1, int(pull_ring)))]
             self._prepared = {}  # key-buffer address -> (slot, L) of a prefetched batch
+            self._prepared_keep = {}  # key-buffer address -> its storage (kept alive while prepared)
             self._prepared_out = {}  # key-buffer address -> pooled output of a prefetch_pull
             self._next_slot = 0
             self._cur = self._slots[0]
@@ -579,6 +580,14 @@ class SparseEngine:
             sl.ws.run(keys, False)
             self.table.t.probe_into(sl.ws.uniq_h[:L], sl.ws.u_count, sl.rows)
         self._prepared[keys.data_ptr()] = (sl, L)
+        self._keep_keys(keys)
+
+    def _keep_keys(self, keys: torch.Tensor):
+        """Prepared pulls are looked up by the key buffer's address: keep that
+        buffer's storage alive while its entry exists, so a later batch can
+        never get the same address and pick up this batch's prepared state
+        (ADVICE r4).  Dropped with the entries (clear_prefetch)."""
+        self._prepared_keep[keys.data_ptr()] = keys.untyped_storage()
 
     def can_prefetch_pull(self) -> bool:
         if self.sharded:
@@ -639,6 +648,7 @@ class SparseEngine:
                                   occ_slot=sl.occ_slot, occ_ins=sl.occ_ins)
         self._prepared[keys.data_ptr()] = (sl, L, st)
         self._prepared_out[keys.data_ptr()] = sl.pre_out
+        self._keep_keys(keys)
 
     def prefetch_dedup(self, keys: torch.Tensor, slot: int = 0) -> bool:
         """The key half of prefetch_pull (table dedup + probe into the slot):
@@ -716,6 +726,7 @@ class SparseEngine:
                                   occ_slot=sl.occ_slot, occ_ins=sl.occ_ins, scatter_ws=ws)
         self._prepared[keys.data_ptr()] = (sl, L)
         self._prepared_out[keys.data_ptr()] = sl.pre_out
+        self._keep_keys(keys)
         return True
 
     def prepared_output(self, keys: torch.Tensor) -> Optional[torch.Tensor]:
@@ -728,6 +739,7 @@ class SparseEngine:
         does not carry the clean-up; SparseEngine._pull_split)."""
         self._prepared.clear()
         self._prepared_out.clear()
+        getattr(self, "_prepared_keep", {}).clear()
         if reset_rows and self.is_gpu:
             for sl in getattr(self, "_slots", []):
                 if getattr(sl.ws, "rows_occ_dirty", False):

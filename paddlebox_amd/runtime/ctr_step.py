@@ -97,13 +97,15 @@ class CtrTrainStep:
         # data_norm summary update; grads zeroed by the same kernel
         self.opt = FlatAdam(self.arena, lr=lr, clear_grad=True)
         tower = getattr(model, "tower", None)
-        # PBX_ADAM_OVERLAP=1 (one rank, fused tower): the update runs on the dW
-        # side stream after the data_norm summary update, and the NEXT step's
-        # head (data_norm + concat) starts once that summary update is done --
-        # only the tower forward waits for Adam (the step boundary no longer
-        # serialises head_fwd behind the optimizer)
+        # PBX_ADAM_OVERLAP (default on; one rank, fused tower): the update runs
+        # on the dW side stream after the data_norm summary update, and the
+        # NEXT step's head (data_norm + concat) starts once that summary update
+        # is done -- only the tower forward waits for Adam (the step boundary
+        # no longer serialises head_fwd behind the optimizer).  fp32 DeepFM
+        # 0.3613 / 0.3610 -> 0.3559 / 0.3547 ms/step (profiles/r5_ab_finish_side_adam_overlap.txt);
+        # DCN-V2 joins it before its cross forward (the cross weights are Adam's too)
         self.adam_overlap = (not multi and self.fused and tower is not None
-                             and os.environ.get("PBX_ADAM_OVERLAP", "0") == "1")
+                             and os.environ.get("PBX_ADAM_OVERLAP", "1") == "1")
         if self.fused:
             # the overlap keeps the data_norm update out of the Adam launch
             self.opt.fuse(mlps=[model.mlp], data_norms=[] if self.adam_overlap else [model.dn])

@@ -38,7 +38,7 @@ def _train(pipeline: bool, precision: str, K: int = 1, n_batches: int = 8):
     return flat, losses, hk[o].cpu(), v[o].cpu()
 
 
-def _run(eng, hbs, S, pipeline: bool, precision: str, K: int = 1):
+def _run(eng, hbs, S, pipeline: bool, precision: str, K: int = 1, model: str = "deepfm"):
     """One training program over the engine: warm batch 0 eagerly, then the
     rest of the batches through the graphed step (K steps per graph)."""
     from paddlebox_amd.runtime.ctr_step import CtrTrainStep
@@ -46,7 +46,7 @@ def _run(eng, hbs, S, pipeline: bool, precision: str, K: int = 1):
 
     eng.clear_prefetch(reset_rows=True)
     torch.manual_seed(0)
-    step = CtrTrainStep(eng, "deepfm", precision, num_slots=S, hidden=(64, 64, 64))
+    step = CtrTrainStep(eng, model, precision, num_slots=S, hidden=(64, 64, 64))
     pipe = (lambda b, j: step.prefetch(b, j), step.set_next, eng.clear_prefetch) if pipeline else None
     losses = []
     g = GraphedTrainStep(step.train_step, hbs[0], DEV, warmup=0, warm_batches=[hbs[0]],
@@ -140,3 +140,19 @@ def test_dedup_finish_on_side_stream_matches_plain(K, overlap, monkeypatch):
     torch.testing.assert_close(f1, f0, rtol=1e-6, atol=1e-7)
     assert torch.equal(k1, k0)
     torch.testing.assert_close(v1, v0, rtol=1e-6, atol=1e-7)
+
+
+def test_dcn_v2_adam_overlap_matches_plain(monkeypatch):
+    """with PBX_ADAM_OVERLAP=1 the DCN-V2 cross forward must see
+    the updated cross weights (the overlapped Adam is joined before it)."""
+    eng, hbs, S = _setup(ring=4, n_batches=9)
+    f0, l0 = _run(eng, hbs, S, False, "bf16", 2, model="dcn_v2")
+    k0, v0 = eng.table.export(True)
+    eng2, hbs2, _ = _setup(ring=4, n_batches=9)
+    monkeypatch.setenv("PBX_ADAM_OVERLAP", "1")
+    f1, l1 = _run(eng2, hbs2, S, False, "bf16", 2, model="dcn_v2")
+    k1, v1 = eng2.table.export(True)
+    assert l1 == pytest.approx(l0, rel=1e-4, abs=1e-5)
+    torch.testing.assert_close(f1, f0, rtol=1e-4, atol=1e-5)
+    o0, o1 = torch.argsort(k0), torch.argsort(k1)
+    torch.testing.assert_close(v1[o1], v0[o0], rtol=1e-4, atol=1e-5)
