@@ -211,6 +211,9 @@ class Session:
                     if isinstance(o, FlatAdam) and all(w.untyped_storage().data_ptr() == fs for w in t.mlp.w):
                         o.fuse(mlps=list(o._fuse_mlps) + [t.mlp],
                                data_norms=list(o._fuse_dns) + ([t.dn] if t.dn is not None else []))
+                        # the packed copy predates the last (unfused) update:
+                        # the next forward packs, later updates re-pack
+                        t.mlp.invalidate_pack()
                         t._opt_fused = True
                         break
             if metrics is not None and t.auc is not None and (

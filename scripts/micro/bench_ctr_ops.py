@@ -36,14 +36,23 @@ def timed(fn, iters):
     return a.elapsed_time(b) / iters * 1e3  # us
 
 
-def report(name, shape, flops_fwd, f_fwd, f_train, ref_fn, iters):
+def report(name, shape, flops_fwd, f_fwd, f_train, ref_fn, iters, bwd_args=None):
+    """bwd_args = (inputs, d): the backward alone, timed as
+    torch.autograd.grad over a retained graph (no .grad accumulation kernels,
+    no forward) -- the number the VERDICT targets."""
     us_f = timed(f_fwd, iters)
     us_t = timed(f_train, iters)
     us_r = timed(ref_fn, iters)
-    print(json.dumps({"op": name, "shape": shape, "fwd_us": round(us_f, 1), "fwd_bwd_us": round(us_t, 1),
-                      "fwd_tflops": round(flops_fwd / us_f / 1e6, 2),
-                      "fwd_bwd_tflops": round(3 * flops_fwd / us_t / 1e6, 2),
-                      "torch_fp32_matmul_same_flops_us": round(us_r, 1)}), flush=True)
+    rec = {"op": name, "shape": shape, "fwd_us": round(us_f, 1), "fwd_bwd_us": round(us_t, 1),
+           "fwd_tflops": round(flops_fwd / us_f / 1e6, 2), "fwd_bwd_tflops": round(3 * flops_fwd / us_t / 1e6, 2),
+           "torch_fp32_matmul_same_flops_us": round(us_r, 1)}
+    if bwd_args is not None:
+        ins, d = bwd_args
+        y = f_fwd()
+        us_b = timed(lambda: torch.autograd.grad(y, ins, d, retain_graph=True), iters)
+        rec["bwd_us"] = round(us_b, 1)
+        rec["bwd_tflops"] = round(2 * flops_fwd / us_b / 1e6, 2)
+    print(json.dumps(rec), flush=True)
 
 
 def main():
@@ -61,7 +70,7 @@ def main():
     d = torch.randn(P, N, O, device=DEV)
     xr, wr = x.detach(), W.detach()
     report("batch_fc", [P, N, I, O], 2.0 * P * N * I * O, lambda: cx.batch_fc(x, W, bb),
-           lambda: cx.batch_fc(x, W, bb).backward(d), lambda: torch.bmm(xr, wr), it)
+           lambda: cx.batch_fc(x, W, bb).backward(d), lambda: torch.bmm(xr, wr), it, ([x, W, bb], d))
 
     # scaled_fc: [N, K] x [K, O]
     N, K, O = 8192, 400, 400
@@ -71,7 +80,7 @@ def main():
     d = torch.randn(N, O, device=DEV)
     xr, wr = x.detach(), W.detach()
     report("scaled_fc", [N, K, O], 2.0 * N * K * O, lambda: cx.scaled_fc(x, W, bb, 8.0, 2.0),
-           lambda: cx.scaled_fc(x, W, bb, 8.0, 2.0).backward(d), lambda: xr @ wr, it)
+           lambda: cx.scaled_fc(x, W, bb, 8.0, 2.0).backward(d), lambda: xr @ wr, it, ([x, W, bb], d))
 
     # rank_attention: B instances, R ranks, x width C, output P
     for R in (3, 8):
@@ -84,7 +93,7 @@ def main():
         xr = torch.randn(B, R * C, device=DEV)
         wr = torch.randn(R * C, Pp, device=DEV)
         report(f"rank_attention_R{R}", [B, R, C, Pp], 2.0 * B * R * C * Pp, lambda: cx.rank_attention(x, ro, W, R),
-               lambda: cx.rank_attention(x, ro, W, R).backward(d), lambda: xr @ wr, it)
+               lambda: cx.rank_attention(x, ro, W, R).backward(d), lambda: xr @ wr, it, ([x, W], d))
 
     # scaled_int8fc: int8 MFMA forward, fp32 straight-through backward
     # (scaled_int8fc_op.cu:290-440 registers both)
@@ -97,7 +106,7 @@ def main():
     at = dict(input_expand_factor=10.0, input_clip_factor=3.0, weight_expand_factor=40.0, weight_clip_factor=5.0,
               int8_range=127.0)
     report("scaled_int8fc", [N, K, O], 2.0 * N * K * O, lambda: cx.scaled_int8fc(x, W, bb, at),
-           lambda: cx.scaled_int8fc(x, W, bb, at).backward(d), lambda: xr @ wr, it)
+           lambda: cx.scaled_int8fc(x, W, bb, at).backward(d), lambda: xr @ wr, it, ([x, W, bb], d))
 
 
 if __name__ == "__main__":
