@@ -159,8 +159,8 @@ def main():
                     help="after the measurement, time this many more K-step windows (stderr only)")
     ap.add_argument("--graph-steps", type=int, default=-1,
                     help="training steps per captured HIP graph (0 = auto: the largest k <= 8 dividing both --steps "
-                         "and --warmup).  Default -1: 2 when it divides --steps (pipelined fp32 step 0.371 vs 0.393 "
-                         "ms at K = 1, 0.377 at K = 5, profiles/r4_graph_steps_ab.txt), else 1")
+                         "and --warmup).  Default -1: 4 on one rank when it divides --steps, else 2 when it "
+                         "does, else 1 (multi-rank: 2); see graph_steps_for")
     ap.add_argument("--graph-warm", type=int, default=32,
                     help="load+replay cycles run right after capture (runtime warm-up, part of graph setup)")
     ap.add_argument("--trace-steps", type=int, default=0,

@@ -62,6 +62,59 @@ void sgemm(const Tensor& A, const Tensor& B, Tensor C, const c10::optional<Tenso
   launch_sgemm(g, cs());
 }
 
+// batch_fc with slots of at most 64 x 64 (launch_batch_fc_fwd / _bwd).
+// strides = (sx, rx, sw, rw, sy, ry, sb); False when the shape / alignment
+// does not fit the dedicated kernels (nothing launched).
+BfcArgs bfc_args(const Tensor& x, const Tensor& W, const Tensor& yy, int64_t Pn, int64_t N, int64_t I, int64_t O,
+                 const std::vector<int64_t>& st) {
+  f32(x, "x");
+  f32(W, "W");
+  f32(yy, "y/dy");
+  CX_CHECK(st.size() == 7, "strides are (sx, rx, sw, rw, sy, ry, sb)");
+  BfcArgs a;
+  a.P = (int)Pn; a.N = (int)N; a.I = (int)I; a.O = (int)O;
+  a.sx = st[0]; a.rx = st[1]; a.sw = st[2]; a.rw = st[3]; a.sy = st[4]; a.ry = st[5]; a.sb = st[6];
+  auto span = [](int64_t b, int64_t sb, int64_t r, int64_t sr, int64_t c) { return (b - 1) * sb + (r - 1) * sr + c - 1; };
+  if (Pn > 0 && N > 0) {
+    CX_CHECK(span(Pn, a.sx, N, a.rx, I) < x.numel(), "x too small for its strides");
+    CX_CHECK(span(Pn, a.sw, I, a.rw, O) < W.numel(), "W too small for its strides");
+    CX_CHECK(span(Pn, a.sy, N, a.ry, O) < yy.numel(), "y too small for its strides");
+  }
+  return a;
+}
+
+bool batch_fc_fwd(const Tensor& x, const Tensor& W, const Tensor& b, Tensor y, int64_t Pn, int64_t N, int64_t I,
+                  int64_t O, std::vector<int64_t> st) {
+  BfcArgs a = bfc_args(x, W, y, Pn, N, I, O, st);
+  f32(b, "b");
+  CX_CHECK(Pn == 0 || (Pn - 1) * a.sb + O <= b.numel(), "b too small for its stride");
+  a.x = P<float>(x);
+  a.W = P<float>(W);
+  a.b = P<float>(b);
+  a.y = P<float>(y);
+  return launch_batch_fc_fwd(a, cs());
+}
+
+bool batch_fc_bwd(const Tensor& x, const Tensor& W, const Tensor& dy, Tensor dx, Tensor dW, Tensor db, int64_t Pn,
+                  int64_t N, int64_t I, int64_t O, std::vector<int64_t> st) {
+  BfcArgs a = bfc_args(x, W, dy, Pn, N, I, O, st);
+  f32(dx, "dx");
+  f32(dW, "dW");
+  f32(db, "db");
+  CX_CHECK(dx.numel() == x.numel() && dW.numel() == W.numel(), "dx / dW must have x / W's layout");
+  CX_CHECK(Pn == 0 || (Pn - 1) * a.sb + O <= db.numel(), "db too small for its stride");
+  a.x = P<float>(x);
+  a.W = P<float>(W);
+  a.dy = P<float>(dy);
+  a.dx = P<float>(dx);
+  a.dW = P<float>(dW);
+  a.db = P<float>(db);
+  const int64_t G = batch_fc_bwd_groups(a.P, a.N);
+  Tensor ws = torch::empty({std::max<int64_t>(1, G * Pn * kBfcPart)}, x.options());
+  a.ws = P<float>(ws);
+  return launch_batch_fc_bwd(a, cs());
+}
+
 // scaled_fc's fp16 GEMM (launch_hgemm): C [M, ldc] fp32 from strided fp32
 // A [M x K] (rsA, csA) and B [K x N] (rsB, csB) with the reference rounding
 void hgemm(const Tensor& A, const Tensor& B, Tensor C, const c10::optional<Tensor>& bias, int64_t M, int64_t N,
@@ -171,19 +224,27 @@ std::vector<Tensor> rank_attention_fwd(const Tensor& x, const Tensor& ro, const 
   return {out, bucket};
 }
 
+// part 0: dx and dW; 1: dx only (dexp + the gather merge); 2: dW only --
+// parts 1 and 2 are independent (both read dout): the caller may run them on
+// two streams
 std::vector<Tensor> rank_attention_bwd(const Tensor& x, const Tensor& ro, const Tensor& W, const Tensor& dout,
-                                       const Tensor& bucket, int64_t R) {
+                                       const Tensor& bucket, int64_t R, int64_t part) {
   f32(x, "x");
   f32(dout, "dout");
   CX_CHECK(bucket.scalar_type() == torch::kInt32 && bucket.numel() == rank_attention_bucket_ints((int)x.size(0), (int)R),
            "bucket must come from rank_attention_fwd with the same B and R");
   const int B = (int)x.size(0), C = (int)x.size(1), P_ = (int)W.size(1);
   auto xc = x.contiguous(), Wc = W.contiguous(), roc = ro.contiguous(), dc = dout.contiguous();
-  auto dexp = torch::empty({B, R, C}, x.options());
-  auto dx = torch::empty_like(xc);
-  auto dW = torch::zeros_like(Wc);
+  CX_CHECK(part >= 0 && part <= 2, "rank_attention_bwd: part");
+  Tensor dexp, dx, dW;
+  if (part != 2) {
+    dexp = torch::empty({B, R, C}, x.options());
+    dx = torch::empty_like(xc);
+  }
+  if (part != 1) dW = torch::zeros_like(Wc);
   launch_rank_attention_bwd(P<float>(xc), P<float>(dc), P<int>(roc), (int)roc.size(1), P<float>(Wc), B, C, P_,
-                            (int)R, P<int>(bucket), P<float>(dexp), P<float>(dx), P<float>(dW), cs());
+                            (int)R, P<int>(bucket), part != 2 ? P<float>(dexp) : nullptr,
+                            part != 2 ? P<float>(dx) : nullptr, part != 1 ? P<float>(dW) : nullptr, cs());
   return {dx, dW};
 }
 
@@ -441,7 +502,10 @@ void bind_ctr(py::module& m) {
   m.def("sfc", &sfc);
   m.def("int8_fc", &int8_fc);
   m.def("rank_attention_fwd", &rank_attention_fwd);
-  m.def("rank_attention_bwd", &rank_attention_bwd);
+  m.def("batch_fc_fwd", &batch_fc_fwd);
+  m.def("batch_fc_bwd", &batch_fc_bwd);
+  m.def("rank_attention_bwd", &rank_attention_bwd, py::arg("x"), py::arg("ro"), py::arg("W"), py::arg("dout"),
+        py::arg("bucket"), py::arg("R"), py::arg("part") = 0);
   m.def("cvm_fwd", &cvm_fwd);
   m.def("cvm_bwd", &cvm_bwd);
   m.def("masked_dn_fwd", &masked_dn_fwd);

@@ -743,6 +743,43 @@ struct SgemmArgs {
   int ksplit = 1;  // set by launch_sgemm: K slices per output tile (fp32 atomics)
 };
 void launch_sgemm(const SgemmArgs& g, hipStream_t s);
+// batch_fc with every slot's fc at most 64 x 64 (the CTR shapes): one block
+// per (slot, run of 64-row tiles) keeps W_p in LDS and streams x / dy tiles
+// through it.  Operands are (slot stride, row stride) with unit columns:
+// x, dx (sx, rx); W, dW (sw, rw); y, dy (sy, ry); b, db (sb).  The backward
+// computes dx, dW and db from one read of x and dy: every block writes its
+// dW / db partial to ws ([P][G][64*64 + 64], G = batch_fc_bwd_groups) and an
+// ordered second pass sums them (deterministic, no atomics).  Both return
+// false when the shapes or alignment do not fit (the caller runs the generic
+// k_mgemm path).
+struct BfcArgs {
+  const float* x = nullptr;
+  const float* W = nullptr;
+  const float* b = nullptr;
+  float* y = nullptr;
+  const float* dy = nullptr;
+  float* dx = nullptr;
+  float* dW = nullptr;
+  float* db = nullptr;
+  int P = 0, N = 0, I = 0, O = 0;
+  int64_t sx = 0, rx = 0, sw = 0, rw = 0, sy = 0, ry = 0, sb = 0;
+  float* ws = nullptr;  // backward partials, batch_fc_bwd_groups(P, N) * P * kBfcPart floats
+  int tiles = 1;        // 64-row tiles per block (set by the launcher)
+};
+constexpr int kBfcPart = 64 * 64 + 64;
+// 64-row tiles per block: about `blocks` blocks over the launch
+inline int batch_fc_tiles(int P, int N, int blocks) {
+  const int ntile = (N + 63) / 64;
+  const int want = blocks / (P > 0 ? P : 1) > 0 ? blocks / (P > 0 ? P : 1) : 1;
+  const int t = (ntile + want - 1) / want;
+  return t > 0 ? t : 1;
+}
+inline int batch_fc_bwd_groups(int P, int N) {
+  const int tiles = batch_fc_tiles(P, N, 768);
+  return ((N + 63) / 64 + tiles - 1) / tiles;
+}
+bool launch_batch_fc_fwd(const BfcArgs& a, hipStream_t s);
+bool launch_batch_fc_bwd(const BfcArgs& a, hipStream_t s);
 // scaled_fc's fp16 GEMMs with the reference's rounding points
 // (scaled_fc_op.cu:144-330): operands a_scale * A, b_scale * B rounded to
 // fp16, fp32-accumulated MFMA (v_mfma_f32_16x16x32_f16), then

@@ -14,6 +14,7 @@ CPU path and the fp32 reference the GPU tests compare against
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -676,7 +677,17 @@ class _RankAttentionHip(torch.autograd.Function):
     def backward(ctx, dout):
         x, ro, W, bucket = ctx.saved_tensors
         h = _native.hip()
-        dx, dW = h.rank_attention_bwd(x, ro, W.contiguous(), dout.contiguous(), bucket, ctx.R)
+        dout = dout.contiguous()
+        Wc = W.contiguous()
+        # dW (per-rank A^T dout) beside dexp + the gather merge on a side stream
+        cur = torch.cuda.current_stream(dout.device)
+        side = _ctr_side(dout.device, want=ctx.R >= 6)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            _, dW = h.rank_attention_bwd(x, ro, Wc, dout, bucket, ctx.R, 2)
+        dx, _ = h.rank_attention_bwd(x, ro, Wc, dout, bucket, ctx.R, 1)
+        cur.wait_stream(side)
+        dW.record_stream(cur)  # allocated on the side stream, consumed here
         return dx, None, dW, None
 
 
@@ -714,24 +725,31 @@ class _BatchFcHip(torch.autograd.Function):
     def forward(ctx, x, W, b, mode):
         P, N, I, O, xst, wst, (sC, ldc), sb, oshape = _batch_fc_geom(mode, x.shape, W.shape)
         y = x.new_empty(oshape)
-        _sg(x, W, y, N, O, I, P, xst, wst, sC, ldc, b, sb)
+        # slots of at most 64 x 64 (CTR shapes): k_bfc_fwd keeps W_p in LDS and
+        # streams x once; otherwise the strided batched k_mgemm
+        st = [xst[0], xst[1], wst[0], wst[1], sC, ldc, sb]
+        if not _native.hip().batch_fc_fwd(x, W, b, y, P, N, I, O, st):
+            _sg(x, W, y, N, O, I, P, xst, wst, sC, ldc, b, sb)
         ctx.save_for_backward(x, W)
-        ctx.geom, ctx.bshape = (P, N, I, O, xst, wst, sC, ldc), b.shape
+        ctx.geom, ctx.bshape = (P, N, I, O, xst, wst, sC, ldc, sb), b.shape
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
-        P, N, I, O, xst, wst, sC, ldc = ctx.geom
+        P, N, I, O, xst, wst, sC, ldc, sb = ctx.geom
         dy = dy.float().contiguous()
         h = _native.hip()
         dx = torch.empty_like(x)
+        # fused: dx, dW, db from one pass over x and dy (k_bfc_bwd + ordered reduce)
+        dW = torch.empty_like(W)
+        db = x.new_empty(ctx.bshape)
+        if h.batch_fc_bwd(x, W, dy, dx, dW, db, P, N, I, O, [xst[0], xst[1], wst[0], wst[1], sC, ldc, sb]):
+            return dx, dW, db, None
         # dx[p] (N x I) = dy[p] (N x O) . W[p]^T (O x I); dx shares x's strides
         _sg(dy, W, dx, N, I, O, P, (sC, ldc, 1), (wst[0], wst[2], wst[1]), xst[0], xst[1])
         # dW[p] (I x O) = x[p]^T (I x N) . dy[p] (N x O); dW shares W's strides
-        dW = torch.empty_like(W)
         _sg(x, dy, dW, I, O, N, P, (xst[0], xst[2], xst[1]), (sC, ldc, 1), wst[0], wst[1])
-        db = x.new_empty(ctx.bshape)
         h.colsum_strided(dy, P, N, O, sC, ldc, db, O, False)
         return dx, dW, db, None
 
@@ -763,6 +781,22 @@ def batch_fc(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, batchcount: int 
 
 
 # ================================================================== scaled fc family
+def _ctr_side(device, want: bool = True):
+    """Side stream of a CTR op backward: its weight-gradient GEMM runs there
+    beside the input-gradient GEMM, or -- ``want`` False, or
+    PBX_CTR_BWD_SIDE=0/1 forcing either way -- the calling stream.  Measured
+    GPU time of the graphed backward, side vs one stream
+    (profiles/r5_ctr_ops_side_ab.txt): scaled_fc 83.0 vs 70.8 us, scaled_int8fc
+    120.1 vs 102.5, rank_attention R3 44.8 vs 41.3 but R8 69.6 vs 79.8 -- both
+    halves fill the GPU alone except rank_attention's wide-R dW."""
+    from ..runtime.streams import side_stream
+
+    force = os.environ.get("PBX_CTR_BWD_SIDE", "")
+    if force in ("0", "1"):
+        want = force == "1"
+    return side_stream(device, "ctr_bwd") if want else torch.cuda.current_stream(device)
+
+
 def _fc_backward_hip(x, W, dy):
     """dx = dy W^T, dW = x^T dy, db = colsum(dy) for x [N, K], W [K, O]."""
     N, K = x.shape
@@ -874,15 +908,24 @@ class _ScaledFc(torch.autograd.Function):
         O = W.shape[1]
         if ctx.fused:
             h = _native.hip()
-            # dx = fp16(dy * gs / in_scale) @ W16^T in one launch (k_sfc, Bk = W16 [K, O])
+            # dx = fp16(dy * gs / in_scale) @ W16^T in one launch (k_sfc, Bk = W16
+            # [K, O]); dW = x16^T d16 in one split-K launch (k_hgemm: both casts
+            # and the reference fp16 epilogue in the kernel, ~256 rows of N per
+            # split) and db = colsum(dy) -- on _ctr_side's stream choice
+            cur = torch.cuda.current_stream(dy.device)
+            side = _ctr_side(dy.device, want=False)
+            side.wait_stream(cur)
+            dW = W.new_empty(K, O)
+            db = dy.new_empty(O)
             dx = h.sfc(dy, _half_of(W), None, gs / in_scale, in_scale, 1.0, 1.0 / gs)
-            d16 = (dy * (gs / in_scale)).half()
-            dWa = _mm16(x.half().t(), d16) if dx is not None else None
-            if dWa is not None:
-                h.h16_epi(dWa, None, in_scale, 1.0, 1.0 / gs)
-                db = dy.new_empty(O)
-                h.colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
-                return dx, dWa, db.reshape(ctx.bshape), None, None, None
+            if dx is not None:
+                with torch.cuda.stream(side):
+                    h.hgemm(x, dy, dW, None, K, O, N, [1, K], [O, 1], O, 1.0, gs / in_scale, in_scale, 1.0, 1.0 / gs,
+                            max(1, min(64, N // 256)))
+                    h.colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
+                cur.wait_stream(side)
+                return dx, dW, db.reshape(ctx.bshape), None, None, None
+            cur.wait_stream(side)
         if ctx.half_ops:  # x, W are the forward's fp16 casts
             h = _native.hip()
             d16 = (dy * (gs / in_scale)).half()
@@ -960,7 +1003,21 @@ class _ScaledInt8Fc(torch.autograd.Function):
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
         if x.is_cuda:
-            dx, dW, db = _fc_backward_hip(x, W, dy)
+            # the reference straight-through backward is two fp32 GEMMs
+            # (scaled_int8fc_op.cu:382-440): library fp32 GEMMs (hipBLASLt)
+            # and the column sum, on _ctr_side's stream choice
+            dy = dy.float().contiguous()
+            cur = torch.cuda.current_stream(dy.device)
+            side = _ctr_side(dy.device, want=False)
+            side.wait_stream(cur)
+            N, O = dy.shape
+            dW = torch.empty_like(W)
+            db = dy.new_empty(O)
+            dx = torch.mm(dy, W.t())
+            with torch.cuda.stream(side):
+                torch.mm(x.t(), dy, out=dW)
+                _native.hip().colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
+            cur.wait_stream(side)
         else:
             dx, dW, db = dy @ W.t(), x.t() @ dy, dy.sum(0)
         return dx, dW, db.reshape(ctx.bshape), None

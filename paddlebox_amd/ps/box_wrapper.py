@@ -355,7 +355,7 @@ class BoxWrapper:
         """Host tier current: finish the background write-back and, inside a
         pass, write the live GPU rows back synchronously first."""
         if self.tier is not None:
-            if self.in_pass:
+            if self.in_pass or self.tier.retained:
                 self.tier.flush()
             self.tier.wait_writeback()
         elif self.mode == "tiered" and self.engine is not None and self.in_pass:
@@ -363,19 +363,24 @@ class BoxWrapper:
             self.host.assign(h.cpu(), v.cpu())
 
     def _reset_delta_live(self, hk: torch.Tensor):
-        """save_xbox reset delta_score of the saved rows in the host tier; in a
-        pass the live GPU rows must see the reset too, or the EndPass write-back
-        would restore the old scores."""
-        if self.mode != "tiered" or not self.in_pass or self.engine is None or hk.numel() == 0:
+        """save_xbox reset delta_score of the saved rows in the host tier; the
+        live GPU rows must see the reset too -- in a pass, or between passes
+        with the GPU tier (its activation carries live rows into the next
+        pass) -- or a later write-back would restore the old scores."""
+        if self.mode != "tiered" or self.engine is None or hk.numel() == 0:
             return
-        t = self.engine.table
-        h = hk.to(t.device)
-        rows = t.probe(h)
-        ok = rows >= 0
-        if bool(ok.any()):
-            v = t.values[rows[ok]].clone()
-            v[:, row_layout(self.cfg.embedx_dim)["delta_score"]] = 0
-            t.t.assign(rows[ok], v)
+        if not self.in_pass and self.tier is None:
+            return
+        # the staged next pass gathered its host rows before this reset
+        tables = self.tier.staged_tables() if self.tier is not None else [self.engine.table]
+        for t in tables:
+            h = hk.to(t.device)
+            rows = t.probe(h)
+            ok = rows >= 0
+            if bool(ok.any()):
+                v = t.values[rows[ok]].clone()
+                v[:, row_layout(self.cfg.embedx_dim)["delta_score"]] = 0
+                t.t.assign(rows[ok], v)
 
     def save_base(self, batch_model_path: str, xbox_model_path: str, date: str = "") -> str:
         """Full batch model + xbox base (box_wrapper.cc:1286-1305)."""
@@ -543,11 +548,15 @@ class BoxWrapper:
         """ShrinkTable (box_wrapper.h:638): decay show/click, age, delete
         (ctr_accessor.cc:63-80) over the whole table -- in tiered mode the
         host tier and every SSD record.  Inside a pass the live GPU rows are
-        shrunk by the same rule, so the next write-back keeps the result."""
+        shrunk by the same rule, so the next write-back keeps the result (and
+        between passes with the GPU tier, whose activation carries live rows
+        into the next pass)."""
         t = self._authoritative()
         gone = t.shrink(self.cfg.shrink)
-        if self.mode == "tiered" and self.in_pass and self.engine is not None:
+        if self.mode == "tiered" and self.engine is not None and (self.in_pass or self.tier is not None):
             self.engine.table.shrink(self.cfg.shrink)
+        if self.tier is not None and not self.in_pass:
+            self.tier.restage()  # a staged next pass read its host rows before the shrink
         return gone
 
     def shrink_resource(self):

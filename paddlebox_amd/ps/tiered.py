@@ -257,7 +257,7 @@ class TierView:
 
 class TieredStore:
     def __init__(self, engine, host: HostTable, ssd: Optional[SsdTier] = None, sgd: Optional[SparseSGDConfig] = None,
-                 spill_unseen: float = 1.0, host_cap_rows: int = 0):
+                 spill_unseen: float = 1.0, host_cap_rows: int = 0, retain: bool = True):
         from .gpu_table import GpuSparseTable
 
         self.engine = engine
@@ -267,6 +267,11 @@ class TieredStore:
         self.spill_unseen = spill_unseen
         self.host_cap_rows = int(host_cap_rows)
         self.epoch = 0  # pass stamp of host rows: write-back count
+        # keep rows the next pass uses again on the GPU across the pass
+        # boundary: the staging looks up only keys the live table lacks and
+        # the write-back moves only rows the next pass drops
+        self.retain = bool(retain)
+        self.retained = False  # the last write-back left rows newer than their host copy on the GPU
         live = engine.table
         self.live = live
         if live.codec is not None:
@@ -290,9 +295,11 @@ class TieredStore:
         # out from under a staging gather
         self._tier_lock = threading.Lock()
         self._staged_keys: Optional[torch.Tensor] = None
+        self._staged_src: Optional[torch.Tensor] = None  # the staged pass's keys as given (CPU)
         self._pin = {}  # reusable pinned staging buffers (pinning is slow)
         self.stats = {"stage_s": 0.0, "writeback_s": 0.0, "activate_s": 0.0, "spill_s": 0.0, "ssd_hits": 0,
-                      "spilled": 0, "spilled_cap": 0, "staged_rows": 0, "new_rows": 0, "host_rows_staged": 0}
+                      "spilled": 0, "spilled_cap": 0, "staged_rows": 0, "new_rows": 0, "host_rows_staged": 0,
+                      "retained_rows": 0, "wb_retained_rows": 0}
 
     def _pinned(self, name: str, shape, dtype) -> torch.Tensor:
         n = 1
@@ -320,6 +327,19 @@ class TieredStore:
         locked = False
         try:
             t0 = time.perf_counter()
+            dev = self.live.device
+            hd_all = None
+            self._staged_src = hc
+            if self.retain and self.live.size() > 0:
+                # keys the live table already holds come from it at activation
+                # (newest values): only the rest is looked up in the host / SSD
+                # tiers.  The probe only reads keys -- the running pass updates
+                # values, never the key set -- so it runs beside the training.
+                with torch.cuda.device(dev), torch.cuda.stream(self.stream):
+                    hd_all = hc.to(dev, non_blocking=True)
+                    outside = (self.live.probe(hd_all) < 0).cpu()
+                hc_all, hc = hc, hc[outside]
+                self.stats["retained_rows"] += int(hc_all.numel() - hc.numel())
             self.wait_writeback()  # host values of earlier passes must be final
             self._tier_lock.acquire()
             locked = True
@@ -342,11 +362,10 @@ class TieredStore:
             self.host._native.gather(rows[known].contiguous(), buf)
             self._tier_lock.release()
             locked = False
-            dev = self.live.device
             with torch.cuda.device(dev), torch.cuda.stream(self.stream):
                 st = self.stage_table
                 st.clear()
-                hd = hc.to(dev, non_blocking=True)
+                hd = hd_all if hd_all is not None else hc.to(dev, non_blocking=True)
                 st.insert_mixed(hd, self.sgd)  # new keys get the standard GPU init
                 if kh.numel():
                     st.assign(kh.to(dev, non_blocking=True), buf.to(dev, non_blocking=True))
@@ -360,6 +379,20 @@ class TieredStore:
             self._stage_err = e
             if locked:
                 self._tier_lock.release()
+
+    def restage(self):
+        """Stage the already-staged next pass again: its rows were gathered
+        before a between-pass mutation of the tiers (ShrinkTable) that they
+        must see."""
+        self.wait_stage()
+        if self._staged_keys is not None and self._staged_src is not None:
+            self.stage(self._staged_src)
+
+    def staged_tables(self):
+        """The GPU tables whose rows become (or stay) live at the next
+        activation: the live table, plus the staged one when a pass is staged."""
+        self.wait_stage()
+        return [self.live] + ([self.stage_table] if self._staged_keys is not None else [])
 
     def wait_stage(self):
         if self._stage_thread is not None:
@@ -392,11 +425,24 @@ class TieredStore:
         self.stats["activate_s"] += time.perf_counter() - t0
 
     # ------------------------------------------------------------ EndPass
-    def writeback(self, block: bool = False):
+    def writeback(self, block: bool = False, full: bool = False):
         """Export the live table and move it into the host tier (then spill
-        cold rows to SSD) in the background."""
+        cold rows to SSD) in the background.  With ``retain`` and the next
+        pass staged, rows the next pass uses again stay on the GPU (activation
+        carries them over) and only the others are written back; ``full``
+        (flush: a save / shrink needs the host tier current) writes every row."""
         self.wait_writeback()
         k, v = self.live.export(True)  # device copies: the live table may change after this
+        self.retained = False
+        if self.retain and not full and self._stage_thread is not None:
+            self.wait_stage()  # the next pass's key set decides what stays
+        if self.retain and not full and self._staged_keys is not None and k.numel():
+            keep = self.stage_table.probe(k) < 0  # not in the next pass: evicted from the GPU
+            n_ret = int(k.numel()) - int(keep.sum())
+            if n_ret:
+                k, v = k[keep], v[keep]
+                self.retained = True
+                self.stats["wb_retained_rows"] += n_ret
         ev = torch.cuda.Event()
         main = torch.cuda.current_stream(self.live.device)
         self.stream.wait_stream(main)  # the export kernel has to finish first
@@ -461,5 +507,6 @@ class TieredStore:
                 raise e
 
     def flush(self):
-        """Synchronous write-back of the live table (save in the middle of a pass)."""
-        self.writeback(block=True)
+        """Synchronous write-back of every live row (a save / shrink in the
+        middle of a pass, or after an EndPass that retained rows)."""
+        self.writeback(block=True, full=True)

@@ -8,8 +8,11 @@ optimizer are captured once into a HIP graph and replayed per batch (the
 reference instead runs an op list with several stream syncs per batch,
 ``boxps_worker.cc:1296-1324``).
 
-Input buffers are double-buffered with one graph per buffer set, so the H2D
-copy of batch i+1 (copy stream) overlaps the replay of batch i.
+Input buffers are double-buffered with one graph per buffer set, so the copy
+of batch i+1 (copy stream) overlaps the replay of batch i.  The bench and the
+device-pass trainer keep whole passes resident in HBM, so that copy is a D2D
+gather into the graph's input buffers; host batches (``--inputs host``, the
+host-assembly fallback) arrive through one pinned H2D copy per buffer set.
 """
 from __future__ import annotations
 
@@ -85,10 +88,13 @@ class GraphedTrainStep:
         ``run`` trains all K).  Inside one graph consecutive steps are
         separated by a kernel boundary only; between graphs the replay pays
         the graph-launch boundary and the wait on the batch copy once per K
-        steps.  Measured no faster for the DeepFM step on MI355X (K = 5, 8 vs
-        1: 0.27-0.29 vs 0.27 ms/step, profiles/r3_s2_multistep_graph.txt):
-        the ~20 us between replays is not launch overhead, so K = 1 stays the
-        default.
+        steps.  The constructor's default stays K = 1 (a single-step graph
+        is what eager-equivalence tests and the host-input path use); the
+        bench and the fluid trainer pass K = 4 with the pipelined front
+        (``bench.py --graph-steps``, FLAGS_padbox_train_steps_per_graph),
+        where K = 4 vs 2 vs 1 measured 0.362-0.364 vs ~0.368 vs 0.393
+        ms/step (profiles/r4_input_stall.txt, r4_graph_steps_ab.txt; the
+        round-3 measurement without the pipelined front showed no gain).
         ``prefetch``: optional (engine, keys_of) -- pipelined sparse pull:
         graph j also runs the dedup + probe of buffer j+1's keys on a side
         stream while batch j trains (SparseEngine.prefetch, pull slot = buffer

@@ -36,11 +36,38 @@ def timed(fn, iters):
     return a.elapsed_time(b) / iters * 1e3  # us
 
 
-def report(name, shape, flops_fwd, f_fwd, f_train, ref_fn, iters, bwd_args=None):
+def graphed(fn, iters):
+    """GPU time of fn without the host launch/autograd overhead: fn captured
+    once into a HIP graph (warmed on a side stream first), the replay timed.
+    None when fn cannot be captured (a host sync inside)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(g):
+            fn()
+    except RuntimeError:
+        return None
+    return timed(g.replay, iters)
+
+
+def report(name, shape, flops_fwd, f_fwd, f_train, ref_fn, iters, bwd_args=None, fwd_of=None):
     """bwd_args = (inputs, d): the backward alone, timed as
     torch.autograd.grad over a retained graph (no .grad accumulation kernels,
     no forward) -- the number the VERDICT targets."""
     us_f = timed(f_fwd, iters)
+    if bwd_args is not None:  # a training step starts from zero_grad(set_to_none=True): no .grad accumulation adds
+        f_train0 = f_train
+
+        def f_train():
+            for t in bwd_args[0]:
+                t.grad = None
+            f_train0()
     us_t = timed(f_train, iters)
     us_r = timed(ref_fn, iters)
     rec = {"op": name, "shape": shape, "fwd_us": round(us_f, 1), "fwd_bwd_us": round(us_t, 1),
@@ -48,10 +75,25 @@ def report(name, shape, flops_fwd, f_fwd, f_train, ref_fn, iters, bwd_args=None)
            "torch_fp32_matmul_same_flops_us": round(us_r, 1)}
     if bwd_args is not None:
         ins, d = bwd_args
+        fwd_of = fwd_of or (lambda *a: f_fwd())
         y = f_fwd()
         us_b = timed(lambda: torch.autograd.grad(y, ins, d, retain_graph=True), iters)
         rec["bwd_us"] = round(us_b, 1)
         rec["bwd_tflops"] = round(2 * flops_fwd / us_b / 1e6, 2)
+        # forward and forward+backward replayed from HIP graphs: GPU time
+        # alone (the eager numbers above include the autograd engine's host
+        # time, which dominates at these ~50 us shapes).  The forward is
+        # captured with its backward: autograd runs a backward op on the
+        # stream its forward ran on, so both must be on the capture stream.
+        # fresh leaves: the eager runs above left AccumulateGrad nodes bound
+        # to the default stream on the originals
+        fresh = [t.detach().clone().requires_grad_() for t in ins]
+        print(f"# {name}: capturing", file=sys.stderr, flush=True)
+        gf = graphed(lambda: fwd_of(*fresh), iters)
+        gt = graphed(lambda: torch.autograd.grad(fwd_of(*fresh), fresh, d), iters)
+        rec["fwd_graph_us"] = None if gf is None else round(gf, 1)
+        rec["fwd_bwd_graph_us"] = None if gt is None else round(gt, 1)
+        rec["bwd_graph_us"] = None if gf is None or gt is None else round(gt - gf, 1)
     print(json.dumps(rec), flush=True)
 
 
@@ -70,7 +112,8 @@ def main():
     d = torch.randn(P, N, O, device=DEV)
     xr, wr = x.detach(), W.detach()
     report("batch_fc", [P, N, I, O], 2.0 * P * N * I * O, lambda: cx.batch_fc(x, W, bb),
-           lambda: cx.batch_fc(x, W, bb).backward(d), lambda: torch.bmm(xr, wr), it, ([x, W, bb], d))
+           lambda: cx.batch_fc(x, W, bb).backward(d), lambda: torch.bmm(xr, wr), it, ([x, W, bb], d),
+           fwd_of=lambda x, W, bb: cx.batch_fc(x, W, bb))
 
     # scaled_fc: [N, K] x [K, O]
     N, K, O = 8192, 400, 400
@@ -80,7 +123,8 @@ def main():
     d = torch.randn(N, O, device=DEV)
     xr, wr = x.detach(), W.detach()
     report("scaled_fc", [N, K, O], 2.0 * N * K * O, lambda: cx.scaled_fc(x, W, bb, 8.0, 2.0),
-           lambda: cx.scaled_fc(x, W, bb, 8.0, 2.0).backward(d), lambda: xr @ wr, it, ([x, W, bb], d))
+           lambda: cx.scaled_fc(x, W, bb, 8.0, 2.0).backward(d), lambda: xr @ wr, it, ([x, W, bb], d),
+           fwd_of=lambda x, W, bb: cx.scaled_fc(x, W, bb, 8.0, 2.0))
 
     # rank_attention: B instances, R ranks, x width C, output P
     for R in (3, 8):
@@ -93,7 +137,8 @@ def main():
         xr = torch.randn(B, R * C, device=DEV)
         wr = torch.randn(R * C, Pp, device=DEV)
         report(f"rank_attention_R{R}", [B, R, C, Pp], 2.0 * B * R * C * Pp, lambda: cx.rank_attention(x, ro, W, R),
-               lambda: cx.rank_attention(x, ro, W, R).backward(d), lambda: xr @ wr, it, ([x, W], d))
+               lambda: cx.rank_attention(x, ro, W, R).backward(d), lambda: xr @ wr, it, ([x, W], d),
+               fwd_of=lambda x, W, ro=ro, R=R: cx.rank_attention(x, ro, W, R))
 
     # scaled_int8fc: int8 MFMA forward, fp32 straight-through backward
     # (scaled_int8fc_op.cu:290-440 registers both)
@@ -106,7 +151,8 @@ def main():
     at = dict(input_expand_factor=10.0, input_clip_factor=3.0, weight_expand_factor=40.0, weight_clip_factor=5.0,
               int8_range=127.0)
     report("scaled_int8fc", [N, K, O], 2.0 * N * K * O, lambda: cx.scaled_int8fc(x, W, bb, at),
-           lambda: cx.scaled_int8fc(x, W, bb, at).backward(d), lambda: xr @ wr, it, ([x, W, bb], d))
+           lambda: cx.scaled_int8fc(x, W, bb, at).backward(d), lambda: xr @ wr, it, ([x, W, bb], d),
+           fwd_of=lambda x, W, bb: cx.scaled_int8fc(x, W, bb, at))
 
 
 if __name__ == "__main__":

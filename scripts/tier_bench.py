@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--spill-unseen", type=float, default=-1.0,
                     help="also spill host rows unseen for >= this many days (-1: off)")
     ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32")
+    ap.add_argument("--no-retain", action="store_true",
+                    help="write back / restage every row at each pass boundary (no GPU retention of next-pass rows)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -64,6 +66,8 @@ def main():
     cap = int(args.hbm_cap) if args.mode == "tiered" else int(args.hbm_cap) * args.passes
     box.initialize_gpu_and_load_model(slot_vector=list(range(1, S + 1)), max_keys=args.batch * S, capacity=cap,
                                       mode=args.mode, ssd_path=(args.ssd or None) if args.mode == "tiered" else None)
+    if box.tier is not None:
+        box.tier.retain = not args.no_retain
     t0 = time.perf_counter()
     passes = []
     for p in range(args.passes):
@@ -119,6 +123,9 @@ def main():
     wall = time.perf_counter() - t_all
     st = dict(box.tier.stats) if box.tier is not None else {}
     steady = rows[1:] if len(rows) > 1 else rows
+    mid = rows[1:-1] if len(rows) > 2 else steady
+    mid_wall = sum(r["begin_pass_ms"] + r["feed_call_ms"] + r["train_ms"] + r["end_pass_ms"] for r in mid) / 1e3
+    mid_train = sum(r["train_ms"] for r in mid) / 1e3
     train_s = sum(r["train_ms"] for r in rows) / 1e3
     out = {
         "mode": args.mode, "precision": args.precision, "passes": args.passes, "steps_per_pass": args.steps,
@@ -126,6 +133,13 @@ def main():
         "wall_s": round(wall, 3), "samples_per_s": round(args.passes * args.steps * args.batch / wall, 1),
         "train_only_samples_per_s": round(args.passes * args.steps * args.batch / train_s, 1),
         "train_ms_per_step": round(sum(r["train_ms"] for r in steady) / (len(steady) * args.steps), 4),
+        # steady state: passes 1 .. N-2 (pass 0 pays the first staging and the
+        # graph capture, the last one the final full write-back), each pass's
+        # main-thread wall = begin + feed call + train + end
+        "steady_passes": len(mid),
+        "steady_samples_per_s": round(len(mid) * args.steps * args.batch / max(mid_wall, 1e-9), 1),
+        "steady_train_only_samples_per_s": round(len(mid) * args.steps * args.batch / max(mid_train, 1e-9), 1),
+        "steady_ratio": round(mid_train / max(mid_wall, 1e-9), 4),
         "begin_pass_ms_mean": round(sum(r["begin_pass_ms"] for r in steady) / len(steady), 2),
         "end_pass_ms_mean": round(sum(r["end_pass_ms"] for r in steady) / len(steady), 2),
         "live_rows_mean": int(sum(r["live_rows"] for r in rows) / len(rows)),
@@ -135,6 +149,7 @@ def main():
         "writeback_hidden_passes": sum(1 for r in rows if r["writeback_done_in_pass"]),
         "tier_stats": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()},
         "ssd_direct_io": bool(box.ssd.direct_io) if box.ssd is not None else None,
+        "retain": bool(box.tier.retain) if box.tier is not None else None,
     }
     print(json.dumps(out), flush=True)
 

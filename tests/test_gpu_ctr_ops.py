@@ -68,10 +68,14 @@ def test_rank_attention_gpu_skewed_ranks():
     _close(wg.grad, wc.grad, rtol=1e-4, atol=2e-3)
 
 
+@pytest.mark.parametrize("dims", [(4, 150, 70, 90), (5, 1000, 64, 64), (3, 4133, 36, 20), (26, 8192, 64, 64)])
 @pytest.mark.parametrize("mode", ["default", "transpose", "batchcount"])
-def test_batch_fc_gpu(mode):
+def test_batch_fc_gpu(mode, dims):
+    """(70, 90) runs the generic strided k_mgemm; the <= 64 x 64 slots run
+    k_bfc_fwd / k_bfc_bwd (W_p in LDS, fused dx + dW + db with the ordered
+    partial reduce), ragged row tiles and padded columns included."""
     g = torch.Generator().manual_seed(5)
-    P, N, I, O = 4, 150, 70, 90
+    P, N, I, O = dims
     if mode == "default":
         shapes = [(P, N, I), (P, I, O), (P, O)]
         kw = {}
