@@ -2,6 +2,7 @@
 
 #include <dirent.h>
 #include <fcntl.h>
+#include <omp.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -763,24 +764,42 @@ void SsdLog::get(const uint64_t* h, int64_t n, uint8_t* found, float* out, int o
     int64_t i;
     int64_t slot;
   };
+  // index lookups in parallel (read-only probes; most requested keys of a
+  // staging are brand new and miss): per-thread want lists, concatenated in
+  // thread order
+  const int nt = n > 65536 ? std::max(1, std::min(16, omp_get_max_threads())) : 1;
+  std::vector<std::vector<Want>> parts(nt);
+#pragma omp parallel num_threads(nt)
+  {
+    std::vector<Want>& mine = parts[omp_get_thread_num()];
+#pragma omp for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+      float* o = out + i * out_stride;
+      const Loc* it = index_.find(h[i]);
+      if (it == nullptr) {
+        found[i] = 0;
+        std::memset(o, 0, (size_t)out_stride * 4);
+        continue;
+      }
+      const Loc l = *it;
+      found[i] = 1;
+      if (l.seg == active) {
+        const char* rec = active_buf_ + page_of(l.slot) * kPage + (l.slot % per_page_) * rec_bytes_;
+        std::memcpy(o, rec + 12, (size_t)w * 4);
+        if (out_stride > w) std::memset(o + w, 0, (size_t)(out_stride - w) * 4);
+      } else {
+        mine.push_back(Want{l.seg, page_of(l.slot), i, l.slot});
+      }
+    }
+  }
   std::vector<Want> want;
-  for (int64_t i = 0; i < n; ++i) {
-    float* o = out + i * out_stride;
-    const Loc* it = index_.find(h[i]);
-    if (it == nullptr) {
-      found[i] = 0;
-      std::memset(o, 0, (size_t)out_stride * 4);
-      continue;
-    }
-    const Loc l = *it;
-    found[i] = 1;
-    if (l.seg == active) {
-      const char* rec = active_buf_ + page_of(l.slot) * kPage + (l.slot % per_page_) * rec_bytes_;
-      std::memcpy(o, rec + 12, (size_t)w * 4);
-      if (out_stride > w) std::memset(o + w, 0, (size_t)(out_stride - w) * 4);
-    } else {
-      want.push_back(Want{l.seg, page_of(l.slot), i, l.slot});
-    }
+  if (nt == 1) {
+    want.swap(parts[0]);
+  } else {
+    size_t tot = 0;
+    for (auto& q : parts) tot += q.size();
+    want.reserve(tot);
+    for (auto& q : parts) want.insert(want.end(), q.begin(), q.end());
   }
   if (want.empty()) return;
   std::sort(want.begin(), want.end(), [](const Want& a, const Want& b) {

@@ -355,9 +355,9 @@ class BoxWrapper:
         """Host tier current: finish the background write-back and, inside a
         pass, write the live GPU rows back synchronously first."""
         if self.tier is not None:
+            self.tier.wait_writeback()  # also settles tier.retained
             if self.in_pass or self.tier.retained:
                 self.tier.flush()
-            self.tier.wait_writeback()
         elif self.mode == "tiered" and self.engine is not None and self.in_pass:
             h, v = self.engine.table.export(True)
             self.host.assign(h.cpu(), v.cpu())

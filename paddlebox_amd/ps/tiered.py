@@ -317,13 +317,15 @@ class TieredStore:
         staged GPU table in the background."""
         self.wait_stage()
         self._stage_err = None
-        self._stage_thread = threading.Thread(target=self._stage_run, args=(h.reshape(-1).cpu().contiguous(),),
-                                              daemon=True)
+        # the write-back in flight now is the one whose host rows this staging
+        # must see (a later one waits for THIS staging: joining it would deadlock)
+        self._stage_thread = threading.Thread(target=self._stage_run,
+                                              args=(h.reshape(-1).cpu().contiguous(), self._wb_thread), daemon=True)
         self._stage_thread.start()
         if block:
             self.wait_stage()
 
-    def _stage_run(self, hc: torch.Tensor):
+    def _stage_run(self, hc: torch.Tensor, wb_before: Optional[threading.Thread] = None):
         locked = False
         try:
             t0 = time.perf_counter()
@@ -340,7 +342,8 @@ class TieredStore:
                     outside = (self.live.probe(hd_all) < 0).cpu()
                 hc_all, hc = hc, hc[outside]
                 self.stats["retained_rows"] += int(hc_all.numel() - hc.numel())
-            self.wait_writeback()  # host values of earlier passes must be final
+            if wb_before is not None:
+                wb_before.join()  # host values of earlier passes must be final (its error: wait_writeback)
             self._tier_lock.acquire()
             locked = True
             rows = self.host.probe(hc)
@@ -429,40 +432,45 @@ class TieredStore:
         """Export the live table and move it into the host tier (then spill
         cold rows to SSD) in the background.  With ``retain`` and the next
         pass staged, rows the next pass uses again stay on the GPU (activation
-        carries them over) and only the others are written back; ``full``
-        (flush: a save / shrink needs the host tier current) writes every row."""
+        carries them over) and only the others are written back -- the
+        background thread waits for the staging to know which; ``full``
+        (flush: a save / shrink needs the host tier current) writes every row.
+        ``retained`` is final once ``wait_writeback`` returns."""
         self.wait_writeback()
         k, v = self.live.export(True)  # device copies: the live table may change after this
         self.retained = False
-        if self.retain and not full and self._stage_thread is not None:
-            self.wait_stage()  # the next pass's key set decides what stays
-        if self.retain and not full and self._staged_keys is not None and k.numel():
-            keep = self.stage_table.probe(k) < 0  # not in the next pass: evicted from the GPU
-            n_ret = int(k.numel()) - int(keep.sum())
-            if n_ret:
-                k, v = k[keep], v[keep]
-                self.retained = True
-                self.stats["wb_retained_rows"] += n_ret
+        filt = self.retain and not full and (self._stage_thread is not None or self._staged_keys is not None)
         ev = torch.cuda.Event()
-        main = torch.cuda.current_stream(self.live.device)
-        self.stream.wait_stream(main)  # the export kernel has to finish first
-        with torch.cuda.stream(self.stream):
-            kh = self._pinned("wb_keys", tuple(k.shape), k.dtype)
-            vh = self._pinned("wb_vals", tuple(v.shape), v.dtype)
-            kh.copy_(k, non_blocking=True)
-            vh.copy_(v, non_blocking=True)
-            ev.record(self.stream)
+        ev.record(torch.cuda.current_stream(self.live.device))  # the export kernel has to finish first
         self._wb_err = None
-        self._wb_thread = threading.Thread(target=self._wb_run, args=(ev, kh, vh, k, v), daemon=True)
+        self._wb_thread = threading.Thread(target=self._wb_run, args=(ev, k, v, filt), daemon=True)
         self._wb_thread.start()
         if block:
             self.wait_writeback()
 
-    def _wb_run(self, ev, kh, vh, k_dev, v_dev):
+    def _wb_run(self, ev, k, v, filt):
         try:
             t0 = time.perf_counter()
-            ev.synchronize()
-            del k_dev, v_dev
+            dev = self.live.device
+            with torch.cuda.device(dev), torch.cuda.stream(self.stream):
+                self.stream.wait_event(ev)
+                if filt:
+                    st = self._stage_thread
+                    if st is not None:
+                        st.join()  # its error surfaces at the next wait_stage
+                    if self._staged_keys is not None and k.numel():
+                        keep = self.stage_table.probe(k) < 0  # not in the next pass: evicted from the GPU
+                        n_ret = int(k.numel()) - int(keep.sum())
+                        if n_ret:
+                            k, v = k[keep], v[keep]
+                            self.retained = True
+                            self.stats["wb_retained_rows"] += n_ret
+                kh = self._pinned("wb_keys", tuple(k.shape), k.dtype)
+                vh = self._pinned("wb_vals", tuple(v.shape), v.dtype)
+                kh.copy_(k, non_blocking=True)
+                vh.copy_(v, non_blocking=True)
+                self.stream.synchronize()
+            del k, v
             with self._tier_lock:
                 self._wb_locked(kh, vh)
             self.stats["writeback_s"] += time.perf_counter() - t0
