@@ -563,6 +563,20 @@ struct DedupWorkspace {
 };
 
 // --------------------------------------------------------------- free ops
+// process-wide sticky guard word of the kernels without a table of their own
+// (seqpool): kSeqpoolGuard* bits, read by SparseEngine.check_guards
+static Tensor& guard_tensor(const c10::Device& dev) {
+  static Tensor* t = new Tensor();  // never destroyed: no device free after the runtime's teardown
+  if (!t->defined() || t->device() != dev) *t = torch::zeros({1}, torch::dtype(torch::kInt32).device(dev));
+  return *t;
+}
+static int32_t* guard_word(const c10::Device& dev) { return ptr<int32_t>(guard_tensor(dev)); }
+static int64_t guard_bits_get(const std::string& device) {
+  Tensor& t = guard_tensor(c10::Device(device));
+  return (int64_t)t.item<int32_t>();
+}
+static void guard_bits_clear(const std::string& device) { guard_tensor(c10::Device(device)).zero_(); }
+
 static void fill_occurrence(const Tensor& lod, int S, int B, Tensor occ_slot, Tensor occ_ins) {
   check_cuda(lod, "lod");
   PBX_CHECK(lod.numel() == (int64_t)S * (B + 1), "lod shape");
@@ -639,6 +653,7 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
               "dense must be f32 [B, Dd]");
     PBX_CHECK(S > 0 && dense_col >= 0 && dense_col + dense->size(1) <= out.size(1), "dense columns out of range");
     PBX_CHECK(dense->stride(1) == 1 || dense->size(1) == 1, "dense: rows must be unit-stride");
+    PBX_CHECK(dense->stride(0) >= dense->size(1) || dense->size(0) == 1, "dense: overlapping rows (expanded view)");
     a.dense = ptr<float>(*dense);
     a.dense_dim = (int)dense->size(1);
     a.dense_col = dense_col;
@@ -658,6 +673,19 @@ static void seqpool_cvm_fwd(const Tensor& src, const c10::optional<Tensor>& src_
     a.probe_keys = reinterpret_cast<const uint64_t*>(probe_keys->data_ptr<int64_t>());
     a.probe_t = probe_table->view();
     a.rows_out = ptr<int64_t>(*rows_out);
+  }
+  // index guards: the buffers the lod's occurrence indices, the unique ids
+  // and the record indices may address (a violation is skipped and flagged)
+  {
+    int64_t n_occ = INT64_MAX;
+    if (a.uid) n_occ = std::min<int64_t>(n_occ, uid->numel());
+    if (a.occ_slot) n_occ = std::min<int64_t>(n_occ, std::min(occ_slot->numel(), occ_ins->numel()));
+    if (a.probe_keys) n_occ = std::min<int64_t>(n_occ, probe_keys->numel());
+    if (a.src_index && !a.uid && !a.probe_keys) n_occ = std::min<int64_t>(n_occ, src_index->numel());
+    a.n_occ = n_occ == INT64_MAX ? 0 : std::max<int64_t>(n_occ, 1);
+    a.n_index = (a.src_index && a.uid) ? std::max<int64_t>(src_index->numel(), 1) : 0;
+    a.src_rows = std::max<int64_t>(src.size(0), 1);
+    a.err = guard_word(src.device());
   }
   launch_seqpool_cvm_fwd(a, cur_stream());
 }
@@ -1361,6 +1389,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("M", &MlpWorkspace::M);
   m.attr("kSaveMaxCols") = kSaveMaxCols;
   m.def("fill_occurrence", &fill_occurrence);
+  m.def("guard_bits", &guard_bits_get);
+  m.def("clear_guard_bits", &guard_bits_clear);
   m.def("seqpool_cvm_fwd", &seqpool_cvm_fwd, py::arg("src"), py::arg("src_index"), py::arg("uid"), py::arg("lod"),
         py::arg("S"), py::arg("B"), py::arg("E"), py::arg("out"), py::arg("col_offset"), py::arg("use_cvm"),
         py::arg("cvm_offset"), py::arg("clk_filter"), py::arg("pad_value"), py::arg("need_filter"),

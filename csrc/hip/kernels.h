@@ -175,7 +175,15 @@ struct SeqpoolCvmArgs {
   int32_t* sc_perm = nullptr;
   int32_t* sc_acc = nullptr;
   int32_t* sc_u_count = nullptr;
+  // index guards (0: unchecked): occurrence k < n_occ, unique id < n_index
+  // (src_index length), record < src_rows; a violating occurrence is skipped
+  // and sets a kSeqpoolGuard* bit of *err (sticky; read by check_guards)
+  int64_t n_occ = 0, n_index = 0, src_rows = 0;
+  int32_t* err = nullptr;
 };
+constexpr int32_t kSeqpoolGuardOcc = 16;  // lod walks past the occurrence buffers
+constexpr int32_t kSeqpoolGuardUid = 32;  // unique id past src_index
+constexpr int32_t kSeqpoolGuardRow = 64;  // record past src
 int seqpool_cvm_out_width(const SeqpoolCvmArgs& a);
 void launch_seqpool_cvm_fwd(const SeqpoolCvmArgs& a, hipStream_t s);
 

@@ -109,7 +109,25 @@ __device__ __forceinline__ int64_t seqpool_record(const SeqpoolCvmArgs& a, int64
   }
   const int32_t u = a.uid ? a.uid[k] : (int32_t)k;
   if (u < 0) return -1;
-  return a.src_index ? a.src_index[u] : (int64_t)u;
+  if (a.n_index && a.src_index && u >= a.n_index) {
+    if (a.err) atomicOr(a.err, kSeqpoolGuardUid);
+    return -1;
+  }
+  const int64_t r = a.src_index ? a.src_index[u] : (int64_t)u;
+  if (a.src_rows && r >= a.src_rows) {
+    if (a.err) atomicOr(a.err, kSeqpoolGuardRow);
+    return -1;
+  }
+  return r;
+}
+
+// occurrence k inside the buffers the lod may index
+__device__ __forceinline__ bool seqpool_occ_ok(const SeqpoolCvmArgs& a, int64_t k) {
+  if (a.n_occ && (k < 0 || k >= a.n_occ)) {
+    if (a.err) atomicOr(a.err, kSeqpoolGuardOcc);
+    return false;
+  }
+  return true;
 }
 
 template <int E>
@@ -132,6 +150,7 @@ __global__ __launch_bounds__(256) void k_seqpool_cvm(SeqpoolCvmArgs a) {
 #pragma unroll
   for (int c = 0; c < E; ++c) acc[c] = a.pad_value;
   for (int64_t k = st; k < en; ++k) {
+    if (!seqpool_occ_ok(a, k)) continue;
     if (a.occ_slot) {
       a.occ_slot[k] = s;
       a.occ_ins[k] = b;
@@ -216,6 +235,7 @@ __global__ void k_seqpool_cvm_generic(SeqpoolCvmArgs a) {
   float* o = a.out + (int64_t)b * a.out_stride + a.col_offset + (int64_t)s * Eo;
   if (a.occ_slot) {
     for (int64_t k = st; k < en; ++k) {
+      if (!seqpool_occ_ok(a, k)) continue;
       a.occ_slot[k] = s;
       a.occ_ins[k] = b;
     }
@@ -224,9 +244,8 @@ __global__ void k_seqpool_cvm_generic(SeqpoolCvmArgs a) {
   for (int c = 0; c < E; ++c) {
     float acc = a.pad_value;
     for (int64_t k = st; k < en; ++k) {
-      const int32_t u = a.uid ? a.uid[k] : (int32_t)k;
-      if (u < 0) continue;
-      const int64_t ri = a.src_index ? a.src_index[u] : (int64_t)u;
+      if (!seqpool_occ_ok(a, k)) continue;
+      const int64_t ri = seqpool_record(a, k);
       if (ri < 0) continue;
       const float* v = a.src + ri * (int64_t)a.src_stride;
       if ((a.need_filter || a.embed_threshold_filter) &&

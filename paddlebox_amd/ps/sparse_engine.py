@@ -139,9 +139,10 @@ def _dense_rows(dense: torch.Tensor) -> torch.Tensor:
     a unit-stride column slice of the batch's dense block (the launch takes
     the row stride), copied otherwise."""
     dense = dense.float()
-    if dense.dim() == 2 and (dense.stride(1) == 1 or dense.shape[1] == 1):
+    if (dense.dim() == 2 and (dense.stride(1) == 1 or dense.shape[1] == 1)
+            and (dense.stride(0) >= dense.shape[1] or dense.shape[0] == 1)):
         return dense
-    return dense.contiguous()
+    return dense.contiguous()  # an expanded (row stride 0) or column-strided view: copied
 
 
 def _push_run_scratch(max_keys: int, device) -> torch.Tensor:
@@ -255,6 +256,9 @@ class SparseEngine:
         if self.is_gpu:
             self.table = GpuSparseTable(self.dim, shard_cap, self.device, codec=self.codec)
             self._hip = _native.hip()
+            self._guard_dev = str(torch.device("cuda", self.device.index if self.device.index is not None
+                                               else torch.cuda.current_device()))
+            self._hip.clear_guard_bits(self._guard_dev)  # allocates the seqpool guard word outside any capture
             self._sgd_native = cfg.sgd.to_native(self._hip)
             if self.sharded:
                 # per-peer exchange slots: exact when the pass's batches were
@@ -998,7 +1002,9 @@ class SparseEngine:
         return self.slot_ids
 
     GUARD_BITS = {1: "push: table row outside the table", 2: "dedup: row without a unique id of its batch",
-                  4: "dedup: perm slot outside the batch", 8: "push: occurrence / unique id outside the batch"}
+                  4: "dedup: perm slot outside the batch", 8: "push: occurrence / unique id outside the batch",
+                  16: "seqpool: lod occurrence outside the occurrence buffers",
+                  32: "seqpool: unique id outside the record index", 64: "seqpool: record outside the pulled source"}
 
     def check_guards(self):
         """Raise if a kernel met an out-of-range index (skipped, not followed:
@@ -1006,8 +1012,11 @@ class SparseEngine:
         if not self.is_gpu:
             return
         bits = int(self.table.t.error_bits())
+        dev = self._guard_dev
+        bits |= int(self._hip.guard_bits(dev))  # the seqpool's (process-wide word)
         if bits:
             self.table.t.clear_error()
+            self._hip.clear_guard_bits(dev)
             what = "; ".join(v for b, v in self.GUARD_BITS.items() if bits & b)
             raise RuntimeError(f"sparse engine index guard tripped (bits {bits:#x}): {what}")
 

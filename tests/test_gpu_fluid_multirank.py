@@ -183,6 +183,12 @@ def test_fluid_two_ranks_match_union_oracle(tmp_path, monkeypatch, transpile):
     h = _native.hip()
     orig = h.data_norm_update
     monkeypatch.setattr(h, "data_norm_update", lambda bs, bsum, bsq, st, dec: orig(bs, bsum, bsq, st * W, dec))
+    # ... which the oracle must call: keep its summary update out of the
+    # fused Adam launch (where the statistics are not scaled)
+    from paddlebox_amd.parallel.dense import FlatAdam
+
+    fuse = FlatAdam.fuse
+    monkeypatch.setattr(FlatAdam, "fuse", lambda self, mlps=(), data_norms=(), **kw: fuse(self, mlps=mlps, **kw))
     _, union = _write_files(d, W)
     o_dense, o_h, o_v, _ = _train(fluid, [union], W * B, 0, 1, False)
     o_h, o_v = torch.from_numpy(o_h), torch.from_numpy(o_v)

@@ -144,7 +144,18 @@ def _oracle(W, B, steps):
                        slot_ids=[float(s + 1) for s in range(S)])
     eng.insert_local_mixed(_union_keys(union).to(dev), init_embedx=True)
     torch.manual_seed(0)
-    step = CtrTrainStep(eng, "deepfm", "fp32", num_slots=S, hidden=HIDDEN, multi=False)
+    # the plain eager step: the loop below runs Adam itself, after scaling the
+    # statistics (no optimizer inside the backward)
+    prev = os.environ.get("PBX_ADAM_OVERLAP")
+    os.environ["PBX_ADAM_OVERLAP"] = "0"
+    try:
+        step = CtrTrainStep(eng, "deepfm", "fp32", num_slots=S, hidden=HIDDEN, multi=False)
+    finally:
+        if prev is None:
+            os.environ.pop("PBX_ADAM_OVERLAP", None)
+        else:
+            os.environ["PBX_ADAM_OVERLAP"] = prev
+    assert not step.adam_overlap
     model = step.model
     losses = []
     for u in union:
