@@ -135,6 +135,12 @@ PBX_HD float hash_uniform(uint64_t a, uint64_t b) {
   return (float)(z >> 40) * (1.0f / 16777216.0f);
 }
 
+// Salt of a row's lazily created embedx (hash_uniform(salt, d) * mf_initial_range):
+// a function of the row's mixed key only -- not of the push counter -- so the
+// same feature gets the same initial vector in eager steps, captured-graph
+// replays (which would repeat a captured counter) and under any sharding.
+PBX_HD uint64_t mf_create_salt(uint64_t rkey) { return 0x6D665F637265ULL ^ rkey * 0x9E3779B97F4A7C15ULL; }
+
 constexpr uint64_t kEmptyKey = 0xFFFFFFFFFFFFFFFFULL;  // sentinel in tables / padding
 constexpr int kBucketSlots = 16;                       // 16 x 8 B = one 128-B line
 

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void k_codec_update(TableDev t, CodecDev c, co
     if (create) {
       if (cfg.nonclk_coeff * (show - click) + cfg.clk_coeff * click >= cfg.mf_create_thresholds) {
         v[c.mf] = 1.f;
-        const uint64_t salt = seed ^ table_row_key(t, r) * 0x9E3779B97F4A7C15ULL;
+        const uint64_t salt = mf_create_salt(table_row_key(t, r));
         for (int j = 0; j < DX; ++j) store_col(c, v, j, hash_uniform(salt, j) * cfg.mf_initial_range);
         xp[0] = c.beta1;
         xp[1] = c.beta2;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void k_codec_update(TableDev t, CodecDev c, co
   if (create) {
     if (cfg.nonclk_coeff * (show - click) + cfg.clk_coeff * click >= cfg.mf_create_thresholds) {
       v[c.mf] = 1.f;
-      const uint64_t salt = seed ^ table_row_key(t, r) * 0x9E3779B97F4A7C15ULL;
+      const uint64_t salt = mf_create_salt(table_row_key(t, r));
       const int nc = c.kind == 3 ? (expand_slot(c, slot) ? c.De : c.D) : DX;
       if (c.kind == 3) v[c.xsz] = (float)nc;
       for (int j = 0; j < nc; ++j) store_col(c, v, j, hash_uniform(salt, j) * cfg.mf_initial_range);
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void k_codec_update(TableDev t, CodecDev c, co
     // columns (fresh draws, fresh g2sum), as a push-created row would be
     const int want = expand_slot(c, slot) ? c.De : c.D;
     if (xs != want) {
-      const uint64_t salt = seed ^ table_row_key(t, r) * 0x9E3779B97F4A7C15ULL;
+      const uint64_t salt = mf_create_salt(table_row_key(t, r));
       for (int j = 0; j < want; ++j) store_col(c, v, j, hash_uniform(salt, j) * cfg.mf_initial_range);
       for (int j = want; j < c.Wx; ++j) store_col(c, v, j, 0.f);
       v[c.xsz] = (float)want;

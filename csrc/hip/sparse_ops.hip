@@ -426,7 +426,7 @@ __global__ __launch_bounds__(256) void k_push_adagrad(TableDev t, const int64_t*
   if (v[l.mf_size] == 0.f) {
     if (cfg.nonclk_coeff * (show - click) + cfg.clk_coeff * click >= cfg.mf_create_thresholds) {
       v[l.mf_size] = 1.f;
-      const uint64_t salt = seed ^ table_row_key(t, r) * 0x9E3779B97F4A7C15ULL;
+      const uint64_t salt = mf_create_salt(table_row_key(t, r));
       for (int d = 0; d < t.dim; ++d) v[kEmbedx + d] = hash_uniform(salt, d) * cfg.mf_initial_range;
     }
   } else {
@@ -489,7 +489,7 @@ __device__ __forceinline__ void adagrad_row(float* __restrict__ row, const float
   if (v[L::kMf] == 0.f) {
     if (cfg.nonclk_coeff * (show - click) + cfg.clk_coeff * click >= cfg.mf_create_thresholds) {
       v[L::kMf] = 1.f;
-      const uint64_t salt = seed ^ rkey * 0x9E3779B97F4A7C15ULL;
+      const uint64_t salt = mf_create_salt(rkey);
 #pragma unroll
       for (int d = 0; d < D; ++d) v[kEmbedx + d] = hash_uniform(salt, d) * cfg.mf_initial_range;
     }

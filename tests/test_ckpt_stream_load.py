@@ -72,7 +72,9 @@ def _worker(rank, port, root, q):
             box.initialize_gpu_and_load_model(slot_vector=[1], max_keys=1000)
             n = box.load_model(os.path.join(root, name))
             h, v = box.engine.table.export(True)
-            out[name] = (n, h, v)
+            # numpy, not torch: a torch tensor crosses the queue as a shared fd
+            # served by this process (gone once it exits)
+            out[name] = (n, h.numpy(), v.numpy())
         q.put((rank, out))
     finally:
         dist.barrier()
@@ -91,6 +93,7 @@ def test_streamed_per_rank_load_routes_rows_to_owners(tmp_path):
     for p in ps:
         p.start()
     res = dict(q.get(timeout=180) for _ in ps)
+    res = {r: {k: (n, torch.from_numpy(a), torch.from_numpy(b)) for k, (n, a, b) in o.items()} for r, o in res.items()}
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -77,11 +77,12 @@ def test_train_from_dataset_gpu_eager_and_graph(tmp_path):
         assert gst["batches"] == 10 and gst.get("graph_replays", 0) > 0
         assert bool(gst.get("device_pass", False)) == dpass
         # same data, same order, same init: the captured step trains the same
-        # model (up to float atomics in the sparse push / column reductions,
-        # which Adam's normalised steps amplify on near-zero gradients)
-        np.testing.assert_allclose(graphed["w1"], eager["w1"], rtol=0, atol=5e-3)
+        # model (lazily created embedx rows draw from their key, not from the
+        # push counter a capture would freeze -- that made graph replays and
+        # eager steps diverge by ~1e-4 before round 5)
+        np.testing.assert_allclose(graphed["w1"], eager["w1"], rtol=0, atol=1e-4)
         keep = [c for c in range(eager["table"].shape[1]) if c != 14]  # "slot" field: last occurrence, racy
-        torch.testing.assert_close(graphed["table"][:, keep], eager["table"][:, keep], rtol=1e-2, atol=5e-3)
+        torch.testing.assert_close(graphed["table"][:, keep], eager["table"][:, keep], rtol=1e-4, atol=1e-5)
         assert abs(graphed["auc"] - eager["auc"]) < 0.01
 
 
@@ -97,13 +98,12 @@ def test_graphed_loop_is_bench_step(tmp_path):
     assert plain["stats"][-1]["steps_per_graph"] == 1 and not plain["stats"][-1]["pipelined_front"]
     assert fast["n"] == plain["n"] == 3 * 640  # every batch's AUC counted (inside the graphs)
     assert abs(fast["auc"] - plain["auc"]) < 1e-6
-    # up to the float atomics of the dW split / sparse push, which Adam's
-    # normalised steps amplify on near-zero gradients (as eager vs graphed)
-    np.testing.assert_allclose(fast["w1"], plain["w1"], rtol=0, atol=5e-3)
+    # up to the float atomics of the dW split / sparse push
+    np.testing.assert_allclose(fast["w1"], plain["w1"], rtol=0, atol=1e-4)
     keep = [c for c in range(plain["table"].shape[1]) if c != 14]  # "slot" field: last occurrence, racy
-    torch.testing.assert_close(fast["table"][:, keep], plain["table"][:, keep], rtol=1e-2, atol=5e-3)
+    torch.testing.assert_close(fast["table"][:, keep], plain["table"][:, keep], rtol=1e-4, atol=1e-5)
     for k in fast["dn"]:
-        np.testing.assert_allclose(fast["dn"][k], plain["dn"][k], rtol=1e-2, atol=2e-3)
+        np.testing.assert_allclose(fast["dn"][k], plain["dn"][k], rtol=1e-4, atol=1e-4)
 
 
 def test_fc_precision_fp32_matches_cpu_oracle(tmp_path):
@@ -234,7 +234,7 @@ def test_transpiled_program_captured_on_gpu(tmp_path):
     plain = _run(tmp_path / "p", graph=True, passes=1)
     tr = _run(tmp_path / "t", graph=True, passes=1, transpile=True)
     assert tr["stats"][-1].get("graph_replays", 0) > 0
-    np.testing.assert_allclose(tr["w1"], plain["w1"], rtol=0, atol=5e-3)
+    np.testing.assert_allclose(tr["w1"], plain["w1"], rtol=0, atol=1e-4)
 
 
 def test_checkpoint_resume_on_gpu(tmp_path):
@@ -249,4 +249,4 @@ def test_checkpoint_resume_on_gpu(tmp_path):
     res_dense, res_h, _ = _resume_run(tmp_path, files, 0, 1, restore=ck, device="cuda:0")
     assert torch.equal(res_h, ref_h)
     for n in ref_dense:
-        np.testing.assert_allclose(res_dense[n], ref_dense[n], rtol=0, atol=5e-3, err_msg=n)
+        np.testing.assert_allclose(res_dense[n], ref_dense[n], rtol=0, atol=1e-4, err_msg=n)
