@@ -128,6 +128,20 @@ def _make_opt(spec: dict, arena: DenseArena, lr_mult: float = 1.0):
     return FlatSGD(arena, lr)
 
 
+def _side_adam_hook(sess, opt, tower):
+    """The tower's dense-grads hook for Session._side_adam, holding the
+    session and tower weakly (no tower <-> hook reference cycle)."""
+    import weakref
+
+    sr, tr = weakref.ref(sess), weakref.ref(tower)
+
+    def hook():
+        s, t = sr(), tr()
+        if s is not None and t is not None:
+            s._side_adam(opt, t)
+    return hook
+
+
 class Session:
     def __init__(self, program: Program, scope: Scope, device: torch.device, fetch_names=(), group=None,
                  sync_mode: Optional[str] = None, sync_k: int = 1, fuse: bool = True):
@@ -159,6 +173,7 @@ class Session:
         # pipelined front (graphed train loop): (batch, pull slot) pooled right
         # after this step's sparse push, so the next step starts at the dense head
         self._next = None
+        self._side_stepped = set()  # optimizers the tower hook already stepped this step
 
     def close(self):
         """Release the session's IPC mesh (each session's mesh stayed
@@ -209,8 +224,15 @@ class Session:
                 for a, o in zip(self.arenas, self.opts):
                     fs = a.flat.untyped_storage().data_ptr()
                     if isinstance(o, FlatAdam) and all(w.untyped_storage().data_ptr() == fs for w in t.mlp.w):
+                        side = self._adam_overlap_ok(a, o, t)
+                        # overlapped: the data_norm update stays in the tower's
+                        # dense tail, ahead of the side-stream Adam
                         o.fuse(mlps=list(o._fuse_mlps) + [t.mlp],
-                               data_norms=list(o._fuse_dns) + ([t.dn] if t.dn is not None else []))
+                               data_norms=list(o._fuse_dns) + ([t.dn] if t.dn is not None and not side else []))
+                        if side:
+                            if t.dn is not None:
+                                t.dn.fused_update = False
+                            t.on_dense_grads = _side_adam_hook(self, o, t)
                         # the packed copy predates the last (unfused) update:
                         # the next forward packs, later updates re-pack
                         t.mlp.invalidate_pack()
@@ -230,6 +252,33 @@ class Session:
                         t.auc_metric, t.auc_metric_obj = name, m
                         m.fused_tower = t
                         break
+
+    def _adam_overlap_ok(self, arena, opt, tower) -> bool:
+        """The overlapped optimizer of bench.py's step (CtrTrainStep
+        adam_overlap, PBX_ADAM_OVERLAP): one rank, a plain (untranspiled)
+        program, and an arena holding only this tower's parameters."""
+        if os.environ.get("PBX_ADAM_OVERLAP", "1") != "1":
+            return False
+        if self.group is not None or getattr(self, "async_dense", None) or not tower.fp32:
+            return False
+        lw = self.lowered
+        if lw.backward_ops or lw.optimize_ops:
+            return False
+        tp = {p.data_ptr() for p in tower._params}
+        return all(p.data_ptr() in tp for p in arena.params)
+
+    def _side_adam(self, opt, tower):
+        """Tower dense-grads hook (on the dW side stream, after the data_norm
+        summary update): mark where the next step's head may start, then the
+        fused Adam -- the next forward joins it before the tower reads the
+        weights (parallel.dense pre-head events)."""
+        from ..parallel.dense import set_pre_head_event
+
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        set_pre_head_event(tower.uid, ev)
+        opt.step(1.0, join=False)
+        self._side_stepped.add(id(opt))
 
     def repack_towers(self):
         """Eager re-pack of every fused tower workspace (start of a graphed
@@ -503,12 +552,19 @@ class Session:
             prof.end("backward (all grad ops + sparse push)", t0)
             t0 = prof.begin()
         lw = self.lowered
+        side = self._side_stepped
         if lw.backward_ops or lw.optimize_ops:
             self._transpiled_sync(ctx)
         else:
             for s, o in zip(self.syncs, self.opts):
-                s.apply(o)
-        join_grad_producers()  # an update issued behind the dW side stream
+                if id(o) in side:  # already issued on the dW side stream by the tower's hook
+                    s.after_step(o)
+                else:
+                    s.apply(o)
+        if side:
+            side.clear()  # the next forward joins the side-stream update
+        else:
+            join_grad_producers()  # an update issued behind the dW side stream
         if prof is not None:
             prof.end("dense sync + optimizer", t0)
 

@@ -757,7 +757,15 @@ def _tower_for(ctx, op, C: int):
     # Session.fuse_towers binds an AUC metric by these names
     t.io = (op.outputs["Pred"][0].name, {op.inputs["Label"][0].name, a.get("label_alias") or ""} - {""})
     if ctx.training and hasattr(ctx.s, "on_tower_grads"):
-        t.on_dense_grads = lambda: ctx.s.on_tower_grads(t)
+        import weakref
+
+        sr, tr = weakref.ref(ctx.s), weakref.ref(t)  # no tower <-> hook reference cycle
+
+        def hook():
+            s_, t_ = sr(), tr()
+            if s_ is not None and t_ is not None:
+                s_.on_tower_grads(t_)
+        t.on_dense_grads = hook
     ctx.cache[key] = t
     return t
 

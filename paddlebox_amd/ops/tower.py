@@ -52,7 +52,7 @@ class _CtrTowerFn(torch.autograd.Function):
     def forward(ctx, x, extra, label, t: "CtrTower", *params):
         h = _native.hip()
         mlp, dn = t.mlp, t.dn
-        pre_head = pop_pre_head_event(id(t)) if x.is_cuda else None
+        pre_head = pop_pre_head_event(t.uid) if x.is_cuda else None
         if pre_head is not None:
             # overlapped optimizer: the previous step's dW (which reads this
             # head's output buffers) and data_norm update are done; its Adam
@@ -221,6 +221,8 @@ class CtrTower:
     S slot blocks of width Eo (embed_w at ew_col, D embedx after it) followed by
     dense columns make up the input x [B, C]."""
 
+    _n = 0  # towers created (CtrTower.uid)
+
     def __init__(self, mlp, dn, S: int, Eo: int, ew_col: int, D: int, use_head_lin: bool = True, cross=None,
                  fp32: bool = False):
         """``cross``: optional (CrossNetV2, w_c) whose width is the tower's
@@ -236,6 +238,11 @@ class CtrTower:
         self._yt = None
         self.S, self.Eo, self.ew_col, self.D = S, Eo, ew_col, D
         self.use_head_lin = use_head_lin
+        # key of the overlapped optimizer's pre-head event (parallel.dense):
+        # unique per tower for the process, unlike id(), which a later
+        # tower can reuse while an event of the old one is still registered
+        CtrTower._n += 1
+        self.uid = CtrTower._n
         self.auc = None  # (table [2, T] f64, stats [5] f64, mask or None): fused AUC accumulation
         # called in the backward once every dense gradient (and data_norm
         # statistic) of the tower is final, before the sparse push runs

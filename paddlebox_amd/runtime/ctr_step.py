@@ -173,7 +173,7 @@ class CtrTrainStep:
 
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
-        set_pre_head_event(id(self.model.tower), ev)
+        set_pre_head_event(self.model.tower.uid, ev)
         self.opt.step(1.0, join=False)
 
     def set_next(self, batch, slot: int = 0):

@@ -156,9 +156,46 @@ class GraphedTrainStep:
             pipeline[0](self.bufs[0], 0)  # graph 0's pull finds buffer 0 pooled
         nK = n_buffers * self.K  # batch buffers (= pull slots of the pipeline)
         self.graphs = []
+        _drain_collective_watchdog()
+        # no cyclic garbage collection inside a capture: an unreachable object
+        # cycle of an earlier session (tower <-> its hooks) can hold graph
+        # execs, events and tensors whose destructors must not run while this
+        # thread captures (seen as an abort in a capture right after another
+        # session's pass)
+        import gc
+
+        gc.collect()
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            self._capture_all(n_buffers, nK, prefetch, pipeline, join_each_step, step_fn)
+        finally:
+            if gc_was:
+                gc.enable()
+        if prefetch is not None:
+            prefetch[0].clear_prefetch()
+        if pipeline is not None:
+            pipeline[1](None, 0)
+            if len(pipeline) > 2:
+                pipeline[2]()  # the host-side prepared entries only steer captures
+        torch.cuda.synchronize(self.device)
+        self.copy_stream = side_stream(self.device, "graph_copy")
+        self.ready = [torch.cuda.Event() for _ in range(n_buffers)]
+        self.free = [torch.cuda.Event() for _ in range(n_buffers)]
+        for e in self.free:
+            e.record(cur)
+        # Host throttle: replay i waits (on the host) for replay i - max_inflight
+        # to finish.  Unthrottled, the host runs tens of steps ahead and the
+        # runtime periodically blocks it for 6-12 ms to recycle its launch
+        # resources (profiles/r2_h2d_stall.txt) -- far longer than the queued
+        # GPU work -- so a bounded queue is both steadier and faster.
+        self.max_inflight = max(1, int(max_inflight))
+        self.done = [torch.cuda.Event() for _ in range(self.max_inflight)]
+        self.step_no = 0
+
+    def _capture_all(self, n_buffers, nK, prefetch, pipeline, join_each_step, step_fn):
         pool = None
         n = n_buffers
-        _drain_collective_watchdog()
         for j in range(n_buffers):
             g = torch.cuda.CUDAGraph()
             # thread_local: RCCL's watchdog thread keeps querying the events of
@@ -187,26 +224,6 @@ class GraphedTrainStep:
                     torch.cuda.current_stream(self.device).wait_stream(self._side)
             pool = g.pool()
             self.graphs.append((g, out))
-        if prefetch is not None:
-            prefetch[0].clear_prefetch()
-        if pipeline is not None:
-            pipeline[1](None, 0)
-            if len(pipeline) > 2:
-                pipeline[2]()  # the host-side prepared entries only steer captures
-        torch.cuda.synchronize(self.device)
-        self.copy_stream = side_stream(self.device, "graph_copy")
-        self.ready = [torch.cuda.Event() for _ in range(n_buffers)]
-        self.free = [torch.cuda.Event() for _ in range(n_buffers)]
-        for e in self.free:
-            e.record(cur)
-        # Host throttle: replay i waits (on the host) for replay i - max_inflight
-        # to finish.  Unthrottled, the host runs tens of steps ahead and the
-        # runtime periodically blocks it for 6-12 ms to recycle its launch
-        # resources (profiles/r2_h2d_stall.txt) -- far longer than the queued
-        # GPU work -- so a bounded queue is both steadier and faster.
-        self.max_inflight = max(1, int(max_inflight))
-        self.done = [torch.cuda.Event() for _ in range(self.max_inflight)]
-        self.step_no = 0
 
     @property
     def n(self) -> int:

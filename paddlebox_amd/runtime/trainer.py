@@ -27,6 +27,8 @@ from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
 import torch
+
+from ..parallel.dense import join_grad_producers
 import torch.distributed as dist
 
 from .. import _native
@@ -374,6 +376,7 @@ class BoxPSWorker:
                 s.feed_batch(ctx, bt)
                 s.step(ctx)
                 metrics((ctx, bt))
+        join_grad_producers()
         torch.cuda.synchronize(dev)
         el = time.time() - t0
         return {"batches": self.batches, "instances": n_ins, "seconds": el,
@@ -546,6 +549,7 @@ class BoxPSWorker:
         for c, dbs in warm.items():
             for db in dbs:
                 eager(db, c)
+        join_grad_producers()  # the last step's side-stream update (overlapped Adam) and its pre-head event
         torch.cuda.synchronize(dev)
         if dp.overflowed():
             raise RuntimeError("device batch assembly: a batch had more keys than the captured key buffer")
@@ -622,6 +626,7 @@ class BoxPSWorker:
                 self._print_fetch(ctx)
             last = time.time()
         if dev.type == "cuda":
+            join_grad_producers()
             torch.cuda.synchronize(dev)
         el = time.time() - t0
         return {"batches": self.batches, "instances": n_ins, "seconds": el,
