@@ -370,7 +370,7 @@ def main():
                 graphed = GraphedTrainStep(train_step, host_batches[0], device, prefetch=pre,
                                            steps_per_graph=K if pre is None else 1,
                                            n_buffers=3 if pipe is not None else 2, pipeline=pipe,
-                                           join_each_step=not step.adam_overlap)
+                                           join_each_step=not (step.adam_overlap or step.adam_overlap_multi))
                 if args.inputs == "hbm":
                     graphed.stage_inputs(host_batches)
                 graphed.warm(host_batches, replays=args.graph_warm)

@@ -174,6 +174,7 @@ class Session:
         # after this step's sparse push, so the next step starts at the dense head
         self._next = None
         self._side_stepped = set()  # optimizers the tower hook already stepped this step
+        self.side_adam = False  # a tower's update runs on its dW side stream (no join at the step end)
 
     def close(self):
         """Release the session's IPC mesh (each session's mesh stayed
@@ -233,6 +234,7 @@ class Session:
                             if t.dn is not None:
                                 t.dn.fused_update = False
                             t.on_dense_grads = _side_adam_hook(self, o, t)
+                            self.side_adam = True
                         # the packed copy predates the last (unfused) update:
                         # the next forward packs, later updates re-pack
                         t.mlp.invalidate_pack()

@@ -123,6 +123,7 @@ class CtrTrainStep:
         # tower's dense-grads hook on the dW side stream (measured no faster)
         self.adam_side = ((not multi) and os.environ.get("PBX_ADAM_ON_SIDE", "0") == "1" and tower is not None
                           and not self.adam_overlap)
+        self.adam_overlap_multi = False
         if self.adam_overlap:
             tower.on_dense_grads = self._side_update
         elif self.adam_side:
@@ -130,6 +131,17 @@ class CtrTrainStep:
         elif tower is not None and (self.ipc is not None or not multi):
             # start the IPC all-reduce as soon as the tower's gradients are final
             tower.on_dense_grads = self.sync.launch
+            # PBX_ADAM_OVERLAP_MULTI (default on; multi-rank, IPC dense mesh,
+            # fused DeepFM tower): the Adam launch (with the data_norm update
+            # fused in) follows the all-reduce on its own stream, so it runs
+            # beside the sparse exchange chain instead of after it; the next
+            # step's forward waits for it (pre-head event + grad-producer
+            # join).  1-rank rehearsal 0.4227 / 0.4237 -> 0.4169 / 0.4192
+            # ms/step (profiles/r5_adam_overlap_multi_ab.txt)
+            if (multi and self.ipc is not None and self.fused and not dcn
+                    and os.environ.get("PBX_ADAM_OVERLAP_MULTI", "1") == "1"):
+                self.adam_overlap_multi = True
+                tower.on_dense_grads = self._side_update_multi
             # multi-rank with the IPC dense mesh: the dW GEMM (and the all-reduce
             # it launches) may run on the side stream beside the head backward
             # and the sparse push exchange (PBX_OVERLAP_DW_IPC=1)
@@ -175,6 +187,22 @@ class CtrTrainStep:
         ev.record(torch.cuda.current_stream(self.device))
         set_pre_head_event(self.model.tower.uid, ev)
         self.opt.step(1.0, join=False)
+
+    def _side_update_multi(self):
+        """Tower dense-grads hook (multi-rank overlapped optimizer): the
+        gradient + statistics all-reduce, then Adam (data_norm update fused)
+        on the all-reduce's stream; the next forward joins that stream."""
+        from ..parallel.dense import add_grad_producer, set_pre_head_event
+
+        self.sync.launch()
+        st = self.sync._stream
+        with torch.cuda.stream(st):
+            self.opt.step(self.sync.grad_scale(), join=False)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        self.sync._launched = False  # joined by the next forward, not by before_step
+        set_pre_head_event(self.model.tower.uid, ev)
+        add_grad_producer(st)
 
     def set_next(self, batch, slot: int = 0):
         """Batch to prefetch (pool) at the end of each train_step (None: off)."""
@@ -234,7 +262,7 @@ class CtrTrainStep:
                 self.model.prefetch_pool(self.next_batch, self.next_slot)
             else:
                 self.prefetch(self.next_batch, self.next_slot)
-        if self.adam_overlap:
+        if self.adam_overlap or self.adam_overlap_multi:
             pass  # the side stream runs the update; the next forward joins it after its head
         elif self.adam_side:
             join_grad_producers()  # the side stream ran the update

@@ -522,9 +522,12 @@ class BoxPSWorker:
                         lh = db.lod.cpu()
                         if pipe_on:
                             eng.ensure_pull_ring(n_buf * K)
+                        # the overlapped Adam of a step may run on under the next
+                        # step of the same graph (that step's forward joins it)
                         g = GraphedTrainStep(step_for(c, lh), warm[c][0], dev, warmup=0, warm_batches=warm[c],
                                              on_warm=None if in_graph else metrics, n_buffers=n_buf,
-                                             pipeline=pipe_for(c, lh), steps_per_graph=K)
+                                             pipeline=pipe_for(c, lh), steps_per_graph=K,
+                                             join_each_step=not s.side_adam)
                         g.metrics_in_graph = in_graph
                         invalidate_others(c)
                         graphs[c] = g

@@ -143,7 +143,8 @@ def main():
            "graph_replays": last.get("graph_replays", 0), "auc": box.get_metric_msg("auc")[0],
            "fc_precision": args.fc_precision, "steps_per_graph": last.get("steps_per_graph", 1),
            "pipelined_front": last.get("pipelined_front", False), "table_rows": box.engine.table.size(),
-           "step_s": round(last.get("step", 0.0), 4)}
+           "step_s": round(last.get("step", 0.0), 4),
+           "adam_overlap": bool(getattr(exe.sessions_for(main_p)[0], "side_adam", False))}
     print(json.dumps(out), flush=True)
 
 

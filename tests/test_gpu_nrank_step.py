@@ -62,8 +62,11 @@ def _union_keys(union):
 
 def _worker(rank, W, port, B, steps, q, mode="plain"):
     try:
-        if mode in ("overlap_dw", "both", "both_split3"):
+        if mode in ("overlap_dw", "both", "both_split3", "both_adam"):
             os.environ["PBX_OVERLAP_DW_IPC"] = "1"
+        # the overlapped multi-rank Adam (default) only in its own mode: the
+        # others keep covering the in-order update
+        os.environ["PBX_ADAM_OVERLAP_MULTI"] = "1" if mode == "both_adam" else "0"
         if mode == "both_split3":
             os.environ["PBX_SPLIT_PREFETCH"] = "3"
         import torch.distributed as dist
@@ -94,14 +97,15 @@ def _worker(rank, W, port, B, steps, q, mode="plain"):
         losses = []
         # step 0 eagerly through the graph's buffers, then the captured replays
         pipe = None
-        if mode in ("pipeline", "both", "both_split3"):
+        if mode in ("pipeline", "both", "both_split3", "both_adam"):
             # sharded pipelined front: each step pulls the next batch (dedup,
             # both exchanges, owner gather, pooling) right after its own push
             assert eng.can_prefetch_pull()
             pipe = (lambda b, j: step.prefetch(b, j), step.set_next, eng.clear_prefetch)
         g = GraphedTrainStep(step.train_step, hbs[0], dev, warmup=0, warm_batches=[hbs[0]],
                              on_warm=lambda out: losses.append(float(out)), n_buffers=3 if pipe else 2,
-                             pipeline=pipe)
+                             pipeline=pipe, join_each_step=not step.adam_overlap_multi)
+        assert step.adam_overlap_multi == (mode == "both_adam")
         ahead = 2 if pipe else 1
         for a in range(1, min(1 + ahead, steps)):
             g.load(a % g.n, hbs[a])
@@ -173,14 +177,15 @@ def _oracle(W, B, steps):
 
 
 @pytest.mark.parametrize("W,mode", [(2, "plain"), (4, "plain"), (2, "overlap_dw"), (2, "pipeline"),
-                                    (4, "pipeline"), (2, "both"), (2, "both_split3"), (4, "both_split3")])
+                                    (4, "pipeline"), (2, "both"), (2, "both_split3"), (4, "both_split3"),
+                                    (2, "both_adam"), (4, "both_adam")])
 def test_nrank_graphed_deepfm_step_matches_union_oracle(W, mode):
     """mode: plain graphed step; overlap_dw = the dW GEMM and its IPC dense
     all-reduce on the side stream (PBX_OVERLAP_DW_IPC); pipeline = the sharded
     pipelined front (SparseEngine prefetch_pull with the exchanges inside)."""
     from paddlebox_amd.ops import reference as ref
 
-    B, steps = 256, 4 if mode in ("pipeline", "both", "both_split3") else 3
+    B, steps = 256, 4 if mode in ("pipeline", "both", "both_split3", "both_adam") else 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
