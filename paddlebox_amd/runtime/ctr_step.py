@@ -169,7 +169,13 @@ class CtrTrainStep:
         #      until this step's dX chain is done), beside the head and tower
         #      forward / backward -- for the sharded step, whose dedup + exchange
         #      chain after the push is far longer than the dW GEMM
-        mode = os.environ.get("PBX_SPLIT_PREFETCH", "0")
+        # default 3 on several ranks: the sharded chain after the push (owner
+        # update, sender hash dedup, two exchanges, owner gather) is far longer
+        # than the dW GEMM -- 1-rank rehearsal 0.4221 / 0.4225 -> 0.3899 /
+        # 0.3910 ms/step (mode 2: 0.449, profiles/r5_sharded_split3_ab.txt);
+        # on one rank the dedup beside the tower measured slower (0.372 vs
+        # 0.356, profiles/r5_split_prefetch_1rank_ab.txt)
+        mode = os.environ.get("PBX_SPLIT_PREFETCH", "3" if multi else "0")
         self.split_mode = mode if mode in ("1", "2", "3") else "0"
         self.split_prefetch = self.split_mode != "0" and tower is not None and hasattr(model, "prefetch_pool")
         if self.split_prefetch:

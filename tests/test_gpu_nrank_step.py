@@ -67,8 +67,9 @@ def _worker(rank, W, port, B, steps, q, mode="plain"):
         # the overlapped multi-rank Adam (default) only in its own mode: the
         # others keep covering the in-order update
         os.environ["PBX_ADAM_OVERLAP_MULTI"] = "1" if mode == "both_adam" else "0"
-        if mode == "both_split3":
-            os.environ["PBX_SPLIT_PREFETCH"] = "3"
+        # the multi-rank defaults: the next batch's dedup at the step start
+        # (split 3) in the both_split3 / both_adam modes, off in the others
+        os.environ["PBX_SPLIT_PREFETCH"] = "3" if mode in ("both_split3", "both_adam") else "0"
         import torch.distributed as dist
 
         from paddlebox_amd.ops import reference as ref
