@@ -138,7 +138,7 @@ class _CtrTowerFn(torch.autograd.Function):
             if dn_on and not getattr(dn, "stats_in_grad_bucket", False):
                 if dn.sync_stats and dn.group is not None and collective_active(dn.group):
                     allreduce_sum(dn.stats, dn.group)  # the group's IPC mesh when registered
-            if dn_on and not dn.fused_update:
+            if dn_on and not dn.fused_update and not getattr(dn, "update_in_hook", False):
                 h.data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, dn.stats, dn.decay)
             if t.on_dense_grads is not None:  # e.g. start the dense all-reduce, overlapped with the sparse push
                 if t.cross is not None and not hook["after_cross"]:

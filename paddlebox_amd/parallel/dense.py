@@ -50,6 +50,19 @@ def pop_pre_head_event(key: int):
     return _PRE_HEAD.pop(key, None)
 
 
+def join_grad_producer_upto_now(stream) -> None:
+    """Make the current stream wait for what ``stream`` has queued so far and
+    stop tracking it as a gradient producer -- work queued on it afterwards
+    (e.g. the next batch's dedup on the dW stream) is not waited for by a
+    later ``join_grad_producers``.  Other producers and pre-head events stay."""
+    if stream in _GRAD_PRODUCERS:
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        torch.cuda.current_stream(stream.device).wait_event(ev)
+        while stream in _GRAD_PRODUCERS:
+            _GRAD_PRODUCERS.remove(stream)
+
+
 def join_grad_producers() -> None:
     """Make the current stream wait for every pending gradient producer."""
     while _GRAD_PRODUCERS:

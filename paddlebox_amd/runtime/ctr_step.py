@@ -26,7 +26,9 @@ from typing import Optional, Sequence
 import torch
 import torch.distributed as dist
 
-from ..parallel.dense import DenseArena, DenseSync, FlatAdam, join_grad_producers
+from .. import _native
+
+from ..parallel.dense import DenseArena, DenseSync, FlatAdam, join_grad_producer_upto_now, join_grad_producers
 
 
 def make_ipc_mesh(nbytes: int, device, group=None, log=None):
@@ -142,6 +144,12 @@ class CtrTrainStep:
                     and os.environ.get("PBX_ADAM_OVERLAP_MULTI", "1") == "1"):
                 self.adam_overlap_multi = True
                 tower.on_dense_grads = self._side_update_multi
+                # the data_norm update leaves the Adam launch: the hook runs it
+                # right after the all-reduce (which sums the statistics), and
+                # the next step's head waits for it only, not for Adam
+                self.opt.fuse(mlps=[model.mlp], data_norms=[])
+                model.dn.fused_update = False
+                model.dn.update_in_hook = True
             # multi-rank with the IPC dense mesh: the dW GEMM (and the all-reduce
             # it launches) may run on the side stream beside the head backward
             # and the sparse push exchange (PBX_OVERLAP_DW_IPC=1)
@@ -202,10 +210,13 @@ class CtrTrainStep:
 
         self.sync.launch()
         st = self.sync._stream
+        dn = self.model.dn
         with torch.cuda.stream(st):
-            self.opt.step(self.sync.grad_scale(), join=False)
+            if dn.training and dn.update_norm:  # the statistics just summed in the gradient tail
+                _native.hip().data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, dn.stats, dn.decay)
             ev = torch.cuda.Event()
-            ev.record(st)
+            ev.record(st)  # the next step's head may start here
+            self.opt.step(self.sync.grad_scale(), join=False)
         self.sync._launched = False  # joined by the next forward, not by before_step
         set_pre_head_event(self.model.tower.uid, ev)
         add_grad_producer(st)
@@ -242,9 +253,16 @@ class CtrTrainStep:
         nb = self.next_batch
         if nb is None or not self.engine.can_prefetch_pull():
             return
-        join_grad_producers()  # the forward's own join below then finds nothing to wait for
         cur = torch.cuda.current_stream(self.device)
         st = self.model.tower._side_stream(self.device)
+        if self.adam_overlap_multi:
+            # only the dW stream's work so far (the previous dW reads the
+            # activations this forward rewrites): the overlapped Adam on the
+            # all-reduce stream stays pending -- the head waits for its
+            # pre-head event, the tower for its join
+            join_grad_producer_upto_now(st)
+        else:
+            join_grad_producers()  # the forward's own join below then finds nothing to wait for
         st.wait_stream(cur)
         with torch.cuda.stream(st):
             self.engine.prefetch_dedup(nb.keys, self.next_slot)
