@@ -451,7 +451,16 @@ class PadBoxSlotDataset(DatasetBase):
             if pin:
                 with torch.cuda.stream(stream):
                     db = hb.to(dev, non_blocking=True)
-                torch.cuda.current_stream(dev).wait_stream(stream)
+                cur = torch.cuda.current_stream(dev)
+                cur.wait_stream(stream)
+                # the device batch is allocated on the copy stream but read on
+                # the compute stream: without this its memory returns to the copy
+                # stream's pool when the batch is dropped, and a later batch's
+                # H2D copy can overwrite it while the step that read it is
+                # still queued (the host runs ahead in the eager loop)
+                for t in (db.keys, db.lod, db.dense, *db.extra.values()):
+                    if isinstance(t, torch.Tensor) and t.is_cuda:
+                        t.record_stream(cur)
                 yield db
             else:
                 yield hb

@@ -150,8 +150,11 @@ def _worker(rank, W, port, d, transpile, q):
         q.put((rank, repr(e) + traceback.format_exc()))
 
 
-@pytest.mark.parametrize("transpile", [True, False])
-def test_fluid_two_ranks_match_union_oracle(tmp_path, monkeypatch, transpile):
+@pytest.mark.parametrize("transpile,graph", [(True, True), (False, True), (False, False)])
+def test_fluid_two_ranks_match_union_oracle(tmp_path, monkeypatch, transpile, graph):
+    """graph=False: the eager loop (a device batch read on the compute stream
+    after its H2D copy on a side stream once returned its memory to the copy
+    stream's pool early: corrupted batches / a stalled rank, round 5)."""
     from paddlebox_amd import _native
     from paddlebox_amd.ops import reference as ref
 
@@ -159,6 +162,7 @@ def test_fluid_two_ranks_match_union_oracle(tmp_path, monkeypatch, transpile):
 
     W = 2
     d = str(tmp_path)
+    monkeypatch.setenv("PBX_TEST_FLUID_GRAPH", "1" if graph else "0")  # inherited by the spawned ranks
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
