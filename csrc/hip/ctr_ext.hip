@@ -584,8 +584,19 @@ __global__ __launch_bounds__(256) void k_colsum_strided(const float* __restrict_
   const int m0 = blockIdx.y * kColSlice, m1 = min(M, m0 + kColSlice);
   float s = 0.f;
   if (n < N) {
+    // 8 independent row loads in flight per thread (a dependent chain of
+    // single loads left this memory-bound kernel latency-bound)
     const float* p = x + (int64_t)b * sb + n;
-    for (int m = m0 + ph; m < m1; m += 4) s += p[(int64_t)m * ld];
+    float a[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = 0.f;
+    int m = m0 + ph;
+    for (; m + 28 < m1; m += 32) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += p[(int64_t)(m + 4 * j) * ld];
+    }
+    for (; m < m1; m += 4) a[0] += p[(int64_t)m * ld];
+    s = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   }
   part[ph][threadIdx.x & 63] = s;
   __syncthreads();
@@ -973,10 +984,12 @@ __global__ __launch_bounds__(256) void k_ra_dexp(const float* __restrict__ dout,
     for (int k = 0; k < R; ++k) spf[k][t] = pf[k];
   }
   __syncthreads();
-  if (blockIdx.y == 0) {  // zero rows of invalid pairs (every pair of a rank-less instance)
-    for (int e = t; e < n * R * C; e += 256) {
-      const int jj = e / (R * C), rem = e - jj * R * C, k = rem / C;
-      if (spf[k][jj] < 0) dexp[(int64_t)sperm[jj] * R * C + rem] = 0.f;
+  {  // zero rows of invalid pairs (every pair of a rank-less instance): each
+     // column block zeroes its own 64 columns of the R*C row
+    const int cw = min(64, KT - n0);
+    for (int e = t; e < n * cw; e += 256) {
+      const int jj = e / cw, col = n0 + (e - jj * cw), k = col / C;
+      if (spf[k][jj] < 0) dexp[(int64_t)sperm[jj] * KT + col] = 0.f;
     }
   }
   if (q == R) return;
