@@ -54,6 +54,41 @@ __global__ __launch_bounds__(kScanThreads) void k_batch_scan(BatchSrc src, int64
   // together (order -> offsets is a dependent pair per record; one record at
   // a time left the 26 workgroups latency-bound: 38 us per batch)
   constexpr int kScanUnroll = 8;
+  if (per <= kScanUnroll) {
+    // one round (B <= 8192): the lengths stay in registers for the offset
+    // pass (re-reading the just-written lod entries was a serial chain of
+    // global round trips per thread)
+    int64_t iv[kScanUnroll], n[kScanUnroll];
+#pragma unroll
+    for (int u = 0; u < kScanUnroll; ++u) iv[u] = b0 + u < b1 ? order[b0 + u] : -1;
+#pragma unroll
+    for (int u = 0; u < kScanUnroll; ++u) {
+      n[u] = 0;
+      if (iv[u] >= 0) {
+        const int64_t* o = uoff + iv[u] * src.nu + j;
+        n[u] = o[1] - o[0];
+      }
+      sum += n[u];
+    }
+    const int64_t incl = wave_incl_scan(sum);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) wsum[w] = incl;
+    __syncthreads();
+    int64_t before = 0, all = 0;
+    for (int k = 0; k < kScanThreads / 64; ++k) {
+      if (k < w) before += wsum[k];
+      all += wsum[k];
+    }
+    int64_t run = before + incl - sum;
+#pragma unroll
+    for (int u = 0; u < kScanUnroll; ++u)
+      if (b0 + u < b1) {
+        l[b0 + u] = run;
+        run += n[u];
+      }
+    if (threadIdx.x == 0) tot[s] = all;
+    return;
+  }
   for (int bb = b0; bb < b1; bb += kScanUnroll) {
     int64_t iv[kScanUnroll], n[kScanUnroll];
 #pragma unroll
