@@ -689,13 +689,13 @@ __global__ __launch_bounds__(256) void k_i8_gemm(const signed char* __restrict__
 // sit contiguously: W_r = W[r*R*C : (r+1)*R*C] viewed as [R*C, P].  With
 //   A_i[f*C + c] = sum over valid peers k of i with faster_k = f of x[idx_k][c]
 // the op is, per rank r over the instances of that rank,
-//   out_i = A_i W_r,   G_i = dout_i W_r^T (the dexp rows),   dW_r = sum_i A_i^T dout_i
+//   out_i = A_i W_r,   G_i = dout_i W_r^T (the input-gradient rows),   dW_r = sum_i A_i^T dout_i
 // -- dense GEMMs (K = R*C for out / G, K = the rank's instances for dW) that
 // never visit a block an instance does not use.  k_ra_bucket counting-sorts
 // the instances by rank once (stable, one workgroup); the forward keeps the
 // permutation + tile table for the backward.  Exact fp32 (v_mfma_f32_16x16x4_f32).
 // A pair (i, k) is valid when rank_i in 1..R, faster_k + 1 in 1..R and
-// 0 <= idx_k < B; invalid pairs contribute nothing and get zero dexp rows.
+// 0 <= idx_k < B; invalid pairs contribute nothing (k_ra_dx skips them).
 constexpr int kRaT = 32;  // instances per tile
 constexpr int kRaBucketThreads = 1024;
 constexpr int kRaSeg = 256;  // dW: peer tables staged per segment of instances
@@ -805,10 +805,17 @@ __global__ __launch_bounds__(kRaBucketThreads) void k_ra_bucket(const int* __res
 template <int R>
 __device__ __forceinline__ bool ra_tile(const int* __restrict__ meta, int x, int* q, int* start, int* n) {
   constexpr int Q = R + 1;
-  if (x >= meta[3 * Q]) return false;
+  // the tile prefix is non-decreasing: the bucket is the number of prefix
+  // entries <= x, every entry loaded at once (a search loop made each step a
+  // dependent load)
+  int pre[R + 1];
+#pragma unroll
+  for (int j = 0; j <= R; ++j) pre[j] = meta[2 * Q + 1 + j];
+  if (x >= pre[R]) return false;
   int b = 0;
-  while (b < R && x >= meta[2 * Q + b + 1]) ++b;
-  const int lt = x - meta[2 * Q + b];
+#pragma unroll
+  for (int j = 0; j < R; ++j) b += x >= pre[j];
+  const int lt = x - (b ? pre[b - 1] : 0);
   *q = b;
   *start = meta[Q + b] + lt * kRaT;
   *n = min(kRaT, meta[b] - lt * kRaT);
@@ -959,50 +966,46 @@ __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, con
   }
 }
 
-// dexp[j][k][c] = valid(j,k) ? G_j[faster_k*C + c] : 0, G_j = dout_j W_q^T.
-// Tile: 32 instances x 64 columns of R*C; K = P.  Grid.y == 0 also writes
-// the zero rows of invalid pairs.
+// G_j = dout_j W_q^T for every instance j of a valid rank q, dense [B][R*C]
+// (row j, column f*C + c: the gradient reaching the peer of j whose faster
+// rank is f).  Tile: 32 instances; a workgroup runs `cbs` 64-column blocks of
+// R*C (blockIdx.y, + gridDim.y, ...), so the bucket lookup, the perm read and
+// -- when P <= 64 -- the dout tile are paid once per tile, not once per
+// column block; the next block's W_q^T chunk is loaded into registers while
+// the current one runs on MFMA.  Invalid pairs are resolved by k_ra_dx (no
+// zero rows, no per-peer scatter).
 template <int R>
-__global__ __launch_bounds__(256) void k_ra_dexp(const float* __restrict__ dout, const int* __restrict__ ro, int ld,
-                                                 const float* __restrict__ W, int B, int C, int P,
-                                                 const int* __restrict__ perm, const int* __restrict__ meta,
-                                                 float* __restrict__ dexp) {
+__global__ __launch_bounds__(256) void k_ra_g(const float* __restrict__ dout, const float* __restrict__ W, int B,
+                                              int C, int P, const int* __restrict__ perm,
+                                              const int* __restrict__ meta, float* __restrict__ G) {
   constexpr int KC = 64;
   __shared__ float Ds[KC][kRaT + 4];  // [p][instance]
   __shared__ float Ws[KC][68];        // [p][column]
-  __shared__ int sperm[kRaT], spf[R][kRaT];
+  __shared__ int sperm[kRaT];
   int q, start, n;
   if (!ra_tile<R>(meta, blockIdx.x, &q, &start, &n)) return;
+  if (q == R) return;  // rank-less instances: no valid pair reads their G row
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int n0 = blockIdx.y * 64, KT = R * C;
-  if (t < kRaT) {
-    const int i = t < n ? perm[start + t] : -1;
-    sperm[t] = i;
-    int pf[R], px[R];
-    ra_peers<R>(ro, ld, (q < R) ? i : -1, B, pf, px);
-#pragma unroll
-    for (int k = 0; k < R; ++k) spf[k][t] = pf[k];
-  }
+  const int KT = R * C, ncb = (KT + 63) / 64, npc = (P + KC - 1) / KC;
+  const int nmine = blockIdx.y < ncb ? (ncb - 1 - blockIdx.y) / gridDim.y + 1 : 0;
+  const int nit = nmine * npc;  // (column block, p chunk) iterations, p fastest
+  if (nit == 0) return;
+  if (t < kRaT) sperm[t] = t < n ? perm[start + t] : -1;
   __syncthreads();
-  {  // zero rows of invalid pairs (every pair of a rank-less instance): each
-     // column block zeroes its own 64 columns of the R*C row
-    const int cw = min(64, KT - n0);
-    for (int e = t; e < n * cw; e += 256) {
-      const int jj = e / cw, col = n0 + (e - jj * cw), k = col / C;
-      if (spf[k][jj] < 0) dexp[(int64_t)sperm[jj] * KT + col] = 0.f;
-    }
-  }
-  if (q == R) return;
   const float* Wq = W + (int64_t)q * KT * P;
   const int ii = t & 31, pa = (t >> 5) * 8;    // dout staging: instance ii, p .. p + 7
   const int wn = t >> 2, wpa = (t & 3) * 16;   // W staging: column wn, p .. p + 15
   const int64_t drow = sperm[ii] >= 0 ? (int64_t)sperm[ii] * P : -1;
+  const bool dout_once = npc == 1;             // the dout tile is the same for every column block
   float rd[8], rw[16];
-  auto load = [&](int pc) {
+  auto load = [&](int it) {
+    const int n0 = (blockIdx.y + (it / npc) * gridDim.y) * 64, pc = (it % npc) * KC;
+    if (!dout_once || it == 0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int p = pc + pa + j;
-      rd[j] = (drow >= 0 && p < P) ? dout[drow + p] : 0.f;
+      for (int j = 0; j < 8; ++j) {
+        const int p = pc + pa + j;
+        rd[j] = (drow >= 0 && p < P) ? dout[drow + p] : 0.f;
+      }
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -1013,54 +1016,73 @@ __global__ __launch_bounds__(256) void k_ra_dexp(const float* __restrict__ dout,
   const int fr = lane & 15, fk = lane >> 4, mi = (w & 1) * 16, nb = (w >> 1) * 32;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   load(0);
-  for (int pc = 0; pc < P; pc += KC) {
+  for (int it = 0; it < nit; ++it) {
     __syncthreads();
+    if (!dout_once || it == 0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) Ds[pa + j][ii] = rd[j];
+      for (int j = 0; j < 8; ++j) Ds[pa + j][ii] = rd[j];
+    }
 #pragma unroll
     for (int j = 0; j < 16; ++j) Ws[wpa + j][wn] = rw[j];
     __syncthreads();
-    if (pc + KC < P) load(pc + KC);
+    if (it + 1 < nit) load(it + 1);
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 4) {
       const float a = Ds[kk + fk][mi + fr];
       acc0 = mfma4(a, Ws[kk + fk][nb + fr], acc0);
       acc1 = mfma4(a, Ws[kk + fk][nb + 16 + fr], acc1);
     }
-  }
+    if ((it + 1) % npc) continue;
+    const int n0 = (blockIdx.y + (it / npc) * gridDim.y) * 64;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int col = n0 + nb + 16 * h + fr;
-    if (col >= KT) continue;
-    const int f = col / C, c = col - f * C;
+    for (int h = 0; h < 2; ++h) {
+      const int col = n0 + nb + 16 * h + fr;
+      if (col >= KT) continue;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = mi + 4 * fk + r;
-      if (m >= n) continue;
-      const float v = h ? acc1[r] : acc0[r];
-      float* d = dexp + (int64_t)sperm[m] * R * C + c;
-#pragma unroll
-      for (int k = 0; k < R; ++k)
-        if (spf[k][m] == f) d[k * C] = v;
+      for (int r = 0; r < 4; ++r) {
+        const int m = mi + 4 * fk + r;
+        if (m < n) G[(int64_t)sperm[m] * KT + col] = h ? acc1[r] : acc0[r];
+      }
     }
+    acc0 = (f32x4){0.f, 0.f, 0.f, 0.f};
+    acc1 = acc0;
   }
 }
 
-// dx[i][c] = sum_t dexp[ro[i][2t+2]][rank_i - 1][c]   (reference gather form,
-// merge_input_gradient_kernel: exact for consistent page-view rank data)
-__global__ void k_ra_dx(const float* __restrict__ dexp, const int* __restrict__ ro, int ld, int B, int C, int R,
-                        float* __restrict__ dx) {
+// dx[i][c] = sum over the peers j = ro[i][2t+2] of dexp[j][rank_i - 1][c]
+// (the reference's gather form, merge_input_gradient_kernel), where
+// dexp[j][k] = G_j[faster_{j,k} C : +C] when j's pair k is valid (rank_j,
+// faster_{j,k} in 1..R, its index in [0, B)) and 0 otherwise -- resolved here
+// from j's rank_offset row instead of materialising the zero rows
+template <int R>
+__global__ __launch_bounds__(256) void k_ra_dx(const float* __restrict__ G, const int* __restrict__ ro, int ld,
+                                               int B, int C, float* __restrict__ dx) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)B * C) return;
   const int i = (int)(t / C), c = (int)(t % C);
-  const int rank = ro[(int64_t)i * ld];
+  const int* ri = ro + (int64_t)i * ld;
+  const int rank = ri[0];
   float s = 0.f;
   if (rank >= 1 && rank <= R) {
-    for (int q = 0; q < R; ++q) {
-      const int j = ro[(int64_t)i * ld + 2 * q + 2];
-      if (j < 0 || j >= B) continue;
-      s += dexp[((int64_t)j * R + (rank - 1)) * C + c];
+    // three rounds of independent loads (peer ids, their rank_offset
+    // entries, the G values) instead of a dependent chain per peer
+    const int k = rank - 1;
+    int j[R], f[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) j[u] = ri[2 * u + 2];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      f[u] = -1;
+      if (j[u] < 0 || j[u] >= B) continue;
+      const int* rj = ro + (int64_t)j[u] * ld;
+      const int rkj = rj[0], ff = rj[2 * k + 1] - 1, id = rj[2 * k + 2];
+      if (rkj >= 1 && rkj <= R && ff >= 0 && ff < R && id >= 0 && id < B) f[u] = ff;
     }
+    float v[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) v[u] = f[u] >= 0 ? G[((int64_t)j[u] * R + f[u]) * C + c] : 0.f;
+#pragma unroll
+    for (int u = 0; u < R; ++u) s += v[u];
   }
   dx[t] = s;
 }
@@ -1073,7 +1095,7 @@ template <int R>
 __global__ __launch_bounds__(256) void k_ra_dw(const float* __restrict__ x, const float* __restrict__ dout,
                                                const int* __restrict__ ro, int ld, int B, int C, int P,
                                                const int* __restrict__ perm, const int* __restrict__ meta, int splits,
-                                               float* __restrict__ dW) {
+                                               float* __restrict__ dW, int dbg) {
   constexpr int Q = R + 1, KC = 32;
   __shared__ float Xs[KC][68];  // [instance][m]
   __shared__ float Ds[KC][68];  // [instance][p]
@@ -1145,6 +1167,11 @@ __global__ __launch_bounds__(256) void k_ra_dw(const float* __restrict__ x, cons
         acc[1][1] = mfma4(a1, b1, acc[1][1]);
       }
     }
+  }
+  if (dbg & 1) {  // keep the GEMM live, skip the atomics
+    const float z = acc[0][0][0] + acc[0][1][1] + acc[1][0][2] + acc[1][1][3];
+    if (z == 1234.5f) dW[t] = z;
+    return;
   }
   float* dWq = dW + (int64_t)q * KT * P;
 #pragma unroll
@@ -1541,17 +1568,27 @@ void launch_rank_attention_bwd(const float* x, const float* dout, const int* ro,
   if (B == 0) return;
   const int* perm = bucket;
   const int* meta = bucket + B;
-  if (dx != nullptr) {  // dexp (dout W_r^T per peer row) then the gather merge
-    PBX_RA_DISPATCH(k_ra_dexp, dim3(ra_max_tiles(B, R), (R * C + 63) / 64), 256, dout, ro, ld, W, B, C, P, perm, meta,
-                    dexp);
-    hipLaunchKernelGGL(k_ra_dx, dim3(nblk((int64_t)B * C)), dim3(256), 0, s, dexp, ro, ld, B, C, R, dx);
+  // timing experiments: PBX_RA_DEBUG 1 (dW without its atomics),
+  // PBX_RA_DW_SPLITS, PBX_RA_G_BLOCKS (column blocks per k_ra_g workgroup)
+  static const int dbg = getenv("PBX_RA_DEBUG") ? atoi(getenv("PBX_RA_DEBUG")) : 0;
+  static const int dw_splits = getenv("PBX_RA_DW_SPLITS") ? atoi(getenv("PBX_RA_DW_SPLITS")) : 0;
+  static const int g_blocks = getenv("PBX_RA_G_BLOCKS") ? atoi(getenv("PBX_RA_G_BLOCKS")) : 0;
+  if (dx != nullptr) {  // G = dout W_r^T per instance, then the gather merge
+    const int tiles = ra_max_tiles(B, R), ncb = (R * C + 63) / 64;
+    int gy = std::min(ncb, std::max(1, (512 + tiles - 1) / tiles));
+    if (g_blocks > 0) gy = (ncb + g_blocks - 1) / g_blocks;
+    PBX_RA_DISPATCH(k_ra_g, dim3(tiles, gy), 256, dout, W, B, C, P, perm, meta, dexp);
+    PBX_RA_DISPATCH(k_ra_dx, dim3(nblk((int64_t)B * C)), 256, dexp, ro, ld, B, C, dx);
   }
   if (dW == nullptr) return;
-  // ~128 instances per split at an even rank mix; dW zeroed by the caller
-  int splits = (B + R * 128 - 1) / (R * 128);
+  // ~64 instances per split at an even rank mix (measured at B = 5k R = 8:
+  // 128 per split 40 us, 64 25 us, 32 29 us -- the loop is latency bound, the
+  // atomics grow with the splits); dW zeroed by the caller
+  int splits = (B + R * 64 - 1) / (R * 64);
   splits = splits < 1 ? 1 : (splits > 64 ? 64 : splits);
+  if (dw_splits > 0) splits = dw_splits;
   PBX_RA_DISPATCH(k_ra_dw, dim3((R * C + 63) / 64, (P + 63) / 64, R * splits), 256, x, dout, ro, ld, B, C, P, perm,
-                  meta, splits, dW);
+                  meta, splits, dW, dbg);
 }
 
 void launch_cvm_fwd(const float* x, int64_t n, int W, bool use_cvm, float* y, hipStream_t s) {

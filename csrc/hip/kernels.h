@@ -827,7 +827,7 @@ void launch_i8_gemm(const signed char* qx, const signed char* qwt, int M, int N,
 int rank_attention_bucket_ints(int B, int R);
 void launch_rank_attention_fwd(const float* x, const int* ro, int ld, const float* W, int B, int C, int P, int R,
                                int* bucket, float* out, hipStream_t s);
-// dexp: scratch [B][R][C]; dx overwritten; dW accumulated (atomics: zero it first)
+// dexp: scratch [B][R][C] (the G rows); dx overwritten; dW accumulated (atomics: zero it first)
 void launch_rank_attention_bwd(const float* x, const float* dout, const int* ro, int ld, const float* W, int B, int C,
                                int P, int R, const int* bucket, float* dexp, float* dx, float* dW, hipStream_t s);
 void launch_cvm_fwd(const float* x, int64_t n, int W, bool use_cvm, float* y, hipStream_t s);
