@@ -977,10 +977,15 @@ __global__ __launch_bounds__(256) void k_ra_fwd(const float* __restrict__ x, con
 template <int R>
 __global__ __launch_bounds__(256) void k_ra_g(const float* __restrict__ dout, const float* __restrict__ W, int B,
                                               int C, int P, const int* __restrict__ perm,
-                                              const int* __restrict__ meta, float* __restrict__ G) {
+                                              const int* __restrict__ meta, float* __restrict__ G, int dbg) {
   constexpr int KC = 64;
-  __shared__ float Ds[KC][kRaT + 4];  // [p][instance]
-  __shared__ float Ws[KC][68];        // [p][column]
+  // staging: thread t reads 4 consecutive p (one float4 when P % 4 == 0) of
+  // rows t / 16 + 16 j, so a wave instruction covers 4 whole 256 B rows --
+  // coalesced (a lane-per-row mapping touched 64 segments per instruction
+  // and made the kernel TA-bound: 21.5 us at B = 5k R = 8).  Row strides 33 /
+  // 65: the transposed LDS stores hit 64 distinct banks.
+  __shared__ float Ds[KC][kRaT + 1];  // [p][instance]
+  __shared__ float Ws[KC][65];        // [p][column]
   __shared__ int sperm[kRaT];
   int q, start, n;
   if (!ra_tile<R>(meta, blockIdx.x, &q, &start, &n)) return;
@@ -993,25 +998,36 @@ __global__ __launch_bounds__(256) void k_ra_g(const float* __restrict__ dout, co
   if (t < kRaT) sperm[t] = t < n ? perm[start + t] : -1;
   __syncthreads();
   const float* Wq = W + (int64_t)q * KT * P;
-  const int ii = t & 31, pa = (t >> 5) * 8;    // dout staging: instance ii, p .. p + 7
-  const int wn = t >> 2, wpa = (t & 3) * 16;   // W staging: column wn, p .. p + 15
-  const int64_t drow = sperm[ii] >= 0 ? (int64_t)sperm[ii] * P : -1;
-  const bool dout_once = npc == 1;             // the dout tile is the same for every column block
-  float rd[8], rw[16];
+  const int sr = t >> 4, sp = (t & 15) * 4;
+  const bool vec = (P % 4) == 0 && ((reinterpret_cast<uintptr_t>(dout) | reinterpret_cast<uintptr_t>(W)) & 15) == 0;
+  int64_t drow[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) drow[j] = sperm[sr + 16 * j] >= 0 ? (int64_t)sperm[sr + 16 * j] * P : -1;
+  const bool dout_once = npc == 1;  // the dout tile is the same for every column block
+  float4 rd[2], rw[4];
+  auto ld4 = [&](const float* row, int p, bool ok) {
+    if (!ok || p >= P) return make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vec) return *reinterpret_cast<const float4*>(row + p);
+    return make_float4(row[p], p + 1 < P ? row[p + 1] : 0.f, p + 2 < P ? row[p + 2] : 0.f,
+                       p + 3 < P ? row[p + 3] : 0.f);
+  };
   auto load = [&](int it) {
     const int n0 = (blockIdx.y + (it / npc) * gridDim.y) * 64, pc = (it % npc) * KC;
     if (!dout_once || it == 0) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int p = pc + pa + j;
-        rd[j] = (drow >= 0 && p < P) ? dout[drow + p] : 0.f;
-      }
+      for (int j = 0; j < 2; ++j) rd[j] = ld4(dout + (drow[j] >= 0 ? drow[j] : 0), pc + sp, drow[j] >= 0);
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int p = pc + wpa + j;
-      rw[j] = (n0 + wn < KT && p < P) ? Wq[(int64_t)(n0 + wn) * P + p] : 0.f;
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + sr + 16 * j;
+      rw[j] = ld4(Wq + (int64_t)(col < KT ? col : 0) * P, pc + sp, col < KT);
     }
+  };
+  auto put4 = [](float* base, int stride, const float4& v) {
+    base[0] = v.x;
+    base[stride] = v.y;
+    base[2 * stride] = v.z;
+    base[3 * stride] = v.w;
   };
   const int fr = lane & 15, fk = lane >> 4, mi = (w & 1) * 16, nb = (w >> 1) * 32;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -1020,10 +1036,10 @@ __global__ __launch_bounds__(256) void k_ra_g(const float* __restrict__ dout, co
     __syncthreads();
     if (!dout_once || it == 0) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) Ds[pa + j][ii] = rd[j];
+      for (int j = 0; j < 2; ++j) put4(&Ds[sp][sr + 16 * j], kRaT + 1, rd[j]);
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) Ws[wpa + j][wn] = rw[j];
+    for (int j = 0; j < 4; ++j) put4(&Ws[sp][sr + 16 * j], 65, rw[j]);
     __syncthreads();
     if (it + 1 < nit) load(it + 1);
 #pragma unroll
@@ -1034,6 +1050,12 @@ __global__ __launch_bounds__(256) void k_ra_g(const float* __restrict__ dout, co
     }
     if ((it + 1) % npc) continue;
     const int n0 = (blockIdx.y + (it / npc) * gridDim.y) * 64;
+    if (dbg & 2) {  // timing experiment: keep the GEMM live, skip the stores
+      if (acc0[0] + acc1[3] == 1234.5f) G[t] = acc0[1];
+      acc0 = (f32x4){0.f, 0.f, 0.f, 0.f};
+      acc1 = acc0;
+      continue;
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int col = n0 + nb + 16 * h + fr;
@@ -1100,6 +1122,10 @@ __global__ __launch_bounds__(256) void k_ra_dw(const float* __restrict__ x, cons
   __shared__ float Xs[KC][68];  // [instance][m]
   __shared__ float Ds[KC][68];  // [instance][p]
   __shared__ int sinst[kRaSeg], spf[R][kRaSeg], spx[R][kRaSeg];
+  // per instance and faster rank f: the x row of its first peer of rank f
+  // (-1: none), and a bit per f with further peers of that rank
+  __shared__ int spm[R][kRaSeg];
+  __shared__ unsigned sdup[kRaSeg];
   const int q = blockIdx.z / splits, s = blockIdx.z % splits;
   const int cnt = meta[q], per = (cnt + splits - 1) / splits;
   const int beg = meta[Q + q] + s * per, end = meta[Q + q] + min(cnt, (s + 1) * per);
@@ -1125,30 +1151,65 @@ __global__ __launch_bounds__(256) void k_ra_dw(const float* __restrict__ x, cons
       int pf[R], px[R];
       ra_peers<R>(ro, ld, i, B, pf, px);
       sinst[t] = i;
+      unsigned dup = 0;
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         spf[k][t] = pf[k];
         spx[k][t] = px[k];
       }
+#pragma unroll
+      for (int ff = 0; ff < R; ++ff) {
+        int m = -1, cnt = 0;
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+          if (pf[k] == ff) {
+            if (m < 0) m = px[k];
+            ++cnt;
+          }
+        spm[ff][t] = m;
+        if (cnt > 1) dup |= 1u << ff;
+      }
+      sdup[t] = dup;
     }
     __syncthreads();
+    // every row's x / dout address first (one LDS read each, from the
+    // per-rank match table: a compare chain over the peer table made every
+    // row wait on R dependent LDS reads), then all 16 loads unconditionally
+    // (clamped addresses, select after the load).  Further peers with the
+    // same faster rank (never in page-view data) are added by `add_extra`.
+    unsigned extra = 0;
     auto load = [&](int k0) {
+      int64_t xa[8], da[8];
+      extra = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int u = k0 + tr + 4 * j;
-        float a = 0.f, d = 0.f;
-        if (u < sn) {
+        const bool ok = u < sn;
+        const int m = (ok && f >= 0) ? spm[f][u] : -1;
+        xa[j] = m >= 0 ? (int64_t)m * C + c : -1;
+        if (ok && f >= 0 && ((sdup[u] >> f) & 1u)) extra |= 1u << j;
+        da[j] = (ok && pok) ? (int64_t)sinst[u] * P + p0 + tm : -1;
+      }
 #pragma unroll
-          for (int k = 0; k < R; ++k)
-            if (spf[k][u] == f) a += x[(int64_t)spx[k][u] * C + c];
-          if (pok) d = dout[(int64_t)sinst[u] * P + p0 + tm];
-        }
-        rx[j] = a;
-        rd[j] = d;
+      for (int j = 0; j < 8; ++j) {
+        const float a = x[xa[j] >= 0 ? xa[j] : 0], d = dout[da[j] >= 0 ? da[j] : 0];
+        rx[j] = xa[j] >= 0 ? a : 0.f;
+        rd[j] = da[j] >= 0 ? d : 0.f;
+      }
+    };
+    auto add_extra = [&](int k0) {  // the further same-rank peers of flagged rows
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (!(extra & (1u << j))) continue;
+        const int u = k0 + tr + 4 * j;
+        int hits = 0;
+        for (int k = 0; k < R; ++k)
+          if (spf[k][u] == f && hits++ > 0) rx[j] += x[(int64_t)spx[k][u] * C + c];
       }
     };
     load(0);
     for (int k0 = 0; k0 < sn; k0 += KC) {
+      if (extra) add_extra(k0);
       __syncthreads();
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -1568,7 +1629,7 @@ void launch_rank_attention_bwd(const float* x, const float* dout, const int* ro,
   if (B == 0) return;
   const int* perm = bucket;
   const int* meta = bucket + B;
-  // timing experiments: PBX_RA_DEBUG 1 (dW without its atomics),
+  // timing experiments: PBX_RA_DEBUG 1 (dW without its atomics), 2 (G without its stores),
   // PBX_RA_DW_SPLITS, PBX_RA_G_BLOCKS (column blocks per k_ra_g workgroup)
   static const int dbg = getenv("PBX_RA_DEBUG") ? atoi(getenv("PBX_RA_DEBUG")) : 0;
   static const int dw_splits = getenv("PBX_RA_DW_SPLITS") ? atoi(getenv("PBX_RA_DW_SPLITS")) : 0;
@@ -1577,7 +1638,7 @@ void launch_rank_attention_bwd(const float* x, const float* dout, const int* ro,
     const int tiles = ra_max_tiles(B, R), ncb = (R * C + 63) / 64;
     int gy = std::min(ncb, std::max(1, (512 + tiles - 1) / tiles));
     if (g_blocks > 0) gy = (ncb + g_blocks - 1) / g_blocks;
-    PBX_RA_DISPATCH(k_ra_g, dim3(tiles, gy), 256, dout, W, B, C, P, perm, meta, dexp);
+    PBX_RA_DISPATCH(k_ra_g, dim3(tiles, gy), 256, dout, W, B, C, P, perm, meta, dexp, dbg);
     PBX_RA_DISPATCH(k_ra_dx, dim3(nblk((int64_t)B * C)), 256, dexp, ro, ld, B, C, dx);
   }
   if (dW == nullptr) return;

@@ -68,6 +68,50 @@ def test_rank_attention_gpu_skewed_ranks():
     _close(wg.grad, wc.grad, rtol=1e-4, atol=2e-3)
 
 
+@pytest.mark.parametrize("R,C,P", [(3, 37, 70), (8, 64, 64)])
+def test_rank_attention_gpu_inconsistent_ranks(R, C, P):
+    """Random rank_offset rows (not page-view consistent): duplicate faster
+    ranks among one instance's peers (k_ra_dw's multi-hit path), ranks and
+    indices out of range.  out and dW against the fp64 torch path; dx against
+    the reference's gather form (merge_input_gradient_kernel: dx[i] = sum over
+    i's peers j of j's input-gradient row at slot rank_i - 1, zero for invalid
+    pairs), which is what the GPU kernel implements."""
+    g = torch.Generator().manual_seed(100 + R)
+    B = 700
+    ro = torch.empty(B, 2 * R + 1, dtype=torch.int32)
+    ro[:, 0] = torch.randint(-1, R + 2, (B,), generator=g)
+    ro[:, 1::2] = torch.randint(0, R + 2, (B, R), generator=g)  # faster rank + 1 (0 / > R: invalid)
+    ro[:, 1::2][torch.rand(B, R, generator=g) < 0.5] = 1  # many duplicates of faster rank 1
+    ro[:, 2::2] = torch.randint(-1, B + 1, (B, R), generator=g)
+    (xc, xg), (wc, wg) = _pair(torch.rand(B, C, generator=g), torch.rand(R * R * C, P, generator=g))
+    yc = cx.rank_attention(xc, ro, wc, R)
+    yg = cx.rank_attention(xg, ro.to(DEV), wg, R)
+    _close(yg, yc, atol=1e-3)
+    d = torch.randn(B, P, generator=g, dtype=torch.float64)
+    yc.backward(d)
+    yg.backward(d.float().to(DEV))
+    _close(wg.grad, wc.grad, rtol=1e-4, atol=2e-3)
+    Wb = wc.detach().reshape(R * R, C, P)
+    rol = ro.long()
+
+    def dexp_row(j, k):
+        q, f, idx = int(rol[j, 0]) - 1, int(rol[j, 2 * k + 1]) - 1, int(rol[j, 2 * k + 2])
+        if not (0 <= q < R and 0 <= f < R and 0 <= idx < B):
+            return torch.zeros(C, dtype=torch.float64)
+        return Wb[q * R + f] @ d[j]
+
+    dx_ref = torch.zeros(B, C, dtype=torch.float64)
+    for i in range(B):
+        r = int(rol[i, 0])
+        if not 1 <= r <= R:
+            continue
+        for u in range(R):
+            j = int(rol[i, 2 * u + 2])
+            if 0 <= j < B:
+                dx_ref[i] += dexp_row(j, r - 1)
+    _close(xg.grad, dx_ref, atol=1e-3)
+
+
 @pytest.mark.parametrize("dims", [(4, 150, 70, 90), (5, 1000, 64, 64), (3, 4133, 36, 20), (26, 8192, 64, 64)])
 @pytest.mark.parametrize("mode", ["default", "transpose", "batchcount"])
 def test_batch_fc_gpu(mode, dims):
