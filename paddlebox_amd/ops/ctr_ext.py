@@ -679,9 +679,15 @@ class _RankAttentionHip(torch.autograd.Function):
         h = _native.hip()
         dout = dout.contiguous()
         Wc = W.contiguous()
-        # dW (per-rank A^T dout) beside dexp + the gather merge on a side stream
+        # dW (per-rank A^T dout), then G + the gather merge, on the calling
+        # stream (_ctr_side's default here: graphed R8 backward 41.3 us on one
+        # stream vs 53.4 with dW on the side stream, R3 26.8 vs 37.2 --
+        # profiles/r5_ctr_ops_side_ab_v2.txt)
         cur = torch.cuda.current_stream(dout.device)
-        side = _ctr_side(dout.device, want=ctx.R >= 6)
+        side = _ctr_side(dout.device, want=False)
+        if side is cur:
+            dx, dW = h.rank_attention_bwd(x, ro, Wc, dout, bucket, ctx.R, 0)
+            return dx, None, dW, None
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             _, dW = h.rank_attention_bwd(x, ro, Wc, dout, bucket, ctx.R, 2)
@@ -786,9 +792,10 @@ def _ctr_side(device, want: bool = True):
     beside the input-gradient GEMM, or -- ``want`` False, or
     PBX_CTR_BWD_SIDE=0/1 forcing either way -- the calling stream.  Measured
     GPU time of the graphed backward, side vs one stream
-    (profiles/r5_ctr_ops_side_ab.txt): scaled_fc 83.0 vs 70.8 us, scaled_int8fc
-    120.1 vs 102.5, rank_attention R3 44.8 vs 41.3 but R8 69.6 vs 79.8 -- both
-    halves fill the GPU alone except rank_attention's wide-R dW."""
+    (profiles/r5_ctr_ops_side_ab.txt, r5_ctr_ops_side_ab_v2.txt after the
+    rank_attention / split-K dW rework): scaled_fc 76.7 vs 62.2 us,
+    scaled_int8fc 97.3 vs 82.3, rank_attention R8 53.4 vs 41.3, R3 37.2 vs
+    26.8 -- both halves fill the GPU alone, so every op defaults to one stream."""
     from ..runtime.streams import side_stream
 
     force = os.environ.get("PBX_CTR_BWD_SIDE", "")
@@ -920,8 +927,10 @@ class _ScaledFc(torch.autograd.Function):
             dx = h.sfc(dy, _half_of(W), None, gs / in_scale, in_scale, 1.0, 1.0 / gs)
             if dx is not None:
                 with torch.cuda.stream(side):
+                    # ~512 rows of N per split (scripts/micro/dw_gemm_sweep.py at
+                    # N = 8192, 400 x 400: 4 splits 73 us, 8 44.7, 16 39.9, 32 42.7)
                     h.hgemm(x, dy, dW, None, K, O, N, [1, K], [O, 1], O, 1.0, gs / in_scale, in_scale, 1.0, 1.0 / gs,
-                            max(1, min(64, N // 256)))
+                            max(1, min(64, N // 512)))
                     h.colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
                 cur.wait_stream(side)
                 return dx, dW, db.reshape(ctx.bshape), None, None, None
@@ -1015,12 +1024,29 @@ class _ScaledInt8Fc(torch.autograd.Function):
             db = dy.new_empty(O)
             dx = torch.mm(dy, W.t())
             with torch.cuda.stream(side):
-                torch.mm(x.t(), dy, out=dW)
+                _mm_tn_splitk(x, dy, dW)
                 _native.hip().colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
             cur.wait_stream(side)
         else:
             dx, dW, db = dy @ W.t(), x.t() @ dy, dy.sum(0)
         return dx, dW, db.reshape(ctx.bshape), None
+
+
+def _mm_tn_splitk(x: torch.Tensor, dy: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out = x^T dy for a long shared dimension N (a weight gradient over the
+    batch): S library GEMMs over contiguous row blocks in one batched call,
+    then their fixed-order sum -- deterministic, and at N = 8192, 512 x 512
+    39.7 us vs 57.6 for the single library GEMM, whose tile choice leaves the
+    long K serial (scripts/micro/dw_gemm_sweep.py; split 2 45.7, 4 41.1,
+    16 41.2)."""
+    N, K = x.shape
+    S = 8
+    while S > 1 and (N % S or N // S < 512):
+        S //= 2
+    if S == 1:
+        return torch.mm(x.t(), dy, out=out)
+    part = torch.bmm(x.reshape(S, N // S, K).transpose(1, 2), dy.reshape(S, N // S, dy.shape[1]))
+    return torch.sum(part, 0, out=out)
 
 
 def scaled_int8fc(x, W, b, attrs):

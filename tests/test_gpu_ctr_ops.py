@@ -181,6 +181,24 @@ def test_scaled_int8fc_gpu_exact(shape):
     torch.testing.assert_close(yg.cpu(), yc, rtol=1e-6, atol=1e-5)
 
 
+@pytest.mark.parametrize("shape", [(4096, 96, 80), (1500, 64, 32), (300, 20, 10)])
+def test_scaled_int8fc_gpu_backward(shape):
+    """The fp32 straight-through backward: dx = dy W^T, dW = x^T dy (split-K
+    batched GEMMs + fixed-order sum at N >= 1024), db = colsum(dy)."""
+    N, K, O = shape
+    g = torch.Generator().manual_seed(N)
+    x, W, b = torch.randn(N, K, generator=g), torch.randn(K, O, generator=g) * 0.2, torch.randn(O, generator=g)
+    a = dict(input_expand_factor=10.0, input_clip_factor=3.0, weight_expand_factor=40.0, weight_clip_factor=5.0,
+             int8_range=127.0)
+    (xc, xg), (wc, wg), (bc, bg) = _pair(x, W, b)
+    d = torch.randn(N, O, generator=g)
+    cx.scaled_int8fc(xc, wc, bc, a).backward(d.double())
+    cx.scaled_int8fc(xg, wg, bg, a).backward(d.to(DEV))
+    _close(xg.grad, xc.grad, rtol=1e-5, atol=1e-4)
+    _close(wg.grad, wc.grad, rtol=1e-5, atol=1e-3)
+    _close(bg.grad, bc.grad, rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("use_cvm", [True, False])
 def test_cvm_gpu(use_cvm):
     g = torch.Generator().manual_seed(7)
