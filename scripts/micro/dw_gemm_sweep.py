@@ -59,6 +59,31 @@ def main():
         print(json.dumps({"gemm": "scaled_fc_dW_hgemm", "ksplit": ks, "us": round(us, 2), "maxdiff_vs_ks4": err}),
               flush=True)
 
+    # library alternative: fp16 casts, S row-block fp16 GEMMs with fp32
+    # outputs (fp32 accumulate), fixed-order sum, the fp16 epilogue
+    ref16 = dW.clone()
+    h.hgemm(x, dy, ref16, None, K, O, N, [1, K], [O, 1], O, 1.0, 0.25, 8.0, 1.0, 0.5, 16)
+    for S in (4, 8, 16):
+        part = torch.empty(S, K, O, device=DEV)
+
+        def f(S=S, part=part):
+            x16 = x.half()
+            d16 = (dy * 0.25).half()
+            torch.bmm(x16.view(S, N // S, K).transpose(1, 2), d16.view(S, N // S, O), out_dtype=torch.float32,
+                      out=part)
+            torch.sum(part, 0, out=dW)
+            h.h16_epi(dW, None, 8.0, 1.0, 0.5)
+        try:
+            us = graph_us(f)
+        except Exception as e:  # noqa: BLE001
+            print(json.dumps({"gemm": "scaled_fc_dW_lib16", "S": S, "error": str(e)[:200]}), flush=True)
+            break
+        f()
+        torch.cuda.synchronize()
+        err = float(((dW - ref16).abs() / (ref16.abs() + 1e-3)).max())
+        print(json.dumps({"gemm": "scaled_fc_dW_lib16", "S": S, "us": round(us, 2), "max_rel_vs_hgemm": err}),
+              flush=True)
+
     N, K, O = 8192, 512, 512
     x = torch.randn(N, K, device=DEV)
     dy = torch.randn(N, O, device=DEV)
