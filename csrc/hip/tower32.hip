@@ -42,6 +42,21 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// The m-packed activation / dZ copies (MP32) are written once per step and
+// read once by a later kernel: non-temporal stores and loads stream them past
+// L2, which then keeps the layer weights every workgroup re-reads
+// (TowerArgs.debug 256: plain accesses, for the A/B).
+__device__ __forceinline__ void mp_store(float* p, const f32x4& v, int debug) {
+  if (debug & 256)
+    *reinterpret_cast<f32x4*>(p) = v;
+  else
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+}
+__device__ __forceinline__ f32x4 mp_load(const float* p, int debug) {
+  if (debug & 256) return *reinterpret_cast<const f32x4*>(p);
+  return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+}
+
 // The weight ring: kT32Ring k-groups of B fragments in flight per wave (one
 // dwordx4 per lane each), in named registers (an 8-deep ring, with segments
 // padded to 8, measured slower: 92.9 vs 87.9 us forward).
@@ -182,8 +197,9 @@ __device__ __forceinline__ void t32_layer(const float* src, int ldl, const f32x4
   }
   const float* A0 = src + c * ldl + 4 * g;
   const float* A1 = A0 + 16 * ldl;
-  for (int i = 0; i < s.q; ++i) {
-    const int col = 8 * i + w;
+  const int nu = s.q + (t32_has_extra(s, w) ? 1 : 0);
+  for (int i = 0; i < nu; ++i) {
+    const int col = i < s.q ? 8 * i + w : ncol - 8 + w;  // the extra unit: tower32_sched.h
     const f32x4 p0 = pre(col, 0), p1 = pre(col, 1);
     __builtin_amdgcn_sched_barrier(0);  // issue the epilogue operands before the chain
     f32x4 acc0 = (f32x4){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
@@ -284,12 +300,12 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
         o[t] = v > 0.f ? v : 0.f;
         dst[(16 * mb + 4 * g + t) * ldl + n] = o[t];
       }
-      *reinterpret_cast<f32x4*>(ly.xmpf + mp32(m0 / 16 + mb, NB, nbb) + lane * 4) = o;
+      mp_store(ly.xmpf + mp32(m0 / 16 + mb, NB, nbb) + lane * 4, o, a.debug);
     };
     t32_layer<XP>(src, ldl, wp, NB, KG, w, lane, part, pre, epi);
     if (stp && lane == 0) stp[1 + 2 * l] = __builtin_amdgcn_s_memtime();
     lds_barrier();
-    if (NB % 8) {
+    if (t32_sched(NB, KG).R) {
       t32_layer_rem(NB, KG, w, lane, part, pre, epi);
       lds_barrier();
     }
@@ -365,7 +381,7 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
       const int k = nb * 16 + cc;
       const float wk = k < NL ? a.w_out[k] : 0.f;
       const int64_t off = mp32(m0 / 16 + mb, NBL, nb) + l * 4;
-      const f32x4 x4 = *reinterpret_cast<const f32x4*>(lastl.xmpf + off);
+      const f32x4 x4 = mp_load(lastl.xmpf + off, a.debug);
       f32x4 o;
       float dbs = 0.f, dws = 0.f;
 #pragma unroll
@@ -378,7 +394,7 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
         dbs += d;
         dws += gr * x;
       }
-      *reinterpret_cast<f32x4*>(lastl.dzmpf + off) = o;
+      mp_store(lastl.dzmpf + off, o, a.debug);
       red[(mb * 4 + gg) * NpL + k] = dbs;
       red[8 * NpL + (mb * 4 + gg) * NpL + k] = dws;
     }
@@ -411,7 +427,7 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
       const TowerLayerDev& prev = a.ly[i - 1];
       const int PNB = prev.Np / 16;
       auto pre = [&](int kbb, int mb) {
-        return *reinterpret_cast<const f32x4*>(prev.xmpf + mp32(m0 / 16 + mb, PNB, kbb) + lane * 4);
+        return mp_load(prev.xmpf + mp32(m0 / 16 + mb, PNB, kbb) + lane * 4, a.debug);
       };
       auto epi = [&](const f32x4& acc, int kbb, int mb, const f32x4& x4) {
         const int64_t off = mp32(m0 / 16 + mb, PNB, kbb) + lane * 4;
@@ -423,14 +439,14 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
           s += o[t];
           dst[(16 * mb + 4 * g + t) * ldl + kbb * 16 + c] = o[t];
         }
-        *reinterpret_cast<f32x4*>(prev.dzmpf + off) = o;
+        mp_store(prev.dzmpf + off, o, a.debug);
         s += __shfl_xor(s, 16);
         s += __shfl_xor(s, 32);
         if (g == 0) cs[mb][kbb * 16 + c] = s;
       };
       t32_layer<XP>(src, ldl, wtp, KB, NG, w, lane, part, pre, epi);
       lds_barrier();
-      if (KB % 8) {
+      if (t32_sched(KB, NG).R) {
         t32_layer_rem(KB, NG, w, lane, part, pre, epi);
         lds_barrier();
       }
@@ -443,7 +459,7 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
       };
       t32_layer<XP>(src, ldl, wtp, KB, NG, w, lane, part, pre, epi);
       lds_barrier();
-      if (KB % 8) {
+      if (t32_sched(KB, NG).R) {
         t32_layer_rem(KB, NG, w, lane, part, pre, epi);
         lds_barrier();
       }
@@ -805,7 +821,7 @@ int tower32_lds_ld(int maxw) {
 // blocks past a multiple of 8 (fwd: Np / 16, bwd: Kp / 16)
 bool tower32_needs_part(const TowerArgs& a) {
   for (int l = 0; l < a.L; ++l)
-    if ((a.ly[l].Np / 16) % 8 || (a.ly[l].Kp / 16) % 8) return true;
+    if (t32_sched(a.ly[l].Np / 16, a.ly[l].Kp / 16).R || t32_sched(a.ly[l].Kp / 16, a.ly[l].Np / 16).R) return true;
   return false;
 }
 size_t tower32_lds_bytes_for(int lds_ld, bool part, int bias_floats) {
