@@ -41,8 +41,8 @@ namespace pbx {
 // ncol / 8 full units per wave.)
 // Measured (profiles/r5_t32_schedule_ab.txt): the high-priority waves then
 // finish first anyway and the low-priority ones still end ~53k cycles into
-// the layer -- no gain (0.356-0.358 ms/step vs 0.352-0.354 with the
-// remainder on waves 4-7 below), so it is off by default.
+// the layer -- no gain (0.356-0.358 ms/step vs 0.355-0.357 even), so it
+// is off by default.
 #ifndef PBX_T32_PRIO_SPLIT
 #define PBX_T32_PRIO_SPLIT 0
 #endif
@@ -66,13 +66,16 @@ T32_HD inline bool t32_has_extra(const T32Sched& s, int w) { return s.x && w >= 
 // segment padding granularity
 constexpr int kT32Ring = 4;
 T32_HD inline int t32_ceil4(int x) { return (x + kT32Ring - 1) / kT32Ring * kT32Ring; }
-// Which waves take the remainder K-ranges: with R <= 4 blocks and no extra
-// units, the four high-priority waves 4-7 only (a range of at most ng
-// k-groups still spans at most two blocks): 0.352-0.354 ms/step vs
-// 0.355-0.357 for all eight (profiles/r5_t32_schedule_ab.txt).
+// Which waves take the remainder K-ranges: all eight (default), or with
+// R <= 4 blocks and no extra units the four waves 4-7 / 0-3 only (a range
+// of at most ng k-groups still spans at most two blocks).  Waves 4-7 only
+// measured 0.352-0.354 ms/step vs 0.355-0.357 (profiles/
+// r5_t32_schedule_ab.txt) but made the pipelined-vs-plain equality tests
+// (tests/test_gpu_pipeline.py, 1e-6) fail intermittently -- a
+// timing-dependent difference not yet explained -- so it stays off.
 // PBX_T32_REM: 0 all eight waves, 1 waves 4-7, 2 waves 0-3.
 #ifndef PBX_T32_REM
-#define PBX_T32_REM 1
+#define PBX_T32_REM 0
 #endif
 // first flattened remainder pair of wave w (w = 8: T)
 T32_HD inline int t32_rem_lo(const T32Sched& s, int w) {
