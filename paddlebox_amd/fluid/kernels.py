@@ -465,7 +465,9 @@ def _pull_op_args(ctx, op):
     sp = SeqpoolParams(use_cvm=a["use_cvm"], cvm_offset=a["cvm_offset"], clk_filter=a["clk_filter"],
                        pad_value=a["pad_value"], need_filter=a["need_filter"], show_coeff=a["show_coeff"],
                        clk_coeff=a["clk_coeff"], threshold=a["threshold"], quant_ratio=a["quant_ratio"],
-                       embed_threshold_filter=a["embed_threshold_filter"], embed_threshold=a["embed_threshold"],
+                       # the op nests the embedding-norm filter under need_filter (fused_seqpool_cvm_op.cu:580-581)
+                       embed_threshold_filter=bool(a["need_filter"] and a["embed_threshold_filter"]),
+                       embed_threshold=a["embed_threshold"],
                        embed_thres_size=a["embed_thres_size"])
     dense = None
     if op.inputs.get("Dense"):

@@ -140,13 +140,14 @@ class _SeqpoolCvmVariant(torch.autograd.Function):
             seg = _seg_ids(off, L)
             show, clk = x[:, 0], x[:, 1] if E > 1 else x[:, 0]
             keep = torch.ones(L, dtype=torch.bool, device=x.device)
-            if a.get("need_filter"):
+            need_f, embed_f = _filters(variant, a)
+            if need_f:
                 thr = a["threshold"]
                 if variant == "diff_thres" and a.get("xbox_diff_thres_filter"):
                     thr = a["threshold_vec"][len(outs)]
                 keep &= (show - clk) * a["show_coeff"] + clk * a["clk_coeff"] >= thr
             co = a.get("cvm_offset", 2)
-            if a.get("embed_threshold_filter"):
+            if embed_f:
                 ets = a.get("embed_thres_size", 0)
                 ets = ets if ets > 0 else E - co  # 0 = the whole embedding (op.cu:596-599)
                 emb = x[:, co:co + ets]
@@ -204,6 +205,21 @@ class _SeqpoolCvmVariant(torch.autograd.Function):
                 g = full
             grads.append(g)
         return (None, None, None, None, None, None) + tuple(grads)
+
+
+def _filters(variant, a):
+    """(show/click filter, embedding-norm filter) as the reference applies
+    them in the pooling kernels:
+      * the embedding-norm filter only runs under need_filter
+        (fused_seqpool_cvm_op.cu:580-581 nests it);
+      * with embedx_concate_size > 1 a record is filtered only when
+        embedx_concate_filter is set (op.cu:215, 352); the conv variant never
+        filters in concat mode (fused_seqpool_cvm_with_conv_op.cu:345-383)."""
+    need = bool(a.get("need_filter"))
+    embed = need and bool(a.get("embed_threshold_filter")) if variant == "std" else False
+    if a.get("embedx_concate_size", 1) > 1 and not (variant == "std" and a.get("embedx_concate_filter")):
+        need = embed = False
+    return need, embed
 
 
 def _concat_pool(vals, off, B, ecs, pad):
@@ -413,7 +429,8 @@ class _SeqpoolCvmVariantHip(torch.autograd.Function):
         co = a.get("cvm_offset", 2)
         ecs = a.get("embedx_concate_size", 1)
         ets = a.get("embed_thres_size", 0)
-        ints = [int(bool(a.get("need_filter"))), int(bool(a.get("embed_threshold_filter"))),
+        need_f, embed_f = _filters(variant, a)
+        ints = [int(need_f), int(embed_f),
                 ets if ets > 0 else E - co, co, int(a.get("quant_ratio", 0)),
                 a.get("max_cvm_offset", co) if variant == "pcoc" else co,
                 int(variant == "tradew"), a.get("trade_num", 0) if variant == "tradew" else 0,
