@@ -15,9 +15,11 @@ Adam; the same run also times the bf16-MFMA tower and DCN-V2 (BASELINE config 5)
 as secondaries in ``config``.  The feature table is pre-populated with
 all 1e9 features (random-init weights, as if a base model was loaded) and
 sharded across GPUs by hash; keys are exchanged with all-to-all each step.
-Weak scaling: the per-GPU batch is fixed.  Each timed step = H2D of the batch
-(from pinned host memory) + pull + forward + backward + sparse push/Adagrad +
-dense all-reduce + Adam.
+Weak scaling: the per-GPU batch is fixed.  Each timed step = a device-to-device
+copy of the step's batch into the captured graph's inputs (the pass's
+synthetic batches are HBM-resident, ``--inputs hbm``, default; ``--inputs
+host`` copies it H2D from pinned host memory instead) + pull + forward +
+backward + sparse push/Adagrad + dense all-reduce + Adam.
 """
 from __future__ import annotations
 

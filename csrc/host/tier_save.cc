@@ -3,8 +3,9 @@
 // (csrc/common/ckpt_format.h), streamed so memory stays bounded whatever the
 // table size:
 //
-//   host tier  shards in groups (one per pool thread, each under its lock):
-//              selected rows copied out, delta_score reset in place
+//   host tier  shards in groups (one per pool thread, each under its lock,
+//              groups narrowed to ~4M selected rows): selected rows copied
+//              out and written shard by shard, delta_score reset in place
 //   SSD log    SsdLog::rewrite -- sequential segment runs; the reset is
 //              written back into the records' pages in place
 //   writer     batch model: raw .npy appends; xbox: T formatter threads
@@ -45,11 +46,16 @@ class PartWriter {
   std::vector<float> vals;
 
   void flush() {
-    const int64_t n = (int64_t)keys.size();
+    write_rows(keys.data(), vals.data(), (int64_t)keys.size());
+    keys.clear();
+    vals.clear();
+  }
+  // rows straight from the caller's buffers (no staging copy)
+  void write_rows(const uint64_t* keys, const float* vals, int64_t n) {
     if (n == 0) return;
     if (kind_ == 0) {
-      fk_->write(keys.data(), n * sizeof(uint64_t));
-      fv_->write(vals.data(), n * (size_t)stride_ * sizeof(float));
+      fk_->write(keys, n * sizeof(uint64_t));
+      fv_->write(vals, n * (size_t)stride_ * sizeof(float));
     } else {
       const int T = (int)std::min<int64_t>(threads_, std::max<int64_t>(1, n / 4096));
       std::vector<std::string> outs(T);
@@ -57,15 +63,12 @@ class PartWriter {
       for (int w = 0; w < T; ++w)
         ws.emplace_back([&, w]() {
           outs[w].reserve((size_t)(n / T + 1) * 160);
-          format_xbox_rows(keys.data(), vals.data(), n * w / T, n * (w + 1) / T, dim_, stride_, l_, sel_, ex_thr_,
-                           outs[w]);
+          format_xbox_rows(keys, vals, n * w / T, n * (w + 1) / T, dim_, stride_, l_, sel_, ex_thr_, outs[w]);
         });
       for (auto& t : ws) t.join();
       for (auto& o : outs) fk_->write(o.data(), o.size());
     }
     rows_ += n;
-    keys.clear();
-    vals.clear();
   }
   int64_t finish() {
     flush();
@@ -105,8 +108,13 @@ TierSaveStats save_tiers(HostTier* host, SsdLog* ssd, int kind, const SaveSelect
   constexpr size_t kFlushRows = 1 << 20;
   if (host) {
     // groups of shards, one shard per pool thread: each shard's rows land in
-    // its own list (no shared state in fn), appended in shard order
-    const int G = std::max(1, host->threads());
+    // its own list (no shared state in fn) and go to the writer straight from
+    // it, shard by shard.  Memory bound: the selected rows of one group; the
+    // group is narrowed so that it holds at most ~kGroupRows rows (the
+    // shards are hash-balanced: size / kNumShards rows each).
+    constexpr int64_t kGroupRows = 1 << 22;
+    const int64_t per_shard = std::max<int64_t>(1, host->size() / HostTier::kNumShards);
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(host->threads(), kGroupRows / per_shard));
     std::vector<std::vector<uint64_t>> gk(HostTier::kNumShards);
     std::vector<std::vector<float>> gv(HostTier::kNumShards);
     for (int s0 = 0; s0 < HostTier::kNumShards; s0 += G) {
@@ -118,16 +126,14 @@ TierSaveStats save_tiers(HostTier* host, SsdLog* ssd, int kind, const SaveSelect
         if (sel.reset_delta) v[l.delta_score] = 0.f;
       });
       for (int si = s0; si < s1; ++si) {
-        for (uint64_t h : gk[si]) {
-          out.keys.push_back(unmix64(h));
-          if (saved_mixed) saved_mixed->push_back(h);
-        }
-        out.vals.insert(out.vals.end(), gv[si].begin(), gv[si].end());
-        st.host_rows += (int64_t)gk[si].size();
-        std::vector<uint64_t>().swap(gk[si]);
+        auto& k = gk[si];
+        if (saved_mixed) saved_mixed->insert(saved_mixed->end(), k.begin(), k.end());
+        for (auto& h : k) h = unmix64(h);
+        out.write_rows(k.data(), gv[si].data(), (int64_t)k.size());
+        st.host_rows += (int64_t)k.size();
+        std::vector<uint64_t>().swap(k);
         std::vector<float>().swap(gv[si]);
       }
-      if (out.keys.size() >= kFlushRows) out.flush();
     }
   }
   if (ssd) {

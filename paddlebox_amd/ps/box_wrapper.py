@@ -19,6 +19,7 @@ Tiers:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
 import time
@@ -355,6 +356,11 @@ class BoxWrapper:
         """Host tier current: finish the background write-back and, inside a
         pass, write the live GPU rows back synchronously first."""
         if self.tier is not None:
+            # a next-pass staging still running moves SSD rows into the host
+            # tier (host insert, then SSD delete) without the caller holding
+            # the tier lock: a save / shrink walking the tiers meanwhile could
+            # miss such a row or see it twice
+            self.tier.wait_stage()
             self.tier.wait_writeback()  # also settles tier.retained
             if self.in_pass or self.tier.retained:
                 self.tier.flush()
@@ -362,25 +368,46 @@ class BoxWrapper:
             h, v = self.engine.table.export(True)
             self.host.assign(h.cpu(), v.cpu())
 
-    def _reset_delta_live(self, hk: torch.Tensor):
-        """save_xbox reset delta_score of the saved rows in the host tier; the
-        live GPU rows must see the reset too -- in a pass, or between passes
-        with the GPU tier (its activation carries live rows into the next
-        pass) -- or a later write-back would restore the old scores."""
-        if self.mode != "tiered" or self.engine is None or hk.numel() == 0:
-            return
-        if not self.in_pass and self.tier is None:
-            return
-        # the staged next pass gathered its host rows before this reset
-        tables = self.tier.staged_tables() if self.tier is not None else [self.engine.table]
-        for t in tables:
-            h = hk.to(t.device)
-            rows = t.probe(h)
+    def _live_tables(self):
+        """GPU tables holding live copies of tier rows: in a pass the live
+        table; between passes with the GPU tier also the staged next pass
+        (its activation carries live rows into the next pass)."""
+        if self.mode != "tiered" or self.engine is None:
+            return []
+        if self.tier is not None:
+            return self.tier.staged_tables()
+        return [self.engine.table] if self.in_pass else []
+
+    def _reset_delta_live(self, mode: str):
+        """save_xbox reset delta_score of the saved rows in the host / SSD
+        tiers; the live GPU rows must see the reset too, or a later write-back
+        would restore the old scores.  Decided on the GPU rows themselves (the
+        live ones were flushed into the host tier just before the save, so the
+        save rule gives the same answer on both; a staged row the live table
+        lacks is the host row) -- no per-saved-key list crosses host memory or
+        the bus, whatever the size of the host + SSD model."""
+        sg = self.cfg.sgd
+        dcol = row_layout(self.cfg.embedx_dim)["delta_score"]
+        for t in self._live_tables():
+            if t.size() == 0:
+                continue
+            h, v = t.export(True)
+            keep = ckpt.select_rows(h, v, self.cfg.embedx_dim, mode, self.cfg.save, sg.nonclk_coeff, sg.clk_coeff)
+            if bool(keep.any()):
+                vk = v[keep].clone()
+                vk[:, dcol] = 0
+                t.assign(h[keep], vk)
+
+    def _push_live(self, h: torch.Tensor, v: torch.Tensor):
+        """A tiered load / merge wrote rows into the host tier: GPU tables
+        holding live copies of those keys take the loaded rows too (else the
+        next activation or write-back brings the pre-load values back)."""
+        for t in self._live_tables():
+            hd = h.to(t.device)
+            rows = t.probe(hd)
             ok = rows >= 0
             if bool(ok.any()):
-                v = t.values[rows[ok]].clone()
-                v[:, row_layout(self.cfg.embedx_dim)["delta_score"]] = 0
-                t.t.assign(rows[ok], v)
+                t.assign(hd[ok], v.to(t.device)[ok])
 
     def save_base(self, batch_model_path: str, xbox_model_path: str, date: str = "") -> str:
         """Full batch model + xbox base (box_wrapper.cc:1286-1305)."""
@@ -388,7 +415,7 @@ class BoxWrapper:
         n = ckpt.save_batch_model(t, batch_model_path, self.rank, date, world=self.world)
         sg = self.cfg.sgd
         x = ckpt.save_xbox(t, xbox_model_path, "base", self.cfg.save, sg.nonclk_coeff, sg.clk_coeff, self.rank,
-                           on_reset=self._reset_delta_live)
+                           reset_live=self._reset_delta_live if self.mode == "tiered" else None)
         if self.rank == 0:
             ckpt.write_manifest(os.path.dirname(os.path.abspath(batch_model_path)) or ".", date=date,
                                 pass_id=self.pass_id, embedx_dim=self.cfg.embedx_dim, world=self.world,
@@ -400,7 +427,7 @@ class BoxWrapper:
         t = self._authoritative()
         sg = self.cfg.sgd
         x = ckpt.save_xbox(t, xbox_model_path, "delta", self.cfg.save, sg.nonclk_coeff, sg.clk_coeff, self.rank,
-                           on_reset=self._reset_delta_live)
+                           reset_live=self._reset_delta_live if self.mode == "tiered" else None)
         return f"{xbox_model_path} xbox_delta={x}"
 
     def load_model(self, model_path: str, merge: bool = False, update_type: str = "add", model_index: int = 0):
@@ -436,6 +463,8 @@ class BoxWrapper:
                 v = self._merge_rows(cur, v, found, update_type, int(model_index))
             t.insert_mixed(h, self.cfg.sgd)
             t.assign(h, v)
+            if self.mode == "tiered":
+                self._push_live(h, v)
             return int(h.numel())
 
         def mixed(keys: np.ndarray) -> torch.Tensor:
@@ -529,20 +558,42 @@ class BoxWrapper:
                        for j, p in enumerate(path))
         return self.load_model(path, merge=True, update_type=str(update_type), model_index=int(model_index))
 
-    def load_ssd2mem(self, date: Optional[str] = None):
-        """Preload SSD rows into host memory (LoadSSD2Mem)."""
+    # rows per load_ssd2mem chunk: one chunk's keys + values are in host RAM at a time
+    SSD2MEM_CHUNK_ROWS = 1 << 20
+
+    def load_ssd2mem(self, date: Optional[str] = None, max_rows: Optional[int] = None) -> int:
+        """LoadSSD2Mem (box_wrapper.cc:1320-1324): move SSD rows into the host
+        tier, streamed in chunks of ``SSD2MEM_CHUNK_ROWS`` and bounded by the
+        host-tier row cap (``cfg.tier.ssd_spill_threshold``; ``max_rows`` caps
+        it further): rows that would not fit stay on SSD, so the next
+        write-back does not spill them straight back.  Returns the rows moved."""
         if self.ssd is None or self.host is None:
             return 0
-        if self.tier is not None:
-            self.tier.wait_writeback()
-        h = self.ssd.keys()
-        if h.numel() == 0:
+        self._sync_tiers()
+        cap = int(self.cfg.tier.ssd_spill_threshold)
+        room = max(0, cap - self.host.size()) if cap > 0 else len(self.ssd)
+        if max_rows is not None:
+            room = min(room, int(max_rows))
+        if room == 0 or len(self.ssd) == 0:
             return 0
-        found, vals = self.ssd.get(h)
-        self.host.insert_mixed(h[found], self.cfg.sgd)
-        self.host.assign(h[found], vals[found])
-        self.ssd.delete(h[found])
-        return int(found.sum())
+        lock = self.tier._tier_lock if self.tier is not None else contextlib.nullcontext()
+        moved = 0
+        with lock:
+            h_all = self.ssd.keys()
+            step = max(1, int(self.SSD2MEM_CHUNK_ROWS))
+            for a in range(0, min(int(h_all.numel()), room), step):
+                h = h_all[a:min(a + step, room)]
+                found, vals = self.ssd.get(h)
+                hk = h[found]
+                if hk.numel() == 0:
+                    continue
+                rows, _ = self.host._native.insert(hk)
+                self.host._native.scatter(rows, vals[found])
+                if self.tier is not None:
+                    self.host._native.stamp(rows, self.tier.epoch)
+                self.ssd.delete(hk)
+                moved += int(hk.numel())
+        return moved
 
     def shrink_table(self) -> int:
         """ShrinkTable (box_wrapper.h:638): decay show/click, age, delete

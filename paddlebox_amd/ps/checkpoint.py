@@ -231,11 +231,12 @@ def iter_part_chunks(path: str, part: int, chunk_rows: int):
 
 
 def save_xbox(table, path: str, mode: str, cfg: SaveConfig, nonclk: float, clk: float, rank: int = 0,
-              on_reset=None) -> int:
+              on_reset=None, reset_live=None) -> int:
     """Write the xbox text model ('base' or 'delta'); resets delta_score of
     the saved rows (ctr_accessor.cc:121-124,153-162).  ``on_reset(h)`` is
     called with the saved mixed keys (another tier holding live copies of
-    the rows applies the same reset)."""
+    the rows applies the same reset); for the tiers ``reset_live(mode)``
+    instead re-applies the save rule to the live copies (no key list)."""
     os.makedirs(path, exist_ok=True)
     # rows are canonical: a codec table's embedding block is embedx + expand
     codec = getattr(table, "codec", None)
@@ -244,10 +245,12 @@ def save_xbox(table, path: str, mode: str, cfg: SaveConfig, nonclk: float, clk: 
     fn = os.path.join(path, f"part-{rank:05d}.txt")
     if _tiered(table):
         n, saved = table.save_tiers(1, 1 if mode == "base" else 2, True, cfg, nonclk, clk, fn,
-                                    collect=on_reset is not None)
+                                    collect=on_reset is not None and reset_live is None)
         last_save_stats.clear()
         last_save_stats.update(table.last_save)
-        if on_reset is not None and saved is not None and saved.numel():
+        if reset_live is not None:
+            reset_live(mode)
+        elif on_reset is not None and saved is not None and saved.numel():
             on_reset(saved)
         return n
     if _streamable(table):

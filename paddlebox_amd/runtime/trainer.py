@@ -505,8 +505,29 @@ class BoxPSWorker:
             metrics((ctx, bt))
             invalidate_others(None)
 
+        def drain(c):
+            # everything of size c still pending, in plan order: its filled
+            # buffer sets, then the batches short of a whole graph and the
+            # warm-up batches (eagerly) -- before a batch of another size runs,
+            # so the pass trains in the plan's order (sparse and Adam updates
+            # are order-dependent)
+            st = state.get(c)
+            if c in graphs and st is not None:
+                while st[1] < st[0]:
+                    run_one(c)
+            for b0 in queue.pop(c, []):
+                db = dev_buf(c)
+                dp.assemble_sync(b0, c, db.keys, db.lod, db.dense)
+                eager(db, c)
+            for db in warm.pop(c, []):
+                eager(db, c)
+
+        last_c = None
         for (b0, c) in plan:
             t_s = time.time()
+            if last_c is not None and c != last_c:
+                drain(last_c)
+            last_c = c
             if c in graphs:
                 q = queue.setdefault(c, [])
                 q.append(b0)

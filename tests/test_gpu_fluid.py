@@ -23,7 +23,7 @@ def _box():
 
 
 def _run(tmp_path, graph: bool, passes: int = 3, device_pass: bool = True, transpile: bool = False,
-         steps_per_graph: int = 0, pipelined: bool = True):
+         steps_per_graph: int = 0, pipelined: bool = True, n_per_file: int = 320):
     tmp_path.mkdir(parents=True, exist_ok=True)
     set_flags({"FLAGS_padbox_device_pass": device_pass, "FLAGS_padbox_train_steps_per_graph": steps_per_graph,
                "FLAGS_padbox_pipelined_front": pipelined})
@@ -39,7 +39,7 @@ def _run(tmp_path, graph: bool, passes: int = 3, device_pass: bool = True, trans
         ds = fluid.DatasetFactory().create_dataset("PadBoxSlotDataset")
         ds.set_use_var([label] + slots + [dense])
         ds.set_batch_size(64)
-        ds.set_filelist(_files(tmp_path, 2, 320))
+        ds.set_filelist(_files(tmp_path, 2, n_per_file))
         ds.disable_shuffle()
         box.init_metric("AucCalculator", "auc", label.name, pred.name, bucket_size=1000)
         boxps = fluid.core.BoxPS(ds)
@@ -104,6 +104,22 @@ def test_graphed_loop_is_bench_step(tmp_path):
     torch.testing.assert_close(fast["table"][:, keep], plain["table"][:, keep], rtol=1e-4, atol=1e-5)
     for k in fast["dn"]:
         np.testing.assert_allclose(fast["dn"][k], plain["dn"][k], rtol=1e-4, atol=1e-4)
+
+
+def test_graphed_loop_mixed_batch_sizes_keeps_order(tmp_path):
+    """a pass whose plan mixes batch sizes (1204 records in 19
+    batches: 7 of 64, then 12 of 63) trains in plan order under K = 4 steps
+    per graph with the pipelined front -- the batches short of a whole graph
+    and the filled sets of one size run before the first batch of the next
+    size -- so it matches the eager loop."""
+    eager = _run(tmp_path / "e", graph=False, n_per_file=602)
+    fast = _run(tmp_path / "f", graph=True, n_per_file=602)
+    st = fast["stats"][-1]
+    assert st["batches"] == 19 and st["steps_per_graph"] == 4 and st.get("graph_replays", 0) > 0
+    assert fast["n"] == eager["n"] == 3 * 1204
+    np.testing.assert_allclose(fast["w1"], eager["w1"], rtol=0, atol=1e-4)
+    keep = [c for c in range(eager["table"].shape[1]) if c != 14]
+    torch.testing.assert_close(fast["table"][:, keep], eager["table"][:, keep], rtol=1e-4, atol=1e-5)
 
 
 def test_fc_precision_fp32_matches_cpu_oracle(tmp_path):

@@ -246,3 +246,92 @@ def test_tiered_save_between_passes_with_retained_rows(tmp_path):
         torch.testing.assert_close(got[:, keep], exp[:, keep], rtol=1e-5, atol=1e-6)
     finally:
         BoxWrapper._instance = None
+
+
+def test_tiered_save_and_shrink_right_after_staging(tmp_path):
+    """a next-pass staging moves SSD rows into the host tier
+    in the background.  A SaveBase / ShrinkTable issued right after the feed
+    pass that started it must see every key exactly once and the same values
+    as the all-in-HBM oracle."""
+    import numpy as np
+
+    try:
+        ob = _box("hbm", 100000)
+        h = _train(ob, overlap=False)
+        exp = ob.engine.table.read(h.to(DEV)).cpu()
+    finally:
+        BoxWrapper._instance = None
+    try:
+        tb = _box("tiered", 2400, ssd=str(tmp_path / "ssd"))
+        _train(tb, overlap=True)
+        tb.tier.wait_writeback()
+        ssd_keys = tb.ssd.keys()
+        assert ssd_keys.numel() > 0
+        slot = tb.host.layout["slot"]
+        keep = [c for c in range(exp.shape[1]) if c != slot]
+        # stage keys that live on SSD, then save at once
+        tb.feed_pass(ref.unmix64(ssd_keys[:2000].clone()))
+        tb.save_base(str(tmp_path / "t_batch"), str(tmp_path / "t_xbox"))
+        tk = np.load(str(tmp_path / "t_batch" / "part-00000.keys.npy"), allow_pickle=False)
+        tv = np.load(str(tmp_path / "t_batch" / "part-00000.vals.npy"), allow_pickle=False)
+        assert tk.shape[0] == h.numel() and np.unique(tk).shape[0] == tk.shape[0]
+        mk = ref.mix64(torch.from_numpy(tk.view(np.int64).copy()))
+        order = torch.argsort(mk)
+        hs = torch.sort(h).values
+        assert torch.equal(mk[order], hs)
+        eo = exp[torch.argsort(h)]
+        torch.testing.assert_close(torch.from_numpy(tv)[order][:, keep], eo[:, keep], rtol=1e-5, atol=1e-6)
+        # and a shrink right after another staging: same deletions as the oracle
+        tb.feed_pass(ref.unmix64(ssd_keys[2000:4000].clone()))
+        for b in (tb, ob):
+            b.cfg.shrink.delete_threshold = 0.5
+        assert tb.shrink_table() == ob.shrink_table() > 0
+        th, _ = tb._authoritative().export(False)
+        oh, _ = ob.engine.table.export(False)
+        assert th.numel() == torch.unique(th).numel()
+        assert torch.equal(torch.sort(th).values, torch.sort(oh.cpu()).values)
+    finally:
+        BoxWrapper._instance = None
+
+
+def test_tiered_load_reaches_live_rows(tmp_path):
+    """a load between passes (next pass staged, rows
+    retained on the GPU) and a load inside a pass must not be undone by the
+    activation or the next write-back: the loaded rows are what the tiers
+    hold at the end."""
+    try:
+        ob = _box("hbm", 100000)
+        h = _train(ob, overlap=False)
+        ob.save_base(str(tmp_path / "m_batch"), str(tmp_path / "m_xbox"))
+        exp = ob.engine.table.read(h.to(DEV)).cpu()
+    finally:
+        BoxWrapper._instance = None
+
+    def check(box):
+        got = _tier_rows(box, h)
+        slot = box.host.layout["slot"]
+        keep = [c for c in range(exp.shape[1]) if c != slot]
+        torch.testing.assert_close(got[:, keep], exp[:, keep], rtol=1e-5, atol=1e-6)
+
+    for inside in (False, True):
+        try:
+            tb = _box("tiered", 2400, ssd=str(tmp_path / f"ssd{int(inside)}"))
+            tb.cfg.sgd.learning_rate = 0.05  # a different model than the saved one
+            k0 = torch.cat([b.keys for b in _pass_batches(0)])
+            tb.feed_pass(k0)
+            tb.begin_pass()
+            if inside:
+                tb.load_model(str(tmp_path / "m_batch"))  # live rows of pass 0 take the loaded values
+                tb.end_pass()
+            else:
+                tb.end_pass()
+                tb.feed_pass(k0)  # staged: pass 0's rows are retained on the GPU
+                tb.tier.wait_writeback()
+                tb.load_model(str(tmp_path / "m_batch"))
+                tb.begin_pass()  # activation carries the live rows on
+                tb.end_pass()
+            tb.tier.wait_writeback()
+            tb.tier.flush()
+            check(tb)
+        finally:
+            BoxWrapper._instance = None

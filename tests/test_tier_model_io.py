@@ -233,3 +233,31 @@ def test_host_insert_stamps_current_epoch():
     rc, fresh = t._native.insert_fresh(torch.cat([c, a[10:12]]))
     assert fresh.tolist() == [True] * 10 + [False] * 2
     assert bool((t._native.epochs(rc[:10]) == 5).all())
+
+
+def test_load_ssd2mem_streams_within_host_cap(tmp_path):
+    """LoadSSD2Mem moves SSD rows into the host tier in
+    bounded chunks and never past the host-tier row cap; the rows it moves
+    keep their values and leave the SSD (one tier per key)."""
+    box = _box("tiered", tmp_path, cap=120)
+    try:
+        for p, b in enumerate(_batches()):
+            _run_pass(box, b, p)
+        total = box.host.size() + len(box.ssd)
+        assert len(box.ssd) > 100
+        before_h, before_v = _rows(box._authoritative())
+        box.SSD2MEM_CHUNK_ROWS = 7  # many chunks
+        box.cfg.tier.ssd_spill_threshold = box.host.size() + 50
+        moved = box.load_ssd2mem()
+        assert moved == 50 and box.host.size() == box.cfg.tier.ssd_spill_threshold
+        assert box.host.size() + len(box.ssd) == total
+        assert box.load_ssd2mem() == 0  # host tier at its cap
+        box.cfg.tier.ssd_spill_threshold = 0  # no cap: everything
+        rest = len(box.ssd)
+        assert box.load_ssd2mem() == rest
+        assert len(box.ssd) == 0 and box.host.size() == total
+        after_h, after_v = _rows(box._authoritative())
+        assert torch.equal(before_h, after_h)
+        torch.testing.assert_close(after_v, before_v)
+    finally:
+        BoxWrapper._instance = None
