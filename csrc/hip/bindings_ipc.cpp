@@ -48,6 +48,44 @@ int64_t ipc_open(const py::bytes& hb, int64_t off) {
 
 void ipc_close(int64_t base) { hip_ok(hipIpcCloseMemHandle(reinterpret_cast<void*>(base)), "hipIpcCloseMemHandle"); }
 
+// Mesh memory that peers write while a kernel of this GPU spins on it:
+// hipExtMallocWithFlags(hipDeviceMallocUncached) -- no L2 / MALL caching of
+// the lines on any agent, so a peer's xGMI store is visible to a running
+// kernel's (system-scope acquire) loads, which HIP guarantees for
+// coarse-grained hipMalloc memory only at dispatch / sync boundaries.
+// hipDeviceMallocFinegrained (coherent, cacheable) is the other legal choice.
+// Zero-filled; freed when the returned tensor dies.
+Tensor ipc_buffer(int64_t nbytes, int64_t device, bool uncached) {
+  IPC_CHECK(nbytes > 0, "ipc_buffer: size");
+  int cur = 0;
+  hip_ok(hipGetDevice(&cur), "hipGetDevice");
+  hip_ok(hipSetDevice((int)device), "hipSetDevice");
+  void* p = nullptr;
+  const hipError_t e = hipExtMallocWithFlags(&p, (size_t)nbytes,
+                                             uncached ? hipDeviceMallocUncached : hipDeviceMallocFinegrained);
+  if (e == hipSuccess) {
+    const hipError_t z = hipMemset(p, 0, (size_t)nbytes);
+    if (z != hipSuccess) {
+      (void)hipFree(p);
+      (void)hipSetDevice(cur);
+      hip_ok(z, "hipMemset");
+    }
+  }
+  (void)hipSetDevice(cur);
+  hip_ok(e, "hipExtMallocWithFlags");
+  auto opts = torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, (int)device);
+  return torch::from_blob(p, {nbytes}, [](void* q) { (void)hipFree(q); }, opts);
+}
+
+// (memory type, device, allocation flags) of a device pointer: the mesh test
+// asserts its buffers are the uncached kind
+py::tuple ptr_attrs(int64_t ptr) {
+  hipPointerAttribute_t a;
+  std::memset(&a, 0, sizeof(a));
+  hip_ok(hipPointerGetAttributes(&a, reinterpret_cast<void*>(ptr)), "hipPointerGetAttributes");
+  return py::make_tuple((int)a.type, a.device, (int64_t)a.allocationFlags);
+}
+
 class IpcComm {
  public:
   // state: own int64 [4] = epoch, arrive|depart (2 x u32), err, pad
@@ -78,6 +116,12 @@ class IpcComm {
     p_.inbox[p] = reinterpret_cast<unsigned char*>(inbox);
     p_.flags[p] = reinterpret_cast<uint64_t*>(flags);
   }
+  // bound of every later wait (polls of ~55 ns each)
+  void set_spin_limit(int64_t v) {
+    IPC_CHECK(v > 0, "spin_limit");
+    p_.spin_limit = v;
+  }
+  int64_t spin_limit() const { return p_.spin_limit; }
   void check_ready() const {
     for (int p = 0; p < p_.world; ++p) IPC_CHECK(p_.inbox[p] && p_.flags[p], "peer pointers not set");
   }
@@ -144,7 +188,13 @@ void bind_ipc(py::module& m) {
   m.def("ipc_handle", &ipc_handle);
   m.def("ipc_open", &ipc_open);
   m.def("ipc_close", &ipc_close);
+  m.def("ipc_buffer", &ipc_buffer, py::arg("nbytes"), py::arg("device"), py::arg("uncached") = true);
+  m.def("ptr_attrs", &ptr_attrs);
+  m.attr("kIpcMallocUncached") = (int)hipDeviceMallocUncached;
+  m.attr("kIpcMallocFinegrained") = (int)hipDeviceMallocFinegrained;
   py::class_<IpcComm>(m, "IpcComm")
+      .def("set_spin_limit", &IpcComm::set_spin_limit)
+      .def("spin_limit", &IpcComm::spin_limit)
       .def(py::init<int, int, int64_t, const Tensor&, int, int, int64_t>(), py::arg("rank"), py::arg("world"),
            py::arg("slot_bytes"), py::arg("state"), py::arg("blocks"), py::arg("depth"), py::arg("spin_limit"))
       .def("set_peer", &IpcComm::set_peer)

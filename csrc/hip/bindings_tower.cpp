@@ -121,6 +121,14 @@ class TowerWorkspace {
     loss_ = torch::zeros({1}, of);
     part_ = torch::zeros({nwg * 8}, of);
     ticket_ = torch::zeros({1}, oi);
+    if (fp32 && splits_ > 1) {
+      // split-M dW slabs + per-tile arrival counters (tower32.hip t32_dw_combine)
+      int64_t tiles = 0;
+      for (int l = 0; l < L_; ++l)
+        tiles += ((pad(dims[l + 1], 16) / 16 + 3) / 4) * ((pad(dims[l], 16) / 16 + 3) / 4);
+      dw_slab_ = torch::empty({tiles * splits_ * 4096}, of);
+      dw_cnt_ = torch::zeros({tiles}, oi);
+    }
   }
 
   // fp32 master weights W_l [N_l][K_l] -> packed bf16 copies (one launch)
@@ -294,6 +302,10 @@ class TowerWorkspace {
     a.dwout_off = dwout_off_;
     a.dbout_off = dbout_off_;
     a.dw_splits = (int)splits_;
+    if (dw_slab_.defined()) {
+      a.dw_slab = P<float>(dw_slab_);
+      a.dw_cnt = P<int>(dw_cnt_);
+    }
     static const int dbg = [] {
       const char* e = getenv("PBX_TOWER_DEBUG");
       return e ? atoi(e) : 0;
@@ -309,7 +321,7 @@ class TowerWorkspace {
   int64_t wpad_ = 32;
   int L_ = 0, lds_ld_ = 0, bias_ld_ = 0, dwout_off_ = 0, dbout_off_ = 0;
   std::vector<int64_t> boff_;
-  Tensor x0_, x0mp_, dx0_, bias_part_, pred_, dz_, loss_, part_, ticket_, stamps_;
+  Tensor x0_, x0mp_, dx0_, bias_part_, pred_, dz_, loss_, part_, ticket_, stamps_, dw_slab_, dw_cnt_;
   std::vector<Tensor> wp_, wtp_, xmp_, dzmp_;
   std::vector<Tensor> pos_, posT_;  // fp32: wave-stream group position per (column block, k-group), W and W^T
 };

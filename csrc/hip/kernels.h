@@ -667,6 +667,11 @@ struct TowerArgs {
   float dn_eps = 0.f;
   float* dn_stats = nullptr;
   int dw_splits = 2;
+  // fp32 dW split-M partials, reduced in split order (no float atomics: the
+  // update is bit-reproducible): slab [tiles][dw_splits][64 x 64] and one
+  // arrival counter per 64x64 output tile (zero between launches)
+  float* dw_slab = nullptr;
+  int* dw_cnt = nullptr;
   int debug = 0;  // timing experiments only (PBX_TOWER_DEBUG): 1 no loss reduction, 2 no dW reductions, 4 no dW GEMM,
                   // 8 no fwd m-packed stores, 16 no output layer / loss, 32 fp32 tower: no s_setprio on waves 4-7,
                   // 64 fp32 fwd/bwd: no weight loads in the k-loop, 256 fp32 fwd/bwd: plain (not

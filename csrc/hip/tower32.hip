@@ -13,8 +13,11 @@
 //              activations, per-tile column sums for the bias gradients.
 //   k_t32_dw   dW = dZ^T X as one grouped GEMM over 64x64 output tiles, both
 //              operands streamed HBM/L2 -> LDS by global_load_lds (1 KB per
-//              wave instruction), M split over workgroups with fp32 atomics;
-//              extra workgroups reduce bias partials and data_norm statistics.
+//              wave instruction), M split over workgroups; each split stores
+//              its partial tile (a slab), the last arriving split of a tile
+//              sums the slabs in split order (deterministic, no fp32
+//              atomics); extra workgroups reduce bias partials and data_norm
+//              statistics.
 //
 // Why 16x16x4 and not 32x32x2: the f32 MFMA rate is 64 FLOP/clk/SIMD either
 // way; 16-wide blocks pad a 400-unit layer to 400 (not 416) and split a layer
@@ -509,6 +512,90 @@ __device__ __forceinline__ void wait_stages(int ahead) {
   }
 }
 
+// Split-M combine of one 64x64 dW tile (256 threads, wave w owns the 16x16
+// blocks part[w][i][j], i, j < 2, as 16x16x4 accumulators: lane (c, g),
+// register q = element [16 i' + 4g + q][16 j' + c]).  S = 1: the tile is
+// added to dW directly.  Otherwise every split writes its partial to its slab
+// (plain 16-B stores, 1 KB per wave instruction), publishes it with one
+// agent-scope release and an arrival on the tile's counter; the split that
+// arrives last acquires, sums the S slabs in split order 0..S-1 (the result
+// does not depend on which split finished last, or where it ran) and adds the
+// sum to dW -- one writer per element, so dW keeps its accumulate (+=)
+// contract and the update is bit-reproducible.  flag: one LDS int.
+// (MI355X_MICROARCH.md / cdna_hip_programming.md: the counter form of the
+// split-K hand-off, release before the ticket, acquire in the reducer.)
+__device__ __forceinline__ void t32_dw_combine(const TowerArgs& a, const TowerLayerDev& ly, int tile_g, int split,
+                                               int tn, int tk, int w, int lane, bool active, const f32x4 (&acc)[2][2],
+                                               int* flag) {
+  const int S = a.dw_splits;
+  const int NBn = ly.Np / 16, NBk = ly.Kp / 16;
+  const int wn = w & 1, wk = w >> 1;
+  const int c = lane & 15, g = lane >> 4;
+  auto add_out = [&](int i, int j, const f32x4& v) {
+    const int nb = tn * 4 + 2 * wn + i, kb = tk * 4 + 2 * wk + j;
+    const int k = kb * 16 + c;
+    if (nb >= NBn || kb >= NBk || k >= ly.K) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = nb * 16 + 4 * g + q;
+      if (n < ly.N) ly.dw[(int64_t)n * ly.K + k] += v[q];
+    }
+  };
+  if (S == 1) {
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) add_out(i, j, acc[i][j]);
+    }
+    return;
+  }
+  float* tile_slab = a.dw_slab + (int64_t)tile_g * S * 4096;
+  // slab layout: [split][wave][i][j][lane][4] (inactive waves write zeros:
+  // every slab is whole, the reducer reads them unconditionally)
+  {
+    f32x4* my = reinterpret_cast<f32x4*>(tile_slab + (int64_t)split * 4096) + w * 4 * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) my[(i * 2 + j) * 64] = active ? acc[i][j] : (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(&a.dw_cnt[tile_g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == S - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // the next launch starts from zero (a dispatch boundary orders it)
+      __hip_atomic_store(&a.dw_cnt[tile_g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag || !active) return;
+  f32x4 sum[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) sum[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const f32x4* base = reinterpret_cast<const f32x4*>(tile_slab) + w * 4 * 64 + lane;
+  for (int sp = 0; sp < S; ++sp) {
+    const f32x4* src = base + (int64_t)sp * 1024;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) sum[i][j] += src[(i * 2 + j) * 64];
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) add_out(i, j, sum[i][j]);
+}
+
 template <int DS, int NS>
 __global__ __launch_bounds__(256) void k_t32_dw(TowerArgs a, int ndw) {
   static_assert(NS >= 3 && NS - 2 <= 4, "wait_stages covers up to 4 stages ahead");
@@ -533,6 +620,7 @@ __global__ __launch_bounds__(256) void k_t32_dw(TowerArgs a, int ndw) {
     t = wid / S;
     split = wid % S;
   }
+  const int tile_g = t;  // tile index over all layers (slab / counter)
   int l = 0;
   for (; l < a.L; ++l) {
     const int nt = dw32_tiles(a.ly[l]);
@@ -598,169 +686,9 @@ __global__ __launch_bounds__(256) void k_t32_dw(TowerArgs a, int ndw) {
       }
     }
   }
-  if (!active) return;
-  // epilogue: lane (c, g) register q -> dW[16 nb + 4g + q][16 kb + c]
-  const int c = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int nb = tn * 4 + 2 * wn + i;
-    if (nb >= NBn) continue;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kb = tk * 4 + 2 * wk + j;
-      const int k = kb * 16 + c;
-      if (kb >= NBk || k >= ly.K) continue;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n = nb * 16 + 4 * g + q;
-        if (n < ly.N) atomicAdd(&ly.dw[(int64_t)n * ly.K + k], acc[i][j][q]);
-      }
-    }
-  }
-}
-
-// Register-streamed dW (PBX_T32_DW_RING=0; measured slower than the LDS ring,
-// kept for the A/B): each wave owns the whole 64x64 tile for every 4th m16
-// step of its split (K split inside the workgroup), so its operands go
-// L2 -> VGPRs with global_load_dwordx4 -- a chunk's fragment order IS the
-// MFMA operand order -- in a ring of R steps: no LDS staging and no barrier
-// in the loop, and R-1 steps (8 loads each) in flight per wave.  The four
-// partial tiles meet in LDS at the end; one fp32 atomic per output element
-// and workgroup, as in k_t32_dw.
-// one wave's K loop of k_t32_dw_reg over a tile with VN x VK valid 16-blocks
-// (only valid chunks are loaded and multiplied: fixed load count per step)
-// NST > 0: the step count is NST and the loop is unrolled completely -- a
-// loop header merges the load-ordering state of its two edges and hipcc then
-// waits for all but the newest step there (1 step in flight per R)
-template <int R, int VN, int VK, int NST>
-__device__ __forceinline__ void dw_reg_loop(const float* const* pa, const float* const* pb, int64_t sA, int64_t sB,
-                                            int nsteps_rt, f32x4 (&acc)[4][4]) {
-  const int nsteps = NST > 0 ? NST : nsteps_rt;
-  f32x4 ring[R][VN + VK];
-  auto load = [&](f32x4* slot, int st) {
-    const int64_t oa = (int64_t)st * 4 * sA, ob = (int64_t)st * 4 * sB;
-#pragma unroll
-    for (int i = 0; i < VN; ++i) slot[i] = *reinterpret_cast<const f32x4*>(pa[i] + oa);
-#pragma unroll
-    for (int j = 0; j < VK; ++j) slot[VN + j] = *reinterpret_cast<const f32x4*>(pb[j] + ob);
-  };
-#pragma unroll
-  for (int p = 0; p < R - 1; ++p) load(ring[p], p);
-#pragma unroll NST > 0 ? NST / R : 1
-  for (int s0 = 0; s0 < nsteps; s0 += R) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      // the step R-1 ahead (the tail re-reads the last step: no branch around loads)
-      load(ring[(r + R - 1) % R], min(s0 + r + R - 1, nsteps - 1));
-      // pin the ring: the loads stay R-1 steps ahead of their MFMAs
-      __builtin_amdgcn_sched_barrier(0);
-      const f32x4* c = ring[r];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int i = 0; i < VN; ++i)
-#pragma unroll
-          for (int j = 0; j < VK; ++j) acc[i][j] = mfma4(c[i][q], c[VN + j][q], acc[i][j]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-}
-
-template <int R>
-__global__ __launch_bounds__(256, 2) void k_t32_dw_reg(TowerArgs a, int ndw) {
-  const int tid = threadIdx.x;
-  if ((int)blockIdx.x >= ndw) {
-    tower_col_reduce(a, (int)blockIdx.x - ndw, BM);
-    return;
-  }
-  __shared__ f32x4 red[4][16][64];  // 64 KB: the waves' partial tiles
-  const int S = a.dw_splits;
-  int t, split;
-  if (S == 8) {
-    split = (int)blockIdx.x & 7;  // one M split per XCD (see k_t32_dw)
-    t = (int)blockIdx.x >> 3;
-  } else {
-    const int wid = xcd_work_id((int)blockIdx.x, ndw);
-    t = wid / S;
-    split = wid % S;
-  }
-  int l = 0;
-  for (; l < a.L; ++l) {
-    const int nt = dw32_tiles(a.ly[l]);
-    if (t < nt) break;
-    t -= nt;
-  }
-  const TowerLayerDev& ly = a.ly[l];
-  const int NBn = ly.Np / 16, NBk = ly.Kp / 16;
-  const int tk_n = (NBk + 3) / 4;
-  const int tn = t / tk_n, tk = t % tk_n;
-  const int vn = min(4, NBn - tn * 4), vk = min(4, NBk - tk * 4);  // valid 16-blocks of the tile
-  const float* Amp = ly.dzmpf;
-  const float* Bmp = l == 0 ? a.x0mpf : a.ly[l - 1].xmpf;
-  const int lane = tid & 63, w = tid >> 6;
-  const int64_t sA = (int64_t)NBn * 256, sB = (int64_t)NBk * 256;
-  // chunk pointers of this wave's first step (invalid blocks re-read the last valid one: uniform load counts)
-  const int per = a.Mp / 16 / S;
-  const int64_t m0 = (int64_t)split * per + w;
-  const float* pa[4];
-  const float* pb[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    pa[i] = Amp + m0 * sA + (int64_t)min(tn * 4 + i, NBn - 1) * 256 + lane * 4;
-    pb[i] = Bmp + m0 * sB + (int64_t)min(tk * 4 + i, NBk - 1) * 256 + lane * 4;
-  }
-  const int nsteps = per / 4;  // multiple of R (host check)
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  // the valid block counts select a branch-free loop (branches between the
-  // MFMAs make hipcc wait for every older load, not just the oldest step's)
-#define PBX_DW_REG(VN, VK)                                                   \
-  if (nsteps == 16) dw_reg_loop<R, VN, VK, 16>(pa, pb, sA, sB, nsteps, acc); \
-  else dw_reg_loop<R, VN, VK, 0>(pa, pb, sA, sB, nsteps, acc)
-  switch (vn * 4 + vk) {
-    case 5: PBX_DW_REG(1, 1); break;
-    case 6: PBX_DW_REG(1, 2); break;
-    case 7: PBX_DW_REG(1, 3); break;
-    case 8: PBX_DW_REG(1, 4); break;
-    case 9: PBX_DW_REG(2, 1); break;
-    case 10: PBX_DW_REG(2, 2); break;
-    case 11: PBX_DW_REG(2, 3); break;
-    case 12: PBX_DW_REG(2, 4); break;
-    case 13: PBX_DW_REG(3, 1); break;
-    case 14: PBX_DW_REG(3, 2); break;
-    case 15: PBX_DW_REG(3, 3); break;
-    case 16: PBX_DW_REG(3, 4); break;
-    case 17: PBX_DW_REG(4, 1); break;
-    case 18: PBX_DW_REG(4, 2); break;
-    case 19: PBX_DW_REG(4, 3); break;
-    default: PBX_DW_REG(4, 4); break;
-  }
-#undef PBX_DW_REG
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) red[w][i * 4 + j][lane] = acc[i][j];
+  // the ring's LDS is free: its first word carries the reducer flag
   __syncthreads();
-  // wave w sums row-block i = w of the four partials: lane (c, g) register q -> dW[16 nb + 4g + q][16 kb + c]
-  if (w >= vn) return;
-  const int c = lane & 15, g = lane >> 4;
-  const int nb = tn * 4 + w;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (j >= vk) continue;
-    const int k = (tk * 4 + j) * 16 + c;
-    const f32x4 v = red[0][w * 4 + j][lane] + red[1][w * 4 + j][lane] + red[2][w * 4 + j][lane] +
-                    red[3][w * 4 + j][lane];
-    if (k >= ly.K) continue;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int n = nb * 16 + 4 * g + q;
-      if (n < ly.N) atomicAdd(&ly.dw[(int64_t)n * ly.K + k], v[q]);
-    }
-  }
+  t32_dw_combine(a, ly, tile_g, split, tn, tk, w, lane, active, acc, reinterpret_cast<int*>(smem));
 }
 
 // ---------------------------------------------------------------- weight packing (index maps: tower_common.h)
@@ -879,21 +807,13 @@ void launch_tower32_dw(const TowerArgs& a, hipStream_t s) {
   const int nred = (a.bias_ld + 31) / 32 + (a.dn_part ? (a.dn_C + 31) / 32 : 0);
   static const int ring = [] {
     const char* e = getenv("PBX_T32_DW_RING");
-    // DS * 10 + NS of the LDS ring (default 2x3), 0 / 2: the register-streamed
-    // kernel with a ring of 4 / 2 steps.  Same box, tower dW alone: 2x3
-    // 99.9 us, 1x6 106.9, reg-4 116.7, reg-2 110.3 (profiles/r4_dw_variants.txt)
+    // DS * 10 + NS of the LDS ring (default 2x3).  Same box, tower dW alone:
+    // 2x3 99.9 us, 1x6 106.9; a register-streamed variant (no LDS) measured
+    // 110-117 and was removed (profiles/r4_dw_variants.txt)
     return e ? atoi(e) : 23;
   }();
   const dim3 g(ndw + nred), b(256);
-  // the register-streamed kernel needs every wave's step count to divide by its ring
-  const bool reg_ok = (a.Mp / 16) % (a.dw_splits * 4 * 4) == 0;  // ring 4 (ring 2 divides whenever 4 does)
-  switch (ring == 0 && !reg_ok ? 23 : ring) {
-    case 0:
-      hipLaunchKernelGGL((k_t32_dw_reg<4>), g, b, 0, s, a, ndw);
-      break;
-    case 2:
-      hipLaunchKernelGGL((k_t32_dw_reg<2>), g, b, 0, s, a, ndw);
-      break;
+  switch (ring) {
     case 16: {
       static const bool big = hipFuncSetAttribute((const void*)k_t32_dw<1, 6>,
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 6 * kDwStep * 4) ==

@@ -217,7 +217,7 @@ class FusedMLP(nn.Module):
         tw = tws.get(key)
         if tw is None:
             dims = [self.in_dim] + list(self.hidden)
-            # dW split over M (fp32 atomics between splits)
+            # dW split over M (fp32: partial slabs summed in split order; bf16: fp32 atomics)
             if fp32:
                 splits = int(os.environ.get("PBX_TOWER32_DW_SPLITS", "8"))
             else:

@@ -51,12 +51,13 @@ class IpcMeshError(RuntimeError):
 
 
 _TRACE = os.environ.get("PBX_IPC_TRACE", "0") == "1"
+_VERIFY = os.environ.get("PBX_IPC_VERIFY", "0") == "1"
 _N_MESHES = [0]
 
 
 class IpcMesh:
     def __init__(self, slot_bytes: int, group=None, device=None, blocks: Optional[int] = None, depth: int = 2,
-                 spin_limit: Optional[int] = None, stream: Optional[str] = None):
+                 spin_limit: Optional[int] = None, stream: Optional[str] = None, self_test: bool = True):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -82,8 +83,17 @@ class IpcMesh:
         # power of two: the arrive / depart counters find the last block by
         # count % grid and wrap at 2^32
         blocks = 1 << max(0, int(blocks).bit_length() - 1)
-        self.inbox = torch.zeros(self.depth * 2 * W * self.slot_bytes, dtype=torch.uint8, device=self.device)
-        self.flags = torch.zeros(2 * W, dtype=torch.int64, device=self.device)
+        # inbox + flags: written by peers over xGMI while this GPU's kernels
+        # spin on them, so they live in uncached device memory
+        # (hipExtMallocWithFlags, hipDeviceMallocUncached; PBX_IPC_MEM=fine:
+        # fine-grained) -- not on the caching allocator, whose coarse-grained
+        # hipMalloc memory is only coherent across devices at dispatch / sync
+        # boundaries
+        self.mem_kind = os.environ.get("PBX_IPC_MEM", "uncached")
+        unc = self.mem_kind != "fine"
+        dix = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.inbox = h.ipc_buffer(self.depth * 2 * W * self.slot_bytes, dix, unc)
+        self.flags = h.ipc_buffer(2 * W * 8, dix, unc).view(torch.int64)
         self.state = torch.zeros(4, dtype=torch.int64, device=self.device)
         self.comm = h.IpcComm(self.rank, W, self.slot_bytes, self.state, int(blocks), self.depth,
                               int(spin_limit or DEFAULT_SPIN_LIMIT))
@@ -133,6 +143,21 @@ class IpcMesh:
         if bad:
             self.close()
             raise IpcMeshError(f"IPC mesh setup failed on some rank (this rank: {err or 'ok'})")
+        # every construction proves the mesh end to end: known payloads through
+        # both exchange phases and both all-reduce forms, checked word by word
+        # and agreed on by all ranks (a collective: every rank constructs)
+        if self_test:
+            # at the default wait bound (construction skew between ranks can
+            # exceed a short one), aligned by a barrier
+            lim = self.comm.spin_limit()
+            self.comm.set_spin_limit(max(lim, DEFAULT_SPIN_LIMIT))
+            if W > 1:
+                dist.barrier(group=group)
+            ok = self.self_test(agree=True)
+            self.comm.set_spin_limit(lim)
+            if not ok:
+                self.close()
+                raise IpcMeshError("IPC mesh self-test failed on some rank (payload / count mismatch)")
 
     def _all_min(self, v: int) -> int:
         t = torch.tensor([int(v)], dtype=torch.int32)
@@ -195,10 +220,20 @@ class IpcMesh:
 
     def check(self):
         """Raise if a collective on this mesh failed (call outside the hot
-        loop: at pass ends, checkpoints and the end of a benchmark)."""
+        loop: at pass ends, checkpoints and the end of a benchmark).  With
+        PBX_IPC_VERIFY=1 (debug) every check also re-runs the payload
+        self-test -- a collective: every rank checks at the same points."""
         if self.world > 1 and self.error():
             raise IpcMeshError(f"IPC mesh rank {self.rank}: a peer did not arrive within the spin bound; "
                                "results since then are poisoned (NaN / empty)")
+        if _VERIFY and self.world > 1 and not torch.cuda.is_current_stream_capturing():
+            if not self.self_test(agree=True):
+                raise IpcMeshError(f"IPC mesh rank {self.rank}: periodic payload self-test failed")
+
+    def memory_attrs(self):
+        """hipPointerGetAttributes (type, device, allocation flags) of the inbox and flags."""
+        h = _native.hip()
+        return h.ptr_attrs(self.inbox.data_ptr()), h.ptr_attrs(self.flags.data_ptr())
 
     def self_test(self, agree: bool = True) -> bool:
         """Exchange known patterns with every peer (both phases, several

@@ -47,12 +47,7 @@ def make_ipc_mesh(nbytes: int, device, group=None, log=None):
         if log:
             log(f"IPC mesh unavailable ({e}); RCCL all-reduce")
         return None
-    if not m.self_test(agree=True):
-        m.close()
-        if log:
-            log("IPC mesh self-test failed; RCCL all-reduce")
-        return None
-    return m
+    return m  # self-tested by its constructor (payload check, agreed over the group)
 
 
 class CtrTrainStep:

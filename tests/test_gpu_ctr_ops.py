@@ -276,6 +276,7 @@ _GPU_VARIANTS = [
     ("fused_seqpool_cvm", dict(use_cvm=True, cvm_offset=2, need_filter=True, show_coeff=0.2, clk_coeff=1.0,
                                threshold=1.5, quant_ratio=64, clk_filter=True)),
     ("fused_seqpool_cvm", dict(use_cvm=False, cvm_offset=2, need_filter=True, quant_ratio=128, threshold=0.5,
+                               show_coeff=0.2, clk_coeff=1.0,
                                embed_threshold_filter=True, embed_threshold=1.2,
                                embed_thres_size=4)),
     ("fused_seqpool_cvm", dict(use_cvm=True, cvm_offset=2, embedx_concate_size=3, pad_value=0.1)),

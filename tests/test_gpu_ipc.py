@@ -31,6 +31,13 @@ def _worker(rank, world, port, q):
         n = 5000
         mesh = IpcMesh(n * 4, device=dev, blocks=8)
         errs = []
+        # inbox + flags in uncached device memory (hipExtMallocWithFlags), not
+        # the caching allocator's coarse-grained hipMalloc memory
+        from paddlebox_amd import _native
+
+        unc = int(_native.hip().kIpcMallocUncached)
+        for typ, d, flags in mesh.memory_attrs():
+            errs.append(0.0 if (d == 0 and flags == unc) else 1000.0 + flags)
         for it in range(5):  # both parities, several epochs
             t = torch.arange(n, dtype=torch.float32, device=dev) * (rank + 1) + it
             mesh.allreduce_(t)

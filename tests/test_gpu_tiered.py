@@ -302,8 +302,8 @@ def test_tiered_load_reaches_live_rows(tmp_path):
     try:
         ob = _box("hbm", 100000)
         h = _train(ob, overlap=False)
+        exp = ob.engine.table.read(h.to(DEV)).cpu()  # = the batch model (written before the xbox delta reset)
         ob.save_base(str(tmp_path / "m_batch"), str(tmp_path / "m_xbox"))
-        exp = ob.engine.table.read(h.to(DEV)).cpu()
     finally:
         BoxWrapper._instance = None
 
