@@ -86,9 +86,9 @@ class TowerWorkspace {
     for (int l = 0; l < L_; ++l) {
       const int64_t Kp = pad(dims[l], wpad_), Np = pad(dims[l + 1], wpad_);
       // fp32: the wave-stream layout (tower32_sched.h: per-wave streams,
-      // segments padded to the ring depth) + slack for the weight ring, which
-      // loads kT32Ring k-groups (1 KB each) past a stream's end
-      const int64_t slack = 256 * 2 * kT32Ring;
+      // units / segments padded to the ring depth) + slack for the weight
+      // ring, which loads kT32Ring steps (2 KB each) past a stream's end
+      const int64_t slack = 256 * 2 * 2 * kT32Ring;
       const int64_t n_wp = fp32 ? t32_stream_groups((int)(Np / 16), (int)(Kp / 16)) * 256 + slack : Np * Kp;
       const int64_t n_wtp = fp32 ? t32_stream_groups((int)(Kp / 16), (int)(Np / 16)) * 256 + slack : Np * Kp;
       wp_.push_back(torch::zeros({n_wp}, ob));

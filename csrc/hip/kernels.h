@@ -673,7 +673,7 @@ struct TowerArgs {
   float* dw_slab = nullptr;
   int* dw_cnt = nullptr;
   int debug = 0;  // timing experiments only (PBX_TOWER_DEBUG): 1 no loss reduction, 2 no dW reductions, 4 no dW GEMM,
-                  // 8 no fwd m-packed stores, 16 no output layer / loss, 32 fp32 tower: no s_setprio on waves 4-7,
+                  // 8 no fwd m-packed stores (fp32: no MP32 stores in the fwd / bwd layer epilogues), 16 no output layer / loss, 32 fp32 tower: no s_setprio on waves 4-7,
                   // 64 fp32 fwd/bwd: no weight loads in the k-loop, 256 fp32 fwd/bwd: plain (not
                   // non-temporal) MP32 stores / loads
   // fp32 tower (f32 = 1): fp32 X0 row-major / MP32, fp32 dX0; widths padded to 16

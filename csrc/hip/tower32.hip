@@ -2,13 +2,16 @@
 // precision (paddle/phi/kernels/gpu/matmul_kernel.cu runs fp32 GEMMs) with the
 // same three-launch structure as the bf16 tower (tower.hip):
 //
-//   k_t32_fwd  one 512-thread workgroup per 32-row tile; the tile's fp32
-//              activations stay in LDS across all layers; every wave streams
-//              packed fp32 weight fragments (1 KB per 16x16 block and 16-deep
-//              k-group, one dwordx4 per lane) and runs v_mfma_f32_16x16x4_f32.
-//              Epilogue: bias + ReLU -> LDS and the MP32 copy (one dwordx4 per
-//              lane: the accumulator IS the dW operand fragment).  Output GEMV,
-//              sigmoid, log-loss, d loss/d logit and the AUC histogram fused.
+//   k_t32_fwd  one 256-thread workgroup (ONE wave per SIMD) per 32-row tile;
+//              the tile's fp32 activations stay in LDS across all layers;
+//              every wave streams packed fp32 weight fragments (2 KB per
+//              step: two 16-column blocks x one 16-deep k-group, one dwordx4
+//              per lane each) through a register ring and runs
+//              v_mfma_f32_16x16x4_f32 on four independent accumulators (2
+//              column blocks x 2 row halves).  Epilogue: bias + ReLU -> LDS
+//              and the MP32 copy (one dwordx4 per lane: the accumulator IS the
+//              dW operand fragment).  Output GEMV, sigmoid, log-loss,
+//              d loss/d logit and the AUC histogram fused.
 //   k_t32_bwd  same tiling for the dX chain with ReLU masks read from the MP32
 //              activations, per-tile column sums for the bias gradients.
 //   k_t32_dw   dW = dZ^T X as one grouped GEMM over 64x64 output tiles, both
@@ -19,11 +22,14 @@
 //              atomics); extra workgroups reduce bias partials and data_norm
 //              statistics.
 //
+// Why one wave per SIMD (tower32_sched.h): with two, the waves shared the
+// matrix pipe fully until the first finished its share of a layer, and the
+// second then ran its tail at ~1/4 of the MFMA rate (per-wave s_memtime
+// stamps, profiles/r5_t32_schedule_ab.txt); rebalancing work between them
+// did not move the end.  One wave per SIMD has no tail by construction; its
+// latency cover is a deeper register ring (kT32Ring steps = 16 MFMAs each).
 // Why 16x16x4 and not 32x32x2: the f32 MFMA rate is 64 FLOP/clk/SIMD either
-// way; 16-wide blocks pad a 400-unit layer to 400 (not 416) and split a layer
-// into 25 column blocks x 2 row blocks, which balances over the 4 SIMDs.
-// The 16x16x4 dependent latency (40 cycles) is covered by two accumulators
-// per wave (both 16-row halves of the tile share every weight fragment).
+// way; 16-wide blocks pad a 400-unit layer to 400 (not 416).
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -34,10 +40,9 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 32;    // rows per fwd / bwd workgroup
-constexpr int NT = 512;   // threads per fwd / bwd workgroup
-constexpr int NW = NT / 64;
-constexpr int PF = 4;     // weight-fragment prefetch depth (16-deep k-groups)
+constexpr int BM = 32;          // rows per fwd / bwd workgroup
+constexpr int NW = kT32Waves;   // waves per fwd / bwd workgroup (one per SIMD)
+constexpr int NT = NW * 64;     // threads per fwd / bwd workgroup
 
 __device__ __forceinline__ int64_t mp32(int m16, int nb16, int n16) { return ((int64_t)m16 * nb16 + n16) * 256; }
 
@@ -60,167 +65,154 @@ __device__ __forceinline__ f32x4 mp_load(const float* p, int debug) {
   return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
 }
 
-// The weight ring: kT32Ring k-groups of B fragments in flight per wave (one
-// dwordx4 per lane each), in named registers (an 8-deep ring, with segments
-// padded to 8, measured slower: 92.9 vs 87.9 us forward).
+// The weight ring: kT32Ring steps of B fragments in flight per wave (two
+// dwordx4 per lane each), refilled in stream order right after each step's
+// MFMAs with the step kT32Ring ahead -- across unit / segment boundaries
+// (tower32_sched.h pads every unit and segment to whole rings), so a unit
+// starts with its first fragments in flight instead of cold.
 struct Ring {
-  f32x4 b0, b1, b2, b3, b4, b5, b6, b7;
+  f32x4 b[kT32Ring][2];
 };
-static_assert(kT32Ring == 4 || kT32Ring == 8, "t32_seg is written for a 4- or 8-slot ring");
 
-// acc{0,1} += A{0,1}(16 rows x 16 n k-groups, LDS) x B (the wave's weight
-// stream at bp): one segment of the wave's stream, led by p pad groups up to
-// a multiple of kT32Ring (tower32_sched.h).  Each ring slot is re-loaded
-// right after its 8 MFMAs with the k-group kT32Ring ahead IN THE STREAM --
-// across the segment's end into the next segment (next unit, or the
-// remainder range), so a unit starts with its first fragments in flight
-// instead of cold.  The pads keep every refill in stream order (slot 0
-// first): in-order vmcnt then covers exactly the oldest load, and no
-// register moves are needed (a rotating ring made hipcc copy registers and
-// drain vmcnt(0)).  A fragments are loaded one k-group ahead; sched_barriers
-// pin the order so hipcc keeps the loads in flight.
-// Timing experiment (TowerArgs.debug 64, its own instantiation XP = 64): no
-// weight loads in the loop (stale ring).
 template <int XP>
-__device__ __forceinline__ void t32_seg(Ring& rg, const f32x4*& bp, const float* A0, const float* A1, int n,
-                                        f32x4& acc0, f32x4& acc1) {
-  constexpr int R = kT32Ring;
-  auto step = [&](const f32x4& a0, const f32x4& a1, const f32x4& b) {
+__device__ __forceinline__ void ring_fill(Ring& rg, const f32x4* bp) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      acc0 = mfma4(a0[t], b[t], acc0);
-      acc1 = mfma4(a1[t], b[t], acc1);
-    }
-  };
-  constexpr bool noB = XP & 64;
-  auto lda = [](const float* p, int g, const f32x4&) { return *reinterpret_cast<const f32x4*>(p + 16 * g); };
-  // first block, always run (n >= 1): slots 0 .. p-1 hold pad groups, slots
-  // p .. R-1 the segment's first R - p groups; every slot is refilled in
-  // order (the refills stay on the straight path, only the MFMAs are
-  // conditional), so at least R loads follow whatever was issued before the
-  // segment (hipcc's vmcnt for the epilogue operands counts on it)
-  const int p = (R - (n & (R - 1))) & (R - 1);
-  f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = e0;  // A of even groups
-  f32x4 o0 = e0, o1 = e0;                    // A of odd groups
-  {
-    const float* a0p = A0 - 16 * p;
-    const float* a1p = A1 - 16 * p;
-#define T32_FIRST(S, B)                                       \
-  if (p <= S) {                                               \
-    e0 = lda(a0p, S, e0);                                     \
-    e1 = lda(a1p, S, e1);                                     \
-    step(e0, e1, B);                                          \
-  }                                                           \
-  __builtin_amdgcn_sched_barrier(0);                          \
-  if constexpr (!noB) B = bp[(R + S) * 64];                   \
-  __builtin_amdgcn_sched_barrier(0);
-    T32_FIRST(0, rg.b0)
-    T32_FIRST(1, rg.b1)
-    T32_FIRST(2, rg.b2)
-    if constexpr (R == 8) {
-      T32_FIRST(3, rg.b3)
-      T32_FIRST(4, rg.b4)
-      T32_FIRST(5, rg.b5)
-      T32_FIRST(6, rg.b6)
-      e0 = lda(a0p, 7, e0);
-      e1 = lda(a1p, 7, e1);
-      step(e0, e1, rg.b7);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!noB) rg.b7 = bp[(R + 7) * 64];
-    } else {
-      e0 = lda(a0p, 3, e0);
-      e1 = lda(a1p, 3, e1);
-      step(e0, e1, rg.b3);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!noB) rg.b3 = bp[(R + 3) * 64];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#undef T32_FIRST
-    bp += R * 64;
-    A0 += 16 * (R - p);
-    A1 += 16 * (R - p);
+  for (int r = 0; r < kT32Ring; ++r) {
+    rg.b[r][0] = bp[(2 * r) * 64];
+    rg.b[r][1] = bp[(2 * r + 1) * 64];
   }
-  const int nb = (n - (R - p)) / R;  // whole blocks left
-  e0 = lda(A0, 0, e0);
-  e1 = lda(A1, 0, e1);
-#define T32_SLOT(S, B, CUR0, CUR1, NXT0, NXT1) \
-  NXT0 = lda(A0, S + 1, NXT0);                 \
-  NXT1 = lda(A1, S + 1, NXT1);                 \
-  __builtin_amdgcn_sched_barrier(0);           \
-  step(CUR0, CUR1, B);                         \
-  __builtin_amdgcn_sched_barrier(0);           \
-  if constexpr (!noB) B = bp[(R + S) * 64];
-  for (int k = 0; k < nb; ++k) {
-    T32_SLOT(0, rg.b0, e0, e1, o0, o1)
-    T32_SLOT(1, rg.b1, o0, o1, e0, e1)
-    T32_SLOT(2, rg.b2, e0, e1, o0, o1)
-    T32_SLOT(3, rg.b3, o0, o1, e0, e1)
-    if constexpr (R == 8) {
-      T32_SLOT(4, rg.b4, e0, e1, o0, o1)
-      T32_SLOT(5, rg.b5, o0, o1, e0, e1)
-      T32_SLOT(6, rg.b6, e0, e1, o0, o1)
-      T32_SLOT(7, rg.b7, o0, o1, e0, e1)
-    }
-    bp += R * 64;
-    A0 += 16 * R;
-    A1 += 16 * R;
-  }
-#undef T32_SLOT
 }
 
-// LDS scratch of the remainder partial sums: [8 waves][2 segments][2 halves][64 lanes][4]
-constexpr int kPartFloats = 8 * 2 * 2 * 256;
+// steps [0, nsteps) of one unit (PAIR: 2 column blocks x k-group g = step)
+// or leftover segment (!PAIR: one block, k-groups 2 step and 2 step + 1 from
+// A0 / A1), nsteps a whole number of rings; the MFMAs of steps >= n_real are
+// skipped (pads), bp advances past them.  acc[j][h]: column block (PAIR) or
+// k-group parity (!PAIR) j, row half h.  The activation fragments (LDS) are
+// read one step ahead in an even / odd register pair: with no partner wave on
+// the SIMD nothing else would cover the ds_read latency.  Reads past a row's
+// end (one step ahead of the last) land in the tile's LDS slack, never used.
+// Timing experiment (TowerArgs.debug 64, its own instantiation XP = 64): no
+// weight loads in the loop (stale ring).
+template <int XP, bool PAIR>
+__device__ __forceinline__ void t32_run(Ring& rg, const f32x4*& bp, const float* A0, const float* A1, int n_real,
+                                        int nsteps, int len, f32x4 (&acc)[2][2]) {
+  constexpr int R = kT32Ring;
+  static_assert(R % 2 == 0, "the even / odd activation buffers need an even ring");
+  constexpr bool noB = XP & 64;
+  constexpr int SA = PAIR ? 16 : 32;  // floats of A per step
+  struct AF {
+    f32x4 a0, a1, c0, c1;
+  };
+  auto lda = [&](AF& f, int st) {
+    f.a0 = *reinterpret_cast<const f32x4*>(A0 + SA * st);
+    f.a1 = *reinterpret_cast<const f32x4*>(A1 + SA * st);
+    if (!PAIR) {
+      f.c0 = *reinterpret_cast<const f32x4*>(A0 + SA * st + 16);
+      f.c1 = *reinterpret_cast<const f32x4*>(A1 + SA * st + 16);
+    }
+  };
+  auto step = [&](const AF& f, int r, int st) {
+    if (PAIR) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[0][0] = mfma4(f.a0[t], rg.b[r][0][t], acc[0][0]);
+        acc[0][1] = mfma4(f.a1[t], rg.b[r][0][t], acc[0][1]);
+        acc[1][0] = mfma4(f.a0[t], rg.b[r][1][t], acc[1][0]);
+        acc[1][1] = mfma4(f.a1[t], rg.b[r][1][t], acc[1][1]);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[0][0] = mfma4(f.a0[t], rg.b[r][0][t], acc[0][0]);
+        acc[0][1] = mfma4(f.a1[t], rg.b[r][0][t], acc[0][1]);
+      }
+      if (2 * st + 1 < len) {  // the step's second k-group (wave-uniform)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          acc[1][0] = mfma4(f.c0[t], rg.b[r][1][t], acc[1][0]);
+          acc[1][1] = mfma4(f.c1[t], rg.b[r][1][t], acc[1][1]);
+        }
+      }
+    }
+  };
+  AF fe, fo;
+  lda(fe, 0);
+  for (int s0 = 0; s0 < nsteps; s0 += R) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int st = s0 + r;
+      AF& cur = (r & 1) ? fo : fe;
+      AF& nxt = (r & 1) ? fe : fo;
+      lda(nxt, st + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (st < n_real) step(cur, r, st);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!noB) {
+        rg.b[r][0] = bp[(2 * (st + R)) * 64];
+        rg.b[r][1] = bp[(2 * (st + R) + 1) * 64];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  bp += (int64_t)nsteps * 128;
+}
+
+// LDS scratch of the leftover partial sums: [waves][kT32MaxSeg][2 halves][64 lanes][4]
+constexpr int kPartFloats = kT32Waves * kT32MaxSeg * 2 * 256;
 
 // Workgroup barrier for LDS only: the global stores / loads in flight (MP32
 // copies, the next unit's weight fragments) are NOT drained (a
 // __syncthreads() fence would wait vmcnt(0)).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// One layer of the wave-stream schedule (tower_common.h): this wave's full
-// units (epi(acc, col, half, pre) after each; pre(col, half) is fetched before
-// its MFMA chain so the load hides under it), then its remainder range, whose
-// K-partial sums go to LDS.  t32_layer_rem (after an LDS barrier) reduces the
-// remainder blocks in wave order -- deterministic -- and applies epi.
+// One layer of the wave-stream schedule (tower32_sched.h): this wave's full
+// pair units (epi(acc, col, half, pre) after each; pre(col, half) is fetched
+// before its MFMA chain so the load hides under it), then its leftover
+// range, whose K-partial sums go to LDS.  t32_layer_rem (after an LDS
+// barrier) reduces the leftover blocks in wave order -- deterministic -- and
+// applies epi.
 template <int XP, typename Pre, typename Epi>
 __device__ __forceinline__ void t32_layer(const float* src, int ldl, const f32x4* wl, int ncol, int ng, int w,
                                           int lane, float* part, Pre&& pre, Epi&& epi) {
   const int c = lane & 15, g = lane >> 4;
   const T32Sched s = t32_sched(ncol, ng);
-  const f32x4* bp = wl + t32_wave_off(s, ng, w) * 64 + lane;
+  const f32x4* bp = wl + t32_wave_off(s, ng, w) * 128 + lane;
   Ring rg;
-  rg.b0 = bp[0];
-  rg.b1 = bp[64];
-  rg.b2 = bp[128];
-  rg.b3 = bp[192];
-  if constexpr (kT32Ring == 8) {
-    rg.b4 = bp[256];
-    rg.b5 = bp[320];
-    rg.b6 = bp[384];
-    rg.b7 = bp[448];
-  }
+  ring_fill<XP>(rg, bp);
   const float* A0 = src + c * ldl + 4 * g;
   const float* A1 = A0 + 16 * ldl;
-  const int nu = s.q + (t32_has_extra(s, w) ? 1 : 0);
-  for (int i = 0; i < nu; ++i) {
-    const int col = i < s.q ? 8 * i + w : ncol - 8 + w;  // the extra unit: tower32_sched.h
-    const f32x4 p0 = pre(col, 0), p1 = pre(col, 1);
+  const int ngp = t32_ceil_ring(ng);
+  for (int u = 0; u < s.q; ++u) {
+    const int col = 2 * (u * NW + w);
+    const f32x4 p00 = pre(col, 0), p01 = pre(col, 1), p10 = pre(col + 1, 0), p11 = pre(col + 1, 1);
     __builtin_amdgcn_sched_barrier(0);  // issue the epilogue operands before the chain
-    f32x4 acc0 = (f32x4){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-    t32_seg<XP>(rg, bp, A0, A1, ng, acc0, acc1);
-    epi(acc0, col, 0, p0);
-    epi(acc1, col, 1, p1);
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    t32_run<XP, true>(rg, bp, A0, A1, ng, ngp, ng, acc);
+    epi(acc[0][0], col, 0, p00);
+    epi(acc[0][1], col, 1, p01);
+    epi(acc[1][0], col + 1, 0, p10);
+    epi(acc[1][1], col + 1, 1, p11);
   }
-  if (s.R == 0) return;
+  if (s.Rb == 0) return;
   const int lo = t32_rem_lo(s, w), hi = t32_rem_lo(s, w + 1);
   int seg = 0;
   for (int f = lo; f < hi; ++seg) {
     const int j = f / ng, g0 = f - j * ng;
     const int len = min(ng - g0, hi - f);
-    f32x4 acc0 = (f32x4){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-    t32_seg<XP>(rg, bp, A0 + 16 * g0, A1 + 16 * g0, len, acc0, acc1);
-    float* sl = part + ((w * 2 + seg) * 2) * 256 + lane * 4;
-    *reinterpret_cast<f32x4*>(sl) = acc0;
-    *reinterpret_cast<f32x4*>(sl + 256) = acc1;
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int nst = (len + 1) / 2;
+    t32_run<XP, false>(rg, bp, A0 + 16 * g0, A1 + 16 * g0, nst, t32_seg_steps(len), len, acc);
+    float* sl = part + ((w * kT32MaxSeg + seg) * 2) * 256 + lane * 4;
+    *reinterpret_cast<f32x4*>(sl) = acc[0][0] + acc[1][0];
+    *reinterpret_cast<f32x4*>(sl + 256) = acc[0][1] + acc[1][1];
     f += len;
   }
 }
@@ -229,21 +221,22 @@ template <typename Pre, typename Epi>
 __device__ __forceinline__ void t32_layer_rem(int ncol, int ng, int w, int lane, const float* part, Pre&& pre,
                                               Epi&& epi) {
   const T32Sched s = t32_sched(ncol, ng);
-  if (w >= s.R) return;
-  const int j = w, col = 8 * s.q + j;
-  const f32x4 p0 = pre(col, 0), p1 = pre(col, 1);
-  const int wa = t32_rem_wave(s, j * ng), wb = t32_rem_wave(s, (j + 1) * ng - 1);
-  f32x4 s0 = (f32x4){0.f, 0.f, 0.f, 0.f}, s1 = s0;
-  for (int ww = wa; ww <= wb; ++ww) {
-    const int lo = t32_rem_lo(s, ww);
-    if (lo == t32_rem_lo(s, ww + 1)) continue;  // empty range
-    const int seg = j - lo / ng;
-    const float* sl = part + ((ww * 2 + seg) * 2) * 256 + lane * 4;
-    s0 += *reinterpret_cast<const f32x4*>(sl);
-    s1 += *reinterpret_cast<const f32x4*>(sl + 256);
+  for (int j = w; j < s.Rb; j += NW) {
+    const int col = 8 * s.q + j;
+    const f32x4 p0 = pre(col, 0), p1 = pre(col, 1);
+    const int wa = t32_rem_wave(s, j * ng), wb = t32_rem_wave(s, (j + 1) * ng - 1);
+    f32x4 s0 = (f32x4){0.f, 0.f, 0.f, 0.f}, s1 = s0;
+    for (int ww = wa; ww <= wb; ++ww) {
+      const int lo = t32_rem_lo(s, ww);
+      if (lo == t32_rem_lo(s, ww + 1)) continue;  // empty range
+      const int seg = j - lo / ng;
+      const float* sl = part + ((ww * kT32MaxSeg + seg) * 2) * 256 + lane * 4;
+      s0 += *reinterpret_cast<const f32x4*>(sl);
+      s1 += *reinterpret_cast<const f32x4*>(sl + 256);
+    }
+    epi(s0, col, 0, p0);
+    epi(s1, col, 1, p1);
   }
-  epi(s0, col, 0, p0);
-  epi(s1, col, 1, p1);
 }
 
 template <int XP>
@@ -254,9 +247,6 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
   const int m0 = blockIdx.x * BM;
   float* src = lds32;
   float* dst = lds32 + BM * ldl;
-  // waves 4-7 share SIMDs with 0-3 and lose every arbitration at equal
-  // priority (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (w >= 4 && !(a.debug & 32)) __builtin_amdgcn_s_setprio(1);
   long long* stp = a.stamps ? a.stamps + ((int64_t)blockIdx.x * NW + w) * 8 : nullptr;
   if (stp && lane == 0) stp[0] = __builtin_amdgcn_s_memtime();
   // loss-tail inputs and the output-layer weights, loaded ahead of the layers
@@ -277,7 +267,7 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
     }
   }
   __syncthreads();
-  float* part = lds32 + 2 * BM * ldl + 64;  // remainder partial sums
+  float* part = lds32 + 2 * BM * ldl + 64;  // leftover partial sums
   // every layer's bias in LDS (at its bias_off): the epilogues then depend
   // on no global load, so hipcc has no reason to drain the weight ring
   float* sbias = part + (a.t32_part ? kPartFloats : 0);
@@ -303,12 +293,12 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
         o[t] = v > 0.f ? v : 0.f;
         dst[(16 * mb + 4 * g + t) * ldl + n] = o[t];
       }
-      mp_store(ly.xmpf + mp32(m0 / 16 + mb, NB, nbb) + lane * 4, o, a.debug);
+      if (!(a.debug & 8)) mp_store(ly.xmpf + mp32(m0 / 16 + mb, NB, nbb) + lane * 4, o, a.debug);
     };
     t32_layer<XP>(src, ldl, wp, NB, KG, w, lane, part, pre, epi);
     if (stp && lane == 0) stp[1 + 2 * l] = __builtin_amdgcn_s_memtime();
     lds_barrier();
-    if (t32_sched(NB, KG).R) {
+    if (t32_sched(NB, KG).Rb) {
       t32_layer_rem(NB, KG, w, lane, part, pre, epi);
       lds_barrier();
     }
@@ -317,7 +307,7 @@ __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
     src = dst;
     dst = t;
   }
-  // output layer: 4 rows per wave, independent accumulations, w_out from
+  // output layer: 8 rows per wave, independent accumulations, w_out from
   // registers; the logits meet in LDS for the loss tail
   __shared__ float zrow[BM];
   {
@@ -367,8 +357,7 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
   float* src = lds32;
   float* dst = lds32 + BM * ldl;
   float* bp = a.bias_part + (int64_t)blockIdx.x * a.bias_ld;
-  float* part = lds32 + 2 * BM * ldl + 64;  // remainder partial sums
-  if (w >= 4 && !(a.debug & 32)) __builtin_amdgcn_s_setprio(1);
+  float* part = lds32 + 2 * BM * ldl + 64;  // leftover partial sums
   const float gl = a.dloss ? a.dloss[0] : 1.f;
   if (tid < BM) gs[tid] = (m0 + tid < a.M) ? a.dz[m0 + tid] * gl : 0.f;
   __syncthreads();
@@ -442,14 +431,14 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
           s += o[t];
           dst[(16 * mb + 4 * g + t) * ldl + kbb * 16 + c] = o[t];
         }
-        mp_store(prev.dzmpf + off, o, a.debug);
+        if (!(a.debug & 8)) mp_store(prev.dzmpf + off, o, a.debug);
         s += __shfl_xor(s, 16);
         s += __shfl_xor(s, 32);
         if (g == 0) cs[mb][kbb * 16 + c] = s;
       };
       t32_layer<XP>(src, ldl, wtp, KB, NG, w, lane, part, pre, epi);
       lds_barrier();
-      if (t32_sched(KB, NG).R) {
+      if (t32_sched(KB, NG).Rb) {
         t32_layer_rem(KB, NG, w, lane, part, pre, epi);
         lds_barrier();
       }
@@ -462,7 +451,7 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
       };
       t32_layer<XP>(src, ldl, wtp, KB, NG, w, lane, part, pre, epi);
       lds_barrier();
-      if (t32_sched(KB, NG).R) {
+      if (t32_sched(KB, NG).Rb) {
         t32_layer_rem(KB, NG, w, lane, part, pre, epi);
         lds_barrier();
       }
@@ -552,19 +541,26 @@ __device__ __forceinline__ void t32_dw_combine(const TowerArgs& a, const TowerLa
   }
   float* tile_slab = a.dw_slab + (int64_t)tile_g * S * 4096;
   // slab layout: [split][wave][i][j][lane][4] (inactive waves write zeros:
-  // every slab is whole, the reducer reads them unconditionally)
+  // every slab is whole, the reducer reads them unconditionally).  Stored
+  // write-through (sc1: the line leaves this XCD's L2 with the store), so the
+  // publish needs no L2 write-back fence -- a release per workgroup
+  // (buffer_wbl2, ~1.7-6.5 us each) cost the 1064-workgroup launch ~12 us.
   {
-    f32x4* my = reinterpret_cast<f32x4*>(tile_slab + (int64_t)split * 4096) + w * 4 * 64 + lane;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(tile_slab + (int64_t)split * 4096, 0, 4096 * 4, 0x00020000);
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) my[(i * 2 + j) * 64] = active ? acc[i][j] : (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 2; ++j) {
+        const f32x4 v = active ? acc[i][j] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs,
+                                               ((w * 4 + i * 2 + j) * 64 + lane) * 16, 0, 16 /* sc1 */);
+      }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int old = __hip_atomic_fetch_add(&a.dw_cnt[tile_g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == S - 1;
     if (last) {
@@ -749,7 +745,7 @@ int tower32_lds_ld(int maxw) {
 // blocks past a multiple of 8 (fwd: Np / 16, bwd: Kp / 16)
 bool tower32_needs_part(const TowerArgs& a) {
   for (int l = 0; l < a.L; ++l)
-    if (t32_sched(a.ly[l].Np / 16, a.ly[l].Kp / 16).R || t32_sched(a.ly[l].Kp / 16, a.ly[l].Np / 16).R) return true;
+    if (t32_sched(a.ly[l].Np / 16, a.ly[l].Kp / 16).Rb || t32_sched(a.ly[l].Kp / 16, a.ly[l].Np / 16).Rb) return true;
   return false;
 }
 size_t tower32_lds_bytes_for(int lds_ld, bool part, int bias_floats) {

@@ -93,6 +93,11 @@ class _PullSlot:
         self.occ_ins = torch.empty(eng.max_keys, dtype=torch.int32, device=dev)
         self.rows = None  # persistent probe rows of a prefetched batch
         self.pre_out = None  # persistent pooled output of a prefetched seqpool (prefetch_pull)
+        # one persistent pooled output per batch shape: graphs captured for
+        # different batch sizes (a pass's 64- and 63-row batches) keep the
+        # address they were captured with -- re-allocating on a shape change
+        # freed the buffer a graph of the other size still wrote / read
+        self.pre_outs = {}
         self.gen = 0
         # no-dedup pull: table row of every key occurrence
         self.rows_occ = None if eng.dedup else torch.empty(eng.max_keys, dtype=torch.int64, device=dev)
@@ -109,6 +114,13 @@ class _PullSlot:
             self.resp = torch.empty(n, eng.P, device=dev)
             self.resp_back = torch.empty(n, eng.P, device=dev)
             self.rows_r = None
+
+    def pooled_out(self, shape, device) -> torch.Tensor:
+        t = self.pre_outs.get(shape)
+        if t is None:
+            t = self.pre_outs[shape] = torch.empty(shape, dtype=torch.float32, device=device)
+        self.pre_out = t
+        return t
 
 
 @dataclass
@@ -634,8 +646,7 @@ class SparseEngine:
         Eo = sp.out_width(self.E)
         Dd = 0 if dense is None else int(dense.shape[1])
         shape = (B, S * Eo + Dd)
-        if sl.pre_out is None or tuple(sl.pre_out.shape) != shape:
-            sl.pre_out = torch.empty(shape, dtype=torch.float32, device=self.device)
+        sl.pooled_out(shape, self.device)
         self._hip.seqpool_cvm_fwd(sl.resp_back, sl.send_index, sl.ws.uid, lod, S, B, self.E, sl.pre_out, 0,
                                   sp.use_cvm, sp.cvm_offset, sp.clk_filter, sp.pad_value, sp.need_filter,
                                   sp.show_coeff, sp.clk_coeff, sp.threshold, sp.quant_ratio,
@@ -709,8 +720,7 @@ class SparseEngine:
         Eo = sp.out_width(self.E)
         Dd = 0 if dense is None else int(dense.shape[1])
         shape = (B, S * Eo + Dd)
-        if sl.pre_out is None or tuple(sl.pre_out.shape) != shape:
-            sl.pre_out = torch.empty(shape, dtype=torch.float32, device=self.device)
+        sl.pooled_out(shape, self.device)
         if self.seqpool_rows_occ:
             src_index, uid = ws.rows_occ[:L], None
         else:
