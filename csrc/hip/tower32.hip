@@ -74,12 +74,20 @@ struct Ring {
   f32x4 b[kT32Ring][2];
 };
 
-template <int XP>
-__device__ __forceinline__ void ring_fill(Ring& rg, const f32x4* bp) {
+// The wave's stream is read through a buffer resource: the step offset is
+// one SGPR add per step (soffset) and the lane offset a constant VGPR, so a
+// refill costs two buffer loads and no 64-bit address arithmetic -- with no
+// partner wave on the SIMD, every instruction between two MFMA groups that
+// does not fit the MFMA's issue shadow is exposed.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 ld_frag(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+__device__ __forceinline__ void ring_fill(Ring& rg, __amdgpu_buffer_rsrc_t rs, int voff) {
 #pragma unroll
   for (int r = 0; r < kT32Ring; ++r) {
-    rg.b[r][0] = bp[(2 * r) * 64];
-    rg.b[r][1] = bp[(2 * r + 1) * 64];
+    rg.b[r][0] = ld_frag(rs, voff, r * 2048);
+    rg.b[r][1] = ld_frag(rs, voff + 1024, r * 2048);
   }
 }
 
@@ -94,8 +102,8 @@ __device__ __forceinline__ void ring_fill(Ring& rg, const f32x4* bp) {
 // Timing experiment (TowerArgs.debug 64, its own instantiation XP = 64): no
 // weight loads in the loop (stale ring).
 template <int XP, bool PAIR>
-__device__ __forceinline__ void t32_run(Ring& rg, const f32x4*& bp, const float* A0, const float* A1, int n_real,
-                                        int nsteps, int len, f32x4 (&acc)[2][2]) {
+__device__ __forceinline__ void t32_run(Ring& rg, __amdgpu_buffer_rsrc_t rs, int voff, int& sbase, const float* A0,
+                                        const float* A1, int n_real, int nsteps, int len, f32x4 (&acc)[2][2]) {
   constexpr int R = kT32Ring;
   static_assert(R % 2 == 0, "the even / odd activation buffers need an even ring");
   constexpr bool noB = XP & 64;
@@ -148,13 +156,14 @@ __device__ __forceinline__ void t32_run(Ring& rg, const f32x4*& bp, const float*
       if (st < n_real) step(cur, r, st);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (!noB) {
-        rg.b[r][0] = bp[(2 * (st + R)) * 64];
-        rg.b[r][1] = bp[(2 * (st + R) + 1) * 64];
+        const int so = (sbase + st + R) * 2048;
+        rg.b[r][0] = ld_frag(rs, voff, so);
+        rg.b[r][1] = ld_frag(rs, voff + 1024, so);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  bp += (int64_t)nsteps * 128;
+  sbase += nsteps;
 }
 
 // LDS scratch of the leftover partial sums: [waves][kT32MaxSeg][2 halves][64 lanes][4]
@@ -176,9 +185,14 @@ __device__ __forceinline__ void t32_layer(const float* src, int ldl, const f32x4
                                           int lane, float* part, Pre&& pre, Epi&& epi) {
   const int c = lane & 15, g = lane >> 4;
   const T32Sched s = t32_sched(ncol, ng);
-  const f32x4* bp = wl + t32_wave_off(s, ng, w) * 128 + lane;
+  // this wave's stream; the ring reads kT32Ring steps past its end (into the
+  // next wave's stream, or the allocation's slack after the last)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<f32x4*>(wl + t32_wave_off(s, ng, w) * 128), 0, 0x7ffffff0, 0x00020000);
+  const int voff = lane * 16;
+  int sbase = 0;
   Ring rg;
-  ring_fill<XP>(rg, bp);
+  ring_fill(rg, rs, voff);
   const float* A0 = src + c * ldl + 4 * g;
   const float* A1 = A0 + 16 * ldl;
   const int ngp = t32_ceil_ring(ng);
@@ -191,7 +205,7 @@ __device__ __forceinline__ void t32_layer(const float* src, int ldl, const f32x4
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    t32_run<XP, true>(rg, bp, A0, A1, ng, ngp, ng, acc);
+    t32_run<XP, true>(rg, rs, voff, sbase, A0, A1, ng, ngp, ng, acc);
     epi(acc[0][0], col, 0, p00);
     epi(acc[0][1], col, 1, p01);
     epi(acc[1][0], col + 1, 0, p10);
@@ -209,7 +223,7 @@ __device__ __forceinline__ void t32_layer(const float* src, int ldl, const f32x4
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const int nst = (len + 1) / 2;
-    t32_run<XP, false>(rg, bp, A0 + 16 * g0, A1 + 16 * g0, nst, t32_seg_steps(len), len, acc);
+    t32_run<XP, false>(rg, rs, voff, sbase, A0 + 16 * g0, A1 + 16 * g0, nst, t32_seg_steps(len), len, acc);
     float* sl = part + ((w * kT32MaxSeg + seg) * 2) * 256 + lane * 4;
     *reinterpret_cast<f32x4*>(sl) = acc[0][0] + acc[1][0];
     *reinterpret_cast<f32x4*>(sl + 256) = acc[0][1] + acc[1][1];
@@ -243,7 +257,8 @@ template <int XP>
 __global__ __launch_bounds__(NT) void k_t32_fwd(TowerArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds32[];
   const int ldl = a.lds_ld;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR): the stream's buffer resource
   const int m0 = blockIdx.x * BM;
   float* src = lds32;
   float* dst = lds32 + BM * ldl;
@@ -351,7 +366,8 @@ __global__ __launch_bounds__(NT) void k_t32_bwd(TowerArgs a) {
   // layer parity so layer i's readers never race layer i-1's writers
   __shared__ float csum[2][2][kTower32MaxWidth];
   const int ldl = a.lds_ld;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR): the stream's buffer resource
   const int c = lane & 15, g = lane >> 4;
   const int m0 = blockIdx.x * BM;
   float* src = lds32;

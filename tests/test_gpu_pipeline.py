@@ -96,8 +96,14 @@ def test_pipelined_front_matches_plain_graphed_step(precision, K, split, overlap
     monkeypatch.setenv("PBX_ADAM_OVERLAP", overlap)
     monkeypatch.setenv("PBX_FUSED_SCATTER", fs)  # the dedup scatter inside the prefetched pooling launch
     f1, l1, k1, v1 = _train(True, precision, K, nb)
-    # the dW split-K atomics sum in any order: fp32-rounding-level differences
-    rt, at = (1e-6, 1e-7) if precision == "fp32" else (1e-4, 1e-5)
+    # the dense update is bit-reproducible (fixed-order dW split reduce,
+    # test_gpu_tower32.py::test_tower32_deterministic); the sparse push is
+    # not: a key's occurrences are summed in fp32 in the order the dedup's
+    # atomics placed them (rank within the key, run placement) and the pieces
+    # of a run that straddles waves meet in fp32 atomics, so two runs differ
+    # at fp32 rounding level (seen: 4e-7 abs / 1.7e-6 rel in 1 of 190k table
+    # values), which Adam's m / sqrt(v) can lift a little in the dense params
+    rt, at = (1e-5, 1e-6) if precision == "fp32" else (1e-4, 1e-5)
     assert l1 == pytest.approx(l0, rel=rt, abs=at)
     torch.testing.assert_close(f1, f0, rtol=rt, atol=at)
     assert torch.equal(k1, k0)
@@ -136,10 +142,11 @@ def test_dedup_finish_on_side_stream_matches_plain(K, overlap, monkeypatch):
     monkeypatch.setenv("PBX_TD_FINISH_SIDE", "1")
     monkeypatch.setenv("PBX_ADAM_OVERLAP", overlap)
     f1, l1, k1, v1 = _train(True, "fp32", K, nb)
-    assert l1 == pytest.approx(l0, rel=1e-6, abs=1e-7)
-    torch.testing.assert_close(f1, f0, rtol=1e-6, atol=1e-7)
+    # tolerance: the sparse push's fp32 summation order (see above)
+    assert l1 == pytest.approx(l0, rel=1e-5, abs=1e-6)
+    torch.testing.assert_close(f1, f0, rtol=1e-5, atol=1e-6)
     assert torch.equal(k1, k0)
-    torch.testing.assert_close(v1, v0, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(v1, v0, rtol=1e-5, atol=1e-6)
 
 
 def test_dcn_v2_adam_overlap_matches_plain(monkeypatch):
