@@ -124,7 +124,12 @@ class CrossWorkspace {
         a.z[l] = fp(z_[l]);
         a.xmp[l] = bp(xmp_[l]);
       }
-      launch_cross_pack(wl, wpl, wtpl, (int)L_, (int)D_, (int)kp_, (int)np_, s);
+      // the packed bf16 copies: re-packed by the fused Adam after each update
+      // when the optimizer owns them (FlatAdam.fuse), else every forward
+      if (!pack_by_opt_ || !packed_) {
+        launch_cross_pack(wl, wpl, wtpl, (int)L_, (int)D_, (int)kp_, (int)np_, s);
+        packed_ = true;
+      }
       a.xlast = fp(xf_[L_ - 1]);
       a.ldf = (int)ld_;
       a.wc = fp(wc);
@@ -308,6 +313,17 @@ class CrossWorkspace {
 
   Tensor x_out() const { return xf_[L_ - 1].narrow(1, 0, D_); }
   bool fused() const { return fused_; }
+  // (wp, wtp, N, K, Np, Kp, None, None) per layer: the bf16 pack regions of
+  // the fused Adam (the tower's bf16 layout, wp_index / wtp_index)
+  std::vector<py::tuple> pack_regions() const {
+    std::vector<py::tuple> r;
+    if (!fused_) return r;
+    for (int l = 0; l < L_; ++l)
+      r.push_back(py::make_tuple(wp_[l], wtp_[l], D_, D_, np_, kp_, py::none(), py::none()));
+    return r;
+  }
+  void set_pack_by_optimizer(bool v) { pack_by_opt_ = v; }
+  void invalidate_pack() { packed_ = false; }
 
  private:
   void check_x0(const Tensor& y) const {
@@ -317,6 +333,7 @@ class CrossWorkspace {
   }
   int64_t M_, D_, L_, ks_, ld_ = 0, ldM_ = 0, np_ = 0, kp_ = 0, mp_ = 0, bias_ld_ = 0;
   bool fused_ = false;
+  bool pack_by_opt_ = false, packed_ = false;
   std::vector<Tensor> wb_, wtb_, xf_, xb_, xt_, z_, g_, u_, ut_, wp_, wtp_, xmp_, ump_;
   Tensor acc_, dy_, s_, part_, biasp_;
 };
@@ -330,6 +347,9 @@ void bind_cross(py::module& m) {
       .def("backward", &CrossWorkspace::backward, py::arg("y"), py::arg("yt"), py::arg("ds"), py::arg("dW"),
            py::arg("db"), py::arg("wc"), py::arg("dwc"), py::arg("dy_out") = py::none())
       .def("x_out", &CrossWorkspace::x_out)
+      .def("pack_regions", &CrossWorkspace::pack_regions)
+      .def("set_pack_by_optimizer", &CrossWorkspace::set_pack_by_optimizer)
+      .def("invalidate_pack", &CrossWorkspace::invalidate_pack)
       .def_property_readonly("fused_forward", [](const CrossWorkspace& w) { return w.fused(); });
 }
 

@@ -91,7 +91,28 @@ class CrossNetV2(nn.Module):
             ks = int(os.environ.get("PBX_CROSS_KSPLIT", "1024"))
             self._xw = _native.hip().CrossWorkspace(M, self.dim, len(self.w), y.device.index or 0, ks)
             self._xw_key = (M, ld, y.device)
+            self._xw.set_pack_by_optimizer(self.packed_by_optimizer)
         return self._xw
+
+    # The fused Adam (parallel/dense.py FlatAdam.fuse) re-packs the bf16 copies
+    # of the cross weights after each update, as it does the tower's, instead
+    # of a k_cross_pack launch in every forward (the FusedMLP interface).
+    @property
+    def packed_by_optimizer(self) -> bool:
+        return bool(self.__dict__.get("_pack_by_opt", False))
+
+    @packed_by_optimizer.setter
+    def packed_by_optimizer(self, v: bool):
+        self.__dict__["_pack_by_opt"] = bool(v)
+        if self._xw is not None:
+            self._xw.set_pack_by_optimizer(bool(v))
+
+    def invalidate_pack(self):
+        if self._xw is not None:
+            self._xw.invalidate_pack()
+
+    def tower_workspaces(self):
+        return [self._xw] if self._xw is not None else []
 
     def forward(self, x0: torch.Tensor) -> torch.Tensor:
         """fp32 reference stack (CPU path and the GPU kernels' oracle)."""

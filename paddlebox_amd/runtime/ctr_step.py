@@ -105,7 +105,9 @@ class CtrTrainStep:
                              and os.environ.get("PBX_ADAM_OVERLAP", "1") == "1")
         if self.fused:
             # the overlap keeps the data_norm update out of the Adam launch
-            self.opt.fuse(mlps=[model.mlp], data_norms=[] if self.adam_overlap else [model.dn])
+            # (DCN-V2: the cross weights' bf16 copies are re-packed there too)
+            self.opt.fuse(mlps=[model.mlp] + self._cross_of(model),
+                          data_norms=[] if self.adam_overlap else [model.dn])
         self.ipc = None
         if multi and (dense == "ipc" or same_gpu):
             self.ipc = make_ipc_mesh(self.arena.grad.numel() * 4, device, log=log)
@@ -142,7 +144,7 @@ class CtrTrainStep:
                 # the data_norm update leaves the Adam launch: the hook runs it
                 # right after the all-reduce (which sums the statistics), and
                 # the next step's head waits for it only, not for Adam
-                self.opt.fuse(mlps=[model.mlp], data_norms=[])
+                self.opt.fuse(mlps=[model.mlp] + self._cross_of(model), data_norms=[])
                 model.dn.fused_update = False
                 model.dn.update_in_hook = True
             # multi-rank with the IPC dense mesh: the dW GEMM (and the all-reduce
@@ -186,6 +188,11 @@ class CtrTrainStep:
                 tower.on_dx_done = self._dedup_next
             elif mode == "2":
                 tower.on_head_done = self._dedup_next
+
+    @staticmethod
+    def _cross_of(model):
+        cross = getattr(model, "cross", None)
+        return [cross] if cross is not None and hasattr(cross, "tower_workspaces") else []
 
     def _side_update(self):
         """On the dW side stream, after the data_norm summary update: mark the
