@@ -177,8 +177,11 @@ class CrossWorkspace {
   // ADDED to (e.g. the fused tower's dX0, before its data_norm backward)
   Tensor backward(const Tensor& y, const Tensor& yt, const Tensor& ds, const std::vector<Tensor>& dW,
                   const std::vector<Tensor>& db, const Tensor& wc, const Tensor& dwc,
-                  const c10::optional<Tensor>& dy_out) {
+                  const c10::optional<Tensor>& dy_out, int64_t parts, const c10::optional<Tensor>& ds_scale) {
     check_x0(y);
+    if (ds_scale.has_value() && ds_scale->defined())
+      CR_CHECK(fused_ && ds_scale->is_cuda() && ds_scale->numel() == 1 && ds_scale->scalar_type() == torch::kFloat32,
+               "ds_scale: one f32 on the GPU, fused stack only");
     CR_CHECK(yt.is_cuda() && yt.scalar_type() == torch::kBFloat16 && yt.is_contiguous() && yt.dim() == 2 &&
                  yt.size(0) >= D_ + 1 && yt.size(1) == ldM_,
              "x0^T must be the MLP's bf16 [pad64(D+1), pad64(M)] transposed input");
@@ -194,7 +197,11 @@ class CrossWorkspace {
     CR_CHECK(wc.is_cuda() && wc.numel() == D_ && wc.is_contiguous(), "w_c");
     CR_CHECK(dwc.is_cuda() && dwc.numel() == D_ && dwc.scalar_type() == torch::kFloat32 && dwc.is_contiguous(), "dwc");
     auto s = xs();
-    if (fused_) return backward_fused(y, yt, ds, dW, db, wc, dwc, dy_out, s);
+    // parts (fused stack only): bit 0 = top + dX chain (k_cross_bwd), bit 1 =
+    // the grouped dW + db / dw_c reductions -- the caller may issue them on
+    // different streams (the dW after the chain, beside the head backward)
+    CR_CHECK(parts == 3 || (fused_ && (parts == 1 || parts == 2)), "parts: 3, or 1 / 2 with the fused stack");
+    if (fused_) return backward_fused(y, yt, ds, dW, db, wc, dwc, dy_out, s, (int)parts, ds_scale);
     int cur = 0;  // ping-pong index holding g_{l+1}, u_l, u_l^T
     launch_cross_top_bwd(fp(xf_[L_ - 1]), bp(y), fp(z_[L_ - 1]), fp(wc), fp(ds), (int)M_, (int)D_, (int)ld_,
                          fp(g_[cur]), bp(u_[cur]), bp(ut_[cur]), (int)ldM_, fp(acc_), fp(part_), fp(dwc), s);
@@ -257,7 +264,8 @@ class CrossWorkspace {
   // workgroups reduce the db and dw_c column partials
   Tensor backward_fused(const Tensor& y, const Tensor& yt, const Tensor& ds, const std::vector<Tensor>& dW,
                         const std::vector<Tensor>& db, const Tensor& wc, const Tensor& dwc,
-                        const c10::optional<Tensor>& dy_out, hipStream_t s) {
+                        const c10::optional<Tensor>& dy_out, hipStream_t s, int parts,
+                        const c10::optional<Tensor>& ds_scale) {
     (void)yt;
     const bool add = dy_out.has_value() && dy_out->defined();
     if (add)
@@ -275,6 +283,7 @@ class CrossWorkspace {
     a.xlast = fp(xf_[L_ - 1]);
     a.ldf = (int)ld_;
     a.ds = fp(ds);
+    a.ds_scale = ds_scale.has_value() && ds_scale->defined() ? fp(*ds_scale) : nullptr;
     a.wc = fp(wc);
     a.dy = add ? bp(*dy_out) : bp(dy_);
     a.ldy = (int)ld_;
@@ -285,7 +294,8 @@ class CrossWorkspace {
     a.D = (int)D_;
     a.L = (int)L_;
     a.Np = (int)np_;
-    launch_cross_bwd(a, s);
+    if (parts & 1) launch_cross_bwd(a, s);
+    if (!(parts & 2)) return add ? *dy_out : dy_;
     TowerArgs t;
     t.M = (int)M_;
     t.Mp = (int)mp_;
@@ -345,7 +355,8 @@ void bind_cross(py::module& m) {
       .def(py::init<int64_t, int64_t, int64_t, int, int64_t>())
       .def("forward", &CrossWorkspace::forward)
       .def("backward", &CrossWorkspace::backward, py::arg("y"), py::arg("yt"), py::arg("ds"), py::arg("dW"),
-           py::arg("db"), py::arg("wc"), py::arg("dwc"), py::arg("dy_out") = py::none())
+           py::arg("db"), py::arg("wc"), py::arg("dwc"), py::arg("dy_out") = py::none(), py::arg("parts") = 3,
+           py::arg("ds_scale") = py::none())
       .def("x_out", &CrossWorkspace::x_out)
       .def("pack_regions", &CrossWorkspace::pack_regions)
       .def("set_pack_by_optimizer", &CrossWorkspace::set_pack_by_optimizer)

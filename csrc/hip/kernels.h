@@ -580,6 +580,7 @@ struct CrossBwdArgs {
   const float* xlast = nullptr;        // x_L [M][ldf]
   int ldf = 0;
   const float* ds = nullptr;  // [M]
+  const float* ds_scale = nullptr;  // scalar multiplier of ds (the upstream loss grad; nullable = 1)
   const float* wc = nullptr;  // [D]
   unsigned short* ump[kMaxMlpLayers] = {};  // m-packed u_l (dW GEMM A operand)
   unsigned short* dy = nullptr;  // [M][ldy]

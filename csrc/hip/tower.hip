@@ -811,7 +811,7 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
   float* gs = reinterpret_cast<float*>(dst + TBM * ldl);  // g_{l+1}, updated in place
   float* as = gs + TBM * ldf;                             // sum_l z_l * g_{l+1}
   __shared__ float dss[TBM];
-  if (tid < TBM) dss[tid] = m0 + tid < a.M ? a.ds[m0 + tid] : 0.f;
+  if (tid < TBM) dss[tid] = m0 + tid < a.M ? a.ds[m0 + tid] * (a.ds_scale ? a.ds_scale[0] : 1.f) : 0.f;
   {
     const int c8n = P / 8;
     for (int i = tid; i < TBM * c8n; i += TNT) {

@@ -168,10 +168,36 @@ class _CtrTowerFn(torch.autograd.Function):
             # cross backward (d logit = dz); its x0 gradient is added into the
             # tower's dX0 before the data_norm / head backward below
             net, w_c = t.cross
-            ds = ctx.dz if gl is None else (ctx.dz * gl).contiguous()
-            net._xw.backward(ws.x0(), ctx.yt, ds, [_ensure_grad(w) for w in net.w],
-                             [_ensure_grad(b) for b in net.b], w_c.detach(), _ensure_grad(w_c), dy_out=dx0)
-            hook["after_cross"] = True
+            fusedx = net._xw.fused_forward
+            # the fused chain scales d logit by the loss grad itself (no
+            # elementwise launch on the critical path)
+            ds = ctx.dz if (gl is None or fusedx) else (ctx.dz * gl).contiguous()
+            dsk = {"ds_scale": gl} if (gl is not None and fusedx) else {}
+            cargs = (ws.x0(), ctx.yt, ds, [_ensure_grad(w) for w in net.w], [_ensure_grad(b) for b in net.b],
+                     w_c.detach(), _ensure_grad(w_c))
+            # the cross dW (grouped GEMM + db / dw_c reductions) only feeds the
+            # optimizer: on the side stream after the cross dX chain, beside the
+            # head backward and the sparse push (PBX_CROSS_DW_SIDE=0: inline)
+            cross_side = (t.overlap_dw and x.is_cuda and fusedx
+                          and (t.overlap_dw_collectives or not _collectives_in_step())
+                          and os.environ.get("PBX_CROSS_DW_SIDE", "1") == "1")
+            if cross_side:
+                cur = torch.cuda.current_stream(x.device)
+                net._xw.backward(*cargs, dy_out=dx0, parts=1, **dsk)
+                chain = torch.cuda.Event()
+                chain.record(cur)
+                side = t._side_stream(x.device)
+                side.wait_event(chain)
+                with torch.cuda.stream(side):
+                    net._xw.backward(*cargs, dy_out=dx0, parts=2, **dsk)
+                    if hook.get("pending"):  # the dense tail ran: the cross grads are final here
+                        t.on_dense_grads()
+                add_grad_producer(side)
+                hook["after_cross"] = True
+                hook["pending"] = False
+            else:
+                net._xw.backward(*cargs, dy_out=dx0, **dsk)
+                hook["after_cross"] = True
             if hook.get("pending"):
                 # the dense tail already ran (on the dW side stream, or inline):
                 # fire the hook where it ran, once the cross gradients are final
