@@ -325,7 +325,10 @@ def main():
         # on the side stream (rehearsal 0.526 -> 0.434 ms/step with both,
         # either alone no faster: profiles/r4_sharded_pipeline_ab.txt);
         # PBX_SHARDED_PIPELINE=0 turns the multi-rank form off
-        want_pipe = args.pipeline == "on" or (args.pipeline == "auto" and mlp_dtype == "fp32" and not dcn)
+        # and DCN-V2 on one rank, with the next batch's dedup after the head
+        # backward (CtrTrainStep's default there, profiles/r6_dcn_split_ab.txt)
+        want_pipe = args.pipeline == "on" or (args.pipeline == "auto" and (
+            (mlp_dtype == "fp32" and not dcn) or (dcn and not multi)))
         pipe_ok = args.graph and engine.can_prefetch_pull() and (
             not engine.sharded or os.environ.get("PBX_SHARDED_PIPELINE", "1") == "1")
         use_pipe = want_pipe and pipe_ok and not (args.prefetch and engine.can_prefetch())

@@ -180,7 +180,12 @@ class CtrTrainStep:
         # 0.3910 ms/step (mode 2: 0.449, profiles/r5_sharded_split3_ab.txt);
         # on one rank the dedup beside the tower measured slower (0.372 vs
         # 0.356, profiles/r5_split_prefetch_1rank_ab.txt)
-        mode = os.environ.get("PBX_SPLIT_PREFETCH", "3" if multi else "0")
+        # DCN-V2 on one rank: 2 -- its latency-bound cross kernels leave room
+        # for the dedup beside the push and the side-stream dW GEMMs (pipelined
+        # front on: 0.3342 / 0.3341 vs 0.3513 / 0.3497 ms/step without the
+        # pipeline, 0.374 / 0.353 with it and mode 0, 0.366 / 0.364 mode 3;
+        # profiles/r6_dcn_split_ab.txt)
+        mode = os.environ.get("PBX_SPLIT_PREFETCH", "3" if multi else ("2" if dcn else "0"))
         self.split_mode = mode if mode in ("1", "2", "3") else "0"
         self.split_prefetch = self.split_mode != "0" and tower is not None and hasattr(model, "prefetch_pool")
         if self.split_prefetch:
