@@ -327,8 +327,10 @@ def main():
         # PBX_SHARDED_PIPELINE=0 turns the multi-rank form off
         # and DCN-V2 on one rank, with the next batch's dedup after the head
         # backward (CtrTrainStep's default there, profiles/r6_dcn_split_ab.txt)
+        # bf16 DeepFM on one rank too: 0.2161 / 0.2165 vs 0.2188 / 0.2199
+        # ms/step without it (profiles/r6_pipeline_bf16_split_ab.txt)
         want_pipe = args.pipeline == "on" or (args.pipeline == "auto" and (
-            (mlp_dtype == "fp32" and not dcn) or (dcn and not multi)))
+            (mlp_dtype == "fp32" and not dcn) or (not multi)))
         pipe_ok = args.graph and engine.can_prefetch_pull() and (
             not engine.sharded or os.environ.get("PBX_SHARDED_PIPELINE", "1") == "1")
         use_pipe = want_pipe and pipe_ok and not (args.prefetch and engine.can_prefetch())
