@@ -673,12 +673,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       })
       .def("erase", [](HostTier& t, const Tensor& h) {
         auto hc = h.contiguous();
+        py::gil_scoped_release g;  // millions of keys from a write-back thread: the trainer keeps the GIL
         return t.erase(reinterpret_cast<const uint64_t*>(hc.data_ptr<int64_t>()), hc.numel());
       })
       .def("export_all", [](const HostTier& t) {
         std::vector<uint64_t> k;
         std::vector<float> v;
-        t.export_all(&k, &v);
+        {
+          py::gil_scoped_release g;
+          t.export_all(&k, &v);
+        }
         return py::make_tuple(to_tensor_u64(k), to_tensor_f(v, t.stride()));
       })
       .def("shrink", &HostTier::shrink, py::arg("decay"), py::arg("unseen_col"), py::arg("nonclk_coeff"),
@@ -753,6 +757,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       })
       .def("erase", [](SsdLog& s, const Tensor& h) {
         auto hc = h.contiguous();
+        py::gil_scoped_release g;
         return s.erase(reinterpret_cast<const uint64_t*>(hc.data_ptr<int64_t>()), hc.numel());
       })
       .def("compact", &SsdLog::compact, py::arg("min_live") = 0.5, py::call_guard<py::gil_scoped_release>())

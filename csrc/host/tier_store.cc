@@ -806,6 +806,9 @@ void SsdLog::get(const uint64_t* h, int64_t n, uint8_t* found, float* out, int o
     return a.seg != b.seg ? a.seg < b.seg : a.page < b.page;
   });
   constexpr int64_t kBatchPages = 8192;
+  // wanted pages at most this far apart are read as one run (the gap read
+  // along); reads are cut to kReadPages pages for the thread pool
+  constexpr int64_t kGapPages = 8, kReadPages = 256;
   char* buf = nullptr;
   if (posix_memalign(reinterpret_cast<void**>(&buf), kPage, (size_t)(kBatchPages * kPage)) != 0)
     throw std::runtime_error("SsdLog: alloc");
@@ -824,11 +827,18 @@ void SsdLog::get(const uint64_t* h, int64_t n, uint8_t* found, float* out, int o
     for (; wj < want.size(); ++wj) {
       const Want& q = want[wj];
       const bool same = !runs.empty() && runs.back().seg == q.seg;
-      if (same && runs.back().page + runs.back().npages - 1 == q.page) {  // page already in the run
-      } else if (same && runs.back().page + runs.back().npages == q.page) {
-        if (used == kBatchPages) break;
-        runs.back().npages++;
-        used++;
+      const int64_t end = same ? runs.back().page + runs.back().npages : 0;  // first page past the run
+      if (same && end - 1 == q.page) {  // page already in the run
+      } else if (same && q.page >= end && q.page - end <= kGapPages) {
+        // the next wanted page is close: read through the gap -- one
+        // sequential read instead of one 4 KiB read per page once a reload
+        // touches a dense part of a spilled segment (a pass's spill is one
+        // contiguous run of pages, so a reload of 1 in 5 of its rows hits
+        // nearly every page)
+        const int64_t add = q.page - end + 1;
+        if (used + add > kBatchPages) break;
+        runs.back().npages += add;
+        used += add;
       } else {
         if (used == kBatchPages) break;
         runs.push_back(Run{q.seg, q.page, 1, used});
@@ -837,21 +847,27 @@ void SsdLog::get(const uint64_t* h, int64_t n, uint8_t* found, float* out, int o
       const Run& r = runs.back();
       where.emplace_back(wj, r.buf_page + (q.page - r.page));
     }
-    const int T = (int)std::min<int64_t>(16, std::max<int64_t>(1, (int64_t)runs.size() / 8));
+    // reads of at most kReadPages pages, spread over up to 16 threads (the
+    // device sees a queue of them instead of one long read at a time)
+    std::vector<Run> reads;
+    for (const Run& r : runs)
+      for (int64_t o = 0; o < r.npages; o += kReadPages)
+        reads.push_back(Run{r.seg, r.page + o, std::min<int64_t>(kReadPages, r.npages - o), r.buf_page + o});
+    const int T = (int)std::min<int64_t>(16, std::max<int64_t>(1, (int64_t)reads.size() / 4));
     std::atomic<bool> bad{false};
     auto read_runs = [&](size_t r0, size_t r1) {
       for (size_t k = r0; k < r1; ++k) {
-        const Run& r = runs[k];
+        const Run& r = reads[k];
         const ssize_t bytes = (ssize_t)(r.npages * kPage);
         if (pread(segs_[r.seg]->fd, buf + r.buf_page * kPage, (size_t)bytes, r.page * kPage) != bytes) bad = true;
       }
     };
     if (T == 1) {
-      read_runs(0, runs.size());
+      read_runs(0, reads.size());
     } else {
       std::vector<std::thread> th;
       for (int t = 0; t < T; ++t)
-        th.emplace_back(read_runs, runs.size() * t / T, runs.size() * (t + 1) / T);
+        th.emplace_back(read_runs, reads.size() * t / T, reads.size() * (t + 1) / T);
       for (auto& x : th) x.join();
     }
     if (bad) throw std::runtime_error("SsdLog: read failed");
