@@ -299,7 +299,12 @@ class TieredStore:
         self._pin = {}  # reusable pinned staging buffers (pinning is slow)
         self.stats = {"stage_s": 0.0, "writeback_s": 0.0, "activate_s": 0.0, "spill_s": 0.0, "ssd_hits": 0,
                       "spilled": 0, "spilled_cap": 0, "staged_rows": 0, "new_rows": 0, "host_rows_staged": 0,
-                      "retained_rows": 0, "wb_retained_rows": 0}
+                      "retained_rows": 0, "wb_retained_rows": 0,
+                      # phase times of the background threads (seconds, summed)
+                      "stage_live_probe_s": 0.0, "stage_wait_s": 0.0, "stage_ssd_get_s": 0.0,
+                      "stage_ssd_delete_s": 0.0, "stage_host_s": 0.0, "stage_gpu_s": 0.0, "wb_d2h_s": 0.0,
+                      "wb_lock_wait_s": 0.0, "wb_host_insert_s": 0.0, "wb_ssd_delete_s": 0.0,
+                      "spill_select_s": 0.0, "spill_put_s": 0.0}
 
     def _pinned(self, name: str, shape, dtype) -> torch.Tensor:
         n = 1
@@ -342,20 +347,28 @@ class TieredStore:
                     outside = (self.live.probe(hd_all) < 0).cpu()
                 hc_all, hc = hc, hc[outside]
                 self.stats["retained_rows"] += int(hc_all.numel() - hc.numel())
+            tq = time.perf_counter()
+            self.stats["stage_live_probe_s"] += tq - t0
             if wb_before is not None:
                 wb_before.join()  # host values of earlier passes must be final (its error: wait_writeback)
             self._tier_lock.acquire()
             locked = True
+            tl = time.perf_counter()
+            self.stats["stage_wait_s"] += tl - tq
             rows = self.host.probe(hc)
             miss = rows < 0
             if self.ssd is not None and bool(miss.any()):
+                t_s = time.perf_counter()
                 found, vals = self.ssd.get(hc[miss])
+                self.stats["stage_ssd_get_s"] += time.perf_counter() - t_s
                 if bool(found.any()):
                     mk = hc[miss][found]
                     r, _ = self.host._native.insert(mk)
                     self.host._native.scatter(r, vals[found])
                     self.host._native.stamp(r, self.epoch)  # reloaded for the coming pass: newest
+                    t_d = time.perf_counter()
                     self.ssd.delete(mk)
+                    self.stats["stage_ssd_delete_s"] += time.perf_counter() - t_d
                     self.stats["ssd_hits"] += int(mk.numel())
                     rows = self.host.probe(hc)
                     miss = rows < 0
@@ -365,6 +378,8 @@ class TieredStore:
             self.host._native.gather(rows[known].contiguous(), buf)
             self._tier_lock.release()
             locked = False
+            tg = time.perf_counter()
+            self.stats["stage_host_s"] += tg - tl
             with torch.cuda.device(dev), torch.cuda.stream(self.stream):
                 st = self.stage_table
                 st.clear()
@@ -374,6 +389,7 @@ class TieredStore:
                     st.assign(kh.to(dev, non_blocking=True), buf.to(dev, non_blocking=True))
                 self._staged_keys = hd
                 self.stream.synchronize()
+            self.stats["stage_gpu_s"] += time.perf_counter() - tg
             self.stats["staged_rows"] += int(kh.numel())
             self.stats["host_rows_staged"] += int(kh.numel())
             self.stats["new_rows"] += int(miss.sum())
@@ -471,7 +487,10 @@ class TieredStore:
                 vh.copy_(v, non_blocking=True)
                 self.stream.synchronize()
             del k, v
+            tw = time.perf_counter()
+            self.stats["wb_d2h_s"] += tw - t0
             with self._tier_lock:
+                self.stats["wb_lock_wait_s"] += time.perf_counter() - tw
                 self._wb_locked(kh, vh)
             self.stats["writeback_s"] += time.perf_counter() - t0
         except BaseException as e:
@@ -480,14 +499,18 @@ class TieredStore:
     def _wb_locked(self, kh, vh):
         """Host scatter of the written-back rows, then the SSD spill (holds the tier lock)."""
         self.epoch += 1
+        t_i = time.perf_counter()
         rows, fresh = self.host._native.insert_fresh(kh)
         self.host._native.scatter(rows, vh)
         self.host._native.stamp(rows, self.epoch)
+        t_d = time.perf_counter()
+        self.stats["wb_host_insert_s"] += t_d - t_i
         if self.ssd is not None and len(self.ssd) > 0 and bool(fresh.any()):
             # a key re-entering the host tier may still have a copy on SSD
             # (spilled by an earlier write-back while its pass was live):
             # the host row is newer -- one tier per key
             self.ssd.delete(kh[fresh])
+        self.stats["wb_ssd_delete_s"] += time.perf_counter() - t_d
         if self.ssd is not None:
             l = self.host.layout
             t0 = time.perf_counter()
@@ -498,9 +521,13 @@ class TieredStore:
                     self.host.erase(ck)
                     self.stats["spilled"] += int(ck.numel())
             if self.host_cap_rows > 0:
+                t_sel = time.perf_counter()
                 ck, cv = self.host._native.spill_oldest(self.host_cap_rows)
+                t_put = time.perf_counter()
+                self.stats["spill_select_s"] += t_put - t_sel
                 if ck.numel():
                     self.ssd.put(ck, cv)
+                    self.stats["spill_put_s"] += time.perf_counter() - t_put
                     self.stats["spilled"] += int(ck.numel())
                     self.stats["spilled_cap"] += int(ck.numel())
             self.stats["spill_s"] += time.perf_counter() - t0

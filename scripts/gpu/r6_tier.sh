@@ -8,7 +8,7 @@ timeout -k 10 300 python -u bench.py --steps 200 --warmup 50 --secondary-dtype n
 hm=$(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r6_tier_head.json | awk '{print $2}')
 echo "headline ms/step $hm"
 rm -rf /tmp/pbx_ssd_r6
-timeout -k 10 900 python -u scripts/tier_bench.py --passes 10 --steps 1000 --hbm-cap 4e7 --host-cap 3e7 --ssd /tmp/pbx_ssd_r6 \
+timeout -k 10 900 python -u scripts/tier_bench.py --passes 8 --steps 1000 --hbm-cap 4e7 --host-cap 3e7 --ssd /tmp/pbx_ssd_r6 \
   --headline-ms "$hm" > gpurun_out/r6_tier.json 2> gpurun_out/r6_tier.err
 rc=$?
 rm -rf /tmp/pbx_ssd_r6
