@@ -199,6 +199,30 @@ class GpuTable {
     launch_probe_gather(view(), ptr<uint64_t>(h), h.numel(), ptr<int64_t>(rows), ptr<float>(out), (int)out.size(1),
                         cur_stream());
   }
+  // the sharded pull's answer exchange with this owner's probe + gather fused
+  // in (ipc.hip k_ipc_answer_exchange) over the IPC mesh whose peer table is
+  // at peers (IpcComm.peers_ptr): recv [world * cap] keys (rcnt [world]
+  // valid per peer), rows [world * cap] out, dst [world * cap, rec] answers
+  void answer_exchange(int64_t peers, int64_t blocks, const Tensor& recv, const Tensor& rcnt, int64_t cap,
+                       Tensor rows, Tensor dst) {
+    check_cuda(recv, "recv");
+    check_cuda(rcnt, "rcnt");
+    check_cuda(rows, "rows");
+    check_cuda(dst, "dst");
+    const IpcPeers& pt = *reinterpret_cast<const IpcPeers*>((uintptr_t)peers);
+    PBX_CHECK(peers != 0 && blocks > 0, "answer_exchange: mesh");
+    PBX_CHECK(recv.scalar_type() == torch::kInt64 && recv.is_contiguous() && recv.numel() == pt.world * cap,
+              "answer_exchange: recv must be [world * cap] int64");
+    PBX_CHECK(rcnt.scalar_type() == torch::kInt32 && rcnt.numel() >= pt.world, "answer_exchange: rcnt");
+    PBX_CHECK(rows.scalar_type() == torch::kInt64 && rows.is_contiguous() && rows.numel() >= recv.numel(),
+              "answer_exchange: rows");
+    PBX_CHECK(dst.dim() == 2 && dst.is_contiguous() && dst.size(0) == recv.numel() && dst.size(1) % 4 == 0 &&
+                  dst.size(1) <= stride_ && stride_ % 4 == 0,
+              "answer_exchange: dst must be contiguous [world * cap, rec], rec % 4 == 0, <= row stride");
+    PBX_CHECK(dst.size(1) * 4 <= pt.slot_bytes, "answer_exchange: record larger than the mesh slot");
+    launch_ipc_answer_exchange(pt, view(), ptr<uint64_t>(recv), ptr<int32_t>(rcnt), cap, (int)dst.size(1),
+                               ptr<int64_t>(rows), ptr<float>(dst), (int)blocks, cur_stream());
+  }
   // no-dedup pull: rows[k] = row of raw feasign keys[k] (-1: padding / absent)
   void probe_raw(const Tensor& keys, Tensor rows) {
     check_cuda(keys, "keys");
@@ -1339,6 +1363,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("push_adagrad_seg", &GpuTable::push_adagrad_seg)
       .def("push_merge_apply", &GpuTable::push_merge_apply)
       .def("probe_gather", &GpuTable::probe_gather)
+      .def("answer_exchange", &GpuTable::answer_exchange)
       .def("probe_raw", &GpuTable::probe_raw)
       .def("save_stream", &GpuTable::save_stream)
       .def_property_readonly_static("occ_replicas", [](py::object) { return kOccRep; })

@@ -4,6 +4,7 @@
 #include <torch/extension.h>
 
 #include <stdexcept>
+#include <unordered_map>
 
 #include "kernels.h"
 
@@ -175,6 +176,80 @@ Tensor sfc(const Tensor& A, const Tensor& Bk, const c10::optional<Tensor>& bias,
   if (!launch_sfc(P<float>(A), static_cast<const void*>(Bk.data_ptr<at::Half>()), M, Nd, Kd, (float)a_scale,
                   OP<float>(bias), (float)alpha, (float)bias_scale, (float)out_scale, P<float>(out), cs()))
     return Tensor();
+  return out;
+}
+
+// scaled_fc weight + bias gradient (launch_sfc_dw): dW [K, O] and db [O] from
+// x [N, K], d [N, O] (contiguous fp32) split S ways over N.  The tile counters
+// come from a per-device ring of zeroed slots (the kernel leaves its slot
+// zeroed), so back-to-back launches -- and launches on different streams, up
+// to kSfcDwSlots in flight -- never share a counter.  false: the shapes do
+// not fit the kernel (the caller takes the k_hgemm path).
+constexpr int kSfcDwSlots = 64, kSfcDwSlotInts = 1024;
+bool sfc_dw(const Tensor& x, const Tensor& d, Tensor dW, const c10::optional<Tensor>& db, double a_scale,
+            double b_scale, double alpha, double out_scale, int64_t splits, int64_t mode) {
+  f32(x, "x");
+  f32(d, "d");
+  f32(dW, "dW");
+  CX_CHECK(x.dim() == 2 && d.dim() == 2 && x.is_contiguous() && d.is_contiguous() && x.size(0) == d.size(0),
+           "sfc_dw: x [N, K], d [N, O] contiguous");
+  SfcDwArgs a;
+  a.N = (int)x.size(0);
+  a.K = (int)x.size(1);
+  a.O = (int)d.size(1);
+  CX_CHECK(dW.is_contiguous() && dW.numel() == (int64_t)a.K * a.O, "dW must be a contiguous [K, O] tensor");
+  a.x = P<float>(x);
+  a.d = P<float>(d);
+  a.dW = P<float>(dW);
+  a.ldx = a.K;
+  a.ldd = a.O;
+  if (db.has_value() && db->defined()) {
+    f32(*db, "db");
+    CX_CHECK(db->is_contiguous() && db->numel() == a.O, "db must be a contiguous [O] tensor");
+    a.db = P<float>(*db);
+  }
+  const int tiles = sfc_dw_tiles(a.K, a.O);
+  int S = (int)std::max<int64_t>(1, splits);
+  if (S > 1) {
+    a.chunk = sfc_dw_chunk(a.N, S);
+    S = (a.N + a.chunk - 1) / a.chunk;  // no empty splits
+  }
+  if (S <= 1 || tiles > kSfcDwSlotInts) S = 1;
+  a.S = S;
+  Tensor slab;
+  if (S > 1) {
+    const int nto = (a.O + 79) / 80;
+    slab = torch::empty({(int64_t)tiles * S * 6400 + (int64_t)nto * S * 80}, x.options());
+    a.slab = P<float>(slab);
+    a.db_slab = a.slab + (int64_t)tiles * S * 6400;
+    // device -> (slots, next slot); never destroyed (no tensor release after the runtime's teardown)
+    static auto* ring = new std::unordered_map<int, std::pair<Tensor, int>>();
+    auto& r = (*ring)[x.get_device()];
+    if (!r.first.defined()) r.first = torch::zeros({kSfcDwSlots * kSfcDwSlotInts}, x.options().dtype(torch::kInt));
+    a.cnt = r.first.data_ptr<int>() + (int64_t)r.second * kSfcDwSlotInts;
+    r.second = (r.second + 1) % kSfcDwSlots;
+  }
+  a.a_scale = (float)a_scale;
+  a.b_scale = (float)b_scale;
+  a.alpha = (float)alpha;
+  a.out_scale = (float)out_scale;
+  a.mode = (int)mode;
+  return launch_sfc_dw(a, cs());
+}
+
+// out [M, Nd] = A [M, Kd] @ (Bh + Bl)^T: fp32 A, B as its bf16 split (two
+// contiguous [Nd, Kd] bf16 tensors) -- launch_f3gemm_nt.  Undefined tensor
+// when the shapes do not fit the kernel.
+Tensor f3gemm_nt(const Tensor& A, const Tensor& Bh, const Tensor& Bl) {
+  f32(A, "A");
+  CX_CHECK(A.dim() == 2 && A.is_contiguous(), "A must be a contiguous [M, Kd] tensor");
+  for (const Tensor* b : {&Bh, &Bl})
+    CX_CHECK(b->is_cuda() && b->scalar_type() == torch::kBFloat16 && b->dim() == 2 && b->is_contiguous() &&
+                 b->size(1) == A.size(1) && b->size(0) == Bh.size(0),
+             "Bh / Bl must be contiguous bf16 [Nd, Kd] tensors");
+  const int M = (int)A.size(0), Kd = (int)A.size(1), Nd = (int)Bh.size(0);
+  auto out = torch::empty({M, Nd}, A.options());
+  if (!launch_f3gemm_nt(P<float>(A), Bh.data_ptr(), Bl.data_ptr(), M, Nd, Kd, P<float>(out), cs())) return Tensor();
   return out;
 }
 
@@ -498,6 +573,9 @@ void bind_ctr(py::module& m) {
         py::arg("sBias") = 0, py::arg("bias_scale") = 1.0, py::arg("alpha") = 1.0, py::arg("accumulate") = false);
   m.def("colsum_strided", &colsum_strided);
   m.def("hgemm", &hgemm);
+  m.def("sfc_dw", &sfc_dw, py::arg("x"), py::arg("d"), py::arg("dW"), py::arg("db"), py::arg("a_scale"),
+        py::arg("b_scale"), py::arg("alpha"), py::arg("out_scale"), py::arg("splits"), py::arg("mode") = 0);
+  m.def("f3gemm_nt", &f3gemm_nt);
   m.def("h16_epi", &h16_epi);
   m.def("sfc", &sfc);
   m.def("int8_fc", &int8_fc);

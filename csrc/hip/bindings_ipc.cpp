@@ -4,6 +4,8 @@
 #include <ATen/hip/HIPContext.h>
 #include <torch/extension.h>
 
+#include <cstdlib>
+
 #include <cstring>
 #include <stdexcept>
 
@@ -110,7 +112,10 @@ class IpcComm {
     p_.arrive = reinterpret_cast<unsigned int*>(st + 1);
     p_.depart = reinterpret_cast<unsigned int*>(st + 1) + 1;
     p_.err = reinterpret_cast<int*>(st + 2);
+    const char* f = std::getenv("PBX_IPC_FENCE");
+    p_.fence = (f && f[0] == '0') ? 0 : 1;
   }
+  bool fence() const { return p_.fence != 0; }
   void set_peer(int p, int64_t inbox, int64_t flags) {
     IPC_CHECK(p >= 0 && p < p_.world && inbox && flags, "peer");
     p_.inbox[p] = reinterpret_cast<unsigned char*>(inbox);
@@ -177,6 +182,40 @@ class IpcComm {
                         at::hip::getCurrentHIPStream().stream());
   }
 
+  // the mesh's peer table (address, for GpuTable.answer_exchange in the same
+  // module) and grid size; the mesh must outlive every launch that uses them
+  int64_t peers_ptr() {
+    check_ready();
+    return (int64_t)reinterpret_cast<uintptr_t>(&p_);
+  }
+  int blocks() const { return blocks_; }
+  // key exchange with the owner pack fused in (launch_ipc_pack_exchange):
+  // uniq_h int64 [>= U] (U = u_count[0] on the device), send_index int64,
+  // ocnt / rcounts int32 [world] (ocnt zero on entry), overflow int32 [1],
+  // dst int64 [world, cap] with cap * 8 <= slot_bytes
+  void pack_exchange(const Tensor& uniq_h, const Tensor& u_count, int64_t cap, Tensor send_index, Tensor ocnt,
+                     Tensor overflow, Tensor dst, Tensor rcounts) {
+    check_ready();
+    for (const Tensor* t : std::initializer_list<const Tensor*>{&uniq_h, &u_count, &send_index, &ocnt, &overflow, &dst,
+                                                                  &rcounts})
+      IPC_CHECK(t->is_cuda() && t->is_contiguous(), "pack_exchange: contiguous device tensors");
+    IPC_CHECK(uniq_h.scalar_type() == torch::kInt64 && send_index.scalar_type() == torch::kInt64 &&
+                  dst.scalar_type() == torch::kInt64, "pack_exchange: uniq_h / send_index / dst are int64");
+    IPC_CHECK(u_count.scalar_type() == torch::kInt32 && ocnt.scalar_type() == torch::kInt32 &&
+                  rcounts.scalar_type() == torch::kInt32 && overflow.scalar_type() == torch::kInt32,
+              "pack_exchange: counts are int32");
+    IPC_CHECK(cap > 0 && cap * 8 <= p_.slot_bytes && cap < ((int64_t)1 << kIpcCountBits), "pack_exchange: cap");
+    IPC_CHECK(dst.numel() == (int64_t)p_.world * cap, "pack_exchange: dst must be [world, cap]");
+    IPC_CHECK(send_index.numel() >= uniq_h.numel(), "pack_exchange: send_index shorter than uniq_h");
+    IPC_CHECK(ocnt.numel() >= p_.world && rcounts.numel() >= p_.world, "pack_exchange: ocnt / rcounts");
+    launch_ipc_pack_exchange(p_, reinterpret_cast<const uint64_t*>(uniq_h.data_ptr()),
+                             reinterpret_cast<const int32_t*>(u_count.data_ptr()), cap,
+                             reinterpret_cast<int64_t*>(send_index.data_ptr()),
+                             reinterpret_cast<int32_t*>(ocnt.data_ptr()), reinterpret_cast<int32_t*>(overflow.data_ptr()),
+                             reinterpret_cast<uint64_t*>(dst.data_ptr()), reinterpret_cast<int32_t*>(rcounts.data_ptr()),
+                             blocks_, at::hip::getCurrentHIPStream().stream());
+  }
+
  private:
   IpcPeers p_;
   int blocks_;
@@ -201,7 +240,11 @@ void bind_ipc(py::module& m) {
       .def("allreduce", &IpcComm::allreduce, py::arg("src"), py::arg("out"), py::arg("scale"),
            py::arg("two_phase"))
       .def("exchange", &IpcComm::exchange, py::arg("send"), py::arg("dst"), py::arg("counts"), py::arg("rec_bytes"),
-           py::arg("fill_tail"), py::arg("rcounts"));
+           py::arg("fill_tail"), py::arg("rcounts"))
+      .def("pack_exchange", &IpcComm::pack_exchange)
+      .def("peers_ptr", &IpcComm::peers_ptr)
+      .def("blocks", &IpcComm::blocks)
+      .def("fence", &IpcComm::fence);
 }
 
 }  // namespace pbx

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -562,12 +563,399 @@ __global__ __launch_bounds__(256) void k_sfc(const float* __restrict__ A, const 
   }
 }
 
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+// round-to-nearest-even fp32 -> bf16 bits, and back
+__device__ __forceinline__ unsigned short f3_bf(float f) {
+  unsigned int u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+__device__ __forceinline__ float f3_f(unsigned short h) { return __uint_as_float(((unsigned int)h) << 16); }
+// x = hi + lo + r, |r| <~ 2^-17 |x|: the split of the fp32 x 3 bf16 GEMMs (four values)
+__device__ __forceinline__ void f3_split4(const float4& x, s16x4& hi, s16x4& lo) {
+  const float v[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const unsigned short h = f3_bf(v[j]);
+    hi[j] = (short)h;
+    lo[j] = (short)f3_bf(v[j] - f3_f(h));
+  }
+}
+
+// ---------------------------------------------------------------- fp32 GEMM as three bf16 products
+// out[M][Nd] = A[M][Kd] (fp32) @ B^T, B given as its bf16 split Bh + Bl
+// ([Nd][Kd], k-minor: a weight split once per optimizer step), A split in the
+// staging pass: out = Ah Bh + Ah Bl + Al Bh with fp32 accumulation -- the
+// product error of the dropped Al Bl and the split residuals is ~2^-16
+// relative, i.e. tighter than the TF32 the reference's cuBLAS applies to its
+// fp32 GEMMs in training (gpu_context.cc:61-67 enable_cublas_tf32_op_math,
+// CublasCall), at 3 bf16 MFMAs (v_mfma_f32_16x16x32_bf16) instead of 8 fp32
+// ones.  scaled_int8fc's straight-through dx.  Tiles as k_sfc (64 x 80, 4
+// waves of 16 x 80, XCD-grouped row blocks); K in chunks of 32, double
+// buffered: 4 LDS images (A hi / lo, B hi / lo) of 80-B rows (conflict-free
+// 16-B fragment reads), 46 KB, 3 workgroups per CU.
+constexpr int kF3KC = 32, kF3Pad = 40;
+__global__ __launch_bounds__(256) void k_f3gemm_nt(const float* __restrict__ A, const short* __restrict__ Bh,
+                                                   const short* __restrict__ Bl, int M, int Nd, int Kd,
+                                                   float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) short As[2][2][kSfcBM * kF3Pad];  // [buffer][hi / lo]
+  __shared__ __attribute__((aligned(16))) short Bs[2][2][kSfcBN * kF3Pad];
+  typedef short s8v __attribute__((ext_vector_type(8)));
+  const int ntn = (Nd + kSfcBN - 1) / kSfcBN, ntiles = ntn * ((M + kSfcBM - 1) / kSfcBM);
+  const int wid = sfc_xcd_id((int)blockIdx.x, ntiles);
+  const int m0 = (wid / ntn) * kSfcBM, n0 = (wid % ntn) * kSfcBN;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  // A staging: row t >> 2, k 8 (t & 3) .. + 7 (two float4 -> one 16-B write per
+  // image); B: 640 16-B chunks, image idx / 320, row (idx % 320) / 4, chunk idx % 4.
+  // Range-checked buffer loads (rows past M / Nd and k past Kd read zeros), so
+  // the loads are unconditional and a 3-deep register ring keeps 2 chunks of
+  // loads in flight under the MFMAs.
+  constexpr int D = 3;
+  const int ar = t >> 2, ak = (t & 3) * 8;
+  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t as = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(A + (int64_t)m0 * Kd), 0, (int)((int64_t)min(kSfcBM, M - m0) * Kd * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t bhs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<short*>(Bh + (int64_t)n0 * Kd), 0, (int)((int64_t)min(kSfcBN, Nd - n0) * Kd * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t bls = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<short*>(Bl + (int64_t)n0 * Kd), 0, (int)((int64_t)min(kSfcBN, Nd - n0) * Kd * 2), 0x00020000);
+  float4 ra[D][2];
+  s8v rb[D][3];
+  auto load = [&](auto jc, int k0) {
+    constexpr int J = decltype(jc)::value;
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int k = k0 + ak + 4 * v;
+      ra[J][v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(as, k < Kd ? (ar * Kd + k) * 4 : 0x7ffffff0, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int idx = t + 256 * i, im = idx >= 320, r = (idx - 320 * im) >> 2, k = k0 + (idx & 3) * 8;
+      const int off = (idx < 640 && k < Kd) ? (r * Kd + k) * 2 : 0x7ffffff0;
+      rb[J][i] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(im ? bls : bhs, off, 0, 0));
+    }
+  };
+  auto stage = [&](auto jc, int buf) {
+    constexpr int J = decltype(jc)::value;
+    s16x4 h0, l0, h1, l1;
+    f3_split4(ra[J][0], h0, l0);
+    f3_split4(ra[J][1], h1, l1);
+    *reinterpret_cast<s8v*>(&As[buf][0][ar * kF3Pad + ak]) = (s8v){h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+    *reinterpret_cast<s8v*>(&As[buf][1][ar * kF3Pad + ak]) = (s8v){l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int idx = t + 256 * i, im = idx >= 320, r = (idx - 320 * im) >> 2;
+      if (idx < 640) *reinterpret_cast<s8v*>(&Bs[buf][im][r * kF3Pad + (idx & 3) * 8]) = rb[J][i];
+    }
+  };
+  f32x4 acc[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf) {
+    const s8v ah = *reinterpret_cast<const s8v*>(&As[buf][0][(16 * w + fr) * kF3Pad + 8 * fk]);
+    const s8v al = *reinterpret_cast<const s8v*>(&As[buf][1][(16 * w + fr) * kF3Pad + 8 * fk]);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const s8v bh = *reinterpret_cast<const s8v*>(&Bs[buf][0][(16 * j + fr) * kF3Pad + 8 * fk]);
+      const s8v bl = *reinterpret_cast<const s8v*>(&Bs[buf][1][(16 * j + fr) * kF3Pad + 8 * fk]);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[j], 0, 0, 0);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  auto body = [&](auto jc, int c) {  // chunk c lives in ring set c % D = J
+    constexpr int J = decltype(jc)::value;
+    load(jc, (c + D) * kF3KC);  // set J was staged at chunk c - 1
+    compute(c & 1);
+    stage(std::integral_constant<int, (J + 1) % D>{}, (c + 1) & 1);
+    __syncthreads();
+  };
+  // chunks rounded up to whole rings: the extra chunks load and multiply zeros
+  const int nch = (Kd + kF3KC * D - 1) / (kF3KC * D) * D;
+  load(I0{}, 0);
+  load(I1{}, kF3KC);
+  load(I2{}, 2 * kF3KC);
+  stage(I0{}, 0);
+  __syncthreads();
+  for (int c0 = 0; c0 < nch; c0 += D) {
+    body(I0{}, c0);
+    body(I1{}, c0 + 1);
+    body(I2{}, c0 + 2);
+  }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int n = n0 + 16 * j + fr;
+    if (n >= Nd) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + 16 * w + 4 * fk + r;
+      if (m < M) out[(int64_t)m * Nd + n] = acc[j][r];
+    }
+  }
+}
+
 // split-K second pass: the fp16 epilogue over the fp32 sums
 __global__ void k_hgemm_epi(HgemmArgs g) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)g.M * g.N) return;
   const int m = (int)(e / g.N), n = (int)(e % g.N);
   g.C[(int64_t)m * g.ldc + n] = h16_epi(g.ws[e], g.bias ? g.bias[n] : 0.f, g);
+}
+
+// ---------------------------------------------------------------- scaled_fc weight gradient
+// dW [K][O] = h16_epi( sum_n fp16(x[n][k] * a_scale) fp16(d[n][o] * b_scale) ) and
+// db [O] = sum_n d[n][o] (fp32, unscaled) in ONE launch (scaled_fc_op.cu:232-330's
+// dW GEMM + bias column sum).  Both operands are row-major over the reduction
+// index n, so a workgroup stages 32 rows of x[n][k0 .. k0 + 79] and d[n][o0 ..
+// o0 + 79] as fp16 into LDS exactly as they lie ([n][col] images, one 8-B
+// write per float4) and the MFMA fragments, which want 8 consecutive n per
+// lane, come out of ds_read_b64_tr_b16 (two per fragment: rows 8g .. 8g + 3
+// and 8g + 4 .. 8g + 7 of the 16-lane group g).  Image rows are 256 B with
+// the five 32-B column groups XOR-swizzled by (r & 3) | ((r >> 3) & 1) << 2, so
+// the 8 rows a 32-lane half reads land on 8 disjoint 8-bank windows.
+// Tile 80 x 80 of dW, 5 waves: wave w owns columns 16w .. 16w + 15 and all
+// five 16-row blocks (5 accumulators; one B fragment feeds 5 MFMAs).  The
+// batch is split over S workgroups per tile (split-K over n); every split
+// stores its partial to a slab, the last arriving split sums the slabs in
+// split order and applies the fp16 epilogue -- deterministic, no fp32 atomics,
+// no memset, no second launch.  Tiles with k0 == 0 also sum their d columns
+// (a fixed-order reduce in LDS, then the same slab hand-off) for db.
+constexpr int kSdwT = 80, kSdwNT = 320, kSdwRowB = 256;
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int sdw_off(int r, int c) {
+  const int h = (r & 3) | (((r >> 3) & 1) << 2);
+  return r * kSdwRowB + ((((c >> 4) ^ h)) << 5) + ((c & 15) << 1);
+}
+
+__device__ __forceinline__ s16x8 sdw_frag(const unsigned char* img, int r, int c) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + sdw_off(r, c)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + sdw_off(r + 4, c)));
+  return (s16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// MODE 0: scaled_fc (fp16 operands scaled by a_scale / b_scale, the fp16
+// epilogue, two images).  MODE 1: fp32 x^T d as three bf16 MFMA products per
+// pair (hi.hi + hi.lo + lo.hi of the operands' bf16 splits; scaled_int8fc's
+// straight-through dW), fp32 result, four images (x hi, x lo, d hi, d lo).
+// Steps of 32 rows, double-buffered in LDS, fed by a 4-deep register ring.
+template <int MODE>
+__global__ __launch_bounds__(kSdwNT) void k_sfc_dw(SfcDwArgs a) {
+  constexpr int ROWS = 32, NIMG = MODE ? 4 : 2, IMG = ROWS * kSdwRowB, NI = ROWS / 16;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * NIMG * IMG];  // [buffer][image]
+  __shared__ int flag;
+  auto img = [&](int buf, int m) { return lds + (buf * NIMG + m) * IMG; };
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int tiles = a.ntk * a.nto;
+  const int wid = sfc_xcd_id((int)blockIdx.x, tiles * a.S);  // one XCD: consecutive splits, all tiles
+  const int split = wid / tiles, tile = wid % tiles;
+  const int tk = tile / a.nto, to = tile % a.nto;
+  const int k0 = tk * kSdwT, o0 = to * kSdwT;
+  const int nbeg = split * a.chunk, nend = min(a.N, nbeg + a.chunk);
+  // staging: float4 column c4 = t % 20 of rows t / 20 + 16 i (i < NI) -- the
+  // same column for every item, so the db partial is a per-thread float4
+  const int c4 = t % 20, r0 = t / 20;
+  const bool kx = k0 + 4 * c4 < a.K, ko = o0 + 4 * c4 < a.O;
+  const bool do_db = a.db != nullptr && tk == 0;
+  const float* xp = a.x + k0 + 4 * c4;
+  const float* dp = a.d + o0 + 4 * c4;
+  // register ring of D steps: the loads of step s + D are issued at the start
+  // of step s, so D - 1 steps of loads stay in flight under the MFMAs (one step
+  // in flight left every step waiting a full memory latency)
+  constexpr int D = 4;
+  float4 rx[D][NI], rd[D][NI];
+  float4 dsum = make_float4(0.f, 0.f, 0.f, 0.f);
+  // buffer loads over [nbeg, nend) only: rows past the split and columns past
+  // K / O (voffset pushed out of range) read as zeros, so every load is
+  // unconditional and the compiler's vmcnt tracking stays exact across steps
+  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+  const int rows_here = nend > nbeg ? nend - nbeg : 0;
+  const __amdgpu_buffer_rsrc_t xs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.x + (int64_t)nbeg * a.ldx), 0, (int)((int64_t)rows_here * a.ldx * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ds = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.d + (int64_t)nbeg * a.ldd), 0, (int)((int64_t)rows_here * a.ldd * 4), 0x00020000);
+  const int xcol = kx ? (k0 + 4 * c4) * 4 : 0x7ffffff0, dcol = ko ? (o0 + 4 * c4) * 4 : 0x7ffffff0;
+  auto load = [&](auto jc, int rb) {  // rb: first row of the step, relative to nbeg
+    constexpr int J = decltype(jc)::value;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int n = rb + r0 + 16 * i;
+      rx[J][i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xs, kx ? n * (int)a.ldx * 4 + xcol : xcol, 0, 0));
+      rd[J][i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ds, ko ? n * (int)a.ldd * 4 + dcol : dcol, 0, 0));
+    }
+  };
+  auto stage = [&](auto jc, int buf) {
+    constexpr int J = decltype(jc)::value;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int off = sdw_off(r0 + 16 * i, 4 * c4);
+      const float4 vx = rx[J][i], vd = rd[J][i];
+      if (MODE == 0) {
+        const h16x4 hx = {(_Float16)(vx.x * a.a_scale), (_Float16)(vx.y * a.a_scale), (_Float16)(vx.z * a.a_scale),
+                          (_Float16)(vx.w * a.a_scale)};
+        const h16x4 hd = {(_Float16)(vd.x * a.b_scale), (_Float16)(vd.y * a.b_scale), (_Float16)(vd.z * a.b_scale),
+                          (_Float16)(vd.w * a.b_scale)};
+        *reinterpret_cast<h16x4*>(img(buf, 0) + off) = hx;
+        *reinterpret_cast<h16x4*>(img(buf, 1) + off) = hd;
+      } else {
+        s16x4 xh, xl, dh, dl;
+        f3_split4(vx, xh, xl);
+        f3_split4(vd, dh, dl);
+        *reinterpret_cast<s16x4*>(img(buf, 0) + off) = xh;
+        *reinterpret_cast<s16x4*>(img(buf, 1) + off) = xl;
+        *reinterpret_cast<s16x4*>(img(buf, 2) + off) = dh;
+        *reinterpret_cast<s16x4*>(img(buf, 3) + off) = dl;
+      }
+      if (do_db) {
+        dsum.x += vd.x; dsum.y += vd.y; dsum.z += vd.z; dsum.w += vd.w;
+      }
+    }
+  };
+  f32x4 acc[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // tr-read addressing: lane 16g + 4q + p reads row 8g + q, columns 4p .. 4p + 3 of a 16-column block
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int s2 = 0; s2 < ROWS / 32; ++s2) {
+      const int r = 32 * s2 + 8 * g + q;
+      if (MODE == 0) {
+        const h16x8 b = __builtin_bit_cast(h16x8, sdw_frag(img(buf, 1), r, 16 * w + 4 * p));
+#pragma unroll
+        for (int kb = 0; kb < 5; ++kb) {
+          const h16x8 av = __builtin_bit_cast(h16x8, sdw_frag(img(buf, 0), r, 16 * kb + 4 * p));
+          acc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b, acc[kb], 0, 0, 0);
+        }
+      } else {
+        const s16x8 bh = sdw_frag(img(buf, 2), r, 16 * w + 4 * p);
+        const s16x8 bl = sdw_frag(img(buf, 3), r, 16 * w + 4 * p);
+#pragma unroll
+        for (int kb = 0; kb < 5; ++kb) {
+          const s16x8 ah = sdw_frag(img(buf, 0), r, 16 * kb + 4 * p);
+          const s16x8 al = sdw_frag(img(buf, 1), r, 16 * kb + 4 * p);
+          acc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[kb], 0, 0, 0);
+          acc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[kb], 0, 0, 0);
+          acc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[kb], 0, 0, 0);
+        }
+      }
+    }
+  };
+  // steps rounded up to whole rings: the extra steps load and multiply zeros
+  const int nsteps = rows_here > 0 ? (rows_here + ROWS * D - 1) / (ROWS * D) * D : 0;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3 % D>;
+  auto body = [&](auto jc, int s) {  // step s lives in ring set s % D = J
+    constexpr int J = decltype(jc)::value;
+    load(jc, (s + D) * ROWS);  // set J was staged at step s - 1
+    compute(s & 1);
+    stage(std::integral_constant<int, (J + 1) % D>{}, (s + 1) & 1);
+    __syncthreads();
+  };
+  if (nsteps > 0) {
+    load(I0{}, 0);
+    load(I1{}, ROWS);
+    load(I2{}, 2 * ROWS);
+    if (D > 3) load(I3{}, 3 * ROWS);
+    stage(I0{}, 0);
+    __syncthreads();
+    for (int s0 = 0; s0 < nsteps; s0 += D) {
+      body(I0{}, s0);
+      body(I1{}, s0 + 1);
+      body(I2{}, s0 + 2);
+      if (D > 3) body(I3{}, s0 + 3);
+    }
+  }
+  // db partial of this split: the 16 threads of one float4 column meet in LDS, summed in row order
+  float* dpart = reinterpret_cast<float*>(lds);  // staging is done (barrier above)
+  if (do_db) {
+    reinterpret_cast<float4*>(dpart)[r0 * 20 + c4] = dsum;
+    __syncthreads();
+    if (t < kSdwT) {
+      float v = 0.f;
+      for (int rr = 0; rr < 16; ++rr) v += dpart[rr * kSdwT + t];
+      dpart[16 * kSdwT + t] = v;
+    }
+    __syncthreads();
+  }
+  HgemmArgs ep;
+  ep.alpha = a.alpha;
+  ep.bias = nullptr;
+  ep.out_scale = a.out_scale;
+  const int c = lane & 15;
+  auto store_out = [&](const f32x4 (&v)[5]) {
+    const int o = o0 + 16 * w + c;
+    if (o >= a.O) return;
+#pragma unroll
+    for (int kb = 0; kb < 5; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + 16 * kb + 4 * g + r;
+        if (k < a.K) a.dW[(int64_t)k * a.O + o] = MODE == 0 ? h16_epi(v[kb][r], 0.f, ep) : v[kb][r];
+      }
+  };
+  if (a.S == 1) {
+    store_out(acc);
+    if (do_db && t < kSdwT && o0 + t < a.O) a.db[o0 + t] = dpart[16 * kSdwT + t];
+    return;
+  }
+  // hand-off: slab [tile][split][wave][kb][lane][4] (+ db slab [to][split][80]),
+  // write-through stores, then one arrival per workgroup on the tile counter
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  float* tile_slab = a.slab + (int64_t)tile * a.S * (kSdwT * kSdwT);
+  {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        tile_slab + (int64_t)split * (kSdwT * kSdwT), 0, kSdwT * kSdwT * 4, 0x00020000);
+#pragma unroll
+    for (int kb = 0; kb < 5; ++kb)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[kb]), rs, ((w * 5 + kb) * 64 + lane) * 16, 0,
+                                             16 /* sc1 */);
+    if (do_db && t < kSdwT / 4) {
+      const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+          a.db_slab + ((int64_t)to * a.S + split) * kSdwT, 0, kSdwT * 4, 0x00020000);
+      const f32x4 v = reinterpret_cast<const f32x4*>(dpart + 16 * kSdwT)[t];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rb, t * 16, 0, 16 /* sc1 */);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const int old = __hip_atomic_fetch_add(&a.cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == a.S - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&a.cnt[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+    }
+    flag = last;
+  }
+  __syncthreads();
+  if (!flag) return;
+  f32x4 sum[5];
+#pragma unroll
+  for (int kb = 0; kb < 5; ++kb) sum[kb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const f32x4* base = reinterpret_cast<const f32x4*>(tile_slab) + w * 5 * 64 + lane;
+  for (int sp = 0; sp < a.S; ++sp) {
+    const f32x4* src = base + (int64_t)sp * (kSdwT * kSdwT / 4);
+#pragma unroll
+    for (int kb = 0; kb < 5; ++kb) sum[kb] += src[kb * 64];
+  }
+  store_out(sum);
+  if (do_db && t < kSdwT && o0 + t < a.O) {
+    const float* src = a.db_slab + (int64_t)to * a.S * kSdwT + t;
+    float v = 0.f;
+    for (int sp = 0; sp < a.S; ++sp) v += src[(int64_t)sp * kSdwT];
+    a.db[o0 + t] = v;
+  }
 }
 
 // column sums of a [batch][M][N] strided matrix into out[batch][N] (+=): bias
@@ -1549,6 +1937,37 @@ bool launch_sfc(const float* A, const void* Bk_, int M, int Nd, int Kd, float a_
   const int tiles = ((Nd + kSfcBN - 1) / kSfcBN) * ((M + kSfcBM - 1) / kSfcBM);
   hipLaunchKernelGGL(k_sfc, dim3(tiles), dim3(256), 0, s, A, Bk, M, Nd, Kd, a_scale, bias, alpha, bias_scale, out_scale,
                      out);
+  return true;
+}
+
+bool launch_f3gemm_nt(const float* A, const void* Bh, const void* Bl, int M, int Nd, int Kd, float* out,
+                      hipStream_t s) {
+  if ((Kd % 8) != 0 || ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(Bh) |
+                         reinterpret_cast<uintptr_t>(Bl)) & 15) != 0)
+    return false;
+  if ((int64_t)M * Nd == 0) return true;
+  const int tiles = ((Nd + kSfcBN - 1) / kSfcBN) * ((M + kSfcBM - 1) / kSfcBM);
+  hipLaunchKernelGGL(k_f3gemm_nt, dim3(tiles), dim3(256), 0, s, A, static_cast<const short*>(Bh),
+                     static_cast<const short*>(Bl), M, Nd, Kd, out);
+  return true;
+}
+
+bool launch_sfc_dw(const SfcDwArgs& a0, hipStream_t s) {
+  const uintptr_t al = reinterpret_cast<uintptr_t>(a0.x) | reinterpret_cast<uintptr_t>(a0.d);
+  if (a0.K % 4 || a0.O % 4 || a0.ldx % 4 || a0.ldd % 4 || (al & 15)) return false;
+  if ((int64_t)a0.K * a0.O == 0) return true;
+  SfcDwArgs a = a0;
+  a.ntk = (a.K + kSdwT - 1) / kSdwT;
+  a.nto = (a.O + kSdwT - 1) / kSdwT;
+  if (a.N == 0) a.S = 1;
+  if (a.S > 1 && (a.chunk % 64 || (int64_t)(a.S - 1) * a.chunk >= a.N || !a.slab || !a.cnt ||
+                  (a.db && !a.db_slab)))
+    return false;
+  if (a.S == 1) a.chunk = a.N;
+  if (a.mode == 1)
+    hipLaunchKernelGGL(k_sfc_dw<1>, dim3(a.ntk * a.nto * a.S), dim3(kSdwNT), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_sfc_dw<0>, dim3(a.ntk * a.nto * a.S), dim3(kSdwNT), 0, s, a);
   return true;
 }
 

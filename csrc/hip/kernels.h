@@ -244,6 +244,7 @@ struct IpcPeers {
   unsigned int* arrive;  // own, device
   unsigned int* depart;  // own, device
   int* err;              // own, device: 1 = a wait timed out (sticky)
+  int fence;             // 1: also a system-scope release / acquire per block (PBX_IPC_FENCE=1)
 };
 // send / dst [world][slot_bytes]; counts (device [world], nullable = whole
 // slots) of rec_bytes records go to each peer; the received records land in
@@ -251,6 +252,19 @@ struct IpcPeers {
 // fill_tail writes 0xFF over the rest of each dst slot
 void launch_ipc_exchange(const IpcPeers& pt, const void* send, void* dst, const int32_t* counts, int64_t rec_bytes,
                          bool fill_tail, int32_t* rcounts, int blocks, hipStream_t s);
+// the sharded pull's key exchange with the owner pack fused in (ipc.hip
+// k_ipc_pack_exchange): uniq_h [*u_count] keys -> owners' inbox slots, send_index
+// [u] = owner * cap + position, ocnt (zeroed on entry) = per-owner counts, dst
+// [world][cap] keys received (tail -1), rcounts [world] received counts
+void launch_ipc_pack_exchange(const IpcPeers& pt, const uint64_t* uniq_h, const int32_t* u_count, int64_t cap,
+                              int64_t* send_index, int32_t* ocnt, int32_t* overflow, uint64_t* dst, int32_t* rcounts,
+                              int blocks, hipStream_t s);
+// the sharded pull's answer exchange with the owner probe + gather fused in
+// (ipc.hip k_ipc_answer_exchange): recv [world][cap] keys of rcnt[src] valid
+// each -> rows [world * cap] (-1 past the counts), answers of rec floats into
+// the askers' inboxes, dst [world][cap][rec] the answers to this rank's keys
+void launch_ipc_answer_exchange(const IpcPeers& pt, const TableDev& t, const uint64_t* recv, const int32_t* rcnt,
+                                int64_t cap, int rec, int64_t* rows, float* dst, int blocks, hipStream_t s);
 // out = scale * sum over ranks of src (n floats; out may alias src)
 void launch_ipc_allreduce(const IpcPeers& pt, const float* src, float* out, int64_t n, float scale, bool two_phase,
                           int blocks, hipStream_t s);
@@ -822,6 +836,33 @@ bool launch_sfc(const float* A, const void* Bk_, int M, int Nd, int Kd, float a_
 void launch_h16_epi(const float* acc, const float* bias, int M, int N, float alpha, float bias_scale, float out_scale,
                     float* out, hipStream_t s);
 void launch_hgemm(const HgemmArgs& g, hipStream_t s);
+// scaled_fc weight + bias gradient in one launch (k_sfc_dw): dW [K][O] =
+// h16_epi(fp16(x * a_scale)^T fp16(d * b_scale)) over n < N, db [O] = colsum(d)
+// (db may be null).  80 x 80 tiles split S ways over n (chunk rows each, a
+// multiple of 64); slab: ntk * nto * S * 6400 + nto * S * 80 floats; cnt:
+// ntk * nto zeroed ints, left zeroed by the launch.  (false: K or O not a
+// multiple of 4, or operands not 16-B aligned -- the caller takes k_hgemm.)
+struct SfcDwArgs {
+  const float* x = nullptr;
+  const float* d = nullptr;
+  float* dW = nullptr;
+  float* db = nullptr;
+  float* slab = nullptr;
+  float* db_slab = nullptr;
+  int* cnt = nullptr;
+  int N = 0, K = 0, O = 0;
+  int64_t ldx = 0, ldd = 0;
+  int ntk = 0, nto = 0, S = 1, chunk = 0;
+  float a_scale = 1.f, b_scale = 1.f, alpha = 1.f, out_scale = 1.f;
+  int mode = 0;  // 0: scaled_fc fp16 chain; 1: fp32 as three bf16 products (scales / epilogue unused)
+};
+inline int sfc_dw_tiles(int K, int O) { return ((K + 79) / 80) * ((O + 79) / 80); }
+inline int sfc_dw_chunk(int N, int S) { return ((N + S - 1) / S + 63) / 64 * 64; }
+bool launch_sfc_dw(const SfcDwArgs& a, hipStream_t s);
+// out [M][Nd] = A [M][Kd] fp32 @ (Bh + Bl)^T with B's bf16 split [Nd][Kd] (k_f3gemm_nt:
+// three bf16 MFMA products, fp32 accumulate; false: Kd % 8 != 0 or misaligned operands)
+bool launch_f3gemm_nt(const float* A, const void* Bh, const void* Bl, int M, int Nd, int Kd, float* out,
+                      hipStream_t s);
 void launch_colsum_strided(const float* x, int batch, int M, int N, int64_t sb, int64_t ld, float* out, int64_t so,
                            bool accumulate, hipStream_t s);
 void launch_i8_quant(const float* x, int R, int C, int ldo, float expand, float clip, float range, bool transpose,

@@ -883,6 +883,19 @@ def _half_of(W: torch.Tensor, transposed: bool = False) -> torch.Tensor:
     return W16
 
 
+def _sfc_dw_splits(N: int, K: int, O: int) -> int:
+    """Workgroups per 80 x 80 dW tile of k_sfc_dw (split-K over the batch):
+    about one workgroup per CU over the whole launch, at least 256 rows of
+    the batch each; PBX_SFC_DW_SPLIT overrides."""
+    env = os.environ.get("PBX_SFC_DW_SPLIT", "")
+    if env:
+        return max(1, int(env))
+    tiles = ((K + 79) // 80) * ((O + 79) // 80)
+    # ~200 workgroups (one per CU): N = 8192, 400 x 400 (25 tiles) -> 8 splits,
+    # 25.5 us vs 28.5 at 16 and 34.6 at 20 (profiles/r6_ctr_bwd_kernels.txt)
+    return max(1, min(200 // tiles, N // 256, 64))
+
+
 class _ScaledFc(torch.autograd.Function):
     """scaled_fc (operators/scaled_fc_op.cu:144-330) with the reference's
     fp16 arithmetic on fp16 MFMA (csrc/hip/ctr_ext.hip k_hgemm):
@@ -942,6 +955,9 @@ class _ScaledFc(torch.autograd.Function):
             dW = W.new_empty(K, O)
             db = dy.new_empty(O)
             dx = h.sfc(dy, _half_of(W), None, gs / in_scale, in_scale, 1.0, 1.0 / gs)
+            if dx is not None and h.sfc_dw(x, dy, dW, db, 1.0, gs / in_scale, in_scale, 1.0 / gs, _sfc_dw_splits(N, K, O)):
+                # dW and db in one launch (k_sfc_dw: split-K over N with a fixed-order reduce)
+                return dx, dW, db.reshape(ctx.bshape), None, None, None
             if dx is not None:
                 with torch.cuda.stream(side):
                     # ~512 rows of N per split (scripts/micro/dw_gemm_sweep.py at
@@ -1030,23 +1046,55 @@ class _ScaledInt8Fc(torch.autograd.Function):
         x, W = ctx.saved_tensors
         if x.is_cuda:
             # the reference straight-through backward is two fp32 GEMMs
-            # (scaled_int8fc_op.cu:382-440): library fp32 GEMMs (hipBLASLt)
-            # and the column sum, on _ctr_side's stream choice
+            # (scaled_int8fc_op.cu:382-440), which its cuBLAS runs in TF32 in
+            # training (gpu_context.cc:61-67, enable_cublas_tf32_op_math on).
+            # Default here: exact fp32 library GEMMs (dW split-K batched with
+            # a fixed-order sum).  PBX_INT8FC_BWD=bf16x3: both as three bf16
+            # MFMA products of the operands' bf16 splits (~2^-16 relative per
+            # product, tighter than TF32): dx in k_f3gemm_nt against W's split
+            # (cached per optimizer step), dW + db in one k_sfc_dw launch --
+            # measured slower than the library so far (dx 37 vs 36 us, dW 63
+            # vs ~40 at 8192 x 512 x 512, profiles/r6_ctr_bwd_kernels.txt).
             dy = dy.float().contiguous()
+            N, O = dy.shape
+            K = x.shape[1]
+            dW = torch.empty_like(W)
+            db = dy.new_empty(O)
+            h = _native.hip()
+            if os.environ.get("PBX_INT8FC_BWD", "fp32") == "bf16x3":
+                Wh, Wl = _bf16_split_of(W)
+                dx = h.f3gemm_nt(dy, Wh, Wl)
+                if dx is not None and h.sfc_dw(x, dy, dW, db, 1.0, 1.0, 1.0, 1.0, _sfc_dw_splits(N, K, O), mode=1):
+                    return dx, dW, db.reshape(ctx.bshape), None
             cur = torch.cuda.current_stream(dy.device)
             side = _ctr_side(dy.device, want=False)
             side.wait_stream(cur)
-            N, O = dy.shape
-            dW = torch.empty_like(W)
-            db = dy.new_empty(O)
             dx = torch.mm(dy, W.t())
             with torch.cuda.stream(side):
                 _mm_tn_splitk(x, dy, dW)
-                _native.hip().colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
+                h.colsum_strided(dy, 1, N, O, 0, O, db, 0, False)
             cur.wait_stream(side)
         else:
             dx, dW, db = dy @ W.t(), x.t() @ dy, dy.sum(0)
         return dx, dW, db.reshape(ctx.bshape), None
+
+
+def _bf16_split_of(W: torch.Tensor):
+    """(hi, lo) bf16 split of an fp32 weight, W = hi + lo + O(2^-17 |W|)
+    (round-to-nearest-even both times), cached on the tensor until it is
+    modified in place -- one split per optimizer step."""
+    key = (W._version, W.data_ptr(), tuple(W.shape))
+    c = getattr(W, "_pbx_bf16_split", None)
+    if c is not None and c[0] == key:
+        return c[1]
+    Wd = W.detach().contiguous()
+    hi = Wd.to(torch.bfloat16)
+    lo = (Wd - hi.float()).to(torch.bfloat16)
+    try:
+        setattr(W, "_pbx_bf16_split", (key, (hi, lo)))
+    except (AttributeError, RuntimeError):
+        pass
+    return hi, lo
 
 
 def _mm_tn_splitk(x: torch.Tensor, dy: torch.Tensor, out: torch.Tensor) -> torch.Tensor:

@@ -214,6 +214,19 @@ class IpcMesh:
             self.comm.exchange(send, dst, counts, int(rec_bytes), bool(fill_tail), rcounts)
         return dst
 
+    def pack_exchange(self, uniq_h: torch.Tensor, u_count: torch.Tensor, cap: int, send_index: torch.Tensor,
+                      ocnt: torch.Tensor, overflow: torch.Tensor, dst: torch.Tensor,
+                      rcounts: torch.Tensor) -> torch.Tensor:
+        """The sharded pull's key exchange with the owner pack fused in: the
+        unique keys uniq_h[:u_count[0]] go straight to their owners' inbox
+        slots (send_index[u] = owner * cap + position, ocnt = per-owner
+        counts, zero on entry); dst [world, cap] receives every peer's keys
+        (tail -1), rcounts their counts.  One launch instead of pack + send
+        buffer + exchange (ipc.hip k_ipc_pack_exchange)."""
+        with self._serial("pack_exchange"):
+            self.comm.pack_exchange(uniq_h, u_count, int(cap), send_index, ocnt, overflow, dst, rcounts)
+        return dst
+
     def error(self) -> bool:
         """True once any wait on this mesh timed out (device read: syncs)."""
         return bool(int(self.state[2].item()) != 0)

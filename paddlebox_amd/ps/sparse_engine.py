@@ -51,6 +51,18 @@ from .feature_types import FeatureCodec
 from .gpu_table import GpuSparseTable
 from ..runtime.streams import side_stream
 
+# sharded pull over the IPC mesh, PBX_PACK_EXCHANGE=1: the owner pack inside
+# the key exchange's put phase (ipc.hip k_ipc_pack_exchange) and the owner's
+# probe + gather inside the answer exchange (k_ipc_answer_exchange).  Off by
+# default: measured slower than pack -> exchange -> probe + gather -> exchange
+# (1-rank rehearsal 0.390-0.391 vs 0.380-0.381 ms/step,
+# profiles/r6_sharded_rehearsal.txt) -- the fused puts scatter 8-B keys and
+# 48-B records into the uncached inbox one transaction each, where the plain
+# exchange streams a packed buffer in full 16-B lanes, and the fused kernels
+# run on the exchange's co-resident grid instead of a grid per key
+def _pack_exchange() -> bool:
+    return os.environ.get("PBX_PACK_EXCHANGE", "0") == "1"
+
 
 @dataclass
 class SeqpoolParams:
@@ -855,11 +867,21 @@ class SparseEngine:
         h = self._hip
         ws = sl.ws
         ipc = self.xmesh is not None
+        fused = (ipc and _pack_exchange() and hasattr(self.xmesh[0].comm, "pack_exchange")
+                 and hasattr(self.table.t, "answer_exchange"))
         st = PullState(B=B, S=S, L=L, lod=lod, uid=ws.uid, perm=ws.perm, counts=ws.u_count, slot=sl, gen=sl.gen)
         # sharded: pack per-owner, exchange keys, owner-side dedup/probe/gather
-        h.shard_pack_hash(ws.uniq_h, ws.u_count, self.world, self.C, sl.send, sl.send_index, sl.ocnt, self.overflow,
-                          ipc)
-        if self.xmesh is not None:
+        if fused:
+            # the pack inside the key exchange's put phase: the dedup output
+            # goes straight to the owners' inboxes (no send buffer)
+            self.xmesh[0].pack_exchange(ws.uniq_h, ws.u_count, self.C, sl.send_index, sl.ocnt, self.overflow,
+                                        sl.recv.view(self.world, -1), sl.rcnt)
+        else:
+            h.shard_pack_hash(ws.uniq_h, ws.u_count, self.world, self.C, sl.send, sl.send_index, sl.ocnt,
+                              self.overflow, ipc)
+        if fused:
+            pass  # keys already exchanged
+        elif self.xmesh is not None:
             # only the valid keys of each peer slot travel; the receiver
             # fills the rest of its slots with -1 (padding for the dedup)
             self.xmesh[0].exchange(sl.send.view(self.world, -1), sl.recv.view(self.world, -1), sl.ocnt, 8, True,
@@ -870,6 +892,16 @@ class SparseEngine:
             # owner answers in one launch: probe + record copy per received
             # key, no dedup (a key asked by several peers is read twice)
             rows_r = sl.rows_recv
+            if fused and not (self.auto_insert and not self.test_mode):
+                # ... straight into the askers' inboxes inside the answer
+                # exchange (no answer buffer in between)
+                m = self.xmesh[1]
+                with m._serial("answer_exchange"):
+                    self.table.t.answer_exchange(m.comm.peers_ptr(), m.comm.blocks(), sl.recv, sl.rcnt, self.C,
+                                                 rows_r, sl.resp_back)
+                st.send_index = sl.send_index[:L]
+                st.rows_r = rows_r
+                return st
             self.table.t.probe_gather(sl.recv, rows_r, sl.resp)
             if self.auto_insert and not self.test_mode:
                 miss = (rows_r < 0) & (sl.recv != -1)

@@ -55,6 +55,10 @@ def main():
         out[f"hgemm_dW_split{sp}"] = timed(
             lambda sp=sp: h.hgemm(x, dy, dW, None, K, O, N, [1, K], [O, 1], O, 1.0, gs / in_scale, in_scale, 1.0,
                                   1.0 / gs, sp))
+    for sp in (1, 8, 12, 16, 19, 24, 32, 48):
+        out[f"sfc_dw_split{sp}"] = timed(
+            lambda sp=sp: h.sfc_dw(x, dy, dW, db, 1.0, gs / in_scale, in_scale, 1.0 / gs, sp))
+    out["sfc_dw_default_split"] = cx._sfc_dw_splits(N, K, O)
     out["torch_mm_fp32_dW"] = timed(lambda: x.t() @ dy)
     out["torch_mm_fp32_dx"] = timed(lambda: dy @ W.t())
     out["torch_sum_db"] = timed(lambda: dy.sum(0))
@@ -65,6 +69,13 @@ def main():
     dy2 = torch.randn(N2, O2, device=DEV)
     out["i8_ksgemm_bwd"] = timed(lambda: cx._fc_backward_hip(x2, W2, dy2))
     out["i8_torch_bwd"] = timed(lambda: (dy2 @ W2.t(), x2.t() @ dy2, dy2.sum(0)))
+    Wh, Wl = cx._bf16_split_of(W2)
+    out["i8_f3_dx"] = timed(lambda: h.f3gemm_nt(dy2, Wh, Wl))
+    dW2, db2 = W2.new_empty(K2, O2), dy2.new_empty(O2)
+    for sp in (4, 8, 10, 16):
+        out[f"i8_f3_dw_split{sp}"] = timed(lambda sp=sp: h.sfc_dw(x2, dy2, dW2, db2, 1.0, 1.0, 1.0, 1.0, sp, mode=1))
+    out["i8_f3_dw_default_split"] = cx._sfc_dw_splits(N2, K2, O2)
+    out["i8_torch_dx"] = timed(lambda: dy2 @ W2.t())
     print(json.dumps(out), flush=True)
 
 

@@ -167,6 +167,36 @@ def test_scaled_fc_gpu(shape):
     torch.testing.assert_close(bg.grad.cpu(), bc.grad, rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("shape,splits", [((8192, 400, 400), 19), ((777, 132, 36), 3), ((777, 132, 36), 1),
+                                          ((4096, 512, 256), 16), ((100, 8, 404), 1), ((3000, 84, 168), 7)])
+def test_scaled_fc_dw_kernel(shape, splits):
+    """k_sfc_dw (scaled_fc dW + db in one launch, split-K over the batch with
+    a fixed-order slab reduce) against the fp16 rounding chain in torch (fp64
+    accumulation): one fp16 ulp of the epilogue; db to fp32 summation order;
+    two launches bit-identical (no atomics in the sums)."""
+    from paddlebox_amd import _native
+
+    N, K, O = shape
+    g = torch.Generator().manual_seed(N + K + O)
+    x = torch.randn(N, K, generator=g)
+    d = torch.randn(N, O, generator=g) * 0.02
+    in_scale, gs = 8.0, 256.0
+    h = _native.hip()
+    xg, dg = x.to(DEV), d.to(DEV)
+    outs = []
+    for _ in range(2):
+        dW, db = torch.full((K, O), float("nan"), device=DEV), torch.full((O,), float("nan"), device=DEV)
+        assert h.sfc_dw(xg, dg, dW, db, 1.0, gs / in_scale, in_scale, 1.0 / gs, splits)
+        outs.append((dW.cpu(), db.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    hf = torch.float16
+    acc = x.to(hf).double().t() @ (d * (gs / in_scale)).to(hf).double()
+    ref = (float(torch.tensor(in_scale, dtype=hf)) * acc.float()).to(hf).float() * (1.0 / gs)
+    scale = float(ref.abs().max()) + 1e-6
+    torch.testing.assert_close(outs[0][0], ref, rtol=2e-3, atol=2e-3 * scale)
+    torch.testing.assert_close(outs[0][1], d.double().sum(0).float(), rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("shape", [(1, 1, 1), (257, 100, 65), (64, 32, 64)])
 def test_scaled_int8fc_gpu_exact(shape):
     """int8 MFMA accumulation is exact: the GPU result equals the fp64 oracle
@@ -181,10 +211,17 @@ def test_scaled_int8fc_gpu_exact(shape):
     torch.testing.assert_close(yg.cpu(), yc, rtol=1e-6, atol=1e-5)
 
 
-@pytest.mark.parametrize("shape", [(4096, 96, 80), (1500, 64, 32), (300, 20, 10)])
-def test_scaled_int8fc_gpu_backward(shape):
-    """The fp32 straight-through backward: dx = dy W^T, dW = x^T dy (split-K
-    batched GEMMs + fixed-order sum at N >= 1024), db = colsum(dy)."""
+@pytest.mark.parametrize("shape", [(4096, 96, 80), (1500, 64, 32), (300, 20, 10), (8192, 512, 512), (777, 136, 44)])
+@pytest.mark.parametrize("mode", ["bf16x3", "fp32"])
+def test_scaled_int8fc_gpu_backward(shape, mode, monkeypatch):
+    """The straight-through backward: dx = dy W^T, dW = x^T dy, db = colsum(dy).
+    fp32: library GEMMs (split-K batched + fixed-order sum for dW), fp32-close
+    to the fp64 oracle (the default).  bf16x3: three bf16 MFMA products of the
+    operands' bf16 splits -- every element within 2^-14 of the sum of |terms|
+    (the GEMM error bound), and no worse than the TF32 arithmetic the
+    reference's cuBLAS runs this GEMM in (10-bit mantissa operands, emulated
+    here in fp64)."""
+    monkeypatch.setenv("PBX_INT8FC_BWD", mode)
     N, K, O = shape
     g = torch.Generator().manual_seed(N)
     x, W, b = torch.randn(N, K, generator=g), torch.randn(K, O, generator=g) * 0.2, torch.randn(O, generator=g)
@@ -194,9 +231,22 @@ def test_scaled_int8fc_gpu_backward(shape):
     d = torch.randn(N, O, generator=g)
     cx.scaled_int8fc(xc, wc, bc, a).backward(d.double())
     cx.scaled_int8fc(xg, wg, bg, a).backward(d.to(DEV))
-    _close(xg.grad, xc.grad, rtol=1e-5, atol=1e-4)
-    _close(wg.grad, wc.grad, rtol=1e-5, atol=1e-3)
     _close(bg.grad, bc.grad, rtol=1e-5, atol=1e-4)
+    if mode == "fp32":
+        _close(xg.grad, xc.grad, rtol=1e-5, atol=1e-4)
+        _close(wg.grad, wc.grad, rtol=1e-5, atol=1e-3)
+        return
+
+    def tf32(t):  # round to a 10-bit mantissa (nearest): the TF32 operand format
+        m, e = torch.frexp(t.double())
+        return torch.ldexp(torch.round(m * 2048) / 2048, e)
+
+    xd, wd, dd = x.double(), W.double(), d.double()
+    for got, ref, bound, tf in ((xg.grad, xc.grad, dd.abs() @ wd.abs().t(), tf32(dd) @ tf32(wd).t()),
+                                (wg.grad, wc.grad, xd.abs().t() @ dd.abs(), tf32(xd).t() @ tf32(dd))):
+        err = (got.cpu().double() - ref.double()).abs()
+        assert bool((err <= 2.0 ** -14 * bound + 1e-6).all()), float((err / (bound + 1e-30)).max())
+        assert float(err.max()) <= float((tf - ref.double()).abs().max()), (float(err.max()),)
 
 
 @pytest.mark.parametrize("use_cvm", [True, False])
