@@ -15,9 +15,7 @@ namespace {
 constexpr int kTile = 64;
 
 __device__ __forceinline__ unsigned short f2bf_c(float f) {
-  unsigned int u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));  // v_cvt_pk_bf16_f32, RNE
 }
 
 __global__ __launch_bounds__(256) void k_cross_dot(const float* __restrict__ x, int M, int N, int ld,

@@ -31,11 +31,10 @@ __host__ __device__ inline int head_ys_width(int C, int Cp) {
 }
 
 __device__ __forceinline__ unsigned short f2bf(float f) {
-  // round-to-nearest-even
-  unsigned int u = __float_as_uint(f);
-  const unsigned int lsb = (u >> 16) & 1u;
-  u += 0x7FFFu + lsb;
-  return (unsigned short)(u >> 16);
+  // v_cvt_pk_bf16_f32 (gfx950): round-to-nearest-even in one instruction per
+  // pair -- the same bits as the integer rounding (u + 0x7fff + lsb) >> 16
+  // for every finite input, at a quarter of the VALU work
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));
 }
 __device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(((unsigned int)h) << 16); }
 

@@ -45,9 +45,10 @@ constexpr int PF = 6;     // default weight-fragment prefetch depth (k-steps; PB
 constexpr int kMpAlign = 128;
 
 __device__ __forceinline__ u16 f2bf(float f) {
-  unsigned int u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (u16)(u >> 16);
+  // v_cvt_pk_bf16_f32 (gfx950): round-to-nearest-even in one instruction per
+  // pair -- the same bits as the integer rounding (u + 0x7fff + lsb) >> 16
+  // for every finite input, at a quarter of the VALU work
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));
 }
 __device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float(((unsigned int)h) << 16); }
 
@@ -649,6 +650,17 @@ __global__ __launch_bounds__(256) void k_adam_fused(float* __restrict__ p, float
 }
 
 
+// A per-layer pointer out of the kernel-argument arrays by a uniform layer
+// index: a select chain (s_cselect) instead of dynamic indexing, which made
+// hipcc copy the argument arrays to scratch and reload from it
+template <typename T>
+__device__ __forceinline__ T pick_layer(T const (&arr)[kMaxMlpLayers], int i) {
+  T r = arr[0];
+#pragma unroll
+  for (int j = 1; j < kMaxMlpLayers; ++j) r = (i == j) ? arr[j] : r;
+  return r;
+}
+
 // ---------------------------------------------------------------- DCN-V2 cross forward
 // x_{l+1} = x_0 * (x_l W_l^T + b_l) + x_l for l < L, then s = x_L . w_c,
 // one 512-thread workgroup per 32-row tile (kernels.h CrossFwdArgs).
@@ -658,7 +670,8 @@ __device__ __forceinline__ int cross_ldf(int P) { return P + 4; }
 template <int PFv>
 __global__ __launch_bounds__(TNT) void k_cross_fwd(CrossFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
-  const int P = a.Np > a.Kp ? a.Np : a.Kp;
+  const int Np = a.Np, Kp = a.Kp;
+  const int P = Np > Kp ? Np : Kp;
   const int ldl = cross_ldl(P), ldf = cross_ldf(P);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int m0 = blockIdx.x * TBM;
@@ -672,7 +685,7 @@ __global__ __launch_bounds__(TNT) void k_cross_fwd(CrossFwdArgs a) {
 #pragma unroll
   for (int j = 0; j < WO; ++j) wo[j] = lane + 64 * j < a.D ? a.wc[lane + 64 * j] : 0.f;
   {  // stage x_0: bf16 (epilogue operand + first A operand) and its fp32 residual
-    const int c8n = a.Kp / 8;
+    const int c8n = Kp / 8;
     for (int i = tid; i < TBM * c8n; i += TNT) {
       const int r = i / c8n, c = i - r * c8n;
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -685,26 +698,29 @@ __global__ __launch_bounds__(TNT) void k_cross_fwd(CrossFwdArgs a) {
     }
   }
   __syncthreads();
-  const int NB = a.Np / 32, KS = a.Kp / 16;
+  const int NB = Np / 32, KS = Kp / 16;
   // m-packed x_0 (the layer-0 dW operand): 8 rows of one column = 16 B
-  for (int i = tid; i < a.Np * (TBM / 8); i += TNT) {
+  for (int i = tid; i < Np * (TBM / 8); i += TNT) {
     const int n = i / (TBM / 8), g8 = i - n * (TBM / 8);
     unsigned int pk[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       pk[e] = (unsigned)x0b[(8 * g8 + 2 * e) * ldl + n] | ((unsigned)x0b[(8 * g8 + 2 * e + 1) * ldl + n] << 16);
     const int r0 = 8 * g8;
-    *reinterpret_cast<uint4*>(a.xmp[0] + mp_off(m0 / 16 + r0 / 16, NB, n >> 5, (n & 31) + 32 * ((r0 & 15) >> 3))) =
+    *reinterpret_cast<uint4*>(pick_layer(a.xmp, 0) + mp_off(m0 / 16 + r0 / 16, NB, n >> 5, (n & 31) + 32 * ((r0 & 15) >> 3))) =
         make_uint4(pk[0], pk[1], pk[2], pk[3]);
   }
   for (int l = 0; l < a.L; ++l) {
-    const bf16x8* wp = reinterpret_cast<const bf16x8*>(a.wp[l]);
+    const bf16x8* wp = reinterpret_cast<const bf16x8*>(pick_layer(a.wp, l));
+    const float* bias_l = pick_layer(a.bias, l);
+    float* z_l = pick_layer(a.z, l);
+    unsigned short* xmp_n = pick_layer(a.xmp, l + 1 < kMaxMlpLayers ? l + 1 : 0);
     const bool last = l + 1 == a.L;
     auto epi = [&](const f32x16& acc, int nb) {
       const int c = lane & 31, h = lane >> 5;
       const int n = nb * 32 + c;
       const bool nv = n < a.D;
-      const float bn = nv ? a.bias[l][n] : 0.f;
+      const float bn = nv ? bias_l[n] : 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         u16 o[4];
@@ -718,7 +734,7 @@ __global__ __launch_bounds__(TNT) void k_cross_fwd(CrossFwdArgs a) {
           o[t] = f2bf(xn);
           dst[r * ldl + n] = o[t];
           if (nv && m < a.M) {
-            a.z[l][(int64_t)m * a.ldf + n] = z;
+            z_l[(int64_t)m * a.ldf + n] = z;
             if (last) a.xlast[(int64_t)m * a.ldf + n] = xn;
           }
           if (m >= a.M) o[t] = 0;
@@ -727,7 +743,7 @@ __global__ __launch_bounds__(TNT) void k_cross_fwd(CrossFwdArgs a) {
           uint2 pk;
           pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
           pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
-          *reinterpret_cast<uint2*>(a.xmp[l + 1] + mp_off(m0 / 16 + (q >> 1), NB, nb, c + 32 * (q & 1)) + 4 * h) = pk;
+          *reinterpret_cast<uint2*>(xmp_n + mp_off(m0 / 16 + (q >> 1), NB, nb, c + 32 * (q & 1)) + 4 * h) = pk;
         }
       }
     };
@@ -827,22 +843,29 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
   // of loads in flight): g_L = ds w_c, u_{L-1} = bf16(x_0 g_L),
   // acc = z_{L-1} g_L, and the tile's dw_c partial sum_m ds x_L
   const int NB = P / 32, NS = P / 16;
+  const float* z_top = pick_layer(a.z, L - 1);
+  unsigned short* ump_top = pick_layer(a.ump, L - 1);
   float* bpart = a.bias_part + (int64_t)blockIdx.x * a.bias_ld;
   for (int n = tid; n < P; n += TNT) {
     const bool nv = n < a.D;
     const float wcn = nv ? a.wc[n] : 0.f;
     float p = 0.f, du = 0.f;
-    // all 32 rows' z / x_L loads in flight at once (64 per thread, before any use)
-    float zv[TBM], xv[TBM];
+    // 16 rows' z / x_L loads in flight at once (32 per thread, before any use;
+    // all 32 rows at once pushed the kernel past 256 VGPRs into scratch)
+    constexpr int TH = TBM / 2;
+#pragma unroll 1
+    for (int hr = 0; hr < TBM; hr += TH) {
+    float zv[TH], xv[TH];
 #pragma unroll
-    for (int e = 0; e < TBM; ++e) {
-      const int m = m0 + e;
+    for (int e = 0; e < TH; ++e) {
+      const int m = m0 + hr + e;
       const bool ok = nv && m < a.M;
-      zv[e] = ok ? a.z[L - 1][(int64_t)m * a.ldf + n] : 0.f;
+      zv[e] = ok ? z_top[(int64_t)m * a.ldf + n] : 0.f;
       xv[e] = ok ? a.xlast[(int64_t)m * a.ldf + n] : 0.f;
     }
 #pragma unroll
-    for (int r0 = 0; r0 < TBM; r0 += 8) {
+    for (int rh = 0; rh < TH; rh += 8) {
+      const int r0 = hr + rh;
       u16 uo[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -852,20 +875,23 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
         uo[e] = nv ? f2bf(bf2f(x0b[r * ldl + n]) * g) : (u16)0;
         src[r * ldl + n] = uo[e];
         du += bf2f(uo[e]);
-        as[r * ldf + n] = zv[r] * g;
-        p += dss[r] * xv[r];
+        as[r * ldf + n] = zv[rh + e] * g;
+        p += dss[r] * xv[rh + e];
       }
       // m-packed u_{L-1}: these 8 rows of column n are 16 contiguous bytes
-      *reinterpret_cast<uint4*>(a.ump[L - 1] + mp_off(m0 / 16 + r0 / 16, NB, n >> 5, (n & 31) + 32 * ((r0 & 15) >> 3))) =
+      *reinterpret_cast<uint4*>(ump_top + mp_off(m0 / 16 + r0 / 16, NB, n >> 5, (n & 31) + 32 * ((r0 & 15) >> 3))) =
           make_uint4((unsigned)uo[0] | ((unsigned)uo[1] << 16), (unsigned)uo[2] | ((unsigned)uo[3] << 16),
                      (unsigned)uo[4] | ((unsigned)uo[5] << 16), (unsigned)uo[6] | ((unsigned)uo[7] << 16));
+    }
     }
     bpart[(L - 1) * P + n] = du;
     if (nv) bpart[L * P + n] = p;
   }
   __syncthreads();
   for (int l = L - 1; l >= 0; --l) {
-    const bf16x8* wtp = reinterpret_cast<const bf16x8*>(a.wtp[l]);
+    const bf16x8* wtp = reinterpret_cast<const bf16x8*>(pick_layer(a.wtp, l));
+    const float* z_prev = pick_layer(a.z, l > 0 ? l - 1 : 0);
+    unsigned short* ump_prev = pick_layer(a.ump, l > 0 ? l - 1 : 0);
     auto epi = [&](const f32x16& acc, int kb, const float* zp) {
       const int c = lane & 31, h = lane >> 5;
       const int k = kb * 32 + c;
@@ -897,7 +923,7 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
           uint2 pk;
           pk.x = (unsigned)o[0] | ((unsigned)o[1] << 16);
           pk.y = (unsigned)o[2] | ((unsigned)o[3] << 16);
-          *reinterpret_cast<uint2*>(a.ump[l - 1] + mp_off(m0 / 16 + (q >> 1), NB, kb, c + 32 * (q & 1)) + 4 * h) = pk;
+          *reinterpret_cast<uint2*>(ump_prev + mp_off(m0 / 16 + (q >> 1), NB, kb, c + 32 * (q & 1)) + 4 * h) = pk;
         }
       }
       if (l > 0) {  // db_{l-1} partial: column sum of the tile's u_{l-1}
@@ -915,8 +941,8 @@ __global__ __launch_bounds__(TNT) void k_cross_bwd(CrossBwdArgs a) {
         const int r = 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
         const int m = m0 + r;
         const int k0 = kb0 * 32 + (lane & 31), k1 = kb1 * 32 + (lane & 31);
-        z0[e] = (l > 0 && m < a.M && k0 < a.D) ? a.z[l - 1][(int64_t)m * a.ldf + k0] : 0.f;
-        z1[e] = (l > 0 && two && m < a.M && k1 < a.D) ? a.z[l - 1][(int64_t)m * a.ldf + k1] : 0.f;
+        z0[e] = (l > 0 && m < a.M && k0 < a.D) ? z_prev[(int64_t)m * a.ldf + k0] : 0.f;
+        z1[e] = (l > 0 && two && m < a.M && k1 < a.D) ? z_prev[(int64_t)m * a.ldf + k1] : 0.f;
       }
       f32x16 acc0 = (f32x16){0}, acc1 = (f32x16){0};
       const bf16x8* w0p = wtp + (int64_t)kb0 * NS * 64 + lane;

@@ -954,10 +954,18 @@ class _ScaledFc(torch.autograd.Function):
             side.wait_stream(cur)
             dW = W.new_empty(K, O)
             db = dy.new_empty(O)
+            if K % 4 == 0 and O % 8 == 0:  # k_sfc_dw (K, O % 4) and the dx k_sfc (O % 8)
+                # dW and db in one launch (k_sfc_dw: split-K over N with a
+                # fixed-order reduce), on _ctr_side's stream beside dx when
+                # PBX_CTR_BWD_SIDE=1 (k_sfc_dw holds ~one workgroup per CU)
+                with torch.cuda.stream(side):
+                    ok = h.sfc_dw(x, dy, dW, db, 1.0, gs / in_scale, in_scale, 1.0 / gs, _sfc_dw_splits(N, K, O))
+                if ok:
+                    dx = h.sfc(dy, _half_of(W), None, gs / in_scale, in_scale, 1.0, 1.0 / gs)
+                    cur.wait_stream(side)  # (everything side touched is ordered before cur's later work)
+                    if dx is not None:
+                        return dx, dW, db.reshape(ctx.bshape), None, None, None
             dx = h.sfc(dy, _half_of(W), None, gs / in_scale, in_scale, 1.0, 1.0 / gs)
-            if dx is not None and h.sfc_dw(x, dy, dW, db, 1.0, gs / in_scale, in_scale, 1.0 / gs, _sfc_dw_splits(N, K, O)):
-                # dW and db in one launch (k_sfc_dw: split-K over N with a fixed-order reduce)
-                return dx, dW, db.reshape(ctx.bshape), None, None, None
             if dx is not None:
                 with torch.cuda.stream(side):
                     # ~512 rows of N per split (scripts/micro/dw_gemm_sweep.py at
