@@ -3,6 +3,10 @@
 #include <dirent.h>
 #include <fcntl.h>
 #include <omp.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -662,26 +666,51 @@ void SsdLog::open_segment() {
   if (fd < 0) throw std::runtime_error("SsdLog: cannot create " + s->path);
   s->fd = fd;
   segs_.push_back(std::move(s));
-  std::memset(active_buf_, 0xFF, (size_t)(seg_pages_ * kPage));
+  // no clearing of the whole mirror (a 0xFF memset of every segment's
+  // buffer on one thread): write_batch packs pages from slot 0 and fills the
+  // unused slots of a partly written last page with 0xFF before its flush,
+  // and nothing reads past the written slots (replay stops at empty keys)
 }
 
 void SsdLog::flush_pages(Seg* s, int64_t first_page, int64_t npages) {
   if (npages <= 0) return;
-  const char* src = active_buf_ + first_page * kPage;
-  const int64_t bytes = npages * kPage;
-  int64_t done = 0;
-  while (done < bytes) {
-    const ssize_t w = pwrite(s->fd, src + done, (size_t)(bytes - done), first_page * kPage + done);
-    if (w < 0 && errno == EINVAL && direct_) {
-      // O_DIRECT refused this write: fall back to buffered IO on this fd
-      int fl = fcntl(s->fd, F_GETFL);
-      fcntl(s->fd, F_SETFL, fl & ~O_DIRECT);
-      direct_ = false;
-      continue;
+  // large flushes as up to 8 concurrent pwrites of >= 4 MiB page ranges (an
+  // NVMe drive serves several writes in flight; one synchronous pwrite of a
+  // whole spill leaves it mostly idle)
+  constexpr int64_t kMinPages = 1024;
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(8, npages / kMinPages));
+  std::atomic<bool> failed{false};
+  auto write_range = [&](int64_t p0, int64_t np) {
+    const char* src = active_buf_ + p0 * kPage;
+    const int64_t bytes = np * kPage;
+    int64_t done = 0;
+    while (done < bytes) {
+      const ssize_t w = pwrite(s->fd, src + done, (size_t)(bytes - done), p0 * kPage + done);
+      if (w <= 0) {
+        failed = true;
+        return;
+      }
+      done += w;
     }
-    if (w <= 0) throw std::runtime_error("SsdLog: write failed");
-    done += w;
+  };
+  if (nt > 1) {
+#pragma omp parallel for num_threads(nt) schedule(static, 1)
+    for (int t = 0; t < nt; ++t) {
+      const int64_t b = npages * t / nt, e = npages * (t + 1) / nt;
+      write_range(first_page + b, e - b);
+    }
+  } else {
+    write_range(first_page, npages);
   }
+  if (failed && direct_) {
+    // O_DIRECT refused a write (e.g. tmpfs): buffered IO on this fd, once more
+    int fl = fcntl(s->fd, F_GETFL);
+    fcntl(s->fd, F_SETFL, fl & ~O_DIRECT);
+    direct_ = false;
+    failed = false;
+    write_range(first_page, npages);
+  }
+  if (failed) throw std::runtime_error("SsdLog: write failed");
 }
 
 // append records (tomb: deletions) in page-aligned batches, one pwrite per
@@ -696,7 +725,10 @@ void SsdLog::write_batch(const uint64_t* h, const float* vals, int64_t n, int vs
     const int64_t slot0 = s->slots;
     const int64_t first_page = page_of(slot0);
     const int64_t take = std::min<int64_t>(seg_pages_ * per_page_ - slot0, n - i);
-    // records land in consecutive slots: pack them in parallel
+    const size_t pbase = placed->size();
+    placed->resize(pbase + (size_t)take);
+    // records land in consecutive slots: pack them (and their index
+    // entries) in parallel
 #pragma omp parallel for schedule(static) if (take > 65536)
     for (int64_t j = 0; j < take; ++j) {
       const int64_t slot = slot0 + j;
@@ -710,10 +742,16 @@ void SsdLog::write_batch(const uint64_t* h, const float* vals, int64_t n, int vs
         std::memcpy(rec + 12, vals + (i + j) * vstride, (size_t)w * 4);
         if (w < stride_) std::memset(rec + 12 + (size_t)w * 4, 0, (size_t)(stride_ - w) * 4);
       }
+      (*placed)[pbase + (size_t)j] = std::make_pair(h[i + j], Loc{tomb ? -1 : s->id, slot});
     }
-    for (int64_t j = 0; j < take; ++j) placed->emplace_back(h[i + j], Loc{tomb ? -1 : s->id, slot0 + j});
     s->slots += take;
     i += take;
+    {  // unused slots of the last, partly written page read as empty (0xFF keys)
+      const int64_t end_slot = s->slots, page_end = (page_of(end_slot - 1) + 1) * per_page_;
+      if (end_slot < page_end)
+        std::memset(active_buf_ + page_of(end_slot - 1) * kPage + (end_slot % per_page_) * rec_bytes_, 0xFF,
+                    (size_t)((page_end - end_slot) * rec_bytes_));
+    }
     flush_pages(s, first_page, page_of(s->slots - 1) - first_page + 1);
   }
 }
@@ -722,26 +760,32 @@ void SsdLog::put(const uint64_t* h, const float* vals, int64_t n, int vstride) {
   std::lock_guard<std::mutex> lk(mu_);
   std::vector<std::pair<uint64_t, Loc>> placed;
   placed.reserve(n);
+  const auto t0 = std::chrono::steady_clock::now();
   write_batch(h, vals, n, vstride, false, &placed);
-  index_.reserve_more((int64_t)placed.size());
-  const size_t np = placed.size();
-  constexpr size_t kAhead = 16;  // the index is random access: prefetch ahead
-  for (size_t i = 0; i < np; ++i) {
-    if (i + kAhead < np) index_.prefetch(placed[i + kAhead].first);
-    const auto& kl = placed[i];
-    const int32_t old = index_.set(kl.first, kl.second);
-    if (old >= 0) segs_[old]->live--;
-    segs_[kl.second.seg]->live++;
+  const auto t1 = std::chrono::steady_clock::now();
+  // index updates shard-parallel; live counts from the returned previous
+  // segments (sequential over a few segments' counters)
+  std::vector<int32_t> old;
+  index_.set_many(placed, &old);
+  const auto t2 = std::chrono::steady_clock::now();
+  for (size_t i = 0; i < placed.size(); ++i) {
+    if (old[i] >= 0) segs_[old[i]]->live--;
+    segs_[placed[i].second.seg]->live++;
   }
+  if (getenv("PBX_SSD_TIMING"))
+    std::fprintf(stderr, "[ssd] put %lld: write %.3f s, index %.3f s, live %.3f s\n", (long long)n,
+                 std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count(),
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t2).count());
 }
 
 int64_t SsdLog::erase(const uint64_t* h, int64_t n) {
   std::lock_guard<std::mutex> lk(mu_);
   std::vector<uint64_t> dead;
+  std::vector<int32_t> old;
+  index_.erase_many(h, n, &old);  // shard-parallel
   for (int64_t i = 0; i < n; ++i) {
-    const int32_t old = index_.erase(h[i]);
-    if (old < 0) continue;
-    segs_[old]->live--;
+    if (old[(size_t)i] < 0) continue;
+    segs_[old[(size_t)i]]->live--;
     dead.push_back(h[i]);
   }
   std::vector<std::pair<uint64_t, Loc>> placed;

@@ -31,6 +31,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <omp.h>
+
 #include "../common/pbx_common.h"
 #include "runtime.h"
 
@@ -215,6 +217,80 @@ class LocIndex {
   int64_t n_ = 0;
 };
 
+// The SSD record index split into 64 independent LocIndex shards by the
+// key's top bits: bulk insert / erase of a spill (millions of keys per
+// write-back) run one shard per thread -- the single open-addressing table
+// took most of an 8.6M-row SsdLog::put in one thread.  Single-key calls keep
+// the LocIndex interface.
+class ShardedLocIndex {
+ public:
+  using Loc = LocIndex::Loc;
+  static constexpr int kShards = 64;
+  int64_t size() const {
+    int64_t n = 0;
+    for (const auto& s : sh_) n += s.size();
+    return n;
+  }
+  const Loc* find(uint64_t k) const { return sh_[shard(k)].find(k); }
+  int32_t set(uint64_t k, Loc l) { return sh_[shard(k)].set(k, l); }
+  int32_t erase(uint64_t k) { return sh_[shard(k)].erase(k); }
+  void prefetch(uint64_t k) const { sh_[shard(k)].prefetch(k); }
+  template <class F>
+  void for_each(F f) const {
+    for (const auto& s : sh_) s.for_each(f);
+  }
+  // old[i] = set(keys[i], locs[i]) for every i, shards in parallel
+  void set_many(const std::vector<std::pair<uint64_t, Loc>>& kl, std::vector<int32_t>* old) {
+    const int64_t n = (int64_t)kl.size();
+    old->assign((size_t)n, -1);
+    std::vector<std::vector<int64_t>> by(kShards);
+    bucket(n, [&](int64_t i) { return kl[(size_t)i].first; }, &by);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int q = 0; q < kShards; ++q) {
+      LocIndex& s = sh_[q];
+      s.reserve_more((int64_t)by[q].size());
+      const auto& ids = by[q];
+      for (size_t j = 0; j < ids.size(); ++j) {
+        if (j + 16 < ids.size()) s.prefetch(kl[(size_t)ids[j + 16]].first);
+        (*old)[(size_t)ids[j]] = s.set(kl[(size_t)ids[j]].first, kl[(size_t)ids[j]].second);
+      }
+    }
+  }
+  // old[i] = erase(keys[i]), shards in parallel
+  void erase_many(const uint64_t* keys, int64_t n, std::vector<int32_t>* old) {
+    old->assign((size_t)n, -1);
+    std::vector<std::vector<int64_t>> by(kShards);
+    bucket(n, [&](int64_t i) { return keys[i]; }, &by);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int q = 0; q < kShards; ++q)
+      for (int64_t i : by[q]) (*old)[(size_t)i] = sh_[q].erase(keys[i]);
+  }
+
+ private:
+  static int shard(uint64_t k) { return (int)((k * 0x9E3779B97F4A7C15ULL) >> 58); }
+  template <class K>
+  static void bucket(int64_t n, K key, std::vector<std::vector<int64_t>>* by) {
+    // per-thread buckets, concatenated in thread order: each shard's keys
+    // stay in input order (a repeated key keeps its last placement)
+    const int nt = n > 65536 ? std::max(1, std::min(16, omp_get_max_threads())) : 1;
+    std::vector<std::vector<std::vector<int64_t>>> part(nt, std::vector<std::vector<int64_t>>(kShards));
+#pragma omp parallel num_threads(nt)
+    {
+      const int t = omp_get_thread_num();
+      const int64_t b = n * t / nt, e = n * (t + 1) / nt;
+      for (int64_t i = b; i < e; ++i) part[t][shard(key(i))].push_back(i);
+    }
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int q = 0; q < kShards; ++q) {
+      size_t tot = 0;
+      for (int t = 0; t < nt; ++t) tot += part[t][q].size();
+      (*by)[q].reserve(tot);
+      for (int t = 0; t < nt; ++t) (*by)[q].insert((*by)[q].end(), part[t][q].begin(), part[t][q].end());
+    }
+  }
+  LocIndex sh_[kShards];
+};
+
 class SsdLog {
  public:
   SsdLog(const std::string& dir, int stride, int64_t segment_bytes = 64ll << 20);
@@ -269,7 +345,7 @@ class SsdLog {
   int64_t seg_pages_;
   bool direct_ = true;
   std::vector<std::unique_ptr<Seg>> segs_;  // segs_[i]->id == i (closed segments keep their fd)
-  LocIndex index_;
+  ShardedLocIndex index_;
   // the active segment is mirrored in memory (page-aligned, written through)
   char* active_buf_ = nullptr;
   mutable std::mutex mu_;

@@ -370,8 +370,11 @@ class TieredStore:
                     self.ssd.delete(mk)
                     self.stats["stage_ssd_delete_s"] += time.perf_counter() - t_d
                     self.stats["ssd_hits"] += int(mk.numel())
-                    rows = self.host.probe(hc)
-                    miss = rows < 0
+                    # the reloaded keys' host rows are known: no second probe
+                    # of every staged key
+                    at = miss.nonzero().squeeze(1)[found]
+                    rows[at] = r.to(rows.dtype)
+                    miss[at] = False
             known = ~miss
             kh = hc[known]
             buf = self._pinned("stage", (int(kh.numel()), self.host.stride), torch.float32)
