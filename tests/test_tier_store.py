@@ -161,3 +161,38 @@ def test_host_tier_spill_oldest_passes_first():
     t.clear()
     t._native.insert(passes[0])
     assert float(t.read(passes[0]).abs().sum()) == 0.0
+
+
+def test_ssd_log_bulk_sharded_index_duplicates_and_partial_pages(tmp_path):
+    """Bulk paths of the 64-shard SSD index (> 64K keys: per-thread bucketing,
+    shard-parallel set / erase): a key repeated inside one put keeps its LAST
+    record, erase of present + absent keys, and puts that end inside a page
+    (its unused slots must read as empty on replay now that a new segment's
+    mirror is no longer cleared up front) continue in the same page."""
+    d = str(tmp_path / "ssd")
+    s = SsdTier(d, STRIDE, segment_bytes=1 << 20)
+    h = _keys(150_000, 7)
+    n = h.numel()
+    v = torch.randn(n, STRIDE)
+    # one batch holding every key twice: the second copy (v + 1) wins
+    s.put(torch.cat([h, h]), torch.cat([v, v + 1]))
+    assert len(s) == n
+    f, got = s.get(h)
+    assert bool(f.all()) and torch.equal(got, v + 1)
+    # odd-sized puts: each ends inside a page, the next continues it
+    for a, b in ((0, 1001), (1001, 70_003), (70_003, n)):
+        s.put(h[a:b], v[a:b] * 2)
+    absent = _keys(80_000, 8)
+    absent = absent[~torch.isin(absent, h)]
+    gone = s._native.erase(torch.cat([h[: n // 3], absent]))
+    assert gone == n // 3
+    live = n - n // 3
+    assert len(s) == live
+    f, got = s.get(h)
+    assert int(f.sum()) == live and not bool(f[: n // 3].any())
+    assert torch.equal(got[f], v[f] * 2)
+    del s
+    s2 = SsdTier(d, STRIDE, segment_bytes=1 << 20)  # replay: same index, no phantom records
+    assert len(s2) == live
+    f2, got2 = s2.get(h)
+    assert torch.equal(f2, f) and torch.equal(got2[f2], v[f2] * 2)
