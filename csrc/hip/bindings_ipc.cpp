@@ -112,8 +112,10 @@ class IpcComm {
     p_.arrive = reinterpret_cast<unsigned int*>(st + 1);
     p_.depart = reinterpret_cast<unsigned int*>(st + 1) + 1;
     p_.err = reinterpret_cast<int*>(st + 2);
-    const char* f = std::getenv("PBX_IPC_FENCE");
-    p_.fence = (f && f[0] == '0') ? 0 : 1;
+    // the per-workgroup system-scope release / acquire stay on: without them
+    // (system-coherent inbox accesses alone) the payload self-test failed on
+    // a 10 MB, 16-block mesh (profiles/r6_ipc_exchange_bench.txt)
+    p_.fence = 1;
   }
   bool fence() const { return p_.fence != 0; }
   void set_peer(int p, int64_t inbox, int64_t flags) {

@@ -35,8 +35,8 @@
 // (hipDeviceMallocUncached), and a producer's s_waitcnt vmcnt(0) orders its
 // completed payload stores before its flag store -- and on top of that each
 // block still issues the system-scope release before it arrives and the
-// acquire after its wait (PBX_IPC_FENCE=0 drops the fences: measured equal on
-// the plain exchanges, 1-rank rehearsal 0.3805 vs 0.3801-0.3858 ms/step).
+// acquire after its wait (required: with the accesses alone the payload
+// self-test failed on one mesh shape, profiles/r6_ipc_exchange_bench.txt).
 // Failure: a wait that exceeds its bound sets the sticky err word, poisons the
 // result (NaN sums / zero counts and -1 keys) and later launches skip their
 // waits, so a lost peer fails every rank fast instead of hanging the GPU or

@@ -244,7 +244,7 @@ struct IpcPeers {
   unsigned int* arrive;  // own, device
   unsigned int* depart;  // own, device
   int* err;              // own, device: 1 = a wait timed out (sticky)
-  int fence;             // 1: also a system-scope release / acquire per block (PBX_IPC_FENCE=1)
+  int fence;             // 1: a system-scope release / acquire per block (always on)
 };
 // send / dst [world][slot_bytes]; counts (device [world], nullable = whole
 // slots) of rec_bytes records go to each peer; the received records land in

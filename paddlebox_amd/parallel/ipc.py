@@ -74,11 +74,14 @@ class IpcMesh:
         if blocks is None:
             # ~16 KB of payload per workgroup (4 x 16 B in flight per lane:
             # about one pass of the unrolled copy loop), so the puts and the
-            # copy-out are not latency-bound; 16..256 workgroups
+            # copy-out are not latency-bound; 16..64 workgroups -- more cost
+            # more in the arrive / publish / wait than they save in the copy
+            # (1-rank exchange of a 10 MB slot: 64 blocks 10.3 us, 256 blocks
+            # 17.6 us, 16 blocks 17.0 us; profiles/r6_ipc_exchange_bench.txt)
             # (PBX_IPC_MAX_BLOCKS caps it: every workgroup of every rank's
             # collective must be resident at once -- the waits spin -- which
             # matters when several ranks share one GPU, see bench --same-gpu)
-            cap = int(os.environ.get("PBX_IPC_MAX_BLOCKS", "256"))
+            cap = int(os.environ.get("PBX_IPC_MAX_BLOCKS", "64"))
             blocks = max(min(16, cap), min(cap, (W * self.slot_bytes) >> 14))
         # power of two: the arrive / depart counters find the last block by
         # count % grid and wrap at 2^32

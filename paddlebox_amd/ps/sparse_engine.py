@@ -64,6 +64,17 @@ def _pack_exchange() -> bool:
     return os.environ.get("PBX_PACK_EXCHANGE", "0") == "1"
 
 
+def _early_key_exchange() -> bool:
+    """Sharded split prefetch, PBX_EARLY_KEY_EXCHANGE=1: the next batch's owner
+    pack + key exchange right after its dedup (at step start on the dW stream)
+    instead of with the pooling after the push.  Off by default: it takes 18
+    us off the sparse chain, but the step does not gain (1-rank rehearsal
+    0.3821 vs 0.3794-0.3811 ms/step) -- the dense all-reduce behind the dW
+    GEMM becomes the critical path and the longer step-start chain delays the
+    tower forward (profiles/r6_sharded_rehearsal.txt)."""
+    return os.environ.get("PBX_EARLY_KEY_EXCHANGE", "0") == "1"
+
+
 @dataclass
 class SeqpoolParams:
     use_cvm: bool = True
@@ -126,6 +137,7 @@ class _PullSlot:
             self.resp = torch.empty(n, eng.P, device=dev)
             self.resp_back = torch.empty(n, eng.P, device=dev)
             self.rows_r = None
+            self.keys_exchanged = False  # prefetch_dedup ran this slot's pack + key exchange
 
     def pooled_out(self, shape, device) -> torch.Tensor:
         t = self.pre_outs.get(shape)
@@ -682,6 +694,12 @@ class SparseEngine:
             # the sender dedup only (keys -> uniques, per-owner counts); the
             # pack, both exchanges and the pooling follow in prefetch_pool
             self._hash_dedup(sl, keys.reshape(-1))
+            if self.xmesh is not None and _early_key_exchange():
+                # the key exchange too: it reads only this batch's keys, so it
+                # runs here, off the step's sparse chain (the owners' probe +
+                # gather and the answer exchange wait for the push: prefetch_pool)
+                self._key_exchange(sl)
+                sl.keys_exchanged = True
             return True
         if self._finish_side():
             # the pooling needs only the probe + rank launch (rows_occ); the
@@ -861,33 +879,43 @@ class SparseEngine:
         ipc = self.sharded and self.xmesh is not None
         sl.ws.run(keys, False, sl.ocnt if ipc else None)
 
-    def _sharded_after_dedup(self, sl: _PullSlot, L: int, lod, B: int, S: int) -> PullState:
-        """Sharded pull after the sender dedup: pack per owner, key exchange,
-        owner probe + gather, answer exchange."""
-        h = self._hip
+    def _fused_exchanges(self) -> bool:
+        return (self.xmesh is not None and _pack_exchange() and hasattr(self.xmesh[0].comm, "pack_exchange")
+                and hasattr(self.table.t, "answer_exchange"))
+
+    def _key_exchange(self, sl: _PullSlot):
+        """Sender half of a sharded pull after its dedup: pack the unique keys
+        per owner and exchange them (the keys only -- no table access, so it
+        may run ahead of the previous batch's push: prefetch_dedup)."""
         ws = sl.ws
         ipc = self.xmesh is not None
-        fused = (ipc and _pack_exchange() and hasattr(self.xmesh[0].comm, "pack_exchange")
-                 and hasattr(self.table.t, "answer_exchange"))
-        st = PullState(B=B, S=S, L=L, lod=lod, uid=ws.uid, perm=ws.perm, counts=ws.u_count, slot=sl, gen=sl.gen)
-        # sharded: pack per-owner, exchange keys, owner-side dedup/probe/gather
-        if fused:
+        if self._fused_exchanges():
             # the pack inside the key exchange's put phase: the dedup output
             # goes straight to the owners' inboxes (no send buffer)
             self.xmesh[0].pack_exchange(ws.uniq_h, ws.u_count, self.C, sl.send_index, sl.ocnt, self.overflow,
                                         sl.recv.view(self.world, -1), sl.rcnt)
-        else:
-            h.shard_pack_hash(ws.uniq_h, ws.u_count, self.world, self.C, sl.send, sl.send_index, sl.ocnt,
-                              self.overflow, ipc)
-        if fused:
-            pass  # keys already exchanged
-        elif self.xmesh is not None:
+            return
+        self._hip.shard_pack_hash(ws.uniq_h, ws.u_count, self.world, self.C, sl.send, sl.send_index, sl.ocnt,
+                                  self.overflow, ipc)
+        if ipc:
             # only the valid keys of each peer slot travel; the receiver
             # fills the rest of its slots with -1 (padding for the dedup)
             self.xmesh[0].exchange(sl.send.view(self.world, -1), sl.recv.view(self.world, -1), sl.ocnt, 8, True,
                                    sl.rcnt)
         else:
             self.comm.all_to_all_single(sl.recv, sl.send)
+
+    def _sharded_after_dedup(self, sl: _PullSlot, L: int, lod, B: int, S: int) -> PullState:
+        """Sharded pull after the sender dedup: pack per owner, key exchange
+        (unless prefetch_dedup already ran them), owner probe + gather, answer
+        exchange."""
+        fused = self._fused_exchanges()
+        st = PullState(B=B, S=S, L=L, lod=lod, uid=sl.ws.uid, perm=sl.ws.perm, counts=sl.ws.u_count, slot=sl,
+                       gen=sl.gen)
+        if sl.keys_exchanged:
+            sl.keys_exchanged = False
+        else:
+            self._key_exchange(sl)
         if self.codec is None:
             # owner answers in one launch: probe + record copy per received
             # key, no dedup (a key asked by several peers is read twice)

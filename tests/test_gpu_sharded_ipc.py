@@ -85,16 +85,13 @@ def _worker(rank, W, port, B, S, steps, q):
         q.put((rank, repr(e) + traceback.format_exc(), None, None, None))
 
 
-@pytest.mark.parametrize("W,mode", [(2, "unfused"), (4, "unfused"), (2, "fused"), (4, "bare")])
+@pytest.mark.parametrize("W,mode", [(2, "unfused"), (4, "unfused"), (2, "fused"), (4, "fused")])
 def test_sharded_gpu_step_multiprocess_ipc(W, mode, monkeypatch):
     """mode: fused = the owner pack inside the key exchange and the owner
     probe + gather inside the answer exchange (k_ipc_pack_exchange /
     k_ipc_answer_exchange, PBX_PACK_EXCHANGE=1); unfused = pack, exchange,
-    probe + gather, exchange as four launches (the default); fenced / bare =
-    with / without the per-workgroup system-scope release / acquire on top of
-    the system-coherent inbox accesses (PBX_IPC_FENCE, default on)."""
-    monkeypatch.setenv("PBX_PACK_EXCHANGE", "1" if mode in ("fused", "bare") else "0")
-    monkeypatch.setenv("PBX_IPC_FENCE", "0" if mode == "bare" else "1")
+    probe + gather, exchange as four launches (the default)."""
+    monkeypatch.setenv("PBX_PACK_EXCHANGE", "1" if mode == "fused" else "0")
     from paddlebox_amd.ops import reference as ref
     from paddlebox_amd.ps.sparse_engine import SeqpoolParams, SparseEngine
     from tests.test_sharded_loopback import concat_batches
