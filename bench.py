@@ -241,7 +241,7 @@ def main():
 
     if args.same_gpu:
         # all ranks' spinning IPC collectives share one GPU's workgroup slots
-        os.environ.setdefault("PBX_IPC_MAX_BLOCKS", str(max(8, 256 // max(1, world))))
+        os.environ.setdefault("PBX_IPC_MAX_BLOCKS", str(max(8, min(64, 256 // max(1, world)))))
     gpu_index = 0 if args.same_gpu else local_rank
     torch.cuda.set_device(gpu_index)
     device = torch.device("cuda", gpu_index)

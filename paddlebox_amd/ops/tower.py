@@ -181,24 +181,40 @@ class _CtrTowerFn(torch.autograd.Function):
             cross_side = (t.overlap_dw and x.is_cuda and fusedx
                           and (t.overlap_dw_collectives or not _collectives_in_step())
                           and os.environ.get("PBX_CROSS_DW_SIDE", "1") == "1")
+            cross_late = None
             if cross_side:
                 cur = torch.cuda.current_stream(x.device)
                 net._xw.backward(*cargs, dy_out=dx0, parts=1, **dsk)
                 chain = torch.cuda.Event()
                 chain.record(cur)
-                side = t._side_stream(x.device)
-                side.wait_event(chain)
-                with torch.cuda.stream(side):
-                    net._xw.backward(*cargs, dy_out=dx0, parts=2, **dsk)
-                    if hook.get("pending"):  # the dense tail ran: the cross grads are final here
-                        t.on_dense_grads()
-                add_grad_producer(side)
-                hook["after_cross"] = True
-                hook["pending"] = False
+
+                def cross_dw():
+                    side = t._side_stream(x.device)
+                    side.wait_event(chain)
+                    with torch.cuda.stream(side):
+                        net._xw.backward(*cargs, dy_out=dx0, parts=2, **dsk)
+                        if hook.get("pending"):  # the dense tail ran: the cross grads are final here
+                            t.on_dense_grads()
+                    add_grad_producer(side)
+                    hook["after_cross"] = True
+                    hook["pending"] = False
+
+                # PBX_CROSS_DW_AFTER_HEAD=1: enqueue the side-stream cross dW
+                # after the head backward, so the head follows the cross dX
+                # chain on the compute stream without a fork in between
+                if os.environ.get("PBX_CROSS_DW_AFTER_HEAD", "0") == "1":
+                    # a pending dense tail (the tower dW ran first) fires inside
+                    # cross_dw on the side stream; a later tower dW's tail runs
+                    # after it on the same stream
+                    cross_late = cross_dw
+                    if not hook.get("pending"):
+                        hook["after_cross"] = True
+                else:
+                    cross_dw()
             else:
                 net._xw.backward(*cargs, dy_out=dx0, **dsk)
                 hook["after_cross"] = True
-            if hook.get("pending"):
+            if hook.get("pending") and cross_late is None:
                 # the dense tail already ran (on the dW side stream, or inline):
                 # fire the hook where it ran, once the cross gradients are final
                 cur = torch.cuda.current_stream(x.device)
@@ -216,6 +232,8 @@ class _CtrTowerFn(torch.autograd.Function):
         dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, ws.K0p,
                            ctx.means, ctx.scales, dn.eps if dn is not None else 0.0, dlin_scale=gl,
                            want_stats=False)
+        if t.cross is not None and cross_late is not None:
+            cross_late()
         if deferred_dw is not None:
             # issued after the head backward (and the cross backward): both
             # depend only on the dX chain, and a dW launch enqueued first
@@ -288,11 +306,14 @@ class CtrTower:
         self.overlap_dw_collectives = False
         # ... enqueued after the head backward, or right after the dX chain.
         # Measured (profiles/r3_s2_dw_after_head.txt): after the head for
-        # DeepFM (0.255 vs 0.278 ms/step), right after the dX chain with a
-        # DCN-V2 cross stack, whose long backward then hides the dW (0.399 vs
-        # 0.410).  PBX_DW_AFTER_HEAD=1/0 forces either.
+        # DeepFM (0.255 vs 0.278 ms/step); with a DCN-V2 cross stack too since
+        # the cross dW moved to the side stream: the compute stream then runs
+        # dX chain -> cross dX chain -> head with no fork between them
+        # (0.306-0.308 vs 0.325-0.326 ms/step; the cross dW after the head as
+        # well, PBX_CROSS_DW_AFTER_HEAD=1: 0.339, profiles/r6_dcn_enqueue_order.txt).
+        # PBX_DW_AFTER_HEAD=1/0 forces either.
         env = os.environ.get("PBX_DW_AFTER_HEAD")
-        self.dw_after_head = (env != "0") if env is not None else cross is None
+        self.dw_after_head = (env != "0") if env is not None else True
         self._side = None
         self._part = None
         self._params = list(mlp.parameters())
