@@ -55,7 +55,7 @@ def main():
         out[f"hgemm_dW_split{sp}"] = timed(
             lambda sp=sp: h.hgemm(x, dy, dW, None, K, O, N, [1, K], [O, 1], O, 1.0, gs / in_scale, in_scale, 1.0,
                                   1.0 / gs, sp))
-    for sp in (1, 8, 12, 16, 19, 24, 32, 48):
+    for sp in (1, 4, 5, 6, 7, 8, 10, 12, 16, 19, 24, 32):
         out[f"sfc_dw_split{sp}"] = timed(
             lambda sp=sp: h.sfc_dw(x, dy, dW, db, 1.0, gs / in_scale, in_scale, 1.0 / gs, sp))
     out["sfc_dw_default_split"] = cx._sfc_dw_splits(N, K, O)
