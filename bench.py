@@ -577,7 +577,8 @@ def main():
         import gc
 
         gc.collect()
-        torch.cuda.empty_cache()
+        if os.environ.get("PBX_BENCH_KEEP_CACHE", "0") != "1":
+            torch.cuda.empty_cache()
 
     if sec_dtype != "none" and sec_dtype != args.mlp_dtype:
         # same run, same sparse engine: the other MLP precision's step time

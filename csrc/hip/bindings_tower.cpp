@@ -187,7 +187,9 @@ class TowerWorkspace {
   Tensor backward(const c10::optional<Tensor>& dloss, const Tensor& w_out, const std::vector<Tensor>& dW,
                   const std::vector<Tensor>& db, const Tensor& dw_out, const Tensor& db_out, bool need_dx,
                   const c10::optional<Tensor>& dn_part,
-                  int64_t dn_rows, double dn_eps, const c10::optional<Tensor>& dn_stats, int64_t parts) {
+                  int64_t dn_rows, double dn_eps, const c10::optional<Tensor>& dn_stats, int64_t parts,
+                  const c10::optional<Tensor>& dn_bsize, const c10::optional<Tensor>& dn_bsum,
+                  const c10::optional<Tensor>& dn_bsq, double dn_decay) {
     TW_CHECK((int)dW.size() == L_ && (int)db.size() == L_, "backward: layer count");
     TowerArgs a = base();
     for (int l = 0; l < L_; ++l) {
@@ -216,6 +218,15 @@ class TowerWorkspace {
       a.dn_C = C;
       a.dn_eps = (float)dn_eps;
       a.dn_stats = OP<float>(dn_stats);
+      if (dn_bsize.has_value() && dn_bsize->defined()) {
+        check_f32(*dn_bsize, C, "dn_bsize");
+        check_f32(*dn_bsum, C, "dn_bsum");
+        check_f32(*dn_bsq, C, "dn_bsq");
+        a.dn_bsize = P<float>(*dn_bsize);
+        a.dn_bsum = P<float>(*dn_bsum);
+        a.dn_bsq = P<float>(*dn_bsq);
+        a.dn_decay = (float)dn_decay;
+      }
     }
     // parts: bit 0 = dX chain (k_tower_bwd), bit 1 = dW / bias / data_norm
     // reductions (k_tower_dw); the caller may issue them on different streams
@@ -407,7 +418,9 @@ void bind_tower(py::module& m) {
       .def("backward", &TowerWorkspace::backward, py::arg("dloss"), py::arg("w_out"), py::arg("dW"), py::arg("db"),
            py::arg("dw_out"),
            py::arg("db_out"), py::arg("need_dx"), py::arg("dn_part") = py::none(), py::arg("dn_rows") = 0,
-           py::arg("dn_eps") = 0.0, py::arg("dn_stats") = py::none(), py::arg("parts") = 3)
+           py::arg("dn_eps") = 0.0, py::arg("dn_stats") = py::none(), py::arg("parts") = 3,
+           py::arg("dn_bsize") = py::none(), py::arg("dn_bsum") = py::none(), py::arg("dn_bsq") = py::none(),
+           py::arg("dn_decay") = 1.0)
       .def("pack_regions", &TowerWorkspace::pack_regions)
       .def("set_stamps", &TowerWorkspace::set_stamps)
       .def("x0", &TowerWorkspace::x0)

@@ -681,6 +681,12 @@ struct TowerArgs {
   int dn_rows = 0, dn_C = 0;
   float dn_eps = 0.f;
   float* dn_stats = nullptr;
+  // optional: the summaries updated in place from those stats by the same
+  // workgroup (bsize = bsize * decay + 1, ...), instead of a k_dn_update launch
+  float* dn_bsize = nullptr;
+  float* dn_bsum = nullptr;
+  float* dn_bsq = nullptr;
+  float dn_decay = 1.f;
   int dw_splits = 2;
   // fp32 dW split-M partials, reduced in split order (no float atomics: the
   // update is bit-reproducible): slab [tiles][dw_splits][64 x 64] and one

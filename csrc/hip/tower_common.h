@@ -79,9 +79,15 @@ __device__ inline void tower_col_reduce(const TowerArgs& a, int rb, int tbm) {
       tx += red[0][g][cl];
       tq += red[1][g][cl];
     }
+    const float mx = tx / (float)a.M, sq = tq / (float)a.M + a.dn_eps;
     a.dn_stats[c] = 1.f;
-    a.dn_stats[C + c] = tx / (float)a.M;
-    a.dn_stats[2 * C + c] = tq / (float)a.M + a.dn_eps;
+    a.dn_stats[C + c] = mx;
+    a.dn_stats[2 * C + c] = sq;
+    if (a.dn_bsize) {  // same arithmetic as k_dn_update (dense_ops.hip)
+      a.dn_bsize[c] = a.dn_bsize[c] * a.dn_decay + 1.f;
+      a.dn_bsum[c] = a.dn_bsum[c] * a.dn_decay + mx;
+      a.dn_bsq[c] = a.dn_bsq[c] * a.dn_decay + sq;
+    }
   }
 }
 

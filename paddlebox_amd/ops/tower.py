@@ -133,12 +133,24 @@ class _CtrTowerFn(torch.autograd.Function):
         # fire on_dense_grads (the all-reduce / overlapped Adam would read the
         # cross weights' gradients unfinished)
         hook = {"after_cross": False}
+        # single-process statistics: the dW launch's reduction workgroups also
+        # fold them into the summaries (one k_dn_update launch less on the
+        # side stream, ahead of the next step's head forward)
+        dn_inline = (dn_on and not dn.fused_update and not getattr(dn, "update_in_hook", False)
+                     and not getattr(dn, "stats_in_grad_bucket", False)
+                     and not (dn.sync_stats and dn.group is not None and collective_active(dn.group))
+                     and os.environ.get("PBX_DN_INLINE_UPDATE", "1") == "1")
+        dnk = ({"dn_bsize": dn.batch_size, "dn_bsum": dn.batch_sum, "dn_bsq": dn.batch_square_sum,
+                "dn_decay": float(dn.decay)} if dn_inline else {})
+
+        def bwd(parts=3):
+            return ws.backward(*args, parts=parts, **dnk)
 
         def dense_tail():
             if dn_on and not getattr(dn, "stats_in_grad_bucket", False):
                 if dn.sync_stats and dn.group is not None and collective_active(dn.group):
                     allreduce_sum(dn.stats, dn.group)  # the group's IPC mesh when registered
-            if dn_on and not dn.fused_update and not getattr(dn, "update_in_hook", False):
+            if dn_on and not dn_inline and not dn.fused_update and not getattr(dn, "update_in_hook", False):
                 h.data_norm_update(dn.batch_size, dn.batch_sum, dn.batch_square_sum, dn.stats, dn.decay)
             if t.on_dense_grads is not None:  # e.g. start the dense all-reduce, overlapped with the sparse push
                 if t.cross is not None and not hook["after_cross"]:
@@ -153,16 +165,16 @@ class _CtrTowerFn(torch.autograd.Function):
             # stream, concurrent with the head backward and the sparse push;
             # the optimizer joins it (parallel.dense.join_grad_producers)
             cur = torch.cuda.current_stream(x.device)
-            dx0 = ws.backward(*args, parts=1)
+            dx0 = bwd(1)
             deferred_dw = torch.cuda.Event()
             deferred_dw.record(cur)
             if t.on_dx_done is not None:  # e.g. the next batch's key dedup on a side stream
                 t.on_dx_done(deferred_dw)
             if not t.dw_after_head:
-                _launch_dw(t, ws, args, dense_tail, x.device, deferred_dw)
+                _launch_dw(t, bwd, dense_tail, x.device, deferred_dw)
                 deferred_dw = None
         else:
-            dx0 = ws.backward(*args)
+            dx0 = bwd()
             dense_tail()
         if t.cross is not None:
             # cross backward (d logit = dz); its x0 gradient is added into the
@@ -239,7 +251,7 @@ class _CtrTowerFn(torch.autograd.Function):
             # depend only on the dX chain, and a dW launch enqueued first
             # fills the CUs and starves the head's workgroups (fp32 tower:
             # head_bwd 13 -> 95 us beside k_t32_dw, profiles/r3_s2_dw_after_head.txt)
-            _launch_dw(t, ws, args, dense_tail, x.device, deferred_dw)
+            _launch_dw(t, bwd, dense_tail, x.device, deferred_dw)
         if t.on_head_done is not None:  # e.g. the next batch's key dedup beside the sparse push
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(x.device))
@@ -248,13 +260,13 @@ class _CtrTowerFn(torch.autograd.Function):
         return (dx, d_extra, None, None) + (None,) * (len(t._params))
 
 
-def _launch_dw(t, ws, args, dense_tail, device, after: "torch.cuda.Event"):
+def _launch_dw(t, bwd, dense_tail, device, after: "torch.cuda.Event"):
     """The tower's dW GEMM + reductions and the dense tail on its side stream,
     ordered after the dX chain (event ``after``) only."""
     side = t._side_stream(device)
     side.wait_event(after)
     with torch.cuda.stream(side):
-        ws.backward(*args, parts=2)
+        bwd(2)
         dense_tail()
     add_grad_producer(side)
 
