@@ -231,3 +231,23 @@ def test_deepfm_fp32_vs_bf16_training_auc():
         aucs[prec] = (float(ranks[y > 0.5].sum()) - npos * (npos + 1) / 2) / (npos * nneg)
     assert aucs["fp32"] > 0.6, aucs
     assert abs(aucs["fp32"] - aucs["bf16"]) < 0.002, aucs
+
+
+@pytest.mark.parametrize("T", [4, 1000])
+def test_tower_auc_histogram_exact(T):
+    """The fused loss tail's AUC histogram (wave-merged adds) equals a
+    bincount of the stored predictions; T = 4 puts most rows of every wave on
+    one bucket (the converged-model case the per-wave merge is for)."""
+    B = 8192
+    S, Eo, Dd, D = 26, 11, 13, 8
+    x, label, dn, mlp = _make(B, S, Eo, Dd, (400, 400, 400))
+    tg = CtrTower(copy.deepcopy(mlp).to(DEV), copy.deepcopy(dn).to(DEV), S, Eo, 2, D, fp32=True)
+    tg.auc = (torch.zeros(2 * T, dtype=torch.float64, device=DEV), torch.zeros(5, dtype=torch.float64, device=DEV),
+              None)
+    _, pg = tg(x.to(DEV), label.to(DEV))
+    torch.cuda.synchronize()
+    p = pg.detach().float().cpu().view(-1)
+    pos = (p * T).to(torch.int64).clamp(0, T - 1)
+    lab = (label.view(-1) > 0.5).to(torch.int64)
+    want = torch.bincount(lab * T + pos, minlength=2 * T).double()
+    assert torch.equal(tg.auc[0].cpu(), want)
