@@ -169,10 +169,10 @@ def main():
                     help="before warmup, print per-step host time of load / replay for this many steps (stderr)")
     ap.add_argument("--host-diag", action="store_true",
                     help="after the measurement, split host time into replay / H2D load (stderr only)")
-    ap.add_argument("--mlp-dtype", choices=("bf16", "fp32"), default="fp32",
+    ap.add_argument("--mlp-dtype", choices=("bf16", "fp32", "fp32x3"), default="fp32",
                     help="fp32: the reference's fp32 fc precision (default headline, exact fp32 MFMA tower); "
                          "bf16: the bf16 MFMA tower")
-    ap.add_argument("--secondary-dtype", choices=("auto", "fp32", "bf16", "none"), default="auto",
+    ap.add_argument("--secondary-dtype", choices=("auto", "fp32", "fp32x3", "bf16", "none"), default="auto",
                     help="after the headline measurement, time the same K steps at this MLP precision in the same "
                          "run and report it in config (auto: the other precision when the headline is DeepFM on "
                          "one GPU)")
@@ -312,7 +312,7 @@ def main():
         # the pull slots' occurrence rows are all -1 again (a pipelined run
         # leaves rows there, which a split pull must not read as occurrences)
         engine.clear_prefetch(reset_rows=True)
-        if dcn and mlp_dtype == "fp32":
+        if dcn and mlp_dtype in ("fp32", "fp32x3"):
             raise SystemExit("DCN-V2 (BASELINE config 5) is a bf16-MLP config: run it with --mlp-dtype bf16")
         auc_table = torch.zeros(2 * 1_000_000, dtype=torch.float64, device=device)
         auc_stats = torch.zeros(5, dtype=torch.float64, device=device)
@@ -330,7 +330,7 @@ def main():
         # bf16 DeepFM on one rank too: 0.2161 / 0.2165 vs 0.2188 / 0.2199
         # ms/step without it (profiles/r6_pipeline_bf16_split_ab.txt)
         want_pipe = args.pipeline == "on" or (args.pipeline == "auto" and (
-            (mlp_dtype == "fp32" and not dcn) or (not multi)))
+            (mlp_dtype in ("fp32", "fp32x3") and not dcn) or (not multi)))
         pipe_ok = args.graph and engine.can_prefetch_pull() and (
             not engine.sharded or os.environ.get("PBX_SHARDED_PIPELINE", "1") == "1")
         use_pipe = want_pipe and pipe_ok and not (args.prefetch and engine.can_prefetch())

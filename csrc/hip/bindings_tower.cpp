@@ -45,8 +45,12 @@ class TowerWorkspace {
  public:
   // fp32 = true: the exact-fp32 tower (tower32.hip, reference fc precision):
   // fp32 activations / weights, widths padded to 16, Mp to 256
-  TowerWorkspace(int64_t M, std::vector<int64_t> dims, int device, int64_t dw_splits, bool fp32)
-      : M_(M), dims_(dims), splits_(dw_splits), fp32_(fp32) {
+  // x3 = true (with fp32 = false): fp32 precision on bf16 MFMA (tower_x3.hip):
+  // the bf16 layouts with lo twins, fp32 X0 / dX0 rows, dW one writer per tile
+  TowerWorkspace(int64_t M, std::vector<int64_t> dims, int device, int64_t dw_splits, bool fp32, bool x3)
+      : M_(M), dims_(dims), splits_(dw_splits), fp32_(fp32), x3_(x3) {
+    TW_CHECK(!(fp32 && x3), "fp32 and x3 are different towers");
+    if (x3) splits_ = dw_splits = 1;
     TW_CHECK(dims.size() >= 2 && dims.size() - 1 <= (size_t)kMaxTowerLayers, "1..8 hidden layers");
     TW_CHECK(M > 0, "M > 0");
     if (fp32) TW_CHECK(dw_splits == 1 || dw_splits == 2 || dw_splits == 4 || dw_splits == 8, "dw_splits in {1,2,4,8}");
@@ -54,6 +58,7 @@ class TowerWorkspace {
     const int64_t wmax = fp32 ? kTower32MaxWidth : 2048;
     for (auto d : dims) TW_CHECK(d > 0 && d <= wmax, "layer widths exceed the fused tower's limit");
     auto ob = torch::TensorOptions().dtype(fp32 ? torch::kFloat32 : torch::kBFloat16).device(torch::kCUDA, device);
+    const int64_t tw = x3 ? 2 : 1;  // x3: hi + lo halves of every bf16 buffer
     auto of = torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device);
     auto oi = torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device);
     wpad_ = fp32 ? 16 : 32;
@@ -76,12 +81,12 @@ class TowerWorkspace {
       // batch that cannot be cut in 4 falls back to 2 (always valid: Mp % 128 == 0)
       if ((Mp_ / 16) % (4 * splits_) != 0) splits_ = 2;
       lds_ld_ = (int)maxw + 8;
-      TW_CHECK((size_t)2 * 32 * lds_ld_ * 2 <= 150 * 1024, "widths exceed the LDS tile budget");
+      TW_CHECK((size_t)2 * tw * 32 * lds_ld_ * 2 <= 150 * 1024, "widths exceed the LDS tile budget");
     }
     const int64_t K0p = pad(dims[0], wpad_);
-    x0_ = torch::zeros({M, K0p}, ob);
-    x0mp_ = torch::zeros({Mp_ * K0p}, ob);
-    dx0_ = torch::zeros({M, K0p}, ob);
+    x0_ = torch::zeros({M, K0p}, x3 ? of : ob);
+    x0mp_ = torch::zeros({tw * Mp_ * K0p}, ob);
+    dx0_ = torch::zeros({M, K0p}, x3 ? of : ob);
     int64_t boff = 0;
     for (int l = 0; l < L_; ++l) {
       const int64_t Kp = pad(dims[l], wpad_), Np = pad(dims[l + 1], wpad_);
@@ -89,8 +94,8 @@ class TowerWorkspace {
       // units / segments padded to the ring depth) + slack for the weight
       // ring, which loads kT32Ring steps (2 KB each) past a stream's end
       const int64_t slack = 256 * 2 * 2 * kT32Ring;
-      const int64_t n_wp = fp32 ? t32_stream_groups((int)(Np / 16), (int)(Kp / 16)) * 256 + slack : Np * Kp;
-      const int64_t n_wtp = fp32 ? t32_stream_groups((int)(Kp / 16), (int)(Np / 16)) * 256 + slack : Np * Kp;
+      const int64_t n_wp = fp32 ? t32_stream_groups((int)(Np / 16), (int)(Kp / 16)) * 256 + slack : tw * Np * Kp;
+      const int64_t n_wtp = fp32 ? t32_stream_groups((int)(Kp / 16), (int)(Np / 16)) * 256 + slack : tw * Np * Kp;
       wp_.push_back(torch::zeros({n_wp}, ob));
       wtp_.push_back(torch::zeros({n_wtp}, ob));
       if (fp32) {
@@ -106,8 +111,8 @@ class TowerWorkspace {
         pos_.push_back(pos.to(x0_.device()));
         posT_.push_back(posT.to(x0_.device()));
       }
-      xmp_.push_back(torch::zeros({Mp_ * Np}, ob));
-      dzmp_.push_back(torch::zeros({Mp_ * Np}, ob));
+      xmp_.push_back(torch::zeros({tw * Mp_ * Np}, ob));
+      dzmp_.push_back(torch::zeros({tw * Mp_ * Np}, ob));
       boff_.push_back(boff);
       boff += Np;
     }
@@ -141,6 +146,7 @@ class TowerWorkspace {
       w[l] = P<float>(W[l]);
     }
     if (fp32_) launch_tower32_pack(a, w, stream());
+    else if (x3_) launch_tower_x3_pack(a, w, stream());
     else launch_tower_pack(a, w, stream());
   }
 
@@ -178,6 +184,7 @@ class TowerWorkspace {
     }
     if (stamps_.defined()) a.stamps = reinterpret_cast<long long*>(stamps_.data_ptr());
     if (fp32_) launch_tower32_fwd(a, stream());
+    else if (x3_) launch_tower_x3_fwd(a, stream());
     else launch_tower_fwd(a, stream());
     return {loss_, pred_, dz_};
   }
@@ -206,7 +213,7 @@ class TowerWorkspace {
     a.db_out = P<float>(db_out);
     a.dloss = OP<float>(dloss);
     a.need_dx0 = need_dx ? 1 : 0;
-    if (fp32_) a.dx0f = P<float>(dx0_);
+    if (fp32_ || x3_) a.dx0f = P<float>(dx0_);
     else a.dx0 = BP(dx0_);
     a.lddx0 = (int)dx0_.size(1);
     if (dn_part.has_value() && dn_part->defined()) {
@@ -235,6 +242,9 @@ class TowerWorkspace {
     if (fp32_) {
       if (parts & 1) launch_tower32_bwd(a, s);
       if (parts & 2) launch_tower32_dw(a, s);
+    } else if (x3_) {
+      if (parts & 1) launch_tower_x3_bwd(a, s);
+      if (parts & 2) launch_tower_x3_dw(a, s);
     } else {
       if (parts & 1) launch_tower_bwd(a, s);
       if (parts & 2) launch_tower_dw(a, s);
@@ -248,7 +258,7 @@ class TowerWorkspace {
     for (int l = 0; l < L_; ++l)
       r.push_back(py::make_tuple(wp_[l], wtp_[l], dims_[l + 1], dims_[l], pad(dims_[l + 1], wpad_), pad(dims_[l], wpad_),
                                  fp32_ ? py::object(py::cast(pos_[l])) : py::object(py::none()),
-                                 fp32_ ? py::object(py::cast(posT_[l])) : py::object(py::none())));
+                                 fp32_ ? py::object(py::cast(posT_[l])) : py::object(py::none()), x3_));
     return r;
   }
 
@@ -265,6 +275,7 @@ class TowerWorkspace {
   // timing experiments: per-wave s_memtime stamps of the fp32 forward
   void set_stamps(const Tensor& t) { stamps_ = t; }
   bool fp32() const { return fp32_; }
+  bool x3() const { return x3_; }
   int64_t dw_splits() const { return splits_; }
   int64_t lds_ld() const { return lds_ld_; }
 
@@ -280,6 +291,9 @@ class TowerWorkspace {
     if (fp32_) {
       a.x0f = P<float>(x0_);
       a.x0mpf = P<float>(x0mp_);
+    } else if (x3_) {
+      a.x0f = P<float>(x0_);
+      a.x0mp = BP(x0mp_);
     } else {
       a.x0 = BP(x0_);
       a.x0mp = BP(x0mp_);
@@ -328,7 +342,7 @@ class TowerWorkspace {
   int64_t M_, Mp_ = 0;
   std::vector<int64_t> dims_;
   int64_t splits_;
-  bool fp32_ = false;
+  bool fp32_ = false, x3_ = false;
   int64_t wpad_ = 32;
   int L_ = 0, lds_ld_ = 0, bias_ld_ = 0, dwout_off_ = 0, dbout_off_ = 0;
   std::vector<int64_t> boff_;
@@ -367,6 +381,7 @@ static void adam_fused(Tensor p, Tensor g, Tensor m, Tensor v, Tensor pows, Tens
       x.pack_pos32[i] = P<int>(t[7].cast<Tensor>());
       x.pack_posT32[i] = P<int>(t[8].cast<Tensor>());
     }
+    x.pack_x3[i] = (t.size() >= 10 && !t[9].is_none() && t[9].cast<bool>()) ? 1 : 0;
     x.pack_N[i] = t[3].cast<int>();
     x.pack_K[i] = t[4].cast<int>();
     x.pack_Np[i] = t[5].cast<int>();
@@ -409,8 +424,8 @@ static void memcpy_h2d(Tensor dst, const Tensor& src) {
 void bind_tower(py::module& m) {
   m.def("memcpy_h2d", &memcpy_h2d, py::arg("dst"), py::arg("src"));
   py::class_<TowerWorkspace>(m, "TowerWorkspace")
-      .def(py::init<int64_t, std::vector<int64_t>, int, int64_t, bool>(), py::arg("M"), py::arg("dims"),
-           py::arg("device"), py::arg("dw_splits") = 2, py::arg("fp32") = false)
+      .def(py::init<int64_t, std::vector<int64_t>, int, int64_t, bool, bool>(), py::arg("M"), py::arg("dims"),
+           py::arg("device"), py::arg("dw_splits") = 2, py::arg("fp32") = false, py::arg("x3") = false)
       .def("pack", &TowerWorkspace::pack)
       .def("forward", &TowerWorkspace::forward, py::arg("b"), py::arg("w_out"), py::arg("b_out"), py::arg("lin"),
            py::arg("label"), py::arg("auc_table") = py::none(), py::arg("auc_stats") = py::none(),
@@ -434,6 +449,7 @@ void bind_tower(py::module& m) {
       .def_property_readonly("Mp", &TowerWorkspace::Mp)
       .def_property_readonly("K0p", &TowerWorkspace::K0p)
       .def_property_readonly("fp32", &TowerWorkspace::fp32)
+      .def_property_readonly("x3", &TowerWorkspace::x3)
       .def_property_readonly("dw_splits", &TowerWorkspace::dw_splits)
       .def_property_readonly("lds_ld", &TowerWorkspace::lds_ld);
   m.def("adam_fused", &adam_fused, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pows"),

@@ -731,6 +731,16 @@ void launch_tower32_bwd(const TowerArgs& a, hipStream_t s);
 void launch_tower32_dw(const TowerArgs& a, hipStream_t s);
 void launch_tower32_pack(const TowerArgs& a, const float* const* w, hipStream_t s);
 
+// fp32-precision tower on bf16 MFMA (tower_x3.hip): the bf16 tower's layouts
+// with a lo twin after every bf16 buffer (packed W / W^T: + Np Kp; MP
+// activations / dZ: + Mp Np; MP(X0): + Mp K0p), fp32 X0 rows in (x0f), fp32
+// dX0 rows out (dx0f); 4 LDS planes of 32 x lds_ld bf16
+size_t tower_x3_lds_bytes(int lds_ld);
+void launch_tower_x3_fwd(const TowerArgs& a, hipStream_t s);
+void launch_tower_x3_bwd(const TowerArgs& a, hipStream_t s);
+void launch_tower_x3_dw(const TowerArgs& a, hipStream_t s);
+void launch_tower_x3_pack(const TowerArgs& a, const float* const* w, hipStream_t s);
+
 // Flat Adam with fused extras: beta powers advanced by the last workgroup
 // (ticket), weight regions re-packed to bf16 tower layouts, data_norm
 // summaries updated from their batch statistics.
@@ -747,6 +757,8 @@ struct AdamExtras {
   // fp32: group position tables [Np/16][Kp/16] and [Kp/16][Np/16] (tower_wp32_index_pos)
   const int* pack_pos32[kMaxPackRegions];
   const int* pack_posT32[kMaxPackRegions];
+  // x3 tower regions: the bf16 copies also get their lo halves, Np Kp after
+  int pack_x3[kMaxPackRegions] = {};
   int n_dn = 0;
   const float* dn_stats[kMaxDnUpdates];
   float* dn_bsize[kMaxDnUpdates];

@@ -622,8 +622,15 @@ __global__ __launch_bounds__(256) void k_adam_fused(float* __restrict__ p, float
           continue;
         }
         const u16 bv = f2bf(pa[k]);
-        x.pack_wp[r][wp_index(nn, kk, x.pack_Kp[r])] = bv;
-        x.pack_wtp[r][wtp_index(nn, kk, x.pack_Np[r])] = bv;
+        const int64_t pi = wp_index(nn, kk, x.pack_Kp[r]), ti = wtp_index(nn, kk, x.pack_Np[r]);
+        x.pack_wp[r][pi] = bv;
+        x.pack_wtp[r][ti] = bv;
+        if (x.pack_x3[r]) {  // x3 tower: lo half after the hi copy
+          const int64_t lo = (int64_t)x.pack_Np[r] * x.pack_Kp[r];
+          const u16 lv = f2bf(pa[k] - bf2f(bv));
+          x.pack_wp[r][lo + pi] = lv;
+          x.pack_wtp[r][lo + ti] = lv;
+        }
       }
     }
   }

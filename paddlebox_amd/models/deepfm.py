@@ -77,10 +77,16 @@ class DeepFM(nn.Module):
         self.precision = "bf16"
 
     def set_precision(self, precision: str):
-        if precision not in ("bf16", "fp32"):
+        """"bf16", "fp32" (exact fp32 products, tower32.hip) or "fp32x3"
+        (fp32 operands as bf16 hi + lo halves, three bf16 MFMA products per
+        step, tower_x3.hip: finer than the TF32 math the reference's fp32 fc
+        runs on by default, gpu_context.cc:65-67,580-588)."""
+        if precision not in ("bf16", "fp32", "fp32x3"):
             raise ValueError(precision)
-        self.precision = precision
-        self.tower.fp32 = precision == "fp32" and self.mlp.tower_fp32_ok()
+        x3 = precision == "fp32x3" and self.mlp.tower_x3_ok()
+        self.precision = "fp32" if precision == "fp32x3" else precision
+        self.tower.x3 = x3
+        self.tower.fp32 = self.precision == "fp32" and not x3 and self.mlp.tower_fp32_ok()
         self.mlp.invalidate_pack()
 
     def prefetch(self, batch, slot: int) -> bool:
@@ -97,7 +103,7 @@ class DeepFM(nn.Module):
     def forward(self, batch):
         B, S = batch.B, batch.S
         x = pull_seqpool_cvm_concat(self.engine, batch.keys, batch.lod, B, S, batch.cvm, batch.dense, self.sp)
-        if self.precision == "fp32" and x.is_cuda and not (self.use_tower and self.tower.fp32):
+        if self.precision == "fp32" and x.is_cuda and not (self.use_tower and (self.tower.fp32 or self.tower.x3)):
             return self._forward_fp32(x, batch.label)
         if self.use_tower or not x.is_cuda:
             return self.tower(x, batch.label)

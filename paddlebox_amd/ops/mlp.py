@@ -19,6 +19,10 @@ from torch import nn
 from .. import _native
 
 
+def pad32(n: int) -> int:
+    return (n + 31) // 32 * 32
+
+
 def pad8(n: int) -> int:
     return (n + 7) // 8 * 8
 
@@ -205,7 +209,7 @@ class FusedMLP(nn.Module):
         self.packed_by_optimizer = False
 
     # ---- fused tower path (csrc/hip/tower.hip)
-    def tower_workspace(self, M: int, device: torch.device, fp32: bool = False):
+    def tower_workspace(self, M: int, device: torch.device, fp32: bool = False, x3: bool = False):
         """Persistent buffers of the fused tower for batch M.  fp32=True is the
         exact-fp32 tower (csrc/hip/tower32.hip, the reference fc precision),
         else the bf16-operand tower (csrc/hip/tower.hip).  One workspace per
@@ -213,7 +217,7 @@ class FusedMLP(nn.Module):
         at one batch size keeps its workspace's addresses while steps of
         another size (a pass's last partial batch) use their own."""
         tws = self.__dict__.setdefault("_tws", {})
-        key = (int(M), bool(fp32))
+        key = (int(M), bool(fp32), bool(x3))
         tw = tws.get(key)
         if tw is None:
             dims = [self.in_dim] + list(self.hidden)
@@ -222,7 +226,9 @@ class FusedMLP(nn.Module):
                 splits = int(os.environ.get("PBX_TOWER32_DW_SPLITS", "8"))
             else:
                 splits = int(os.environ.get("PBX_TOWER_DW_SPLITS", "2"))
-            tw = tws[key] = _native.hip().TowerWorkspace(M, dims, device.index or 0, splits, bool(fp32))
+            if x3:
+                splits = 1  # x3 dW: one writer per element (bit-reproducible)
+            tw = tws[key] = _native.hip().TowerWorkspace(M, dims, device.index or 0, splits, bool(fp32), bool(x3))
         if self._tw is not tw:
             self._tw = tw
             self._packed = False
@@ -238,6 +244,12 @@ class FusedMLP(nn.Module):
         a multiple of 128: widths <= 464, or <= 512 when all are multiples of
         128 (bindings_tower.cpp checks the exact budget)."""
         return tower_fp32_fits([self.in_dim] + list(self.hidden))
+
+    def tower_x3_ok(self) -> bool:
+        """The x3 tower (fp32 precision on bf16 MFMA, csrc/hip/tower_x3.hip)
+        keeps hi + lo planes of two 32-row bf16 tiles in LDS: padded widths
+        <= 592."""
+        return max(pad32(d) for d in [self.in_dim] + list(self.hidden)) + 8 <= 600
 
     def ensure_packed(self):
         """Pack the current workspace's tower weights unless the optimizer

@@ -62,20 +62,22 @@ class _CtrTowerFn(torch.autograd.Function):
         elif x.is_cuda:
             join_grad_producers()  # a previous dW still reading the activations (no optimizer step between)
         B = x.shape[0]
-        ws = mlp.tower_workspace(B, x.device, fp32=t.fp32)
+        ws = mlp.tower_workspace(B, x.device, fp32=t.fp32, x3=t.x3)
         if pre_head is None:
             mlp.ensure_packed()
         x = x.contiguous()
         yt = t._cross_yt(B, x.device) if t.cross is not None else None
-        Cp = ws.K0p  # MLP input width: padded to 32 (bf16 tower) / 16 (fp32 tower)
+        Cp = ws.K0p  # MLP input width: padded to 32 (bf16 / x3 tower) / 16 (fp32 tower)
+        # the x3 tower takes fp32 rows and m-packs their hi / lo halves itself
+        ymp = None if t.x3 else ws.x0mp()
         if dn is not None:
             part = t._dn_part(B, x.device)
             _, lin, means, scales = h.head_fwd(x, t.S, t.Eo, t.ew_col, t.D, Cp, dn.batch_size,
                                                dn.batch_sum, dn.batch_square_sum, y_out=ws.x0(), yT_out=yt,
-                                               ymp_out=ws.x0mp(), stat_part=part)
+                                               ymp_out=ymp, stat_part=part)
         else:
             _, lin, means, scales = h.head_fwd(x, t.S, t.Eo, t.ew_col, t.D, Cp, None, None, None,
-                                               y_out=ws.x0(), yT_out=yt, ymp_out=ws.x0mp())
+                                               y_out=ws.x0(), yT_out=yt, ymp_out=ymp)
         if extra is not None:
             lin_use = extra.detach().contiguous().float().view(-1)
         elif t.use_head_lin:
@@ -289,6 +291,9 @@ class CtrTower:
         if fp32 and cross is not None:
             raise ValueError("the fp32 tower does not carry the DCN-V2 cross stack")
         self.fp32 = bool(fp32)
+        # x3: fp32-precision tower on bf16 MFMA (tower_x3.hip: hi / lo bf16
+        # halves, 3 products per MFMA step); set by the model's precision
+        self.x3 = False
         self.mlp, self.dn = mlp, dn
         self.cross = cross
         self._yt = None

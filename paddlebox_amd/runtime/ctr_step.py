@@ -67,7 +67,7 @@ class CtrTrainStep:
         self.device = device
         self.engine = engine
         dcn = model_name == "dcn_v2"
-        fp32 = precision == "fp32"
+        fp32 = precision in ("fp32", "fp32x3")
         if dcn:
             if fp32:
                 raise ValueError("DCN-V2 (BASELINE config 5) is a bf16-MLP config")
@@ -76,10 +76,10 @@ class CtrTrainStep:
         else:
             model = DeepFM(engine, num_slots=num_slots, dense_dim=dense_dim, hidden=tuple(hidden)).to(device)
         if fp32:
-            model.set_precision("fp32")
+            model.set_precision(precision)
         self.model = model
         # the fused tower runs the whole dense side (bf16 operands, or exact fp32)
-        self.fused = getattr(model, "use_tower", False) and (not fp32 or model.tower.fp32)
+        self.fused = getattr(model, "use_tower", False) and (not fp32 or model.tower.fp32 or model.tower.x3)
         C = model.dn.C
         self.arena = DenseArena(model.parameters(), device, extra_grad=3 * C if multi and not dcn else 0)
         if multi:

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--dims", type=str, default="304,400,400,400")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--fp32", action="store_true", help="exact-fp32 tower (tower32.hip)")
+    ap.add_argument("--x3", action="store_true", help="fp32 precision on bf16 MFMA (tower_x3.hip)")
     args = ap.parse_args()
     dims = [int(d) for d in args.dims.split(",")]
     dev = torch.device("cuda:0")
@@ -32,7 +33,7 @@ def main():
     mlp = FusedMLP(dims[0], dims[1:], 1).to(dev)
     arena = DenseArena(mlp.parameters(), dev)
     opt = FlatAdam(arena, lr=1e-3, clear_grad=True).fuse(mlps=[mlp])
-    ws = mlp.tower_workspace(args.M, dev, fp32=args.fp32)
+    ws = mlp.tower_workspace(args.M, dev, fp32=args.fp32, x3=args.x3)
     mlp.ensure_packed()
     ws.x0()[:, :dims[0]] = torch.randn(args.M, dims[0], device=dev).to(ws.x0().dtype)
     lin = torch.randn(args.M, device=dev)
