@@ -10,9 +10,11 @@ Criteo-1TB-shape"): 26 sparse slots over a 1e9-feature space (Criteo-1TB
 per-slot cardinalities scaled to 1B, power-law id popularity), 13 dense
 features, 8-dim embedx (+show/click/embed_w = 11-wide pull records), sparse
 Adagrad in the GPU parameter server, DeepFM (FM + data_norm + MLP 400-400-400)
-with the MLP in exact fp32 (the reference's fc precision) on fp32 MFMA and fused
-Adam; the same run also times the bf16-MFMA tower and DCN-V2 (BASELINE config 5)
-as secondaries in ``config``.  The feature table is pre-populated with
+with the MLP at fp32 precision (fp32 storage and accumulation, every product as
+three bf16 MFMAs on hi + lo halves: finer than the TF32 math the reference's
+fp32 fc runs on by default) and fused Adam; the same run also times the
+exact-fp32 tower (fp32 MFMA products) and DCN-V2 (BASELINE config 5) as
+secondaries in ``config``.  The feature table is pre-populated with
 all 1e9 features (random-init weights, as if a base model was loaded) and
 sharded across GPUs by hash; keys are exchanged with all-to-all each step.
 Weak scaling: the per-GPU batch is fixed.  Each timed step = a device-to-device
@@ -169,9 +171,11 @@ def main():
                     help="before warmup, print per-step host time of load / replay for this many steps (stderr)")
     ap.add_argument("--host-diag", action="store_true",
                     help="after the measurement, split host time into replay / H2D load (stderr only)")
-    ap.add_argument("--mlp-dtype", choices=("bf16", "fp32", "fp32x3"), default="fp32",
-                    help="fp32: the reference's fp32 fc precision (default headline, exact fp32 MFMA tower); "
-                         "bf16: the bf16 MFMA tower")
+    ap.add_argument("--mlp-dtype", choices=("bf16", "fp32", "fp32x3"), default="fp32x3",
+                    help="fp32x3 (default headline): fp32 operands / accumulation with every product as three "
+                         "bf16 MFMAs on hi + lo halves (tower_x3.hip) -- finer than the TF32 math the reference's "
+                         "fp32 fc runs on by default (gpu_context.cc:65-67,580-588); fp32: exact fp32 products "
+                         "(tower32.hip, v_mfma_f32_16x16x4_f32); bf16: the bf16 MFMA tower"),
     ap.add_argument("--secondary-dtype", choices=("auto", "fp32", "fp32x3", "bf16", "none"), default="auto",
                     help="after the headline measurement, time the same K steps at this MLP precision in the same "
                          "run and report it in config (auto: the other precision when the headline is DeepFM on "
@@ -554,7 +558,7 @@ def main():
 
     hidden = tuple(int(x) for x in args.hidden.split(","))
     dcn = args.model == "dcn_v2"
-    if dcn and args.mlp_dtype == "fp32":
+    if dcn and args.mlp_dtype in ("fp32", "fp32x3"):
         args.mlp_dtype = "bf16"  # config 5 names a bf16 MLP
     res = measure(args.mlp_dtype, True)
     dt, t_enq, loss, auc_stats, ipc = res["dt"], res["t_enq"], res["loss"], res["auc_stats"], res["ipc"]
@@ -565,6 +569,7 @@ def main():
     sec_dtype = args.secondary_dtype
     if sec_dtype == "auto":
         # one GPU: the driver's headline run; the N-GPU scaling runs keep one measurement
+        # (fp32x3 headline: the exact-fp32 step, so both fp32-class numbers come from one run)
         sec_dtype = ("bf16" if args.mlp_dtype == "fp32" else "fp32") if (not dcn and world == 1) else "none"
     if dcn:
         sec_dtype = "none"
@@ -637,6 +642,13 @@ def main():
                 "steps_per_graph": res.get("graph_steps", 1),
                 "key_dedup": bool(engine.dedup),
                 "mlp_dtype": args.mlp_dtype,
+                **({"mlp_precision": "fp32 activations / weights / accumulation; each fp32 operand carried as bf16 "
+                                     "hi + lo halves (16 significant bits) and each product as hi*hi + hi*lo + "
+                                     "lo*hi on bf16 MFMA: dot-product error <= ~2^-15 of sum |terms| (tested "
+                                     "element-wise at 2^-13 against fp64, tests/test_gpu_tower_x3.py); the "
+                                     "reference's fp32 fc runs TF32 by default (11-bit inputs, ~2^-10): "
+                                     "paddle/phi/backends/gpu/gpu_context.cc:65-67,580-588"}
+                   if args.mlp_dtype == "fp32x3" else {}),
                 **({f"{sec_dtype}_ms_per_step": round(second["dt"] / args.steps * 1e3, 4),
                     f"{sec_dtype}_samples_per_s": round(B * world * args.steps / second["dt"], 1),
                     f"{sec_dtype}_mlp": ("exact fp32 products on v_mfma_f32_16x16x4_f32 (the reference fc "

@@ -50,7 +50,7 @@ class TowerWorkspace {
   TowerWorkspace(int64_t M, std::vector<int64_t> dims, int device, int64_t dw_splits, bool fp32, bool x3)
       : M_(M), dims_(dims), splits_(dw_splits), fp32_(fp32), x3_(x3) {
     TW_CHECK(!(fp32 && x3), "fp32 and x3 are different towers");
-    if (x3) splits_ = dw_splits = 1;
+    if (x3) TW_CHECK(dw_splits == 1 || dw_splits == 2 || dw_splits == 4, "x3 dw_splits in {1, 2, 4}");
     TW_CHECK(dims.size() >= 2 && dims.size() - 1 <= (size_t)kMaxTowerLayers, "1..8 hidden layers");
     TW_CHECK(M > 0, "M > 0");
     if (fp32) TW_CHECK(dw_splits == 1 || dw_splits == 2 || dw_splits == 4 || dw_splits == 8, "dw_splits in {1,2,4,8}");
@@ -126,6 +126,13 @@ class TowerWorkspace {
     loss_ = torch::zeros({1}, of);
     part_ = torch::zeros({nwg * 8}, of);
     ticket_ = torch::zeros({1}, oi);
+    if (x3 && splits_ > 1) {
+      // split-M dW slabs + per-tile arrival counters (tower_x3.hip k_tx3_dw)
+      int64_t tiles = 0;
+      for (int l = 0; l < L_; ++l) tiles += ((pad(dims[l + 1], 32) + 63) / 64) * ((pad(dims[l], 32) + 63) / 64);
+      dw_slab_ = torch::empty({tiles * splits_ * 4096}, of);
+      dw_cnt_ = torch::zeros({tiles}, oi);
+    }
     if (fp32 && splits_ > 1) {
       // split-M dW slabs + per-tile arrival counters (tower32.hip t32_dw_combine)
       int64_t tiles = 0;

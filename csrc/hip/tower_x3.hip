@@ -22,9 +22,10 @@
 //              again for the next layer; output GEMV on hi + lo, loss tail.
 //   k_tx3_bwd  the dX chain the same way; dX0 leaves as fp32 rows.
 //   k_tx3_dw   dW = dZ^T X over 64x64 tiles, the hi / lo panels of both
-//              operands streamed by LDS-DMA; one workgroup per tile over the
-//              whole batch, so each dW element has one writer (bit-reproducible,
-//              no atomics); the bias / data_norm reductions ride along.
+//              operands streamed by LDS-DMA; M split over dw_splits
+//              workgroups per tile whose partials the last arriving split sums
+//              in split order (bit-reproducible, no fp32 atomics); the bias /
+//              data_norm reductions ride along.
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -459,7 +460,12 @@ __global__ __launch_bounds__(256) void k_tx3_dw(TowerArgs a, int ndw) {
     return;
   }
   __shared__ __attribute__((aligned(16))) u16 smem[X3_NST * X3_STAGE];
-  int t = xcd_work_id((int)blockIdx.x, ndw);
+  // work id -> (tile, split): the splits of one tile are consecutive ids
+  const int S = a.dw_splits;
+  const int wid = xcd_work_id((int)blockIdx.x, ndw);
+  const int split = wid % S;
+  const int tile_g = wid / S;
+  int t = tile_g;
   int l = 0;
   for (; l < a.L; ++l) {
     const int nt = ((a.ly[l].Np + 63) / 64) * ((a.ly[l].Kp + 63) / 64);
@@ -488,13 +494,15 @@ __global__ __launch_bounds__(256) void k_tx3_dw(TowerArgs a, int ndw) {
     glo = (int64_t)a.Mp * ly.Kp;
     gstride = NBk * 512;
   }
-  const int nstage = a.Mp / 16 / X3_STEPS;
+  const int per = a.Mp / 16 / S;  // m16 steps of this split (a multiple of X3_STEPS: Mp % 128 == 0, S <= 4)
+  const int mb0 = split * per;
+  const int nstage = per / X3_STEPS;
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(tower_lds_addr(smem));
   auto issue = [&](int slot, int stage) {
     const unsigned base = lds0 + (unsigned)(slot * X3_STAGE) * 2u;
 #pragma unroll
     for (int st = 0; st < X3_STEPS; ++st) {
-      const int64_t mb = (int64_t)(stage * X3_STEPS + st) * gstride;
+      const int64_t mb = (int64_t)(mb0 + stage * X3_STEPS + st) * gstride;
       tower_glds16(gsrc + mb, __builtin_amdgcn_readfirstlane(base + st * 8192u + (unsigned)w * 1024u));
       tower_glds16(gsrc + glo + mb, __builtin_amdgcn_readfirstlane(base + st * 8192u + (unsigned)(4 + w) * 1024u));
     }
@@ -523,17 +531,70 @@ __global__ __launch_bounds__(256) void k_tx3_dw(TowerArgs a, int ndw) {
       accd = mf(al, bh, accd);
     }
   }
-  // one writer per dW element: plain read-modify-write (grads accumulate)
   const int nb = tn * 2 + wn, kb = tk * 2 + wk;
-  if (nb >= NBn || kb >= NBk) return;
   const int c = lane & 31, h = lane >> 5;
   const int k = kb * 32 + c;
-  if (k >= ly.K) return;
+  const bool active = nb < NBn && kb < NBk && k < ly.K;
+  f32x16 v;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int n = nb * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
-    if (n < ly.N) ly.dw[(int64_t)n * ly.K + k] += acc[r] + (accc[r] + accd[r]);
+  for (int r = 0; r < 16; ++r) v[r] = acc[r] + (accc[r] + accd[r]);
+  auto add_out = [&](const f32x16& x) {  // grads accumulate (+=); one writer per element
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = nb * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+      if (n < ly.N) ly.dw[(int64_t)n * ly.K + k] += x[r];
+    }
+  };
+  if (S == 1) {
+    if (active) add_out(v);
+    return;
   }
+  // split-M partials: every split stores its 64x64 partial (a slab,
+  // write-through sc1 stores), the tile's last arriving split sums the slabs
+  // in split order -- bit-reproducible, no fp32 atomics (the tower32.hip
+  // t32_dw_combine hand-off: counter after the drained stores, acquire in
+  // the reducer)
+  float* tile_slab = a.dw_slab + (int64_t)tile_g * S * 4096;
+  {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(tile_slab + (int64_t)split * 4096, 0, 4096 * 4, 0x00020000);
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 f = active ? make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3])
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f), rs, ((w * 4 + q) * 64 + lane) * 16, 0,
+                                             16 /* sc1 */);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);  // the ring is drained: reuse its first word
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(&a.dw_cnt[tile_g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == S - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&a.dw_cnt[tile_g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch from 0
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag || !active) return;
+  f32x16 sum = (f32x16){0};
+  const float4* base = reinterpret_cast<const float4*>(tile_slab) + w * 4 * 64 + lane;
+  for (int sp = 0; sp < S; ++sp) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 f = base[(int64_t)sp * 1024 + q * 64];
+      sum[4 * q] += f.x;
+      sum[4 * q + 1] += f.y;
+      sum[4 * q + 2] += f.z;
+      sum[4 * q + 3] += f.w;
+    }
+  }
+  add_out(sum);
 }
 
 // ---------------------------------------------------------------- packing
@@ -600,7 +661,7 @@ void launch_tower_x3_dw(const TowerArgs& a, hipStream_t s) {
   int tiles = 0;
   for (int l = 0; l < a.L; ++l) tiles += ((a.ly[l].Np + 63) / 64) * ((a.ly[l].Kp + 63) / 64);
   const int nred = (a.bias_ld + 31) / 32 + (a.dn_part ? (a.dn_C + 31) / 32 : 0);
-  hipLaunchKernelGGL(k_tx3_dw, dim3(tiles + nred), dim3(256), 0, s, a, tiles);
+  hipLaunchKernelGGL(k_tx3_dw, dim3(tiles * a.dw_splits + nred), dim3(256), 0, s, a, tiles * a.dw_splits);
 }
 
 void launch_tower_x3_pack(const TowerArgs& a, const float* const* w, hipStream_t s) {

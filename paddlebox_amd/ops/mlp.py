@@ -227,7 +227,8 @@ class FusedMLP(nn.Module):
             else:
                 splits = int(os.environ.get("PBX_TOWER_DW_SPLITS", "2"))
             if x3:
-                splits = 1  # x3 dW: one writer per element (bit-reproducible)
+                # split-M partials summed in split order by the last split (bit-reproducible)
+                splits = int(os.environ.get("PBX_TOWER_X3_DW_SPLITS", "2"))
             tw = tws[key] = _native.hip().TowerWorkspace(M, dims, device.index or 0, splits, bool(fp32), bool(x3))
         if self._tw is not tw:
             self._tw = tw
