@@ -261,7 +261,7 @@ class Session:
         program, and an arena holding only this tower's parameters."""
         if os.environ.get("PBX_ADAM_OVERLAP", "1") != "1":
             return False
-        if self.group is not None or getattr(self, "async_dense", None) or not tower.fp32:
+        if self.group is not None or getattr(self, "async_dense", None) or not (tower.fp32 or tower.x3):
             return False
         lw = self.lowered
         if lw.backward_ops or lw.optimize_ops:

@@ -715,10 +715,18 @@ def k_fused_seq_tensor(ctx, op):
 # ----------------------------------------------------------------- lowered dense chains
 def _fc_fp32() -> bool:
     """FLAGS_padbox_fc_precision: fp32 (default, the reference fc precision,
-    python/paddle/fluid/layers/nn.py:243) or bf16 MFMA operands."""
+    python/paddle/fluid/layers/nn.py:243), fp32x3 (fp32-class: bf16 hi + lo
+    halves, three MFMA products, finer than the reference's default TF32
+    math) or bf16 MFMA operands."""
     from ..utils import flags as _flags
 
     return _flags.get("padbox_fc_precision").lower() != "bf16"
+
+
+def _fc_x3() -> bool:
+    from ..utils import flags as _flags
+
+    return _flags.get("padbox_fc_precision").lower() == "fp32x3"
 
 
 def _tower_for(ctx, op, C: int):
@@ -755,7 +763,9 @@ def _tower_for(ctx, op, C: int):
     dn.group = _stats_group(ctx)
     # the reference fc precision by default (FLAGS_padbox_fc_precision):
     # the lowering only forms the tower when the fp32 tower takes its widths
-    t = CtrTower(mlp, dn, 0, 1, 0, 0, use_head_lin=False, fp32=_fc_fp32())
+    x3 = _fc_x3()
+    t = CtrTower(mlp, dn, 0, 1, 0, 0, use_head_lin=False, fp32=_fc_fp32() and not x3)
+    t.x3 = x3
     # Session.fuse_towers binds an AUC metric by these names
     t.io = (op.outputs["Pred"][0].name, {op.inputs["Label"][0].name, a.get("label_alias") or ""} - {""})
     if ctx.training and hasattr(ctx.s, "on_tower_grads"):

@@ -23,8 +23,11 @@ design (documented, not silently ignored):
 * ``padbox_fc_precision`` (this engine's, not the reference's) -- operand
   precision of the fluid ``fc`` chains the lowering fuses: ``fp32`` (default,
   the reference fc precision: the exact-fp32 MFMA tower, or library fp32
-  GEMMs for chains the tower does not take) or ``bf16`` (bf16 MFMA operands,
-  fp32 accumulate).
+  GEMMs for chains the tower does not take), ``fp32x3`` (fp32 storage and
+  accumulation, every product as three bf16 MFMAs on hi + lo halves --
+  finer than the TF32 math the reference's fp32 fc runs on by default,
+  phi/backends/gpu/gpu_context.cc:65-67,580-588; the bench headline) or
+  ``bf16`` (bf16 MFMA operands, fp32 accumulate).
 * ``padbox_train_steps_per_graph`` / ``padbox_pipelined_front`` (this
   engine's) -- the graphed ``train_from_dataset`` loop: training steps per
   captured HIP graph (0 = auto) and the pipelined front (each step pools the

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--marker", default="k_t32_fwd")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--timeline", action="store_true",
+                    help="also list every kernel of the last step (us from its marker launch)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, queue_id from kernels order by start").fetchall()
@@ -68,6 +70,12 @@ def main():
     print(f"|---|---|---|---|")
     for n in sorted(tot, key=lambda k: -exposed[k] - 1e-3 * tot[k])[:a.top]:
         print(f"| {n} | {cnt[n] / steps:.2f} | {tot[n] / steps / 1e3:.1f} | {exposed[n] / steps / 1e3:.1f} |")
+    if a.timeline:
+        a0, a1 = marks[-2], marks[-1]
+        print(f"\ntimeline of the last step (us from its '{a.marker}' start; queue id)")
+        for n, s, e, q in rows:
+            if e > a0 - 200_000 and s < a1:
+                print(f"  {(s - a0) / 1e3:8.1f} {(e - a0) / 1e3:8.1f} {(e - s) / 1e3:6.1f}  q{q}  {short(n)}")
 
 
 if __name__ == "__main__":

@@ -200,6 +200,19 @@ def test_tower_lowering_matches_unfused_program(tmp_path):
             outs[fuse] = (ctx.get(pred).detach().float().view(-1).cpu(), float(ctx.get(loss)))
         torch.testing.assert_close(outs[True][0], outs[False][0], rtol=0, atol=2e-5)
         assert abs(outs[True][1] - outs[False][1]) < 2e-5
+        # fp32x3: the x3 tower (bf16 hi + lo halves, three products per step)
+        set_flags({"FLAGS_padbox_fc_precision": "fp32x3"})
+        scope = fluid.Scope()
+        exe = fluid.Executor(fluid.CUDAPlace(0))
+        exe.run(startup, scope=scope)
+        s = Session(main, scope, torch.device("cuda:0"), fuse=True)
+        s.training = False
+        ctx = ExecContext(s, batch, training=False)
+        s.feed_batch(ctx, batch)
+        s.forward(ctx)
+        t = next(v for k, v in s.cache.items() if isinstance(k, tuple) and k[0] == "tower")
+        assert t.x3 and not t.fp32
+        torch.testing.assert_close(ctx.get(pred).detach().float().view(-1).cpu(), outs[False][0], rtol=0, atol=1e-4)
         set_flags({"FLAGS_padbox_fc_precision": "bf16"})
         scope = fluid.Scope()
         exe = fluid.Executor(fluid.CUDAPlace(0))
