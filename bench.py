@@ -244,8 +244,12 @@ def main():
     from paddlebox_amd.ps.sparse_engine import SparseEngine
 
     if args.same_gpu:
-        # all ranks' spinning IPC collectives share one GPU's workgroup slots
-        os.environ.setdefault("PBX_IPC_MAX_BLOCKS", str(max(8, min(64, 256 // max(1, world)))))
+        # all ranks' spinning IPC collectives share one GPU's workgroup slots:
+        # together they hold at most half the CUs, so a peer's whole-CU kernels
+        # (the x3 tower: 104 KB LDS and 2 x 237 VGPRs per SIMD per workgroup)
+        # still find CUs to run on while the others spin (with 256 // W blocks
+        # per rank the 4-rank rehearsal hit the IPC spin bound)
+        os.environ.setdefault("PBX_IPC_MAX_BLOCKS", str(max(8, min(64, 128 // max(1, world)))))
     gpu_index = 0 if args.same_gpu else local_rank
     torch.cuda.set_device(gpu_index)
     device = torch.device("cuda", gpu_index)
