@@ -183,12 +183,13 @@ def _dense_rows(dense: torch.Tensor) -> torch.Tensor:
 
 def _push_run_scratch(max_keys: int, device) -> torch.Tensor:
     """Runs of a key's occurrences that straddle waves in the fused merge +
-    update: the int32 per-wave run owners of the two-launch form
-    (k_push_finish, default), or with PBX_PUSH_FINISH=0 int64 arrival
-    counters per unique (one launch: the piece that completes a run applies
-    it; the first form of it fenced every piece and measured 0.49 vs 0.38
-    ms/step)."""
-    if os.environ.get("PBX_PUSH_FINISH", "1") == "1":
+    update: int64 arrival counters per unique (one launch, default: the
+    piece that completes a run applies it; the first form of it fenced every
+    piece and measured 0.49 vs 0.38 ms/step), or with PBX_PUSH_FINISH=1 the
+    int32 per-wave run owners of the two-launch form (k_push_finish).  With
+    the x3 tower the push sits on the step's critical path: one launch is
+    0.2515-0.2518 vs 0.2569-0.2577 ms/step (profiles/r6_x3_sparse_knob_ab.txt)."""
+    if os.environ.get("PBX_PUSH_FINISH", "0") == "1":
         return torch.empty((max_keys + 63) // 64 + 1, dtype=torch.int32, device=device)
     return torch.zeros(max_keys, dtype=torch.int64, device=device)
 

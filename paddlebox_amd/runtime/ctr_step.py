@@ -204,10 +204,18 @@ class CtrTrainStep:
         point the next step's head may start from, then Adam."""
         from ..parallel.dense import set_pre_head_event
 
+        # PBX_HEAD_AFTER_ADAM=1: the mark after Adam instead -- the head then
+        # waits for the update and the tower forward's own join of the side
+        # stream is already satisfied (one cross-stream edge fewer on the
+        # critical path when Adam ends before the pooling does)
+        after = os.environ.get("PBX_HEAD_AFTER_ADAM", "0") == "1"
+        if after:
+            self.opt.step(1.0, join=False)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         set_pre_head_event(self.model.tower.uid, ev)
-        self.opt.step(1.0, join=False)
+        if not after:
+            self.opt.step(1.0, join=False)
 
     def _side_update_multi(self):
         """Tower dense-grads hook (multi-rank overlapped optimizer): the

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--timeline", action="store_true",
                     help="also list every kernel of the last step (us from its marker launch)")
+    ap.add_argument("--which", type=int, default=1, help="with --timeline: the k-th last step")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, queue_id from kernels order by start").fetchall()
@@ -71,7 +72,7 @@ def main():
     for n in sorted(tot, key=lambda k: -exposed[k] - 1e-3 * tot[k])[:a.top]:
         print(f"| {n} | {cnt[n] / steps:.2f} | {tot[n] / steps / 1e3:.1f} | {exposed[n] / steps / 1e3:.1f} |")
     if a.timeline:
-        a0, a1 = marks[-2], marks[-1]
+        a0, a1 = marks[-a.which - 1], marks[-a.which]
         print(f"\ntimeline of the last step (us from its '{a.marker}' start; queue id)")
         for n, s, e, q in rows:
             if e > a0 - 200_000 and s < a1:

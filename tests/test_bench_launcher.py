@@ -70,15 +70,15 @@ def test_graph_steps_default_and_explicit():
 
 
 def test_push_run_scratch_forms(monkeypatch):
-    """The fused push's straddling-run scratch: int32 per-wave owners (two
-    launches, default) or int64 per-unique arrival counters (PBX_PUSH_FINISH=0)."""
+    """The fused push's straddling-run scratch: int64 per-unique arrival
+    counters (one launch, default) or int32 per-wave owners (PBX_PUSH_FINISH=1)."""
     import torch
 
     from paddlebox_amd.ps.sparse_engine import _push_run_scratch
 
-    monkeypatch.delenv("PBX_PUSH_FINISH", raising=False)
+    monkeypatch.setenv("PBX_PUSH_FINISH", "1")
     t = _push_run_scratch(1000, "cpu")
     assert t.dtype == torch.int32 and t.numel() == (1000 + 63) // 64 + 1
-    monkeypatch.setenv("PBX_PUSH_FINISH", "0")
+    monkeypatch.delenv("PBX_PUSH_FINISH", raising=False)
     t = _push_run_scratch(1000, "cpu")
     assert t.dtype == torch.int64 and t.numel() == 1000 and int(t.abs().sum()) == 0

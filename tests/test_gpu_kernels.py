@@ -148,8 +148,12 @@ def test_seqpool_filter_quant():
     torch.testing.assert_close(out, exp, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("push_finish", ["0", "1"])
 @pytest.mark.parametrize("ragged", [False, True])
-def test_push_adagrad_matches_reference(ragged):
+def test_push_adagrad_matches_reference(ragged, push_finish, monkeypatch):
+    """Fused merge + Adagrad vs the reference, in both straddling-run forms:
+    per-unique arrival counters (one launch, default) and k_push_finish."""
+    monkeypatch.setenv("PBX_PUSH_FINISH", push_finish)
     torch.manual_seed(4)
     if ragged:
         b = ragged_batch(64, 6, 6, 30, seed=9, device=DEV)
