@@ -28,6 +28,8 @@
 //              data_norm reductions ride along.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.h"
 #include "tower_common.h"
 
@@ -41,8 +43,10 @@ typedef unsigned short u16;
 constexpr int XBM = 32;   // rows per fwd / bwd workgroup
 constexpr int XNT = 512;  // threads (8 waves, 2 per SIMD)
 constexpr int XNW = XNT / 64;
-constexpr int XPF_F = 4;  // weight-ring depth (k-steps, 4 fragments each) of the forward
-constexpr int XPF_B = 3;  // ... of the backward (4 spills registers)
+// weight-ring depth (k-steps, 4 fragments each): forward 4, backward 3 (4
+// spills registers there); PBX_X3_PF_F / PBX_X3_PF_B pick 3-5 / 2-3 for A/Bs
+constexpr int kX3PfF = 4;
+constexpr int kX3PfB = 3;
 
 __device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f)); }
 __device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float(((unsigned int)h) << 16); }
@@ -173,6 +177,7 @@ __device__ __forceinline__ void fwd_ep3(const f32x16& h, const f32x16& cc, const
   }
 }
 
+template <int XPF_F>
 __global__ __launch_bounds__(XNT) void k_tx3_fwd(TowerArgs a) {
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
   const int ldl = a.lds_ld, plane = XBM * ldl;
@@ -335,6 +340,7 @@ __device__ __forceinline__ void bwd_ep3(const f32x16& hacc, const f32x16& cc, co
   if (h == 0) bp[prev.bias_off + kb * 32 + c] = cs;
 }
 
+template <int XPF_B>
 __global__ __launch_bounds__(XNT) void k_tx3_bwd(TowerArgs a) {
   extern __shared__ __attribute__((aligned(16))) u16 lds[];
   __shared__ float gs[XBM];
@@ -630,14 +636,25 @@ __global__ void k_tx3_pack(TowerArgs a, X3PackJob j) {
   wtp[lo_off + ti] = lo;
 }
 
+template <typename K>
+void x3_big_lds_one(K f) {
+  if (hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
+    (void)hipGetLastError();
+}
 void x3_big_lds() {
   static const bool once = [] {
-    for (const void* f : {(const void*)k_tx3_fwd, (const void*)k_tx3_bwd})
-      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
-        (void)hipGetLastError();
+    x3_big_lds_one(k_tx3_fwd<3>);
+    x3_big_lds_one(k_tx3_fwd<4>);
+    x3_big_lds_one(k_tx3_fwd<5>);
+    x3_big_lds_one(k_tx3_bwd<2>);
+    x3_big_lds_one(k_tx3_bwd<3>);
     return true;
   }();
   (void)once;
+}
+int x3_env(const char* n, int d) {
+  const char* e = getenv(n);
+  return e ? atoi(e) : d;
 }
 
 }  // namespace
@@ -647,13 +664,20 @@ size_t tower_x3_lds_bytes(int lds_ld) { return (size_t)4 * XBM * lds_ld * sizeof
 void launch_tower_x3_fwd(const TowerArgs& a, hipStream_t s) {
   if (a.M == 0) return;
   x3_big_lds();
-  hipLaunchKernelGGL(k_tx3_fwd, dim3(a.Mp / XBM), dim3(XNT), tower_x3_lds_bytes(a.lds_ld), s, a);
+  static const int pf = x3_env("PBX_X3_PF_F", kX3PfF);
+  const dim3 g(a.Mp / XBM);
+  const size_t lb = tower_x3_lds_bytes(a.lds_ld);
+  if (pf == 3) hipLaunchKernelGGL(k_tx3_fwd<3>, g, dim3(XNT), lb, s, a);
+  else if (pf == 5) hipLaunchKernelGGL(k_tx3_fwd<5>, g, dim3(XNT), lb, s, a);
+  else hipLaunchKernelGGL(k_tx3_fwd<4>, g, dim3(XNT), lb, s, a);
 }
 
 void launch_tower_x3_bwd(const TowerArgs& a, hipStream_t s) {
   if (a.M == 0) return;
   x3_big_lds();
-  hipLaunchKernelGGL(k_tx3_bwd, dim3(a.Mp / XBM), dim3(XNT), tower_x3_lds_bytes(a.lds_ld), s, a);
+  static const int pf = x3_env("PBX_X3_PF_B", kX3PfB);
+  if (pf == 2) hipLaunchKernelGGL(k_tx3_bwd<2>, dim3(a.Mp / XBM), dim3(XNT), tower_x3_lds_bytes(a.lds_ld), s, a);
+  else hipLaunchKernelGGL(k_tx3_bwd<3>, dim3(a.Mp / XBM), dim3(XNT), tower_x3_lds_bytes(a.lds_ld), s, a);
 }
 
 void launch_tower_x3_dw(const TowerArgs& a, hipStream_t s) {
