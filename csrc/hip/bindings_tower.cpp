@@ -203,9 +203,33 @@ class TowerWorkspace {
                   const c10::optional<Tensor>& dn_part,
                   int64_t dn_rows, double dn_eps, const c10::optional<Tensor>& dn_stats, int64_t parts,
                   const c10::optional<Tensor>& dn_bsize, const c10::optional<Tensor>& dn_bsum,
-                  const c10::optional<Tensor>& dn_bsq, double dn_decay) {
+                  const c10::optional<Tensor>& dn_bsq, double dn_decay, const c10::optional<Tensor>& head_x,
+                  const c10::optional<Tensor>& head_scales, int64_t hS, int64_t hEo, int64_t hew, int64_t hD,
+                  bool hlin) {
     TW_CHECK((int)dW.size() == L_ && (int)db.size() == L_, "backward: layer count");
     TowerArgs a = base();
+    Tensor hdx;
+    if (head_x.has_value() && head_x->defined() && (parts & 1)) {
+      // x3: the DeepFM head backward fused into the dX0 epilogue
+      TW_CHECK(x3_ && need_dx, "fused head backward: x3 tower with dX0 only");
+      check_f32(*head_x, -1, "head_x");
+      TW_CHECK(head_x->dim() == 2 && head_x->size(0) == M_ && head_x->size(1) <= pad(dims_[0], wpad_) &&
+                   hD >= 0 && hD <= 16 && hS >= 0 && hS * hEo <= head_x->size(1) && (hS == 0 || hew + hD < hEo),
+               "head_x: [M, C <= K0p], D <= 16, slot blocks inside the row");
+      hdx = torch::empty_like(*head_x);
+      a.hx = P<float>(*head_x);
+      a.hdx = P<float>(hdx);
+      a.hC = (int)head_x->size(1);
+      if (head_scales.has_value() && head_scales->defined()) {
+        check_f32(*head_scales, a.hC, "head_scales");
+        a.hscales = P<float>(*head_scales);
+      }
+      a.hS = (int)hS;
+      a.hEo = (int)hEo;
+      a.hew = (int)hew;
+      a.hD = (int)hD;
+      a.hlin = hlin ? 1 : 0;
+    }
     for (int l = 0; l < L_; ++l) {
       check_f32(dW[l], dims_[l + 1] * dims_[l], "dW");
       check_f32(db[l], dims_[l + 1], "db");
@@ -256,6 +280,7 @@ class TowerWorkspace {
       if (parts & 1) launch_tower_bwd(a, s);
       if (parts & 2) launch_tower_dw(a, s);
     }
+    if (hdx.defined()) return hdx;
     return need_dx ? dx0_ : Tensor();
   }
 
@@ -442,7 +467,8 @@ void bind_tower(py::module& m) {
            py::arg("db_out"), py::arg("need_dx"), py::arg("dn_part") = py::none(), py::arg("dn_rows") = 0,
            py::arg("dn_eps") = 0.0, py::arg("dn_stats") = py::none(), py::arg("parts") = 3,
            py::arg("dn_bsize") = py::none(), py::arg("dn_bsum") = py::none(), py::arg("dn_bsq") = py::none(),
-           py::arg("dn_decay") = 1.0)
+           py::arg("dn_decay") = 1.0, py::arg("head_x") = py::none(), py::arg("head_scales") = py::none(),
+           py::arg("hS") = 0, py::arg("hEo") = 0, py::arg("hew") = 0, py::arg("hD") = 0, py::arg("hlin") = false)
       .def("pack_regions", &TowerWorkspace::pack_regions)
       .def("set_stamps", &TowerWorkspace::set_stamps)
       .def("x0", &TowerWorkspace::x0)

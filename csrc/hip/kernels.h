@@ -703,6 +703,13 @@ struct TowerArgs {
   const float* x0f = nullptr;
   const float* x0mpf = nullptr;
   float* dx0f = nullptr;
+  // x3 tower: the DeepFM head backward fused into the dX0 epilogue (k_head_bwd
+  // semantics): hdx[m][c] = dX0[m][c] * hscales[c] (+ d lin terms of the
+  // first-order / FM columns when hlin); hx: the head input rows [M][hC]
+  const float* hx = nullptr;
+  float* hdx = nullptr;
+  const float* hscales = nullptr;
+  int hC = 0, hS = 0, hEo = 0, hew = 0, hD = 0, hlin = 0;
 };
 int tower_nwg(int M);
 size_t tower_lds_bytes(const TowerArgs& a);

@@ -45,6 +45,7 @@ constexpr int XNT = 512;  // threads (8 waves, 2 per SIMD)
 constexpr int XNW = XNT / 64;
 // weight-ring depth (k-steps, 4 fragments each): forward 4, backward 3 (4
 // spills registers there); PBX_X3_PF_F / PBX_X3_PF_B pick 3-5 / 2-3 for A/Bs
+constexpr int kX3HeadMaxD = 16;  // fused head backward: embedx dims held per row in LDS
 constexpr int kX3PfF = 4;
 constexpr int kX3PfB = 3;
 
@@ -349,9 +350,21 @@ __global__ __launch_bounds__(XNT) void k_tx3_bwd(TowerArgs a) {
   const int m0 = blockIdx.x * XBM;
   u16* src = lds;
   u16* dst = lds + 2 * plane;
+  __shared__ float s1s[XBM * kX3HeadMaxD];  // fused head: per-row FM sums over the slots
   float* bp = a.bias_part + (int64_t)blockIdx.x * a.bias_ld;
   const float gl = a.dloss ? a.dloss[0] : 1.f;
   if (tid < XBM) gs[tid] = (m0 + tid < a.M) ? a.dz[m0 + tid] * gl : 0.f;
+  if (a.hdx && a.hlin) {
+    for (int i = tid; i < XBM * a.hD; i += XNT) {
+      const int r = i / a.hD, d = i - r * a.hD;
+      float s1 = 0.f;
+      if (m0 + r < a.M) {
+        const float* xr = a.hx + (int64_t)(m0 + r) * a.hC + a.hew + 1 + d;
+        for (int sl = 0; sl < a.hS; ++sl) s1 += xr[sl * a.hEo];
+      }
+      s1s[r * kX3HeadMaxD + d] = s1;
+    }
+  }
   __syncthreads();
   // dZ_L = (g w_out^T) . relu'(X_L), X_L = hi + lo from its m-packed halves
   const TowerLayerDev& lastl = a.ly[a.L - 1];
@@ -430,15 +443,14 @@ __global__ __launch_bounds__(XNT) void k_tx3_bwd(TowerArgs a) {
         if (two) mk1 = bwd_mask3(a.ly[i - 1], kb1, m0, lane);
         bwd_ep3(c.h0, c.c0, c.d0, a.ly[i - 1], mk0, kb0, m0, dst, plane, ldl, a.Mp, bp, lane);
         if (two) bwd_ep3(c.h1, c.c1, c.d1, a.ly[i - 1], mk1, kb1, m0, dst, plane, ldl, a.Mp, bp, lane);
-      } else {
+      } else {  // dX0 as fp32 rows into the free tile (its 2 planes = 32 x ldl floats)
+        float* t32 = reinterpret_cast<float*>(dst);
         const int cl = lane & 31, h = lane >> 5;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + 8 * (r >> 2) + 4 * h + (r & 3);
-          if (m < a.M) {
-            a.dx0f[(int64_t)m * a.lddx0 + kb0 * 32 + cl] = c.h0[r] + (c.c0[r] + c.d0[r]);
-            if (two) a.dx0f[(int64_t)m * a.lddx0 + kb1 * 32 + cl] = c.h1[r] + (c.c1[r] + c.d1[r]);
-          }
+          const int row = 8 * (r >> 2) + 4 * h + (r & 3);
+          t32[row * ldl + kb0 * 32 + cl] = c.h0[r] + (c.c0[r] + c.d0[r]);
+          if (two) t32[row * ldl + kb1 * 32 + cl] = c.h1[r] + (c.c1[r] + c.d1[r]);
         }
       }
     }
@@ -446,6 +458,38 @@ __global__ __launch_bounds__(XNT) void k_tx3_bwd(TowerArgs a) {
     u16* t = src;
     src = dst;
     dst = t;
+  }
+  if (a.need_dx0 && !a.hdx) {  // dX0 tile -> fp32 rows, 16-B stores
+    const float* t32 = reinterpret_cast<const float*>(src);
+    const int c4n = a.ly[0].Kp / 4;
+    for (int i = tid; i < XBM * c4n; i += XNT) {
+      const int r = i / c4n, cq = i - r * c4n;
+      if (m0 + r < a.M)
+        *reinterpret_cast<float4*>(a.dx0f + (int64_t)(m0 + r) * a.lddx0 + cq * 4) =
+            *reinterpret_cast<const float4*>(t32 + r * ldl + cq * 4);
+    }
+  }
+  if (a.hdx && a.need_dx0) {
+    // the DeepFM head backward (head_ops.hip k_head_bwd semantics) on the
+    // dX0 tile: dx = dX0 * scale (data_norm), plus on the sparse slots'
+    // columns the d lin terms (d lin = dz * dloss = gs[row]): embed_w gets
+    // d lin, embedx dim d gets d lin * (sum over slots of embedx d - x).
+    // Saves the head launch and the dX0 round trip on the critical path.
+    const float* t32 = reinterpret_cast<const float*>(src);
+    const int C = a.hC;
+    for (int i = tid; i < XBM * C; i += XNT) {
+      const int r = i / C, col = i - r * C;
+      const int m = m0 + r;
+      if (m >= a.M) break;  // rows are walked in order
+      float g = t32[r * ldl + col] * (a.hscales ? a.hscales[col] : 1.f);
+      if (a.hlin && col < a.hS * a.hEo) {
+        const int j = col % a.hEo;
+        if (j == a.hew) g += gs[r];
+        else if (j > a.hew && j <= a.hew + a.hD)
+          g += gs[r] * (s1s[r * kX3HeadMaxD + (j - a.hew - 1)] - a.hx[(int64_t)m * C + col]);
+      }
+      a.hdx[(int64_t)m * C + col] = g;
+    }
   }
 }
 

@@ -145,8 +145,20 @@ class _CtrTowerFn(torch.autograd.Function):
         dnk = ({"dn_bsize": dn.batch_size, "dn_bsum": dn.batch_sum, "dn_bsq": dn.batch_square_sum,
                 "dn_decay": float(dn.decay)} if dn_inline else {})
 
+        # PBX_X3_FUSED_HEAD=1 (x3 tower, no cross stack): the head backward
+        # inside the dX chain's last epilogue (k_tx3_bwd), one launch less --
+        # measured slower (0.2611-0.2629 vs 0.2484-0.2487 ms/step with the
+        # separate k_head_bwd, profiles/r6_x3_fused_head_ab.txt: the pass runs
+        # at one 512-thread workgroup per CU behind the chain's LDS tiles,
+        # where k_head_bwd spreads 1024 small workgroups), so off by default
+        use_lin = t.use_head_lin and not ctx.has_extra
+        fuse_head = (ws.x3 and t.cross is None and os.environ.get("PBX_X3_FUSED_HEAD", "0") == "1"
+                     and x.dim() == 2 and x.dtype == torch.float32 and x.is_contiguous())
+        hk = ({"head_x": x, "head_scales": ctx.scales, "hS": t.S, "hEo": t.Eo, "hew": t.ew_col, "hD": t.D,
+               "hlin": bool(use_lin)} if fuse_head else {})
+
         def bwd(parts=3):
-            return ws.backward(*args, parts=parts, **dnk)
+            return ws.backward(*args, parts=parts, **dnk, **(hk if parts & 1 else {}))
 
         def dense_tail():
             if dn_on and not getattr(dn, "stats_in_grad_bucket", False):
@@ -242,10 +254,12 @@ class _CtrTowerFn(torch.autograd.Function):
                         t.on_dense_grads()
                 else:
                     t.on_dense_grads()
-        use_lin = t.use_head_lin and not ctx.has_extra
-        dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, ws.K0p,
-                           ctx.means, ctx.scales, dn.eps if dn is not None else 0.0, dlin_scale=gl,
-                           want_stats=False)
+        if fuse_head:
+            dx = dx0  # the fused epilogue's head gradient
+        else:
+            dx, _ = h.head_bwd(x, dx0, ctx.dz if use_lin else None, t.S, t.Eo, t.ew_col, t.D, ws.K0p,
+                               ctx.means, ctx.scales, dn.eps if dn is not None else 0.0, dlin_scale=gl,
+                               want_stats=False)
         if t.cross is not None and cross_late is not None:
             cross_late()
         if deferred_dw is not None:

@@ -252,3 +252,29 @@ def test_deepfm_x3_training_matches_fp32():
     assert res["fp32"][0] > 0.6, res
     assert abs(res["fp32"][0] - res["fp32x3"][0]) < 1e-3, res
     assert abs(res["fp32"][1] - res["fp32x3"][1]) < 1e-3 * res["fp32"][1], res
+
+
+@pytest.mark.parametrize("B,use_dn", [(700, True), (8192, True), (513, False)])
+def test_x3_fused_head_backward_equals_head_kernel(B, use_dn, monkeypatch):
+    """The DeepFM head backward fused into k_tx3_bwd's dX0 epilogue
+    (PBX_X3_FUSED_HEAD=1, opt-in) gives the
+    gradient of the separate k_head_bwd launch (same fp32 ops; the compilers'
+    multiply-add contraction may differ by an ulp); every parameter gradient
+    is bitwise unchanged."""
+    S, Eo, Dd, D = 26, 11, 13, 8
+    x, label, dn, mlp = _make(B, S, Eo, Dd, (400, 400, 400))
+    grads = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("PBX_X3_FUSED_HEAD", fused)
+        d, m = (copy.deepcopy(dn).to(DEV) if use_dn else None), copy.deepcopy(mlp).to(DEV)
+        t = CtrTower(m, d, S, Eo, 2, D)
+        t.x3 = True
+        xg = x.to(DEV).requires_grad_(True)
+        loss, _ = t(xg, label.to(DEV))
+        loss.backward()
+        torch.cuda.synchronize()
+        grads[fused] = [xg.grad.clone()] + [p.grad.clone() for p in m.parameters()]
+    ref = grads["0"][0]
+    torch.testing.assert_close(grads["1"][0], ref, rtol=1e-6, atol=1e-6 * float(ref.abs().max()))
+    for a, b in zip(grads["1"][1:], grads["0"][1:]):
+        assert torch.equal(a, b)
