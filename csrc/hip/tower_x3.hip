@@ -43,10 +43,11 @@ typedef unsigned short u16;
 constexpr int XBM = 32;   // rows per fwd / bwd workgroup
 constexpr int XNT = 512;  // threads (8 waves, 2 per SIMD)
 constexpr int XNW = XNT / 64;
-// weight-ring depth (k-steps, 4 fragments each): forward 4, backward 3 (4
+// weight-ring depth (k-steps, 4 fragments each): forward 3 (0.2435 / 0.2472 vs
+// 0.2488 / 0.2512 ms/step at 4, profiles/r6_x3_ring_depth_ab.txt), backward 3 (4
 // spills registers there); PBX_X3_PF_F / PBX_X3_PF_B pick 3-5 / 2-3 for A/Bs
 constexpr int kX3HeadMaxD = 16;  // fused head backward: embedx dims held per row in LDS
-constexpr int kX3PfF = 4;
+constexpr int kX3PfF = 3;
 constexpr int kX3PfB = 3;
 
 __device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f)); }
