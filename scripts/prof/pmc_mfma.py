@@ -28,8 +28,18 @@ def main():
     a = ap.parse_args()
     per = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
-    with open(a.csv) as f:
-        for r in csv.DictReader(f):
+    if a.csv.endswith(".db"):  # rocprofv3's default rocpd database: its counters_collection view
+        import sqlite3
+
+        con = sqlite3.connect(a.csv)
+        rows_in = [{"Kernel_Name": k, "Counter_Name": n, "Counter_Value": v, "Dispatch_Id": d}
+                   for (k, n, v, d) in con.execute(
+                       "select kernel_name, counter_name, value, dispatch_id from counters_collection")]
+    else:
+        with open(a.csv) as f:
+            rows_in = list(csv.DictReader(f))
+    if True:
+        for r in rows_in:
             k = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
             k = k.replace("pbx::(anonymous namespace)::", "").replace("void ", "").split("(")[0][:48]
             per[k][r["Counter_Name"]] += float(r["Counter_Value"])
