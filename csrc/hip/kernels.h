@@ -710,6 +710,7 @@ struct TowerArgs {
   float* hdx = nullptr;
   const float* hscales = nullptr;
   int hC = 0, hS = 0, hEo = 0, hew = 0, hD = 0, hlin = 0;
+  int x3_rot = 5;  // x3 tower: k-step rotation multiplier per workgroup (start = blockIdx * x3_rot mod KS)
 };
 int tower_nwg(int M);
 size_t tower_lds_bytes(const TowerArgs& a);

@@ -244,10 +244,10 @@ __global__ __launch_bounds__(XNT) void k_tx3_fwd(TowerArgs a) {
       acc3_zero(c);
       const bf16x8* w0p = wp + (int64_t)nb0 * KS * 64 + lane;
       if (two)
-        mma3<true, XPF_F>(src, src + plane, ldl, w0p, wp + (int64_t)nb1 * KS * 64 + lane, lo_off, KS, (int)blockIdx.x * 5, c,
+        mma3<true, XPF_F>(src, src + plane, ldl, w0p, wp + (int64_t)nb1 * KS * 64 + lane, lo_off, KS, (int)blockIdx.x * a.x3_rot, c,
                    lane);
       else
-        mma3<false, XPF_F>(src, src + plane, ldl, w0p, w0p, lo_off, KS, (int)blockIdx.x * 5, c, lane);
+        mma3<false, XPF_F>(src, src + plane, ldl, w0p, w0p, lo_off, KS, (int)blockIdx.x * a.x3_rot, c, lane);
       fwd_ep3(c.h0, c.c0, c.d0, ly, nb0, m0, dst, plane, ldl, a.Mp, lane);
       if (two) fwd_ep3(c.h1, c.c1, c.d1, ly, nb1, m0, dst, plane, ldl, a.Mp, lane);
     }
@@ -432,10 +432,10 @@ __global__ __launch_bounds__(XNT) void k_tx3_bwd(TowerArgs a) {
       acc3_zero(c);
       const bf16x8* w0p = wtp + (int64_t)kb0 * NS * 64 + lane;
       if (two)
-        mma3<true, XPF_B>(src, src + plane, ldl, w0p, wtp + (int64_t)kb1 * NS * 64 + lane, lo_off, NS, (int)blockIdx.x * 5,
+        mma3<true, XPF_B>(src, src + plane, ldl, w0p, wtp + (int64_t)kb1 * NS * 64 + lane, lo_off, NS, (int)blockIdx.x * a.x3_rot,
                    c, lane);
       else
-        mma3<false, XPF_B>(src, src + plane, ldl, w0p, w0p, lo_off, NS, (int)blockIdx.x * 5, c, lane);
+        mma3<false, XPF_B>(src, src + plane, ldl, w0p, w0p, lo_off, NS, (int)blockIdx.x * a.x3_rot, c, lane);
       if (i > 0) {
         // relu' masks loaded after the MMAs (before them they cost the ring
         // registers a spill)
@@ -706,8 +706,17 @@ int x3_env(const char* n, int d) {
 
 size_t tower_x3_lds_bytes(int lds_ld) { return (size_t)4 * XBM * lds_ld * sizeof(u16); }
 
-void launch_tower_x3_fwd(const TowerArgs& a, hipStream_t s) {
-  if (a.M == 0) return;
+// PBX_X3_ROT: the per-workgroup k-step rotation multiplier (A/B knob)
+static TowerArgs x3_args(const TowerArgs& a0) {
+  static const int rot = x3_env("PBX_X3_ROT", 5);
+  TowerArgs a = a0;
+  a.x3_rot = rot > 0 ? rot : 5;
+  return a;
+}
+
+void launch_tower_x3_fwd(const TowerArgs& a0, hipStream_t s) {
+  if (a0.M == 0) return;
+  const TowerArgs a = x3_args(a0);
   x3_big_lds();
   static const int pf = x3_env("PBX_X3_PF_F", kX3PfF);
   const dim3 g(a.Mp / XBM);
@@ -717,8 +726,9 @@ void launch_tower_x3_fwd(const TowerArgs& a, hipStream_t s) {
   else hipLaunchKernelGGL(k_tx3_fwd<4>, g, dim3(XNT), lb, s, a);
 }
 
-void launch_tower_x3_bwd(const TowerArgs& a, hipStream_t s) {
-  if (a.M == 0) return;
+void launch_tower_x3_bwd(const TowerArgs& a0, hipStream_t s) {
+  if (a0.M == 0) return;
+  const TowerArgs a = x3_args(a0);
   x3_big_lds();
   static const int pf = x3_env("PBX_X3_PF_B", kX3PfB);
   if (pf == 2) hipLaunchKernelGGL(k_tx3_bwd<2>, dim3(a.Mp / XBM), dim3(XNT), tower_x3_lds_bytes(a.lds_ld), s, a);
