@@ -1070,12 +1070,16 @@ void launch_tower_pack(const TowerArgs& a, const float* const* w, hipStream_t s)
   hipLaunchKernelGGL(k_tower_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, j);
 }
 
+// Grid cap of the fused Adam (PBX_ADAM_MAX_BLOCKS): it runs on the side
+// stream beside the critical-path pooling, and a smaller grid leaves that
+// kernel more CUs -- x3 step 0.2452-0.2462 ms at 256 vs 0.2470-0.2472 at 512,
+// 0.2494-0.2504 at 128 (profiles/r6_x3_adam_blocks_ab.txt)
 static int adam_max_blocks() {
   static const int v = [] {
     const char* e = getenv("PBX_ADAM_MAX_BLOCKS");
-    return e ? atoi(e) : 512;
+    return e ? atoi(e) : 256;
   }();
-  return v > 0 ? v : 512;
+  return v > 0 ? v : 256;
 }
 
 void launch_adam_fused(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
@@ -1084,7 +1088,7 @@ void launch_adam_fused(float* p, float* g, float* m, float* v, int64_t n, float 
   int64_t n4 = (n + 3) / 4;
   for (int d = 0; d < x.n_dn; ++d) n4 = n4 > x.dn_C[d] ? n4 : x.dn_C[d];
   if (n4 == 0) return;
-  // <= 2 workgroups per CU (grid-stride loop inside): few ticket atomics
+  // <= 1 workgroup per CU by default (grid-stride loop inside): few ticket atomics
   int64_t blocks = (n4 + 255) / 256;
   const int64_t cap = (int64_t)adam_max_blocks();
   blocks = blocks < cap ? blocks : cap;
