@@ -655,8 +655,10 @@ def main():
                    if args.mlp_dtype == "fp32x3" else {}),
                 **({f"{sec_dtype}_ms_per_step": round(second["dt"] / args.steps * 1e3, 4),
                     f"{sec_dtype}_samples_per_s": round(B * world * args.steps / second["dt"], 1),
-                    f"{sec_dtype}_mlp": ("exact fp32 products on v_mfma_f32_16x16x4_f32 (the reference fc "
-                                         "precision)" if sec_dtype == "fp32" else "bf16 operands on bf16 MFMA, fp32 "
+                    f"{sec_dtype}_mlp": ("exact fp32 products on v_mfma_f32_16x16x4_f32 (the reference fc with "
+                                         "FLAGS_enable_cublas_tf32_op_math off)" if sec_dtype == "fp32" else
+                                         "fp32x3: fp32 via bf16 hi + lo halves, three MFMA products"
+                                         if sec_dtype == "fp32x3" else "bf16 operands on bf16 MFMA, fp32 "
                                          "accumulate") + ", same run, same sparse engine"}
                    if second is not None else {}),
                 **({"dcn_v2_ms_per_step": round(dcn_res["dt"] / args.steps * 1e3, 4),
